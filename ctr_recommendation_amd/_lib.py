@@ -1,0 +1,110 @@
+"""ctypes binding of libfibinet_hip.so (the C-ABI declared in include/fibinet.h).
+
+The library is loaded once; a missing or un-loadable library raises immediately -- there is
+no CPU fallback anywhere in the product path.  Every call goes through :func:`call`, which
+raises ``RuntimeError`` with ``fbn_last_error()`` on a non-zero return code.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfibinet_hip.so")
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+LL = ctypes.c_longlong
+F = ctypes.c_float
+D = ctypes.c_double
+SZ = ctypes.c_size_t
+U = ctypes.c_uint
+
+# name -> (restype, argtypes); the single source of truth mirrored by include/fibinet.h
+SIGNATURES = {
+    "fbn_version": (I, []),
+    "fbn_last_error": (ctypes.c_char_p, []),
+    "fbn_device_ok": (I, []),
+    "fbn_gemm_workspace_size": (SZ, [I, I, I, I]),
+    "fbn_gemm": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, F, I, P, SZ, P]),
+    "fbn_fields_fwd": (I, [P, P, P, P, P, P, P, F, P, I, P, LL, P, P, P, P, P, I, P, P, P, I, P, P, P, P, P, P,
+                           I, I, I, P]),
+    "fbn_fields_bwd_partials_size": (I, [I, I, I]),
+    "fbn_fields_bwd_grid": (I, [I, I]),
+    "fbn_fields_bwd": (I, [P, P, P, P, P, P, F, P, P, P, I, I, P, P, P, P, P, P, P, P, P, LL, P, P, I, I, I, P]),
+    "fbn_pairs_fwd": (I, [P, P, P, I, I, I, I, P]),
+    "fbn_pairs_bwd": (I, [P, P, P, P, P, I, I, I, I, P]),
+    "fbn_bn_workspace_size": (SZ, [I, I]),
+    "fbn_bn_stats_pass": (I, [P, I, I, P, P, P, P]),
+    "fbn_bn_mean": (I, [P, D, I, P, P]),
+    "fbn_bn_finalize": (I, [P, P, D, I, P, P, P, P, F, F, I, P]),
+    "fbn_bn_stats": (I, [P, I, I, P, P, P, P, F, F, I, P, P]),
+    "fbn_bn_eval_params": (I, [P, P, P, P, I, F, P]),
+    "fbn_bn_act_fwd": (I, [P, P, I, I, P, P, P, P, F, P, U, P, P]),
+    "fbn_bn_bwd_reduce": (I, [P, P, P, P, F, P, P, I, I, P, P, P]),
+    "fbn_bn_bwd_apply": (I, [P, P, P, P, F, P, P, P, P, I, I, P, D, P, P, P, P, P, P]),
+    "fbn_bn_bwd": (I, [P, P, P, P, F, P, P, P, P, I, I, P, P, P, P, P, P]),
+    "fbn_colsum_workspace_size": (SZ, [I, I]),
+    "fbn_colsum": (I, [P, I, I, I, P, F, P, P]),
+    "fbn_head_fwd": (I, [P, P, P, I, I, P, P, P, P, P, F, P]),
+    "fbn_sigmoid_bwd": (I, [P, P, P, I, P]),
+    "fbn_outer": (I, [P, P, P, I, I, P]),
+    "fbn_sum": (I, [P, I, P, F, P]),
+    "fbn_sumsq": (I, [P, LL, P, I, P, P]),
+    "fbn_clip_coef": (I, [P, F, P, P, P]),
+    "fbn_adam_dense": (I, [P, P, P, P, LL, P, P, P, F, F, F, P]),
+    "fbn_adam_table": (I, [P, P, P, LL, I, P, P, P, P, P, F, F, F, P]),
+    "fbn_step_end": (I, [P, P, P, P, P]),
+    "fbn_zero_rows": (I, [P, P, I, P]),
+    "fbn_route": (I, [P, P, I, I, LL, LL, I, P, P, P, P, P, P, P]),
+    "fbn_owner_gather": (I, [P, I, P, P, P, P, P, I, I, P]),
+    "fbn_owner_scatter": (I, [P, I, P, P, P, I, I, P]),
+}
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: build it with `python -m ctr_recommendation_amd.build` "
+                "(the FiBiNET path has no CPU fallback)")
+        h = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = h
+    return _lib
+
+
+def call(name: str, *args) -> int:
+    rc = getattr(lib(), name)(*args)
+    if isinstance(rc, int) and rc != 0 and name not in ("fbn_version", "fbn_device_ok") and not name.endswith(
+            ("_size", "_grid")):
+        msg = lib().fbn_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed (code {rc}): {msg}")
+    return rc
+
+
+def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(device: Optional[torch.device] = None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_hip(t: torch.Tensor, what: str = "input") -> None:
+    if t.device.type != "cuda":
+        raise RuntimeError(
+            f"{what} is on {t.device}; the MI355X FiBiNET path runs only on a HIP device "
+            "(no CPU fallback: move the model and batch with .to('cuda'))")

@@ -1,0 +1,58 @@
+"""Build libfibinet_hip.so in-tree with hipcc for gfx950 (no CUDA, no torch extension API).
+
+``python -m ctr_recommendation_amd.build`` or ``__graft_entry__.build()``.  Objects are
+compiled in parallel and cached by source mtime under ``build/``; the shared library lands
+next to this file so it travels with the repo snapshot to the GPU box.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+ROOT = os.path.dirname(HERE)
+BUILD = os.path.join(ROOT, "build", "fibinet_hip")
+LIB = os.path.join(HERE, "libfibinet_hip.so")
+SOURCES = ["capi.cpp", "gemm.hip", "fields.hip", "mlp.hip", "optim.hip", "exchange.hip"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result",
+         "-I", CSRC, "-I", os.path.join(ROOT, "include")]
+
+
+def _compile(src: str) -> str:
+    path = os.path.join(CSRC, src)
+    obj = os.path.join(BUILD, src + ".o")
+    deps = [path, os.path.join(CSRC, "common.h")]
+    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
+        return obj
+    cmd = [HIPCC] + FLAGS + ["-c", path, "-o", obj]
+    if src.endswith(".cpp"):
+        cmd = [HIPCC, "-O3", "-fPIC", "-std=c++17", "-c", path, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed on {src}:\n{r.stderr}")
+    return obj
+
+
+def build(verbose: bool = True) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    with ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
+        objs = list(ex.map(_compile, SOURCES))
+    newest = max(os.path.getmtime(o) for o in objs)
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < newest:
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr}")
+    if verbose:
+        print(f"built {LIB}")
+    return LIB
+
+
+if __name__ == "__main__":
+    build()
+    sys.exit(0)

@@ -1,0 +1,168 @@
+// Row-sharded embedding exchange (multi-GPU, one process per GPU, RCCL all-to-all between).
+//
+// The item table E (V x D) is split into N contiguous row blocks of Vl = ceil(V/N) rows:
+// owner(id) = id / Vl, local row = id - owner*Vl.  Per step:
+//   requester: route_count  -> counts[o]       (entries per owner: item slot + non-padding history slots)
+//              route_fill   -> send_ids[...]   (local row ids grouped by owner), pos[b][t] (entry position)
+//   [all_to_all_single of counts, then ids]
+//   owner:     owner_gather -> reply rows (E_local[id]); registers the rows in the sparse-grad map
+//   [all_to_all_single of rows back]
+//   requester: fields_fwd MODE 1 reads rows at pos[b][t]  (fields.hip)
+// Backward mirrors it: fields_bwd MODE 1 writes one gradient row per entry at pos[b][t],
+// all_to_all back to the owners, owner_scatter adds them into the compact gradient rows
+// (the sparse reduce-scatter).  Ids stay int64 until routed; routed ids are int32 local rows.
+#include "common.h"
+
+// entry (b, t): t = 0 item id (always routed, even id 0 -> owner 0, row 0), t >= 1 history slot
+// t-1 (routed only if non-zero).  Invalid ids set *err and are not routed (pos = -1).
+__device__ __forceinline__ long long entry_id(const int64_t* item, const int64_t* seq, int L, int b, int t) {
+  return t == 0 ? item[b] : seq[(size_t)b * L + (t - 1)];
+}
+
+__global__ void route_count_kernel(const int64_t* __restrict__ item, const int64_t* __restrict__ seq, int B, int L,
+                                   long long V, long long Vl, int nranks, int* __restrict__ counts, int* err) {
+  __shared__ int hist[64];
+  for (int i = threadIdx.x; i < 64; i += blockDim.x) hist[i] = 0;
+  __syncthreads();
+  const long long total = (long long)B * (L + 1);
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int b = (int)(e / (L + 1)), t = (int)(e % (L + 1));
+    const long long id = entry_id(item, seq, L, b, t);
+    if (id < 0 || id >= V) { atomicOr(err, 1); continue; }
+    if (t > 0 && id == 0) continue;
+    atomicAdd(&hist[(int)(id / Vl)], 1);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nranks; i += blockDim.x)
+    if (hist[i]) atomicAdd(&counts[i], hist[i]);
+}
+
+// offsets = exclusive scan of counts (N <= 64, one thread); cursor zeroed
+__global__ void route_scan_kernel(const int* counts, int nranks, int* offsets, int* cursor) {
+  int s = 0;
+  for (int i = 0; i < nranks; ++i) { offsets[i] = s; s += counts[i]; cursor[i] = 0; }
+  offsets[nranks] = s;
+}
+
+__global__ void route_fill_kernel(const int64_t* __restrict__ item, const int64_t* __restrict__ seq, int B, int L,
+                                  long long V, long long Vl, const int* __restrict__ offsets, int* __restrict__ cursor,
+                                  int* __restrict__ send_ids, int* __restrict__ pos) {
+  const long long total = (long long)B * (L + 1);
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int b = (int)(e / (L + 1)), t = (int)(e % (L + 1));
+    const long long id = entry_id(item, seq, L, b, t);
+    int p = -1;
+    if (id >= 0 && id < V && !(t > 0 && id == 0)) {
+      const int o = (int)(id / Vl);
+      p = offsets[o] + atomicAdd(&cursor[o], 1);
+      send_ids[p] = (int)(id - (long long)o * Vl);
+    }
+    pos[e] = p;
+  }
+}
+
+__device__ __forceinline__ void map_insert_x(int* map, int* n_uniq, int* uniq_rows, int r) {
+  if (__hip_atomic_load(map + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != -1) return;
+  int expected = -1;
+  if (__hip_atomic_compare_exchange_strong(map + r, &expected, -2, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT)) {
+    const int u = atomicAdd(n_uniq, 1);
+    uniq_rows[u] = r;
+    __hip_atomic_store(map + r, u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// owner side: out[i] = E_local[ids[i]]; G = D/4 lanes per row.  Rows with global id 0
+// (rank 0, local row 0) are padding: gathered (the item lookup of id 0 reads row 0) but
+// never registered for a gradient.
+template <int D>
+__global__ void __launch_bounds__(256) owner_gather_kernel(const int* __restrict__ ids, int n, const float* __restrict__ E,
+                                                           float* __restrict__ out, int* map, int* n_uniq, int* uniq_rows,
+                                                           int rank) {
+  constexpr int G = D / 4, RPW = 64 / G;
+  const int lane = threadIdx.x & 63, q = lane % G;
+  const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+  for (long long i0 = gw * RPW; i0 < n; i0 += nw * RPW) {
+    const long long i = i0 + lane / G;
+    if (i >= n) continue;
+    const int r = ids[i];
+    *reinterpret_cast<f32x4*>(out + i * D + 4 * q) = *reinterpret_cast<const f32x4*>(E + (size_t)r * D + 4 * q);
+    if (map && q == 0 && !(rank == 0 && r == 0)) map_insert_x(map, n_uniq, uniq_rows, r);
+  }
+}
+
+// owner side backward: gU[map[ids[i]]] += grad[i]
+template <int D>
+__global__ void __launch_bounds__(256) owner_scatter_kernel(const int* __restrict__ ids, int n,
+                                                            const float* __restrict__ grad, const int* __restrict__ map,
+                                                            float* __restrict__ gU, int rank) {
+  constexpr int G = D / 4, RPW = 64 / G;
+  const int lane = threadIdx.x & 63, q = lane % G;
+  const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+  for (long long i0 = gw * RPW; i0 < n; i0 += nw * RPW) {
+    const long long i = i0 + lane / G;
+    if (i >= n) continue;
+    const int r = ids[i];
+    if (rank == 0 && r == 0) continue;
+    const f32x4 g = *reinterpret_cast<const f32x4*>(grad + i * D + 4 * q);
+    float* dst = gU + (size_t)map[r] * D + 4 * q;
+    atomicAdd(dst + 0, g[0]); atomicAdd(dst + 1, g[1]); atomicAdd(dst + 2, g[2]); atomicAdd(dst + 3, g[3]);
+  }
+}
+
+// ------------------------------------------------------------------ C ABI
+extern "C" int fbn_route(const int64_t* item, const int64_t* seq, int B, int L, long long V, long long Vl, int nranks,
+                         int* counts, int* offsets, int* cursor, int* send_ids, int* pos, int* err, void* stream) {
+  if (nranks < 1 || nranks > 64) { fbn_set_error("route: 1 <= nranks <= 64"); return FBN_ERR_ARG; }
+  hipStream_t st = (hipStream_t)stream;
+  (void)hipMemsetAsync(counts, 0, sizeof(int) * nranks, st);
+  const long long total = (long long)B * (L + 1);
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(route_count_kernel, dim3(blocks), dim3(256), 0, st, item, L > 0 ? seq : nullptr, B, L, V, Vl,
+                     nranks, counts, err);
+  hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(1), 0, st, counts, nranks, offsets, cursor);
+  hipLaunchKernelGGL(route_fill_kernel, dim3(blocks), dim3(256), 0, st, item, L > 0 ? seq : nullptr, B, L, V, Vl,
+                     offsets, cursor, send_ids, pos);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+#define FBN_DISPATCH_D(KERNEL, D, GRID, ...)                                                         \
+  switch (D) {                                                                                      \
+    case 16: hipLaunchKernelGGL((KERNEL<16>), GRID, dim3(256), 0, st, __VA_ARGS__); break;          \
+    case 32: hipLaunchKernelGGL((KERNEL<32>), GRID, dim3(256), 0, st, __VA_ARGS__); break;          \
+    case 64: hipLaunchKernelGGL((KERNEL<64>), GRID, dim3(256), 0, st, __VA_ARGS__); break;          \
+    case 128: hipLaunchKernelGGL((KERNEL<128>), GRID, dim3(256), 0, st, __VA_ARGS__); break;        \
+    case 256: hipLaunchKernelGGL((KERNEL<256>), GRID, dim3(256), 0, st, __VA_ARGS__); break;        \
+    default: fbn_set_error("exchange: D must be 16/32/64/128/256"); return FBN_ERR_UNSUPPORTED;      \
+  }
+
+static dim3 rows_grid(long long n, int D) {
+  const int rpw = 256 / D;
+  long long blocks = ((n + rpw - 1) / rpw + 3) / 4;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 8192) blocks = 8192;
+  return dim3((unsigned)blocks);
+}
+
+extern "C" int fbn_owner_gather(const int* ids, int n, const float* E, float* out, int* map, int* n_uniq,
+                                int* uniq_rows, int rank, int D, void* stream) {
+  if (n <= 0) return FBN_OK;
+  hipStream_t st = (hipStream_t)stream;
+  FBN_DISPATCH_D(owner_gather_kernel, D, rows_grid(n, D), ids, n, E, out, map, n_uniq, uniq_rows, rank);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+extern "C" int fbn_owner_scatter(const int* ids, int n, const float* grad, const int* map, float* gU, int rank, int D,
+                                 void* stream) {
+  if (n <= 0) return FBN_OK;
+  hipStream_t st = (hipStream_t)stream;
+  FBN_DISPATCH_D(owner_scatter_kernel, D, rows_grid(n, D), ids, n, grad, map, gU, rank);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}

@@ -1,0 +1,453 @@
+// K1 / K2 / K4: FiBiNET field construction, SENET and the embedding scatter-add gradient.
+//
+// Forward (one "sample group" of D/4 lanes per sample, each lane owning 4 contiguous
+// columns, so a D=128 fp32 row is one 512-B coalesced read by 32 lanes):
+//   X1 = C[likes], X2 = C[views], X3 = E[item_id], X4 = ReLU(LN(h_mm)),
+//   X5 = sum_{t: s_t != 0} E[s_t] / max(1, #nonzero)         (model_fibinet.py:152-176)
+//   z_f = mean_d X_f ; a = sigmoid(W2 relu(W1 z + b1) + b2) ; V_f = X_f * a_f   (:24-35)
+// All 21 table rows of a sample are issued before any is consumed (21 x 16 B in flight per
+// lane); the (B,20,d) history tensor of the reference is never materialised.
+// V_0 == 0 (the user field is all zeros, :152), so only fields 1..5 are stored.
+//
+// Backward: SENET + mean + LayerNorm + ReLU backward per sample, then the embedding
+// gradient: E rows get dX3 (item) and dX5/count (each non-padding history slot); row 0 is
+// never written (padding_idx=0, :100).  The table gradient is accumulated either into a
+// dense V x d buffer (torch drop-in semantics) or into a compact per-unique-row buffer
+// addressed through a row->slot map (the native trainer: see DESIGN.md "sparse table grad").
+// Small parameter gradients (SENET, LN, cate table) are reduced per block in LDS and
+// written as per-block partial slabs summed by fbn_reduce_partials (deterministic).
+#include "common.h"
+
+#define FBN_MAXR 8   // max SENET reduced width supported (reference: 3)
+
+struct FieldArgs {
+  const int64_t* item_id;   // [B]
+  const int64_t* item_seq;  // [B][L] or null (L = 0)
+  const int64_t* likes;     // [B]
+  const int64_t* views;     // [B]
+  const float* hmm;         // [B][D] pre-LayerNorm mm projection (bias included)
+  const float* ln_g;        // [D]
+  const float* ln_b;        // [D]
+  const float* cate;        // [n_cate][D]
+  const float* table;       // mode 0: [V][D] rows; mode 1: exchanged row buffer
+  const int* pos;           // mode 1: [B][L+1] row index into `table` (-1 = none)
+  const float* w1; const float* b1; const float* w2; const float* b2;  // SENET [R][6],[R],[6][R],[6]
+  float* X;                 // [B][5][D] fields 1..5 (pre-SENET)
+  float* Vc;                // [B][5][D] fields 1..5 (post-SENET)
+  float* c;                 // [B][ldc]; cols [0,5D) <- Vc (MLP input, compact layout)
+  float* a_out;             // [B][6]
+  float* cnt_out;           // [B]
+  int* err;                 // id range violations (sticky flag)
+  int* map;                 // sparse-grad map [V] (-1 = untouched) or null
+  int* n_uniq;              // number of unique rows (device counter)
+  int* uniq_rows;           // [cap] unique row list
+  long long V;              // rows of the table (mode 0)
+  int B, L, ldc, R, n_cate;
+  float ln_eps;
+};
+
+__device__ __forceinline__ void map_insert(int* map, int* n_uniq, int* uniq_rows, int r) {
+  if (__hip_atomic_load(map + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != -1) return;
+  int expected = -1;
+  if (__hip_atomic_compare_exchange_strong(map + r, &expected, -2, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT)) {
+    const int u = atomicAdd(n_uniq, 1);
+    uniq_rows[u] = r;
+    __hip_atomic_store(map + r, u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <int D>
+__device__ __forceinline__ void senet_excite(const float (&z)[6], const float* w1, const float* b1,
+                                             const float* w2, const float* b2, int R, float (&q)[FBN_MAXR],
+                                             float (&a)[6]) {
+  for (int j = 0; j < R; ++j) {
+    float s = b1[j];
+#pragma unroll
+    for (int f = 0; f < 6; ++f) s += w1[j * 6 + f] * z[f];
+    q[j] = s;
+  }
+#pragma unroll
+  for (int f = 0; f < 6; ++f) {
+    float s = b2[f];
+    for (int j = 0; j < R; ++j) s += w2[f * R + j] * fmaxf(q[j], 0.f);
+    a[f] = 1.f / (1.f + __expf(-s));
+  }
+}
+
+template <int D, int MODE>
+__global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
+  constexpr int G = D / 4;                  // lanes per sample
+  constexpr int SPW = 64 / G;               // samples per wave
+  constexpr int HCH = 10;
+  const int lane = threadIdx.x & 63;
+  const int q = lane % G;
+  const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  const int L = p.L;
+
+  for (int b0 = gw * SPW; b0 < p.B; b0 += nwaves * SPW) {
+    const int b = b0 + lane / G;
+    if (b >= p.B) continue;
+    // ---------------- ids + validation
+    long long item = p.item_id[b];
+    long long lk = p.likes[b], vw = p.views[b];
+    bool bad = false;
+    if (lk < 0 || lk >= p.n_cate) { bad = true; lk = 0; }
+    if (vw < 0 || vw >= p.n_cate) { bad = true; vw = 0; }
+    // history rows are issued in chunks of HCH slots (all loads of a chunk in flight before
+    // any is consumed) and summed in slot order like the reference's sum over dim 1
+    f32x4 rit = {0.f, 0.f, 0.f, 0.f};
+    f32x4 hs = {0.f, 0.f, 0.f, 0.f};
+    int nnz = 0;
+    const int* pb = MODE == 1 ? p.pos + (size_t)b * (L + 1) : nullptr;
+    if (MODE == 0) {
+      if (item < 0 || item >= p.V) { bad = true; item = -1; }
+      if (item >= 0) rit = *reinterpret_cast<const f32x4*>(p.table + item * D + 4 * q);
+    } else {
+      const int pi = pb[0];
+      if (pi >= 0) rit = *reinterpret_cast<const f32x4*>(p.table + (size_t)pi * D + 4 * q);
+    }
+    for (int t0 = 0; t0 < L; t0 += HCH) {
+      f32x4 hist[HCH];
+#pragma unroll
+      for (int u = 0; u < HCH; ++u) {
+        hist[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        const int t = t0 + u;
+        if (t < L) {
+          if (MODE == 0) {
+            long long s = p.item_seq[(size_t)b * L + t];
+            if (s < 0 || s >= p.V) { bad = true; s = 0; }
+            if (s != 0) { hist[u] = *reinterpret_cast<const f32x4*>(p.table + s * D + 4 * q); ++nnz; }
+          } else {
+            const int ps = pb[t + 1];
+            if (ps >= 0) { hist[u] = *reinterpret_cast<const f32x4*>(p.table + (size_t)ps * D + 4 * q); ++nnz; }
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < HCH; ++u) hs += hist[u];
+    }
+    const f32x4 c1 = *reinterpret_cast<const f32x4*>(p.cate + lk * D + 4 * q);
+    const f32x4 c2 = *reinterpret_cast<const f32x4*>(p.cate + vw * D + 4 * q);
+    const f32x4 h = *reinterpret_cast<const f32x4*>(p.hmm + (size_t)b * D + 4 * q);
+    if (bad && q == 0) atomicOr(p.err, 1);
+
+    // ---------------- history masked mean
+    const float cnt = fmaxf((float)nnz, 1.f);
+    f32x4 x5 = hs / cnt;
+
+    // ---------------- mm field: LayerNorm(eps) + ReLU
+    float s1 = group_sum<G>(h[0] + h[1] + h[2] + h[3]);
+    const float mean = s1 / (float)D;
+    f32x4 dh = h - mean;
+    float s2 = group_sum<G>(dh[0] * dh[0] + dh[1] * dh[1] + dh[2] * dh[2] + dh[3] * dh[3]);
+    const float rstd = 1.f / sqrtf(s2 / (float)D + p.ln_eps);
+    const f32x4 g4 = *reinterpret_cast<const f32x4*>(p.ln_g + 4 * q);
+    const f32x4 bb4 = *reinterpret_cast<const f32x4*>(p.ln_b + 4 * q);
+    f32x4 x4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x4[e] = fmaxf(dh[e] * rstd * g4[e] + bb4[e], 0.f);
+
+    // ---------------- SENET
+    const f32x4 xs[5] = {c1, c2, rit, x4, x5};
+    float z[6];
+    z[0] = 0.f;
+#pragma unroll
+    for (int f = 0; f < 5; ++f) z[f + 1] = group_sum<G>(xs[f][0] + xs[f][1] + xs[f][2] + xs[f][3]) / (float)D;
+    float qv[FBN_MAXR], a[6];
+    senet_excite<D>(z, p.w1, p.b1, p.w2, p.b2, p.R, qv, a);
+
+    // ---------------- stores
+    float* Xb = p.X + (size_t)b * 5 * D + 4 * q;
+    float* Vb = p.Vc + (size_t)b * 5 * D + 4 * q;
+    float* cb = p.c + (size_t)b * p.ldc + 4 * q;
+#pragma unroll
+    for (int f = 0; f < 5; ++f) {
+      const f32x4 v = xs[f] * a[f + 1];
+      *reinterpret_cast<f32x4*>(Xb + f * D) = xs[f];
+      *reinterpret_cast<f32x4*>(Vb + f * D) = v;
+      *reinterpret_cast<f32x4*>(cb + f * D) = v;
+    }
+#pragma unroll
+    for (int f = 0; f < 6; ++f)
+      if (f % G == q) p.a_out[(size_t)b * 6 + f] = a[f];   // G may be < 6 (D = 16)
+    if (q == 0) p.cnt_out[b] = cnt;
+
+    // ---------------- sparse-grad map insert (rows that will receive a gradient)
+    if (MODE == 0 && p.map) {
+      for (int t = q; t <= L; t += G) {
+        long long r = (t == 0) ? item : p.item_seq[(size_t)b * L + (t - 1)];
+        if (r > 0 && r < p.V) map_insert(p.map, p.n_uniq, p.uniq_rows, (int)r);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ backward
+struct FieldBwdArgs {
+  const int64_t* item_id; const int64_t* item_seq; const int64_t* likes; const int64_t* views;
+  const float* hmm; const float* ln_g;
+  const float* w1; const float* b1; const float* w2;
+  const float* X;      // [B][5][D]
+  const float* a;      // [B][6]
+  const float* cnt;    // [B]
+  const float* dV;     // [B][5][D] total gradient wrt V_1..V_5
+  float* dhmm;         // [B][D] gradient wrt the pre-LN projection
+  float* partials;     // [gridDim.x][P]; P = 6R + R + 6R + 6 + 2D + n_cate*D
+  // table gradient, mode 0: dense (gtab[V][D]) if map == null, else sparse gU[u][D] via map
+  float* gtab; const int* map;
+  // mode 1: rows written to sendbuf at pos[b][t]
+  const int* pos; float* sendbuf;
+  long long V;
+  int B, L, R, n_cate;
+  float ln_eps;
+};
+
+__device__ __forceinline__ void atomic_add_row4(float* dst, const f32x4& v) {
+  atomicAdd(dst + 0, v[0]); atomicAdd(dst + 1, v[1]); atomicAdd(dst + 2, v[2]); atomicAdd(dst + 3, v[3]);
+}
+
+template <int D, int MODE>
+__global__ void __launch_bounds__(256) fields_bwd_kernel(FieldBwdArgs p) {
+  constexpr int G = D / 4;
+  constexpr int SPW = 64 / G;
+  extern __shared__ __attribute__((aligned(16))) float sp[];   // P floats of block partials
+  const int R = p.R;
+  const int P = 13 * R + 6 + 2 * D + p.n_cate * D;
+  float* s_w1 = sp;                 // [R][6]
+  float* s_b1 = s_w1 + 6 * R;       // [R]
+  float* s_w2 = s_b1 + R;           // [6][R]
+  float* s_b2 = s_w2 + 6 * R;       // [6]
+  float* s_lg = s_b2 + 6;           // [D]
+  float* s_lb = s_lg + D;           // [D]
+  float* s_ct = s_lb + D;           // [n_cate][D]
+  for (int i = threadIdx.x; i < P; i += blockDim.x) sp[i] = 0.f;
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int q = lane % G;
+  const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  const int L = p.L;
+
+  for (int b0 = gw * SPW; b0 < p.B; b0 += nwaves * SPW) {
+    const int b = b0 + lane / G;
+    if (b >= p.B) continue;
+    const float* Xb = p.X + (size_t)b * 5 * D + 4 * q;
+    const float* dVb = p.dV + (size_t)b * 5 * D + 4 * q;
+    f32x4 x[5], dv[5];
+#pragma unroll
+    for (int f = 0; f < 5; ++f) {
+      x[f] = *reinterpret_cast<const f32x4*>(Xb + f * D);
+      dv[f] = *reinterpret_cast<const f32x4*>(dVb + f * D);
+    }
+    float a[6];
+#pragma unroll
+    for (int f = 0; f < 6; ++f) a[f] = p.a[(size_t)b * 6 + f];
+    // recompute squeeze + hidden exactly as the forward did
+    float z[6];
+    z[0] = 0.f;
+#pragma unroll
+    for (int f = 0; f < 5; ++f) z[f + 1] = group_sum<G>(x[f][0] + x[f][1] + x[f][2] + x[f][3]) / (float)D;
+    float qv[FBN_MAXR];
+    for (int j = 0; j < R; ++j) {
+      float s = p.b1[j];
+#pragma unroll
+      for (int f = 0; f < 6; ++f) s += p.w1[j * 6 + f] * z[f];
+      qv[j] = s;
+    }
+    // excitation backward
+    float ds[6];
+    ds[0] = 0.f;   // da_0 = sum(dV_0 * X_0) = 0 since X_0 == 0
+#pragma unroll
+    for (int f = 0; f < 5; ++f) {
+      const float da = group_sum<G>(dv[f][0] * x[f][0] + dv[f][1] * x[f][1] + dv[f][2] * x[f][2] + dv[f][3] * x[f][3]);
+      ds[f + 1] = da * (1.f - a[f + 1]) * a[f + 1];
+    }
+    float dz[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < R; ++j) {
+      float dr = 0.f;
+#pragma unroll
+      for (int f = 0; f < 6; ++f) dr += p.w2[f * R + j] * ds[f];
+      const float rj = fmaxf(qv[j], 0.f);
+      const float dq = qv[j] > 0.f ? dr : 0.f;
+      if (q == 0) {
+#pragma unroll
+        for (int f = 0; f < 6; ++f) {
+          atomicAdd(&s_w2[f * R + j], ds[f] * rj);
+          atomicAdd(&s_w1[j * 6 + f], dq * z[f]);
+        }
+        atomicAdd(&s_b1[j], dq);
+      }
+#pragma unroll
+      for (int f = 0; f < 6; ++f) dz[f] += p.w1[j * 6 + f] * dq;
+    }
+    if (q == 0) {
+#pragma unroll
+      for (int f = 0; f < 6; ++f) atomicAdd(&s_b2[f], ds[f]);
+    }
+    f32x4 dx[5];
+#pragma unroll
+    for (int f = 0; f < 5; ++f) dx[f] = dv[f] * a[f + 1] + dz[f + 1] / (float)D;
+
+    // field 4: ReLU + LayerNorm backward -> d(h_mm)
+    {
+      const f32x4 h = *reinterpret_cast<const f32x4*>(p.hmm + (size_t)b * D + 4 * q);
+      const float mean = group_sum<G>(h[0] + h[1] + h[2] + h[3]) / (float)D;
+      const f32x4 dh = h - mean;
+      const float s2 = group_sum<G>(dh[0] * dh[0] + dh[1] * dh[1] + dh[2] * dh[2] + dh[3] * dh[3]);
+      const float rstd = 1.f / sqrtf(s2 / (float)D + p.ln_eps);
+      const f32x4 gam = *reinterpret_cast<const f32x4*>(p.ln_g + 4 * q);
+      f32x4 gl, xh, gx;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        gl[e] = x[3][e] > 0.f ? dx[3][e] : 0.f;
+        xh[e] = dh[e] * rstd;
+        gx[e] = gl[e] * gam[e];
+        atomicAdd(&s_lg[4 * q + e], gl[e] * xh[e]);
+        atomicAdd(&s_lb[4 * q + e], gl[e]);
+      }
+      const float m1 = group_sum<G>(gx[0] + gx[1] + gx[2] + gx[3]) / (float)D;
+      const float m2 = group_sum<G>(gx[0] * xh[0] + gx[1] * xh[1] + gx[2] * xh[2] + gx[3] * xh[3]) / (float)D;
+      f32x4 out;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) out[e] = rstd * (gx[e] - m1 - xh[e] * m2);
+      *reinterpret_cast<f32x4*>(p.dhmm + (size_t)b * D + 4 * q) = out;
+    }
+    // cate table (likes, views share one table)
+    {
+      long long lk = p.likes[b], vw = p.views[b];
+      if (lk >= 0 && lk < p.n_cate)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) atomicAdd(&s_ct[lk * D + 4 * q + e], dx[0][e]);
+      if (vw >= 0 && vw < p.n_cate)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) atomicAdd(&s_ct[vw * D + 4 * q + e], dx[1][e]);
+    }
+    // item table: dX3 -> row item_id, dX5 / count -> each non-padding history row
+    const f32x4 gh = dx[4] / p.cnt[b];
+    if (MODE == 0) {
+      const long long item = p.item_id[b];
+      if (item > 0 && item < p.V) {
+        float* dst = p.map ? p.gtab + (size_t)p.map[item] * D : p.gtab + item * D;
+        atomic_add_row4(dst + 4 * q, dx[2]);
+      }
+      for (int t = 0; t < L; ++t) {
+        const long long s = p.item_seq[(size_t)b * L + t];
+        if (s > 0 && s < p.V) {
+          float* dst = p.map ? p.gtab + (size_t)p.map[s] * D : p.gtab + s * D;
+          atomic_add_row4(dst + 4 * q, gh);
+        }
+      }
+    } else {
+      const int* pb = p.pos + (size_t)b * (L + 1);
+      if (pb[0] >= 0) *reinterpret_cast<f32x4*>(p.sendbuf + (size_t)pb[0] * D + 4 * q) = dx[2];
+      for (int t = 0; t < L; ++t)
+        if (pb[t + 1] >= 0) *reinterpret_cast<f32x4*>(p.sendbuf + (size_t)pb[t + 1] * D + 4 * q) = gh;
+    }
+  }
+  __syncthreads();
+  float* out = p.partials + (size_t)blockIdx.x * P;
+  for (int i = threadIdx.x; i < P; i += blockDim.x) out[i] = sp[i];
+}
+
+// Sum per-block partial slabs in block order: out[i] = sum_b part[b][i]  (deterministic)
+__global__ void reduce_partials_kernel(const float* part, int nblk, int P, float* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += part[(size_t)b * P + i];
+  out[i] = s;
+}
+
+// ------------------------------------------------------------------------------ C ABI
+static int fields_grid(int B, int D) {
+  const int spw = 64 / (D / 4);
+  const int waves = (B + spw - 1) / spw;
+  int blocks = (waves + 3) / 4;
+  return blocks < 1 ? 1 : (blocks > 1024 ? 1024 : blocks);
+}
+
+template <int MODE>
+static int launch_fields_fwd(const FieldArgs& a, int D, hipStream_t st) {
+  const int grid = fields_grid(a.B, D);
+  switch (D) {
+    case 16: hipLaunchKernelGGL((fields_fwd_kernel<16, MODE>), dim3(grid), dim3(256), 0, st, a); break;
+    case 32: hipLaunchKernelGGL((fields_fwd_kernel<32, MODE>), dim3(grid), dim3(256), 0, st, a); break;
+    case 64: hipLaunchKernelGGL((fields_fwd_kernel<64, MODE>), dim3(grid), dim3(256), 0, st, a); break;
+    case 128: hipLaunchKernelGGL((fields_fwd_kernel<128, MODE>), dim3(grid), dim3(256), 0, st, a); break;
+    case 256: hipLaunchKernelGGL((fields_fwd_kernel<256, MODE>), dim3(grid), dim3(256), 0, st, a); break;
+    default: fbn_set_error("fields: embedding_dim must be one of 16,32,64,128,256"); return FBN_ERR_UNSUPPORTED;
+  }
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+extern "C" int fbn_fields_fwd(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes,
+                              const int64_t* views, const float* hmm, const float* ln_g, const float* ln_b,
+                              float ln_eps, const float* cate, int n_cate, const float* table, long long V,
+                              const int* pos, const float* w1, const float* b1, const float* w2,
+                              const float* b2, int R, float* X, float* Vc, float* c, int ldc, float* a_out,
+                              float* cnt_out, int* err, int* map, int* n_uniq, int* uniq_rows, int B, int L,
+                              int D, void* stream) {
+  if (B <= 0) return FBN_OK;
+  if (L < 0 || L > 32 || R < 1 || R > FBN_MAXR || (ldc & 3)) {
+    fbn_set_error("fbn_fields_fwd: need 0 <= L <= 32, 1 <= R <= 8, ldc % 4 == 0");
+    return FBN_ERR_ARG;
+  }
+  FieldArgs a;
+  a.item_id = item_id; a.item_seq = L > 0 ? item_seq : nullptr; a.likes = likes; a.views = views;
+  a.hmm = hmm; a.ln_g = ln_g; a.ln_b = ln_b; a.cate = cate; a.table = table; a.pos = pos;
+  a.w1 = w1; a.b1 = b1; a.w2 = w2; a.b2 = b2;
+  a.X = X; a.Vc = Vc; a.c = c; a.a_out = a_out; a.cnt_out = cnt_out; a.err = err;
+  a.map = map; a.n_uniq = n_uniq; a.uniq_rows = uniq_rows;
+  a.V = V; a.B = B; a.L = L; a.ldc = ldc; a.R = R; a.n_cate = n_cate; a.ln_eps = ln_eps;
+  if (pos) return launch_fields_fwd<1>(a, D, (hipStream_t)stream);
+  return launch_fields_fwd<0>(a, D, (hipStream_t)stream);
+}
+
+extern "C" int fbn_fields_bwd_partials_size(int D, int R, int n_cate) { return 13 * R + 6 + 2 * D + n_cate * D; }
+extern "C" int fbn_fields_bwd_grid(int B, int D) { return fields_grid(B, D); }
+
+template <int MODE>
+static int launch_fields_bwd(const FieldBwdArgs& a, int D, hipStream_t st) {
+  const int grid = fields_grid(a.B, D);
+  const size_t lds = (size_t)(13 * a.R + 6 + 2 * D + a.n_cate * D) * sizeof(float);
+  switch (D) {
+    case 16: hipLaunchKernelGGL((fields_bwd_kernel<16, MODE>), dim3(grid), dim3(256), lds, st, a); break;
+    case 32: hipLaunchKernelGGL((fields_bwd_kernel<32, MODE>), dim3(grid), dim3(256), lds, st, a); break;
+    case 64: hipLaunchKernelGGL((fields_bwd_kernel<64, MODE>), dim3(grid), dim3(256), lds, st, a); break;
+    case 128: hipLaunchKernelGGL((fields_bwd_kernel<128, MODE>), dim3(grid), dim3(256), lds, st, a); break;
+    case 256: hipLaunchKernelGGL((fields_bwd_kernel<256, MODE>), dim3(grid), dim3(256), lds, st, a); break;
+    default: fbn_set_error("fields: embedding_dim must be one of 16,32,64,128,256"); return FBN_ERR_UNSUPPORTED;
+  }
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+// partials: [fbn_fields_bwd_grid(B,D)][fbn_fields_bwd_partials_size(D,R,n_cate)] scratch;
+// param_grads: [P] output in the order w1, b1, w2, b2, ln_g, ln_b, cate.
+extern "C" int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes,
+                              const int64_t* views, const float* hmm, const float* ln_g, float ln_eps,
+                              const float* w1, const float* b1, const float* w2, int R, int n_cate,
+                              const float* X, const float* a, const float* cnt, const float* dV, float* dhmm,
+                              float* partials, float* param_grads, float* gtab, const int* map, long long V,
+                              const int* pos, float* sendbuf, int B, int L, int D, void* stream) {
+  if (B <= 0) return FBN_OK;
+  if (L < 0 || L > 32 || R < 1 || R > FBN_MAXR) { fbn_set_error("fbn_fields_bwd: bad L/R"); return FBN_ERR_ARG; }
+  FieldBwdArgs p;
+  p.item_id = item_id; p.item_seq = L > 0 ? item_seq : nullptr; p.likes = likes; p.views = views;
+  p.hmm = hmm; p.ln_g = ln_g; p.w1 = w1; p.b1 = b1; p.w2 = w2;
+  p.X = X; p.a = a; p.cnt = cnt; p.dV = dV; p.dhmm = dhmm; p.partials = partials;
+  p.gtab = gtab; p.map = map; p.pos = pos; p.sendbuf = sendbuf;
+  p.V = V; p.B = B; p.L = L; p.R = R; p.n_cate = n_cate; p.ln_eps = ln_eps;
+  hipStream_t st = (hipStream_t)stream;
+  int rc = pos ? launch_fields_bwd<1>(p, D, st) : launch_fields_bwd<0>(p, D, st);
+  if (rc) return rc;
+  const int P = 13 * R + 6 + 2 * D + n_cate * D;
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(fbn_cdiv(P, 256)), dim3(256), 0, st, partials,
+                     fields_grid(B, D), P, param_grads);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}

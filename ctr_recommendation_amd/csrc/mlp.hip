@@ -1,0 +1,512 @@
+// K5 epilogue / K6 / K7: bilinear pair products, BatchNorm(+ReLU+dropout), sigmoid + BCE head.
+//
+// Bilinear "all" (model_fibinet.py:69-79): U_f = V_f W (an MFMA GEMM, gemm.hip), then
+// p_ij = V_i (.) U_j for 1 <= i < j <= 5 written straight into the compact MLP input
+// c = [V_1..V_5 | p_12 .. p_45].  Pairs (0, j) are identically zero because V_0 == 0
+// (:152) and their weight columns are skipped by the GEMM remap (DESIGN.md "zero columns").
+// Bilinear "each" (:81-86, opt-in): p_ij = (V_i W_i) (.) V_j, U_i = V_i W_i.
+//
+// BatchNorm follows ATen's CPU formulas so the fp32 path matches to rounding:
+//   train: two-pass mean / biased var in double, y = x * (invstd*g) + (b - mean*invstd*g),
+//          running stats with momentum and unbiased var;
+//   bwd:   dotp = sum (x-mean) dy, dx = (dy - sum(dy)/N - (x-mean) * dotp*invstd^2/N) * invstd * g.
+// ReLU and dropout are fused into the same elementwise pass.  Dropout keep-masks come from a
+// Philox4x32-10 stream keyed by (seed, offset) so the backward never stores them: the
+// backward factor is recovered from the stored activation (h_act > 0 <=> kept and positive).
+#include "common.h"
+
+// ------------------------------------------------------------------ bilinear pairs
+// pair index k enumerates (i,j), 1<=i<j<=5 lexicographically: (1,2)(1,3)(1,4)(1,5)(2,3)...(4,5)
+__constant__ int c_pi[10] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3};
+__constant__ int c_pj[10] = {1, 2, 3, 4, 2, 3, 4, 3, 4, 4};
+
+// mode 0 ("all"): p = V_i * U_j ; mode 1 ("each"): p = U_i * V_j   (field indices 0..4 = fields 1..5)
+__global__ void pairs_fwd_kernel(const float* __restrict__ Vc, const float* __restrict__ U, float* __restrict__ c,
+                                 int B, int D, int ldc, int mode) {
+  const int q4 = D / 4;
+  const size_t total = (size_t)B * q4;
+  for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
+    const int b = (int)(idx / q4), col = (int)(idx % q4) * 4;
+    f32x4 v[5], u[5];
+#pragma unroll
+    for (int f = 0; f < 5; ++f) {
+      v[f] = *reinterpret_cast<const f32x4*>(Vc + ((size_t)b * 5 + f) * D + col);
+      u[f] = *reinterpret_cast<const f32x4*>(U + ((size_t)b * 5 + f) * D + col);
+    }
+    float* out = c + (size_t)b * ldc + 5 * D + col;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      const f32x4 pr = mode == 0 ? v[c_pi[k]] * u[c_pj[k]] : u[c_pi[k]] * v[c_pj[k]];
+      *reinterpret_cast<f32x4*>(out + k * D) = pr;
+    }
+  }
+}
+
+// dV (out) = dc_V + sum of pair-grad terms that land on V ; dU (out) = pair-grad terms that land on U
+__global__ void pairs_bwd_kernel(const float* __restrict__ dc, const float* __restrict__ Vc, const float* __restrict__ U,
+                                 float* __restrict__ dV, float* __restrict__ dU, int B, int D, int ldc, int mode) {
+  const int q4 = D / 4;
+  const size_t total = (size_t)B * q4;
+  for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
+    const int b = (int)(idx / q4), col = (int)(idx % q4) * 4;
+    f32x4 v[5], u[5], gv[5], gu[5];
+    const float* dcb = dc + (size_t)b * ldc + col;
+#pragma unroll
+    for (int f = 0; f < 5; ++f) {
+      v[f] = *reinterpret_cast<const f32x4*>(Vc + ((size_t)b * 5 + f) * D + col);
+      u[f] = *reinterpret_cast<const f32x4*>(U + ((size_t)b * 5 + f) * D + col);
+      gv[f] = *reinterpret_cast<const f32x4*>(dcb + f * D);
+      gu[f] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      const f32x4 g = *reinterpret_cast<const f32x4*>(dcb + (5 + k) * D);
+      const int i = c_pi[k], j = c_pj[k];
+      if (mode == 0) { gv[i] += g * u[j]; gu[j] += g * v[i]; }
+      else { gu[i] += g * v[j]; gv[j] += g * u[i]; }
+    }
+#pragma unroll
+    for (int f = 0; f < 5; ++f) {
+      *reinterpret_cast<f32x4*>(dV + ((size_t)b * 5 + f) * D + col) = gv[f];
+      *reinterpret_cast<f32x4*>(dU + ((size_t)b * 5 + f) * D + col) = gu[f];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ column statistics
+// Partial column sums over a chunk of rows: part[chunk][c] (double).  mode 0: sum x ;
+// mode 1: sum (x - mean[c])^2.  Block = 256 threads covering 64 columns x 4 row lanes.
+__global__ void colstat_partial_kernel(const float* __restrict__ X, int B, int C, int ldx, int rows_per_chunk,
+                                       const double* __restrict__ mean, double* __restrict__ part, int mode) {
+  __shared__ double red[4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rl = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * rows_per_chunk, r1 = min(B, r0 + rows_per_chunk);
+  double s = 0.0;
+  if (col < C) {
+    const double mu = mode ? mean[col] : 0.0;
+    for (int r = r0 + rl; r < r1; r += 4) {
+      const double x = (double)X[(size_t)r * ldx + col];
+      s += mode ? (x - mu) * (x - mu) : x;
+    }
+  }
+  red[rl][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rl == 0 && col < C)
+    part[(size_t)blockIdx.y * C + col] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+
+// out[c] = sum_k part[k][c]   (fixed chunk order: deterministic)
+__global__ void chunk_reduce_kernel(const double* part, int nchunk, int C, double* out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0;
+  for (int k = 0; k < nchunk; ++k) s += part[(size_t)k * C + c];
+  out[c] = s;
+}
+
+__global__ void bn_mean_kernel(const double* sum, double ntot, int C, double* mean) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < C) mean[c] = sum[c] / ntot;
+}
+
+// finalize BN train stats from the (global) sum of squared deviations: invstd, float mean,
+// running-stat update (momentum, unbiased var)
+__global__ void bn_finalize_kernel(const double* m2, const double* mean_d, double ntot, int C, float* mean,
+                                   float* invstd, float* run_mean, float* run_var, float momentum, float eps,
+                                   int update_running) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double s = m2[c];
+  const float var_b = (float)(s / ntot);
+  mean[c] = (float)mean_d[c];
+  invstd[c] = 1.f / sqrtf(var_b + eps);
+  if (update_running) {
+    const float unb = ntot > 1.0 ? (float)(s / (ntot - 1.0)) : var_b;
+    run_mean[c] = momentum * (float)mean_d[c] + (1.f - momentum) * run_mean[c];
+    run_var[c] = momentum * unb + (1.f - momentum) * run_var[c];
+  }
+}
+
+__global__ void bn_eval_params_kernel(const float* run_mean, const float* run_var, float* mean, float* invstd,
+                                      int C, float eps) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  mean[c] = run_mean[c];
+  invstd[c] = 1.f / sqrtf(run_var[c] + eps);
+}
+
+// y = relu(x*alpha + beta'), alpha = invstd*g, beta' = b - mean*alpha ; then dropout (train)
+__global__ void bn_act_fwd_kernel(const float* __restrict__ X, float* __restrict__ Y, int B, int C,
+                                  const float* __restrict__ mean, const float* __restrict__ invstd,
+                                  const float* __restrict__ g, const float* __restrict__ bta, float p_drop,
+                                  const unsigned long long* __restrict__ rng, unsigned stream_id,
+                                  unsigned char* __restrict__ mask_out) {
+  const size_t total4 = (size_t)B * C / 4;
+  const float keep = 1.f - p_drop;
+  const float scale = p_drop > 0.f ? 1.0f / keep : 1.f;
+  uint32_t k0 = 0, k1 = 0, off = 0;
+  if (rng) { k0 = (uint32_t)rng[0]; k1 = (uint32_t)(rng[0] >> 32); off = (uint32_t)rng[1]; }
+  for (size_t i4 = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i4 < total4; i4 += (size_t)gridDim.x * blockDim.x) {
+    const size_t i = i4 * 4;
+    const int col = (int)(i % C);
+    f32x4 x = *reinterpret_cast<const f32x4*>(X + i);
+    f32x4 y;
+    float um[4] = {1.f, 1.f, 1.f, 1.f};
+    if (p_drop > 0.f) {
+      const Philox4 r = philox4x32_10((uint32_t)i4, (uint32_t)(i4 >> 32), stream_id, off, k0, k1);
+      um[0] = u01(r.x); um[1] = u01(r.y); um[2] = u01(r.z); um[3] = u01(r.w);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float alpha = invstd[col + e] * g[col + e];
+      const float bp = bta[col + e] - mean[col + e] * alpha;
+      float v = fmaxf(x[e] * alpha + bp, 0.f);
+      if (p_drop > 0.f) {
+        const bool kept = um[e] < keep;
+        v = kept ? v * scale : 0.f;
+        if (mask_out) mask_out[i + e] = kept ? 1 : 0;
+      }
+      y[e] = v;
+    }
+    *reinterpret_cast<f32x4*>(Y + i) = y;
+  }
+}
+
+// ------------------------------------------------------------------ BN backward
+// dy[b][c] = G[b][c] * fac(hact)  (matrix source)  or  gvec[b] * w[c] * fac(hact)  (rank-1 head source)
+// fac = scale if hact > 0 else 0  (ReLU-after-BN + dropout recovered from the stored activation)
+struct BnBwdSrc {
+  const float* G;      // [B][C] or null
+  const float* gvec;   // [B] (rank-1 source)
+  const float* w;      // [C]
+  const float* hact;   // [B][C]
+  float scale;
+};
+__device__ __forceinline__ float bn_dy(const BnBwdSrc& s, int b, int c, int C) {
+  const size_t i = (size_t)b * C + c;
+  const float d = s.G ? s.G[i] : s.gvec[b] * s.w[c];
+  return s.hact[i] > 0.f ? d * s.scale : 0.f;
+}
+
+// partials over row chunks: part0 = sum dy, part1 = sum (x-mean)*dy, part2 (rank-1 only) = sum gvec*hact
+__global__ void bn_bwd_partial_kernel(BnBwdSrc s, const float* __restrict__ Xpre, const float* __restrict__ mean,
+                                      int B, int C, int rows_per_chunk, double* part) {
+  __shared__ double red[3][4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rl = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * rows_per_chunk, r1 = min(B, r0 + rows_per_chunk);
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+  if (c < C) {
+    const float mu = mean[c];
+    for (int r = r0 + rl; r < r1; r += 4) {
+      const float dy = bn_dy(s, r, c, C);
+      s0 += dy;
+      s1 += (double)((Xpre[(size_t)r * C + c] - mu) * dy);
+      if (!s.G) s2 += (double)(s.gvec[r] * s.hact[(size_t)r * C + c]);
+    }
+  }
+  red[0][rl][threadIdx.x & 63] = s0;
+  red[1][rl][threadIdx.x & 63] = s1;
+  red[2][rl][threadIdx.x & 63] = s2;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    const int t = threadIdx.x;
+    double* pp = part + (size_t)blockIdx.y * 3 * C;
+    pp[c] = red[0][0][t] + red[0][1][t] + red[0][2][t] + red[0][3][t];
+    pp[C + c] = red[1][0][t] + red[1][1][t] + red[1][2][t] + red[1][3][t];
+    pp[2 * C + c] = red[2][0][t] + red[2][1][t] + red[2][2][t] + red[2][3][t];
+  }
+}
+
+// red = {sum dy, sum (x-mean) dy, sum gvec*hact} (global sums, [3][C]).
+// coef[c] = {gm = sum dy / N, k = dotp * invstd^2 / N}; dgamma = dotp*invstd, dbeta = sum dy; dw = sum gvec*hact
+__global__ void bn_bwd_finalize_kernel(const double* red, int C, double ntot, const float* invstd, float* coef,
+                                       float* dgamma, float* dbeta, float* dw) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float is = invstd[c];
+  const float sdy = (float)red[c], dotp = (float)red[C + c];
+  coef[c] = sdy / (float)ntot;
+  coef[C + c] = dotp * is * is / (float)ntot;
+  if (dgamma) dgamma[c] = dotp * is;
+  if (dbeta) dbeta[c] = sdy;
+  if (dw) dw[c] = (float)red[2 * C + c];
+}
+
+__global__ void bn_bwd_apply_kernel(BnBwdSrc s, const float* __restrict__ Xpre, const float* __restrict__ mean,
+                                    const float* __restrict__ invstd, const float* __restrict__ g,
+                                    const float* __restrict__ coef, float* __restrict__ dX, int B, int C) {
+  const size_t total = (size_t)B * C;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int b = (int)(i / C), c = (int)(i % C);
+    const float dy = bn_dy(s, b, c, C);
+    dX[i] = (dy - coef[c] - (Xpre[i] - mean[c]) * coef[C + c]) * invstd[c] * g[c];
+  }
+}
+
+// ------------------------------------------------------------------ column sums (bias grads)
+__global__ void colsum_partial_kernel(const float* __restrict__ X, int B, int C, int ldx, int rows_per_chunk,
+                                      float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rl = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * rows_per_chunk, r1 = min(B, r0 + rows_per_chunk);
+  float s = 0.f;
+  if (c < C)
+    for (int r = r0 + rl; r < r1; r += 4) s += X[(size_t)r * ldx + c];
+  red[rl][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rl == 0 && c < C)
+    part[(size_t)blockIdx.y * C + c] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+__global__ void colsum_final_kernel(const float* part, int nchunk, int C, float* out, float beta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int k = 0; k < nchunk; ++k) s += part[(size_t)k * C + c];
+  out[c] = beta != 0.f ? out[c] * beta + s : s;
+}
+
+// ------------------------------------------------------------------ head: o = h.w + b, p = sigmoid(o), BCE
+// one wave per row.  gout[b] = dL/do when labels are given (mean BCE over `denom` samples),
+// using ATen's BCE backward ((p-t)/max((1-p)p, 1e-12)/N) followed by sigmoid backward (g(1-p)p).
+__global__ void head_fwd_kernel(const float* __restrict__ H, const float* __restrict__ w, const float* __restrict__ bias,
+                                int B, int C, float* __restrict__ logits, float* __restrict__ probs,
+                                const float* __restrict__ labels, float* __restrict__ loss_terms,
+                                float* __restrict__ gout, float denom) {
+  const int lane = threadIdx.x & 63;
+  const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (row >= B) return;
+  float s = 0.f;
+  for (int c = lane * 4; c < C; c += 256) {
+    const f32x4 h = *reinterpret_cast<const f32x4*>(H + (size_t)row * C + c);
+    const f32x4 ww = *reinterpret_cast<const f32x4*>(w + c);
+    s += h[0] * ww[0] + h[1] * ww[1] + h[2] * ww[2] + h[3] * ww[3];
+  }
+  s = wave_sum(s);
+  if (lane == 0) {
+    const float o = s + bias[0];
+    const float pr = 1.f / (1.f + expf(-o));
+    if (logits) logits[row] = o;
+    if (probs) probs[row] = pr;
+    if (labels) {
+      const float t = labels[row];
+      const float lp = fmaxf(logf(pr), -100.f), l1p = fmaxf(logf(1.f - pr), -100.f);
+      if (loss_terms) loss_terms[row] = -(t * lp + (1.f - t) * l1p);
+      if (gout) {
+        const float gp = ((pr - t) / fmaxf((1.f - pr) * pr, 1e-12f)) / denom;
+        gout[row] = gp * (1.f - pr) * pr;
+      }
+    }
+  }
+}
+
+// sigmoid backward only (drop-in mode: torch computes BCE and hands us dL/dp)
+__global__ void sigmoid_bwd_kernel(const float* gp, const float* probs, float* gout, int B) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < B) gout[i] = gp[i] * (1.f - probs[i]) * probs[i];
+}
+
+// dH[b][c] = g[b] * w[c]   (rank-1; used by the drop-in backward)
+__global__ void outer_kernel(const float* g, const float* w, float* out, int B, int C) {
+  const size_t total = (size_t)B * C;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x)
+    out[i] = g[i / C] * w[i % C];
+}
+
+__global__ void sum_kernel(const float* x, int n, float* out, float scale) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += x[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = red[0] * scale;
+}
+
+// ------------------------------------------------------------------ C ABI
+static int ew_grid(size_t n) {
+  size_t g = (n + 255) / 256;
+  return (int)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
+}
+static int row_chunks(int B) {
+  int ch = (B + 127) / 128;
+  return ch < 1 ? 1 : (ch > 256 ? 256 : ch);
+}
+
+extern "C" int fbn_pairs_fwd(const float* Vc, const float* U, float* c, int B, int D, int ldc, int mode, void* stream) {
+  if (B <= 0) return FBN_OK;
+  if ((D & 3) || (ldc & 3)) { fbn_set_error("pairs: D and ldc must be multiples of 4"); return FBN_ERR_ARG; }
+  hipLaunchKernelGGL(pairs_fwd_kernel, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream, Vc, U, c,
+                     B, D, ldc, mode);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+extern "C" int fbn_pairs_bwd(const float* dc, const float* Vc, const float* U, float* dV, float* dU, int B, int D,
+                             int ldc, int mode, void* stream) {
+  if (B <= 0) return FBN_OK;
+  hipLaunchKernelGGL(pairs_bwd_kernel, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream, dc, Vc, U,
+                     dV, dU, B, D, ldc, mode);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+// workspace for the BN entry points: chunk partials [nchunk][3][C] doubles + 4*C doubles of scratch
+extern "C" size_t fbn_bn_workspace_size(int B, int C) { return ((size_t)row_chunks(B) * 3 * C + 4 * (size_t)C) * sizeof(double); }
+
+// Local column pass over this rank's rows: out_d[c] = sum_b X[b][c]  (mean_d == null)
+//                                       or  out_d[c] = sum_b (X[b][c] - mean_d[c])^2
+extern "C" int fbn_bn_stats_pass(const float* X, int B, int C, const double* mean_d, double* out_d, void* ws,
+                                 void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const int nch = row_chunks(B), rpc = B > 0 ? (B + nch - 1) / nch : 1;
+  double* part = (double*)ws;
+  hipLaunchKernelGGL(colstat_partial_kernel, dim3(fbn_cdiv(C, 64), nch), dim3(256), 0, st, X, B, C, C, rpc, mean_d,
+                     part, mean_d ? 1 : 0);
+  hipLaunchKernelGGL(chunk_reduce_kernel, dim3(fbn_cdiv(C, 256)), dim3(256), 0, st, part, nch, C, out_d);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+extern "C" int fbn_bn_mean(const double* sum_d, double ntot, int C, double* mean_d, void* stream) {
+  hipLaunchKernelGGL(bn_mean_kernel, dim3(fbn_cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, sum_d, ntot, C, mean_d);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+extern "C" int fbn_bn_finalize(const double* m2_d, const double* mean_d, double ntot, int C, float* mean,
+                               float* invstd, float* run_mean, float* run_var, float momentum, float eps,
+                               int update_running, void* stream) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(fbn_cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, m2_d, mean_d, ntot,
+                     C, mean, invstd, run_mean, run_var, momentum, eps, update_running);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+// single-process convenience: both passes + finalize (ws >= fbn_bn_workspace_size)
+extern "C" int fbn_bn_stats(const float* X, int B, int C, float* mean, float* invstd, float* run_mean, float* run_var,
+                            float momentum, float eps, int update_running, void* ws, void* stream) {
+  if (B <= 0) return FBN_OK;
+  double* scratch = (double*)ws + (size_t)row_chunks(B) * 3 * C;
+  double* sum_d = scratch;
+  double* mean_d = scratch + C;
+  int rc = fbn_bn_stats_pass(X, B, C, nullptr, sum_d, ws, stream);
+  if (!rc) rc = fbn_bn_mean(sum_d, (double)B, C, mean_d, stream);
+  if (!rc) rc = fbn_bn_stats_pass(X, B, C, mean_d, sum_d, ws, stream);
+  if (!rc) rc = fbn_bn_finalize(sum_d, mean_d, (double)B, C, mean, invstd, run_mean, run_var, momentum, eps,
+                                update_running, stream);
+  return rc;
+}
+
+extern "C" int fbn_bn_eval_params(const float* run_mean, const float* run_var, float* mean, float* invstd, int C,
+                                  float eps, void* stream) {
+  hipLaunchKernelGGL(bn_eval_params_kernel, dim3(fbn_cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, run_mean,
+                     run_var, mean, invstd, C, eps);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+// rng: device [seed, offset] (uint64 x2) or null; mask_out (optional, u8 [B][C]) for parity tests
+extern "C" int fbn_bn_act_fwd(const float* X, float* Y, int B, int C, const float* mean, const float* invstd,
+                              const float* g, const float* b, float p_drop, const unsigned long long* rng,
+                              unsigned stream_id, unsigned char* mask_out, void* stream) {
+  if (B <= 0) return FBN_OK;
+  if (C & 3) { fbn_set_error("bn_act: C % 4"); return FBN_ERR_ARG; }
+  if (p_drop > 0.f && !rng) { fbn_set_error("bn_act: dropout needs an rng state"); return FBN_ERR_ARG; }
+  hipLaunchKernelGGL(bn_act_fwd_kernel, dim3(ew_grid((size_t)B * C / 4)), dim3(256), 0, (hipStream_t)stream, X, Y, B,
+                     C, mean, invstd, g, b, p_drop, rng, stream_id, mask_out);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+// BN(+ReLU+dropout) backward, stage 1: local sums red_d[3][C] = {sum dy, sum (x-mean) dy, sum gvec*hact}.
+// Source of dL/d(act): G (matrix) or gvec (x) w (rank-1 head).
+extern "C" int fbn_bn_bwd_reduce(const float* G, const float* gvec, const float* w, const float* hact, float scale,
+                                 const float* Xpre, const float* mean, int B, int C, double* red_d, void* ws,
+                                 void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  BnBwdSrc s{G, gvec, w, hact, scale};
+  const int nch = row_chunks(B), rpc = B > 0 ? (B + nch - 1) / nch : 1;
+  double* part = (double*)ws;
+  hipLaunchKernelGGL(bn_bwd_partial_kernel, dim3(fbn_cdiv(C, 64), nch), dim3(256), 0, st, s, Xpre, mean, B, C, rpc, part);
+  hipLaunchKernelGGL(chunk_reduce_kernel, dim3(fbn_cdiv(3 * C, 256)), dim3(256), 0, st, part, nch, 3 * C, red_d);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+// stage 2 (after an optional all-reduce of red_d): dXpre, dgamma, dbeta, dw (rank-1 only)
+extern "C" int fbn_bn_bwd_apply(const float* G, const float* gvec, const float* w, const float* hact, float scale,
+                                const float* Xpre, const float* mean, const float* invstd, const float* gamma, int B,
+                                int C, const double* red_d, double ntot, float* dXpre, float* dgamma, float* dbeta,
+                                float* dw, void* ws, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  BnBwdSrc s{G, gvec, w, hact, scale};
+  float* coef = (float*)((double*)ws + (size_t)row_chunks(B) * 3 * C + 3 * (size_t)C);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(fbn_cdiv(C, 256)), dim3(256), 0, st, red_d, C, ntot, invstd, coef,
+                     dgamma, dbeta, G ? nullptr : dw);
+  if (B > 0)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid((size_t)B * C)), dim3(256), 0, st, s, Xpre, mean, invstd,
+                       gamma, coef, dXpre, B, C);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+extern "C" int fbn_bn_bwd(const float* G, const float* gvec, const float* w, const float* hact, float scale,
+                          const float* Xpre, const float* mean, const float* invstd, const float* gamma, int B, int C,
+                          float* dXpre, float* dgamma, float* dbeta, float* dw, void* ws, void* stream) {
+  if (B <= 0) return FBN_OK;
+  double* red = (double*)ws + (size_t)row_chunks(B) * 3 * C;   // 3*C doubles
+  int rc = fbn_bn_bwd_reduce(G, gvec, w, hact, scale, Xpre, mean, B, C, red, ws, stream);
+  if (!rc) rc = fbn_bn_bwd_apply(G, gvec, w, hact, scale, Xpre, mean, invstd, gamma, B, C, red, (double)B, dXpre,
+                                 dgamma, dbeta, dw, ws, stream);
+  return rc;
+}
+
+extern "C" size_t fbn_colsum_workspace_size(int B, int C) { return (size_t)row_chunks(B) * C * sizeof(float); }
+
+// out[c] = beta*out[c] + sum_b X[b][c]
+extern "C" int fbn_colsum(const float* X, int B, int C, int ldx, float* out, float beta, void* ws, void* stream) {
+  if (B <= 0) return FBN_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int nch = row_chunks(B), rpc = (B + nch - 1) / nch;
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3(fbn_cdiv(C, 64), nch), dim3(256), 0, st, X, B, C, ldx, rpc, (float*)ws);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(fbn_cdiv(C, 256)), dim3(256), 0, st, (const float*)ws, nch, C, out, beta);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+extern "C" int fbn_head_fwd(const float* H, const float* w, const float* bias, int B, int C, float* logits,
+                            float* probs, const float* labels, float* loss_terms, float* gout, float denom,
+                            void* stream) {
+  if (B <= 0) return FBN_OK;
+  if (C & 3) { fbn_set_error("head: C % 4"); return FBN_ERR_ARG; }
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(fbn_cdiv((long long)B * 64, 256)), dim3(256), 0, (hipStream_t)stream, H, w,
+                     bias, B, C, logits, probs, labels, loss_terms, gout, denom);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+extern "C" int fbn_sigmoid_bwd(const float* gp, const float* probs, float* gout, int B, void* stream) {
+  if (B <= 0) return FBN_OK;
+  hipLaunchKernelGGL(sigmoid_bwd_kernel, dim3(fbn_cdiv(B, 256)), dim3(256), 0, (hipStream_t)stream, gp, probs, gout, B);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+extern "C" int fbn_outer(const float* g, const float* w, float* out, int B, int C, void* stream) {
+  if (B <= 0) return FBN_OK;
+  hipLaunchKernelGGL(outer_kernel, dim3(ew_grid((size_t)B * C)), dim3(256), 0, (hipStream_t)stream, g, w, out, B, C);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+extern "C" int fbn_sum(const float* x, int n, float* out, float scale, void* stream) {
+  hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, x, n, out, scale);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}

@@ -1,0 +1,81 @@
+"""MicroLens-shaped synthetic batches for tests and the benchmark.
+
+The batch_dict contract is the reference collator's (src/dataloader.py:69-121):
+``item_id`` [B] int64, ``item_seq`` [B, max_len] int64 (the LAST max_len items, left-padded
+with 0), ``likes_level`` / ``views_level`` [B] int64 in [0, 10], ``user_id`` [B] int64
+(unused by the model), ``item_emb_d128`` [B, 128] float32; labels [B] float32.
+
+Generation (seeded, numpy ``default_rng``):
+* item_id ~ U[1, V); history: n_valid ~ U{0..L}, left-padded, valid slots ~ U[1, V);
+* likes/views ~ U{0..10}; user_id ~ U[1, 20000);
+* item_emb_d128: N(0,1) rows L2-normalised (mimics Notebooks/task-1.ipynb:237-239);
+* label ~ Bernoulli(sigmoid(score)), score a fixed hash of (item_id mod 97, likes, views) plus
+  a term in the mm vector, so that AUC is non-trivial.
+"""
+from __future__ import annotations
+
+from typing import Dict, Tuple
+
+import numpy as np
+import torch
+
+
+def make_batch_np(rng: np.random.Generator, B: int, V: int, L: int = 20, n_cate: int = 11,
+                  zipf: float = 0.0) -> Tuple[Dict[str, np.ndarray], np.ndarray]:
+    if zipf > 0:
+        item = (rng.zipf(1.0 + zipf, size=B) % (V - 1)) + 1
+    else:
+        item = rng.integers(1, V, size=B)
+    n_valid = rng.integers(0, L + 1, size=B)
+    hist = rng.integers(1, V, size=(B, L))
+    slot = np.arange(L)[None, :]
+    seq = np.where(slot >= (L - n_valid)[:, None], hist, 0)        # left-padded
+    likes = rng.integers(0, n_cate, size=B)
+    views = rng.integers(0, n_cate, size=B)
+    user = rng.integers(1, 20000, size=B)
+    mm = rng.standard_normal((B, 128)).astype(np.float32)
+    mm /= np.linalg.norm(mm, axis=1, keepdims=True)
+    score = (((item % 97) * 7 + likes * 3 - views * 2) % 11 - 5) / 2.5 + 2.0 * mm[:, 0]
+    label = (rng.random(B) < 1.0 / (1.0 + np.exp(-score))).astype(np.float32)
+    batch = {
+        "item_id": item.astype(np.int64),
+        "item_seq": seq.astype(np.int64),
+        "likes_level": likes.astype(np.int64),
+        "views_level": views.astype(np.int64),
+        "user_id": user.astype(np.int64),
+        "item_emb_d128": mm,
+    }
+    return batch, label
+
+
+def to_torch(batch: Dict[str, np.ndarray], label: np.ndarray, device="cpu"):
+    return {k: torch.from_numpy(np.ascontiguousarray(v)).to(device) for k, v in batch.items()}, \
+        torch.from_numpy(label).to(device)
+
+
+def make_batch(seed: int, B: int, V: int, L: int = 20, device="cpu", zipf: float = 0.0):
+    rng = np.random.default_rng(seed)
+    b, y = make_batch_np(rng, B, V, L, zipf=zipf)
+    return to_torch(b, y, device)
+
+
+def make_device_batches(n: int, B: int, V: int, L: int, device, seed: int = 2025):
+    """Pre-generate ``n`` batches directly on the device (benchmark input, HBM-resident)."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    out = []
+    for _ in range(n):
+        item = torch.randint(1, V, (B,), generator=g, device=device, dtype=torch.int64)
+        n_valid = torch.randint(0, L + 1, (B,), generator=g, device=device)
+        hist = torch.randint(1, V, (B, L), generator=g, device=device, dtype=torch.int64)
+        slot = torch.arange(L, device=device)[None, :]
+        seq = torch.where(slot >= (L - n_valid)[:, None], hist, torch.zeros_like(hist))
+        likes = torch.randint(0, 11, (B,), generator=g, device=device, dtype=torch.int64)
+        views = torch.randint(0, 11, (B,), generator=g, device=device, dtype=torch.int64)
+        mm = torch.randn((B, 128), generator=g, device=device)
+        mm = mm / mm.norm(dim=1, keepdim=True)
+        score = (((item % 97) * 7 + likes * 3 - views * 2) % 11 - 5).float() / 2.5 + 2.0 * mm[:, 0]
+        label = (torch.rand((B,), generator=g, device=device) < torch.sigmoid(score)).float()
+        out.append(({"item_id": item, "item_seq": seq, "likes_level": likes, "views_level": views,
+                     "item_emb_d128": mm.contiguous()}, label))
+    return out

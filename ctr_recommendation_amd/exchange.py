@@ -1,0 +1,130 @@
+"""Row-sharded item table exchange over torch.distributed (RCCL on MI355X, gloo in CPU tests).
+
+One process per GPU.  The item table E (V x d) is split into contiguous row blocks of
+``Vl = ceil(V / world)`` rows (owner = id // Vl).  Replaces the reference's
+``torch.nn.DataParallel`` (src/train_fibinet.py:69-70), which broadcast the whole table to
+every GPU and reduced its dense gradient back every step.
+
+Forward  (requester -> owner -> requester):
+  route (ids -> per-owner int32 local rows + pos[b][t])  ->  all_to_all(counts)  ->
+  all_to_all(ids)  ->  owner gather (+ register rows for the sparse gradient)  ->
+  all_to_all(rows)  ->  fields_fwd reads rows[pos]
+Backward (the sparse reduce-scatter):
+  fields_bwd writes one gradient row per routed entry  ->  all_to_all(rows)  ->
+  owner scatter-add into its compact gradient rows.
+Split sizes need one host read of the N routed counts per step (all_to_all_single takes
+host split lists); everything else stays on the device.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from ._lib import call, ptr
+
+
+class HipExchangeKernels:
+    """Device kernels of the exchange (exchange.hip)."""
+
+    def route(self, item, seq, B, L, V, Vl, world, counts, offsets, cursor, send_ids, pos, err):
+        call("fbn_route", ptr(item), ptr(seq), B, L, V, Vl, world, ptr(counts), ptr(offsets), ptr(cursor),
+             ptr(send_ids), ptr(pos), ptr(err), _lib.stream_handle(item.device))
+
+    def owner_gather(self, ids, E, out, map_, n_uniq, uniq_rows, rank, d):
+        call("fbn_owner_gather", ptr(ids), ids.shape[0], ptr(E), ptr(out), ptr(map_), ptr(n_uniq), ptr(uniq_rows),
+             rank, d, _lib.stream_handle(E.device))
+
+    def owner_scatter(self, ids, grad, map_, gU, rank, d):
+        call("fbn_owner_scatter", ptr(ids), ids.shape[0], ptr(grad), ptr(map_), ptr(gU), rank, d,
+             _lib.stream_handle(gU.device))
+
+
+class RowExchange:
+    def __init__(self, rank: int, world: int, V: int, d: int, B: int, L: int, device, group=None, kernels=None,
+                 stage_on_cpu: bool = False):
+        self.rank, self.world, self.V, self.d, self.L = rank, world, V, d, L
+        self.Vl = (V + world - 1) // world
+        self.group = group
+        self.k = kernels or HipExchangeKernels()
+        self.device = device
+        self.stage_on_cpu = stage_on_cpu          # gloo on a GPU box: collectives on host copies
+        i32 = dict(dtype=torch.int32, device=device)
+        self.counts = torch.zeros(world, **i32)
+        self.offsets = torch.zeros(world + 1, **i32)
+        self.cursor = torch.zeros(world, **i32)
+        self.send_ids = torch.empty(B * (L + 1), **i32)
+        self.pos = torch.empty((B, L + 1), **i32)
+        self.send_counts = None
+        self.recv_counts = None
+        self.recv_ids = None
+
+    @property
+    def rows_lo(self) -> int:
+        return self.rank * self.Vl
+
+    @property
+    def rows_local(self) -> int:
+        return max(0, min(self.V, (self.rank + 1) * self.Vl) - self.rows_lo)
+
+    def _a2a(self, out, inp, out_splits, in_splits):
+        if not self.stage_on_cpu:
+            dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+            return out
+        o = out.cpu()
+        dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=self.group)
+        out.copy_(o)
+        return out
+
+    def forward(self, item, seq, E_local, sparse, err) -> torch.Tensor:
+        """Returns the requester's row buffer [n_sent, d]; self.pos maps (b, t) -> row (or -1)."""
+        B = item.shape[0]
+        L = 0 if seq is None else seq.shape[1]
+        pos = self.pos[:B, :L + 1] if L == self.L else torch.empty((B, L + 1), dtype=torch.int32, device=item.device)
+        self.cur_pos = pos.contiguous()
+        self.k.route(item, seq, B, L, self.V, self.Vl, self.world, self.counts, self.offsets, self.cursor,
+                     self.send_ids, self.cur_pos, err)
+        recv_counts = torch.empty_like(self.counts)
+        self._a2a(recv_counts, self.counts, None, None)
+        sc = self.counts.tolist()
+        rc = recv_counts.tolist()                  # the one host sync of the step
+        self.send_counts, self.recv_counts = sc, rc
+        n_send, n_recv = sum(sc), sum(rc)
+        self.recv_ids = torch.empty(n_recv, dtype=torch.int32, device=item.device)
+        self._a2a(self.recv_ids, self.send_ids[:n_send], rc, sc)
+        reply = torch.empty((n_recv, self.d), dtype=torch.float32, device=item.device)
+        self.k.owner_gather(self.recv_ids, E_local, reply, sparse["map"], sparse["n_uniq"], sparse["uniq_rows"],
+                            self.rank, self.d)
+        rows = torch.empty((n_send, self.d), dtype=torch.float32, device=item.device)
+        self._a2a(rows, reply, sc, rc)
+        return rows
+
+    def make_sendbuf(self) -> torch.Tensor:
+        return torch.empty((sum(self.send_counts), self.d), dtype=torch.float32, device=self.device)
+
+    def backward(self, sendbuf: torch.Tensor, sparse) -> None:
+        n_recv = sum(self.recv_counts)
+        grad = torch.empty((n_recv, self.d), dtype=torch.float32, device=sendbuf.device)
+        self._a2a(grad, sendbuf, self.recv_counts, self.send_counts)
+        self.k.owner_scatter(self.recv_ids, grad, sparse["map"], sparse["gU"], self.rank, self.d)
+
+
+class DistCollective:
+    """SyncBN / gradient all-reduce hook for ops.forward/backward (sum over ranks)."""
+
+    def __init__(self, world: int, group=None, stage_on_cpu: bool = False):
+        self.world = world
+        self.group = group
+        self.stage_on_cpu = stage_on_cpu
+
+    def allreduce_(self, t: torch.Tensor) -> None:
+        if self.world <= 1:
+            return
+        if self.stage_on_cpu:
+            c = t.cpu()
+            dist.all_reduce(c, group=self.group)
+            t.copy_(c)
+        else:
+            dist.all_reduce(t, group=self.group)

@@ -1,0 +1,292 @@
+"""Kernel sequencing for one FiBiNET forward / backward on a HIP device.
+
+This module owns no math: every arithmetic step is a call into libfibinet_hip.so.  Torch is
+used for device allocation and the current stream only.  Both the drop-in ``MM_FiBiNET``
+(autograd) and the native ``FiBiNETTrainer`` drive these two functions.
+
+Layouts (B = batch, d = embedding dim, L = history length; DESIGN.md "HBM layout"):
+  c      [B, 15d]  compact MLP input [V_1..V_5 | p_12..p_45]; the 6d structurally-zero
+                   columns of the reference's 21d input (V_0 and pairs (0,j)) are never stored:
+                   weight column k' of the compact layout is column remap(k') of mlp.0.weight,
+                   remap = k' + (k' < 5d ? d : 6d).
+  Vc, X  [B, 5, d] fields 1..5 after / before SENET;  U [B, 5, d] = Vc W.
+  hmm    [B, d]    mm projection before LayerNorm.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import torch
+
+from . import _lib
+from ._lib import call, ptr
+
+INT_MAX = 0x7FFFFFFF
+NO_REMAP = (INT_MAX, 0, 0)
+H1, H2 = 512, 256
+LN_EPS = 1e-5
+BN_EPS = 1e-5
+BN_MOMENTUM = 0.1
+
+
+def wa_remap(d: int):
+    """compact MLP-input column -> mlp.0.weight column (skips V_0 and the five (0,j) pairs)."""
+    return (5 * d, d, 6 * d)
+
+
+def _ws(nbytes: int, device) -> Optional[torch.Tensor]:
+    if nbytes <= 0:
+        return None
+    return torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=device)
+
+
+def gemm(A, B, C, M, N, K, lda, ldb, ldc, transA, transB, bias=None, rB=NO_REMAP, rC=NO_REMAP, beta=0.0,
+         bf16=False, stream=None):
+    nbytes = _lib.lib().fbn_gemm_workspace_size(M, N, K, int(bf16))
+    ws = _ws(nbytes, C.device)
+    call("fbn_gemm", ptr(A), ptr(B), ptr(C), ptr(bias), M, N, K, lda, ldb, ldc, int(transA), int(transB),
+         rB[0], rB[1], rB[2], rC[0], rC[1], rC[2], float(beta), int(bf16), ptr(ws), nbytes,
+         stream if stream is not None else _lib.stream_handle())
+
+
+def colsum(X, B, C, ldx, out, beta=0.0, stream=None):
+    ws = _ws(_lib.lib().fbn_colsum_workspace_size(B, C), X.device)
+    call("fbn_colsum", ptr(X), B, C, ldx, ptr(out), float(beta), ptr(ws),
+         stream if stream is not None else _lib.stream_handle())
+
+
+@dataclass
+class FwdConfig:
+    d: int
+    L: int
+    training: bool
+    p_drop: float
+    bf16: bool = False
+    bilinear_each: bool = False
+    R: int = 3
+
+
+class Collective:
+    """Hook for SyncBN: sum a float64 device tensor over ranks in place (identity on 1 rank)."""
+
+    world = 1
+
+    def allreduce_(self, t: torch.Tensor) -> None:  # pragma: no cover - overridden for N > 1
+        return None
+
+
+NO_COLLECTIVE = Collective()
+
+
+def bn_train_stats(h, B, C, mean, invstd, run_mean, run_var, ntot, coll: Collective, stream):
+    """Training-mode BatchNorm statistics over the GLOBAL batch (SyncBN when coll.world > 1)."""
+    dev = h.device
+    ws = _ws(_lib.lib().fbn_bn_workspace_size(B, C), dev)
+    s = torch.empty(C, dtype=torch.float64, device=dev)
+    mean_d = torch.empty(C, dtype=torch.float64, device=dev)
+    call("fbn_bn_stats_pass", ptr(h), B, C, None, ptr(s), ptr(ws), stream)
+    coll.allreduce_(s)
+    call("fbn_bn_mean", ptr(s), float(ntot), C, ptr(mean_d), stream)
+    call("fbn_bn_stats_pass", ptr(h), B, C, ptr(mean_d), ptr(s), ptr(ws), stream)
+    coll.allreduce_(s)
+    call("fbn_bn_finalize", ptr(s), ptr(mean_d), float(ntot), C, ptr(mean), ptr(invstd), ptr(run_mean),
+         ptr(run_var), BN_MOMENTUM, BN_EPS, 1 if run_mean is not None else 0, stream)
+
+
+def bn_backward(G, gvec, w, hact, scale, hpre, mean, invstd, gamma, B, C, ntot, dpre, dgamma, dbeta, dw,
+                coll: Collective, stream):
+    dev = hpre.device
+    ws = _ws(_lib.lib().fbn_bn_workspace_size(B, C), dev)
+    red = torch.empty(3 * C, dtype=torch.float64, device=dev)
+    call("fbn_bn_bwd_reduce", ptr(G), ptr(gvec), ptr(w), ptr(hact), float(scale), ptr(hpre), ptr(mean), B, C,
+         ptr(red), ptr(ws), stream)
+    coll.allreduce_(red)
+    call("fbn_bn_bwd_apply", ptr(G), ptr(gvec), ptr(w), ptr(hact), float(scale), ptr(hpre), ptr(mean), ptr(invstd),
+         ptr(gamma), B, C, ptr(red), float(ntot), ptr(dpre), ptr(dgamma), ptr(dbeta), ptr(dw), ptr(ws), stream)
+
+
+def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: FwdConfig,
+            rng: Optional[torch.Tensor] = None, *, table_rows: Optional[torch.Tensor] = None,
+            pos: Optional[torch.Tensor] = None, sparse: Optional[Dict[str, torch.Tensor]] = None,
+            err: Optional[torch.Tensor] = None, labels: Optional[torch.Tensor] = None,
+            loss_denom: Optional[float] = None, coll: Collective = NO_COLLECTIVE, ntot: Optional[int] = None,
+            masks_out: Optional[Dict[str, torch.Tensor]] = None, acts: Optional[Dict[str, torch.Tensor]] = None
+            ) -> Dict[str, torch.Tensor]:
+    """Run the forward; returns the activation dict (probs, logits and what backward needs).
+
+    p: parameter tensors keyed like the reference state_dict (fp32, contiguous, on device).
+    table_rows/pos: multi-GPU mode (rows already exchanged); otherwise p['item_emb.weight'] is read.
+    sparse: {'map','n_uniq','uniq_rows'} to register touched rows for the native sparse-grad Adam.
+    labels: if given, fuses BCE: acts['loss_terms'] and acts['gout'] (= dL/dlogit).
+    """
+    d, L = cfg.d, cfg.L
+    item_id = batch["item_id"]
+    B = item_id.shape[0]
+    dev = item_id.device
+    st = _lib.stream_handle(dev)
+    ntot = B if ntot is None else ntot
+    f32 = dict(dtype=torch.float32, device=dev)
+    a = acts if acts is not None else {}
+
+    def buf(name, shape, dtype=torch.float32):
+        t = a.get(name)
+        if t is None or tuple(t.shape) != tuple(shape):
+            t = torch.empty(shape, dtype=dtype, device=dev)
+            a[name] = t
+        return t
+
+    seq = batch.get("item_seq", None)
+    Lr = 0 if seq is None else L
+    x_mm = batch["item_emb_d128"]
+    hmm = buf("hmm", (B, d))
+    gemm(x_mm, p["mm_proj.0.weight"], hmm, B, d, 128, 128, 128, d, False, True, bias=p["mm_proj.0.bias"],
+         bf16=cfg.bf16, stream=st)
+    X = buf("X", (B, 5, d))
+    Vc = buf("Vc", (B, 5, d))
+    KC = 15 * d
+    c = buf("c", (B, KC))
+    av = buf("a", (B, 6))
+    cnt = buf("cnt", (B,))
+    if err is None:
+        err = buf("err", (1,), torch.int32)
+        err.zero_()
+    E = p["item_emb.weight"] if table_rows is None else table_rows
+    V = p["item_emb.weight"].shape[0] if table_rows is None else 0
+    sm = sparse or {}
+    call("fbn_fields_fwd", ptr(item_id), ptr(seq) if Lr else None, ptr(batch["likes_level"]),
+         ptr(batch["views_level"]), ptr(hmm), ptr(p["mm_proj.1.weight"]), ptr(p["mm_proj.1.bias"]), LN_EPS,
+         ptr(p["cate_emb.weight"]), p["cate_emb.weight"].shape[0], ptr(E), V, ptr(pos),
+         ptr(p["senet.excitation.0.weight"]), ptr(p["senet.excitation.0.bias"]),
+         ptr(p["senet.excitation.2.weight"]), ptr(p["senet.excitation.2.bias"]), cfg.R, ptr(X), ptr(Vc), ptr(c), KC,
+         ptr(av), ptr(cnt), ptr(err), ptr(sm.get("map")), ptr(sm.get("n_uniq")), ptr(sm.get("uniq_rows")),
+         B, Lr, d, st)
+    # bilinear: U = V W  ("all")  or  U_i = V_i W_i ("each"), then pair products into c
+    U = buf("U", (B, 5, d))
+    if not cfg.bilinear_each:
+        gemm(Vc, p["bilinear.W"], U, 5 * B, d, d, d, d, d, False, False, bf16=cfg.bf16, stream=st)
+    else:
+        U.zero_()
+        for f in range(1, 5):   # field index in Vc: f-1 <-> reference field f; W_list[f]
+            gemm(Vc[:, f - 1], p[f"bilinear.W_list.{f}"], U[:, f - 1], B, d, d, 5 * d, d, 5 * d, False, False,
+                 bf16=cfg.bf16, stream=st)
+    call("fbn_pairs_fwd", ptr(Vc), ptr(U), ptr(c), B, d, KC, int(cfg.bilinear_each), st)
+    # MLP layer 1
+    h1pre = buf("h1pre", (B, H1))
+    gemm(c, p["mlp.0.weight"], h1pre, B, H1, KC, KC, 21 * d, H1, False, True, bias=p["mlp.0.bias"],
+         rB=wa_remap(d), bf16=cfg.bf16, stream=st)
+    mean1, inv1 = buf("mean1", (H1,)), buf("inv1", (H1,))
+    mean2, inv2 = buf("mean2", (H2,)), buf("inv2", (H2,))
+    h1 = buf("h1", (B, H1))
+    h2pre = buf("h2pre", (B, H2))
+    h2 = buf("h2", (B, H2))
+    p_drop = cfg.p_drop if cfg.training else 0.0
+    m1 = masks_out.get("m1") if masks_out else None
+    m2 = masks_out.get("m2") if masks_out else None
+    if cfg.training:
+        bn_train_stats(h1pre, B, H1, mean1, inv1, p["mlp.1.running_mean"], p["mlp.1.running_var"], ntot, coll, st)
+    else:
+        call("fbn_bn_eval_params", ptr(p["mlp.1.running_mean"]), ptr(p["mlp.1.running_var"]), ptr(mean1), ptr(inv1),
+             H1, BN_EPS, st)
+    call("fbn_bn_act_fwd", ptr(h1pre), ptr(h1), B, H1, ptr(mean1), ptr(inv1), ptr(p["mlp.1.weight"]),
+         ptr(p["mlp.1.bias"]), float(p_drop), ptr(rng), 1, ptr(m1), st)
+    gemm(h1, p["mlp.4.weight"], h2pre, B, H2, H1, H1, H1, H2, False, True, bias=p["mlp.4.bias"], bf16=cfg.bf16,
+         stream=st)
+    if cfg.training:
+        bn_train_stats(h2pre, B, H2, mean2, inv2, p["mlp.5.running_mean"], p["mlp.5.running_var"], ntot, coll, st)
+    else:
+        call("fbn_bn_eval_params", ptr(p["mlp.5.running_mean"]), ptr(p["mlp.5.running_var"]), ptr(mean2), ptr(inv2),
+             H2, BN_EPS, st)
+    call("fbn_bn_act_fwd", ptr(h2pre), ptr(h2), B, H2, ptr(mean2), ptr(inv2), ptr(p["mlp.5.weight"]),
+         ptr(p["mlp.5.bias"]), float(p_drop), ptr(rng), 2, ptr(m2), st)
+    logits, probs = buf("logits", (B,)), buf("probs", (B,))
+    lt = buf("loss_terms", (B,)) if labels is not None else None
+    go = buf("gout", (B,)) if labels is not None else None
+    call("fbn_head_fwd", ptr(h2), ptr(p["mlp.8.weight"]), ptr(p["mlp.8.bias"]), B, H2, ptr(logits), ptr(probs),
+         ptr(labels), ptr(lt), ptr(go), float(loss_denom if loss_denom is not None else ntot), st)
+    if cfg.training and "mlp.1.num_batches_tracked" in p:
+        p["mlp.1.num_batches_tracked"].add_(1)
+        p["mlp.5.num_batches_tracked"].add_(1)
+    a["err"] = err
+    a["B"] = B
+    return a
+
+
+def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict[str, torch.Tensor],
+             gout: torch.Tensor, g: Dict[str, torch.Tensor], cfg: FwdConfig, *, table_grad: torch.Tensor,
+             table_map: Optional[torch.Tensor] = None, pos: Optional[torch.Tensor] = None,
+             sendbuf: Optional[torch.Tensor] = None, coll: Collective = NO_COLLECTIVE,
+             ntot: Optional[int] = None) -> None:
+    """Backward from dL/dlogit (gout [B]) into the gradient buffers ``g`` (same keys as ``p``).
+
+    table_grad: dense [V, d] (drop-in) or compact [U, d] rows addressed through table_map
+    (native trainer); in multi-GPU mode (pos given) rows are written to sendbuf instead.
+    Every g[...] buffer is overwritten (not accumulated), except the table gradient which is
+    accumulated into (callers zero it).
+    """
+    d, L = cfg.d, cfg.L
+    B = a["B"]
+    dev = gout.device
+    st = _lib.stream_handle(dev)
+    ntot = B if ntot is None else ntot
+    KC = 15 * d
+    scale = 1.0 / (1.0 - cfg.p_drop) if (cfg.training and cfg.p_drop > 0) else 1.0
+    f32 = dict(dtype=torch.float32, device=dev)
+    # head + BN2 backward (rank-1 source gout (x) Wc)
+    dh2pre = torch.empty((B, H2), **f32)
+    bn_backward(None, gout, p["mlp.8.weight"], a["h2"], scale, a["h2pre"], a["mean2"], a["inv2"],
+                p["mlp.5.weight"], B, H2, ntot, dh2pre, g["mlp.5.weight"], g["mlp.5.bias"], g["mlp.8.weight"],
+                coll, st)
+    call("fbn_sum", ptr(gout), B, ptr(g["mlp.8.bias"]), 1.0, st)
+    colsum(dh2pre, B, H2, H2, g["mlp.4.bias"], stream=st)
+    gemm(dh2pre, a["h1"], g["mlp.4.weight"], H2, H1, B, H2, H1, H1, True, False, bf16=cfg.bf16, stream=st)
+    dh1 = torch.empty((B, H1), **f32)
+    gemm(dh2pre, p["mlp.4.weight"], dh1, B, H1, H2, H2, H1, H1, False, False, bf16=cfg.bf16, stream=st)
+    dh1pre = torch.empty((B, H1), **f32)
+    bn_backward(dh1, None, None, a["h1"], scale, a["h1pre"], a["mean1"], a["inv1"], p["mlp.1.weight"], B, H1, ntot,
+                dh1pre, g["mlp.1.weight"], g["mlp.1.bias"], None, coll, st)
+    colsum(dh1pre, B, H1, H1, g["mlp.0.bias"], stream=st)
+    gemm(dh1pre, a["c"], g["mlp.0.weight"], H1, KC, B, H1, KC, 21 * d, True, False, rC=wa_remap(d), bf16=cfg.bf16,
+         stream=st)
+    dc = torch.empty((B, KC), **f32)
+    gemm(dh1pre, p["mlp.0.weight"], dc, B, KC, H1, H1, 21 * d, KC, False, False, rB=wa_remap(d), bf16=cfg.bf16,
+         stream=st)
+    # bilinear backward
+    dV = torch.empty((B, 5, d), **f32)
+    dU = torch.empty((B, 5, d), **f32)
+    call("fbn_pairs_bwd", ptr(dc), ptr(a["Vc"]), ptr(a["U"]), ptr(dV), ptr(dU), B, d, KC, int(cfg.bilinear_each), st)
+    if not cfg.bilinear_each:
+        gemm(dU, p["bilinear.W"], dV, 5 * B, d, d, d, d, d, False, True, beta=1.0, bf16=cfg.bf16, stream=st)
+        gemm(a["Vc"], dU, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, bf16=cfg.bf16, stream=st)
+    else:
+        g["bilinear.W_list.0"].zero_()
+        for f in range(1, 5):
+            gemm(dU[:, f - 1], p[f"bilinear.W_list.{f}"], dV[:, f - 1], B, d, d, 5 * d, d, 5 * d, False, True,
+                 beta=1.0, bf16=cfg.bf16, stream=st)
+            gemm(a["Vc"][:, f - 1], dU[:, f - 1], g[f"bilinear.W_list.{f}"], d, d, B, 5 * d, 5 * d, d, True, False,
+                 bf16=cfg.bf16, stream=st)
+    # fields backward: SENET, LN, cate + item-table scatter
+    R = cfg.R
+    ncate = p["cate_emb.weight"].shape[0]
+    P = _lib.lib().fbn_fields_bwd_partials_size(d, R, ncate)
+    nblk = _lib.lib().fbn_fields_bwd_grid(B, d)
+    partials = torch.empty((nblk, P), **f32)
+    pg = torch.empty((P,), **f32)
+    dhmm = torch.empty((B, d), **f32)
+    seq = batch.get("item_seq", None)
+    Lr = 0 if seq is None else L
+    V = p["item_emb.weight"].shape[0] if pos is None else 0
+    call("fbn_fields_bwd", ptr(batch["item_id"]), ptr(seq) if Lr else None, ptr(batch["likes_level"]),
+         ptr(batch["views_level"]), ptr(a["hmm"]), ptr(p["mm_proj.1.weight"]), LN_EPS,
+         ptr(p["senet.excitation.0.weight"]), ptr(p["senet.excitation.0.bias"]), ptr(p["senet.excitation.2.weight"]),
+         R, ncate, ptr(a["X"]), ptr(a["a"]), ptr(a["cnt"]), ptr(dV), ptr(dhmm), ptr(partials), ptr(pg),
+         ptr(table_grad), ptr(table_map), V, ptr(pos), ptr(sendbuf), B, Lr, d, st)
+    o = 0
+    for key, n in (("senet.excitation.0.weight", 6 * R), ("senet.excitation.0.bias", R),
+                   ("senet.excitation.2.weight", 6 * R), ("senet.excitation.2.bias", 6),
+                   ("mm_proj.1.weight", d), ("mm_proj.1.bias", d), ("cate_emb.weight", ncate * d)):
+        g[key].view(-1).copy_(pg[o:o + n])
+        o += n
+    gemm(dhmm, batch["item_emb_d128"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True, False, bf16=cfg.bf16,
+         stream=st)
+    colsum(dhmm, B, d, d, g["mm_proj.0.bias"], stream=st)

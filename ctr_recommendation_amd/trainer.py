@@ -1,0 +1,224 @@
+"""Native fused FiBiNET training step on MI355X (single GPU or row-sharded over N GPUs).
+
+Executes, per step, exactly what src/train_fibinet.py:113-123 does around the model:
+  zero_grad -> forward -> BCELoss -> backward -> clip_grad_norm_(10) -> Adam(lr, wd) -> OneCycleLR
+but as a sequence of libfibinet_hip.so launches with no host round trip (N = 1; capturable
+into one hipGraph), and with the item-table gradient kept sparse:
+
+* dense parameters (everything but the two id tables) live in ONE flat fp32 buffer with
+  matching flat grad / Adam-m / Adam-v buffers: one norm pass and one fused Adam launch;
+* the item table gradient is a compact [U, d] buffer addressed through a row->slot map
+  registered by the forward gather; the dense Adam pass over the table reads the gradient
+  only through that map (exact torch semantics: untouched rows still get g = wd * p);
+* user_emb receives no gradient in the reference (the user field is zeros), so torch's Adam
+  skips it; it is kept (state_dict contract) and never updated here either.
+
+Multi-GPU (world > 1): one process per GPU; rows of E are block-sharded (exchange.py),
+BatchNorm statistics are synchronised (SyncBN: the global-batch statistics the single-process
+reference computes), dense gradients are all-reduced, the clip norm sums the table shards.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib, ops
+from ._lib import call, ptr
+from .exchange import DistCollective, RowExchange
+from .model_fibinet import build_model
+from .schedule import OneCycle, adam_table
+
+TABLE = "item_emb.weight"
+FROZEN = ("user_emb.weight",)
+BUFFERS = ("mlp.1.running_mean", "mlp.1.running_var", "mlp.1.num_batches_tracked",
+           "mlp.5.running_mean", "mlp.5.running_var", "mlp.5.num_batches_tracked")
+
+
+def _pad4(n: int) -> int:
+    return (n + 3) // 4 * 4
+
+
+class FiBiNETTrainer:
+    def __init__(self, model_cfg: Dict, total_steps: int, batch_size: int, *, device=None, max_len: int = 20,
+                 lr: Optional[float] = None, weight_decay: Optional[float] = None, rank: int = 0, world: int = 1,
+                 group=None, init_state: Optional[Dict[str, torch.Tensor]] = None, seed: int = 2025,
+                 stage_on_cpu: bool = False, dropout_seed: Optional[int] = None):
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.type != "cuda":
+            raise RuntimeError("FiBiNETTrainer runs on a HIP device only (no CPU fallback)")
+        self.cfg = dict(model_cfg)
+        self.lr = float(lr if lr is not None else model_cfg.get("learning_rate", 1e-3))
+        self.wd = float(weight_decay if weight_decay is not None else model_cfg.get("weight_decay", 1e-5))
+        self.beta2, self.eps, self.max_norm = 0.999, 1e-8, 10.0
+        self.rank, self.world, self.group = rank, world, group
+        self.B = batch_size                     # per-rank batch
+        self.L = max_len
+        if init_state is None:
+            torch.manual_seed(seed)
+            init_state = build_model(None, self.cfg).state_dict()
+        # model structure (reuses the drop-in module's definition for names / shapes)
+        shape_model = build_model(None, dict(self.cfg, vocab_size=4))
+        self.d = shape_model.emb_dim
+        self.p_drop = shape_model.dropout_p
+        self.fcfg = ops.FwdConfig(d=self.d, L=max_len, training=True, p_drop=self.p_drop,
+                                  bf16=shape_model.compute_bf16,
+                                  bilinear_each=shape_model.bilinear.bilinear_type == "each",
+                                  R=shape_model.senet.excitation[0].out_features)
+        self.V = init_state[TABLE].shape[0]
+        dev = self.device
+        # ---------------- dense parameters: one flat buffer (16-B aligned segments)
+        self.dense_names: List[str] = [n for n, _ in shape_model.named_parameters() if n != TABLE and n not in FROZEN]
+        self.shapes = {n: tuple(init_state[n].shape) for n in init_state}
+        offs, o = {}, 0
+        for n in self.dense_names:
+            offs[n] = o
+            o += _pad4(int(np.prod(self.shapes[n])))
+        self.n_dense = o
+        self.flat_p = torch.zeros(o, dtype=torch.float32, device=dev)
+        self.flat_g = torch.zeros_like(self.flat_p)
+        self.flat_m = torch.zeros_like(self.flat_p)
+        self.flat_v = torch.zeros_like(self.flat_p)
+        self.p: Dict[str, torch.Tensor] = {}
+        self.g: Dict[str, torch.Tensor] = {}
+        for n in self.dense_names:
+            k = int(np.prod(self.shapes[n]))
+            self.p[n] = self.flat_p[offs[n]:offs[n] + k].view(self.shapes[n])
+            self.g[n] = self.flat_g[offs[n]:offs[n] + k].view(self.shapes[n])
+            self.p[n].copy_(init_state[n].to(dev))
+        for n in FROZEN:
+            self.p[n] = init_state[n].to(dev).clone()
+        for n in BUFFERS:
+            self.p[n] = init_state[n].to(dev).clone()
+        # ---------------- item table shard + Adam state + sparse gradient bookkeeping
+        self.Vl = (self.V + world - 1) // world
+        lo = rank * self.Vl
+        hi = min(self.V, lo + self.Vl)
+        self.rows_lo, self.rows_local = lo, hi - lo
+        self.E = init_state[TABLE][lo:hi].to(dev).contiguous()
+        self.Em = torch.zeros_like(self.E)
+        self.Ev = torch.zeros_like(self.E)
+        if world == 1:
+            self.p[TABLE] = self.E
+        cap = min(self.rows_local, world * self.B * (max_len + 1)) + 1
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.sparse = {
+            "map": torch.full((max(1, self.rows_local),), -1, **i32),
+            "n_uniq": torch.zeros(1, **i32),
+            "uniq_rows": torch.zeros(cap, **i32),
+            "gU": torch.zeros((cap, self.d), dtype=torch.float32, device=dev),
+        }
+        # ---------------- optimizer schedule + device step state
+        self.total_steps = total_steps
+        tab, self.lrs = adam_table(total_steps, self.lr, self.beta2, OneCycle(total_steps, self.lr))
+        self.sched = torch.from_numpy(tab).to(dev)
+        self.step_dev = torch.zeros(1, **i32)
+        seed_d = dropout_seed if dropout_seed is not None else (seed * 1000003 + 17)
+        self.rng = torch.tensor([seed_d & 0x7FFFFFFFFFFF, 0], dtype=torch.int64, device=dev)
+        self.sumsq = torch.zeros(1, dtype=torch.float64, device=dev)
+        self.sumsq_tab = torch.zeros(1, dtype=torch.float64, device=dev)
+        self.coef = torch.ones(1, dtype=torch.float32, device=dev)
+        self.norm = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.err = torch.zeros(1, **i32)
+        self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.host_step = 0
+        self.acts: Dict[str, torch.Tensor] = {}
+        self.coll = DistCollective(world, group, stage_on_cpu)
+        self.xchg = RowExchange(rank, world, self.V, self.d, self.B, max_len, dev, group,
+                                stage_on_cpu=stage_on_cpu) if world > 1 else None
+        self.stage_on_cpu = stage_on_cpu
+
+    # ------------------------------------------------------------------ one training step
+    def step(self, batch: Dict[str, torch.Tensor], labels: torch.Tensor) -> torch.Tensor:
+        """One optimizer step on this rank's batch; returns the (device) global-mean BCE loss."""
+        if self.host_step >= self.total_steps:
+            raise ValueError(f"Tried to step {self.host_step + 1} times. The specified number of total steps is "
+                             f"{self.total_steps}")
+        st = _lib.stream_handle(self.device)
+        B = batch["item_id"].shape[0]
+        ntot = B * self.world
+        cfg = self.fcfg
+        if "item_seq" in batch:
+            cfg.L = batch["item_seq"].shape[1]
+        rows = pos = None
+        if self.xchg is not None:
+            rows = self.xchg.forward(batch["item_id"], batch.get("item_seq"), self.E, self.sparse, self.err)
+            pos = self.xchg.cur_pos
+        a = ops.forward(self.p, batch, cfg, self.rng, table_rows=rows, pos=pos,
+                        sparse=self.sparse if self.xchg is None else None, err=self.err, labels=labels,
+                        loss_denom=float(ntot), coll=self.coll, ntot=ntot, acts=self.acts)
+        call("fbn_sum", ptr(a["loss_terms"]), B, ptr(self.loss), 1.0 / ntot, st)
+        sendbuf = self.xchg.make_sendbuf() if self.xchg is not None else None
+        ops.backward(self.p, batch, a, a["gout"], self.g, cfg, table_grad=self.sparse["gU"],
+                     table_map=self.sparse["map"] if self.xchg is None else None, pos=pos, sendbuf=sendbuf,
+                     coll=self.coll, ntot=ntot)
+        if self.xchg is not None:
+            self.coll.allreduce_(self.flat_g)
+            self.xchg.backward(sendbuf, self.sparse)
+        # clip_grad_norm_(10): dense grads (identical on every rank) + disjoint table shards
+        call("fbn_sumsq", ptr(self.sparse["gU"]), 0, ptr(self.sparse["n_uniq"]), self.d, ptr(self.sumsq_tab), st)
+        if self.world > 1:
+            self.coll.allreduce_(self.sumsq_tab)
+        call("fbn_sumsq", ptr(self.flat_g), self.n_dense, None, 0, ptr(self.sumsq), st)
+        self.sumsq.add_(self.sumsq_tab)
+        call("fbn_clip_coef", ptr(self.sumsq), self.max_norm, ptr(self.coef), ptr(self.norm), st)
+        call("fbn_adam_dense", ptr(self.flat_p), ptr(self.flat_g), ptr(self.flat_m), ptr(self.flat_v),
+             self.n_dense, ptr(self.coef), ptr(self.sched), ptr(self.step_dev), self.wd, self.beta2, self.eps, st)
+        call("fbn_adam_table", ptr(self.E), ptr(self.Em), ptr(self.Ev), self.rows_local, self.d,
+             ptr(self.sparse["map"]), ptr(self.sparse["gU"]), ptr(self.coef), ptr(self.sched), ptr(self.step_dev),
+             self.wd, self.beta2, self.eps, st)
+        call("fbn_zero_rows", ptr(self.sparse["gU"]), ptr(self.sparse["n_uniq"]), self.d, st)
+        self.sumsq_tab.zero_()
+        call("fbn_step_end", ptr(self.step_dev), ptr(self.rng), ptr(self.sparse["n_uniq"]), ptr(self.sumsq), st)
+        self.host_step += 1
+        return self.loss
+
+    # ------------------------------------------------------------------ inference
+    @torch.no_grad()
+    def predict(self, batch: Dict[str, torch.Tensor], logits: bool = False) -> torch.Tensor:
+        cfg = ops.FwdConfig(**{**self.fcfg.__dict__, "training": False})
+        if "item_seq" in batch:
+            cfg.L = batch["item_seq"].shape[1]
+        rows = pos = None
+        if self.xchg is not None:
+            scratch = {"map": None, "n_uniq": None, "uniq_rows": None}
+            rows = self.xchg.forward(batch["item_id"], batch.get("item_seq"), self.E, scratch, self.err)
+            pos = self.xchg.cur_pos
+        a = ops.forward(self.p, batch, cfg, None, table_rows=rows, pos=pos, err=self.err)
+        return (a["logits"] if logits else a["probs"]).clone()
+
+    def check_ids(self) -> None:
+        if int(self.err.item()) != 0:
+            raise IndexError("index out of range in self (item/likes/views id outside its embedding table)")
+
+    def current_lr(self) -> float:
+        return self.lrs[min(self.host_step, self.total_steps - 1)]
+
+    # ------------------------------------------------------------------ checkpoint (App. B keys)
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        """Reference state_dict (CPU tensors).  Multi-GPU: collective; the full table on every rank."""
+        import torch.distributed as dist
+        out = {}
+        if self.world > 1:
+            parts = [torch.zeros((self.Vl, self.d), dtype=torch.float32, device=self.device)
+                     for _ in range(self.world)]
+            local = torch.zeros((self.Vl, self.d), dtype=torch.float32, device=self.device)
+            local[:self.rows_local] = self.E
+            if self.stage_on_cpu:
+                cparts = [t.cpu() for t in parts]
+                dist.all_gather(cparts, local.cpu(), group=self.group)
+                full = torch.cat(cparts)[:self.V]
+            else:
+                dist.all_gather(parts, local, group=self.group)
+                full = torch.cat(parts)[:self.V].cpu()
+        else:
+            full = self.E.detach().cpu().clone()
+        order = list(build_model(None, dict(self.cfg, vocab_size=4)).state_dict().keys())
+        for k in order:
+            if k == TABLE:
+                out[k] = full
+            else:
+                out[k] = self.p[k].detach().cpu().clone()
+        return out

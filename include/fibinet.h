@@ -1,0 +1,146 @@
+/*
+ * fibinet.h -- C ABI of libfibinet_hip.so, the MI355X (gfx950) kernels behind the FiBiNET
+ * training path of YOUNESELBOUKNIFY/Ctr_recommendation.
+ *
+ * The reference is pure Python: its "interface" for this path is the PyTorch module
+ * src/model_fibinet.py (build_model / MM_FiBiNET.forward + autograd backward) and the per-step
+ * optimizer code of src/train_fibinet.py.  Each entry point below replaces the implicit ATen
+ * op(s) named in its comment (reference file:line).  The Python binding is
+ * ctr_recommendation_amd/_lib.py (ctypes); INTEGRATION.md shows the reference-side wiring.
+ *
+ * Conventions
+ *  - all tensors are device pointers owned by the caller (torch); the library allocates
+ *    nothing persistent.  Scratch is passed in; size it with the *_workspace_size queries.
+ *  - every call is asynchronous on `stream` (a hipStream_t), takes no locks and keeps no
+ *    global mutable state except a thread-local error string -> reentrant, graph-capturable.
+ *  - return 0 on success, otherwise FBN_ERR_*; fbn_last_error() describes the failure.
+ *  - id range violations never fault: kernels set a sticky int flag (*err) that the caller
+ *    checks lazily (the reference raises IndexError in nn.Embedding).
+ *  - fp32 storage everywhere; `bf16` flags select bf16 MFMA operands with fp32 accumulation.
+ */
+#ifndef FIBINET_H
+#define FIBINET_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FBN_OK 0
+#define FBN_ERR_ARG 1
+#define FBN_ERR_LAUNCH 2
+#define FBN_ERR_UNSUPPORTED 3
+
+const char* fbn_last_error(void);
+int fbn_version(void);
+int fbn_device_ok(void); /* 1 if the current HIP device is gfx950 */
+
+/* ---------------------------------------------------------------- GEMM (MFMA)
+ * C[m][rC(n)] = sum_k A(m,k) B(k,n) + bias[n] + beta*C ; remap r(i) = i + (i < seg ? off0 : off1)
+ * (seg = INT32_MAX: identity).  Replaces addmm/matmul of
+ *   mm_proj Linear           src/model_fibinet.py:105-106,162
+ *   bilinear x @ W            src/model_fibinet.py:72
+ *   MLP Linear x3             src/model_fibinet.py:126,130,134,197
+ * and all of their autograd backward GEMMs.  Split-K slabs need ws >= fbn_gemm_workspace_size. */
+size_t fbn_gemm_workspace_size(int M, int N, int K, int bf16);
+int fbn_gemm(const float* A, const float* B, float* C, const float* bias, int M, int N, int K, int lda, int ldb,
+             int ldc, int transA, int transB, int rB_seg, int rB_off0, int rB_off1, int rC_seg, int rC_off0,
+             int rC_off1, float beta, int bf16, float* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------- K1 + K4: fields + SENET forward
+ * Replaces: nn.Embedding lookups (src/model_fibinet.py:155,156,159,167), masked history mean
+ * (:165-176), LayerNorm+ReLU of mm_proj (:107-108), torch.stack (:180-182), SENetLayer.forward
+ * (:24-35).  table = E [V][D] (pos == NULL) or an exchanged row buffer addressed by
+ * pos[B][L+1] (multi-GPU).  map/n_uniq/uniq_rows (optional) register rows for the sparse
+ * gradient.  D in {16,32,64,128,256}; L <= 32. */
+int fbn_fields_fwd(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes, const int64_t* views,
+                   const float* hmm, const float* ln_g, const float* ln_b, float ln_eps, const float* cate, int n_cate,
+                   const float* table, long long V, const int* pos, const float* w1, const float* b1, const float* w2,
+                   const float* b2, int R, float* X, float* Vc, float* c, int ldc, float* a_out, float* cnt_out,
+                   int* err, int* map, int* n_uniq, int* uniq_rows, int B, int L, int D, void* stream);
+
+/* ---------------------------------------------------------------- K2 + K4 backward
+ * Replaces the autograd of the lines above, including embedding_dense_backward with
+ * padding_idx=0 (src/model_fibinet.py:100).  Table gradient: dense gtab[V][D] (map == NULL),
+ * compact gtab[slot][D] via map (native trainer), or rows into sendbuf at pos (multi-GPU).
+ * param_grads[P] (P = fbn_fields_bwd_partials_size) = {senet W1, b1, W2, b2, LN gamma, beta,
+ * cate table}; partials: [fbn_fields_bwd_grid(B,D)][P] scratch. */
+int fbn_fields_bwd_partials_size(int D, int R, int n_cate);
+int fbn_fields_bwd_grid(int B, int D);
+int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes, const int64_t* views,
+                   const float* hmm, const float* ln_g, float ln_eps, const float* w1, const float* b1, const float* w2,
+                   int R, int n_cate, const float* X, const float* a, const float* cnt, const float* dV, float* dhmm,
+                   float* partials, float* param_grads, float* gtab, const int* map, long long V, const int* pos,
+                   float* sendbuf, int B, int L, int D, void* stream);
+
+/* ---------------------------------------------------------------- K5 bilinear pair products
+ * Replaces the pair loop + stack + cat of src/model_fibinet.py:75-79,89,191-194 ("all", mode 0)
+ * and :81-86 ("each", mode 1).  Pairs (0,j) are structurally zero and not stored. */
+int fbn_pairs_fwd(const float* Vc, const float* U, float* c, int B, int D, int ldc, int mode, void* stream);
+int fbn_pairs_bwd(const float* dc, const float* Vc, const float* U, float* dV, float* dU, int B, int D, int ldc,
+                  int mode, void* stream);
+
+/* ---------------------------------------------------------------- K6 BatchNorm + ReLU + dropout
+ * Replaces nn.BatchNorm1d / ReLU / Dropout(0.2) of src/model_fibinet.py:127-133.  The stats
+ * entry points split into local passes and finalize so that a SyncBN all-reduce of the
+ * float64 sums can run in between (multi-GPU). */
+size_t fbn_bn_workspace_size(int B, int C);
+int fbn_bn_stats_pass(const float* X, int B, int C, const double* mean_d, double* out_d, void* ws, void* stream);
+int fbn_bn_mean(const double* sum_d, double ntot, int C, double* mean_d, void* stream);
+int fbn_bn_finalize(const double* m2_d, const double* mean_d, double ntot, int C, float* mean, float* invstd,
+                    float* run_mean, float* run_var, float momentum, float eps, int update_running, void* stream);
+int fbn_bn_stats(const float* X, int B, int C, float* mean, float* invstd, float* run_mean, float* run_var,
+                 float momentum, float eps, int update_running, void* ws, void* stream);
+int fbn_bn_eval_params(const float* run_mean, const float* run_var, float* mean, float* invstd, int C, float eps,
+                       void* stream);
+int fbn_bn_act_fwd(const float* X, float* Y, int B, int C, const float* mean, const float* invstd, const float* g,
+                   const float* b, float p_drop, const unsigned long long* rng, unsigned stream_id,
+                   unsigned char* mask_out, void* stream);
+int fbn_bn_bwd_reduce(const float* G, const float* gvec, const float* w, const float* hact, float scale,
+                      const float* Xpre, const float* mean, int B, int C, double* red_d, void* ws, void* stream);
+int fbn_bn_bwd_apply(const float* G, const float* gvec, const float* w, const float* hact, float scale,
+                     const float* Xpre, const float* mean, const float* invstd, const float* gamma, int B, int C,
+                     const double* red_d, double ntot, float* dXpre, float* dgamma, float* dbeta, float* dw, void* ws,
+                     void* stream);
+int fbn_bn_bwd(const float* G, const float* gvec, const float* w, const float* hact, float scale, const float* Xpre,
+               const float* mean, const float* invstd, const float* gamma, int B, int C, float* dXpre, float* dgamma,
+               float* dbeta, float* dw, void* ws, void* stream);
+size_t fbn_colsum_workspace_size(int B, int C);
+int fbn_colsum(const float* X, int B, int C, int ldx, float* out, float beta, void* ws, void* stream);
+
+/* ---------------------------------------------------------------- K7 head: Linear(256,1)+sigmoid+BCE
+ * Replaces src/model_fibinet.py:134,136,199 and nn.BCELoss fwd/bwd (src/train_fibinet.py:79,115). */
+int fbn_head_fwd(const float* H, const float* w, const float* bias, int B, int C, float* logits, float* probs,
+                 const float* labels, float* loss_terms, float* gout, float denom, void* stream);
+int fbn_sigmoid_bwd(const float* gp, const float* probs, float* gout, int B, void* stream);
+int fbn_outer(const float* g, const float* w, float* out, int B, int C, void* stream);
+int fbn_sum(const float* x, int n, float* out, float scale, void* stream);
+
+/* ---------------------------------------------------------------- K8 + K9 clip + Adam
+ * Replaces clip_grad_norm_(10) (src/train_fibinet.py:119) and torch.optim.Adam with coupled L2
+ * (:78,121); the schedule table carries OneCycleLR's lr/beta1 per step (:84-92,122). */
+int fbn_sumsq(const float* x, long long n, const int* n_rows, int row_len, double* out, void* stream);
+int fbn_clip_coef(const double* sumsq, float max_norm, float* coef, float* norm, void* stream);
+int fbn_adam_dense(float* p, const float* g, float* m, float* v, long long n, const float* coef,
+                   const void* consts_table, const int* step, float wd, float beta2, float eps, void* stream);
+int fbn_adam_table(float* p, float* m, float* v, long long nrows, int D, int* map, const float* gU, const float* coef,
+                   const void* consts_table, const int* step, float wd, float beta2, float eps, void* stream);
+int fbn_step_end(int* step, unsigned long long* rng, int* n_uniq, double* sumsq, void* stream);
+int fbn_zero_rows(float* gU, const int* n_uniq, int D, void* stream);
+
+/* ---------------------------------------------------------------- row-sharded exchange (multi-GPU)
+ * Replaces torch.nn.DataParallel's replicate/scatter of the whole table (src/train_fibinet.py:69-70)
+ * by routing ids to the owner of each row block; RCCL all-to-all runs between these calls. */
+int fbn_route(const int64_t* item, const int64_t* seq, int B, int L, long long V, long long Vl, int nranks,
+              int* counts, int* offsets, int* cursor, int* send_ids, int* pos, int* err, void* stream);
+int fbn_owner_gather(const int* ids, int n, const float* E, float* out, int* map, int* n_uniq, int* uniq_rows,
+                     int rank, int D, void* stream);
+int fbn_owner_scatter(const int* ids, int n, const float* grad, const int* map, float* gU, int rank, int D,
+                      void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FIBINET_H */

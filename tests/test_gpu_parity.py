@@ -1,0 +1,145 @@
+"""HIP path vs the CPU oracle (parity gate).  Run on an MI355X: pytest -m gpu.
+
+Tolerances (north_star): probabilities / logits within 1e-4 (fp32 path); gradients within
+1e-4 relative to the largest entry of each tensor (fp32 GEMM / atomic summation order only).
+"""
+import numpy as np
+import pytest
+import torch
+
+from ctr_recommendation_amd import ops
+from ctr_recommendation_amd.data import make_batch
+from ctr_recommendation_amd.model_fibinet import build_model
+from oracle.fibinet_oracle import build_model as oracle_build
+
+pytestmark = pytest.mark.gpu
+
+V_SMALL = 5000
+
+
+def _pair(d, seed=0, honour=None):
+    cfg = {"embedding_dim": d, "vocab_size": V_SMALL}
+    if honour:
+        cfg.update(honour)
+        cfg["honour_config"] = True
+    torch.manual_seed(seed)
+    ref = oracle_build(None, cfg, honour_config=bool(honour))
+    torch.manual_seed(seed)
+    hip = build_model(None, cfg)
+    sd_ref = ref.state_dict()
+    for k, v in hip.state_dict().items():
+        assert torch.equal(v, sd_ref[k]), f"seeded init differs for {k}"
+    return ref, hip
+
+
+def _to(batch, dev):
+    return {k: v.to(dev) for k, v in batch.items()}
+
+
+@pytest.mark.parametrize("d", [16, 128])
+def test_forward_eval_parity(hip_device, d):
+    ref, hip = _pair(d)
+    batch, _ = make_batch(1, 96, V_SMALL)
+    ref.eval()
+    hip = hip.to(hip_device).eval()
+    with torch.no_grad():
+        p_ref = ref(batch)
+        p_hip = hip(_to(batch, hip_device)).cpu()
+    assert p_hip.shape == p_ref.shape
+    assert (p_hip - p_ref).abs().max().item() < 1e-4
+
+
+@pytest.mark.parametrize("d", [16, 128])
+def test_forward_train_parity_injected_masks(hip_device, d):
+    ref, hip = _pair(d)
+    B = 128
+    batch, _ = make_batch(2, B, V_SMALL)
+    hip = hip.to(hip_device).train()
+    p = {k: v for k, v in hip.state_dict(keep_vars=False).items()}
+    p = {k: v.contiguous() for k, v in p.items()}
+    cfg = ops.FwdConfig(d=d, L=20, training=True, p_drop=0.2)
+    rng = torch.tensor([1234, 7], dtype=torch.int64, device=hip_device)
+    masks = {"m1": torch.empty((B, 512), dtype=torch.uint8, device=hip_device),
+             "m2": torch.empty((B, 256), dtype=torch.uint8, device=hip_device)}
+    acts = ops.forward(p, _to(batch, hip_device), cfg, rng, masks_out=masks)
+    m1, m2 = masks["m1"].cpu().float(), masks["m2"].cpu().float()
+    keep = torch.cat([m1.flatten(), m2.flatten()]).mean().item()
+    assert 0.75 < keep < 0.85, keep                       # Bernoulli(0.8) keep-rate
+    ref.train()
+    logit_ref = ref(batch, masks=(m1, m2), return_logits=True)
+    lh = acts["logits"].cpu()
+    assert (lh - logit_ref.detach()).abs().max().item() < 1e-4
+    assert (acts["probs"].cpu() - torch.sigmoid(logit_ref.detach())).abs().max().item() < 1e-4
+    # BN running statistics updated like torch (momentum 0.1, unbiased var)
+    for k in ("mlp.1.running_mean", "mlp.1.running_var", "mlp.5.running_mean", "mlp.5.running_var"):
+        assert torch.allclose(p[k].cpu(), ref.state_dict()[k], atol=1e-5, rtol=1e-4), k
+
+
+def _grad_close(g_hip, g_ref, name, rtol=1e-4):
+    scale = max(g_ref.abs().max().item(), 1e-6)
+    err = (g_hip - g_ref).abs().max().item()
+    assert err <= rtol * scale + 1e-7, f"{name}: max err {err:.3e} vs scale {scale:.3e}"
+
+
+@pytest.mark.parametrize("d", [16, 128])
+def test_backward_parity_no_dropout(hip_device, d):
+    ref, hip = _pair(d, honour={"net_dropout": 0.0})
+    B = 128
+    batch, labels = make_batch(3, B, V_SMALL)
+    hip = hip.to(hip_device).train()
+    ref.train()
+    loss_fn = torch.nn.BCELoss()
+    l_ref = loss_fn(ref(batch), labels)
+    l_ref.backward()
+    y = hip(_to(batch, hip_device))
+    l_hip = loss_fn(y, labels.to(hip_device))
+    l_hip.backward()
+    assert abs(l_hip.item() - l_ref.item()) < 1e-5
+    ref_g = {n: p.grad for n, p in ref.named_parameters()}
+    for n, p in hip.named_parameters():
+        if ref_g[n] is None:
+            assert p.grad is None, n
+            continue
+        if n in ("mlp.0.bias", "mlp.4.bias"):   # exactly cancelled by the following BatchNorm
+            assert p.grad.abs().max().item() < 1e-5, n
+            continue
+        _grad_close(p.grad.cpu(), ref_g[n], n)
+
+
+def test_padding_and_empty_history(hip_device):
+    """All-padding history -> zero field (count clamps to 1); id 0 never receives a gradient."""
+    d = 16
+    ref, hip = _pair(d, honour={"net_dropout": 0.0})
+    B = 32
+    batch, labels = make_batch(4, B, V_SMALL)
+    batch["item_seq"][:8] = 0          # all padding
+    batch["item_seq"][8:16, :] = 7     # repeated id (scatter collisions)
+    batch["item_id"][16:20] = 7
+    hip = hip.to(hip_device).train()
+    ref.train()
+    loss_fn = torch.nn.BCELoss()
+    loss_fn(ref(batch), labels).backward()
+    loss_fn(hip(_to(batch, hip_device)), labels.to(hip_device)).backward()
+    g = hip.item_emb.weight.grad.cpu()
+    assert g[0].abs().max().item() == 0.0
+    _grad_close(g, ref.item_emb.weight.grad, "item_emb.weight")
+
+
+def test_out_of_range_id_raises(hip_device):
+    _, hip = _pair(16)
+    batch, _ = make_batch(5, 16, V_SMALL)
+    batch["item_id"][3] = V_SMALL + 10
+    hip = hip.to(hip_device).eval()
+    with pytest.raises(IndexError):
+        with torch.no_grad():
+            hip(_to(batch, hip_device))
+
+
+def test_no_history_key(hip_device):
+    ref, hip = _pair(16)
+    batch, _ = make_batch(6, 64, V_SMALL)
+    del batch["item_seq"]
+    ref.eval()
+    hip = hip.to(hip_device).eval()
+    with torch.no_grad():
+        assert (hip(_to(batch, hip_device)).cpu() - ref(batch)).abs().max().item() < 1e-4
