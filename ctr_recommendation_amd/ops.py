@@ -111,8 +111,8 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
             pos: Optional[torch.Tensor] = None, sparse: Optional[Dict[str, torch.Tensor]] = None,
             err: Optional[torch.Tensor] = None, labels: Optional[torch.Tensor] = None,
             loss_denom: Optional[float] = None, coll: Collective = NO_COLLECTIVE, ntot: Optional[int] = None,
-            masks_out: Optional[Dict[str, torch.Tensor]] = None, acts: Optional[Dict[str, torch.Tensor]] = None
-            ) -> Dict[str, torch.Tensor]:
+            masks_out: Optional[Dict[str, torch.Tensor]] = None, acts: Optional[Dict[str, torch.Tensor]] = None,
+            probe: Optional[Dict[str, list]] = None) -> Dict[str, torch.Tensor]:
     """Run the forward; returns the activation dict (probs, logits and what backward needs).
 
     p: parameter tensors keyed like the reference state_dict (fp32, contiguous, on device).
@@ -154,6 +154,11 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     E = p["item_emb.weight"] if table_rows is None else table_rows
     V = p["item_emb.weight"].shape[0] if table_rows is None else 0
     sm = sparse or {}
+    ev = None
+    if probe is not None:                       # bench: HIP events around the gather kernel
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+        probe.setdefault("fields_fwd", []).append(ev)
     call("fbn_fields_fwd", ptr(item_id), ptr(seq) if Lr else None, ptr(batch["likes_level"]),
          ptr(batch["views_level"]), ptr(hmm), ptr(p["mm_proj.1.weight"]), ptr(p["mm_proj.1.bias"]), LN_EPS,
          ptr(p["cate_emb.weight"]), p["cate_emb.weight"].shape[0], ptr(E), V, ptr(pos),
@@ -161,6 +166,8 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
          ptr(p["senet.excitation.2.weight"]), ptr(p["senet.excitation.2.bias"]), cfg.R, ptr(X), ptr(Vc), ptr(c), KC,
          ptr(av), ptr(cnt), ptr(err), ptr(sm.get("map")), ptr(sm.get("n_uniq")), ptr(sm.get("uniq_rows")),
          B, Lr, d, st)
+    if ev is not None:
+        ev[1].record()
     # bilinear: U = V W  ("all")  or  U_i = V_i W_i ("each"), then pair products into c
     U = buf("U", (B, 5, d))
     if not cfg.bilinear_each:

@@ -37,6 +37,21 @@ BUFFERS = ("mlp.1.running_mean", "mlp.1.running_var", "mlp.1.num_batches_tracked
            "mlp.5.running_mean", "mlp.5.running_var", "mlp.5.num_batches_tracked")
 
 
+def _events(probe, name):
+    """Start a (start, end) HIP-event pair on the current stream for kernel `name` (bench probes)."""
+    if probe is None:
+        return None
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    probe.setdefault(name, []).append((s, e))
+    return e
+
+
+def _events_end(e):
+    if e is not None:
+        e.record()
+
+
 def _pad4(n: int) -> int:
     return (n + 3) // 4 * 4
 
@@ -60,7 +75,8 @@ class FiBiNETTrainer:
             torch.manual_seed(seed)
             init_state = build_model(None, self.cfg).state_dict()
         # model structure (reuses the drop-in module's definition for names / shapes)
-        shape_model = build_model(None, dict(self.cfg, vocab_size=4))
+        with torch.random.fork_rng(devices=[]):            # no side effect on the caller's RNG stream
+            shape_model = build_model(None, dict(self.cfg, vocab_size=4))
         self.d = shape_model.emb_dim
         self.p_drop = shape_model.dropout_p
         self.fcfg = ops.FwdConfig(d=self.d, L=max_len, training=True, p_drop=self.p_drop,
@@ -131,8 +147,13 @@ class FiBiNETTrainer:
         self.stage_on_cpu = stage_on_cpu
 
     # ------------------------------------------------------------------ one training step
-    def step(self, batch: Dict[str, torch.Tensor], labels: torch.Tensor) -> torch.Tensor:
-        """One optimizer step on this rank's batch; returns the (device) global-mean BCE loss."""
+    def step(self, batch: Dict[str, torch.Tensor], labels: torch.Tensor,
+             masks_out: Optional[Dict[str, torch.Tensor]] = None, probe: Optional[Dict[str, list]] = None
+             ) -> torch.Tensor:
+        """One optimizer step on this rank's batch; returns the (device) global-mean BCE loss.
+
+        masks_out (tests only): {'m1': u8 [B,512], 'm2': u8 [B,256]} receives the dropout keep-masks.
+        """
         if self.host_step >= self.total_steps:
             raise ValueError(f"Tried to step {self.host_step + 1} times. The specified number of total steps is "
                              f"{self.total_steps}")
@@ -148,7 +169,8 @@ class FiBiNETTrainer:
             pos = self.xchg.cur_pos
         a = ops.forward(self.p, batch, cfg, self.rng, table_rows=rows, pos=pos,
                         sparse=self.sparse if self.xchg is None else None, err=self.err, labels=labels,
-                        loss_denom=float(ntot), coll=self.coll, ntot=ntot, acts=self.acts)
+                        loss_denom=float(ntot), coll=self.coll, ntot=ntot, acts=self.acts, masks_out=masks_out,
+                        probe=probe)
         call("fbn_sum", ptr(a["loss_terms"]), B, ptr(self.loss), 1.0 / ntot, st)
         sendbuf = self.xchg.make_sendbuf() if self.xchg is not None else None
         ops.backward(self.p, batch, a, a["gout"], self.g, cfg, table_grad=self.sparse["gU"],
@@ -166,9 +188,11 @@ class FiBiNETTrainer:
         call("fbn_clip_coef", ptr(self.sumsq), self.max_norm, ptr(self.coef), ptr(self.norm), st)
         call("fbn_adam_dense", ptr(self.flat_p), ptr(self.flat_g), ptr(self.flat_m), ptr(self.flat_v),
              self.n_dense, ptr(self.coef), ptr(self.sched), ptr(self.step_dev), self.wd, self.beta2, self.eps, st)
+        ev = _events(probe, "adam_table")
         call("fbn_adam_table", ptr(self.E), ptr(self.Em), ptr(self.Ev), self.rows_local, self.d,
              ptr(self.sparse["map"]), ptr(self.sparse["gU"]), ptr(self.coef), ptr(self.sched), ptr(self.step_dev),
              self.wd, self.beta2, self.eps, st)
+        _events_end(ev)
         call("fbn_zero_rows", ptr(self.sparse["gU"]), ptr(self.sparse["n_uniq"]), self.d, st)
         self.sumsq_tab.zero_()
         call("fbn_step_end", ptr(self.step_dev), ptr(self.rng), ptr(self.sparse["n_uniq"]), ptr(self.sumsq), st)
@@ -215,7 +239,8 @@ class FiBiNETTrainer:
                 full = torch.cat(parts)[:self.V].cpu()
         else:
             full = self.E.detach().cpu().clone()
-        order = list(build_model(None, dict(self.cfg, vocab_size=4)).state_dict().keys())
+        with torch.random.fork_rng(devices=[]):
+            order = list(build_model(None, dict(self.cfg, vocab_size=4)).state_dict().keys())
         for k in order:
             if k == TABLE:
                 out[k] = full
