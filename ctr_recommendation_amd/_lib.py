@@ -43,7 +43,7 @@ SIGNATURES = {
     "fbn_bn_finalize": (I, [P, P, D, I, P, P, P, P, F, F, I, P]),
     "fbn_bn_stats": (I, [P, I, I, P, P, P, P, F, F, I, P, P]),
     "fbn_bn_eval_params": (I, [P, P, P, P, I, F, P]),
-    "fbn_bn_act_fwd": (I, [P, P, I, I, P, P, P, P, F, P, U, P, P]),
+    "fbn_bn_act_fwd": (I, [P, P, I, I, P, P, P, P, F, P, U, P, P, P]),
     "fbn_bn_bwd_reduce": (I, [P, P, P, P, F, P, P, I, I, P, P, P]),
     "fbn_bn_bwd_apply": (I, [P, P, P, P, F, P, P, P, P, I, I, P, D, P, P, P, P, P, P]),
     "fbn_bn_bwd": (I, [P, P, P, P, F, P, P, P, P, I, I, P, P, P, P, P, P]),

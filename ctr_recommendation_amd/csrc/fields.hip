@@ -204,8 +204,28 @@ struct FieldBwdArgs {
   float ln_eps;
 };
 
-__device__ __forceinline__ void atomic_add_row4(float* dst, const f32x4& v) {
-  atomicAdd(dst + 0, v[0]); atomicAdd(dst + 1, v[1]); atomicAdd(dst + 2, v[2]); atomicAdd(dst + 3, v[3]);
+// Column-transposed copy of a group's row vector for coalesced atomics: lane q of a G-lane
+// group holds columns 4q..4q+3; after the transpose, t[e] is column e*G + q, so atomic
+// instruction e of the group covers one contiguous G*4-byte run of the row (full-rate
+// global_atomic_add_f32 shape) instead of four 16-B-strided runs.
+template <int G>
+__device__ __forceinline__ f32x4 transpose_cols(const f32x4& v, int lane) {
+  const int base = lane - lane % G, q = lane % G;
+  f32x4 t;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int src = base + e * (G / 4) + q / 4;
+    const float x0 = __shfl(v[0], src, 64), x1 = __shfl(v[1], src, 64);
+    const float x2 = __shfl(v[2], src, 64), x3 = __shfl(v[3], src, 64);
+    const int c = q & 3;
+    t[e] = c == 0 ? x0 : (c == 1 ? x1 : (c == 2 ? x2 : x3));
+  }
+  return t;
+}
+template <int G>
+__device__ __forceinline__ void atomic_add_row_t(float* row, const f32x4& t, int q) {
+  atomicAdd(row + q, t[0]); atomicAdd(row + G + q, t[1]); atomicAdd(row + 2 * G + q, t[2]);
+  atomicAdd(row + 3 * G + q, t[3]);
 }
 
 template <int D, int MODE>
@@ -328,16 +348,18 @@ __global__ void __launch_bounds__(256) fields_bwd_kernel(FieldBwdArgs p) {
     // item table: dX3 -> row item_id, dX5 / count -> each non-padding history row
     const f32x4 gh = dx[4] / p.cnt[b];
     if (MODE == 0) {
+      const f32x4 ti = transpose_cols<G>(dx[2], lane);
+      const f32x4 th = transpose_cols<G>(gh, lane);
       const long long item = p.item_id[b];
       if (item > 0 && item < p.V) {
         float* dst = p.map ? p.gtab + (size_t)p.map[item] * D : p.gtab + item * D;
-        atomic_add_row4(dst + 4 * q, dx[2]);
+        atomic_add_row_t<G>(dst, ti, q);
       }
       for (int t = 0; t < L; ++t) {
         const long long s = p.item_seq[(size_t)b * L + t];
         if (s > 0 && s < p.V) {
           float* dst = p.map ? p.gtab + (size_t)p.map[s] * D : p.gtab + s * D;
-          atomic_add_row4(dst + 4 * q, gh);
+          atomic_add_row_t<G>(dst, th, q);
         }
       }
     } else {
@@ -352,12 +374,30 @@ __global__ void __launch_bounds__(256) fields_bwd_kernel(FieldBwdArgs p) {
   for (int i = threadIdx.x; i < P; i += blockDim.x) out[i] = sp[i];
 }
 
-// Sum per-block partial slabs in block order: out[i] = sum_b part[b][i]  (deterministic)
-__global__ void reduce_partials_kernel(const float* part, int nblk, int P, float* out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// Sum per-block partial slabs: out[i] = sum_b part[b][i], in a fixed order (deterministic).
+// Level 1: grid (ceil(P/64), RED_CH) -- 64 columns x 4 row lanes per block, each chunk of
+// rows summed into part[nblk + chunk][i];  level 2: one wave per column over the chunks.
+#define RED_CH 16
+__global__ void reduce_partials_l1(float* part, int nblk, int P) {
+  __shared__ float red[4][64];
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rl = threadIdx.x >> 6;
+  const int per = (nblk + RED_CH - 1) / RED_CH;
+  const int r0 = blockIdx.y * per, r1 = min(nblk, r0 + per);
+  float s = 0.f;
+  if (i < P)
+    for (int r = r0 + rl; r < r1; r += 4) s += part[(size_t)r * P + i];
+  red[rl][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rl == 0 && i < P)
+    part[(size_t)(nblk + blockIdx.y) * P + i] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+__global__ void reduce_partials_l2(const float* part, int nblk, int P, float* out) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
   if (i >= P) return;
   float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += part[(size_t)b * P + i];
+#pragma unroll
+  for (int k = 0; k < RED_CH; ++k) s += part[(size_t)(nblk + k) * P + i];
   out[i] = s;
 }
 
@@ -408,7 +448,8 @@ extern "C" int fbn_fields_fwd(const int64_t* item_id, const int64_t* item_seq, c
 }
 
 extern "C" int fbn_fields_bwd_partials_size(int D, int R, int n_cate) { return 13 * R + 6 + 2 * D + n_cate * D; }
-extern "C" int fbn_fields_bwd_grid(int B, int D) { return fields_grid(B, D); }
+// rows of the `partials` scratch the caller allocates: one per block + RED_CH reduction rows
+extern "C" int fbn_fields_bwd_grid(int B, int D) { return fields_grid(B, D) + RED_CH; }
 
 template <int MODE>
 static int launch_fields_bwd(const FieldBwdArgs& a, int D, hipStream_t st) {
@@ -427,7 +468,8 @@ static int launch_fields_bwd(const FieldBwdArgs& a, int D, hipStream_t st) {
 }
 
 // partials: [fbn_fields_bwd_grid(B,D)][fbn_fields_bwd_partials_size(D,R,n_cate)] scratch;
-// param_grads: [P] output in the order w1, b1, w2, b2, ln_g, ln_b, cate.
+// partials: [fbn_fields_bwd_grid(B,D)][P] scratch; param_grads: [P] output in the order
+// w1, b1, w2, b2, ln_g, ln_b, cate.
 extern "C" int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes,
                               const int64_t* views, const float* hmm, const float* ln_g, float ln_eps,
                               const float* w1, const float* b1, const float* w2, int R, int n_cate,
@@ -446,8 +488,10 @@ extern "C" int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, c
   int rc = pos ? launch_fields_bwd<1>(p, D, st) : launch_fields_bwd<0>(p, D, st);
   if (rc) return rc;
   const int P = 13 * R + 6 + 2 * D + n_cate * D;
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(fbn_cdiv(P, 256)), dim3(256), 0, st, partials,
-                     fields_grid(B, D), P, param_grads);
+  const int nblk = fields_grid(B, D);
+  hipLaunchKernelGGL(reduce_partials_l1, dim3(fbn_cdiv(P, 64), RED_CH), dim3(256), 0, st, partials, nblk, P);
+  hipLaunchKernelGGL(reduce_partials_l2, dim3(fbn_cdiv(P, 64)), dim3(64), 0, st, (const float*)partials, nblk, P,
+                     param_grads);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

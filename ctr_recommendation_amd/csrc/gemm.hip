@@ -10,11 +10,20 @@
 // without materialising a compacted weight.
 //
 // Tiles: 256 threads = 4 waves in 2x2, each wave (BM/2)x(BN/2) made of 32x32 MFMA tiles.
-//   fp32 path: v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulate), BK = 16.
+//   fp32 path: v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulate), BK = 32.
 //   bf16 path: v_mfma_f32_32x32x16_bf16 (operands rounded to bf16 on the LDS store,
-//              f32 accumulate), BK = 32.
-// LDS holds both operands K-contiguous ([row][k], rows padded to 80 B), double-buffered;
-// global tiles are register-staged with 16-B loads (one barrier per K tile).
+//              f32 accumulate), BK = 64.
+// LDS holds both operands K-contiguous ([row][k], rows padded to 144 B so the 16-lane
+// groups of ds_read_b128 hit 16 distinct bank quads), double-buffered; global tiles are
+// register-staged with 16-B loads one tile ahead (one barrier per K tile).  Operands whose
+// contiguous dimension is M or N (the wgrad "T" A operand and the "N" B operand) are
+// loaded as 4x4 micro-blocks and transposed in registers, so every LDS store is a
+// 4-element k-run (ds_write_b64 / b128).
+// The host picks the tile (64x64 .. 128x128) and a split-K factor so that a launch has
+// >= 4 workgroups per CU: these GEMMs are short (K <= 2688 or M,N <= 512) and a single
+// workgroup per CU cannot hide the global-load latency behind its MFMAs.
+// Workgroups are remapped so that consecutive tiles (which share an A row panel) run on
+// one XCD and hit its L2 (MI355X: round-robin dispatch over 8 XCDs).
 // Split-K (gridDim.z > 1) writes f32 partial slabs that gemm_splitk_reduce sums in slab
 // order (deterministic).
 #include "common.h"
@@ -37,52 +46,71 @@ struct GemmArgs {
 };
 
 template <bool BF16> struct GemmTraits;
-template <> struct GemmTraits<false> { static constexpr int BK = 16; static constexpr int LDK = 20; typedef float T; };
-template <> struct GemmTraits<true>  { static constexpr int BK = 32; static constexpr int LDK = 40; typedef short T; };
+template <> struct GemmTraits<false> { static constexpr int BK = 32; static constexpr int LDK = 36; typedef float T; };
+template <> struct GemmTraits<true>  { static constexpr int BK = 64; static constexpr int LDK = 72; typedef short T; };
 
-// Stage one (rows x BK) operand tile from global into registers.
-// KC (K-contiguous): element (r,k) at P[(row0+r)*ld + map(k0+k)];  otherwise at P[(k0+k)*ld + map(row0+r)].
-template <int ROWS, int BK, bool KC, bool MAPK>
+template <typename T>
+__device__ __forceinline__ void st4(T* dst, float a, float b, float c, float d) {
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<f32x4*>(dst) = (f32x4){a, b, c, d};
+  } else {
+    *reinterpret_cast<bf16x4*>(dst) = (bf16x4){f2bf(a), f2bf(b), f2bf(c), f2bf(d)};
+  }
+}
+
+// Stage one (ROWS x BK) operand tile from global into registers.
+// KC (K-contiguous): element (r,k) at P[(row0+r)*ld + map(k0+k)]; chunks of 4 k per lane.
+// !KC: element (r,k) at P[(k0+k)*ld + map(row0+r)]; 4x4 micro-blocks (4 k x 4 rows) per lane.
+// MAP: apply the remap to the contiguous index (k for KC, the row index otherwise).
+template <int ROWS, int BK, bool KC, bool MAP>
 struct TileLoader {
-  static constexpr int CHUNKS = ROWS * BK / 4;
-  static constexpr int PER_T = CHUNKS / 256;
-  static_assert(CHUNKS % 256 == 0, "tile too small for 256 threads");
-  f32x4 v[PER_T];
+  static constexpr int UNITS = KC ? ROWS * BK / 4 : ROWS * BK / 16;
+  static constexpr int PER_T = (UNITS + 255) / 256;     // UNITS < 256: some lanes idle
+  static constexpr int NV = KC ? PER_T : PER_T * 4;
+  static_assert(UNITS % 256 == 0 || UNITS < 256, "tile / thread mismatch");
+  f32x4 v[NV];
 
-  __device__ __forceinline__ void load(const float* __restrict__ P, int ld, int row0, int nrows, int k0,
-                                       int kend, const Remap& rm) {
+  __device__ __forceinline__ f32x4 ld4(const float* __restrict__ P, int ld, int row, int nrows, int k, int kend,
+                                       const Remap& rm) const {
+    f32x4 x = {0.f, 0.f, 0.f, 0.f};
+    if (KC) {
+      if (row < nrows) {
+        if (k + 3 < kend) {
+          x = *reinterpret_cast<const f32x4*>(P + (size_t)row * ld + (MAP ? remap(rm, k) : k));
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (k + e < kend) x[e] = P[(size_t)row * ld + (MAP ? remap(rm, k + e) : k + e)];
+        }
+      }
+    } else {
+      if (k < kend) {
+        if (row + 3 < nrows) {
+          x = *reinterpret_cast<const f32x4*>(P + (size_t)k * ld + (MAP ? remap(rm, row) : row));
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (row + e < nrows) x[e] = P[(size_t)k * ld + (MAP ? remap(rm, row + e) : row + e)];
+        }
+      }
+    }
+    return x;
+  }
+
+  __device__ __forceinline__ void load(const float* __restrict__ P, int ld, int row0, int nrows, int k0, int kend,
+                                       const Remap& rm) {
 #pragma unroll
     for (int i = 0; i < PER_T; ++i) {
       const int c = threadIdx.x + 256 * i;
-      f32x4 x = {0.f, 0.f, 0.f, 0.f};
+      if (UNITS < 256 && c >= UNITS) continue;
       if (KC) {
         const int r = c / (BK / 4), kk = (c % (BK / 4)) * 4;
-        const int row = row0 + r, k = k0 + kk;
-        if (row < nrows) {
-          if (k + 3 < kend) {
-            const int kg = MAPK ? remap(rm, k) : k;
-            x = *reinterpret_cast<const f32x4*>(P + (size_t)row * ld + kg);
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if (k + e < kend) x[e] = P[(size_t)row * ld + (MAPK ? remap(rm, k + e) : k + e)];
-          }
-        }
+        v[i] = ld4(P, ld, row0 + r, nrows, k0 + kk, kend, rm);
       } else {
-        const int kk = c / (ROWS / 4), r = (c % (ROWS / 4)) * 4;
-        const int k = k0 + kk, row = row0 + r;
-        if (k < kend) {
-          if (row + 3 < nrows) {
-            const int rg = MAPK ? remap(rm, row) : row;
-            x = *reinterpret_cast<const f32x4*>(P + (size_t)k * ld + rg);
-          } else {
+        const int r = (c % (ROWS / 4)) * 4, kk = (c / (ROWS / 4)) * 4;
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if (row + e < nrows) x[e] = P[(size_t)k * ld + (MAPK ? remap(rm, row + e) : row + e)];
-          }
-        }
+        for (int j = 0; j < 4; ++j) v[i * 4 + j] = ld4(P, ld, row0 + r, nrows, k0 + kk + j, kend, rm);
       }
-      v[i] = x;
     }
   }
 
@@ -91,28 +119,22 @@ struct TileLoader {
 #pragma unroll
     for (int i = 0; i < PER_T; ++i) {
       const int c = threadIdx.x + 256 * i;
+      if (UNITS < 256 && c >= UNITS) continue;
       if (KC) {
         const int r = c / (BK / 4), kk = (c % (BK / 4)) * 4;
-        if constexpr (sizeof(T) == 4) {
-          *reinterpret_cast<f32x4*>(S + r * LDK + kk) = v[i];
-        } else {
-          bf16x4 b = {f2bf(v[i][0]), f2bf(v[i][1]), f2bf(v[i][2]), f2bf(v[i][3])};
-          *reinterpret_cast<bf16x4*>(S + r * LDK + kk) = b;
-        }
+        st4<T>(S + r * LDK + kk, v[i][0], v[i][1], v[i][2], v[i][3]);
       } else {
-        const int kk = c / (ROWS / 4), r = (c % (ROWS / 4)) * 4;
+        const int r = (c % (ROWS / 4)) * 4, kk = (c / (ROWS / 4)) * 4;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if constexpr (sizeof(T) == 4) S[(r + e) * LDK + kk] = v[i][e];
-          else S[(r + e) * LDK + kk] = f2bf(v[i][e]);
-        }
+        for (int e = 0; e < 4; ++e)   // row r+e gets the 4-k run (kk..kk+3): register transpose
+          st4<T>(S + (r + e) * LDK + kk, v[i * 4 + 0][e], v[i * 4 + 1][e], v[i * 4 + 2][e], v[i * 4 + 3][e]);
       }
     }
   }
 };
 
 template <int BM, int BN, bool TA, bool TB, bool BF16>
-__global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
+__global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int remap_xcd) {
   typedef GemmTraits<BF16> Tr;
   typedef typename Tr::T T;
   constexpr int BK = Tr::BK, LDK = Tr::LDK;
@@ -120,7 +142,13 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) T sA[2][BM * LDK];
   __shared__ __attribute__((aligned(16))) T sB[2][BN * LDK];
 
-  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  // XCD-aware tile order: dispatch deals blocks round-robin over 8 XCDs, so block b runs on
+  // XCD b % 8; give each XCD a contiguous run of tiles (neighbours share the A row panel).
+  int bid = blockIdx.x;
+  const int nb = gridDim.x;
+  if (remap_xcd) bid = (bid % 8) * (nb / 8) + bid / 8;
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int n0 = tn * BN, m0 = tm * BM;
   const int kbeg = blockIdx.z * g.kchunk;
   const int kend = min(g.K, kbeg + g.kchunk);
   const int ntiles = (kend - kbeg + BK - 1) / BK;
@@ -160,31 +188,27 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
     const T* A_ = sA[buf];
     const T* B_ = sB[buf];
     if constexpr (!BF16) {
-      // k permutation: lane half h covers k in [8h, 8h+8); step s uses k = 8h + s for A and B.
-      f32x4 af[TM][2], bfr[TN][2];
+      // k permutation: lane half h covers k in [16h, 16h+16); step s uses k = 16h + s for A and B.
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const float* p = A_ + (wm * WM + i * 32 + lr) * LDK + lh * 8;
-        af[i][0] = *reinterpret_cast<const f32x4*>(p);
-        af[i][1] = *reinterpret_cast<const f32x4*>(p + 4);
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const float* p = B_ + (wn * WN + j * 32 + lr) * LDK + lh * 8;
-        bfr[j][0] = *reinterpret_cast<const f32x4*>(p);
-        bfr[j][1] = *reinterpret_cast<const f32x4*>(p + 4);
-      }
-#pragma unroll
-      for (int s = 0; s < 8; ++s)
+      for (int q = 0; q < 4; ++q) {
+        f32x4 af[TM], bfr[TN];
 #pragma unroll
         for (int i = 0; i < TM; ++i)
+          af[i] = *reinterpret_cast<const f32x4*>(A_ + (wm * WM + i * 32 + lr) * LDK + lh * 16 + q * 4);
 #pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s >> 2][s & 3], bfr[j][s >> 2][s & 3],
-                                                             acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j)
+          bfr[j] = *reinterpret_cast<const f32x4*>(B_ + (wn * WN + j * 32 + lr) * LDK + lh * 16 + q * 4);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bfr[j][s], acc[i][j], 0, 0, 0);
+      }
     } else {
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
+      for (int s = 0; s < BK / 16; ++s) {
         bf16x8 af[TM], bfr[TN];
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -246,31 +270,48 @@ __global__ void gemm_splitk_reduce(GemmArgs g, int nsplit) {
   }
 }
 
+// ------------------------------------------------------------------ host-side planning
+struct GemmPlan {
+  int bm, bn, split;
+};
+
+static GemmPlan plan_gemm(int M, int N, int K, int bk) {
+  // Prefer the biggest tile that still yields >= 1024 workgroups (4 per CU); otherwise the
+  // smallest tile, then split K until ~1024 workgroups or K per split drops to 4 tiles.
+  const int cand[4][2] = {{128, 128}, {128, 64}, {64, 128}, {64, 64}};
+  GemmPlan p = {64, 64, 1};
+  for (int c = 0; c < 4; ++c) {
+    const int bm = cand[c][0], bn = cand[c][1];
+    if ((bm == 128 && M < 256) || (bn == 128 && N < 256)) continue;   // mostly-empty tiles
+    const long long tiles = (long long)fbn_cdiv(M, bm) * fbn_cdiv(N, bn);
+    if (tiles >= 1024) { p = {bm, bn, 1}; return p; }
+  }
+  const long long tiles = (long long)fbn_cdiv(M, 64) * fbn_cdiv(N, 64);
+  int s = 1;
+  while (tiles * s < 1024 && K / (s * 2) >= 4 * bk && s < 64) s *= 2;
+  p.split = s;
+  return p;
+}
+
 template <int BM, int BN, bool TA, bool TB, bool BF16>
 static void launch_tile(const GemmArgs& g, int nsplit, hipStream_t st) {
-  dim3 grid(fbn_cdiv(g.N, BN), fbn_cdiv(g.M, BM), nsplit);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, TA, TB, BF16>), grid, dim3(256), 0, st, g);
+  const int tn = fbn_cdiv(g.N, BN), tm = fbn_cdiv(g.M, BM);
+  const int nb = tn * tm;
+  dim3 grid(nb, 1, nsplit);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, TA, TB, BF16>), grid, dim3(256), 0, st, g, tn, (nb % 8 == 0) ? 1 : 0);
 }
 
 template <bool TA, bool TB, bool BF16>
-static void launch_sel(const GemmArgs& g, int nsplit, hipStream_t st) {
-  if (g.N <= 64 || g.M <= 64) launch_tile<64, 64, TA, TB, BF16>(g, nsplit, st);
-  else launch_tile<128, 128, TA, TB, BF16>(g, nsplit, st);
-}
-
-// Host-side split-K choice: fill ~2 waves of the 256-CU chip for reduction-heavy (wgrad) shapes.
-static int choose_split(int M, int N, int K, int bk) {
-  const int bm = (N <= 64 || M <= 64) ? 64 : 128;
-  const int tiles = fbn_cdiv(M, bm) * fbn_cdiv(N, bm);
-  int s = 1;
-  while (tiles * s < 512 && K / (s * 2) >= 8 * bk && s < 64) s *= 2;
-  return s;
+static void launch_sel(const GemmArgs& g, const GemmPlan& p, hipStream_t st) {
+  if (p.bm == 128 && p.bn == 128) launch_tile<128, 128, TA, TB, BF16>(g, p.split, st);
+  else if (p.bm == 128) launch_tile<128, 64, TA, TB, BF16>(g, p.split, st);
+  else if (p.bn == 128) launch_tile<64, 128, TA, TB, BF16>(g, p.split, st);
+  else launch_tile<64, 64, TA, TB, BF16>(g, p.split, st);
 }
 
 extern "C" size_t fbn_gemm_workspace_size(int M, int N, int K, int bf16) {
-  const int bk = bf16 ? 32 : 16;
-  const int s = choose_split(M, N, K, bk);
-  return s > 1 ? (size_t)s * M * N * sizeof(float) : 0;
+  const GemmPlan p = plan_gemm(M, N, K, bf16 ? 64 : 32);
+  return p.split > 1 ? (size_t)p.split * M * N * sizeof(float) : 0;
 }
 
 extern "C" int fbn_gemm(const float* A, const float* B, float* C, const float* bias, int M, int N, int K,
@@ -291,32 +332,32 @@ extern "C" int fbn_gemm(const float* A, const float* B, float* C, const float* b
   g.rB = {rB_seg, rB_off0, rB_off1};
   g.rC = {rC_seg, rC_off0, rC_off1};
   g.beta = beta;
-  const int bk = bf16 ? 32 : 16;
-  int nsplit = choose_split(M, N, K, bk);
-  if (nsplit > 1 && (!ws || ws_bytes < (size_t)nsplit * M * N * sizeof(float))) nsplit = 1;
-  int per = fbn_cdiv(K, nsplit);
+  const int bk = bf16 ? 64 : 32;
+  GemmPlan p = plan_gemm(M, N, K, bk);
+  if (p.split > 1 && (!ws || ws_bytes < (size_t)p.split * M * N * sizeof(float))) p.split = 1;
+  int per = fbn_cdiv(K, p.split);
   per = fbn_cdiv(per, bk) * bk;
-  nsplit = K > 0 ? fbn_cdiv(K, per) : 1;
+  p.split = K > 0 ? fbn_cdiv(K, per) : 1;
   g.kchunk = K > 0 ? per : 0;
   g.ws = ws;
   hipStream_t st = (hipStream_t)stream;
   const int key = (transA ? 4 : 0) | (transB ? 2 : 0) | (bf16 ? 1 : 0);
   switch (key) {
-    case 0: launch_sel<false, false, false>(g, nsplit, st); break;
-    case 1: launch_sel<false, false, true>(g, nsplit, st); break;
-    case 2: launch_sel<false, true, false>(g, nsplit, st); break;
-    case 3: launch_sel<false, true, true>(g, nsplit, st); break;
-    case 4: launch_sel<true, false, false>(g, nsplit, st); break;
-    case 5: launch_sel<true, false, true>(g, nsplit, st); break;
-    case 6: launch_sel<true, true, false>(g, nsplit, st); break;
-    default: launch_sel<true, true, true>(g, nsplit, st); break;
+    case 0: launch_sel<false, false, false>(g, p, st); break;
+    case 1: launch_sel<false, false, true>(g, p, st); break;
+    case 2: launch_sel<false, true, false>(g, p, st); break;
+    case 3: launch_sel<false, true, true>(g, p, st); break;
+    case 4: launch_sel<true, false, false>(g, p, st); break;
+    case 5: launch_sel<true, false, true>(g, p, st); break;
+    case 6: launch_sel<true, true, false>(g, p, st); break;
+    default: launch_sel<true, true, true>(g, p, st); break;
   }
   FBN_CHECK_LAUNCH();
-  if (nsplit > 1) {
+  if (p.split > 1) {
     const size_t total = (size_t)M * N;
     int blocks = (int)((total + 255) / 256);
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, st, g, nsplit);
+    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, st, g, p.split);
     FBN_CHECK_LAUNCH();
   }
   return FBN_OK;

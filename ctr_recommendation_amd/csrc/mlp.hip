@@ -17,8 +17,10 @@
 
 // ------------------------------------------------------------------ bilinear pairs
 // pair index k enumerates (i,j), 1<=i<j<=5 lexicographically: (1,2)(1,3)(1,4)(1,5)(2,3)...(4,5)
-__constant__ int c_pi[10] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3};
-__constant__ int c_pj[10] = {1, 2, 3, 4, 2, 3, 4, 3, 4, 4};
+// constexpr (not __constant__) so that fully unrolled loops index register arrays with
+// compile-time constants -- a runtime index would spill the arrays to scratch
+__device__ constexpr int c_pi[10] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3};
+__device__ constexpr int c_pj[10] = {1, 2, 3, 4, 2, 3, 4, 3, 4, 4};
 
 // mode 0 ("all"): p = V_i * U_j ; mode 1 ("each"): p = U_i * V_j   (field indices 0..4 = fields 1..5)
 __global__ void pairs_fwd_kernel(const float* __restrict__ Vc, const float* __restrict__ U, float* __restrict__ c,
@@ -96,13 +98,17 @@ __global__ void colstat_partial_kernel(const float* __restrict__ X, int B, int C
     part[(size_t)blockIdx.y * C + col] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
 }
 
-// out[c] = sum_k part[k][c]   (fixed chunk order: deterministic)
+// out[c] = sum_k part[k][c]: one wave per column, lanes stride the chunks, fixed shuffle tree
+// (deterministic; the chunk loads are independent instead of a serial dependent chain)
 __global__ void chunk_reduce_kernel(const double* part, int nchunk, int C, double* out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
   if (c >= C) return;
   double s = 0.0;
-  for (int k = 0; k < nchunk; ++k) s += part[(size_t)k * C + c];
-  out[c] = s;
+  for (int k = lane; k < nchunk; k += 64) s += part[(size_t)k * C + c];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) out[c] = s;
 }
 
 __global__ void bn_mean_kernel(const double* sum, double ntot, int C, double* mean) {
@@ -141,7 +147,7 @@ __global__ void bn_act_fwd_kernel(const float* __restrict__ X, float* __restrict
                                   const float* __restrict__ mean, const float* __restrict__ invstd,
                                   const float* __restrict__ g, const float* __restrict__ bta, float p_drop,
                                   const unsigned long long* __restrict__ rng, unsigned stream_id,
-                                  unsigned char* __restrict__ mask_out) {
+                                  unsigned char* __restrict__ mask_out, const unsigned char* __restrict__ mask_in) {
   const size_t total4 = (size_t)B * C / 4;
   const float keep = 1.f - p_drop;
   const float scale = p_drop > 0.f ? 1.0f / keep : 1.f;
@@ -153,7 +159,7 @@ __global__ void bn_act_fwd_kernel(const float* __restrict__ X, float* __restrict
     f32x4 x = *reinterpret_cast<const f32x4*>(X + i);
     f32x4 y;
     float um[4] = {1.f, 1.f, 1.f, 1.f};
-    if (p_drop > 0.f) {
+    if (p_drop > 0.f && !mask_in) {
       const Philox4 r = philox4x32_10((uint32_t)i4, (uint32_t)(i4 >> 32), stream_id, off, k0, k1);
       um[0] = u01(r.x); um[1] = u01(r.y); um[2] = u01(r.z); um[3] = u01(r.w);
     }
@@ -163,7 +169,7 @@ __global__ void bn_act_fwd_kernel(const float* __restrict__ X, float* __restrict
       const float bp = bta[col + e] - mean[col + e] * alpha;
       float v = fmaxf(x[e] * alpha + bp, 0.f);
       if (p_drop > 0.f) {
-        const bool kept = um[e] < keep;
+        const bool kept = mask_in ? mask_in[i + e] != 0 : um[e] < keep;
         v = kept ? v * scale : 0.f;
         if (mask_out) mask_out[i + e] = kept ? 1 : 0;
       }
@@ -261,11 +267,13 @@ __global__ void colsum_partial_kernel(const float* __restrict__ X, int B, int C,
     part[(size_t)blockIdx.y * C + c] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
 }
 __global__ void colsum_final_kernel(const float* part, int nchunk, int C, float* out, float beta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
   if (c >= C) return;
   float s = 0.f;
-  for (int k = 0; k < nchunk; ++k) s += part[(size_t)k * C + c];
-  out[c] = beta != 0.f ? out[c] * beta + s : s;
+  for (int k = lane; k < nchunk; k += 64) s += part[(size_t)k * C + c];
+  s = wave_sum(s);
+  if (lane == 0) out[c] = beta != 0.f ? out[c] * beta + s : s;
 }
 
 // ------------------------------------------------------------------ head: o = h.w + b, p = sigmoid(o), BCE
@@ -368,7 +376,7 @@ extern "C" int fbn_bn_stats_pass(const float* X, int B, int C, const double* mea
   double* part = (double*)ws;
   hipLaunchKernelGGL(colstat_partial_kernel, dim3(fbn_cdiv(C, 64), nch), dim3(256), 0, st, X, B, C, C, rpc, mean_d,
                      part, mean_d ? 1 : 0);
-  hipLaunchKernelGGL(chunk_reduce_kernel, dim3(fbn_cdiv(C, 256)), dim3(256), 0, st, part, nch, C, out_d);
+  hipLaunchKernelGGL(chunk_reduce_kernel, dim3(fbn_cdiv(C, 4)), dim3(256), 0, st, part, nch, C, out_d);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -411,15 +419,17 @@ extern "C" int fbn_bn_eval_params(const float* run_mean, const float* run_var, f
   return FBN_OK;
 }
 
-// rng: device [seed, offset] (uint64 x2) or null; mask_out (optional, u8 [B][C]) for parity tests
+// rng: device [seed, offset] (uint64 x2) or null; mask_out (optional, u8 [B][C]) receives the keep-mask;
+// mask_in (optional, u8 [B][C]) replaces the RNG (parity tests against injected masks)
 extern "C" int fbn_bn_act_fwd(const float* X, float* Y, int B, int C, const float* mean, const float* invstd,
                               const float* g, const float* b, float p_drop, const unsigned long long* rng,
-                              unsigned stream_id, unsigned char* mask_out, void* stream) {
+                              unsigned stream_id, unsigned char* mask_out, const unsigned char* mask_in,
+                              void* stream) {
   if (B <= 0) return FBN_OK;
   if (C & 3) { fbn_set_error("bn_act: C % 4"); return FBN_ERR_ARG; }
-  if (p_drop > 0.f && !rng) { fbn_set_error("bn_act: dropout needs an rng state"); return FBN_ERR_ARG; }
+  if (p_drop > 0.f && !rng && !mask_in) { fbn_set_error("bn_act: dropout needs an rng state or a mask"); return FBN_ERR_ARG; }
   hipLaunchKernelGGL(bn_act_fwd_kernel, dim3(ew_grid((size_t)B * C / 4)), dim3(256), 0, (hipStream_t)stream, X, Y, B,
-                     C, mean, invstd, g, b, p_drop, rng, stream_id, mask_out);
+                     C, mean, invstd, g, b, p_drop, rng, stream_id, mask_out, mask_in);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -434,7 +444,7 @@ extern "C" int fbn_bn_bwd_reduce(const float* G, const float* gvec, const float*
   const int nch = row_chunks(B), rpc = B > 0 ? (B + nch - 1) / nch : 1;
   double* part = (double*)ws;
   hipLaunchKernelGGL(bn_bwd_partial_kernel, dim3(fbn_cdiv(C, 64), nch), dim3(256), 0, st, s, Xpre, mean, B, C, rpc, part);
-  hipLaunchKernelGGL(chunk_reduce_kernel, dim3(fbn_cdiv(3 * C, 256)), dim3(256), 0, st, part, nch, 3 * C, red_d);
+  hipLaunchKernelGGL(chunk_reduce_kernel, dim3(fbn_cdiv(3 * C, 4)), dim3(256), 0, st, part, nch, 3 * C, red_d);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -475,7 +485,7 @@ extern "C" int fbn_colsum(const float* X, int B, int C, int ldx, float* out, flo
   hipStream_t st = (hipStream_t)stream;
   const int nch = row_chunks(B), rpc = (B + nch - 1) / nch;
   hipLaunchKernelGGL(colsum_partial_kernel, dim3(fbn_cdiv(C, 64), nch), dim3(256), 0, st, X, B, C, ldx, rpc, (float*)ws);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3(fbn_cdiv(C, 256)), dim3(256), 0, st, (const float*)ws, nch, C, out, beta);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(fbn_cdiv(C, 4)), dim3(256), 0, st, (const float*)ws, nch, C, out, beta);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

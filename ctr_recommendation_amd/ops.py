@@ -112,7 +112,8 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
             err: Optional[torch.Tensor] = None, labels: Optional[torch.Tensor] = None,
             loss_denom: Optional[float] = None, coll: Collective = NO_COLLECTIVE, ntot: Optional[int] = None,
             masks_out: Optional[Dict[str, torch.Tensor]] = None, acts: Optional[Dict[str, torch.Tensor]] = None,
-            probe: Optional[Dict[str, list]] = None) -> Dict[str, torch.Tensor]:
+            probe: Optional[Dict[str, list]] = None, masks_in: Optional[Dict[str, torch.Tensor]] = None
+            ) -> Dict[str, torch.Tensor]:
     """Run the forward; returns the activation dict (probs, logits and what backward needs).
 
     p: parameter tensors keyed like the reference state_dict (fp32, contiguous, on device).
@@ -190,13 +191,15 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     p_drop = cfg.p_drop if cfg.training else 0.0
     m1 = masks_out.get("m1") if masks_out else None
     m2 = masks_out.get("m2") if masks_out else None
+    mi1 = masks_in.get("m1") if masks_in else None
+    mi2 = masks_in.get("m2") if masks_in else None
     if cfg.training:
         bn_train_stats(h1pre, B, H1, mean1, inv1, p["mlp.1.running_mean"], p["mlp.1.running_var"], ntot, coll, st)
     else:
         call("fbn_bn_eval_params", ptr(p["mlp.1.running_mean"]), ptr(p["mlp.1.running_var"]), ptr(mean1), ptr(inv1),
              H1, BN_EPS, st)
     call("fbn_bn_act_fwd", ptr(h1pre), ptr(h1), B, H1, ptr(mean1), ptr(inv1), ptr(p["mlp.1.weight"]),
-         ptr(p["mlp.1.bias"]), float(p_drop), ptr(rng), 1, ptr(m1), st)
+         ptr(p["mlp.1.bias"]), float(p_drop), ptr(rng), 1, ptr(m1), ptr(mi1), st)
     gemm(h1, p["mlp.4.weight"], h2pre, B, H2, H1, H1, H1, H2, False, True, bias=p["mlp.4.bias"], bf16=cfg.bf16,
          stream=st)
     if cfg.training:
@@ -205,7 +208,7 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
         call("fbn_bn_eval_params", ptr(p["mlp.5.running_mean"]), ptr(p["mlp.5.running_var"]), ptr(mean2), ptr(inv2),
              H2, BN_EPS, st)
     call("fbn_bn_act_fwd", ptr(h2pre), ptr(h2), B, H2, ptr(mean2), ptr(inv2), ptr(p["mlp.5.weight"]),
-         ptr(p["mlp.5.bias"]), float(p_drop), ptr(rng), 2, ptr(m2), st)
+         ptr(p["mlp.5.bias"]), float(p_drop), ptr(rng), 2, ptr(m2), ptr(mi2), st)
     logits, probs = buf("logits", (B,)), buf("probs", (B,))
     lt = buf("loss_terms", (B,)) if labels is not None else None
     go = buf("gout", (B,)) if labels is not None else None

@@ -97,7 +97,7 @@ int fbn_bn_eval_params(const float* run_mean, const float* run_var, float* mean,
                        void* stream);
 int fbn_bn_act_fwd(const float* X, float* Y, int B, int C, const float* mean, const float* invstd, const float* g,
                    const float* b, float p_drop, const unsigned long long* rng, unsigned stream_id,
-                   unsigned char* mask_out, void* stream);
+                   unsigned char* mask_out, const unsigned char* mask_in, void* stream);
 int fbn_bn_bwd_reduce(const float* G, const float* gvec, const float* w, const float* hact, float scale,
                       const float* Xpre, const float* mean, int B, int C, double* red_d, void* ws, void* stream);
 int fbn_bn_bwd_apply(const float* G, const float* gvec, const float* w, const float* hact, float scale,

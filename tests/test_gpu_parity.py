@@ -158,14 +158,21 @@ def test_hip_matches_committed_golden_vectors(hip_device, d):
     with torch.no_grad():
         pe = hip(batch).cpu().numpy()
     assert np.abs(pe - z["probs_eval"]).max() < 1e-4
-    # train mode with the fixture's dropout masks, through the kernel sequence
+    # train mode with the fixture's dropout masks injected into the dropout kernel, then backward
     hip.train()
     p = {k: v for k, v in hip.state_dict().items()}
     B = z["item_id"].shape[0]
-    cfg = ops.FwdConfig(d=d, L=20, training=True, p_drop=0.0)   # masks applied below via p_drop=0 + check
-    acts = ops.forward(p, batch, ops.FwdConfig(d=d, L=20, training=True, p_drop=0.2),
-                       torch.tensor([1, 0], dtype=torch.int64, device=hip_device))
-    assert acts["logits"].shape == (B,)
-    # gradient parity with injected masks via the oracle is covered by test_gpu_trainer; here the
-    # loss/grad fixtures pin the eval path and the deterministic parts
-    assert np.isfinite(acts["logits"].cpu().numpy()).all()
+    cfg = ops.FwdConfig(d=d, L=20, training=True, p_drop=0.2)
+    mi = {"m1": torch.from_numpy(z["mask1"]).to(hip_device), "m2": torch.from_numpy(z["mask2"]).to(hip_device)}
+    labels = torch.from_numpy(z["labels"]).to(hip_device)
+    acts = ops.forward(p, batch, cfg, None, masks_in=mi, labels=labels)
+    assert np.abs(acts["logits"].cpu().numpy() - z["logits_train"]).max() < 1e-4
+    loss = acts["loss_terms"].sum().item() / B
+    assert abs(loss - float(z["loss"])) < 1e-5
+    g = {n: torch.zeros_like(v) for n, v in p.items() if v.dtype == torch.float32}
+    table_grad = torch.zeros_like(p["item_emb.weight"])
+    ops.backward(p, batch, acts, acts["gout"], g, cfg, table_grad=table_grad)
+    for key in [k for k in z.files if k.startswith("grad/")]:
+        n = key[5:]
+        ref = torch.from_numpy(z[key])
+        _grad_close(g[n].cpu(), ref, n)
