@@ -101,9 +101,18 @@ def bn_backward(G, gvec, w, hact, scale, hpre, mean, invstd, gamma, B, C, ntot, 
     red = torch.empty(3 * C, dtype=torch.float64, device=dev)
     call("fbn_bn_bwd_reduce", ptr(G), ptr(gvec), ptr(w), ptr(hact), float(scale), ptr(hpre), ptr(mean), B, C,
          ptr(red), ptr(ws), stream)
-    coll.allreduce_(red)
+    red_g = red
+    if coll.world > 1:
+        red_g = red.clone()
+        coll.allreduce_(red_g)            # global sums -> the SyncBN input gradient
     call("fbn_bn_bwd_apply", ptr(G), ptr(gvec), ptr(w), ptr(hact), float(scale), ptr(hpre), ptr(mean), ptr(invstd),
-         ptr(gamma), B, C, ptr(red), float(ntot), ptr(dpre), ptr(dgamma), ptr(dbeta), ptr(dw), ptr(ws), stream)
+         ptr(gamma), B, C, ptr(red_g), float(ntot), ptr(dpre), ptr(dgamma), ptr(dbeta), ptr(dw), ptr(ws), stream)
+    if coll.world > 1:
+        # parameter grads from this rank's sums only (the dense-grad all-reduce adds the ranks);
+        # B = 0 runs just the finalize step, after the apply above has consumed its coefficients
+        call("fbn_bn_bwd_apply", ptr(G), ptr(gvec), ptr(w), ptr(hact), float(scale), ptr(hpre), ptr(mean),
+             ptr(invstd), ptr(gamma), 0, C, ptr(red), float(ntot), None, ptr(dgamma), ptr(dbeta), ptr(dw),
+             ptr(ws), stream)
 
 
 def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: FwdConfig,

@@ -132,6 +132,7 @@ class FiBiNETTrainer:
         self.sched = torch.from_numpy(tab).to(dev)
         self.step_dev = torch.zeros(1, **i32)
         seed_d = dropout_seed if dropout_seed is not None else (seed * 1000003 + 17)
+        seed_d += rank * 0x9E3779B9            # independent dropout stream per rank
         self.rng = torch.tensor([seed_d & 0x7FFFFFFFFFFF, 0], dtype=torch.int64, device=dev)
         self.sumsq = torch.zeros(1, dtype=torch.float64, device=dev)
         self.sumsq_tab = torch.zeros(1, dtype=torch.float64, device=dev)
@@ -178,6 +179,7 @@ class FiBiNETTrainer:
                      coll=self.coll, ntot=ntot)
         if self.xchg is not None:
             self.coll.allreduce_(self.flat_g)
+            self.coll.allreduce_(self.loss)
             self.xchg.backward(sendbuf, self.sparse)
         # clip_grad_norm_(10): dense grads (identical on every rank) + disjoint table shards
         call("fbn_sumsq", ptr(self.sparse["gU"]), 0, ptr(self.sparse["n_uniq"]), self.d, ptr(self.sumsq_tab), st)

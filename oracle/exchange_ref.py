@@ -1,0 +1,55 @@
+"""CPU restatement of the row-shard exchange kernels (exchange.hip) -- TEST INFRASTRUCTURE ONLY.
+
+Lets tests/test_exchange_gloo.py run the real ``RowExchange`` protocol (routing, split
+bookkeeping, all_to_all_single over gloo, sparse reduce-scatter) on CPU ranks.  The
+semantics restated here are the product's own contract for the sharded path (the reference
+has no sharding; it replicates the table with DataParallel, src/train_fibinet.py:69-70):
+owner = id // Vl; item slot always routed; history slot routed iff id != 0; padding row
+(global id 0) gathered but never updated.
+"""
+from __future__ import annotations
+
+import torch
+
+
+class CpuExchangeKernels:
+    def route(self, item, seq, B, L, V, Vl, world, counts, offsets, cursor, send_ids, pos, err):
+        ids = item.view(B, 1) if seq is None or L == 0 else torch.cat([item.view(B, 1), seq.view(B, L)], dim=1)
+        valid = (ids >= 0) & (ids < V)
+        if not bool(valid.all()):
+            err.fill_(1)
+        routed = valid.clone()
+        routed[:, 1:] &= ids[:, 1:] != 0
+        owner = torch.where(routed, ids // Vl, torch.zeros_like(ids))
+        counts.zero_()
+        for o in range(world):
+            counts[o] = int(((owner == o) & routed).sum())
+        offs = torch.zeros(world + 1, dtype=torch.int64)
+        offs[1:] = torch.cumsum(counts.to(torch.int64), 0)
+        offsets.copy_(offs.to(offsets.dtype))
+        cursor.zero_()
+        pos.fill_(-1)
+        cur = offs[:-1].clone()
+        for b in range(B):
+            for t in range(ids.shape[1]):
+                if routed[b, t]:
+                    o = int(owner[b, t])
+                    p = int(cur[o])
+                    cur[o] += 1
+                    send_ids[p] = int(ids[b, t] - o * Vl)
+                    pos[b, t] = p
+
+    def owner_gather(self, ids, E, out, map_, n_uniq, uniq_rows, rank, d):
+        for i, r in enumerate(ids.tolist()):
+            out[i] = E[r]
+            if map_ is not None and not (rank == 0 and r == 0) and int(map_[r]) == -1:
+                u = int(n_uniq[0])
+                map_[r] = u
+                uniq_rows[u] = r
+                n_uniq[0] = u + 1
+
+    def owner_scatter(self, ids, grad, map_, gU, rank, d):
+        for i, r in enumerate(ids.tolist()):
+            if rank == 0 and r == 0:
+                continue
+            gU[int(map_[r])] += grad[i]
