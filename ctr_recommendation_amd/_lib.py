@@ -29,13 +29,13 @@ SIGNATURES = {
     "fbn_last_error": (ctypes.c_char_p, []),
     "fbn_device_ok": (I, []),
     "fbn_gemm_workspace_size": (SZ, [I, I, I, I]),
-    "fbn_gemm": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, F, I, P, SZ, P]),
-    "fbn_fields_fwd": (I, [P, P, P, P, P, P, P, F, P, I, P, LL, P, P, P, P, P, I, P, P, P, I, P, P, P, P, P, P,
+    "fbn_gemm": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, F, I, I, I, P, SZ, P]),
+    "fbn_fields_fwd": (I, [P, P, P, P, P, P, P, F, P, I, P, LL, P, P, P, P, P, I, P, P, P, I, I, P, P, P, P, P,
                            I, I, I, P]),
     "fbn_fields_bwd_partials_size": (I, [I, I, I]),
     "fbn_fields_bwd_grid": (I, [I, I]),
     "fbn_fields_bwd": (I, [P, P, P, P, P, P, F, P, P, P, I, I, P, P, P, P, P, P, P, P, P, LL, P, P, I, I, I, P]),
-    "fbn_pairs_fwd": (I, [P, P, P, I, I, I, I, P]),
+    "fbn_pairs_fwd": (I, [P, P, P, I, I, I, I, I, P]),
     "fbn_pairs_bwd": (I, [P, P, P, P, P, I, I, I, I, P]),
     "fbn_bn_workspace_size": (SZ, [I, I]),
     "fbn_bn_stats_pass": (I, [P, I, I, P, P, P, P]),
@@ -43,9 +43,10 @@ SIGNATURES = {
     "fbn_bn_finalize": (I, [P, P, D, I, P, P, P, P, F, F, I, P]),
     "fbn_bn_stats": (I, [P, I, I, P, P, P, P, F, F, I, P, P]),
     "fbn_bn_eval_params": (I, [P, P, P, P, I, F, P]),
-    "fbn_bn_act_fwd": (I, [P, P, I, I, P, P, P, P, F, P, U, P, P, P]),
+    "fbn_bn_act_fwd": (I, [P, P, I, I, P, P, P, P, F, P, U, P, P, P, P]),
     "fbn_bn_bwd_reduce": (I, [P, P, P, P, F, P, P, I, I, P, P, P]),
-    "fbn_bn_bwd_apply": (I, [P, P, P, P, F, P, P, P, P, I, I, P, D, P, P, P, P, P, P]),
+    "fbn_bn_bwd_apply": (I, [P, P, P, P, F, P, P, P, P, I, I, P, D, P, P, P, P, P, P, P]),
+    "fbn_convert_bf16": (I, [P, I, P]),
     "fbn_bn_bwd": (I, [P, P, P, P, F, P, P, P, P, I, I, P, P, P, P, P, P]),
     "fbn_colsum_workspace_size": (SZ, [I, I]),
     "fbn_colsum": (I, [P, I, I, I, P, F, P, P]),
@@ -56,12 +57,14 @@ SIGNATURES = {
     "fbn_sumsq": (I, [P, LL, P, I, P, P]),
     "fbn_clip_coef": (I, [P, F, P, P, P]),
     "fbn_adam_dense": (I, [P, P, P, P, LL, P, P, P, F, F, F, P]),
-    "fbn_adam_table": (I, [P, P, P, LL, I, P, P, P, P, P, F, F, F, P]),
-    "fbn_step_end": (I, [P, P, P, P, P]),
-    "fbn_zero_rows": (I, [P, P, I, P]),
+    "fbn_sparse_fixup": (I, [P, P, P, I, I, LL, I, P, P, P, P, I, I, P]),
+    "fbn_sumsq_sparse": (I, [P, P, P, I, I, I, P, P]),
+    "fbn_adam_table": (I, [P, P, P, LL, I, P, P, P, P, I, P, P, P, F, F, F, I, P]),
+    "fbn_adam_touched": (I, [P, P, P, I, P, P, P, P, I, I, P, P, P, F, F, F, P]),
+    "fbn_claim_rows": (I, [P, P, I, I, LL, P, P, P]),
+    "fbn_step_end": (I, [P, P, P, P]),
     "fbn_route": (I, [P, P, I, I, LL, LL, I, P, P, P, P, P, P, P]),
-    "fbn_owner_gather": (I, [P, I, P, P, P, P, P, I, I, P]),
-    "fbn_owner_scatter": (I, [P, I, P, P, P, I, I, P]),
+    "fbn_owner_gather": (I, [P, I, P, P, P, P, I, I, P]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

@@ -9,8 +9,9 @@
 //   [all_to_all_single of rows back]
 //   requester: fields_fwd MODE 1 reads rows at pos[b][t]  (fields.hip)
 // Backward mirrors it: fields_bwd MODE 1 writes one gradient row per entry at pos[b][t],
-// all_to_all back to the owners, owner_scatter adds them into the compact gradient rows
-// (the sparse reduce-scatter).  Ids stay int64 until routed; routed ids are int32 local rows.
+// all_to_all back to the owners: the received rows ARE the owner's sparse gradient (slot =
+// received entry), and fbn_sparse_fixup folds duplicates of a row into the entry that claimed
+// it (the sparse reduce-scatter).  Ids stay int64 until routed; routed ids are int32 local rows.
 #include "common.h"
 
 // entry (b, t): t = 0 item id (always routed, even id 0 -> owner 0, row 0), t >= 1 history slot
@@ -61,24 +62,13 @@ __global__ void route_fill_kernel(const int64_t* __restrict__ item, const int64_
   }
 }
 
-__device__ __forceinline__ void map_insert_x(int* map, int* n_uniq, int* uniq_rows, int r) {
-  if (__hip_atomic_load(map + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != -1) return;
-  int expected = -1;
-  if (__hip_atomic_compare_exchange_strong(map + r, &expected, -2, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT)) {
-    const int u = atomicAdd(n_uniq, 1);
-    uniq_rows[u] = r;
-    __hip_atomic_store(map + r, u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// owner side: out[i] = E_local[ids[i]]; G = D/4 lanes per row.  Rows with global id 0
-// (rank 0, local row 0) are padding: gathered (the item lookup of id 0 reads row 0) but
-// never registered for a gradient.
+// owner side: out[i] = E_local[ids[i]]; G = D/4 lanes per row.  Received entry i claims its
+// row for the sparse gradient (map[r] = i, slot_row[i] = r) unless another entry did first.
+// Rows with global id 0 (rank 0, local row 0) are padding: gathered (the item lookup of id 0
+// reads row 0) but never registered for a gradient.
 template <int D>
 __global__ void __launch_bounds__(256) owner_gather_kernel(const int* __restrict__ ids, int n, const float* __restrict__ E,
-                                                           float* __restrict__ out, int* map, int* n_uniq, int* uniq_rows,
-                                                           int rank) {
+                                                           float* __restrict__ out, int* map, int* slot_row, int rank) {
   constexpr int G = D / 4, RPW = 64 / G;
   const int lane = threadIdx.x & 63, q = lane % G;
   const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -88,27 +78,13 @@ __global__ void __launch_bounds__(256) owner_gather_kernel(const int* __restrict
     if (i >= n) continue;
     const int r = ids[i];
     *reinterpret_cast<f32x4*>(out + i * D + 4 * q) = *reinterpret_cast<const f32x4*>(E + (size_t)r * D + 4 * q);
-    if (map && q == 0 && !(rank == 0 && r == 0)) map_insert_x(map, n_uniq, uniq_rows, r);
-  }
-}
-
-// owner side backward: gU[map[ids[i]]] += grad[i]
-template <int D>
-__global__ void __launch_bounds__(256) owner_scatter_kernel(const int* __restrict__ ids, int n,
-                                                            const float* __restrict__ grad, const int* __restrict__ map,
-                                                            float* __restrict__ gU, int rank) {
-  constexpr int G = D / 4, RPW = 64 / G;
-  const int lane = threadIdx.x & 63, q = lane % G;
-  const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
-  for (long long i0 = gw * RPW; i0 < n; i0 += nw * RPW) {
-    const long long i = i0 + lane / G;
-    if (i >= n) continue;
-    const int r = ids[i];
-    if (rank == 0 && r == 0) continue;
-    const f32x4 g = *reinterpret_cast<const f32x4*>(grad + i * D + 4 * q);
-    float* dst = gU + (size_t)map[r] * D + 4 * q;
-    atomicAdd(dst + 0, g[0]); atomicAdd(dst + 1, g[1]); atomicAdd(dst + 2, g[2]); atomicAdd(dst + 3, g[3]);
+    if (map && q == 0 && !(rank == 0 && r == 0) &&
+        __hip_atomic_load(map + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == -1) {
+      int expected = -1;
+      if (__hip_atomic_compare_exchange_strong(map + r, &expected, (int)i, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT))
+        slot_row[i] = r;
+    }
   }
 }
 
@@ -149,20 +125,11 @@ static dim3 rows_grid(long long n, int D) {
   return dim3((unsigned)blocks);
 }
 
-extern "C" int fbn_owner_gather(const int* ids, int n, const float* E, float* out, int* map, int* n_uniq,
-                                int* uniq_rows, int rank, int D, void* stream) {
+extern "C" int fbn_owner_gather(const int* ids, int n, const float* E, float* out, int* map, int* slot_row, int rank,
+                                int D, void* stream) {
   if (n <= 0) return FBN_OK;
   hipStream_t st = (hipStream_t)stream;
-  FBN_DISPATCH_D(owner_gather_kernel, D, rows_grid(n, D), ids, n, E, out, map, n_uniq, uniq_rows, rank);
-  FBN_CHECK_LAUNCH();
-  return FBN_OK;
-}
-
-extern "C" int fbn_owner_scatter(const int* ids, int n, const float* grad, const int* map, float* gU, int rank, int D,
-                                 void* stream) {
-  if (n <= 0) return FBN_OK;
-  hipStream_t st = (hipStream_t)stream;
-  FBN_DISPATCH_D(owner_scatter_kernel, D, rows_grid(n, D), ids, n, grad, map, gU, rank);
+  FBN_DISPATCH_D(owner_gather_kernel, D, rows_grid(n, D), ids, n, E, out, map, slot_row, rank);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

@@ -34,27 +34,26 @@ struct FieldArgs {
   const float* w1; const float* b1; const float* w2; const float* b2;  // SENET [R][6],[R],[6][R],[6]
   float* X;                 // [B][5][D] fields 1..5 (pre-SENET)
   float* Vc;                // [B][5][D] fields 1..5 (post-SENET)
-  float* c;                 // [B][ldc]; cols [0,5D) <- Vc (MLP input, compact layout)
+  void* c;                  // [B][ldc] float or bf16 (c16); cols [0,5D) <- Vc (MLP input, compact layout)
   float* a_out;             // [B][6]
   float* cnt_out;           // [B]
   int* err;                 // id range violations (sticky flag)
-  int* map;                 // sparse-grad map [V] (-1 = untouched) or null
-  int* n_uniq;              // number of unique rows (device counter)
-  int* uniq_rows;           // [cap] unique row list
+  int* map;                 // sparse-grad map [V]: row -> claiming entry (-1 = untouched) or null
+  int* slot_row;            // [B*(L+1)]: entry -> row it claimed, -1 otherwise (pre-filled with -1)
   long long V;              // rows of the table (mode 0)
-  int B, L, ldc, R, n_cate;
+  int B, L, ldc, R, n_cate, c16;
   float ln_eps;
 };
 
-__device__ __forceinline__ void map_insert(int* map, int* n_uniq, int* uniq_rows, int r) {
+// Sparse-gradient registration: the first entry e = b*(L+1)+t that touches row r claims it
+// (map[r] = e, slot_row[e] = r).  Slots are entry indices, so no shared counter is needed:
+// a global "next free slot" atomic serialises on one address (~12 ns per wave-level atomic).
+__device__ __forceinline__ void map_claim(int* map, int* slot_row, int r, int e) {
   if (__hip_atomic_load(map + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != -1) return;
   int expected = -1;
-  if (__hip_atomic_compare_exchange_strong(map + r, &expected, -2, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT)) {
-    const int u = atomicAdd(n_uniq, 1);
-    uniq_rows[u] = r;
-    __hip_atomic_store(map + r, u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (__hip_atomic_compare_exchange_strong(map + r, &expected, e, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT))
+    slot_row[e] = r;
 }
 
 template <int D>
@@ -97,6 +96,10 @@ __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
     if (vw < 0 || vw >= p.n_cate) { bad = true; vw = 0; }
     // history rows are issued in chunks of HCH slots (all loads of a chunk in flight before
     // any is consumed) and summed in slot order like the reference's sum over dim 1
+    // independent loads first (they overlap the row gather below)
+    const f32x4 c1 = *reinterpret_cast<const f32x4*>(p.cate + lk * D + 4 * q);
+    const f32x4 c2 = *reinterpret_cast<const f32x4*>(p.cate + vw * D + 4 * q);
+    const f32x4 h = *reinterpret_cast<const f32x4*>(p.hmm + (size_t)b * D + 4 * q);
     f32x4 rit = {0.f, 0.f, 0.f, 0.f};
     f32x4 hs = {0.f, 0.f, 0.f, 0.f};
     int nnz = 0;
@@ -128,9 +131,6 @@ __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
 #pragma unroll
       for (int u = 0; u < HCH; ++u) hs += hist[u];
     }
-    const f32x4 c1 = *reinterpret_cast<const f32x4*>(p.cate + lk * D + 4 * q);
-    const f32x4 c2 = *reinterpret_cast<const f32x4*>(p.cate + vw * D + 4 * q);
-    const f32x4 h = *reinterpret_cast<const f32x4*>(p.hmm + (size_t)b * D + 4 * q);
     if (bad && q == 0) atomicOr(p.err, 1);
 
     // ---------------- history masked mean
@@ -161,13 +161,15 @@ __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
     // ---------------- stores
     float* Xb = p.X + (size_t)b * 5 * D + 4 * q;
     float* Vb = p.Vc + (size_t)b * 5 * D + 4 * q;
-    float* cb = p.c + (size_t)b * p.ldc + 4 * q;
+    float* cb = p.c16 ? nullptr : (float*)p.c + (size_t)b * p.ldc + 4 * q;
+    short* cb16 = p.c16 ? (short*)p.c + (size_t)b * p.ldc + 4 * q : nullptr;
 #pragma unroll
     for (int f = 0; f < 5; ++f) {
       const f32x4 v = xs[f] * a[f + 1];
       *reinterpret_cast<f32x4*>(Xb + f * D) = xs[f];
       *reinterpret_cast<f32x4*>(Vb + f * D) = v;
-      *reinterpret_cast<f32x4*>(cb + f * D) = v;
+      if (cb16) *reinterpret_cast<bf16x4*>(cb16 + f * D) = (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+      else *reinterpret_cast<f32x4*>(cb + f * D) = v;
     }
 #pragma unroll
     for (int f = 0; f < 6; ++f)
@@ -178,7 +180,7 @@ __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
     if (MODE == 0 && p.map) {
       for (int t = q; t <= L; t += G) {
         long long r = (t == 0) ? item : p.item_seq[(size_t)b * L + (t - 1)];
-        if (r > 0 && r < p.V) map_insert(p.map, p.n_uniq, p.uniq_rows, (int)r);
+        if (r > 0 && r < p.V) map_claim(p.map, p.slot_row, (int)r, b * (L + 1) + t);
       }
     }
   }
@@ -195,8 +197,9 @@ struct FieldBwdArgs {
   const float* dV;     // [B][5][D] total gradient wrt V_1..V_5
   float* dhmm;         // [B][D] gradient wrt the pre-LN projection
   float* partials;     // [gridDim.x][P]; P = 6R + R + 6R + 6 + 2D + n_cate*D
-  // table gradient, mode 0: dense (gtab[V][D]) if map == null, else sparse gU[u][D] via map
-  float* gtab; const int* map;
+  // table gradient, mode 0: dense gtab[V][D] (atomics) if gvec == null; otherwise the two
+  // per-sample vectors gvec[b][0] = dX3 (item row), gvec[b][1] = dX5/count (each history row)
+  float* gtab; float* gvec;
   // mode 1: rows written to sendbuf at pos[b][t]
   const int* pos; float* sendbuf;
   long long V;
@@ -347,19 +350,21 @@ __global__ void __launch_bounds__(256) fields_bwd_kernel(FieldBwdArgs p) {
     }
     // item table: dX3 -> row item_id, dX5 / count -> each non-padding history row
     const f32x4 gh = dx[4] / p.cnt[b];
-    if (MODE == 0) {
+    if (MODE == 0 && p.gvec) {
+      // sparse mode: plain stores; rows are resolved later through map / slot_row
+      *reinterpret_cast<f32x4*>(p.gvec + (size_t)b * 2 * D + 4 * q) = dx[2];
+      *reinterpret_cast<f32x4*>(p.gvec + ((size_t)b * 2 + 1) * D + 4 * q) = gh;
+    } else if (MODE == 0) {
       const f32x4 ti = transpose_cols<G>(dx[2], lane);
       const f32x4 th = transpose_cols<G>(gh, lane);
       const long long item = p.item_id[b];
       if (item > 0 && item < p.V) {
-        float* dst = p.map ? p.gtab + (size_t)p.map[item] * D : p.gtab + item * D;
-        atomic_add_row_t<G>(dst, ti, q);
+        atomic_add_row_t<G>(p.gtab + item * D, ti, q);
       }
       for (int t = 0; t < L; ++t) {
         const long long s = p.item_seq[(size_t)b * L + t];
         if (s > 0 && s < p.V) {
-          float* dst = p.map ? p.gtab + (size_t)p.map[s] * D : p.gtab + s * D;
-          atomic_add_row_t<G>(dst, th, q);
+          atomic_add_row_t<G>(p.gtab + s * D, th, q);
         }
       }
     } else {
@@ -392,13 +397,21 @@ __global__ void reduce_partials_l1(float* part, int nblk, int P) {
   if (rl == 0 && i < P)
     part[(size_t)(nblk + blockIdx.y) * P + i] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
 }
-__global__ void reduce_partials_l2(const float* part, int nblk, int P, float* out) {
+// destinations of the 7 parameter-gradient segments (w1, b1, w2, b2, ln_g, ln_b, cate)
+struct GradOuts {
+  float* p[7];
+  int off[8];
+};
+__global__ void reduce_partials_l2(const float* part, int nblk, int P, GradOuts o) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
   if (i >= P) return;
   float s = 0.f;
 #pragma unroll
   for (int k = 0; k < RED_CH; ++k) s += part[(size_t)(nblk + k) * P + i];
-  out[i] = s;
+  int seg = 0;
+#pragma unroll
+  for (int j = 1; j < 7; ++j) seg += (i >= o.off[j]) ? 1 : 0;
+  o.p[seg][i - o.off[seg]] = s;
 }
 
 // ------------------------------------------------------------------------------ C ABI
@@ -428,8 +441,8 @@ extern "C" int fbn_fields_fwd(const int64_t* item_id, const int64_t* item_seq, c
                               const int64_t* views, const float* hmm, const float* ln_g, const float* ln_b,
                               float ln_eps, const float* cate, int n_cate, const float* table, long long V,
                               const int* pos, const float* w1, const float* b1, const float* w2,
-                              const float* b2, int R, float* X, float* Vc, float* c, int ldc, float* a_out,
-                              float* cnt_out, int* err, int* map, int* n_uniq, int* uniq_rows, int B, int L,
+                              const float* b2, int R, float* X, float* Vc, void* c, int ldc, int c_bf16, float* a_out,
+                              float* cnt_out, int* err, int* map, int* slot_row, int B, int L,
                               int D, void* stream) {
   if (B <= 0) return FBN_OK;
   if (L < 0 || L > 32 || R < 1 || R > FBN_MAXR || (ldc & 3)) {
@@ -441,8 +454,8 @@ extern "C" int fbn_fields_fwd(const int64_t* item_id, const int64_t* item_seq, c
   a.hmm = hmm; a.ln_g = ln_g; a.ln_b = ln_b; a.cate = cate; a.table = table; a.pos = pos;
   a.w1 = w1; a.b1 = b1; a.w2 = w2; a.b2 = b2;
   a.X = X; a.Vc = Vc; a.c = c; a.a_out = a_out; a.cnt_out = cnt_out; a.err = err;
-  a.map = map; a.n_uniq = n_uniq; a.uniq_rows = uniq_rows;
-  a.V = V; a.B = B; a.L = L; a.ldc = ldc; a.R = R; a.n_cate = n_cate; a.ln_eps = ln_eps;
+  a.map = map; a.slot_row = slot_row;
+  a.V = V; a.B = B; a.L = L; a.ldc = ldc; a.R = R; a.n_cate = n_cate; a.ln_eps = ln_eps; a.c16 = c_bf16;
   if (pos) return launch_fields_fwd<1>(a, D, (hipStream_t)stream);
   return launch_fields_fwd<0>(a, D, (hipStream_t)stream);
 }
@@ -468,13 +481,13 @@ static int launch_fields_bwd(const FieldBwdArgs& a, int D, hipStream_t st) {
 }
 
 // partials: [fbn_fields_bwd_grid(B,D)][fbn_fields_bwd_partials_size(D,R,n_cate)] scratch;
-// partials: [fbn_fields_bwd_grid(B,D)][P] scratch; param_grads: [P] output in the order
-// w1, b1, w2, b2, ln_g, ln_b, cate.
+// partials: [fbn_fields_bwd_grid(B,D)][P] scratch; param_grads: host array of 7 device
+// pointers receiving the gradients of w1, b1, w2, b2, ln_g, ln_b, cate.
 extern "C" int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes,
                               const int64_t* views, const float* hmm, const float* ln_g, float ln_eps,
                               const float* w1, const float* b1, const float* w2, int R, int n_cate,
                               const float* X, const float* a, const float* cnt, const float* dV, float* dhmm,
-                              float* partials, float* param_grads, float* gtab, const int* map, long long V,
+                              float* partials, float* const* param_grads, float* gtab, float* gvec, long long V,
                               const int* pos, float* sendbuf, int B, int L, int D, void* stream) {
   if (B <= 0) return FBN_OK;
   if (L < 0 || L > 32 || R < 1 || R > FBN_MAXR) { fbn_set_error("fbn_fields_bwd: bad L/R"); return FBN_ERR_ARG; }
@@ -482,7 +495,7 @@ extern "C" int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, c
   p.item_id = item_id; p.item_seq = L > 0 ? item_seq : nullptr; p.likes = likes; p.views = views;
   p.hmm = hmm; p.ln_g = ln_g; p.w1 = w1; p.b1 = b1; p.w2 = w2;
   p.X = X; p.a = a; p.cnt = cnt; p.dV = dV; p.dhmm = dhmm; p.partials = partials;
-  p.gtab = gtab; p.map = map; p.pos = pos; p.sendbuf = sendbuf;
+  p.gtab = gtab; p.gvec = gvec; p.pos = pos; p.sendbuf = sendbuf;
   p.V = V; p.B = B; p.L = L; p.R = R; p.n_cate = n_cate; p.ln_eps = ln_eps;
   hipStream_t st = (hipStream_t)stream;
   int rc = pos ? launch_fields_bwd<1>(p, D, st) : launch_fields_bwd<0>(p, D, st);
@@ -490,8 +503,15 @@ extern "C" int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, c
   const int P = 13 * R + 6 + 2 * D + n_cate * D;
   const int nblk = fields_grid(B, D);
   hipLaunchKernelGGL(reduce_partials_l1, dim3(fbn_cdiv(P, 64), RED_CH), dim3(256), 0, st, partials, nblk, P);
-  hipLaunchKernelGGL(reduce_partials_l2, dim3(fbn_cdiv(P, 64)), dim3(64), 0, st, (const float*)partials, nblk, P,
-                     param_grads);
+  GradOuts o;
+  const int sizes[7] = {6 * R, R, 6 * R, 6, D, D, n_cate * D};
+  o.off[0] = 0;
+  for (int j = 0; j < 7; ++j) {
+    if (!param_grads[j]) { fbn_set_error("fbn_fields_bwd: null parameter-gradient destination"); return FBN_ERR_ARG; }
+    o.p[j] = param_grads[j];
+    o.off[j + 1] = o.off[j] + sizes[j];
+  }
+  hipLaunchKernelGGL(reduce_partials_l2, dim3(fbn_cdiv(P, 64)), dim3(64), 0, st, (const float*)partials, nblk, P, o);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

@@ -34,8 +34,8 @@ struct Remap {
 __device__ __forceinline__ int remap(const Remap& r, int i) { return i + (i < r.seg ? r.off0 : r.off1); }
 
 struct GemmArgs {
-  const float* A;
-  const float* B;
+  const void* A;   // float or bf16 (see a16 / b16)
+  const void* B;
   float* C;
   const float* bias;
   int M, N, K, lda, ldb, ldc;
@@ -133,7 +133,102 @@ struct TileLoader {
   }
 };
 
-template <int BM, int BN, bool TA, bool TB, bool BF16>
+// bf16-source variant (bf16 compute only; no remap: the host passes compacted operands).
+// KC: one 16-B load = 8 consecutive k of one row.  !KC: 8x8 micro-block (8 rows x 8 k) from 8
+// loads of 16 B at k..k+7, transposed in registers -> 8 row stores of 8 k (16 B each).
+template <int ROWS, int BK, bool KC>
+struct TileLoaderBf16 {
+  static constexpr int UNITS = KC ? ROWS * BK / 8 : ROWS * BK / 64;
+  static constexpr int PER_T = (UNITS + 255) / 256;
+  static constexpr int NV = KC ? PER_T : PER_T * 8;
+  static_assert(UNITS % 256 == 0 || UNITS < 256, "tile / thread mismatch");
+  bf16x8 v[NV];
+
+  __device__ __forceinline__ bf16x8 ld8(const short* __restrict__ P, int ld, int row, int nrows, int k, int kend) const {
+    bf16x8 x = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (KC) {
+      if (row < nrows) {
+        if (k + 7 < kend) {
+          x = *reinterpret_cast<const bf16x8*>(P + (size_t)row * ld + k);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (k + e < kend) x[e] = P[(size_t)row * ld + k + e];
+        }
+      }
+    } else {
+      if (k < kend) {
+        if (row + 7 < nrows) {
+          x = *reinterpret_cast<const bf16x8*>(P + (size_t)k * ld + row);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (row + e < nrows) x[e] = P[(size_t)k * ld + row + e];
+        }
+      }
+    }
+    return x;
+  }
+
+  __device__ __forceinline__ void load(const short* __restrict__ P, int ld, int row0, int nrows, int k0, int kend) {
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      if (UNITS < 256 && c >= UNITS) continue;
+      if (KC) {
+        const int r = c / (BK / 8), kk = (c % (BK / 8)) * 8;
+        v[i] = ld8(P, ld, row0 + r, nrows, k0 + kk, kend);
+      } else {
+        const int r = (c % (ROWS / 8)) * 8, kk = (c / (ROWS / 8)) * 8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i * 8 + j] = ld8(P, ld, row0 + r, nrows, k0 + kk + j, kend);
+      }
+    }
+  }
+
+  template <int LDK>
+  __device__ __forceinline__ void store(short* __restrict__ S) const {
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      if (UNITS < 256 && c >= UNITS) continue;
+      if (KC) {
+        const int r = c / (BK / 8), kk = (c % (BK / 8)) * 8;
+        *reinterpret_cast<bf16x8*>(S + r * LDK + kk) = v[i];
+      } else {
+        const int r = (c % (ROWS / 8)) * 8, kk = (c / (ROWS / 8)) * 8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          bf16x8 t;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) t[j] = v[i * 8 + j][e];
+          *reinterpret_cast<bf16x8*>(S + (r + e) * LDK + kk) = t;
+        }
+      }
+    }
+  }
+};
+
+// Operand loader selector: SRC16 = the operand is bf16 in memory (bf16 compute only).
+template <int ROWS, int BK, bool KC, bool MAP, bool SRC16> struct OpLoader;
+template <int ROWS, int BK, bool KC, bool MAP> struct OpLoader<ROWS, BK, KC, MAP, false> {
+  TileLoader<ROWS, BK, KC, MAP> t;
+  __device__ __forceinline__ void load(const void* P, int ld, int row0, int nrows, int k0, int kend, const Remap& rm) {
+    t.load(reinterpret_cast<const float*>(P), ld, row0, nrows, k0, kend, rm);
+  }
+  template <typename T, int LDK> __device__ __forceinline__ void store(T* S) const { t.template store<T, LDK>(S); }
+};
+template <int ROWS, int BK, bool KC, bool MAP> struct OpLoader<ROWS, BK, KC, MAP, true> {
+  TileLoaderBf16<ROWS, BK, KC> t;
+  __device__ __forceinline__ void load(const void* P, int ld, int row0, int nrows, int k0, int kend, const Remap&) {
+    t.load(reinterpret_cast<const short*>(P), ld, row0, nrows, k0, kend);
+  }
+  template <typename T, int LDK> __device__ __forceinline__ void store(T* S) const {
+    t.template store<LDK>(reinterpret_cast<short*>(S));
+  }
+};
+
+template <int BM, int BN, bool TA, bool TB, bool BF16, bool A16, bool B16>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int remap_xcd) {
   typedef GemmTraits<BF16> Tr;
   typedef typename Tr::T T;
@@ -154,8 +249,8 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
   const int ntiles = (kend - kbeg + BK - 1) / BK;
   const Remap none = {0x7fffffff, 0, 0};
 
-  TileLoader<BM, BK, !TA, false> la;
-  TileLoader<BN, BK, TB, true> lb;
+  OpLoader<BM, BK, !TA, false, A16> la;
+  OpLoader<BN, BK, TB, true, B16> lb;
 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wm = wave & 1, wn = wave >> 1;
@@ -293,20 +388,30 @@ static GemmPlan plan_gemm(int M, int N, int K, int bk) {
   return p;
 }
 
-template <int BM, int BN, bool TA, bool TB, bool BF16>
+template <int BM, int BN, bool TA, bool TB, bool BF16, bool A16, bool B16>
 static void launch_tile(const GemmArgs& g, int nsplit, hipStream_t st) {
   const int tn = fbn_cdiv(g.N, BN), tm = fbn_cdiv(g.M, BM);
   const int nb = tn * tm;
   dim3 grid(nb, 1, nsplit);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, TA, TB, BF16>), grid, dim3(256), 0, st, g, tn, (nb % 8 == 0) ? 1 : 0);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, TA, TB, BF16, A16, B16>), grid, dim3(256), 0, st, g, tn,
+                     (nb % 8 == 0) ? 1 : 0);
 }
 
-template <bool TA, bool TB, bool BF16>
+template <bool TA, bool TB, bool BF16, bool A16, bool B16>
 static void launch_sel(const GemmArgs& g, const GemmPlan& p, hipStream_t st) {
-  if (p.bm == 128 && p.bn == 128) launch_tile<128, 128, TA, TB, BF16>(g, p.split, st);
-  else if (p.bm == 128) launch_tile<128, 64, TA, TB, BF16>(g, p.split, st);
-  else if (p.bn == 128) launch_tile<64, 128, TA, TB, BF16>(g, p.split, st);
-  else launch_tile<64, 64, TA, TB, BF16>(g, p.split, st);
+  if (p.bm == 128 && p.bn == 128) launch_tile<128, 128, TA, TB, BF16, A16, B16>(g, p.split, st);
+  else if (p.bm == 128) launch_tile<128, 64, TA, TB, BF16, A16, B16>(g, p.split, st);
+  else if (p.bn == 128) launch_tile<64, 128, TA, TB, BF16, A16, B16>(g, p.split, st);
+  else launch_tile<64, 64, TA, TB, BF16, A16, B16>(g, p.split, st);
+}
+
+template <bool TA, bool TB>
+static void launch_types(const GemmArgs& g, const GemmPlan& p, int bf16, int a16, int b16, hipStream_t st) {
+  if (!bf16) launch_sel<TA, TB, false, false, false>(g, p, st);
+  else if (a16 && b16) launch_sel<TA, TB, true, true, true>(g, p, st);
+  else if (a16) launch_sel<TA, TB, true, true, false>(g, p, st);
+  else if (b16) launch_sel<TA, TB, true, false, true>(g, p, st);
+  else launch_sel<TA, TB, true, false, false>(g, p, st);
 }
 
 extern "C" size_t fbn_gemm_workspace_size(int M, int N, int K, int bf16) {
@@ -314,16 +419,21 @@ extern "C" size_t fbn_gemm_workspace_size(int M, int N, int K, int bf16) {
   return p.split > 1 ? (size_t)p.split * M * N * sizeof(float) : 0;
 }
 
-extern "C" int fbn_gemm(const float* A, const float* B, float* C, const float* bias, int M, int N, int K,
-                        int lda, int ldb, int ldc, int transA, int transB, int rB_seg, int rB_off0,
-                        int rB_off1, int rC_seg, int rC_off0, int rC_off1, float beta, int bf16,
-                        float* ws, size_t ws_bytes, void* stream) {
+// a16 / b16: the A / B operand is bf16 in memory (requires bf16 = 1, ld % 8 == 0 and no rB remap)
+extern "C" int fbn_gemm(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, int lda,
+                        int ldb, int ldc, int transA, int transB, int rB_seg, int rB_off0, int rB_off1, int rC_seg,
+                        int rC_off0, int rC_off1, float beta, int bf16, int a16, int b16, float* ws, size_t ws_bytes,
+                        void* stream) {
   if (M <= 0 || N <= 0) return FBN_OK;
   if (!A || !B || !C) { fbn_set_error("fbn_gemm: null operand"); return FBN_ERR_ARG; }
   // 16-B vector loads along the contiguous dimension of every operand
   if ((lda & 3) || (ldb & 3) || ((uintptr_t)A & 15) || ((uintptr_t)B & 15) || (rB_off0 & 3) || (rB_off1 & 3) ||
       (rB_seg != 0x7fffffff && (rB_seg & 3))) {
     fbn_set_error("fbn_gemm: operands must be 16-byte aligned with ld % 4 == 0");
+    return FBN_ERR_ARG;
+  }
+  if ((a16 || b16) && (!bf16 || (a16 && (lda & 7)) || (b16 && (ldb & 7)) || (b16 && rB_seg != 0x7fffffff))) {
+    fbn_set_error("fbn_gemm: bf16 operands need bf16 compute, ld % 8 == 0 and no B remap");
     return FBN_ERR_ARG;
   }
   GemmArgs g;
@@ -341,16 +451,12 @@ extern "C" int fbn_gemm(const float* A, const float* B, float* C, const float* b
   g.kchunk = K > 0 ? per : 0;
   g.ws = ws;
   hipStream_t st = (hipStream_t)stream;
-  const int key = (transA ? 4 : 0) | (transB ? 2 : 0) | (bf16 ? 1 : 0);
+  const int key = (transA ? 2 : 0) | (transB ? 1 : 0);
   switch (key) {
-    case 0: launch_sel<false, false, false>(g, p, st); break;
-    case 1: launch_sel<false, false, true>(g, p, st); break;
-    case 2: launch_sel<false, true, false>(g, p, st); break;
-    case 3: launch_sel<false, true, true>(g, p, st); break;
-    case 4: launch_sel<true, false, false>(g, p, st); break;
-    case 5: launch_sel<true, false, true>(g, p, st); break;
-    case 6: launch_sel<true, true, false>(g, p, st); break;
-    default: launch_sel<true, true, true>(g, p, st); break;
+    case 0: launch_types<false, false>(g, p, bf16, a16, b16, st); break;
+    case 1: launch_types<false, true>(g, p, bf16, a16, b16, st); break;
+    case 2: launch_types<true, false>(g, p, bf16, a16, b16, st); break;
+    default: launch_types<true, true>(g, p, bf16, a16, b16, st); break;
   }
   FBN_CHECK_LAUNCH();
   if (p.split > 1) {

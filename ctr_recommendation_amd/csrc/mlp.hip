@@ -23,7 +23,13 @@ __device__ constexpr int c_pi[10] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3};
 __device__ constexpr int c_pj[10] = {1, 2, 3, 4, 2, 3, 4, 3, 4, 4};
 
 // mode 0 ("all"): p = V_i * U_j ; mode 1 ("each"): p = U_i * V_j   (field indices 0..4 = fields 1..5)
-__global__ void pairs_fwd_kernel(const float* __restrict__ Vc, const float* __restrict__ U, float* __restrict__ c,
+// OutT = float, or short (bf16: the MLP input feeding bf16 GEMMs directly)
+__device__ __forceinline__ void store4(float* p, const f32x4& v) { *reinterpret_cast<f32x4*>(p) = v; }
+__device__ __forceinline__ void store4(short* p, const f32x4& v) {
+  *reinterpret_cast<bf16x4*>(p) = (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+}
+template <typename OutT>
+__global__ void pairs_fwd_kernel(const float* __restrict__ Vc, const float* __restrict__ U, OutT* __restrict__ c,
                                  int B, int D, int ldc, int mode) {
   const int q4 = D / 4;
   const size_t total = (size_t)B * q4;
@@ -35,11 +41,11 @@ __global__ void pairs_fwd_kernel(const float* __restrict__ Vc, const float* __re
       v[f] = *reinterpret_cast<const f32x4*>(Vc + ((size_t)b * 5 + f) * D + col);
       u[f] = *reinterpret_cast<const f32x4*>(U + ((size_t)b * 5 + f) * D + col);
     }
-    float* out = c + (size_t)b * ldc + 5 * D + col;
+    OutT* out = c + (size_t)b * ldc + 5 * D + col;
 #pragma unroll
     for (int k = 0; k < 10; ++k) {
       const f32x4 pr = mode == 0 ? v[c_pi[k]] * u[c_pj[k]] : u[c_pi[k]] * v[c_pj[k]];
-      *reinterpret_cast<f32x4*>(out + k * D) = pr;
+      store4(out + k * D, pr);
     }
   }
 }
@@ -147,7 +153,8 @@ __global__ void bn_act_fwd_kernel(const float* __restrict__ X, float* __restrict
                                   const float* __restrict__ mean, const float* __restrict__ invstd,
                                   const float* __restrict__ g, const float* __restrict__ bta, float p_drop,
                                   const unsigned long long* __restrict__ rng, unsigned stream_id,
-                                  unsigned char* __restrict__ mask_out, const unsigned char* __restrict__ mask_in) {
+                                  unsigned char* __restrict__ mask_out, const unsigned char* __restrict__ mask_in,
+                                  short* __restrict__ Y16) {
   const size_t total4 = (size_t)B * C / 4;
   const float keep = 1.f - p_drop;
   const float scale = p_drop > 0.f ? 1.0f / keep : 1.f;
@@ -176,6 +183,7 @@ __global__ void bn_act_fwd_kernel(const float* __restrict__ X, float* __restrict
       y[e] = v;
     }
     *reinterpret_cast<f32x4*>(Y + i) = y;
+    if (Y16) store4(Y16 + i, y);
   }
 }
 
@@ -242,12 +250,15 @@ __global__ void bn_bwd_finalize_kernel(const double* red, int C, double ntot, co
 
 __global__ void bn_bwd_apply_kernel(BnBwdSrc s, const float* __restrict__ Xpre, const float* __restrict__ mean,
                                     const float* __restrict__ invstd, const float* __restrict__ g,
-                                    const float* __restrict__ coef, float* __restrict__ dX, int B, int C) {
+                                    const float* __restrict__ coef, float* __restrict__ dX, short* __restrict__ dX16,
+                                    int B, int C) {
   const size_t total = (size_t)B * C;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
     const int b = (int)(i / C), c = (int)(i % C);
     const float dy = bn_dy(s, b, c, C);
-    dX[i] = (dy - coef[c] - (Xpre[i] - mean[c]) * coef[C + c]) * invstd[c] * g[c];
+    const float v = (dy - coef[c] - (Xpre[i] - mean[c]) * coef[C + c]) * invstd[c] * g[c];
+    dX[i] = v;
+    if (dX16) dX16[i] = f2bf(v);
   }
 }
 
@@ -346,11 +357,17 @@ static int row_chunks(int B) {
   return ch < 1 ? 1 : (ch > 256 ? 256 : ch);
 }
 
-extern "C" int fbn_pairs_fwd(const float* Vc, const float* U, float* c, int B, int D, int ldc, int mode, void* stream) {
+// c_bf16: c is a bf16 [B][ldc] buffer (bf16 GEMM mode) instead of float
+extern "C" int fbn_pairs_fwd(const float* Vc, const float* U, void* c, int B, int D, int ldc, int mode, int c_bf16,
+                             void* stream) {
   if (B <= 0) return FBN_OK;
   if ((D & 3) || (ldc & 3)) { fbn_set_error("pairs: D and ldc must be multiples of 4"); return FBN_ERR_ARG; }
-  hipLaunchKernelGGL(pairs_fwd_kernel, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream, Vc, U, c,
-                     B, D, ldc, mode);
+  if (c_bf16)
+    hipLaunchKernelGGL(pairs_fwd_kernel<short>, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream,
+                       Vc, U, (short*)c, B, D, ldc, mode);
+  else
+    hipLaunchKernelGGL(pairs_fwd_kernel<float>, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream,
+                       Vc, U, (float*)c, B, D, ldc, mode);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -424,12 +441,12 @@ extern "C" int fbn_bn_eval_params(const float* run_mean, const float* run_var, f
 extern "C" int fbn_bn_act_fwd(const float* X, float* Y, int B, int C, const float* mean, const float* invstd,
                               const float* g, const float* b, float p_drop, const unsigned long long* rng,
                               unsigned stream_id, unsigned char* mask_out, const unsigned char* mask_in,
-                              void* stream) {
+                              short* Y16, void* stream) {
   if (B <= 0) return FBN_OK;
   if (C & 3) { fbn_set_error("bn_act: C % 4"); return FBN_ERR_ARG; }
   if (p_drop > 0.f && !rng && !mask_in) { fbn_set_error("bn_act: dropout needs an rng state or a mask"); return FBN_ERR_ARG; }
   hipLaunchKernelGGL(bn_act_fwd_kernel, dim3(ew_grid((size_t)B * C / 4)), dim3(256), 0, (hipStream_t)stream, X, Y, B,
-                     C, mean, invstd, g, b, p_drop, rng, stream_id, mask_out, mask_in);
+                     C, mean, invstd, g, b, p_drop, rng, stream_id, mask_out, mask_in, Y16);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -452,8 +469,8 @@ extern "C" int fbn_bn_bwd_reduce(const float* G, const float* gvec, const float*
 // stage 2 (after an optional all-reduce of red_d): dXpre, dgamma, dbeta, dw (rank-1 only)
 extern "C" int fbn_bn_bwd_apply(const float* G, const float* gvec, const float* w, const float* hact, float scale,
                                 const float* Xpre, const float* mean, const float* invstd, const float* gamma, int B,
-                                int C, const double* red_d, double ntot, float* dXpre, float* dgamma, float* dbeta,
-                                float* dw, void* ws, void* stream) {
+                                int C, const double* red_d, double ntot, float* dXpre, short* dXpre16, float* dgamma,
+                                float* dbeta, float* dw, void* ws, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   BnBwdSrc s{G, gvec, w, hact, scale};
   float* coef = (float*)((double*)ws + (size_t)row_chunks(B) * 3 * C + 3 * (size_t)C);
@@ -461,7 +478,7 @@ extern "C" int fbn_bn_bwd_apply(const float* G, const float* gvec, const float* 
                      dgamma, dbeta, G ? nullptr : dw);
   if (B > 0)
     hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid((size_t)B * C)), dim3(256), 0, st, s, Xpre, mean, invstd,
-                       gamma, coef, dXpre, B, C);
+                       gamma, coef, dXpre, dXpre16, B, C);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -473,7 +490,7 @@ extern "C" int fbn_bn_bwd(const float* G, const float* gvec, const float* w, con
   double* red = (double*)ws + (size_t)row_chunks(B) * 3 * C;   // 3*C doubles
   int rc = fbn_bn_bwd_reduce(G, gvec, w, hact, scale, Xpre, mean, B, C, red, ws, stream);
   if (!rc) rc = fbn_bn_bwd_apply(G, gvec, w, hact, scale, Xpre, mean, invstd, gamma, B, C, red, (double)B, dXpre,
-                                 dgamma, dbeta, dw, ws, stream);
+                                 nullptr, dgamma, dbeta, dw, ws, stream);
   return rc;
 }
 
@@ -517,6 +534,41 @@ extern "C" int fbn_outer(const float* g, const float* w, float* out, int B, int 
 
 extern "C" int fbn_sum(const float* x, int n, float* out, float scale, void* stream) {
   hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, x, n, out, scale);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+// ------------------------------------------------------------------ bf16 weight copies
+// out[i][j] = bf16( T ? src[j*ld + rm(i)] : src[i*ld + rm(j)] ),  i < rows, j < cols,
+// rm(x) = x + (x < seg ? off0 : off1).  Up to 8 jobs per launch (one per blockIdx.y): the
+// compacted / transposed bf16 weight images the bf16 GEMMs read (made once per step).
+struct ConvJob {
+  const float* src;
+  short* dst;
+  int rows, cols, ld, trans, seg, off0, off1;
+};
+struct ConvJobs {
+  ConvJob j[8];
+};
+__global__ void convert_bf16_kernel(ConvJobs jobs) {
+  const ConvJob J = jobs.j[blockIdx.y];
+  const long long n = (long long)J.rows * J.cols;
+  for (long long x = (long long)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += (long long)gridDim.x * blockDim.x) {
+    const int i = (int)(x / J.cols), j = (int)(x % J.cols);
+    const int a = J.trans ? j : i;
+    int b = J.trans ? i : j;
+    b += b < J.seg ? J.off0 : J.off1;
+    J.dst[x] = f2bf(J.src[(size_t)a * J.ld + b]);
+  }
+}
+
+// jobs: host array of n (<= 8) ConvJob records {src, dst, rows, cols, ld, trans, seg, off0, off1}
+extern "C" int fbn_convert_bf16(const void* jobs, int n, void* stream) {
+  if (n <= 0) return FBN_OK;
+  if (n > 8) { fbn_set_error("convert_bf16: at most 8 jobs"); return FBN_ERR_ARG; }
+  ConvJobs J;
+  for (int i = 0; i < 8; ++i) J.j[i] = ((const ConvJob*)jobs)[i < n ? i : 0];
+  hipLaunchKernelGGL(convert_bf16_kernel, dim3(256, n), dim3(256), 0, (hipStream_t)stream, J);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

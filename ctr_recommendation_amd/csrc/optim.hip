@@ -18,6 +18,10 @@
 
 #pragma clang fp contract(off)
 
+// squared-norm accumulators: FBN_SUMSQ_SLOTS doubles, block b adds into slot b % SLOTS (one
+// address per block would serialise the returning-free f64 atomics of thousands of blocks)
+#define FBN_SUMSQ_SLOTS 64
+
 struct AdamConsts {
   float w1;     // 1 - beta1 (as float)
   float nss;    // -lr / bias_correction1 (as float)
@@ -45,12 +49,14 @@ __global__ void sumsq_kernel(const float* __restrict__ x, long long n, const int
     if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
     __syncthreads();
   }
-  if (threadIdx.x == 0) atomicAdd(out, red[0]);
+  if (threadIdx.x == 0) atomicAdd(out + (blockIdx.x & (FBN_SUMSQ_SLOTS - 1)), red[0]);
 }
 
 // coef = min(1, max_norm / (sqrt(total) + 1e-6)); also exposes the norm
 __global__ void clip_coef_kernel(const double* sumsq, float max_norm, float* coef_out, float* norm_out) {
-  const float total = sqrtf((float)sumsq[0]);
+  double s = 0.0;
+  for (int i = 0; i < FBN_SUMSQ_SLOTS; ++i) s += sumsq[i];
+  const float total = sqrtf((float)s);
   float c = max_norm / (total + 1e-6f);
   coef_out[0] = c < 1.f ? c : 1.f;
   if (norm_out) norm_out[0] = total;
@@ -97,11 +103,119 @@ __global__ void adam_dense_kernel(float* __restrict__ p, const float* __restrict
   }
 }
 
-// One group of D/4 lanes per row; rows_per_wave = 256/D.  map[r] = slot of r in gU or -1.
+// ------------------------------------------------------------------ sparse table gradient
+// Slots are entry indices.  Single GPU: entry e = b*(L+1)+t (t = 0 item, t >= 1 history), its
+// gradient vector is gvec[b][t ? 1 : 0] (the backward stores 2 vectors per sample); a row hit
+// by several entries keeps them in `extra` (slot of the claiming entry; FLAG in slot_row).
+// Multi-GPU owner: entry = received row i, its gradient is rows[i] (Lp1 = 1), duplicates are
+// added into the claimer's own row.
+#define FBN_SLOT_FLAG 0x40000000
+struct GradSrc {
+  const float* vec;     // Lp1 > 1: [B][2][D] per-sample vectors;  Lp1 == 1: [n][D] per-entry rows
+  float* extra;         // [n][D] duplicate accumulation (single GPU) or null
+  int* slot_row;        // [n] claimed row | FLAG, or -1
+  int Lp1;
+};
 template <int D>
-__global__ void __launch_bounds__(256) adam_table_kernel(float* __restrict__ p, float* __restrict__ m,
+__device__ __forceinline__ const float* grad_base(const GradSrc& s, int e) {
+  if (s.Lp1 == 1) return s.vec + (size_t)e * D;
+  const int b = e / s.Lp1, t = e - b * s.Lp1;
+  return s.vec + ((size_t)b * 2 + (t ? 1 : 0)) * D;
+}
+
+// duplicates of a claimed row: single GPU -> extra[claimer] += vec(e) (and flag the claimer);
+// owner mode -> rows[claimer] += rows[e].  One G-lane group per entry, contiguous atomics.
+template <int D>
+__global__ void __launch_bounds__(256) sparse_fixup_kernel(const int64_t* __restrict__ item,
+                                                           const int64_t* __restrict__ seq, const int* __restrict__ ids,
+                                                           int n, int L, long long V, int rank,
+                                                           const int* __restrict__ map, GradSrc s) {
+  constexpr int G = D / 4, RPW = 64 / G;
+  const int lane = threadIdx.x & 63, q = lane % G;
+  const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+  for (long long e0 = gw * RPW; e0 < n; e0 += nw * RPW) {
+    const long long e = e0 + lane / G;
+    if (e >= n) continue;
+    long long r;
+    if (ids) {
+      r = ids[e];
+      if (rank == 0 && r == 0) continue;
+    } else {
+      const long long b = e / (L + 1), t = e - b * (L + 1);
+      r = t == 0 ? item[b] : seq[b * L + (t - 1)];
+      if (r <= 0 || r >= V) continue;
+    }
+    const int u = map[r];
+    if (u == (int)e || u < 0) continue;
+    const float* src = grad_base<D>(s, (int)e);
+    float* dst;
+    if (s.extra) {
+      if (q == 0) atomicOr(&s.slot_row[u], FBN_SLOT_FLAG);
+      dst = s.extra + (size_t)u * D;
+    } else {
+      dst = const_cast<float*>(s.vec) + (size_t)u * D;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) atomicAdd(dst + k * G + q, src[k * G + q]);
+  }
+}
+
+// Row claiming for the sparse gradient (single GPU): entry e = b*(L+1)+t claims row r if it is
+// the first to touch it.  Run as the first kernel of a step so the untouched-row Adam can start
+// on the side stream before the forward's GEMMs.
+__global__ void claim_rows_kernel(const int64_t* __restrict__ item, const int64_t* __restrict__ seq, int B, int L,
+                                  long long V, int* __restrict__ map, int* __restrict__ slot_row) {
+  const long long n = (long long)B * (L + 1);
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const long long b = e / (L + 1), t = e - b * (L + 1);
+    const long long r = t == 0 ? item[b] : seq[b * L + (t - 1)];
+    if (r <= 0 || r >= V) continue;
+    if (__hip_atomic_load(map + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != -1) continue;
+    int expected = -1;
+    if (__hip_atomic_compare_exchange_strong(map + r, &expected, (int)e, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT))
+      slot_row[e] = (int)r;
+  }
+}
+
+// sum of squares of the clipped-to-be table gradient, over claiming entries only
+template <int D>
+__global__ void __launch_bounds__(256) sumsq_sparse_kernel(GradSrc s, int n, double* __restrict__ out) {
+  constexpr int G = D / 4, RPW = 64 / G;
+  __shared__ double red[256];
+  const int lane = threadIdx.x & 63, q = lane % G;
+  const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+  double acc = 0.0;
+  for (long long e0 = gw * RPW; e0 < n; e0 += nw * RPW) {
+    const long long e = e0 + lane / G;
+    if (e >= n) continue;
+    const int sr = s.slot_row[e];
+    if (sr == -1) continue;
+    f32x4 v = *reinterpret_cast<const f32x4*>(grad_base<D>(s, (int)e) + 4 * q);
+    if (sr & FBN_SLOT_FLAG) v += *reinterpret_cast<const f32x4*>(s.extra + (size_t)e * D + 4 * q);
+    acc += (double)(v[0] * v[0]) + (double)(v[1] * v[1]) + (double)(v[2] * v[2]) + (double)(v[3] * v[3]);
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) atomicAdd(out + (blockIdx.x & (FBN_SUMSQ_SLOTS - 1)), red[0]);
+}
+
+// One group of D/4 lanes per row; rows_per_wave = 256/D.  map[r] = claiming entry or -1.
+// UNTOUCHED_ONLY: update only rows the batch did not touch (map[r] == -1).  Their gradient is
+// exactly 0, so the update (g = 0*coef + wd*p) does not depend on the backward or the clip
+// coefficient and runs on a side stream concurrently with the whole backward; the touched
+// rows are updated afterwards by adam_touched_kernel.  Otherwise: every row, reading the
+// gradient of touched rows through the map.
+template <int D, bool UNTOUCHED_ONLY>
+__device__ __forceinline__ void adam_table_body(float* __restrict__ p, float* __restrict__ m,
                                                          float* __restrict__ v, long long nrows, int* __restrict__ map,
-                                                         const float* __restrict__ gU, const float* __restrict__ coef_ptr,
+                                                         GradSrc gs, const float* __restrict__ coef_ptr,
                                                          const AdamConsts* __restrict__ table,
                                                          const int* __restrict__ step_ptr, float wd, float b2, float omb2,
                                                          float eps) {
@@ -116,38 +230,134 @@ __global__ void __launch_bounds__(256) adam_table_kernel(float* __restrict__ p, 
     const long long r = r0 + lane / G;
     if (r >= nrows) continue;
     const int u = map[r];
+    if (UNTOUCHED_ONLY && u >= 0) continue;
     const size_t off = (size_t)r * D + 4 * q;
-    f32x4 pp = *reinterpret_cast<f32x4*>(p + off);
-    f32x4 mm = *reinterpret_cast<f32x4*>(m + off);
-    f32x4 vv = *reinterpret_cast<f32x4*>(v + off);
+    f32x4 pp = __builtin_nontemporal_load(reinterpret_cast<f32x4*>(p + off));
+    f32x4 mm = __builtin_nontemporal_load(reinterpret_cast<f32x4*>(m + off));
+    f32x4 vv = __builtin_nontemporal_load(reinterpret_cast<f32x4*>(v + off));
     f32x4 gg = {0.f, 0.f, 0.f, 0.f};
-    if (u >= 0) gg = *reinterpret_cast<const f32x4*>(gU + (size_t)u * D + 4 * q);
+    if (!UNTOUCHED_ONLY && u >= 0) {
+      gg = *reinterpret_cast<const f32x4*>(grad_base<D>(gs, u) + 4 * q);
+      if (gs.extra && (gs.slot_row[u] & FBN_SLOT_FLAG)) {
+        float* ex = gs.extra + (size_t)u * D + 4 * q;
+        gg += *reinterpret_cast<const f32x4*>(ex);
+        *reinterpret_cast<f32x4*>(ex) = (f32x4){0.f, 0.f, 0.f, 0.f};   // keep `extra` all-zero
+      }
+    }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float pe = pp[e], me = mm[e], ve = vv[e];
       adam_elem(pe, me, ve, gg[e], coef, wd, b2, omb2, eps, k);
       pp[e] = pe; mm[e] = me; vv[e] = ve;
     }
-    *reinterpret_cast<f32x4*>(p + off) = pp;
-    *reinterpret_cast<f32x4*>(m + off) = mm;
-    *reinterpret_cast<f32x4*>(v + off) = vv;
-    if (u >= 0 && q == 0) map[r] = -1;
+    __builtin_nontemporal_store(pp, reinterpret_cast<f32x4*>(p + off));
+    __builtin_nontemporal_store(mm, reinterpret_cast<f32x4*>(m + off));
+    __builtin_nontemporal_store(vv, reinterpret_cast<f32x4*>(v + off));
+    if (!UNTOUCHED_ONLY && u >= 0 && q == 0) map[r] = -1;
   }
 }
 
-// end of step: advance Adam step + dropout RNG offset, clear sparse-grad bookkeeping
-__global__ void step_end_kernel(int* step, unsigned long long* rng, int* n_uniq, double* sumsq) {
-  step[0] += 1;
-  if (rng) rng[1] += 1;
-  if (n_uniq) n_uniq[0] = 0;
-  if (sumsq) sumsq[0] = 0.0;
+#define FBN_ADAM_TABLE_ARGS                                                                                  \
+  float *p, float *m, float *v, long long nrows, int *map, GradSrc gs, const float *coef, const AdamConsts *t,   \
+      const int *step, float wd, float b2, float omb2, float eps
+template <int D>
+__global__ void __launch_bounds__(256) adam_table_all(FBN_ADAM_TABLE_ARGS) {
+  adam_table_body<D, false>(p, m, v, nrows, map, gs, coef, t, step, wd, b2, omb2, eps);
 }
 
-// gU rows [0, n_uniq) zero-fill (the next step's scatter target)
-__global__ void zero_rows_kernel(float* gU, const int* n_uniq, int D) {
-  const long long lim = (long long)(*n_uniq) * D;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += (long long)gridDim.x * blockDim.x)
-    gU[i] = 0.f;
+// Untouched rows, as a low-footprint streaming kernel: it runs beside the backward on a side
+// stream, so it must not take the CUs' wave slots from the backward's kernels.  Launched with
+// <= 2 workgroups per CU; each lane keeps UNR rows (3 x 16 B each) in flight so the few waves
+// still stream HBM near its rate (Little: ~12 MB in flight chip-wide).
+template <int D>
+__global__ void __launch_bounds__(256) adam_table_untouched(FBN_ADAM_TABLE_ARGS) {
+  constexpr int G = D / 4, RPW = 64 / G, UNR = 4;
+  const AdamConsts k = t[*step];
+  const int lane = threadIdx.x & 63, q = lane % G;
+  const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+  for (long long r0 = gw * RPW * UNR; r0 < nrows; r0 += nw * RPW * UNR) {
+    f32x4 pp[UNR], mm[UNR], vv[UNR];
+    bool act[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const long long r = r0 + u * RPW + lane / G;
+      act[u] = r < nrows && map[r] < 0;
+      if (act[u]) {
+        const size_t off = (size_t)r * D + 4 * q;
+        pp[u] = __builtin_nontemporal_load(reinterpret_cast<f32x4*>(p + off));
+        mm[u] = __builtin_nontemporal_load(reinterpret_cast<f32x4*>(m + off));
+        vv[u] = __builtin_nontemporal_load(reinterpret_cast<f32x4*>(v + off));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      if (!act[u]) continue;
+      const long long r = r0 + u * RPW + lane / G;
+      const size_t off = (size_t)r * D + 4 * q;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float pe = pp[u][e], me = mm[u][e], ve = vv[u][e];
+        adam_elem(pe, me, ve, 0.f, 1.f, wd, b2, omb2, eps, k);
+        pp[u][e] = pe; mm[u][e] = me; vv[u][e] = ve;
+      }
+      __builtin_nontemporal_store(pp[u], reinterpret_cast<f32x4*>(p + off));
+      __builtin_nontemporal_store(mm[u], reinterpret_cast<f32x4*>(m + off));
+      __builtin_nontemporal_store(vv[u], reinterpret_cast<f32x4*>(v + off));
+    }
+  }
+}
+
+// Touched rows: one group per claiming entry e (slot_row[e] = row | FLAG); gradient =
+// gvec-slot(e) (+ extra[e]); Adam with the clip coefficient; the row's map entry is reset.
+template <int D>
+__global__ void __launch_bounds__(256) adam_touched_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                           float* __restrict__ v, int* __restrict__ map, GradSrc gs,
+                                                           int n, const float* __restrict__ coef_ptr,
+                                                           const AdamConsts* __restrict__ table,
+                                                           const int* __restrict__ step_ptr, float wd, float b2,
+                                                           float omb2, float eps) {
+  constexpr int G = D / 4, RPW = 64 / G;
+  const AdamConsts k = table[*step_ptr];
+  const float coef = coef_ptr ? *coef_ptr : 1.f;
+  const int lane = threadIdx.x & 63, q = lane % G;
+  const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+  for (long long e0 = gw * RPW; e0 < n; e0 += nw * RPW) {
+    const long long e = e0 + lane / G;
+    if (e >= n) continue;
+    const int sr = gs.slot_row[e];
+    if (sr == -1) continue;
+    const long long r = sr & ~FBN_SLOT_FLAG;
+    f32x4 gg = *reinterpret_cast<const f32x4*>(grad_base<D>(gs, (int)e) + 4 * q);
+    if (sr & FBN_SLOT_FLAG) {
+      float* ex = gs.extra + (size_t)e * D + 4 * q;
+      gg += *reinterpret_cast<const f32x4*>(ex);
+      *reinterpret_cast<f32x4*>(ex) = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    const size_t off = (size_t)r * D + 4 * q;
+    f32x4 pp = *reinterpret_cast<f32x4*>(p + off);
+    f32x4 mm = *reinterpret_cast<f32x4*>(m + off);
+    f32x4 vv = *reinterpret_cast<f32x4*>(v + off);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float pe = pp[c], me = mm[c], ve = vv[c];
+      adam_elem(pe, me, ve, gg[c], coef, wd, b2, omb2, eps, k);
+      pp[c] = pe; mm[c] = me; vv[c] = ve;
+    }
+    *reinterpret_cast<f32x4*>(p + off) = pp;
+    *reinterpret_cast<f32x4*>(m + off) = mm;
+    *reinterpret_cast<f32x4*>(v + off) = vv;
+    if (q == 0) map[r] = -1;
+  }
+}
+
+// end of step: advance Adam step + dropout RNG offset, clear the norm accumulator
+__global__ void step_end_kernel(int* step, unsigned long long* rng, double* sumsq) {
+  step[0] += 1;
+  if (rng) rng[1] += 1;
+  if (sumsq)
+    for (int i = 0; i < FBN_SUMSQ_SLOTS; ++i) sumsq[i] = 0.0;
 }
 
 // ------------------------------------------------------------------ C ABI
@@ -181,37 +391,96 @@ extern "C" int fbn_adam_dense(float* p, const float* g, float* m, float* v, long
   return FBN_OK;
 }
 
-extern "C" int fbn_adam_table(float* p, float* m, float* v, long long nrows, int D, int* map, const float* gU,
-                              const float* coef, const void* consts_table, const int* step, float wd, float beta2,
-                              float eps, void* stream) {
-  if (nrows <= 0) return FBN_OK;
+#define FBN_DISPATCH_D(KERNEL, D, GRID, ...)                                                         \
+  switch (D) {                                                                                      \
+    case 16: hipLaunchKernelGGL((KERNEL<16>), GRID, dim3(256), 0, st, __VA_ARGS__); break;          \
+    case 32: hipLaunchKernelGGL((KERNEL<32>), GRID, dim3(256), 0, st, __VA_ARGS__); break;          \
+    case 64: hipLaunchKernelGGL((KERNEL<64>), GRID, dim3(256), 0, st, __VA_ARGS__); break;          \
+    case 128: hipLaunchKernelGGL((KERNEL<128>), GRID, dim3(256), 0, st, __VA_ARGS__); break;        \
+    case 256: hipLaunchKernelGGL((KERNEL<256>), GRID, dim3(256), 0, st, __VA_ARGS__); break;        \
+    default: fbn_set_error("D must be 16/32/64/128/256"); return FBN_ERR_UNSUPPORTED;              \
+  }
+
+static dim3 group_grid(long long n, int D, long long cap) {
   const int rpw = 256 / D;
-  long long waves = (nrows + rpw - 1) / rpw;
-  long long blocks = (waves + 3) / 4;
-  if (blocks > 16384) blocks = 16384;
+  long long blocks = ((n + rpw - 1) / rpw + 3) / 4;
+  if (blocks < 1) blocks = 1;
+  if (blocks > cap) blocks = cap;
+  return dim3((unsigned)blocks);
+}
+
+// gvec: single GPU per-sample vectors [B][2][D] (Lp1 = L+1) or owner per-entry rows [n][D] (Lp1 = 1)
+extern "C" int fbn_sparse_fixup(const int64_t* item, const int64_t* seq, const int* ids, int n, int L, long long V,
+                                int rank, const int* map, const float* gvec, float* extra, int* slot_row, int Lp1,
+                                int D, void* stream) {
+  if (n <= 0) return FBN_OK;
+  hipStream_t st = (hipStream_t)stream;
+  GradSrc s{gvec, extra, slot_row, Lp1};
+  FBN_DISPATCH_D(sparse_fixup_kernel, D, group_grid(n, D, 8192), item, L > 0 ? seq : nullptr, ids, n, L, V, rank,
+                 map, s);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+extern "C" int fbn_sumsq_sparse(const float* gvec, float* extra, int* slot_row, int Lp1, int n, int D, double* out,
+                                void* stream) {
+  if (n <= 0) return FBN_OK;
+  hipStream_t st = (hipStream_t)stream;
+  GradSrc s{gvec, extra, slot_row, Lp1};
+  FBN_DISPATCH_D(sumsq_sparse_kernel, D, group_grid(n, D, 4096), s, n, out);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+// mode 0: every row (touched rows read their gradient through the map and are reset);
+// mode 1: untouched rows only (g = 0, coefficient-independent; run it concurrently with the
+// backward, then fbn_adam_touched once the clip coefficient is known)
+extern "C" int fbn_adam_table(float* p, float* m, float* v, long long nrows, int D, int* map, const float* gvec,
+                              float* extra, int* slot_row, int Lp1, const float* coef, const void* consts_table,
+                              const int* step, float wd, float beta2, float eps, int mode, void* stream) {
+  if (nrows <= 0) return FBN_OK;
   hipStream_t st = (hipStream_t)stream;
   const float omb2 = (float)(1.0 - (double)beta2);
   const AdamConsts* t = (const AdamConsts*)consts_table;
-  switch (D) {
-    case 16: hipLaunchKernelGGL((adam_table_kernel<16>), dim3((int)blocks), dim3(256), 0, st, p, m, v, nrows, map, gU, coef, t, step, wd, beta2, omb2, eps); break;
-    case 32: hipLaunchKernelGGL((adam_table_kernel<32>), dim3((int)blocks), dim3(256), 0, st, p, m, v, nrows, map, gU, coef, t, step, wd, beta2, omb2, eps); break;
-    case 64: hipLaunchKernelGGL((adam_table_kernel<64>), dim3((int)blocks), dim3(256), 0, st, p, m, v, nrows, map, gU, coef, t, step, wd, beta2, omb2, eps); break;
-    case 128: hipLaunchKernelGGL((adam_table_kernel<128>), dim3((int)blocks), dim3(256), 0, st, p, m, v, nrows, map, gU, coef, t, step, wd, beta2, omb2, eps); break;
-    case 256: hipLaunchKernelGGL((adam_table_kernel<256>), dim3((int)blocks), dim3(256), 0, st, p, m, v, nrows, map, gU, coef, t, step, wd, beta2, omb2, eps); break;
-    default: fbn_set_error("adam_table: D must be 16/32/64/128/256"); return FBN_ERR_UNSUPPORTED;
+  GradSrc s{gvec, extra, slot_row, Lp1};
+  const dim3 grid = mode == 1 ? dim3(512) : group_grid(nrows, D, 16384);
+  if (mode == 1) {
+    FBN_DISPATCH_D(adam_table_untouched, D, grid, p, m, v, nrows, map, s, coef, t, step, wd, beta2, omb2, eps);
+  } else {
+    FBN_DISPATCH_D(adam_table_all, D, grid, p, m, v, nrows, map, s, coef, t, step, wd, beta2, omb2, eps);
   }
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
 
-extern "C" int fbn_step_end(int* step, unsigned long long* rng, int* n_uniq, double* sumsq, void* stream) {
-  hipLaunchKernelGGL(step_end_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step, rng, n_uniq, sumsq);
+extern "C" int fbn_adam_touched(float* p, float* m, float* v, int D, int* map, const float* gvec, float* extra,
+                                int* slot_row, int Lp1, int n, const float* coef, const void* consts_table,
+                                const int* step, float wd, float beta2, float eps, void* stream) {
+  if (n <= 0) return FBN_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const float omb2 = (float)(1.0 - (double)beta2);
+  const AdamConsts* t = (const AdamConsts*)consts_table;
+  GradSrc s{gvec, extra, slot_row, Lp1};
+  FBN_DISPATCH_D(adam_touched_kernel, D, group_grid(n, D, 8192), p, m, v, map, s, n, coef, t, step, wd, beta2,
+                 omb2, eps);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
 
-extern "C" int fbn_zero_rows(float* gU, const int* n_uniq, int D, void* stream) {
-  hipLaunchKernelGGL(zero_rows_kernel, dim3(1024), dim3(256), 0, (hipStream_t)stream, gU, n_uniq, D);
+extern "C" int fbn_claim_rows(const int64_t* item, const int64_t* seq, int B, int L, long long V, int* map,
+                              int* slot_row, void* stream) {
+  const long long n = (long long)B * (L + 1);
+  if (n <= 0) return FBN_OK;
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(claim_rows_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, item, L > 0 ? seq : nullptr,
+                     B, L, V, map, slot_row);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+extern "C" int fbn_step_end(int* step, unsigned long long* rng, double* sumsq, void* stream) {
+  hipLaunchKernelGGL(step_end_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step, rng, sumsq);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

@@ -10,8 +10,9 @@ Forward  (requester -> owner -> requester):
   all_to_all(ids)  ->  owner gather (+ register rows for the sparse gradient)  ->
   all_to_all(rows)  ->  fields_fwd reads rows[pos]
 Backward (the sparse reduce-scatter):
-  fields_bwd writes one gradient row per routed entry  ->  all_to_all(rows)  ->
-  owner scatter-add into its compact gradient rows.
+  fields_bwd writes one gradient row per routed entry  ->  all_to_all(rows)  ->  the received
+  rows are the owner's sparse gradient (slot = received entry; fbn_sparse_fixup folds rows hit
+  by several entries into the entry that claimed the row in the forward).
 Split sizes need one host read of the N routed counts per step (all_to_all_single takes
 host split lists); everything else stays on the device.
 """
@@ -33,13 +34,9 @@ class HipExchangeKernels:
         call("fbn_route", ptr(item), ptr(seq), B, L, V, Vl, world, ptr(counts), ptr(offsets), ptr(cursor),
              ptr(send_ids), ptr(pos), ptr(err), _lib.stream_handle(item.device))
 
-    def owner_gather(self, ids, E, out, map_, n_uniq, uniq_rows, rank, d):
-        call("fbn_owner_gather", ptr(ids), ids.shape[0], ptr(E), ptr(out), ptr(map_), ptr(n_uniq), ptr(uniq_rows),
-             rank, d, _lib.stream_handle(E.device))
-
-    def owner_scatter(self, ids, grad, map_, gU, rank, d):
-        call("fbn_owner_scatter", ptr(ids), ids.shape[0], ptr(grad), ptr(map_), ptr(gU), rank, d,
-             _lib.stream_handle(gU.device))
+    def owner_gather(self, ids, E, out, map_, slot_row, rank, d):
+        call("fbn_owner_gather", ptr(ids), ids.shape[0], ptr(E), ptr(out), ptr(map_), ptr(slot_row), rank, d,
+             _lib.stream_handle(E.device))
 
 
 class RowExchange:
@@ -95,8 +92,7 @@ class RowExchange:
         self.recv_ids = torch.empty(n_recv, dtype=torch.int32, device=item.device)
         self._a2a(self.recv_ids, self.send_ids[:n_send], rc, sc)
         reply = torch.empty((n_recv, self.d), dtype=torch.float32, device=item.device)
-        self.k.owner_gather(self.recv_ids, E_local, reply, sparse["map"], sparse["n_uniq"], sparse["uniq_rows"],
-                            self.rank, self.d)
+        self.k.owner_gather(self.recv_ids, E_local, reply, sparse["map"], sparse["slot_row"], self.rank, self.d)
         rows = torch.empty((n_send, self.d), dtype=torch.float32, device=item.device)
         self._a2a(rows, reply, sc, rc)
         return rows
@@ -104,11 +100,12 @@ class RowExchange:
     def make_sendbuf(self) -> torch.Tensor:
         return torch.empty((sum(self.send_counts), self.d), dtype=torch.float32, device=self.device)
 
-    def backward(self, sendbuf: torch.Tensor, sparse) -> None:
+    def backward(self, sendbuf: torch.Tensor) -> torch.Tensor:
+        """Returns the owner's received gradient rows [n_recv, d] (entry i <-> recv_ids[i])."""
         n_recv = sum(self.recv_counts)
         grad = torch.empty((n_recv, self.d), dtype=torch.float32, device=sendbuf.device)
         self._a2a(grad, sendbuf, self.recv_counts, self.send_counts)
-        self.k.owner_scatter(self.recv_ids, grad, sparse["map"], sparse["gU"], self.rank, self.d)
+        return grad
 
 
 class DistCollective:

@@ -14,6 +14,7 @@ Layouts (B = batch, d = embedding dim, L = history length; DESIGN.md "HBM layout
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass
 from typing import Dict, Optional
 
@@ -43,11 +44,45 @@ def _ws(nbytes: int, device) -> Optional[torch.Tensor]:
 
 def gemm(A, B, C, M, N, K, lda, ldb, ldc, transA, transB, bias=None, rB=NO_REMAP, rC=NO_REMAP, beta=0.0,
          bf16=False, stream=None):
+    """C = op(A) op(B) (+bias, +beta C).  A / B may be fp32 or bf16 (torch.bfloat16) tensors."""
     nbytes = _lib.lib().fbn_gemm_workspace_size(M, N, K, int(bf16))
     ws = _ws(nbytes, C.device)
+    a16, b16 = int(A.dtype == torch.bfloat16), int(B.dtype == torch.bfloat16)
     call("fbn_gemm", ptr(A), ptr(B), ptr(C), ptr(bias), M, N, K, lda, ldb, ldc, int(transA), int(transB),
-         rB[0], rB[1], rB[2], rC[0], rC[1], rC[2], float(beta), int(bf16), ptr(ws), nbytes,
+         rB[0], rB[1], rB[2], rC[0], rC[1], rC[2], float(beta), int(bf16 or a16 or b16), a16, b16, ptr(ws), nbytes,
          stream if stream is not None else _lib.stream_handle())
+
+
+class _ConvJob(ctypes.Structure):
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("rows", ctypes.c_int), ("cols", ctypes.c_int),
+                ("ld", ctypes.c_int), ("trans", ctypes.c_int), ("seg", ctypes.c_int), ("off0", ctypes.c_int),
+                ("off1", ctypes.c_int)]
+
+
+def bf16_weights(p: Dict[str, torch.Tensor], d: int, a: Dict[str, torch.Tensor], stream) -> Dict[str, torch.Tensor]:
+    """bf16 images of the GEMM weights, laid out so every bf16 GEMM operand is K-contiguous:
+    Wa_nz [512,15d] (zero columns dropped) and its transpose, Wb and Wb^T, W and W^T, Wp."""
+    dev = p["mlp.0.weight"].device
+    KC = 15 * d
+    spec = [("Wa", p["mlp.0.weight"], H1, KC, 21 * d, 0, wa_remap(d)),
+            ("WaT", p["mlp.0.weight"], KC, H1, 21 * d, 1, wa_remap(d)),
+            ("Wb", p["mlp.4.weight"], H2, H1, H1, 0, NO_REMAP),
+            ("WbT", p["mlp.4.weight"], H1, H2, H1, 1, NO_REMAP),
+            ("Wp", p["mm_proj.0.weight"], d, 128, 128, 0, NO_REMAP)]
+    if "bilinear.W" in p:
+        spec += [("W", p["bilinear.W"], d, d, d, 0, NO_REMAP), ("WT", p["bilinear.W"], d, d, d, 1, NO_REMAP)]
+    jobs = (_ConvJob * 8)()
+    out = {}
+    for i, (name, src, rows, cols, ld, trans, rm) in enumerate(spec):
+        key = "w16_" + name
+        t = a.get(key)
+        if t is None or tuple(t.shape) != (rows, cols):
+            t = torch.empty((rows, cols), dtype=torch.bfloat16, device=dev)
+            a[key] = t
+        out[name] = t
+        jobs[i] = _ConvJob(src.data_ptr(), t.data_ptr(), rows, cols, ld, trans, rm[0], rm[1], rm[2])
+    call("fbn_convert_bf16", ctypes.cast(jobs, ctypes.c_void_p).value, len(spec), stream)
+    return out
 
 
 def colsum(X, B, C, ldx, out, beta=0.0, stream=None):
@@ -95,7 +130,7 @@ def bn_train_stats(h, B, C, mean, invstd, run_mean, run_var, ntot, coll: Collect
 
 
 def bn_backward(G, gvec, w, hact, scale, hpre, mean, invstd, gamma, B, C, ntot, dpre, dgamma, dbeta, dw,
-                coll: Collective, stream):
+                coll: Collective, stream, dpre16=None):
     dev = hpre.device
     ws = _ws(_lib.lib().fbn_bn_workspace_size(B, C), dev)
     red = torch.empty(3 * C, dtype=torch.float64, device=dev)
@@ -106,12 +141,13 @@ def bn_backward(G, gvec, w, hact, scale, hpre, mean, invstd, gamma, B, C, ntot, 
         red_g = red.clone()
         coll.allreduce_(red_g)            # global sums -> the SyncBN input gradient
     call("fbn_bn_bwd_apply", ptr(G), ptr(gvec), ptr(w), ptr(hact), float(scale), ptr(hpre), ptr(mean), ptr(invstd),
-         ptr(gamma), B, C, ptr(red_g), float(ntot), ptr(dpre), ptr(dgamma), ptr(dbeta), ptr(dw), ptr(ws), stream)
+         ptr(gamma), B, C, ptr(red_g), float(ntot), ptr(dpre), ptr(dpre16), ptr(dgamma), ptr(dbeta), ptr(dw), ptr(ws),
+         stream)
     if coll.world > 1:
         # parameter grads from this rank's sums only (the dense-grad all-reduce adds the ranks);
         # B = 0 runs just the finalize step, after the apply above has consumed its coefficients
         call("fbn_bn_bwd_apply", ptr(G), ptr(gvec), ptr(w), ptr(hact), float(scale), ptr(hpre), ptr(mean),
-             ptr(invstd), ptr(gamma), 0, C, ptr(red), float(ntot), None, ptr(dgamma), ptr(dbeta), ptr(dw),
+             ptr(invstd), ptr(gamma), 0, C, ptr(red), float(ntot), None, None, ptr(dgamma), ptr(dbeta), ptr(dw),
              ptr(ws), stream)
 
 
@@ -121,13 +157,13 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
             err: Optional[torch.Tensor] = None, labels: Optional[torch.Tensor] = None,
             loss_denom: Optional[float] = None, coll: Collective = NO_COLLECTIVE, ntot: Optional[int] = None,
             masks_out: Optional[Dict[str, torch.Tensor]] = None, acts: Optional[Dict[str, torch.Tensor]] = None,
-            probe: Optional[Dict[str, list]] = None, masks_in: Optional[Dict[str, torch.Tensor]] = None
-            ) -> Dict[str, torch.Tensor]:
+            probe: Optional[Dict[str, list]] = None, masks_in: Optional[Dict[str, torch.Tensor]] = None,
+            after_gather=None) -> Dict[str, torch.Tensor]:
     """Run the forward; returns the activation dict (probs, logits and what backward needs).
 
     p: parameter tensors keyed like the reference state_dict (fp32, contiguous, on device).
     table_rows/pos: multi-GPU mode (rows already exchanged); otherwise p['item_emb.weight'] is read.
-    sparse: {'map','n_uniq','uniq_rows'} to register touched rows for the native sparse-grad Adam.
+    sparse: {'map','slot_row'} to register touched rows for the native sparse-grad Adam.
     labels: if given, fuses BCE: acts['loss_terms'] and acts['gout'] (= dL/dlogit).
     """
     d, L = cfg.d, cfg.L
@@ -149,13 +185,16 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     seq = batch.get("item_seq", None)
     Lr = 0 if seq is None else L
     x_mm = batch["item_emb_d128"]
+    bf = cfg.bf16
+    w16 = bf16_weights(p, d, a, st) if bf else None
+    a["w16"] = w16
     hmm = buf("hmm", (B, d))
-    gemm(x_mm, p["mm_proj.0.weight"], hmm, B, d, 128, 128, 128, d, False, True, bias=p["mm_proj.0.bias"],
-         bf16=cfg.bf16, stream=st)
+    gemm(x_mm, w16["Wp"] if bf else p["mm_proj.0.weight"], hmm, B, d, 128, 128, 128, d, False, True,
+         bias=p["mm_proj.0.bias"], bf16=bf, stream=st)
     X = buf("X", (B, 5, d))
     Vc = buf("Vc", (B, 5, d))
     KC = 15 * d
-    c = buf("c", (B, KC))
+    c = buf("c", (B, KC), torch.bfloat16 if bf else torch.float32)     # bf16 mode: GEMM-only operand
     av = buf("a", (B, 6))
     cnt = buf("cnt", (B,))
     if err is None:
@@ -174,27 +213,35 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
          ptr(p["cate_emb.weight"]), p["cate_emb.weight"].shape[0], ptr(E), V, ptr(pos),
          ptr(p["senet.excitation.0.weight"]), ptr(p["senet.excitation.0.bias"]),
          ptr(p["senet.excitation.2.weight"]), ptr(p["senet.excitation.2.bias"]), cfg.R, ptr(X), ptr(Vc), ptr(c), KC,
-         ptr(av), ptr(cnt), ptr(err), ptr(sm.get("map")), ptr(sm.get("n_uniq")), ptr(sm.get("uniq_rows")),
-         B, Lr, d, st)
+         int(bf), ptr(av), ptr(cnt), ptr(err), ptr(sm.get("map")), ptr(sm.get("slot_row")), B, Lr, d, st)
     if ev is not None:
         ev[1].record()
+    if after_gather is not None:
+        after_gather()
     # bilinear: U = V W  ("all")  or  U_i = V_i W_i ("each"), then pair products into c
     U = buf("U", (B, 5, d))
     if not cfg.bilinear_each:
-        gemm(Vc, p["bilinear.W"], U, 5 * B, d, d, d, d, d, False, False, bf16=cfg.bf16, stream=st)
+        if bf:   # B(k,n) = W[k][n]: K-contiguous image is W^T
+            gemm(Vc, w16["WT"], U, 5 * B, d, d, d, d, d, False, True, bf16=True, stream=st)
+        else:
+            gemm(Vc, p["bilinear.W"], U, 5 * B, d, d, d, d, d, False, False, stream=st)
     else:
         U.zero_()
         for f in range(1, 5):   # field index in Vc: f-1 <-> reference field f; W_list[f]
             gemm(Vc[:, f - 1], p[f"bilinear.W_list.{f}"], U[:, f - 1], B, d, d, 5 * d, d, 5 * d, False, False,
-                 bf16=cfg.bf16, stream=st)
-    call("fbn_pairs_fwd", ptr(Vc), ptr(U), ptr(c), B, d, KC, int(cfg.bilinear_each), st)
+                 bf16=bf, stream=st)
+    call("fbn_pairs_fwd", ptr(Vc), ptr(U), ptr(c), B, d, KC, int(cfg.bilinear_each), int(bf), st)
     # MLP layer 1
     h1pre = buf("h1pre", (B, H1))
-    gemm(c, p["mlp.0.weight"], h1pre, B, H1, KC, KC, 21 * d, H1, False, True, bias=p["mlp.0.bias"],
-         rB=wa_remap(d), bf16=cfg.bf16, stream=st)
+    if bf:
+        gemm(c, w16["Wa"], h1pre, B, H1, KC, KC, KC, H1, False, True, bias=p["mlp.0.bias"], bf16=True, stream=st)
+    else:
+        gemm(c, p["mlp.0.weight"], h1pre, B, H1, KC, KC, 21 * d, H1, False, True, bias=p["mlp.0.bias"],
+             rB=wa_remap(d), stream=st)
     mean1, inv1 = buf("mean1", (H1,)), buf("inv1", (H1,))
     mean2, inv2 = buf("mean2", (H2,)), buf("inv2", (H2,))
     h1 = buf("h1", (B, H1))
+    h1_16 = buf("h1_16", (B, H1), torch.bfloat16) if bf else None
     h2pre = buf("h2pre", (B, H2))
     h2 = buf("h2", (B, H2))
     p_drop = cfg.p_drop if cfg.training else 0.0
@@ -208,16 +255,18 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
         call("fbn_bn_eval_params", ptr(p["mlp.1.running_mean"]), ptr(p["mlp.1.running_var"]), ptr(mean1), ptr(inv1),
              H1, BN_EPS, st)
     call("fbn_bn_act_fwd", ptr(h1pre), ptr(h1), B, H1, ptr(mean1), ptr(inv1), ptr(p["mlp.1.weight"]),
-         ptr(p["mlp.1.bias"]), float(p_drop), ptr(rng), 1, ptr(m1), ptr(mi1), st)
-    gemm(h1, p["mlp.4.weight"], h2pre, B, H2, H1, H1, H1, H2, False, True, bias=p["mlp.4.bias"], bf16=cfg.bf16,
-         stream=st)
+         ptr(p["mlp.1.bias"]), float(p_drop), ptr(rng), 1, ptr(m1), ptr(mi1), ptr(h1_16), st)
+    if bf:
+        gemm(h1_16, w16["Wb"], h2pre, B, H2, H1, H1, H1, H2, False, True, bias=p["mlp.4.bias"], bf16=True, stream=st)
+    else:
+        gemm(h1, p["mlp.4.weight"], h2pre, B, H2, H1, H1, H1, H2, False, True, bias=p["mlp.4.bias"], stream=st)
     if cfg.training:
         bn_train_stats(h2pre, B, H2, mean2, inv2, p["mlp.5.running_mean"], p["mlp.5.running_var"], ntot, coll, st)
     else:
         call("fbn_bn_eval_params", ptr(p["mlp.5.running_mean"]), ptr(p["mlp.5.running_var"]), ptr(mean2), ptr(inv2),
              H2, BN_EPS, st)
     call("fbn_bn_act_fwd", ptr(h2pre), ptr(h2), B, H2, ptr(mean2), ptr(inv2), ptr(p["mlp.5.weight"]),
-         ptr(p["mlp.5.bias"]), float(p_drop), ptr(rng), 2, ptr(m2), ptr(mi2), st)
+         ptr(p["mlp.5.bias"]), float(p_drop), ptr(rng), 2, ptr(m2), ptr(mi2), None, st)
     logits, probs = buf("logits", (B,)), buf("probs", (B,))
     lt = buf("loss_terms", (B,)) if labels is not None else None
     go = buf("gout", (B,)) if labels is not None else None
@@ -232,13 +281,15 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
 
 
 def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict[str, torch.Tensor],
-             gout: torch.Tensor, g: Dict[str, torch.Tensor], cfg: FwdConfig, *, table_grad: torch.Tensor,
-             table_map: Optional[torch.Tensor] = None, pos: Optional[torch.Tensor] = None,
+             gout: torch.Tensor, g: Dict[str, torch.Tensor], cfg: FwdConfig, *,
+             table_grad: Optional[torch.Tensor] = None, gvec: Optional[torch.Tensor] = None,
+             pos: Optional[torch.Tensor] = None,
              sendbuf: Optional[torch.Tensor] = None, coll: Collective = NO_COLLECTIVE,
              ntot: Optional[int] = None) -> None:
     """Backward from dL/dlogit (gout [B]) into the gradient buffers ``g`` (same keys as ``p``).
 
-    table_grad: dense [V, d] (drop-in) or compact [U, d] rows addressed through table_map
+    table_grad: dense [V, d] (drop-in, accumulated by atomics); or gvec [B, 2, d] (native
+    trainer: per-sample {item-row grad, history-row grad}, resolved through the slot map)
     (native trainer); in multi-GPU mode (pos given) rows are written to sendbuf instead.
     Every g[...] buffer is overwritten (not accumulated), except the table gradient which is
     accumulated into (callers zero it).
@@ -252,31 +303,43 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     scale = 1.0 / (1.0 - cfg.p_drop) if (cfg.training and cfg.p_drop > 0) else 1.0
     f32 = dict(dtype=torch.float32, device=dev)
     # head + BN2 backward (rank-1 source gout (x) Wc)
+    bf = cfg.bf16
+    w16 = a.get("w16")
+    bf16_ = dict(dtype=torch.bfloat16, device=dev)
     dh2pre = torch.empty((B, H2), **f32)
+    dh2pre16 = torch.empty((B, H2), **bf16_) if bf else None
     bn_backward(None, gout, p["mlp.8.weight"], a["h2"], scale, a["h2pre"], a["mean2"], a["inv2"],
                 p["mlp.5.weight"], B, H2, ntot, dh2pre, g["mlp.5.weight"], g["mlp.5.bias"], g["mlp.8.weight"],
-                coll, st)
+                coll, st, dpre16=dh2pre16)
     call("fbn_sum", ptr(gout), B, ptr(g["mlp.8.bias"]), 1.0, st)
     colsum(dh2pre, B, H2, H2, g["mlp.4.bias"], stream=st)
-    gemm(dh2pre, a["h1"], g["mlp.4.weight"], H2, H1, B, H2, H1, H1, True, False, bf16=cfg.bf16, stream=st)
     dh1 = torch.empty((B, H1), **f32)
-    gemm(dh2pre, p["mlp.4.weight"], dh1, B, H1, H2, H2, H1, H1, False, False, bf16=cfg.bf16, stream=st)
+    if bf:
+        gemm(dh2pre16, a["h1_16"], g["mlp.4.weight"], H2, H1, B, H2, H1, H1, True, False, stream=st)
+        gemm(dh2pre16, w16["WbT"], dh1, B, H1, H2, H2, H2, H1, False, True, stream=st)
+    else:
+        gemm(dh2pre, a["h1"], g["mlp.4.weight"], H2, H1, B, H2, H1, H1, True, False, stream=st)
+        gemm(dh2pre, p["mlp.4.weight"], dh1, B, H1, H2, H2, H1, H1, False, False, stream=st)
     dh1pre = torch.empty((B, H1), **f32)
+    dh1pre16 = torch.empty((B, H1), **bf16_) if bf else None
     bn_backward(dh1, None, None, a["h1"], scale, a["h1pre"], a["mean1"], a["inv1"], p["mlp.1.weight"], B, H1, ntot,
-                dh1pre, g["mlp.1.weight"], g["mlp.1.bias"], None, coll, st)
+                dh1pre, g["mlp.1.weight"], g["mlp.1.bias"], None, coll, st, dpre16=dh1pre16)
     colsum(dh1pre, B, H1, H1, g["mlp.0.bias"], stream=st)
-    gemm(dh1pre, a["c"], g["mlp.0.weight"], H1, KC, B, H1, KC, 21 * d, True, False, rC=wa_remap(d), bf16=cfg.bf16,
-         stream=st)
     dc = torch.empty((B, KC), **f32)
-    gemm(dh1pre, p["mlp.0.weight"], dc, B, KC, H1, H1, 21 * d, KC, False, False, rB=wa_remap(d), bf16=cfg.bf16,
-         stream=st)
+    if bf:
+        gemm(dh1pre16, a["c"], g["mlp.0.weight"], H1, KC, B, H1, KC, 21 * d, True, False, rC=wa_remap(d), stream=st)
+        gemm(dh1pre16, w16["WaT"], dc, B, KC, H1, H1, H1, KC, False, True, stream=st)
+    else:
+        gemm(dh1pre, a["c"], g["mlp.0.weight"], H1, KC, B, H1, KC, 21 * d, True, False, rC=wa_remap(d), stream=st)
+        gemm(dh1pre, p["mlp.0.weight"], dc, B, KC, H1, H1, 21 * d, KC, False, False, rB=wa_remap(d), stream=st)
     # bilinear backward
     dV = torch.empty((B, 5, d), **f32)
     dU = torch.empty((B, 5, d), **f32)
     call("fbn_pairs_bwd", ptr(dc), ptr(a["Vc"]), ptr(a["U"]), ptr(dV), ptr(dU), B, d, KC, int(cfg.bilinear_each), st)
     if not cfg.bilinear_each:
-        gemm(dU, p["bilinear.W"], dV, 5 * B, d, d, d, d, d, False, True, beta=1.0, bf16=cfg.bf16, stream=st)
-        gemm(a["Vc"], dU, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, bf16=cfg.bf16, stream=st)
+        gemm(dU, w16["W"] if bf else p["bilinear.W"], dV, 5 * B, d, d, d, d, d, False, True, beta=1.0, bf16=bf,
+             stream=st)
+        gemm(a["Vc"], dU, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, bf16=bf, stream=st)
     else:
         g["bilinear.W_list.0"].zero_()
         for f in range(1, 5):
@@ -290,22 +353,19 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     P = _lib.lib().fbn_fields_bwd_partials_size(d, R, ncate)
     nblk = _lib.lib().fbn_fields_bwd_grid(B, d)
     partials = torch.empty((nblk, P), **f32)
-    pg = torch.empty((P,), **f32)
     dhmm = torch.empty((B, d), **f32)
     seq = batch.get("item_seq", None)
     Lr = 0 if seq is None else L
     V = p["item_emb.weight"].shape[0] if pos is None else 0
+    keys = ("senet.excitation.0.weight", "senet.excitation.0.bias", "senet.excitation.2.weight",
+            "senet.excitation.2.bias", "mm_proj.1.weight", "mm_proj.1.bias", "cate_emb.weight")
+    outs_arr = (ctypes.c_void_p * 7)(*[g[k].data_ptr() for k in keys])   # host array of device pointers
+    outs = ctypes.cast(outs_arr, ctypes.c_void_p).value
     call("fbn_fields_bwd", ptr(batch["item_id"]), ptr(seq) if Lr else None, ptr(batch["likes_level"]),
          ptr(batch["views_level"]), ptr(a["hmm"]), ptr(p["mm_proj.1.weight"]), LN_EPS,
          ptr(p["senet.excitation.0.weight"]), ptr(p["senet.excitation.0.bias"]), ptr(p["senet.excitation.2.weight"]),
-         R, ncate, ptr(a["X"]), ptr(a["a"]), ptr(a["cnt"]), ptr(dV), ptr(dhmm), ptr(partials), ptr(pg),
-         ptr(table_grad), ptr(table_map), V, ptr(pos), ptr(sendbuf), B, Lr, d, st)
-    o = 0
-    for key, n in (("senet.excitation.0.weight", 6 * R), ("senet.excitation.0.bias", R),
-                   ("senet.excitation.2.weight", 6 * R), ("senet.excitation.2.bias", 6),
-                   ("mm_proj.1.weight", d), ("mm_proj.1.bias", d), ("cate_emb.weight", ncate * d)):
-        g[key].view(-1).copy_(pg[o:o + n])
-        o += n
+         R, ncate, ptr(a["X"]), ptr(a["a"]), ptr(a["cnt"]), ptr(dV), ptr(dhmm), ptr(partials), outs,
+         ptr(table_grad), ptr(gvec), V, ptr(pos), ptr(sendbuf), B, Lr, d, st)
     gemm(dhmm, batch["item_emb_d128"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True, False, bf16=cfg.bf16,
          stream=st)
     colsum(dhmm, B, d, d, g["mm_proj.0.bias"], stream=st)

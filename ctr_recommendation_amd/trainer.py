@@ -7,9 +7,12 @@ into one hipGraph), and with the item-table gradient kept sparse:
 
 * dense parameters (everything but the two id tables) live in ONE flat fp32 buffer with
   matching flat grad / Adam-m / Adam-v buffers: one norm pass and one fused Adam launch;
-* the item table gradient is a compact [U, d] buffer addressed through a row->slot map
-  registered by the forward gather; the dense Adam pass over the table reads the gradient
-  only through that map (exact torch semantics: untouched rows still get g = wd * p);
+* the item-table gradient never exists as a dense V x d tensor.  The forward lets the first
+  entry (sample, slot) that touches a row claim it (row -> entry map); the backward stores two
+  vectors per sample (item-row and history-row gradients) with plain stores; a fix-up pass
+  folds duplicate rows into their claimer; the dense Adam pass over the table reads the
+  gradient of row r through the map (exact torch semantics: untouched rows still get
+  g = wd * p) -- 24 B/element instead of zero-fill + scatter + 28 B/element;
 * user_emb receives no gradient in the reference (the user field is zeros), so torch's Adam
   skips it; it is kept (state_dict contract) and never updated here either.
 
@@ -19,8 +22,7 @@ reference computes), dense gradients are all-reduced, the clip norm sums the tab
 """
 from __future__ import annotations
 
-import math
-from typing import Dict, List, Optional, Tuple
+from typing import Dict, List, Optional
 
 import numpy as np
 import torch
@@ -37,19 +39,19 @@ BUFFERS = ("mlp.1.running_mean", "mlp.1.running_var", "mlp.1.num_batches_tracked
            "mlp.5.running_mean", "mlp.5.running_var", "mlp.5.num_batches_tracked")
 
 
-def _events(probe, name):
-    """Start a (start, end) HIP-event pair on the current stream for kernel `name` (bench probes)."""
+def _events(probe, name, stream=None):
+    """Start a (start, end) HIP-event pair on `stream` (default: current) for kernel `name` (bench probes)."""
     if probe is None:
         return None
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
+    s.record(stream)
     probe.setdefault(name, []).append((s, e))
     return e
 
 
-def _events_end(e):
+def _events_end(e, stream=None):
     if e is not None:
-        e.record()
+        e.record(stream)
 
 
 def _pad4(n: int) -> int:
@@ -74,9 +76,9 @@ class FiBiNETTrainer:
         if init_state is None:
             torch.manual_seed(seed)
             init_state = build_model(None, self.cfg).state_dict()
-        # model structure (reuses the drop-in module's definition for names / shapes)
         with torch.random.fork_rng(devices=[]):            # no side effect on the caller's RNG stream
             shape_model = build_model(None, dict(self.cfg, vocab_size=4))
+        self.key_order = list(shape_model.state_dict().keys())
         self.d = shape_model.emb_dim
         self.p_drop = shape_model.dropout_p
         self.fcfg = ops.FwdConfig(d=self.d, L=max_len, training=True, p_drop=self.p_drop,
@@ -85,9 +87,10 @@ class FiBiNETTrainer:
                                   R=shape_model.senet.excitation[0].out_features)
         self.V = init_state[TABLE].shape[0]
         dev = self.device
+        d = self.d
         # ---------------- dense parameters: one flat buffer (16-B aligned segments)
         self.dense_names: List[str] = [n for n, _ in shape_model.named_parameters() if n != TABLE and n not in FROZEN]
-        self.shapes = {n: tuple(init_state[n].shape) for n in init_state}
+        self.shapes = {n: tuple(init_state[n].shape) for n in self.key_order}
         offs, o = {}, 0
         for n in self.dense_names:
             offs[n] = o
@@ -118,14 +121,12 @@ class FiBiNETTrainer:
         self.Ev = torch.zeros_like(self.E)
         if world == 1:
             self.p[TABLE] = self.E
-        cap = min(self.rows_local, world * self.B * (max_len + 1)) + 1
         i32 = dict(dtype=torch.int32, device=dev)
-        self.sparse = {
-            "map": torch.full((max(1, self.rows_local),), -1, **i32),
-            "n_uniq": torch.zeros(1, **i32),
-            "uniq_rows": torch.zeros(cap, **i32),
-            "gU": torch.zeros((cap, self.d), dtype=torch.float32, device=dev),
-        }
+        self.n_entries = self.B * (max_len + 1) if world == 1 else world * self.B * (max_len + 1)
+        self.map = torch.full((max(1, self.rows_local),), -1, **i32)         # row -> claiming entry
+        self.slot_row = torch.full((self.n_entries,), -1, **i32)              # entry -> claimed row
+        self.gvec = torch.zeros((self.B, 2, d), dtype=torch.float32, device=dev) if world == 1 else None
+        self.extra = torch.zeros((self.n_entries, d), dtype=torch.float32, device=dev) if world == 1 else None
         # ---------------- optimizer schedule + device step state
         self.total_steps = total_steps
         tab, self.lrs = adam_table(total_steps, self.lr, self.beta2, OneCycle(total_steps, self.lr))
@@ -134,8 +135,8 @@ class FiBiNETTrainer:
         seed_d = dropout_seed if dropout_seed is not None else (seed * 1000003 + 17)
         seed_d += rank * 0x9E3779B9            # independent dropout stream per rank
         self.rng = torch.tensor([seed_d & 0x7FFFFFFFFFFF, 0], dtype=torch.int64, device=dev)
-        self.sumsq = torch.zeros(1, dtype=torch.float64, device=dev)
-        self.sumsq_tab = torch.zeros(1, dtype=torch.float64, device=dev)
+        self.sumsq = torch.zeros(64, dtype=torch.float64, device=dev)        # FBN_SUMSQ_SLOTS
+        self.sumsq_tab = torch.zeros(64, dtype=torch.float64, device=dev)
         self.coef = torch.ones(1, dtype=torch.float32, device=dev)
         self.norm = torch.zeros(1, dtype=torch.float32, device=dev)
         self.err = torch.zeros(1, **i32)
@@ -143,9 +144,10 @@ class FiBiNETTrainer:
         self.host_step = 0
         self.acts: Dict[str, torch.Tensor] = {}
         self.coll = DistCollective(world, group, stage_on_cpu)
-        self.xchg = RowExchange(rank, world, self.V, self.d, self.B, max_len, dev, group,
+        self.xchg = RowExchange(rank, world, self.V, d, self.B, max_len, dev, group,
                                 stage_on_cpu=stage_on_cpu) if world > 1 else None
         self.stage_on_cpu = stage_on_cpu
+        self.side = torch.cuda.Stream(device=dev)       # untouched-row Adam overlaps the backward
 
     # ------------------------------------------------------------------ one training step
     def step(self, batch: Dict[str, torch.Tensor], labels: torch.Tensor,
@@ -154,50 +156,83 @@ class FiBiNETTrainer:
         """One optimizer step on this rank's batch; returns the (device) global-mean BCE loss.
 
         masks_out (tests only): {'m1': u8 [B,512], 'm2': u8 [B,256]} receives the dropout keep-masks.
+        probe (bench only): collects HIP-event pairs around the gather and table-Adam launches.
         """
         if self.host_step >= self.total_steps:
             raise ValueError(f"Tried to step {self.host_step + 1} times. The specified number of total steps is "
                              f"{self.total_steps}")
         st = _lib.stream_handle(self.device)
         B = batch["item_id"].shape[0]
+        if B > self.B:
+            raise ValueError(f"batch of {B} rows exceeds the trainer's batch_size {self.B}")
         ntot = B * self.world
+        d = self.d
         cfg = self.fcfg
-        if "item_seq" in batch:
-            cfg.L = batch["item_seq"].shape[1]
+        seq = batch.get("item_seq")
+        L = cfg.L = seq.shape[1] if seq is not None else 0
+        if L > self.L:
+            raise ValueError(f"history length {L} exceeds max_len {self.L}")
         rows = pos = None
+        main = torch.cuda.current_stream(self.device)
+
+        def start_untouched_adam():
+            # every row of this shard the batch touches is claimed in `map` by now; the rest get
+            # g = wd * p, independent of the backward -> run them concurrently on the side stream
+            self.side.wait_stream(main)
+            ev = _events(probe, "adam_table", self.side)
+            call("fbn_adam_table", ptr(self.E), ptr(self.Em), ptr(self.Ev), self.rows_local, d, ptr(self.map),
+                 None, None, None, 1, None, ptr(self.sched), ptr(self.step_dev), self.wd, self.beta2, self.eps, 1,
+                 self.side.cuda_stream)
+            _events_end(ev, self.side)
+
         if self.xchg is not None:
-            rows = self.xchg.forward(batch["item_id"], batch.get("item_seq"), self.E, self.sparse, self.err)
+            rows = self.xchg.forward(batch["item_id"], seq, self.E, {"map": self.map, "slot_row": self.slot_row},
+                                     self.err)
             pos = self.xchg.cur_pos
-        a = ops.forward(self.p, batch, cfg, self.rng, table_rows=rows, pos=pos,
-                        sparse=self.sparse if self.xchg is None else None, err=self.err, labels=labels,
+        else:
+            call("fbn_claim_rows", ptr(batch["item_id"]), ptr(seq) if L else None, B, L, self.V, ptr(self.map),
+                 ptr(self.slot_row), st)
+        start_untouched_adam()
+        a = ops.forward(self.p, batch, cfg, self.rng, table_rows=rows, pos=pos, err=self.err, labels=labels,
                         loss_denom=float(ntot), coll=self.coll, ntot=ntot, acts=self.acts, masks_out=masks_out,
                         probe=probe)
         call("fbn_sum", ptr(a["loss_terms"]), B, ptr(self.loss), 1.0 / ntot, st)
         sendbuf = self.xchg.make_sendbuf() if self.xchg is not None else None
-        ops.backward(self.p, batch, a, a["gout"], self.g, cfg, table_grad=self.sparse["gU"],
-                     table_map=self.sparse["map"] if self.xchg is None else None, pos=pos, sendbuf=sendbuf,
-                     coll=self.coll, ntot=ntot)
-        if self.xchg is not None:
+        ops.backward(self.p, batch, a, a["gout"], self.g, cfg, gvec=self.gvec if self.xchg is None else None,
+                     pos=pos, sendbuf=sendbuf, coll=self.coll, ntot=ntot)
+        if self.xchg is None:
+            # single GPU: per-sample vectors; entry e = b*(L+1)+t; duplicates -> extra[claimer]
+            gsrc = (self.gvec, self.extra, L + 1)
+            n_ent = B * (L + 1)
+            call("fbn_sparse_fixup", ptr(batch["item_id"]), ptr(seq) if L else None, None, n_ent, L, self.V, 0,
+                 ptr(self.map), ptr(self.gvec), ptr(self.extra), ptr(self.slot_row), L + 1, d, st)
+        else:
             self.coll.allreduce_(self.flat_g)
             self.coll.allreduce_(self.loss)
-            self.xchg.backward(sendbuf, self.sparse)
+            grows = self.xchg.backward(sendbuf)              # owner: one received row per entry
+            n_ent = grows.shape[0]
+            gsrc = (grows, None, 1)
+            call("fbn_sparse_fixup", None, None, ptr(self.xchg.recv_ids), n_ent, 0, self.V, self.rank, ptr(self.map),
+                 ptr(grows), None, ptr(self.slot_row), 1, d, st)
         # clip_grad_norm_(10): dense grads (identical on every rank) + disjoint table shards
-        call("fbn_sumsq", ptr(self.sparse["gU"]), 0, ptr(self.sparse["n_uniq"]), self.d, ptr(self.sumsq_tab), st)
+        tab_acc = self.sumsq_tab if self.world > 1 else self.sumsq
+        call("fbn_sumsq_sparse", ptr(gsrc[0]), ptr(gsrc[1]), ptr(self.slot_row), gsrc[2], n_ent, d, ptr(tab_acc), st)
+        call("fbn_sumsq", ptr(self.flat_g), self.n_dense, None, 0, ptr(self.sumsq), st)
         if self.world > 1:
             self.coll.allreduce_(self.sumsq_tab)
-        call("fbn_sumsq", ptr(self.flat_g), self.n_dense, None, 0, ptr(self.sumsq), st)
-        self.sumsq.add_(self.sumsq_tab)
+            self.sumsq.add_(self.sumsq_tab)
+            self.sumsq_tab.zero_()
         call("fbn_clip_coef", ptr(self.sumsq), self.max_norm, ptr(self.coef), ptr(self.norm), st)
         call("fbn_adam_dense", ptr(self.flat_p), ptr(self.flat_g), ptr(self.flat_m), ptr(self.flat_v),
              self.n_dense, ptr(self.coef), ptr(self.sched), ptr(self.step_dev), self.wd, self.beta2, self.eps, st)
-        ev = _events(probe, "adam_table")
-        call("fbn_adam_table", ptr(self.E), ptr(self.Em), ptr(self.Ev), self.rows_local, self.d,
-             ptr(self.sparse["map"]), ptr(self.sparse["gU"]), ptr(self.coef), ptr(self.sched), ptr(self.step_dev),
+        main.wait_stream(self.side)                  # untouched pass done before map entries are reset
+        ev = _events(probe, "adam_touched")
+        call("fbn_adam_touched", ptr(self.E), ptr(self.Em), ptr(self.Ev), d, ptr(self.map), ptr(gsrc[0]),
+             ptr(gsrc[1]), ptr(self.slot_row), gsrc[2], n_ent, ptr(self.coef), ptr(self.sched), ptr(self.step_dev),
              self.wd, self.beta2, self.eps, st)
         _events_end(ev)
-        call("fbn_zero_rows", ptr(self.sparse["gU"]), ptr(self.sparse["n_uniq"]), self.d, st)
-        self.sumsq_tab.zero_()
-        call("fbn_step_end", ptr(self.step_dev), ptr(self.rng), ptr(self.sparse["n_uniq"]), ptr(self.sumsq), st)
+        self.slot_row[:n_ent].fill_(-1)
+        call("fbn_step_end", ptr(self.step_dev), ptr(self.rng), ptr(self.sumsq), st)
         self.host_step += 1
         return self.loss
 
@@ -205,12 +240,11 @@ class FiBiNETTrainer:
     @torch.no_grad()
     def predict(self, batch: Dict[str, torch.Tensor], logits: bool = False) -> torch.Tensor:
         cfg = ops.FwdConfig(**{**self.fcfg.__dict__, "training": False})
-        if "item_seq" in batch:
-            cfg.L = batch["item_seq"].shape[1]
+        cfg.L = batch["item_seq"].shape[1] if "item_seq" in batch else 0
         rows = pos = None
         if self.xchg is not None:
-            scratch = {"map": None, "n_uniq": None, "uniq_rows": None}
-            rows = self.xchg.forward(batch["item_id"], batch.get("item_seq"), self.E, scratch, self.err)
+            rows = self.xchg.forward(batch["item_id"], batch.get("item_seq"), self.E, {"map": None, "slot_row": None},
+                                     self.err)
             pos = self.xchg.cur_pos
         a = ops.forward(self.p, batch, cfg, None, table_rows=rows, pos=pos, err=self.err)
         return (a["logits"] if logits else a["probs"]).clone()
@@ -228,24 +262,26 @@ class FiBiNETTrainer:
         import torch.distributed as dist
         out = {}
         if self.world > 1:
-            parts = [torch.zeros((self.Vl, self.d), dtype=torch.float32, device=self.device)
-                     for _ in range(self.world)]
             local = torch.zeros((self.Vl, self.d), dtype=torch.float32, device=self.device)
             local[:self.rows_local] = self.E
             if self.stage_on_cpu:
-                cparts = [t.cpu() for t in parts]
-                dist.all_gather(cparts, local.cpu(), group=self.group)
-                full = torch.cat(cparts)[:self.V]
+                parts = [torch.zeros((self.Vl, self.d)) for _ in range(self.world)]
+                dist.all_gather(parts, local.cpu(), group=self.group)
+                full = torch.cat(parts)[:self.V]
             else:
+                parts = [torch.zeros_like(local) for _ in range(self.world)]
                 dist.all_gather(parts, local, group=self.group)
                 full = torch.cat(parts)[:self.V].cpu()
         else:
             full = self.E.detach().cpu().clone()
-        with torch.random.fork_rng(devices=[]):
-            order = list(build_model(None, dict(self.cfg, vocab_size=4)).state_dict().keys())
-        for k in order:
-            if k == TABLE:
-                out[k] = full
-            else:
-                out[k] = self.p[k].detach().cpu().clone()
+        for k in self.key_order:
+            out[k] = full if k == TABLE else self.p[k].detach().cpu().clone()
         return out
+
+    def load_state_dict(self, sd: Dict[str, torch.Tensor]) -> None:
+        """Load reference-format weights (optimizer state is reset, as the reference never saves it)."""
+        for k in self.key_order:
+            if k == TABLE:
+                self.E.copy_(sd[k][self.rows_lo:self.rows_lo + self.rows_local].to(self.device))
+            else:
+                self.p[k].copy_(sd[k].to(self.device))

@@ -45,40 +45,46 @@ int fbn_device_ok(void); /* 1 if the current HIP device is gfx950 */
  *   MLP Linear x3             src/model_fibinet.py:126,130,134,197
  * and all of their autograd backward GEMMs.  Split-K slabs need ws >= fbn_gemm_workspace_size. */
 size_t fbn_gemm_workspace_size(int M, int N, int K, int bf16);
-int fbn_gemm(const float* A, const float* B, float* C, const float* bias, int M, int N, int K, int lda, int ldb,
+/* a16 / b16: operand A / B is bf16 in memory (bf16 = 1, ld % 8 == 0, no rB remap); otherwise fp32. */
+int fbn_gemm(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, int lda, int ldb,
              int ldc, int transA, int transB, int rB_seg, int rB_off0, int rB_off1, int rC_seg, int rC_off0,
-             int rC_off1, float beta, int bf16, float* ws, size_t ws_bytes, void* stream);
+             int rC_off1, float beta, int bf16, int a16, int b16, float* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------- K1 + K4: fields + SENET forward
  * Replaces: nn.Embedding lookups (src/model_fibinet.py:155,156,159,167), masked history mean
  * (:165-176), LayerNorm+ReLU of mm_proj (:107-108), torch.stack (:180-182), SENetLayer.forward
  * (:24-35).  table = E [V][D] (pos == NULL) or an exchanged row buffer addressed by
- * pos[B][L+1] (multi-GPU).  map/n_uniq/uniq_rows (optional) register rows for the sparse
- * gradient.  D in {16,32,64,128,256}; L <= 32. */
+ * pos[B][L+1] (multi-GPU).  map (optional) registers rows for the sparse gradient: the
+ * first entry e = b*(L+1)+t touching row r claims it (map[r] = e, slot_row[e] = r; slot_row
+ * pre-filled with -1).  D in {16,32,64,128,256}; L <= 32. */
 int fbn_fields_fwd(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes, const int64_t* views,
                    const float* hmm, const float* ln_g, const float* ln_b, float ln_eps, const float* cate, int n_cate,
                    const float* table, long long V, const int* pos, const float* w1, const float* b1, const float* w2,
-                   const float* b2, int R, float* X, float* Vc, float* c, int ldc, float* a_out, float* cnt_out,
-                   int* err, int* map, int* n_uniq, int* uniq_rows, int B, int L, int D, void* stream);
+                   const float* b2, int R, float* X, float* Vc, void* c, int ldc, int c_bf16, float* a_out, float* cnt_out,
+                   int* err, int* map, int* slot_row, int B, int L, int D, void* stream);
 
 /* ---------------------------------------------------------------- K2 + K4 backward
  * Replaces the autograd of the lines above, including embedding_dense_backward with
- * padding_idx=0 (src/model_fibinet.py:100).  Table gradient: dense gtab[V][D] (map == NULL),
- * compact gtab[slot][D] via map (native trainer), or rows into sendbuf at pos (multi-GPU).
- * param_grads[P] (P = fbn_fields_bwd_partials_size) = {senet W1, b1, W2, b2, LN gamma, beta,
- * cate table}; partials: [fbn_fields_bwd_grid(B,D)][P] scratch. */
+ * padding_idx=0 (src/model_fibinet.py:100).  Table gradient: dense gtab[V][D] by f32 atomics
+ * (gvec == NULL, drop-in), two per-sample vectors gvec[B][2][D] = {dX3, dX5/count} (native
+ * trainer: rows resolve through map/slot_row, see fbn_sparse_fixup), or one row per routed
+ * entry into sendbuf at pos (multi-GPU).
+ * param_grads: host array of 7 device pointers that receive the gradients of {senet W1, b1,
+ * W2, b2, LN gamma, beta, cate table}; partials: [fbn_fields_bwd_grid(B,D)][P] scratch with
+ * P = fbn_fields_bwd_partials_size. */
 int fbn_fields_bwd_partials_size(int D, int R, int n_cate);
 int fbn_fields_bwd_grid(int B, int D);
 int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes, const int64_t* views,
                    const float* hmm, const float* ln_g, float ln_eps, const float* w1, const float* b1, const float* w2,
                    int R, int n_cate, const float* X, const float* a, const float* cnt, const float* dV, float* dhmm,
-                   float* partials, float* param_grads, float* gtab, const int* map, long long V, const int* pos,
+                   float* partials, float* const* param_grads, float* gtab, float* gvec, long long V, const int* pos,
                    float* sendbuf, int B, int L, int D, void* stream);
 
 /* ---------------------------------------------------------------- K5 bilinear pair products
  * Replaces the pair loop + stack + cat of src/model_fibinet.py:75-79,89,191-194 ("all", mode 0)
  * and :81-86 ("each", mode 1).  Pairs (0,j) are structurally zero and not stored. */
-int fbn_pairs_fwd(const float* Vc, const float* U, float* c, int B, int D, int ldc, int mode, void* stream);
+int fbn_pairs_fwd(const float* Vc, const float* U, void* c, int B, int D, int ldc, int mode, int c_bf16,
+                  void* stream);
 int fbn_pairs_bwd(const float* dc, const float* Vc, const float* U, float* dV, float* dU, int B, int D, int ldc,
                   int mode, void* stream);
 
@@ -97,16 +103,20 @@ int fbn_bn_eval_params(const float* run_mean, const float* run_var, float* mean,
                        void* stream);
 int fbn_bn_act_fwd(const float* X, float* Y, int B, int C, const float* mean, const float* invstd, const float* g,
                    const float* b, float p_drop, const unsigned long long* rng, unsigned stream_id,
-                   unsigned char* mask_out, const unsigned char* mask_in, void* stream);
+                   unsigned char* mask_out, const unsigned char* mask_in, short* Y16, void* stream);
 int fbn_bn_bwd_reduce(const float* G, const float* gvec, const float* w, const float* hact, float scale,
                       const float* Xpre, const float* mean, int B, int C, double* red_d, void* ws, void* stream);
 int fbn_bn_bwd_apply(const float* G, const float* gvec, const float* w, const float* hact, float scale,
                      const float* Xpre, const float* mean, const float* invstd, const float* gamma, int B, int C,
-                     const double* red_d, double ntot, float* dXpre, float* dgamma, float* dbeta, float* dw, void* ws,
-                     void* stream);
+                     const double* red_d, double ntot, float* dXpre, short* dXpre16, float* dgamma, float* dbeta,
+                     float* dw, void* ws, void* stream);
 int fbn_bn_bwd(const float* G, const float* gvec, const float* w, const float* hact, float scale, const float* Xpre,
                const float* mean, const float* invstd, const float* gamma, int B, int C, float* dXpre, float* dgamma,
                float* dbeta, float* dw, void* ws, void* stream);
+/* bf16 weight images: jobs = host array of n <= 8 records
+ * {const float* src; short* dst; int rows, cols, ld, trans, seg, off0, off1;}
+ * out[i][j] = bf16(trans ? src[j*ld + rm(i)] : src[i*ld + rm(j)]), rm(x) = x + (x < seg ? off0 : off1). */
+int fbn_convert_bf16(const void* jobs, int n, void* stream);
 size_t fbn_colsum_workspace_size(int B, int C);
 int fbn_colsum(const float* X, int B, int C, int ldx, float* out, float beta, void* ws, void* stream);
 
@@ -125,20 +135,40 @@ int fbn_sumsq(const float* x, long long n, const int* n_rows, int row_len, doubl
 int fbn_clip_coef(const double* sumsq, float max_norm, float* coef, float* norm, void* stream);
 int fbn_adam_dense(float* p, const float* g, float* m, float* v, long long n, const float* coef,
                    const void* consts_table, const int* step, float wd, float beta2, float eps, void* stream);
-int fbn_adam_table(float* p, float* m, float* v, long long nrows, int D, int* map, const float* gU, const float* coef,
-                   const void* consts_table, const int* step, float wd, float beta2, float eps, void* stream);
-int fbn_step_end(int* step, unsigned long long* rng, int* n_uniq, double* sumsq, void* stream);
-int fbn_zero_rows(float* gU, const int* n_uniq, int D, void* stream);
+/* Sparse table gradient.  Slots are entry indices; gvec is the per-sample vector buffer of
+ * fbn_fields_bwd (Lp1 = L+1) or the owner's received per-entry rows (Lp1 = 1).  fixup folds
+ * entries whose row was claimed by another entry into that claimer (extra[] + a flag bit in
+ * slot_row for the single-GPU layout, in place for the owner layout); sumsq_sparse and
+ * adam_table read the gradient of row r as gvec-slot(map[r]) (+ extra). */
+int fbn_sparse_fixup(const int64_t* item, const int64_t* seq, const int* ids, int n, int L, long long V, int rank,
+                     const int* map, const float* gvec, float* extra, int* slot_row, int Lp1, int D, void* stream);
+int fbn_sumsq_sparse(const float* gvec, float* extra, int* slot_row, int Lp1, int n, int D, double* out,
+                     void* stream);
+/* adam_table mode 0: every row (touched rows read their gradient through map); mode 1: only the
+ * rows the batch did not touch -- their gradient is 0, so the update is independent of the
+ * backward and the clip coefficient and runs on a side stream concurrently with the backward;
+ * adam_touched then updates the claimed rows (one group per claiming entry) and resets map. */
+int fbn_adam_table(float* p, float* m, float* v, long long nrows, int D, int* map, const float* gvec, float* extra,
+                   int* slot_row, int Lp1, const float* coef, const void* consts_table, const int* step, float wd,
+                   float beta2, float eps, int mode, void* stream);
+int fbn_adam_touched(float* p, float* m, float* v, int D, int* map, const float* gvec, float* extra, int* slot_row,
+                     int Lp1, int n, const float* coef, const void* consts_table, const int* step, float wd,
+                     float beta2, float eps, void* stream);
+/* sumsq accumulators are FBN_SUMSQ_SLOTS (= 64) doubles; fbn_clip_coef sums them and
+ * fbn_step_end zeroes them.  fbn_claim_rows registers the rows of a batch in map/slot_row (the
+ * same claims fbn_fields_fwd makes when given a map), as a tiny kernel at the start of a step. */
+#define FBN_SUMSQ_SLOTS 64
+int fbn_claim_rows(const int64_t* item, const int64_t* seq, int B, int L, long long V, int* map, int* slot_row,
+                   void* stream);
+int fbn_step_end(int* step, unsigned long long* rng, double* sumsq, void* stream);
 
 /* ---------------------------------------------------------------- row-sharded exchange (multi-GPU)
  * Replaces torch.nn.DataParallel's replicate/scatter of the whole table (src/train_fibinet.py:69-70)
  * by routing ids to the owner of each row block; RCCL all-to-all runs between these calls. */
 int fbn_route(const int64_t* item, const int64_t* seq, int B, int L, long long V, long long Vl, int nranks,
               int* counts, int* offsets, int* cursor, int* send_ids, int* pos, int* err, void* stream);
-int fbn_owner_gather(const int* ids, int n, const float* E, float* out, int* map, int* n_uniq, int* uniq_rows,
-                     int rank, int D, void* stream);
-int fbn_owner_scatter(const int* ids, int n, const float* grad, const int* map, float* gU, int rank, int D,
-                      void* stream);
+int fbn_owner_gather(const int* ids, int n, const float* E, float* out, int* map, int* slot_row, int rank, int D,
+                     void* stream);
 
 #ifdef __cplusplus
 }

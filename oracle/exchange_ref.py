@@ -39,17 +39,19 @@ class CpuExchangeKernels:
                     send_ids[p] = int(ids[b, t] - o * Vl)
                     pos[b, t] = p
 
-    def owner_gather(self, ids, E, out, map_, n_uniq, uniq_rows, rank, d):
+    def owner_gather(self, ids, E, out, map_, slot_row, rank, d):
         for i, r in enumerate(ids.tolist()):
             out[i] = E[r]
             if map_ is not None and not (rank == 0 and r == 0) and int(map_[r]) == -1:
-                u = int(n_uniq[0])
-                map_[r] = u
-                uniq_rows[u] = r
-                n_uniq[0] = u + 1
+                map_[r] = i
+                slot_row[i] = r
 
-    def owner_scatter(self, ids, grad, map_, gU, rank, d):
+    @staticmethod
+    def sparse_fixup_owner(ids, grows, map_, rank):
+        """Restates fbn_sparse_fixup's owner mode: fold duplicates into the claiming entry."""
         for i, r in enumerate(ids.tolist()):
             if rank == 0 and r == 0:
                 continue
-            gU[int(map_[r])] += grad[i]
+            u = int(map_[r])
+            if u != i:
+                grows[u] += grows[i]

@@ -44,9 +44,9 @@ def _worker(rank, world, port, V, d, B, L, q):
         xg = RowExchange(rank, world, V, d, B, L, torch.device("cpu"), kernels=CpuExchangeKernels())
         lo, n_local = xg.rows_lo, xg.rows_local
         E_local = E_full[lo:lo + n_local].clone()
-        cap = world * B * (L + 1) + 1
-        sparse = {"map": torch.full((n_local,), -1, dtype=torch.int32), "n_uniq": torch.zeros(1, dtype=torch.int32),
-                  "uniq_rows": torch.zeros(cap, dtype=torch.int32), "gU": torch.zeros((cap, d))}
+        cap = world * B * (L + 1)
+        sparse = {"map": torch.full((n_local,), -1, dtype=torch.int32),
+                  "slot_row": torch.full((cap,), -1, dtype=torch.int32)}
         err = torch.zeros(1, dtype=torch.int32)
         rows = xg.forward(item, seq, E_local, sparse, err)
         pos = xg.cur_pos
@@ -62,7 +62,8 @@ def _worker(rank, world, port, V, d, B, L, q):
         # backward: one random gradient row per routed entry
         sendbuf = xg.make_sendbuf()
         sendbuf.copy_(torch.randn(sendbuf.shape, generator=gb))
-        xg.backward(sendbuf, sparse)
+        grows = xg.backward(sendbuf)
+        CpuExchangeKernels.sparse_fixup_owner(xg.recv_ids, grows, sparse["map"], rank)
         # dense reference: all ranks' scatter over the global table
         dense = torch.zeros((V, d), dtype=torch.float64)
         for b in range(B):
@@ -72,10 +73,13 @@ def _worker(rank, world, port, V, d, B, L, q):
                     dense[int(ids[b, t])] += sendbuf[p].double()
         dist.all_reduce(dense)
         got = torch.zeros((n_local, d), dtype=torch.float64)
-        nu = int(sparse["n_uniq"][0])
-        for u in range(nu):
-            r = int(sparse["uniq_rows"][u])
-            got[r] = sparse["gU"][u].double()
+        nu = 0
+        for i in range(grows.shape[0]):
+            r = int(sparse["slot_row"][i])
+            if r >= 0:
+                assert int(sparse["map"][r]) == i
+                got[r] = grows[i].double()
+                nu += 1
         bwd_err = float((got - dense[lo:lo + n_local]).abs().max())
         touched = (dense[lo:lo + n_local].abs().sum(1) > 0).sum().item()
         c = DistCollective(world)

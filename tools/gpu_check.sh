@@ -22,5 +22,14 @@ for step in "$@"; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- \
         python $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline > $OUT/prof_$TAG.log 2>&1
       rc=$?; echo "prof rc=$rc"; tail -3 $OUT/prof_$TAG.log; cd $R; [ $rc -eq 0 ] || exit $rc ;;
+    pmc)
+      cd /tmp && export TMPDIR=/tmp
+      for C in FETCH_SIZE WRITE_SIZE; do
+        timeout -k 10 600 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/pmc_${TAG}_$C -o run -- \
+          python $R/bench.py --steps 4 --warmup 2 --probe-steps 1 --no-graph --no-cpu-baseline > $OUT/pmc_${TAG}_$C.log 2>&1
+        rc=$?; echo "pmc $C rc=$rc"; [ $rc -eq 0 ] || exit $rc
+      done
+      cd $R ;;
   esac
 done
+# (appended) PMC traffic passes: FETCH_SIZE and WRITE_SIZE in separate runs (slot limits)
