@@ -29,7 +29,8 @@ SIGNATURES = {
     "fbn_last_error": (ctypes.c_char_p, []),
     "fbn_device_ok": (I, []),
     "fbn_gemm_workspace_size": (SZ, [I, I, I, I]),
-    "fbn_gemm": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, F, I, I, I, P, SZ, P]),
+    "fbn_gemm": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, F, I, I, I, P, P, SZ, P]),
+    "fbn_bn_tile_stats": (I, [P, I, I, P, P, P]),
     "fbn_fields_fwd": (I, [P, P, P, P, P, P, P, F, P, I, P, LL, P, P, P, P, P, I, P, P, P, I, I, P, P, P, P, P,
                            I, I, I, P]),
     "fbn_fields_bwd_partials_size": (I, [I, I, I]),

@@ -43,6 +43,7 @@ struct GemmArgs {
   float beta;
   int kchunk;   // K range per split (multiple of BK)
   float* ws;    // split-K slabs [split][M][N]
+  float* stats; // optional [ceil(M/BM)][N][2]: per-tile column (sum, M2 about the tile mean) of C
 };
 
 template <bool BF16> struct GemmTraits;
@@ -349,6 +350,56 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
         }
       }
     }
+  if (g.stats && !split) {
+    // BatchNorm fusion: exact two-pass (sum, M2) of this tile's column values from registers;
+    // the BN finalize merges tiles in f64 (Chan) -- no extra pass over C.
+    float* red = reinterpret_cast<float*>(&sA[0][0]);       // [2][BN] scratch (main loop is done)
+    const int rows = min(BM, g.M - m0);
+    float bvj[TN], mean[TN], ps[TN], sum0[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * WN + j * 32 + lr;
+      bvj[j] = (g.bias && n < g.N) ? g.bias[n] : 0.f;
+      mean[j] = 0.f;
+      sum0[j] = 0.f;
+    }
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int m = m0 + wm * WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+            const float v = acc[i][j][e] + bvj[j];
+            const float t = pass == 0 ? v : (v - mean[j]) * (v - mean[j]);
+            s += m < g.M ? t : 0.f;
+          }
+        s += __shfl_xor(s, 32, 64);
+        ps[j] = s;
+      }
+      if (lh == 0)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) red[wm * BN + wn * WN + j * 32 + lr] = ps[j];
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int c = wn * WN + j * 32 + lr;
+        const float tot = red[c] + red[BN + c];
+        if (pass == 0) {
+          sum0[j] = tot;
+          mean[j] = tot / (float)rows;
+        } else if (wm == 0 && lh == 0 && n0 + c < g.N) {
+          float* o = g.stats + ((size_t)(m0 / BM) * g.N + n0 + c) * 2;
+          o[0] = sum0[j];
+          o[1] = tot;
+        }
+      }
+      __syncthreads();
+    }
+  }
 }
 
 __global__ void gemm_splitk_reduce(GemmArgs g, int nsplit) {
@@ -362,6 +413,58 @@ __global__ void gemm_splitk_reduce(GemmArgs g, int nsplit) {
     float* cp = g.C + (size_t)m * g.ldc + remap(g.rC, n);
     if (g.beta != 0.f) s += g.beta * *cp;
     *cp = s;
+  }
+}
+
+// split-K reduce with the BatchNorm statistics epilogue: one workgroup per 64x64 tile of C;
+// thread (col = tid & 63, rows 16*(tid >> 6) .. +15) -> coalesced slab reads along n.  Sums the
+// K-slabs in the same order as gemm_splitk_reduce (so C is bit-identical with or without stats),
+// then (sum, M2 about the tile mean) of each column from registers.
+__global__ __launch_bounds__(256) void gemm_splitk_reduce_stats(GemmArgs g, int nsplit) {
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + c, m0 = blockIdx.y * 64;
+  const int rows = min(64, g.M - m0);
+  const size_t total = (size_t)g.M * g.N;
+  const bool nok = n < g.N;
+  const float bv = (nok && g.bias) ? g.bias[n] : 0.f;
+  const int nc = nok ? remap(g.rC, n) : 0;
+  float v[16];
+  float s = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + rg * 16 + r;
+    v[r] = 0.f;
+    if (nok && m < g.M) {
+      const size_t idx = (size_t)m * g.N + n;
+      float a = 0.f;
+      for (int z = 0; z < nsplit; ++z) a += g.ws[(size_t)z * total + idx];
+      a += bv;
+      float* cp = g.C + (size_t)m * g.ldc + nc;
+      if (g.beta != 0.f) a += g.beta * *cp;
+      *cp = a;
+      v[r] = a;
+      s += a;
+    }
+  }
+  red[rg][c] = s;
+  __syncthreads();
+  const float sum0 = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+  const float mean = rows > 0 ? sum0 / (float)rows : 0.f;
+  __syncthreads();
+  float q = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + rg * 16 + r;
+    const float t = v[r] - mean;
+    q += m < g.M ? t * t : 0.f;
+  }
+  red[rg][c] = q;
+  __syncthreads();
+  if (rg == 0 && nok) {
+    float* o = g.stats + ((size_t)blockIdx.y * g.N + n) * 2;
+    o[0] = sum0;
+    o[1] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
   }
 }
 
@@ -420,10 +523,12 @@ extern "C" size_t fbn_gemm_workspace_size(int M, int N, int K, int bf16) {
 }
 
 // a16 / b16: the A / B operand is bf16 in memory (requires bf16 = 1, ld % 8 == 0 and no rB remap)
+// stats: optional [ceil(M/64)][N][2] per-64-row-tile column (sum, M2) of C, from the MFMA epilogue (split == 1,
+//        64-row tiles) or the split-K reduce; C is bit-identical with or without stats
 extern "C" int fbn_gemm(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, int lda,
                         int ldb, int ldc, int transA, int transB, int rB_seg, int rB_off0, int rB_off1, int rC_seg,
-                        int rC_off0, int rC_off1, float beta, int bf16, int a16, int b16, float* ws, size_t ws_bytes,
-                        void* stream) {
+                        int rC_off0, int rC_off1, float beta, int bf16, int a16, int b16, float* stats, float* ws,
+                        size_t ws_bytes, void* stream) {
   if (M <= 0 || N <= 0) return FBN_OK;
   if (!A || !B || !C) { fbn_set_error("fbn_gemm: null operand"); return FBN_ERR_ARG; }
   // 16-B vector loads along the contiguous dimension of every operand
@@ -444,10 +549,13 @@ extern "C" int fbn_gemm(const void* A, const void* B, float* C, const float* bia
   g.beta = beta;
   const int bk = bf16 ? 64 : 32;
   GemmPlan p = plan_gemm(M, N, K, bk);
+  g.stats = stats;
   if (p.split > 1 && (!ws || ws_bytes < (size_t)p.split * M * N * sizeof(float))) p.split = 1;
   int per = fbn_cdiv(K, p.split);
   per = fbn_cdiv(per, bk) * bk;
   p.split = K > 0 ? fbn_cdiv(K, per) : 1;
+  // stats: 64-row tiles from the MFMA epilogue (split == 1) or from the split-K reduce
+  if (stats && p.split == 1) p.bm = 64;
   g.kchunk = K > 0 ? per : 0;
   g.ws = ws;
   hipStream_t st = (hipStream_t)stream;
@@ -459,7 +567,11 @@ extern "C" int fbn_gemm(const void* A, const void* B, float* C, const float* bia
     default: launch_types<true, true>(g, p, bf16, a16, b16, st); break;
   }
   FBN_CHECK_LAUNCH();
-  if (p.split > 1) {
+  if (p.split > 1 && stats) {
+    hipLaunchKernelGGL(gemm_splitk_reduce_stats, dim3(fbn_cdiv(N, 64), fbn_cdiv(M, 64)), dim3(256), 0, st, g,
+                       p.split);
+    FBN_CHECK_LAUNCH();
+  } else if (p.split > 1) {
     const size_t total = (size_t)M * N;
     int blocks = (int)((total + 255) / 256);
     if (blocks > 4096) blocks = 4096;

@@ -334,17 +334,24 @@ __global__ void outer_kernel(const float* g, const float* w, float* out, int B, 
     out[i] = g[i / C] * w[i % C];
 }
 
-__global__ void sum_kernel(const float* x, int n, float* out, float scale) {
-  __shared__ float red[256];
-  float s = 0.f;
-  for (int i = threadIdx.x; i < n; i += 256) s += x[i];
-  red[threadIdx.x] = s;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-    __syncthreads();
+// out = scale * sum(x): one 1024-thread block, 4 independent accumulators per thread, wave
+// shuffles + 16-entry LDS stage (fixed order: deterministic)
+__global__ void __launch_bounds__(1024) sum_kernel(const float* x, int n, float* out, float scale) {
+  __shared__ float red[16];
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int i = threadIdx.x;
+  for (; i + 3 * 1024 < n; i += 4 * 1024) {
+    s0 += x[i]; s1 += x[i + 1024]; s2 += x[i + 2048]; s3 += x[i + 3072];
   }
-  if (threadIdx.x == 0) out[0] = red[0] * scale;
+  for (; i < n; i += 1024) s0 += x[i];
+  float s = wave_sum((s0 + s1) + (s2 + s3));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float t = threadIdx.x < 16 ? red[threadIdx.x] : 0.f;
+    t = wave_sum(t);
+    if (threadIdx.x == 0) out[0] = t * scale;
+  }
 }
 
 // ------------------------------------------------------------------ C ABI
@@ -533,7 +540,7 @@ extern "C" int fbn_outer(const float* g, const float* w, float* out, int B, int 
 }
 
 extern "C" int fbn_sum(const float* x, int n, float* out, float scale, void* stream) {
-  hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, x, n, out, scale);
+  hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, x, n, out, scale);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -569,6 +576,40 @@ extern "C" int fbn_convert_bf16(const void* jobs, int n, void* stream) {
   ConvJobs J;
   for (int i = 0; i < 8; ++i) J.j[i] = ((const ConvJob*)jobs)[i < n ? i : 0];
   hipLaunchKernelGGL(convert_bf16_kernel, dim3(256, n), dim3(256), 0, (hipStream_t)stream, J);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+// ------------------------------------------------------------------ BN stats from GEMM tile partials
+// part[t][c] = (sum, M2 about the tile mean) over the rows of 64-row tile t (fbn_gemm stats).
+// mean_d == null: out[c] = sum_t S_t ;  else out[c] = sum_t (M2_t + n_t (S_t/n_t - mean)^2)
+// (Chan's parallel merge, f64; one wave per column, fixed order).
+__global__ void bn_tile_stats_kernel(const float* __restrict__ part, int T, int C, int M, int tile_rows,
+                                     const double* __restrict__ mean_d, double* __restrict__ out) {
+  const int c = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (c >= C) return;
+  double s = 0.0;
+  const double mu = mean_d ? mean_d[c] : 0.0;
+  for (int t = lane; t < T; t += 64) {
+    const float S = part[((size_t)t * C + c) * 2], M2 = part[((size_t)t * C + c) * 2 + 1];
+    if (!mean_d) {
+      s += (double)S;
+    } else {
+      const int nt = min(tile_rows, M - t * tile_rows);
+      const double dm = (double)S / nt - mu;
+      s += (double)M2 + nt * dm * dm;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) out[c] = s;
+}
+
+extern "C" int fbn_bn_tile_stats(const float* part, int M, int C, const double* mean_d, double* out_d, void* stream) {
+  const int T = (M + 63) / 64;
+  hipLaunchKernelGGL(bn_tile_stats_kernel, dim3(fbn_cdiv(C, 4)), dim3(256), 0, (hipStream_t)stream, part, T, C, M, 64,
+                     mean_d, out_d);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

@@ -43,13 +43,14 @@ def _ws(nbytes: int, device) -> Optional[torch.Tensor]:
 
 
 def gemm(A, B, C, M, N, K, lda, ldb, ldc, transA, transB, bias=None, rB=NO_REMAP, rC=NO_REMAP, beta=0.0,
-         bf16=False, stream=None):
+         bf16=False, stream=None, stats=None):
     """C = op(A) op(B) (+bias, +beta C).  A / B may be fp32 or bf16 (torch.bfloat16) tensors."""
     nbytes = _lib.lib().fbn_gemm_workspace_size(M, N, K, int(bf16))
     ws = _ws(nbytes, C.device)
     a16, b16 = int(A.dtype == torch.bfloat16), int(B.dtype == torch.bfloat16)
     call("fbn_gemm", ptr(A), ptr(B), ptr(C), ptr(bias), M, N, K, lda, ldb, ldc, int(transA), int(transB),
-         rB[0], rB[1], rB[2], rC[0], rC[1], rC[2], float(beta), int(bf16 or a16 or b16), a16, b16, ptr(ws), nbytes,
+         rB[0], rB[1], rB[2], rC[0], rC[1], rC[2], float(beta), int(bf16 or a16 or b16), a16, b16, ptr(stats),
+         ptr(ws), nbytes,
          stream if stream is not None else _lib.stream_handle())
 
 
@@ -114,17 +115,25 @@ class Collective:
 NO_COLLECTIVE = Collective()
 
 
-def bn_train_stats(h, B, C, mean, invstd, run_mean, run_var, ntot, coll: Collective, stream):
-    """Training-mode BatchNorm statistics over the GLOBAL batch (SyncBN when coll.world > 1)."""
+def bn_train_stats(h, B, C, mean, invstd, run_mean, run_var, ntot, coll: Collective, stream, tiles=None):
+    """Training-mode BatchNorm statistics over the GLOBAL batch (SyncBN when coll.world > 1).
+    tiles: per-64-row-tile (sum, M2) partials written by the producing GEMM (no pass over h)."""
     dev = h.device
-    ws = _ws(_lib.lib().fbn_bn_workspace_size(B, C), dev)
     s = torch.empty(C, dtype=torch.float64, device=dev)
     mean_d = torch.empty(C, dtype=torch.float64, device=dev)
-    call("fbn_bn_stats_pass", ptr(h), B, C, None, ptr(s), ptr(ws), stream)
-    coll.allreduce_(s)
-    call("fbn_bn_mean", ptr(s), float(ntot), C, ptr(mean_d), stream)
-    call("fbn_bn_stats_pass", ptr(h), B, C, ptr(mean_d), ptr(s), ptr(ws), stream)
-    coll.allreduce_(s)
+    if tiles is not None:
+        call("fbn_bn_tile_stats", ptr(tiles), B, C, None, ptr(s), stream)
+        coll.allreduce_(s)
+        call("fbn_bn_mean", ptr(s), float(ntot), C, ptr(mean_d), stream)
+        call("fbn_bn_tile_stats", ptr(tiles), B, C, ptr(mean_d), ptr(s), stream)
+        coll.allreduce_(s)
+    else:
+        ws = _ws(_lib.lib().fbn_bn_workspace_size(B, C), dev)
+        call("fbn_bn_stats_pass", ptr(h), B, C, None, ptr(s), ptr(ws), stream)
+        coll.allreduce_(s)
+        call("fbn_bn_mean", ptr(s), float(ntot), C, ptr(mean_d), stream)
+        call("fbn_bn_stats_pass", ptr(h), B, C, ptr(mean_d), ptr(s), ptr(ws), stream)
+        coll.allreduce_(s)
     call("fbn_bn_finalize", ptr(s), ptr(mean_d), float(ntot), C, ptr(mean), ptr(invstd), ptr(run_mean),
          ptr(run_var), BN_MOMENTUM, BN_EPS, 1 if run_mean is not None else 0, stream)
 
@@ -233,11 +242,16 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     call("fbn_pairs_fwd", ptr(Vc), ptr(U), ptr(c), B, d, KC, int(cfg.bilinear_each), int(bf), st)
     # MLP layer 1
     h1pre = buf("h1pre", (B, H1))
+    nt = (B + 63) // 64
+    fuse = cfg.training
+    t1 = buf("tiles1", (nt, H1, 2)) if fuse else None      # fused BN statistics (GEMM epilogue)
+    t2 = buf("tiles2", (nt, H2, 2)) if fuse else None
     if bf:
-        gemm(c, w16["Wa"], h1pre, B, H1, KC, KC, KC, H1, False, True, bias=p["mlp.0.bias"], bf16=True, stream=st)
+        gemm(c, w16["Wa"], h1pre, B, H1, KC, KC, KC, H1, False, True, bias=p["mlp.0.bias"], bf16=True, stream=st,
+             stats=t1)
     else:
         gemm(c, p["mlp.0.weight"], h1pre, B, H1, KC, KC, 21 * d, H1, False, True, bias=p["mlp.0.bias"],
-             rB=wa_remap(d), stream=st)
+             rB=wa_remap(d), stream=st, stats=t1)
     mean1, inv1 = buf("mean1", (H1,)), buf("inv1", (H1,))
     mean2, inv2 = buf("mean2", (H2,)), buf("inv2", (H2,))
     h1 = buf("h1", (B, H1))
@@ -250,18 +264,22 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     mi1 = masks_in.get("m1") if masks_in else None
     mi2 = masks_in.get("m2") if masks_in else None
     if cfg.training:
-        bn_train_stats(h1pre, B, H1, mean1, inv1, p["mlp.1.running_mean"], p["mlp.1.running_var"], ntot, coll, st)
+        bn_train_stats(h1pre, B, H1, mean1, inv1, p["mlp.1.running_mean"], p["mlp.1.running_var"], ntot, coll, st,
+                       tiles=t1)
     else:
         call("fbn_bn_eval_params", ptr(p["mlp.1.running_mean"]), ptr(p["mlp.1.running_var"]), ptr(mean1), ptr(inv1),
              H1, BN_EPS, st)
     call("fbn_bn_act_fwd", ptr(h1pre), ptr(h1), B, H1, ptr(mean1), ptr(inv1), ptr(p["mlp.1.weight"]),
          ptr(p["mlp.1.bias"]), float(p_drop), ptr(rng), 1, ptr(m1), ptr(mi1), ptr(h1_16), st)
     if bf:
-        gemm(h1_16, w16["Wb"], h2pre, B, H2, H1, H1, H1, H2, False, True, bias=p["mlp.4.bias"], bf16=True, stream=st)
+        gemm(h1_16, w16["Wb"], h2pre, B, H2, H1, H1, H1, H2, False, True, bias=p["mlp.4.bias"], bf16=True, stream=st,
+             stats=t2)
     else:
-        gemm(h1, p["mlp.4.weight"], h2pre, B, H2, H1, H1, H1, H2, False, True, bias=p["mlp.4.bias"], stream=st)
+        gemm(h1, p["mlp.4.weight"], h2pre, B, H2, H1, H1, H1, H2, False, True, bias=p["mlp.4.bias"], stream=st,
+             stats=t2)
     if cfg.training:
-        bn_train_stats(h2pre, B, H2, mean2, inv2, p["mlp.5.running_mean"], p["mlp.5.running_var"], ntot, coll, st)
+        bn_train_stats(h2pre, B, H2, mean2, inv2, p["mlp.5.running_mean"], p["mlp.5.running_var"], ntot, coll, st,
+                       tiles=t2)
     else:
         call("fbn_bn_eval_params", ptr(p["mlp.5.running_mean"]), ptr(p["mlp.5.running_var"]), ptr(mean2), ptr(inv2),
              H2, BN_EPS, st)

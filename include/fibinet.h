@@ -45,10 +45,14 @@ int fbn_device_ok(void); /* 1 if the current HIP device is gfx950 */
  *   MLP Linear x3             src/model_fibinet.py:126,130,134,197
  * and all of their autograd backward GEMMs.  Split-K slabs need ws >= fbn_gemm_workspace_size. */
 size_t fbn_gemm_workspace_size(int M, int N, int K, int bf16);
-/* a16 / b16: operand A / B is bf16 in memory (bf16 = 1, ld % 8 == 0, no rB remap); otherwise fp32. */
+/* a16 / b16: operand A / B is bf16 in memory (bf16 = 1, ld % 8 == 0, no rB remap); otherwise fp32.
+ * stats (optional): [ceil(M/64)][N][2] per-64-row-tile column (sum, M2) of C for the fused
+ * BatchNorm statistics, from the MFMA epilogue (no split-K: 64-row tiles) or the split-K reduce;
+ * C is bit-identical with or without it. */
 int fbn_gemm(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, int lda, int ldb,
              int ldc, int transA, int transB, int rB_seg, int rB_off0, int rB_off1, int rC_seg, int rC_off0,
-             int rC_off1, float beta, int bf16, int a16, int b16, float* ws, size_t ws_bytes, void* stream);
+             int rC_off1, float beta, int bf16, int a16, int b16, float* stats, float* ws, size_t ws_bytes,
+             void* stream);
 
 /* ---------------------------------------------------------------- K1 + K4: fields + SENET forward
  * Replaces: nn.Embedding lookups (src/model_fibinet.py:155,156,159,167), masked history mean
@@ -99,6 +103,9 @@ int fbn_bn_finalize(const double* m2_d, const double* mean_d, double ntot, int C
                     float* run_mean, float* run_var, float momentum, float eps, int update_running, void* stream);
 int fbn_bn_stats(const float* X, int B, int C, float* mean, float* invstd, float* run_mean, float* run_var,
                  float momentum, float eps, int update_running, void* ws, void* stream);
+/* BN statistics from fbn_gemm tile partials: mean_d == NULL -> out = column sums; else
+ * out = column sums of squared deviations about mean_d (Chan merge, f64). */
+int fbn_bn_tile_stats(const float* part, int M, int C, const double* mean_d, double* out_d, void* stream);
 int fbn_bn_eval_params(const float* run_mean, const float* run_var, float* mean, float* invstd, int C, float eps,
                        void* stream);
 int fbn_bn_act_fwd(const float* X, float* Y, int B, int C, const float* mean, const float* invstd, const float* g,
