@@ -31,6 +31,12 @@ SIGNATURES = {
     "fbn_gemm_workspace_size": (SZ, [I, I, I, I]),
     "fbn_gemm": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, F, I, I, I, P, P, SZ, P]),
     "fbn_bn_tile_stats": (I, [P, I, I, P, P, P]),
+    "fbn_bn_tile_finalize": (I, [P, I, I, D, P, P, P, P, F, F, I, P]),
+    "fbn_bn_colpart_size": (SZ, [I, I]),
+    "fbn_row_chunks": (I, [I]),
+    "fbn_bn_bwd_fused": (I, [P, P, P, P, F, P, P, P, P, I, I, D, P, P, P, P, P, P, P, P]),
+    "fbn_colsum_partial": (I, [P, I, I, I, P, P]),
+    "fbn_sum_jobs": (I, [P, I, P]),
     "fbn_fields_fwd": (I, [P, P, P, P, P, P, P, F, P, I, P, LL, P, P, P, P, P, I, P, P, P, I, I, P, P, P, P, P,
                            I, I, I, P]),
     "fbn_fields_bwd_partials_size": (I, [I, I, I]),
@@ -63,7 +69,7 @@ SIGNATURES = {
     "fbn_adam_table": (I, [P, P, P, LL, I, P, P, P, P, I, P, P, P, F, F, F, I, P]),
     "fbn_adam_touched": (I, [P, P, P, I, P, P, P, P, I, I, P, P, P, F, F, F, P]),
     "fbn_claim_rows": (I, [P, P, I, I, LL, P, P, P]),
-    "fbn_step_end": (I, [P, P, P, P]),
+    "fbn_step_end": (I, [P, P, P, P, P, P]),
     "fbn_route": (I, [P, P, I, I, LL, LL, I, P, P, P, P, P, P, P]),
     "fbn_owner_gather": (I, [P, I, P, P, P, P, I, I, P]),
 }

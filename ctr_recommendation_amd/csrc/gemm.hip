@@ -27,6 +27,8 @@
 // Split-K (gridDim.z > 1) writes f32 partial slabs that gemm_splitk_reduce sums in slab
 // order (deterministic).
 #include "common.h"
+#include <cstdlib>
+#include <cstdio>
 
 struct Remap {
   int seg, off0, off1;
@@ -229,6 +231,87 @@ template <int ROWS, int BK, bool KC, bool MAP> struct OpLoader<ROWS, BK, KC, MAP
   }
 };
 
+// Shared epilogue: bias / beta / remapped C stores or split-K slabs, and the optional fused
+// BatchNorm statistics.  red: LDS scratch of >= 2*BN floats, free (all waves past the main loop).
+template <int BM, int BN, int TM, int TN>
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[TM][TN], int m0, int n0, int wm,
+                                              int wn, int lr, int lh, float* red) {
+  constexpr int WM = BM / 2, WN = BN / 2;
+  // C/D map of the 32x32 MFMA tile: col = lane&31, row = (e&3) + 8*(e>>2) + 4*(lane>>5)
+  const bool split = gridDim.z > 1;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * WN + j * 32 + lr;
+      if (n >= g.N) continue;
+      const float bv = (!split && g.bias) ? g.bias[n] : 0.f;
+      const int nc = remap(g.rC, n);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + wm * WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+        if (m >= g.M) continue;
+        if (split) {
+          g.ws[((size_t)blockIdx.z * g.M + m) * g.N + n] = acc[i][j][e];
+        } else {
+          float* cp = g.C + (size_t)m * g.ldc + nc;
+          float v = acc[i][j][e] + bv;
+          if (g.beta != 0.f) v += g.beta * *cp;
+          *cp = v;
+        }
+      }
+    }
+  if (g.stats && !split) {
+    // BatchNorm fusion: exact two-pass (sum, M2) of this tile's column values from registers;
+    // the BN finalize merges tiles in f64 (Chan) -- no extra pass over C.
+    const int rows = min(BM, g.M - m0);
+    float bvj[TN], mean[TN], ps[TN], sum0[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * WN + j * 32 + lr;
+      bvj[j] = (g.bias && n < g.N) ? g.bias[n] : 0.f;
+      mean[j] = 0.f;
+      sum0[j] = 0.f;
+    }
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int m = m0 + wm * WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+            const float v = acc[i][j][e] + bvj[j];
+            const float t = pass == 0 ? v : (v - mean[j]) * (v - mean[j]);
+            s += m < g.M ? t : 0.f;
+          }
+        s += __shfl_xor(s, 32, 64);
+        ps[j] = s;
+      }
+      if (lh == 0)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) red[wm * BN + wn * WN + j * 32 + lr] = ps[j];
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int c = wn * WN + j * 32 + lr;
+        const float tot = red[c] + red[BN + c];
+        if (pass == 0) {
+          sum0[j] = tot;
+          mean[j] = tot / (float)rows;
+        } else if (wm == 0 && lh == 0 && n0 + c < g.N) {
+          float* o = g.stats + ((size_t)(m0 / BM) * g.N + n0 + c) * 2;
+          o[0] = sum0[j];
+          o[1] = tot;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
 template <int BM, int BN, bool TA, bool TB, bool BF16, bool A16, bool B16>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int remap_xcd) {
   typedef GemmTraits<BF16> Tr;
@@ -326,80 +409,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
     __syncthreads();
   }
 
-  // epilogue: C/D map of the 32x32 MFMA tile: col = lane&31, row = (e&3) + 8*(e>>2) + 4*(lane>>5)
-  const bool split = gridDim.z > 1;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * WN + j * 32 + lr;
-      if (n >= g.N) continue;
-      const float bv = (!split && g.bias) ? g.bias[n] : 0.f;
-      const int nc = remap(g.rC, n);
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int m = m0 + wm * WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
-        if (m >= g.M) continue;
-        if (split) {
-          g.ws[((size_t)blockIdx.z * g.M + m) * g.N + n] = acc[i][j][e];
-        } else {
-          float* cp = g.C + (size_t)m * g.ldc + nc;
-          float v = acc[i][j][e] + bv;
-          if (g.beta != 0.f) v += g.beta * *cp;
-          *cp = v;
-        }
-      }
-    }
-  if (g.stats && !split) {
-    // BatchNorm fusion: exact two-pass (sum, M2) of this tile's column values from registers;
-    // the BN finalize merges tiles in f64 (Chan) -- no extra pass over C.
-    float* red = reinterpret_cast<float*>(&sA[0][0]);       // [2][BN] scratch (main loop is done)
-    const int rows = min(BM, g.M - m0);
-    float bvj[TN], mean[TN], ps[TN], sum0[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * WN + j * 32 + lr;
-      bvj[j] = (g.bias && n < g.N) ? g.bias[n] : 0.f;
-      mean[j] = 0.f;
-      sum0[j] = 0.f;
-    }
-#pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        float s = 0.f;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const int m = m0 + wm * WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
-            const float v = acc[i][j][e] + bvj[j];
-            const float t = pass == 0 ? v : (v - mean[j]) * (v - mean[j]);
-            s += m < g.M ? t : 0.f;
-          }
-        s += __shfl_xor(s, 32, 64);
-        ps[j] = s;
-      }
-      if (lh == 0)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) red[wm * BN + wn * WN + j * 32 + lr] = ps[j];
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int c = wn * WN + j * 32 + lr;
-        const float tot = red[c] + red[BN + c];
-        if (pass == 0) {
-          sum0[j] = tot;
-          mean[j] = tot / (float)rows;
-        } else if (wm == 0 && lh == 0 && n0 + c < g.N) {
-          float* o = g.stats + ((size_t)(m0 / BM) * g.N + n0 + c) * 2;
-          o[0] = sum0[j];
-          o[1] = tot;
-        }
-      }
-      __syncthreads();
-    }
-  }
+  gemm_epilogue<BM, BN>(g, acc, m0, n0, wm, wn, lr, lh, reinterpret_cast<float*>(&sA[0][0]));
 }
 
 __global__ void gemm_splitk_reduce(GemmArgs g, int nsplit) {
@@ -414,6 +424,143 @@ __global__ void gemm_splitk_reduce(GemmArgs g, int nsplit) {
     if (g.beta != 0.f) s += g.beta * *cp;
     *cp = s;
   }
+}
+
+// ------------------------------------------------------------------ bf16 LDS-DMA kernel
+// Both operands bf16 in memory, K % 64 == 0 per split, no B remap.  Each operand is either
+//   KC (k-contiguous: A[m*lda+k] / B[n*ldb+k]; the forward and dgrad GEMMs), or
+//   KM (k-major:      A[k*lda+m] / B[k*ldb+n]; the wgrad GEMMs, batch = k).
+// Staging: global_load_lds_dwordx4 straight into LDS (no VGPR round trip, no ds_write); one
+// DMA wave-instruction writes 1 KiB contiguously (lane L -> bytes 16L..16L+15), so images are
+// unpadded and bank conflicts are removed by XOR-permuting 16-B chunks: the permutation is
+// applied to each lane's SOURCE address and undone on the read (the same involution).
+//   KC image [rows][64 k], 128-B rows; chunk c of row r in slot c ^ ((r >> 1) & 7).  MFMA
+//      fragments by ds_read_b128 (16 lanes = 16 consecutive rows: all 16 bank quads).
+//   KM image [64 k][ROWS], rows of 2*ROWS bytes; chunk c of row k in slot c ^ f(k) with
+//      f = 4*((k>>1)&1) (128-B rows) or 4*(k&3) (256-B rows).  Fragments by two
+//      ds_read_b64_tr_b16 (each 16-lane group reads 4 k-rows x 16 columns and receives them
+//      column-major = the MFMA lane layout); a 32-lane half then covers 16 bank quads.
+// One barrier per K-step: at the top of step t every wave has finished reading stage t-1, so
+// the DMA of stage t+1 into that buffer is issued right after the barrier and lands while the
+// MFMAs of stage t run.
+typedef __attribute__((address_space(1))) void g_void;
+typedef __attribute__((address_space(3))) void l_void;
+typedef short v4s __attribute__((ext_vector_type(4)));
+
+template <int ROWS>
+__device__ __forceinline__ int km_off(int k, int m) {   // byte offset of (k, m) in a KM image
+  constexpr int RB = ROWS * 2;
+  const int f = RB == 128 ? (((k >> 1) & 1) << 2) : ((k & 3) << 2);
+  return k * RB + ((((m >> 3) ^ f)) << 4) + (m & 7) * 2;
+}
+
+// MFMA 32x32x16 fragment (lane l: row l&31, k = 8*(l>>5) + j) of a 32-row slab starting at
+// row r0, k-step s, from a KC or KM image.
+template <int ROWS, bool KM>
+__device__ __forceinline__ bf16x8 frag(const char* img, int r0, int s, int lane) {
+  if constexpr (!KM) {
+    const int r = r0 + (lane & 31);
+    const int co = ((2 * s + (lane >> 5)) ^ ((r >> 1) & 7)) << 4;
+    return *reinterpret_cast<const bf16x8*>(img + r * 128 + co);
+  } else {
+    const int i16 = lane & 15, G = lane >> 4;
+    const int m = r0 + 16 * (G & 1) + 4 * (i16 & 3);
+    const int k = 16 * s + 8 * (G >> 1) + (i16 >> 2);
+    const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(img + km_off<ROWS>(k, m)));
+    const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(img + km_off<ROWS>(k + 4, m)));
+    return (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  }
+}
+
+template <int BM, int BN, bool AKM, bool BKM>
+__global__ void __launch_bounds__(256) gemm_dma16_kernel(GemmArgs g, int tiles_n, int remap_xcd) {
+  constexpr int BK = 64;
+  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
+  constexpr int AB = BM * BK * 2, STAGE = (BM + BN) * BK * 2;   // A image bytes, stage bytes
+  constexpr int GPW = (BM + BN) / 8 / 4;                          // 1-KiB DMA groups per wave per stage
+  static_assert(((BM + BN) / 8) % 4 == 0 && BM % 16 == 0, "tile / wave mismatch");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  int bid = blockIdx.x;
+  const int nb = gridDim.x;
+  if (remap_xcd) bid = (bid % 8) * (nb / 8) + bid / 8;
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int n0 = tn * BN, m0 = tm * BM;
+  const int kbeg = blockIdx.z * g.kchunk;
+  const int kend = min(g.K, kbeg + g.kchunk);
+  const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int lr = lane & 31, lh = lane >> 5;
+
+  // this lane's source for each of its wave's DMA groups, and the per-stage source advance
+  // (rows / columns past M or N are clamped to valid memory: their products land only in C
+  // entries that are not stored)
+  const short* src[GPW];
+  long long adv[GPW];
+#pragma unroll
+  for (int j = 0; j < GPW; ++j) {
+    const int grp = wave * GPW + j;
+    const bool isA = grp < BM / 8;
+    const int off = (isA ? grp : grp - BM / 8) * 1024 + lane * 16;   // byte offset inside the operand image
+    const short* P = reinterpret_cast<const short*>(isA ? g.A : g.B);
+    const int ld = isA ? g.lda : g.ldb, lim = isA ? g.M : g.N, base = isA ? m0 : n0;
+    const bool km = isA ? AKM : BKM;
+    const int rows = isA ? BM : BN;
+    if (!km) {
+      const int r = off >> 7, slot = (off >> 4) & 7;
+      const int row = min(base + r, lim - 1);
+      src[j] = P + (size_t)row * ld + kbeg + ((slot ^ ((r >> 1) & 7)) << 3);
+      adv[j] = BK;
+    } else {
+      const int RB = rows * 2;
+      const int k = off / RB, slot = (off % RB) >> 4;
+      const int f = RB == 128 ? (((k >> 1) & 1) << 2) : ((k & 3) << 2);
+      int col = base + ((slot ^ f) << 3);
+      if (col + 8 > lim) col = 0;
+      src[j] = P + (size_t)(kbeg + k) * ld + col;
+      adv[j] = (long long)BK * ld;
+    }
+  }
+  auto issue = [&](int t, int buf) {
+#pragma unroll
+    for (int j = 0; j < GPW; ++j)
+      __builtin_amdgcn_global_load_lds((g_void*)(src[j] + t * adv[j]), (l_void*)(smem + buf * STAGE + (wave * GPW + j) * 1024),
+                                       16, 0, 0);
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  if (nk > 0) issue(0, 0);
+  for (int t = 0; t < nk; ++t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 1 < nk) issue(t + 1, (t + 1) & 1);
+    const char* SA = smem + (t & 1) * STAGE;
+    const char* SB = SA + AB;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = frag<BM, AKM>(SA, wm * WM + i * 32, s, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = frag<BN, BKM>(SB, wn * WN + j * 32, s, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();   // the stats epilogue reuses the staging LDS
+  gemm_epilogue<BM, BN>(g, acc, m0, n0, wm, wn, lr, lh, reinterpret_cast<float*>(smem));
 }
 
 // split-K reduce with the BatchNorm statistics epilogue: one workgroup per 64x64 tile of C;
@@ -491,6 +638,19 @@ static GemmPlan plan_gemm(int M, int N, int K, int bk) {
   return p;
 }
 
+// LDS-DMA kernel plan (tools/gemm_sweep.py on the C3 shapes): 64x64 tiles whenever they give
+// >= 512 workgroups (no split: F3, F4, dh1, dc, U); small outputs (the wgrad GEMMs, K = batch)
+// split K up to ~512 (128x64 tiles, M, N >= 512) or ~256 (64x64) workgroups, >= 4 K-steps each.
+static GemmPlan plan_dma16(int M, int N, int K) {
+  const long long t64 = (long long)fbn_cdiv(M, 64) * fbn_cdiv(N, 64);
+  if (t64 >= 512) return {64, 64, 1};
+  GemmPlan p = (M >= 512 && N >= 512) ? GemmPlan{128, 64, 1} : GemmPlan{64, 64, 1};
+  const long long tiles = (long long)fbn_cdiv(M, p.bm) * fbn_cdiv(N, p.bn);
+  const long long target = p.bm == 128 ? 512 : 256;
+  while (p.split < 16 && tiles * p.split * 2 <= target && K / (p.split * 2) >= 256) p.split *= 2;
+  return p;
+}
+
 template <int BM, int BN, bool TA, bool TB, bool BF16, bool A16, bool B16>
 static void launch_tile(const GemmArgs& g, int nsplit, hipStream_t st) {
   const int tn = fbn_cdiv(g.N, BN), tm = fbn_cdiv(g.M, BM);
@@ -498,6 +658,22 @@ static void launch_tile(const GemmArgs& g, int nsplit, hipStream_t st) {
   dim3 grid(nb, 1, nsplit);
   hipLaunchKernelGGL((gemm_kernel<BM, BN, TA, TB, BF16, A16, B16>), grid, dim3(256), 0, st, g, tn,
                      (nb % 8 == 0) ? 1 : 0);
+}
+
+template <int BM, int BN, bool AKM, bool BKM>
+static void launch_dma16(const GemmArgs& g, int nsplit, hipStream_t st) {
+  const int tn = fbn_cdiv(g.N, BN), tm = fbn_cdiv(g.M, BM);
+  const int nb = tn * tm;
+  hipLaunchKernelGGL((gemm_dma16_kernel<BM, BN, AKM, BKM>), dim3(nb, 1, nsplit), dim3(256), 0, st, g, tn,
+                     (nb % 8 == 0) ? 1 : 0);
+}
+
+template <bool AKM, bool BKM>
+static void launch_dma16_sel(const GemmArgs& g, const GemmPlan& p, hipStream_t st) {
+  if (p.bm == 128 && p.bn == 128) launch_dma16<128, 128, AKM, BKM>(g, p.split, st);
+  else if (p.bm == 128) launch_dma16<128, 64, AKM, BKM>(g, p.split, st);
+  else if (p.bn == 128) launch_dma16<64, 128, AKM, BKM>(g, p.split, st);
+  else launch_dma16<64, 64, AKM, BKM>(g, p.split, st);
 }
 
 template <bool TA, bool TB, bool BF16, bool A16, bool B16>
@@ -517,8 +693,13 @@ static void launch_types(const GemmArgs& g, const GemmPlan& p, int bf16, int a16
   else launch_sel<TA, TB, true, false, false>(g, p, st);
 }
 
+// upper bound over both kernels' plans (the caller does not say whether the DMA path applies)
 extern "C" size_t fbn_gemm_workspace_size(int M, int N, int K, int bf16) {
-  const GemmPlan p = plan_gemm(M, N, K, bf16 ? 64 : 32);
+  GemmPlan p = plan_gemm(M, N, K, bf16 ? 64 : 32);
+  if (bf16) {
+    const GemmPlan q = plan_dma16(M, N, K);
+    if (q.split > p.split) p = q;
+  }
   return p.split > 1 ? (size_t)p.split * M * N * sizeof(float) : 0;
 }
 
@@ -548,7 +729,15 @@ extern "C" int fbn_gemm(const void* A, const void* B, float* C, const float* bia
   g.rC = {rC_seg, rC_off0, rC_off1};
   g.beta = beta;
   const int bk = bf16 ? 64 : 32;
-  GemmPlan p = plan_gemm(M, N, K, bk);
+  // LDS-DMA path: bf16 operands, K % 64 == 0, 16-B rows; k-major operands need their
+  // M / N extent in whole 8-element chunks
+  const bool dma16 = bf16 && a16 && b16 && rB_seg == 0x7fffffff && K % 64 == 0 && !(lda & 7) && !(ldb & 7) &&
+                     (!transA ? true : !(M & 7)) && (transB ? true : !(N & 7)) && !getenv("FBN_GEMM_NO_DMA16");
+  GemmPlan p = dma16 ? plan_dma16(M, N, K) : plan_gemm(M, N, K, bk);
+  if (const char* f = getenv("FBN_GEMM_FORCE")) {      // tuning sweeps only: "bm,bn,split"
+    int a = 0, b = 0, c = 0;
+    if (sscanf(f, "%d,%d,%d", &a, &b, &c) == 3) p = {a, b, c};
+  }
   g.stats = stats;
   if (p.split > 1 && (!ws || ws_bytes < (size_t)p.split * M * N * sizeof(float))) p.split = 1;
   int per = fbn_cdiv(K, p.split);
@@ -560,7 +749,14 @@ extern "C" int fbn_gemm(const void* A, const void* B, float* C, const float* bia
   g.ws = ws;
   hipStream_t st = (hipStream_t)stream;
   const int key = (transA ? 2 : 0) | (transB ? 1 : 0);
-  switch (key) {
+  if (dma16) {
+    switch (key) {
+      case 0: launch_dma16_sel<false, true>(g, p, st); break;
+      case 1: launch_dma16_sel<false, false>(g, p, st); break;
+      case 2: launch_dma16_sel<true, true>(g, p, st); break;
+      default: launch_dma16_sel<true, false>(g, p, st); break;
+    }
+  } else switch (key) {
     case 0: launch_types<false, false>(g, p, bf16, a16, b16, st); break;
     case 1: launch_types<false, true>(g, p, bf16, a16, b16, st); break;
     case 2: launch_types<true, false>(g, p, bf16, a16, b16, st); break;

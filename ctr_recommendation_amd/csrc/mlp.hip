@@ -287,6 +287,157 @@ __global__ void colsum_final_kernel(const float* part, int nchunk, int C, float*
   if (lane == 0) out[c] = beta != 0.f ? out[c] * beta + s : s;
 }
 
+// ------------------------------------------------------------------ single-process BN fusions
+// Forward statistics from the GEMM's per-64-row-tile (sum, M2) partials in ONE launch: per
+// column one wave sums the tile sums (-> mean), then Chan's merge of the tile M2s about that
+// mean, then the finalize.  Same f64 operations in the same order as fbn_bn_tile_stats x2 +
+// fbn_bn_mean + fbn_bn_finalize (the multi-rank path, which all-reduces in between).
+__global__ void bn_tile_finalize_kernel(const float* __restrict__ part, int T, int C, int M, int tile_rows,
+                                        double ntot, float* mean, float* invstd, float* run_mean, float* run_var,
+                                        float momentum, float eps, int update_running) {
+  const int c = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (c >= C) return;
+  double s = 0.0;
+  for (int t = lane; t < T; t += 64) s += (double)part[((size_t)t * C + c) * 2];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  const double mu = s / ntot;
+  double q = 0.0;
+  for (int t = lane; t < T; t += 64) {
+    const float S = part[((size_t)t * C + c) * 2], M2 = part[((size_t)t * C + c) * 2 + 1];
+    const int nt = min(tile_rows, M - t * tile_rows);
+    const double dm = (double)S / nt - mu;
+    q += (double)M2 + nt * dm * dm;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+  if (lane == 0) {
+    const float var_b = (float)(q / ntot);
+    mean[c] = (float)mu;
+    invstd[c] = 1.f / sqrtf(var_b + eps);
+    if (update_running) {
+      const float unb = ntot > 1.0 ? (float)(q / (ntot - 1.0)) : var_b;
+      run_mean[c] = momentum * (float)mu + (1.f - momentum) * run_mean[c];
+      run_var[c] = momentum * unb + (1.f - momentum) * run_var[c];
+    }
+  }
+}
+
+// Backward: chunk reduce of the three partial sums + the finalize of bn_bwd_finalize_kernel,
+// one wave per column (chunk_reduce_kernel's order).
+__global__ void bn_bwd_reduce_finalize_kernel(const double* __restrict__ part, int nchunk, int C, double ntot,
+                                              const float* __restrict__ invstd, float* coef, float* dgamma,
+                                              float* dbeta, float* dw) {
+  const int c = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (c >= C) return;
+  double r[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    for (int k = lane; k < nchunk; k += 64) r[q] += part[(size_t)k * 3 * C + q * C + c];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) r[q] += __shfl_xor(r[q], o, 64);
+  }
+  if (lane == 0) {
+    const float is = invstd[c];
+    const float sdy = (float)r[0], dotp = (float)r[1];
+    coef[c] = sdy / (float)ntot;
+    coef[C + c] = dotp * is * is / (float)ntot;
+    if (dgamma) dgamma[c] = dotp * is;
+    if (dbeta) dbeta[c] = sdy;
+    if (dw) dw[c] = (float)r[2];
+  }
+}
+
+// Vectorised apply (4 columns per thread, 256 columns x 4 row lanes per block, one row chunk
+// per blockIdx.y) with the column partial sums of dX (the pre-BN Linear's bias gradient) in
+// the same pass: colpart[chunk][c] (null: skipped).
+__global__ void __launch_bounds__(256) bn_bwd_apply4_kernel(BnBwdSrc s, const float* __restrict__ Xpre,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ invstd,
+                                                            const float* __restrict__ g,
+                                                            const float* __restrict__ coef, float* __restrict__ dX,
+                                                            short* __restrict__ dX16, int B, int C,
+                                                            int rows_per_chunk, float* __restrict__ colpart) {
+  __shared__ f32x4 red[4][64];
+  const int q = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 256 + q * 4;
+  const int r0 = blockIdx.y * rows_per_chunk, r1 = min(B, r0 + rows_per_chunk);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    const f32x4 mu = *reinterpret_cast<const f32x4*>(mean + c);
+    const f32x4 is = *reinterpret_cast<const f32x4*>(invstd + c);
+    const f32x4 gg = *reinterpret_cast<const f32x4*>(g + c);
+    const f32x4 c0 = *reinterpret_cast<const f32x4*>(coef + c);
+    const f32x4 c1 = *reinterpret_cast<const f32x4*>(coef + C + c);
+    const f32x4 ww = s.G ? (f32x4){0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(s.w + c);
+    for (int r = r0 + rl; r < r1; r += 4) {
+      const size_t i = (size_t)r * C + c;
+      const f32x4 h = *reinterpret_cast<const f32x4*>(s.hact + i);
+      const f32x4 x = *reinterpret_cast<const f32x4*>(Xpre + i);
+      f32x4 d;
+      if (s.G) d = *reinterpret_cast<const f32x4*>(s.G + i);
+      else { const float gv = s.gvec[r]; d = (f32x4){gv * ww[0], gv * ww[1], gv * ww[2], gv * ww[3]}; }
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float dy = h[e] > 0.f ? d[e] * s.scale : 0.f;
+        v[e] = (dy - c0[e] - (x[e] - mu[e]) * c1[e]) * is[e] * gg[e];
+      }
+      *reinterpret_cast<f32x4*>(dX + i) = v;
+      if (dX16) store4(dX16 + i, v);
+      acc += v;
+    }
+  }
+  if (!colpart) return;
+  red[rl][q] = acc;
+  __syncthreads();
+  if (rl == 0 && c < C)
+    *reinterpret_cast<f32x4*>(colpart + (size_t)blockIdx.y * C + c) = red[0][q] + red[1][q] + red[2][q] + red[3][q];
+}
+
+// Deferred sums, one launch for all of a step's small reductions (bias gradients from column
+// partials, the head-bias gradient and the loss from [B] vectors):
+//   out[c] = beta * out[c] + scale * sum_{k < nch} part[k * C + c]
+// one 256-thread block per output column, fixed-order tree (deterministic).
+struct SumJob {
+  const float* part;
+  float* out;
+  int nch, C;
+  float scale, beta;
+};
+#define FBN_MAX_SUM_JOBS 8
+struct SumJobs {
+  SumJob j[FBN_MAX_SUM_JOBS];
+  int col0[FBN_MAX_SUM_JOBS + 1];
+  int n;
+};
+__global__ void __launch_bounds__(256) sum_jobs_kernel(SumJobs J) {
+  __shared__ float red[4];
+  const int gc = blockIdx.x;
+  int u = 0;
+  while (u + 1 < J.n && gc >= J.col0[u + 1]) ++u;
+  const SumJob jb = J.j[u];
+  const int c = gc - J.col0[u];
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int k = threadIdx.x;
+  for (; k + 768 < jb.nch; k += 1024) {
+    a0 += jb.part[(size_t)k * jb.C + c];
+    a1 += jb.part[(size_t)(k + 256) * jb.C + c];
+    a2 += jb.part[(size_t)(k + 512) * jb.C + c];
+    a3 += jb.part[(size_t)(k + 768) * jb.C + c];
+  }
+  for (; k < jb.nch; k += 256) a0 += jb.part[(size_t)k * jb.C + c];
+  float v = wave_sum((a0 + a1) + (a2 + a3));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float t = jb.scale * ((red[0] + red[1]) + (red[2] + red[3]));
+    jb.out[c] = jb.beta != 0.f ? jb.beta * jb.out[c] + t : t;
+  }
+}
+
 // ------------------------------------------------------------------ head: o = h.w + b, p = sigmoid(o), BCE
 // one wave per row.  gout[b] = dL/do when labels are given (mean BCE over `denom` samples),
 // using ATen's BCE backward ((p-t)/max((1-p)p, 1e-12)/N) followed by sigmoid backward (g(1-p)p).
@@ -483,9 +634,14 @@ extern "C" int fbn_bn_bwd_apply(const float* G, const float* gvec, const float* 
   float* coef = (float*)((double*)ws + (size_t)row_chunks(B) * 3 * C + 3 * (size_t)C);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(fbn_cdiv(C, 256)), dim3(256), 0, st, red_d, C, ntot, invstd, coef,
                      dgamma, dbeta, G ? nullptr : dw);
-  if (B > 0)
+  if (B > 0 && !(C & 3)) {
+    const int nch = row_chunks(B), rpc = (B + nch - 1) / nch;
+    hipLaunchKernelGGL(bn_bwd_apply4_kernel, dim3(fbn_cdiv(C, 256), nch), dim3(256), 0, st, s, Xpre, mean, invstd,
+                       gamma, coef, dXpre, dXpre16, B, C, rpc, nullptr);
+  } else if (B > 0) {
     hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid((size_t)B * C)), dim3(256), 0, st, s, Xpre, mean, invstd,
                        gamma, coef, dXpre, dXpre16, B, C);
+  }
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -610,6 +766,67 @@ extern "C" int fbn_bn_tile_stats(const float* part, int M, int C, const double* 
   const int T = (M + 63) / 64;
   hipLaunchKernelGGL(bn_tile_stats_kernel, dim3(fbn_cdiv(C, 4)), dim3(256), 0, (hipStream_t)stream, part, T, C, M, 64,
                      mean_d, out_d);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+// ------------------------------------------------------------------ single-process BN fusions (C ABI)
+extern "C" int fbn_bn_tile_finalize(const float* part, int M, int C, double ntot, float* mean, float* invstd,
+                                    float* run_mean, float* run_var, float momentum, float eps, int update_running,
+                                    void* stream) {
+  if (M <= 0) return FBN_OK;
+  hipLaunchKernelGGL(bn_tile_finalize_kernel, dim3(fbn_cdiv(C, 4)), dim3(256), 0, (hipStream_t)stream, part,
+                     (M + 63) / 64, C, M, 64, ntot, mean, invstd, run_mean, run_var, momentum, eps, update_running);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+extern "C" size_t fbn_bn_colpart_size(int B, int C) { return (size_t)row_chunks(B) * C * sizeof(float); }
+
+extern "C" int fbn_bn_bwd_fused(const float* G, const float* gvec, const float* w, const float* hact, float scale,
+                                const float* Xpre, const float* mean, const float* invstd, const float* gamma, int B,
+                                int C, double ntot, float* dXpre, short* dXpre16, float* dgamma, float* dbeta,
+                                float* dw, float* colpart, void* ws, void* stream) {
+  if (B <= 0) return FBN_OK;
+  if (C & 3) { fbn_set_error("fbn_bn_bwd_fused: C % 4"); return FBN_ERR_ARG; }
+  hipStream_t st = (hipStream_t)stream;
+  BnBwdSrc s{G, gvec, w, hact, scale};
+  const int nch = row_chunks(B), rpc = (B + nch - 1) / nch;
+  double* part = (double*)ws;
+  float* coef = (float*)((double*)ws + (size_t)nch * 3 * C + 3 * (size_t)C);
+  hipLaunchKernelGGL(bn_bwd_partial_kernel, dim3(fbn_cdiv(C, 64), nch), dim3(256), 0, st, s, Xpre, mean, B, C, rpc, part);
+  hipLaunchKernelGGL(bn_bwd_reduce_finalize_kernel, dim3(fbn_cdiv(C, 4)), dim3(256), 0, st, part, nch, C, ntot, invstd,
+                     coef, dgamma, dbeta, dw);
+  hipLaunchKernelGGL(bn_bwd_apply4_kernel, dim3(fbn_cdiv(C, 256), nch), dim3(256), 0, st, s, Xpre, mean, invstd, gamma,
+                     coef, dXpre, dXpre16, B, C, rpc, colpart);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+extern "C" int fbn_colsum_partial(const float* X, int B, int C, int ldx, float* part, void* stream) {
+  if (B <= 0) return FBN_OK;
+  const int nch = row_chunks(B), rpc = (B + nch - 1) / nch;
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3(fbn_cdiv(C, 64), nch), dim3(256), 0, (hipStream_t)stream, X, B, C,
+                     ldx, rpc, part);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+extern "C" int fbn_row_chunks(int B) { return row_chunks(B); }
+
+// jobs: host array of n (<= 8) {part, out, nch, C, scale, beta} (copied into the kernel argument)
+extern "C" int fbn_sum_jobs(const SumJob* jobs, int n, void* stream) {
+  if (n <= 0) return FBN_OK;
+  if (n > FBN_MAX_SUM_JOBS) { fbn_set_error("fbn_sum_jobs: too many jobs"); return FBN_ERR_ARG; }
+  SumJobs J;
+  J.n = n;
+  J.col0[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    J.j[i] = jobs[i];
+    J.col0[i + 1] = J.col0[i] + jobs[i].C;
+  }
+  if (J.col0[n] <= 0) return FBN_OK;
+  hipLaunchKernelGGL(sum_jobs_kernel, dim3(J.col0[n]), dim3(256), 0, (hipStream_t)stream, J);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

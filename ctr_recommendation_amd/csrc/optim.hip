@@ -15,6 +15,7 @@
 // the gradient only through the row->slot map (4 B/row); untouched rows get g = 0 + wd*p.
 // The map entries of touched rows are reset in the same pass.
 #include "common.h"
+#include <cstdlib>
 
 #pragma clang fp contract(off)
 
@@ -353,9 +354,11 @@ __global__ void __launch_bounds__(256) adam_touched_kernel(float* __restrict__ p
 }
 
 // end of step: advance Adam step + dropout RNG offset, clear the norm accumulator
-__global__ void step_end_kernel(int* step, unsigned long long* rng, double* sumsq) {
+__global__ void step_end_kernel(int* step, unsigned long long* rng, double* sumsq, long long* nbt0, long long* nbt1) {
   step[0] += 1;
   if (rng) rng[1] += 1;
+  if (nbt0) nbt0[0] += 1;   // BatchNorm num_batches_tracked
+  if (nbt1) nbt1[0] += 1;
   if (sumsq)
     for (int i = 0; i < FBN_SUMSQ_SLOTS; ++i) sumsq[i] = 0.0;
 }
@@ -434,7 +437,8 @@ extern "C" int fbn_sumsq_sparse(const float* gvec, float* extra, int* slot_row, 
 
 // mode 0: every row (touched rows read their gradient through the map and are reset);
 // mode 1: untouched rows only (g = 0, coefficient-independent; run it concurrently with the
-// backward, then fbn_adam_touched once the clip coefficient is known)
+// backward, then fbn_adam_touched once the clip coefficient is known), throttled to 512
+// workgroups so it leaves CUs to the backward; mode 2: as mode 1 on the full grid (serial use)
 extern "C" int fbn_adam_table(float* p, float* m, float* v, long long nrows, int D, int* map, const float* gvec,
                               float* extra, int* slot_row, int Lp1, const float* coef, const void* consts_table,
                               const int* step, float wd, float beta2, float eps, int mode, void* stream) {
@@ -443,8 +447,9 @@ extern "C" int fbn_adam_table(float* p, float* m, float* v, long long nrows, int
   const float omb2 = (float)(1.0 - (double)beta2);
   const AdamConsts* t = (const AdamConsts*)consts_table;
   GradSrc s{gvec, extra, slot_row, Lp1};
-  const dim3 grid = mode == 1 ? dim3(512) : group_grid(nrows, D, 16384);
-  if (mode == 1) {
+  static const int throttle = getenv("FBN_ADAM_BLOCKS") ? atoi(getenv("FBN_ADAM_BLOCKS")) : 512;   // tuning knob
+  const dim3 grid = mode == 1 ? dim3(throttle) : group_grid(nrows, D, 16384);
+  if (mode == 1 || mode == 2) {
     FBN_DISPATCH_D(adam_table_untouched, D, grid, p, m, v, nrows, map, s, coef, t, step, wd, beta2, omb2, eps);
   } else {
     FBN_DISPATCH_D(adam_table_all, D, grid, p, m, v, nrows, map, s, coef, t, step, wd, beta2, omb2, eps);
@@ -479,8 +484,9 @@ extern "C" int fbn_claim_rows(const int64_t* item, const int64_t* seq, int B, in
   return FBN_OK;
 }
 
-extern "C" int fbn_step_end(int* step, unsigned long long* rng, double* sumsq, void* stream) {
-  hipLaunchKernelGGL(step_end_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step, rng, sumsq);
+extern "C" int fbn_step_end(int* step, unsigned long long* rng, double* sumsq, long long* nbt0, long long* nbt1,
+                            void* stream) {
+  hipLaunchKernelGGL(step_end_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step, rng, sumsq, nbt0, nbt1);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

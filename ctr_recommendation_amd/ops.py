@@ -86,6 +86,37 @@ def bf16_weights(p: Dict[str, torch.Tensor], d: int, a: Dict[str, torch.Tensor],
     return out
 
 
+class _SumJob(ctypes.Structure):
+    _fields_ = [("part", ctypes.c_void_p), ("out", ctypes.c_void_p), ("nch", ctypes.c_int), ("C", ctypes.c_int),
+                ("scale", ctypes.c_float), ("beta", ctypes.c_float)]
+
+
+class DeferredSums:
+    """Small reductions of one step, finalised together by ONE fbn_sum_jobs launch:
+    out[c] = beta*out[c] + scale * sum_k part[k][c].  Partials must stay alive until flush()."""
+
+    def __init__(self):
+        self.jobs = []
+        self.keep = []
+
+    def add(self, part, nch, C, out, scale=1.0, beta=0.0):
+        self.jobs.append((part.data_ptr(), out.data_ptr(), int(nch), int(C), float(scale), float(beta)))
+        self.keep.append(part)
+
+    def colsum(self, X, B, C, ldx, out, stream):
+        nch = _lib.lib().fbn_row_chunks(B)
+        part = torch.empty((nch, C), dtype=torch.float32, device=X.device)
+        call("fbn_colsum_partial", ptr(X), B, C, ldx, ptr(part), stream)
+        self.add(part, nch, C, out)
+
+    def flush(self, stream):
+        for i in range(0, len(self.jobs), 8):
+            chunk = self.jobs[i:i + 8]
+            arr = (_SumJob * len(chunk))(*[_SumJob(*j) for j in chunk])
+            call("fbn_sum_jobs", ctypes.addressof(arr), len(chunk), stream)
+        self.jobs, self.keep = [], []
+
+
 def colsum(X, B, C, ldx, out, beta=0.0, stream=None):
     ws = _ws(_lib.lib().fbn_colsum_workspace_size(B, C), X.device)
     call("fbn_colsum", ptr(X), B, C, ldx, ptr(out), float(beta), ptr(ws),
@@ -121,6 +152,10 @@ def bn_train_stats(h, B, C, mean, invstd, run_mean, run_var, ntot, coll: Collect
     dev = h.device
     s = torch.empty(C, dtype=torch.float64, device=dev)
     mean_d = torch.empty(C, dtype=torch.float64, device=dev)
+    if tiles is not None and coll.world <= 1:
+        call("fbn_bn_tile_finalize", ptr(tiles), B, C, float(ntot), ptr(mean), ptr(invstd), ptr(run_mean),
+             ptr(run_var), BN_MOMENTUM, BN_EPS, 1 if run_mean is not None else 0, stream)
+        return
     if tiles is not None:
         call("fbn_bn_tile_stats", ptr(tiles), B, C, None, ptr(s), stream)
         coll.allreduce_(s)
@@ -139,9 +174,21 @@ def bn_train_stats(h, B, C, mean, invstd, run_mean, run_var, ntot, coll: Collect
 
 
 def bn_backward(G, gvec, w, hact, scale, hpre, mean, invstd, gamma, B, C, ntot, dpre, dgamma, dbeta, dw,
-                coll: Collective, stream, dpre16=None):
+                coll: Collective, stream, dpre16=None, bias_grad=None, sums: Optional[DeferredSums] = None):
+    """BN (+ReLU/dropout) backward; bias_grad (with sums): the preceding Linear's bias gradient
+    = column sums of dpre, finalised later by sums.flush()."""
     dev = hpre.device
     ws = _ws(_lib.lib().fbn_bn_workspace_size(B, C), dev)
+    if coll.world <= 1:
+        part = None
+        if bias_grad is not None:
+            nch = _lib.lib().fbn_row_chunks(B)
+            part = torch.empty((nch, C), dtype=torch.float32, device=dev)
+            sums.add(part, nch, C, bias_grad)
+        call("fbn_bn_bwd_fused", ptr(G), ptr(gvec), ptr(w), ptr(hact), float(scale), ptr(hpre), ptr(mean),
+             ptr(invstd), ptr(gamma), B, C, float(ntot), ptr(dpre), ptr(dpre16), ptr(dgamma), ptr(dbeta), ptr(dw),
+             ptr(part), ptr(ws), stream)
+        return
     red = torch.empty(3 * C, dtype=torch.float64, device=dev)
     call("fbn_bn_bwd_reduce", ptr(G), ptr(gvec), ptr(w), ptr(hact), float(scale), ptr(hpre), ptr(mean), B, C,
          ptr(red), ptr(ws), stream)
@@ -158,6 +205,8 @@ def bn_backward(G, gvec, w, hact, scale, hpre, mean, invstd, gamma, B, C, ntot, 
         call("fbn_bn_bwd_apply", ptr(G), ptr(gvec), ptr(w), ptr(hact), float(scale), ptr(hpre), ptr(mean),
              ptr(invstd), ptr(gamma), 0, C, ptr(red), float(ntot), None, None, ptr(dgamma), ptr(dbeta), ptr(dw),
              ptr(ws), stream)
+    if bias_grad is not None:
+        sums.colsum(dpre, B, C, C, bias_grad, stream)
 
 
 def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: FwdConfig,
@@ -167,7 +216,7 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
             loss_denom: Optional[float] = None, coll: Collective = NO_COLLECTIVE, ntot: Optional[int] = None,
             masks_out: Optional[Dict[str, torch.Tensor]] = None, acts: Optional[Dict[str, torch.Tensor]] = None,
             probe: Optional[Dict[str, list]] = None, masks_in: Optional[Dict[str, torch.Tensor]] = None,
-            after_gather=None) -> Dict[str, torch.Tensor]:
+            after_gather=None, count_batches: bool = True) -> Dict[str, torch.Tensor]:
     """Run the forward; returns the activation dict (probs, logits and what backward needs).
 
     p: parameter tensors keyed like the reference state_dict (fp32, contiguous, on device).
@@ -290,7 +339,7 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     go = buf("gout", (B,)) if labels is not None else None
     call("fbn_head_fwd", ptr(h2), ptr(p["mlp.8.weight"]), ptr(p["mlp.8.bias"]), B, H2, ptr(logits), ptr(probs),
          ptr(labels), ptr(lt), ptr(go), float(loss_denom if loss_denom is not None else ntot), st)
-    if cfg.training and "mlp.1.num_batches_tracked" in p:
+    if cfg.training and count_batches and "mlp.1.num_batches_tracked" in p:
         p["mlp.1.num_batches_tracked"].add_(1)
         p["mlp.5.num_batches_tracked"].add_(1)
     a["err"] = err
@@ -303,7 +352,7 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
              table_grad: Optional[torch.Tensor] = None, gvec: Optional[torch.Tensor] = None,
              pos: Optional[torch.Tensor] = None,
              sendbuf: Optional[torch.Tensor] = None, coll: Collective = NO_COLLECTIVE,
-             ntot: Optional[int] = None) -> None:
+             ntot: Optional[int] = None, extra_sums=()) -> None:
     """Backward from dL/dlogit (gout [B]) into the gradient buffers ``g`` (same keys as ``p``).
 
     table_grad: dense [V, d] (drop-in, accumulated by atomics); or gvec [B, 2, d] (native
@@ -311,6 +360,8 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     (native trainer); in multi-GPU mode (pos given) rows are written to sendbuf instead.
     Every g[...] buffer is overwritten (not accumulated), except the table gradient which is
     accumulated into (callers zero it).
+    extra_sums: further (part, nch, C, out[, scale, beta]) reductions to finalise in the same
+    fbn_sum_jobs launch as the bias gradients (the trainer's mean loss).
     """
     d, L = cfg.d, cfg.L
     B = a["B"]
@@ -326,11 +377,11 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     bf16_ = dict(dtype=torch.bfloat16, device=dev)
     dh2pre = torch.empty((B, H2), **f32)
     dh2pre16 = torch.empty((B, H2), **bf16_) if bf else None
+    sums = DeferredSums()
     bn_backward(None, gout, p["mlp.8.weight"], a["h2"], scale, a["h2pre"], a["mean2"], a["inv2"],
                 p["mlp.5.weight"], B, H2, ntot, dh2pre, g["mlp.5.weight"], g["mlp.5.bias"], g["mlp.8.weight"],
-                coll, st, dpre16=dh2pre16)
-    call("fbn_sum", ptr(gout), B, ptr(g["mlp.8.bias"]), 1.0, st)
-    colsum(dh2pre, B, H2, H2, g["mlp.4.bias"], stream=st)
+                coll, st, dpre16=dh2pre16, bias_grad=g["mlp.4.bias"], sums=sums)
+    sums.add(gout, B, 1, g["mlp.8.bias"])
     dh1 = torch.empty((B, H1), **f32)
     if bf:
         gemm(dh2pre16, a["h1_16"], g["mlp.4.weight"], H2, H1, B, H2, H1, H1, True, False, stream=st)
@@ -341,8 +392,8 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     dh1pre = torch.empty((B, H1), **f32)
     dh1pre16 = torch.empty((B, H1), **bf16_) if bf else None
     bn_backward(dh1, None, None, a["h1"], scale, a["h1pre"], a["mean1"], a["inv1"], p["mlp.1.weight"], B, H1, ntot,
-                dh1pre, g["mlp.1.weight"], g["mlp.1.bias"], None, coll, st, dpre16=dh1pre16)
-    colsum(dh1pre, B, H1, H1, g["mlp.0.bias"], stream=st)
+                dh1pre, g["mlp.1.weight"], g["mlp.1.bias"], None, coll, st, dpre16=dh1pre16,
+                bias_grad=g["mlp.0.bias"], sums=sums)
     dc = torch.empty((B, KC), **f32)
     if bf:
         gemm(dh1pre16, a["c"], g["mlp.0.weight"], H1, KC, B, H1, KC, 21 * d, True, False, rC=wa_remap(d), stream=st)
@@ -386,4 +437,7 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
          ptr(table_grad), ptr(gvec), V, ptr(pos), ptr(sendbuf), B, Lr, d, st)
     gemm(dhmm, batch["item_emb_d128"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True, False, bf16=cfg.bf16,
          stream=st)
-    colsum(dhmm, B, d, d, g["mm_proj.0.bias"], stream=st)
+    sums.colsum(dhmm, B, d, d, g["mm_proj.0.bias"], st)
+    for job in extra_sums:              # e.g. the trainer's mean loss
+        sums.add(*job)
+    sums.flush(st)

@@ -22,6 +22,7 @@ reference computes), dense gradients are all-reduced, the clip norm sums the tab
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -148,6 +149,7 @@ class FiBiNETTrainer:
                                 stage_on_cpu=stage_on_cpu) if world > 1 else None
         self.stage_on_cpu = stage_on_cpu
         self.side = torch.cuda.Stream(device=dev)       # untouched-row Adam overlaps the backward
+        self.serial_adam = os.environ.get("FBN_SERIAL_ADAM", "0") == "1"   # profiling knob: no overlap
 
     # ------------------------------------------------------------------ one training step
     def step(self, batch: Dict[str, torch.Tensor], labels: torch.Tensor,
@@ -175,15 +177,17 @@ class FiBiNETTrainer:
         rows = pos = None
         main = torch.cuda.current_stream(self.device)
 
+        side = main if self.serial_adam else self.side
+
         def start_untouched_adam():
             # every row of this shard the batch touches is claimed in `map` by now; the rest get
             # g = wd * p, independent of the backward -> run them concurrently on the side stream
-            self.side.wait_stream(main)
-            ev = _events(probe, "adam_table", self.side)
+            side.wait_stream(main)
+            ev = _events(probe, "adam_table", side)
             call("fbn_adam_table", ptr(self.E), ptr(self.Em), ptr(self.Ev), self.rows_local, d, ptr(self.map),
-                 None, None, None, 1, None, ptr(self.sched), ptr(self.step_dev), self.wd, self.beta2, self.eps, 1,
-                 self.side.cuda_stream)
-            _events_end(ev, self.side)
+                 None, None, None, 1, None, ptr(self.sched), ptr(self.step_dev), self.wd, self.beta2, self.eps,
+                 2 if self.serial_adam else 1, side.cuda_stream)
+            _events_end(ev, side)
 
         if self.xchg is not None:
             rows = self.xchg.forward(batch["item_id"], seq, self.E, {"map": self.map, "slot_row": self.slot_row},
@@ -195,11 +199,11 @@ class FiBiNETTrainer:
         start_untouched_adam()
         a = ops.forward(self.p, batch, cfg, self.rng, table_rows=rows, pos=pos, err=self.err, labels=labels,
                         loss_denom=float(ntot), coll=self.coll, ntot=ntot, acts=self.acts, masks_out=masks_out,
-                        probe=probe)
-        call("fbn_sum", ptr(a["loss_terms"]), B, ptr(self.loss), 1.0 / ntot, st)
+                        probe=probe, count_batches=False)     # num_batches_tracked: fbn_step_end
         sendbuf = self.xchg.make_sendbuf() if self.xchg is not None else None
         ops.backward(self.p, batch, a, a["gout"], self.g, cfg, gvec=self.gvec if self.xchg is None else None,
-                     pos=pos, sendbuf=sendbuf, coll=self.coll, ntot=ntot)
+                     pos=pos, sendbuf=sendbuf, coll=self.coll, ntot=ntot,
+                     extra_sums=[(a["loss_terms"], B, 1, self.loss, 1.0 / ntot)])
         if self.xchg is None:
             # single GPU: per-sample vectors; entry e = b*(L+1)+t; duplicates -> extra[claimer]
             gsrc = (self.gvec, self.extra, L + 1)
@@ -225,14 +229,15 @@ class FiBiNETTrainer:
         call("fbn_clip_coef", ptr(self.sumsq), self.max_norm, ptr(self.coef), ptr(self.norm), st)
         call("fbn_adam_dense", ptr(self.flat_p), ptr(self.flat_g), ptr(self.flat_m), ptr(self.flat_v),
              self.n_dense, ptr(self.coef), ptr(self.sched), ptr(self.step_dev), self.wd, self.beta2, self.eps, st)
-        main.wait_stream(self.side)                  # untouched pass done before map entries are reset
+        main.wait_stream(side)                       # untouched pass done before map entries are reset
         ev = _events(probe, "adam_touched")
         call("fbn_adam_touched", ptr(self.E), ptr(self.Em), ptr(self.Ev), d, ptr(self.map), ptr(gsrc[0]),
              ptr(gsrc[1]), ptr(self.slot_row), gsrc[2], n_ent, ptr(self.coef), ptr(self.sched), ptr(self.step_dev),
              self.wd, self.beta2, self.eps, st)
         _events_end(ev)
         self.slot_row[:n_ent].fill_(-1)
-        call("fbn_step_end", ptr(self.step_dev), ptr(self.rng), ptr(self.sumsq), st)
+        call("fbn_step_end", ptr(self.step_dev), ptr(self.rng), ptr(self.sumsq), ptr(self.p["mlp.1.num_batches_tracked"]),
+             ptr(self.p["mlp.5.num_batches_tracked"]), st)
         self.host_step += 1
         return self.loss
 

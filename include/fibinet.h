@@ -106,6 +106,10 @@ int fbn_bn_stats(const float* X, int B, int C, float* mean, float* invstd, float
 /* BN statistics from fbn_gemm tile partials: mean_d == NULL -> out = column sums; else
  * out = column sums of squared deviations about mean_d (Chan merge, f64). */
 int fbn_bn_tile_stats(const float* part, int M, int C, const double* mean_d, double* out_d, void* stream);
+/* Single-process form of the above + fbn_bn_mean + fbn_bn_finalize in one launch (same f64
+ * operations in the same order; the multi-GPU path needs the all-reduces in between). */
+int fbn_bn_tile_finalize(const float* part, int M, int C, double ntot, float* mean, float* invstd, float* run_mean,
+                         float* run_var, float momentum, float eps, int update_running, void* stream);
 int fbn_bn_eval_params(const float* run_mean, const float* run_var, float* mean, float* invstd, int C, float eps,
                        void* stream);
 int fbn_bn_act_fwd(const float* X, float* Y, int B, int C, const float* mean, const float* invstd, const float* g,
@@ -120,12 +124,29 @@ int fbn_bn_bwd_apply(const float* G, const float* gvec, const float* w, const fl
 int fbn_bn_bwd(const float* G, const float* gvec, const float* w, const float* hact, float scale, const float* Xpre,
                const float* mean, const float* invstd, const float* gamma, int B, int C, float* dXpre, float* dgamma,
                float* dbeta, float* dw, void* ws, void* stream);
+/* Single-process BN backward in three launches (partials -> reduce + finalize -> vectorised
+ * apply).  colpart (optional, fbn_bn_colpart_size bytes): per-row-chunk column sums of dXpre =
+ * the partials of the preceding Linear's bias gradient (finalised by fbn_sum_jobs). */
+size_t fbn_bn_colpart_size(int B, int C);
+int fbn_row_chunks(int B);
+int fbn_bn_bwd_fused(const float* G, const float* gvec, const float* w, const float* hact, float scale,
+                     const float* Xpre, const float* mean, const float* invstd, const float* gamma, int B, int C,
+                     double ntot, float* dXpre, short* dXpre16, float* dgamma, float* dbeta, float* dw,
+                     float* colpart, void* ws, void* stream);
 /* bf16 weight images: jobs = host array of n <= 8 records
  * {const float* src; short* dst; int rows, cols, ld, trans, seg, off0, off1;}
  * out[i][j] = bf16(trans ? src[j*ld + rm(i)] : src[i*ld + rm(j)]), rm(x) = x + (x < seg ? off0 : off1). */
 int fbn_convert_bf16(const void* jobs, int n, void* stream);
 size_t fbn_colsum_workspace_size(int B, int C);
 int fbn_colsum(const float* X, int B, int C, int ldx, float* out, float beta, void* ws, void* stream);
+/* column partials only: part[fbn_row_chunks(B)][C] (finalised by fbn_sum_jobs) */
+int fbn_colsum_partial(const float* X, int B, int C, int ldx, float* part, void* stream);
+/* Deferred sums of one step in ONE launch: jobs = host array of n <= 8 records
+ * {const float* part; float* out; int nch, C; float scale, beta;}:
+ * out[c] = beta * out[c] + scale * sum_{k < nch} part[k * C + c]   (fixed-order tree).
+ * Used for the bias gradients (sum over the batch, autograd of src/model_fibinet.py:105,126,130,134)
+ * and the mean BCE loss (src/train_fibinet.py:115). */
+int fbn_sum_jobs(const void* jobs, int n, void* stream);
 
 /* ---------------------------------------------------------------- K7 head: Linear(256,1)+sigmoid+BCE
  * Replaces src/model_fibinet.py:134,136,199 and nn.BCELoss fwd/bwd (src/train_fibinet.py:79,115). */
@@ -167,7 +188,9 @@ int fbn_adam_touched(float* p, float* m, float* v, int D, int* map, const float*
 #define FBN_SUMSQ_SLOTS 64
 int fbn_claim_rows(const int64_t* item, const int64_t* seq, int B, int L, long long V, int* map, int* slot_row,
                    void* stream);
-int fbn_step_end(int* step, unsigned long long* rng, double* sumsq, void* stream);
+/* end of step: step counter, dropout counter, zero the sumsq slots, and the BatchNorm
+ * num_batches_tracked buffers (nbt0 / nbt1 may be NULL; model_fibinet.py:127,131 BN1d). */
+int fbn_step_end(int* step, unsigned long long* rng, double* sumsq, long long* nbt0, long long* nbt1, void* stream);
 
 /* ---------------------------------------------------------------- row-sharded exchange (multi-GPU)
  * Replaces torch.nn.DataParallel's replicate/scatter of the whole table (src/train_fibinet.py:69-70)

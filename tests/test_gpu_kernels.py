@@ -59,3 +59,24 @@ def test_gemm_fused_bn_stats(hip_device, M, N, K, bf16):
     var = Cd.var(0, unbiased=False)
     assert torch.allclose(mean.double(), Cd.mean(0), rtol=1e-6, atol=1e-6)
     assert torch.allclose(inv.double(), 1.0 / torch.sqrt(var + ops.BN_EPS), rtol=1e-5)
+
+
+@pytest.mark.parametrize("transA,transB", [(False, True), (False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(8192, 512, 1920), (200, 136, 256), (512, 1920, 8192), (256, 512, 4096),
+                                   (1000, 72, 128)])
+def test_gemm_bf16_all_layouts(hip_device, transA, transB, M, N, K):
+    """bf16 operands in every storage layout (the LDS-DMA kernel: K % 64 == 0; ragged M / N
+    tiles; the split-K plans of the wgrad shapes) against torch with the same bf16 inputs."""
+    g = torch.Generator(device="cpu").manual_seed(3)
+    A = torch.randn((K, M) if transA else (M, K), generator=g).to(hip_device).bfloat16()
+    Bm = torch.randn((N, K) if transB else (K, N), generator=g).to(hip_device).bfloat16()
+    bias = torch.randn((N,), generator=g).to(hip_device)
+    C = torch.full((M, N), float("nan"), device=hip_device)
+    lda = M if transA else K
+    ldb = K if transB else N
+    ops.gemm(A, Bm, C, M, N, K, lda, ldb, N, transA, transB, bias=bias)
+    a = A.double().T if transA else A.double()
+    b = Bm.double().T if transB else Bm.double()
+    ref = a @ b + bias.double()
+    err = (C.double() - ref).abs().max().item()
+    assert err < 2e-5 * K ** 0.5 * 4, err
