@@ -37,13 +37,12 @@ SIGNATURES = {
     "fbn_bn_bwd_fused": (I, [P, P, P, P, F, P, P, P, P, I, I, D, P, P, P, P, P, P, P, P]),
     "fbn_colsum_partial": (I, [P, I, I, I, P, P]),
     "fbn_sum_jobs": (I, [P, I, P]),
-    "fbn_fields_fwd": (I, [P, P, P, P, P, P, P, F, P, I, P, LL, P, P, P, P, P, I, P, P, P, I, I, P, P, P, P, P,
-                           I, I, I, P]),
+    "fbn_fields_fwd": (I, [P, P, P, P, P, P, P, F, P, I, P, LL, P, P, P, P, P, I, P, P, P, P, I, I, P, P, P, P, P, I, I, I, P]),
     "fbn_fields_bwd_partials_size": (I, [I, I, I]),
     "fbn_fields_bwd_grid": (I, [I, I]),
-    "fbn_fields_bwd": (I, [P, P, P, P, P, P, F, P, P, P, I, I, P, P, P, P, P, P, P, P, P, LL, P, P, I, I, I, P]),
+    "fbn_fields_bwd": (I, [P, P, P, P, P, P, F, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P, LL, P, P, I, I, I, P]),
     "fbn_pairs_fwd": (I, [P, P, P, I, I, I, I, I, P]),
-    "fbn_pairs_bwd": (I, [P, P, P, P, P, I, I, I, I, P]),
+    "fbn_pairs_bwd": (I, [P, P, P, P, P, P, I, I, I, I, P]),
     "fbn_bn_workspace_size": (SZ, [I, I]),
     "fbn_bn_stats_pass": (I, [P, I, I, P, P, P, P]),
     "fbn_bn_mean": (I, [P, D, I, P, P]),

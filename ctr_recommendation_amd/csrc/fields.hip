@@ -34,6 +34,7 @@ struct FieldArgs {
   const float* w1; const float* b1; const float* w2; const float* b2;  // SENET [R][6],[R],[6][R],[6]
   float* X;                 // [B][5][D] fields 1..5 (pre-SENET)
   float* Vc;                // [B][5][D] fields 1..5 (post-SENET)
+  short* Vc16;              // optional bf16 copy of Vc (GEMM operand of the bilinear U = V W and its wgrad)
   void* c;                  // [B][ldc] float or bf16 (c16); cols [0,5D) <- Vc (MLP input, compact layout)
   float* a_out;             // [B][6]
   float* cnt_out;           // [B]
@@ -168,8 +169,10 @@ __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
       const f32x4 v = xs[f] * a[f + 1];
       *reinterpret_cast<f32x4*>(Xb + f * D) = xs[f];
       *reinterpret_cast<f32x4*>(Vb + f * D) = v;
-      if (cb16) *reinterpret_cast<bf16x4*>(cb16 + f * D) = (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+      const bf16x4 v16 = (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+      if (cb16) *reinterpret_cast<bf16x4*>(cb16 + f * D) = v16;
       else *reinterpret_cast<f32x4*>(cb + f * D) = v;
+      if (p.Vc16) *reinterpret_cast<bf16x4*>(p.Vc16 + ((size_t)b * 5 + f) * D + 4 * q) = v16;
     }
 #pragma unroll
     for (int f = 0; f < 6; ++f)
@@ -196,6 +199,7 @@ struct FieldBwdArgs {
   const float* cnt;    // [B]
   const float* dV;     // [B][5][D] total gradient wrt V_1..V_5
   float* dhmm;         // [B][D] gradient wrt the pre-LN projection
+  short* dhmm16;       // optional bf16 copy (operand of the mm_proj weight-gradient GEMM)
   float* partials;     // [gridDim.x][P]; P = 6R + R + 6R + 6 + 2D + n_cate*D
   // table gradient, mode 0: dense gtab[V][D] (atomics) if gvec == null; otherwise the two
   // per-sample vectors gvec[b][0] = dX3 (item row), gvec[b][1] = dX5/count (each history row)
@@ -337,6 +341,9 @@ __global__ void __launch_bounds__(256) fields_bwd_kernel(FieldBwdArgs p) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) out[e] = rstd * (gx[e] - m1 - xh[e] * m2);
       *reinterpret_cast<f32x4*>(p.dhmm + (size_t)b * D + 4 * q) = out;
+      if (p.dhmm16)
+        *reinterpret_cast<bf16x4*>(p.dhmm16 + (size_t)b * D + 4 * q) = (bf16x4){f2bf(out[0]), f2bf(out[1]), f2bf(out[2]),
+                                                                                 f2bf(out[3])};
     }
     // cate table (likes, views share one table)
     {
@@ -441,7 +448,8 @@ extern "C" int fbn_fields_fwd(const int64_t* item_id, const int64_t* item_seq, c
                               const int64_t* views, const float* hmm, const float* ln_g, const float* ln_b,
                               float ln_eps, const float* cate, int n_cate, const float* table, long long V,
                               const int* pos, const float* w1, const float* b1, const float* w2,
-                              const float* b2, int R, float* X, float* Vc, void* c, int ldc, int c_bf16, float* a_out,
+                              const float* b2, int R, float* X, float* Vc, short* Vc16, void* c, int ldc, int c_bf16,
+                              float* a_out,
                               float* cnt_out, int* err, int* map, int* slot_row, int B, int L,
                               int D, void* stream) {
   if (B <= 0) return FBN_OK;
@@ -453,7 +461,7 @@ extern "C" int fbn_fields_fwd(const int64_t* item_id, const int64_t* item_seq, c
   a.item_id = item_id; a.item_seq = L > 0 ? item_seq : nullptr; a.likes = likes; a.views = views;
   a.hmm = hmm; a.ln_g = ln_g; a.ln_b = ln_b; a.cate = cate; a.table = table; a.pos = pos;
   a.w1 = w1; a.b1 = b1; a.w2 = w2; a.b2 = b2;
-  a.X = X; a.Vc = Vc; a.c = c; a.a_out = a_out; a.cnt_out = cnt_out; a.err = err;
+  a.X = X; a.Vc = Vc; a.Vc16 = Vc16; a.c = c; a.a_out = a_out; a.cnt_out = cnt_out; a.err = err;
   a.map = map; a.slot_row = slot_row;
   a.V = V; a.B = B; a.L = L; a.ldc = ldc; a.R = R; a.n_cate = n_cate; a.ln_eps = ln_eps; a.c16 = c_bf16;
   if (pos) return launch_fields_fwd<1>(a, D, (hipStream_t)stream);
@@ -487,14 +495,14 @@ extern "C" int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, c
                               const int64_t* views, const float* hmm, const float* ln_g, float ln_eps,
                               const float* w1, const float* b1, const float* w2, int R, int n_cate,
                               const float* X, const float* a, const float* cnt, const float* dV, float* dhmm,
-                              float* partials, float* const* param_grads, float* gtab, float* gvec, long long V,
+                              short* dhmm16, float* partials, float* const* param_grads, float* gtab, float* gvec, long long V,
                               const int* pos, float* sendbuf, int B, int L, int D, void* stream) {
   if (B <= 0) return FBN_OK;
   if (L < 0 || L > 32 || R < 1 || R > FBN_MAXR) { fbn_set_error("fbn_fields_bwd: bad L/R"); return FBN_ERR_ARG; }
   FieldBwdArgs p;
   p.item_id = item_id; p.item_seq = L > 0 ? item_seq : nullptr; p.likes = likes; p.views = views;
   p.hmm = hmm; p.ln_g = ln_g; p.w1 = w1; p.b1 = b1; p.w2 = w2;
-  p.X = X; p.a = a; p.cnt = cnt; p.dV = dV; p.dhmm = dhmm; p.partials = partials;
+  p.X = X; p.a = a; p.cnt = cnt; p.dV = dV; p.dhmm = dhmm; p.dhmm16 = dhmm16; p.partials = partials;
   p.gtab = gtab; p.gvec = gvec; p.pos = pos; p.sendbuf = sendbuf;
   p.V = V; p.B = B; p.L = L; p.R = R; p.n_cate = n_cate; p.ln_eps = ln_eps;
   hipStream_t st = (hipStream_t)stream;

@@ -30,6 +30,10 @@
 #include <cstdlib>
 #include <cstdio>
 
+#ifndef FBN_DMA_STAGES
+#define FBN_DMA_STAGES 2
+#endif
+
 struct Remap {
   int seg, off0, off1;
 };
@@ -472,14 +476,27 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int r0, int s, int lane)
   }
 }
 
-template <int BM, int BN, bool AKM, bool BKM>
+// wait until at most n of this wave's DMA groups are outstanding (n: compile-time multiple of GPW)
+template <int GPW, int S>
+__device__ __forceinline__ void wait_dma(int ahead) {   // ahead = stages allowed to stay in flight (0 .. S-2)
+  if constexpr (S >= 4) {
+    if (ahead >= 2) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GPW) : "memory"); return; }
+  }
+  if constexpr (S >= 3) {
+    if (ahead >= 1) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW) : "memory"); return; }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int BM, int BN, bool AKM, bool BKM, int S>
 __global__ void __launch_bounds__(256) gemm_dma16_kernel(GemmArgs g, int tiles_n, int remap_xcd) {
   constexpr int BK = 64;
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
   constexpr int AB = BM * BK * 2, STAGE = (BM + BN) * BK * 2;   // A image bytes, stage bytes
   constexpr int GPW = (BM + BN) / 8 / 4;                          // 1-KiB DMA groups per wave per stage
   static_assert(((BM + BN) / 8) % 4 == 0 && BM % 16 == 0, "tile / wave mismatch");
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  static_assert(S >= 2 && S <= 4, "stages");
+  __shared__ __attribute__((aligned(1024))) char smem[S * STAGE];
 
   int bid = blockIdx.x;
   const int nb = gridDim.x;
@@ -538,12 +555,19 @@ __global__ void __launch_bounds__(256) gemm_dma16_kernel(GemmArgs g, int tiles_n
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  if (nk > 0) issue(0, 0);
+  // S-stage ring: stages t+1 .. t+S-2 stay in flight across the barrier of step t (counted
+  // vmcnt + raw s_barrier; __syncthreads() would drain every DMA with vmcnt(0)).  The barrier
+  // also certifies that every wave finished step t-1, whose buffer the DMA of stage t+S-1
+  // overwrites.
+#pragma unroll
+  for (int q = 0; q < S - 1; ++q)
+    if (q < nk) issue(q, q);
   for (int t = 0; t < nk; ++t) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t + 1 < nk) issue(t + 1, (t + 1) & 1);
-    const char* SA = smem + (t & 1) * STAGE;
+    wait_dma<GPW, S>(min(S - 2, nk - 1 - t));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t + S - 1 < nk) issue(t + S - 1, (t + S - 1) % S);
+    const char* SA = smem + (t % S) * STAGE;
     const char* SB = SA + AB;
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {
@@ -664,8 +688,15 @@ template <int BM, int BN, bool AKM, bool BKM>
 static void launch_dma16(const GemmArgs& g, int nsplit, hipStream_t st) {
   const int tn = fbn_cdiv(g.N, BN), tm = fbn_cdiv(g.M, BM);
   const int nb = tn * tm;
-  hipLaunchKernelGGL((gemm_dma16_kernel<BM, BN, AKM, BKM>), dim3(nb, 1, nsplit), dim3(256), 0, st, g, tn,
-                     (nb % 8 == 0) ? 1 : 0);
+  const int rx = (nb % 8 == 0) ? 1 : 0;
+  const char* e = getenv("FBN_GEMM_STAGES");   // tuning knob
+  const int S = e ? atoi(e) : FBN_DMA_STAGES;
+  if (S <= 2)
+    hipLaunchKernelGGL((gemm_dma16_kernel<BM, BN, AKM, BKM, 2>), dim3(nb, 1, nsplit), dim3(256), 0, st, g, tn, rx);
+  else if (S == 3)
+    hipLaunchKernelGGL((gemm_dma16_kernel<BM, BN, AKM, BKM, 3>), dim3(nb, 1, nsplit), dim3(256), 0, st, g, tn, rx);
+  else
+    hipLaunchKernelGGL((gemm_dma16_kernel<BM, BN, AKM, BKM, 4>), dim3(nb, 1, nsplit), dim3(256), 0, st, g, tn, rx);
 }
 
 template <bool AKM, bool BKM>

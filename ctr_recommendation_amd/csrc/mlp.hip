@@ -51,8 +51,13 @@ __global__ void pairs_fwd_kernel(const float* __restrict__ Vc, const float* __re
 }
 
 // dV (out) = dc_V + sum of pair-grad terms that land on V ; dU (out) = pair-grad terms that land on U
-__global__ void pairs_bwd_kernel(const float* __restrict__ dc, const float* __restrict__ Vc, const float* __restrict__ U,
-                                 float* __restrict__ dV, float* __restrict__ dU, int B, int D, int ldc, int mode) {
+// MODE (bilinear "all" = 0 / "each" = 1) is a template parameter and the pair loop is unrolled
+// with compile-time indices: with runtime indices the five-field register arrays go to scratch.
+template <int MODE>
+__global__ void __launch_bounds__(256) pairs_bwd_kernel(const float* __restrict__ dc, const float* __restrict__ Vc,
+                                                        const float* __restrict__ U, float* __restrict__ dV,
+                                                        float* __restrict__ dU, short* __restrict__ dU16, int B, int D,
+                                                        int ldc) {
   const int q4 = D / 4;
   const size_t total = (size_t)B * q4;
   for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
@@ -66,17 +71,19 @@ __global__ void pairs_bwd_kernel(const float* __restrict__ dc, const float* __re
       gv[f] = *reinterpret_cast<const f32x4*>(dcb + f * D);
       gu[f] = (f32x4){0.f, 0.f, 0.f, 0.f};
     }
+    constexpr int PI[10] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3};
+    constexpr int PJ[10] = {1, 2, 3, 4, 2, 3, 4, 3, 4, 4};
 #pragma unroll
     for (int k = 0; k < 10; ++k) {
       const f32x4 g = *reinterpret_cast<const f32x4*>(dcb + (5 + k) * D);
-      const int i = c_pi[k], j = c_pj[k];
-      if (mode == 0) { gv[i] += g * u[j]; gu[j] += g * v[i]; }
-      else { gu[i] += g * v[j]; gv[j] += g * u[i]; }
+      if constexpr (MODE == 0) { gv[PI[k]] += g * u[PJ[k]]; gu[PJ[k]] += g * v[PI[k]]; }
+      else { gu[PI[k]] += g * v[PJ[k]]; gv[PJ[k]] += g * u[PI[k]]; }
     }
 #pragma unroll
     for (int f = 0; f < 5; ++f) {
       *reinterpret_cast<f32x4*>(dV + ((size_t)b * 5 + f) * D + col) = gv[f];
       *reinterpret_cast<f32x4*>(dU + ((size_t)b * 5 + f) * D + col) = gu[f];
+      if (dU16) store4(dU16 + ((size_t)b * 5 + f) * D + col, gu[f]);
     }
   }
 }
@@ -530,11 +537,15 @@ extern "C" int fbn_pairs_fwd(const float* Vc, const float* U, void* c, int B, in
   return FBN_OK;
 }
 
-extern "C" int fbn_pairs_bwd(const float* dc, const float* Vc, const float* U, float* dV, float* dU, int B, int D,
-                             int ldc, int mode, void* stream) {
+extern "C" int fbn_pairs_bwd(const float* dc, const float* Vc, const float* U, float* dV, float* dU, short* dU16,
+                             int B, int D, int ldc, int mode, void* stream) {
   if (B <= 0) return FBN_OK;
-  hipLaunchKernelGGL(pairs_bwd_kernel, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream, dc, Vc, U,
-                     dV, dU, B, D, ldc, mode);
+  if (mode == 0)
+    hipLaunchKernelGGL(pairs_bwd_kernel<0>, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream, dc, Vc,
+                       U, dV, dU, dU16, B, D, ldc);
+  else
+    hipLaunchKernelGGL(pairs_bwd_kernel<1>, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream, dc, Vc,
+                       U, dV, dU, dU16, B, D, ldc);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

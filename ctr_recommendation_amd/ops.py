@@ -60,9 +60,11 @@ class _ConvJob(ctypes.Structure):
                 ("off1", ctypes.c_int)]
 
 
-def bf16_weights(p: Dict[str, torch.Tensor], d: int, a: Dict[str, torch.Tensor], stream) -> Dict[str, torch.Tensor]:
+def bf16_weights(p: Dict[str, torch.Tensor], d: int, a: Dict[str, torch.Tensor], stream,
+                 x: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
     """bf16 images of the GEMM weights, laid out so every bf16 GEMM operand is K-contiguous:
-    Wa_nz [512,15d] (zero columns dropped) and its transpose, Wb and Wb^T, W and W^T, Wp."""
+    Wa_nz [512,15d] (zero columns dropped) and its transpose, Wb and Wb^T, W and W^T, Wp;
+    plus x (the batch's item_emb_d128, [B,128]) when given -- all in one launch."""
     dev = p["mlp.0.weight"].device
     KC = 15 * d
     spec = [("Wa", p["mlp.0.weight"], H1, KC, 21 * d, 0, wa_remap(d)),
@@ -72,6 +74,8 @@ def bf16_weights(p: Dict[str, torch.Tensor], d: int, a: Dict[str, torch.Tensor],
             ("Wp", p["mm_proj.0.weight"], d, 128, 128, 0, NO_REMAP)]
     if "bilinear.W" in p:
         spec += [("W", p["bilinear.W"], d, d, d, 0, NO_REMAP), ("WT", p["bilinear.W"], d, d, d, 1, NO_REMAP)]
+    if x is not None:
+        spec.append(("x", x, x.shape[0], x.shape[1], x.shape[1], 0, NO_REMAP))
     jobs = (_ConvJob * 8)()
     out = {}
     for i, (name, src, rows, cols, ld, trans, rm) in enumerate(spec):
@@ -244,13 +248,14 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     Lr = 0 if seq is None else L
     x_mm = batch["item_emb_d128"]
     bf = cfg.bf16
-    w16 = bf16_weights(p, d, a, st) if bf else None
+    w16 = bf16_weights(p, d, a, st, x=x_mm) if bf else None
     a["w16"] = w16
     hmm = buf("hmm", (B, d))
-    gemm(x_mm, w16["Wp"] if bf else p["mm_proj.0.weight"], hmm, B, d, 128, 128, 128, d, False, True,
-         bias=p["mm_proj.0.bias"], bf16=bf, stream=st)
+    gemm(w16["x"] if bf else x_mm, w16["Wp"] if bf else p["mm_proj.0.weight"], hmm, B, d, 128, 128, 128, d, False,
+         True, bias=p["mm_proj.0.bias"], bf16=bf, stream=st)
     X = buf("X", (B, 5, d))
     Vc = buf("Vc", (B, 5, d))
+    Vc16 = buf("Vc16", (B, 5, d), torch.bfloat16) if (bf and not cfg.bilinear_each) else None
     KC = 15 * d
     c = buf("c", (B, KC), torch.bfloat16 if bf else torch.float32)     # bf16 mode: GEMM-only operand
     av = buf("a", (B, 6))
@@ -270,7 +275,8 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
          ptr(batch["views_level"]), ptr(hmm), ptr(p["mm_proj.1.weight"]), ptr(p["mm_proj.1.bias"]), LN_EPS,
          ptr(p["cate_emb.weight"]), p["cate_emb.weight"].shape[0], ptr(E), V, ptr(pos),
          ptr(p["senet.excitation.0.weight"]), ptr(p["senet.excitation.0.bias"]),
-         ptr(p["senet.excitation.2.weight"]), ptr(p["senet.excitation.2.bias"]), cfg.R, ptr(X), ptr(Vc), ptr(c), KC,
+         ptr(p["senet.excitation.2.weight"]), ptr(p["senet.excitation.2.bias"]), cfg.R, ptr(X), ptr(Vc), ptr(Vc16),
+         ptr(c), KC,
          int(bf), ptr(av), ptr(cnt), ptr(err), ptr(sm.get("map")), ptr(sm.get("slot_row")), B, Lr, d, st)
     if ev is not None:
         ev[1].record()
@@ -280,7 +286,7 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     U = buf("U", (B, 5, d))
     if not cfg.bilinear_each:
         if bf:   # B(k,n) = W[k][n]: K-contiguous image is W^T
-            gemm(Vc, w16["WT"], U, 5 * B, d, d, d, d, d, False, True, bf16=True, stream=st)
+            gemm(Vc16, w16["WT"], U, 5 * B, d, d, d, d, d, False, True, bf16=True, stream=st)
         else:
             gemm(Vc, p["bilinear.W"], U, 5 * B, d, d, d, d, d, False, False, stream=st)
     else:
@@ -404,11 +410,16 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     # bilinear backward
     dV = torch.empty((B, 5, d), **f32)
     dU = torch.empty((B, 5, d), **f32)
-    call("fbn_pairs_bwd", ptr(dc), ptr(a["Vc"]), ptr(a["U"]), ptr(dV), ptr(dU), B, d, KC, int(cfg.bilinear_each), st)
+    dU16 = torch.empty((B, 5, d), dtype=torch.bfloat16, device=dev) if (bf and not cfg.bilinear_each) else None
+    call("fbn_pairs_bwd", ptr(dc), ptr(a["Vc"]), ptr(a["U"]), ptr(dV), ptr(dU), ptr(dU16), B, d, KC,
+         int(cfg.bilinear_each), st)
     if not cfg.bilinear_each:
-        gemm(dU, w16["W"] if bf else p["bilinear.W"], dV, 5 * B, d, d, d, d, d, False, True, beta=1.0, bf16=bf,
-             stream=st)
-        gemm(a["Vc"], dU, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, bf16=bf, stream=st)
+        if bf:
+            gemm(dU16, w16["W"], dV, 5 * B, d, d, d, d, d, False, True, beta=1.0, stream=st)
+            gemm(a["Vc16"], dU16, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=st)
+        else:
+            gemm(dU, p["bilinear.W"], dV, 5 * B, d, d, d, d, d, False, True, beta=1.0, stream=st)
+            gemm(a["Vc"], dU, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=st)
     else:
         g["bilinear.W_list.0"].zero_()
         for f in range(1, 5):
@@ -423,6 +434,7 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     nblk = _lib.lib().fbn_fields_bwd_grid(B, d)
     partials = torch.empty((nblk, P), **f32)
     dhmm = torch.empty((B, d), **f32)
+    dhmm16 = torch.empty((B, d), dtype=torch.bfloat16, device=dev) if bf else None
     seq = batch.get("item_seq", None)
     Lr = 0 if seq is None else L
     V = p["item_emb.weight"].shape[0] if pos is None else 0
@@ -433,10 +445,12 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     call("fbn_fields_bwd", ptr(batch["item_id"]), ptr(seq) if Lr else None, ptr(batch["likes_level"]),
          ptr(batch["views_level"]), ptr(a["hmm"]), ptr(p["mm_proj.1.weight"]), LN_EPS,
          ptr(p["senet.excitation.0.weight"]), ptr(p["senet.excitation.0.bias"]), ptr(p["senet.excitation.2.weight"]),
-         R, ncate, ptr(a["X"]), ptr(a["a"]), ptr(a["cnt"]), ptr(dV), ptr(dhmm), ptr(partials), outs,
+         R, ncate, ptr(a["X"]), ptr(a["a"]), ptr(a["cnt"]), ptr(dV), ptr(dhmm), ptr(dhmm16), ptr(partials), outs,
          ptr(table_grad), ptr(gvec), V, ptr(pos), ptr(sendbuf), B, Lr, d, st)
-    gemm(dhmm, batch["item_emb_d128"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True, False, bf16=cfg.bf16,
-         stream=st)
+    if bf:
+        gemm(dhmm16, w16["x"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True, False, stream=st)
+    else:
+        gemm(dhmm, batch["item_emb_d128"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True, False, stream=st)
     sums.colsum(dhmm, B, d, d, g["mm_proj.0.bias"], st)
     for job in extra_sums:              # e.g. the trainer's mean loss
         sums.add(*job)

@@ -64,7 +64,8 @@ int fbn_gemm(const void* A, const void* B, float* C, const float* bias, int M, i
 int fbn_fields_fwd(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes, const int64_t* views,
                    const float* hmm, const float* ln_g, const float* ln_b, float ln_eps, const float* cate, int n_cate,
                    const float* table, long long V, const int* pos, const float* w1, const float* b1, const float* w2,
-                   const float* b2, int R, float* X, float* Vc, void* c, int ldc, int c_bf16, float* a_out, float* cnt_out,
+                   const float* b2, int R, float* X, float* Vc, short* Vc16, void* c, int ldc, int c_bf16, float* a_out,
+                   float* cnt_out,
                    int* err, int* map, int* slot_row, int B, int L, int D, void* stream);
 
 /* ---------------------------------------------------------------- K2 + K4 backward
@@ -78,10 +79,12 @@ int fbn_fields_fwd(const int64_t* item_id, const int64_t* item_seq, const int64_
  * P = fbn_fields_bwd_partials_size. */
 int fbn_fields_bwd_partials_size(int D, int R, int n_cate);
 int fbn_fields_bwd_grid(int B, int D);
+/* Vc16 / dhmm16 / dU16 (optional, may be NULL): bf16 copies written beside the fp32 outputs,
+ * the operands of the bf16 GEMMs that consume them (compute_dtype bf16). */
 int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes, const int64_t* views,
                    const float* hmm, const float* ln_g, float ln_eps, const float* w1, const float* b1, const float* w2,
                    int R, int n_cate, const float* X, const float* a, const float* cnt, const float* dV, float* dhmm,
-                   float* partials, float* const* param_grads, float* gtab, float* gvec, long long V, const int* pos,
+                   short* dhmm16, float* partials, float* const* param_grads, float* gtab, float* gvec, long long V, const int* pos,
                    float* sendbuf, int B, int L, int D, void* stream);
 
 /* ---------------------------------------------------------------- K5 bilinear pair products
@@ -89,8 +92,8 @@ int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, const int64_
  * and :81-86 ("each", mode 1).  Pairs (0,j) are structurally zero and not stored. */
 int fbn_pairs_fwd(const float* Vc, const float* U, void* c, int B, int D, int ldc, int mode, int c_bf16,
                   void* stream);
-int fbn_pairs_bwd(const float* dc, const float* Vc, const float* U, float* dV, float* dU, int B, int D, int ldc,
-                  int mode, void* stream);
+int fbn_pairs_bwd(const float* dc, const float* Vc, const float* U, float* dV, float* dU, short* dU16, int B, int D,
+                  int ldc, int mode, void* stream);
 
 /* ---------------------------------------------------------------- K6 BatchNorm + ReLU + dropout
  * Replaces nn.BatchNorm1d / ReLU / Dropout(0.2) of src/model_fibinet.py:127-133.  The stats
