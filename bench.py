@@ -11,9 +11,11 @@ per GPU, row-sharded (N = 8 -> the 10 M rows of config C4).  Weak scaling: per-G
 per-GPU table shard are fixed as N grows.
 
 One JSON line on rank 0 with the contract keys plus
-  roofline:      the dominant kernel (dense Adam over the table shard), HIP events around its
-                 launches inside the probe pass (same stream), algorithmic bytes per launch;
-  roofline_gather: the fused embedding gather (fields_fwd) with SURVEY §8(d)'s 12,984 B/sample;
+  roofline:      the dominant kernel of the step (largest average launch time among the probed
+                 ones), HIP events around its launches inside an eager probe pass (same stream),
+                 algorithmic work per launch (bytes or FLOPs) / that time, against the HBM or
+                 MFMA peak; traffic = PMC-measured HBM bytes per launch when committed;
+  rooflines:     the same for every probed kernel (gather, lazy table-Adam catch-up, MLP GEMM);
   cpu_baseline:  the oracle's torch-CPU restatement of the reference train step (rank 0, N=1).
 """
 from __future__ import annotations
@@ -31,6 +33,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+MFMA_PEAK_TFS = 2500.0         # dense bf16 MFMA (2.5 PFLOP/s, no sparsity)
+FP32_MFMA_PEAK_TFS = 157.0     # fp32 matrix
 ROWS_PER_GPU = 1_250_000
 
 
@@ -45,7 +49,7 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=6)
+    ap.add_argument("--cpu-steps", type=int, default=20)
     ap.add_argument("--probe-steps", type=int, default=10)
     return ap.parse_args()
 
@@ -55,9 +59,22 @@ def gather_bytes_per_sample(d: int, L: int = 20) -> int:
     return (L + 1) * d * 4 + (L + 3) * 8 + 4 * d * 4
 
 
-def adam_table_bytes(rows: int, d: int, touched: int) -> int:
-    # read+write p, m, v (24 B/elem) + the row->slot map (4 B/row) + the touched gradient rows
-    return 24 * rows * d + 4 * rows + 4 * touched * d
+def catchup_bytes(rows: int, d: int, entries: int) -> int:
+    # every row brought up to date: read + write p, m, v (24 B/elem) and last[] (8 B); the
+    # claim list (4 B per entry)
+    return rows * (24 * d + 8) + 4 * entries
+
+
+def _pmc_traffic() -> dict:
+    """HBM bytes per launch from the committed rocprofv3 PMC pass (profiles/*pmc*.json), if any."""
+    import glob
+    out = {}
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json"))):
+        try:
+            out.update({k: v.get("bytes_per_launch") for k, v in json.load(open(f)).items()})
+        except (OSError, ValueError, AttributeError):
+            pass
+    return out
 
 
 def cpu_baseline(args, world):
@@ -197,8 +214,7 @@ def main():
         ev = probe.get(name, [])
         return sum(s.elapsed_time(e) for s, e in ev) / max(1, len(ev))
 
-    adam_ms, gather_ms = avg_ms("adam_table"), avg_ms("fields_fwd")
-    # touched rows of one batch (for the table-Adam byte count): unique non-zero ids routed here
+    # per-launch algorithmic work of the probed kernels (DESIGN.md "Measurement")
     b0 = batches[0][0]
     ids = torch.cat([b0["item_id"], b0["item_seq"].flatten()])
     ids = ids[(ids > 0) & (ids >= tr.rows_lo) & (ids < tr.rows_lo + tr.rows_local)]
@@ -207,10 +223,29 @@ def main():
         tt = torch.tensor([touched], device=dev)
         dist.all_reduce(tt)
         touched = int(tt.item()) // world
-    a_bytes = adam_table_bytes(tr.rows_local, d, touched)
-    a_gbs = a_bytes / (adam_ms * 1e-3) / 1e9
-    g_bytes = gather_bytes_per_sample(d) * B
-    g_gbs = g_bytes / (gather_ms * 1e-3) / 1e9
+    window = -(-tr.rows_local // tr.lazy_window)
+    rooflines = []
+
+    def add(name, kernel, ms, work, unit, peak, bound, detail):
+        if ms > 0:
+            ach = work / (ms * 1e-3) / (1e9 if unit == "GB/s" else 1e12)
+            rooflines.append({"kernel": kernel, "bound": bound, "achieved": round(ach, 1), "peak": peak, "unit": unit,
+                              "frac": round(ach / peak, 4), "traffic": traffic.get(name), "avg_launch_ms": round(ms, 4),
+                              "work_per_launch": work, "work_basis": detail})
+
+    traffic = _pmc_traffic()
+    add("fields_fwd", "fields_fwd (fused gather + history mean + LN + SENET)", avg_ms("fields_fwd"),
+        gather_bytes_per_sample(d) * B, "GB/s", HBM_PEAK_GBS, "hbm", "SURVEY 8(d) 12,984 B/sample x batch")
+    add("adam_catchup", "adam_catchup (lazy table Adam: claimed rows + rolling window)", avg_ms("adam_catchup"),
+        catchup_bytes(touched + window, d, B * (L + 1)), "GB/s", HBM_PEAK_GBS, "hbm",
+        f"(touched {touched} + window {window} rows) x (24 B x d + 8 B) + 4 B per entry")
+    add("gemm_mlp0", "gemm MLP layer 1 (B x 15d -> 512, bf16 MFMA)", avg_ms("gemm_mlp0"),
+        2.0 * B * 512 * 15 * d, "TFLOP/s", MFMA_PEAK_TFS if args.dtype == "bf16" else FP32_MFMA_PEAK_TFS, "mfma",
+        "2 x B x 512 x 15d")
+    if tr.table_adam == "eager":
+        add("adam_table", "adam_table (eager: every untouched row each step)", avg_ms("adam_table"),
+            24 * tr.rows_local * d + 4 * tr.rows_local, "GB/s", HBM_PEAK_GBS, "hbm", "24 B x rows x d + 4 B x rows")
+    dominant = max(rooflines, key=lambda r: r["avg_launch_ms"]) if rooflines else None
 
     if rank == 0:
         samples = K * B * world
@@ -233,14 +268,9 @@ def main():
                        "item_rows": V, "item_rows_per_gpu": tr.rows_local, "emb_dim": d,
                        "parallelism": f"row-shard{world}" if world > 1 else "single",
                        "hipgraph": bool(graphs)},
-            "roofline": {"kernel": "adam_table (dense Adam over the item-table shard)", "bound": "hbm",
-                         "achieved": round(a_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(a_gbs / HBM_PEAK_GBS, 4), "traffic": None,
-                         "bytes_per_launch": a_bytes, "avg_launch_ms": round(adam_ms, 4)},
-            "roofline_gather": {"kernel": "fields_fwd (fused gather + LN + SENET)", "bound": "hbm",
-                                "achieved": round(g_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                "frac": round(g_gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": g_bytes,
-                                "avg_launch_ms": round(gather_ms, 4)},
+            "roofline": dominant,
+            "rooflines": rooflines,
+            "table_adam": tr.table_adam,
             "final_loss": round(loss, 5),
         }
         if world == 1 and not args.no_cpu_baseline:

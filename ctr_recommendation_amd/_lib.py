@@ -62,14 +62,17 @@ SIGNATURES = {
     "fbn_sum": (I, [P, I, P, F, P]),
     "fbn_sumsq": (I, [P, LL, P, I, P, P]),
     "fbn_clip_coef": (I, [P, F, P, P, P]),
-    "fbn_adam_dense": (I, [P, P, P, P, LL, P, P, P, F, F, F, P]),
+    "fbn_adam_dense": (I, [P, P, P, P, LL, P, P, P, F, F, F, P, F, P, P, P]),
     "fbn_sparse_fixup": (I, [P, P, P, I, I, LL, I, P, P, P, P, I, I, P]),
     "fbn_sumsq_sparse": (I, [P, P, P, I, I, I, P, P]),
     "fbn_adam_table": (I, [P, P, P, LL, I, P, P, P, P, I, P, P, P, F, F, F, I, P]),
-    "fbn_adam_touched": (I, [P, P, P, I, P, P, P, P, I, I, P, P, P, F, F, F, P]),
+    "fbn_adam_touched": (I, [P, P, P, I, P, P, P, P, I, I, P, P, P, F, F, F, P, P]),
+    "fbn_adam_catchup": (I, [P, P, P, LL, I, P, I, P, I, P, P, P, F, F, F, P]),
+    "fbn_adam_flush": (I, [P, P, P, LL, I, P, P, P, F, F, F, P]),
     "fbn_claim_rows": (I, [P, P, I, I, LL, P, P, P]),
     "fbn_step_end": (I, [P, P, P, P, P, P]),
     "fbn_route": (I, [P, P, I, I, LL, LL, I, P, P, P, P, P, P, P]),
+    "fbn_owner_claim": (I, [P, I, P, P, I, P]),
     "fbn_owner_gather": (I, [P, I, P, P, P, P, I, I, P]),
 }
 

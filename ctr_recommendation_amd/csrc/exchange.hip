@@ -88,7 +88,30 @@ __global__ void __launch_bounds__(256) owner_gather_kernel(const int* __restrict
   }
 }
 
+// Registration only (the lazy table Adam must replay the claimed rows BEFORE they are
+// gathered): same claims as owner_gather_kernel's map path.
+__global__ void owner_claim_kernel(const int* __restrict__ ids, int n, int* map, int* slot_row, int rank) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int r = ids[i];
+    if (rank == 0 && r == 0) continue;
+    if (__hip_atomic_load(map + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != -1) continue;
+    int expected = -1;
+    if (__hip_atomic_compare_exchange_strong(map + r, &expected, i, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT))
+      slot_row[i] = r;
+  }
+}
+
 // ------------------------------------------------------------------ C ABI
+extern "C" int fbn_owner_claim(const int* ids, int n, int* map, int* slot_row, int rank, void* stream) {
+  if (n <= 0) return FBN_OK;
+  int blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(owner_claim_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, ids, n, map, slot_row, rank);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
 extern "C" int fbn_route(const int64_t* item, const int64_t* seq, int B, int L, long long V, long long Vl, int nranks,
                          int* counts, int* offsets, int* cursor, int* send_ids, int* pos, int* err, void* stream) {
   if (nranks < 1 || nranks > 64) { fbn_set_error("route: 1 <= nranks <= 64"); return FBN_ERR_ARG; }

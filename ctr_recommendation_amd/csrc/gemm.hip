@@ -587,6 +587,23 @@ __global__ void __launch_bounds__(256) gemm_dma16_kernel(GemmArgs g, int tiles_n
   gemm_epilogue<BM, BN>(g, acc, m0, n0, wm, wn, lr, lh, reinterpret_cast<float*>(smem));
 }
 
+// vectorised split-K reduce: 4 consecutive columns per thread (N, ldc and the C remap in
+// multiples of 4, C 16-B aligned); same slab order as gemm_splitk_reduce (bit-identical)
+__global__ void gemm_splitk_reduce4(GemmArgs g, int nsplit) {
+  const int N4 = g.N >> 2;
+  const size_t total4 = (size_t)g.M * N4, total = (size_t)g.M * g.N;
+  for (size_t i4 = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i4 < total4; i4 += (size_t)gridDim.x * blockDim.x) {
+    const int m = (int)(i4 / N4), n = (int)(i4 - (size_t)m * N4) * 4;
+    const size_t idx = (size_t)m * g.N + n;
+    f32x4 s = *reinterpret_cast<const f32x4*>(g.ws + idx);
+    for (int z = 1; z < nsplit; ++z) s += *reinterpret_cast<const f32x4*>(g.ws + (size_t)z * total + idx);
+    if (g.bias) s += *reinterpret_cast<const f32x4*>(g.bias + n);
+    float* cp = g.C + (size_t)m * g.ldc + remap(g.rC, n);
+    if (g.beta != 0.f) s += g.beta * *reinterpret_cast<const f32x4*>(cp);
+    *reinterpret_cast<f32x4*>(cp) = s;
+  }
+}
+
 // split-K reduce with the BatchNorm statistics epilogue: one workgroup per 64x64 tile of C;
 // thread (col = tid & 63, rows 16*(tid >> 6) .. +15) -> coalesced slab reads along n.  Sums the
 // K-slabs in the same order as gemm_splitk_reduce (so C is bit-identical with or without stats),
@@ -667,7 +684,13 @@ static GemmPlan plan_gemm(int M, int N, int K, int bk) {
 // split K up to ~512 (128x64 tiles, M, N >= 512) or ~256 (64x64) workgroups, >= 4 K-steps each.
 static GemmPlan plan_dma16(int M, int N, int K) {
   const long long t64 = (long long)fbn_cdiv(M, 64) * fbn_cdiv(N, 64);
-  if (t64 >= 512) return {64, 64, 1};
+  if (t64 >= 512) {
+    if (const char* e = getenv("FBN_DMA_BIG_TILE")) {   // tuning knob: "bm,bn" for large outputs
+      int a = 64, b = 64;
+      if (sscanf(e, "%d,%d", &a, &b) == 2) return {a, b, 1};
+    }
+    return {64, 64, 1};
+  }
   GemmPlan p = (M >= 512 && N >= 512) ? GemmPlan{128, 64, 1} : GemmPlan{64, 64, 1};
   const long long tiles = (long long)fbn_cdiv(M, p.bm) * fbn_cdiv(N, p.bn);
   const long long target = p.bm == 128 ? 512 : 256;
@@ -799,10 +822,13 @@ extern "C" int fbn_gemm(const void* A, const void* B, float* C, const float* bia
                        p.split);
     FBN_CHECK_LAUNCH();
   } else if (p.split > 1) {
-    const size_t total = (size_t)M * N;
+    const bool v4 = !(N & 3) && !(ldc & 3) && !((uintptr_t)C & 15) && (!bias || !((uintptr_t)bias & 15)) &&
+                    (rC_seg == 0x7fffffff || !(rC_seg & 3)) && !(rC_off0 & 3) && !(rC_off1 & 3);
+    const size_t total = v4 ? (size_t)M * N / 4 : (size_t)M * N;
     int blocks = (int)((total + 255) / 256);
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, st, g, p.split);
+    if (v4) hipLaunchKernelGGL(gemm_splitk_reduce4, dim3(blocks), dim3(256), 0, st, g, p.split);
+    else hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, st, g, p.split);
     FBN_CHECK_LAUNCH();
   }
   return FBN_OK;

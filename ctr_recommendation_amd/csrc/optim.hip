@@ -75,12 +75,41 @@ __device__ __forceinline__ float adam_elem(float& p, float& m, float& v, float g
   return p;
 }
 
+// clip coefficient of clip_grad_norm_ from the sumsq slots (same sequential order as
+// clip_coef_kernel, so the value is bit-identical)
+__device__ __forceinline__ float clip_from_slots(const double* sumsq, float max_norm, float* total_out) {
+  double s = 0.0;
+  for (int i = 0; i < FBN_SUMSQ_SLOTS; ++i) s += sumsq[i];
+  const float total = sqrtf((float)s);
+  const float c = max_norm / (total + 1e-6f);
+  *total_out = total;
+  return c < 1.f ? c : 1.f;
+}
+
+// sumsq != null: the clip coefficient is computed here (every block, thread 0) and block 0
+// publishes it (coef_out, norm_out) for the table passes that follow -- no clip_coef launch.
 __global__ void adam_dense_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                   float* __restrict__ v, long long n, const float* __restrict__ coef_ptr,
                                   const AdamConsts* __restrict__ table, const int* __restrict__ step_ptr, float wd,
-                                  float b2, float omb2, float eps) {
+                                  float b2, float omb2, float eps, const double* __restrict__ sumsq, float max_norm,
+                                  float* coef_out, float* norm_out) {
   const AdamConsts k = table[*step_ptr];
-  const float coef = coef_ptr ? *coef_ptr : 1.f;
+  float coef;
+  if (sumsq) {
+    __shared__ float sc;
+    if (threadIdx.x == 0) {
+      float total;
+      sc = clip_from_slots(sumsq, max_norm, &total);
+      if (blockIdx.x == 0) {
+        if (coef_out) *coef_out = sc;
+        if (norm_out) *norm_out = total;
+      }
+    }
+    __syncthreads();
+    coef = sc;
+  } else {
+    coef = coef_ptr ? *coef_ptr : 1.f;
+  }
   const long long n4 = n / 4;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
     f32x4 pp = *reinterpret_cast<f32x4*>(p + 4 * i);
@@ -309,6 +338,108 @@ __global__ void __launch_bounds__(256) adam_table_untouched(FBN_ADAM_TABLE_ARGS)
   }
 }
 
+// ------------------------------------------------------------------ lazy table Adam (exact)
+// A row whose loss gradient is zero at step s still gets torch's coupled-L2 Adam update
+// (g = 0 * coef + wd * p, then m, v, p).  That update depends only on the row and on step s's
+// schedule constants, so it can be REPLAYED later with the same float operations in the same
+// order: bit-identical to stepping it eagerly.  last[r] = number of Adam steps applied to row r.
+// Each step, before the gather reads the table, fbn_adam_catchup brings every row the batch
+// claimed, plus a rolling window of nrows/F rows (window (step mod F)), up to `step`; the rolling
+// window bounds every row's lag by F steps.  fbn_adam_touched then applies the step with the real
+// gradient (last = step + 1).  fbn_adam_flush brings the whole table up to date (checkpoint,
+// evaluation).  The schedule constants of the last W <= FBN_LAZY_MAX_LAG steps sit in LDS.
+#define FBN_LAZY_MAX_LAG 512
+
+template <int D>
+__device__ __forceinline__ void replay_rows(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
+                                            long long r, int q, int k0, int t, const AdamConsts* __restrict__ win,
+                                            int w0, const AdamConsts* __restrict__ table, float wd, float b2,
+                                            float omb2, float eps) {
+  const size_t off = (size_t)r * D + 4 * q;
+  f32x4 pp = *reinterpret_cast<f32x4*>(p + off);
+  f32x4 mm = *reinterpret_cast<f32x4*>(m + off);
+  f32x4 vv = *reinterpret_cast<f32x4*>(v + off);
+  for (int s = k0; s < t; ++s) {
+    const AdamConsts k = s >= w0 ? win[s - w0] : table[s];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float pe = pp[e], me = mm[e], ve = vv[e];
+      adam_elem(pe, me, ve, 0.f, 1.f, wd, b2, omb2, eps, k);
+      pp[e] = pe; mm[e] = me; vv[e] = ve;
+    }
+  }
+  *reinterpret_cast<f32x4*>(p + off) = pp;
+  *reinterpret_cast<f32x4*>(m + off) = mm;
+  *reinterpret_cast<f32x4*>(v + off) = vv;
+}
+
+// items [0, n_ent): claiming entries (slot_row != -1); items [n_ent, n_ent + chunk): rows of the
+// rolling window not claimed this step.  nrows_total / F / chunk describe the window.
+template <int D>
+__global__ void __launch_bounds__(256) adam_catchup_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                           float* __restrict__ v, const int* __restrict__ slot_row,
+                                                           int n_ent, const int* __restrict__ map, long long nrows,
+                                                           int F, long long chunk, int* __restrict__ last,
+                                                           const AdamConsts* __restrict__ table,
+                                                           const int* __restrict__ step, float wd, float b2,
+                                                           float omb2, float eps) {
+  constexpr int G = D / 4, RPW = 64 / G;
+  __shared__ AdamConsts win[FBN_LAZY_MAX_LAG];
+  const int t = *step;
+  const int w0 = t > FBN_LAZY_MAX_LAG ? t - FBN_LAZY_MAX_LAG : 0;
+  for (int i = threadIdx.x; i < t - w0; i += blockDim.x) win[i] = table[w0 + i];
+  __syncthreads();
+  const long long roll0 = (long long)(t % F) * chunk;
+  const long long nroll = roll0 < nrows ? min(chunk, nrows - roll0) : 0;
+  const long long n = n_ent + nroll;
+  const int lane = threadIdx.x & 63, q = lane % G;
+  const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+  for (long long i0 = gw * RPW; i0 < n; i0 += nw * RPW) {
+    const long long i = i0 + lane / G;
+    if (i >= n) continue;
+    long long r;
+    if (i < n_ent) {
+      const int sr = slot_row[i];
+      if (sr == -1) continue;
+      r = sr & ~FBN_SLOT_FLAG;
+    } else {
+      r = roll0 + (i - n_ent);
+      if (map && map[r] != -1) continue;   // claimed this step: its claiming entry replays it
+    }
+    const int k0 = last[r];
+    if (k0 >= t) continue;
+    replay_rows<D>(p, m, v, r, q, k0, t, win, w0, table, wd, b2, omb2, eps);
+    if (q == 0) last[r] = t;
+  }
+}
+
+// every row up to `step` (checkpoint / evaluation)
+template <int D>
+__global__ void __launch_bounds__(256) adam_flush_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                         float* __restrict__ v, long long nrows, int* __restrict__ last,
+                                                         const AdamConsts* __restrict__ table,
+                                                         const int* __restrict__ step, float wd, float b2, float omb2,
+                                                         float eps) {
+  constexpr int G = D / 4, RPW = 64 / G;
+  __shared__ AdamConsts win[FBN_LAZY_MAX_LAG];
+  const int t = *step;
+  const int w0 = t > FBN_LAZY_MAX_LAG ? t - FBN_LAZY_MAX_LAG : 0;
+  for (int i = threadIdx.x; i < t - w0; i += blockDim.x) win[i] = table[w0 + i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, q = lane % G;
+  const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+  for (long long r0 = gw * RPW; r0 < nrows; r0 += nw * RPW) {
+    const long long r = r0 + lane / G;
+    if (r >= nrows) continue;
+    const int k0 = last[r];
+    if (k0 >= t) continue;
+    replay_rows<D>(p, m, v, r, q, k0, t, win, w0, table, wd, b2, omb2, eps);
+    if (q == 0) last[r] = t;
+  }
+}
+
 // Touched rows: one group per claiming entry e (slot_row[e] = row | FLAG); gradient =
 // gvec-slot(e) (+ extra[e]); Adam with the clip coefficient; the row's map entry is reset.
 template <int D>
@@ -317,7 +448,7 @@ __global__ void __launch_bounds__(256) adam_touched_kernel(float* __restrict__ p
                                                            int n, const float* __restrict__ coef_ptr,
                                                            const AdamConsts* __restrict__ table,
                                                            const int* __restrict__ step_ptr, float wd, float b2,
-                                                           float omb2, float eps) {
+                                                           float omb2, float eps, int* __restrict__ last) {
   constexpr int G = D / 4, RPW = 64 / G;
   const AdamConsts k = table[*step_ptr];
   const float coef = coef_ptr ? *coef_ptr : 1.f;
@@ -349,7 +480,10 @@ __global__ void __launch_bounds__(256) adam_touched_kernel(float* __restrict__ p
     *reinterpret_cast<f32x4*>(p + off) = pp;
     *reinterpret_cast<f32x4*>(m + off) = mm;
     *reinterpret_cast<f32x4*>(v + off) = vv;
-    if (q == 0) map[r] = -1;
+    if (q == 0) {
+      map[r] = -1;
+      if (last) last[r] = *step_ptr + 1;
+    }
   }
 }
 
@@ -379,7 +513,7 @@ extern "C" int fbn_clip_coef(const double* sumsq, float max_norm, float* coef, f
 
 extern "C" int fbn_adam_dense(float* p, const float* g, float* m, float* v, long long n, const float* coef,
                               const void* consts_table, const int* step, float wd, float beta2, float eps,
-                              void* stream) {
+                              const double* sumsq, float max_norm, float* coef_out, float* norm_out, void* stream) {
   if (n <= 0) return FBN_OK;
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) {
     fbn_set_error("adam_dense: 16-byte alignment required");
@@ -389,7 +523,8 @@ extern "C" int fbn_adam_dense(float* p, const float* g, float* m, float* v, long
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(adam_dense_kernel, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, coef,
-                     (const AdamConsts*)consts_table, step, wd, beta2, (float)(1.0 - (double)beta2), eps);
+                     (const AdamConsts*)consts_table, step, wd, beta2, (float)(1.0 - (double)beta2), eps, sumsq,
+                     max_norm, coef_out, norm_out);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -460,14 +595,14 @@ extern "C" int fbn_adam_table(float* p, float* m, float* v, long long nrows, int
 
 extern "C" int fbn_adam_touched(float* p, float* m, float* v, int D, int* map, const float* gvec, float* extra,
                                 int* slot_row, int Lp1, int n, const float* coef, const void* consts_table,
-                                const int* step, float wd, float beta2, float eps, void* stream) {
+                                const int* step, float wd, float beta2, float eps, int* last, void* stream) {
   if (n <= 0) return FBN_OK;
   hipStream_t st = (hipStream_t)stream;
   const float omb2 = (float)(1.0 - (double)beta2);
   const AdamConsts* t = (const AdamConsts*)consts_table;
   GradSrc s{gvec, extra, slot_row, Lp1};
   FBN_DISPATCH_D(adam_touched_kernel, D, group_grid(n, D, 8192), p, m, v, map, s, n, coef, t, step, wd, beta2,
-                 omb2, eps);
+                 omb2, eps, last);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -487,6 +622,34 @@ extern "C" int fbn_claim_rows(const int64_t* item, const int64_t* seq, int B, in
 extern "C" int fbn_step_end(int* step, unsigned long long* rng, double* sumsq, long long* nbt0, long long* nbt1,
                             void* stream) {
   hipLaunchKernelGGL(step_end_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step, rng, sumsq, nbt0, nbt1);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+
+// lazy table Adam: replay the zero-loss-gradient steps of the claimed rows and of rolling window
+// (step mod F) (chunk = ceil(nrows / F) rows) up to `step`; last: [nrows] steps applied per row
+extern "C" int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, int D, const int* slot_row, int n_ent,
+                                const int* map, int F, int* last, const void* consts_table, const int* step, float wd,
+                                float beta2, float eps, void* stream) {
+  if (nrows <= 0) return FBN_OK;
+  if (F < 1 || F > FBN_LAZY_MAX_LAG) { fbn_set_error("fbn_adam_catchup: 1 <= F <= 512"); return FBN_ERR_ARG; }
+  hipStream_t st = (hipStream_t)stream;
+  const float omb2 = (float)(1.0 - (double)beta2);
+  const long long chunk = (nrows + F - 1) / F;
+  FBN_DISPATCH_D(adam_catchup_kernel, D, group_grid(n_ent + chunk, D, 8192), p, m, v, slot_row, n_ent, map, nrows, F,
+                 chunk, last, (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+extern "C" int fbn_adam_flush(float* p, float* m, float* v, long long nrows, int D, int* last, const void* consts_table,
+                              const int* step, float wd, float beta2, float eps, void* stream) {
+  if (nrows <= 0) return FBN_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const float omb2 = (float)(1.0 - (double)beta2);
+  FBN_DISPATCH_D(adam_flush_kernel, D, group_grid(nrows, D, 16384), p, m, v, nrows, last,
+                 (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

@@ -34,6 +34,9 @@ class HipExchangeKernels:
         call("fbn_route", ptr(item), ptr(seq), B, L, V, Vl, world, ptr(counts), ptr(offsets), ptr(cursor),
              ptr(send_ids), ptr(pos), ptr(err), _lib.stream_handle(item.device))
 
+    def owner_claim(self, ids, map_, slot_row, rank):
+        call("fbn_owner_claim", ptr(ids), ids.shape[0], ptr(map_), ptr(slot_row), rank, _lib.stream_handle(ids.device))
+
     def owner_gather(self, ids, E, out, map_, slot_row, rank, d):
         call("fbn_owner_gather", ptr(ids), ids.shape[0], ptr(E), ptr(out), ptr(map_), ptr(slot_row), rank, d,
              _lib.stream_handle(E.device))
@@ -75,8 +78,10 @@ class RowExchange:
         out.copy_(o)
         return out
 
-    def forward(self, item, seq, E_local, sparse, err) -> torch.Tensor:
-        """Returns the requester's row buffer [n_sent, d]; self.pos maps (b, t) -> row (or -1)."""
+    def forward(self, item, seq, E_local, sparse, err, before_gather=None) -> torch.Tensor:
+        """Returns the requester's row buffer [n_sent, d]; self.pos maps (b, t) -> row (or -1).
+        before_gather(n_recv): runs at the owner between registering the requested rows in the
+        sparse map and gathering them (the lazy table Adam brings them up to date there)."""
         B = item.shape[0]
         L = 0 if seq is None else seq.shape[1]
         pos = self.pos[:B, :L + 1] if L == self.L else torch.empty((B, L + 1), dtype=torch.int32, device=item.device)
@@ -92,7 +97,12 @@ class RowExchange:
         self.recv_ids = torch.empty(n_recv, dtype=torch.int32, device=item.device)
         self._a2a(self.recv_ids, self.send_ids[:n_send], rc, sc)
         reply = torch.empty((n_recv, self.d), dtype=torch.float32, device=item.device)
-        self.k.owner_gather(self.recv_ids, E_local, reply, sparse["map"], sparse["slot_row"], self.rank, self.d)
+        if before_gather is not None and sparse.get("map") is not None:
+            self.k.owner_claim(self.recv_ids, sparse["map"], sparse["slot_row"], self.rank)
+            before_gather(n_recv)
+            self.k.owner_gather(self.recv_ids, E_local, reply, None, None, self.rank, self.d)
+        else:
+            self.k.owner_gather(self.recv_ids, E_local, reply, sparse["map"], sparse["slot_row"], self.rank, self.d)
         rows = torch.empty((n_send, self.d), dtype=torch.float32, device=item.device)
         self._a2a(rows, reply, sc, rc)
         return rows

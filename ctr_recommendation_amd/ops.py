@@ -301,12 +301,19 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     fuse = cfg.training
     t1 = buf("tiles1", (nt, H1, 2)) if fuse else None      # fused BN statistics (GEMM epilogue)
     t2 = buf("tiles2", (nt, H2, 2)) if fuse else None
+    ev1 = None
+    if probe is not None:                       # bench: HIP events around the MLP's first GEMM
+        ev1 = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev1[0].record()
+        probe.setdefault("gemm_mlp0", []).append(ev1)
     if bf:
         gemm(c, w16["Wa"], h1pre, B, H1, KC, KC, KC, H1, False, True, bias=p["mlp.0.bias"], bf16=True, stream=st,
              stats=t1)
     else:
         gemm(c, p["mlp.0.weight"], h1pre, B, H1, KC, KC, 21 * d, H1, False, True, bias=p["mlp.0.bias"],
              rB=wa_remap(d), stream=st, stats=t1)
+    if ev1 is not None:
+        ev1[1].record()
     mean1, inv1 = buf("mean1", (H1,)), buf("inv1", (H1,))
     mean2, inv2 = buf("mean2", (H2,)), buf("inv2", (H2,))
     h1 = buf("h1", (B, H1))

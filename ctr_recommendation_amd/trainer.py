@@ -63,7 +63,8 @@ class FiBiNETTrainer:
     def __init__(self, model_cfg: Dict, total_steps: int, batch_size: int, *, device=None, max_len: int = 20,
                  lr: Optional[float] = None, weight_decay: Optional[float] = None, rank: int = 0, world: int = 1,
                  group=None, init_state: Optional[Dict[str, torch.Tensor]] = None, seed: int = 2025,
-                 stage_on_cpu: bool = False, dropout_seed: Optional[int] = None):
+                 stage_on_cpu: bool = False, dropout_seed: Optional[int] = None, table_adam: str = "lazy",
+                 lazy_window: int = 128):
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise RuntimeError("FiBiNETTrainer runs on a HIP device only (no CPU fallback)")
@@ -148,8 +149,16 @@ class FiBiNETTrainer:
         self.xchg = RowExchange(rank, world, self.V, d, self.B, max_len, dev, group,
                                 stage_on_cpu=stage_on_cpu) if world > 1 else None
         self.stage_on_cpu = stage_on_cpu
-        self.side = torch.cuda.Stream(device=dev)       # untouched-row Adam overlaps the backward
-        self.serial_adam = os.environ.get("FBN_SERIAL_ADAM", "0") == "1"   # profiling knob: no overlap
+        # item-table Adam: "lazy" (default) replays the zero-gradient steps of a row when the row
+        # is next claimed or its rolling window comes round (exact; see fbn_adam_catchup) --
+        # "eager" streams every untouched row each step on a side stream (the reference's dense
+        # update order, kept for A/B measurements)
+        self.table_adam = os.environ.get("FBN_TABLE_ADAM", table_adam)
+        if self.table_adam not in ("lazy", "eager"):
+            raise ValueError(f"table_adam must be 'lazy' or 'eager', not {self.table_adam!r}")
+        self.lazy_window = int(lazy_window)
+        self.last = torch.zeros(max(1, self.rows_local), **i32)     # Adam steps applied per table row
+        self.side = torch.cuda.Stream(device=dev) if self.table_adam == "eager" else None
 
     # ------------------------------------------------------------------ one training step
     def step(self, batch: Dict[str, torch.Tensor], labels: torch.Tensor,
@@ -177,29 +186,40 @@ class FiBiNETTrainer:
         rows = pos = None
         main = torch.cuda.current_stream(self.device)
 
-        side = main if self.serial_adam else self.side
+        lazy = self.table_adam == "lazy"
+
+        def catch_up(n_ent):
+            # lazy table Adam: rows claimed this step (and rolling window step % F) -> `step`
+            # Adam steps, before anything reads them
+            ev = _events(probe, "adam_catchup")
+            call("fbn_adam_catchup", ptr(self.E), ptr(self.Em), ptr(self.Ev), self.rows_local, d, ptr(self.slot_row),
+                 n_ent, ptr(self.map), self.lazy_window, ptr(self.last), ptr(self.sched), ptr(self.step_dev), self.wd,
+                 self.beta2, self.eps, st)
+            _events_end(ev)
 
         def start_untouched_adam():
-            # every row of this shard the batch touches is claimed in `map` by now; the rest get
-            # g = wd * p, independent of the backward -> run them concurrently on the side stream
-            side.wait_stream(main)
-            ev = _events(probe, "adam_table", side)
+            # eager mode: every row this shard's batch does not touch gets g = wd * p, independent
+            # of the backward -> concurrently on the side stream
+            self.side.wait_stream(main)
+            ev = _events(probe, "adam_table", self.side)
             call("fbn_adam_table", ptr(self.E), ptr(self.Em), ptr(self.Ev), self.rows_local, d, ptr(self.map),
-                 None, None, None, 1, None, ptr(self.sched), ptr(self.step_dev), self.wd, self.beta2, self.eps,
-                 2 if self.serial_adam else 1, side.cuda_stream)
-            _events_end(ev, side)
+                 None, None, None, 1, None, ptr(self.sched), ptr(self.step_dev), self.wd, self.beta2, self.eps, 1,
+                 self.side.cuda_stream)
+            _events_end(ev, self.side)
 
         if self.xchg is not None:
             rows = self.xchg.forward(batch["item_id"], seq, self.E, {"map": self.map, "slot_row": self.slot_row},
-                                     self.err)
+                                     self.err, before_gather=catch_up if lazy else None)
             pos = self.xchg.cur_pos
         else:
             call("fbn_claim_rows", ptr(batch["item_id"]), ptr(seq) if L else None, B, L, self.V, ptr(self.map),
                  ptr(self.slot_row), st)
-        start_untouched_adam()
+            if lazy:
+                catch_up(B * (L + 1))
         a = ops.forward(self.p, batch, cfg, self.rng, table_rows=rows, pos=pos, err=self.err, labels=labels,
                         loss_denom=float(ntot), coll=self.coll, ntot=ntot, acts=self.acts, masks_out=masks_out,
-                        probe=probe, count_batches=False)     # num_batches_tracked: fbn_step_end
+                        probe=probe, count_batches=False,     # num_batches_tracked: fbn_step_end
+                        after_gather=None if lazy else start_untouched_adam)
         sendbuf = self.xchg.make_sendbuf() if self.xchg is not None else None
         ops.backward(self.p, batch, a, a["gout"], self.g, cfg, gvec=self.gvec if self.xchg is None else None,
                      pos=pos, sendbuf=sendbuf, coll=self.coll, ntot=ntot,
@@ -226,14 +246,16 @@ class FiBiNETTrainer:
             self.coll.allreduce_(self.sumsq_tab)
             self.sumsq.add_(self.sumsq_tab)
             self.sumsq_tab.zero_()
-        call("fbn_clip_coef", ptr(self.sumsq), self.max_norm, ptr(self.coef), ptr(self.norm), st)
+        # clip_grad_norm_(10) is applied inside the dense Adam launch (it publishes coef / norm)
         call("fbn_adam_dense", ptr(self.flat_p), ptr(self.flat_g), ptr(self.flat_m), ptr(self.flat_v),
-             self.n_dense, ptr(self.coef), ptr(self.sched), ptr(self.step_dev), self.wd, self.beta2, self.eps, st)
-        main.wait_stream(side)                       # untouched pass done before map entries are reset
+             self.n_dense, None, ptr(self.sched), ptr(self.step_dev), self.wd, self.beta2, self.eps, ptr(self.sumsq),
+             self.max_norm, ptr(self.coef), ptr(self.norm), st)
+        if not lazy:
+            main.wait_stream(self.side)              # untouched pass done before map entries are reset
         ev = _events(probe, "adam_touched")
         call("fbn_adam_touched", ptr(self.E), ptr(self.Em), ptr(self.Ev), d, ptr(self.map), ptr(gsrc[0]),
              ptr(gsrc[1]), ptr(self.slot_row), gsrc[2], n_ent, ptr(self.coef), ptr(self.sched), ptr(self.step_dev),
-             self.wd, self.beta2, self.eps, st)
+             self.wd, self.beta2, self.eps, ptr(self.last) if lazy else None, st)
         _events_end(ev)
         self.slot_row[:n_ent].fill_(-1)
         call("fbn_step_end", ptr(self.step_dev), ptr(self.rng), ptr(self.sumsq), ptr(self.p["mlp.1.num_batches_tracked"]),
@@ -242,8 +264,15 @@ class FiBiNETTrainer:
         return self.loss
 
     # ------------------------------------------------------------------ inference
+    def flush(self) -> None:
+        """Bring every table row up to the current step (lazy table Adam); a no-op when eager."""
+        if self.table_adam == "lazy":
+            call("fbn_adam_flush", ptr(self.E), ptr(self.Em), ptr(self.Ev), self.rows_local, self.d, ptr(self.last),
+                 ptr(self.sched), ptr(self.step_dev), self.wd, self.beta2, self.eps, _lib.stream_handle(self.device))
+
     @torch.no_grad()
     def predict(self, batch: Dict[str, torch.Tensor], logits: bool = False) -> torch.Tensor:
+        self.flush()
         cfg = ops.FwdConfig(**{**self.fcfg.__dict__, "training": False})
         cfg.L = batch["item_seq"].shape[1] if "item_seq" in batch else 0
         rows = pos = None
@@ -265,6 +294,7 @@ class FiBiNETTrainer:
     def state_dict(self) -> Dict[str, torch.Tensor]:
         """Reference state_dict (CPU tensors).  Multi-GPU: collective; the full table on every rank."""
         import torch.distributed as dist
+        self.flush()
         out = {}
         if self.world > 1:
             local = torch.zeros((self.Vl, self.d), dtype=torch.float32, device=self.device)
@@ -285,8 +315,10 @@ class FiBiNETTrainer:
 
     def load_state_dict(self, sd: Dict[str, torch.Tensor]) -> None:
         """Load reference-format weights (optimizer state is reset, as the reference never saves it)."""
+        self.flush()
         for k in self.key_order:
             if k == TABLE:
                 self.E.copy_(sd[k][self.rows_lo:self.rows_lo + self.rows_local].to(self.device))
             else:
                 self.p[k].copy_(sd[k].to(self.device))
+        self.last.fill_(self.host_step)             # loaded rows are current

@@ -164,8 +164,12 @@ int fbn_sum(const float* x, int n, float* out, float scale, void* stream);
  * (:78,121); the schedule table carries OneCycleLR's lr/beta1 per step (:84-92,122). */
 int fbn_sumsq(const float* x, long long n, const int* n_rows, int row_len, double* out, void* stream);
 int fbn_clip_coef(const double* sumsq, float max_norm, float* coef, float* norm, void* stream);
+/* sumsq (optional): the FBN_SUMSQ_SLOTS norm accumulators -- the kernel then applies
+ * clip_grad_norm_(max_norm) itself (same arithmetic as fbn_clip_coef) and writes the coefficient
+ * and the total norm to coef_out / norm_out for the table passes that follow; else coef is read. */
 int fbn_adam_dense(float* p, const float* g, float* m, float* v, long long n, const float* coef,
-                   const void* consts_table, const int* step, float wd, float beta2, float eps, void* stream);
+                   const void* consts_table, const int* step, float wd, float beta2, float eps, const double* sumsq,
+                   float max_norm, float* coef_out, float* norm_out, void* stream);
 /* Sparse table gradient.  Slots are entry indices; gvec is the per-sample vector buffer of
  * fbn_fields_bwd (Lp1 = L+1) or the owner's received per-entry rows (Lp1 = 1).  fixup folds
  * entries whose row was claimed by another entry into that claimer (extra[] + a flag bit in
@@ -184,7 +188,20 @@ int fbn_adam_table(float* p, float* m, float* v, long long nrows, int D, int* ma
                    float beta2, float eps, int mode, void* stream);
 int fbn_adam_touched(float* p, float* m, float* v, int D, int* map, const float* gvec, float* extra, int* slot_row,
                      int Lp1, int n, const float* coef, const void* consts_table, const int* step, float wd,
+                     float beta2, float eps, int* last, void* stream);
+/* Lazy table Adam (exact): last[r] = Adam steps applied to row r.  fbn_adam_catchup replays the
+ * zero-loss-gradient steps (coupled L2 decay only: g = 0*coef + wd*p) of the rows claimed in
+ * slot_row and of rolling window (step mod F) (ceil(nrows/F) rows) up to *step, with the same
+ * float operations in the same order as stepping them (bit-identical); fbn_adam_touched(last)
+ * then applies the step with the gradient; fbn_adam_flush brings every row up to date.
+ * Replaces the per-step dense Adam pass of torch.optim.Adam over item_emb.weight
+ * (src/train_fibinet.py:78,121) by O(touched + nrows/F) rows per step.  F <= 512. */
+int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, int D, const int* slot_row, int n_ent,
+                     const int* map, int F, int* last, const void* consts_table, const int* step, float wd,
                      float beta2, float eps, void* stream);
+int fbn_adam_flush(float* p, float* m, float* v, long long nrows, int D, int* last, const void* consts_table,
+                   const int* step, float wd, float beta2, float eps, void* stream);
+
 /* sumsq accumulators are FBN_SUMSQ_SLOTS (= 64) doubles; fbn_clip_coef sums them and
  * fbn_step_end zeroes them.  fbn_claim_rows registers the rows of a batch in map/slot_row (the
  * same claims fbn_fields_fwd makes when given a map), as a tiny kernel at the start of a step. */
@@ -200,6 +217,8 @@ int fbn_step_end(int* step, unsigned long long* rng, double* sumsq, long long* n
  * by routing ids to the owner of each row block; RCCL all-to-all runs between these calls. */
 int fbn_route(const int64_t* item, const int64_t* seq, int B, int L, long long V, long long Vl, int nranks,
               int* counts, int* offsets, int* cursor, int* send_ids, int* pos, int* err, void* stream);
+/* claims only (the lazy table Adam replays the claimed rows before fbn_owner_gather(map = NULL)) */
+int fbn_owner_claim(const int* ids, int n, int* map, int* slot_row, int rank, void* stream);
 int fbn_owner_gather(const int* ids, int n, const float* E, float* out, int* map, int* slot_row, int rank, int D,
                      void* stream);
 

@@ -39,6 +39,13 @@ class CpuExchangeKernels:
                     send_ids[p] = int(ids[b, t] - o * Vl)
                     pos[b, t] = p
 
+    def owner_claim(self, ids, map_, slot_row, rank):
+        """Restates fbn_owner_claim: first entry referencing a row claims it (padding row excluded)."""
+        for i, r in enumerate(ids.tolist()):
+            if not (rank == 0 and r == 0) and int(map_[r]) == -1:
+                map_[r] = i
+                slot_row[i] = r
+
     def owner_gather(self, ids, E, out, map_, slot_row, rank, d):
         for i, r in enumerate(ids.tolist()):
             out[i] = E[r]

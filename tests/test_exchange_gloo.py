@@ -25,7 +25,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, V, d, B, L, q):
+def _worker(rank, world, port, V, d, B, L, q, hook=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -48,7 +48,17 @@ def _worker(rank, world, port, V, d, B, L, q):
         sparse = {"map": torch.full((n_local,), -1, dtype=torch.int32),
                   "slot_row": torch.full((cap,), -1, dtype=torch.int32)}
         err = torch.zeros(1, dtype=torch.int32)
-        rows = xg.forward(item, seq, E_local, sparse, err)
+        seen = {}
+
+        def before_gather(n_recv):
+            # the lazy table Adam's slot: every requested non-padding row is claimed by now
+            # and nothing has been gathered yet -> shift the claimed rows; requesters must see it
+            sr = sparse["slot_row"][:n_recv]
+            claimed = sr[sr >= 0].long()
+            seen["n"] = int(claimed.numel())
+            E_local[claimed] += 1000.0
+
+        rows = xg.forward(item, seq, E_local, sparse, err, before_gather=before_gather if hook else None)
         pos = xg.cur_pos
         ids = torch.cat([item.view(B, 1), seq], dim=1)
         ok_fwd = True
@@ -58,7 +68,8 @@ def _worker(rank, world, port, V, d, B, L, q):
                 if t > 0 and int(ids[b, t]) == 0:
                     ok_fwd &= p == -1
                     continue
-                ok_fwd &= p >= 0 and torch.equal(rows[p], E_full[int(ids[b, t])])
+                want = E_full[int(ids[b, t])] + (1000.0 if hook and int(ids[b, t]) != 0 else 0.0)
+                ok_fwd &= p >= 0 and torch.equal(rows[p], want)
         # backward: one random gradient row per routed entry
         sendbuf = xg.make_sendbuf()
         sendbuf.copy_(torch.randn(sendbuf.shape, generator=gb))
@@ -90,13 +101,14 @@ def _worker(rank, world, port, V, d, B, L, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_row_exchange_protocol(world):
+@pytest.mark.parametrize("world,hook", [(2, False), (3, False), (2, True)])
+def test_row_exchange_protocol(world, hook):
+    """hook: the owner-side claim -> before_gather -> gather split used by the lazy table Adam."""
     V, d, B, L = 101, 8, 12, 6
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, V, d, B, L, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, V, d, B, L, q, hook)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
