@@ -360,12 +360,36 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     return a
 
 
+class _SideWork:
+    """Weight-gradient GEMMs off the dgrad critical path: each is forked onto `side` once its
+    operands exist (side waits for the main stream's work so far) and all are joined at the
+    end of the backward.  Torch's current stream is `side` while they are issued, so their
+    workspaces come from the side stream's allocator pool."""
+
+    def __init__(self, side: Optional["torch.cuda.Stream"], dev):
+        self.side = side
+        self.dev = dev
+        self.main = torch.cuda.current_stream(dev) if side is not None else None
+
+    def run(self, fn):
+        if self.side is None:
+            fn(_lib.stream_handle(self.dev))
+            return
+        self.side.wait_stream(self.main)
+        with torch.cuda.stream(self.side):
+            fn(self.side.cuda_stream)
+
+    def join(self):
+        if self.side is not None:
+            self.main.wait_stream(self.side)
+
+
 def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict[str, torch.Tensor],
              gout: torch.Tensor, g: Dict[str, torch.Tensor], cfg: FwdConfig, *,
              table_grad: Optional[torch.Tensor] = None, gvec: Optional[torch.Tensor] = None,
              pos: Optional[torch.Tensor] = None,
              sendbuf: Optional[torch.Tensor] = None, coll: Collective = NO_COLLECTIVE,
-             ntot: Optional[int] = None, extra_sums=()) -> None:
+             ntot: Optional[int] = None, extra_sums=(), side: Optional["torch.cuda.Stream"] = None) -> None:
     """Backward from dL/dlogit (gout [B]) into the gradient buffers ``g`` (same keys as ``p``).
 
     table_grad: dense [V, d] (drop-in, accumulated by atomics); or gvec [B, 2, d] (native
@@ -375,6 +399,9 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     accumulated into (callers zero it).
     extra_sums: further (part, nch, C, out[, scale, beta]) reductions to finalise in the same
     fbn_sum_jobs launch as the bias gradients (the trainer's mean loss).
+    side: optional stream for the weight-gradient GEMMs (overlap with the dgrad chain).  Off in
+    the trainer: at C3 every GEMM fills the chip, and two side by side measured slower than in
+    sequence (dWa beside dc: 67 + 67 us vs 37 + 37 us).
     """
     d, L = cfg.d, cfg.L
     B = a["B"]
@@ -391,16 +418,17 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     dh2pre = torch.empty((B, H2), **f32)
     dh2pre16 = torch.empty((B, H2), **bf16_) if bf else None
     sums = DeferredSums()
+    wg = _SideWork(side, dev)
     bn_backward(None, gout, p["mlp.8.weight"], a["h2"], scale, a["h2pre"], a["mean2"], a["inv2"],
                 p["mlp.5.weight"], B, H2, ntot, dh2pre, g["mlp.5.weight"], g["mlp.5.bias"], g["mlp.8.weight"],
                 coll, st, dpre16=dh2pre16, bias_grad=g["mlp.4.bias"], sums=sums)
     sums.add(gout, B, 1, g["mlp.8.bias"])
     dh1 = torch.empty((B, H1), **f32)
     if bf:
-        gemm(dh2pre16, a["h1_16"], g["mlp.4.weight"], H2, H1, B, H2, H1, H1, True, False, stream=st)
+        wg.run(lambda s: gemm(dh2pre16, a["h1_16"], g["mlp.4.weight"], H2, H1, B, H2, H1, H1, True, False, stream=s))
         gemm(dh2pre16, w16["WbT"], dh1, B, H1, H2, H2, H2, H1, False, True, stream=st)
     else:
-        gemm(dh2pre, a["h1"], g["mlp.4.weight"], H2, H1, B, H2, H1, H1, True, False, stream=st)
+        wg.run(lambda s: gemm(dh2pre, a["h1"], g["mlp.4.weight"], H2, H1, B, H2, H1, H1, True, False, stream=s))
         gemm(dh2pre, p["mlp.4.weight"], dh1, B, H1, H2, H2, H1, H1, False, False, stream=st)
     dh1pre = torch.empty((B, H1), **f32)
     dh1pre16 = torch.empty((B, H1), **bf16_) if bf else None
@@ -409,10 +437,12 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
                 bias_grad=g["mlp.0.bias"], sums=sums)
     dc = torch.empty((B, KC), **f32)
     if bf:
-        gemm(dh1pre16, a["c"], g["mlp.0.weight"], H1, KC, B, H1, KC, 21 * d, True, False, rC=wa_remap(d), stream=st)
+        wg.run(lambda s: gemm(dh1pre16, a["c"], g["mlp.0.weight"], H1, KC, B, H1, KC, 21 * d, True, False,
+                              rC=wa_remap(d), stream=s))
         gemm(dh1pre16, w16["WaT"], dc, B, KC, H1, H1, H1, KC, False, True, stream=st)
     else:
-        gemm(dh1pre, a["c"], g["mlp.0.weight"], H1, KC, B, H1, KC, 21 * d, True, False, rC=wa_remap(d), stream=st)
+        wg.run(lambda s: gemm(dh1pre, a["c"], g["mlp.0.weight"], H1, KC, B, H1, KC, 21 * d, True, False,
+                              rC=wa_remap(d), stream=s))
         gemm(dh1pre, p["mlp.0.weight"], dc, B, KC, H1, H1, 21 * d, KC, False, False, rB=wa_remap(d), stream=st)
     # bilinear backward
     dV = torch.empty((B, 5, d), **f32)
@@ -422,11 +452,11 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
          int(cfg.bilinear_each), st)
     if not cfg.bilinear_each:
         if bf:
+            wg.run(lambda s: gemm(a["Vc16"], dU16, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=s))
             gemm(dU16, w16["W"], dV, 5 * B, d, d, d, d, d, False, True, beta=1.0, stream=st)
-            gemm(a["Vc16"], dU16, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=st)
         else:
+            wg.run(lambda s: gemm(a["Vc"], dU, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=s))
             gemm(dU, p["bilinear.W"], dV, 5 * B, d, d, d, d, d, False, True, beta=1.0, stream=st)
-            gemm(a["Vc"], dU, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=st)
     else:
         g["bilinear.W_list.0"].zero_()
         for f in range(1, 5):
@@ -455,10 +485,12 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
          R, ncate, ptr(a["X"]), ptr(a["a"]), ptr(a["cnt"]), ptr(dV), ptr(dhmm), ptr(dhmm16), ptr(partials), outs,
          ptr(table_grad), ptr(gvec), V, ptr(pos), ptr(sendbuf), B, Lr, d, st)
     if bf:
-        gemm(dhmm16, w16["x"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True, False, stream=st)
+        wg.run(lambda s: gemm(dhmm16, w16["x"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True, False, stream=s))
     else:
-        gemm(dhmm, batch["item_emb_d128"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True, False, stream=st)
+        wg.run(lambda s: gemm(dhmm, batch["item_emb_d128"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True,
+                              False, stream=s))
     sums.colsum(dhmm, B, d, d, g["mm_proj.0.bias"], st)
     for job in extra_sums:              # e.g. the trainer's mean loss
         sums.add(*job)
     sums.flush(st)
+    wg.join()
