@@ -107,11 +107,21 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # rehearsal of the N > 1 path on a one-GPU box: FBN_BENCH_BACKEND=gloo puts every rank on
+    # cuda:0 with host-staged collectives (RCCL refuses two ranks on one device); timings from
+    # it are not scaling numbers
+    backend = os.environ.get("FBN_BENCH_BACKEND", "nccl")
+    rehearsal = backend != "nccl"
+    if rehearsal:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     group = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearsal:
+            dist.init_process_group(backend)
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     from ctr_recommendation_amd.data import make_device_batches
     from ctr_recommendation_amd.trainer import FiBiNETTrainer
 
@@ -145,7 +155,7 @@ def main():
                 return t
         init["item_emb.weight"] = _Shard()
     tr = FiBiNETTrainer(cfg, total_steps=total, batch_size=B, device=dev, rank=rank, world=world,
-                        init_state=init)
+                        init_state=init, stage_on_cpu=rehearsal)
     del table
     batches = make_device_batches(4, B, V, L, dev, seed=2025 + rank)
     # static inputs for graph replay
@@ -198,7 +208,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+        tt = torch.tensor([dt], device="cpu" if rehearsal else dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     loss = float(tr.loss.item())
@@ -220,7 +230,7 @@ def main():
     ids = ids[(ids > 0) & (ids >= tr.rows_lo) & (ids < tr.rows_lo + tr.rows_local)]
     touched = int(torch.unique(ids).numel())
     if world > 1:
-        tt = torch.tensor([touched], device=dev)
+        tt = torch.tensor([touched], device="cpu" if rehearsal else dev)
         dist.all_reduce(tt)
         touched = int(tt.item()) // world
     window = -(-tr.rows_local // tr.lazy_window)
@@ -267,7 +277,7 @@ def main():
                        "model": "MM_FiBiNET", "global_batch": B * world, "seq_len": L,
                        "item_rows": V, "item_rows_per_gpu": tr.rows_local, "emb_dim": d,
                        "parallelism": f"row-shard{world}" if world > 1 else "single",
-                       "hipgraph": bool(graphs)},
+                       "hipgraph": bool(graphs), **({"rehearsal": backend} if rehearsal else {})},
             "roofline": dominant,
             "rooflines": rooflines,
             "table_adam": tr.table_adam,
