@@ -31,6 +31,8 @@ SIGNATURES = {
     "fbn_gemm_workspace_size": (SZ, [I, I, I, I]),
     "fbn_gemm": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, F, I, I, I, P, P, SZ, P]),
     "fbn_bn_tile_stats": (I, [P, I, I, P, P, P]),
+    "fbn_bn_tile_moments": (I, [P, I, I, P, P]),
+    "fbn_bn_moments_finalize": (I, [P, D, I, P, P, P, P, F, F, I, P]),
     "fbn_bn_tile_finalize": (I, [P, I, I, D, P, P, P, P, F, F, I, P]),
     "fbn_bn_colpart_size": (SZ, [I, I]),
     "fbn_row_chunks": (I, [I]),
@@ -70,6 +72,8 @@ SIGNATURES = {
     "fbn_adam_catchup": (I, [P, P, P, LL, I, P, I, P, I, P, P, P, F, F, F, P]),
     "fbn_adam_flush": (I, [P, P, P, LL, I, P, P, P, F, F, F, P]),
     "fbn_claim_rows": (I, [P, P, I, I, LL, P, P, P]),
+    "fbn_pack_extras": (I, [P, P, P, P]),
+    "fbn_unpack_extras": (I, [P, P, P, P]),
     "fbn_step_end": (I, [P, P, P, P, P, P]),
     "fbn_route": (I, [P, P, I, I, LL, LL, I, P, P, P, P, P, P, P]),
     "fbn_owner_claim": (I, [P, I, P, P, I, P]),

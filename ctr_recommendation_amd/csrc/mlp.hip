@@ -331,6 +331,47 @@ __global__ void bn_tile_finalize_kernel(const float* __restrict__ part, int T, i
   }
 }
 
+// SyncBN (multi-GPU) forward statistics with ONE all-reduce per layer: each rank turns its
+// tile partials into raw f64 moments {sum x, sum x^2} (sum x^2 = sum_t M2_t + S_t^2 / n_t);
+// after the all-reduce, M2 = sum x^2 - sum x * mean in f64 (relative error ~1e-16 * mean^2/var).
+__global__ void bn_tile_moments_kernel(const float* __restrict__ part, int T, int C, int M, int tile_rows,
+                                       double* __restrict__ out) {
+  const int c = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (c >= C) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int t = lane; t < T; t += 64) {
+    const double S = part[((size_t)t * C + c) * 2], M2 = part[((size_t)t * C + c) * 2 + 1];
+    const int nt = min(tile_rows, M - t * tile_rows);
+    s1 += S;
+    s2 += M2 + S * S / nt;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o, 64);
+    s2 += __shfl_xor(s2, o, 64);
+  }
+  if (lane == 0) { out[c] = s1; out[C + c] = s2; }
+}
+
+__global__ void bn_moments_finalize_kernel(const double* __restrict__ mom, double ntot, int C, float* mean,
+                                           float* invstd, float* run_mean, float* run_var, float momentum, float eps,
+                                           int update_running) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double mu = mom[c] / ntot;
+  double q = mom[C + c] - mom[c] * mu;
+  if (q < 0.0) q = 0.0;
+  const float var_b = (float)(q / ntot);
+  mean[c] = (float)mu;
+  invstd[c] = 1.f / sqrtf(var_b + eps);
+  if (update_running) {
+    const float unb = ntot > 1.0 ? (float)(q / (ntot - 1.0)) : var_b;
+    run_mean[c] = momentum * (float)mu + (1.f - momentum) * run_mean[c];
+    run_var[c] = momentum * unb + (1.f - momentum) * run_var[c];
+  }
+}
+
 // Backward: chunk reduce of the three partial sums + the finalize of bn_bwd_finalize_kernel,
 // one wave per column (chunk_reduce_kernel's order).
 __global__ void bn_bwd_reduce_finalize_kernel(const double* __restrict__ part, int nchunk, int C, double ntot,
@@ -838,6 +879,23 @@ extern "C" int fbn_sum_jobs(const SumJob* jobs, int n, void* stream) {
   }
   if (J.col0[n] <= 0) return FBN_OK;
   hipLaunchKernelGGL(sum_jobs_kernel, dim3(J.col0[n]), dim3(256), 0, (hipStream_t)stream, J);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+extern "C" int fbn_bn_tile_moments(const float* part, int M, int C, double* out_d, void* stream) {
+  if (M <= 0) { (void)hipMemsetAsync(out_d, 0, 2 * sizeof(double) * C, (hipStream_t)stream); return FBN_OK; }
+  hipLaunchKernelGGL(bn_tile_moments_kernel, dim3(fbn_cdiv(C, 4)), dim3(256), 0, (hipStream_t)stream, part,
+                     (M + 63) / 64, C, M, 64, out_d);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+extern "C" int fbn_bn_moments_finalize(const double* mom_d, double ntot, int C, float* mean, float* invstd,
+                                       float* run_mean, float* run_var, float momentum, float eps, int update_running,
+                                       void* stream) {
+  hipLaunchKernelGGL(bn_moments_finalize_kernel, dim3(fbn_cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, mom_d, ntot,
+                     C, mean, invstd, run_mean, run_var, momentum, eps, update_running);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

@@ -653,3 +653,30 @@ extern "C" int fbn_adam_flush(float* p, float* m, float* v, long long nrows, int
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
+
+// Multi-GPU: the loss and this rank's table-gradient sum of squares ride in the dense-gradient
+// all-reduce (two floats appended to it): pack before, unpack after (sumsq += all ranks' table
+// norms; the loss becomes the global mean).  One thread each.
+__global__ void pack_extras_kernel(const float* loss, double* tab_slots, float* out) {
+  double s = 0.0;
+  for (int i = 0; i < FBN_SUMSQ_SLOTS; ++i) {
+    s += tab_slots[i];
+    tab_slots[i] = 0.0;
+  }
+  out[0] = *loss;
+  out[1] = (float)s;
+}
+__global__ void unpack_extras_kernel(const float* in, float* loss, double* sumsq) {
+  *loss = in[0];
+  sumsq[0] += (double)in[1];
+}
+extern "C" int fbn_pack_extras(const float* loss, double* tab_slots, float* out, void* stream) {
+  hipLaunchKernelGGL(pack_extras_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, loss, tab_slots, out);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+extern "C" int fbn_unpack_extras(const float* in, float* loss, double* sumsq, void* stream) {
+  hipLaunchKernelGGL(unpack_extras_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, in, loss, sumsq);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}

@@ -161,11 +161,13 @@ def bn_train_stats(h, B, C, mean, invstd, run_mean, run_var, ntot, coll: Collect
              ptr(run_var), BN_MOMENTUM, BN_EPS, 1 if run_mean is not None else 0, stream)
         return
     if tiles is not None:
-        call("fbn_bn_tile_stats", ptr(tiles), B, C, None, ptr(s), stream)
-        coll.allreduce_(s)
-        call("fbn_bn_mean", ptr(s), float(ntot), C, ptr(mean_d), stream)
-        call("fbn_bn_tile_stats", ptr(tiles), B, C, ptr(mean_d), ptr(s), stream)
-        coll.allreduce_(s)
+        # SyncBN: raw f64 moments, ONE all-reduce per layer
+        mom = torch.empty(2 * C, dtype=torch.float64, device=dev)
+        call("fbn_bn_tile_moments", ptr(tiles), B, C, ptr(mom), stream)
+        coll.allreduce_(mom)
+        call("fbn_bn_moments_finalize", ptr(mom), float(ntot), C, ptr(mean), ptr(invstd), ptr(run_mean),
+             ptr(run_var), BN_MOMENTUM, BN_EPS, 1 if run_mean is not None else 0, stream)
+        return
     else:
         ws = _ws(_lib.lib().fbn_bn_workspace_size(B, C), dev)
         call("fbn_bn_stats_pass", ptr(h), B, C, None, ptr(s), ptr(ws), stream)

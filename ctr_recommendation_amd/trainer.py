@@ -99,7 +99,9 @@ class FiBiNETTrainer:
             o += _pad4(int(np.prod(self.shapes[n])))
         self.n_dense = o
         self.flat_p = torch.zeros(o, dtype=torch.float32, device=dev)
-        self.flat_g = torch.zeros_like(self.flat_p)
+        # dense grads + 2 trailing floats (loss, table sumsq) for the multi-GPU all-reduce
+        self.flat_g_ext = torch.zeros(o + 4, dtype=torch.float32, device=dev)
+        self.flat_g = self.flat_g_ext[:o]
         self.flat_m = torch.zeros_like(self.flat_p)
         self.flat_v = torch.zeros_like(self.flat_p)
         self.p: Dict[str, torch.Tensor] = {}
@@ -231,8 +233,6 @@ class FiBiNETTrainer:
             call("fbn_sparse_fixup", ptr(batch["item_id"]), ptr(seq) if L else None, None, n_ent, L, self.V, 0,
                  ptr(self.map), ptr(self.gvec), ptr(self.extra), ptr(self.slot_row), L + 1, d, st)
         else:
-            self.coll.allreduce_(self.flat_g)
-            self.coll.allreduce_(self.loss)
             grows = self.xchg.backward(sendbuf)              # owner: one received row per entry
             n_ent = grows.shape[0]
             gsrc = (grows, None, 1)
@@ -241,11 +241,13 @@ class FiBiNETTrainer:
         # clip_grad_norm_(10): dense grads (identical on every rank) + disjoint table shards
         tab_acc = self.sumsq_tab if self.world > 1 else self.sumsq
         call("fbn_sumsq_sparse", ptr(gsrc[0]), ptr(gsrc[1]), ptr(self.slot_row), gsrc[2], n_ent, d, ptr(tab_acc), st)
-        call("fbn_sumsq", ptr(self.flat_g), self.n_dense, None, 0, ptr(self.sumsq), st)
         if self.world > 1:
-            self.coll.allreduce_(self.sumsq_tab)
-            self.sumsq.add_(self.sumsq_tab)
-            self.sumsq_tab.zero_()
+            # ONE all-reduce: dense grads + the loss + this shard's table-gradient sumsq
+            o = self.n_dense
+            call("fbn_pack_extras", ptr(self.loss), ptr(self.sumsq_tab), ptr(self.flat_g_ext[o:]), st)
+            self.coll.allreduce_(self.flat_g_ext[:o + 2])
+            call("fbn_unpack_extras", ptr(self.flat_g_ext[o:]), ptr(self.loss), ptr(self.sumsq), st)
+        call("fbn_sumsq", ptr(self.flat_g), self.n_dense, None, 0, ptr(self.sumsq), st)
         # clip_grad_norm_(10) is applied inside the dense Adam launch (it publishes coef / norm)
         call("fbn_adam_dense", ptr(self.flat_p), ptr(self.flat_g), ptr(self.flat_m), ptr(self.flat_v),
              self.n_dense, None, ptr(self.sched), ptr(self.step_dev), self.wd, self.beta2, self.eps, ptr(self.sumsq),

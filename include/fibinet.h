@@ -111,6 +111,11 @@ int fbn_bn_stats(const float* X, int B, int C, float* mean, float* invstd, float
 int fbn_bn_tile_stats(const float* part, int M, int C, const double* mean_d, double* out_d, void* stream);
 /* Single-process form of the above + fbn_bn_mean + fbn_bn_finalize in one launch (same f64
  * operations in the same order; the multi-GPU path needs the all-reduces in between). */
+/* SyncBN (multi-GPU) with one all-reduce per layer: per-rank raw moments out[2C] = {sum x,
+ * sum x^2} from the tile partials, all-reduced by the caller, then the finalize. */
+int fbn_bn_tile_moments(const float* part, int M, int C, double* out_d, void* stream);
+int fbn_bn_moments_finalize(const double* mom_d, double ntot, int C, float* mean, float* invstd, float* run_mean,
+                            float* run_var, float momentum, float eps, int update_running, void* stream);
 int fbn_bn_tile_finalize(const float* part, int M, int C, double ntot, float* mean, float* invstd, float* run_mean,
                          float* run_var, float momentum, float eps, int update_running, void* stream);
 int fbn_bn_eval_params(const float* run_mean, const float* run_var, float* mean, float* invstd, int C, float eps,
@@ -208,6 +213,10 @@ int fbn_adam_flush(float* p, float* m, float* v, long long nrows, int D, int* la
 #define FBN_SUMSQ_SLOTS 64
 int fbn_claim_rows(const int64_t* item, const int64_t* seq, int B, int L, long long V, int* map, int* slot_row,
                    void* stream);
+/* Multi-GPU: pack {loss, this rank's table-gradient sumsq (slots zeroed)} into the two floats
+ * appended to the dense-gradient all-reduce buffer; unpack after it (sumsq[0] += table norms). */
+int fbn_pack_extras(const float* loss, double* tab_slots, float* out, void* stream);
+int fbn_unpack_extras(const float* in, float* loss, double* sumsq, void* stream);
 /* end of step: step counter, dropout counter, zero the sumsq slots, and the BatchNorm
  * num_batches_tracked buffers (nbt0 / nbt1 may be NULL; model_fibinet.py:127,131 BN1d). */
 int fbn_step_end(int* step, unsigned long long* rng, double* sumsq, long long* nbt0, long long* nbt1, void* stream);
