@@ -13,7 +13,7 @@ from typing import Optional
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfibinet_hip.so")
+LIB_PATH = os.environ.get("FBN_LIB_PATH") or os.path.join(_HERE, "libfibinet_hip.so")   # override: tuning tools
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -43,8 +43,8 @@ SIGNATURES = {
     "fbn_fields_bwd_partials_size": (I, [I, I, I]),
     "fbn_fields_bwd_grid": (I, [I, I]),
     "fbn_fields_bwd": (I, [P, P, P, P, P, P, F, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P, LL, P, P, I, I, I, P]),
-    "fbn_pairs_fwd": (I, [P, P, P, I, I, I, I, I, P]),
-    "fbn_pairs_bwd": (I, [P, P, P, P, P, P, I, I, I, I, P]),
+    "fbn_pairs_fwd": (I, [P, P, P, P, I, I, I, I, I, P]),
+    "fbn_pairs_bwd": (I, [P, P, P, P, P, P, P, I, I, I, I, P]),
     "fbn_bn_workspace_size": (SZ, [I, I]),
     "fbn_bn_stats_pass": (I, [P, I, I, P, P, P, P]),
     "fbn_bn_mean": (I, [P, D, I, P, P]),

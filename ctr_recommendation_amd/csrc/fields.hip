@@ -19,6 +19,10 @@
 #include "common.h"
 
 #define FBN_MAXR 8   // max SENET reduced width supported (reference: 3)
+#define FBN_MAX_L 32 // max history length (the reference keeps the last 20)
+#ifndef FBN_HCH
+#define FBN_HCH 5    // history rows in flight per sample before they are summed (tools/time_fields.py)
+#endif
 
 struct FieldArgs {
   const int64_t* item_id;   // [B]
@@ -79,7 +83,7 @@ template <int D, int MODE>
 __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
   constexpr int G = D / 4;                  // lanes per sample
   constexpr int SPW = 64 / G;               // samples per wave
-  constexpr int HCH = 10;
+  constexpr int HCH = FBN_HCH;
   const int lane = threadIdx.x & 63;
   const int q = lane % G;
   const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -112,6 +116,27 @@ __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
       const int pi = pb[0];
       if (pi >= 0) rit = *reinterpret_cast<const f32x4*>(p.table + (size_t)pi * D + 4 * q);
     }
+    // all history ids in ONE round (lane q of the group holds slots q, q+G, ...), broadcast by
+    // shuffles, then every row load is issued before any is consumed (two dependent round trips
+    // per sample instead of one per chunk); summed in slot order like the reference
+    constexpr int IPL = (FBN_MAX_L + G - 1) / G;      // ids per lane
+    int sid[IPL];
+#pragma unroll
+    for (int j = 0; j < IPL; ++j) {
+      const int t = q + j * G;
+      int r = -1;
+      if (t < L) {
+        if (MODE == 0) {
+          long long s = p.item_seq[(size_t)b * L + t];
+          if (s < 0 || s >= p.V) { bad = true; s = 0; }
+          r = s != 0 ? (int)s : -1;
+        } else {
+          r = pb[t + 1];
+        }
+      }
+      sid[j] = r;
+    }
+    const int gbase = lane - q;
     for (int t0 = 0; t0 < L; t0 += HCH) {
       f32x4 hist[HCH];
 #pragma unroll
@@ -119,20 +144,17 @@ __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
         hist[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
         const int t = t0 + u;
         if (t < L) {
-          if (MODE == 0) {
-            long long s = p.item_seq[(size_t)b * L + t];
-            if (s < 0 || s >= p.V) { bad = true; s = 0; }
-            if (s != 0) { hist[u] = *reinterpret_cast<const f32x4*>(p.table + s * D + 4 * q); ++nnz; }
-          } else {
-            const int ps = pb[t + 1];
-            if (ps >= 0) { hist[u] = *reinterpret_cast<const f32x4*>(p.table + (size_t)ps * D + 4 * q); ++nnz; }
-          }
+          int r = -1;
+#pragma unroll
+          for (int j = 0; j < IPL; ++j)
+            if ((t / G) == j) r = __shfl(sid[j], gbase + (t % G), 64);
+          if (r >= 0) { hist[u] = *reinterpret_cast<const f32x4*>(p.table + (size_t)r * D + 4 * q); ++nnz; }
         }
       }
 #pragma unroll
       for (int u = 0; u < HCH; ++u) hs += hist[u];
     }
-    if (bad && q == 0) atomicOr(p.err, 1);
+    if (bad) atomicOr(p.err, 1);        // any lane: history ids are validated by the lane holding them
 
     // ---------------- history masked mean
     const float cnt = fmaxf((float)nnz, 1.f);
@@ -161,14 +183,14 @@ __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
 
     // ---------------- stores
     float* Xb = p.X + (size_t)b * 5 * D + 4 * q;
-    float* Vb = p.Vc + (size_t)b * 5 * D + 4 * q;
+    float* Vb = p.Vc ? p.Vc + (size_t)b * 5 * D + 4 * q : nullptr;
     float* cb = p.c16 ? nullptr : (float*)p.c + (size_t)b * p.ldc + 4 * q;
     short* cb16 = p.c16 ? (short*)p.c + (size_t)b * p.ldc + 4 * q : nullptr;
 #pragma unroll
     for (int f = 0; f < 5; ++f) {
       const f32x4 v = xs[f] * a[f + 1];
       *reinterpret_cast<f32x4*>(Xb + f * D) = xs[f];
-      *reinterpret_cast<f32x4*>(Vb + f * D) = v;
+      if (p.Vc) *reinterpret_cast<f32x4*>(Vb + f * D) = v;   // bf16 mode: only the bf16 copies
       const bf16x4 v16 = (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
       if (cb16) *reinterpret_cast<bf16x4*>(cb16 + f * D) = v16;
       else *reinterpret_cast<f32x4*>(cb + f * D) = v;

@@ -28,9 +28,19 @@ __device__ __forceinline__ void store4(float* p, const f32x4& v) { *reinterpret_
 __device__ __forceinline__ void store4(short* p, const f32x4& v) {
   *reinterpret_cast<bf16x4*>(p) = (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
 }
+// V from the fp32 fields (fp32 mode) or from their bf16 copy (bf16 mode: the fp32 copy is not
+// written at all; U = V W is computed from the same bf16 V by the GEMM)
+__device__ __forceinline__ f32x4 load_v4(const float* __restrict__ V, const short* __restrict__ V16, size_t off) {
+  if (V16) {
+    const bf16x4 t = *reinterpret_cast<const bf16x4*>(V16 + off);
+    return (f32x4){bf2f(t[0]), bf2f(t[1]), bf2f(t[2]), bf2f(t[3])};
+  }
+  return *reinterpret_cast<const f32x4*>(V + off);
+}
+
 template <typename OutT>
-__global__ void pairs_fwd_kernel(const float* __restrict__ Vc, const float* __restrict__ U, OutT* __restrict__ c,
-                                 int B, int D, int ldc, int mode) {
+__global__ void pairs_fwd_kernel(const float* __restrict__ Vc, const short* __restrict__ Vc16,
+                                 const float* __restrict__ U, OutT* __restrict__ c, int B, int D, int ldc, int mode) {
   const int q4 = D / 4;
   const size_t total = (size_t)B * q4;
   for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
@@ -38,7 +48,7 @@ __global__ void pairs_fwd_kernel(const float* __restrict__ Vc, const float* __re
     f32x4 v[5], u[5];
 #pragma unroll
     for (int f = 0; f < 5; ++f) {
-      v[f] = *reinterpret_cast<const f32x4*>(Vc + ((size_t)b * 5 + f) * D + col);
+      v[f] = load_v4(Vc, Vc16, ((size_t)b * 5 + f) * D + col);
       u[f] = *reinterpret_cast<const f32x4*>(U + ((size_t)b * 5 + f) * D + col);
     }
     OutT* out = c + (size_t)b * ldc + 5 * D + col;
@@ -55,6 +65,7 @@ __global__ void pairs_fwd_kernel(const float* __restrict__ Vc, const float* __re
 // with compile-time indices: with runtime indices the five-field register arrays go to scratch.
 template <int MODE>
 __global__ void __launch_bounds__(256) pairs_bwd_kernel(const float* __restrict__ dc, const float* __restrict__ Vc,
+                                                        const short* __restrict__ Vc16,
                                                         const float* __restrict__ U, float* __restrict__ dV,
                                                         float* __restrict__ dU, short* __restrict__ dU16, int B, int D,
                                                         int ldc) {
@@ -66,7 +77,7 @@ __global__ void __launch_bounds__(256) pairs_bwd_kernel(const float* __restrict_
     const float* dcb = dc + (size_t)b * ldc + col;
 #pragma unroll
     for (int f = 0; f < 5; ++f) {
-      v[f] = *reinterpret_cast<const f32x4*>(Vc + ((size_t)b * 5 + f) * D + col);
+      v[f] = load_v4(Vc, Vc16, ((size_t)b * 5 + f) * D + col);
       u[f] = *reinterpret_cast<const f32x4*>(U + ((size_t)b * 5 + f) * D + col);
       gv[f] = *reinterpret_cast<const f32x4*>(dcb + f * D);
       gu[f] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -564,29 +575,29 @@ static int row_chunks(int B) {
 }
 
 // c_bf16: c is a bf16 [B][ldc] buffer (bf16 GEMM mode) instead of float
-extern "C" int fbn_pairs_fwd(const float* Vc, const float* U, void* c, int B, int D, int ldc, int mode, int c_bf16,
-                             void* stream) {
+extern "C" int fbn_pairs_fwd(const float* Vc, const short* Vc16, const float* U, void* c, int B, int D, int ldc,
+                             int mode, int c_bf16, void* stream) {
   if (B <= 0) return FBN_OK;
   if ((D & 3) || (ldc & 3)) { fbn_set_error("pairs: D and ldc must be multiples of 4"); return FBN_ERR_ARG; }
   if (c_bf16)
     hipLaunchKernelGGL(pairs_fwd_kernel<short>, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream,
-                       Vc, U, (short*)c, B, D, ldc, mode);
+                       Vc, Vc16, U, (short*)c, B, D, ldc, mode);
   else
     hipLaunchKernelGGL(pairs_fwd_kernel<float>, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream,
-                       Vc, U, (float*)c, B, D, ldc, mode);
+                       Vc, Vc16, U, (float*)c, B, D, ldc, mode);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
 
-extern "C" int fbn_pairs_bwd(const float* dc, const float* Vc, const float* U, float* dV, float* dU, short* dU16,
-                             int B, int D, int ldc, int mode, void* stream) {
+extern "C" int fbn_pairs_bwd(const float* dc, const float* Vc, const short* Vc16, const float* U, float* dV,
+                             float* dU, short* dU16, int B, int D, int ldc, int mode, void* stream) {
   if (B <= 0) return FBN_OK;
   if (mode == 0)
     hipLaunchKernelGGL(pairs_bwd_kernel<0>, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream, dc, Vc,
-                       U, dV, dU, dU16, B, D, ldc);
+                       Vc16, U, dV, dU, dU16, B, D, ldc);
   else
     hipLaunchKernelGGL(pairs_bwd_kernel<1>, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream, dc, Vc,
-                       U, dV, dU, dU16, B, D, ldc);
+                       Vc16, U, dV, dU, dU16, B, D, ldc);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

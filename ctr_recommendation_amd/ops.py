@@ -256,8 +256,10 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     gemm(w16["x"] if bf else x_mm, w16["Wp"] if bf else p["mm_proj.0.weight"], hmm, B, d, 128, 128, 128, d, False,
          True, bias=p["mm_proj.0.bias"], bf16=bf, stream=st)
     X = buf("X", (B, 5, d))
-    Vc = buf("Vc", (B, 5, d))
-    Vc16 = buf("Vc16", (B, 5, d), torch.bfloat16) if (bf and not cfg.bilinear_each) else None
+    # bf16 mode: the fields after SENET exist only as bf16 (GEMM operand and pair-kernel input)
+    v16 = bf and not cfg.bilinear_each
+    Vc = None if v16 else buf("Vc", (B, 5, d))
+    Vc16 = buf("Vc16", (B, 5, d), torch.bfloat16) if v16 else None
     KC = 15 * d
     c = buf("c", (B, KC), torch.bfloat16 if bf else torch.float32)     # bf16 mode: GEMM-only operand
     av = buf("a", (B, 6))
@@ -296,7 +298,7 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
         for f in range(1, 5):   # field index in Vc: f-1 <-> reference field f; W_list[f]
             gemm(Vc[:, f - 1], p[f"bilinear.W_list.{f}"], U[:, f - 1], B, d, d, 5 * d, d, 5 * d, False, False,
                  bf16=bf, stream=st)
-    call("fbn_pairs_fwd", ptr(Vc), ptr(U), ptr(c), B, d, KC, int(cfg.bilinear_each), int(bf), st)
+    call("fbn_pairs_fwd", ptr(Vc), ptr(Vc16), ptr(U), ptr(c), B, d, KC, int(cfg.bilinear_each), int(bf), st)
     # MLP layer 1
     h1pre = buf("h1pre", (B, H1))
     nt = (B + 63) // 64
@@ -450,8 +452,9 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     dV = torch.empty((B, 5, d), **f32)
     dU = torch.empty((B, 5, d), **f32)
     dU16 = torch.empty((B, 5, d), dtype=torch.bfloat16, device=dev) if (bf and not cfg.bilinear_each) else None
-    call("fbn_pairs_bwd", ptr(dc), ptr(a["Vc"]), ptr(a["U"]), ptr(dV), ptr(dU), ptr(dU16), B, d, KC,
-         int(cfg.bilinear_each), st)
+    v16 = bf and not cfg.bilinear_each
+    call("fbn_pairs_bwd", ptr(dc), None if v16 else ptr(a["Vc"]), ptr(a["Vc16"]) if v16 else None, ptr(a["U"]),
+         ptr(dV), ptr(dU), ptr(dU16), B, d, KC, int(cfg.bilinear_each), st)
     if not cfg.bilinear_each:
         if bf:
             wg.run(lambda s: gemm(a["Vc16"], dU16, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=s))

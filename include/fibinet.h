@@ -90,10 +90,12 @@ int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, const int64_
 /* ---------------------------------------------------------------- K5 bilinear pair products
  * Replaces the pair loop + stack + cat of src/model_fibinet.py:75-79,89,191-194 ("all", mode 0)
  * and :81-86 ("each", mode 1).  Pairs (0,j) are structurally zero and not stored. */
-int fbn_pairs_fwd(const float* Vc, const float* U, void* c, int B, int D, int ldc, int mode, int c_bf16,
-                  void* stream);
-int fbn_pairs_bwd(const float* dc, const float* Vc, const float* U, float* dV, float* dU, short* dU16, int B, int D,
-                  int ldc, int mode, void* stream);
+/* V is read from Vc (fp32) or, when Vc16 is given, from the bf16 copy (bf16 mode; fbn_fields_fwd
+ * then writes no fp32 Vc). */
+int fbn_pairs_fwd(const float* Vc, const short* Vc16, const float* U, void* c, int B, int D, int ldc, int mode,
+                  int c_bf16, void* stream);
+int fbn_pairs_bwd(const float* dc, const float* Vc, const short* Vc16, const float* U, float* dV, float* dU,
+                  short* dU16, int B, int D, int ldc, int mode, void* stream);
 
 /* ---------------------------------------------------------------- K6 BatchNorm + ReLU + dropout
  * Replaces nn.BatchNorm1d / ReLU / Dropout(0.2) of src/model_fibinet.py:127-133.  The stats

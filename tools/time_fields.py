@@ -1,0 +1,30 @@
+"""Time fbn_fields_fwd alone at C3 shapes (B=8192, d=128, L=20, V=1.25M, bf16 c) for the library
+selected by FBN_LIB_PATH; prints the average launch time and the SURVEY 8(d) roofline fraction."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from ctr_recommendation_amd import ops
+from ctr_recommendation_amd.data import make_device_batches
+from ctr_recommendation_amd.model_fibinet import build_model
+
+dev = torch.device("cuda", 0)
+B, d, L, V = 8192, 128, 20, 1_250_000
+cfg = {"embedding_dim": d, "vocab_size": 4}
+small = build_model(None, cfg).state_dict()
+p = {k: v.to(dev) for k, v in small.items()}
+p["item_emb.weight"] = torch.randn((V, d), device=dev)
+batch, _ = make_device_batches(1, B, V, L, dev, seed=3)[0]
+a = {}
+fc = ops.FwdConfig(d=d, L=L, training=True, p_drop=0.0, bf16=True, bilinear_each=False, R=3)
+probe = {}
+for i in range(30):
+    ops.forward(p, batch, fc, None, acts=a, probe=probe)
+torch.cuda.synchronize()
+ev = probe["fields_fwd"][10:]
+ms = sum(s.elapsed_time(e) for s, e in ev) / len(ev)
+byts = ((L + 1) * d * 4 + (L + 3) * 8 + 4 * d * 4) * B
+print(f"{os.environ.get('FBN_LIB_PATH', 'default')}: fields_fwd {ms * 1e3:.1f} us  {byts / ms / 1e6:.0f} GB/s "
+      f"({byts / ms / 1e6 / 8000:.3f} of 8 TB/s)")
