@@ -42,7 +42,9 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=5)
+    # the lazy table Adam's per-row lag settles after ~1/p = V/touched-per-step steps: warm up
+    # into steady-state training (warm-up steps are < 1 ms each)
+    ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--batch", type=int, default=8192, help="per-GPU batch")
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--rows-per-gpu", type=int, default=ROWS_PER_GPU)

@@ -69,7 +69,7 @@ SIGNATURES = {
     "fbn_sumsq_sparse": (I, [P, P, P, I, I, I, P, P]),
     "fbn_adam_table": (I, [P, P, P, LL, I, P, P, P, P, I, P, P, P, F, F, F, I, P]),
     "fbn_adam_touched": (I, [P, P, P, I, P, P, P, P, I, I, P, P, P, F, F, F, P, P]),
-    "fbn_adam_catchup": (I, [P, P, P, LL, I, P, I, P, I, P, P, P, F, F, F, P]),
+    "fbn_adam_catchup": (I, [P, P, P, LL, I, P, I, P, I, I, P, P, P, F, F, F, P]),
     "fbn_adam_flush": (I, [P, P, P, LL, I, P, P, P, F, F, F, P]),
     "fbn_claim_rows": (I, [P, P, I, I, LL, P, P, P]),
     "fbn_pack_extras": (I, [P, P, P, P]),

@@ -360,7 +360,9 @@ __device__ __forceinline__ void replay_rows(float* __restrict__ p, float* __rest
   f32x4 mm = *reinterpret_cast<f32x4*>(m + off);
   f32x4 vv = *reinterpret_cast<f32x4*>(v + off);
   for (int s = k0; s < t; ++s) {
-    const AdamConsts k = s >= w0 ? win[s - w0] : table[s];
+    // the rolling window keeps every row within F <= FBN_LAZY_MAX_LAG steps, so the constants of
+    // steps k0 .. t-1 are all in the LDS window (a global fallback would turn this into flat loads)
+    const AdamConsts k = win[s - w0];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float pe = pp[e], me = mm[e], ve = vv[e];
@@ -379,7 +381,7 @@ template <int D>
 __global__ void __launch_bounds__(256) adam_catchup_kernel(float* __restrict__ p, float* __restrict__ m,
                                                            float* __restrict__ v, const int* __restrict__ slot_row,
                                                            int n_ent, const int* __restrict__ map, long long nrows,
-                                                           int F, long long chunk, int* __restrict__ last,
+                                                           int F, long long chunk, int parts, int* __restrict__ last,
                                                            const AdamConsts* __restrict__ table,
                                                            const int* __restrict__ step, float wd, float b2,
                                                            float omb2, float eps) {
@@ -390,7 +392,8 @@ __global__ void __launch_bounds__(256) adam_catchup_kernel(float* __restrict__ p
   for (int i = threadIdx.x; i < t - w0; i += blockDim.x) win[i] = table[w0 + i];
   __syncthreads();
   const long long roll0 = (long long)(t % F) * chunk;
-  const long long nroll = roll0 < nrows ? min(chunk, nrows - roll0) : 0;
+  const long long nroll = (parts & 2) && roll0 < nrows ? min(chunk, nrows - roll0) : 0;
+  if (!(parts & 1)) n_ent = 0;
   const long long n = n_ent + nroll;
   const int lane = threadIdx.x & 63, q = lane % G;
   const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -629,16 +632,24 @@ extern "C" int fbn_step_end(int* step, unsigned long long* rng, double* sumsq, l
 
 // lazy table Adam: replay the zero-loss-gradient steps of the claimed rows and of rolling window
 // (step mod F) (chunk = ceil(nrows / F) rows) up to `step`; last: [nrows] steps applied per row
+// parts: 1 = the claimed rows (must precede the gather), 2 = the rolling window (unclaimed rows:
+// nothing else reads them this step -> may run on a side stream), 3 = both
 extern "C" int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, int D, const int* slot_row, int n_ent,
-                                const int* map, int F, int* last, const void* consts_table, const int* step, float wd,
-                                float beta2, float eps, void* stream) {
+                                const int* map, int F, int parts, int* last, const void* consts_table, const int* step,
+                                float wd, float beta2, float eps, void* stream) {
   if (nrows <= 0) return FBN_OK;
   if (F < 1 || F > FBN_LAZY_MAX_LAG) { fbn_set_error("fbn_adam_catchup: 1 <= F <= 512"); return FBN_ERR_ARG; }
   hipStream_t st = (hipStream_t)stream;
   const float omb2 = (float)(1.0 - (double)beta2);
   const long long chunk = (nrows + F - 1) / F;
-  FBN_DISPATCH_D(adam_catchup_kernel, D, group_grid(n_ent + chunk, D, 8192), p, m, v, slot_row, n_ent, map, nrows, F,
-                 chunk, last, (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps);
+  const long long items = ((parts & 1) ? n_ent : 0) + ((parts & 2) ? chunk : 0);
+  if (items <= 0) return FBN_OK;
+  // the window-only pass runs beside the step: a few workgroups per CU leave the CUs' wave
+  // slots to the main stream while its four-chain replay keeps the VALU busy
+  static const int wcap = getenv("FBN_WINDOW_BLOCKS") ? atoi(getenv("FBN_WINDOW_BLOCKS")) : 256;   // tools/window_sweep.sh
+  const long long cap = parts == 2 ? wcap : 8192;
+  FBN_DISPATCH_D(adam_catchup_kernel, D, group_grid(items, D, cap), p, m, v, slot_row, n_ent, map, nrows, F, chunk,
+                 parts, last, (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

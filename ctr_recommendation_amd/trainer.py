@@ -160,7 +160,7 @@ class FiBiNETTrainer:
             raise ValueError(f"table_adam must be 'lazy' or 'eager', not {self.table_adam!r}")
         self.lazy_window = int(lazy_window)
         self.last = torch.zeros(max(1, self.rows_local), **i32)     # Adam steps applied per table row
-        self.side = torch.cuda.Stream(device=dev) if self.table_adam == "eager" else None
+        self.side = torch.cuda.Stream(device=dev)      # eager untouched pass / lazy rolling window
 
     # ------------------------------------------------------------------ one training step
     def step(self, batch: Dict[str, torch.Tensor], labels: torch.Tensor,
@@ -191,13 +191,20 @@ class FiBiNETTrainer:
         lazy = self.table_adam == "lazy"
 
         def catch_up(n_ent):
-            # lazy table Adam: rows claimed this step (and rolling window step % F) -> `step`
-            # Adam steps, before anything reads them
+            # lazy table Adam: the rows claimed this step are brought to `step` Adam steps before
+            # anything reads them; the rolling window (step % F; unclaimed rows, read by nothing
+            # this step) replays on the side stream beside the rest of the step
             ev = _events(probe, "adam_catchup")
             call("fbn_adam_catchup", ptr(self.E), ptr(self.Em), ptr(self.Ev), self.rows_local, d, ptr(self.slot_row),
-                 n_ent, ptr(self.map), self.lazy_window, ptr(self.last), ptr(self.sched), ptr(self.step_dev), self.wd,
-                 self.beta2, self.eps, st)
+                 n_ent, ptr(self.map), self.lazy_window, 1, ptr(self.last), ptr(self.sched), ptr(self.step_dev),
+                 self.wd, self.beta2, self.eps, st)
             _events_end(ev)
+            self.side.wait_stream(main)
+            ev = _events(probe, "adam_window", self.side)
+            call("fbn_adam_catchup", ptr(self.E), ptr(self.Em), ptr(self.Ev), self.rows_local, d, None, 0,
+                 ptr(self.map), self.lazy_window, 2, ptr(self.last), ptr(self.sched), ptr(self.step_dev), self.wd,
+                 self.beta2, self.eps, self.side.cuda_stream)
+            _events_end(ev, self.side)
 
         def start_untouched_adam():
             # eager mode: every row this shard's batch does not touch gets g = wd * p, independent
@@ -252,8 +259,7 @@ class FiBiNETTrainer:
         call("fbn_adam_dense", ptr(self.flat_p), ptr(self.flat_g), ptr(self.flat_m), ptr(self.flat_v),
              self.n_dense, None, ptr(self.sched), ptr(self.step_dev), self.wd, self.beta2, self.eps, ptr(self.sumsq),
              self.max_norm, ptr(self.coef), ptr(self.norm), st)
-        if not lazy:
-            main.wait_stream(self.side)              # untouched pass done before map entries are reset
+        main.wait_stream(self.side)   # side-stream table pass done before map entries are reset
         ev = _events(probe, "adam_touched")
         call("fbn_adam_touched", ptr(self.E), ptr(self.Em), ptr(self.Ev), d, ptr(self.map), ptr(gsrc[0]),
              ptr(gsrc[1]), ptr(self.slot_row), gsrc[2], n_ent, ptr(self.coef), ptr(self.sched), ptr(self.step_dev),

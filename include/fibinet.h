@@ -203,8 +203,10 @@ int fbn_adam_touched(float* p, float* m, float* v, int D, int* map, const float*
  * then applies the step with the gradient; fbn_adam_flush brings every row up to date.
  * Replaces the per-step dense Adam pass of torch.optim.Adam over item_emb.weight
  * (src/train_fibinet.py:78,121) by O(touched + nrows/F) rows per step.  F <= 512. */
+/* parts: 1 = claimed rows (before the gather), 2 = rolling window (unclaimed rows; may overlap the
+ * step on another stream), 3 = both. */
 int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, int D, const int* slot_row, int n_ent,
-                     const int* map, int F, int* last, const void* consts_table, const int* step, float wd,
+                     const int* map, int F, int parts, int* last, const void* consts_table, const int* step, float wd,
                      float beta2, float eps, void* stream);
 int fbn_adam_flush(float* p, float* m, float* v, long long nrows, int D, int* last, const void* consts_table,
                    const int* step, float wd, float beta2, float eps, void* stream);

@@ -20,7 +20,7 @@ for step in "$@"; do
     prof)
       cd /tmp && export TMPDIR=/tmp
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- \
-        python $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline > $OUT/prof_$TAG.log 2>&1
+        python $R/bench.py --no-cpu-baseline > $OUT/prof_$TAG.log 2>&1
       rc=$?; echo "prof rc=$rc"; tail -3 $OUT/prof_$TAG.log; cd $R; [ $rc -eq 0 ] || exit $rc ;;
     pmc)
       cd /tmp && export TMPDIR=/tmp
