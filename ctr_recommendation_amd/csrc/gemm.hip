@@ -604,6 +604,36 @@ __global__ void gemm_splitk_reduce4(GemmArgs g, int nsplit) {
   }
 }
 
+// wide split-K reduce for many slabs over a small C (the wgrad GEMMs with K = 5B or B): block =
+// 16 column quads x 16 slab groups; slab group zg sums slabs zg, zg+16, ...; the 16 partials are
+// combined in a fixed order (deterministic)
+__global__ void __launch_bounds__(256) gemm_splitk_reduce4_wide(GemmArgs g, int nsplit) {
+  __shared__ f32x4 red[16][16];
+  const int qd = threadIdx.x & 15, zg = threadIdx.x >> 4;
+  const int N4 = g.N >> 2;
+  const size_t total4 = (size_t)g.M * N4, total = (size_t)g.M * g.N;
+  const size_t i4 = (size_t)blockIdx.x * 16 + qd;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  size_t idx = 0;
+  if (i4 < total4) {
+    const int m = (int)(i4 / N4), n = (int)(i4 - (size_t)m * N4) * 4;
+    idx = (size_t)m * g.N + n;
+    for (int z = zg; z < nsplit; z += 16) acc += *reinterpret_cast<const f32x4*>(g.ws + (size_t)z * total + idx);
+  }
+  red[zg][qd] = acc;
+  __syncthreads();
+  if (zg == 0 && i4 < total4) {
+    f32x4 s = red[0][qd];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) s += red[k][qd];
+    const int m = (int)(i4 / N4), n = (int)(i4 - (size_t)m * N4) * 4;
+    if (g.bias) s += *reinterpret_cast<const f32x4*>(g.bias + n);
+    float* cp = g.C + (size_t)m * g.ldc + remap(g.rC, n);
+    if (g.beta != 0.f) s += g.beta * *reinterpret_cast<const f32x4*>(cp);
+    *reinterpret_cast<f32x4*>(cp) = s;
+  }
+}
+
 // split-K reduce with the BatchNorm statistics epilogue: one workgroup per 64x64 tile of C;
 // thread (col = tid & 63, rows 16*(tid >> 6) .. +15) -> coalesced slab reads along n.  Sums the
 // K-slabs in the same order as gemm_splitk_reduce (so C is bit-identical with or without stats),
@@ -694,7 +724,7 @@ static GemmPlan plan_dma16(int M, int N, int K) {
   GemmPlan p = (M >= 512 && N >= 512) ? GemmPlan{128, 64, 1} : GemmPlan{64, 64, 1};
   const long long tiles = (long long)fbn_cdiv(M, p.bm) * fbn_cdiv(N, p.bn);
   const long long target = p.bm == 128 ? 512 : 256;
-  while (p.split < 16 && tiles * p.split * 2 <= target && K / (p.split * 2) >= 256) p.split *= 2;
+  while (p.split < 64 && tiles * p.split * 2 <= target && K / (p.split * 2) >= 256) p.split *= 2;
   return p;
 }
 
@@ -827,7 +857,9 @@ extern "C" int fbn_gemm(const void* A, const void* B, float* C, const float* bia
     const size_t total = v4 ? (size_t)M * N / 4 : (size_t)M * N;
     int blocks = (int)((total + 255) / 256);
     if (blocks > 4096) blocks = 4096;
-    if (v4) hipLaunchKernelGGL(gemm_splitk_reduce4, dim3(blocks), dim3(256), 0, st, g, p.split);
+    if (v4 && p.split >= 16 && total < (size_t)65536)
+      hipLaunchKernelGGL(gemm_splitk_reduce4_wide, dim3((unsigned)((total + 15) / 16)), dim3(256), 0, st, g, p.split);
+    else if (v4) hipLaunchKernelGGL(gemm_splitk_reduce4, dim3(blocks), dim3(256), 0, st, g, p.split);
     else hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, st, g, p.split);
     FBN_CHECK_LAUNCH();
   }

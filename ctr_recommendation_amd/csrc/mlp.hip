@@ -205,6 +205,55 @@ __global__ void bn_act_fwd_kernel(const float* __restrict__ X, float* __restrict
   }
 }
 
+// Column-blocked form: block = 64 column quads (256 columns) x 4 row lanes over a chunk of rows,
+// the per-column affine (alpha, beta') computed once per thread, no index division.  Same
+// Philox counter (flat quad index) and arithmetic as bn_act_fwd_kernel.
+__global__ void __launch_bounds__(256) bn_act_fwd2_kernel(const float* __restrict__ X, float* __restrict__ Y, int B,
+                                                          int C, int rows_per_chunk, const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd,
+                                                          const float* __restrict__ g, const float* __restrict__ bta,
+                                                          float p_drop, const unsigned long long* __restrict__ rng,
+                                                          unsigned stream_id, unsigned char* __restrict__ mask_out,
+                                                          const unsigned char* __restrict__ mask_in,
+                                                          short* __restrict__ Y16) {
+  const int q = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 256 + q * 4;
+  if (c >= C) return;
+  const int r0 = blockIdx.y * rows_per_chunk, r1 = min(B, r0 + rows_per_chunk);
+  const float keep = 1.f - p_drop;
+  const float scale = p_drop > 0.f ? 1.0f / keep : 1.f;
+  uint32_t k0 = 0, k1 = 0, off = 0;
+  if (rng) { k0 = (uint32_t)rng[0]; k1 = (uint32_t)(rng[0] >> 32); off = (uint32_t)rng[1]; }
+  float alpha[4], bp[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    alpha[e] = invstd[c + e] * g[c + e];
+    bp[e] = bta[c + e] - mean[c + e] * alpha[e];
+  }
+  for (int r = r0 + rl; r < r1; r += 4) {
+    const size_t i = (size_t)r * C + c, i4 = i >> 2;
+    const f32x4 x = *reinterpret_cast<const f32x4*>(X + i);
+    float um[4] = {1.f, 1.f, 1.f, 1.f};
+    if (p_drop > 0.f && !mask_in) {
+      const Philox4 rr = philox4x32_10((uint32_t)i4, (uint32_t)(i4 >> 32), stream_id, off, k0, k1);
+      um[0] = u01(rr.x); um[1] = u01(rr.y); um[2] = u01(rr.z); um[3] = u01(rr.w);
+    }
+    f32x4 y;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float v = fmaxf(x[e] * alpha[e] + bp[e], 0.f);
+      if (p_drop > 0.f) {
+        const bool kept = mask_in ? mask_in[i + e] != 0 : um[e] < keep;
+        v = kept ? v * scale : 0.f;
+        if (mask_out) mask_out[i + e] = kept ? 1 : 0;
+      }
+      y[e] = v;
+    }
+    *reinterpret_cast<f32x4*>(Y + i) = y;
+    if (Y16) store4(Y16 + i, y);
+  }
+}
+
 // ------------------------------------------------------------------ BN backward
 // dy[b][c] = G[b][c] * fac(hact)  (matrix source)  or  gvec[b] * w[c] * fac(hact)  (rank-1 head source)
 // fac = scale if hact > 0 else 0  (ReLU-after-BN + dropout recovered from the stored activation)
@@ -666,8 +715,9 @@ extern "C" int fbn_bn_act_fwd(const float* X, float* Y, int B, int C, const floa
   if (B <= 0) return FBN_OK;
   if (C & 3) { fbn_set_error("bn_act: C % 4"); return FBN_ERR_ARG; }
   if (p_drop > 0.f && !rng && !mask_in) { fbn_set_error("bn_act: dropout needs an rng state or a mask"); return FBN_ERR_ARG; }
-  hipLaunchKernelGGL(bn_act_fwd_kernel, dim3(ew_grid((size_t)B * C / 4)), dim3(256), 0, (hipStream_t)stream, X, Y, B,
-                     C, mean, invstd, g, b, p_drop, rng, stream_id, mask_out, mask_in, Y16);
+  const int rpc = 16;
+  hipLaunchKernelGGL(bn_act_fwd2_kernel, dim3(fbn_cdiv(C, 256), fbn_cdiv(B, rpc)), dim3(256), 0, (hipStream_t)stream, X,
+                     Y, B, C, rpc, mean, invstd, g, b, p_drop, rng, stream_id, mask_out, mask_in, Y16);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

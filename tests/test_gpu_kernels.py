@@ -63,7 +63,7 @@ def test_gemm_fused_bn_stats(hip_device, M, N, K, bf16):
 
 @pytest.mark.parametrize("transA,transB", [(False, True), (False, False), (True, False), (True, True)])
 @pytest.mark.parametrize("M,N,K", [(8192, 512, 1920), (200, 136, 256), (512, 1920, 8192), (256, 512, 4096),
-                                   (1000, 72, 128)])
+                                   (1000, 72, 128), (128, 128, 16384)])
 def test_gemm_bf16_all_layouts(hip_device, transA, transB, M, N, K):
     """bf16 operands in every storage layout (the LDS-DMA kernel: K % 64 == 0; ragged M / N
     tiles; the split-K plans of the wgrad shapes) against torch with the same bf16 inputs."""
