@@ -257,155 +257,214 @@ __device__ __forceinline__ void atomic_add_row_t(float* row, const f32x4& t, int
   atomicAdd(row + 3 * G + q, t[3]);
 }
 
-template <int D, int MODE>
+// Backward of the fields.  No LDS atomics (they serialised on the few hot addresses every
+// sample adds into -- the LN columns, 11 cate rows, the SENET weights -- and cost ~25 LDS cycles
+// each): the LN and SENET parameter gradients accumulate in registers (SENET's group-uniform
+// entries spread over the group's lanes: entry k in lane k mod G), the cate rows by plain
+// read-modify-write into a per-wave LDS slice with the wave's sample groups taking turns; each
+// wave folds its groups with shuffles into its slice, and the block sums its 4 slices into its
+// partial row (same layout as before).
+template <int D, int MODE, int RMAX>
 __global__ void __launch_bounds__(256) fields_bwd_kernel(FieldBwdArgs p) {
   constexpr int G = D / 4;
   constexpr int SPW = 64 / G;
-  extern __shared__ __attribute__((aligned(16))) float sp[];   // P floats of block partials
+  constexpr int NPMAX = 13 * RMAX + 6;
+  constexpr int SJ = (NPMAX + G - 1) / G;          // SENET entries per lane
+  extern __shared__ __attribute__((aligned(16))) float sp[];   // 4 wave slices of P floats + SENET staging
   const int R = p.R;
-  const int P = 13 * R + 6 + 2 * D + p.n_cate * D;
-  float* s_w1 = sp;                 // [R][6]
-  float* s_b1 = s_w1 + 6 * R;       // [R]
-  float* s_w2 = s_b1 + R;           // [6][R]
-  float* s_b2 = s_w2 + 6 * R;       // [6]
-  float* s_lg = s_b2 + 6;           // [D]
-  float* s_lb = s_lg + D;           // [D]
-  float* s_ct = s_lb + D;           // [n_cate][D]
-  for (int i = threadIdx.x; i < P; i += blockDim.x) sp[i] = 0.f;
+  const int NP = 13 * R + 6;
+  const int P = NP + 2 * D + p.n_cate * D;
+  const int wave = threadIdx.x >> 6;
+  float* ws = sp + wave * P;                       // this wave's slice
+  // per group: {ds[6], z[6], dq[R], rj[R]} staged for the lanes that own SENET entries
+  float* sv = sp + 4 * P + (wave * SPW + (threadIdx.x & 63) / G) * (12 + 2 * RMAX);
+  for (int i = threadIdx.x; i < 4 * P; i += blockDim.x) sp[i] = 0.f;
   __syncthreads();
+  float* w_lg = ws + NP;
+  float* w_ct = w_lg + 2 * D;
 
   const int lane = threadIdx.x & 63;
-  const int q = lane % G;
+  const int q = lane % G, grp = lane / G;
   const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nwaves = (gridDim.x * blockDim.x) >> 6;
   const int L = p.L;
+  f32x4 acc_lg = {0.f, 0.f, 0.f, 0.f}, acc_lb = {0.f, 0.f, 0.f, 0.f};
+  float acc_se[SJ];
+#pragma unroll
+  for (int j = 0; j < SJ; ++j) acc_se[j] = 0.f;
 
   for (int b0 = gw * SPW; b0 < p.B; b0 += nwaves * SPW) {
-    const int b = b0 + lane / G;
-    if (b >= p.B) continue;
-    const float* Xb = p.X + (size_t)b * 5 * D + 4 * q;
-    const float* dVb = p.dV + (size_t)b * 5 * D + 4 * q;
-    f32x4 x[5], dv[5];
+    const int b = b0 + grp;
+    const bool live = b < p.B;
+    f32x4 dx0 = {0.f, 0.f, 0.f, 0.f}, dx1 = {0.f, 0.f, 0.f, 0.f};
+    long long lk = -1, vw = -1;
+    if (live) {
+      const float* Xb = p.X + (size_t)b * 5 * D + 4 * q;
+      const float* dVb = p.dV + (size_t)b * 5 * D + 4 * q;
+      f32x4 x[5], dv[5];
 #pragma unroll
-    for (int f = 0; f < 5; ++f) {
-      x[f] = *reinterpret_cast<const f32x4*>(Xb + f * D);
-      dv[f] = *reinterpret_cast<const f32x4*>(dVb + f * D);
-    }
-    float a[6];
+      for (int f = 0; f < 5; ++f) {
+        x[f] = *reinterpret_cast<const f32x4*>(Xb + f * D);
+        dv[f] = *reinterpret_cast<const f32x4*>(dVb + f * D);
+      }
+      const f32x4 h = *reinterpret_cast<const f32x4*>(p.hmm + (size_t)b * D + 4 * q);
+      lk = p.likes[b];
+      vw = p.views[b];
+      float a[6];
 #pragma unroll
-    for (int f = 0; f < 6; ++f) a[f] = p.a[(size_t)b * 6 + f];
-    // recompute squeeze + hidden exactly as the forward did
-    float z[6];
-    z[0] = 0.f;
+      for (int f = 0; f < 6; ++f) a[f] = p.a[(size_t)b * 6 + f];
+      // recompute squeeze + hidden exactly as the forward did
+      float z[6];
+      z[0] = 0.f;
 #pragma unroll
-    for (int f = 0; f < 5; ++f) z[f + 1] = group_sum<G>(x[f][0] + x[f][1] + x[f][2] + x[f][3]) / (float)D;
-    float qv[FBN_MAXR];
-    for (int j = 0; j < R; ++j) {
-      float s = p.b1[j];
+      for (int f = 0; f < 5; ++f) z[f + 1] = group_sum<G>(x[f][0] + x[f][1] + x[f][2] + x[f][3]) / (float)D;
+      float qv[RMAX], rj[RMAX], dq[RMAX];
 #pragma unroll
-      for (int f = 0; f < 6; ++f) s += p.w1[j * 6 + f] * z[f];
-      qv[j] = s;
-    }
-    // excitation backward
-    float ds[6];
-    ds[0] = 0.f;   // da_0 = sum(dV_0 * X_0) = 0 since X_0 == 0
+      for (int j = 0; j < RMAX; ++j) {
+        float s = 0.f;
+        if (j < R) {
+          s = p.b1[j];
 #pragma unroll
-    for (int f = 0; f < 5; ++f) {
-      const float da = group_sum<G>(dv[f][0] * x[f][0] + dv[f][1] * x[f][1] + dv[f][2] * x[f][2] + dv[f][3] * x[f][3]);
-      ds[f + 1] = da * (1.f - a[f + 1]) * a[f + 1];
-    }
-    float dz[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int j = 0; j < R; ++j) {
-      float dr = 0.f;
+          for (int f = 0; f < 6; ++f) s += p.w1[j * 6 + f] * z[f];
+        }
+        qv[j] = s;
+        rj[j] = fmaxf(s, 0.f);
+      }
+      // excitation backward
+      float ds[6];
+      ds[0] = 0.f;   // da_0 = sum(dV_0 * X_0) = 0 since X_0 == 0
 #pragma unroll
-      for (int f = 0; f < 6; ++f) dr += p.w2[f * R + j] * ds[f];
-      const float rj = fmaxf(qv[j], 0.f);
-      const float dq = qv[j] > 0.f ? dr : 0.f;
+      for (int f = 0; f < 5; ++f) {
+        const float da = group_sum<G>(dv[f][0] * x[f][0] + dv[f][1] * x[f][1] + dv[f][2] * x[f][2] + dv[f][3] * x[f][3]);
+        ds[f + 1] = da * (1.f - a[f + 1]) * a[f + 1];
+      }
+      float dz[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < RMAX; ++j) {
+        float dr = 0.f;
+        if (j < R) {
+#pragma unroll
+          for (int f = 0; f < 6; ++f) dr += p.w2[f * R + j] * ds[f];
+        }
+        dq[j] = (j < R && qv[j] > 0.f) ? dr : 0.f;
+        if (j < R) {
+#pragma unroll
+          for (int f = 0; f < 6; ++f) dz[f] += p.w1[j * 6 + f] * dq[j];
+        }
+      }
+      // SENET parameter-gradient entries (group-uniform): lane q owns entries q, q+G, ... of the
+      // flattened [w1 R*6 | b1 R | w2 6*R | b2 6]; the values come through LDS (runtime indices
+      // into registers would go to scratch)
       if (q == 0) {
 #pragma unroll
-        for (int f = 0; f < 6; ++f) {
-          atomicAdd(&s_w2[f * R + j], ds[f] * rj);
-          atomicAdd(&s_w1[j * 6 + f], dq * z[f]);
-        }
-        atomicAdd(&s_b1[j], dq);
+        for (int f = 0; f < 6; ++f) { sv[f] = ds[f]; sv[6 + f] = z[f]; }
+#pragma unroll
+        for (int jj = 0; jj < RMAX; ++jj) { sv[12 + jj] = dq[jj]; sv[12 + RMAX + jj] = rj[jj]; }
       }
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int f = 0; f < 6; ++f) dz[f] += p.w1[j * 6 + f] * dq;
-    }
-    if (q == 0) {
+      for (int j = 0; j < SJ; ++j) {
+        const int k = q + j * G;
+        float v = 0.f;
+        if (k < 6 * R) v = sv[12 + k / 6] * sv[6 + k % 6];                                  // dq_j * z_f
+        else if (k < 7 * R) v = sv[12 + (k - 6 * R)];                                        // dq_j
+        else if (k < 13 * R) v = sv[(k - 7 * R) / R] * sv[12 + RMAX + (k - 7 * R) % R];      // ds_f * r_j
+        else if (k < NP) v = sv[k - 13 * R];                                                 // ds_f
+        acc_se[j] += v;
+      }
+      __builtin_amdgcn_wave_barrier();
+      f32x4 dx[5];
 #pragma unroll
-      for (int f = 0; f < 6; ++f) atomicAdd(&s_b2[f], ds[f]);
-    }
-    f32x4 dx[5];
-#pragma unroll
-    for (int f = 0; f < 5; ++f) dx[f] = dv[f] * a[f + 1] + dz[f + 1] / (float)D;
+      for (int f = 0; f < 5; ++f) dx[f] = dv[f] * a[f + 1] + dz[f + 1] / (float)D;
+      dx0 = dx[0];
+      dx1 = dx[1];
 
-    // field 4: ReLU + LayerNorm backward -> d(h_mm)
-    {
-      const f32x4 h = *reinterpret_cast<const f32x4*>(p.hmm + (size_t)b * D + 4 * q);
-      const float mean = group_sum<G>(h[0] + h[1] + h[2] + h[3]) / (float)D;
-      const f32x4 dh = h - mean;
-      const float s2 = group_sum<G>(dh[0] * dh[0] + dh[1] * dh[1] + dh[2] * dh[2] + dh[3] * dh[3]);
-      const float rstd = 1.f / sqrtf(s2 / (float)D + p.ln_eps);
-      const f32x4 gam = *reinterpret_cast<const f32x4*>(p.ln_g + 4 * q);
-      f32x4 gl, xh, gx;
+      // field 4: ReLU + LayerNorm backward -> d(h_mm)
+      {
+        const float mean = group_sum<G>(h[0] + h[1] + h[2] + h[3]) / (float)D;
+        const f32x4 dh = h - mean;
+        const float s2 = group_sum<G>(dh[0] * dh[0] + dh[1] * dh[1] + dh[2] * dh[2] + dh[3] * dh[3]);
+        const float rstd = 1.f / sqrtf(s2 / (float)D + p.ln_eps);
+        const f32x4 gam = *reinterpret_cast<const f32x4*>(p.ln_g + 4 * q);
+        f32x4 gl, xh, gx;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        gl[e] = x[3][e] > 0.f ? dx[3][e] : 0.f;
-        xh[e] = dh[e] * rstd;
-        gx[e] = gl[e] * gam[e];
-        atomicAdd(&s_lg[4 * q + e], gl[e] * xh[e]);
-        atomicAdd(&s_lb[4 * q + e], gl[e]);
+        for (int e = 0; e < 4; ++e) {
+          gl[e] = x[3][e] > 0.f ? dx[3][e] : 0.f;
+          xh[e] = dh[e] * rstd;
+          gx[e] = gl[e] * gam[e];
+          acc_lg[e] += gl[e] * xh[e];
+          acc_lb[e] += gl[e];
+        }
+        const float m1 = group_sum<G>(gx[0] + gx[1] + gx[2] + gx[3]) / (float)D;
+        const float m2 = group_sum<G>(gx[0] * xh[0] + gx[1] * xh[1] + gx[2] * xh[2] + gx[3] * xh[3]) / (float)D;
+        f32x4 out;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) out[e] = rstd * (gx[e] - m1 - xh[e] * m2);
+        *reinterpret_cast<f32x4*>(p.dhmm + (size_t)b * D + 4 * q) = out;
+        if (p.dhmm16)
+          *reinterpret_cast<bf16x4*>(p.dhmm16 + (size_t)b * D + 4 * q) = (bf16x4){f2bf(out[0]), f2bf(out[1]),
+                                                                                   f2bf(out[2]), f2bf(out[3])};
       }
-      const float m1 = group_sum<G>(gx[0] + gx[1] + gx[2] + gx[3]) / (float)D;
-      const float m2 = group_sum<G>(gx[0] * xh[0] + gx[1] * xh[1] + gx[2] * xh[2] + gx[3] * xh[3]) / (float)D;
-      f32x4 out;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) out[e] = rstd * (gx[e] - m1 - xh[e] * m2);
-      *reinterpret_cast<f32x4*>(p.dhmm + (size_t)b * D + 4 * q) = out;
-      if (p.dhmm16)
-        *reinterpret_cast<bf16x4*>(p.dhmm16 + (size_t)b * D + 4 * q) = (bf16x4){f2bf(out[0]), f2bf(out[1]), f2bf(out[2]),
-                                                                                 f2bf(out[3])};
-    }
-    // cate table (likes, views share one table)
-    {
-      long long lk = p.likes[b], vw = p.views[b];
-      if (lk >= 0 && lk < p.n_cate)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) atomicAdd(&s_ct[lk * D + 4 * q + e], dx[0][e]);
-      if (vw >= 0 && vw < p.n_cate)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) atomicAdd(&s_ct[vw * D + 4 * q + e], dx[1][e]);
-    }
-    // item table: dX3 -> row item_id, dX5 / count -> each non-padding history row
-    const f32x4 gh = dx[4] / p.cnt[b];
-    if (MODE == 0 && p.gvec) {
-      // sparse mode: plain stores; rows are resolved later through map / slot_row
-      *reinterpret_cast<f32x4*>(p.gvec + (size_t)b * 2 * D + 4 * q) = dx[2];
-      *reinterpret_cast<f32x4*>(p.gvec + ((size_t)b * 2 + 1) * D + 4 * q) = gh;
-    } else if (MODE == 0) {
-      const f32x4 ti = transpose_cols<G>(dx[2], lane);
-      const f32x4 th = transpose_cols<G>(gh, lane);
-      const long long item = p.item_id[b];
-      if (item > 0 && item < p.V) {
-        atomic_add_row_t<G>(p.gtab + item * D, ti, q);
+      // item table: dX3 -> row item_id, dX5 / count -> each non-padding history row
+      const f32x4 gh = dx[4] / p.cnt[b];
+      if (MODE == 0 && p.gvec) {
+        // sparse mode: plain stores; rows are resolved later through map / slot_row
+        *reinterpret_cast<f32x4*>(p.gvec + (size_t)b * 2 * D + 4 * q) = dx[2];
+        *reinterpret_cast<f32x4*>(p.gvec + ((size_t)b * 2 + 1) * D + 4 * q) = gh;
+      } else if (MODE == 0) {
+        const f32x4 ti = transpose_cols<G>(dx[2], lane);
+        const f32x4 th = transpose_cols<G>(gh, lane);
+        const long long item = p.item_id[b];
+        if (item > 0 && item < p.V) atomic_add_row_t<G>(p.gtab + item * D, ti, q);
+        for (int t = 0; t < L; ++t) {
+          const long long s = p.item_seq[(size_t)b * L + t];
+          if (s > 0 && s < p.V) atomic_add_row_t<G>(p.gtab + s * D, th, q);
+        }
+      } else {
+        const int* pb = p.pos + (size_t)b * (L + 1);
+        if (pb[0] >= 0) *reinterpret_cast<f32x4*>(p.sendbuf + (size_t)pb[0] * D + 4 * q) = dx[2];
+        for (int t = 0; t < L; ++t)
+          if (pb[t + 1] >= 0) *reinterpret_cast<f32x4*>(p.sendbuf + (size_t)pb[t + 1] * D + 4 * q) = gh;
       }
-      for (int t = 0; t < L; ++t) {
-        const long long s = p.item_seq[(size_t)b * L + t];
-        if (s > 0 && s < p.V) {
-          atomic_add_row_t<G>(p.gtab + s * D, th, q);
+    }
+    // cate table (likes, views share one table): the wave's groups take turns on its slice
+#pragma unroll
+    for (int gi = 0; gi < SPW; ++gi) {
+      if (grp == gi && live) {
+        if (lk >= 0 && lk < p.n_cate) {
+          f32x4* c = reinterpret_cast<f32x4*>(w_ct + lk * D + 4 * q);
+          *c = *c + dx0;
+        }
+        if (vw >= 0 && vw < p.n_cate) {
+          f32x4* c = reinterpret_cast<f32x4*>(w_ct + vw * D + 4 * q);
+          *c = *c + dx1;
         }
       }
-    } else {
-      const int* pb = p.pos + (size_t)b * (L + 1);
-      if (pb[0] >= 0) *reinterpret_cast<f32x4*>(p.sendbuf + (size_t)pb[0] * D + 4 * q) = dx[2];
-      for (int t = 0; t < L; ++t)
-        if (pb[t + 1] >= 0) *reinterpret_cast<f32x4*>(p.sendbuf + (size_t)pb[t + 1] * D + 4 * q) = gh;
+    }
+  }
+  // fold the wave's groups (lanes q, q+G, ... hold the same entries / columns) into group 0
+#pragma unroll
+  for (int o = G; o < 64; o <<= 1) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      acc_lg[e] += __shfl_xor(acc_lg[e], o, 64);
+      acc_lb[e] += __shfl_xor(acc_lb[e], o, 64);
+    }
+#pragma unroll
+    for (int j = 0; j < SJ; ++j) acc_se[j] += __shfl_xor(acc_se[j], o, 64);
+  }
+  if (grp == 0) {
+    *reinterpret_cast<f32x4*>(w_lg + 4 * q) = acc_lg;
+    *reinterpret_cast<f32x4*>(w_lg + D + 4 * q) = acc_lb;
+#pragma unroll
+    for (int j = 0; j < SJ; ++j) {
+      const int k = q + j * G;
+      if (k < NP) ws[k] = acc_se[j];
     }
   }
   __syncthreads();
   float* out = p.partials + (size_t)blockIdx.x * P;
-  for (int i = threadIdx.x; i < P; i += blockDim.x) out[i] = sp[i];
+  for (int i = threadIdx.x; i < P; i += blockDim.x) out[i] = (sp[i] + sp[P + i]) + (sp[2 * P + i] + sp[3 * P + i]);
 }
 
 // Sum per-block partial slabs: out[i] = sum_b part[b][i], in a fixed order (deterministic).
@@ -444,11 +503,14 @@ __global__ void reduce_partials_l2(const float* part, int nblk, int P, GradOuts 
 }
 
 // ------------------------------------------------------------------------------ C ABI
-static int fields_grid(int B, int D) {
+#ifndef FBN_FB_MAXBLK
+#define FBN_FB_MAXBLK 512    // backward: partial rows to reduce vs samples in flight (tools/time_fields.py)
+#endif
+static int fields_grid(int B, int D, int cap = 1024) {
   const int spw = 64 / (D / 4);
   const int waves = (B + spw - 1) / spw;
   int blocks = (waves + 3) / 4;
-  return blocks < 1 ? 1 : (blocks > 1024 ? 1024 : blocks);
+  return blocks < 1 ? 1 : (blocks > cap ? cap : blocks);
 }
 
 template <int MODE>
@@ -492,22 +554,29 @@ extern "C" int fbn_fields_fwd(const int64_t* item_id, const int64_t* item_seq, c
 
 extern "C" int fbn_fields_bwd_partials_size(int D, int R, int n_cate) { return 13 * R + 6 + 2 * D + n_cate * D; }
 // rows of the `partials` scratch the caller allocates: one per block + RED_CH reduction rows
-extern "C" int fbn_fields_bwd_grid(int B, int D) { return fields_grid(B, D) + RED_CH; }
+extern "C" int fbn_fields_bwd_grid(int B, int D) { return fields_grid(B, D, FBN_FB_MAXBLK) + RED_CH; }
 
-template <int MODE>
-static int launch_fields_bwd(const FieldBwdArgs& a, int D, hipStream_t st) {
-  const int grid = fields_grid(a.B, D);
-  const size_t lds = (size_t)(13 * a.R + 6 + 2 * D + a.n_cate * D) * sizeof(float);
+template <int MODE, int RMAX>
+static int launch_fields_bwd_r(const FieldBwdArgs& a, int D, hipStream_t st) {
+  const int grid = fields_grid(a.B, D, FBN_FB_MAXBLK);
+  const size_t lds = (4 * (size_t)(13 * a.R + 6 + 2 * D + a.n_cate * D) + 4 * (64 / (D / 4)) * (12 + 2 * RMAX)) *
+                     sizeof(float);   // 4 wave slices + SENET staging
   switch (D) {
-    case 16: hipLaunchKernelGGL((fields_bwd_kernel<16, MODE>), dim3(grid), dim3(256), lds, st, a); break;
-    case 32: hipLaunchKernelGGL((fields_bwd_kernel<32, MODE>), dim3(grid), dim3(256), lds, st, a); break;
-    case 64: hipLaunchKernelGGL((fields_bwd_kernel<64, MODE>), dim3(grid), dim3(256), lds, st, a); break;
-    case 128: hipLaunchKernelGGL((fields_bwd_kernel<128, MODE>), dim3(grid), dim3(256), lds, st, a); break;
-    case 256: hipLaunchKernelGGL((fields_bwd_kernel<256, MODE>), dim3(grid), dim3(256), lds, st, a); break;
+    case 16: hipLaunchKernelGGL((fields_bwd_kernel<16, MODE, RMAX>), dim3(grid), dim3(256), lds, st, a); break;
+    case 32: hipLaunchKernelGGL((fields_bwd_kernel<32, MODE, RMAX>), dim3(grid), dim3(256), lds, st, a); break;
+    case 64: hipLaunchKernelGGL((fields_bwd_kernel<64, MODE, RMAX>), dim3(grid), dim3(256), lds, st, a); break;
+    case 128: hipLaunchKernelGGL((fields_bwd_kernel<128, MODE, RMAX>), dim3(grid), dim3(256), lds, st, a); break;
+    case 256: hipLaunchKernelGGL((fields_bwd_kernel<256, MODE, RMAX>), dim3(grid), dim3(256), lds, st, a); break;
     default: fbn_set_error("fields: embedding_dim must be one of 16,32,64,128,256"); return FBN_ERR_UNSUPPORTED;
   }
   FBN_CHECK_LAUNCH();
   return FBN_OK;
+}
+
+// the reference's SENET width is 3 (reduction ratio 3 over 6 fields): register arrays sized 3
+template <int MODE>
+static int launch_fields_bwd(const FieldBwdArgs& a, int D, hipStream_t st) {
+  return a.R <= 3 ? launch_fields_bwd_r<MODE, 3>(a, D, st) : launch_fields_bwd_r<MODE, FBN_MAXR>(a, D, st);
 }
 
 // partials: [fbn_fields_bwd_grid(B,D)][fbn_fields_bwd_partials_size(D,R,n_cate)] scratch;
@@ -531,7 +600,7 @@ extern "C" int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, c
   int rc = pos ? launch_fields_bwd<1>(p, D, st) : launch_fields_bwd<0>(p, D, st);
   if (rc) return rc;
   const int P = 13 * R + 6 + 2 * D + n_cate * D;
-  const int nblk = fields_grid(B, D);
+  const int nblk = fields_grid(B, D, FBN_FB_MAXBLK);
   hipLaunchKernelGGL(reduce_partials_l1, dim3(fbn_cdiv(P, 64), RED_CH), dim3(256), 0, st, partials, nblk, P);
   GradOuts o;
   const int sizes[7] = {6 * R, R, 6 * R, 6, D, D, n_cate * D};

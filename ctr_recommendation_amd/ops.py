@@ -393,7 +393,8 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
              table_grad: Optional[torch.Tensor] = None, gvec: Optional[torch.Tensor] = None,
              pos: Optional[torch.Tensor] = None,
              sendbuf: Optional[torch.Tensor] = None, coll: Collective = NO_COLLECTIVE,
-             ntot: Optional[int] = None, extra_sums=(), side: Optional["torch.cuda.Stream"] = None) -> None:
+             ntot: Optional[int] = None, extra_sums=(), side: Optional["torch.cuda.Stream"] = None,
+             probe: Optional[Dict[str, list]] = None) -> None:
     """Backward from dL/dlogit (gout [B]) into the gradient buffers ``g`` (same keys as ``p``).
 
     table_grad: dense [V, d] (drop-in, accumulated by atomics); or gvec [B, 2, d] (native
@@ -484,11 +485,18 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
             "senet.excitation.2.bias", "mm_proj.1.weight", "mm_proj.1.bias", "cate_emb.weight")
     outs_arr = (ctypes.c_void_p * 7)(*[g[k].data_ptr() for k in keys])   # host array of device pointers
     outs = ctypes.cast(outs_arr, ctypes.c_void_p).value
+    evb = None
+    if probe is not None:                       # bench / tools: events around the fields backward
+        evb = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        evb[0].record()
+        probe.setdefault("fields_bwd", []).append(evb)
     call("fbn_fields_bwd", ptr(batch["item_id"]), ptr(seq) if Lr else None, ptr(batch["likes_level"]),
          ptr(batch["views_level"]), ptr(a["hmm"]), ptr(p["mm_proj.1.weight"]), LN_EPS,
          ptr(p["senet.excitation.0.weight"]), ptr(p["senet.excitation.0.bias"]), ptr(p["senet.excitation.2.weight"]),
          R, ncate, ptr(a["X"]), ptr(a["a"]), ptr(a["cnt"]), ptr(dV), ptr(dhmm), ptr(dhmm16), ptr(partials), outs,
          ptr(table_grad), ptr(gvec), V, ptr(pos), ptr(sendbuf), B, Lr, d, st)
+    if evb is not None:
+        evb[1].record()
     if bf:
         wg.run(lambda s: gemm(dhmm16, w16["x"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True, False, stream=s))
     else:

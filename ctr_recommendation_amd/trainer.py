@@ -232,7 +232,7 @@ class FiBiNETTrainer:
         sendbuf = self.xchg.make_sendbuf() if self.xchg is not None else None
         ops.backward(self.p, batch, a, a["gout"], self.g, cfg, gvec=self.gvec if self.xchg is None else None,
                      pos=pos, sendbuf=sendbuf, coll=self.coll, ntot=ntot,
-                     extra_sums=[(a["loss_terms"], B, 1, self.loss, 1.0 / ntot)])
+                     extra_sums=[(a["loss_terms"], B, 1, self.loss, 1.0 / ntot)], probe=probe)
         if self.xchg is None:
             # single GPU: per-sample vectors; entry e = b*(L+1)+t; duplicates -> extra[claimer]
             gsrc = (self.gvec, self.extra, L + 1)

@@ -1,5 +1,5 @@
-"""Time fbn_fields_fwd alone at C3 shapes (B=8192, d=128, L=20, V=1.25M, bf16 c) for the library
-selected by FBN_LIB_PATH; prints the average launch time and the SURVEY 8(d) roofline fraction."""
+"""Time fbn_fields_fwd and fbn_fields_bwd (with its partial reductions) at C3 shapes (B=8192,
+d=128, L=20, V=1.25M, bf16) for the library selected by FBN_LIB_PATH."""
 import os
 import sys
 
@@ -16,15 +16,24 @@ cfg = {"embedding_dim": d, "vocab_size": 4}
 small = build_model(None, cfg).state_dict()
 p = {k: v.to(dev) for k, v in small.items()}
 p["item_emb.weight"] = torch.randn((V, d), device=dev)
-batch, _ = make_device_batches(1, B, V, L, dev, seed=3)[0]
+g = {k: torch.zeros_like(v) for k, v in p.items() if v.is_floating_point()}
+batch, labels = make_device_batches(1, B, V, L, dev, seed=3)[0]
+gvec = torch.zeros((B, 2, d), device=dev)
 a = {}
 fc = ops.FwdConfig(d=d, L=L, training=True, p_drop=0.0, bf16=True, bilinear_each=False, R=3)
 probe = {}
 for i in range(30):
-    ops.forward(p, batch, fc, None, acts=a, probe=probe)
+    a = ops.forward(p, batch, fc, None, acts=a, probe=probe, labels=labels, loss_denom=float(B))
+    ops.backward(p, batch, a, a["gout"], g, fc, gvec=gvec, probe=probe)
 torch.cuda.synchronize()
-ev = probe["fields_fwd"][10:]
-ms = sum(s.elapsed_time(e) for s, e in ev) / len(ev)
+
+
+def avg(name):
+    ev = probe[name][10:]
+    return sum(s.elapsed_time(e) for s, e in ev) / len(ev)
+
+
+fwd, bwd = avg("fields_fwd"), avg("fields_bwd")
 byts = ((L + 1) * d * 4 + (L + 3) * 8 + 4 * d * 4) * B
-print(f"{os.environ.get('FBN_LIB_PATH', 'default')}: fields_fwd {ms * 1e3:.1f} us  {byts / ms / 1e6:.0f} GB/s "
-      f"({byts / ms / 1e6 / 8000:.3f} of 8 TB/s)")
+print(f"{os.environ.get('FBN_LIB_PATH', 'default')}: fields_fwd {fwd * 1e3:.1f} us ({byts / fwd / 1e6 / 8000:.3f} "
+      f"of 8 TB/s)  fields_bwd {bwd * 1e3:.1f} us")

@@ -16,13 +16,21 @@ OUT = os.path.join(ROOT, "tools", "variants")
 
 
 def build_variant(name, flags):
+    """flags may contain SRC=<dir> to compile the sources of another tree (e.g. a git worktree)."""
     os.makedirs(OUT, exist_ok=True)
+    csrc = B.CSRC
+    fl = []
+    for f in flags.split():
+        if f.startswith("SRC="):
+            csrc = f[4:]
+        else:
+            fl.append(f)
     objs = []
     for src in B.SOURCES:
         obj = os.path.join(OUT, f"{name}_{src}.o")
-        cmd = [B.HIPCC] + B.FLAGS + flags.split() + ["-c", os.path.join(B.CSRC, src), "-o", obj]
+        cmd = [B.HIPCC] + B.FLAGS + fl + ["-I", csrc, "-c", os.path.join(csrc, src), "-o", obj]
         if src.endswith(".cpp"):
-            cmd = [B.HIPCC, "-O3", "-fPIC", "-std=c++17", "-c", os.path.join(B.CSRC, src), "-o", obj]
+            cmd = [B.HIPCC, "-O3", "-fPIC", "-std=c++17", "-c", os.path.join(csrc, src), "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode:
             raise SystemExit(r.stderr)
