@@ -248,16 +248,22 @@ def main():
     traffic = _pmc_traffic()
     add("fields_fwd", "fields_fwd (fused gather + history mean + LN + SENET)", avg_ms("fields_fwd"),
         gather_bytes_per_sample(d) * B, "GB/s", HBM_PEAK_GBS, "hbm", "SURVEY 8(d) 12,984 B/sample x batch")
-    add("adam_catchup", "adam_catchup (lazy table Adam: claimed rows + rolling window)", avg_ms("adam_catchup"),
-        catchup_bytes(touched + window, d, B * (L + 1)), "GB/s", HBM_PEAK_GBS, "hbm",
-        f"(touched {touched} + window {window} rows) x (24 B x d + 8 B) + 4 B per entry")
+    # the probed launch is the claimed-row pass only (the rolling window runs on the side stream)
+    add("adam_catchup", "adam_catchup (lazy table Adam: rows claimed this step)", avg_ms("adam_catchup"),
+        catchup_bytes(touched, d, B * (L + 1)), "GB/s", HBM_PEAK_GBS, "hbm",
+        f"touched {touched} rows x (24 B x d + 8 B) + 4 B per entry")
+    add("adam_window", "adam_catchup (lazy table Adam: rolling window, side stream)", avg_ms("adam_window"),
+        catchup_bytes(window, d, 0), "GB/s", HBM_PEAK_GBS, "hbm",
+        f"window {window} rows x (24 B x d + 8 B); VALU-bound replay of up to F steps per row")
     add("gemm_mlp0", "gemm MLP layer 1 (B x 15d -> 512, bf16 MFMA)", avg_ms("gemm_mlp0"),
         2.0 * B * 512 * 15 * d, "TFLOP/s", MFMA_PEAK_TFS if args.dtype == "bf16" else FP32_MFMA_PEAK_TFS, "mfma",
         "2 x B x 512 x 15d")
     if tr.table_adam == "eager":
         add("adam_table", "adam_table (eager: every untouched row each step)", avg_ms("adam_table"),
             24 * tr.rows_local * d + 4 * tr.rows_local, "GB/s", HBM_PEAK_GBS, "hbm", "24 B x rows x d + 4 B x rows")
-    dominant = max(rooflines, key=lambda r: r["avg_launch_ms"]) if rooflines else None
+    # the dominant kernel of the step's critical path (main stream; the window replay overlaps it)
+    main_k = [r for r in rooflines if "side stream" not in r["kernel"]]
+    dominant = max(main_k, key=lambda r: r["avg_launch_ms"]) if main_k else None
 
     if rank == 0:
         samples = K * B * world

@@ -1,0 +1,74 @@
+"""HBM bytes per launch of the bench's roofline kernels from two rocprofv3 --pmc passes.
+
+  python tools/pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json
+
+FETCH_DIR / WRITE_DIR hold run_counter_collection.csv of `--pmc FETCH_SIZE` and `--pmc WRITE_SIZE`
+runs of `bench.py --no-graph` (separate passes: FETCH_SIZE takes 3 of the 4 TCC slots).
+Corrections (MI355X_MICROARCH.md, HBM section): the counters are KiB; on gfx950 FETCH_SIZE
+reports half the bytes of a 16-B-per-lane read (every read of these kernels is one), so it is
+doubled; WRITE_SIZE is exact for 16-B stores.  Per kernel the median over the steady dispatches
+is kept (the first dispatch of a run is a cold step).
+"""
+import csv
+import json
+import statistics
+import sys
+
+# probe name (bench.py) -> (kernel-name substring, grid size in threads or None, pick)
+# pick "max": of several dispatches with the same name and grid per step, the ones whose FETCH
+# is at least half the largest (MLP layer 1 forward shares its grid with MLP layer 2's dgrad)
+KERNELS = {
+    "fields_fwd": ("fields_fwd_kernel<128", None, None),
+    "adam_catchup": ("adam_catchup_kernel<128", "!65536", None),   # claimed rows (the window runs on 256 WGs)
+    "adam_window": ("adam_catchup_kernel<128", "65536", None),
+    "gemm_mlp0": ("gemm_dma16_kernel<64, 64, false, false", "262144", "max"),
+    "adam_touched": ("adam_touched_kernel<128", None, None),
+}
+
+
+def load(d, counter):
+    rows = []
+    for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
+        if r["Counter_Name"] == counter:
+            rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"], r["Grid_Size"], float(r["Counter_Value"])))
+    return sorted(rows)
+
+
+def select(rows, sub, grid):
+    out = []
+    for _, name, g, val in rows:
+        if sub not in name:
+            continue
+        if grid is not None and (g == grid[1:] if grid.startswith("!") else g != grid):
+            continue
+        out.append(val)
+    return out
+
+
+def main():
+    fdir, wdir, outp = sys.argv[1:4]
+    fr, wr = load(fdir, "FETCH_SIZE"), load(wdir, "WRITE_SIZE")
+    res = {}
+    for key, (sub, grid, pick) in KERNELS.items():
+        f, w = select(fr, sub, grid), select(wr, sub, grid)
+        if not f or not w:
+            continue
+        if pick == "max":
+            mf = max(f)
+            idx = [i for i, v in enumerate(f) if v >= 0.5 * mf]
+            f = [f[i] for i in idx]
+            w = [w[i] for i in idx if i < len(w)]
+        f, w = f[1:] or f, w[1:] or w                      # drop the cold first dispatch
+        fb = 2.0 * statistics.median(f) * 1024.0
+        wb = statistics.median(w) * 1024.0
+        res[key] = {"kernel": sub, "fetch_bytes": round(fb), "write_bytes": round(wb),
+                    "bytes_per_launch": round(fb + wb), "dispatches": len(f),
+                    "note": "FETCH_SIZE KiB x 2 (gfx950 16-B-lane reads) + WRITE_SIZE KiB"}
+    json.dump(res, open(outp, "w"), indent=1)
+    for k, v in res.items():
+        print(f"{k:14s} fetch {v['fetch_bytes'] / 1e6:9.2f} MB  write {v['write_bytes'] / 1e6:9.2f} MB  "
+              f"total {v['bytes_per_launch'] / 1e6:9.2f} MB  (n={v['dispatches']})")
+
+
+if __name__ == "__main__":
+    main()
