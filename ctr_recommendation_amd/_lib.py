@@ -36,13 +36,14 @@ SIGNATURES = {
     "fbn_bn_tile_finalize": (I, [P, I, I, D, P, P, P, P, F, F, I, P]),
     "fbn_bn_colpart_size": (SZ, [I, I]),
     "fbn_row_chunks": (I, [I]),
+    "fbn_bn_bwd_chunks": (I, [I, I]),
     "fbn_bn_bwd_fused": (I, [P, P, P, P, F, P, P, P, P, I, I, D, P, P, P, P, P, P, P, P]),
     "fbn_colsum_partial": (I, [P, I, I, I, P, P]),
     "fbn_sum_jobs": (I, [P, I, P]),
     "fbn_fields_fwd": (I, [P, P, P, P, P, P, P, F, P, I, P, LL, P, P, P, P, P, I, P, P, P, P, I, I, P, P, P, P, P, I, I, I, P]),
     "fbn_fields_bwd_partials_size": (I, [I, I, I]),
     "fbn_fields_bwd_grid": (I, [I, I]),
-    "fbn_fields_bwd": (I, [P, P, P, P, P, P, F, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P, LL, P, P, I, I, I, P]),
+    "fbn_fields_bwd": (I, [P, P, P, P, P, P, F, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P, P, LL, P, P, I, I, I, P]),
     "fbn_pairs_fwd": (I, [P, P, P, P, I, I, I, I, I, P]),
     "fbn_pairs_bwd": (I, [P, P, P, P, P, P, P, I, I, I, I, P]),
     "fbn_bn_workspace_size": (SZ, [I, I]),
@@ -67,11 +68,13 @@ SIGNATURES = {
     "fbn_adam_dense": (I, [P, P, P, P, LL, P, P, P, F, F, F, P, F, P, P, P]),
     "fbn_sparse_fixup": (I, [P, P, P, I, I, LL, I, P, P, P, P, I, I, P]),
     "fbn_sumsq_sparse": (I, [P, P, P, I, I, I, P, P]),
+    "fbn_sparse_fixup_dup": (I, [P, I, P, P, P, I, I, P]),
+    "fbn_sumsq_sparse_norms": (I, [P, P, P, P, I, I, I, P, P]),
     "fbn_adam_table": (I, [P, P, P, LL, I, P, P, P, P, I, P, P, P, F, F, F, I, P]),
     "fbn_adam_touched": (I, [P, P, P, I, P, P, P, P, I, I, P, P, P, F, F, F, P, P]),
     "fbn_adam_catchup": (I, [P, P, P, LL, I, P, I, P, I, I, P, P, P, F, F, F, P]),
     "fbn_adam_flush": (I, [P, P, P, LL, I, P, P, P, F, F, F, P]),
-    "fbn_claim_rows": (I, [P, P, I, I, LL, P, P, P]),
+    "fbn_claim_rows": (I, [P, P, I, I, LL, P, P, P, P]),
     "fbn_pack_extras": (I, [P, P, P, P]),
     "fbn_unpack_extras": (I, [P, P, P, P]),
     "fbn_step_end": (I, [P, P, P, P, P, P]),

@@ -226,6 +226,7 @@ struct FieldBwdArgs {
   // table gradient, mode 0: dense gtab[V][D] (atomics) if gvec == null; otherwise the two
   // per-sample vectors gvec[b][0] = dX3 (item row), gvec[b][1] = dX5/count (each history row)
   float* gtab; float* gvec;
+  double* gnorm;       // optional with gvec: [B][2] sums of squares of the two vectors (clip norm)
   // mode 1: rows written to sendbuf at pos[b][t]
   const int* pos; float* sendbuf;
   long long V;
@@ -411,6 +412,23 @@ __global__ void __launch_bounds__(256) fields_bwd_kernel(FieldBwdArgs p) {
         // sparse mode: plain stores; rows are resolved later through map / slot_row
         *reinterpret_cast<f32x4*>(p.gvec + (size_t)b * 2 * D + 4 * q) = dx[2];
         *reinterpret_cast<f32x4*>(p.gvec + ((size_t)b * 2 + 1) * D + 4 * q) = gh;
+        if (p.gnorm) {
+          double si = 0.0, sh = 0.0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            si += (double)(dx[2][e] * dx[2][e]);
+            sh += (double)(gh[e] * gh[e]);
+          }
+#pragma unroll
+          for (int o = G / 2; o > 0; o >>= 1) {
+            si += __shfl_xor(si, o, 64);
+            sh += __shfl_xor(sh, o, 64);
+          }
+          if (q == 0) {
+            p.gnorm[(size_t)b * 2] = si;
+            p.gnorm[(size_t)b * 2 + 1] = sh;
+          }
+        }
       } else if (MODE == 0) {
         const f32x4 ti = transpose_cols<G>(dx[2], lane);
         const f32x4 th = transpose_cols<G>(gh, lane);
@@ -586,15 +604,16 @@ extern "C" int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, c
                               const int64_t* views, const float* hmm, const float* ln_g, float ln_eps,
                               const float* w1, const float* b1, const float* w2, int R, int n_cate,
                               const float* X, const float* a, const float* cnt, const float* dV, float* dhmm,
-                              short* dhmm16, float* partials, float* const* param_grads, float* gtab, float* gvec, long long V,
-                              const int* pos, float* sendbuf, int B, int L, int D, void* stream) {
+                              short* dhmm16, float* partials, float* const* param_grads, float* gtab, float* gvec,
+                              double* gnorm, long long V, const int* pos, float* sendbuf, int B, int L, int D,
+                              void* stream) {
   if (B <= 0) return FBN_OK;
   if (L < 0 || L > 32 || R < 1 || R > FBN_MAXR) { fbn_set_error("fbn_fields_bwd: bad L/R"); return FBN_ERR_ARG; }
   FieldBwdArgs p;
   p.item_id = item_id; p.item_seq = L > 0 ? item_seq : nullptr; p.likes = likes; p.views = views;
   p.hmm = hmm; p.ln_g = ln_g; p.w1 = w1; p.b1 = b1; p.w2 = w2;
   p.X = X; p.a = a; p.cnt = cnt; p.dV = dV; p.dhmm = dhmm; p.dhmm16 = dhmm16; p.partials = partials;
-  p.gtab = gtab; p.gvec = gvec; p.pos = pos; p.sendbuf = sendbuf;
+  p.gtab = gtab; p.gvec = gvec; p.gnorm = gvec ? gnorm : nullptr; p.pos = pos; p.sendbuf = sendbuf;
   p.V = V; p.B = B; p.L = L; p.R = R; p.n_cate = n_cate; p.ln_eps = ln_eps;
   hipStream_t st = (hipStream_t)stream;
   int rc = pos ? launch_fields_bwd<1>(p, D, st) : launch_fields_bwd<0>(p, D, st);

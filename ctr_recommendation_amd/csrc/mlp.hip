@@ -300,6 +300,55 @@ __global__ void bn_bwd_partial_kernel(BnBwdSrc s, const float* __restrict__ Xpre
   }
 }
 
+// Vectorised partials for the fused backward: 4 columns per lane (256 columns per block), the
+// block's 4 waves take rows r0+w, r0+w+4, ...; f64 accumulation; part[chunk][3][C].
+__global__ void __launch_bounds__(256) bn_bwd_partial4_kernel(BnBwdSrc s, const float* __restrict__ Xpre,
+                                                              const float* __restrict__ mean, int B, int C,
+                                                              int rows_per_chunk, double* __restrict__ part) {
+  __shared__ double red[3][4][256];
+  const int q = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 256 + q * 4;
+  const int r0 = blockIdx.y * rows_per_chunk, r1 = min(B, r0 + rows_per_chunk);
+  double s0[4] = {0.0, 0.0, 0.0, 0.0}, s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  if (c < C) {
+    const f32x4 mu = *reinterpret_cast<const f32x4*>(mean + c);
+    const f32x4 ww = s.G ? (f32x4){0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(s.w + c);
+#pragma unroll 4
+    for (int r = r0 + rl; r < r1; r += 4) {
+      const size_t i = (size_t)r * C + c;
+      const f32x4 h = *reinterpret_cast<const f32x4*>(s.hact + i);
+      const f32x4 x = *reinterpret_cast<const f32x4*>(Xpre + i);
+      f32x4 d;
+      float gv = 0.f;
+      if (s.G) d = *reinterpret_cast<const f32x4*>(s.G + i);
+      else { gv = s.gvec[r]; d = (f32x4){gv * ww[0], gv * ww[1], gv * ww[2], gv * ww[3]}; }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float dy = h[e] > 0.f ? d[e] * s.scale : 0.f;
+        s0[e] += dy;
+        s1[e] += (double)((x[e] - mu[e]) * dy);
+        if (!s.G) s2[e] += (double)(gv * h[e]);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    red[0][rl][q * 4 + e] = s0[e];
+    red[1][rl][q * 4 + e] = s1[e];
+    red[2][rl][q * 4 + e] = s2[e];
+  }
+  __syncthreads();
+  // 768 outputs per block: thread t writes entries t, t+256, t+512 of {sum dy | sum (x-mu)dy | sum gvec*hact}
+  double* pp = part + (size_t)blockIdx.y * 3 * C;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int cc = blockIdx.x * 256 + threadIdx.x;
+    if (cc < C)
+      pp[(size_t)k * C + cc] = red[k][0][threadIdx.x] + red[k][1][threadIdx.x] + red[k][2][threadIdx.x] +
+                               red[k][3][threadIdx.x];
+  }
+}
+
 // red = {sum dy, sum (x-mean) dy, sum gvec*hact} (global sums, [3][C]).
 // coef[c] = {gm = sum dy / N, k = dotp * invstd^2 / N}; dgamma = dotp*invstd, dbeta = sum dy; dw = sum gvec*hact
 __global__ void bn_bwd_finalize_kernel(const double* red, int C, double ntot, const float* invstd, float* coef,
@@ -622,6 +671,16 @@ static int row_chunks(int B) {
   int ch = (B + 127) / 128;
   return ch < 1 ? 1 : (ch > 256 ? 256 : ch);
 }
+// row chunks of the fused BN backward (partial + apply): >= 512 workgroups of 256 columns x
+// rows_per_chunk, at least 16 rows per chunk
+static int bn_bwd_chunks(int B, int C) {
+  const int cg = (C + 255) / 256;
+  int ch = (512 + cg - 1) / cg;
+  const int cap = (B + 15) / 16;
+  if (ch > cap) ch = cap;
+  if (ch > 1024) ch = 1024;
+  return ch < 1 ? 1 : ch;
+}
 
 // c_bf16: c is a bf16 [B][ldc] buffer (bf16 GEMM mode) instead of float
 extern "C" int fbn_pairs_fwd(const float* Vc, const short* Vc16, const float* U, void* c, int B, int D, int ldc,
@@ -652,7 +711,11 @@ extern "C" int fbn_pairs_bwd(const float* dc, const float* Vc, const short* Vc16
 }
 
 // workspace for the BN entry points: chunk partials [nchunk][3][C] doubles + 4*C doubles of scratch
-extern "C" size_t fbn_bn_workspace_size(int B, int C) { return ((size_t)row_chunks(B) * 3 * C + 4 * (size_t)C) * sizeof(double); }
+extern "C" size_t fbn_bn_workspace_size(int B, int C) {
+  const int nch = row_chunks(B) > bn_bwd_chunks(B, C) ? row_chunks(B) : bn_bwd_chunks(B, C);
+  return ((size_t)nch * 3 * C + 4 * (size_t)C) * sizeof(double);
+}
+extern "C" int fbn_bn_bwd_chunks(int B, int C) { return bn_bwd_chunks(B, C); }
 
 // Local column pass over this rank's rows: out_d[c] = sum_b X[b][c]  (mean_d == null)
 //                                       or  out_d[c] = sum_b (X[b][c] - mean_d[c])^2
@@ -894,7 +957,7 @@ extern "C" int fbn_bn_tile_finalize(const float* part, int M, int C, double ntot
   return FBN_OK;
 }
 
-extern "C" size_t fbn_bn_colpart_size(int B, int C) { return (size_t)row_chunks(B) * C * sizeof(float); }
+extern "C" size_t fbn_bn_colpart_size(int B, int C) { return (size_t)bn_bwd_chunks(B, C) * C * sizeof(float); }
 
 extern "C" int fbn_bn_bwd_fused(const float* G, const float* gvec, const float* w, const float* hact, float scale,
                                 const float* Xpre, const float* mean, const float* invstd, const float* gamma, int B,
@@ -904,10 +967,11 @@ extern "C" int fbn_bn_bwd_fused(const float* G, const float* gvec, const float* 
   if (C & 3) { fbn_set_error("fbn_bn_bwd_fused: C % 4"); return FBN_ERR_ARG; }
   hipStream_t st = (hipStream_t)stream;
   BnBwdSrc s{G, gvec, w, hact, scale};
-  const int nch = row_chunks(B), rpc = (B + nch - 1) / nch;
+  const int nch = bn_bwd_chunks(B, C), rpc = (B + nch - 1) / nch;
   double* part = (double*)ws;
   float* coef = (float*)((double*)ws + (size_t)nch * 3 * C + 3 * (size_t)C);
-  hipLaunchKernelGGL(bn_bwd_partial_kernel, dim3(fbn_cdiv(C, 64), nch), dim3(256), 0, st, s, Xpre, mean, B, C, rpc, part);
+  hipLaunchKernelGGL(bn_bwd_partial4_kernel, dim3(fbn_cdiv(C, 256), nch), dim3(256), 0, st, s, Xpre, mean, B, C, rpc,
+                     part);
   hipLaunchKernelGGL(bn_bwd_reduce_finalize_kernel, dim3(fbn_cdiv(C, 4)), dim3(256), 0, st, part, nch, C, ntot, invstd,
                      coef, dgamma, dbeta, dw);
   hipLaunchKernelGGL(bn_bwd_apply4_kernel, dim3(fbn_cdiv(C, 256), nch), dim3(256), 0, st, s, Xpre, mean, invstd, gamma,

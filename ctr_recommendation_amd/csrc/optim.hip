@@ -194,19 +194,77 @@ __global__ void __launch_bounds__(256) sparse_fixup_kernel(const int64_t* __rest
 // Row claiming for the sparse gradient (single GPU): entry e = b*(L+1)+t claims row r if it is
 // the first to touch it.  Run as the first kernel of a step so the untouched-row Adam can start
 // on the side stream before the forward's GEMMs.
+// dup (optional): dup[e] = the entry that claimed e's row when that is not e itself, else -1
+// (a claim never changes within a step, so the value a failed claim observes is final); the
+// fix-up then reads dup coalesced instead of re-resolving every id through the map.
 __global__ void claim_rows_kernel(const int64_t* __restrict__ item, const int64_t* __restrict__ seq, int B, int L,
-                                  long long V, int* __restrict__ map, int* __restrict__ slot_row) {
+                                  long long V, int* __restrict__ map, int* __restrict__ slot_row, int* __restrict__ dup) {
   const long long n = (long long)B * (L + 1);
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
     const long long b = e / (L + 1), t = e - b * (L + 1);
     const long long r = t == 0 ? item[b] : seq[b * L + (t - 1)];
-    if (r <= 0 || r >= V) continue;
-    if (__hip_atomic_load(map + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != -1) continue;
-    int expected = -1;
-    if (__hip_atomic_compare_exchange_strong(map + r, &expected, (int)e, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT))
-      slot_row[e] = (int)r;
+    int owner = -1;
+    if (r > 0 && r < V) {
+      owner = __hip_atomic_load(map + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (owner == -1) {
+        int expected = -1;
+        if (__hip_atomic_compare_exchange_strong(map + r, &expected, (int)e, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+          slot_row[e] = (int)r;
+        else
+          owner = expected;
+      }
+    }
+    if (dup) dup[e] = owner;
   }
+}
+
+// duplicates resolved at claim time (single GPU): extra[dup[e]] += vec(e), claimer flagged
+template <int D>
+__global__ void __launch_bounds__(256) sparse_fixup_dup_kernel(const int* __restrict__ dup, int n, GradSrc s) {
+  constexpr int G = D / 4, RPW = 64 / G;
+  const int lane = threadIdx.x & 63, q = lane % G;
+  const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+  for (long long e0 = gw * RPW; e0 < n; e0 += nw * RPW) {
+    const long long e = e0 + lane / G;
+    const int u = e < n ? dup[e] : -1;
+    if (u < 0) continue;
+    const float* src = grad_base<D>(s, (int)e);
+    if (q == 0) atomicOr(&s.slot_row[u], FBN_SLOT_FLAG);
+    float* dst = s.extra + (size_t)u * D;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) atomicAdd(dst + k * G + q, src[k * G + q]);
+  }
+}
+
+// sum of squares of the table gradient from per-sample vector norms (fbn_fields_bwd's gnorm
+// [B][2]): a claiming entry without duplicates adds its vector's norm; one with duplicates
+// (FLAG) sums vector + extra explicitly.  One thread per entry, coalesced slot_row reads.
+template <int D>
+__global__ void __launch_bounds__(256) sumsq_norms_kernel(GradSrc s, const double* __restrict__ gnorm, int n,
+                                                          double* __restrict__ out) {
+  __shared__ double red[4];
+  double acc = 0.0;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const int sr = s.slot_row[e];
+    if (sr == -1) continue;
+    const int b = (int)(e / s.Lp1), t = (int)(e - (long long)b * s.Lp1);
+    if (!(sr & FBN_SLOT_FLAG)) {
+      acc += gnorm[(size_t)b * 2 + (t ? 1 : 0)];
+    } else {
+      const float* v = grad_base<D>(s, (int)e);
+      const float* x = s.extra + (size_t)e * D;
+      for (int k = 0; k < D; ++k) {
+        const float y = v[k] + x[k];
+        acc += (double)(y * y);
+      }
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out + (blockIdx.x & (FBN_SUMSQ_SLOTS - 1)), (red[0] + red[1]) + (red[2] + red[3]));
 }
 
 // sum of squares of the clipped-to-be table gradient, over claiming entries only
@@ -563,6 +621,32 @@ extern "C" int fbn_sparse_fixup(const int64_t* item, const int64_t* seq, const i
   return FBN_OK;
 }
 
+// single GPU: the fix-up from claim-time duplicates (fbn_claim_rows' dup), then the table
+// gradient's sum of squares from fbn_fields_bwd's per-sample norms
+extern "C" int fbn_sparse_fixup_dup(const int* dup, int n, const float* gvec, float* extra, int* slot_row, int Lp1,
+                                    int D, void* stream) {
+  if (n <= 0) return FBN_OK;
+  if (!dup || !extra) { fbn_set_error("fbn_sparse_fixup_dup: dup and extra are required"); return FBN_ERR_ARG; }
+  hipStream_t st = (hipStream_t)stream;
+  GradSrc s{gvec, extra, slot_row, Lp1};
+  FBN_DISPATCH_D(sparse_fixup_dup_kernel, D, group_grid(n, D, 4096), dup, n, s);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+extern "C" int fbn_sumsq_sparse_norms(const double* gnorm, const float* gvec, float* extra, int* slot_row, int Lp1,
+                                      int n, int D, double* out, void* stream) {
+  if (n <= 0) return FBN_OK;
+  if (Lp1 < 2) { fbn_set_error("fbn_sumsq_sparse_norms: per-sample vectors only (Lp1 >= 2)"); return FBN_ERR_ARG; }
+  hipStream_t st = (hipStream_t)stream;
+  GradSrc s{gvec, extra, slot_row, Lp1};
+  int blocks = (n + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  FBN_DISPATCH_D(sumsq_norms_kernel, D, dim3(blocks), s, gnorm, n, out);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
 extern "C" int fbn_sumsq_sparse(const float* gvec, float* extra, int* slot_row, int Lp1, int n, int D, double* out,
                                 void* stream) {
   if (n <= 0) return FBN_OK;
@@ -611,13 +695,13 @@ extern "C" int fbn_adam_touched(float* p, float* m, float* v, int D, int* map, c
 }
 
 extern "C" int fbn_claim_rows(const int64_t* item, const int64_t* seq, int B, int L, long long V, int* map,
-                              int* slot_row, void* stream) {
+                              int* slot_row, int* dup, void* stream) {
   const long long n = (long long)B * (L + 1);
   if (n <= 0) return FBN_OK;
   int blocks = (int)((n + 255) / 256);
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(claim_rows_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, item, L > 0 ? seq : nullptr,
-                     B, L, V, map, slot_row);
+                     B, L, V, map, slot_row, dup);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

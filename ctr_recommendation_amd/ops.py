@@ -188,7 +188,7 @@ def bn_backward(G, gvec, w, hact, scale, hpre, mean, invstd, gamma, B, C, ntot, 
     if coll.world <= 1:
         part = None
         if bias_grad is not None:
-            nch = _lib.lib().fbn_row_chunks(B)
+            nch = _lib.lib().fbn_bn_bwd_chunks(B, C)
             part = torch.empty((nch, C), dtype=torch.float32, device=dev)
             sums.add(part, nch, C, bias_grad)
         call("fbn_bn_bwd_fused", ptr(G), ptr(gvec), ptr(w), ptr(hact), float(scale), ptr(hpre), ptr(mean),
@@ -391,6 +391,7 @@ class _SideWork:
 def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict[str, torch.Tensor],
              gout: torch.Tensor, g: Dict[str, torch.Tensor], cfg: FwdConfig, *,
              table_grad: Optional[torch.Tensor] = None, gvec: Optional[torch.Tensor] = None,
+             gnorm: Optional[torch.Tensor] = None,
              pos: Optional[torch.Tensor] = None,
              sendbuf: Optional[torch.Tensor] = None, coll: Collective = NO_COLLECTIVE,
              ntot: Optional[int] = None, extra_sums=(), side: Optional["torch.cuda.Stream"] = None,
@@ -494,7 +495,7 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
          ptr(batch["views_level"]), ptr(a["hmm"]), ptr(p["mm_proj.1.weight"]), LN_EPS,
          ptr(p["senet.excitation.0.weight"]), ptr(p["senet.excitation.0.bias"]), ptr(p["senet.excitation.2.weight"]),
          R, ncate, ptr(a["X"]), ptr(a["a"]), ptr(a["cnt"]), ptr(dV), ptr(dhmm), ptr(dhmm16), ptr(partials), outs,
-         ptr(table_grad), ptr(gvec), V, ptr(pos), ptr(sendbuf), B, Lr, d, st)
+         ptr(table_grad), ptr(gvec), ptr(gnorm), V, ptr(pos), ptr(sendbuf), B, Lr, d, st)
     if evb is not None:
         evb[1].record()
     if bf:

@@ -131,6 +131,9 @@ class FiBiNETTrainer:
         self.slot_row = torch.full((self.n_entries,), -1, **i32)              # entry -> claimed row
         self.gvec = torch.zeros((self.B, 2, d), dtype=torch.float32, device=dev) if world == 1 else None
         self.extra = torch.zeros((self.n_entries, d), dtype=torch.float32, device=dev) if world == 1 else None
+        # single GPU: claim-time duplicate list (entry -> claiming entry) and per-sample gradient norms
+        self.dup = torch.full((self.n_entries,), -1, **i32) if world == 1 else None
+        self.gnorm = torch.zeros((self.B, 2), dtype=torch.float64, device=dev) if world == 1 else None
         # ---------------- optimizer schedule + device step state
         self.total_steps = total_steps
         tab, self.lrs = adam_table(total_steps, self.lr, self.beta2, OneCycle(total_steps, self.lr))
@@ -222,7 +225,7 @@ class FiBiNETTrainer:
             pos = self.xchg.cur_pos
         else:
             call("fbn_claim_rows", ptr(batch["item_id"]), ptr(seq) if L else None, B, L, self.V, ptr(self.map),
-                 ptr(self.slot_row), st)
+                 ptr(self.slot_row), ptr(self.dup), st)
             if lazy:
                 catch_up(B * (L + 1))
         a = ops.forward(self.p, batch, cfg, self.rng, table_rows=rows, pos=pos, err=self.err, labels=labels,
@@ -231,14 +234,15 @@ class FiBiNETTrainer:
                         after_gather=None if lazy else start_untouched_adam)
         sendbuf = self.xchg.make_sendbuf() if self.xchg is not None else None
         ops.backward(self.p, batch, a, a["gout"], self.g, cfg, gvec=self.gvec if self.xchg is None else None,
+                     gnorm=self.gnorm if self.xchg is None else None,
                      pos=pos, sendbuf=sendbuf, coll=self.coll, ntot=ntot,
                      extra_sums=[(a["loss_terms"], B, 1, self.loss, 1.0 / ntot)], probe=probe)
         if self.xchg is None:
             # single GPU: per-sample vectors; entry e = b*(L+1)+t; duplicates -> extra[claimer]
             gsrc = (self.gvec, self.extra, L + 1)
             n_ent = B * (L + 1)
-            call("fbn_sparse_fixup", ptr(batch["item_id"]), ptr(seq) if L else None, None, n_ent, L, self.V, 0,
-                 ptr(self.map), ptr(self.gvec), ptr(self.extra), ptr(self.slot_row), L + 1, d, st)
+            call("fbn_sparse_fixup_dup", ptr(self.dup), n_ent, ptr(self.gvec), ptr(self.extra), ptr(self.slot_row),
+                 L + 1, d, st)
         else:
             grows = self.xchg.backward(sendbuf)              # owner: one received row per entry
             n_ent = grows.shape[0]
@@ -247,7 +251,12 @@ class FiBiNETTrainer:
                  ptr(grows), None, ptr(self.slot_row), 1, d, st)
         # clip_grad_norm_(10): dense grads (identical on every rank) + disjoint table shards
         tab_acc = self.sumsq_tab if self.world > 1 else self.sumsq
-        call("fbn_sumsq_sparse", ptr(gsrc[0]), ptr(gsrc[1]), ptr(self.slot_row), gsrc[2], n_ent, d, ptr(tab_acc), st)
+        if self.xchg is None and L > 0:
+            call("fbn_sumsq_sparse_norms", ptr(self.gnorm), ptr(gsrc[0]), ptr(gsrc[1]), ptr(self.slot_row), gsrc[2],
+                 n_ent, d, ptr(tab_acc), st)
+        else:
+            call("fbn_sumsq_sparse", ptr(gsrc[0]), ptr(gsrc[1]), ptr(self.slot_row), gsrc[2], n_ent, d, ptr(tab_acc),
+                 st)
         if self.world > 1:
             # ONE all-reduce: dense grads + the loss + this shard's table-gradient sumsq
             o = self.n_dense

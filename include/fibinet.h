@@ -84,8 +84,10 @@ int fbn_fields_bwd_grid(int B, int D);
 int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes, const int64_t* views,
                    const float* hmm, const float* ln_g, float ln_eps, const float* w1, const float* b1, const float* w2,
                    int R, int n_cate, const float* X, const float* a, const float* cnt, const float* dV, float* dhmm,
-                   short* dhmm16, float* partials, float* const* param_grads, float* gtab, float* gvec, long long V, const int* pos,
-                   float* sendbuf, int B, int L, int D, void* stream);
+                   short* dhmm16, float* partials, float* const* param_grads, float* gtab, float* gvec,
+                   double* gnorm, long long V, const int* pos, float* sendbuf, int B, int L, int D, void* stream);
+/* gnorm (optional, with gvec): [B][2] float64 sums of squares of the two per-sample vectors,
+ * read by fbn_sumsq_sparse_norms for the clip_grad_norm_ total (src/train_fibinet.py:119). */
 
 /* ---------------------------------------------------------------- K5 bilinear pair products
  * Replaces the pair loop + stack + cat of src/model_fibinet.py:75-79,89,191-194 ("all", mode 0)
@@ -139,6 +141,8 @@ int fbn_bn_bwd(const float* G, const float* gvec, const float* w, const float* h
  * the partials of the preceding Linear's bias gradient (finalised by fbn_sum_jobs). */
 size_t fbn_bn_colpart_size(int B, int C);
 int fbn_row_chunks(int B);
+/* row chunks of fbn_bn_bwd_fused (its colpart is [fbn_bn_bwd_chunks(B, C)][C]) */
+int fbn_bn_bwd_chunks(int B, int C);
 int fbn_bn_bwd_fused(const float* G, const float* gvec, const float* w, const float* hact, float scale,
                      const float* Xpre, const float* mean, const float* invstd, const float* gamma, int B, int C,
                      double ntot, float* dXpre, short* dXpre16, float* dgamma, float* dbeta, float* dw,
@@ -186,6 +190,13 @@ int fbn_sparse_fixup(const int64_t* item, const int64_t* seq, const int* ids, in
                      const int* map, const float* gvec, float* extra, int* slot_row, int Lp1, int D, void* stream);
 int fbn_sumsq_sparse(const float* gvec, float* extra, int* slot_row, int Lp1, int n, int D, double* out,
                      void* stream);
+/* Single-GPU fast forms: fixup from the claim-time duplicate list dup[n] of fbn_claim_rows (no
+ * id re-resolution through map), and the table-gradient sum of squares from fbn_fields_bwd's
+ * per-sample norms gnorm[B][2] (vectors re-read only for rows with duplicates). */
+int fbn_sparse_fixup_dup(const int* dup, int n, const float* gvec, float* extra, int* slot_row, int Lp1, int D,
+                         void* stream);
+int fbn_sumsq_sparse_norms(const double* gnorm, const float* gvec, float* extra, int* slot_row, int Lp1, int n, int D,
+                           double* out, void* stream);
 /* adam_table mode 0: every row (touched rows read their gradient through map); mode 1: only the
  * rows the batch did not touch -- their gradient is 0, so the update is independent of the
  * backward and the clip coefficient and runs on a side stream concurrently with the backward;
@@ -215,8 +226,10 @@ int fbn_adam_flush(float* p, float* m, float* v, long long nrows, int D, int* la
  * fbn_step_end zeroes them.  fbn_claim_rows registers the rows of a batch in map/slot_row (the
  * same claims fbn_fields_fwd makes when given a map), as a tiny kernel at the start of a step. */
 #define FBN_SUMSQ_SLOTS 64
+/* dup (optional, [B*(L+1)]): the claiming entry of each entry's row when another entry claimed
+ * it, else -1 (input of fbn_sparse_fixup_dup). */
 int fbn_claim_rows(const int64_t* item, const int64_t* seq, int B, int L, long long V, int* map, int* slot_row,
-                   void* stream);
+                   int* dup, void* stream);
 /* Multi-GPU: pack {loss, this rank's table-gradient sumsq (slots zeroed)} into the two floats
  * appended to the dense-gradient all-reduce buffer; unpack after it (sumsq[0] += table norms). */
 int fbn_pack_extras(const float* loss, double* tab_slots, float* out, void* stream);
