@@ -248,10 +248,14 @@ def main():
     traffic = _pmc_traffic()
     add("fields_fwd", "fields_fwd (fused gather + history mean + LN + SENET)", avg_ms("fields_fwd"),
         gather_bytes_per_sample(d) * B, "GB/s", HBM_PEAK_GBS, "hbm", "SURVEY 8(d) 12,984 B/sample x batch")
-    # the probed launch is the claimed-row pass only (the rolling window runs on the side stream)
+    # the probed launch is the claimed-row pass only (the rolling window runs on the side stream);
+    # with deferred table gradients it also reads each row's pending gradient vector (4 B x d) and
+    # its pend entry (+8 B)
+    dfr = getattr(tr, "deferred", False)
     add("adam_catchup", "adam_catchup (lazy table Adam: rows claimed this step)", avg_ms("adam_catchup"),
-        catchup_bytes(touched, d, B * (L + 1)), "GB/s", HBM_PEAK_GBS, "hbm",
-        f"touched {touched} rows x (24 B x d + 8 B) + 4 B per entry")
+        catchup_bytes(touched, d, B * (L + 1)) + (touched * (4 * d + 8) if dfr else 0), "GB/s", HBM_PEAK_GBS, "hbm",
+        f"touched {touched} rows x (24 B x d + 8 B{' + 4 B x d + 8 B deferred gradient' if dfr else ''}) "
+        f"+ 4 B per entry")
     add("adam_window", "adam_catchup (lazy table Adam: rolling window, side stream)", avg_ms("adam_window"),
         catchup_bytes(window, d, 0), "GB/s", HBM_PEAK_GBS, "hbm",
         f"window {window} rows x (24 B x d + 8 B); VALU-bound replay of up to F steps per row")

@@ -30,6 +30,7 @@ SIGNATURES = {
     "fbn_device_ok": (I, []),
     "fbn_gemm_workspace_size": (SZ, [I, I, I, I]),
     "fbn_gemm": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, F, I, I, I, P, P, SZ, P]),
+    "fbn_gemm_split": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, P, P, SZ, P, I, I, P, I, I, P]),
     "fbn_bn_tile_stats": (I, [P, I, I, P, P, P]),
     "fbn_bn_tile_moments": (I, [P, I, I, P, P]),
     "fbn_bn_moments_finalize": (I, [P, D, I, P, P, P, P, F, F, I, P]),
@@ -43,7 +44,8 @@ SIGNATURES = {
     "fbn_fields_fwd": (I, [P, P, P, P, P, P, P, F, P, I, P, LL, P, P, P, P, P, I, P, P, P, P, I, I, P, P, P, P, P, I, I, I, P]),
     "fbn_fields_bwd_partials_size": (I, [I, I, I]),
     "fbn_fields_bwd_grid": (I, [I, I]),
-    "fbn_fields_bwd": (I, [P, P, P, P, P, P, F, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P, P, LL, P, P, I, I, I, P]),
+    "fbn_fields_bwd": (I, [P, P, P, P, P, P, P, F, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P, P, P, LL, P, P, I, I,
+                           I, P]),
     "fbn_pairs_fwd": (I, [P, P, P, P, I, I, I, I, I, P]),
     "fbn_pairs_bwd": (I, [P, P, P, P, P, P, P, I, I, I, I, P]),
     "fbn_bn_workspace_size": (SZ, [I, I]),
@@ -72,8 +74,10 @@ SIGNATURES = {
     "fbn_sumsq_sparse_norms": (I, [P, P, P, P, I, I, I, P, P]),
     "fbn_adam_table": (I, [P, P, P, LL, I, P, P, P, P, I, P, P, P, F, F, F, I, P]),
     "fbn_adam_touched": (I, [P, P, P, I, P, P, P, P, I, I, P, P, P, F, F, F, P, P]),
-    "fbn_adam_catchup": (I, [P, P, P, LL, I, P, I, P, I, I, P, P, P, F, F, F, P]),
-    "fbn_adam_flush": (I, [P, P, P, LL, I, P, P, P, F, F, F, P]),
+    "fbn_adam_catchup": (I, [P, P, P, LL, I, P, I, P, I, I, P, P, P, F, F, F, P, P, P, LL, I, P]),
+    "fbn_adam_flush": (I, [P, P, P, LL, I, P, P, P, F, F, F, P, P, P, LL, I, P]),
+    "fbn_adam_selftest": (I, [I, ctypes.c_uint, P, P]),
+    "fbn_adam_commit": (I, [P, P, P, I, P, P, P, P, I, I, P, P, P, F, F, F, P, P, P, P, I, I, P]),
     "fbn_claim_rows": (I, [P, P, I, I, LL, P, P, P, P]),
     "fbn_pack_extras": (I, [P, P, P, P]),
     "fbn_unpack_extras": (I, [P, P, P, P]),

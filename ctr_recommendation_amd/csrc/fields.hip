@@ -36,10 +36,12 @@ struct FieldArgs {
   const float* table;       // mode 0: [V][D] rows; mode 1: exchanged row buffer
   const int* pos;           // mode 1: [B][L+1] row index into `table` (-1 = none)
   const float* w1; const float* b1; const float* w2; const float* b2;  // SENET [R][6],[R],[6][R],[6]
-  float* X;                 // [B][5][D] fields 1..5 (pre-SENET)
+  float* X;                 // [B][2][D] fields 3 and 5 (item row, history mean); the backward
+                            // recomputes fields 1, 2 (cate rows) and 4 (LN of hmm) bit-identically
   float* Vc;                // [B][5][D] fields 1..5 (post-SENET)
   short* Vc16;              // optional bf16 copy of Vc (GEMM operand of the bilinear U = V W and its wgrad)
-  void* c;                  // [B][ldc] float or bf16 (c16); cols [0,5D) <- Vc (MLP input, compact layout)
+  void* c;                  // [B][ldc] float or bf16 (c16); cols [0,5D) <- Vc (MLP input, compact layout);
+                            // null: not written (the bf16 GEMMs read those columns from Vc16)
   float* a_out;             // [B][6]
   float* cnt_out;           // [B]
   int* err;                 // id range violations (sticky flag)
@@ -59,6 +61,24 @@ __device__ __forceinline__ void map_claim(int* map, int* slot_row, int r, int e)
   if (__hip_atomic_compare_exchange_strong(map + r, &expected, e, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT))
     slot_row[e] = r;
+}
+
+// field 4 = ReLU(LayerNorm(h)) for this lane's 4 columns; shared by the forward and the
+// backward's recompute so both run the same operations (bit-identical)
+template <int G>
+__device__ __forceinline__ f32x4 ln_relu(const f32x4& h, const float* ln_g, const float* ln_b, float eps, int q) {
+  constexpr int D = 4 * G;
+  const float s1 = group_sum<G>(h[0] + h[1] + h[2] + h[3]);
+  const float mean = s1 / (float)D;
+  const f32x4 dh = h - mean;
+  const float s2 = group_sum<G>(dh[0] * dh[0] + dh[1] * dh[1] + dh[2] * dh[2] + dh[3] * dh[3]);
+  const float rstd = 1.f / sqrtf(s2 / (float)D + eps);
+  const f32x4 g4 = *reinterpret_cast<const f32x4*>(ln_g + 4 * q);
+  const f32x4 bb4 = *reinterpret_cast<const f32x4*>(ln_b + 4 * q);
+  f32x4 x4;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) x4[e] = fmaxf(dh[e] * rstd * g4[e] + bb4[e], 0.f);
+  return x4;
 }
 
 template <int D>
@@ -161,16 +181,7 @@ __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
     f32x4 x5 = hs / cnt;
 
     // ---------------- mm field: LayerNorm(eps) + ReLU
-    float s1 = group_sum<G>(h[0] + h[1] + h[2] + h[3]);
-    const float mean = s1 / (float)D;
-    f32x4 dh = h - mean;
-    float s2 = group_sum<G>(dh[0] * dh[0] + dh[1] * dh[1] + dh[2] * dh[2] + dh[3] * dh[3]);
-    const float rstd = 1.f / sqrtf(s2 / (float)D + p.ln_eps);
-    const f32x4 g4 = *reinterpret_cast<const f32x4*>(p.ln_g + 4 * q);
-    const f32x4 bb4 = *reinterpret_cast<const f32x4*>(p.ln_b + 4 * q);
-    f32x4 x4;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) x4[e] = fmaxf(dh[e] * rstd * g4[e] + bb4[e], 0.f);
+    const f32x4 x4 = ln_relu<G>(h, p.ln_g, p.ln_b, p.ln_eps, q);
 
     // ---------------- SENET
     const f32x4 xs[5] = {c1, c2, rit, x4, x5};
@@ -182,18 +193,19 @@ __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
     senet_excite<D>(z, p.w1, p.b1, p.w2, p.b2, p.R, qv, a);
 
     // ---------------- stores
-    float* Xb = p.X + (size_t)b * 5 * D + 4 * q;
+    float* Xb = p.X + (size_t)b * 2 * D + 4 * q;
+    *reinterpret_cast<f32x4*>(Xb) = rit;
+    *reinterpret_cast<f32x4*>(Xb + D) = x5;
     float* Vb = p.Vc ? p.Vc + (size_t)b * 5 * D + 4 * q : nullptr;
-    float* cb = p.c16 ? nullptr : (float*)p.c + (size_t)b * p.ldc + 4 * q;
-    short* cb16 = p.c16 ? (short*)p.c + (size_t)b * p.ldc + 4 * q : nullptr;
+    float* cb = (p.c && !p.c16) ? (float*)p.c + (size_t)b * p.ldc + 4 * q : nullptr;
+    short* cb16 = (p.c && p.c16) ? (short*)p.c + (size_t)b * p.ldc + 4 * q : nullptr;
 #pragma unroll
     for (int f = 0; f < 5; ++f) {
       const f32x4 v = xs[f] * a[f + 1];
-      *reinterpret_cast<f32x4*>(Xb + f * D) = xs[f];
       if (p.Vc) *reinterpret_cast<f32x4*>(Vb + f * D) = v;   // bf16 mode: only the bf16 copies
       const bf16x4 v16 = (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
       if (cb16) *reinterpret_cast<bf16x4*>(cb16 + f * D) = v16;
-      else *reinterpret_cast<f32x4*>(cb + f * D) = v;
+      else if (cb) *reinterpret_cast<f32x4*>(cb + f * D) = v;
       if (p.Vc16) *reinterpret_cast<bf16x4*>(p.Vc16 + ((size_t)b * 5 + f) * D + 4 * q) = v16;
     }
 #pragma unroll
@@ -216,7 +228,9 @@ struct FieldBwdArgs {
   const int64_t* item_id; const int64_t* item_seq; const int64_t* likes; const int64_t* views;
   const float* hmm; const float* ln_g;
   const float* w1; const float* b1; const float* w2;
-  const float* X;      // [B][5][D]
+  const float* X;      // [B][2][D] fields 3, 5 (fields 1, 2, 4 are recomputed)
+  const float* cate;   // [n_cate][D] (field 1, 2 recompute)
+  const float* ln_b;   // [D] (field 4 recompute)
   const float* a;      // [B][6]
   const float* cnt;    // [B]
   const float* dV;     // [B][5][D] total gradient wrt V_1..V_5
@@ -300,17 +314,21 @@ __global__ void __launch_bounds__(256) fields_bwd_kernel(FieldBwdArgs p) {
     f32x4 dx0 = {0.f, 0.f, 0.f, 0.f}, dx1 = {0.f, 0.f, 0.f, 0.f};
     long long lk = -1, vw = -1;
     if (live) {
-      const float* Xb = p.X + (size_t)b * 5 * D + 4 * q;
+      const float* Xb = p.X + (size_t)b * 2 * D + 4 * q;
       const float* dVb = p.dV + (size_t)b * 5 * D + 4 * q;
       f32x4 x[5], dv[5];
-#pragma unroll
-      for (int f = 0; f < 5; ++f) {
-        x[f] = *reinterpret_cast<const f32x4*>(Xb + f * D);
-        dv[f] = *reinterpret_cast<const f32x4*>(dVb + f * D);
-      }
-      const f32x4 h = *reinterpret_cast<const f32x4*>(p.hmm + (size_t)b * D + 4 * q);
       lk = p.likes[b];
       vw = p.views[b];
+      // fields 1, 2 as the forward read them (an out-of-range id read row 0 and raised the flag)
+      const long long lkc = (lk >= 0 && lk < p.n_cate) ? lk : 0, vwc = (vw >= 0 && vw < p.n_cate) ? vw : 0;
+      x[0] = *reinterpret_cast<const f32x4*>(p.cate + lkc * D + 4 * q);
+      x[1] = *reinterpret_cast<const f32x4*>(p.cate + vwc * D + 4 * q);
+      x[2] = *reinterpret_cast<const f32x4*>(Xb);
+      x[4] = *reinterpret_cast<const f32x4*>(Xb + D);
+#pragma unroll
+      for (int f = 0; f < 5; ++f) dv[f] = *reinterpret_cast<const f32x4*>(dVb + f * D);
+      const f32x4 h = *reinterpret_cast<const f32x4*>(p.hmm + (size_t)b * D + 4 * q);
+      x[3] = ln_relu<G>(h, p.ln_g, p.ln_b, p.ln_eps, q);
       float a[6];
 #pragma unroll
       for (int f = 0; f < 6; ++f) a[f] = p.a[(size_t)b * 6 + f];
@@ -601,9 +619,9 @@ static int launch_fields_bwd(const FieldBwdArgs& a, int D, hipStream_t st) {
 // partials: [fbn_fields_bwd_grid(B,D)][P] scratch; param_grads: host array of 7 device
 // pointers receiving the gradients of w1, b1, w2, b2, ln_g, ln_b, cate.
 extern "C" int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes,
-                              const int64_t* views, const float* hmm, const float* ln_g, float ln_eps,
-                              const float* w1, const float* b1, const float* w2, int R, int n_cate,
-                              const float* X, const float* a, const float* cnt, const float* dV, float* dhmm,
+                              const int64_t* views, const float* hmm, const float* ln_g, const float* ln_b,
+                              float ln_eps, const float* w1, const float* b1, const float* w2, int R, int n_cate,
+                              const float* cate, const float* X, const float* a, const float* cnt, const float* dV, float* dhmm,
                               short* dhmm16, float* partials, float* const* param_grads, float* gtab, float* gvec,
                               double* gnorm, long long V, const int* pos, float* sendbuf, int B, int L, int D,
                               void* stream) {
@@ -611,7 +629,7 @@ extern "C" int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, c
   if (L < 0 || L > 32 || R < 1 || R > FBN_MAXR) { fbn_set_error("fbn_fields_bwd: bad L/R"); return FBN_ERR_ARG; }
   FieldBwdArgs p;
   p.item_id = item_id; p.item_seq = L > 0 ? item_seq : nullptr; p.likes = likes; p.views = views;
-  p.hmm = hmm; p.ln_g = ln_g; p.w1 = w1; p.b1 = b1; p.w2 = w2;
+  p.hmm = hmm; p.ln_g = ln_g; p.ln_b = ln_b; p.w1 = w1; p.b1 = b1; p.w2 = w2; p.cate = cate;
   p.X = X; p.a = a; p.cnt = cnt; p.dV = dV; p.dhmm = dhmm; p.dhmm16 = dhmm16; p.partials = partials;
   p.gtab = gtab; p.gvec = gvec; p.gnorm = gvec ? gnorm : nullptr; p.pos = pos; p.sendbuf = sendbuf;
   p.V = V; p.B = B; p.L = L; p.R = R; p.n_cate = n_cate; p.ln_eps = ln_eps;

@@ -50,6 +50,12 @@ struct GemmArgs {
   int kchunk;   // K range per split (multiple of BK)
   float* ws;    // split-K slabs [split][M][N]
   float* stats; // optional [ceil(M/BM)][N][2]: per-tile column (sum, M2 about the tile mean) of C
+  // split operands (LDS-DMA kernel only): a k-contiguous A is [A | A2] along K (A(m,k) for k >= kseg
+  // at A2[m*lda2 + k - kseg]); a k-major B is [B | B2] along N (B(k,n) for n >= nseg at
+  // B2[k*ldb2 + n - nseg]).  kseg / nseg are multiples of the tile and BK; INT_MAX = unused.
+  const void* A2;
+  const void* B2;
+  int lda2, kseg, ldb2, nseg;
 };
 
 template <bool BF16> struct GemmTraits;
@@ -515,22 +521,33 @@ __global__ void __launch_bounds__(256) gemm_dma16_kernel(GemmArgs g, int tiles_n
   // (rows / columns past M or N are clamped to valid memory: their products land only in C
   // entries that are not stored)
   const short* src[GPW];
+  const short* src2[GPW];   // split A ([A | A2] along K): the same lane's chunk in A2, k rebased to kseg
   long long adv[GPW];
+  const int t2 = kbeg < g.kseg ? (g.kseg - kbeg) / BK : 0;   // first K-step read from A2
 #pragma unroll
   for (int j = 0; j < GPW; ++j) {
     const int grp = wave * GPW + j;
     const bool isA = grp < BM / 8;
     const int off = (isA ? grp : grp - BM / 8) * 1024 + lane * 16;   // byte offset inside the operand image
     const short* P = reinterpret_cast<const short*>(isA ? g.A : g.B);
-    const int ld = isA ? g.lda : g.ldb, lim = isA ? g.M : g.N, base = isA ? m0 : n0;
+    int ld = isA ? g.lda : g.ldb, lim = isA ? g.M : g.N, base = isA ? m0 : n0;
     const bool km = isA ? AKM : BKM;
     const int rows = isA ? BM : BN;
+    src2[j] = nullptr;
     if (!km) {
       const int r = off >> 7, slot = (off >> 4) & 7;
       const int row = min(base + r, lim - 1);
-      src[j] = P + (size_t)row * ld + kbeg + ((slot ^ ((r >> 1) & 7)) << 3);
+      const int sw = (slot ^ ((r >> 1) & 7)) << 3;
+      src[j] = P + (size_t)row * ld + kbeg + sw;
+      if (isA && g.A2) src2[j] = reinterpret_cast<const short*>(g.A2) + (size_t)row * g.lda2 + (kbeg - g.kseg) + sw;
       adv[j] = BK;
     } else {
+      if (!isA && g.B2 && n0 >= g.nseg) {   // this tile's columns lie in B2 (nseg is a multiple of BN)
+        P = reinterpret_cast<const short*>(g.B2);
+        ld = g.ldb2;
+        lim -= g.nseg;
+        base -= g.nseg;
+      }
       const int RB = rows * 2;
       const int k = off / RB, slot = (off % RB) >> 4;
       const int f = RB == 128 ? (((k >> 1) & 1) << 2) : ((k & 3) << 2);
@@ -542,9 +559,11 @@ __global__ void __launch_bounds__(256) gemm_dma16_kernel(GemmArgs g, int tiles_n
   }
   auto issue = [&](int t, int buf) {
 #pragma unroll
-    for (int j = 0; j < GPW; ++j)
-      __builtin_amdgcn_global_load_lds((g_void*)(src[j] + t * adv[j]), (l_void*)(smem + buf * STAGE + (wave * GPW + j) * 1024),
+    for (int j = 0; j < GPW; ++j) {
+      const short* s0 = (src2[j] && t >= t2) ? src2[j] : src[j];
+      __builtin_amdgcn_global_load_lds((g_void*)(s0 + t * adv[j]), (l_void*)(smem + buf * STAGE + (wave * GPW + j) * 1024),
                                        16, 0, 0);
+    }
   };
 
   f32x16 acc[TM][TN];
@@ -790,10 +809,42 @@ extern "C" size_t fbn_gemm_workspace_size(int M, int N, int K, int bf16) {
 // a16 / b16: the A / B operand is bf16 in memory (requires bf16 = 1, ld % 8 == 0 and no rB remap)
 // stats: optional [ceil(M/64)][N][2] per-64-row-tile column (sum, M2) of C, from the MFMA epilogue (split == 1,
 //        64-row tiles) or the split-K reduce; C is bit-identical with or without stats
+static int gemm_impl(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, int lda,
+                     int ldb, int ldc, int transA, int transB, int rB_seg, int rB_off0, int rB_off1, int rC_seg,
+                     int rC_off0, int rC_off1, float beta, int bf16, int a16, int b16, float* stats, float* ws,
+                     size_t ws_bytes, const void* A2, int lda2, int kseg, const void* B2, int ldb2, int nseg,
+                     void* stream);
+
 extern "C" int fbn_gemm(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, int lda,
                         int ldb, int ldc, int transA, int transB, int rB_seg, int rB_off0, int rB_off1, int rC_seg,
                         int rC_off0, int rC_off1, float beta, int bf16, int a16, int b16, float* stats, float* ws,
                         size_t ws_bytes, void* stream) {
+  return gemm_impl(A, B, C, bias, M, N, K, lda, ldb, ldc, transA, transB, rB_seg, rB_off0, rB_off1, rC_seg, rC_off0,
+                   rC_off1, beta, bf16, a16, b16, stats, ws, ws_bytes, nullptr, 0, 0x7fffffff, nullptr, 0, 0x7fffffff,
+                   stream);
+}
+
+// Split operands (bf16 LDS-DMA path only): A2/kseg for a k-contiguous A = [A | A2] along K,
+// B2/nseg for a k-major B = [B | B2] along N; kseg, nseg multiples of 128, ld2 % 8 == 0.
+extern "C" int fbn_gemm_split(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, int lda,
+                              int ldb, int ldc, int transA, int transB, int rC_seg, int rC_off0, int rC_off1,
+                              float beta, float* stats, float* ws, size_t ws_bytes, const void* A2, int lda2,
+                              int kseg, const void* B2, int ldb2, int nseg, void* stream) {
+  if ((A2 && (transA || (kseg & 127) || (lda2 & 7) || ((uintptr_t)A2 & 15))) ||
+      (B2 && (transB || (nseg & 127) || (ldb2 & 7) || ((uintptr_t)B2 & 15)))) {
+    fbn_set_error("fbn_gemm_split: A2 needs a k-contiguous A, B2 a k-major B; segments % 128, ld % 8, 16-B aligned");
+    return FBN_ERR_ARG;
+  }
+  return gemm_impl(A, B, C, bias, M, N, K, lda, ldb, ldc, transA, transB, 0x7fffffff, 0, 0, rC_seg, rC_off0, rC_off1,
+                   beta, 1, 1, 1, stats, ws, ws_bytes, A2, lda2, A2 ? kseg : 0x7fffffff, B2, ldb2,
+                   B2 ? nseg : 0x7fffffff, stream);
+}
+
+static int gemm_impl(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, int lda,
+                     int ldb, int ldc, int transA, int transB, int rB_seg, int rB_off0, int rB_off1, int rC_seg,
+                     int rC_off0, int rC_off1, float beta, int bf16, int a16, int b16, float* stats, float* ws,
+                     size_t ws_bytes, const void* A2, int lda2, int kseg, const void* B2, int ldb2, int nseg,
+                     void* stream) {
   if (M <= 0 || N <= 0) return FBN_OK;
   if (!A || !B || !C) { fbn_set_error("fbn_gemm: null operand"); return FBN_ERR_ARG; }
   // 16-B vector loads along the contiguous dimension of every operand
@@ -812,11 +863,17 @@ extern "C" int fbn_gemm(const void* A, const void* B, float* C, const float* bia
   g.rB = {rB_seg, rB_off0, rB_off1};
   g.rC = {rC_seg, rC_off0, rC_off1};
   g.beta = beta;
+  g.A2 = A2; g.lda2 = lda2; g.kseg = kseg;
+  g.B2 = B2; g.ldb2 = ldb2; g.nseg = nseg;
   const int bk = bf16 ? 64 : 32;
   // LDS-DMA path: bf16 operands, K % 64 == 0, 16-B rows; k-major operands need their
   // M / N extent in whole 8-element chunks
   const bool dma16 = bf16 && a16 && b16 && rB_seg == 0x7fffffff && K % 64 == 0 && !(lda & 7) && !(ldb & 7) &&
                      (!transA ? true : !(M & 7)) && (transB ? true : !(N & 7)) && !getenv("FBN_GEMM_NO_DMA16");
+  if ((A2 || B2) && !dma16) {
+    fbn_set_error("fbn_gemm_split: split operands need the bf16 LDS-DMA path (K % 64 == 0, bf16 operands)");
+    return FBN_ERR_ARG;
+  }
   GemmPlan p = dma16 ? plan_dma16(M, N, K) : plan_gemm(M, N, K, bk);
   if (const char* f = getenv("FBN_GEMM_FORCE")) {      // tuning sweeps only: "bm,bn,split"
     int a = 0, b = 0, c = 0;

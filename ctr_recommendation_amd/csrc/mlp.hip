@@ -888,16 +888,44 @@ struct ConvJob {
 };
 struct ConvJobs {
   ConvJob j[8];
+  int tile0[9];   // first 64x64 output tile of each job (prefix sum)
 };
-__global__ void convert_bf16_kernel(ConvJobs jobs) {
-  const ConvJob J = jobs.j[blockIdx.y];
-  const long long n = (long long)J.rows * J.cols;
-  for (long long x = (long long)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += (long long)gridDim.x * blockDim.x) {
-    const int i = (int)(x / J.cols), j = (int)(x % J.cols);
-    const int a = J.trans ? j : i;
-    int b = J.trans ? i : j;
-    b += b < J.seg ? J.off0 : J.off1;
-    J.dst[x] = f2bf(J.src[(size_t)a * J.ld + b]);
+// One 64x64 output tile per workgroup.  A transposed job reads its source tile along the
+// source's contiguous dimension into LDS (coalesced) and writes the output rows from LDS.
+__global__ void __launch_bounds__(256) convert_bf16_kernel(ConvJobs jobs, int njobs) {
+  __shared__ float tile[64][65];
+  int jb = 0;
+  while (jb + 1 < njobs && (int)blockIdx.x >= jobs.tile0[jb + 1]) ++jb;
+  const ConvJob J = jobs.j[jb];
+  const int t = blockIdx.x - jobs.tile0[jb];
+  const int tcols = (J.cols + 63) / 64;
+  const int i0 = (t / tcols) * 64, j0 = (t % tcols) * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  if (!J.trans) {
+    const int j = j0 + tx;
+    if (j < J.cols) {
+      const int b = j + (j < J.seg ? J.off0 : J.off1);
+      for (int r = ty; r < 64; r += 4) {
+        const int i = i0 + r;
+        if (i < J.rows) J.dst[(size_t)i * J.cols + j] = f2bf(J.src[(size_t)i * J.ld + b]);
+      }
+    }
+    return;
+  }
+  // out[i][j] = src[j][rm(i)]: lanes run along i, the source's contiguous dimension
+  {
+    const int i = i0 + tx;
+    const int b = i + (i < J.seg ? J.off0 : J.off1);
+    for (int r = ty; r < 64; r += 4) {
+      const int j = j0 + r;
+      tile[r][tx] = (i < J.rows && j < J.cols) ? J.src[(size_t)j * J.ld + b] : 0.f;
+    }
+  }
+  __syncthreads();
+  const int j = j0 + tx;
+  for (int r = ty; r < 64; r += 4) {
+    const int i = i0 + r;
+    if (i < J.rows && j < J.cols) J.dst[(size_t)i * J.cols + j] = f2bf(tile[tx][r]);
   }
 }
 
@@ -906,8 +934,13 @@ extern "C" int fbn_convert_bf16(const void* jobs, int n, void* stream) {
   if (n <= 0) return FBN_OK;
   if (n > 8) { fbn_set_error("convert_bf16: at most 8 jobs"); return FBN_ERR_ARG; }
   ConvJobs J;
-  for (int i = 0; i < 8; ++i) J.j[i] = ((const ConvJob*)jobs)[i < n ? i : 0];
-  hipLaunchKernelGGL(convert_bf16_kernel, dim3(256, n), dim3(256), 0, (hipStream_t)stream, J);
+  J.tile0[0] = 0;
+  for (int i = 0; i < 8; ++i) {
+    J.j[i] = ((const ConvJob*)jobs)[i < n ? i : 0];
+    J.tile0[i + 1] = J.tile0[i] + (i < n ? fbn_cdiv(J.j[i].rows, 64) * fbn_cdiv(J.j[i].cols, 64) : 0);
+  }
+  if (J.tile0[n] <= 0) return FBN_OK;
+  hipLaunchKernelGGL(convert_bf16_kernel, dim3(J.tile0[n]), dim3(256), 0, (hipStream_t)stream, J, n);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

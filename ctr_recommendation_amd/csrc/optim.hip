@@ -27,7 +27,7 @@ struct AdamConsts {
   float w1;     // 1 - beta1 (as float)
   float nss;    // -lr / bias_correction1 (as float)
   float bc2s;   // sqrt(bias_correction2) (as float)
-  float pad;
+  float pad;    // host: lr (unused on the device); LDS windows: div_recip(bc2s)
 };
 
 // ------------------------------------------------------------------ squared norm partials
@@ -73,6 +73,107 @@ __device__ __forceinline__ float adam_elem(float& p, float& m, float& v, float g
   const float denom = sqrtf(v) / k.bc2s + eps;
   p = p + (k.nss * m) / denom;
   return p;
+}
+
+// ------------------------------------------------------------------ fast exact zero-gradient step
+// The replay of zero-gradient steps (lazy table Adam) is VALU-bound: ~46 instructions per element
+// with the compiler's IEEE f32 division (v_div_scale x2, v_rcp, 6 FMAs, v_div_fmas, v_div_fixup)
+// and correctly rounded sqrt (scaling + two neighbour tests + class fix-up).  adam_zero4 runs the
+// same arithmetic on element pairs with packed f32 ops (v_pk_mul/add/fma_f32) and WITHOUT the
+// range-handling parts of those sequences: v_div_scale / v_div_fmas only rescale and v_div_fixup
+// only rewrites special cases when an operand or the quotient is near the f32 range limits, and
+// the sqrt scaling only applies below 2^-96.  Each pair checks that its operands lie well inside
+// the ranges where those steps are identities ([2^-96, 2^100] for v, [2^-90, 2^50] for the
+// numerator, [2^-40, 2^30] for the denominator; bc2s in (0.03, 1]) and otherwise recomputes with
+// adam_elem -- so every result is bit-identical to adam_elem (tests: the eager-vs-lazy
+// comparison; fbn_adam_selftest on random operands across the f32 range).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// v_rcp + the Newton step of the compiler's f32 division
+__device__ __forceinline__ float div_recip(float b) {
+  const float r = __builtin_amdgcn_rcpf(b);
+  return __builtin_fmaf(__builtin_fmaf(-b, r, 1.f), r, r);
+}
+__device__ __forceinline__ f32x2 div_recip2(f32x2 b) {
+  const f32x2 r = {__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)};
+  return fma2(fma2(-b, r, (f32x2){1.f, 1.f}), r, r);
+}
+// quotient refinement of the compiler's f32 division given its reciprocal r of b
+__device__ __forceinline__ f32x2 div_refine2(f32x2 a, f32x2 b, f32x2 r) {
+  f32x2 q = a * r;
+  q = fma2(fma2(-b, q, a), r, q);
+  return fma2(fma2(-b, q, a), r, q);
+}
+// correctly rounded sqrt (the compiler's neighbour test) for x in [2^-96, 2^100]
+__device__ __forceinline__ f32x2 sqrt2_exact(f32x2 x) {
+  f32x2 s = {__builtin_amdgcn_sqrtf(x.x), __builtin_amdgcn_sqrtf(x.y)};
+  const i32x2 si = __builtin_bit_cast(i32x2, s);
+  const f32x2 sdn = __builtin_bit_cast(f32x2, si - 1), sup = __builtin_bit_cast(f32x2, si + 1);
+  const f32x2 rdn = fma2(-sdn, s, x), rup = fma2(-sup, s, x);
+  s.x = rdn.x <= 0.f ? sdn.x : s.x;
+  s.y = rdn.y <= 0.f ? sdn.y : s.y;
+  s.x = rup.x > 0.f ? sup.x : s.x;
+  s.y = rup.y > 0.f ? sup.y : s.y;
+  return s;
+}
+// Guard: v in [2^-60, 2^10], |nss*m| in [2^-70, 2^0], denom in [2^-40, 2^30] -- well inside the
+// ranges where the skipped steps are identities (sqrt scaling below 2^-96; division scaling when
+// the exponent difference reaches 96, the numerator is below 2^-103 or the quotient denormal).
+// Each range spans 70 binades, so one unsigned max3 + compare tests all three per element.
+#define FBN_G_SPAN 0x23000000u    // 70 binades
+#define FBN_G_V_LO 0x21800000u    // 2^-60
+#define FBN_G_A_LO 0x1c800000u    // 2^-70
+#define FBN_G_D_LO 0x2b800000u    // 2^-40
+__device__ __forceinline__ unsigned guard3(float v, float a, float den) {
+  const unsigned x = __float_as_uint(v) - FBN_G_V_LO, y = (__float_as_uint(a) & 0x7fffffffu) - FBN_G_A_LO;
+  return max(max(x, y), __float_as_uint(den) - FBN_G_D_LO);
+}
+// |x| in [lo, hi] (positive normal bounds) by an unsigned compare on the magnitude bits
+__device__ __forceinline__ bool in_range(float x, unsigned lo, unsigned hi) {
+  return (unsigned)((__float_as_uint(x) & 0x7fffffffu) - lo) <= hi - lo;
+}
+
+// one zero-gradient step (g = 0*1 + wd*p) of 4 elements; rc = div_recip(bc2s).  Both pairs are
+// computed branch-free (the scheduler interleaves their dependency chains), then one guard.
+__device__ __forceinline__ void adam_zero4(f32x4& pp, f32x4& mm, f32x4& vv, float wd, float b2, float omb2, float eps,
+                                           float w1, float nss, float bc2s, float rc) {
+  f32x2 P[2], M1[2], V1[2], Q[2];
+  unsigned g = 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    P[h] = (f32x2){pp[2 * h], pp[2 * h + 1]};
+    const f32x2 M = {mm[2 * h], mm[2 * h + 1]}, Vv = {vv[2 * h], vv[2 * h + 1]};
+    const f32x2 G = wd * P[h];
+    M1[h] = M + w1 * (G - M);
+    V1[h] = Vv * b2;
+    V1[h] = V1[h] + (omb2 * G) * G;
+    const f32x2 X = sqrt2_exact(V1[h]);
+    const f32x2 Den = div_refine2(X, (f32x2){bc2s, bc2s}, (f32x2){rc, rc}) + eps;
+    const f32x2 A = nss * M1[h];
+    Q[h] = div_refine2(A, Den, div_recip2(Den));
+    g = max(g, max(guard3(V1[h].x, A.x, Den.x), guard3(V1[h].y, A.y, Den.y)));
+  }
+  if (__builtin_expect(g <= FBN_G_SPAN, 1)) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x2 P1 = P[h] + Q[h];
+      pp[2 * h] = P1.x; pp[2 * h + 1] = P1.y;
+      mm[2 * h] = M1[h].x; mm[2 * h + 1] = M1[h].y;
+      vv[2 * h] = V1[h].x; vv[2 * h + 1] = V1[h].y;
+    }
+  } else {
+    AdamConsts k;
+    k.w1 = w1; k.nss = nss; k.bc2s = bc2s; k.pad = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float pe = pp[e], me = mm[e], ve = vv[e];
+      adam_elem(pe, me, ve, 0.f, 1.f, wd, b2, omb2, eps, k);
+      pp[e] = pe; mm[e] = me; vv[e] = ve;
+    }
+  }
 }
 
 // clip coefficient of clip_grad_norm_ from the sumsq slots (same sequential order as
@@ -219,50 +320,61 @@ __global__ void claim_rows_kernel(const int64_t* __restrict__ item, const int64_
   }
 }
 
-// duplicates resolved at claim time (single GPU): extra[dup[e]] += vec(e), claimer flagged
+// duplicates resolved at claim time (single GPU): extra[dup[e]] += vec(e), claimer flagged.
+// One entry per lane for the scan; each duplicate (rare) is then added by the whole wave
+// (D/64 consecutive floats per lane: coalesced atomics).
 template <int D>
 __global__ void __launch_bounds__(256) sparse_fixup_dup_kernel(const int* __restrict__ dup, int n, GradSrc s) {
-  constexpr int G = D / 4, RPW = 64 / G;
-  const int lane = threadIdx.x & 63, q = lane % G;
-  const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
-  for (long long e0 = gw * RPW; e0 < n; e0 += nw * RPW) {
-    const long long e = e0 + lane / G;
+  const int lane = threadIdx.x & 63;
+  for (long long e0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) - lane; e0 < n;
+       e0 += (long long)gridDim.x * blockDim.x) {
+    const long long e = e0 + lane;
     const int u = e < n ? dup[e] : -1;
-    if (u < 0) continue;
-    const float* src = grad_base<D>(s, (int)e);
-    if (q == 0) atomicOr(&s.slot_row[u], FBN_SLOT_FLAG);
-    float* dst = s.extra + (size_t)u * D;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) atomicAdd(dst + k * G + q, src[k * G + q]);
+    unsigned long long mask = __ballot(u >= 0);
+    while (mask) {
+      const int l = __ffsll((long long)mask) - 1;
+      mask &= mask - 1;
+      const int ue = __shfl(u, l, 64);
+      const float* src = grad_base<D>(s, (int)(e0 + l));
+      float* dst = s.extra + (size_t)ue * D;
+      if (lane == 0) atomicOr(&s.slot_row[ue], FBN_SLOT_FLAG);
+      for (int k = lane; k < D; k += 64) atomicAdd(dst + k, src[k]);
+    }
   }
 }
 
 // sum of squares of the table gradient from per-sample vector norms (fbn_fields_bwd's gnorm
 // [B][2]): a claiming entry without duplicates adds its vector's norm; one with duplicates
-// (FLAG) sums vector + extra explicitly.  One thread per entry, coalesced slot_row reads.
+// (FLAG, rare) sums vector + extra explicitly, cooperatively across the wave.  One entry per lane.
 template <int D>
 __global__ void __launch_bounds__(256) sumsq_norms_kernel(GradSrc s, const double* __restrict__ gnorm, int n,
                                                           double* __restrict__ out) {
   __shared__ double red[4];
+  const int lane = threadIdx.x & 63;
   double acc = 0.0;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
-    const int sr = s.slot_row[e];
-    if (sr == -1) continue;
-    const int b = (int)(e / s.Lp1), t = (int)(e - (long long)b * s.Lp1);
-    if (!(sr & FBN_SLOT_FLAG)) {
+  for (long long e0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) - lane; e0 < n;
+       e0 += (long long)gridDim.x * blockDim.x) {
+    const long long e = e0 + lane;
+    const int sr = e < n ? s.slot_row[e] : -1;
+    const bool flag = sr != -1 && (sr & FBN_SLOT_FLAG);
+    if (sr != -1 && !flag) {
+      const int b = (int)(e / s.Lp1), t = (int)(e - (long long)b * s.Lp1);
       acc += gnorm[(size_t)b * 2 + (t ? 1 : 0)];
-    } else {
-      const float* v = grad_base<D>(s, (int)e);
-      const float* x = s.extra + (size_t)e * D;
-      for (int k = 0; k < D; ++k) {
+    }
+    unsigned long long mask = __ballot(flag);
+    while (mask) {
+      const int l = __ffsll((long long)mask) - 1;
+      mask &= mask - 1;
+      const float* v = grad_base<D>(s, (int)(e0 + l));
+      const float* x = s.extra + (size_t)(e0 + l) * D;
+      for (int k = lane; k < D; k += 64) {
         const float y = v[k] + x[k];
         acc += (double)(y * y);
       }
     }
   }
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  if (lane == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
   if (threadIdx.x == 0) atomicAdd(out + (blockIdx.x & (FBN_SUMSQ_SLOTS - 1)), (red[0] + red[1]) + (red[2] + red[3]));
 }
@@ -396,6 +508,64 @@ __global__ void __launch_bounds__(256) adam_table_untouched(FBN_ADAM_TABLE_ARGS)
   }
 }
 
+// ------------------------------------------------------------------ self-test of adam_zero4
+// n threads x 4 elements of random (p, m, v) whose exponents span the f32 range (plus zeros,
+// denormals and exact powers of two) under random step constants: adam_zero4 against adam_elem,
+// bit for bit.  mism[0] += mismatching elements, mism[1] += elements that took the fast path.
+__device__ __forceinline__ unsigned st_hash(unsigned x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
+}
+__device__ float st_value(unsigned h, unsigned h2, int lo_exp, int hi_exp, bool sign) {
+  const unsigned kind = h2 & 31;
+  if (kind == 0) return 0.f;
+  if (kind == 1) return __uint_as_float(h & 0x007fffffu);                        // denormal
+  const int ex = lo_exp + (int)(h2 >> 8) % (hi_exp - lo_exp + 1);
+  const unsigned mant = kind == 2 ? 0u : (h & 0x007fffffu);                          // power of two
+  const unsigned bits = ((unsigned)(ex + 127) << 23) | mant | ((sign && (h2 & 64)) ? 0x80000000u : 0u);
+  return __uint_as_float(bits);
+}
+__global__ void adam_selftest_kernel(int n, unsigned seed, unsigned long long* mism) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  unsigned h = st_hash(seed * 0x9E3779B9u + (unsigned)i);
+  AdamConsts k;
+  k.w1 = 0.05f + 0.1f * (float)(st_hash(h + 1) & 0xffff) / 65536.f;
+  k.nss = -1e-4f * (1.f + 200.f * (float)(st_hash(h + 2) & 0xffff) / 65536.f);
+  k.bc2s = 0.0316f + 0.968f * (float)(st_hash(h + 3) & 0xffff) / 65536.f;
+  const float wd = (st_hash(h + 4) & 1) ? 1e-5f : 3e-2f, b2 = 0.999f, omb2 = (float)(1.0 - 0.999), eps = 1e-8f;
+  k.pad = div_recip(k.bc2s);
+  f32x4 p, m, v;
+  for (int e = 0; e < 4; ++e) {
+    const unsigned a = st_hash(h + 10 + 3 * e), b = st_hash(a), c = st_hash(b);
+    p[e] = st_value(a, st_hash(a + 7), -60, 40, true);
+    m[e] = st_value(b, st_hash(b + 7), -80, 20, true);
+    v[e] = fabsf(st_value(c, st_hash(c + 7), -126, 60, false));
+  }
+  f32x4 pf = p, mf = m, vf = v;
+  adam_zero4(pf, mf, vf, wd, b2, omb2, eps, k.w1, k.nss, k.bc2s, k.pad);
+  unsigned long long bad = 0, fast = 0;
+  for (int e = 0; e < 4; ++e) {
+    float pe = p[e], me = m[e], ve = v[e];
+    adam_elem(pe, me, ve, 0.f, 1.f, wd, b2, omb2, eps, k);
+    const bool same = __float_as_uint(pe) == __float_as_uint(pf[e]) && __float_as_uint(me) == __float_as_uint(mf[e]) &&
+                      __float_as_uint(ve) == __float_as_uint(vf[e]);
+    const bool nan_same = pe != pe && pf[e] != pf[e];                 // NaN payloads may differ
+    bad += (same || nan_same) ? 0 : 1;
+    const float a = k.nss * mf[e];
+    fast += guard3(vf[e], a, 1.f) <= FBN_G_SPAN ? 1 : 0;
+  }
+  if (bad) atomicAdd(mism, bad);
+  atomicAdd(mism + 1, fast);
+}
+
+extern "C" int fbn_adam_selftest(int n, unsigned seed, unsigned long long* mism, void* stream) {
+  if (n <= 0) return FBN_OK;
+  hipLaunchKernelGGL(adam_selftest_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, n, seed, mism);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
 // ------------------------------------------------------------------ lazy table Adam (exact)
 // A row whose loss gradient is zero at step s still gets torch's coupled-L2 Adam update
 // (g = 0 * coef + wd * p, then m, v, p).  That update depends only on the row and on step s's
@@ -404,29 +574,57 @@ __global__ void __launch_bounds__(256) adam_table_untouched(FBN_ADAM_TABLE_ARGS)
 // Each step, before the gather reads the table, fbn_adam_catchup brings every row the batch
 // claimed, plus a rolling window of nrows/F rows (window (step mod F)), up to `step`; the rolling
 // window bounds every row's lag by F steps.  fbn_adam_touched then applies the step with the real
-// gradient (last = step + 1).  fbn_adam_flush brings the whole table up to date (checkpoint,
-// evaluation).  The schedule constants of the last W <= FBN_LAZY_MAX_LAG steps sit in LDS.
+// gradient (last = step + 1) -- or, single GPU, fbn_adam_commit DEFERS it: the row records which
+// per-sample gradient vector it received (pend[r]), the step's vectors are kept in a ring of
+// F+1 steps and its clip coefficient in coef_hist, and the next replay of the row applies step
+// last[r] with that gradient before the zero-gradient steps (same operations, same order: still
+// bit-identical to eager Adam), so a touched row is read and written once per visit instead of
+// twice.  fbn_adam_flush brings the whole table up to date (checkpoint, evaluation).  The schedule
+// constants of the last W <= FBN_LAZY_MAX_LAG steps sit in LDS.
 #define FBN_LAZY_MAX_LAG 512
+
+// deferred gradients: pend[r] = index (b*2 + slot) of the per-sample vector row r received at step
+// last[r] (-1 = none); ring[(s % ring_n) * ring_stride + idx * D] holds step s's vectors
+struct PendSrc {
+  int* pend;
+  const float* ring;
+  const float* coef_hist;   // [steps] clip coefficient of each step
+  long long ring_stride;    // floats per ring slot (B * 2 * D)
+  int ring_n;
+};
 
 template <int D>
 __device__ __forceinline__ void replay_rows(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
                                             long long r, int q, int k0, int t, const AdamConsts* __restrict__ win,
                                             int w0, const AdamConsts* __restrict__ table, float wd, float b2,
-                                            float omb2, float eps) {
+                                            float omb2, float eps, const PendSrc& ps) {
   const size_t off = (size_t)r * D + 4 * q;
   f32x4 pp = *reinterpret_cast<f32x4*>(p + off);
   f32x4 mm = *reinterpret_cast<f32x4*>(m + off);
   f32x4 vv = *reinterpret_cast<f32x4*>(v + off);
-  for (int s = k0; s < t; ++s) {
-    // the rolling window keeps every row within F <= FBN_LAZY_MAX_LAG steps, so the constants of
-    // steps k0 .. t-1 are all in the LDS window (a global fallback would turn this into flat loads)
-    const AdamConsts k = win[s - w0];
+  int s = k0;
+  if (ps.pend) {
+    const int pe = ps.pend[r];
+    if (pe >= 0) {   // step k0 with the deferred gradient (what fbn_adam_touched would have applied)
+      const f32x4 gg = *reinterpret_cast<const f32x4*>(ps.ring + (size_t)(k0 % ps.ring_n) * ps.ring_stride +
+                                                       (size_t)pe * D + 4 * q);
+      const float coef = ps.coef_hist[k0];
+      const AdamConsts k = win[k0 - w0];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float pe = pp[e], me = mm[e], ve = vv[e];
-      adam_elem(pe, me, ve, 0.f, 1.f, wd, b2, omb2, eps, k);
-      pp[e] = pe; mm[e] = me; vv[e] = ve;
+      for (int e = 0; e < 4; ++e) {
+        float pe_ = pp[e], me = mm[e], ve = vv[e];
+        adam_elem(pe_, me, ve, gg[e], coef, wd, b2, omb2, eps, k);
+        pp[e] = pe_; mm[e] = me; vv[e] = ve;
+      }
+      s = k0 + 1;
     }
+  }
+  for (; s < t; ++s) {
+    // the rolling window keeps every row within F <= FBN_LAZY_MAX_LAG steps, so the constants of
+    // steps k0 .. t-1 are all in the LDS window (a global fallback would turn this into flat loads);
+    // pad holds div_recip(bc2s), computed when the window was loaded
+    const AdamConsts k = win[s - w0];
+    adam_zero4(pp, mm, vv, wd, b2, omb2, eps, k.w1, k.nss, k.bc2s, k.pad);
   }
   *reinterpret_cast<f32x4*>(p + off) = pp;
   *reinterpret_cast<f32x4*>(m + off) = mm;
@@ -442,12 +640,17 @@ __global__ void __launch_bounds__(256) adam_catchup_kernel(float* __restrict__ p
                                                            int F, long long chunk, int parts, int* __restrict__ last,
                                                            const AdamConsts* __restrict__ table,
                                                            const int* __restrict__ step, float wd, float b2,
-                                                           float omb2, float eps) {
+                                                           float omb2, float eps, PendSrc ps) {
   constexpr int G = D / 4, RPW = 64 / G;
   __shared__ AdamConsts win[FBN_LAZY_MAX_LAG];
   const int t = *step;
   const int w0 = t > FBN_LAZY_MAX_LAG ? t - FBN_LAZY_MAX_LAG : 0;
-  for (int i = threadIdx.x; i < t - w0; i += blockDim.x) win[i] = table[w0 + i];
+  for (int i = threadIdx.x; i < t - w0; i += blockDim.x) {
+    AdamConsts c = table[w0 + i];
+    // outside (2^-20, 2): NaN forces adam_zero4's exact fallback
+    c.pad = in_range(c.bc2s, 0x35800000u, 0x40000000u) ? div_recip(c.bc2s) : __builtin_nanf("");
+    win[i] = c;
+  }
   __syncthreads();
   const long long roll0 = (long long)(t % F) * chunk;
   const long long nroll = (parts & 2) && roll0 < nrows ? min(chunk, nrows - roll0) : 0;
@@ -470,8 +673,11 @@ __global__ void __launch_bounds__(256) adam_catchup_kernel(float* __restrict__ p
     }
     const int k0 = last[r];
     if (k0 >= t) continue;
-    replay_rows<D>(p, m, v, r, q, k0, t, win, w0, table, wd, b2, omb2, eps);
-    if (q == 0) last[r] = t;
+    replay_rows<D>(p, m, v, r, q, k0, t, win, w0, table, wd, b2, omb2, eps, ps);
+    if (q == 0) {
+      last[r] = t;
+      if (ps.pend) ps.pend[r] = -1;
+    }
   }
 }
 
@@ -481,12 +687,17 @@ __global__ void __launch_bounds__(256) adam_flush_kernel(float* __restrict__ p, 
                                                          float* __restrict__ v, long long nrows, int* __restrict__ last,
                                                          const AdamConsts* __restrict__ table,
                                                          const int* __restrict__ step, float wd, float b2, float omb2,
-                                                         float eps) {
+                                                         float eps, PendSrc ps) {
   constexpr int G = D / 4, RPW = 64 / G;
   __shared__ AdamConsts win[FBN_LAZY_MAX_LAG];
   const int t = *step;
   const int w0 = t > FBN_LAZY_MAX_LAG ? t - FBN_LAZY_MAX_LAG : 0;
-  for (int i = threadIdx.x; i < t - w0; i += blockDim.x) win[i] = table[w0 + i];
+  for (int i = threadIdx.x; i < t - w0; i += blockDim.x) {
+    AdamConsts c = table[w0 + i];
+    // outside (2^-20, 2): NaN forces adam_zero4's exact fallback
+    c.pad = in_range(c.bc2s, 0x35800000u, 0x40000000u) ? div_recip(c.bc2s) : __builtin_nanf("");
+    win[i] = c;
+  }
   __syncthreads();
   const int lane = threadIdx.x & 63, q = lane % G;
   const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -496,8 +707,11 @@ __global__ void __launch_bounds__(256) adam_flush_kernel(float* __restrict__ p, 
     if (r >= nrows) continue;
     const int k0 = last[r];
     if (k0 >= t) continue;
-    replay_rows<D>(p, m, v, r, q, k0, t, win, w0, table, wd, b2, omb2, eps);
-    if (q == 0) last[r] = t;
+    replay_rows<D>(p, m, v, r, q, k0, t, win, w0, table, wd, b2, omb2, eps, ps);
+    if (q == 0) {
+      last[r] = t;
+      if (ps.pend) ps.pend[r] = -1;
+    }
   }
 }
 
@@ -544,6 +758,84 @@ __global__ void __launch_bounds__(256) adam_touched_kernel(float* __restrict__ p
     if (q == 0) {
       map[r] = -1;
       if (last) last[r] = *step_ptr + 1;
+    }
+  }
+}
+
+// Single-GPU end of step with deferred table gradients: each claiming entry e (row r) either
+// records its gradient vector in pend[r] (no duplicates: the gradient is one per-sample vector),
+// or -- claimer of a row several entries hit (FLAG) -- applies the step now as adam_touched does.
+// map[r] and slot_row[e] are reset; the step's vectors are copied into ring slot step % ring_n and
+// the clip coefficient into coef_hist[step].
+template <int D>
+__global__ void __launch_bounds__(256) adam_commit_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                          float* __restrict__ v, int* __restrict__ map, GradSrc gs,
+                                                          int n, const float* __restrict__ coef_ptr,
+                                                          const AdamConsts* __restrict__ table,
+                                                          const int* __restrict__ step_ptr, float wd, float b2,
+                                                          float omb2, float eps, int* __restrict__ last, PendSrc ps,
+                                                          float* __restrict__ coef_hist, int B) {
+  constexpr int G = D / 4, RPW = 64 / G;
+  const int t = *step_ptr;
+  const AdamConsts k = table[t];
+  const float coef = coef_ptr ? *coef_ptr : 1.f;
+  if (blockIdx.x == 0 && threadIdx.x == 0) coef_hist[t] = coef;
+  // ring copy of this step's per-sample vectors
+  float* dst = const_cast<float*>(ps.ring) + (size_t)(t % ps.ring_n) * ps.ring_stride;
+  const long long n4 = (long long)B * 2 * D / 4;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x)
+    reinterpret_cast<f32x4*>(dst)[i] = reinterpret_cast<const f32x4*>(gs.vec)[i];
+  // one entry per lane: an unflagged claimer records its vector in pend; flagged claimers (rare)
+  // are updated by the wave's G-lane groups afterwards
+  const int lane = threadIdx.x & 63, q = lane % G;
+  for (long long e0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) - lane; e0 < n;
+       e0 += (long long)gridDim.x * blockDim.x) {
+    const long long e = e0 + lane;
+    const int sr = e < n ? gs.slot_row[e] : -1;
+    const bool flag = sr != -1 && (sr & FBN_SLOT_FLAG);
+    if (sr != -1 && !flag) {
+      const int b = (int)(e / gs.Lp1), tt = (int)(e - (long long)b * gs.Lp1);
+      ps.pend[sr] = b * 2 + (tt ? 1 : 0);
+      map[sr] = -1;
+      gs.slot_row[e] = -1;
+    }
+    unsigned long long mask = __ballot(flag);
+    while (mask) {
+      // up to RPW flagged entries per round, one per G-lane group
+      int mine = -1;
+#pragma unroll
+      for (int gi = 0; gi < RPW; ++gi) {
+        if (!mask) break;
+        const int l = __ffsll((long long)mask) - 1;
+        mask &= mask - 1;
+        if (lane / G == gi) mine = l;
+      }
+      const int sr_l = __shfl(sr, mine < 0 ? 0 : mine, 64);
+      if (mine < 0) continue;
+      const long long ee = e0 + mine;
+      const long long r = sr_l & ~FBN_SLOT_FLAG;
+      f32x4 gg = *reinterpret_cast<const f32x4*>(grad_base<D>(gs, (int)ee) + 4 * q);
+      float* ex = gs.extra + (size_t)ee * D + 4 * q;
+      gg += *reinterpret_cast<const f32x4*>(ex);
+      *reinterpret_cast<f32x4*>(ex) = (f32x4){0.f, 0.f, 0.f, 0.f};
+      const size_t off = (size_t)r * D + 4 * q;
+      f32x4 pp = *reinterpret_cast<f32x4*>(p + off);
+      f32x4 mm = *reinterpret_cast<f32x4*>(m + off);
+      f32x4 vv = *reinterpret_cast<f32x4*>(v + off);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float pe = pp[c], me = mm[c], ve = vv[c];
+        adam_elem(pe, me, ve, gg[c], coef, wd, b2, omb2, eps, k);
+        pp[c] = pe; mm[c] = me; vv[c] = ve;
+      }
+      *reinterpret_cast<f32x4*>(p + off) = pp;
+      *reinterpret_cast<f32x4*>(m + off) = mm;
+      *reinterpret_cast<f32x4*>(v + off) = vv;
+      if (q == 0) {
+        map[r] = -1;
+        last[r] = t + 1;
+        gs.slot_row[ee] = -1;
+      }
     }
   }
 }
@@ -629,7 +921,9 @@ extern "C" int fbn_sparse_fixup_dup(const int* dup, int n, const float* gvec, fl
   if (!dup || !extra) { fbn_set_error("fbn_sparse_fixup_dup: dup and extra are required"); return FBN_ERR_ARG; }
   hipStream_t st = (hipStream_t)stream;
   GradSrc s{gvec, extra, slot_row, Lp1};
-  FBN_DISPATCH_D(sparse_fixup_dup_kernel, D, group_grid(n, D, 4096), dup, n, s);
+  int blocks = (n + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  FBN_DISPATCH_D(sparse_fixup_dup_kernel, D, dim3(blocks), dup, n, s);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -694,6 +988,28 @@ extern "C" int fbn_adam_touched(float* p, float* m, float* v, int D, int* map, c
   return FBN_OK;
 }
 
+// single GPU, lazy table Adam with deferred gradients: see adam_commit_kernel.  ring: [ring_n][B][2][D]
+extern "C" int fbn_adam_commit(float* p, float* m, float* v, int D, int* map, const float* gvec, float* extra,
+                               int* slot_row, int Lp1, int n, const float* coef, const void* consts_table,
+                               const int* step, float wd, float beta2, float eps, int* last, int* pend, float* ring,
+                               float* coef_hist, int ring_n, int B, void* stream) {
+  if (n <= 0) return FBN_OK;
+  if (!pend || !ring || !coef_hist || !extra || ring_n < 2 || Lp1 < 2) {
+    fbn_set_error("fbn_adam_commit: pend, ring, coef_hist and extra are required (single-GPU layout)");
+    return FBN_ERR_ARG;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const float omb2 = (float)(1.0 - (double)beta2);
+  GradSrc s{gvec, extra, slot_row, Lp1};
+  const PendSrc ps{pend, ring, coef_hist, (long long)B * 2 * D, ring_n};
+  int blocks = (n + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  FBN_DISPATCH_D(adam_commit_kernel, D, dim3(blocks), p, m, v, map, s, n, coef,
+                 (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, last, ps, coef_hist, B);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
 extern "C" int fbn_claim_rows(const int64_t* item, const int64_t* seq, int B, int L, long long V, int* map,
                               int* slot_row, int* dup, void* stream) {
   const long long n = (long long)B * (L + 1);
@@ -720,7 +1036,8 @@ extern "C" int fbn_step_end(int* step, unsigned long long* rng, double* sumsq, l
 // nothing else reads them this step -> may run on a side stream), 3 = both
 extern "C" int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, int D, const int* slot_row, int n_ent,
                                 const int* map, int F, int parts, int* last, const void* consts_table, const int* step,
-                                float wd, float beta2, float eps, void* stream) {
+                                float wd, float beta2, float eps, int* pend, const float* ring,
+                                const float* coef_hist, long long ring_stride, int ring_n, void* stream) {
   if (nrows <= 0) return FBN_OK;
   if (F < 1 || F > FBN_LAZY_MAX_LAG) { fbn_set_error("fbn_adam_catchup: 1 <= F <= 512"); return FBN_ERR_ARG; }
   hipStream_t st = (hipStream_t)stream;
@@ -732,19 +1049,26 @@ extern "C" int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, i
   // slots to the main stream while its four-chain replay keeps the VALU busy
   static const int wcap = getenv("FBN_WINDOW_BLOCKS") ? atoi(getenv("FBN_WINDOW_BLOCKS")) : 256;   // tools/window_sweep.sh
   const long long cap = parts == 2 ? wcap : 8192;
+  if (pend && (!ring || !coef_hist || ring_n <= F)) {
+    fbn_set_error("fbn_adam_catchup: deferred gradients need ring, coef_hist and ring_n > F");
+    return FBN_ERR_ARG;
+  }
+  const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
   FBN_DISPATCH_D(adam_catchup_kernel, D, group_grid(items, D, cap), p, m, v, slot_row, n_ent, map, nrows, F, chunk,
-                 parts, last, (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps);
+                 parts, last, (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
 
 extern "C" int fbn_adam_flush(float* p, float* m, float* v, long long nrows, int D, int* last, const void* consts_table,
-                              const int* step, float wd, float beta2, float eps, void* stream) {
+                              const int* step, float wd, float beta2, float eps, int* pend, const float* ring,
+                              const float* coef_hist, long long ring_stride, int ring_n, void* stream) {
   if (nrows <= 0) return FBN_OK;
   hipStream_t st = (hipStream_t)stream;
   const float omb2 = (float)(1.0 - (double)beta2);
+  const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
   FBN_DISPATCH_D(adam_flush_kernel, D, group_grid(nrows, D, 16384), p, m, v, nrows, last,
-                 (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps);
+                 (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

@@ -54,6 +54,22 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, transA, transB, bias=None, rB=NO_REMAP
          stream if stream is not None else _lib.stream_handle())
 
 
+def split_mlp_input(d: int) -> bool:
+    """bf16 MLP-input GEMMs read [Vc16 | pair block of c] as a split operand (LDS-DMA path:
+    the 5d-column boundary must be a multiple of 128)."""
+    return (5 * d) % 128 == 0
+
+
+def gemm_split(A, B, C, M, N, K, lda, ldb, ldc, transA, transB, bias=None, rC=NO_REMAP, beta=0.0, stream=None,
+               stats=None, A2=None, lda2=0, kseg=INT_MAX, B2=None, ldb2=0, nseg=INT_MAX):
+    """bf16 C = op(A) op(B) with A = [A | A2] along K (k-contiguous A) or B = [B | B2] along N (k-major B)."""
+    nbytes = _lib.lib().fbn_gemm_workspace_size(M, N, K, 1)
+    ws = _ws(nbytes, C.device)
+    call("fbn_gemm_split", ptr(A), ptr(B), ptr(C), ptr(bias), M, N, K, lda, ldb, ldc, int(transA), int(transB),
+         rC[0], rC[1], rC[2], float(beta), ptr(stats), ptr(ws), nbytes, ptr(A2), lda2, kseg, ptr(B2), ldb2, nseg,
+         stream if stream is not None else _lib.stream_handle())
+
+
 class _ConvJob(ctypes.Structure):
     _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("rows", ctypes.c_int), ("cols", ctypes.c_int),
                 ("ld", ctypes.c_int), ("trans", ctypes.c_int), ("seg", ctypes.c_int), ("off0", ctypes.c_int),
@@ -255,13 +271,16 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     hmm = buf("hmm", (B, d))
     gemm(w16["x"] if bf else x_mm, w16["Wp"] if bf else p["mm_proj.0.weight"], hmm, B, d, 128, 128, 128, d, False,
          True, bias=p["mm_proj.0.bias"], bf16=bf, stream=st)
-    X = buf("X", (B, 5, d))
+    X = buf("X", (B, 2, d))                     # fields 3 and 5 (the backward recomputes 1, 2, 4)
     # bf16 mode: the fields after SENET exist only as bf16 (GEMM operand and pair-kernel input)
     v16 = bf and not cfg.bilinear_each
     Vc = None if v16 else buf("Vc", (B, 5, d))
     Vc16 = buf("Vc16", (B, 5, d), torch.bfloat16) if v16 else None
     KC = 15 * d
     c = buf("c", (B, KC), torch.bfloat16 if bf else torch.float32)     # bf16 mode: GEMM-only operand
+    # bf16 LDS-DMA mode: c's V block is never written -- the MLP GEMMs read [Vc16 | c[:, 5d:]] (split operand)
+    split_c = v16 and split_mlp_input(d)
+    a["split_c"] = split_c
     av = buf("a", (B, 6))
     cnt = buf("cnt", (B,))
     if err is None:
@@ -280,7 +299,7 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
          ptr(p["cate_emb.weight"]), p["cate_emb.weight"].shape[0], ptr(E), V, ptr(pos),
          ptr(p["senet.excitation.0.weight"]), ptr(p["senet.excitation.0.bias"]),
          ptr(p["senet.excitation.2.weight"]), ptr(p["senet.excitation.2.bias"]), cfg.R, ptr(X), ptr(Vc), ptr(Vc16),
-         ptr(c), KC,
+         None if split_c else ptr(c), KC,
          int(bf), ptr(av), ptr(cnt), ptr(err), ptr(sm.get("map")), ptr(sm.get("slot_row")), B, Lr, d, st)
     if ev is not None:
         ev[1].record()
@@ -310,7 +329,10 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
         ev1 = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev1[0].record()
         probe.setdefault("gemm_mlp0", []).append(ev1)
-    if bf:
+    if split_c:
+        gemm_split(Vc16, w16["Wa"], h1pre, B, H1, KC, 5 * d, KC, H1, False, True, bias=p["mlp.0.bias"], stream=st,
+                   stats=t1, A2=c[:, 5 * d:], lda2=KC, kseg=5 * d)
+    elif bf:
         gemm(c, w16["Wa"], h1pre, B, H1, KC, KC, KC, H1, False, True, bias=p["mlp.0.bias"], bf16=True, stream=st,
              stats=t1)
     else:
@@ -442,7 +464,11 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
                 dh1pre, g["mlp.1.weight"], g["mlp.1.bias"], None, coll, st, dpre16=dh1pre16,
                 bias_grad=g["mlp.0.bias"], sums=sums)
     dc = torch.empty((B, KC), **f32)
-    if bf:
+    if a.get("split_c"):
+        wg.run(lambda s: gemm_split(dh1pre16, a["Vc16"], g["mlp.0.weight"], H1, KC, B, H1, 5 * d, 21 * d, True,
+                                    False, rC=wa_remap(d), stream=s, B2=a["c"][:, 5 * d:], ldb2=KC, nseg=5 * d))
+        gemm(dh1pre16, w16["WaT"], dc, B, KC, H1, H1, H1, KC, False, True, stream=st)
+    elif bf:
         wg.run(lambda s: gemm(dh1pre16, a["c"], g["mlp.0.weight"], H1, KC, B, H1, KC, 21 * d, True, False,
                               rC=wa_remap(d), stream=s))
         gemm(dh1pre16, w16["WaT"], dc, B, KC, H1, H1, H1, KC, False, True, stream=st)
@@ -492,9 +518,9 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
         evb[0].record()
         probe.setdefault("fields_bwd", []).append(evb)
     call("fbn_fields_bwd", ptr(batch["item_id"]), ptr(seq) if Lr else None, ptr(batch["likes_level"]),
-         ptr(batch["views_level"]), ptr(a["hmm"]), ptr(p["mm_proj.1.weight"]), LN_EPS,
+         ptr(batch["views_level"]), ptr(a["hmm"]), ptr(p["mm_proj.1.weight"]), ptr(p["mm_proj.1.bias"]), LN_EPS,
          ptr(p["senet.excitation.0.weight"]), ptr(p["senet.excitation.0.bias"]), ptr(p["senet.excitation.2.weight"]),
-         R, ncate, ptr(a["X"]), ptr(a["a"]), ptr(a["cnt"]), ptr(dV), ptr(dhmm), ptr(dhmm16), ptr(partials), outs,
+         R, ncate, ptr(p["cate_emb.weight"]), ptr(a["X"]), ptr(a["a"]), ptr(a["cnt"]), ptr(dV), ptr(dhmm), ptr(dhmm16), ptr(partials), outs,
          ptr(table_grad), ptr(gvec), ptr(gnorm), V, ptr(pos), ptr(sendbuf), B, Lr, d, st)
     if evb is not None:
         evb[1].record()

@@ -64,7 +64,7 @@ class FiBiNETTrainer:
                  lr: Optional[float] = None, weight_decay: Optional[float] = None, rank: int = 0, world: int = 1,
                  group=None, init_state: Optional[Dict[str, torch.Tensor]] = None, seed: int = 2025,
                  stage_on_cpu: bool = False, dropout_seed: Optional[int] = None, table_adam: str = "lazy",
-                 lazy_window: int = 128):
+                 lazy_window: int = 128, defer_table_grads: bool = True):
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise RuntimeError("FiBiNETTrainer runs on a HIP device only (no CPU fallback)")
@@ -163,6 +163,15 @@ class FiBiNETTrainer:
             raise ValueError(f"table_adam must be 'lazy' or 'eager', not {self.table_adam!r}")
         self.lazy_window = int(lazy_window)
         self.last = torch.zeros(max(1, self.rows_local), **i32)     # Adam steps applied per table row
+        # single GPU, lazy: deferred table gradients (fbn_adam_commit) -- pend[r] = per-sample vector
+        # row r received at step last[r]; the vectors of the last F+1 steps stay in a ring
+        self.deferred = self.table_adam == "lazy" and world == 1 and defer_table_grads
+        self.pend = self.ring = self.coef_hist = None
+        self.ring_n = self.lazy_window + 1
+        if self.deferred:
+            self.pend = torch.full((max(1, self.rows_local),), -1, **i32)
+            self.ring = torch.zeros((self.ring_n, self.B, 2, d), dtype=torch.float32, device=dev)
+            self.coef_hist = torch.ones(total_steps + 1, dtype=torch.float32, device=dev)
         self.side = torch.cuda.Stream(device=dev)      # eager untouched pass / lazy rolling window
 
     # ------------------------------------------------------------------ one training step
@@ -200,13 +209,13 @@ class FiBiNETTrainer:
             ev = _events(probe, "adam_catchup")
             call("fbn_adam_catchup", ptr(self.E), ptr(self.Em), ptr(self.Ev), self.rows_local, d, ptr(self.slot_row),
                  n_ent, ptr(self.map), self.lazy_window, 1, ptr(self.last), ptr(self.sched), ptr(self.step_dev),
-                 self.wd, self.beta2, self.eps, st)
+                 self.wd, self.beta2, self.eps, *self._pend_args(), st)
             _events_end(ev)
             self.side.wait_stream(main)
             ev = _events(probe, "adam_window", self.side)
             call("fbn_adam_catchup", ptr(self.E), ptr(self.Em), ptr(self.Ev), self.rows_local, d, None, 0,
                  ptr(self.map), self.lazy_window, 2, ptr(self.last), ptr(self.sched), ptr(self.step_dev), self.wd,
-                 self.beta2, self.eps, self.side.cuda_stream)
+                 self.beta2, self.eps, *self._pend_args(), self.side.cuda_stream)
             _events_end(ev, self.side)
 
         def start_untouched_adam():
@@ -269,23 +278,40 @@ class FiBiNETTrainer:
              self.n_dense, None, ptr(self.sched), ptr(self.step_dev), self.wd, self.beta2, self.eps, ptr(self.sumsq),
              self.max_norm, ptr(self.coef), ptr(self.norm), st)
         main.wait_stream(self.side)   # side-stream table pass done before map entries are reset
-        ev = _events(probe, "adam_touched")
-        call("fbn_adam_touched", ptr(self.E), ptr(self.Em), ptr(self.Ev), d, ptr(self.map), ptr(gsrc[0]),
-             ptr(gsrc[1]), ptr(self.slot_row), gsrc[2], n_ent, ptr(self.coef), ptr(self.sched), ptr(self.step_dev),
-             self.wd, self.beta2, self.eps, ptr(self.last) if lazy else None, st)
-        _events_end(ev)
-        self.slot_row[:n_ent].fill_(-1)
+        if self.deferred:
+            # the step's table gradient is applied at each row's next replay (flagged rows: now);
+            # map and slot_row are reset in the same launch
+            ev = _events(probe, "adam_commit")
+            call("fbn_adam_commit", ptr(self.E), ptr(self.Em), ptr(self.Ev), d, ptr(self.map), ptr(gsrc[0]),
+                 ptr(gsrc[1]), ptr(self.slot_row), gsrc[2], n_ent, ptr(self.coef), ptr(self.sched),
+                 ptr(self.step_dev), self.wd, self.beta2, self.eps, ptr(self.last), ptr(self.pend), ptr(self.ring),
+                 ptr(self.coef_hist), self.ring_n, self.B, st)
+            _events_end(ev)
+        else:
+            ev = _events(probe, "adam_touched")
+            call("fbn_adam_touched", ptr(self.E), ptr(self.Em), ptr(self.Ev), d, ptr(self.map), ptr(gsrc[0]),
+                 ptr(gsrc[1]), ptr(self.slot_row), gsrc[2], n_ent, ptr(self.coef), ptr(self.sched),
+                 ptr(self.step_dev), self.wd, self.beta2, self.eps, ptr(self.last) if lazy else None, st)
+            _events_end(ev)
+            self.slot_row[:n_ent].fill_(-1)
         call("fbn_step_end", ptr(self.step_dev), ptr(self.rng), ptr(self.sumsq), ptr(self.p["mlp.1.num_batches_tracked"]),
              ptr(self.p["mlp.5.num_batches_tracked"]), st)
         self.host_step += 1
         return self.loss
+
+    def _pend_args(self):
+        """(pend, ring, coef_hist, ring_stride, ring_n) of the deferred table gradients (NULLs when off)."""
+        if not self.deferred:
+            return (None, None, None, 0, 0)
+        return (ptr(self.pend), ptr(self.ring), ptr(self.coef_hist), self.B * 2 * self.d, self.ring_n)
 
     # ------------------------------------------------------------------ inference
     def flush(self) -> None:
         """Bring every table row up to the current step (lazy table Adam); a no-op when eager."""
         if self.table_adam == "lazy":
             call("fbn_adam_flush", ptr(self.E), ptr(self.Em), ptr(self.Ev), self.rows_local, self.d, ptr(self.last),
-                 ptr(self.sched), ptr(self.step_dev), self.wd, self.beta2, self.eps, _lib.stream_handle(self.device))
+                 ptr(self.sched), ptr(self.step_dev), self.wd, self.beta2, self.eps, *self._pend_args(),
+                 _lib.stream_handle(self.device))
 
     @torch.no_grad()
     def predict(self, batch: Dict[str, torch.Tensor], logits: bool = False) -> torch.Tensor:
@@ -339,3 +365,5 @@ class FiBiNETTrainer:
             else:
                 self.p[k].copy_(sd[k].to(self.device))
         self.last.fill_(self.host_step)             # loaded rows are current
+        if self.pend is not None:
+            self.pend.fill_(-1)

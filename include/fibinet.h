@@ -53,6 +53,14 @@ int fbn_gemm(const void* A, const void* B, float* C, const float* bias, int M, i
              int ldc, int transA, int transB, int rB_seg, int rB_off0, int rB_off1, int rC_seg, int rC_off0,
              int rC_off1, float beta, int bf16, int a16, int b16, float* stats, float* ws, size_t ws_bytes,
              void* stream);
+/* bf16 GEMM over a split operand (LDS-DMA path): A2/kseg -- a k-contiguous A is [A | A2] along K
+ * (A(m,k), k >= kseg, at A2[m*lda2 + k - kseg]); B2/nseg -- a k-major B is [B | B2] along N
+ * (B(k,n), n >= nseg, at B2[k*ldb2 + n - nseg]); segments multiples of 128.  The MLP input
+ * [V_1..V_5 | pairs] is read from the bf16 fields (Vc16) and the pair block of c without a copy. */
+int fbn_gemm_split(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, int lda, int ldb,
+                   int ldc, int transA, int transB, int rC_seg, int rC_off0, int rC_off1, float beta, float* stats,
+                   float* ws, size_t ws_bytes, const void* A2, int lda2, int kseg, const void* B2, int ldb2, int nseg,
+                   void* stream);
 
 /* ---------------------------------------------------------------- K1 + K4: fields + SENET forward
  * Replaces: nn.Embedding lookups (src/model_fibinet.py:155,156,159,167), masked history mean
@@ -82,8 +90,8 @@ int fbn_fields_bwd_grid(int B, int D);
 /* Vc16 / dhmm16 / dU16 (optional, may be NULL): bf16 copies written beside the fp32 outputs,
  * the operands of the bf16 GEMMs that consume them (compute_dtype bf16). */
 int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes, const int64_t* views,
-                   const float* hmm, const float* ln_g, float ln_eps, const float* w1, const float* b1, const float* w2,
-                   int R, int n_cate, const float* X, const float* a, const float* cnt, const float* dV, float* dhmm,
+                   const float* hmm, const float* ln_g, const float* ln_b, float ln_eps, const float* w1,
+                   const float* b1, const float* w2, int R, int n_cate, const float* cate, const float* X, const float* a, const float* cnt, const float* dV, float* dhmm,
                    short* dhmm16, float* partials, float* const* param_grads, float* gtab, float* gvec,
                    double* gnorm, long long V, const int* pos, float* sendbuf, int B, int L, int D, void* stream);
 /* gnorm (optional, with gvec): [B][2] float64 sums of squares of the two per-sample vectors,
@@ -216,11 +224,29 @@ int fbn_adam_touched(float* p, float* m, float* v, int D, int* map, const float*
  * (src/train_fibinet.py:78,121) by O(touched + nrows/F) rows per step.  F <= 512. */
 /* parts: 1 = claimed rows (before the gather), 2 = rolling window (unclaimed rows; may overlap the
  * step on another stream), 3 = both. */
+/* Deferred gradients (single GPU; pend == NULL disables): pend[r] = index b*2+slot of the
+ * per-sample gradient vector row r received at step last[r] (-1 = none); ring [ring_n][B][2][D]
+ * holds step s's vectors in slot s % ring_n (ring_stride = B*2*D floats, ring_n > F);
+ * coef_hist[s] = step s's clip coefficient.  A replay applies that step with the gradient first. */
 int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, int D, const int* slot_row, int n_ent,
                      const int* map, int F, int parts, int* last, const void* consts_table, const int* step, float wd,
-                     float beta2, float eps, void* stream);
+                     float beta2, float eps, int* pend, const float* ring, const float* coef_hist,
+                     long long ring_stride, int ring_n, void* stream);
 int fbn_adam_flush(float* p, float* m, float* v, long long nrows, int D, int* last, const void* consts_table,
-                   const int* step, float wd, float beta2, float eps, void* stream);
+                   const int* step, float wd, float beta2, float eps, int* pend, const float* ring,
+                   const float* coef_hist, long long ring_stride, int ring_n, void* stream);
+/* Self-test of the packed exact zero-gradient Adam step of the lazy replay: n x 4 random operands
+ * across the f32 range against the reference element step, bit for bit; mism[0] += mismatching
+ * elements, mism[1] += elements on the fast path (device counters, caller zeroes). */
+int fbn_adam_selftest(int n, unsigned seed, unsigned long long* mism, void* stream);
+/* Single-GPU end of step with deferred table gradients (replaces fbn_adam_touched + the slot_row
+ * reset): a claiming entry without duplicates records its vector in pend (applied at the row's
+ * next replay); one with duplicates (FLAG) is updated now; map and slot_row are reset; the step's
+ * vectors go to ring slot step % ring_n and the clip coefficient to coef_hist[step]. */
+int fbn_adam_commit(float* p, float* m, float* v, int D, int* map, const float* gvec, float* extra, int* slot_row,
+                    int Lp1, int n, const float* coef, const void* consts_table, const int* step, float wd,
+                    float beta2, float eps, int* last, int* pend, float* ring, float* coef_hist, int ring_n, int B,
+                    void* stream);
 
 /* sumsq accumulators are FBN_SUMSQ_SLOTS (= 64) doubles; fbn_clip_coef sums them and
  * fbn_step_end zeroes them.  fbn_claim_rows registers the rows of a batch in map/slot_row (the

@@ -42,7 +42,25 @@ def main():
             continue
         A, Bm, lda, ldb, ref = operands(M, N, K, tA, tB)
         C = torch.empty((M, N), device=dev)
-        modes = ("old", "dma16")
+        # library reference point: torch.mm (hipBLASLt) on the same bf16 operands, f32 output
+        Aop = A.T if tA else A
+        Bop = Bm.T if tB else Bm
+        try:
+            for _ in range(3):
+                torch.mm(Aop, Bop, out_dtype=torch.float32)
+            lib = lambda: torch.mm(Aop, Bop, out_dtype=torch.float32)
+        except (TypeError, RuntimeError):
+            lib = lambda: torch.mm(Aop, Bop)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(20):
+            lib()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / 20 * 1e3
+        print(f"torch {name:15s} M={M:5d} N={N:5d} K={K:5d} {us:6.1f}us ({2 * M * N * K / us / 1e6:5.0f} TF)", flush=True)
+        modes = ("dma16",) if os.environ.get("FBN_SWEEP_DMA_ONLY") else ("old", "dma16")
         for mode in modes:
             if mode == "old":
                 os.environ["FBN_GEMM_NO_DMA16"] = "1"
