@@ -55,6 +55,7 @@ SIGNATURES = {
     "fbn_bn_stats": (I, [P, I, I, P, P, P, P, F, F, I, P, P]),
     "fbn_bn_eval_params": (I, [P, P, P, P, I, F, P]),
     "fbn_bn_act_fwd": (I, [P, P, I, I, P, P, P, P, F, P, U, P, P, P, P]),
+    "fbn_bn_act_head_fwd": (I, [P, P, I, I, P, P, P, P, F, P, U, P, P, P, P, P, P, P, P, P, F, P]),
     "fbn_bn_bwd_reduce": (I, [P, P, P, P, F, P, P, I, I, P, P, P]),
     "fbn_bn_bwd_apply": (I, [P, P, P, P, F, P, P, P, P, I, I, P, D, P, P, P, P, P, P, P]),
     "fbn_convert_bf16": (I, [P, I, P]),
@@ -77,6 +78,8 @@ SIGNATURES = {
     "fbn_adam_catchup": (I, [P, P, P, LL, I, P, I, P, I, I, P, P, P, F, F, F, P, P, P, LL, I, P]),
     "fbn_adam_flush": (I, [P, P, P, LL, I, P, P, P, F, F, F, P, P, P, LL, I, P]),
     "fbn_adam_selftest": (I, [I, ctypes.c_uint, P, P]),
+    "fbn_adam_step_tail": (I, [P, P, P, P, LL, P, F, P, P, P, P, P, I, P, P, P, P, I, I, P, P, F, F, F, P, P, P, P, I, I,
+                               P, P, P, P, P]),
     "fbn_adam_commit": (I, [P, P, P, I, P, P, P, P, I, I, P, P, P, F, F, F, P, P, P, P, I, I, P]),
     "fbn_claim_rows": (I, [P, P, I, I, LL, P, P, P, P]),
     "fbn_pack_extras": (I, [P, P, P, P]),

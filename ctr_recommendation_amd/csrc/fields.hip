@@ -288,7 +288,7 @@ __global__ void __launch_bounds__(256) fields_bwd_kernel(FieldBwdArgs p) {
   extern __shared__ __attribute__((aligned(16))) float sp[];   // 4 wave slices of P floats + SENET staging
   const int R = p.R;
   const int NP = 13 * R + 6;
-  const int P = NP + 2 * D + p.n_cate * D;
+  const int P = NP + 3 * D + p.n_cate * D;      // ... | cate rows | mm_proj bias (column sums of dhmm)
   const int wave = threadIdx.x >> 6;
   float* ws = sp + wave * P;                       // this wave's slice
   // per group: {ds[6], z[6], dq[R], rj[R]} staged for the lanes that own SENET entries
@@ -297,13 +297,14 @@ __global__ void __launch_bounds__(256) fields_bwd_kernel(FieldBwdArgs p) {
   __syncthreads();
   float* w_lg = ws + NP;
   float* w_ct = w_lg + 2 * D;
+  float* w_hb = w_ct + p.n_cate * D;
 
   const int lane = threadIdx.x & 63;
   const int q = lane % G, grp = lane / G;
   const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nwaves = (gridDim.x * blockDim.x) >> 6;
   const int L = p.L;
-  f32x4 acc_lg = {0.f, 0.f, 0.f, 0.f}, acc_lb = {0.f, 0.f, 0.f, 0.f};
+  f32x4 acc_lg = {0.f, 0.f, 0.f, 0.f}, acc_lb = {0.f, 0.f, 0.f, 0.f}, acc_hb = {0.f, 0.f, 0.f, 0.f};
   float acc_se[SJ];
 #pragma unroll
   for (int j = 0; j < SJ; ++j) acc_se[j] = 0.f;
@@ -420,6 +421,7 @@ __global__ void __launch_bounds__(256) fields_bwd_kernel(FieldBwdArgs p) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) out[e] = rstd * (gx[e] - m1 - xh[e] * m2);
         *reinterpret_cast<f32x4*>(p.dhmm + (size_t)b * D + 4 * q) = out;
+        acc_hb += out;                              // mm_proj.0.bias gradient (sum over the batch)
         if (p.dhmm16)
           *reinterpret_cast<bf16x4*>(p.dhmm16 + (size_t)b * D + 4 * q) = (bf16x4){f2bf(out[0]), f2bf(out[1]),
                                                                                    f2bf(out[2]), f2bf(out[3])};
@@ -485,6 +487,7 @@ __global__ void __launch_bounds__(256) fields_bwd_kernel(FieldBwdArgs p) {
     for (int e = 0; e < 4; ++e) {
       acc_lg[e] += __shfl_xor(acc_lg[e], o, 64);
       acc_lb[e] += __shfl_xor(acc_lb[e], o, 64);
+      acc_hb[e] += __shfl_xor(acc_hb[e], o, 64);
     }
 #pragma unroll
     for (int j = 0; j < SJ; ++j) acc_se[j] += __shfl_xor(acc_se[j], o, 64);
@@ -492,6 +495,7 @@ __global__ void __launch_bounds__(256) fields_bwd_kernel(FieldBwdArgs p) {
   if (grp == 0) {
     *reinterpret_cast<f32x4*>(w_lg + 4 * q) = acc_lg;
     *reinterpret_cast<f32x4*>(w_lg + D + 4 * q) = acc_lb;
+    *reinterpret_cast<f32x4*>(w_hb + 4 * q) = acc_hb;
 #pragma unroll
     for (int j = 0; j < SJ; ++j) {
       const int k = q + j * G;
@@ -503,40 +507,33 @@ __global__ void __launch_bounds__(256) fields_bwd_kernel(FieldBwdArgs p) {
   for (int i = threadIdx.x; i < P; i += blockDim.x) out[i] = (sp[i] + sp[P + i]) + (sp[2 * P + i] + sp[3 * P + i]);
 }
 
-// Sum per-block partial slabs: out[i] = sum_b part[b][i], in a fixed order (deterministic).
-// Level 1: grid (ceil(P/64), RED_CH) -- 64 columns x 4 row lanes per block, each chunk of
-// rows summed into part[nblk + chunk][i];  level 2: one wave per column over the chunks.
-#define RED_CH 16
-__global__ void reduce_partials_l1(float* part, int nblk, int P) {
-  __shared__ float red[4][64];
-  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int rl = threadIdx.x >> 6;
-  const int per = (nblk + RED_CH - 1) / RED_CH;
-  const int r0 = blockIdx.y * per, r1 = min(nblk, r0 + per);
+// destinations of the 8 parameter-gradient segments (w1, b1, w2, b2, ln_g, ln_b, cate, mm_proj bias)
+struct GradOuts {
+  float* p[8];
+  int off[9];
+};
+// One launch: 64 columns per 1024-thread block, the 16 waves stride over the partial rows, a
+// fixed-order fold across the waves (deterministic), then each column to its destination.
+__global__ void __launch_bounds__(1024) reduce_partials_one(const float* __restrict__ part, int nblk, int P, GradOuts o) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;
   float s = 0.f;
   if (i < P)
-    for (int r = r0 + rl; r < r1; r += 4) s += part[(size_t)r * P + i];
-  red[rl][threadIdx.x & 63] = s;
+    for (int r = w; r < nblk; r += 16) s += part[(size_t)r * P + i];
+  red[w][lane] = s;
   __syncthreads();
-  if (rl == 0 && i < P)
-    part[(size_t)(nblk + blockIdx.y) * P + i] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-}
-// destinations of the 7 parameter-gradient segments (w1, b1, w2, b2, ln_g, ln_b, cate)
-struct GradOuts {
-  float* p[7];
-  int off[8];
-};
-__global__ void reduce_partials_l2(const float* part, int nblk, int P, GradOuts o) {
-  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-  if (i >= P) return;
-  float s = 0.f;
+  if (w == 0 && i < P) {
+    float t = 0.f;
 #pragma unroll
-  for (int k = 0; k < RED_CH; ++k) s += part[(size_t)(nblk + k) * P + i];
-  int seg = 0;
+    for (int k = 0; k < 16; ++k) t += red[k][lane];
+    int seg = 0;
 #pragma unroll
-  for (int j = 1; j < 7; ++j) seg += (i >= o.off[j]) ? 1 : 0;
-  o.p[seg][i - o.off[seg]] = s;
+    for (int j = 1; j < 8; ++j) seg += (i >= o.off[j]) ? 1 : 0;
+    if (o.p[seg]) o.p[seg][i - o.off[seg]] = t;
+  }
 }
+
 
 // ------------------------------------------------------------------------------ C ABI
 #ifndef FBN_FB_MAXBLK
@@ -588,14 +585,14 @@ extern "C" int fbn_fields_fwd(const int64_t* item_id, const int64_t* item_seq, c
   return launch_fields_fwd<0>(a, D, (hipStream_t)stream);
 }
 
-extern "C" int fbn_fields_bwd_partials_size(int D, int R, int n_cate) { return 13 * R + 6 + 2 * D + n_cate * D; }
-// rows of the `partials` scratch the caller allocates: one per block + RED_CH reduction rows
-extern "C" int fbn_fields_bwd_grid(int B, int D) { return fields_grid(B, D, FBN_FB_MAXBLK) + RED_CH; }
+extern "C" int fbn_fields_bwd_partials_size(int D, int R, int n_cate) { return 13 * R + 6 + 3 * D + n_cate * D; }
+// rows of the `partials` scratch the caller allocates: one per block
+extern "C" int fbn_fields_bwd_grid(int B, int D) { return fields_grid(B, D, FBN_FB_MAXBLK); }
 
 template <int MODE, int RMAX>
 static int launch_fields_bwd_r(const FieldBwdArgs& a, int D, hipStream_t st) {
   const int grid = fields_grid(a.B, D, FBN_FB_MAXBLK);
-  const size_t lds = (4 * (size_t)(13 * a.R + 6 + 2 * D + a.n_cate * D) + 4 * (64 / (D / 4)) * (12 + 2 * RMAX)) *
+  const size_t lds = (4 * (size_t)(13 * a.R + 6 + 3 * D + a.n_cate * D) + 4 * (64 / (D / 4)) * (12 + 2 * RMAX)) *
                      sizeof(float);   // 4 wave slices + SENET staging
   switch (D) {
     case 16: hipLaunchKernelGGL((fields_bwd_kernel<16, MODE, RMAX>), dim3(grid), dim3(256), lds, st, a); break;
@@ -616,7 +613,7 @@ static int launch_fields_bwd(const FieldBwdArgs& a, int D, hipStream_t st) {
 }
 
 // partials: [fbn_fields_bwd_grid(B,D)][fbn_fields_bwd_partials_size(D,R,n_cate)] scratch;
-// partials: [fbn_fields_bwd_grid(B,D)][P] scratch; param_grads: host array of 7 device
+// partials: [fbn_fields_bwd_grid(B,D)][P] scratch; param_grads: host array of 8 device
 // pointers receiving the gradients of w1, b1, w2, b2, ln_g, ln_b, cate.
 extern "C" int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes,
                               const int64_t* views, const float* hmm, const float* ln_g, const float* ln_b,
@@ -636,18 +633,21 @@ extern "C" int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, c
   hipStream_t st = (hipStream_t)stream;
   int rc = pos ? launch_fields_bwd<1>(p, D, st) : launch_fields_bwd<0>(p, D, st);
   if (rc) return rc;
-  const int P = 13 * R + 6 + 2 * D + n_cate * D;
+  const int P = 13 * R + 6 + 3 * D + n_cate * D;
   const int nblk = fields_grid(B, D, FBN_FB_MAXBLK);
-  hipLaunchKernelGGL(reduce_partials_l1, dim3(fbn_cdiv(P, 64), RED_CH), dim3(256), 0, st, partials, nblk, P);
+
   GradOuts o;
-  const int sizes[7] = {6 * R, R, 6 * R, 6, D, D, n_cate * D};
+  const int sizes[8] = {6 * R, R, 6 * R, 6, D, D, n_cate * D, D};
   o.off[0] = 0;
-  for (int j = 0; j < 7; ++j) {
-    if (!param_grads[j]) { fbn_set_error("fbn_fields_bwd: null parameter-gradient destination"); return FBN_ERR_ARG; }
-    o.p[j] = param_grads[j];
+  for (int j = 0; j < 8; ++j) {
+    if (j < 7 && !param_grads[j]) {
+      fbn_set_error("fbn_fields_bwd: null parameter-gradient destination");
+      return FBN_ERR_ARG;
+    }
+    o.p[j] = param_grads[j];   // [7] (mm_proj bias) may be null: not written
     o.off[j + 1] = o.off[j] + sizes[j];
   }
-  hipLaunchKernelGGL(reduce_partials_l2, dim3(fbn_cdiv(P, 64)), dim3(64), 0, st, (const float*)partials, nblk, P, o);
+  hipLaunchKernelGGL(reduce_partials_one, dim3(fbn_cdiv(P, 64)), dim3(1024), 0, st, (const float*)partials, nblk, P, o);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

@@ -588,18 +588,28 @@ __global__ void __launch_bounds__(256) gemm_dma16_kernel(GemmArgs g, int tiles_n
     if (t + S - 1 < nk) issue(t + S - 1, (t + S - 1) % S);
     const char* SA = smem + (t % S) * STAGE;
     const char* SB = SA + AB;
+    // fragments double-buffered in registers: the LDS reads of sub-step s+1 are in flight while
+    // the MFMAs of sub-step s run (one wave per SIMD at 128x128 tiles cannot hide them otherwise)
+    bf16x8 af[2][TM], bfr[2][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[0][i] = frag<BM, AKM>(SA, wm * WM + i * 32, 0, lane);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bfr[0][j] = frag<BN, BKM>(SB, wn * WN + j * 32, 0, lane);
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {
-      bf16x8 af[TM], bfr[TN];
+      const int cb = s & 1, nb = cb ^ 1;
+      if (s + 1 < BK / 16) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = frag<BM, AKM>(SA, wm * WM + i * 32, s, lane);
+        for (int i = 0; i < TM; ++i) af[nb][i] = frag<BM, AKM>(SA, wm * WM + i * 32, s + 1, lane);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[j] = frag<BN, BKM>(SB, wn * WN + j * 32, s, lane);
+        for (int j = 0; j < TN; ++j) bfr[nb][j] = frag<BN, BKM>(SB, wn * WN + j * 32, s + 1, lane);
+      }
+      __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of this sub-step's MFMAs
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[cb][i], bfr[cb][j], acc[i][j], 0, 0, 0);
     }
   }
   __syncthreads();   // the stats epilogue reuses the staging LDS

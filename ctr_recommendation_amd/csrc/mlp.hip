@@ -205,9 +205,39 @@ __global__ void bn_act_fwd_kernel(const float* __restrict__ X, float* __restrict
   }
 }
 
+struct HeadArgs {
+  const float* w; const float* bias;
+  float* logits; float* probs; const float* labels; float* loss_terms; float* gout;
+  float denom;
+};
+// Linear(C,1) + sigmoid + BCE terms + dL/dlogit of one row from the wave's lane partials
+// (lane q holds columns 4q..4q+3): shared by head_fwd_kernel and the fused BN2 + head kernel
+__device__ __forceinline__ void head_row(float s, int row, int lane, const HeadArgs& h) {
+  s = wave_sum(s);
+  if (lane == 0) {
+    const float o = s + h.bias[0];
+    const float pr = 1.f / (1.f + expf(-o));
+    if (h.logits) h.logits[row] = o;
+    if (h.probs) h.probs[row] = pr;
+    if (h.labels) {
+      const float t = h.labels[row];
+      const float lp = fmaxf(logf(pr), -100.f), l1p = fmaxf(logf(1.f - pr), -100.f);
+      if (h.loss_terms) h.loss_terms[row] = -(t * lp + (1.f - t) * l1p);
+      if (h.gout) {
+        const float gp = ((pr - t) / fmaxf((1.f - pr) * pr, 1e-12f)) / h.denom;
+        h.gout[row] = gp * (1.f - pr) * pr;
+      }
+    }
+  }
+}
+
 // Column-blocked form: block = 64 column quads (256 columns) x 4 row lanes over a chunk of rows,
 // the per-column affine (alpha, beta') computed once per thread, no index division.  Same
 // Philox counter (flat quad index) and arithmetic as bn_act_fwd_kernel.
+// HEAD (C == 256, one column block): each wave holds whole rows, so the head Linear(256,1) +
+// sigmoid + BCE of src/model_fibinet.py:134,136 runs on the activations still in registers
+// (the same lane partials and reduction as head_fwd_kernel: bit-identical, one launch fewer).
+template <bool HEAD>
 __global__ void __launch_bounds__(256) bn_act_fwd2_kernel(const float* __restrict__ X, float* __restrict__ Y, int B,
                                                           int C, int rows_per_chunk, const float* __restrict__ mean,
                                                           const float* __restrict__ invstd,
@@ -215,7 +245,7 @@ __global__ void __launch_bounds__(256) bn_act_fwd2_kernel(const float* __restric
                                                           float p_drop, const unsigned long long* __restrict__ rng,
                                                           unsigned stream_id, unsigned char* __restrict__ mask_out,
                                                           const unsigned char* __restrict__ mask_in,
-                                                          short* __restrict__ Y16) {
+                                                          short* __restrict__ Y16, HeadArgs head) {
   const int q = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 256 + q * 4;
   if (c >= C) return;
@@ -251,6 +281,10 @@ __global__ void __launch_bounds__(256) bn_act_fwd2_kernel(const float* __restric
     }
     *reinterpret_cast<f32x4*>(Y + i) = y;
     if (Y16) store4(Y16 + i, y);
+    if (HEAD) {
+      const f32x4 ww = *reinterpret_cast<const f32x4*>(head.w + c);
+      head_row(y[0] * ww[0] + y[1] * ww[1] + y[2] * ww[2] + y[3] * ww[3], r, q, head);
+    }
   }
 }
 
@@ -483,20 +517,34 @@ __global__ void bn_moments_finalize_kernel(const double* __restrict__ mom, doubl
 
 // Backward: chunk reduce of the three partial sums + the finalize of bn_bwd_finalize_kernel,
 // one wave per column (chunk_reduce_kernel's order).
-__global__ void bn_bwd_reduce_finalize_kernel(const double* __restrict__ part, int nchunk, int C, double ntot,
-                                              const float* __restrict__ invstd, float* coef, float* dgamma,
-                                              float* dbeta, float* dw) {
-  const int c = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (c >= C) return;
-  double r[3] = {0.0, 0.0, 0.0};
-#pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    for (int k = lane; k < nchunk; k += 64) r[q] += part[(size_t)k * 3 * C + q * C + c];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) r[q] += __shfl_xor(r[q], o, 64);
+// 64 columns per 1024-thread block: lanes run along the columns (coalesced rows of the partial
+// slab), the 16 waves stride over the chunks, then a fixed-order fold across the waves
+// (deterministic) and the finalize.
+__global__ void __launch_bounds__(1024) bn_bwd_reduce_finalize_kernel(const double* __restrict__ part, int nchunk,
+                                                                      int C, double ntot,
+                                                                      const float* __restrict__ invstd, float* coef,
+                                                                      float* dgamma, float* dbeta, float* dw) {
+  __shared__ double red[16][3][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  double r0 = 0.0, r1 = 0.0, r2 = 0.0;
+  if (c < C) {
+    for (int k = w; k < nchunk; k += 16) {
+      const double* pk = part + (size_t)k * 3 * C + c;
+      r0 += pk[0];
+      r1 += pk[C];
+      r2 += pk[2 * C];
+    }
   }
-  if (lane == 0) {
+  red[w][0][lane] = r0;
+  red[w][1][lane] = r1;
+  red[w][2][lane] = r2;
+  __syncthreads();
+  if (w == 0 && c < C) {
+    double r[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      for (int k = 0; k < 16; ++k) r[q] += red[k][q][lane];
     const float is = invstd[c];
     const float sdy = (float)r[0], dotp = (float)r[1];
     coef[c] = sdy / (float)ntot;
@@ -611,22 +659,7 @@ __global__ void head_fwd_kernel(const float* __restrict__ H, const float* __rest
     const f32x4 ww = *reinterpret_cast<const f32x4*>(w + c);
     s += h[0] * ww[0] + h[1] * ww[1] + h[2] * ww[2] + h[3] * ww[3];
   }
-  s = wave_sum(s);
-  if (lane == 0) {
-    const float o = s + bias[0];
-    const float pr = 1.f / (1.f + expf(-o));
-    if (logits) logits[row] = o;
-    if (probs) probs[row] = pr;
-    if (labels) {
-      const float t = labels[row];
-      const float lp = fmaxf(logf(pr), -100.f), l1p = fmaxf(logf(1.f - pr), -100.f);
-      if (loss_terms) loss_terms[row] = -(t * lp + (1.f - t) * l1p);
-      if (gout) {
-        const float gp = ((pr - t) / fmaxf((1.f - pr) * pr, 1e-12f)) / denom;
-        gout[row] = gp * (1.f - pr) * pr;
-      }
-    }
-  }
+  head_row(s, row, lane, HeadArgs{w, bias, logits, probs, labels, loss_terms, gout, denom});
 }
 
 // sigmoid backward only (drop-in mode: torch computes BCE and hands us dL/dp)
@@ -779,8 +812,26 @@ extern "C" int fbn_bn_act_fwd(const float* X, float* Y, int B, int C, const floa
   if (C & 3) { fbn_set_error("bn_act: C % 4"); return FBN_ERR_ARG; }
   if (p_drop > 0.f && !rng && !mask_in) { fbn_set_error("bn_act: dropout needs an rng state or a mask"); return FBN_ERR_ARG; }
   const int rpc = 16;
-  hipLaunchKernelGGL(bn_act_fwd2_kernel, dim3(fbn_cdiv(C, 256), fbn_cdiv(B, rpc)), dim3(256), 0, (hipStream_t)stream, X,
-                     Y, B, C, rpc, mean, invstd, g, b, p_drop, rng, stream_id, mask_out, mask_in, Y16);
+  hipLaunchKernelGGL(bn_act_fwd2_kernel<false>, dim3(fbn_cdiv(C, 256), fbn_cdiv(B, rpc)), dim3(256), 0,
+                     (hipStream_t)stream, X, Y, B, C, rpc, mean, invstd, g, b, p_drop, rng, stream_id, mask_out, mask_in,
+                     Y16, HeadArgs{});
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+// BN + ReLU + dropout of the last hidden layer (C = 256) fused with the head (fbn_head_fwd's outputs)
+extern "C" int fbn_bn_act_head_fwd(const float* X, float* Y, int B, int C, const float* mean, const float* invstd,
+                                   const float* g, const float* b, float p_drop, const unsigned long long* rng,
+                                   unsigned stream_id, unsigned char* mask_out, const unsigned char* mask_in,
+                                   const float* hw, const float* hbias, float* logits, float* probs,
+                                   const float* labels, float* loss_terms, float* gout, float denom, void* stream) {
+  if (B <= 0) return FBN_OK;
+  if (C != 256) { fbn_set_error("bn_act_head: the fused head needs C == 256"); return FBN_ERR_UNSUPPORTED; }
+  if (p_drop > 0.f && !rng && !mask_in) { fbn_set_error("bn_act: dropout needs an rng state or a mask"); return FBN_ERR_ARG; }
+  const int rpc = 16;
+  hipLaunchKernelGGL(bn_act_fwd2_kernel<true>, dim3(1, fbn_cdiv(B, rpc)), dim3(256), 0, (hipStream_t)stream, X, Y, B,
+                     C, rpc, mean, invstd, g, b, p_drop, rng, stream_id, mask_out, mask_in, nullptr,
+                     HeadArgs{hw, hbias, logits, probs, labels, loss_terms, gout, denom});
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -1005,7 +1056,7 @@ extern "C" int fbn_bn_bwd_fused(const float* G, const float* gvec, const float* 
   float* coef = (float*)((double*)ws + (size_t)nch * 3 * C + 3 * (size_t)C);
   hipLaunchKernelGGL(bn_bwd_partial4_kernel, dim3(fbn_cdiv(C, 256), nch), dim3(256), 0, st, s, Xpre, mean, B, C, rpc,
                      part);
-  hipLaunchKernelGGL(bn_bwd_reduce_finalize_kernel, dim3(fbn_cdiv(C, 4)), dim3(256), 0, st, part, nch, C, ntot, invstd,
+  hipLaunchKernelGGL(bn_bwd_reduce_finalize_kernel, dim3(fbn_cdiv(C, 64)), dim3(1024), 0, st, part, nch, C, ntot, invstd,
                      coef, dgamma, dbeta, dw);
   hipLaunchKernelGGL(bn_bwd_apply4_kernel, dim3(fbn_cdiv(C, 256), nch), dim3(256), 0, st, s, Xpre, mean, invstd, gamma,
                      coef, dXpre, dXpre16, B, C, rpc, colpart);

@@ -189,6 +189,34 @@ __device__ __forceinline__ float clip_from_slots(const double* sumsq, float max_
 
 // sumsq != null: the clip coefficient is computed here (every block, thread 0) and block 0
 // publishes it (coef_out, norm_out) for the table passes that follow -- no clip_coef launch.
+// dense Adam over elements [0, n) by `nblk` blocks (block index `bid`)
+__device__ __forceinline__ void adam_dense_body(float* __restrict__ p, const float* __restrict__ g,
+                                                float* __restrict__ m, float* __restrict__ v, long long n, float coef,
+                                                const AdamConsts& k, float wd, float b2, float omb2, float eps,
+                                                long long bid, long long nblk) {
+  const long long n4 = n / 4;
+  for (long long i = bid * blockDim.x + threadIdx.x; i < n4; i += nblk * blockDim.x) {
+    f32x4 pp = *reinterpret_cast<f32x4*>(p + 4 * i);
+    f32x4 mm = *reinterpret_cast<f32x4*>(m + 4 * i);
+    f32x4 vv = *reinterpret_cast<f32x4*>(v + 4 * i);
+    const f32x4 gg = *reinterpret_cast<const f32x4*>(g + 4 * i);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float pe = pp[e], me = mm[e], ve = vv[e];
+      adam_elem(pe, me, ve, gg[e], coef, wd, b2, omb2, eps, k);
+      pp[e] = pe; mm[e] = me; vv[e] = ve;
+    }
+    *reinterpret_cast<f32x4*>(p + 4 * i) = pp;
+    *reinterpret_cast<f32x4*>(m + 4 * i) = mm;
+    *reinterpret_cast<f32x4*>(v + 4 * i) = vv;
+  }
+  for (long long i = n4 * 4 + bid * blockDim.x + threadIdx.x; i < n; i += nblk * blockDim.x) {
+    float pp = p[i], mm = m[i], vv = v[i];
+    adam_elem(pp, mm, vv, g[i], coef, wd, b2, omb2, eps, k);
+    p[i] = pp; m[i] = mm; v[i] = vv;
+  }
+}
+
 __global__ void adam_dense_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                   float* __restrict__ v, long long n, const float* __restrict__ coef_ptr,
                                   const AdamConsts* __restrict__ table, const int* __restrict__ step_ptr, float wd,
@@ -211,27 +239,7 @@ __global__ void adam_dense_kernel(float* __restrict__ p, const float* __restrict
   } else {
     coef = coef_ptr ? *coef_ptr : 1.f;
   }
-  const long long n4 = n / 4;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
-    f32x4 pp = *reinterpret_cast<f32x4*>(p + 4 * i);
-    f32x4 mm = *reinterpret_cast<f32x4*>(m + 4 * i);
-    f32x4 vv = *reinterpret_cast<f32x4*>(v + 4 * i);
-    const f32x4 gg = *reinterpret_cast<const f32x4*>(g + 4 * i);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float pe = pp[e], me = mm[e], ve = vv[e];
-      adam_elem(pe, me, ve, gg[e], coef, wd, b2, omb2, eps, k);
-      pp[e] = pe; mm[e] = me; vv[e] = ve;
-    }
-    *reinterpret_cast<f32x4*>(p + 4 * i) = pp;
-    *reinterpret_cast<f32x4*>(m + 4 * i) = mm;
-    *reinterpret_cast<f32x4*>(v + 4 * i) = vv;
-  }
-  for (long long i = n4 * 4 + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    float pp = p[i], mm = m[i], vv = v[i];
-    adam_elem(pp, mm, vv, g[i], coef, wd, b2, omb2, eps, k);
-    p[i] = pp; m[i] = mm; v[i] = vv;
-  }
+  adam_dense_body(p, g, m, v, n, coef, k, wd, b2, omb2, eps, blockIdx.x, gridDim.x);
 }
 
 // ------------------------------------------------------------------ sparse table gradient
@@ -768,28 +776,21 @@ __global__ void __launch_bounds__(256) adam_touched_kernel(float* __restrict__ p
 // map[r] and slot_row[e] are reset; the step's vectors are copied into ring slot step % ring_n and
 // the clip coefficient into coef_hist[step].
 template <int D>
-__global__ void __launch_bounds__(256) adam_commit_kernel(float* __restrict__ p, float* __restrict__ m,
-                                                          float* __restrict__ v, int* __restrict__ map, GradSrc gs,
-                                                          int n, const float* __restrict__ coef_ptr,
-                                                          const AdamConsts* __restrict__ table,
-                                                          const int* __restrict__ step_ptr, float wd, float b2,
-                                                          float omb2, float eps, int* __restrict__ last, PendSrc ps,
-                                                          float* __restrict__ coef_hist, int B) {
+__device__ __forceinline__ void adam_commit_body(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
+                                                 int* __restrict__ map, const GradSrc& gs, int n, float coef,
+                                                 const AdamConsts& k, int t, float wd, float b2, float omb2, float eps,
+                                                 int* __restrict__ last, const PendSrc& ps, int B, long long bid,
+                                                 long long nblk) {
   constexpr int G = D / 4, RPW = 64 / G;
-  const int t = *step_ptr;
-  const AdamConsts k = table[t];
-  const float coef = coef_ptr ? *coef_ptr : 1.f;
-  if (blockIdx.x == 0 && threadIdx.x == 0) coef_hist[t] = coef;
   // ring copy of this step's per-sample vectors
   float* dst = const_cast<float*>(ps.ring) + (size_t)(t % ps.ring_n) * ps.ring_stride;
   const long long n4 = (long long)B * 2 * D / 4;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x)
+  for (long long i = bid * blockDim.x + threadIdx.x; i < n4; i += nblk * blockDim.x)
     reinterpret_cast<f32x4*>(dst)[i] = reinterpret_cast<const f32x4*>(gs.vec)[i];
   // one entry per lane: an unflagged claimer records its vector in pend; flagged claimers (rare)
   // are updated by the wave's G-lane groups afterwards
   const int lane = threadIdx.x & 63, q = lane % G;
-  for (long long e0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) - lane; e0 < n;
-       e0 += (long long)gridDim.x * blockDim.x) {
+  for (long long e0 = (bid * blockDim.x + threadIdx.x) - lane; e0 < n; e0 += nblk * blockDim.x) {
     const long long e = e0 + lane;
     const int sr = e < n ? gs.slot_row[e] : -1;
     const bool flag = sr != -1 && (sr & FBN_SLOT_FLAG);
@@ -837,6 +838,86 @@ __global__ void __launch_bounds__(256) adam_commit_kernel(float* __restrict__ p,
         gs.slot_row[ee] = -1;
       }
     }
+  }
+}
+
+// Single-GPU end of step with deferred table gradients: each claiming entry e (row r) either
+// records its gradient vector in pend[r] (no duplicates: the gradient is one per-sample vector),
+// or -- claimer of a row several entries hit (FLAG) -- applies the step now as adam_touched does.
+// map[r] and slot_row[e] are reset; the step's vectors are copied into ring slot step % ring_n and
+// the clip coefficient into coef_hist[step].
+template <int D>
+__global__ void __launch_bounds__(256) adam_commit_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                          float* __restrict__ v, int* __restrict__ map, GradSrc gs,
+                                                          int n, const float* __restrict__ coef_ptr,
+                                                          const AdamConsts* __restrict__ table,
+                                                          const int* __restrict__ step_ptr, float wd, float b2,
+                                                          float omb2, float eps, int* __restrict__ last, PendSrc ps,
+                                                          float* __restrict__ coef_hist, int B) {
+  const int t = *step_ptr;
+  const AdamConsts k = table[t];
+  const float coef = coef_ptr ? *coef_ptr : 1.f;
+  if (blockIdx.x == 0 && threadIdx.x == 0) coef_hist[t] = coef;
+  adam_commit_body<D>(p, m, v, map, gs, n, coef, k, t, wd, b2, omb2, eps, last, ps, B, blockIdx.x, gridDim.x);
+}
+
+// The whole single-GPU step tail in ONE launch (each kernel boundary costs a few microseconds):
+// blocks [0, ndense) run the dense Adam (clip coefficient from the norm slots, as adam_dense),
+// the rest the deferred-gradient commit; the last block to finish (ticket counter) advances the
+// step, the dropout offset and num_batches_tracked and clears the norm slots (fbn_step_end).
+struct StepEnd {
+  int* step;
+  unsigned long long* rng;
+  double* sumsq;
+  long long* nbt0;
+  long long* nbt1;
+  unsigned* ticket;   // zero at rest; the last block resets it
+};
+template <int D>
+__global__ void __launch_bounds__(256) adam_tail_kernel(float* __restrict__ dp, const float* __restrict__ dg,
+                                                        float* __restrict__ dm, float* __restrict__ dv,
+                                                        long long ndense_elems, int ndense, float max_norm,
+                                                        float* coef_out, float* norm_out, float* __restrict__ p,
+                                                        float* __restrict__ m, float* __restrict__ v,
+                                                        int* __restrict__ map, GradSrc gs, int n,
+                                                        const AdamConsts* __restrict__ table, float wd, float b2,
+                                                        float omb2, float eps, int* __restrict__ last, PendSrc ps,
+                                                        float* __restrict__ coef_hist, int B, StepEnd se) {
+  __shared__ float sc;
+  __shared__ unsigned is_last;
+  const int t = *se.step;
+  const AdamConsts k = table[t];
+  if (threadIdx.x == 0) {
+    float total;
+    sc = clip_from_slots(se.sumsq, max_norm, &total);
+    if (blockIdx.x == 0) {
+      if (coef_out) *coef_out = sc;
+      if (norm_out) *norm_out = total;
+      coef_hist[t] = sc;
+    }
+  }
+  __syncthreads();
+  const float coef = sc;
+  if ((int)blockIdx.x < ndense)
+    adam_dense_body(dp, dg, dm, dv, ndense_elems, coef, k, wd, b2, omb2, eps, blockIdx.x, ndense);
+  else
+    adam_commit_body<D>(p, m, v, map, gs, n, coef, k, t, wd, b2, omb2, eps, last, ps, B, blockIdx.x - ndense,
+                        gridDim.x - ndense);
+  // Every block consumed its reads of step and the norm slots (above) before it draws its ticket,
+  // and the last block publishes nothing another block of this launch reads: a relaxed ticket
+  // needs no release/acquire fences (an agent-scope release writes back the XCD's L2 -- in every
+  // block that costs tens of microseconds).  The next launch sees the stores at the kernel boundary.
+  __syncthreads();
+  if (threadIdx.x == 0)
+    is_last = __hip_atomic_fetch_add(se.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (is_last && threadIdx.x == 0) {
+    se.step[0] = t + 1;
+    if (se.rng) se.rng[1] += 1;
+    if (se.nbt0) se.nbt0[0] += 1;
+    if (se.nbt1) se.nbt1[0] += 1;
+    for (int i = 0; i < FBN_SUMSQ_SLOTS; ++i) se.sumsq[i] = 0.0;
+    *se.ticket = 0u;
   }
 }
 
@@ -1006,6 +1087,36 @@ extern "C" int fbn_adam_commit(float* p, float* m, float* v, int D, int* map, co
   if (blocks > 2048) blocks = 2048;
   FBN_DISPATCH_D(adam_commit_kernel, D, dim3(blocks), p, m, v, map, s, n, coef,
                  (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, last, ps, coef_hist, B);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+// single-GPU step tail: dense Adam (+ clip) + deferred-gradient commit + step end in one launch.
+// ticket: one device unsigned, zero before the first call (the kernel leaves it zero).
+extern "C" int fbn_adam_step_tail(float* dp, const float* dg, float* dm, float* dv, long long n_dense,
+                                  const double* sumsq, float max_norm, float* coef_out, float* norm_out, float* p,
+                                  float* m, float* v, int D, int* map, const float* gvec, float* extra, int* slot_row,
+                                  int Lp1, int n, const void* consts_table, int* step, float wd, float beta2, float eps,
+                                  int* last, int* pend, float* ring, float* coef_hist, int ring_n, int B,
+                                  unsigned long long* rng, long long* nbt0, long long* nbt1, unsigned* ticket,
+                                  void* stream) {
+  if (!pend || !ring || !coef_hist || !extra || !sumsq || !ticket || ring_n < 2 || Lp1 < 2) {
+    fbn_set_error("fbn_adam_step_tail: pend, ring, coef_hist, extra, sumsq and ticket are required");
+    return FBN_ERR_ARG;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const float omb2 = (float)(1.0 - (double)beta2);
+  GradSrc s{gvec, extra, slot_row, Lp1};
+  const PendSrc ps{pend, ring, coef_hist, (long long)B * 2 * D, ring_n};
+  const StepEnd se{step, rng, (double*)sumsq, nbt0, nbt1, ticket};
+  long long nd = (n_dense / 4 + 255) / 256;
+  if (nd > 512) nd = 512;
+  if (nd < 1) nd = 1;
+  long long nc = ((long long)(n > 0 ? n : 1) + 255) / 256;
+  if (nc > 2048) nc = 2048;
+  FBN_DISPATCH_D(adam_tail_kernel, D, dim3((unsigned)(nd + nc)), dp, dg, dm, dv, n_dense, (int)nd, max_norm, coef_out,
+                 norm_out, p, m, v, map, s, n, (const AdamConsts*)consts_table, wd, beta2, omb2, eps, last, ps,
+                 coef_hist, B, se);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

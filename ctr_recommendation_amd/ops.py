@@ -238,7 +238,7 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
             loss_denom: Optional[float] = None, coll: Collective = NO_COLLECTIVE, ntot: Optional[int] = None,
             masks_out: Optional[Dict[str, torch.Tensor]] = None, acts: Optional[Dict[str, torch.Tensor]] = None,
             probe: Optional[Dict[str, list]] = None, masks_in: Optional[Dict[str, torch.Tensor]] = None,
-            after_gather=None, count_batches: bool = True) -> Dict[str, torch.Tensor]:
+            after_gather=None, count_batches: bool = True, w16_ready: bool = False) -> Dict[str, torch.Tensor]:
     """Run the forward; returns the activation dict (probs, logits and what backward needs).
 
     p: parameter tensors keyed like the reference state_dict (fp32, contiguous, on device).
@@ -266,7 +266,8 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     Lr = 0 if seq is None else L
     x_mm = batch["item_emb_d128"]
     bf = cfg.bf16
-    w16 = bf16_weights(p, d, a, st, x=x_mm) if bf else None
+    # w16_ready: the caller already converted this step's bf16 images (a["w16"]) on another stream
+    w16 = (a["w16"] if w16_ready else bf16_weights(p, d, a, st, x=x_mm)) if bf else None
     a["w16"] = w16
     hmm = buf("hmm", (B, d))
     gemm(w16["x"] if bf else x_mm, w16["Wp"] if bf else p["mm_proj.0.weight"], hmm, B, d, 128, 128, 128, d, False,
@@ -371,13 +372,14 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     else:
         call("fbn_bn_eval_params", ptr(p["mlp.5.running_mean"]), ptr(p["mlp.5.running_var"]), ptr(mean2), ptr(inv2),
              H2, BN_EPS, st)
-    call("fbn_bn_act_fwd", ptr(h2pre), ptr(h2), B, H2, ptr(mean2), ptr(inv2), ptr(p["mlp.5.weight"]),
-         ptr(p["mlp.5.bias"]), float(p_drop), ptr(rng), 2, ptr(m2), ptr(mi2), None, st)
     logits, probs = buf("logits", (B,)), buf("probs", (B,))
     lt = buf("loss_terms", (B,)) if labels is not None else None
     go = buf("gout", (B,)) if labels is not None else None
-    call("fbn_head_fwd", ptr(h2), ptr(p["mlp.8.weight"]), ptr(p["mlp.8.bias"]), B, H2, ptr(logits), ptr(probs),
-         ptr(labels), ptr(lt), ptr(go), float(loss_denom if loss_denom is not None else ntot), st)
+    # BN2 + ReLU + dropout with the head Linear(256,1) + sigmoid + BCE in the same launch
+    call("fbn_bn_act_head_fwd", ptr(h2pre), ptr(h2), B, H2, ptr(mean2), ptr(inv2), ptr(p["mlp.5.weight"]),
+         ptr(p["mlp.5.bias"]), float(p_drop), ptr(rng), 2, ptr(m2), ptr(mi2), ptr(p["mlp.8.weight"]),
+         ptr(p["mlp.8.bias"]), ptr(logits), ptr(probs), ptr(labels), ptr(lt), ptr(go),
+         float(loss_denom if loss_denom is not None else ntot), st)
     if cfg.training and count_batches and "mlp.1.num_batches_tracked" in p:
         p["mlp.1.num_batches_tracked"].add_(1)
         p["mlp.5.num_batches_tracked"].add_(1)
@@ -509,8 +511,8 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     Lr = 0 if seq is None else L
     V = p["item_emb.weight"].shape[0] if pos is None else 0
     keys = ("senet.excitation.0.weight", "senet.excitation.0.bias", "senet.excitation.2.weight",
-            "senet.excitation.2.bias", "mm_proj.1.weight", "mm_proj.1.bias", "cate_emb.weight")
-    outs_arr = (ctypes.c_void_p * 7)(*[g[k].data_ptr() for k in keys])   # host array of device pointers
+            "senet.excitation.2.bias", "mm_proj.1.weight", "mm_proj.1.bias", "cate_emb.weight", "mm_proj.0.bias")
+    outs_arr = (ctypes.c_void_p * 8)(*[g[k].data_ptr() for k in keys])   # host array of device pointers
     outs = ctypes.cast(outs_arr, ctypes.c_void_p).value
     evb = None
     if probe is not None:                       # bench / tools: events around the fields backward
@@ -529,7 +531,6 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     else:
         wg.run(lambda s: gemm(dhmm, batch["item_emb_d128"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True,
                               False, stream=s))
-    sums.colsum(dhmm, B, d, d, g["mm_proj.0.bias"], st)
     for job in extra_sums:              # e.g. the trainer's mean loss
         sums.add(*job)
     sums.flush(st)

@@ -172,6 +172,7 @@ class FiBiNETTrainer:
             self.pend = torch.full((max(1, self.rows_local),), -1, **i32)
             self.ring = torch.zeros((self.ring_n, self.B, 2, d), dtype=torch.float32, device=dev)
             self.coef_hist = torch.ones(total_steps + 1, dtype=torch.float32, device=dev)
+            self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)     # fbn_adam_step_tail
         self.side = torch.cuda.Stream(device=dev)      # eager untouched pass / lazy rolling window
 
     # ------------------------------------------------------------------ one training step
@@ -228,6 +229,16 @@ class FiBiNETTrainer:
                  self.side.cuda_stream)
             _events_end(ev, self.side)
 
+        w16_ev = None
+        if cfg.bf16 and self.xchg is None:
+            # bf16 weight images (they depend only on the weights the previous step wrote) on the side
+            # stream, beside the row claims and the claimed-row catch-up
+            self.side.wait_stream(main)
+            with torch.cuda.stream(self.side):
+                self.acts["w16"] = ops.bf16_weights(self.p, d, self.acts, self.side.cuda_stream,
+                                                    x=batch["item_emb_d128"])
+            w16_ev = torch.cuda.Event()
+            w16_ev.record(self.side)
         if self.xchg is not None:
             rows = self.xchg.forward(batch["item_id"], seq, self.E, {"map": self.map, "slot_row": self.slot_row},
                                      self.err, before_gather=catch_up if lazy else None)
@@ -237,7 +248,10 @@ class FiBiNETTrainer:
                  ptr(self.slot_row), ptr(self.dup), st)
             if lazy:
                 catch_up(B * (L + 1))
+        if w16_ev is not None:
+            main.wait_event(w16_ev)
         a = ops.forward(self.p, batch, cfg, self.rng, table_rows=rows, pos=pos, err=self.err, labels=labels,
+                        w16_ready=w16_ev is not None,
                         loss_denom=float(ntot), coll=self.coll, ntot=ntot, acts=self.acts, masks_out=masks_out,
                         probe=probe, count_batches=False,     # num_batches_tracked: fbn_step_end
                         after_gather=None if lazy else start_untouched_adam)
@@ -273,29 +287,32 @@ class FiBiNETTrainer:
             self.coll.allreduce_(self.flat_g_ext[:o + 2])
             call("fbn_unpack_extras", ptr(self.flat_g_ext[o:]), ptr(self.loss), ptr(self.sumsq), st)
         call("fbn_sumsq", ptr(self.flat_g), self.n_dense, None, 0, ptr(self.sumsq), st)
-        # clip_grad_norm_(10) is applied inside the dense Adam launch (it publishes coef / norm)
-        call("fbn_adam_dense", ptr(self.flat_p), ptr(self.flat_g), ptr(self.flat_m), ptr(self.flat_v),
-             self.n_dense, None, ptr(self.sched), ptr(self.step_dev), self.wd, self.beta2, self.eps, ptr(self.sumsq),
-             self.max_norm, ptr(self.coef), ptr(self.norm), st)
         main.wait_stream(self.side)   # side-stream table pass done before map entries are reset
         if self.deferred:
-            # the step's table gradient is applied at each row's next replay (flagged rows: now);
-            # map and slot_row are reset in the same launch
-            ev = _events(probe, "adam_commit")
-            call("fbn_adam_commit", ptr(self.E), ptr(self.Em), ptr(self.Ev), d, ptr(self.map), ptr(gsrc[0]),
-                 ptr(gsrc[1]), ptr(self.slot_row), gsrc[2], n_ent, ptr(self.coef), ptr(self.sched),
-                 ptr(self.step_dev), self.wd, self.beta2, self.eps, ptr(self.last), ptr(self.pend), ptr(self.ring),
-                 ptr(self.coef_hist), self.ring_n, self.B, st)
+            # ONE launch: dense Adam with clip_grad_norm_(10), the table step (deferred to each row's
+            # next replay; rows with duplicates now), map/slot_row reset, step end
+            ev = _events(probe, "adam_tail")
+            call("fbn_adam_step_tail", ptr(self.flat_p), ptr(self.flat_g), ptr(self.flat_m), ptr(self.flat_v),
+                 self.n_dense, ptr(self.sumsq), self.max_norm, ptr(self.coef), ptr(self.norm), ptr(self.E),
+                 ptr(self.Em), ptr(self.Ev), d, ptr(self.map), ptr(gsrc[0]), ptr(gsrc[1]), ptr(self.slot_row), gsrc[2],
+                 n_ent, ptr(self.sched), ptr(self.step_dev), self.wd, self.beta2, self.eps, ptr(self.last),
+                 ptr(self.pend), ptr(self.ring), ptr(self.coef_hist), self.ring_n, self.B, ptr(self.rng),
+                 ptr(self.p["mlp.1.num_batches_tracked"]), ptr(self.p["mlp.5.num_batches_tracked"]), ptr(self.ticket),
+                 st)
             _events_end(ev)
         else:
+            # clip_grad_norm_(10) is applied inside the dense Adam launch (it publishes coef / norm)
+            call("fbn_adam_dense", ptr(self.flat_p), ptr(self.flat_g), ptr(self.flat_m), ptr(self.flat_v),
+                 self.n_dense, None, ptr(self.sched), ptr(self.step_dev), self.wd, self.beta2, self.eps,
+                 ptr(self.sumsq), self.max_norm, ptr(self.coef), ptr(self.norm), st)
             ev = _events(probe, "adam_touched")
             call("fbn_adam_touched", ptr(self.E), ptr(self.Em), ptr(self.Ev), d, ptr(self.map), ptr(gsrc[0]),
                  ptr(gsrc[1]), ptr(self.slot_row), gsrc[2], n_ent, ptr(self.coef), ptr(self.sched),
                  ptr(self.step_dev), self.wd, self.beta2, self.eps, ptr(self.last) if lazy else None, st)
             _events_end(ev)
             self.slot_row[:n_ent].fill_(-1)
-        call("fbn_step_end", ptr(self.step_dev), ptr(self.rng), ptr(self.sumsq), ptr(self.p["mlp.1.num_batches_tracked"]),
-             ptr(self.p["mlp.5.num_batches_tracked"]), st)
+            call("fbn_step_end", ptr(self.step_dev), ptr(self.rng), ptr(self.sumsq),
+                 ptr(self.p["mlp.1.num_batches_tracked"]), ptr(self.p["mlp.5.num_batches_tracked"]), st)
         self.host_step += 1
         return self.loss
 

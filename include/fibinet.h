@@ -82,8 +82,8 @@ int fbn_fields_fwd(const int64_t* item_id, const int64_t* item_seq, const int64_
  * (gvec == NULL, drop-in), two per-sample vectors gvec[B][2][D] = {dX3, dX5/count} (native
  * trainer: rows resolve through map/slot_row, see fbn_sparse_fixup), or one row per routed
  * entry into sendbuf at pos (multi-GPU).
- * param_grads: host array of 7 device pointers that receive the gradients of {senet W1, b1,
- * W2, b2, LN gamma, beta, cate table}; partials: [fbn_fields_bwd_grid(B,D)][P] scratch with
+ * param_grads: host array of 8 device pointers that receive the gradients of {senet W1, b1,
+ * W2, b2, LN gamma, beta, cate table, mm_proj bias (may be NULL)}; partials: [fbn_fields_bwd_grid(B,D)][P] scratch with
  * P = fbn_fields_bwd_partials_size. */
 int fbn_fields_bwd_partials_size(int D, int R, int n_cate);
 int fbn_fields_bwd_grid(int B, int D);
@@ -135,6 +135,12 @@ int fbn_bn_eval_params(const float* run_mean, const float* run_var, float* mean,
 int fbn_bn_act_fwd(const float* X, float* Y, int B, int C, const float* mean, const float* invstd, const float* g,
                    const float* b, float p_drop, const unsigned long long* rng, unsigned stream_id,
                    unsigned char* mask_out, const unsigned char* mask_in, short* Y16, void* stream);
+/* fbn_bn_act_fwd of the last hidden layer (C = 256) fused with fbn_head_fwd (same outputs). */
+int fbn_bn_act_head_fwd(const float* X, float* Y, int B, int C, const float* mean, const float* invstd, const float* g,
+                        const float* b, float p_drop, const unsigned long long* rng, unsigned stream_id,
+                        unsigned char* mask_out, const unsigned char* mask_in, const float* hw, const float* hbias,
+                        float* logits, float* probs, const float* labels, float* loss_terms, float* gout, float denom,
+                        void* stream);
 int fbn_bn_bwd_reduce(const float* G, const float* gvec, const float* w, const float* hact, float scale,
                       const float* Xpre, const float* mean, int B, int C, double* red_d, void* ws, void* stream);
 int fbn_bn_bwd_apply(const float* G, const float* gvec, const float* w, const float* hact, float scale,
@@ -235,6 +241,15 @@ int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, int D, const
 int fbn_adam_flush(float* p, float* m, float* v, long long nrows, int D, int* last, const void* consts_table,
                    const int* step, float wd, float beta2, float eps, int* pend, const float* ring,
                    const float* coef_hist, long long ring_stride, int ring_n, void* stream);
+/* Single-GPU step tail in ONE launch: fbn_adam_dense (clip from the sumsq slots) on the flat dense
+ * parameters + fbn_adam_commit on the table + fbn_step_end; ticket = one device unsigned, zero
+ * before the first call (the kernel's last block resets it). */
+int fbn_adam_step_tail(float* dp, const float* dg, float* dm, float* dv, long long n_dense, const double* sumsq,
+                       float max_norm, float* coef_out, float* norm_out, float* p, float* m, float* v, int D, int* map,
+                       const float* gvec, float* extra, int* slot_row, int Lp1, int n, const void* consts_table,
+                       int* step, float wd, float beta2, float eps, int* last, int* pend, float* ring,
+                       float* coef_hist, int ring_n, int B, unsigned long long* rng, long long* nbt0, long long* nbt1,
+                       unsigned* ticket, void* stream);
 /* Self-test of the packed exact zero-gradient Adam step of the lazy replay: n x 4 random operands
  * across the f32 range against the reference element step, bit for bit; mism[0] += mismatching
  * elements, mism[1] += elements on the fast path (device counters, caller zeroes). */

@@ -24,6 +24,7 @@ KERNELS = {
     "gemm_mlp0": ("gemm_dma16_kernel<64, 64, false, false", "262144", "max"),
     "adam_touched": ("adam_touched_kernel<128", None, None),
     "adam_commit": ("adam_commit_kernel<128", None, None),
+    "adam_tail": ("adam_tail_kernel<128", None, None),
 }
 
 
