@@ -31,7 +31,7 @@ def test_workspace_queries_are_host_only():
     h = _lib.lib()
     assert h.fbn_gemm_workspace_size(16384, 1024, 512, 1) == 0         # enough tiles: no split-K
     assert h.fbn_gemm_workspace_size(512, 1920, 8192, 1) > 0          # wgrad: split-K slabs
-    assert h.fbn_fields_bwd_partials_size(128, 3, 11) == 13 * 3 + 6 + 2 * 128 + 11 * 128
+    assert h.fbn_fields_bwd_partials_size(128, 3, 11) == 13 * 3 + 6 + 3 * 128 + 11 * 128   # + mm_proj bias partial row
     assert h.fbn_bn_workspace_size(8192, 512) > 0
 
 
