@@ -1,3 +1,4 @@
+#include <cstdlib>
 // K5 epilogue / K6 / K7: bilinear pair products, BatchNorm(+ReLU+dropout), sigmoid + BCE head.
 //
 // Bilinear "all" (model_fibinet.py:69-79): U_f = V_f W (an MFMA GEMM, gemm.hip), then
@@ -555,6 +556,48 @@ __global__ void __launch_bounds__(1024) bn_bwd_reduce_finalize_kernel(const doub
   }
 }
 
+// Same reduction on 16 columns per block (C / 16 workgroups instead of C / 64): 64 chunk streams
+// per column, 16 lanes reading one 128-B row segment of the slab; then 48 threads fold the 64
+// streams of one (quantity, column) in fixed order (deterministic) and 16 finalize.
+__global__ void __launch_bounds__(1024) bn_bwd_reduce_finalize16_kernel(const double* __restrict__ part, int nchunk,
+                                                                        int C, double ntot,
+                                                                        const float* __restrict__ invstd, float* coef,
+                                                                        float* dgamma, float* dbeta, float* dw) {
+  __shared__ double red[64][3][16];
+  __shared__ double tot[3][16];
+  const int col = threadIdx.x & 15, str = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + col;
+  double r0 = 0.0, r1 = 0.0, r2 = 0.0;
+  if (c < C) {
+    for (int k = str; k < nchunk; k += 64) {
+      const double* pk = part + (size_t)k * 3 * C + c;
+      r0 += pk[0];
+      r1 += pk[C];
+      r2 += pk[2 * C];
+    }
+  }
+  red[str][0][col] = r0;
+  red[str][1][col] = r1;
+  red[str][2][col] = r2;
+  __syncthreads();
+  if (threadIdx.x < 48) {
+    const int q = threadIdx.x >> 4, cc = threadIdx.x & 15;
+    double r = 0.0;
+    for (int k = 0; k < 64; ++k) r += red[k][q][cc];
+    tot[q][cc] = r;
+  }
+  __syncthreads();
+  if (threadIdx.x < 16 && c < C) {
+    const float is = invstd[c];
+    const float sdy = (float)tot[0][col], dotp = (float)tot[1][col];
+    coef[c] = sdy / (float)ntot;
+    coef[C + c] = dotp * is * is / (float)ntot;
+    if (dgamma) dgamma[c] = dotp * is;
+    if (dbeta) dbeta[c] = sdy;
+    if (dw) dw[c] = (float)tot[2][col];
+  }
+}
+
 // Vectorised apply (4 columns per thread, 256 columns x 4 row lanes per block, one row chunk
 // per blockIdx.y) with the column partial sums of dX (the pre-BN Linear's bias gradient) in
 // the same pass: colpart[chunk][c] (null: skipped).
@@ -1056,8 +1099,13 @@ extern "C" int fbn_bn_bwd_fused(const float* G, const float* gvec, const float* 
   float* coef = (float*)((double*)ws + (size_t)nch * 3 * C + 3 * (size_t)C);
   hipLaunchKernelGGL(bn_bwd_partial4_kernel, dim3(fbn_cdiv(C, 256), nch), dim3(256), 0, st, s, Xpre, mean, B, C, rpc,
                      part);
-  hipLaunchKernelGGL(bn_bwd_reduce_finalize_kernel, dim3(fbn_cdiv(C, 64)), dim3(1024), 0, st, part, nch, C, ntot, invstd,
-                     coef, dgamma, dbeta, dw);
+  static const bool wide = !getenv("FBN_BN_REDUCE64");   // A/B knob: 64 columns per workgroup
+  if (wide)
+    hipLaunchKernelGGL(bn_bwd_reduce_finalize16_kernel, dim3(fbn_cdiv(C, 16)), dim3(1024), 0, st, part, nch, C, ntot,
+                       invstd, coef, dgamma, dbeta, dw);
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce_finalize_kernel, dim3(fbn_cdiv(C, 64)), dim3(1024), 0, st, part, nch, C, ntot,
+                       invstd, coef, dgamma, dbeta, dw);
   hipLaunchKernelGGL(bn_bwd_apply4_kernel, dim3(fbn_cdiv(C, 256), nch), dim3(256), 0, st, s, Xpre, mean, invstd, gamma,
                      coef, dXpre, dXpre16, B, C, rpc, colpart);
   FBN_CHECK_LAUNCH();
