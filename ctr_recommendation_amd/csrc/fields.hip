@@ -1,3 +1,4 @@
+#include <cstdlib>
 // K1 / K2 / K4: FiBiNET field construction, SENET and the embedding scatter-add gradient.
 //
 // Forward (one "sample group" of D/4 lanes per sample, each lane owning 4 contiguous
@@ -534,6 +535,27 @@ __global__ void __launch_bounds__(1024) reduce_partials_one(const float* __restr
   }
 }
 
+// Same reduction on 16 columns per block (P / 16 workgroups): 64 partial-row streams per column,
+// 16 lanes reading one 64-B segment, then a fixed-order fold over the 64 streams (deterministic).
+__global__ void __launch_bounds__(1024) reduce_partials_one16(const float* __restrict__ part, int nblk, int P, GradOuts o) {
+  __shared__ float red[64][16];
+  const int col = threadIdx.x & 15, str = threadIdx.x >> 4;
+  const int i = blockIdx.x * 16 + col;
+  float s = 0.f;
+  if (i < P)
+    for (int r = str; r < nblk; r += 64) s += part[(size_t)r * P + i];
+  red[str][col] = s;
+  __syncthreads();
+  if (threadIdx.x < 16 && i < P) {
+    float t = 0.f;
+    for (int k = 0; k < 64; ++k) t += red[k][col];
+    int seg = 0;
+#pragma unroll
+    for (int j = 1; j < 8; ++j) seg += (i >= o.off[j]) ? 1 : 0;
+    if (o.p[seg]) o.p[seg][i - o.off[seg]] = t;
+  }
+}
+
 
 // ------------------------------------------------------------------------------ C ABI
 #ifndef FBN_FB_MAXBLK
@@ -647,7 +669,12 @@ extern "C" int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, c
     o.p[j] = param_grads[j];   // [7] (mm_proj bias) may be null: not written
     o.off[j + 1] = o.off[j] + sizes[j];
   }
-  hipLaunchKernelGGL(reduce_partials_one, dim3(fbn_cdiv(P, 64)), dim3(1024), 0, st, (const float*)partials, nblk, P, o);
+  static const bool narrow = getenv("FBN_PARTIALS64") != nullptr;   // A/B knob: 64 columns per workgroup
+  if (narrow)
+    hipLaunchKernelGGL(reduce_partials_one, dim3(fbn_cdiv(P, 64)), dim3(1024), 0, st, (const float*)partials, nblk, P, o);
+  else
+    hipLaunchKernelGGL(reduce_partials_one16, dim3(fbn_cdiv(P, 16)), dim3(1024), 0, st, (const float*)partials, nblk, P,
+                       o);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
