@@ -79,12 +79,12 @@ SIGNATURES = {
     "fbn_adam_flush": (I, [P, P, P, LL, I, P, P, P, F, F, F, P, P, P, LL, I, P]),
     "fbn_adam_selftest": (I, [I, ctypes.c_uint, P, P]),
     "fbn_adam_step_tail": (I, [P, P, P, P, LL, P, F, P, P, P, P, P, I, P, P, P, P, I, I, P, P, F, F, F, P, P, P, P, I, I,
-                               P, P, P, P, P]),
+                               P, P, P, P, I, P, P]),
     "fbn_adam_commit": (I, [P, P, P, I, P, P, P, P, I, I, P, P, P, F, F, F, P, P, P, P, I, I, P]),
     "fbn_claim_rows": (I, [P, P, I, I, LL, P, P, P, P]),
     "fbn_pack_extras": (I, [P, P, P, P]),
     "fbn_unpack_extras": (I, [P, P, P, P]),
-    "fbn_step_end": (I, [P, P, P, P, P, P]),
+    "fbn_step_end": (I, [P, P, P, P, P, I, P, P]),
     "fbn_route": (I, [P, P, I, I, LL, LL, I, P, P, P, P, P, P, P]),
     "fbn_owner_claim": (I, [P, I, P, P, I, P]),
     "fbn_owner_gather": (I, [P, I, P, P, P, P, I, I, P]),

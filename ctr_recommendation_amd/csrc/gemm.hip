@@ -242,11 +242,14 @@ template <int ROWS, int BK, bool KC, bool MAP> struct OpLoader<ROWS, BK, KC, MAP
 };
 
 // Shared epilogue: bias / beta / remapped C stores or split-K slabs, and the optional fused
-// BatchNorm statistics.  red: LDS scratch of >= 2*BN floats, free (all waves past the main loop).
-template <int BM, int BN, int TM, int TN>
+// BatchNorm statistics.  Waves form a WGM x WGN grid over the tile (wave (wm, wn) owns rows
+// wm*BM/WGM.. and columns wn*BN/WGN..).  Statistics are per 64-row tile of C: a wave's rows lie
+// in one such tile (BM/WGM divides 64).  red: LDS scratch of >= WGM*BN floats, free (all waves
+// past the main loop).
+template <int BM, int BN, int WGM, int WGN, int TM, int TN>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[TM][TN], int m0, int n0, int wm,
                                               int wn, int lr, int lh, float* red) {
-  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
   // C/D map of the 32x32 MFMA tile: col = lane&31, row = (e&3) + 8*(e>>2) + 4*(lane>>5)
   const bool split = gridDim.z > 1;
 #pragma unroll
@@ -272,9 +275,12 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[T
       }
     }
   if (g.stats && !split) {
-    // BatchNorm fusion: exact two-pass (sum, M2) of this tile's column values from registers;
-    // the BN finalize merges tiles in f64 (Chan) -- no extra pass over C.
-    const int rows = min(BM, g.M - m0);
+    // BatchNorm fusion: exact two-pass (sum, M2) of each 64-row tile's column values from
+    // registers; the BN finalize merges tiles in f64 (Chan) -- no extra pass over C.
+    static_assert(64 % WM == 0, "a wave's rows must lie in one 64-row statistics tile");
+    constexpr int WPG = 64 / WM;                      // waves (along M) per statistics tile
+    const int grp = (wm * WM) / 64;                   // this wave's statistics tile inside the block
+    const int rows = min(64, g.M - (m0 + grp * 64));
     float bvj[TN], mean[TN], ps[TN], sum0[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -307,12 +313,14 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[T
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int c = wn * WN + j * 32 + lr;
-        const float tot = red[c] + red[BN + c];
+        float tot = 0.f;
+#pragma unroll
+        for (int k = 0; k < WPG; ++k) tot += red[(grp * WPG + k) * BN + c];
         if (pass == 0) {
           sum0[j] = tot;
-          mean[j] = tot / (float)rows;
-        } else if (wm == 0 && lh == 0 && n0 + c < g.N) {
-          float* o = g.stats + ((size_t)(m0 / BM) * g.N + n0 + c) * 2;
+          mean[j] = rows > 0 ? tot / (float)rows : 0.f;
+        } else if (wm % WPG == 0 && lh == 0 && n0 + c < g.N && rows > 0) {
+          float* o = g.stats + ((size_t)(m0 / 64 + grp) * g.N + n0 + c) * 2;
           o[0] = sum0[j];
           o[1] = tot;
         }
@@ -419,7 +427,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
     __syncthreads();
   }
 
-  gemm_epilogue<BM, BN>(g, acc, m0, n0, wm, wn, lr, lh, reinterpret_cast<float*>(&sA[0][0]));
+  gemm_epilogue<BM, BN, 2, 2>(g, acc, m0, n0, wm, wn, lr, lh, reinterpret_cast<float*>(&sA[0][0]));
 }
 
 __global__ void gemm_splitk_reduce(GemmArgs g, int nsplit) {
@@ -494,19 +502,32 @@ __device__ __forceinline__ void wait_dma(int ahead) {   // ahead = stages allowe
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int BM, int BN, bool AKM, bool BKM, int S>
-__global__ void __launch_bounds__(256) gemm_dma16_kernel(GemmArgs g, int tiles_n, int remap_xcd) {
+// XCD-aware, bijective block -> tile order: blocks b and b+8 share an XCD (round-robin
+// dispatch); give each XCD a contiguous run of tile ids so neighbouring tiles (which share an A
+// row panel) hit one L2.  Bijective for any grid size (remainder blocks spread over the first
+// nb % 8 XCD slots).
+__device__ __forceinline__ int xcd_tile(int bid, int nb) {
+  const int q = nb / 8, r = nb % 8, x = bid % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
+// WGM x WGN waves (64 * WGM * WGN threads); wave (wm, wn) owns a (BM/WGM) x (BN/WGN) sub-tile
+// of 32x32 MFMA blocks.  8 waves on a 128x128 tile: two waves per SIMD, each with 2 MFMAs per
+// 3 fragment reads (4 waves on 64x64 tiles: 1 MFMA per 2 reads).
+template <int BM, int BN, bool AKM, bool BKM, int S, int WGM = 2, int WGN = 2>
+__global__ void __launch_bounds__(64 * WGM * WGN) gemm_dma16_kernel(GemmArgs g, int tiles_n, int remap_xcd) {
+  constexpr int NW = WGM * WGN;
   constexpr int BK = 64;
-  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
+  constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 32, TN = WN / 32;
   constexpr int AB = BM * BK * 2, STAGE = (BM + BN) * BK * 2;   // A image bytes, stage bytes
-  constexpr int GPW = (BM + BN) / 8 / 4;                          // 1-KiB DMA groups per wave per stage
-  static_assert(((BM + BN) / 8) % 4 == 0 && BM % 16 == 0, "tile / wave mismatch");
+  constexpr int GPW = (BM + BN) / 8 / NW;                         // 1-KiB DMA groups per wave per stage
+  static_assert(((BM + BN) / 8) % NW == 0 && BM % 16 == 0 && WM % 32 == 0 && WN % 32 == 0, "tile / wave mismatch");
   static_assert(S >= 2 && S <= 4, "stages");
   __shared__ __attribute__((aligned(1024))) char smem[S * STAGE];
 
   int bid = blockIdx.x;
   const int nb = gridDim.x;
-  if (remap_xcd) bid = (bid % 8) * (nb / 8) + bid / 8;
+  if (remap_xcd) bid = xcd_tile(bid, nb);
   const int tm = bid / tiles_n, tn = bid % tiles_n;
   const int n0 = tn * BN, m0 = tm * BM;
   const int kbeg = blockIdx.z * g.kchunk;
@@ -514,7 +535,7 @@ __global__ void __launch_bounds__(256) gemm_dma16_kernel(GemmArgs g, int tiles_n
   const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wm = wave & 1, wn = wave >> 1;
+  const int wm = wave % WGM, wn = wave / WGM;
   const int lr = lane & 31, lh = lane >> 5;
 
   // this lane's source for each of its wave's DMA groups, and the per-stage source advance
@@ -613,7 +634,7 @@ __global__ void __launch_bounds__(256) gemm_dma16_kernel(GemmArgs g, int tiles_n
     }
   }
   __syncthreads();   // the stats epilogue reuses the staging LDS
-  gemm_epilogue<BM, BN>(g, acc, m0, n0, wm, wn, lr, lh, reinterpret_cast<float*>(smem));
+  gemm_epilogue<BM, BN, WGM, WGN>(g, acc, m0, n0, wm, wn, lr, lh, reinterpret_cast<float*>(smem));
 }
 
 // vectorised split-K reduce: 4 consecutive columns per thread (N, ldc and the C remap in
@@ -718,6 +739,8 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_stats(GemmArgs g, int 
 // ------------------------------------------------------------------ host-side planning
 struct GemmPlan {
   int bm, bn, split;
+  int waves = 4;   // LDS-DMA kernel: 4 (2x2) or 8 (2 along M x 4 along N)
+  int stages = 0;  // LDS-DMA ring depth (0 = FBN_DMA_STAGES)
 };
 
 static GemmPlan plan_gemm(int M, int N, int K, int bk) {
@@ -766,27 +789,35 @@ static void launch_tile(const GemmArgs& g, int nsplit, hipStream_t st) {
                      (nb % 8 == 0) ? 1 : 0);
 }
 
-template <int BM, int BN, bool AKM, bool BKM>
-static void launch_dma16(const GemmArgs& g, int nsplit, hipStream_t st) {
+template <int BM, int BN, bool AKM, bool BKM, int WGM, int WGN>
+static void launch_dma16(const GemmArgs& g, const GemmPlan& p, hipStream_t st) {
   const int tn = fbn_cdiv(g.N, BN), tm = fbn_cdiv(g.M, BM);
   const int nb = tn * tm;
-  const int rx = (nb % 8 == 0) ? 1 : 0;
+  const int rx = nb >= 8 ? 1 : 0;
   const char* e = getenv("FBN_GEMM_STAGES");   // tuning knob
-  const int S = e ? atoi(e) : FBN_DMA_STAGES;
+  const int S = e ? atoi(e) : (p.stages ? p.stages : FBN_DMA_STAGES);
+  const dim3 grid(nb, 1, p.split), blk(64 * WGM * WGN);
   if (S <= 2)
-    hipLaunchKernelGGL((gemm_dma16_kernel<BM, BN, AKM, BKM, 2>), dim3(nb, 1, nsplit), dim3(256), 0, st, g, tn, rx);
+    hipLaunchKernelGGL((gemm_dma16_kernel<BM, BN, AKM, BKM, 2, WGM, WGN>), grid, blk, 0, st, g, tn, rx);
   else if (S == 3)
-    hipLaunchKernelGGL((gemm_dma16_kernel<BM, BN, AKM, BKM, 3>), dim3(nb, 1, nsplit), dim3(256), 0, st, g, tn, rx);
+    hipLaunchKernelGGL((gemm_dma16_kernel<BM, BN, AKM, BKM, 3, WGM, WGN>), grid, blk, 0, st, g, tn, rx);
   else
-    hipLaunchKernelGGL((gemm_dma16_kernel<BM, BN, AKM, BKM, 4>), dim3(nb, 1, nsplit), dim3(256), 0, st, g, tn, rx);
+    hipLaunchKernelGGL((gemm_dma16_kernel<BM, BN, AKM, BKM, 4, WGM, WGN>), grid, blk, 0, st, g, tn, rx);
 }
 
 template <bool AKM, bool BKM>
 static void launch_dma16_sel(const GemmArgs& g, const GemmPlan& p, hipStream_t st) {
-  if (p.bm == 128 && p.bn == 128) launch_dma16<128, 128, AKM, BKM>(g, p.split, st);
-  else if (p.bm == 128) launch_dma16<128, 64, AKM, BKM>(g, p.split, st);
-  else if (p.bn == 128) launch_dma16<64, 128, AKM, BKM>(g, p.split, st);
-  else launch_dma16<64, 64, AKM, BKM>(g, p.split, st);
+  if (p.waves == 8) {
+    if (p.bm == 128 && p.bn == 128) launch_dma16<128, 128, AKM, BKM, 2, 4>(g, p, st);
+    else if (p.bm == 128) launch_dma16<128, 64, AKM, BKM, 4, 2>(g, p, st);
+    else if (p.bn == 128) launch_dma16<64, 128, AKM, BKM, 2, 4>(g, p, st);
+    else launch_dma16<64, 64, AKM, BKM, 2, 2>(g, p, st);
+    return;
+  }
+  if (p.bm == 128 && p.bn == 128) launch_dma16<128, 128, AKM, BKM, 2, 2>(g, p, st);
+  else if (p.bm == 128) launch_dma16<128, 64, AKM, BKM, 2, 2>(g, p, st);
+  else if (p.bn == 128) launch_dma16<64, 128, AKM, BKM, 2, 2>(g, p, st);
+  else launch_dma16<64, 64, AKM, BKM, 2, 2>(g, p, st);
 }
 
 template <bool TA, bool TB, bool BF16, bool A16, bool B16>
@@ -885,17 +916,18 @@ static int gemm_impl(const void* A, const void* B, float* C, const float* bias, 
     return FBN_ERR_ARG;
   }
   GemmPlan p = dma16 ? plan_dma16(M, N, K) : plan_gemm(M, N, K, bk);
-  if (const char* f = getenv("FBN_GEMM_FORCE")) {      // tuning sweeps only: "bm,bn,split"
-    int a = 0, b = 0, c = 0;
-    if (sscanf(f, "%d,%d,%d", &a, &b, &c) == 3) p = {a, b, c};
+  if (const char* f = getenv("FBN_GEMM_FORCE")) {      // tuning sweeps only: "bm,bn,split[,waves[,stages]]"
+    int a = 0, b = 0, c = 0, w = 4, sg = 0;
+    if (sscanf(f, "%d,%d,%d,%d,%d", &a, &b, &c, &w, &sg) >= 3) p = {a, b, c, w, sg};
   }
   g.stats = stats;
   if (p.split > 1 && (!ws || ws_bytes < (size_t)p.split * M * N * sizeof(float))) p.split = 1;
   int per = fbn_cdiv(K, p.split);
   per = fbn_cdiv(per, bk) * bk;
   p.split = K > 0 ? fbn_cdiv(K, per) : 1;
-  // stats: 64-row tiles from the MFMA epilogue (split == 1) or from the split-K reduce
-  if (stats && p.split == 1) p.bm = 64;
+  // stats: 64-row tiles from the MFMA epilogue (split == 1; a wave's rows inside one 64-row
+  // tile) or from the split-K reduce
+  if (stats && p.split == 1 && !(dma16 && p.waves == 8 && p.bm == 128)) p.bm = 64;
   g.kchunk = K > 0 ? per : 0;
   g.ws = ws;
   hipStream_t st = (hipStream_t)stream;

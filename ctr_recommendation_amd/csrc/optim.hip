@@ -872,6 +872,8 @@ struct StepEnd {
   long long* nbt0;
   long long* nbt1;
   unsigned* ticket;   // zero at rest; the last block resets it
+  int max_step;       // total_steps: the counter saturates there (schedule table / coef_hist bounds)
+  int* err;           // bit 2 set on a step past max_step (graph replays cannot raise on the host)
 };
 template <int D>
 __global__ void __launch_bounds__(256) adam_tail_kernel(float* __restrict__ dp, const float* __restrict__ dg,
@@ -912,7 +914,8 @@ __global__ void __launch_bounds__(256) adam_tail_kernel(float* __restrict__ dp, 
     is_last = __hip_atomic_fetch_add(se.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();
   if (is_last && threadIdx.x == 0) {
-    se.step[0] = t + 1;
+    if (t + 1 <= se.max_step) se.step[0] = t + 1;
+    else if (se.err) atomicOr(se.err, 2);
     if (se.rng) se.rng[1] += 1;
     if (se.nbt0) se.nbt0[0] += 1;
     if (se.nbt1) se.nbt1[0] += 1;
@@ -922,8 +925,10 @@ __global__ void __launch_bounds__(256) adam_tail_kernel(float* __restrict__ dp, 
 }
 
 // end of step: advance Adam step + dropout RNG offset, clear the norm accumulator
-__global__ void step_end_kernel(int* step, unsigned long long* rng, double* sumsq, long long* nbt0, long long* nbt1) {
-  step[0] += 1;
+__global__ void step_end_kernel(int* step, unsigned long long* rng, double* sumsq, long long* nbt0, long long* nbt1,
+                                int max_step, int* err) {
+  if (step[0] + 1 <= max_step) step[0] += 1;
+  else if (err) atomicOr(err, 2);   // past total_steps: the counter saturates (table bounds), flag it
   if (rng) rng[1] += 1;
   if (nbt0) nbt0[0] += 1;   // BatchNorm num_batches_tracked
   if (nbt1) nbt1[0] += 1;
@@ -1099,7 +1104,7 @@ extern "C" int fbn_adam_step_tail(float* dp, const float* dg, float* dm, float* 
                                   int Lp1, int n, const void* consts_table, int* step, float wd, float beta2, float eps,
                                   int* last, int* pend, float* ring, float* coef_hist, int ring_n, int B,
                                   unsigned long long* rng, long long* nbt0, long long* nbt1, unsigned* ticket,
-                                  void* stream) {
+                                  int max_step, int* err, void* stream) {
   if (!pend || !ring || !coef_hist || !extra || !sumsq || !ticket || ring_n < 2 || Lp1 < 2) {
     fbn_set_error("fbn_adam_step_tail: pend, ring, coef_hist, extra, sumsq and ticket are required");
     return FBN_ERR_ARG;
@@ -1108,7 +1113,7 @@ extern "C" int fbn_adam_step_tail(float* dp, const float* dg, float* dm, float* 
   const float omb2 = (float)(1.0 - (double)beta2);
   GradSrc s{gvec, extra, slot_row, Lp1};
   const PendSrc ps{pend, ring, coef_hist, (long long)B * 2 * D, ring_n};
-  const StepEnd se{step, rng, (double*)sumsq, nbt0, nbt1, ticket};
+  const StepEnd se{step, rng, (double*)sumsq, nbt0, nbt1, ticket, max_step, err};
   long long nd = (n_dense / 4 + 255) / 256;
   if (nd > 512) nd = 512;
   if (nd < 1) nd = 1;
@@ -1134,8 +1139,9 @@ extern "C" int fbn_claim_rows(const int64_t* item, const int64_t* seq, int B, in
 }
 
 extern "C" int fbn_step_end(int* step, unsigned long long* rng, double* sumsq, long long* nbt0, long long* nbt1,
-                            void* stream) {
-  hipLaunchKernelGGL(step_end_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step, rng, sumsq, nbt0, nbt1);
+                            int max_step, int* err, void* stream) {
+  hipLaunchKernelGGL(step_end_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step, rng, sumsq, nbt0, nbt1,
+                     max_step, err);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

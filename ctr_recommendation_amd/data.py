@@ -21,7 +21,10 @@ import torch
 
 
 def make_batch_np(rng: np.random.Generator, B: int, V: int, L: int = 20, n_cate: int = 11,
-                  zipf: float = 0.0) -> Tuple[Dict[str, np.ndarray], np.ndarray]:
+                  zipf: float = 0.0, signal: str = "hash") -> Tuple[Dict[str, np.ndarray], np.ndarray]:
+    """signal "hash": the planted score of SURVEY §8(d); "fields": a score a few training steps
+    can learn (the cate levels and the mm vector carry it) -- for AUC-parity tests, where an
+    AUC near 0.5 would say nothing."""
     if zipf > 0:
         item = (rng.zipf(1.0 + zipf, size=B) % (V - 1)) + 1
     else:
@@ -35,7 +38,10 @@ def make_batch_np(rng: np.random.Generator, B: int, V: int, L: int = 20, n_cate:
     user = rng.integers(1, 20000, size=B)
     mm = rng.standard_normal((B, 128)).astype(np.float32)
     mm /= np.linalg.norm(mm, axis=1, keepdims=True)
-    score = (((item % 97) * 7 + likes * 3 - views * 2) % 11 - 5) / 2.5 + 2.0 * mm[:, 0]
+    if signal == "fields":
+        score = (likes - 5) / 1.5 - (views - 5) / 2.5 + 12.0 * mm[:, 0]
+    else:
+        score = (((item % 97) * 7 + likes * 3 - views * 2) % 11 - 5) / 2.5 + 2.0 * mm[:, 0]
     label = (rng.random(B) < 1.0 / (1.0 + np.exp(-score))).astype(np.float32)
     batch = {
         "item_id": item.astype(np.int64),
@@ -53,9 +59,9 @@ def to_torch(batch: Dict[str, np.ndarray], label: np.ndarray, device="cpu"):
         torch.from_numpy(label).to(device)
 
 
-def make_batch(seed: int, B: int, V: int, L: int = 20, device="cpu", zipf: float = 0.0):
+def make_batch(seed: int, B: int, V: int, L: int = 20, device="cpu", zipf: float = 0.0, signal: str = "hash"):
     rng = np.random.default_rng(seed)
-    b, y = make_batch_np(rng, B, V, L, zipf=zipf)
+    b, y = make_batch_np(rng, B, V, L, zipf=zipf, signal=signal)
     return to_torch(b, y, device)
 
 

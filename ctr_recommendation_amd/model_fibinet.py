@@ -22,6 +22,7 @@ operands and fp32 accumulation (config C3).
 """
 from __future__ import annotations
 
+import functools
 from typing import Dict, List, Tuple
 
 import torch
@@ -135,12 +136,15 @@ class MM_FiBiNET(nn.Module):
             nn.Linear(256, 1))
         self.sigmoid = nn.Sigmoid()
         self._param_names = [n for n, _ in self.named_parameters()]
-        self._rng = None
+        # dropout streams, one per device.  The dict object is shared by nn.DataParallel replicas
+        # (replicate() copies __dict__ shallowly), so each device's counter advances across steps
+        # although the replicas themselves are rebuilt every forward (train_fibinet.py:69-70)
+        self._rngs: Dict[int, torch.Tensor] = {}
         self._strict_ids = True
 
     # ---------------------------------------------------------------- helpers
     def _buffers_dict(self) -> Dict[str, torch.Tensor]:
-        return {n: b for n, b in self.named_buffers()}
+        return {n: b for n, b in self.named_buffers()}     # replicas keep their buffers registered
 
     def _fwd_cfg(self) -> ops.FwdConfig:
         return ops.FwdConfig(d=self.emb_dim, L=0, training=self.training, p_drop=self.dropout_p,
@@ -148,10 +152,24 @@ class MM_FiBiNET(nn.Module):
                              R=self.senet.excitation[0].out_features)
 
     def _rng_state(self, device) -> torch.Tensor:
-        if self._rng is None or self._rng.device != device:
-            seed = torch.initial_seed() & 0xFFFFFFFFFFFF   # does not advance torch's RNG stream
-            self._rng = torch.tensor([seed, 0], dtype=torch.int64, device=device)
-        return self._rng
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        rng = self._rngs.get(idx)
+        if rng is None:
+            # does not advance torch's RNG stream; an independent stream per device
+            seed = (torch.initial_seed() + idx * 0x9E3779B9) & 0xFFFFFFFFFFFF
+            rng = torch.tensor([seed, 0], dtype=torch.int64, device=device)
+            self._rngs[idx] = rng
+        return rng
+
+    def _param_tensors(self) -> List[torch.Tensor]:
+        """The parameters in ``_param_names`` order, resolved by attribute.  On an nn.DataParallel
+        replica ``named_parameters()`` is empty: replicate() sets the broadcast copies as plain
+        attributes (non-leaf tensors whose grads flow back to the originals), which this finds."""
+        out = []
+        for n in self._param_names:
+            t = functools.reduce(getattr, n.split("."), self)
+            out.append(t if t.is_contiguous() else t.contiguous())
+        return out
 
     def _check_ids(self, err: torch.Tensor) -> None:
         # the reference raises IndexError on an out-of-range id (nn.Embedding); the kernels set a
@@ -173,8 +191,7 @@ class MM_FiBiNET(nn.Module):
         seq = batch_dict.get("item_seq", None)
         if seq is not None:
             batch["item_seq"] = seq.long().contiguous()
-        params = [p if p.is_contiguous() else p.contiguous() for _, p in self.named_parameters()]
-        return _FiBiNETFn.apply(self, batch, *params)
+        return _FiBiNETFn.apply(self, batch, *self._param_tensors())
 
 
 def build_model(feature_map, model_cfg):

@@ -64,14 +64,16 @@ class FiBiNETTrainer:
                  lr: Optional[float] = None, weight_decay: Optional[float] = None, rank: int = 0, world: int = 1,
                  group=None, init_state: Optional[Dict[str, torch.Tensor]] = None, seed: int = 2025,
                  stage_on_cpu: bool = False, dropout_seed: Optional[int] = None, table_adam: str = "lazy",
-                 lazy_window: int = 128, defer_table_grads: bool = True):
+                 lazy_window: int = 128, defer_table_grads: bool = True, max_norm: float = 10.0):
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise RuntimeError("FiBiNETTrainer runs on a HIP device only (no CPU fallback)")
         self.cfg = dict(model_cfg)
         self.lr = float(lr if lr is not None else model_cfg.get("learning_rate", 1e-3))
         self.wd = float(weight_decay if weight_decay is not None else model_cfg.get("weight_decay", 1e-5))
-        self.beta2, self.eps, self.max_norm = 0.999, 1e-8, 10.0
+        # clip_grad_norm_(model.parameters(), max_norm=10.0) (train_fibinet.py:119); settable so
+        # tests can make the clip engage
+        self.beta2, self.eps, self.max_norm = 0.999, 1e-8, float(max_norm)
         self.rank, self.world, self.group = rank, world, group
         self.B = batch_size                     # per-rank batch
         self.L = max_len
@@ -298,7 +300,7 @@ class FiBiNETTrainer:
                  n_ent, ptr(self.sched), ptr(self.step_dev), self.wd, self.beta2, self.eps, ptr(self.last),
                  ptr(self.pend), ptr(self.ring), ptr(self.coef_hist), self.ring_n, self.B, ptr(self.rng),
                  ptr(self.p["mlp.1.num_batches_tracked"]), ptr(self.p["mlp.5.num_batches_tracked"]), ptr(self.ticket),
-                 st)
+                 self.total_steps, ptr(self.err), st)
             _events_end(ev)
         else:
             # clip_grad_norm_(10) is applied inside the dense Adam launch (it publishes coef / norm)
@@ -312,7 +314,8 @@ class FiBiNETTrainer:
             _events_end(ev)
             self.slot_row[:n_ent].fill_(-1)
             call("fbn_step_end", ptr(self.step_dev), ptr(self.rng), ptr(self.sumsq),
-                 ptr(self.p["mlp.1.num_batches_tracked"]), ptr(self.p["mlp.5.num_batches_tracked"]), st)
+                 ptr(self.p["mlp.1.num_batches_tracked"]), ptr(self.p["mlp.5.num_batches_tracked"]), self.total_steps,
+                 ptr(self.err), st)
         self.host_step += 1
         return self.loss
 
@@ -344,11 +347,23 @@ class FiBiNETTrainer:
         return (a["logits"] if logits else a["probs"]).clone()
 
     def check_ids(self) -> None:
-        if int(self.err.item()) != 0:
+        """Raise what the reference would have raised since the last check (one 4-byte read):
+        IndexError for an id outside its table (nn.Embedding), ValueError for a step past
+        total_steps (OneCycleLR) -- the latter is how graph replays, which never pass through
+        step()'s host-side guard, report it (the device step counter saturates)."""
+        e = int(self.err.item())
+        if e & 1:
             raise IndexError("index out of range in self (item/likes/views id outside its embedding table)")
+        if e & 2:
+            raise ValueError(f"Tried to step more than {self.total_steps} times. The specified number of total steps "
+                             f"is {self.total_steps}")
+
+    def device_step(self) -> int:
+        """Optimizer steps taken (the device counter: also advanced by hipGraph replays)."""
+        return int(self.step_dev.item())
 
     def current_lr(self) -> float:
-        return self.lrs[min(self.host_step, self.total_steps - 1)]
+        return self.lrs[min(self.device_step(), self.total_steps - 1)]
 
     # ------------------------------------------------------------------ checkpoint (App. B keys)
     def state_dict(self) -> Dict[str, torch.Tensor]:
@@ -374,13 +389,15 @@ class FiBiNETTrainer:
         return out
 
     def load_state_dict(self, sd: Dict[str, torch.Tensor]) -> None:
-        """Load reference-format weights (optimizer state is reset, as the reference never saves it)."""
+        """Load reference-format weights (App. B keys).  Like ``model.load_state_dict`` under the
+        reference's loop, the optimizer state (Adam moments, step count, schedule position) is
+        kept: only the weights and BatchNorm buffers change."""
         self.flush()
         for k in self.key_order:
             if k == TABLE:
                 self.E.copy_(sd[k][self.rows_lo:self.rows_lo + self.rows_local].to(self.device))
             else:
                 self.p[k].copy_(sd[k].to(self.device))
-        self.last.fill_(self.host_step)             # loaded rows are current
+        self.last.copy_(self.step_dev.expand_as(self.last))     # loaded rows are current (device step)
         if self.pend is not None:
             self.pend.fill_(-1)

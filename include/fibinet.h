@@ -243,13 +243,13 @@ int fbn_adam_flush(float* p, float* m, float* v, long long nrows, int D, int* la
                    const float* coef_hist, long long ring_stride, int ring_n, void* stream);
 /* Single-GPU step tail in ONE launch: fbn_adam_dense (clip from the sumsq slots) on the flat dense
  * parameters + fbn_adam_commit on the table + fbn_step_end; ticket = one device unsigned, zero
- * before the first call (the kernel's last block resets it). */
+ * before the first call (the kernel's last block resets it); max_step / err as fbn_step_end. */
 int fbn_adam_step_tail(float* dp, const float* dg, float* dm, float* dv, long long n_dense, const double* sumsq,
                        float max_norm, float* coef_out, float* norm_out, float* p, float* m, float* v, int D, int* map,
                        const float* gvec, float* extra, int* slot_row, int Lp1, int n, const void* consts_table,
                        int* step, float wd, float beta2, float eps, int* last, int* pend, float* ring,
                        float* coef_hist, int ring_n, int B, unsigned long long* rng, long long* nbt0, long long* nbt1,
-                       unsigned* ticket, void* stream);
+                       unsigned* ticket, int max_step, int* err, void* stream);
 /* Self-test of the packed exact zero-gradient Adam step of the lazy replay: n x 4 random operands
  * across the f32 range against the reference element step, bit for bit; mism[0] += mismatching
  * elements, mism[1] += elements on the fast path (device counters, caller zeroes). */
@@ -276,8 +276,12 @@ int fbn_claim_rows(const int64_t* item, const int64_t* seq, int B, int L, long l
 int fbn_pack_extras(const float* loss, double* tab_slots, float* out, void* stream);
 int fbn_unpack_extras(const float* in, float* loss, double* sumsq, void* stream);
 /* end of step: step counter, dropout counter, zero the sumsq slots, and the BatchNorm
- * num_batches_tracked buffers (nbt0 / nbt1 may be NULL; model_fibinet.py:127,131 BN1d). */
-int fbn_step_end(int* step, unsigned long long* rng, double* sumsq, long long* nbt0, long long* nbt1, void* stream);
+ * num_batches_tracked buffers (nbt0 / nbt1 may be NULL; model_fibinet.py:127,131 BN1d).
+ * max_step (= total_steps): the counter saturates there and sets bit 2 of *err (err may be NULL)
+ * -- OneCycleLR raises past total_steps (train_fibinet.py:84-92); a replayed hipGraph cannot, so
+ * the device keeps every schedule read in bounds and the host raises at its next check. */
+int fbn_step_end(int* step, unsigned long long* rng, double* sumsq, long long* nbt0, long long* nbt1, int max_step,
+                 int* err, void* stream);
 
 /* ---------------------------------------------------------------- row-sharded exchange (multi-GPU)
  * Replaces torch.nn.DataParallel's replicate/scatter of the whole table (src/train_fibinet.py:69-70)

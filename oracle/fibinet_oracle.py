@@ -128,12 +128,14 @@ class OracleFiBiNET(nn.Module):
     def fields(self, batch: Dict[str, torch.Tensor]) -> torch.Tensor:
         """X = [0, C[likes], C[views], E[item], mm(x), masked-mean E[seq]]  (:140-182)."""
         item_id = batch["item_id"].long()
-        x_mm = batch["item_emb_d128"].float()
+        # .float() in the reference (:141); a float64 copy of the oracle (tests' arbiter) keeps f64
+        ft = self.item_emb.weight.dtype
+        x_mm = batch["item_emb_d128"].to(ft)
         likes = batch["likes_level"].long()
         views = batch["views_level"].long()
         seq = batch.get("item_seq", None)
         b = item_id.shape[0]
-        user = torch.zeros((b, self.emb_dim), device=item_id.device)
+        user = torch.zeros((b, self.emb_dim), device=item_id.device, dtype=ft)
         f_like = self.cate_emb(likes)
         f_view = self.cate_emb(views)
         f_item = self.item_emb(item_id)
@@ -141,8 +143,8 @@ class OracleFiBiNET(nn.Module):
         if seq is not None:
             seq = seq.long()
             keep = (seq != 0)
-            rows = self.item_emb(seq) * keep.unsqueeze(-1).float()
-            cnt = keep.float().sum(dim=1, keepdim=True).clamp(min=1)
+            rows = self.item_emb(seq) * keep.unsqueeze(-1).to(ft)
+            cnt = keep.to(ft).sum(dim=1, keepdim=True).clamp(min=1)
             f_hist = rows.sum(dim=1) / cnt
         else:
             f_hist = torch.zeros_like(f_item)
@@ -190,8 +192,10 @@ class OracleTrainer:
     """
 
     def __init__(self, model: OracleFiBiNET, lr: float = 1e-3, weight_decay: float = 1e-5,
-                 total_steps: int = 1000):
+                 total_steps: int = 1000, max_norm: float = 10.0):
         self.model = model
+        self.max_norm = max_norm            # train_fibinet.py:119 uses 10.0; tests lower it to engage the clip
+        self.last_total_norm = None
         self.opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=weight_decay)
         self.loss_fn = nn.BCELoss()
         self.sched = torch.optim.lr_scheduler.OneCycleLR(
@@ -204,7 +208,7 @@ class OracleTrainer:
         y = self.model(batch, masks=masks)
         loss = self.loss_fn(y, labels)
         loss.backward()
-        torch.nn.utils.clip_grad_norm_(self.model.parameters(), max_norm=10.0)
+        self.last_total_norm = float(torch.nn.utils.clip_grad_norm_(self.model.parameters(), max_norm=self.max_norm))
         self.opt.step()
         self.sched.step()
         return float(loss.item()), y.detach()

@@ -172,7 +172,13 @@ def test_hip_matches_committed_golden_vectors(hip_device, d):
     g = {n: torch.zeros_like(v) for n, v in p.items() if v.dtype == torch.float32}
     table_grad = torch.zeros_like(p["item_emb.weight"])
     ops.backward(p, batch, acts, acts["gout"], g, cfg, table_grad=table_grad)
+    g["item_emb.weight"] = table_grad           # the scatter-add into the dense table gradient
     for key in [k for k in z.files if k.startswith("grad/")]:
         n = key[5:]
         ref = torch.from_numpy(z[key])
         _grad_close(g[n].cpu(), ref, n)
+    assert torch.equal(table_grad[0].cpu(), torch.zeros(d))      # padding_idx=0 row never written
+    for key in [k for k in z.files if k.startswith("gradrows/")]:  # first rows of the largest GEMM's wgrad
+        n = key[9:]
+        ref = torch.from_numpy(z[key])
+        _grad_close(g[n][:ref.shape[0]].cpu(), ref, n)

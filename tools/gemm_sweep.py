@@ -25,7 +25,8 @@ SH = {  # name: (M, N, K, transA, transB)
     "dWa  dh1^T c": (512, KC, B, True, False),
     "dW4  dh2^T h1": (256, 512, B, True, False),
 }
-PLANS = [None] + [(bm, bn, s) for bm, bn in ((64, 64), (128, 64), (64, 128), (128, 128)) for s in (1, 2, 4, 8)]
+PLANS = [None] + [(bm, bn, s) for bm, bn in ((64, 64), (128, 64), (64, 128), (128, 128)) for s in (1, 2, 4, 8)] \
+    + [(bm, bn, s, 8, st) for bm, bn in ((128, 128), (128, 64), (64, 128)) for s in (1, 2, 4, 8) for st in (2, 3, 4)]
 
 
 def operands(M, N, K, tA, tB):
@@ -60,7 +61,7 @@ def main():
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / 20 * 1e3
         print(f"torch {name:15s} M={M:5d} N={N:5d} K={K:5d} {us:6.1f}us ({2 * M * N * K / us / 1e6:5.0f} TF)", flush=True)
-        modes = ("dma16",) if os.environ.get("FBN_SWEEP_DMA_ONLY") else ("old", "dma16")
+        modes = ("old", "dma16") if os.environ.get("FBN_SWEEP_OLD") else ("dma16",)
         for mode in modes:
             if mode == "old":
                 os.environ["FBN_GEMM_NO_DMA16"] = "1"
@@ -74,7 +75,7 @@ def main():
                 else:
                     if K // pl[2] < 64:
                         continue
-                    os.environ["FBN_GEMM_FORCE"] = "%d,%d,%d" % pl
+                    os.environ["FBN_GEMM_FORCE"] = ",".join(str(x) for x in pl)
                     split = pl[2]
                 nb = max(ops._lib.lib().fbn_gemm_workspace_size(M, N, K, 1), split * M * N * 4)
                 ws = torch.empty(nb // 8 + 1, dtype=torch.float64, device=dev)
@@ -101,6 +102,9 @@ def main():
                 res.append((us, pl, err))
             bad = [r for r in res if not (r[2] < 1e-3)]
             res.sort(key=lambda r: r[0])
+            if os.environ.get("FBN_SWEEP_ALL"):
+                for u, p_, e in res:
+                    print(f"    {name:15s} {p_}: {u:.1f}us err {e:.1e}", flush=True)
             dflt = [r for r in res if r[1] is None][0][0]
             fl = 2 * M * N * K
             print(f"{mode:5s} {name:15s} M={M:5d} N={N:5d} K={K:5d} default {dflt:6.1f}us ({fl / dflt / 1e6:5.0f} TF)"
