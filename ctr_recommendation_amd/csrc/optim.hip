@@ -16,6 +16,7 @@
 // The map entries of touched rows are reset in the same pass.
 #include "common.h"
 #include <cstdlib>
+#include <algorithm>
 
 #pragma clang fp contract(off)
 
@@ -27,7 +28,7 @@ struct AdamConsts {
   float w1;     // 1 - beta1 (as float)
   float nss;    // -lr / bias_correction1 (as float)
   float bc2s;   // sqrt(bias_correction2) (as float)
-  float pad;    // host: lr (unused on the device); LDS windows: div_recip(bc2s)
+  float rbc2s;  // 1 / sqrt(bias_correction2) (as float; the table-row step multiplies by it)
 };
 
 // ------------------------------------------------------------------ squared norm partials
@@ -75,105 +76,41 @@ __device__ __forceinline__ float adam_elem(float& p, float& m, float& v, float g
   return p;
 }
 
-// ------------------------------------------------------------------ fast exact zero-gradient step
-// The replay of zero-gradient steps (lazy table Adam) is VALU-bound: ~46 instructions per element
-// with the compiler's IEEE f32 division (v_div_scale x2, v_rcp, 6 FMAs, v_div_fmas, v_div_fixup)
-// and correctly rounded sqrt (scaling + two neighbour tests + class fix-up).  adam_zero4 runs the
-// same arithmetic on element pairs with packed f32 ops (v_pk_mul/add/fma_f32) and WITHOUT the
-// range-handling parts of those sequences: v_div_scale / v_div_fmas only rescale and v_div_fixup
-// only rewrites special cases when an operand or the quotient is near the f32 range limits, and
-// the sqrt scaling only applies below 2^-96.  Each pair checks that its operands lie well inside
-// the ranges where those steps are identities ([2^-96, 2^100] for v, [2^-90, 2^50] for the
-// numerator, [2^-40, 2^30] for the denominator; bc2s in (0.03, 1]) and otherwise recomputes with
-// adam_elem -- so every result is bit-identical to adam_elem (tests: the eager-vs-lazy
-// comparison; fbn_adam_selftest on random operands across the f32 range).
+// ------------------------------------------------------------------ table-row Adam step
+// item_emb.weight is updated with the same operations as adam_elem except that the square root and
+// the division use the hardware v_sqrt_f32 / v_rcp_f32 (about 1 ulp each) and the moment updates
+// use fused multiply-adds:
+//   g = g*coef + wd*p;  m = fma(w1, g - m, m);  v = fma((1-b2)*g, g, v*b2)
+//   p = fma(nss*m, rcp(fma(sqrt(v), 1/sqrt(bc2), eps)), p)
+// 13 VALU issue-slot equivalents per element instead of ~50 for IEEE division + correctly rounded
+// sqrt.  Every table kernel (eager pass, lazy replay, touched / deferred commit, flush) uses this one
+// function, so the lazy replay stays bit-identical to eager dense Adam; the deviation from the IEEE
+// step is bounded by fbn_adam_selftest (a few ulp of the update, far inside the parity tolerance).
+// rbc2s = 1/sqrt(bc2) from the host schedule table (column 4, computed in double).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef int i32x2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
-
-// v_rcp + the Newton step of the compiler's f32 division
-__device__ __forceinline__ float div_recip(float b) {
-  const float r = __builtin_amdgcn_rcpf(b);
-  return __builtin_fmaf(__builtin_fmaf(-b, r, 1.f), r, r);
+__device__ __forceinline__ float adam_tab1(float p, float& m, float& v, float g, float wd, float b2, float omb2,
+                                           float eps, float w1, float nss, float rbc2s) {
+  g = __builtin_fmaf(wd, p, g);
+  m = __builtin_fmaf(w1, g - m, m);
+  v = __builtin_fmaf(omb2 * g, g, v * b2);
+  const float den = __builtin_fmaf(__builtin_amdgcn_sqrtf(v), rbc2s, eps);
+  return __builtin_fmaf(nss * m, __builtin_amdgcn_rcpf(den), p);
 }
-__device__ __forceinline__ f32x2 div_recip2(f32x2 b) {
-  const f32x2 r = {__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)};
-  return fma2(fma2(-b, r, (f32x2){1.f, 1.f}), r, r);
-}
-// quotient refinement of the compiler's f32 division given its reciprocal r of b
-__device__ __forceinline__ f32x2 div_refine2(f32x2 a, f32x2 b, f32x2 r) {
-  f32x2 q = a * r;
-  q = fma2(fma2(-b, q, a), r, q);
-  return fma2(fma2(-b, q, a), r, q);
-}
-// correctly rounded sqrt (the compiler's neighbour test) for x in [2^-96, 2^100]
-__device__ __forceinline__ f32x2 sqrt2_exact(f32x2 x) {
-  f32x2 s = {__builtin_amdgcn_sqrtf(x.x), __builtin_amdgcn_sqrtf(x.y)};
-  const i32x2 si = __builtin_bit_cast(i32x2, s);
-  const f32x2 sdn = __builtin_bit_cast(f32x2, si - 1), sup = __builtin_bit_cast(f32x2, si + 1);
-  const f32x2 rdn = fma2(-sdn, s, x), rup = fma2(-sup, s, x);
-  s.x = rdn.x <= 0.f ? sdn.x : s.x;
-  s.y = rdn.y <= 0.f ? sdn.y : s.y;
-  s.x = rup.x > 0.f ? sup.x : s.x;
-  s.y = rup.y > 0.f ? sup.y : s.y;
-  return s;
-}
-// Guard: v in [2^-60, 2^10], |nss*m| in [2^-70, 2^0], denom in [2^-40, 2^30] -- well inside the
-// ranges where the skipped steps are identities (sqrt scaling below 2^-96; division scaling when
-// the exponent difference reaches 96, the numerator is below 2^-103 or the quotient denormal).
-// Each range spans 70 binades, so one unsigned max3 + compare tests all three per element.
-#define FBN_G_SPAN 0x23000000u    // 70 binades
-#define FBN_G_V_LO 0x21800000u    // 2^-60
-#define FBN_G_A_LO 0x1c800000u    // 2^-70
-#define FBN_G_D_LO 0x2b800000u    // 2^-40
-__device__ __forceinline__ unsigned guard3(float v, float a, float den) {
-  const unsigned x = __float_as_uint(v) - FBN_G_V_LO, y = (__float_as_uint(a) & 0x7fffffffu) - FBN_G_A_LO;
-  return max(max(x, y), __float_as_uint(den) - FBN_G_D_LO);
-}
-// |x| in [lo, hi] (positive normal bounds) by an unsigned compare on the magnitude bits
-__device__ __forceinline__ bool in_range(float x, unsigned lo, unsigned hi) {
-  return (unsigned)((__float_as_uint(x) & 0x7fffffffu) - lo) <= hi - lo;
-}
-
-// one zero-gradient step (g = 0*1 + wd*p) of 4 elements; rc = div_recip(bc2s).  Both pairs are
-// computed branch-free (the scheduler interleaves their dependency chains), then one guard.
-__device__ __forceinline__ void adam_zero4(f32x4& pp, f32x4& mm, f32x4& vv, float wd, float b2, float omb2, float eps,
-                                           float w1, float nss, float bc2s, float rc) {
-  f32x2 P[2], M1[2], V1[2], Q[2];
-  unsigned g = 0;
+// four elements; gg already scaled by the clip coefficient (zero for a zero-gradient step)
+__device__ __forceinline__ void adam_tab4(f32x4& pp, f32x4& mm, f32x4& vv, f32x4 gg, float wd, float b2, float omb2,
+                                          float eps, float w1, float nss, float rbc2s) {
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    P[h] = (f32x2){pp[2 * h], pp[2 * h + 1]};
-    const f32x2 M = {mm[2 * h], mm[2 * h + 1]}, Vv = {vv[2 * h], vv[2 * h + 1]};
-    const f32x2 G = wd * P[h];
-    M1[h] = M + w1 * (G - M);
-    V1[h] = Vv * b2;
-    V1[h] = V1[h] + (omb2 * G) * G;
-    const f32x2 X = sqrt2_exact(V1[h]);
-    const f32x2 Den = div_refine2(X, (f32x2){bc2s, bc2s}, (f32x2){rc, rc}) + eps;
-    const f32x2 A = nss * M1[h];
-    Q[h] = div_refine2(A, Den, div_recip2(Den));
-    g = max(g, max(guard3(V1[h].x, A.x, Den.x), guard3(V1[h].y, A.y, Den.y)));
+  for (int e = 0; e < 4; ++e) {
+    float me = mm[e], ve = vv[e];
+    pp[e] = adam_tab1(pp[e], me, ve, gg[e], wd, b2, omb2, eps, w1, nss, rbc2s);
+    mm[e] = me;
+    vv[e] = ve;
   }
-  if (__builtin_expect(g <= FBN_G_SPAN, 1)) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const f32x2 P1 = P[h] + Q[h];
-      pp[2 * h] = P1.x; pp[2 * h + 1] = P1.y;
-      mm[2 * h] = M1[h].x; mm[2 * h + 1] = M1[h].y;
-      vv[2 * h] = V1[h].x; vv[2 * h + 1] = V1[h].y;
-    }
-  } else {
-    AdamConsts k;
-    k.w1 = w1; k.nss = nss; k.bc2s = bc2s; k.pad = 0.f;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float pe = pp[e], me = mm[e], ve = vv[e];
-      adam_elem(pe, me, ve, 0.f, 1.f, wd, b2, omb2, eps, k);
-      pp[e] = pe; mm[e] = me; vv[e] = ve;
-    }
-  }
+}
+__device__ __forceinline__ void adam_zero_tab4(f32x4& pp, f32x4& mm, f32x4& vv, float wd, float b2, float omb2,
+                                               float eps, float w1, float nss, float rbc2s) {
+  adam_tab4(pp, mm, vv, (f32x4){0.f, 0.f, 0.f, 0.f}, wd, b2, omb2, eps, w1, nss, rbc2s);
 }
 
 // clip coefficient of clip_grad_norm_ from the sumsq slots (same sequential order as
@@ -452,12 +389,7 @@ __device__ __forceinline__ void adam_table_body(float* __restrict__ p, float* __
         *reinterpret_cast<f32x4*>(ex) = (f32x4){0.f, 0.f, 0.f, 0.f};   // keep `extra` all-zero
       }
     }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float pe = pp[e], me = mm[e], ve = vv[e];
-      adam_elem(pe, me, ve, gg[e], coef, wd, b2, omb2, eps, k);
-      pp[e] = pe; mm[e] = me; vv[e] = ve;
-    }
+    adam_tab4(pp, mm, vv, gg * coef, wd, b2, omb2, eps, k.w1, k.nss, k.rbc2s);
     __builtin_nontemporal_store(pp, reinterpret_cast<f32x4*>(p + off));
     __builtin_nontemporal_store(mm, reinterpret_cast<f32x4*>(m + off));
     __builtin_nontemporal_store(vv, reinterpret_cast<f32x4*>(v + off));
@@ -503,12 +435,7 @@ __global__ void __launch_bounds__(256) adam_table_untouched(FBN_ADAM_TABLE_ARGS)
       if (!act[u]) continue;
       const long long r = r0 + u * RPW + lane / G;
       const size_t off = (size_t)r * D + 4 * q;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float pe = pp[u][e], me = mm[u][e], ve = vv[u][e];
-        adam_elem(pe, me, ve, 0.f, 1.f, wd, b2, omb2, eps, k);
-        pp[u][e] = pe; mm[u][e] = me; vv[u][e] = ve;
-      }
+      adam_zero_tab4(pp[u], mm[u], vv[u], wd, b2, omb2, eps, k.w1, k.nss, k.rbc2s);
       __builtin_nontemporal_store(pp[u], reinterpret_cast<f32x4*>(p + off));
       __builtin_nontemporal_store(mm[u], reinterpret_cast<f32x4*>(m + off));
       __builtin_nontemporal_store(vv[u], reinterpret_cast<f32x4*>(v + off));
@@ -516,65 +443,68 @@ __global__ void __launch_bounds__(256) adam_table_untouched(FBN_ADAM_TABLE_ARGS)
   }
 }
 
-// ------------------------------------------------------------------ self-test of adam_zero4
-// n threads x 4 elements of random (p, m, v) whose exponents span the f32 range (plus zeros,
-// denormals and exact powers of two) under random step constants: adam_zero4 against adam_elem,
-// bit for bit.  mism[0] += mismatching elements, mism[1] += elements that took the fast path.
+// ------------------------------------------------------------------ self-test of adam_tab4
+// n threads x 4 elements of random Adam states (p in [2^-10, 4), m in [2^-30, 2^-2), v = m^2 x
+// [1, 1025) -- |m| <= sqrt(v) as Adam's moments keep it -- and g zero or in [2^-30, 2^-2)) under
+// random step constants and clip coefficients: the table-row step (hardware sqrt / rcp, fused
+// moments) against the IEEE element step adam_elem.  dev[0..2] = max deviation of m, v, p in 1/16
+// ulp of each update's scale (m: |m| + |g*coef| + |wd*p|; v: max(v, (1-b2) * that^2);
+// p: max(|p|, |IEEE update|)).
 __device__ __forceinline__ unsigned st_hash(unsigned x) {
   x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
   return x;
 }
-__device__ float st_value(unsigned h, unsigned h2, int lo_exp, int hi_exp, bool sign) {
-  const unsigned kind = h2 & 31;
-  if (kind == 0) return 0.f;
-  if (kind == 1) return __uint_as_float(h & 0x007fffffu);                        // denormal
-  const int ex = lo_exp + (int)(h2 >> 8) % (hi_exp - lo_exp + 1);
-  const unsigned mant = kind == 2 ? 0u : (h & 0x007fffffu);                          // power of two
-  const unsigned bits = ((unsigned)(ex + 127) << 23) | mant | ((sign && (h2 & 64)) ? 0x80000000u : 0u);
+__device__ float st_value(unsigned h, int lo_exp, int hi_exp, bool sign) {
+  const int ex = lo_exp + (int)(st_hash(h + 3) % (unsigned)(hi_exp - lo_exp + 1));
+  const unsigned bits = ((unsigned)(ex + 127) << 23) | (h & 0x007fffffu) | ((sign && (h & 0x80000000u)) ? 0x80000000u : 0u);
   return __uint_as_float(bits);
 }
-__global__ void adam_selftest_kernel(int n, unsigned seed, unsigned long long* mism) {
+__device__ __forceinline__ float ulp_of(float x) {   // ulp of |x| (normal range)
+  return __uint_as_float(((__float_as_uint(fabsf(x)) >> 23) - 23u) << 23);
+}
+__global__ void adam_selftest_kernel(int n, unsigned seed, unsigned long long* dev) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  unsigned h = st_hash(seed * 0x9E3779B9u + (unsigned)i);
+  const unsigned h = st_hash(seed * 0x9E3779B9u + (unsigned)i);
   AdamConsts k;
   k.w1 = 0.05f + 0.1f * (float)(st_hash(h + 1) & 0xffff) / 65536.f;
   k.nss = -1e-4f * (1.f + 200.f * (float)(st_hash(h + 2) & 0xffff) / 65536.f);
   k.bc2s = 0.0316f + 0.968f * (float)(st_hash(h + 3) & 0xffff) / 65536.f;
-  const float wd = (st_hash(h + 4) & 1) ? 1e-5f : 3e-2f, b2 = 0.999f, omb2 = (float)(1.0 - 0.999), eps = 1e-8f;
-  k.pad = div_recip(k.bc2s);
-  f32x4 p, m, v;
+  k.rbc2s = (float)(1.0 / (double)k.bc2s);
+  const float coef = (st_hash(h + 5) & 1) ? 1.f : 0.01f + 0.99f * (float)(st_hash(h + 6) & 0xffff) / 65536.f;
+  const float wd = 1e-5f, b2 = 0.999f, omb2 = (float)(1.0 - 0.999), eps = 1e-8f;
+  f32x4 p, m, v, g;
   for (int e = 0; e < 4; ++e) {
-    const unsigned a = st_hash(h + 10 + 3 * e), b = st_hash(a), c = st_hash(b);
-    p[e] = st_value(a, st_hash(a + 7), -60, 40, true);
-    m[e] = st_value(b, st_hash(b + 7), -80, 20, true);
-    v[e] = fabsf(st_value(c, st_hash(c + 7), -126, 60, false));
+    const unsigned a = st_hash(h + 10 + 4 * e), b = st_hash(a), c = st_hash(b), d = st_hash(c);
+    p[e] = st_value(a, -10, 1, true);
+    m[e] = st_value(b, -30, -3, true);
+    v[e] = m[e] * m[e] * (1.f + (float)(c & 0xffff) / 64.f);
+    g[e] = (d & 3) ? 0.f : st_value(d, -30, -3, true);
   }
   f32x4 pf = p, mf = m, vf = v;
-  adam_zero4(pf, mf, vf, wd, b2, omb2, eps, k.w1, k.nss, k.bc2s, k.pad);
-  unsigned long long bad = 0, fast = 0;
+  adam_tab4(pf, mf, vf, g * coef, wd, b2, omb2, eps, k.w1, k.nss, k.rbc2s);
+  float dm = 0.f, dv = 0.f, dp = 0.f;
   for (int e = 0; e < 4; ++e) {
     float pe = p[e], me = m[e], ve = v[e];
-    adam_elem(pe, me, ve, 0.f, 1.f, wd, b2, omb2, eps, k);
-    const bool same = __float_as_uint(pe) == __float_as_uint(pf[e]) && __float_as_uint(me) == __float_as_uint(mf[e]) &&
-                      __float_as_uint(ve) == __float_as_uint(vf[e]);
-    const bool nan_same = pe != pe && pf[e] != pf[e];                 // NaN payloads may differ
-    bad += (same || nan_same) ? 0 : 1;
-    const float a = k.nss * mf[e];
-    fast += guard3(vf[e], a, 1.f) <= FBN_G_SPAN ? 1 : 0;
+    adam_elem(pe, me, ve, g[e], coef, wd, b2, omb2, eps, k);
+    const float gs = fabsf(g[e] * coef) + fabsf(wd * p[e]);
+    dm = fmaxf(dm, fabsf(mf[e] - me) / ulp_of(fmaxf(fabsf(m[e]), gs)));
+    dv = fmaxf(dv, fabsf(vf[e] - ve) / ulp_of(fmaxf(v[e], omb2 * gs * gs)));
+    dp = fmaxf(dp, fabsf(pf[e] - pe) / ulp_of(fmaxf(fabsf(p[e]), fabsf(pe - p[e]))));
   }
-  if (bad) atomicAdd(mism, bad);
-  atomicAdd(mism + 1, fast);
+  atomicMax(dev + 0, (unsigned long long)(dm * 16.f));
+  atomicMax(dev + 1, (unsigned long long)(dv * 16.f));
+  atomicMax(dev + 2, (unsigned long long)(dp * 16.f));
 }
 
-extern "C" int fbn_adam_selftest(int n, unsigned seed, unsigned long long* mism, void* stream) {
+extern "C" int fbn_adam_selftest(int n, unsigned seed, unsigned long long* dev, void* stream) {
   if (n <= 0) return FBN_OK;
-  hipLaunchKernelGGL(adam_selftest_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, n, seed, mism);
+  hipLaunchKernelGGL(adam_selftest_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, n, seed, dev);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
 
-// ------------------------------------------------------------------ lazy table Adam (exact)
+// ------------------------------------------------------------------ lazy table Adam (bit-identical to eager)
 // A row whose loss gradient is zero at step s still gets torch's coupled-L2 Adam update
 // (g = 0 * coef + wd * p, then m, v, p).  That update depends only on the row and on step s's
 // schedule constants, so it can be REPLAYED later with the same float operations in the same
@@ -618,21 +548,15 @@ __device__ __forceinline__ void replay_rows(float* __restrict__ p, float* __rest
                                                        (size_t)pe * D + 4 * q);
       const float coef = ps.coef_hist[k0];
       const AdamConsts k = win[k0 - w0];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float pe_ = pp[e], me = mm[e], ve = vv[e];
-        adam_elem(pe_, me, ve, gg[e], coef, wd, b2, omb2, eps, k);
-        pp[e] = pe_; mm[e] = me; vv[e] = ve;
-      }
+      adam_tab4(pp, mm, vv, gg * coef, wd, b2, omb2, eps, k.w1, k.nss, k.rbc2s);
       s = k0 + 1;
     }
   }
   for (; s < t; ++s) {
     // the rolling window keeps every row within F <= FBN_LAZY_MAX_LAG steps, so the constants of
-    // steps k0 .. t-1 are all in the LDS window (a global fallback would turn this into flat loads);
-    // pad holds div_recip(bc2s), computed when the window was loaded
+    // steps k0 .. t-1 are all in the LDS window (a global fallback would turn this into flat loads)
     const AdamConsts k = win[s - w0];
-    adam_zero4(pp, mm, vv, wd, b2, omb2, eps, k.w1, k.nss, k.bc2s, k.pad);
+    adam_zero_tab4(pp, mm, vv, wd, b2, omb2, eps, k.w1, k.nss, k.rbc2s);
   }
   *reinterpret_cast<f32x4*>(p + off) = pp;
   *reinterpret_cast<f32x4*>(m + off) = mm;
@@ -654,37 +578,61 @@ __global__ void __launch_bounds__(256) adam_catchup_kernel(float* __restrict__ p
   const int t = *step;
   const int w0 = t > FBN_LAZY_MAX_LAG ? t - FBN_LAZY_MAX_LAG : 0;
   for (int i = threadIdx.x; i < t - w0; i += blockDim.x) {
-    AdamConsts c = table[w0 + i];
-    // outside (2^-20, 2): NaN forces adam_zero4's exact fallback
-    c.pad = in_range(c.bc2s, 0x35800000u, 0x40000000u) ? div_recip(c.bc2s) : __builtin_nanf("");
-    win[i] = c;
+    win[i] = table[w0 + i];
   }
   __syncthreads();
   const long long roll0 = (long long)(t % F) * chunk;
   const long long nroll = (parts & 2) && roll0 < nrows ? min(chunk, nrows - roll0) : 0;
   if (!(parts & 1)) n_ent = 0;
   const long long n = n_ent + nroll;
-  const int lane = threadIdx.x & 63, q = lane % G;
+  // Each wave takes SCAN items, one per lane, sorts them by replay start (rows that need no replay
+  // last) with a bitonic network over lane shuffles, and its RPW lane groups replay the sorted rows
+  // RPW at a time: the rows of a round have similar replay lengths (their group finishes together)
+  // and duplicate / padding entries, claimed window rows and up-to-date rows cost nothing.
+  // SCAN = 16 at D >= 64 gives ~10 waves per SIMD at C3, enough to hide each round's row loads.
+  constexpr int SCAN = D >= 64 ? 16 : 64;
+  const int lane = threadIdx.x & 63, q = lane % G, grp = lane / G;
   const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
-  for (long long i0 = gw * RPW; i0 < n; i0 += nw * RPW) {
-    const long long i = i0 + lane / G;
-    if (i >= n) continue;
-    long long r;
-    if (i < n_ent) {
-      const int sr = slot_row[i];
-      if (sr == -1) continue;
-      r = sr & ~FBN_SLOT_FLAG;
-    } else {
-      r = roll0 + (i - n_ent);
-      if (map && map[r] != -1) continue;   // claimed this step: its claiming entry replays it
+  for (long long i0 = gw * SCAN; i0 < n; i0 += nw * SCAN) {
+    const long long i = i0 + lane;
+    int r = -1, key = 0x7fffffff;
+    if (lane < SCAN && i < n) {
+      if (i < n_ent) {
+        const int sr = slot_row[i];
+        if (sr != -1) r = sr & ~FBN_SLOT_FLAG;
+      } else {
+        const long long rr = roll0 + (i - n_ent);
+        if (!map || map[rr] == -1) r = (int)rr;   // claimed rows are replayed by their claiming entry
+      }
+      if (r >= 0) {
+        const int k0 = last[r];
+        if (k0 < t) key = k0;
+      }
     }
-    const int k0 = last[r];
-    if (k0 >= t) continue;
-    replay_rows<D>(p, m, v, r, q, k0, t, win, w0, table, wd, b2, omb2, eps, ps);
-    if (q == 0) {
-      last[r] = t;
-      if (ps.pend) ps.pend[r] = -1;
+    const int cnt = __popcll(__ballot(key != 0x7fffffff));
+    if (cnt == 0) continue;
+#pragma unroll
+    for (int kk = 2; kk <= SCAN; kk <<= 1)
+#pragma unroll
+      for (int j = kk >> 1; j > 0; j >>= 1) {
+        const int ok = __shfl_xor(key, j, 64), orr = __shfl_xor(r, j, 64);
+        const bool up = (lane & kk) == 0, lower = (lane & j) == 0;
+        if (lower == up ? ok < key : ok > key) {
+          key = ok;
+          r = orr;
+        }
+      }
+    for (int j0 = 0; j0 < cnt; j0 += RPW) {
+      const int src = j0 + grp;
+      const int rr = __shfl(r, src < 64 ? src : 0, 64);
+      const int k0 = __shfl(key, src < 64 ? src : 0, 64);
+      if (src >= cnt) continue;
+      replay_rows<D>(p, m, v, rr, q, k0, t, win, w0, table, wd, b2, omb2, eps, ps);
+      if (q == 0) {
+        last[rr] = t;
+        if (ps.pend) ps.pend[rr] = -1;
+      }
     }
   }
 }
@@ -701,10 +649,7 @@ __global__ void __launch_bounds__(256) adam_flush_kernel(float* __restrict__ p, 
   const int t = *step;
   const int w0 = t > FBN_LAZY_MAX_LAG ? t - FBN_LAZY_MAX_LAG : 0;
   for (int i = threadIdx.x; i < t - w0; i += blockDim.x) {
-    AdamConsts c = table[w0 + i];
-    // outside (2^-20, 2): NaN forces adam_zero4's exact fallback
-    c.pad = in_range(c.bc2s, 0x35800000u, 0x40000000u) ? div_recip(c.bc2s) : __builtin_nanf("");
-    win[i] = c;
+    win[i] = table[w0 + i];
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, q = lane % G;
@@ -754,12 +699,7 @@ __global__ void __launch_bounds__(256) adam_touched_kernel(float* __restrict__ p
     f32x4 pp = *reinterpret_cast<f32x4*>(p + off);
     f32x4 mm = *reinterpret_cast<f32x4*>(m + off);
     f32x4 vv = *reinterpret_cast<f32x4*>(v + off);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      float pe = pp[c], me = mm[c], ve = vv[c];
-      adam_elem(pe, me, ve, gg[c], coef, wd, b2, omb2, eps, k);
-      pp[c] = pe; mm[c] = me; vv[c] = ve;
-    }
+    adam_tab4(pp, mm, vv, gg * coef, wd, b2, omb2, eps, k.w1, k.nss, k.rbc2s);
     *reinterpret_cast<f32x4*>(p + off) = pp;
     *reinterpret_cast<f32x4*>(m + off) = mm;
     *reinterpret_cast<f32x4*>(v + off) = vv;
@@ -823,12 +763,7 @@ __device__ __forceinline__ void adam_commit_body(float* __restrict__ p, float* _
       f32x4 pp = *reinterpret_cast<f32x4*>(p + off);
       f32x4 mm = *reinterpret_cast<f32x4*>(m + off);
       f32x4 vv = *reinterpret_cast<f32x4*>(v + off);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        float pe = pp[c], me = mm[c], ve = vv[c];
-        adam_elem(pe, me, ve, gg[c], coef, wd, b2, omb2, eps, k);
-        pp[c] = pe; mm[c] = me; vv[c] = ve;
-      }
+      adam_tab4(pp, mm, vv, gg * coef, wd, b2, omb2, eps, k.w1, k.nss, k.rbc2s);
       *reinterpret_cast<f32x4*>(p + off) = pp;
       *reinterpret_cast<f32x4*>(m + off) = mm;
       *reinterpret_cast<f32x4*>(v + off) = vv;
@@ -1171,7 +1106,10 @@ extern "C" int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, i
     return FBN_ERR_ARG;
   }
   const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
-  FBN_DISPATCH_D(adam_catchup_kernel, D, group_grid(items, D, cap), p, m, v, slot_row, n_ent, map, nrows, F, chunk,
+  // one wave per SCAN items (16 at D >= 64, else 64; sorted and compacted inside the kernel)
+  const long long scan = D >= 64 ? 16 : 64;
+  const dim3 grid((unsigned)std::min<long long>(cap, (items + 4 * scan - 1) / (4 * scan)));
+  FBN_DISPATCH_D(adam_catchup_kernel, D, grid, p, m, v, slot_row, n_ent, map, nrows, F, chunk,
                  parts, last, (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
   FBN_CHECK_LAUNCH();
   return FBN_OK;

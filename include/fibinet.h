@@ -221,7 +221,7 @@ int fbn_adam_table(float* p, float* m, float* v, long long nrows, int D, int* ma
 int fbn_adam_touched(float* p, float* m, float* v, int D, int* map, const float* gvec, float* extra, int* slot_row,
                      int Lp1, int n, const float* coef, const void* consts_table, const int* step, float wd,
                      float beta2, float eps, int* last, void* stream);
-/* Lazy table Adam (exact): last[r] = Adam steps applied to row r.  fbn_adam_catchup replays the
+/* Lazy table Adam (bit-identical to the eager table pass): last[r] = Adam steps applied to row r.  fbn_adam_catchup replays the
  * zero-loss-gradient steps (coupled L2 decay only: g = 0*coef + wd*p) of the rows claimed in
  * slot_row and of rolling window (step mod F) (ceil(nrows/F) rows) up to *step, with the same
  * float operations in the same order as stepping them (bit-identical); fbn_adam_touched(last)
@@ -250,10 +250,11 @@ int fbn_adam_step_tail(float* dp, const float* dg, float* dm, float* dv, long lo
                        int* step, float wd, float beta2, float eps, int* last, int* pend, float* ring,
                        float* coef_hist, int ring_n, int B, unsigned long long* rng, long long* nbt0, long long* nbt1,
                        unsigned* ticket, int max_step, int* err, void* stream);
-/* Self-test of the packed exact zero-gradient Adam step of the lazy replay: n x 4 random operands
- * across the f32 range against the reference element step, bit for bit; mism[0] += mismatching
- * elements, mism[1] += elements on the fast path (device counters, caller zeroes). */
-int fbn_adam_selftest(int n, unsigned seed, unsigned long long* mism, void* stream);
+/* Self-test of the table-row Adam step (hardware sqrt / rcp, fused moment updates; used by every
+ * item_emb.weight kernel) against the IEEE element step of fbn_adam_dense: n x 4 random operands
+ * in training ranges; dev[0..2] = max deviation of m, v, p in 1/16 ulp of each update's largest
+ * term (device counters, caller zeroes). */
+int fbn_adam_selftest(int n, unsigned seed, unsigned long long* dev, void* stream);
 /* Single-GPU end of step with deferred table gradients (replaces fbn_adam_touched + the slot_row
  * reset): a claiming entry without duplicates records its vector in pend (applied at the row's
  * next replay); one with duplicates (FLAG) is updated now; map and slot_row are reset; the step's

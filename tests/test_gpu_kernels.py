@@ -83,16 +83,20 @@ def test_gemm_bf16_all_layouts(hip_device, transA, transB, M, N, K):
 
 
 @pytest.mark.gpu
-def test_adam_fast_zero_step_is_bit_exact(hip_device):
-    """The packed zero-gradient Adam step of the lazy replay (no division scaling / fix-up, no
-    sqrt scaling; exact fallback outside the guarded ranges) against the reference element step
-    on 16M random operands spanning the f32 range: every p, m, v bit-identical."""
+def test_table_adam_step_vs_ieee(hip_device):
+    """The table-row Adam step (v_sqrt_f32 / v_rcp_f32, fused moment updates) that every
+    item_emb.weight kernel uses, against the IEEE element step (correctly rounded sqrt and
+    division, torch's operation order) on 16M random Adam states (|m| <= sqrt(v)): m within 2 ulp
+    of its update's scale, v and p within 8 ulp (p: of max(|p|, |update|)).  The differences come
+    from the fused multiply-adds (one rounding where torch has two; under cancellation in
+    g*coef + wd*p the fused form is the accurate one) and the ~1 ulp hardware sqrt / rcp."""
     from ctr_recommendation_amd import _lib
-    mism = torch.zeros(2, dtype=torch.int64, device=hip_device)
+    dev = torch.zeros(3, dtype=torch.int64, device=hip_device)
     n = 1 << 22
     for seed in (1, 2, 3, 4):
-        _lib.call("fbn_adam_selftest", n, seed, _lib.ptr(mism), _lib.stream_handle(hip_device))
+        _lib.call("fbn_adam_selftest", n, seed, _lib.ptr(dev), _lib.stream_handle(hip_device))
     torch.cuda.synchronize()
-    bad, fast = int(mism[0]), int(mism[1])
-    assert bad == 0, bad
-    assert fast > n          # the guarded fast path covers most realistic operands
+    dm, dv, dp = (int(x) / 16 for x in dev.cpu())
+    print(f"table Adam step vs IEEE: m {dm} ulp, v {dv} ulp, p {dp} ulp")
+    assert dm <= 2.0 and dv <= 8.0, (dm, dv)
+    assert dp <= 8.0, dp
