@@ -761,9 +761,13 @@ static GemmPlan plan_gemm(int M, int N, int K, int bk) {
   return p;
 }
 
-// LDS-DMA kernel plan (tools/gemm_sweep.py on the C3 shapes): 64x64 tiles whenever they give
-// >= 512 workgroups (no split: F3, F4, dh1, dc, U); small outputs (the wgrad GEMMs, K = batch)
-// split K up to ~512 (128x64 tiles, M, N >= 512) or ~256 (64x64) workgroups, >= 4 K-steps each.
+// LDS-DMA kernel plan (tools/gemm_sweep.py on the C3 shapes, MI355X, profiles/r02_gemm_sweep.log):
+// * large outputs (>= 512 64x64 tiles, no split): 8 waves on 64x128 tiles (each wave 32x32 of a
+//   2x4 wave grid), or 128x128 tiles when N >= 1024 and they still give >= 256 workgroups -- 8
+//   waves (two per SIMD) keep the MFMA pipe busy while the partner wave waits on its LDS reads;
+//   F3 30.9 -> 26.8 us, dc 36.2 -> 32.5 us, U 11.4 -> 9.4 us;
+// * small outputs (the wgrad GEMMs, K = batch): split K to ~512 workgroups; M, N >= 512 take
+//   128x128 tiles with 8 waves (dWa 42.5 -> 35.1 us), else 64x64 with 4 waves.
 static GemmPlan plan_dma16(int M, int N, int K) {
   const long long t64 = (long long)fbn_cdiv(M, 64) * fbn_cdiv(N, 64);
   if (t64 >= 512) {
@@ -771,9 +775,11 @@ static GemmPlan plan_dma16(int M, int N, int K) {
       int a = 64, b = 64;
       if (sscanf(e, "%d,%d", &a, &b) == 2) return {a, b, 1};
     }
+    if (N >= 1024 && (long long)fbn_cdiv(M, 128) * fbn_cdiv(N, 128) >= 256) return {128, 128, 1, 8};
+    if (N >= 128) return {64, 128, 1, 8};
     return {64, 64, 1};
   }
-  GemmPlan p = (M >= 512 && N >= 512) ? GemmPlan{128, 64, 1} : GemmPlan{64, 64, 1};
+  GemmPlan p = (M >= 512 && N >= 512) ? GemmPlan{128, 128, 1, 8} : GemmPlan{64, 64, 1};
   const long long tiles = (long long)fbn_cdiv(M, p.bm) * fbn_cdiv(N, p.bn);
   const long long target = p.bm == 128 ? 512 : 256;
   while (p.split < 64 && tiles * p.split * 2 <= target && K / (p.split * 2) >= 256) p.split *= 2;
