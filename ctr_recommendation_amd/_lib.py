@@ -88,6 +88,8 @@ SIGNATURES = {
     "fbn_route": (I, [P, P, I, I, LL, LL, I, P, P, P, P, P, P, P]),
     "fbn_owner_claim": (I, [P, I, P, P, I, P]),
     "fbn_owner_gather": (I, [P, I, P, P, P, P, I, I, P]),
+    "fbn_collate": (I, [P, I, P, P, I, I, P, P, P, P, P, LL, P, I, P, P, P, P, P, P, P, P, P]),
+    "fbn_collate_zero_if": (I, [P, LL, P, P]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

@@ -85,3 +85,55 @@ def make_device_batches(n: int, B: int, V: int, L: int, device, seed: int = 2025
         out.append(({"item_id": item, "item_seq": seq, "likes_level": likes, "views_level": views,
                      "item_emb_d128": mm.contiguous()}, label))
     return out
+
+
+def write_microlens_parquet(out_dir: str, n_train: int, n_valid: int = 0, n_test: int = 0, n_items: int = 5000,
+                            seq_width: int = 20, seed: int = 2025, item_id_stride: int = 1,
+                            missing_ids=(), signal: str = "fields") -> Dict[str, str]:
+    """Synthetic MicroLens_1M_x1-shaped parquet files (the schema of config/fibinet_config.yaml:30-37):
+    train / valid / test with columns user_id, item_seq (list of seq_width ids, left-padded with 0),
+    likes_level, views_level, item_id, label (test: no label), and item_info.parquet with item_id
+    and item_emb_d128 (list of 128 float32, L2-normalised).  Item ids are 1 + k * item_id_stride
+    (non-contiguous when the stride is > 1); ids in ``missing_ids`` are left out of item_info.
+    Returns the dataset_config-style paths."""
+    import os
+
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+
+    os.makedirs(out_dir, exist_ok=True)
+    rng = np.random.default_rng(seed)
+    ids = 1 + np.arange(n_items, dtype=np.int64) * item_id_stride
+    emb = rng.standard_normal((n_items, 128)).astype(np.float32)
+    emb /= np.linalg.norm(emb, axis=1, keepdims=True)
+    keep = ~np.isin(ids, np.asarray(list(missing_ids), dtype=np.int64))
+    info = pa.table({"item_id": pa.array(ids[keep]),
+                     "item_emb_d128": pa.array(list(emb[keep]), type=pa.list_(pa.float32()))})
+    paths = {"item_info": os.path.join(out_dir, "item_info.parquet")}
+    pq.write_table(info, paths["item_info"])
+    for split, n in (("train", n_train), ("valid", n_valid), ("test", n_test)):
+        if n <= 0:
+            continue
+        k = rng.integers(0, n_items, size=n)
+        item = ids[k]
+        n_valid = rng.integers(0, seq_width + 1, size=n)
+        hist = ids[rng.integers(0, n_items, size=(n, seq_width))]
+        slot = np.arange(seq_width)[None, :]
+        seq = np.where(slot >= (seq_width - n_valid)[:, None], hist, 0)
+        likes = rng.integers(0, 11, size=n)
+        views = rng.integers(0, 11, size=n)
+        mm0 = emb[k, 0]
+        score = (likes - 5) / 1.5 - (views - 5) / 2.5 + 12.0 * mm0 if signal == "fields" else \
+            (((item % 97) * 7 + likes * 3 - views * 2) % 11 - 5) / 2.5 + 2.0 * mm0
+        label = (rng.random(n) < 1.0 / (1.0 + np.exp(-score))).astype(np.float32)
+        cols = {"user_id": pa.array(rng.integers(1, 20000, size=n)),
+                "item_seq": pa.array(list(seq.astype(np.int64)), type=pa.list_(pa.int64())),
+                "likes_level": pa.array(likes.astype(np.int64)),
+                "views_level": pa.array(views.astype(np.int64)),
+                "item_id": pa.array(item)}
+        if split != "test":
+            cols["label"] = pa.array(label)
+        path = os.path.join(out_dir, f"{split}.parquet")
+        pq.write_table(pa.table(cols), path)
+        paths[f"{split}_data"] = path
+    return paths

@@ -1,0 +1,161 @@
+"""Training launcher: the process-per-GPU counterpart of src/train_fibinet.py.
+
+    python -m ctr_recommendation_amd.train [--config ../config/fibinet_config.yaml] [--epochs E]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \\
+        -m ctr_recommendation_amd.train [--config ...]
+
+Same surface and loop as the reference script:
+
+* the YAML config (src/train_fibinet.py:18-28) -- the keys it reads: ``dataset_id``,
+  ``base_expid``, ``dataset_config[id].{train_data, valid_data, item_info}`` and
+  ``model_cfg.{embedding_dim, batch_size, max_len, learning_rate, weight_decay, epochs, seed}``;
+  optional keys this build adds: ``compute_dtype`` ("fp32" default, "bf16" = C3's mode),
+  ``table_adam`` ("lazy" default: exact), and ``honour_config`` (see model_fibinet.build_model);
+* ``set_seed(seed)`` then ``build_model`` (:33, :67): the seeded init of the reference;
+* Adam(lr, weight_decay) + BCELoss + clip_grad_norm_(10) + OneCycleLR(max_lr = 10 lr,
+  epochs x steps_per_epoch, pct_start 0.3, div 25, final_div 1000) (:74-92, :113-123) -- all inside
+  FiBiNETTrainer's device step;
+* the epoch loop (:103-152): loss printed every 200 steps with the current lr, the epoch's mean
+  train loss, valid AUC (utils.compute_auc, :133-146), and the best-AUC checkpoint
+  (App. B keys, no ``module.`` prefix: :148-152).
+
+What differs is underneath: batches come from the HBM-resident loader (loader.py: one collate
+launch per batch, no worker processes, no pageable copies); the loss is accumulated on the device
+and read at the print points (the reference syncs every step with ``loss.item()``); at N > 1
+each process owns one GPU and a block of table rows (row-sharded trainer, SyncBN statistics,
+one dense all-reduce) instead of DataParallel (:69-70), and the trainer drops the final partial
+training batch so every rank steps on an equal share (the schedule's total follows).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import time
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+import torch
+
+
+def load_config(path: Optional[str] = None) -> Tuple[Dict, Dict, Dict]:
+    """(cfg, dataset_cfg, model_cfg) as src/train_fibinet.py:18-28 reads them."""
+    import yaml
+    if path is None:
+        path = "../config/fibinet_config.yaml"
+        if not os.path.exists(path):
+            path = "config/fibinet_config.yaml"
+    with open(path) as f:
+        cfg = yaml.safe_load(f)
+    dataset_cfg = cfg["dataset_config"][cfg["dataset_id"]]
+    model_cfg = cfg[cfg["base_expid"]]
+    return cfg, dataset_cfg, model_cfg
+
+
+def set_seed(seed: int) -> None:
+    """src/utils.py:6-16 (python, numpy, torch; the device generators are seeded by torch)."""
+    import random
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+
+
+def _gather_host(x: np.ndarray, world: int) -> np.ndarray:
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    parts = [None] * world
+    dist.all_gather_object(parts, x)
+    return np.concatenate(parts)
+
+
+def run(config: Optional[str] = None, *, epochs: Optional[int] = None, checkpoint: Optional[str] = None,
+        log=print, overrides: Optional[Dict] = None) -> Dict:
+    """Train as src/train_fibinet.py does; returns {"best_auc", "history": [(epoch, loss, auc)]}."""
+    import torch.distributed as dist
+
+    from .loader import make_loaders
+    from .model_fibinet import build_model
+    from .trainer import FiBiNETTrainer
+    from .utils import compute_auc
+
+    cfg, dataset_cfg, model_cfg = load_config(config)
+    model_cfg = dict(model_cfg, **(overrides or {}))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1 and not dist.is_initialized():
+        dist.init_process_group("nccl", device_id=device)
+    seed = int(model_cfg.get("seed", 2025))
+    set_seed(seed)
+    log0 = log if rank == 0 else (lambda *a, **k: None)
+    log0(f"Training FiBiNET on {world} x {torch.cuda.get_device_name(device)}")
+
+    train_loader, valid_loader, _ = make_loaders(dataset_cfg, model_cfg, device, rank, world, seed)
+    if world > 1:
+        train_loader.drop_last = True
+    n_epochs = int(epochs if epochs is not None else model_cfg.get("epochs", 30))
+    steps_per_epoch = len(train_loader)
+    set_seed(seed)                                        # build_model after set_seed, as :33 / :67
+    init = build_model(None, model_cfg).state_dict()
+    trainer = FiBiNETTrainer(model_cfg, total_steps=n_epochs * steps_per_epoch,
+                             batch_size=train_loader.batch_size // world, device=device, rank=rank, world=world,
+                             init_state=init, seed=seed, table_adam=str(model_cfg.get("table_adam", "lazy")))
+    del init
+    best_auc, history = 0.0, []
+    ckpt = checkpoint or os.path.join("..", "checkpoints", "FiBiNET_best.pth")
+    for epoch in range(n_epochs):
+        t0 = time.perf_counter()
+        total = torch.zeros((), dtype=torch.float64, device=device)
+        steps = 0
+        for batch, labels in train_loader:
+            loss = trainer.step(batch, labels)
+            total += loss[0].double()
+            steps += 1
+            if steps % 200 == 0:
+                log0(f"Epoch {epoch + 1} | Step {steps} | Loss: {loss.item():.4f} | LR: {trainer.current_lr():.6f}")
+        trainer.check_ids()
+        train_loader.check()
+        avg_loss = float(total.item()) / steps if steps else 0.0
+        dt = time.perf_counter() - t0
+        # validation (:133-146): eval-mode probabilities of the whole split, AUC on the host
+        ys, ps = [], []
+        for batch, labels in valid_loader:
+            ps.append(trainer.predict(batch).cpu().numpy())
+            ys.append(labels.cpu().numpy())
+        valid_loader.check()
+        auc = None
+        if ys:
+            y = _gather_host(np.concatenate(ys), world)
+            p = _gather_host(np.concatenate(ps), world)
+            auc = float(compute_auc(y, p))
+        history.append((epoch + 1, avg_loss, auc))
+        log0(f"Epoch {epoch + 1} | Train Loss: {avg_loss:.4f} | Valid AUC: {auc if auc is None else round(auc, 4)} | "
+             f"{steps * train_loader.batch_size / dt:.0f} samples/s")
+        if auc is not None and auc > best_auc:
+            best_auc = auc
+            sd = trainer.state_dict()                     # collective at N > 1 (table shards gathered)
+            if rank == 0:
+                os.makedirs(os.path.dirname(os.path.abspath(ckpt)), exist_ok=True)
+                torch.save(sd, ckpt)
+                log0(f"New best FiBiNET AUC; saved to {ckpt}")
+    log0(f"Done. Best AUC: {best_auc:.4f}")
+    return {"best_auc": best_auc, "history": history, "trainer": trainer}
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--config")
+    ap.add_argument("--epochs", type=int)
+    ap.add_argument("--checkpoint")
+    args = ap.parse_args(argv)
+    run(args.config, epochs=args.epochs, checkpoint=args.checkpoint)
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -294,6 +294,22 @@ int fbn_owner_claim(const int* ids, int n, int* map, int* slot_row, int rank, vo
 int fbn_owner_gather(const int* ids, int n, const float* E, float* out, int* map, int* slot_row, int rank, int D,
                      void* stream);
 
+/* ---------------------------------------------------------------- device collator
+ * Replaces BatchCollator.__call__ (src/dataloader.py:69-121) and InferenceCollator.__call__
+ * (src/Prediction.py:28-52): batch row b = dataset row perm[b] of HBM-resident columns item [N],
+ * seq [N][Ls] (the last L columns are kept: src/dataloader.py:111-116), likes, views, user [N]
+ * int64 and label [N] f32 (any of those may be NULL), and o_emb[b] = emb[slot_of_id[item]] (the
+ * item_info lookup of :91-95; E floats per row).  An item id without an item_info row gets a zero
+ * row and sets *missing (the training collator's KeyError, raised by the host when it checks). */
+int fbn_collate(const int64_t* perm, int B, const int64_t* item, const int64_t* seq, int Ls, int L,
+                const int64_t* likes, const int64_t* views, const int64_t* user, const float* label,
+                const int* slot_of_id, long long n_ids, const float* emb, int E, int64_t* o_item, int64_t* o_seq,
+                int64_t* o_likes, int64_t* o_views, int64_t* o_user, float* o_label, float* o_emb, int* missing,
+                void* stream);
+/* x[0:n] = 0 when *flag != 0: the inference collator's whole-batch zero fallback
+ * (src/Prediction.py:39-42) on the batch's own missing flag, with no host round trip. */
+int fbn_collate_zero_if(float* x, long long n, const int* flag, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -2,12 +2,13 @@
 
 This package restates the reference algorithm (YOUNESELBOUKNIFY/Ctr_recommendation,
 ``src/model_fibinet.py`` + the per-step part of ``src/train_fibinet.py``) with stock
-PyTorch CPU ops.  It exists to *check* the HIP path, never to run it:
+PyTorch CPU ops, and the data path (``src/dataloader.py``, ``src/Prediction.py``'s collator and
+export) with pandas / numpy (``oracle/collate_ref.py``).  It exists to *check* the HIP path, never to run it:
 
 * only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg
   may import it;
-* nothing in ``ctr_recommendation_amd/`` imports it (``tests/test_no_oracle_in_product.py``
-  enforces this).
+* nothing in ``ctr_recommendation_amd/`` imports it (``tests/test_lib.py::
+  test_product_never_imports_oracle`` enforces this).
 
 Pinning (see DESIGN.md "Oracle"): the reference ships no tests or fixtures and running it
 was denied in the survey container, so the oracle is pinned by
