@@ -227,9 +227,9 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
     for _ in range(args.probe_steps):
         load(i)
         i += 1
-        # a ~1 ms spin ahead of the step keeps the GPU behind the host's launches, so each event
+        # a ~10 ms spin ahead of the step keeps the GPU behind the host's launches, so each event
         # pair brackets only its kernel (as in the graph replays), not host enqueue gaps
-        torch.cuda._sleep(2_000_000)
+        torch.cuda._sleep(20_000_000)
         tr.step(sb, sl, probe=probe)
     torch.cuda.synchronize()
 

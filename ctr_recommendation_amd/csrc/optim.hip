@@ -29,6 +29,8 @@ struct AdamConsts {
   float nss;    // -lr / bias_correction1 (as float)
   float bc2s;   // sqrt(bias_correction2) (as float)
   float rbc2s;  // 1 / sqrt(bias_correction2) (as float; the table-row step multiplies by it)
+  float dmul;   // AdamW's decoupled decay factor 1 - lr * weight_decay (1 for Adam: p * 1 == p exactly)
+  float pad0, pad1, pad2;
 };
 
 // ------------------------------------------------------------------ squared norm partials
@@ -68,6 +70,7 @@ __device__ __forceinline__ float adam_elem(float& p, float& m, float& v, float g
                                            float omb2, float eps, const AdamConsts& k) {
   g = g * coef;
   g = g + wd * p;
+  p = p * k.dmul;   // AdamW: param.mul_(1 - lr * wd) (torch.optim.AdamW); Adam: dmul == 1, exact
   m = m + k.w1 * (g - m);
   v = v * b2;
   v = v + (omb2 * g) * g;
@@ -89,28 +92,34 @@ __device__ __forceinline__ float adam_elem(float& p, float& m, float& v, float g
 // rbc2s = 1/sqrt(bc2) from the host schedule table (column 4, computed in double).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// DW: apply AdamW's decoupled decay p *= dmul (opt-in); the zero-gradient replay of the Adam path
+// instantiates DW = false and skips the multiply -- bit-identical, as p * 1 == p.
+template <bool DW>
 __device__ __forceinline__ float adam_tab1(float p, float& m, float& v, float g, float wd, float b2, float omb2,
-                                           float eps, float w1, float nss, float rbc2s) {
+                                           float eps, const AdamConsts& k) {
   g = __builtin_fmaf(wd, p, g);
-  m = __builtin_fmaf(w1, g - m, m);
+  if (DW) p = p * k.dmul;
+  m = __builtin_fmaf(k.w1, g - m, m);
   v = __builtin_fmaf(omb2 * g, g, v * b2);
-  const float den = __builtin_fmaf(__builtin_amdgcn_sqrtf(v), rbc2s, eps);
-  return __builtin_fmaf(nss * m, __builtin_amdgcn_rcpf(den), p);
+  const float den = __builtin_fmaf(__builtin_amdgcn_sqrtf(v), k.rbc2s, eps);
+  return __builtin_fmaf(k.nss * m, __builtin_amdgcn_rcpf(den), p);
 }
 // four elements; gg already scaled by the clip coefficient (zero for a zero-gradient step)
+template <bool DW>
 __device__ __forceinline__ void adam_tab4(f32x4& pp, f32x4& mm, f32x4& vv, f32x4 gg, float wd, float b2, float omb2,
-                                          float eps, float w1, float nss, float rbc2s) {
+                                          float eps, const AdamConsts& k) {
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     float me = mm[e], ve = vv[e];
-    pp[e] = adam_tab1(pp[e], me, ve, gg[e], wd, b2, omb2, eps, w1, nss, rbc2s);
+    pp[e] = adam_tab1<DW>(pp[e], me, ve, gg[e], wd, b2, omb2, eps, k);
     mm[e] = me;
     vv[e] = ve;
   }
 }
+template <bool DW>
 __device__ __forceinline__ void adam_zero_tab4(f32x4& pp, f32x4& mm, f32x4& vv, float wd, float b2, float omb2,
-                                               float eps, float w1, float nss, float rbc2s) {
-  adam_tab4(pp, mm, vv, (f32x4){0.f, 0.f, 0.f, 0.f}, wd, b2, omb2, eps, w1, nss, rbc2s);
+                                               float eps, const AdamConsts& k) {
+  adam_tab4<DW>(pp, mm, vv, (f32x4){0.f, 0.f, 0.f, 0.f}, wd, b2, omb2, eps, k);
 }
 
 // clip coefficient of clip_grad_norm_ from the sumsq slots (same sequential order as
@@ -389,7 +398,7 @@ __device__ __forceinline__ void adam_table_body(float* __restrict__ p, float* __
         *reinterpret_cast<f32x4*>(ex) = (f32x4){0.f, 0.f, 0.f, 0.f};   // keep `extra` all-zero
       }
     }
-    adam_tab4(pp, mm, vv, gg * coef, wd, b2, omb2, eps, k.w1, k.nss, k.rbc2s);
+    adam_tab4<true>(pp, mm, vv, gg * coef, wd, b2, omb2, eps, k);
     __builtin_nontemporal_store(pp, reinterpret_cast<f32x4*>(p + off));
     __builtin_nontemporal_store(mm, reinterpret_cast<f32x4*>(m + off));
     __builtin_nontemporal_store(vv, reinterpret_cast<f32x4*>(v + off));
@@ -435,7 +444,7 @@ __global__ void __launch_bounds__(256) adam_table_untouched(FBN_ADAM_TABLE_ARGS)
       if (!act[u]) continue;
       const long long r = r0 + u * RPW + lane / G;
       const size_t off = (size_t)r * D + 4 * q;
-      adam_zero_tab4(pp[u], mm[u], vv[u], wd, b2, omb2, eps, k.w1, k.nss, k.rbc2s);
+      adam_zero_tab4<true>(pp[u], mm[u], vv[u], wd, b2, omb2, eps, k);
       __builtin_nontemporal_store(pp[u], reinterpret_cast<f32x4*>(p + off));
       __builtin_nontemporal_store(mm[u], reinterpret_cast<f32x4*>(m + off));
       __builtin_nontemporal_store(vv[u], reinterpret_cast<f32x4*>(v + off));
@@ -482,7 +491,8 @@ __global__ void adam_selftest_kernel(int n, unsigned seed, unsigned long long* d
     g[e] = (d & 3) ? 0.f : st_value(d, -30, -3, true);
   }
   f32x4 pf = p, mf = m, vf = v;
-  adam_tab4(pf, mf, vf, g * coef, wd, b2, omb2, eps, k.w1, k.nss, k.rbc2s);
+  k.dmul = 1.f;
+  adam_tab4<true>(pf, mf, vf, g * coef, wd, b2, omb2, eps, k);
   float dm = 0.f, dv = 0.f, dp = 0.f;
   for (int e = 0; e < 4; ++e) {
     float pe = p[e], me = m[e], ve = v[e];
@@ -531,7 +541,7 @@ struct PendSrc {
   int ring_n;
 };
 
-template <int D>
+template <int D, bool DW>
 __device__ __forceinline__ void replay_rows(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
                                             long long r, int q, int k0, int t, const AdamConsts* __restrict__ win,
                                             int w0, const AdamConsts* __restrict__ table, float wd, float b2,
@@ -548,7 +558,7 @@ __device__ __forceinline__ void replay_rows(float* __restrict__ p, float* __rest
                                                        (size_t)pe * D + 4 * q);
       const float coef = ps.coef_hist[k0];
       const AdamConsts k = win[k0 - w0];
-      adam_tab4(pp, mm, vv, gg * coef, wd, b2, omb2, eps, k.w1, k.nss, k.rbc2s);
+      adam_tab4<DW>(pp, mm, vv, gg * coef, wd, b2, omb2, eps, k);
       s = k0 + 1;
     }
   }
@@ -556,7 +566,7 @@ __device__ __forceinline__ void replay_rows(float* __restrict__ p, float* __rest
     // the rolling window keeps every row within F <= FBN_LAZY_MAX_LAG steps, so the constants of
     // steps k0 .. t-1 are all in the LDS window (a global fallback would turn this into flat loads)
     const AdamConsts k = win[s - w0];
-    adam_zero_tab4(pp, mm, vv, wd, b2, omb2, eps, k.w1, k.nss, k.rbc2s);
+    adam_zero_tab4<DW>(pp, mm, vv, wd, b2, omb2, eps, k);
   }
   *reinterpret_cast<f32x4*>(p + off) = pp;
   *reinterpret_cast<f32x4*>(m + off) = mm;
@@ -565,7 +575,7 @@ __device__ __forceinline__ void replay_rows(float* __restrict__ p, float* __rest
 
 // items [0, n_ent): claiming entries (slot_row != -1); items [n_ent, n_ent + chunk): rows of the
 // rolling window not claimed this step.  nrows_total / F / chunk describe the window.
-template <int D>
+template <int D, bool DW>
 __global__ void __launch_bounds__(256) adam_catchup_kernel(float* __restrict__ p, float* __restrict__ m,
                                                            float* __restrict__ v, const int* __restrict__ slot_row,
                                                            int n_ent, const int* __restrict__ map, long long nrows,
@@ -628,7 +638,7 @@ __global__ void __launch_bounds__(256) adam_catchup_kernel(float* __restrict__ p
       const int rr = __shfl(r, src < 64 ? src : 0, 64);
       const int k0 = __shfl(key, src < 64 ? src : 0, 64);
       if (src >= cnt) continue;
-      replay_rows<D>(p, m, v, rr, q, k0, t, win, w0, table, wd, b2, omb2, eps, ps);
+      replay_rows<D, DW>(p, m, v, rr, q, k0, t, win, w0, table, wd, b2, omb2, eps, ps);
       if (q == 0) {
         last[rr] = t;
         if (ps.pend) ps.pend[rr] = -1;
@@ -638,7 +648,7 @@ __global__ void __launch_bounds__(256) adam_catchup_kernel(float* __restrict__ p
 }
 
 // every row up to `step` (checkpoint / evaluation)
-template <int D>
+template <int D, bool DW>
 __global__ void __launch_bounds__(256) adam_flush_kernel(float* __restrict__ p, float* __restrict__ m,
                                                          float* __restrict__ v, long long nrows, int* __restrict__ last,
                                                          const AdamConsts* __restrict__ table,
@@ -660,7 +670,7 @@ __global__ void __launch_bounds__(256) adam_flush_kernel(float* __restrict__ p, 
     if (r >= nrows) continue;
     const int k0 = last[r];
     if (k0 >= t) continue;
-    replay_rows<D>(p, m, v, r, q, k0, t, win, w0, table, wd, b2, omb2, eps, ps);
+    replay_rows<D, DW>(p, m, v, r, q, k0, t, win, w0, table, wd, b2, omb2, eps, ps);
     if (q == 0) {
       last[r] = t;
       if (ps.pend) ps.pend[r] = -1;
@@ -699,7 +709,7 @@ __global__ void __launch_bounds__(256) adam_touched_kernel(float* __restrict__ p
     f32x4 pp = *reinterpret_cast<f32x4*>(p + off);
     f32x4 mm = *reinterpret_cast<f32x4*>(m + off);
     f32x4 vv = *reinterpret_cast<f32x4*>(v + off);
-    adam_tab4(pp, mm, vv, gg * coef, wd, b2, omb2, eps, k.w1, k.nss, k.rbc2s);
+    adam_tab4<true>(pp, mm, vv, gg * coef, wd, b2, omb2, eps, k);
     *reinterpret_cast<f32x4*>(p + off) = pp;
     *reinterpret_cast<f32x4*>(m + off) = mm;
     *reinterpret_cast<f32x4*>(v + off) = vv;
@@ -763,7 +773,7 @@ __device__ __forceinline__ void adam_commit_body(float* __restrict__ p, float* _
       f32x4 pp = *reinterpret_cast<f32x4*>(p + off);
       f32x4 mm = *reinterpret_cast<f32x4*>(m + off);
       f32x4 vv = *reinterpret_cast<f32x4*>(v + off);
-      adam_tab4(pp, mm, vv, gg * coef, wd, b2, omb2, eps, k.w1, k.nss, k.rbc2s);
+      adam_tab4<true>(pp, mm, vv, gg * coef, wd, b2, omb2, eps, k);
       *reinterpret_cast<f32x4*>(p + off) = pp;
       *reinterpret_cast<f32x4*>(m + off) = mm;
       *reinterpret_cast<f32x4*>(v + off) = vv;
@@ -910,6 +920,17 @@ extern "C" int fbn_adam_dense(float* p, const float* g, float* m, float* v, long
     case 64: hipLaunchKernelGGL((KERNEL<64>), GRID, dim3(256), 0, st, __VA_ARGS__); break;          \
     case 128: hipLaunchKernelGGL((KERNEL<128>), GRID, dim3(256), 0, st, __VA_ARGS__); break;        \
     case 256: hipLaunchKernelGGL((KERNEL<256>), GRID, dim3(256), 0, st, __VA_ARGS__); break;        \
+    default: fbn_set_error("D must be 16/32/64/128/256"); return FBN_ERR_UNSUPPORTED;              \
+  }
+
+// the same for a kernel templated on <D, bool>
+#define FBN_DISPATCH_D_B(KERNEL, B, D, GRID, ...)                                                    \
+  switch (D) {                                                                                      \
+    case 16: hipLaunchKernelGGL((KERNEL<16, B>), GRID, dim3(256), 0, st, __VA_ARGS__); break;       \
+    case 32: hipLaunchKernelGGL((KERNEL<32, B>), GRID, dim3(256), 0, st, __VA_ARGS__); break;       \
+    case 64: hipLaunchKernelGGL((KERNEL<64, B>), GRID, dim3(256), 0, st, __VA_ARGS__); break;       \
+    case 128: hipLaunchKernelGGL((KERNEL<128, B>), GRID, dim3(256), 0, st, __VA_ARGS__); break;     \
+    case 256: hipLaunchKernelGGL((KERNEL<256, B>), GRID, dim3(256), 0, st, __VA_ARGS__); break;     \
     default: fbn_set_error("D must be 16/32/64/128/256"); return FBN_ERR_UNSUPPORTED;              \
   }
 
@@ -1089,7 +1110,8 @@ extern "C" int fbn_step_end(int* step, unsigned long long* rng, double* sumsq, l
 extern "C" int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, int D, const int* slot_row, int n_ent,
                                 const int* map, int F, int parts, int* last, const void* consts_table, const int* step,
                                 float wd, float beta2, float eps, int* pend, const float* ring,
-                                const float* coef_hist, long long ring_stride, int ring_n, void* stream) {
+                                const float* coef_hist, long long ring_stride, int ring_n, int decoupled,
+                                void* stream) {
   if (nrows <= 0) return FBN_OK;
   if (F < 1 || F > FBN_LAZY_MAX_LAG) { fbn_set_error("fbn_adam_catchup: 1 <= F <= 512"); return FBN_ERR_ARG; }
   hipStream_t st = (hipStream_t)stream;
@@ -1109,21 +1131,32 @@ extern "C" int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, i
   // one wave per SCAN items (16 at D >= 64, else 64; sorted and compacted inside the kernel)
   const long long scan = D >= 64 ? 16 : 64;
   const dim3 grid((unsigned)std::min<long long>(cap, (items + 4 * scan - 1) / (4 * scan)));
-  FBN_DISPATCH_D(adam_catchup_kernel, D, grid, p, m, v, slot_row, n_ent, map, nrows, F, chunk,
-                 parts, last, (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+  if (decoupled) {
+    FBN_DISPATCH_D_B(adam_catchup_kernel, true, D, grid, p, m, v, slot_row, n_ent, map, nrows, F, chunk, parts, last,
+                     (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+  } else {
+    FBN_DISPATCH_D_B(adam_catchup_kernel, false, D, grid, p, m, v, slot_row, n_ent, map, nrows, F, chunk, parts, last,
+                     (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+  }
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
 
 extern "C" int fbn_adam_flush(float* p, float* m, float* v, long long nrows, int D, int* last, const void* consts_table,
                               const int* step, float wd, float beta2, float eps, int* pend, const float* ring,
-                              const float* coef_hist, long long ring_stride, int ring_n, void* stream) {
+                              const float* coef_hist, long long ring_stride, int ring_n, int decoupled,
+                              void* stream) {
   if (nrows <= 0) return FBN_OK;
   hipStream_t st = (hipStream_t)stream;
   const float omb2 = (float)(1.0 - (double)beta2);
   const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
-  FBN_DISPATCH_D(adam_flush_kernel, D, group_grid(nrows, D, 16384), p, m, v, nrows, last,
-                 (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+  if (decoupled) {
+    FBN_DISPATCH_D_B(adam_flush_kernel, true, D, group_grid(nrows, D, 16384), p, m, v, nrows, last,
+                     (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+  } else {
+    FBN_DISPATCH_D_B(adam_flush_kernel, false, D, group_grid(nrows, D, 16384), p, m, v, nrows, last,
+                     (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+  }
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

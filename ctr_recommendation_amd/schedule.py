@@ -53,11 +53,13 @@ class OneCycle:
 
 
 def adam_table(total_steps: int, base_lr: float = 1e-3, beta2: float = 0.999,
-               sched: OneCycle = None) -> Tuple[np.ndarray, List[float]]:
-    """float32 [total_steps, 4] rows (1 - beta1, -lr/bc1, sqrt(bc2), 1/sqrt(bc2)) for optimizer steps
-    1..T (column 4: the table-row step multiplies by it), and the lr of each step."""
+               sched: OneCycle = None, decoupled_wd: float = 0.0) -> Tuple[np.ndarray, List[float]]:
+    """float32 [total_steps + 1, 8] rows (1 - beta1, -lr/bc1, sqrt(bc2), 1/sqrt(bc2), dmul, 0, 0, 0)
+    for optimizer steps 1..T (column 4: the table-row step multiplies by it; dmul = 1 - lr * wd,
+    torch.optim.AdamW's decoupled decay, when ``decoupled_wd`` is given, else 1), and the lr of
+    each step.  The extra last row repeats step T (the device counter saturates there)."""
     sched = sched or OneCycle(total_steps, base_lr)
-    tab = np.zeros((total_steps + 1, 4), dtype=np.float32)
+    tab = np.zeros((total_steps + 1, 8), dtype=np.float32)
     lrs = []
     for t in range(1, total_steps + 1):
         lr, b1 = sched.at(t - 1)
@@ -65,7 +67,7 @@ def adam_table(total_steps: int, base_lr: float = 1e-3, beta2: float = 0.999,
         bc1 = 1 - b1 ** step
         bc2 = 1 - beta2 ** step
         step_size = lr / bc1
-        tab[t - 1] = (1 - b1, -step_size, bc2 ** 0.5, 1.0 / bc2 ** 0.5)
+        tab[t - 1, :5] = (1 - b1, -step_size, bc2 ** 0.5, 1.0 / bc2 ** 0.5, 1.0 - lr * decoupled_wd)
         lrs.append(lr)
     tab[total_steps] = tab[total_steps - 1]
     return tab, lrs

@@ -186,7 +186,9 @@ int fbn_sum(const float* x, int n, float* out, float scale, void* stream);
 
 /* ---------------------------------------------------------------- K8 + K9 clip + Adam
  * Replaces clip_grad_norm_(10) (src/train_fibinet.py:119) and torch.optim.Adam with coupled L2
- * (:78,121); the schedule table carries OneCycleLR's lr/beta1 per step (:84-92,122). */
+ * (:78,121); the schedule table carries OneCycleLR's lr/beta1 per step (:84-92,122): 8 floats per
+ * step {1-beta1, -lr/bc1, sqrt(bc2), 1/sqrt(bc2), dmul, 0, 0, 0}, dmul = 1 - lr*wd for the opt-in
+ * AdamW (config/fibinet_config.yaml:62; pass wd = 0 then), 1 for Adam. */
 int fbn_sumsq(const float* x, long long n, const int* n_rows, int row_len, double* out, void* stream);
 int fbn_clip_coef(const double* sumsq, float max_norm, float* coef, float* norm, void* stream);
 /* sumsq (optional): the FBN_SUMSQ_SLOTS norm accumulators -- the kernel then applies
@@ -234,13 +236,15 @@ int fbn_adam_touched(float* p, float* m, float* v, int D, int* map, const float*
  * per-sample gradient vector row r received at step last[r] (-1 = none); ring [ring_n][B][2][D]
  * holds step s's vectors in slot s % ring_n (ring_stride = B*2*D floats, ring_n > F);
  * coef_hist[s] = step s's clip coefficient.  A replay applies that step with the gradient first. */
+/* decoupled: the opt-in AdamW mode (weight decay by the schedule table's dmul = 1 - lr*wd per
+ * step, wd = 0 in the gradient); 0 = Adam with coupled L2, the reference's optimizer. */
 int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, int D, const int* slot_row, int n_ent,
                      const int* map, int F, int parts, int* last, const void* consts_table, const int* step, float wd,
                      float beta2, float eps, int* pend, const float* ring, const float* coef_hist,
-                     long long ring_stride, int ring_n, void* stream);
+                     long long ring_stride, int ring_n, int decoupled, void* stream);
 int fbn_adam_flush(float* p, float* m, float* v, long long nrows, int D, int* last, const void* consts_table,
                    const int* step, float wd, float beta2, float eps, int* pend, const float* ring,
-                   const float* coef_hist, long long ring_stride, int ring_n, void* stream);
+                   const float* coef_hist, long long ring_stride, int ring_n, int decoupled, void* stream);
 /* Single-GPU step tail in ONE launch: fbn_adam_dense (clip from the sumsq slots) on the flat dense
  * parameters + fbn_adam_commit on the table + fbn_step_end; ticket = one device unsigned, zero
  * before the first call (the kernel's last block resets it); max_step / err as fbn_step_end. */

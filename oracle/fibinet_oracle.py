@@ -189,26 +189,72 @@ class OracleTrainer:
     Adam(lr, weight_decay) with coupled L2 (:78), BCELoss (:79), OneCycleLR(max_lr=10*lr,
     pct_start=0.3, div 25, final_div 1000, cos, beta1 cycled 0.95<->0.85) (:84-92),
     zero_grad -> fwd -> BCE -> bwd -> clip_grad_norm_(10) -> step -> sched.step (:113-123).
+
+    Opt-in variants the build offers (non-parity with the reference's code, which uses Adam):
+    optimizer="adamw" -> torch.optim.AdamW (the config's dead ``optimizer: adamw``,
+    config/fibinet_config.yaml:62); table_optimizer="sparse" -> item_emb.weight is updated only
+    on the rows the batch touches (torch.optim.SparseAdam's rule: moments and weights of the other
+    rows stay as they are; bias corrections of the global step), with the optimizer's weight-decay
+    rule applied to those rows.
     """
 
     def __init__(self, model: OracleFiBiNET, lr: float = 1e-3, weight_decay: float = 1e-5,
-                 total_steps: int = 1000, max_norm: float = 10.0):
+                 total_steps: int = 1000, max_norm: float = 10.0, optimizer: str = "adam",
+                 table_optimizer: str = "dense"):
         self.model = model
         self.max_norm = max_norm            # train_fibinet.py:119 uses 10.0; tests lower it to engage the clip
         self.last_total_norm = None
-        self.opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=weight_decay)
+        self.sparse_table = table_optimizer == "sparse"
+        self.decoupled = optimizer == "adamw"
+        params = [p for n, p in model.named_parameters() if not (self.sparse_table and n == "item_emb.weight")]
+        cls = torch.optim.AdamW if self.decoupled else torch.optim.Adam
+        self.opt = cls(params, lr=lr, weight_decay=weight_decay)
         self.loss_fn = nn.BCELoss()
         self.sched = torch.optim.lr_scheduler.OneCycleLR(
             self.opt, max_lr=lr * 10, total_steps=total_steps, pct_start=0.3,
             div_factor=25.0, final_div_factor=1000.0)
+        self.t = 0
+        if self.sparse_table:
+            E = model.item_emb.weight
+            self.Em, self.Ev = torch.zeros_like(E), torch.zeros_like(E)
+
+    def _sparse_table_step(self, batch) -> None:
+        E = self.model.item_emb.weight
+        ids = [batch["item_id"].long().flatten()]
+        if "item_seq" in batch:
+            ids.append(batch["item_seq"].long().flatten())
+        rows = torch.unique(torch.cat(ids))
+        rows = rows[rows != 0]                                 # padding_idx=0 never receives a gradient
+        grp = self.opt.param_groups[0]
+        lr, (b1, b2), wd, eps = grp["lr"], grp["betas"], grp["weight_decay"], grp["eps"]
+        t = self.t
+        with torch.no_grad():
+            p = E[rows]
+            g = E.grad[rows]
+            if self.decoupled:
+                p = p * (1 - lr * wd)
+            else:
+                g = g + wd * p
+            m = self.Em[rows].lerp(g, 1 - b1)
+            v = self.Ev[rows] * b2 + (1 - b2) * g * g
+            bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
+            p = p + (-lr / bc1) * m / (v.sqrt() / math.sqrt(bc2) + eps)
+            E[rows] = p
+            self.Em[rows] = m
+            self.Ev[rows] = v
 
     def step(self, batch, labels, masks=None) -> Tuple[float, torch.Tensor]:
         self.model.train()
         self.opt.zero_grad()
+        if self.sparse_table:
+            self.model.item_emb.weight.grad = None
         y = self.model(batch, masks=masks)
         loss = self.loss_fn(y, labels)
         loss.backward()
         self.last_total_norm = float(torch.nn.utils.clip_grad_norm_(self.model.parameters(), max_norm=self.max_norm))
+        self.t += 1
+        if self.sparse_table:
+            self._sparse_table_step(batch)
         self.opt.step()
         self.sched.step()
         return float(loss.item()), y.detach()

@@ -109,6 +109,7 @@ def test_schedule_matches_torch_onecycle_and_adam():
         assert tab[t - 1][1] == np.float32(-(lr / (1 - b1 ** t)))
         assert tab[t - 1][2] == np.float32((1 - 0.999 ** t) ** 0.5)
         assert tab[t - 1][3] == np.float32(1.0 / (1 - 0.999 ** t) ** 0.5)
+        assert tab[t - 1][4] == 1.0
         ol, ob = one_cycle_lr_beta1(t - 1, total)
         assert abs(ol - lr) < 1e-15 and abs(ob - b1) < 1e-15
         p.grad = torch.ones(3)
