@@ -89,6 +89,8 @@ __device__ __forceinline__ float adam_elem(float& p, float& m, float& v, float g
 // sqrt.  Every table kernel (eager pass, lazy replay, touched / deferred commit, flush) uses this one
 // function, so the lazy replay stays bit-identical to eager dense Adam; the deviation from the IEEE
 // step is bounded by fbn_adam_selftest (a few ulp of the update, far inside the parity tolerance).
+// The dense parameters use the same step (adam_dense_body): adam_elem, the IEEE form in torch's
+// operation order, remains as the self-test's reference.
 // rbc2s = 1/sqrt(bc2) from the host schedule table (column 4, computed in double).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -146,20 +148,15 @@ __device__ __forceinline__ void adam_dense_body(float* __restrict__ p, const flo
     f32x4 mm = *reinterpret_cast<f32x4*>(m + 4 * i);
     f32x4 vv = *reinterpret_cast<f32x4*>(v + 4 * i);
     const f32x4 gg = *reinterpret_cast<const f32x4*>(g + 4 * i);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float pe = pp[e], me = mm[e], ve = vv[e];
-      adam_elem(pe, me, ve, gg[e], coef, wd, b2, omb2, eps, k);
-      pp[e] = pe; mm[e] = me; vv[e] = ve;
-    }
+    adam_tab4<true>(pp, mm, vv, gg * coef, wd, b2, omb2, eps, k);
     *reinterpret_cast<f32x4*>(p + 4 * i) = pp;
     *reinterpret_cast<f32x4*>(m + 4 * i) = mm;
     *reinterpret_cast<f32x4*>(v + 4 * i) = vv;
   }
   for (long long i = n4 * 4 + bid * blockDim.x + threadIdx.x; i < n; i += nblk * blockDim.x) {
-    float pp = p[i], mm = m[i], vv = v[i];
-    adam_elem(pp, mm, vv, g[i], coef, wd, b2, omb2, eps, k);
-    p[i] = pp; m[i] = mm; v[i] = vv;
+    float mm = m[i], vv = v[i];
+    p[i] = adam_tab1<true>(p[i], mm, vv, g[i] * coef, wd, b2, omb2, eps, k);
+    m[i] = mm; v[i] = vv;
   }
 }
 
@@ -575,6 +572,19 @@ __device__ __forceinline__ void replay_rows(float* __restrict__ p, float* __rest
 
 // items [0, n_ent): claiming entries (slot_row != -1); items [n_ent, n_ent + chunk): rows of the
 // rolling window not claimed this step.  nrows_total / F / chunk describe the window.
+// In-kernel row claims (single GPU, fbn_adam_claim_catchup): item != null -> entry e = b*(L+1)+t
+// claims its row as claim_rows_kernel does (first CAS wins; map, slot_row, dup written), and a
+// winning entry's row joins the replay at once -- one launch instead of claim + catch-up.
+struct ClaimSrc {
+  const int64_t* item;
+  const int64_t* seq;
+  int L;
+  long long V;
+  int* map;
+  int* slot_row;
+  int* dup;
+};
+
 template <int D, bool DW>
 __global__ void __launch_bounds__(256) adam_catchup_kernel(float* __restrict__ p, float* __restrict__ m,
                                                            float* __restrict__ v, const int* __restrict__ slot_row,
@@ -582,7 +592,7 @@ __global__ void __launch_bounds__(256) adam_catchup_kernel(float* __restrict__ p
                                                            int F, long long chunk, int parts, int* __restrict__ last,
                                                            const AdamConsts* __restrict__ table,
                                                            const int* __restrict__ step, float wd, float b2,
-                                                           float omb2, float eps, PendSrc ps) {
+                                                           float omb2, float eps, PendSrc ps, ClaimSrc cs) {
   constexpr int G = D / 4, RPW = 64 / G;
   __shared__ AdamConsts win[FBN_LAZY_MAX_LAG];
   const int t = *step;
@@ -608,7 +618,22 @@ __global__ void __launch_bounds__(256) adam_catchup_kernel(float* __restrict__ p
     const long long i = i0 + lane;
     int r = -1, key = 0x7fffffff;
     if (lane < SCAN && i < n) {
-      if (i < n_ent) {
+      if (i < n_ent && cs.item) {
+        const long long b = i / (cs.L + 1), tt = i - b * (cs.L + 1);
+        const long long id = tt == 0 ? cs.item[b] : cs.seq[b * cs.L + (tt - 1)];
+        int owner = -1;
+        if (id > 0 && id < cs.V) {
+          int expected = -1;
+          if (__hip_atomic_compare_exchange_strong(cs.map + id, &expected, (int)i, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)) {
+            cs.slot_row[i] = (int)id;
+            r = (int)id;
+          } else {
+            owner = expected;
+          }
+        }
+        if (cs.dup) cs.dup[i] = owner;
+      } else if (i < n_ent) {
         const int sr = slot_row[i];
         if (sr != -1) r = sr & ~FBN_SLOT_FLAG;
       } else {
@@ -1071,10 +1096,12 @@ extern "C" int fbn_adam_step_tail(float* dp, const float* dg, float* dm, float* 
   const PendSrc ps{pend, ring, coef_hist, (long long)B * 2 * D, ring_n};
   const StepEnd se{step, rng, (double*)sumsq, nbt0, nbt1, ticket, max_step, err};
   long long nd = (n_dense / 4 + 255) / 256;
-  if (nd > 512) nd = 512;
+  // few, fat blocks: every block draws the step-end ticket (one returning atomic on one word,
+  // ~88 per microsecond chip-wide), so the block count, not the work, sets the tail's floor
+  if (nd > 256) nd = 256;
   if (nd < 1) nd = 1;
   long long nc = ((long long)(n > 0 ? n : 1) + 255) / 256;
-  if (nc > 2048) nc = 2048;
+  if (nc > 256) nc = 256;
   FBN_DISPATCH_D(adam_tail_kernel, D, dim3((unsigned)(nd + nc)), dp, dg, dm, dv, n_dense, (int)nd, max_norm, coef_out,
                  norm_out, p, m, v, map, s, n, (const AdamConsts*)consts_table, wd, beta2, omb2, eps, last, ps,
                  coef_hist, B, se);
@@ -1131,12 +1158,48 @@ extern "C" int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, i
   // one wave per SCAN items (16 at D >= 64, else 64; sorted and compacted inside the kernel)
   const long long scan = D >= 64 ? 16 : 64;
   const dim3 grid((unsigned)std::min<long long>(cap, (items + 4 * scan - 1) / (4 * scan)));
+  const ClaimSrc cs{nullptr, nullptr, 0, 0, nullptr, nullptr, nullptr};
   if (decoupled) {
     FBN_DISPATCH_D_B(adam_catchup_kernel, true, D, grid, p, m, v, slot_row, n_ent, map, nrows, F, chunk, parts, last,
-                     (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+                     (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, cs);
   } else {
     FBN_DISPATCH_D_B(adam_catchup_kernel, false, D, grid, p, m, v, slot_row, n_ent, map, nrows, F, chunk, parts, last,
-                     (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+                     (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, cs);
+  }
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+// single GPU: fbn_claim_rows + fbn_adam_catchup(parts = 1) in one launch (see ClaimSrc)
+extern "C" int fbn_adam_claim_catchup(const int64_t* item, const int64_t* seq, int B, int L, long long V, int* map,
+                                      int* slot_row, int* dup, float* p, float* m, float* v, long long nrows, int D,
+                                      int F, int* last, const void* consts_table, const int* step, float wd,
+                                      float beta2, float eps, int* pend, const float* ring, const float* coef_hist,
+                                      long long ring_stride, int ring_n, int decoupled, void* stream) {
+  const long long n = (long long)B * (L + 1);
+  if (n <= 0 || nrows <= 0) return FBN_OK;
+  if (!item || (L > 0 && !seq) || !map || !slot_row) {
+    fbn_set_error("fbn_adam_claim_catchup: item, seq (L > 0), map and slot_row are required");
+    return FBN_ERR_ARG;
+  }
+  if (F < 1 || F > FBN_LAZY_MAX_LAG) { fbn_set_error("fbn_adam_claim_catchup: 1 <= F <= 512"); return FBN_ERR_ARG; }
+  if (pend && (!ring || !coef_hist || ring_n <= F)) {
+    fbn_set_error("fbn_adam_claim_catchup: deferred gradients need ring, coef_hist and ring_n > F");
+    return FBN_ERR_ARG;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const float omb2 = (float)(1.0 - (double)beta2);
+  const long long chunk = (nrows + F - 1) / F;
+  const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
+  const ClaimSrc cs{item, L > 0 ? seq : nullptr, L, V, map, slot_row, dup};
+  const long long scan = D >= 64 ? 16 : 64;
+  const dim3 grid((unsigned)std::min<long long>(8192, (n + 4 * scan - 1) / (4 * scan)));
+  if (decoupled) {
+    FBN_DISPATCH_D_B(adam_catchup_kernel, true, D, grid, p, m, v, slot_row, (int)n, map, nrows, F, chunk, 1, last,
+                     (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, cs);
+  } else {
+    FBN_DISPATCH_D_B(adam_catchup_kernel, false, D, grid, p, m, v, slot_row, (int)n, map, nrows, F, chunk, 1, last,
+                     (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, cs);
   }
   FBN_CHECK_LAUNCH();
   return FBN_OK;

@@ -220,14 +220,21 @@ class FiBiNETTrainer:
 
         lazy = self.table_adam == "lazy"
 
-        def catch_up(n_ent):
+        def catch_up(n_ent, claim=False):
             # lazy table Adam: the rows claimed this step are brought to `step` Adam steps before
             # anything reads them; the rolling window (step % F; unclaimed rows, read by nothing
-            # this step) replays on the side stream beside the rest of the step
+            # this step) replays on the side stream beside the rest of the step.  claim (single
+            # GPU): the row claims are made inside the same launch (fbn_adam_claim_catchup)
             ev = _events(probe, "adam_catchup")
-            call("fbn_adam_catchup", ptr(self.E), ptr(self.Em), ptr(self.Ev), self.rows_local, d, ptr(self.slot_row),
-                 n_ent, ptr(self.map), self.lazy_window, 1, ptr(self.last), ptr(self.sched), ptr(self.step_dev),
-                 self.wd_g, self.beta2, self.eps, *self._pend_args(), int(self.decoupled), st)
+            if claim:
+                call("fbn_adam_claim_catchup", ptr(batch["item_id"]), ptr(seq) if L else None, B, L, self.V,
+                     ptr(self.map), ptr(self.slot_row), ptr(self.dup), ptr(self.E), ptr(self.Em), ptr(self.Ev),
+                     self.rows_local, d, self.lazy_window, ptr(self.last), ptr(self.sched), ptr(self.step_dev),
+                     self.wd_g, self.beta2, self.eps, *self._pend_args(), int(self.decoupled), st)
+            else:
+                call("fbn_adam_catchup", ptr(self.E), ptr(self.Em), ptr(self.Ev), self.rows_local, d,
+                     ptr(self.slot_row), n_ent, ptr(self.map), self.lazy_window, 1, ptr(self.last), ptr(self.sched),
+                     ptr(self.step_dev), self.wd_g, self.beta2, self.eps, *self._pend_args(), int(self.decoupled), st)
             _events_end(ev)
             self.side.wait_stream(main)
             ev = _events(probe, "adam_window", self.side)
@@ -260,11 +267,11 @@ class FiBiNETTrainer:
             rows = self.xchg.forward(batch["item_id"], seq, self.E, {"map": self.map, "slot_row": self.slot_row},
                                      self.err, before_gather=catch_up if lazy else None)
             pos = self.xchg.cur_pos
+        elif lazy:
+            catch_up(B * (L + 1), claim=True)
         else:
             call("fbn_claim_rows", ptr(batch["item_id"]), ptr(seq) if L else None, B, L, self.V, ptr(self.map),
                  ptr(self.slot_row), ptr(self.dup), st)
-            if lazy:
-                catch_up(B * (L + 1))
         if w16_ev is not None:
             main.wait_event(w16_ev)
         a = ops.forward(self.p, batch, cfg, self.rng, table_rows=rows, pos=pos, err=self.err, labels=labels,

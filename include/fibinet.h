@@ -242,6 +242,14 @@ int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, int D, const
                      const int* map, int F, int parts, int* last, const void* consts_table, const int* step, float wd,
                      float beta2, float eps, int* pend, const float* ring, const float* coef_hist,
                      long long ring_stride, int ring_n, int decoupled, void* stream);
+/* Single GPU: fbn_claim_rows + fbn_adam_catchup(parts = 1) in ONE launch -- each entry claims its
+ * row (first CAS wins: map, slot_row, dup as fbn_claim_rows) and a winning entry's row is brought
+ * up to date at once. */
+int fbn_adam_claim_catchup(const int64_t* item, const int64_t* seq, int B, int L, long long V, int* map, int* slot_row,
+                           int* dup, float* p, float* m, float* v, long long nrows, int D, int F, int* last,
+                           const void* consts_table, const int* step, float wd, float beta2, float eps, int* pend,
+                           const float* ring, const float* coef_hist, long long ring_stride, int ring_n, int decoupled,
+                           void* stream);
 int fbn_adam_flush(float* p, float* m, float* v, long long nrows, int D, int* last, const void* consts_table,
                    const int* step, float wd, float beta2, float eps, int* pend, const float* ring,
                    const float* coef_hist, long long ring_stride, int ring_n, int decoupled, void* stream);

@@ -2,7 +2,7 @@
 
   python tools/step_timeline.py run_kernel_trace.csv [--steps N] [--verbose]
 
-Steps are split at claim_rows_kernel.  The rolling-window Adam replay (adam_catchup on 256
+Steps are split at claim_rows_kernel (or, fused, the claimed-row adam_catchup).  The rolling-window Adam replay (adam_catchup on 256
 workgroups) runs on the side stream; every other kernel is on the main stream.  Prints, per step,
 the span, the main stream's busy time and idle gaps, the window's span, and (--verbose) the
 kernels in order with their durations and how much of each overlapped the window.
@@ -20,6 +20,11 @@ def main():
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"],
                  int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0)) for r in rows)
     starts = [i for i, e in enumerate(ev) if "claim_rows" in e[2]]
+    if not starts:
+        # fused claim + catch-up (lazy single GPU): steps start at the claimed-row catch-up, the
+        # adam_catchup launch with the largest grid
+        gmax = max((e[3] for e in ev if "adam_catchup" in e[2]), default=0)
+        starts = [i for i, e in enumerate(ev) if "adam_catchup" in e[2] and e[3] == gmax]
     match = sys.argv[sys.argv.index("--match") + 1] if "--match" in sys.argv else "gemm_dma16"
     # steps of the run being studied (bench.py also times an fp32 run: its GEMMs are gemm_kernel)
     starts = [s for j, s in enumerate(starts[:-1]) if any(match in e[2] for e in ev[s:starts[j + 1]])] + starts[-1:]
