@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=20)
     ap.add_argument("--probe-steps", type=int, default=10)
     ap.add_argument("--batches", type=int, default=0, help="distinct HBM-resident batches (default F + 32)")
+    ap.add_argument("--lazy-window", type=int, default=128, help="lazy table-Adam window F (rows per step: V/F)")
     ap.add_argument("--no-fp32", dest="also_fp32", action="store_false",
                     help="skip the second (fp32) C3 measurement embedded in the line")
     return ap.parse_args()
@@ -144,7 +145,7 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
     V = args.rows_per_gpu * world
     cfg = {"embedding_dim": d, "vocab_size": V, "compute_dtype": dtype}
     K, W = args.steps, args.warmup
-    F = 128                                   # lazy table-Adam window (FiBiNETTrainer default)
+    F = args.lazy_window                      # lazy table-Adam window (FiBiNETTrainer default 128)
     # fresh ids every step: more distinct HBM-resident batches than the window F, so every row a
     # timed step claims was last touched at the lag fresh uniform ids give (bounded by F), never
     # replayed from a batch seen a few steps earlier

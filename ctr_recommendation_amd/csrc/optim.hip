@@ -554,14 +554,16 @@ __device__ __forceinline__ void replay_rows(float* __restrict__ p, float* __rest
       const f32x4 gg = *reinterpret_cast<const f32x4*>(ps.ring + (size_t)(k0 % ps.ring_n) * ps.ring_stride +
                                                        (size_t)pe * D + 4 * q);
       const float coef = ps.coef_hist[k0];
-      const AdamConsts k = win[k0 - w0];
+      const AdamConsts k = k0 >= w0 ? win[k0 - w0] : table[k0];
       adam_tab4<DW>(pp, mm, vv, gg * coef, wd, b2, omb2, eps, k);
       s = k0 + 1;
     }
   }
+  // the rolling window keeps every row within F steps, so the constants of steps k0 .. t-1 sit in
+  // the LDS window [w0, t); steps before w0 (a row the window has not reached: only if F changed)
+  // read the global table in a loop of their own, so the hot loop's reads stay ds_read
+  for (; s < t && s < w0; ++s) adam_zero_tab4<DW>(pp, mm, vv, wd, b2, omb2, eps, table[s]);
   for (; s < t; ++s) {
-    // the rolling window keeps every row within F <= FBN_LAZY_MAX_LAG steps, so the constants of
-    // steps k0 .. t-1 are all in the LDS window (a global fallback would turn this into flat loads)
     const AdamConsts k = win[s - w0];
     adam_zero_tab4<DW>(pp, mm, vv, wd, b2, omb2, eps, k);
   }
@@ -596,7 +598,8 @@ __global__ void __launch_bounds__(256) adam_catchup_kernel(float* __restrict__ p
   constexpr int G = D / 4, RPW = 64 / G;
   __shared__ AdamConsts win[FBN_LAZY_MAX_LAG];
   const int t = *step;
-  const int w0 = t > FBN_LAZY_MAX_LAG ? t - FBN_LAZY_MAX_LAG : 0;
+  // every row is within F steps of t (the rolling window): only steps [t - F, t) are staged
+  const int w0 = t > F ? t - F : 0;
   for (int i = threadIdx.x; i < t - w0; i += blockDim.x) {
     win[i] = table[w0 + i];
   }

@@ -148,14 +148,19 @@ def test_bf16_mode_tracks_fp32(hip_device):
     assert abs(a32 - a16) < 5e-3, (a32, a16)
 
 
-@pytest.mark.parametrize("window", [4, 128])
+@pytest.mark.parametrize("window", [4, 128, "8->2"])
 def test_lazy_table_adam_matches_eager(hip_device, window):
     """Lazy table Adam (zero-gradient steps replayed when a row is claimed, its rolling window
     comes round, or at flush) against the eager per-step pass over every row.  Rows no batch
     touched are written by the replay alone: bit-identical.  Touched rows and dense params may
     differ only by the float-atomic fold of duplicate rows (order-dependent last bits that
-    Adam's sign-like early steps can turn into O(lr) flips in ANY two runs)."""
+    Adam's sign-like early steps can turn into O(lr) flips in ANY two runs).  "8->2": the window
+    shrinks mid-run, so rows lag more than F steps and replay their oldest steps from the global
+    schedule table (the path outside the LDS-staged window)."""
     V, B, steps = 6000, 128, 12
+    shrink = window == "8->2"
+    if shrink:
+        window = 8
     cfg = {"embedding_dim": 128, "vocab_size": V}
     torch.manual_seed(0)
     init = oracle_build(None, cfg).state_dict()
@@ -164,6 +169,8 @@ def test_lazy_table_adam_matches_eager(hip_device, window):
                           lazy_window=window)
     touched = torch.zeros(V, dtype=torch.bool)
     for s in range(steps):
+        if shrink and s == 6:
+            lazy.lazy_window = 2
         b, y = make_batch(60 + s, B, V)
         touched[b["item_id"]] = True
         touched[b["item_seq"].flatten()] = True
