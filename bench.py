@@ -190,6 +190,10 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
     def run_step(i):
         if graphs:
             graphs[i % nb].replay()
+        elif world > 1:
+            # N > 1: the next batch is routed during this step (no mid-step host sync)
+            b, y = batches[i % nb]
+            tr.step(b, y, next_batch=batches[(i + 1) % nb][0])
         else:
             load(i)
             tr.step(sb, sl)

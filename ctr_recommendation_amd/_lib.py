@@ -41,7 +41,8 @@ SIGNATURES = {
     "fbn_bn_bwd_fused": (I, [P, P, P, P, F, P, P, P, P, I, I, D, P, P, P, P, P, P, P, P]),
     "fbn_colsum_partial": (I, [P, I, I, I, P, P]),
     "fbn_sum_jobs": (I, [P, I, P]),
-    "fbn_fields_fwd": (I, [P, P, P, P, P, P, P, F, P, I, P, LL, P, P, P, P, P, I, P, P, P, P, I, I, P, P, P, P, P, I, I, I, P]),
+    "fbn_fields_fwd": (I, [P, P, P, P, P, P, P, F, P, I, P, LL, P, P, P, P, P, I, P, P, P, P, I, I, P, P, P, P, P, I, I, I, I,
+                           P]),
     "fbn_fields_bwd_partials_size": (I, [I, I, I]),
     "fbn_fields_bwd_grid": (I, [I, I]),
     "fbn_fields_bwd": (I, [P, P, P, P, P, P, P, F, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P, P, P, LL, P, P, I, I,
@@ -88,7 +89,7 @@ SIGNATURES = {
     "fbn_step_end": (I, [P, P, P, P, P, I, P, P]),
     "fbn_route": (I, [P, P, I, I, LL, LL, I, P, P, P, P, P, P, P]),
     "fbn_owner_claim": (I, [P, I, P, P, I, P]),
-    "fbn_owner_gather": (I, [P, I, P, P, P, P, I, I, P]),
+    "fbn_owner_gather": (I, [P, I, P, P, P, P, I, I, I, P]),
     "fbn_collate": (I, [P, I, P, P, I, I, P, P, P, P, P, LL, P, I, P, P, P, P, P, P, P, P, P]),
     "fbn_collate_zero_if": (I, [P, LL, P, P]),
 }

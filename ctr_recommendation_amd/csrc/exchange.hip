@@ -68,7 +68,8 @@ __global__ void route_fill_kernel(const int64_t* __restrict__ item, const int64_
 // reads row 0) but never registered for a gradient.
 template <int D>
 __global__ void __launch_bounds__(256) owner_gather_kernel(const int* __restrict__ ids, int n, const float* __restrict__ E,
-                                                           float* __restrict__ out, int* map, int* slot_row, int rank) {
+                                                           float* __restrict__ out, int* map, int* slot_row, int rank,
+                                                           int out_bf16) {
   constexpr int G = D / 4, RPW = 64 / G;
   const int lane = threadIdx.x & 63, q = lane % G;
   const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -77,7 +78,12 @@ __global__ void __launch_bounds__(256) owner_gather_kernel(const int* __restrict
     const long long i = i0 + lane / G;
     if (i >= n) continue;
     const int r = ids[i];
-    *reinterpret_cast<f32x4*>(out + i * D + 4 * q) = *reinterpret_cast<const f32x4*>(E + (size_t)r * D + 4 * q);
+    const f32x4 row = *reinterpret_cast<const f32x4*>(E + (size_t)r * D + 4 * q);
+    if (out_bf16)   // bf16 mode: the rows cross the wire as bf16 (half the all-to-all bytes)
+      *reinterpret_cast<bf16x4*>(reinterpret_cast<short*>(out) + i * D + 4 * q) =
+          (bf16x4){f2bf(row[0]), f2bf(row[1]), f2bf(row[2]), f2bf(row[3])};
+    else
+      *reinterpret_cast<f32x4*>(out + i * D + 4 * q) = row;
     if (map && q == 0 && !(rank == 0 && r == 0) &&
         __hip_atomic_load(map + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == -1) {
       int expected = -1;
@@ -148,11 +154,11 @@ static dim3 rows_grid(long long n, int D) {
   return dim3((unsigned)blocks);
 }
 
-extern "C" int fbn_owner_gather(const int* ids, int n, const float* E, float* out, int* map, int* slot_row, int rank,
-                                int D, void* stream) {
+extern "C" int fbn_owner_gather(const int* ids, int n, const float* E, void* out, int* map, int* slot_row, int rank,
+                                int D, int out_bf16, void* stream) {
   if (n <= 0) return FBN_OK;
   hipStream_t st = (hipStream_t)stream;
-  FBN_DISPATCH_D(owner_gather_kernel, D, rows_grid(n, D), ids, n, E, out, map, slot_row, rank);
+  FBN_DISPATCH_D(owner_gather_kernel, D, rows_grid(n, D), ids, n, E, (float*)out, map, slot_row, rank, out_bf16);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

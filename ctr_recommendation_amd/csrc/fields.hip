@@ -100,6 +100,17 @@ __device__ __forceinline__ void senet_excite(const float (&z)[6], const float* w
   }
 }
 
+// row r of the exchanged row buffer (MODE 1: f32 rows; MODE 2: bf16 rows, the bf16 mode's wire format)
+template <int D, int MODE>
+__device__ __forceinline__ f32x4 load_row(const FieldArgs& p, size_t r, int q) {
+  if constexpr (MODE == 2) {
+    const bf16x4 h = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const short*>(p.table) + r * D + 4 * q);
+    return (f32x4){bf2f(h[0]), bf2f(h[1]), bf2f(h[2]), bf2f(h[3])};
+  } else {
+    return *reinterpret_cast<const f32x4*>(p.table + r * D + 4 * q);
+  }
+}
+
 template <int D, int MODE>
 __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
   constexpr int G = D / 4;                  // lanes per sample
@@ -129,13 +140,13 @@ __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
     f32x4 rit = {0.f, 0.f, 0.f, 0.f};
     f32x4 hs = {0.f, 0.f, 0.f, 0.f};
     int nnz = 0;
-    const int* pb = MODE == 1 ? p.pos + (size_t)b * (L + 1) : nullptr;
+    const int* pb = MODE >= 1 ? p.pos + (size_t)b * (L + 1) : nullptr;
     if (MODE == 0) {
       if (item < 0 || item >= p.V) { bad = true; item = -1; }
       if (item >= 0) rit = *reinterpret_cast<const f32x4*>(p.table + item * D + 4 * q);
     } else {
       const int pi = pb[0];
-      if (pi >= 0) rit = *reinterpret_cast<const f32x4*>(p.table + (size_t)pi * D + 4 * q);
+      if (pi >= 0) rit = load_row<D, MODE>(p, pi, q);
     }
     // all history ids in ONE round (lane q of the group holds slots q, q+G, ...), broadcast by
     // shuffles, then every row load is issued before any is consumed (two dependent round trips
@@ -169,7 +180,7 @@ __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
 #pragma unroll
           for (int j = 0; j < IPL; ++j)
             if ((t / G) == j) r = __shfl(sid[j], gbase + (t % G), 64);
-          if (r >= 0) { hist[u] = *reinterpret_cast<const f32x4*>(p.table + (size_t)r * D + 4 * q); ++nnz; }
+          if (r >= 0) { hist[u] = load_row<D, MODE>(p, r, q); ++nnz; }
         }
       }
 #pragma unroll
@@ -590,7 +601,7 @@ extern "C" int fbn_fields_fwd(const int64_t* item_id, const int64_t* item_seq, c
                               const float* b2, int R, float* X, float* Vc, short* Vc16, void* c, int ldc, int c_bf16,
                               float* a_out,
                               float* cnt_out, int* err, int* map, int* slot_row, int B, int L,
-                              int D, void* stream) {
+                              int D, int rows_bf16, void* stream) {
   if (B <= 0) return FBN_OK;
   if (L < 0 || L > 32 || R < 1 || R > FBN_MAXR || (ldc & 3)) {
     fbn_set_error("fbn_fields_fwd: need 0 <= L <= 32, 1 <= R <= 8, ldc % 4 == 0");
@@ -603,6 +614,7 @@ extern "C" int fbn_fields_fwd(const int64_t* item_id, const int64_t* item_seq, c
   a.X = X; a.Vc = Vc; a.Vc16 = Vc16; a.c = c; a.a_out = a_out; a.cnt_out = cnt_out; a.err = err;
   a.map = map; a.slot_row = slot_row;
   a.V = V; a.B = B; a.L = L; a.ldc = ldc; a.R = R; a.n_cate = n_cate; a.ln_eps = ln_eps; a.c16 = c_bf16;
+  if (pos && rows_bf16) return launch_fields_fwd<2>(a, D, (hipStream_t)stream);
   if (pos) return launch_fields_fwd<1>(a, D, (hipStream_t)stream);
   return launch_fields_fwd<0>(a, D, (hipStream_t)stream);
 }

@@ -13,8 +13,11 @@ Backward (the sparse reduce-scatter):
   fields_bwd writes one gradient row per routed entry  ->  all_to_all(rows)  ->  the received
   rows are the owner's sparse gradient (slot = received entry; fbn_sparse_fixup folds rows hit
   by several entries into the entry that claimed the row in the forward).
-Split sizes need one host read of the N routed counts per step (all_to_all_single takes
-host split lists); everything else stays on the device.
+Split sizes need a host read of the N routed counts per step (all_to_all_single takes host
+split lists).  ``prepare(next_batch)`` takes that read off the critical path: the next batch is
+routed and its counts exchanged on a side stream while the current step runs, and the counts
+land in pinned host memory -- the next forward reads them without waiting on the main stream
+(two routing buffer sets alternate).  Without it the forward reads them inline (one sync).
 """
 from __future__ import annotations
 
@@ -39,24 +42,40 @@ class HipExchangeKernels:
 
     def owner_gather(self, ids, E, out, map_, slot_row, rank, d):
         call("fbn_owner_gather", ptr(ids), ids.shape[0], ptr(E), ptr(out), ptr(map_), ptr(slot_row), rank, d,
+             int(out.dtype == torch.bfloat16),
              _lib.stream_handle(E.device))
 
 
 class RowExchange:
     def __init__(self, rank: int, world: int, V: int, d: int, B: int, L: int, device, group=None, kernels=None,
-                 stage_on_cpu: bool = False):
+                 stage_on_cpu: bool = False, rows_bf16: bool = False):
         self.rank, self.world, self.V, self.d, self.L = rank, world, V, d, L
         self.Vl = (V + world - 1) // world
         self.group = group
         self.k = kernels or HipExchangeKernels()
         self.device = device
         self.stage_on_cpu = stage_on_cpu          # gloo on a GPU box: collectives on host copies
+        # bf16 mode: looked-up rows cross the wire as bf16 (half the forward all-to-all bytes; the
+        # fields kernel widens them on load); gradient rows stay f32
+        self.row_dtype = torch.bfloat16 if rows_bf16 else torch.float32
         i32 = dict(dtype=torch.int32, device=device)
-        self.counts = torch.zeros(world, **i32)
-        self.offsets = torch.zeros(world + 1, **i32)
-        self.cursor = torch.zeros(world, **i32)
-        self.send_ids = torch.empty(B * (L + 1), **i32)
-        self.pos = torch.empty((B, L + 1), **i32)
+        # two routing buffer sets: the step in flight uses one while prepare() fills the other
+        self.sets = []
+        for _ in range(2):
+            self.sets.append({"counts": torch.zeros(world, **i32), "offsets": torch.zeros(world + 1, **i32),
+                              "cursor": torch.zeros(world, **i32), "send_ids": torch.empty(B * (L + 1), **i32),
+                              "pos": torch.empty((B, L + 1), **i32), "recv_counts": torch.zeros(world, **i32),
+                              "host": torch.zeros(2 * world, dtype=torch.int32,
+                                                  pin_memory=torch.device(device).type == "cuda"),
+                              "event": None, "key": None})
+        self.cur = 0
+        self.side = None
+        self.route_group = group
+        if torch.device(device).type == "cuda" and world > 1 and dist.is_initialized():
+            self.side = torch.cuda.Stream(device=device)
+            # a communicator of its own: the next batch's counts exchange runs beside this step's
+            # collectives instead of queueing between them (every rank creates it here, in order)
+            self.route_group = dist.new_group(ranks=list(range(world)))
         self.send_counts = None
         self.recv_counts = None
         self.recv_ids = None
@@ -69,14 +88,56 @@ class RowExchange:
     def rows_local(self) -> int:
         return max(0, min(self.V, (self.rank + 1) * self.Vl) - self.rows_lo)
 
-    def _a2a(self, out, inp, out_splits, in_splits):
+    def _a2a(self, out, inp, out_splits, in_splits, group=None):
+        group = group if group is not None else self.group
         if not self.stage_on_cpu:
-            dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+            dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
             return out
         o = out.cpu()
-        dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=self.group)
+        dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=group)
         out.copy_(o)
         return out
+
+    @property
+    def pos(self):
+        return self.sets[self.cur]["pos"]
+
+    def _route(self, st, item, seq, err, group=None):
+        B = item.shape[0]
+        L = 0 if seq is None else seq.shape[1]
+        if L != self.L:
+            st["pos"] = torch.empty((B, L + 1), dtype=torch.int32, device=item.device)
+        pos = st["pos"][:B, :L + 1]
+        self.k.route(item, seq, B, L, self.V, self.Vl, self.world, st["counts"], st["offsets"], st["cursor"],
+                     st["send_ids"], pos, err)
+        self._a2a(st["recv_counts"], st["counts"], None, None, group)
+        return pos
+
+    @staticmethod
+    def _key(item, seq):
+        # the prepared routing is used only for the very tensors it was computed from
+        return (item.data_ptr(), item.shape[0], 0 if seq is None else seq.data_ptr(), 0 if seq is None else seq.shape[1])
+
+    def prepare(self, item, seq, err) -> None:
+        """Route the NEXT step's batch now, on a side stream (HIP device only): its forward then
+        reads the counts from pinned host memory without a sync on the main stream.  It is used by
+        the next forward() only if that forward gets the same (unmodified) id tensors; otherwise
+        that forward routes inline."""
+        if self.side is None:
+            return
+        st = self.sets[1 - self.cur]
+        main = torch.cuda.current_stream(item.device)
+        self.side.wait_stream(main)                 # the ids and the buffer set are free
+        with torch.cuda.stream(self.side):
+            st["pos_view"] = self._route(st, item, seq, err, self.route_group)
+            st["host"][:self.world].copy_(st["counts"], non_blocking=True)
+            st["host"][self.world:].copy_(st["recv_counts"], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+        for t in (item, seq, err):
+            if t is not None:
+                t.record_stream(self.side)
+        st["event"], st["key"] = ev, self._key(item, seq)
 
     def forward(self, item, seq, E_local, sparse, err, before_gather=None) -> torch.Tensor:
         """Returns the requester's row buffer [n_sent, d]; self.pos maps (b, t) -> row (or -1).
@@ -84,26 +145,39 @@ class RowExchange:
         sparse map and gathering them (the lazy table Adam brings them up to date there)."""
         B = item.shape[0]
         L = 0 if seq is None else seq.shape[1]
-        pos = self.pos[:B, :L + 1] if L == self.L else torch.empty((B, L + 1), dtype=torch.int32, device=item.device)
+        nxt = self.sets[1 - self.cur]
+        if nxt["event"] is not None and nxt["key"] == self._key(item, seq):
+            # routed ahead by prepare(): wait for the side stream's copy only, then order the
+            # main stream after the side stream's routing work
+            self.cur = 1 - self.cur
+            st = self.sets[self.cur]
+            st["event"].synchronize()
+            torch.cuda.current_stream(item.device).wait_event(st["event"])
+            st["event"] = None
+            h = st["host"].tolist()
+            sc, rc = h[:self.world], h[self.world:]
+            pos = st["pos_view"]
+        else:
+            if nxt["event"] is not None:              # prepared for other tensors: drop it
+                nxt["event"].synchronize()
+                nxt["event"] = None
+            st = self.sets[self.cur]
+            pos = self._route(st, item, seq, err)
+            sc = st["counts"].tolist()
+            rc = st["recv_counts"].tolist()       # the one host sync of the step
         self.cur_pos = pos.contiguous()
-        self.k.route(item, seq, B, L, self.V, self.Vl, self.world, self.counts, self.offsets, self.cursor,
-                     self.send_ids, self.cur_pos, err)
-        recv_counts = torch.empty_like(self.counts)
-        self._a2a(recv_counts, self.counts, None, None)
-        sc = self.counts.tolist()
-        rc = recv_counts.tolist()                  # the one host sync of the step
         self.send_counts, self.recv_counts = sc, rc
         n_send, n_recv = sum(sc), sum(rc)
         self.recv_ids = torch.empty(n_recv, dtype=torch.int32, device=item.device)
-        self._a2a(self.recv_ids, self.send_ids[:n_send], rc, sc)
-        reply = torch.empty((n_recv, self.d), dtype=torch.float32, device=item.device)
+        self._a2a(self.recv_ids, st["send_ids"][:n_send], rc, sc)
+        reply = torch.empty((n_recv, self.d), dtype=self.row_dtype, device=item.device)
         if before_gather is not None and sparse.get("map") is not None:
             self.k.owner_claim(self.recv_ids, sparse["map"], sparse["slot_row"], self.rank)
             before_gather(n_recv)
             self.k.owner_gather(self.recv_ids, E_local, reply, None, None, self.rank, self.d)
         else:
             self.k.owner_gather(self.recv_ids, E_local, reply, sparse["map"], sparse["slot_row"], self.rank, self.d)
-        rows = torch.empty((n_send, self.d), dtype=torch.float32, device=item.device)
+        rows = torch.empty((n_send, self.d), dtype=self.row_dtype, device=item.device)
         self._a2a(rows, reply, sc, rc)
         return rows
 

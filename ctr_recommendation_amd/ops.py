@@ -301,7 +301,8 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
          ptr(p["senet.excitation.0.weight"]), ptr(p["senet.excitation.0.bias"]),
          ptr(p["senet.excitation.2.weight"]), ptr(p["senet.excitation.2.bias"]), cfg.R, ptr(X), ptr(Vc), ptr(Vc16),
          None if split_c else ptr(c), KC,
-         int(bf), ptr(av), ptr(cnt), ptr(err), ptr(sm.get("map")), ptr(sm.get("slot_row")), B, Lr, d, st)
+         int(bf), ptr(av), ptr(cnt), ptr(err), ptr(sm.get("map")), ptr(sm.get("slot_row")), B, Lr, d,
+         int(table_rows is not None and table_rows.dtype == torch.bfloat16), st)
     if ev is not None:
         ev[1].record()
     if after_gather is not None:

@@ -165,8 +165,8 @@ class FiBiNETTrainer:
         self.host_step = 0
         self.acts: Dict[str, torch.Tensor] = {}
         self.coll = DistCollective(world, group, stage_on_cpu)
-        self.xchg = RowExchange(rank, world, self.V, d, self.B, max_len, dev, group,
-                                stage_on_cpu=stage_on_cpu) if world > 1 else None
+        self.xchg = RowExchange(rank, world, self.V, d, self.B, max_len, dev, group, stage_on_cpu=stage_on_cpu,
+                                rows_bf16=self.fcfg.bf16) if world > 1 else None
         self.stage_on_cpu = stage_on_cpu
         # item-table Adam: "lazy" (default) replays the zero-gradient steps of a row when the row
         # is next claimed or its rolling window comes round (bit-identical to eager; see
@@ -194,12 +194,16 @@ class FiBiNETTrainer:
 
     # ------------------------------------------------------------------ one training step
     def step(self, batch: Dict[str, torch.Tensor], labels: torch.Tensor,
-             masks_out: Optional[Dict[str, torch.Tensor]] = None, probe: Optional[Dict[str, list]] = None
-             ) -> torch.Tensor:
+             masks_out: Optional[Dict[str, torch.Tensor]] = None, probe: Optional[Dict[str, list]] = None,
+             next_batch: Optional[Dict[str, torch.Tensor]] = None) -> torch.Tensor:
         """One optimizer step on this rank's batch; returns the (device) global-mean BCE loss.
 
         masks_out (tests only): {'m1': u8 [B,512], 'm2': u8 [B,256]} receives the dropout keep-masks.
         probe (bench only): collects HIP-event pairs around the gather and table-Adam launches.
+        next_batch (N > 1): the batch of the FOLLOWING step; its ids are routed and their counts
+        exchanged during this step on a side stream (RowExchange.prepare), so the next step needs
+        no host sync on the main stream.  That step uses the routing only if it is given the very
+        same id tensors (unmodified); otherwise it routes inline.
         """
         if self.host_step >= self.total_steps:
             raise ValueError(f"Tried to step {self.host_step + 1} times. The specified number of total steps is "
@@ -267,6 +271,8 @@ class FiBiNETTrainer:
             rows = self.xchg.forward(batch["item_id"], seq, self.E, {"map": self.map, "slot_row": self.slot_row},
                                      self.err, before_gather=catch_up if lazy else None)
             pos = self.xchg.cur_pos
+            if next_batch is not None:
+                self.xchg.prepare(next_batch["item_id"], next_batch.get("item_seq"), self.err)
         elif lazy:
             catch_up(B * (L + 1), claim=True)
         else:

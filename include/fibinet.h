@@ -74,7 +74,7 @@ int fbn_fields_fwd(const int64_t* item_id, const int64_t* item_seq, const int64_
                    const float* table, long long V, const int* pos, const float* w1, const float* b1, const float* w2,
                    const float* b2, int R, float* X, float* Vc, short* Vc16, void* c, int ldc, int c_bf16, float* a_out,
                    float* cnt_out,
-                   int* err, int* map, int* slot_row, int B, int L, int D, void* stream);
+                   int* err, int* map, int* slot_row, int B, int L, int D, int rows_bf16, void* stream);
 
 /* ---------------------------------------------------------------- K2 + K4 backward
  * Replaces the autograd of the lines above, including embedding_dense_backward with
@@ -303,8 +303,9 @@ int fbn_route(const int64_t* item, const int64_t* seq, int B, int L, long long V
               int* counts, int* offsets, int* cursor, int* send_ids, int* pos, int* err, void* stream);
 /* claims only (the lazy table Adam replays the claimed rows before fbn_owner_gather(map = NULL)) */
 int fbn_owner_claim(const int* ids, int n, int* map, int* slot_row, int rank, void* stream);
-int fbn_owner_gather(const int* ids, int n, const float* E, float* out, int* map, int* slot_row, int rank, int D,
-                     void* stream);
+/* out_bf16: reply rows as bf16 (the bf16 mode's wire format; fbn_fields_fwd(rows_bf16 = 1) reads them) */
+int fbn_owner_gather(const int* ids, int n, const float* E, void* out, int* map, int* slot_row, int rank, int D,
+                     int out_bf16, void* stream);
 
 /* ---------------------------------------------------------------- device collator
  * Replaces BatchCollator.__call__ (src/dataloader.py:69-121) and InferenceCollator.__call__

@@ -48,7 +48,7 @@ class CpuExchangeKernels:
 
     def owner_gather(self, ids, E, out, map_, slot_row, rank, d):
         for i, r in enumerate(ids.tolist()):
-            out[i] = E[r]
+            out[i] = E[r]                     # a bf16 `out` (the bf16 mode's wire rows) rounds here
             if map_ is not None and not (rank == 0 and r == 0) and int(map_[r]) == -1:
                 map_[r] = i
                 slot_row[i] = r

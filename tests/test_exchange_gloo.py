@@ -1,4 +1,4 @@
-"""Row-sharded exchange protocol on 2 (and 3) gloo CPU ranks -- covers the N > 1 host path.
+"""Row-sharded exchange protocol on 2, 3 and 4 gloo CPU ranks -- covers the N > 1 host path.
 
 Runs the product's RowExchange (routing bookkeeping, split sizes, all_to_all_single, owner
 gather, sparse reduce-scatter) with the CPU restatement of its kernels
@@ -25,7 +25,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, V, d, B, L, q, hook=False):
+def _worker(rank, world, port, V, d, B, L, q, hook=False, bf16=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -41,7 +41,7 @@ def _worker(rank, world, port, V, d, B, L, q, hook=False):
         seq = torch.randint(0, V, (B, L), generator=gb)
         seq[0] = 0
         seq[1, :3] = 5
-        xg = RowExchange(rank, world, V, d, B, L, torch.device("cpu"), kernels=CpuExchangeKernels())
+        xg = RowExchange(rank, world, V, d, B, L, torch.device("cpu"), kernels=CpuExchangeKernels(), rows_bf16=bf16)
         lo, n_local = xg.rows_lo, xg.rows_local
         E_local = E_full[lo:lo + n_local].clone()
         cap = world * B * (L + 1)
@@ -69,7 +69,7 @@ def _worker(rank, world, port, V, d, B, L, q, hook=False):
                     ok_fwd &= p == -1
                     continue
                 want = E_full[int(ids[b, t])] + (1000.0 if hook and int(ids[b, t]) != 0 else 0.0)
-                ok_fwd &= p >= 0 and torch.equal(rows[p], want)
+                ok_fwd &= p >= 0 and torch.equal(rows[p], want.to(rows.dtype))
         # backward: one random gradient row per routed entry
         sendbuf = xg.make_sendbuf()
         sendbuf.copy_(torch.randn(sendbuf.shape, generator=gb))
@@ -101,14 +101,16 @@ def _worker(rank, world, port, V, d, B, L, q, hook=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,hook", [(2, False), (3, False), (2, True)])
-def test_row_exchange_protocol(world, hook):
-    """hook: the owner-side claim -> before_gather -> gather split used by the lazy table Adam."""
+@pytest.mark.parametrize("world,hook,bf16", [(2, False, False), (3, False, False), (2, True, False),
+                                             (4, False, False), (4, True, False), (4, False, True)])
+def test_row_exchange_protocol(world, hook, bf16):
+    """hook: the owner-side claim -> before_gather -> gather split used by the lazy table Adam.
+    bf16: the bf16 mode's wire rows (each delivered row == E[id] rounded to bf16)."""
     V, d, B, L = 101, 8, 12, 6
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, V, d, B, L, q, hook)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, V, d, B, L, q, hook, bf16)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
