@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--probe-steps", type=int, default=10)
     ap.add_argument("--batches", type=int, default=0, help="distinct HBM-resident batches (default F + 32)")
     ap.add_argument("--lazy-window", type=int, default=128, help="lazy table-Adam window F (rows per step: V/F)")
+    ap.add_argument("--prime", type=int, default=-1,
+                    help="untimed priming steps before the warm-up (default: top the warm-up up to 2F)")
     ap.add_argument("--no-fp32", dest="also_fp32", action="store_false",
                     help="skip the second (fp32) C3 measurement embedded in the line")
     return ap.parse_args()
@@ -152,7 +154,7 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
     nb = args.batches if args.batches else F + 32
     # steady state of the lazy table Adam whatever --warmup says: a row's replay length settles
     # only after ~2F steps; warm-up steps are < 1 ms each
-    prime = max(0, 2 * F - W)
+    prime = max(0, 2 * F - W) if args.prime < 0 else args.prime
     use_graph = world == 1 and not args.no_graph
     total = 1 + (nb if use_graph else 0) + prime + W + K + args.probe_steps + 16
     init = _initial_state(cfg, V, world, rank, dev)
@@ -199,9 +201,11 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
             tr.step(sb, sl)
 
     i = 0
-    for _ in range(prime + W):
+    for j in range(prime + W):
         run_step(i)
         i += 1
+        if (j + 1) % 64 == 0 and rank == 0:
+            print(f"[bench] {dtype}: {j + 1}/{prime + W} untimed steps", file=sys.stderr, flush=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

@@ -19,9 +19,11 @@ import sys
 # is at least half the largest (MLP layer 1 forward shares its grid with MLP layer 2's dgrad)
 KERNELS = {
     "fields_fwd": ("fields_fwd_kernel<128", None, None),
-    "adam_catchup": ("adam_catchup_kernel<128", "!65536", None),   # claimed rows (the window runs on 256 WGs)
-    "adam_window": ("adam_catchup_kernel<128", "65536", None),
-    "gemm_mlp0": ("gemm_dma16_kernel<64, 64, false, false", "262144", "max"),
+    # the claimed-row catch-up (fused with the row claims) is the adam_catchup launch with the
+    # largest grid, the rolling window (side stream) the one with the smallest
+    "adam_catchup": ("adam_catchup_kernel<128", "max", None),
+    "adam_window": ("adam_catchup_kernel<128", "min", None),
+    "gemm_mlp0": ("gemm_dma16_kernel<64, 128, false, false", "262144", "max"),
     "adam_touched": ("adam_touched_kernel<128", None, None),
     "adam_commit": ("adam_commit_kernel<128", None, None),
     "adam_tail": ("adam_tail_kernel<128", None, None),
@@ -37,6 +39,11 @@ def load(d, counter):
 
 
 def select(rows, sub, grid):
+    if grid in ("max", "min"):
+        grids = [int(g) for _, name, g, _ in rows if sub in name]
+        if not grids:
+            return []
+        grid = str(max(grids) if grid == "max" else min(grids))
     out = []
     for _, name, g, val in rows:
         if sub not in name:
