@@ -73,17 +73,19 @@ SIGNATURES = {
     "fbn_sparse_fixup": (I, [P, P, P, I, I, LL, I, P, P, P, P, I, I, P]),
     "fbn_sumsq_sparse": (I, [P, P, P, I, I, I, P, P]),
     "fbn_sparse_fixup_dup": (I, [P, I, P, P, P, I, I, P]),
-    "fbn_sumsq_sparse_norms": (I, [P, P, P, P, I, I, I, P, P]),
+    "fbn_sumsq_sparse_norms": (I, [P, P, P, P, I, I, I, P, P, P]),
+    "fbn_sparse_fold_fx": (I, [P, P, I, P, P, I, I, P, P]),
     "fbn_adam_table": (I, [P, P, P, LL, I, P, P, P, P, I, P, P, P, F, F, F, I, P]),
     "fbn_adam_touched": (I, [P, P, P, I, P, P, P, P, I, I, P, P, P, F, F, F, P, P]),
     "fbn_adam_catchup": (I, [P, P, P, LL, I, P, I, P, I, I, P, P, P, F, F, F, P, P, P, LL, I, I, P]),
-    "fbn_adam_claim_catchup": (I, [P, P, I, I, LL, P, P, P, P, P, P, LL, I, I, P, P, P, F, F, F, P, P, P, LL, I, I, P]),
+    "fbn_adam_claim_catchup": (I, [P, P, I, I, LL, P, P, P, P, P, P, P, LL, I, I, P, P, P, F, F, F, P, P, P, LL, I, I,
+                                   P]),
     "fbn_adam_flush": (I, [P, P, P, LL, I, P, P, P, F, F, F, P, P, P, LL, I, I, P]),
     "fbn_adam_selftest": (I, [I, ctypes.c_uint, P, P]),
     "fbn_adam_step_tail": (I, [P, P, P, P, LL, P, F, P, P, P, P, P, I, P, P, P, P, I, I, P, P, F, F, F, P, P, P, P, I, I,
                                P, P, P, P, I, P, P]),
     "fbn_adam_commit": (I, [P, P, P, I, P, P, P, P, I, I, P, P, P, F, F, F, P, P, P, P, I, I, P]),
-    "fbn_claim_rows": (I, [P, P, I, I, LL, P, P, P, P]),
+    "fbn_claim_rows": (I, [P, P, I, I, LL, P, P, P, P, P]),
     "fbn_pack_extras": (I, [P, P, P, P]),
     "fbn_unpack_extras": (I, [P, P, P, P]),
     "fbn_step_end": (I, [P, P, P, P, P, I, P, P]),

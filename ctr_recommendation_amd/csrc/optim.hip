@@ -192,12 +192,20 @@ __global__ void adam_dense_kernel(float* __restrict__ p, const float* __restrict
 // Multi-GPU owner: entry = received row i, its gradient is rows[i] (Lp1 = 1), duplicates are
 // added into the claimer's own row.
 #define FBN_SLOT_FLAG 0x40000000
+// Lp1 | FBN_GRAD_FULL (deterministic mode): extra[e] of a flagged claimer holds the row's FULL
+// gradient (fbn_sparse_fold_fx), not the sum of its duplicates
+#define FBN_GRAD_FULL 0x10000
 struct GradSrc {
   const float* vec;     // Lp1 > 1: [B][2][D] per-sample vectors;  Lp1 == 1: [n][D] per-entry rows
   float* extra;         // [n][D] duplicate accumulation (single GPU) or null
   int* slot_row;        // [n] claimed row | FLAG, or -1
   int Lp1;
+  int full;             // extra of a flagged claimer = the whole row gradient
 };
+static inline GradSrc make_src(const float* vec, float* extra, int* slot_row, int lp1_flags) {
+  return GradSrc{vec, extra, slot_row, lp1_flags & 0xffff, (lp1_flags & FBN_GRAD_FULL) ? 1 : 0};
+}
+
 template <int D>
 __device__ __forceinline__ const float* grad_base(const GradSrc& s, int e) {
   if (s.Lp1 == 1) return s.vec + (size_t)e * D;
@@ -250,7 +258,8 @@ __global__ void __launch_bounds__(256) sparse_fixup_kernel(const int64_t* __rest
 // (a claim never changes within a step, so the value a failed claim observes is final); the
 // fix-up then reads dup coalesced instead of re-resolving every id through the map.
 __global__ void claim_rows_kernel(const int64_t* __restrict__ item, const int64_t* __restrict__ seq, int B, int L,
-                                  long long V, int* __restrict__ map, int* __restrict__ slot_row, int* __restrict__ dup) {
+                                  long long V, int* __restrict__ map, int* __restrict__ slot_row, int* __restrict__ dup,
+                                  int* __restrict__ hasdup) {
   const long long n = (long long)B * (L + 1);
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
     const long long b = e / (L + 1), t = e - b * (L + 1);
@@ -268,6 +277,7 @@ __global__ void claim_rows_kernel(const int64_t* __restrict__ item, const int64_
       }
     }
     if (dup) dup[e] = owner;
+    if (hasdup && owner >= 0) hasdup[owner] = 1;   // benign race: every writer stores 1
   }
 }
 
@@ -294,12 +304,49 @@ __global__ void __launch_bounds__(256) sparse_fixup_dup_kernel(const int* __rest
   }
 }
 
+// Deterministic duplicate fold (single GPU, deterministic mode).  Every entry of a row that
+// several entries hit -- its claimer included -- adds its vector into the claimer's int64
+// fixed-point accumulator acc[claimer] (scale 2^FBN_FX_SHIFT): integer addition is associative, so
+// the row's total depends neither on the order the atomics land in nor on which entry won the
+// claim.  The claimer flags itself (only it writes its own slot_row) and clears hasdup.
+// fbn_sumsq_sparse_norms(acc) then turns each total into extra[claimer] (float, the FULL row
+// gradient) and resets acc.  |element| < 2^23, resolution 2^-40 (9e-13).
+#define FBN_FX_SHIFT 40
+__device__ __forceinline__ long long to_fx(float x) { return __double2ll_rn((double)x * 1099511627776.0); }
+template <int D>
+__global__ void __launch_bounds__(256) sparse_fold_fx_kernel(const int* __restrict__ dup, int* __restrict__ hasdup,
+                                                             int n, GradSrc s, unsigned long long* __restrict__ acc) {
+  const int lane = threadIdx.x & 63;
+  for (long long e0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) - lane; e0 < n;
+       e0 += (long long)gridDim.x * blockDim.x) {
+    const long long e = e0 + lane;
+    int u = -1;
+    if (e < n) {
+      u = dup[e];
+      if (u < 0 && hasdup[e]) {          // a claimer whose row other entries hit
+        u = (int)e;
+        hasdup[e] = 0;
+        s.slot_row[e] |= FBN_SLOT_FLAG;
+      }
+    }
+    unsigned long long mask = __ballot(u >= 0);
+    while (mask) {
+      const int l = __ffsll((long long)mask) - 1;
+      mask &= mask - 1;
+      const int ue = __shfl(u, l, 64);
+      const float* src = grad_base<D>(s, (int)(e0 + l));
+      unsigned long long* dst = acc + (size_t)ue * D;
+      for (int k = lane; k < D; k += 64) atomicAdd(dst + k, (unsigned long long)to_fx(src[k]));
+    }
+  }
+}
+
 // sum of squares of the table gradient from per-sample vector norms (fbn_fields_bwd's gnorm
 // [B][2]): a claiming entry without duplicates adds its vector's norm; one with duplicates
 // (FLAG, rare) sums vector + extra explicitly, cooperatively across the wave.  One entry per lane.
 template <int D>
 __global__ void __launch_bounds__(256) sumsq_norms_kernel(GradSrc s, const double* __restrict__ gnorm, int n,
-                                                          double* __restrict__ out) {
+                                                          double* __restrict__ out, unsigned long long* __restrict__ fx) {
   __shared__ double red[4];
   const int lane = threadIdx.x & 63;
   double acc = 0.0;
@@ -317,7 +364,17 @@ __global__ void __launch_bounds__(256) sumsq_norms_kernel(GradSrc s, const doubl
       const int l = __ffsll((long long)mask) - 1;
       mask &= mask - 1;
       const float* v = grad_base<D>(s, (int)(e0 + l));
-      const float* x = s.extra + (size_t)(e0 + l) * D;
+      float* x = s.extra + (size_t)(e0 + l) * D;
+      if (fx) {   // deterministic fold: the full row gradient from the fixed-point total
+        unsigned long long* a = fx + (size_t)(e0 + l) * D;
+        for (int k = lane; k < D; k += 64) {
+          const float y = (float)((double)(long long)a[k] * (1.0 / 1099511627776.0));
+          x[k] = y;
+          a[k] = 0ull;
+          acc += (double)(y * y);
+        }
+        continue;
+      }
       for (int k = lane; k < D; k += 64) {
         const float y = v[k] + x[k];
         acc += (double)(y * y);
@@ -345,7 +402,10 @@ __global__ void __launch_bounds__(256) sumsq_sparse_kernel(GradSrc s, int n, dou
     const int sr = s.slot_row[e];
     if (sr == -1) continue;
     f32x4 v = *reinterpret_cast<const f32x4*>(grad_base<D>(s, (int)e) + 4 * q);
-    if (sr & FBN_SLOT_FLAG) v += *reinterpret_cast<const f32x4*>(s.extra + (size_t)e * D + 4 * q);
+    if (sr & FBN_SLOT_FLAG) {
+      const f32x4 x = *reinterpret_cast<const f32x4*>(s.extra + (size_t)e * D + 4 * q);
+      v = s.full ? x : v + x;
+    }
     acc += (double)(v[0] * v[0]) + (double)(v[1] * v[1]) + (double)(v[2] * v[2]) + (double)(v[3] * v[3]);
   }
   red[threadIdx.x] = acc;
@@ -391,7 +451,7 @@ __device__ __forceinline__ void adam_table_body(float* __restrict__ p, float* __
       gg = *reinterpret_cast<const f32x4*>(grad_base<D>(gs, u) + 4 * q);
       if (gs.extra && (gs.slot_row[u] & FBN_SLOT_FLAG)) {
         float* ex = gs.extra + (size_t)u * D + 4 * q;
-        gg += *reinterpret_cast<const f32x4*>(ex);
+        gg = gs.full ? *reinterpret_cast<const f32x4*>(ex) : gg + *reinterpret_cast<const f32x4*>(ex);
         *reinterpret_cast<f32x4*>(ex) = (f32x4){0.f, 0.f, 0.f, 0.f};   // keep `extra` all-zero
       }
     }
@@ -585,6 +645,7 @@ struct ClaimSrc {
   int* map;
   int* slot_row;
   int* dup;
+  int* hasdup;   // optional: hasdup[claimer] = 1 when another entry hit its row (deterministic fold)
 };
 
 template <int D, bool DW>
@@ -636,6 +697,7 @@ __global__ void __launch_bounds__(256) adam_catchup_kernel(float* __restrict__ p
           }
         }
         if (cs.dup) cs.dup[i] = owner;
+        if (cs.hasdup && owner >= 0) cs.hasdup[owner] = 1;
       } else if (i < n_ent) {
         const int sr = slot_row[i];
         if (sr != -1) r = sr & ~FBN_SLOT_FLAG;
@@ -730,7 +792,7 @@ __global__ void __launch_bounds__(256) adam_touched_kernel(float* __restrict__ p
     f32x4 gg = *reinterpret_cast<const f32x4*>(grad_base<D>(gs, (int)e) + 4 * q);
     if (sr & FBN_SLOT_FLAG) {
       float* ex = gs.extra + (size_t)e * D + 4 * q;
-      gg += *reinterpret_cast<const f32x4*>(ex);
+      gg = gs.full ? *reinterpret_cast<const f32x4*>(ex) : gg + *reinterpret_cast<const f32x4*>(ex);
       *reinterpret_cast<f32x4*>(ex) = (f32x4){0.f, 0.f, 0.f, 0.f};
     }
     const size_t off = (size_t)r * D + 4 * q;
@@ -795,7 +857,7 @@ __device__ __forceinline__ void adam_commit_body(float* __restrict__ p, float* _
       const long long r = sr_l & ~FBN_SLOT_FLAG;
       f32x4 gg = *reinterpret_cast<const f32x4*>(grad_base<D>(gs, (int)ee) + 4 * q);
       float* ex = gs.extra + (size_t)ee * D + 4 * q;
-      gg += *reinterpret_cast<const f32x4*>(ex);
+      gg = gs.full ? *reinterpret_cast<const f32x4*>(ex) : gg + *reinterpret_cast<const f32x4*>(ex);
       *reinterpret_cast<f32x4*>(ex) = (f32x4){0.f, 0.f, 0.f, 0.f};
       const size_t off = (size_t)r * D + 4 * q;
       f32x4 pp = *reinterpret_cast<f32x4*>(p + off);
@@ -976,7 +1038,7 @@ extern "C" int fbn_sparse_fixup(const int64_t* item, const int64_t* seq, const i
                                 int D, void* stream) {
   if (n <= 0) return FBN_OK;
   hipStream_t st = (hipStream_t)stream;
-  GradSrc s{gvec, extra, slot_row, Lp1};
+  const GradSrc s = make_src(gvec, extra, slot_row, Lp1);
   FBN_DISPATCH_D(sparse_fixup_kernel, D, group_grid(n, D, 8192), item, L > 0 ? seq : nullptr, ids, n, L, V, rank,
                  map, s);
   FBN_CHECK_LAUNCH();
@@ -990,7 +1052,7 @@ extern "C" int fbn_sparse_fixup_dup(const int* dup, int n, const float* gvec, fl
   if (n <= 0) return FBN_OK;
   if (!dup || !extra) { fbn_set_error("fbn_sparse_fixup_dup: dup and extra are required"); return FBN_ERR_ARG; }
   hipStream_t st = (hipStream_t)stream;
-  GradSrc s{gvec, extra, slot_row, Lp1};
+  const GradSrc s = make_src(gvec, extra, slot_row, Lp1);
   int blocks = (n + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   FBN_DISPATCH_D(sparse_fixup_dup_kernel, D, dim3(blocks), dup, n, s);
@@ -998,15 +1060,31 @@ extern "C" int fbn_sparse_fixup_dup(const int* dup, int n, const float* gvec, fl
   return FBN_OK;
 }
 
-extern "C" int fbn_sumsq_sparse_norms(const double* gnorm, const float* gvec, float* extra, int* slot_row, int Lp1,
-                                      int n, int D, double* out, void* stream) {
+extern "C" int fbn_sparse_fold_fx(const int* dup, int* hasdup, int n, const float* gvec, int* slot_row, int Lp1, int D,
+                                  unsigned long long* acc, void* stream) {
   if (n <= 0) return FBN_OK;
-  if (Lp1 < 2) { fbn_set_error("fbn_sumsq_sparse_norms: per-sample vectors only (Lp1 >= 2)"); return FBN_ERR_ARG; }
+  if (!dup || !hasdup || !acc || (Lp1 & 0xffff) < 2) {
+    fbn_set_error("fbn_sparse_fold_fx: dup, hasdup, acc and per-sample vectors (Lp1 >= 2) are required");
+    return FBN_ERR_ARG;
+  }
   hipStream_t st = (hipStream_t)stream;
-  GradSrc s{gvec, extra, slot_row, Lp1};
+  const GradSrc s = make_src(gvec, nullptr, slot_row, Lp1);
+  int blocks = (n + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  FBN_DISPATCH_D(sparse_fold_fx_kernel, D, dim3(blocks), dup, hasdup, n, s, acc);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+extern "C" int fbn_sumsq_sparse_norms(const double* gnorm, const float* gvec, float* extra, int* slot_row, int Lp1,
+                                      int n, int D, double* out, unsigned long long* fx, void* stream) {
+  if (n <= 0) return FBN_OK;
+  if ((Lp1 & 0xffff) < 2) { fbn_set_error("fbn_sumsq_sparse_norms: per-sample vectors only (Lp1 >= 2)"); return FBN_ERR_ARG; }
+  hipStream_t st = (hipStream_t)stream;
+  const GradSrc s = make_src(gvec, extra, slot_row, Lp1);
   int blocks = (n + 255) / 256;
   if (blocks > 1024) blocks = 1024;
-  FBN_DISPATCH_D(sumsq_norms_kernel, D, dim3(blocks), s, gnorm, n, out);
+  FBN_DISPATCH_D(sumsq_norms_kernel, D, dim3(blocks), s, gnorm, n, out, fx);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -1015,7 +1093,7 @@ extern "C" int fbn_sumsq_sparse(const float* gvec, float* extra, int* slot_row, 
                                 void* stream) {
   if (n <= 0) return FBN_OK;
   hipStream_t st = (hipStream_t)stream;
-  GradSrc s{gvec, extra, slot_row, Lp1};
+  const GradSrc s = make_src(gvec, extra, slot_row, Lp1);
   FBN_DISPATCH_D(sumsq_sparse_kernel, D, group_grid(n, D, 4096), s, n, out);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
@@ -1032,7 +1110,7 @@ extern "C" int fbn_adam_table(float* p, float* m, float* v, long long nrows, int
   hipStream_t st = (hipStream_t)stream;
   const float omb2 = (float)(1.0 - (double)beta2);
   const AdamConsts* t = (const AdamConsts*)consts_table;
-  GradSrc s{gvec, extra, slot_row, Lp1};
+  const GradSrc s = make_src(gvec, extra, slot_row, Lp1);
   static const int throttle = getenv("FBN_ADAM_BLOCKS") ? atoi(getenv("FBN_ADAM_BLOCKS")) : 512;   // tuning knob
   const dim3 grid = mode == 1 ? dim3(throttle) : group_grid(nrows, D, 16384);
   if (mode == 1 || mode == 2) {
@@ -1051,7 +1129,7 @@ extern "C" int fbn_adam_touched(float* p, float* m, float* v, int D, int* map, c
   hipStream_t st = (hipStream_t)stream;
   const float omb2 = (float)(1.0 - (double)beta2);
   const AdamConsts* t = (const AdamConsts*)consts_table;
-  GradSrc s{gvec, extra, slot_row, Lp1};
+  const GradSrc s = make_src(gvec, extra, slot_row, Lp1);
   FBN_DISPATCH_D(adam_touched_kernel, D, group_grid(n, D, 8192), p, m, v, map, s, n, coef, t, step, wd, beta2,
                  omb2, eps, last);
   FBN_CHECK_LAUNCH();
@@ -1064,13 +1142,13 @@ extern "C" int fbn_adam_commit(float* p, float* m, float* v, int D, int* map, co
                                const int* step, float wd, float beta2, float eps, int* last, int* pend, float* ring,
                                float* coef_hist, int ring_n, int B, void* stream) {
   if (n <= 0) return FBN_OK;
-  if (!pend || !ring || !coef_hist || !extra || ring_n < 2 || Lp1 < 2) {
+  if (!pend || !ring || !coef_hist || !extra || ring_n < 2 || (Lp1 & 0xffff) < 2) {
     fbn_set_error("fbn_adam_commit: pend, ring, coef_hist and extra are required (single-GPU layout)");
     return FBN_ERR_ARG;
   }
   hipStream_t st = (hipStream_t)stream;
   const float omb2 = (float)(1.0 - (double)beta2);
-  GradSrc s{gvec, extra, slot_row, Lp1};
+  const GradSrc s = make_src(gvec, extra, slot_row, Lp1);
   const PendSrc ps{pend, ring, coef_hist, (long long)B * 2 * D, ring_n};
   int blocks = (n + 255) / 256;
   if (blocks > 2048) blocks = 2048;
@@ -1089,13 +1167,13 @@ extern "C" int fbn_adam_step_tail(float* dp, const float* dg, float* dm, float* 
                                   int* last, int* pend, float* ring, float* coef_hist, int ring_n, int B,
                                   unsigned long long* rng, long long* nbt0, long long* nbt1, unsigned* ticket,
                                   int max_step, int* err, void* stream) {
-  if (!pend || !ring || !coef_hist || !extra || !sumsq || !ticket || ring_n < 2 || Lp1 < 2) {
+  if (!pend || !ring || !coef_hist || !extra || !sumsq || !ticket || ring_n < 2 || (Lp1 & 0xffff) < 2) {
     fbn_set_error("fbn_adam_step_tail: pend, ring, coef_hist, extra, sumsq and ticket are required");
     return FBN_ERR_ARG;
   }
   hipStream_t st = (hipStream_t)stream;
   const float omb2 = (float)(1.0 - (double)beta2);
-  GradSrc s{gvec, extra, slot_row, Lp1};
+  const GradSrc s = make_src(gvec, extra, slot_row, Lp1);
   const PendSrc ps{pend, ring, coef_hist, (long long)B * 2 * D, ring_n};
   const StepEnd se{step, rng, (double*)sumsq, nbt0, nbt1, ticket, max_step, err};
   long long nd = (n_dense / 4 + 255) / 256;
@@ -1113,13 +1191,13 @@ extern "C" int fbn_adam_step_tail(float* dp, const float* dg, float* dm, float* 
 }
 
 extern "C" int fbn_claim_rows(const int64_t* item, const int64_t* seq, int B, int L, long long V, int* map,
-                              int* slot_row, int* dup, void* stream) {
+                              int* slot_row, int* dup, int* hasdup, void* stream) {
   const long long n = (long long)B * (L + 1);
   if (n <= 0) return FBN_OK;
   int blocks = (int)((n + 255) / 256);
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(claim_rows_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, item, L > 0 ? seq : nullptr,
-                     B, L, V, map, slot_row, dup);
+                     B, L, V, map, slot_row, dup, hasdup);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -1161,7 +1239,7 @@ extern "C" int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, i
   // one wave per SCAN items (16 at D >= 64, else 64; sorted and compacted inside the kernel)
   const long long scan = D >= 64 ? 16 : 64;
   const dim3 grid((unsigned)std::min<long long>(cap, (items + 4 * scan - 1) / (4 * scan)));
-  const ClaimSrc cs{nullptr, nullptr, 0, 0, nullptr, nullptr, nullptr};
+  const ClaimSrc cs{nullptr, nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr};
   if (decoupled) {
     FBN_DISPATCH_D_B(adam_catchup_kernel, true, D, grid, p, m, v, slot_row, n_ent, map, nrows, F, chunk, parts, last,
                      (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, cs);
@@ -1175,7 +1253,7 @@ extern "C" int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, i
 
 // single GPU: fbn_claim_rows + fbn_adam_catchup(parts = 1) in one launch (see ClaimSrc)
 extern "C" int fbn_adam_claim_catchup(const int64_t* item, const int64_t* seq, int B, int L, long long V, int* map,
-                                      int* slot_row, int* dup, float* p, float* m, float* v, long long nrows, int D,
+                                      int* slot_row, int* dup, int* hasdup, float* p, float* m, float* v, long long nrows, int D,
                                       int F, int* last, const void* consts_table, const int* step, float wd,
                                       float beta2, float eps, int* pend, const float* ring, const float* coef_hist,
                                       long long ring_stride, int ring_n, int decoupled, void* stream) {
@@ -1194,7 +1272,7 @@ extern "C" int fbn_adam_claim_catchup(const int64_t* item, const int64_t* seq, i
   const float omb2 = (float)(1.0 - (double)beta2);
   const long long chunk = (nrows + F - 1) / F;
   const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
-  const ClaimSrc cs{item, L > 0 ? seq : nullptr, L, V, map, slot_row, dup};
+  const ClaimSrc cs{item, L > 0 ? seq : nullptr, L, V, map, slot_row, dup, hasdup};
   const long long scan = D >= 64 ? 16 : 64;
   const dim3 grid((unsigned)std::min<long long>(8192, (n + 4 * scan - 1) / (4 * scan)));
   if (decoupled) {

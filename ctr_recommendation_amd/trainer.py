@@ -35,6 +35,7 @@ from .model_fibinet import build_model
 from .schedule import OneCycle, adam_table
 
 TABLE = "item_emb.weight"
+FBN_GRAD_FULL = 0x10000      # include/fibinet.h: extra holds the full row gradient (deterministic fold)
 FROZEN = ("user_emb.weight",)
 BUFFERS = ("mlp.1.running_mean", "mlp.1.running_var", "mlp.1.num_batches_tracked",
            "mlp.5.running_mean", "mlp.5.running_var", "mlp.5.num_batches_tracked")
@@ -65,7 +66,7 @@ class FiBiNETTrainer:
                  group=None, init_state: Optional[Dict[str, torch.Tensor]] = None, seed: int = 2025,
                  stage_on_cpu: bool = False, dropout_seed: Optional[int] = None, table_adam: str = "lazy",
                  lazy_window: int = 128, defer_table_grads: bool = True, max_norm: float = 10.0,
-                 optimizer: Optional[str] = None):
+                 optimizer: Optional[str] = None, deterministic: Optional[bool] = None):
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise RuntimeError("FiBiNETTrainer runs on a HIP device only (no CPU fallback)")
@@ -147,6 +148,14 @@ class FiBiNETTrainer:
         # single GPU: claim-time duplicate list (entry -> claiming entry) and per-sample gradient norms
         self.dup = torch.full((self.n_entries,), -1, **i32) if world == 1 else None
         self.gnorm = torch.zeros((self.B, 2), dtype=torch.float64, device=dev) if world == 1 else None
+        # deterministic mode (single GPU): rows hit by several entries are folded by
+        # order-independent int64 fixed-point sums (fbn_sparse_fold_fx) instead of float atomics, so
+        # two runs from the same state produce bit-identical table gradients and weights
+        if deterministic is None:
+            deterministic = bool(model_cfg.get("deterministic", False)) or os.environ.get("FBN_DETERMINISTIC") == "1"
+        self.deterministic = bool(deterministic) and world == 1
+        self.hasdup = torch.zeros((self.n_entries,), **i32) if self.deterministic else None
+        self.fx = torch.zeros((self.n_entries, d), dtype=torch.int64, device=dev) if self.deterministic else None
         # ---------------- optimizer schedule + device step state
         self.total_steps = total_steps
         tab, self.lrs = adam_table(total_steps, self.lr, self.beta2, OneCycle(total_steps, self.lr),
@@ -232,7 +241,8 @@ class FiBiNETTrainer:
             ev = _events(probe, "adam_catchup")
             if claim:
                 call("fbn_adam_claim_catchup", ptr(batch["item_id"]), ptr(seq) if L else None, B, L, self.V,
-                     ptr(self.map), ptr(self.slot_row), ptr(self.dup), ptr(self.E), ptr(self.Em), ptr(self.Ev),
+                     ptr(self.map), ptr(self.slot_row), ptr(self.dup), ptr(self.hasdup), ptr(self.E), ptr(self.Em),
+                     ptr(self.Ev),
                      self.rows_local, d, self.lazy_window, ptr(self.last), ptr(self.sched), ptr(self.step_dev),
                      self.wd_g, self.beta2, self.eps, *self._pend_args(), int(self.decoupled), st)
             else:
@@ -277,7 +287,7 @@ class FiBiNETTrainer:
             catch_up(B * (L + 1), claim=True)
         else:
             call("fbn_claim_rows", ptr(batch["item_id"]), ptr(seq) if L else None, B, L, self.V, ptr(self.map),
-                 ptr(self.slot_row), ptr(self.dup), st)
+                 ptr(self.slot_row), ptr(self.dup), ptr(self.hasdup), st)
         if w16_ev is not None:
             main.wait_event(w16_ev)
         a = ops.forward(self.p, batch, cfg, self.rng, table_rows=rows, pos=pos, err=self.err, labels=labels,
@@ -292,10 +302,18 @@ class FiBiNETTrainer:
                      extra_sums=[(a["loss_terms"], B, 1, self.loss, 1.0 / ntot)], probe=probe)
         if self.xchg is None:
             # single GPU: per-sample vectors; entry e = b*(L+1)+t; duplicates -> extra[claimer]
-            gsrc = (self.gvec, self.extra, L + 1)
             n_ent = B * (L + 1)
-            call("fbn_sparse_fixup_dup", ptr(self.dup), n_ent, ptr(self.gvec), ptr(self.extra), ptr(self.slot_row),
-                 L + 1, d, st)
+            if self.deterministic:
+                if L == 0:
+                    raise ValueError("deterministic mode needs the item_seq history (L > 0)")
+                # extra[claimer] becomes the FULL row gradient (Lp1 | FBN_GRAD_FULL for the readers)
+                gsrc = (self.gvec, self.extra, (L + 1) | FBN_GRAD_FULL)
+                call("fbn_sparse_fold_fx", ptr(self.dup), ptr(self.hasdup), n_ent, ptr(self.gvec), ptr(self.slot_row),
+                     gsrc[2], d, ptr(self.fx), st)
+            else:
+                gsrc = (self.gvec, self.extra, L + 1)
+                call("fbn_sparse_fixup_dup", ptr(self.dup), n_ent, ptr(self.gvec), ptr(self.extra),
+                     ptr(self.slot_row), L + 1, d, st)
         else:
             grows = self.xchg.backward(sendbuf)              # owner: one received row per entry
             n_ent = grows.shape[0]
@@ -306,7 +324,7 @@ class FiBiNETTrainer:
         tab_acc = self.sumsq_tab if self.world > 1 else self.sumsq
         if self.xchg is None and L > 0:
             call("fbn_sumsq_sparse_norms", ptr(self.gnorm), ptr(gsrc[0]), ptr(gsrc[1]), ptr(self.slot_row), gsrc[2],
-                 n_ent, d, ptr(tab_acc), st)
+                 n_ent, d, ptr(tab_acc), ptr(self.fx), st)
         else:
             call("fbn_sumsq_sparse", ptr(gsrc[0]), ptr(gsrc[1]), ptr(self.slot_row), gsrc[2], n_ent, d, ptr(tab_acc),
                  st)

@@ -212,7 +212,16 @@ int fbn_sumsq_sparse(const float* gvec, float* extra, int* slot_row, int Lp1, in
 int fbn_sparse_fixup_dup(const int* dup, int n, const float* gvec, float* extra, int* slot_row, int Lp1, int D,
                          void* stream);
 int fbn_sumsq_sparse_norms(const double* gnorm, const float* gvec, float* extra, int* slot_row, int Lp1, int n, int D,
-                           double* out, void* stream);
+                           double* out, unsigned long long* fx, void* stream);
+/* Deterministic mode (no float atomics on the table gradient): every entry of a row several
+ * entries hit -- claimer included -- adds its vector into acc[claimer] ([n][D] int64 fixed point,
+ * scale 2^40: order-independent sums); claimers are flagged.  fbn_sumsq_sparse_norms(fx = acc)
+ * then writes the FULL row gradient to extra[claimer] (and resets acc): pass Lp1 | FBN_GRAD_FULL
+ * to the table-Adam entry points so they read it as the whole gradient.  hasdup [n]: set by the
+ * row claims (fbn_claim_rows / fbn_adam_claim_catchup), cleared here. */
+#define FBN_GRAD_FULL 0x10000
+int fbn_sparse_fold_fx(const int* dup, int* hasdup, int n, const float* gvec, int* slot_row, int Lp1, int D,
+                       unsigned long long* acc, void* stream);
 /* adam_table mode 0: every row (touched rows read their gradient through map); mode 1: only the
  * rows the batch did not touch -- their gradient is 0, so the update is independent of the
  * backward and the clip coefficient and runs on a side stream concurrently with the backward;
@@ -246,7 +255,7 @@ int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, int D, const
  * row (first CAS wins: map, slot_row, dup as fbn_claim_rows) and a winning entry's row is brought
  * up to date at once. */
 int fbn_adam_claim_catchup(const int64_t* item, const int64_t* seq, int B, int L, long long V, int* map, int* slot_row,
-                           int* dup, float* p, float* m, float* v, long long nrows, int D, int F, int* last,
+                           int* dup, int* hasdup, float* p, float* m, float* v, long long nrows, int D, int F, int* last,
                            const void* consts_table, const int* step, float wd, float beta2, float eps, int* pend,
                            const float* ring, const float* coef_hist, long long ring_stride, int ring_n, int decoupled,
                            void* stream);
@@ -283,7 +292,7 @@ int fbn_adam_commit(float* p, float* m, float* v, int D, int* map, const float* 
 /* dup (optional, [B*(L+1)]): the claiming entry of each entry's row when another entry claimed
  * it, else -1 (input of fbn_sparse_fixup_dup). */
 int fbn_claim_rows(const int64_t* item, const int64_t* seq, int B, int L, long long V, int* map, int* slot_row,
-                   int* dup, void* stream);
+                   int* dup, int* hasdup, void* stream);
 /* Multi-GPU: pack {loss, this rank's table-gradient sumsq (slots zeroed)} into the two floats
  * appended to the dense-gradient all-reduce buffer; unpack after it (sumsq[0] += table norms). */
 int fbn_pack_extras(const float* loss, double* tab_slots, float* out, void* stream);
