@@ -92,6 +92,9 @@ SIGNATURES = {
     "fbn_route": (I, [P, P, I, I, LL, LL, I, P, P, P, P, P, P, P]),
     "fbn_owner_claim": (I, [P, I, P, P, I, P]),
     "fbn_owner_gather": (I, [P, I, P, P, P, P, I, I, I, P]),
+    "fbn_bilinear_supported": (I, [I]),
+    "fbn_bilinear_fwd": (I, [P, P, P, I, I, I, P]),
+    "fbn_bilinear_bwd": (I, [P, I, P, P, P, P, P, I, I, P]),
     "fbn_collate": (I, [P, I, P, P, I, I, P, P, P, P, P, LL, P, I, P, P, P, P, P, P, P, P, P]),
     "fbn_collate_zero_if": (I, [P, LL, P, P]),
 }

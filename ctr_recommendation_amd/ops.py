@@ -14,6 +14,8 @@ Layouts (B = batch, d = embedding dim, L = history length; DESIGN.md "HBM layout
 """
 from __future__ import annotations
 
+import os
+
 import ctypes
 from dataclasses import dataclass
 from typing import Dict, Optional
@@ -52,6 +54,12 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, transA, transB, bias=None, rB=NO_REMAP
          rB[0], rB[1], rB[2], rC[0], rC[1], rC[2], float(beta), int(bf16 or a16 or b16), a16, b16, ptr(stats),
          ptr(ws), nbytes,
          stream if stream is not None else _lib.stream_handle())
+
+
+def fused_bilinear(d: int) -> bool:
+    """bf16 "all" bilinear as one fused MFMA + pair-product launch each way (csrc/bilinear.hip);
+    FBN_NO_FUSED_BILINEAR=1 selects the GEMM + pair-kernel path (A/B measurements)."""
+    return os.environ.get("FBN_NO_FUSED_BILINEAR") != "1" and bool(_lib.lib().fbn_bilinear_supported(d))
 
 
 def split_mlp_input(d: int) -> bool:
@@ -308,8 +316,15 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     if after_gather is not None:
         after_gather()
     # bilinear: U = V W  ("all")  or  U_i = V_i W_i ("each"), then pair products into c
-    U = buf("U", (B, 5, d))
-    if not cfg.bilinear_each:
+    fused_bil = bf and not cfg.bilinear_each and fused_bilinear(d)
+    a["fused_bilinear"] = fused_bil
+    if fused_bil:
+        # one launch: MFMA U = V W in registers, pair products straight into c (U never stored)
+        call("fbn_bilinear_fwd", ptr(Vc16), ptr(w16["WT"]), ptr(c), B, d, KC, st)
+    U = None if fused_bil else buf("U", (B, 5, d))
+    if fused_bil:
+        pass
+    elif not cfg.bilinear_each:
         if bf:   # B(k,n) = W[k][n]: K-contiguous image is W^T
             gemm(Vc16, w16["WT"], U, 5 * B, d, d, d, d, d, False, True, bf16=True, stream=st)
         else:
@@ -319,7 +334,8 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
         for f in range(1, 5):   # field index in Vc: f-1 <-> reference field f; W_list[f]
             gemm(Vc[:, f - 1], p[f"bilinear.W_list.{f}"], U[:, f - 1], B, d, d, 5 * d, d, 5 * d, False, False,
                  bf16=bf, stream=st)
-    call("fbn_pairs_fwd", ptr(Vc), ptr(Vc16), ptr(U), ptr(c), B, d, KC, int(cfg.bilinear_each), int(bf), st)
+    if not fused_bil:
+        call("fbn_pairs_fwd", ptr(Vc), ptr(Vc16), ptr(U), ptr(c), B, d, KC, int(cfg.bilinear_each), int(bf), st)
     # MLP layer 1
     h1pre = buf("h1pre", (B, H1))
     nt = (B + 63) // 64
@@ -481,12 +497,20 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
         gemm(dh1pre, p["mlp.0.weight"], dc, B, KC, H1, H1, 21 * d, KC, False, False, rB=wa_remap(d), stream=st)
     # bilinear backward
     dV = torch.empty((B, 5, d), **f32)
-    dU = torch.empty((B, 5, d), **f32)
-    dU16 = torch.empty((B, 5, d), dtype=torch.bfloat16, device=dev) if (bf and not cfg.bilinear_each) else None
     v16 = bf and not cfg.bilinear_each
-    call("fbn_pairs_bwd", ptr(dc), None if v16 else ptr(a["Vc"]), ptr(a["Vc16"]) if v16 else None, ptr(a["U"]),
-         ptr(dV), ptr(dU), ptr(dU16), B, d, KC, int(cfg.bilinear_each), st)
-    if not cfg.bilinear_each:
+    dU16 = torch.empty((B, 5, d), dtype=torch.bfloat16, device=dev) if v16 else None
+    if a.get("fused_bilinear"):
+        # one launch: dU and dV = dc_V + pair terms + dU W^T (U recomputed on the MFMA)
+        call("fbn_bilinear_bwd", ptr(dc), KC, ptr(a["Vc16"]), ptr(w16["WT"]), ptr(w16["W"]), ptr(dV), ptr(dU16), B,
+             d, st)
+        wg.run(lambda s: gemm(a["Vc16"], dU16, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=s))
+    else:
+        dU = torch.empty((B, 5, d), **f32)
+        call("fbn_pairs_bwd", ptr(dc), None if v16 else ptr(a["Vc"]), ptr(a["Vc16"]) if v16 else None, ptr(a["U"]),
+             ptr(dV), ptr(dU), ptr(dU16), B, d, KC, int(cfg.bilinear_each), st)
+    if a.get("fused_bilinear"):
+        pass
+    elif not cfg.bilinear_each:
         if bf:
             wg.run(lambda s: gemm(a["Vc16"], dU16, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=s))
             gemm(dU16, w16["W"], dV, 5 * B, d, d, d, d, d, False, True, beta=1.0, stream=st)

@@ -316,6 +316,19 @@ int fbn_owner_claim(const int* ids, int n, int* map, int* slot_row, int rank, vo
 int fbn_owner_gather(const int* ids, int n, const float* E, void* out, int* map, int* slot_row, int rank, int D,
                      int out_bf16, void* stream);
 
+/* ---------------------------------------------------------------- fused bilinear (bf16 mode, "all")
+ * Replaces BilinearInteraction "all" (src/model_fibinet.py:60-79,89) and its autograd in ONE launch
+ * each way, MFMA for the W contraction, pair products in the epilogue:
+ *   fwd: c[:, 5D + k*D + n] (bf16) = V_i (.) (V_j W) for pair k = (i, j)   (V16 [B][5][D] bf16,
+ *        WT16 = W^T [D][D] bf16); U = V W is never stored;
+ *   bwd: dU16 [B][5][D] (bf16) and dV [B][5][D] (f32) = dc_V + pair terms + dU W^T from dc [B][ldc]
+ *        (f32: V block at 0, pairs at 5D), recomputing U on the MFMA (W16 = W [D][D] bf16).
+ * fbn_bilinear_supported(D): 1 for the D these kernels are built for (64, 128). */
+int fbn_bilinear_supported(int D);
+int fbn_bilinear_fwd(const short* V16, const short* WT16, short* c, int B, int D, int ldc, void* stream);
+int fbn_bilinear_bwd(const float* dc, int ldc, const short* V16, const short* WT16, const short* W16, float* dV,
+                     short* dU16, int B, int D, void* stream);
+
 /* ---------------------------------------------------------------- device collator
  * Replaces BatchCollator.__call__ (src/dataloader.py:69-121) and InferenceCollator.__call__
  * (src/Prediction.py:28-52): batch row b = dataset row perm[b] of HBM-resident columns item [N],

@@ -100,3 +100,54 @@ def test_table_adam_step_vs_ieee(hip_device):
     print(f"table Adam step vs IEEE: m {dm} ulp, v {dv} ulp, p {dp} ulp")
     assert dm <= 2.0 and dv <= 8.0, (dm, dv)
     assert dp <= 8.0, dp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d,B", [(128, 8192), (128, 100), (64, 333)])
+def test_fused_bilinear_matches_unfused_math(hip_device, d, B):
+    """fbn_bilinear_fwd / _bwd (one MFMA + pair-product launch each way, U never stored) against
+    the same arithmetic in torch on the same bf16 operands: pairs and dU16 within 1 bf16 ulp (U's
+    f32 sums may round differently), dV within 2e-5 x max|dV|.  B = 100 / 333: a partial last
+    tile of samples."""
+    from ctr_recommendation_amd import _lib
+    g = torch.Generator(device=hip_device).manual_seed(3)
+    V16 = (torch.randn((B, 5, d), generator=g, device=hip_device) * 0.5).to(torch.bfloat16)
+    W = torch.randn((d, d), generator=g, device=hip_device) / d ** 0.5
+    W16, WT16 = W.to(torch.bfloat16).contiguous(), W.t().contiguous().to(torch.bfloat16)
+    KC = 15 * d
+    c = torch.zeros((B, KC), dtype=torch.bfloat16, device=hip_device)
+    st = _lib.stream_handle(hip_device)
+    _lib.call("fbn_bilinear_fwd", _lib.ptr(V16), _lib.ptr(WT16), _lib.ptr(c), B, d, KC, st)
+    Vf, Wf = V16.float(), W16.float()
+    U = torch.einsum("bfk,kn->bfn", Vf, Wf)
+    pairs = [(0, 1), (0, 2), (0, 3), (0, 4), (1, 2), (1, 3), (1, 4), (2, 3), (2, 4), (3, 4)]
+    Uabs = torch.einsum("bfk,kn->bfn", Vf.abs(), Wf.abs())          # scale of U's summands
+    ref = torch.cat([(Vf[:, i] * U[:, j]) for i, j in pairs], 1).to(torch.bfloat16).float()
+    got = c[:, 5 * d:].float()
+    # 1 bf16 ulp of the larger value, plus U's f32 summation-order term (U can cancel: its relative
+    # error is then not small although its absolute error is)
+    slack = torch.cat([(Vf[:, i].abs() * Uabs[:, j]) for i, j in pairs], 1) * 2.0 ** -16
+    tol = torch.maximum(ref.abs(), got.abs()) * 2.0 ** -7 + slack
+    assert bool(((got - ref).abs() <= tol).all()), ((got - ref).abs() - tol).max().item()
+    assert bool((c[:, :5 * d] == 0).all())                       # the V block is not the kernel's
+    # backward
+    dc = torch.randn((B, KC), generator=g, device=hip_device) * 1e-3
+    dV = torch.empty((B, 5, d), device=hip_device)
+    dU16 = torch.empty((B, 5, d), dtype=torch.bfloat16, device=hip_device)
+    _lib.call("fbn_bilinear_bwd", _lib.ptr(dc), KC, _lib.ptr(V16), _lib.ptr(WT16), _lib.ptr(W16), _lib.ptr(dV),
+              _lib.ptr(dU16), B, d, st)
+    gv = dc[:, :5 * d].view(B, 5, d).clone()
+    gu = torch.zeros((B, 5, d), device=hip_device)
+    for k, (i, j) in enumerate(pairs):
+        gp = dc[:, (5 + k) * d:(6 + k) * d]
+        gv[:, i] += gp * U[:, j]
+        gu[:, j] += gp * Vf[:, i]
+    gu16 = gu.to(torch.bfloat16)
+    guabs = torch.zeros_like(gu)
+    for k, (i, j) in enumerate(pairs):
+        guabs[:, j] += dc[:, (5 + k) * d:(6 + k) * d].abs() * Vf[:, i].abs()
+    tol = torch.maximum(gu16.float().abs(), dU16.float().abs()) * 2.0 ** -7 + guabs * 2.0 ** -20
+    assert bool(((dU16.float() - gu16.float()).abs() <= tol).all())
+    dV_ref = gv + torch.einsum("bfn,kn->bfk", dU16.float(), Wf)
+    err = (dV - dV_ref).abs().max().item()
+    assert err <= 2e-5 * dV_ref.abs().max().item(), err

@@ -1,0 +1,63 @@
+"""Time the fused bilinear kernels against the GEMM + pair-kernel path at C3 (tuning aid).
+
+  python tools/time_bilinear.py [B] [d]
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from ctr_recommendation_amd import _lib, ops
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
+d = int(sys.argv[2]) if len(sys.argv) > 2 else 128
+dev = torch.device("cuda")
+st = _lib.stream_handle(dev)
+P = _lib.ptr
+V16 = torch.randn((B, 5, d), device=dev).to(torch.bfloat16)
+W = torch.randn((d, d), device=dev) / d ** 0.5
+W16, WT16 = W.to(torch.bfloat16).contiguous(), W.t().contiguous().to(torch.bfloat16)
+KC = 15 * d
+c = torch.zeros((B, KC), dtype=torch.bfloat16, device=dev)
+dc = torch.randn((B, KC), device=dev) * 1e-3
+dV = torch.empty((B, 5, d), device=dev)
+dU = torch.empty((B, 5, d), device=dev)
+dU16 = torch.empty((B, 5, d), dtype=torch.bfloat16, device=dev)
+U = torch.empty((B, 5, d), device=dev)
+
+
+def timeit(fn, n=50):
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n * 1e3
+
+
+def fused_fwd():
+    _lib.call("fbn_bilinear_fwd", P(V16), P(WT16), P(c), B, d, KC, st)
+
+
+def old_fwd():
+    ops.gemm(V16, WT16, U, 5 * B, d, d, d, d, d, False, True, bf16=True, stream=st)
+    _lib.call("fbn_pairs_fwd", None, P(V16), P(U), P(c), B, d, KC, 0, 1, st)
+
+
+def fused_bwd():
+    _lib.call("fbn_bilinear_bwd", P(dc), KC, P(V16), P(WT16), P(W16), P(dV), P(dU16), B, d, st)
+
+
+def old_bwd():
+    _lib.call("fbn_pairs_bwd", P(dc), None, P(V16), P(U), P(dV), P(dU), P(dU16), B, d, KC, 0, st)
+    ops.gemm(dU16, W16, dV, 5 * B, d, d, d, d, d, False, True, beta=1.0, stream=st)
+
+
+for name, fn in (("fused fwd", fused_fwd), ("gemm+pairs fwd", old_fwd), ("fused bwd", fused_bwd),
+                 ("pairs+gemm bwd", old_bwd)):
+    print(f"{name:16s} {timeit(fn):8.1f} us", flush=True)
