@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--probe-steps", type=int, default=10)
     ap.add_argument("--batches", type=int, default=0, help="distinct HBM-resident batches (default F + 32)")
     ap.add_argument("--lazy-window", type=int, default=128, help="lazy table-Adam window F (rows per step: V/F)")
+    ap.add_argument("--no-prefetch", dest="prefetch", action="store_false",
+                    help="N = 1: no ahead-of-time catch-up of the next batch's rows (fbn_adam_prefetch)")
     ap.add_argument("--prime", type=int, default=-1,
                     help="untimed priming steps before the warm-up (default: top the warm-up up to 2F)")
     ap.add_argument("--no-fp32", dest="also_fp32", action="store_false",
@@ -159,7 +161,7 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
     total = 1 + (nb if use_graph else 0) + prime + W + K + args.probe_steps + 16
     init = _initial_state(cfg, V, world, rank, dev)
     tr = FiBiNETTrainer(cfg, total_steps=total, batch_size=B, device=dev, rank=rank, world=world,
-                        init_state=init, stage_on_cpu=rehearsal, lazy_window=F)
+                        init_state=init, stage_on_cpu=rehearsal, lazy_window=F, prefetch_rows=args.prefetch)
     del init
     batches = make_device_batches(nb, B, V, L, dev, seed=2025 + rank)
     sb = {k: v.clone() for k, v in batches[0][0].items()}
@@ -181,10 +183,10 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
         torch.cuda.current_stream().wait_stream(s)
         # one graph per HBM-resident batch (shared memory pool): every step is one replay
         pool = None
-        for b, y in batches:
+        for j, (b, y) in enumerate(batches):
             gr = torch.cuda.CUDAGraph()
             with torch.cuda.graph(gr, pool=pool):
-                tr.step(b, y)
+                tr.step(b, y, next_batch=batches[(j + 1) % nb][0])   # next batch's rows caught up ahead
             pool = gr.pool()
             graphs.append(gr)
         torch.cuda.synchronize()
@@ -198,7 +200,7 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
             tr.step(b, y, next_batch=batches[(i + 1) % nb][0])
         else:
             load(i)
-            tr.step(sb, sl)
+            tr.step(sb, sl, next_batch=batches[(i + 1) % nb][0])
 
     i = 0
     for j in range(prime + W):
@@ -230,6 +232,10 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
     ids = ids[(ids > 0) & (ids >= tr.rows_lo) & (ids < tr.rows_lo + tr.rows_local)]
     uniq = torch.unique(ids) - tr.rows_lo
     lag = (tr.step_dev.to(torch.int64) - tr.last[uniq].to(torch.int64)).double().mean().item()
+    # rows the next step's claimed-row catch-up still has to replay (with the next-batch prefetch,
+    # only rows the previous batch also touched; the rest were replayed beside the previous step)
+    stale = int((tr.last[uniq] < tr.step_dev).sum().item())
+    prefetch = bool(getattr(tr, "prefetch_rows", False)) and world == 1
 
     # ---- probe pass: eager steps with HIP events around the dominant kernels (same stream)
     probe = {}
@@ -239,7 +245,7 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
         # a ~10 ms spin ahead of the step keeps the GPU behind the host's launches, so each event
         # pair brackets only its kernel (as in the graph replays), not host enqueue gaps
         torch.cuda._sleep(20_000_000)
-        tr.step(sb, sl, probe=probe)
+        tr.step(sb, sl, probe=probe, next_batch=batches[i % nb][0] if world == 1 else None)
     torch.cuda.synchronize()
 
     def avg_ms(name):
@@ -272,10 +278,17 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
     add("fields_fwd", "fields_fwd (fused gather + history mean + LN + SENET)", avg_ms("fields_fwd"),
         gather_bytes_per_sample(d) * B, "GB/s", HBM_PEAK_GBS, "hbm", "SURVEY 8(d) 12,984 B/sample x batch")
     dfr = getattr(tr, "deferred", False)
+    # claimed-row catch-up: every entry's id, claim, slot and last (20 B) + the rows it replays
+    crit = stale if prefetch else touched
     add("adam_catchup", "adam_catchup (lazy table Adam: rows claimed this step)", avg_ms("adam_catchup"),
-        catchup_bytes(touched, d, B * (L + 1)) + (touched * (4 * d + 8) if dfr else 0), "GB/s", HBM_PEAK_GBS, "hbm",
-        f"touched {touched} rows x (24 B x d + 8 B{' + 4 B x d + 8 B deferred gradient' if dfr else ''}) "
-        f"+ 4 B per entry; mean replay {lag:.1f} steps per row")
+        catchup_bytes(crit, d, 5 * B * (L + 1)) + (crit * (4 * d + 8) if dfr else 0), "GB/s", HBM_PEAK_GBS, "hbm",
+        f"{B * (L + 1)} entries x 20 B + {crit} replayed rows x (24 B x d + 8 B"
+        f"{' + 4 B x d + 8 B deferred gradient' if dfr else ''}); mean lag {lag:.1f} steps over the {touched} rows")
+    if prefetch:
+        ahead = max(0, touched - stale)
+        add("adam_prefetch", "adam_prefetch (next batch's rows caught up ahead, side stream)", avg_ms("adam_prefetch"),
+            catchup_bytes(ahead, d, 5 * B * (L + 1)) + (ahead * (4 * d + 8) if dfr else 0), "GB/s", HBM_PEAK_GBS,
+            "hbm", f"~{ahead} rows x (24 B x d + 8 B + deferred gradient) + {B * (L + 1)} entries x 20 B")
     add("adam_window", "adam_catchup (lazy table Adam: rolling window, side stream)", avg_ms("adam_window"),
         catchup_bytes(window, d, 0), "GB/s", HBM_PEAK_GBS, "hbm",
         f"window {window} rows x (24 B x d + 8 B); VALU-bound replay of up to F steps per row")
@@ -289,7 +302,7 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
     dominant = max(main_k, key=lambda r: r["avg_launch_ms"]) if main_k else None
     out = {"dt": dt, "K": K, "W": W, "B": B, "L": L, "V": V, "d": d, "rows_local": tr.rows_local, "loss": loss,
            "rooflines": rooflines, "roofline": dominant, "table_adam": tr.table_adam, "graphs": bool(graphs),
-           "prime": prime, "batches": nb, "lag": lag}
+           "prime": prime, "batches": nb, "lag": lag, "stale": stale, "touched": touched, "prefetch": prefetch}
     del graphs, tr, batches
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -352,8 +365,14 @@ def main():
             "table_adam": r["table_adam"],
             "steady_state": {"priming_steps": r["prime"], "warmup_steps": args.warmup,
                              "mean_replay_steps_per_claimed_row": round(r["lag"], 2),
+                             "rows_touched_next_step": r["touched"],
+                             "rows_replayed_on_critical_path": r["stale"],
+                             "next_batch_prefetch": r["prefetch"],
                              "note": "untimed priming tops the warm-up up to 2F = 256 steps so the lazy "
-                                     "table Adam is at steady state whatever --warmup is"},
+                                     "table Adam is at steady state whatever --warmup is; with the next-batch "
+                                     "prefetch the rows of step t+1 that step t does not touch are replayed on "
+                                     "the side stream during step t (exact), so the claimed-row catch-up on the "
+                                     "critical path replays only rows_replayed_on_critical_path rows"},
             "final_loss": round(r["loss"], 5),
         }
         if alt is not None:

@@ -632,6 +632,170 @@ __device__ __forceinline__ void replay_rows(float* __restrict__ p, float* __rest
   *reinterpret_cast<f32x4*>(v + off) = vv;
 }
 
+// One row's replay split into its loads and its arithmetic, so a wave can issue the next round's
+// loads before it computes the current round (adam_catchup_kernel).  pe = pend[r] (read with
+// last[r] while scanning).
+struct RowRegs {
+  f32x4 p, m, v, g;
+  float c;
+  AdamConsts k;   // step k0's constants (the deferred-gradient step), read with the row
+};
+template <int D>
+__device__ __forceinline__ void row_load(RowRegs& x, const float* __restrict__ p, const float* __restrict__ m,
+                                         const float* __restrict__ v, int r, int q, int k0, int pe,
+                                         const PendSrc& ps, const AdamConsts* __restrict__ table) {
+  const size_t off = (size_t)r * D + 4 * q;
+  x.p = *reinterpret_cast<const f32x4*>(p + off);
+  x.m = *reinterpret_cast<const f32x4*>(m + off);
+  x.v = *reinterpret_cast<const f32x4*>(v + off);
+  // branch-free (a load under a branch makes hipcc wait vmcnt(0) at the next use of any load,
+  // which would drain the next round's loads): no deferred gradient -> an L2-resident dummy line
+  const float* ring = ps.ring ? ps.ring : p;
+  const float* coef = ps.coef_hist ? ps.coef_hist : p;
+  const size_t go = pe >= 0 ? (size_t)(k0 % ps.ring_n) * ps.ring_stride + (size_t)pe * D : 0;
+  x.g = *reinterpret_cast<const f32x4*>(ring + go + 4 * q);
+  x.c = coef[pe >= 0 ? k0 : 0];
+  x.k = table[k0];
+}
+template <int D, bool DW>
+__device__ __forceinline__ void row_replay_store(RowRegs& x, float* __restrict__ p, float* __restrict__ m,
+                                                 float* __restrict__ v, int r, int q, int k0, bool deferred, int t,
+                                                 const AdamConsts* __restrict__ win, int w0,
+                                                 const AdamConsts* __restrict__ table, float wd, float b2, float omb2,
+                                                 float eps) {
+  int s = k0;
+  if (deferred) {   // step k0 with the deferred gradient (what fbn_adam_touched would have applied)
+    adam_tab4<DW>(x.p, x.m, x.v, x.g * x.c, wd, b2, omb2, eps, x.k);
+    s = k0 + 1;
+  }
+  for (; s < t && s < w0; ++s) adam_zero_tab4<DW>(x.p, x.m, x.v, wd, b2, omb2, eps, table[s]);
+  for (; s < t; ++s) {
+    const AdamConsts k = win[s - w0];
+    adam_zero_tab4<DW>(x.p, x.m, x.v, wd, b2, omb2, eps, k);
+  }
+  const size_t off = (size_t)r * D + 4 * q;
+  *reinterpret_cast<f32x4*>(p + off) = x.p;
+  *reinterpret_cast<f32x4*>(m + off) = x.m;
+  *reinterpret_cast<f32x4*>(v + off) = x.v;
+}
+
+// D >= 128: one row per round, 64 lanes x D/64 elements.  The row, its replay start k0 and its
+// deferred vector are wave-uniform, so the step loop is scalar and each step's constants arrive by
+// scalar loads (no LDS window, no sort, no lane groups waiting on a longer neighbour row).
+template <int N> struct FVec;
+template <> struct FVec<2> { typedef float T __attribute__((ext_vector_type(2))); };
+template <> struct FVec<4> { typedef f32x4 T; };
+template <bool DW, int N>
+__device__ __forceinline__ void adam_tabv(typename FVec<N>::T& pp, typename FVec<N>::T& mm, typename FVec<N>::T& vv,
+                                          typename FVec<N>::T gg, float wd, float b2, float omb2, float eps,
+                                          const AdamConsts& k) {
+#pragma unroll
+  for (int e = 0; e < N; ++e) {
+    float me = mm[e], ve = vv[e];
+    pp[e] = adam_tab1<DW>(pp[e], me, ve, gg[e], wd, b2, omb2, eps, k);
+    mm[e] = me;
+    vv[e] = ve;
+  }
+}
+template <int D>
+struct WideRow {
+  static constexpr int N = D / 64;
+  typedef typename FVec<N>::T V;
+  V p, m, v, g;
+  float c;
+};
+template <int D>
+__device__ __forceinline__ void wide_load(WideRow<D>& x, const float* __restrict__ p, const float* __restrict__ m,
+                                          const float* __restrict__ v, int r, int k0, int pe, const PendSrc& ps,
+                                          int lane) {
+  typedef typename WideRow<D>::V V;
+  constexpr int N = WideRow<D>::N;
+  const size_t off = (size_t)r * D + lane * N;
+  x.p = *reinterpret_cast<const V*>(p + off);
+  x.m = *reinterpret_cast<const V*>(m + off);
+  x.v = *reinterpret_cast<const V*>(v + off);
+  const float* ring = ps.ring ? ps.ring : p;   // branch-free, as row_load
+  const float* coef = ps.coef_hist ? ps.coef_hist : p;
+  const size_t go = pe >= 0 ? (size_t)(k0 % ps.ring_n) * ps.ring_stride + (size_t)pe * D : 0;
+  x.g = *reinterpret_cast<const V*>(ring + go + lane * N);
+  x.c = coef[pe >= 0 ? k0 : 0];
+}
+// rows a and b (k0a <= k0b after the sort): deferred-gradient steps, then the steps both still
+// need side by side, then the longer row's remaining steps alone (all loop bounds wave-uniform)
+template <int D, bool DW>
+__device__ __forceinline__ void wide_replay_pair(WideRow<D>& a, int ka, int pa, WideRow<D>& b, int kb, int pb, int t,
+                                                 const AdamConsts* __restrict__ table, float wd, float b2,
+                                                 float omb2, float eps) {
+  typedef typename WideRow<D>::V V;
+  constexpr int N = WideRow<D>::N;
+  if (pa >= 0) adam_tabv<DW, N>(a.p, a.m, a.v, a.g * a.c, wd, b2, omb2, eps, table[ka]);
+  if (pb >= 0) adam_tabv<DW, N>(b.p, b.m, b.v, b.g * b.c, wd, b2, omb2, eps, table[kb]);
+  int sa = ka + (pa >= 0 ? 1 : 0), sb = kb + (pb >= 0 ? 1 : 0);
+  const V zero = {};
+  const int both = min(t - sa, t - sb);
+  for (int i = 0; i < both; ++i) {
+    const AdamConsts k1 = table[sa + i], k2 = table[sb + i];
+    adam_tabv<DW, N>(a.p, a.m, a.v, zero, wd, b2, omb2, eps, k1);
+    adam_tabv<DW, N>(b.p, b.m, b.v, zero, wd, b2, omb2, eps, k2);
+  }
+  sa += both > 0 ? both : 0;
+  sb += both > 0 ? both : 0;
+  for (; sa < t; ++sa) adam_tabv<DW, N>(a.p, a.m, a.v, zero, wd, b2, omb2, eps, table[sa]);
+  for (; sb < t; ++sb) adam_tabv<DW, N>(b.p, b.m, b.v, zero, wd, b2, omb2, eps, table[sb]);
+}
+template <int D>
+__device__ __forceinline__ void wide_store(const WideRow<D>& x, float* __restrict__ p, float* __restrict__ m,
+                                           float* __restrict__ v, int r, int lane) {
+  typedef typename WideRow<D>::V V;
+  const size_t off = (size_t)r * D + lane * WideRow<D>::N;
+  *reinterpret_cast<V*>(p + off) = x.p;
+  *reinterpret_cast<V*>(m + off) = x.m;
+  *reinterpret_cast<V*>(v + off) = x.v;
+}
+
+// A wave's cnt rows (lanes 0..cnt-1 hold row r, replay start key, deferred vector pe; sorted by
+// key), brought to T steps two at a time: consecutive rows of the sorted order (similar replay
+// lengths) share the step loop -- four independent update chains per lane -- and the next pair's
+// loads are in flight meanwhile.  Slots past cnt: row 0 with no steps, not stored.
+template <int D, bool DW>
+__device__ __forceinline__ void wide_rows(int r, int key, int pe, int cnt, int T, float* __restrict__ p,
+                                          float* __restrict__ m, float* __restrict__ v, int* __restrict__ last,
+                                          const AdamConsts* __restrict__ table, float wd, float b2, float omb2,
+                                          float eps, const PendSrc& ps, int lane) {
+  auto get = [&](int idx, int& rr, int& kk, int& pp) {   // idx wave-uniform
+    const int sl = idx < cnt ? idx : 0;
+    rr = __builtin_amdgcn_readlane(r, sl);
+    kk = __builtin_amdgcn_readlane(key, sl);
+    pp = __builtin_amdgcn_readlane(pe, sl);
+    if (idx >= cnt) { rr = 0; kk = T; pp = -1; }
+  };
+  int ra, ka, pa, rb, kb, pb;
+  get(0, ra, ka, pa);
+  get(1, rb, kb, pb);
+  WideRow<D> xa, xb;
+  wide_load<D>(xa, p, m, v, ra, ka, pa, ps, lane);
+  wide_load<D>(xb, p, m, v, rb, kb, pb, ps, lane);
+  for (int j0 = 0; j0 < cnt; j0 += 2) {
+    int rna, kna, pna, rnb, knb, pnb;
+    get(j0 + 2, rna, kna, pna);
+    get(j0 + 3, rnb, knb, pnb);
+    WideRow<D> na, nb;
+    wide_load<D>(na, p, m, v, rna, kna, pna, ps, lane);
+    wide_load<D>(nb, p, m, v, rnb, knb, pnb, ps, lane);
+    wide_replay_pair<D, DW>(xa, ka, pa, xb, kb, pb, T, table, wd, b2, omb2, eps);
+    wide_store<D>(xa, p, m, v, ra, lane);
+    last[ra] = T;   // every lane, one address
+    if (ps.pend) ps.pend[ra] = -1;
+    if (j0 + 1 < cnt) {
+      wide_store<D>(xb, p, m, v, rb, lane);
+      last[rb] = T;
+      if (ps.pend) ps.pend[rb] = -1;
+    }
+    xa = na; ra = rna; ka = kna; pa = pna;
+    xb = nb; rb = rnb; kb = knb; pb = pnb;
+  }
+}
+
 // items [0, n_ent): claiming entries (slot_row != -1); items [n_ent, n_ent + chunk): rows of the
 // rolling window not claimed this step.  nrows_total / F / chunk describe the window.
 // In-kernel row claims (single GPU, fbn_adam_claim_catchup): item != null -> entry e = b*(L+1)+t
@@ -661,10 +825,12 @@ __global__ void __launch_bounds__(256) adam_catchup_kernel(float* __restrict__ p
   const int t = *step;
   // every row is within F steps of t (the rolling window): only steps [t - F, t) are staged
   const int w0 = t > F ? t - F : 0;
-  for (int i = threadIdx.x; i < t - w0; i += blockDim.x) {
-    win[i] = table[w0 + i];
+  if constexpr (D < 128) {   // the wide-row path reads the constants by scalar loads
+    for (int i = threadIdx.x; i < t - w0; i += blockDim.x) {
+      win[i] = table[w0 + i];
+    }
+    __syncthreads();
   }
-  __syncthreads();
   const long long roll0 = (long long)(t % F) * chunk;
   const long long nroll = (parts & 2) && roll0 < nrows ? min(chunk, nrows - roll0) : 0;
   if (!(parts & 1)) n_ent = 0;
@@ -680,7 +846,7 @@ __global__ void __launch_bounds__(256) adam_catchup_kernel(float* __restrict__ p
   const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
   for (long long i0 = gw * SCAN; i0 < n; i0 += nw * SCAN) {
     const long long i = i0 + lane;
-    int r = -1, key = 0x7fffffff;
+    int r = -1, key = 0x7fffffff, pe = -1;
     if (lane < SCAN && i < n) {
       if (i < n_ent && cs.item) {
         const long long b = i / (cs.L + 1), tt = i - b * (cs.L + 1);
@@ -707,7 +873,10 @@ __global__ void __launch_bounds__(256) adam_catchup_kernel(float* __restrict__ p
       }
       if (r >= 0) {
         const int k0 = last[r];
-        if (k0 < t) key = k0;
+        if (k0 < t) {
+          key = k0;
+          if (ps.pend) pe = ps.pend[r];
+        }
       }
     }
     const int cnt = __popcll(__ballot(key != 0x7fffffff));
@@ -716,24 +885,100 @@ __global__ void __launch_bounds__(256) adam_catchup_kernel(float* __restrict__ p
     for (int kk = 2; kk <= SCAN; kk <<= 1)
 #pragma unroll
       for (int j = kk >> 1; j > 0; j >>= 1) {
-        const int ok = __shfl_xor(key, j, 64), orr = __shfl_xor(r, j, 64);
+        const int ok = __shfl_xor(key, j, 64), orr = __shfl_xor(r, j, 64), ope = __shfl_xor(pe, j, 64);
         const bool up = (lane & kk) == 0, lower = (lane & j) == 0;
         if (lower == up ? ok < key : ok > key) {
           key = ok;
           r = orr;
+          pe = ope;
         }
       }
-    for (int j0 = 0; j0 < cnt; j0 += RPW) {
+    if constexpr (D >= 128) {
+      wide_rows<D, DW>(r, key, pe, cnt, t, p, m, v, last, table, wd, b2, omb2, eps, ps, lane);
+      continue;
+    }
+    // rounds of RPW rows, software-pipelined: round j+1's loads are issued before round j's
+    // arithmetic (lanes past cnt load row 0 and store nothing)
+    auto fetch = [&](int j0, int& rr, int& k0, int& pp) {
       const int src = j0 + grp;
-      const int rr = __shfl(r, src < 64 ? src : 0, 64);
-      const int k0 = __shfl(key, src < 64 ? src : 0, 64);
-      if (src >= cnt) continue;
-      replay_rows<D, DW>(p, m, v, rr, q, k0, t, win, w0, table, wd, b2, omb2, eps, ps);
-      if (q == 0) {
-        last[rr] = t;
-        if (ps.pend) ps.pend[rr] = -1;
+      const int sl = src < 64 ? src : 0;
+      rr = __shfl(r, sl, 64);
+      k0 = __shfl(key, sl, 64);
+      pp = __shfl(pe, sl, 64);
+      if (src >= cnt) { rr = 0; k0 = 0; pp = -1; }
+    };
+    int rc, kc, pc;
+    fetch(0, rc, kc, pc);
+    RowRegs cur;
+    row_load<D>(cur, p, m, v, rc, q, kc, pc, ps, table);
+    for (int j0 = 0; j0 < cnt; j0 += RPW) {
+      int rn, kn, pn;
+      fetch(j0 + RPW, rn, kn, pn);
+      RowRegs nxt;
+      row_load<D>(nxt, p, m, v, rn, q, kn, pn, ps, table);   // past the last round: row 0, discarded
+      if (j0 + grp < cnt) {
+        row_replay_store<D, DW>(cur, p, m, v, rc, q, kc, pc >= 0, t, win, w0, table, wd, b2, omb2, eps);
+        if (q == 0) {
+          last[rc] = t;
+          if (ps.pend) ps.pend[rc] = -1;
+        }
+      }
+      cur = nxt;
+      rc = rn;
+      kc = kn;
+      pc = pn;
+    }
+  }
+}
+
+// Ahead-of-time catch-up of the NEXT batch (single GPU, D >= 128), on the side stream during step
+// t, after step t's claims: a row of the next batch that batch t does not touch (map == -1) takes
+// only zero-gradient steps through step t inclusive -- g = 0 * coef + wd * p, whatever step t's
+// clip coefficient -- so it is brought to last = t + 1 now (same operations, same order: still
+// bit-identical to eager Adam) and step t + 1's claimed-row catch-up finds it up to date.  A row
+// is taken by the entry whose CAS moves last[r] from its old value to t + 1 (duplicates skip).
+template <int D, bool DW>
+__global__ void __launch_bounds__(256) adam_prefetch_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                            float* __restrict__ v, ClaimSrc cs, int n,
+                                                            int* __restrict__ last,
+                                                            const AdamConsts* __restrict__ table,
+                                                            const int* __restrict__ step, float wd, float b2,
+                                                            float omb2, float eps, PendSrc ps) {
+  constexpr int SCAN = 16;
+  const int T = *step + 1;
+  const int lane = threadIdx.x & 63;
+  const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+  for (long long i0 = gw * SCAN; i0 < n; i0 += nw * SCAN) {
+    const long long i = i0 + lane;
+    int r = -1, key = 0x7fffffff, pe = -1;
+    if (lane < SCAN && i < n) {
+      const long long b = i / (cs.L + 1), tt = i - b * (cs.L + 1);
+      const long long id = tt == 0 ? cs.item[b] : cs.seq[b * cs.L + (tt - 1)];
+      if (id > 0 && id < cs.V && cs.map[id] == -1) {
+        const int k0 = last[id];
+        if (k0 < T && atomicCAS(last + id, k0, T) == k0) {
+          r = (int)id;
+          key = k0;
+          if (ps.pend) pe = ps.pend[id];
+        }
       }
     }
+    const int cnt = __popcll(__ballot(key != 0x7fffffff));
+    if (cnt == 0) continue;
+#pragma unroll
+    for (int kk = 2; kk <= SCAN; kk <<= 1)
+#pragma unroll
+      for (int j = kk >> 1; j > 0; j >>= 1) {
+        const int ok = __shfl_xor(key, j, 64), orr = __shfl_xor(r, j, 64), ope = __shfl_xor(pe, j, 64);
+        const bool up = (lane & kk) == 0, lower = (lane & j) == 0;
+        if (lower == up ? ok < key : ok > key) {
+          key = ok;
+          r = orr;
+          pe = ope;
+        }
+      }
+    wide_rows<D, DW>(r, key, pe, cnt, T, p, m, v, last, table, wd, b2, omb2, eps, ps, lane);
   }
 }
 
@@ -1246,6 +1491,46 @@ extern "C" int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, i
   } else {
     FBN_DISPATCH_D_B(adam_catchup_kernel, false, D, grid, p, m, v, slot_row, n_ent, map, nrows, F, chunk, parts, last,
                      (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, cs);
+  }
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+// single GPU, D >= 128: ahead-of-time catch-up of the next batch's rows (adam_prefetch_kernel);
+// call on the stream of the rolling window, after this step's claims and before its step tail
+extern "C" int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B, int L, long long V, const int* map,
+                                 float* p, float* m, float* v, int D, int* last, const void* consts_table,
+                                 const int* step, float wd, float beta2, float eps, int* pend, const float* ring,
+                                 const float* coef_hist, long long ring_stride, int ring_n, int decoupled,
+                                 void* stream) {
+  const long long n = (long long)B * (L + 1);
+  if (n <= 0) return FBN_OK;
+  if (D < 128 || (D != 128 && D != 256)) { fbn_set_error("fbn_adam_prefetch: D = 128 or 256"); return FBN_ERR_ARG; }
+  if (!item || (L > 0 && !seq) || !map || !last) {
+    fbn_set_error("fbn_adam_prefetch: item, seq (L > 0), map and last are required");
+    return FBN_ERR_ARG;
+  }
+  if (pend && (!ring || !coef_hist)) { fbn_set_error("fbn_adam_prefetch: pend needs ring and coef_hist"); return FBN_ERR_ARG; }
+  const float omb2 = (float)(1.0 - (double)beta2);
+  const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
+  const ClaimSrc cs{item, L > 0 ? seq : nullptr, L, V, const_cast<int*>(map), nullptr, nullptr, nullptr};
+  static const int pcap = getenv("FBN_PREFETCH_BLOCKS") ? atoi(getenv("FBN_PREFETCH_BLOCKS")) : 256;   // tools/ab_prefetch.sh
+  const dim3 grid((unsigned)std::min<long long>(pcap, (n + 63) / 64));
+  hipStream_t st = (hipStream_t)stream;
+  if (D == 128) {
+    if (decoupled)
+      hipLaunchKernelGGL((adam_prefetch_kernel<128, true>), grid, dim3(256), 0, st, p, m, v, cs, (int)n, last,
+                         (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+    else
+      hipLaunchKernelGGL((adam_prefetch_kernel<128, false>), grid, dim3(256), 0, st, p, m, v, cs, (int)n, last,
+                         (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+  } else {
+    if (decoupled)
+      hipLaunchKernelGGL((adam_prefetch_kernel<256, true>), grid, dim3(256), 0, st, p, m, v, cs, (int)n, last,
+                         (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+    else
+      hipLaunchKernelGGL((adam_prefetch_kernel<256, false>), grid, dim3(256), 0, st, p, m, v, cs, (int)n, last,
+                         (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
   }
   FBN_CHECK_LAUNCH();
   return FBN_OK;

@@ -66,7 +66,8 @@ class FiBiNETTrainer:
                  group=None, init_state: Optional[Dict[str, torch.Tensor]] = None, seed: int = 2025,
                  stage_on_cpu: bool = False, dropout_seed: Optional[int] = None, table_adam: str = "lazy",
                  lazy_window: int = 128, defer_table_grads: bool = True, max_norm: float = 10.0,
-                 optimizer: Optional[str] = None, deterministic: Optional[bool] = None):
+                 optimizer: Optional[str] = None, deterministic: Optional[bool] = None,
+                 prefetch_rows: bool = True):
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise RuntimeError("FiBiNETTrainer runs on a HIP device only (no CPU fallback)")
@@ -154,6 +155,9 @@ class FiBiNETTrainer:
         if deterministic is None:
             deterministic = bool(model_cfg.get("deterministic", False)) or os.environ.get("FBN_DETERMINISTIC") == "1"
         self.deterministic = bool(deterministic) and world == 1
+        # lazy table Adam, single GPU, d = 128 / 256: step(..., next_batch=...) brings the next
+        # batch's rows up to date on the side stream during this step (fbn_adam_prefetch)
+        self.prefetch_rows = bool(prefetch_rows) and world == 1 and self.d in (128, 256)
         self.hasdup = torch.zeros((self.n_entries,), **i32) if self.deterministic else None
         self.fx = torch.zeros((self.n_entries, d), dtype=torch.int64, device=dev) if self.deterministic else None
         # ---------------- optimizer schedule + device step state
@@ -209,10 +213,12 @@ class FiBiNETTrainer:
 
         masks_out (tests only): {'m1': u8 [B,512], 'm2': u8 [B,256]} receives the dropout keep-masks.
         probe (bench only): collects HIP-event pairs around the gather and table-Adam launches.
-        next_batch (N > 1): the batch of the FOLLOWING step; its ids are routed and their counts
+        next_batch: the batch of the FOLLOWING step.  N > 1: its ids are routed and their counts
         exchanged during this step on a side stream (RowExchange.prepare), so the next step needs
-        no host sync on the main stream.  That step uses the routing only if it is given the very
-        same id tensors (unmodified); otherwise it routes inline.
+        no host sync on the main stream; that step uses the routing only if it is given the very
+        same id tensors (unmodified), otherwise it routes inline.  N = 1 (lazy table Adam, d = 128
+        / 256): its rows that this batch does not touch are brought up to date on the side stream
+        now (fbn_adam_prefetch) -- exact whatever batch the next step actually gets.
         """
         if self.host_step >= self.total_steps:
             raise ValueError(f"Tried to step {self.host_step + 1} times. The specified number of total steps is "
@@ -256,6 +262,17 @@ class FiBiNETTrainer:
                  ptr(self.map), self.lazy_window, 2, ptr(self.last), ptr(self.sched), ptr(self.step_dev), self.wd_g,
                  self.beta2, self.eps, *self._pend_args(), int(self.decoupled), self.side.cuda_stream)
             _events_end(ev, self.side)
+            nb = next_batch
+            if (claim and nb is not None and self.prefetch_rows and nb["item_id"].dtype == torch.int64
+                    and nb["item_id"].device == self.device):
+                nseq = nb.get("item_seq")
+                nL = nseq.shape[1] if nseq is not None else 0
+                ev = _events(probe, "adam_prefetch", self.side)
+                call("fbn_adam_prefetch", ptr(nb["item_id"]), ptr(nseq) if nL else None, nb["item_id"].shape[0], nL,
+                     self.V, ptr(self.map), ptr(self.E), ptr(self.Em), ptr(self.Ev), d, ptr(self.last),
+                     ptr(self.sched), ptr(self.step_dev), self.wd_g, self.beta2, self.eps, *self._pend_args(),
+                     int(self.decoupled), self.side.cuda_stream)
+                _events_end(ev, self.side)
 
         def start_untouched_adam():
             # eager mode: every row this shard's batch does not touch gets g = wd * p, independent

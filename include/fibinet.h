@@ -259,6 +259,16 @@ int fbn_adam_claim_catchup(const int64_t* item, const int64_t* seq, int B, int L
                            const void* consts_table, const int* step, float wd, float beta2, float eps, int* pend,
                            const float* ring, const float* coef_hist, long long ring_stride, int ring_n, int decoupled,
                            void* stream);
+/* Single GPU, D = 128 / 256: ahead-of-time catch-up of the NEXT batch's rows during this step, on
+ * the rolling window's stream after this step's claims and before its step tail.  A next-batch row
+ * that this batch does not touch (map == -1) takes only zero-gradient steps through the current
+ * step inclusive, so it is brought to last = step + 1 now (bit-identical to eager Adam); the next
+ * step's claimed-row catch-up then finds it up to date.  Replaces the reference's dense Adam over
+ * item_emb.weight (train_fibinet.py:78,121) for those rows, one step early. */
+int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B, int L, long long V, const int* map, float* p,
+                      float* m, float* v, int D, int* last, const void* consts_table, const int* step, float wd,
+                      float beta2, float eps, int* pend, const float* ring, const float* coef_hist,
+                      long long ring_stride, int ring_n, int decoupled, void* stream);
 int fbn_adam_flush(float* p, float* m, float* v, long long nrows, int D, int* last, const void* consts_table,
                    const int* step, float wd, float beta2, float eps, int* pend, const float* ring,
                    const float* coef_hist, long long ring_stride, int ring_n, int decoupled, void* stream);

@@ -227,6 +227,55 @@ def test_deferred_table_grads_bit_identical(hip_device):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("defer", [True, False])
+def test_next_batch_prefetch_bit_identical(hip_device, defer):
+    """fbn_adam_prefetch: with step(..., next_batch=...) the next batch's rows that this batch does
+    not touch are brought up to date on the side stream during this step.  Against the same run
+    without prefetch: losses, table, Adam moments, dense parameters and last[] bit-identical (ids
+    unique within a step, recurring across steps, so prefetched rows also carry deferred gradients
+    and meet rolling windows).  The last step's next_batch is never used: rows prefetched for it
+    are simply up to date early."""
+    V, B, L, steps = 40000, 64, 20, 14
+    cfg = {"embedding_dim": 128, "vocab_size": V}
+    torch.manual_seed(0)
+    init = oracle_build(None, cfg).state_dict()
+    kw = dict(total_steps=20, batch_size=B, device=hip_device, init_state=init, table_adam="lazy", lazy_window=4,
+              defer_table_grads=defer)
+    ref = FiBiNETTrainer(cfg, prefetch_rows=False, **kw)
+    pre = FiBiNETTrainer(cfg, prefetch_rows=True, **kw)
+    assert pre.prefetch_rows
+    g = torch.Generator().manual_seed(7)
+    pool = torch.randperm(V - 1, generator=g)[:3000] + 1
+    batches = []
+    for s in range(steps + 1):
+        b, y = make_batch(300 + s, B, V)
+        ids = pool[torch.randperm(len(pool), generator=g)[:B * (L + 1)]].view(B, L + 1)
+        b["item_id"] = ids[:, 0].clone()
+        seq = ids[:, 1:].clone()
+        seq[b["item_seq"] == 0] = 0
+        b["item_seq"] = seq
+        batches.append(({k: v.to(hip_device) for k, v in b.items()}, y.to(hip_device)))
+    for s in range(steps):
+        db, y = batches[s]
+        l1 = ref.step(db, y).item()
+        l2 = pre.step(db, y, next_batch=batches[s + 1][0]).item()
+        assert l1 == l2, (s, l1, l2)
+    torch.cuda.synchronize()
+    # before the flush: the unused last next_batch's rows that the last batch did not touch are
+    # already at `steps` (prefetched); rows it did touch wait for their deferred gradient
+    nxt, cur = batches[steps][0], batches[steps - 1][0]
+    ids = torch.cat([nxt["item_id"], nxt["item_seq"].flatten()])
+    prev = torch.cat([cur["item_id"], cur["item_seq"].flatten()])
+    ids = ids[(ids > 0) & ~torch.isin(ids, prev)]
+    assert ids.numel() > 0 and int(pre.last[ids].min()) == steps
+    ref.flush()
+    pre.flush()
+    torch.cuda.synchronize()
+    for a, c in ((ref.E, pre.E), (ref.Em, pre.Em), (ref.Ev, pre.Ev), (ref.flat_p, pre.flat_p), (ref.last, pre.last)):
+        assert torch.equal(a, c)
+
+
+@pytest.mark.gpu
 def test_deterministic_mode_bit_identical_runs(hip_device):
     """Deterministic mode: duplicate rows are folded by int64 fixed-point sums, so
     two runs from the same state -- many duplicate ids (V = 400 rows, 256 x 21 entries per step),

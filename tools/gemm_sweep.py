@@ -27,6 +27,8 @@ SH = {  # name: (M, N, K, transA, transB)
 }
 PLANS = [None] + [(bm, bn, s) for bm, bn in ((64, 64), (128, 64), (64, 128), (128, 128)) for s in (1, 2, 4, 8)] \
     + [(bm, bn, s, 8, st) for bm, bn in ((128, 128), (128, 64), (64, 128)) for s in (1, 2, 4, 8) for st in (2, 3, 4)]
+if os.environ.get("FBN_SWEEP_PLANS"):   # "bm,bn,split[,waves[,stages]];..." replaces the list
+    PLANS = [None] + [tuple(int(x) for x in p.split(",")) for p in os.environ["FBN_SWEEP_PLANS"].split(";")]
 
 
 def operands(M, N, K, tA, tB):
