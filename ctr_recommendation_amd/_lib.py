@@ -31,6 +31,7 @@ SIGNATURES = {
     "fbn_gemm_workspace_size": (SZ, [I, I, I, I]),
     "fbn_gemm": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, F, I, I, I, P, P, SZ, P]),
     "fbn_gemm_split": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, P, P, SZ, P, I, I, P, I, I, P]),
+    "fbn_gemm_bf16out": (I, [P, P, P, I, I, I, I, I, I, I, I, P]),
     "fbn_bn_tile_stats": (I, [P, I, I, P, P, P]),
     "fbn_bn_tile_moments": (I, [P, I, I, P, P]),
     "fbn_bn_moments_finalize": (I, [P, D, I, P, P, P, P, F, F, I, P]),
@@ -95,7 +96,7 @@ SIGNATURES = {
     "fbn_owner_gather": (I, [P, I, P, P, P, P, I, I, I, P]),
     "fbn_bilinear_supported": (I, [I]),
     "fbn_bilinear_fwd": (I, [P, P, P, I, I, I, P]),
-    "fbn_bilinear_bwd": (I, [P, I, P, P, P, P, P, I, I, P]),
+    "fbn_bilinear_bwd": (I, [P, I, I, P, P, P, P, P, I, I, P]),
     "fbn_collate": (I, [P, I, P, P, I, I, P, P, P, P, P, LL, P, I, P, P, P, P, P, P, P, P, P]),
     "fbn_collate_zero_if": (I, [P, LL, P, P]),
 }

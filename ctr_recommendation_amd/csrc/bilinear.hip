@@ -147,8 +147,15 @@ __global__ void __launch_bounds__(2 * D) bilinear_fwd_kernel(const short* __rest
   }
 }
 
-template <int D>
-__global__ void __launch_bounds__(2 * D, 2) bilinear_bwd_kernel(const float* __restrict__ dc, int ldc,
+// dc row segment (4 consecutive values) as f32: DC16 = dc is bf16 (fbn_gemm_bf16out) or f32
+template <bool DC16>
+__device__ __forceinline__ f32x4 ld_dc4(const void* __restrict__ row, int off) {
+  if constexpr (DC16) return ld_bf4(reinterpret_cast<const short*>(row) + off);
+  else return *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(row) + off);
+}
+
+template <int D, bool DC16>
+__global__ void __launch_bounds__(2 * D, 2) bilinear_bwd_kernel(const void* __restrict__ dc, int ldc,
                                                             const short* __restrict__ V16, const short* __restrict__ WT16,
                                                             const short* __restrict__ W16, float* __restrict__ dV,
                                                             short* __restrict__ dU16, int B) {
@@ -171,7 +178,7 @@ __global__ void __launch_bounds__(2 * D, 2) bilinear_bwd_kernel(const float* __r
   __syncthreads();                          // no wave still reads the V tile: dU may overwrite it
   const int s = lane & 15, lq = lane >> 4;
   const bool live = s < ns;
-  const float* dcr = dc + (size_t)(b0 + (live ? s : 0)) * ldc;
+  const char* dcr = reinterpret_cast<const char*>(dc) + (size_t)(b0 + (live ? s : 0)) * ldc * (DC16 ? 2 : 4);
 #pragma unroll
   for (int rb = 0; rb < 2; ++rb) {
     const int n0 = 32 * w + 16 * rb + 4 * lq;
@@ -179,12 +186,12 @@ __global__ void __launch_bounds__(2 * D, 2) bilinear_bwd_kernel(const float* __r
 #pragma unroll
     for (int f = 0; f < 5; ++f) {
       v[f] = ld_bf4(sV + swz<D>(f * TS + s, n0));
-      gv[f] = live ? *reinterpret_cast<const f32x4*>(dcr + f * D + n0) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      gv[f] = live ? ld_dc4<DC16>(dcr, f * D + n0) : (f32x4){0.f, 0.f, 0.f, 0.f};
       gu[f] = (f32x4){0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int k = 0; k < 10; ++k) {
-      const f32x4 gp = live ? *reinterpret_cast<const f32x4*>(dcr + (5 + k) * D + n0) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      const f32x4 gp = live ? ld_dc4<DC16>(dcr, (5 + k) * D + n0) : (f32x4){0.f, 0.f, 0.f, 0.f};
       gv[PI[k]] += gp * acc[rb][PJ[k]];
       gu[PJ[k]] += gp * v[PI[k]];
     }
@@ -230,18 +237,25 @@ extern "C" int fbn_bilinear_fwd(const short* V16, const short* WT16, short* c, i
   return FBN_OK;
 }
 
-extern "C" int fbn_bilinear_bwd(const float* dc, int ldc, const short* V16, const short* WT16, const short* W16,
-                                float* dV, short* dU16, int B, int D, void* stream) {
+extern "C" int fbn_bilinear_bwd(const void* dc, int ldc, int dc_bf16, const short* V16, const short* WT16,
+                                const short* W16, float* dV, short* dU16, int B, int D, void* stream) {
   if (B <= 0) return FBN_OK;
-  if (!dc || !V16 || !WT16 || !W16 || !dV || !dU16 || (ldc & 3) || ((uintptr_t)dc & 15) || ((uintptr_t)dV & 15) ||
+  if (!dc || !V16 || !WT16 || !W16 || !dV || !dU16 || (ldc & 3) || ((uintptr_t)dc & 7) || ((uintptr_t)dV & 15) ||
       ((uintptr_t)V16 & 15) || ((uintptr_t)WT16 & 15) || ((uintptr_t)W16 & 15) || ((uintptr_t)dU16 & 7)) {
-    fbn_set_error("fbn_bilinear_bwd: all operands required and aligned (16 B; dU16 8 B), ldc % 4 == 0");
+    fbn_set_error("fbn_bilinear_bwd: all operands required and aligned (16 B; dc, dU16 8 B), ldc % 4 == 0");
     return FBN_ERR_ARG;
   }
   const dim3 grid((unsigned)((B + TS - 1) / TS));
   hipStream_t st = (hipStream_t)stream;
-  if (D == 128) hipLaunchKernelGGL(bilinear_bwd_kernel<128>, grid, dim3(256), 0, st, dc, ldc, V16, WT16, W16, dV, dU16, B);
-  else if (D == 64) hipLaunchKernelGGL(bilinear_bwd_kernel<64>, grid, dim3(128), 0, st, dc, ldc, V16, WT16, W16, dV, dU16, B);
+  if (!dc_bf16 && ((uintptr_t)dc & 15)) { fbn_set_error("fbn_bilinear_bwd: f32 dc must be 16-B aligned"); return FBN_ERR_ARG; }
+  if (D == 128 && dc_bf16)
+    hipLaunchKernelGGL((bilinear_bwd_kernel<128, true>), grid, dim3(256), 0, st, dc, ldc, V16, WT16, W16, dV, dU16, B);
+  else if (D == 128)
+    hipLaunchKernelGGL((bilinear_bwd_kernel<128, false>), grid, dim3(256), 0, st, dc, ldc, V16, WT16, W16, dV, dU16, B);
+  else if (D == 64 && dc_bf16)
+    hipLaunchKernelGGL((bilinear_bwd_kernel<64, true>), grid, dim3(128), 0, st, dc, ldc, V16, WT16, W16, dV, dU16, B);
+  else if (D == 64)
+    hipLaunchKernelGGL((bilinear_bwd_kernel<64, false>), grid, dim3(128), 0, st, dc, ldc, V16, WT16, W16, dV, dU16, B);
   else { fbn_set_error("fbn_bilinear_bwd: D must be 64 or 128"); return FBN_ERR_UNSUPPORTED; }
   FBN_CHECK_LAUNCH();
   return FBN_OK;

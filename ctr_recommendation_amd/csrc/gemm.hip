@@ -56,6 +56,7 @@ struct GemmArgs {
   const void* A2;
   const void* B2;
   int lda2, kseg, ldb2, nseg;
+  int c16;      // C is bf16 (short*, ldc in elements): split == 1, no stats / beta (fbn_gemm_bf16out)
 };
 
 template <bool BF16> struct GemmTraits;
@@ -266,6 +267,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[T
         if (m >= g.M) continue;
         if (split) {
           g.ws[((size_t)blockIdx.z * g.M + m) * g.N + n] = acc[i][j][e];
+        } else if (g.c16) {
+          reinterpret_cast<short*>(g.C)[(size_t)m * g.ldc + nc] = f2bf(acc[i][j][e] + bv);
         } else {
           float* cp = g.C + (size_t)m * g.ldc + nc;
           float v = acc[i][j][e] + bv;
@@ -860,7 +863,7 @@ static int gemm_impl(const void* A, const void* B, float* C, const float* bias, 
                      int ldb, int ldc, int transA, int transB, int rB_seg, int rB_off0, int rB_off1, int rC_seg,
                      int rC_off0, int rC_off1, float beta, int bf16, int a16, int b16, float* stats, float* ws,
                      size_t ws_bytes, const void* A2, int lda2, int kseg, const void* B2, int ldb2, int nseg,
-                     void* stream);
+                     void* stream, int c16 = 0);
 
 extern "C" int fbn_gemm(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, int lda,
                         int ldb, int ldc, int transA, int transB, int rB_seg, int rB_off0, int rB_off1, int rC_seg,
@@ -887,11 +890,21 @@ extern "C" int fbn_gemm_split(const void* A, const void* B, float* C, const floa
                    B2 ? nseg : 0x7fffffff, stream);
 }
 
+// bf16 operands, bf16 C (rounded once from the f32 accumulators; C[m * ldc + n]); no bias, beta,
+// remap or statistics, never split along K.  The bf16-mode dgrad of the MLP input (dc), whose only
+// reader (fbn_bilinear_bwd) takes it in bf16: half the bytes written and read.
+extern "C" int fbn_gemm_bf16out(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                                int transA, int transB, void* stream) {
+  return gemm_impl(A, B, reinterpret_cast<float*>(C), nullptr, M, N, K, lda, ldb, ldc, transA, transB, 0x7fffffff, 0, 0,
+                   0x7fffffff, 0, 0, 0.f, 1, 1, 1, nullptr, nullptr, 0, nullptr, 0, 0x7fffffff, nullptr, 0, 0x7fffffff,
+                   stream, 1);
+}
+
 static int gemm_impl(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, int lda,
                      int ldb, int ldc, int transA, int transB, int rB_seg, int rB_off0, int rB_off1, int rC_seg,
                      int rC_off0, int rC_off1, float beta, int bf16, int a16, int b16, float* stats, float* ws,
                      size_t ws_bytes, const void* A2, int lda2, int kseg, const void* B2, int ldb2, int nseg,
-                     void* stream) {
+                     void* stream, int c16) {
   if (M <= 0 || N <= 0) return FBN_OK;
   if (!A || !B || !C) { fbn_set_error("fbn_gemm: null operand"); return FBN_ERR_ARG; }
   // 16-B vector loads along the contiguous dimension of every operand
@@ -912,6 +925,7 @@ static int gemm_impl(const void* A, const void* B, float* C, const float* bias, 
   g.beta = beta;
   g.A2 = A2; g.lda2 = lda2; g.kseg = kseg;
   g.B2 = B2; g.ldb2 = ldb2; g.nseg = nseg;
+  g.c16 = c16;
   const int bk = bf16 ? 64 : 32;
   // LDS-DMA path: bf16 operands, K % 64 == 0, 16-B rows; k-major operands need their
   // M / N extent in whole 8-element chunks
@@ -927,7 +941,7 @@ static int gemm_impl(const void* A, const void* B, float* C, const float* bias, 
     if (sscanf(f, "%d,%d,%d,%d,%d", &a, &b, &c, &w, &sg) >= 3) p = {a, b, c, w, sg};
   }
   g.stats = stats;
-  if (p.split > 1 && (!ws || ws_bytes < (size_t)p.split * M * N * sizeof(float))) p.split = 1;
+  if (p.split > 1 && (c16 || !ws || ws_bytes < (size_t)p.split * M * N * sizeof(float))) p.split = 1;
   int per = fbn_cdiv(K, p.split);
   per = fbn_cdiv(per, bk) * bk;
   p.split = K > 0 ? fbn_cdiv(K, per) : 1;

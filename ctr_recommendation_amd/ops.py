@@ -482,18 +482,25 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     bn_backward(dh1, None, None, a["h1"], scale, a["h1pre"], a["mean1"], a["inv1"], p["mlp.1.weight"], B, H1, ntot,
                 dh1pre, g["mlp.1.weight"], g["mlp.1.bias"], None, coll, st, dpre16=dh1pre16,
                 bias_grad=g["mlp.0.bias"], sums=sums)
-    dc = torch.empty((B, KC), **f32)
+    # weight gradient of the MLP input layer (side work), then its dgrad dc
     if a.get("split_c"):
         wg.run(lambda s: gemm_split(dh1pre16, a["Vc16"], g["mlp.0.weight"], H1, KC, B, H1, 5 * d, 21 * d, True,
                                     False, rC=wa_remap(d), stream=s, B2=a["c"][:, 5 * d:], ldb2=KC, nseg=5 * d))
-        gemm(dh1pre16, w16["WaT"], dc, B, KC, H1, H1, H1, KC, False, True, stream=st)
     elif bf:
         wg.run(lambda s: gemm(dh1pre16, a["c"], g["mlp.0.weight"], H1, KC, B, H1, KC, 21 * d, True, False,
                               rC=wa_remap(d), stream=s))
-        gemm(dh1pre16, w16["WaT"], dc, B, KC, H1, H1, H1, KC, False, True, stream=st)
     else:
         wg.run(lambda s: gemm(dh1pre, a["c"], g["mlp.0.weight"], H1, KC, B, H1, KC, 21 * d, True, False,
                               rC=wa_remap(d), stream=s))
+    if a.get("fused_bilinear"):
+        # dc in bf16: its one reader, the fused bilinear backward, widens it on load
+        dc = torch.empty((B, KC), **bf16_)
+        call("fbn_gemm_bf16out", ptr(dh1pre16), ptr(w16["WaT"]), ptr(dc), B, KC, H1, H1, H1, KC, 0, 1, st)
+    elif bf:
+        dc = torch.empty((B, KC), **f32)
+        gemm(dh1pre16, w16["WaT"], dc, B, KC, H1, H1, H1, KC, False, True, stream=st)
+    else:
+        dc = torch.empty((B, KC), **f32)
         gemm(dh1pre, p["mlp.0.weight"], dc, B, KC, H1, H1, 21 * d, KC, False, False, rB=wa_remap(d), stream=st)
     # bilinear backward
     dV = torch.empty((B, 5, d), **f32)
@@ -501,8 +508,8 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     dU16 = torch.empty((B, 5, d), dtype=torch.bfloat16, device=dev) if v16 else None
     if a.get("fused_bilinear"):
         # one launch: dU and dV = dc_V + pair terms + dU W^T (U recomputed on the MFMA)
-        call("fbn_bilinear_bwd", ptr(dc), KC, ptr(a["Vc16"]), ptr(w16["WT"]), ptr(w16["W"]), ptr(dV), ptr(dU16), B,
-             d, st)
+        call("fbn_bilinear_bwd", ptr(dc), KC, int(dc.dtype == torch.bfloat16), ptr(a["Vc16"]), ptr(w16["WT"]),
+             ptr(w16["W"]), ptr(dV), ptr(dU16), B, d, st)
         wg.run(lambda s: gemm(a["Vc16"], dU16, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=s))
     else:
         dU = torch.empty((B, 5, d), **f32)

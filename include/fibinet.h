@@ -57,6 +57,12 @@ int fbn_gemm(const void* A, const void* B, float* C, const float* bias, int M, i
  * (A(m,k), k >= kseg, at A2[m*lda2 + k - kseg]); B2/nseg -- a k-major B is [B | B2] along N
  * (B(k,n), n >= nseg, at B2[k*ldb2 + n - nseg]); segments multiples of 128.  The MLP input
  * [V_1..V_5 | pairs] is read from the bf16 fields (Vc16) and the pair block of c without a copy. */
+/* bf16 operands (as fbn_gemm with bf16 = a16 = b16 = 1), C stored in bf16 (C[m * ldc + n], rounded
+ * once from the f32 accumulators); no bias, beta, remap or statistics.  The bf16-mode dgrad
+ * dc = dh1 Wa of the MLP input (src/model_fibinet.py:126-130 autograd), read only by
+ * fbn_bilinear_bwd. */
+int fbn_gemm_bf16out(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                     int transA, int transB, void* stream);
 int fbn_gemm_split(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, int lda, int ldb,
                    int ldc, int transA, int transB, int rC_seg, int rC_off0, int rC_off1, float beta, float* stats,
                    float* ws, size_t ws_bytes, const void* A2, int lda2, int kseg, const void* B2, int ldb2, int nseg,
@@ -332,12 +338,13 @@ int fbn_owner_gather(const int* ids, int n, const float* E, void* out, int* map,
  *   fwd: c[:, 5D + k*D + n] (bf16) = V_i (.) (V_j W) for pair k = (i, j)   (V16 [B][5][D] bf16,
  *        WT16 = W^T [D][D] bf16); U = V W is never stored;
  *   bwd: dU16 [B][5][D] (bf16) and dV [B][5][D] (f32) = dc_V + pair terms + dU W^T from dc [B][ldc]
- *        (f32: V block at 0, pairs at 5D), recomputing U on the MFMA (W16 = W [D][D] bf16).
+ *        (V block at 0, pairs at 5D; f32, or bf16 when dc_bf16 -- fbn_gemm_bf16out's output),
+ *        recomputing U on the MFMA (W16 = W [D][D] bf16).
  * fbn_bilinear_supported(D): 1 for the D these kernels are built for (64, 128). */
 int fbn_bilinear_supported(int D);
 int fbn_bilinear_fwd(const short* V16, const short* WT16, short* c, int B, int D, int ldc, void* stream);
-int fbn_bilinear_bwd(const float* dc, int ldc, const short* V16, const short* WT16, const short* W16, float* dV,
-                     short* dU16, int B, int D, void* stream);
+int fbn_bilinear_bwd(const void* dc, int ldc, int dc_bf16, const short* V16, const short* WT16, const short* W16,
+                     float* dV, short* dU16, int B, int D, void* stream);
 
 /* ---------------------------------------------------------------- device collator
  * Replaces BatchCollator.__call__ (src/dataloader.py:69-121) and InferenceCollator.__call__

@@ -103,12 +103,13 @@ def test_table_adam_step_vs_ieee(hip_device):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("d,B", [(128, 8192), (128, 100), (64, 333)])
-def test_fused_bilinear_matches_unfused_math(hip_device, d, B):
+@pytest.mark.parametrize("d,B,dc16", [(128, 8192, 1), (128, 8192, 0), (128, 100, 1), (64, 333, 0)])
+def test_fused_bilinear_matches_unfused_math(hip_device, d, B, dc16):
     """fbn_bilinear_fwd / _bwd (one MFMA + pair-product launch each way, U never stored) against
     the same arithmetic in torch on the same bf16 operands: pairs and dU16 within 1 bf16 ulp (U's
     f32 sums may round differently), dV within 2e-5 x max|dV|.  B = 100 / 333: a partial last
-    tile of samples."""
+    tile of samples.  dc16: the incoming gradient dc in bf16 (fbn_gemm_bf16out's output, the
+    trainer's bf16 mode) or f32."""
     from ctr_recommendation_amd import _lib
     g = torch.Generator(device=hip_device).manual_seed(3)
     V16 = (torch.randn((B, 5, d), generator=g, device=hip_device) * 0.5).to(torch.bfloat16)
@@ -132,10 +133,12 @@ def test_fused_bilinear_matches_unfused_math(hip_device, d, B):
     assert bool((c[:, :5 * d] == 0).all())                       # the V block is not the kernel's
     # backward
     dc = torch.randn((B, KC), generator=g, device=hip_device) * 1e-3
+    dc_in = dc.to(torch.bfloat16) if dc16 else dc
+    dc = dc_in.float()                                            # the values the kernel sees
     dV = torch.empty((B, 5, d), device=hip_device)
     dU16 = torch.empty((B, 5, d), dtype=torch.bfloat16, device=hip_device)
-    _lib.call("fbn_bilinear_bwd", _lib.ptr(dc), KC, _lib.ptr(V16), _lib.ptr(WT16), _lib.ptr(W16), _lib.ptr(dV),
-              _lib.ptr(dU16), B, d, st)
+    _lib.call("fbn_bilinear_bwd", _lib.ptr(dc_in), KC, dc16, _lib.ptr(V16), _lib.ptr(WT16), _lib.ptr(W16),
+              _lib.ptr(dV), _lib.ptr(dU16), B, d, st)
     gv = dc[:, :5 * d].view(B, 5, d).clone()
     gu = torch.zeros((B, 5, d), device=hip_device)
     for k, (i, j) in enumerate(pairs):
@@ -151,3 +154,21 @@ def test_fused_bilinear_matches_unfused_math(hip_device, d, B):
     dV_ref = gv + torch.einsum("bfn,kn->bfk", dU16.float(), Wf)
     err = (dV - dV_ref).abs().max().item()
     assert err <= 2e-5 * dV_ref.abs().max().item(), err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(8192, 1920, 512), (300, 200, 128)])
+def test_gemm_bf16out_is_rounded_f32_gemm(hip_device, M, N, K):
+    """fbn_gemm_bf16out (the bf16-mode dc = dh1 Wa): the same plan and accumulation as fbn_gemm's
+    f32 output, rounded once to bf16 -- bit-identical to the f32 result's round-to-nearest-even."""
+    from ctr_recommendation_amd import _lib
+    g = torch.Generator(device=hip_device).manual_seed(11)
+    A = torch.randn((M, K), generator=g, device=hip_device).to(torch.bfloat16)
+    Bt = torch.randn((N, K), generator=g, device=hip_device).to(torch.bfloat16)     # B^T, as WaT
+    st = _lib.stream_handle(hip_device)
+    C32 = torch.empty((M, N), device=hip_device)
+    ops.gemm(A, Bt, C32, M, N, K, K, K, N, False, True, stream=st)
+    C16 = torch.empty((M, N), dtype=torch.bfloat16, device=hip_device)
+    _lib.call("fbn_gemm_bf16out", _lib.ptr(A), _lib.ptr(Bt), _lib.ptr(C16), M, N, K, K, K, N, 0, 1, st)
+    torch.cuda.synchronize()
+    assert torch.equal(C16, C32.to(torch.bfloat16))

@@ -3,7 +3,8 @@
   python tools/step_timeline.py run_kernel_trace.csv [--steps N] [--verbose]
 
 Steps are split at claim_rows_kernel (or, fused, the claimed-row adam_catchup).  The rolling-window Adam replay (adam_catchup on 256
-workgroups) runs on the side stream; every other kernel is on the main stream.  Prints, per step,
+workgroups) and the next-batch prefetch (adam_prefetch) run on the side stream ("window" below:
+their span); every other kernel is on the main stream.  Prints, per step,
 the span, the main stream's busy time and idle gaps, the window's span, and (--verbose) the
 kernels in order with their durations and how much of each overlapped the window.
 """
@@ -30,7 +31,10 @@ def main():
     starts = [s for j, s in enumerate(starts[:-1]) if any(match in e[2] for e in ev[s:starts[j + 1]])] + starts[-1:]
 
     def is_window(k, ks):
-        # the rolling-window replay: the adam_catchup launch of the step with the smaller grid
+        # side stream: the rolling-window replay (the adam_catchup launch of the step with the
+        # smaller grid) and the next batch's ahead-of-time catch-up (adam_prefetch)
+        if "adam_prefetch" in k[2]:
+            return True
         cs = [c[3] for c in ks if "adam_catchup" in c[2]]
         return "adam_catchup" in k[2] and len(cs) > 1 and k[3] == min(cs)
     agg = defaultdict(list)
@@ -54,7 +58,7 @@ def main():
         for k in main_k[1:]:
             gaps += max(0, k[0] - last)
             last = max(last, k[1])
-        w = win[0] if win else (t0, t0, "", 0)
+        w = (min(k[0] for k in win), max(k[1] for k in win), "", 0) if win else (t0, t0, "", 0)
         print(f"step span {(t1 - t0) / 1e3:7.1f} us | main busy {busy / 1e3:6.1f} gaps {gaps / 1e3:5.1f} | window "
               f"{(w[1] - w[0]) / 1e3:6.1f} us [+{(w[0] - t0) / 1e3:.1f}, +{(w[1] - t0) / 1e3:.1f}]")
         for k in main_k:

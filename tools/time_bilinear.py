@@ -50,7 +50,7 @@ def old_fwd():
 
 
 def fused_bwd():
-    _lib.call("fbn_bilinear_bwd", P(dc), KC, P(V16), P(WT16), P(W16), P(dV), P(dU16), B, d, st)
+    _lib.call("fbn_bilinear_bwd", P(dc), KC, 0, P(V16), P(WT16), P(W16), P(dV), P(dU16), B, d, st)
 
 
 def old_bwd():
