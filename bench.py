@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--probe-steps", type=int, default=10)
     ap.add_argument("--batches", type=int, default=0, help="distinct HBM-resident batches (default F + 32)")
     ap.add_argument("--lazy-window", type=int, default=128, help="lazy table-Adam window F (rows per step: V/F)")
+    ap.add_argument("--zipf", type=float, default=0.0,
+                    help="item / history ids ~ Zipf(s) (SURVEY 8(d): 1.05) instead of uniform")
     ap.add_argument("--no-prefetch", dest="prefetch", action="store_false",
                     help="N = 1: no ahead-of-time catch-up of the next batch's rows (fbn_adam_prefetch)")
     ap.add_argument("--prime", type=int, default=-1,
@@ -163,7 +165,7 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
     tr = FiBiNETTrainer(cfg, total_steps=total, batch_size=B, device=dev, rank=rank, world=world,
                         init_state=init, stage_on_cpu=rehearsal, lazy_window=F, prefetch_rows=args.prefetch)
     del init
-    batches = make_device_batches(nb, B, V, L, dev, seed=2025 + rank)
+    batches = make_device_batches(nb, B, V, L, dev, seed=2025 + rank, zipf=args.zipf)
     sb = {k: v.clone() for k, v in batches[0][0].items()}
     sl = batches[0][1].clone()
 
@@ -352,7 +354,9 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16" if args.dtype == "bf16" else "fp32",
             "data": f"synthetic (MicroLens-shaped, seeded, HBM-resident, {r['batches']} distinct batches cycled: "
-                    f"fresh ids every step; random-init weights)",
+                    f"fresh ids every step, "
+                    + (f"Zipf({args.zipf}) item / history ids" if args.zipf > 0 else "uniform ids")
+                    + "; random-init weights)",
             "config": {"workload": "C3: FiBiNET emb_dim=128 + item_emb_d128, batch 8192/GPU, history 20, "
                                    + ("bf16 GEMM operands / fp32 accumulation + fp32 master weights and Adam"
                                       if args.dtype == "bf16" else "fp32 throughout"),

@@ -79,10 +79,10 @@ SIGNATURES = {
     "fbn_adam_table": (I, [P, P, P, LL, I, P, P, P, P, I, P, P, P, F, F, F, I, P]),
     "fbn_adam_touched": (I, [P, P, P, I, P, P, P, P, I, I, P, P, P, F, F, F, P, P]),
     "fbn_adam_catchup": (I, [P, P, P, LL, I, P, I, P, I, I, P, P, P, F, F, F, P, P, P, LL, I, I, P]),
-    "fbn_adam_claim_catchup": (I, [P, P, I, I, LL, P, P, P, P, P, P, P, LL, I, I, P, P, P, F, F, F, P, P, P, LL, I, I,
-                                   P]),
+    "fbn_adam_claim_catchup": (I, [P, P, I, I, LL, P, P, P, P, P, P, P, P, LL, I, I, P, P, P, F, F, F, P, P, P, LL, I,
+                                   I, P]),
     "fbn_adam_flush": (I, [P, P, P, LL, I, P, P, P, F, F, F, P, P, P, LL, I, I, P]),
-    "fbn_adam_prefetch": (I, [P, P, I, I, LL, P, P, P, P, I, P, P, P, F, F, F, P, P, P, LL, I, I, P]),
+    "fbn_adam_prefetch": (I, [P, P, I, I, LL, P, P, P, P, P, I, P, P, P, F, F, F, P, P, P, LL, I, I, P]),
     "fbn_adam_selftest": (I, [I, ctypes.c_uint, P, P]),
     "fbn_adam_step_tail": (I, [P, P, P, P, LL, P, F, P, P, P, P, P, I, P, P, P, P, I, I, P, P, F, F, F, P, P, P, P, I, I,
                                P, P, P, P, I, P, P]),

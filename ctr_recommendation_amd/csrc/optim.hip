@@ -195,6 +195,8 @@ __global__ void adam_dense_kernel(float* __restrict__ p, const float* __restrict
 // Lp1 | FBN_GRAD_FULL (deterministic mode): extra[e] of a flagged claimer holds the row's FULL
 // gradient (fbn_sparse_fold_fx), not the sum of its duplicates
 #define FBN_GRAD_FULL 0x10000
+#define FBN_FOLD_CHUNKS 1     // sparse_fixup_dup_kernel: 64-entry chunks per wave
+#define FBN_FOLD_THREADS 1024 // sparse_fixup_dup_kernel: 16 waves share one LDS table
 struct GradSrc {
   const float* vec;     // Lp1 > 1: [B][2][D] per-sample vectors;  Lp1 == 1: [n][D] per-entry rows
   float* extra;         // [n][D] duplicate accumulation (single GPU) or null
@@ -282,25 +284,132 @@ __global__ void claim_rows_kernel(const int64_t* __restrict__ item, const int64_
 }
 
 // duplicates resolved at claim time (single GPU): extra[dup[e]] += vec(e), claimer flagged.
-// One entry per lane for the scan; each duplicate (rare) is then added by the whole wave
-// (D/64 consecutive floats per lane: coalesced atomics).
+// One entry per lane.  Popular rows (Zipf ids: the hottest row can take ~9 % of a batch's
+// entries) must not take one row of atomics per duplicate -- same-address atomics serialise at
+// the memory side -- so duplicates are summed on chip first, in two levels:
+//  * wave: a wave's 64 entries span a few samples, each with just two gradient vectors (item
+//    slot, history slots); the wave loads those vectors once, together, and a claimer's sum is
+//    (number of its lanes on each vector) x vector;
+//  * block: a claimer with several lanes in a chunk (a popular row) adds its chunk sum into a small
+//    LDS table keyed by claimer (LDS float atomics, at most 4 probes); the table is flushed with
+//    ONE row of global atomics and ONE flag per (block, claimer).  Single duplicates, and
+//    claimers that find no slot, add straight to global memory.
 template <int D>
-__global__ void __launch_bounds__(256) sparse_fixup_dup_kernel(const int* __restrict__ dup, int n, GradSrc s) {
-  const int lane = threadIdx.x & 63;
-  for (long long e0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) - lane; e0 < n;
-       e0 += (long long)gridDim.x * blockDim.x) {
-    const long long e = e0 + lane;
-    const int u = e < n ? dup[e] : -1;
-    unsigned long long mask = __ballot(u >= 0);
-    while (mask) {
-      const int l = __ffsll((long long)mask) - 1;
-      mask &= mask - 1;
-      const int ue = __shfl(u, l, 64);
-      const float* src = grad_base<D>(s, (int)(e0 + l));
+__global__ void __launch_bounds__(FBN_FOLD_THREADS) sparse_fixup_dup_kernel(const int* __restrict__ dup, int n, GradSrc s) {
+  constexpr int NPL = D / 64 > 0 ? D / 64 : 1;   // floats per lane of a row
+  constexpr int MAXV = 16;                        // distinct vectors of a wave chunk (2 per sample)
+  constexpr int CPW = FBN_FOLD_CHUNKS;            // 64-entry chunks per wave
+  constexpr int NS = D >= 256 ? 32 : 64;          // LDS slots (NS x D floats)
+  __shared__ int skey[NS];
+  __shared__ float sacc[NS * D];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < NS; i += blockDim.x) skey[i] = -1;
+  for (int i = tid; i < NS * D; i += blockDim.x) sacc[i] = 0.f;
+  __syncthreads();
+  const int Lp1 = s.Lp1;
+  const long long base = (long long)blockIdx.x * blockDim.x * CPW;
+  int uu[CPW];
+#pragma unroll
+  for (int c = 0; c < CPW; ++c) {
+    const long long e = base + ((long long)(wave * CPW + c) << 6) + lane;
+    uu[c] = e < n ? dup[e] : -1;
+  }
+  // wave-uniform ue; hot: the claimer has several lanes in this chunk (a popular row) -> LDS table
+  // (at most 4 probes), else one row of global atomics
+  auto add_row = [&](int ue, const float (&acc)[NPL], bool hot) {
+    int slot = -1;
+    if (hot && lane == 0) {
+      for (int k = 0, h = (int)(((unsigned)ue * 2654435761u) >> 20) & (NS - 1); k < 4; ++k, h = (h + 1) & (NS - 1)) {
+        int cur = __hip_atomic_load(skey + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (cur == -1) {
+          int expected = -1;
+          if (__hip_atomic_compare_exchange_strong(skey + h, &expected, ue, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            slot = h;
+            break;
+          }
+          cur = expected;
+        }
+        if (cur == ue) {
+          slot = h;
+          break;
+        }
+      }
+    }
+    slot = __shfl(slot, 0, 64);
+    if (slot >= 0) {
+#pragma unroll
+      for (int k = 0; k < NPL; ++k)
+        if (D >= 64 || lane < D) atomicAdd(sacc + slot * D + (D >= 64 ? k * 64 : 0) + lane, acc[k]);
+    } else {
       float* dst = s.extra + (size_t)ue * D;
       if (lane == 0) atomicOr(&s.slot_row[ue], FBN_SLOT_FLAG);
-      for (int k = lane; k < D; k += 64) atomicAdd(dst + k, src[k]);
+#pragma unroll
+      for (int k = 0; k < NPL; ++k)
+        if (D >= 64 || lane < D) atomicAdd(dst + (D >= 64 ? k * 64 : 0) + lane, acc[k]);
     }
+  };
+#pragma unroll 1
+  for (int c = 0; c < CPW; ++c) {
+    const long long e0 = base + ((long long)(wave * CPW + c) << 6);
+    const long long e = e0 + lane;
+    const int u = uu[c];
+    unsigned long long act = __ballot(u >= 0);
+    if (!act) continue;
+    const long long bs = e0 / Lp1, blast = (min((long long)n, e0 + 64) - 1) / Lp1;
+    const int nv = 2 * (int)(blast - bs + 1);
+    if (Lp1 >= 2 && nv <= MAXV) {
+      int vid = -1;
+      if (u >= 0) {
+        const long long b = e / Lp1, t = e - b * Lp1;
+        vid = 2 * (int)(b - bs) + (t ? 1 : 0);
+      }
+      float vec[MAXV][NPL];
+      unsigned long long vm[MAXV];
+#pragma unroll
+      for (int v = 0; v < MAXV; ++v) {
+        vm[v] = __ballot(vid == v);
+        const float* src = s.vec + ((size_t)bs * 2 + (v < nv ? v : 0)) * D;   // branch-free: all loads in flight
+#pragma unroll
+        for (int k = 0; k < NPL; ++k)
+          vec[v][k] = (D >= 64 || lane < D) ? src[(D >= 64 ? k * 64 : 0) + (lane & (D - 1))] : 0.f;
+      }
+      while (act) {
+        const int l = __ffsll((long long)act) - 1;
+        const int ue = __shfl(u, l, 64);
+        const unsigned long long m = __ballot(u == ue) & act;
+        act &= ~m;
+        float acc[NPL];
+#pragma unroll
+        for (int k = 0; k < NPL; ++k) acc[k] = 0.f;
+#pragma unroll
+        for (int v = 0; v < MAXV; ++v) {
+          const float cnt = (float)__popcll(m & vm[v]);
+#pragma unroll
+          for (int k = 0; k < NPL; ++k) acc[k] = __builtin_fmaf(cnt, vec[v][k], acc[k]);
+        }
+        add_row(ue, acc, __popcll(m) > 1);
+      }
+    } else {   // per-entry rows or very short histories: one duplicate at a time
+      while (act) {
+        const int l = __ffsll((long long)act) - 1;
+        act &= act - 1;
+        const int ue = __shfl(u, l, 64);
+        const float* src = grad_base<D>(s, (int)(e0 + l));
+        float acc[NPL];
+#pragma unroll
+        for (int k = 0; k < NPL; ++k) acc[k] = (D >= 64 || lane < D) ? src[(D >= 64 ? k * 64 : 0) + (lane & (D - 1))] : 0.f;
+        add_row(ue, acc, false);
+      }
+    }
+  }
+  __syncthreads();
+  for (int slot = wave; slot < NS; slot += blockDim.x >> 6) {
+    const int ue = skey[slot];
+    if (ue < 0) continue;
+    if (lane == 0) atomicOr(&s.slot_row[ue], FBN_SLOT_FLAG);
+    float* dst = s.extra + (size_t)ue * D;
+    for (int k = lane; k < D; k += 64) atomicAdd(dst + k, sacc[slot * D + k]);
   }
 }
 
@@ -810,6 +919,10 @@ struct ClaimSrc {
   int* slot_row;
   int* dup;
   int* hasdup;   // optional: hasdup[claimer] = 1 when another entry hit its row (deterministic fold)
+  // optional pre-claims (fbn_adam_prefetch of the previous step, for this very batch): pre[id] =
+  // (step << 32) | (0xFFFFFFFF - the smallest entry index with this id); a claim whose tag is the
+  // current step is final -- no CAS (popular rows would serialise thousands on one word)
+  unsigned long long* pre;
 };
 
 template <int D, bool DW>
@@ -852,14 +965,27 @@ __global__ void __launch_bounds__(256) adam_catchup_kernel(float* __restrict__ p
         const long long b = i / (cs.L + 1), tt = i - b * (cs.L + 1);
         const long long id = tt == 0 ? cs.item[b] : cs.seq[b * cs.L + (tt - 1)];
         int owner = -1;
-        if (id > 0 && id < cs.V) {
-          int expected = -1;
-          if (__hip_atomic_compare_exchange_strong(cs.map + id, &expected, (int)i, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT)) {
+        const unsigned long long pv = (cs.pre && id > 0 && id < cs.V) ? cs.pre[id] : 0ull;
+        if ((int)(pv >> 32) == t && t > 0) {   // pre-claimed: the smallest entry index claims
+          owner = (int)(0xFFFFFFFFu - (unsigned)pv);
+          if (owner == (int)i) {
+            cs.map[id] = (int)i;
             cs.slot_row[i] = (int)id;
             r = (int)id;
-          } else {
-            owner = expected;
+            owner = -1;
+          }
+        } else if (id > 0 && id < cs.V) {
+          // a popular row's later entries see its claim by a plain load: no CAS storm on one word
+          owner = __hip_atomic_load(cs.map + id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (owner == -1) {
+            int expected = -1;
+            if (__hip_atomic_compare_exchange_strong(cs.map + id, &expected, (int)i, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+              cs.slot_row[i] = (int)id;
+              r = (int)id;
+            } else {
+              owner = expected;
+            }
           }
         }
         if (cs.dup) cs.dup[i] = owner;
@@ -955,6 +1081,8 @@ __global__ void __launch_bounds__(256) adam_prefetch_kernel(float* __restrict__ 
     if (lane < SCAN && i < n) {
       const long long b = i / (cs.L + 1), tt = i - b * (cs.L + 1);
       const long long id = tt == 0 ? cs.item[b] : cs.seq[b * cs.L + (tt - 1)];
+      if (cs.pre && id > 0 && id < cs.V)   // next step's claim, decided now (non-returning, tagged)
+        atomicMax(cs.pre + id, ((unsigned long long)T << 32) | (0xFFFFFFFFull - (unsigned long long)i));
       if (id > 0 && id < cs.V && cs.map[id] == -1) {
         const int k0 = last[id];
         if (k0 < T && atomicCAS(last + id, k0, T) == k0) {
@@ -1258,6 +1386,17 @@ extern "C" int fbn_adam_dense(float* p, const float* g, float* m, float* v, long
     default: fbn_set_error("D must be 16/32/64/128/256"); return FBN_ERR_UNSUPPORTED;              \
   }
 
+// the same with a block size of T threads
+#define FBN_DISPATCH_D_T(KERNEL, D, GRID, T, ...)                                                    \
+  switch (D) {                                                                                      \
+    case 16: hipLaunchKernelGGL((KERNEL<16>), GRID, dim3(T), 0, st, __VA_ARGS__); break;            \
+    case 32: hipLaunchKernelGGL((KERNEL<32>), GRID, dim3(T), 0, st, __VA_ARGS__); break;            \
+    case 64: hipLaunchKernelGGL((KERNEL<64>), GRID, dim3(T), 0, st, __VA_ARGS__); break;            \
+    case 128: hipLaunchKernelGGL((KERNEL<128>), GRID, dim3(T), 0, st, __VA_ARGS__); break;          \
+    case 256: hipLaunchKernelGGL((KERNEL<256>), GRID, dim3(T), 0, st, __VA_ARGS__); break;          \
+    default: fbn_set_error("D must be 16/32/64/128/256"); return FBN_ERR_UNSUPPORTED;              \
+  }
+
 // the same for a kernel templated on <D, bool>
 #define FBN_DISPATCH_D_B(KERNEL, B, D, GRID, ...)                                                    \
   switch (D) {                                                                                      \
@@ -1298,9 +1437,9 @@ extern "C" int fbn_sparse_fixup_dup(const int* dup, int n, const float* gvec, fl
   if (!dup || !extra) { fbn_set_error("fbn_sparse_fixup_dup: dup and extra are required"); return FBN_ERR_ARG; }
   hipStream_t st = (hipStream_t)stream;
   const GradSrc s = make_src(gvec, extra, slot_row, Lp1);
-  int blocks = (n + 255) / 256;
-  if (blocks > 2048) blocks = 2048;
-  FBN_DISPATCH_D(sparse_fixup_dup_kernel, D, dim3(blocks), dup, n, s);
+  const int per = FBN_FOLD_THREADS * FBN_FOLD_CHUNKS;
+  const int blocks = (n + per - 1) / per;
+  FBN_DISPATCH_D_T(sparse_fixup_dup_kernel, D, dim3(blocks), FBN_FOLD_THREADS, dup, n, s);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -1484,7 +1623,7 @@ extern "C" int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, i
   // one wave per SCAN items (16 at D >= 64, else 64; sorted and compacted inside the kernel)
   const long long scan = D >= 64 ? 16 : 64;
   const dim3 grid((unsigned)std::min<long long>(cap, (items + 4 * scan - 1) / (4 * scan)));
-  const ClaimSrc cs{nullptr, nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr};
+  const ClaimSrc cs{nullptr, nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
   if (decoupled) {
     FBN_DISPATCH_D_B(adam_catchup_kernel, true, D, grid, p, m, v, slot_row, n_ent, map, nrows, F, chunk, parts, last,
                      (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, cs);
@@ -1499,10 +1638,10 @@ extern "C" int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, i
 // single GPU, D >= 128: ahead-of-time catch-up of the next batch's rows (adam_prefetch_kernel);
 // call on the stream of the rolling window, after this step's claims and before its step tail
 extern "C" int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B, int L, long long V, const int* map,
-                                 float* p, float* m, float* v, int D, int* last, const void* consts_table,
-                                 const int* step, float wd, float beta2, float eps, int* pend, const float* ring,
-                                 const float* coef_hist, long long ring_stride, int ring_n, int decoupled,
-                                 void* stream) {
+                                 unsigned long long* preclaim, float* p, float* m, float* v, int D, int* last,
+                                 const void* consts_table, const int* step, float wd, float beta2, float eps, int* pend,
+                                 const float* ring, const float* coef_hist, long long ring_stride, int ring_n,
+                                 int decoupled, void* stream) {
   const long long n = (long long)B * (L + 1);
   if (n <= 0) return FBN_OK;
   if (D < 128 || (D != 128 && D != 256)) { fbn_set_error("fbn_adam_prefetch: D = 128 or 256"); return FBN_ERR_ARG; }
@@ -1513,7 +1652,7 @@ extern "C" int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B,
   if (pend && (!ring || !coef_hist)) { fbn_set_error("fbn_adam_prefetch: pend needs ring and coef_hist"); return FBN_ERR_ARG; }
   const float omb2 = (float)(1.0 - (double)beta2);
   const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
-  const ClaimSrc cs{item, L > 0 ? seq : nullptr, L, V, const_cast<int*>(map), nullptr, nullptr, nullptr};
+  const ClaimSrc cs{item, L > 0 ? seq : nullptr, L, V, const_cast<int*>(map), nullptr, nullptr, nullptr, preclaim};
   static const int pcap = getenv("FBN_PREFETCH_BLOCKS") ? atoi(getenv("FBN_PREFETCH_BLOCKS")) : 256;   // tools/ab_prefetch.sh
   const dim3 grid((unsigned)std::min<long long>(pcap, (n + 63) / 64));
   hipStream_t st = (hipStream_t)stream;
@@ -1538,7 +1677,8 @@ extern "C" int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B,
 
 // single GPU: fbn_claim_rows + fbn_adam_catchup(parts = 1) in one launch (see ClaimSrc)
 extern "C" int fbn_adam_claim_catchup(const int64_t* item, const int64_t* seq, int B, int L, long long V, int* map,
-                                      int* slot_row, int* dup, int* hasdup, float* p, float* m, float* v, long long nrows, int D,
+                                      int* slot_row, int* dup, int* hasdup, unsigned long long* preclaim, float* p,
+                                      float* m, float* v, long long nrows, int D,
                                       int F, int* last, const void* consts_table, const int* step, float wd,
                                       float beta2, float eps, int* pend, const float* ring, const float* coef_hist,
                                       long long ring_stride, int ring_n, int decoupled, void* stream) {
@@ -1557,7 +1697,7 @@ extern "C" int fbn_adam_claim_catchup(const int64_t* item, const int64_t* seq, i
   const float omb2 = (float)(1.0 - (double)beta2);
   const long long chunk = (nrows + F - 1) / F;
   const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
-  const ClaimSrc cs{item, L > 0 ? seq : nullptr, L, V, map, slot_row, dup, hasdup};
+  const ClaimSrc cs{item, L > 0 ? seq : nullptr, L, V, map, slot_row, dup, hasdup, preclaim};
   const long long scan = D >= 64 ? 16 : 64;
   const dim3 grid((unsigned)std::min<long long>(8192, (n + 4 * scan - 1) / (4 * scan)));
   if (decoupled) {

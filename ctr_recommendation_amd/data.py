@@ -65,15 +65,36 @@ def make_batch(seed: int, B: int, V: int, L: int = 20, device="cpu", zipf: float
     return to_torch(b, y, device)
 
 
-def make_device_batches(n: int, B: int, V: int, L: int, device, seed: int = 2025):
-    """Pre-generate ``n`` batches directly on the device (benchmark input, HBM-resident)."""
+def make_device_batches(n: int, B: int, V: int, L: int, device, seed: int = 2025, zipf: float = 0.0):
+    """Pre-generate ``n`` batches directly on the device (benchmark input, HBM-resident).
+
+    zipf = s > 0: item and history ids follow Zipf(s) over the V - 1 ids (SURVEY §8(d)'s
+    Zipf(1.05) popularity skew): rank k has probability k^-s / H, ranks mapped to ids by a fixed
+    random permutation (hot rows scattered over the table); else ids ~ U[1, V)."""
     g = torch.Generator(device=device)
     g.manual_seed(seed)
+    draw = None
+    if zipf > 0:
+        ranks = torch.arange(1, V, device=device, dtype=torch.float64)
+        cdf = torch.cumsum(ranks.pow(-zipf), 0)
+        cdf = (cdf / cdf[-1]).float()
+        perm = torch.randperm(V - 1, generator=g, device=device) + 1
+
+        def draw(shape):
+            u = torch.rand(shape, generator=g, device=device)
+            k = torch.searchsorted(cdf, u.reshape(-1)).clamp_(max=V - 2)
+            return perm[k].reshape(shape).to(torch.int64)
     out = []
     for _ in range(n):
-        item = torch.randint(1, V, (B,), generator=g, device=device, dtype=torch.int64)
+        if draw is not None:
+            item = draw((B,))
+            hist = draw((B, L))
+        else:
+            item = torch.randint(1, V, (B,), generator=g, device=device, dtype=torch.int64)
+            hist = None
         n_valid = torch.randint(0, L + 1, (B,), generator=g, device=device)
-        hist = torch.randint(1, V, (B, L), generator=g, device=device, dtype=torch.int64)
+        if hist is None:
+            hist = torch.randint(1, V, (B, L), generator=g, device=device, dtype=torch.int64)
         slot = torch.arange(L, device=device)[None, :]
         seq = torch.where(slot >= (L - n_valid)[:, None], hist, torch.zeros_like(hist))
         likes = torch.randint(0, 11, (B,), generator=g, device=device, dtype=torch.int64)

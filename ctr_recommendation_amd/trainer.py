@@ -158,6 +158,10 @@ class FiBiNETTrainer:
         # lazy table Adam, single GPU, d = 128 / 256: step(..., next_batch=...) brings the next
         # batch's rows up to date on the side stream during this step (fbn_adam_prefetch)
         self.prefetch_rows = bool(prefetch_rows) and world == 1 and self.d in (128, 256)
+        # the prefetch also decides the next batch's row claims (tagged, no CAS at claim time);
+        # they are used only by a step given the very id tensors they were made for
+        self.preclaim = torch.zeros(self.V, dtype=torch.int64, device=dev) if self.prefetch_rows else None
+        self._pre_key = None
         self.hasdup = torch.zeros((self.n_entries,), **i32) if self.deterministic else None
         self.fx = torch.zeros((self.n_entries, d), dtype=torch.int64, device=dev) if self.deterministic else None
         # ---------------- optimizer schedule + device step state
@@ -246,8 +250,12 @@ class FiBiNETTrainer:
             # GPU): the row claims are made inside the same launch (fbn_adam_claim_catchup)
             ev = _events(probe, "adam_catchup")
             if claim:
+                key = (batch["item_id"].data_ptr(), seq.data_ptr() if L else 0)
+                pre = self.preclaim if (self.preclaim is not None and key == self._pre_key) else None
+                self._pre_key = None
                 call("fbn_adam_claim_catchup", ptr(batch["item_id"]), ptr(seq) if L else None, B, L, self.V,
-                     ptr(self.map), ptr(self.slot_row), ptr(self.dup), ptr(self.hasdup), ptr(self.E), ptr(self.Em),
+                     ptr(self.map), ptr(self.slot_row), ptr(self.dup), ptr(self.hasdup), ptr(pre), ptr(self.E),
+                     ptr(self.Em),
                      ptr(self.Ev),
                      self.rows_local, d, self.lazy_window, ptr(self.last), ptr(self.sched), ptr(self.step_dev),
                      self.wd_g, self.beta2, self.eps, *self._pend_args(), int(self.decoupled), st)
@@ -268,8 +276,11 @@ class FiBiNETTrainer:
                 nseq = nb.get("item_seq")
                 nL = nseq.shape[1] if nseq is not None else 0
                 ev = _events(probe, "adam_prefetch", self.side)
+                if nb["item_id"].shape[0] == B and nL == L:   # claims made now are valid for that step
+                    self._pre_key = (nb["item_id"].data_ptr(), nseq.data_ptr() if nL else 0)
                 call("fbn_adam_prefetch", ptr(nb["item_id"]), ptr(nseq) if nL else None, nb["item_id"].shape[0], nL,
-                     self.V, ptr(self.map), ptr(self.E), ptr(self.Em), ptr(self.Ev), d, ptr(self.last),
+                     self.V, ptr(self.map), ptr(self.preclaim if self._pre_key is not None else None), ptr(self.E),
+                     ptr(self.Em), ptr(self.Ev), d, ptr(self.last),
                      ptr(self.sched), ptr(self.step_dev), self.wd_g, self.beta2, self.eps, *self._pend_args(),
                      int(self.decoupled), self.side.cuda_stream)
                 _events_end(ev, self.side)

@@ -259,9 +259,13 @@ int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, int D, const
                      long long ring_stride, int ring_n, int decoupled, void* stream);
 /* Single GPU: fbn_claim_rows + fbn_adam_catchup(parts = 1) in ONE launch -- each entry claims its
  * row (first CAS wins: map, slot_row, dup as fbn_claim_rows) and a winning entry's row is brought
- * up to date at once. */
+ * up to date at once.  preclaim (optional, [V] u64, zero-initialised): tagged claims made for THIS
+ * batch by the previous step's fbn_adam_prefetch -- an entry whose tag is the current step takes
+ * the claim from it without a CAS (the smallest entry index of each row claims); pass it only when
+ * that prefetch was given this very batch. */
 int fbn_adam_claim_catchup(const int64_t* item, const int64_t* seq, int B, int L, long long V, int* map, int* slot_row,
-                           int* dup, int* hasdup, float* p, float* m, float* v, long long nrows, int D, int F, int* last,
+                           int* dup, int* hasdup, unsigned long long* preclaim, float* p, float* m, float* v,
+                           long long nrows, int D, int F, int* last,
                            const void* consts_table, const int* step, float wd, float beta2, float eps, int* pend,
                            const float* ring, const float* coef_hist, long long ring_stride, int ring_n, int decoupled,
                            void* stream);
@@ -270,11 +274,14 @@ int fbn_adam_claim_catchup(const int64_t* item, const int64_t* seq, int B, int L
  * that this batch does not touch (map == -1) takes only zero-gradient steps through the current
  * step inclusive, so it is brought to last = step + 1 now (bit-identical to eager Adam); the next
  * step's claimed-row catch-up then finds it up to date.  Replaces the reference's dense Adam over
- * item_emb.weight (train_fibinet.py:78,121) for those rows, one step early. */
-int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B, int L, long long V, const int* map, float* p,
-                      float* m, float* v, int D, int* last, const void* consts_table, const int* step, float wd,
-                      float beta2, float eps, int* pend, const float* ring, const float* coef_hist,
-                      long long ring_stride, int ring_n, int decoupled, void* stream);
+ * item_emb.weight (train_fibinet.py:78,121) for those rows, one step early.  preclaim (optional):
+ * every next-batch entry also records its tagged claim there (non-returning atomic max), for the
+ * next step's fbn_adam_claim_catchup. */
+int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B, int L, long long V, const int* map,
+                      unsigned long long* preclaim, float* p, float* m, float* v, int D, int* last,
+                      const void* consts_table, const int* step, float wd, float beta2, float eps, int* pend,
+                      const float* ring, const float* coef_hist, long long ring_stride, int ring_n, int decoupled,
+                      void* stream);
 int fbn_adam_flush(float* p, float* m, float* v, long long nrows, int D, int* last, const void* consts_table,
                    const int* step, float wd, float beta2, float eps, int* pend, const float* ring,
                    const float* coef_hist, long long ring_stride, int ring_n, int decoupled, void* stream);
