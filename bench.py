@@ -242,12 +242,14 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
     # ---- probe pass: eager steps with HIP events around the dominant kernels (same stream)
     probe = {}
     for _ in range(args.probe_steps):
-        load(i)
+        b, y = batches[i % nb]
         i += 1
         # a ~10 ms spin ahead of the step keeps the GPU behind the host's launches, so each event
-        # pair brackets only its kernel (as in the graph replays), not host enqueue gaps
+        # pair brackets only its kernel (as in the graph replays), not host enqueue gaps; the
+        # HBM-resident batches themselves are passed (as in the graphs), so the next-batch
+        # prefetch's claims are taken up exactly as in the timed replays
         torch.cuda._sleep(20_000_000)
-        tr.step(sb, sl, probe=probe, next_batch=batches[i % nb][0] if world == 1 else None)
+        tr.step(b, y, probe=probe, next_batch=batches[i % nb][0] if world == 1 else None)
     torch.cuda.synchronize()
 
     def avg_ms(name):

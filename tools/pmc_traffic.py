@@ -23,6 +23,7 @@ KERNELS = {
     # largest grid, the rolling window (side stream) the one with the smallest
     "adam_catchup": ("adam_catchup_kernel<128", "max", None),
     "adam_window": ("adam_catchup_kernel<128", "min", None),
+    "adam_prefetch": ("adam_prefetch_kernel<128", None, None),
     "gemm_mlp0": ("gemm_dma16_kernel<64, 128, false, false", "262144", "max"),
     "adam_touched": ("adam_touched_kernel<128", None, None),
     "adam_commit": ("adam_commit_kernel<128", None, None),
