@@ -47,7 +47,7 @@ SIGNATURES = {
     "fbn_fields_bwd_partials_size": (I, [I, I, I]),
     "fbn_fields_bwd_grid": (I, [I, I]),
     "fbn_fields_bwd": (I, [P, P, P, P, P, P, P, F, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P, P, P, LL, P, P, I, I,
-                           I, P]),
+                           I, I, P]),
     "fbn_pairs_fwd": (I, [P, P, P, P, I, I, I, I, I, P]),
     "fbn_pairs_bwd": (I, [P, P, P, P, P, P, P, I, I, I, I, P]),
     "fbn_bn_workspace_size": (SZ, [I, I]),
@@ -94,6 +94,7 @@ SIGNATURES = {
     "fbn_route": (I, [P, P, I, I, LL, LL, I, P, P, P, P, P, P, P]),
     "fbn_owner_claim": (I, [P, I, P, P, I, P]),
     "fbn_owner_gather": (I, [P, I, P, P, P, P, I, I, I, P]),
+    "fbn_widen_bf16": (I, [P, P, LL, P]),
     "fbn_bilinear_supported": (I, [I]),
     "fbn_bilinear_fwd": (I, [P, P, P, I, I, I, P]),
     "fbn_bilinear_bwd": (I, [P, I, I, P, P, P, P, P, I, I, P]),

@@ -162,3 +162,35 @@ extern "C" int fbn_owner_gather(const int* ids, int n, const float* E, void* out
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
+
+// bf16 -> f32, 8 elements per thread (the owner's received bf16 gradient rows, before the sparse
+// fold and the table Adam read them as f32)
+__global__ void __launch_bounds__(256) widen_bf16_kernel(const short* __restrict__ in, float* __restrict__ out,
+                                                         long long n8) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(in + 8 * i);
+    f32x4 a, b;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      a[k] = __uint_as_float((unsigned)(unsigned short)v[k] << 16);
+      b[k] = __uint_as_float((unsigned)(unsigned short)v[k + 4] << 16);
+    }
+    *reinterpret_cast<f32x4*>(out + 8 * i) = a;
+    *reinterpret_cast<f32x4*>(out + 8 * i + 4) = b;
+  }
+}
+
+extern "C" int fbn_widen_bf16(const void* in, float* out, long long n, void* stream) {
+  if (n <= 0) return FBN_OK;
+  if ((n & 7) || ((uintptr_t)in & 15) || ((uintptr_t)out & 15)) {
+    fbn_set_error("fbn_widen_bf16: n % 8 == 0 and 16-B aligned buffers");
+    return FBN_ERR_ARG;
+  }
+  const long long n8 = n / 8;
+  long long blocks = (n8 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(widen_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const short*>(in), out, n8);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}

@@ -253,8 +253,8 @@ struct FieldBwdArgs {
   // per-sample vectors gvec[b][0] = dX3 (item row), gvec[b][1] = dX5/count (each history row)
   float* gtab; float* gvec;
   double* gnorm;       // optional with gvec: [B][2] sums of squares of the two vectors (clip norm)
-  // mode 1: rows written to sendbuf at pos[b][t]
-  const int* pos; float* sendbuf;
+  // mode 1: rows written to sendbuf at pos[b][t] (f32); mode 2: the same in bf16 (bf16 mode's wire)
+  const int* pos; void* sendbuf;
   long long V;
   int B, L, R, n_cate;
   float ln_eps;
@@ -472,9 +472,17 @@ __global__ void __launch_bounds__(256) fields_bwd_kernel(FieldBwdArgs p) {
         }
       } else {
         const int* pb = p.pos + (size_t)b * (L + 1);
-        if (pb[0] >= 0) *reinterpret_cast<f32x4*>(p.sendbuf + (size_t)pb[0] * D + 4 * q) = dx[2];
+        auto put = [&](int row, const f32x4& x) {
+          if constexpr (MODE == 2) {
+            *reinterpret_cast<bf16x4*>(reinterpret_cast<short*>(p.sendbuf) + (size_t)row * D + 4 * q) =
+                (bf16x4){f2bf(x[0]), f2bf(x[1]), f2bf(x[2]), f2bf(x[3])};
+          } else {
+            *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.sendbuf) + (size_t)row * D + 4 * q) = x;
+          }
+        };
+        if (pb[0] >= 0) put(pb[0], dx[2]);
         for (int t = 0; t < L; ++t)
-          if (pb[t + 1] >= 0) *reinterpret_cast<f32x4*>(p.sendbuf + (size_t)pb[t + 1] * D + 4 * q) = gh;
+          if (pb[t + 1] >= 0) put(pb[t + 1], gh);
       }
     }
     // cate table (likes, views share one table): the wave's groups take turns on its slice
@@ -654,8 +662,8 @@ extern "C" int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, c
                               float ln_eps, const float* w1, const float* b1, const float* w2, int R, int n_cate,
                               const float* cate, const float* X, const float* a, const float* cnt, const float* dV, float* dhmm,
                               short* dhmm16, float* partials, float* const* param_grads, float* gtab, float* gvec,
-                              double* gnorm, long long V, const int* pos, float* sendbuf, int B, int L, int D,
-                              void* stream) {
+                              double* gnorm, long long V, const int* pos, void* sendbuf, int send_bf16, int B,
+                              int L, int D, void* stream) {
   if (B <= 0) return FBN_OK;
   if (L < 0 || L > 32 || R < 1 || R > FBN_MAXR) { fbn_set_error("fbn_fields_bwd: bad L/R"); return FBN_ERR_ARG; }
   FieldBwdArgs p;
@@ -665,7 +673,8 @@ extern "C" int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, c
   p.gtab = gtab; p.gvec = gvec; p.gnorm = gvec ? gnorm : nullptr; p.pos = pos; p.sendbuf = sendbuf;
   p.V = V; p.B = B; p.L = L; p.R = R; p.n_cate = n_cate; p.ln_eps = ln_eps;
   hipStream_t st = (hipStream_t)stream;
-  int rc = pos ? launch_fields_bwd<1>(p, D, st) : launch_fields_bwd<0>(p, D, st);
+  int rc = !pos ? launch_fields_bwd<0>(p, D, st) : send_bf16 ? launch_fields_bwd<2>(p, D, st)
+                                                               : launch_fields_bwd<1>(p, D, st);
   if (rc) return rc;
   const int P = 13 * R + 6 + 3 * D + n_cate * D;
   const int nblk = fields_grid(B, D, FBN_FB_MAXBLK);

@@ -45,6 +45,9 @@ class HipExchangeKernels:
              int(out.dtype == torch.bfloat16),
              _lib.stream_handle(E.device))
 
+    def widen(self, inp, out):
+        call("fbn_widen_bf16", ptr(inp), ptr(out), inp.numel(), _lib.stream_handle(out.device))
+
 
 class RowExchange:
     def __init__(self, rank: int, world: int, V: int, d: int, B: int, L: int, device, group=None, kernels=None,
@@ -55,8 +58,9 @@ class RowExchange:
         self.k = kernels or HipExchangeKernels()
         self.device = device
         self.stage_on_cpu = stage_on_cpu          # gloo on a GPU box: collectives on host copies
-        # bf16 mode: looked-up rows cross the wire as bf16 (half the forward all-to-all bytes; the
-        # fields kernel widens them on load); gradient rows stay f32
+        # bf16 mode: looked-up rows AND per-entry gradient rows cross the wire as bf16 (half the
+        # bytes of both all-to-alls; the fields kernel widens the rows on load, the owner widens the
+        # gradient rows on receipt and folds them in f32)
         self.row_dtype = torch.bfloat16 if rows_bf16 else torch.float32
         i32 = dict(dtype=torch.int32, device=device)
         # two routing buffer sets: the step in flight uses one while prepare() fills the other
@@ -182,13 +186,18 @@ class RowExchange:
         return rows
 
     def make_sendbuf(self) -> torch.Tensor:
-        return torch.empty((sum(self.send_counts), self.d), dtype=torch.float32, device=self.device)
+        return torch.empty((sum(self.send_counts), self.d), dtype=self.row_dtype, device=self.device)
 
     def backward(self, sendbuf: torch.Tensor) -> torch.Tensor:
-        """Returns the owner's received gradient rows [n_recv, d] (entry i <-> recv_ids[i])."""
+        """Returns the owner's received gradient rows [n_recv, d] f32 (entry i <-> recv_ids[i])."""
         n_recv = sum(self.recv_counts)
         grad = torch.empty((n_recv, self.d), dtype=torch.float32, device=sendbuf.device)
-        self._a2a(grad, sendbuf, self.recv_counts, self.send_counts)
+        if sendbuf.dtype == torch.float32:
+            self._a2a(grad, sendbuf, self.recv_counts, self.send_counts)
+            return grad
+        wire = torch.empty((n_recv, self.d), dtype=sendbuf.dtype, device=sendbuf.device)
+        self._a2a(wire, sendbuf, self.recv_counts, self.send_counts)
+        self.k.widen(wire, grad)
         return grad
 
 

@@ -555,7 +555,8 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
          ptr(batch["views_level"]), ptr(a["hmm"]), ptr(p["mm_proj.1.weight"]), ptr(p["mm_proj.1.bias"]), LN_EPS,
          ptr(p["senet.excitation.0.weight"]), ptr(p["senet.excitation.0.bias"]), ptr(p["senet.excitation.2.weight"]),
          R, ncate, ptr(p["cate_emb.weight"]), ptr(a["X"]), ptr(a["a"]), ptr(a["cnt"]), ptr(dV), ptr(dhmm), ptr(dhmm16), ptr(partials), outs,
-         ptr(table_grad), ptr(gvec), ptr(gnorm), V, ptr(pos), ptr(sendbuf), B, Lr, d, st)
+         ptr(table_grad), ptr(gvec), ptr(gnorm), V, ptr(pos), ptr(sendbuf),
+         int(sendbuf is not None and sendbuf.dtype == torch.bfloat16), B, Lr, d, st)
     if evb is not None:
         evb[1].record()
     if bf:

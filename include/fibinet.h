@@ -99,9 +99,12 @@ int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, const int64_
                    const float* hmm, const float* ln_g, const float* ln_b, float ln_eps, const float* w1,
                    const float* b1, const float* w2, int R, int n_cate, const float* cate, const float* X, const float* a, const float* cnt, const float* dV, float* dhmm,
                    short* dhmm16, float* partials, float* const* param_grads, float* gtab, float* gvec,
-                   double* gnorm, long long V, const int* pos, float* sendbuf, int B, int L, int D, void* stream);
+                   double* gnorm, long long V, const int* pos, void* sendbuf, int send_bf16, int B, int L, int D,
+                   void* stream);
 /* gnorm (optional, with gvec): [B][2] float64 sums of squares of the two per-sample vectors,
- * read by fbn_sumsq_sparse_norms for the clip_grad_norm_ total (src/train_fibinet.py:119). */
+ * read by fbn_sumsq_sparse_norms for the clip_grad_norm_ total (src/train_fibinet.py:119).
+ * pos / sendbuf (N > 1): one gradient row per routed entry, f32, or bf16 when send_bf16 (the bf16
+ * mode's wire format: half the sparse reduce-scatter's bytes; the owner widens on receipt). */
 
 /* ---------------------------------------------------------------- K5 bilinear pair products
  * Replaces the pair loop + stack + cat of src/model_fibinet.py:75-79,89,191-194 ("all", mode 0)
@@ -338,6 +341,8 @@ int fbn_owner_claim(const int* ids, int n, int* map, int* slot_row, int rank, vo
 /* out_bf16: reply rows as bf16 (the bf16 mode's wire format; fbn_fields_fwd(rows_bf16 = 1) reads them) */
 int fbn_owner_gather(const int* ids, int n, const float* E, void* out, int* map, int* slot_row, int rank, int D,
                      int out_bf16, void* stream);
+/* bf16 -> f32 (n % 8 == 0, 16-B aligned): the owner's received bf16 gradient rows (bf16 mode). */
+int fbn_widen_bf16(const void* in, float* out, long long n, void* stream);
 
 /* ---------------------------------------------------------------- fused bilinear (bf16 mode, "all")
  * Replaces BilinearInteraction "all" (src/model_fibinet.py:60-79,89) and its autograd in ONE launch

@@ -53,6 +53,10 @@ class CpuExchangeKernels:
                 map_[r] = i
                 slot_row[i] = r
 
+    def widen(self, inp, out):
+        """Restates fbn_widen_bf16: the owner's bf16 wire gradient rows to f32 (exact)."""
+        out.copy_(inp.float())
+
     @staticmethod
     def sparse_fixup_owner(ids, grows, map_, rank):
         """Restates fbn_sparse_fixup's owner mode: fold duplicates into the claiming entry."""
