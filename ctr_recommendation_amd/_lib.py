@@ -82,6 +82,7 @@ SIGNATURES = {
     "fbn_adam_claim_catchup": (I, [P, P, I, I, LL, P, P, P, P, P, P, P, P, LL, I, I, P, P, P, F, F, F, P, P, P, LL, I,
                                    I, P]),
     "fbn_adam_flush": (I, [P, P, P, LL, I, P, P, P, F, F, F, P, P, P, LL, I, I, P]),
+    "fbn_adam_prefetch_rows": (I, [P, I, I, LL, P, P, P, P, I, P, P, P, F, F, F, P, P, P, LL, I, I, P]),
     "fbn_adam_prefetch": (I, [P, P, I, I, LL, P, P, P, P, P, I, P, P, P, F, F, F, P, P, P, LL, I, I, P]),
     "fbn_adam_selftest": (I, [I, ctypes.c_uint, P, P]),
     "fbn_adam_step_tail": (I, [P, P, P, P, LL, P, F, P, P, P, P, P, I, P, P, P, P, I, I, P, P, F, F, F, P, P, P, P, I, I,
@@ -95,6 +96,7 @@ SIGNATURES = {
     "fbn_owner_claim": (I, [P, I, P, P, I, P]),
     "fbn_owner_gather": (I, [P, I, P, P, P, P, I, I, I, P]),
     "fbn_widen_bf16": (I, [P, P, LL, P]),
+    "fbn_pad_routes": (I, [P, P, P, I, I, P, P]),
     "fbn_bilinear_supported": (I, [I]),
     "fbn_bilinear_fwd": (I, [P, P, P, I, I, I, P]),
     "fbn_bilinear_bwd": (I, [P, I, I, P, P, P, P, P, I, I, P]),

@@ -194,3 +194,27 @@ extern "C" int fbn_widen_bf16(const void* in, float* out, long long n, void* str
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
+
+// Padded copy of a routing: out[o][j] = the j-th id routed to owner o (send_ids[offsets[o] + j]) for
+// j < counts[o], else -1 -- an all-to-all with equal splits of `cap` then needs no host-side counts
+// (RowExchange.prepare: the next step's requests reach their owners during this step)
+__global__ void pad_routes_kernel(const int* __restrict__ send_ids, const int* __restrict__ offsets,
+                                  const int* __restrict__ counts, int world, int cap, int* __restrict__ out) {
+  const long long total = (long long)world * cap;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int o = (int)(i / cap), j = (int)(i - (long long)o * cap);
+    out[i] = j < counts[o] ? send_ids[offsets[o] + j] : -1;
+  }
+}
+
+extern "C" int fbn_pad_routes(const int* send_ids, const int* offsets, const int* counts, int world, int cap, int* out,
+                              void* stream) {
+  if (world <= 0 || cap <= 0) return FBN_OK;
+  if (!send_ids || !offsets || !counts || !out) { fbn_set_error("fbn_pad_routes: null buffer"); return FBN_ERR_ARG; }
+  long long blocks = ((long long)world * cap + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(pad_routes_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, send_ids, offsets,
+                     counts, world, cap, out);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}

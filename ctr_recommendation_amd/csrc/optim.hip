@@ -923,6 +923,10 @@ struct ClaimSrc {
   // (step << 32) | (0xFFFFFFFF - the smallest entry index with this id); a claim whose tag is the
   // current step is final -- no CAS (popular rows would serialise thousands on one word)
   unsigned long long* pre;
+  // owner mode (N > 1, fbn_adam_prefetch_rows): entry i's row is the local row lids[i] (-1: none;
+  // rank 0's row 0 is the padding id and skipped when skip0); item / seq unused
+  const int* lids;
+  int skip0;
 };
 
 template <int D, bool DW>
@@ -1079,11 +1083,19 @@ __global__ void __launch_bounds__(256) adam_prefetch_kernel(float* __restrict__ 
     const long long i = i0 + lane;
     int r = -1, key = 0x7fffffff, pe = -1;
     if (lane < SCAN && i < n) {
-      const long long b = i / (cs.L + 1), tt = i - b * (cs.L + 1);
-      const long long id = tt == 0 ? cs.item[b] : cs.seq[b * cs.L + (tt - 1)];
-      if (cs.pre && id > 0 && id < cs.V)   // next step's claim, decided now (non-returning, tagged)
+      long long id;
+      bool ok;
+      if (cs.lids) {   // owner mode: local rows; rank 0's row 0 is the padding id
+        id = cs.lids[i];
+        ok = id >= 0 && id < cs.V && !(cs.skip0 && id == 0);
+      } else {
+        const long long b = i / (cs.L + 1), tt = i - b * (cs.L + 1);
+        id = tt == 0 ? cs.item[b] : cs.seq[b * cs.L + (tt - 1)];
+        ok = id > 0 && id < cs.V;
+      }
+      if (cs.pre && ok)   // next step's claim, decided now (non-returning, tagged)
         atomicMax(cs.pre + id, ((unsigned long long)T << 32) | (0xFFFFFFFFull - (unsigned long long)i));
-      if (id > 0 && id < cs.V && cs.map[id] == -1) {
+      if (ok && cs.map[id] == -1) {
         const int k0 = last[id];
         if (k0 < T && atomicCAS(last + id, k0, T) == k0) {
           r = (int)id;
@@ -1669,6 +1681,48 @@ extern "C" int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B,
                          (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
     else
       hipLaunchKernelGGL((adam_prefetch_kernel<256, false>), grid, dim3(256), 0, st, p, m, v, cs, (int)n, last,
+                         (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+  }
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+// N > 1 (the owner's side): the same ahead-of-time catch-up over the local rows the NEXT step's
+// requests name (lids [n], -1 = none: the padded id exchange of RowExchange.prepare); rows this
+// step's requests claimed (map != -1) are left to the next step's claimed-row catch-up
+extern "C" int fbn_adam_prefetch_rows(const int* lids, int n, int skip0, long long nrows, const int* map, float* p,
+                                      float* m, float* v, int D, int* last, const void* consts_table, const int* step,
+                                      float wd, float beta2, float eps, int* pend, const float* ring,
+                                      const float* coef_hist, long long ring_stride, int ring_n, int decoupled,
+                                      void* stream) {
+  if (n <= 0 || nrows <= 0) return FBN_OK;
+  if (D != 128 && D != 256) { fbn_set_error("fbn_adam_prefetch_rows: D = 128 or 256"); return FBN_ERR_ARG; }
+  if (!lids || !map || !last) { fbn_set_error("fbn_adam_prefetch_rows: lids, map and last are required"); return FBN_ERR_ARG; }
+  if (pend && (!ring || !coef_hist)) {
+    fbn_set_error("fbn_adam_prefetch_rows: pend needs ring and coef_hist");
+    return FBN_ERR_ARG;
+  }
+  const float omb2 = (float)(1.0 - (double)beta2);
+  const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
+  ClaimSrc cs{nullptr, nullptr, 0, nrows, const_cast<int*>(map), nullptr, nullptr, nullptr, nullptr};
+  cs.lids = lids;
+  cs.skip0 = skip0;
+  static const int pcap = getenv("FBN_PREFETCH_BLOCKS") ? atoi(getenv("FBN_PREFETCH_BLOCKS")) : 256;
+  const dim3 grid((unsigned)std::min<long long>(pcap, ((long long)n + 63) / 64));
+  hipStream_t st = (hipStream_t)stream;
+  if (D == 128) {
+    if (decoupled)
+      hipLaunchKernelGGL((adam_prefetch_kernel<128, true>), grid, dim3(256), 0, st, p, m, v, cs, n, last,
+                         (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+    else
+      hipLaunchKernelGGL((adam_prefetch_kernel<128, false>), grid, dim3(256), 0, st, p, m, v, cs, n, last,
+                         (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+  } else {
+    if (decoupled)
+      hipLaunchKernelGGL((adam_prefetch_kernel<256, true>), grid, dim3(256), 0, st, p, m, v, cs, n, last,
+                         (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+    else
+      hipLaunchKernelGGL((adam_prefetch_kernel<256, false>), grid, dim3(256), 0, st, p, m, v, cs, n, last,
                          (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
   }
   FBN_CHECK_LAUNCH();

@@ -33,6 +33,10 @@ from ._lib import call, ptr
 class HipExchangeKernels:
     """Device kernels of the exchange (exchange.hip)."""
 
+    def pad_routes(self, send_ids, offsets, counts, world, cap, out):
+        call("fbn_pad_routes", ptr(send_ids), ptr(offsets), ptr(counts), world, cap, ptr(out),
+             _lib.stream_handle(out.device))
+
     def route(self, item, seq, B, L, V, Vl, world, counts, offsets, cursor, send_ids, pos, err):
         call("fbn_route", ptr(item), ptr(seq), B, L, V, Vl, world, ptr(counts), ptr(offsets), ptr(cursor),
              ptr(send_ids), ptr(pos), ptr(err), _lib.stream_handle(item.device))
@@ -83,6 +87,7 @@ class RowExchange:
         self.send_counts = None
         self.recv_counts = None
         self.recv_ids = None
+        self.next_lids = None
 
     @property
     def rows_lo(self) -> int:
@@ -122,11 +127,15 @@ class RowExchange:
         # the prepared routing is used only for the very tensors it was computed from
         return (item.data_ptr(), item.shape[0], 0 if seq is None else seq.data_ptr(), 0 if seq is None else seq.shape[1])
 
-    def prepare(self, item, seq, err) -> None:
+    def prepare(self, item, seq, err, send_rows: bool = False) -> None:
         """Route the NEXT step's batch now, on a side stream (HIP device only): its forward then
         reads the counts from pinned host memory without a sync on the main stream.  It is used by
         the next forward() only if that forward gets the same (unmodified) id tensors; otherwise
-        that forward routes inline."""
+        that forward routes inline.  send_rows: also deliver each owner the local rows the next
+        step's requests will name, as an equal-split all-to-all of the padded routing (no host
+        counts): self.next_lids [world * cap] (-1 = none), ready on self.side -- the owner's
+        table-Adam prefetch (fbn_adam_prefetch_rows) reads them."""
+        self.next_lids = None
         if self.side is None:
             return
         st = self.sets[1 - self.cur]
@@ -138,6 +147,13 @@ class RowExchange:
             st["host"][self.world:].copy_(st["recv_counts"], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self.side)
+            if send_rows:
+                B = item.shape[0]
+                cap = B * (1 + (0 if seq is None else seq.shape[1]))
+                padded = torch.empty(self.world * cap, dtype=torch.int32, device=item.device)
+                self.k.pad_routes(st["send_ids"], st["offsets"], st["counts"], self.world, cap, padded)
+                self.next_lids = torch.empty_like(padded)
+                self._a2a(self.next_lids, padded, None, None, self.route_group)
         for t in (item, seq, err):
             if t is not None:
                 t.record_stream(self.side)

@@ -158,6 +158,9 @@ class FiBiNETTrainer:
         # lazy table Adam, single GPU, d = 128 / 256: step(..., next_batch=...) brings the next
         # batch's rows up to date on the side stream during this step (fbn_adam_prefetch)
         self.prefetch_rows = bool(prefetch_rows) and world == 1 and self.d in (128, 256)
+        # N > 1, the owner's side: the next step's requested rows arrive during this step (the
+        # padded id exchange of RowExchange.prepare) and are caught up ahead (fbn_adam_prefetch_rows)
+        self.prefetch_owner = bool(prefetch_rows) and world > 1 and self.d in (128, 256)
         # the prefetch also decides the next batch's row claims (tagged, no CAS at claim time);
         # they are used only by a step given the very id tensors they were made for
         self.preclaim = torch.zeros(self.V, dtype=torch.int64, device=dev) if self.prefetch_rows else None
@@ -310,7 +313,18 @@ class FiBiNETTrainer:
                                      self.err, before_gather=catch_up if lazy else None)
             pos = self.xchg.cur_pos
             if next_batch is not None:
-                self.xchg.prepare(next_batch["item_id"], next_batch.get("item_seq"), self.err)
+                own = self.prefetch_owner and lazy
+                self.xchg.prepare(next_batch["item_id"], next_batch.get("item_seq"), self.err, send_rows=own)
+                if own and self.xchg.next_lids is not None:
+                    # after this step's claims and window (self.side), once the requests arrived
+                    self.side.wait_stream(self.xchg.side)
+                    ev = _events(probe, "adam_prefetch", self.side)
+                    call("fbn_adam_prefetch_rows", ptr(self.xchg.next_lids), self.xchg.next_lids.numel(),
+                         int(self.rank == 0), self.rows_local, ptr(self.map), ptr(self.E), ptr(self.Em),
+                         ptr(self.Ev), d, ptr(self.last), ptr(self.sched), ptr(self.step_dev), self.wd_g, self.beta2,
+                         self.eps, *self._pend_args(), int(self.decoupled), self.side.cuda_stream)
+                    _events_end(ev, self.side)
+                    self.xchg.next_lids.record_stream(self.side)
         elif lazy:
             catch_up(B * (L + 1), claim=True)
         else:

@@ -285,6 +285,13 @@ int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B, int L, lon
                       const void* consts_table, const int* step, float wd, float beta2, float eps, int* pend,
                       const float* ring, const float* coef_hist, long long ring_stride, int ring_n, int decoupled,
                       void* stream);
+/* N > 1, the owner's side, D = 128 / 256: fbn_adam_prefetch over local rows lids [n] (-1 = none;
+ * skip0: row 0 is the padding id, rank 0) -- the rows the NEXT step's requests name, received
+ * through fbn_pad_routes + an equal-split all-to-all during this step. */
+int fbn_adam_prefetch_rows(const int* lids, int n, int skip0, long long nrows, const int* map, float* p, float* m,
+                           float* v, int D, int* last, const void* consts_table, const int* step, float wd,
+                           float beta2, float eps, int* pend, const float* ring, const float* coef_hist,
+                           long long ring_stride, int ring_n, int decoupled, void* stream);
 int fbn_adam_flush(float* p, float* m, float* v, long long nrows, int D, int* last, const void* consts_table,
                    const int* step, float wd, float beta2, float eps, int* pend, const float* ring,
                    const float* coef_hist, long long ring_stride, int ring_n, int decoupled, void* stream);
@@ -343,6 +350,10 @@ int fbn_owner_gather(const int* ids, int n, const float* E, void* out, int* map,
                      int out_bf16, void* stream);
 /* bf16 -> f32 (n % 8 == 0, 16-B aligned): the owner's received bf16 gradient rows (bf16 mode). */
 int fbn_widen_bf16(const void* in, float* out, long long n, void* stream);
+/* out[o][j] = send_ids[offsets[o] + j] for j < counts[o], else -1 ([world][cap]): the routing of a
+ * NEXT batch as an equal-split all-to-all (no host-side counts), for fbn_adam_prefetch_rows. */
+int fbn_pad_routes(const int* send_ids, const int* offsets, const int* counts, int world, int cap, int* out,
+                   void* stream);
 
 /* ---------------------------------------------------------------- fused bilinear (bf16 mode, "all")
  * Replaces BilinearInteraction "all" (src/model_fibinet.py:60-79,89) and its autograd in ONE launch

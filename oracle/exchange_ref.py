@@ -53,6 +53,13 @@ class CpuExchangeKernels:
                 map_[r] = i
                 slot_row[i] = r
 
+    def pad_routes(self, send_ids, offsets, counts, world, cap, out):
+        """Restates fbn_pad_routes: owner o's routed ids padded with -1 to cap."""
+        out.fill_(-1)
+        for o in range(world):
+            c, off = int(counts[o]), int(offsets[o])
+            out[o * cap:o * cap + c] = send_ids[off:off + c]
+
     def widen(self, inp, out):
         """Restates fbn_widen_bf16: the owner's bf16 wire gradient rows to f32 (exact)."""
         out.copy_(inp.float())

@@ -116,3 +116,68 @@ def test_sharded_trainer_equals_single_process_reference(hip_device, world, D, d
         dr, dh = (v - init[k]).double(), (h - init[k]).double()
         tol = 5e-2 if k in ("mlp.0.bias", "mlp.4.bias") else 1e-3
         assert (dh - dr).norm().item() <= tol * dr.norm().item() + 1e-9, k
+
+
+def _prefetch_worker(rank, world, port, q, out):
+    """Two sharded trainers over the same batches, the owner-side prefetch off and on."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ctr_recommendation_amd.data import make_batch
+        from ctr_recommendation_amd.trainer import FiBiNETTrainer
+        from oracle.fibinet_oracle import build_model
+        dev = torch.device("cuda:0")
+        Vp, Bg, L, steps = 40000, 64, 20, 6
+        cfg = {"embedding_dim": 128, "vocab_size": Vp, "honour_config": True, "net_dropout": 0.0}
+        torch.manual_seed(0)
+        init = build_model(None, cfg, honour_config=True).state_dict()
+        per = Bg // world
+        g = torch.Generator().manual_seed(9)
+        pool = torch.randperm(Vp - 1, generator=g)[:3000] + 1
+        bs = []
+        for s in range(steps + 1):
+            b, y = make_batch(400 + s, Bg, Vp)
+            ids = pool[torch.randperm(len(pool), generator=g)[:Bg * (L + 1)]].view(Bg, L + 1)   # unique in a step
+            b["item_id"] = ids[:, 0].clone()
+            seq = ids[:, 1:].clone()
+            seq[b["item_seq"] == 0] = 0
+            b["item_seq"] = seq
+            bs.append(({k: v[rank * per:(rank + 1) * per].to(dev) for k, v in b.items()},
+                       y[rank * per:(rank + 1) * per].to(dev)))
+        res = []
+        for pf in (False, True):
+            tr = FiBiNETTrainer(cfg, total_steps=20, batch_size=per, device=dev, rank=rank, world=world,
+                                init_state={k: v.clone() for k, v in init.items()}, stage_on_cpu=True,
+                                prefetch_rows=pf)
+            assert tr.prefetch_owner == pf
+            losses = [tr.step(bs[s][0], bs[s][1], next_batch=bs[s + 1][0]).item() for s in range(steps)]
+            torch.cuda.synchronize()
+            # before the flush: the rows the unused last next batch names were caught up ahead
+            lead = int((tr.last > tr.step_dev).sum()) if pf else 0
+            tr.flush()
+            res.append((losses, tr.E.cpu().clone(), tr.Em.cpu().clone(), tr.Ev.cpu().clone(), tr.flat_p.cpu().clone(),
+                        lead))
+        ok = res[0][0] == res[1][0] and all(torch.equal(a, b) for a, b in zip(res[0][1:5], res[1][1:5]))
+        q.put((rank, "ok" if ok else f"mismatch losses {res[0][0]} vs {res[1][0]}", res[1][5]))
+    except Exception as e:
+        q.put((rank, repr(e), 0))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_owner_prefetch_bit_identical(hip_device, tmp_path):
+    """N > 1 owner-side prefetch (RowExchange.prepare's padded id exchange + fbn_adam_prefetch_rows):
+    2 ranks on one MI355X (gloo, host-staged), ids unique within a step and recurring across steps:
+    losses and every table / moment / dense tensor bit-identical to the run without it."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_prefetch_worker, args=(r, world, port, q, str(tmp_path))) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=600) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+    assert all(r[1] == "ok" for r in res), res
