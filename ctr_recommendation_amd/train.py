@@ -109,8 +109,15 @@ def run(config: Optional[str] = None, *, epochs: Optional[int] = None, checkpoin
         t0 = time.perf_counter()
         total = torch.zeros((), dtype=torch.float64, device=device)
         steps = 0
-        for batch, labels in train_loader:
-            loss = trainer.step(batch, labels)
+        # one batch ahead: step() gets the following batch too, whose ids are routed (N > 1) and
+        # whose table rows are caught up (lazy table Adam) during the current step
+        it = iter(train_loader)
+        cur = next(it, None)
+        while cur is not None:
+            nxt = next(it, None)
+            batch, labels = cur
+            loss = trainer.step(batch, labels, next_batch=nxt[0] if nxt is not None else None)
+            cur = nxt
             total += loss[0].double()
             steps += 1
             if steps % 200 == 0:

@@ -172,3 +172,44 @@ def test_gemm_bf16out_is_rounded_f32_gemm(hip_device, M, N, K):
     _lib.call("fbn_gemm_bf16out", _lib.ptr(A), _lib.ptr(Bt), _lib.ptr(C16), M, N, K, K, K, N, 0, 1, st)
     torch.cuda.synchronize()
     assert torch.equal(C16, C32.to(torch.bfloat16))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d,zipf", [(128, 0.0), (128, 1.05), (16, 1.05), (64, 1.2)])
+def test_duplicate_fold_matches_scatter_add(hip_device, d, zipf):
+    """fbn_claim_rows + fbn_sparse_fixup_dup (wave sums per claimer, LDS table for popular rows) against
+    a float64 scatter-add of every entry's vector: each claimed row's gradient (its claimer's vector,
+    plus extra[claimer] when flagged) within 1e-5 of the row's scale; every touched row claimed once.
+    Zipf ids: the hottest rows take thousands of entries of a batch."""
+    from ctr_recommendation_amd import _lib
+    from ctr_recommendation_amd.data import make_device_batches
+    B, L, V = 4096, 20, 200_000
+    (b, _), = make_device_batches(1, B, V, L, hip_device, seed=5, zipf=zipf)
+    n = B * (L + 1)
+    st = _lib.stream_handle(hip_device)
+    i32 = dict(dtype=torch.int32, device=hip_device)
+    map_, slot_row, dup = torch.full((V,), -1, **i32), torch.full((n,), -1, **i32), torch.full((n,), -1, **i32)
+    _lib.call("fbn_claim_rows", _lib.ptr(b["item_id"]), _lib.ptr(b["item_seq"]), B, L, V, _lib.ptr(map_),
+              _lib.ptr(slot_row), _lib.ptr(dup), None, st)
+    g = torch.Generator(device=hip_device).manual_seed(1)
+    gvec = torch.randn((B, 2, d), generator=g, device=hip_device)
+    extra = torch.zeros((n, d), device=hip_device)
+    _lib.call("fbn_sparse_fixup_dup", _lib.ptr(dup), n, _lib.ptr(gvec), _lib.ptr(extra), _lib.ptr(slot_row), L + 1,
+              d, st)
+    torch.cuda.synchronize()
+    ids = torch.cat([b["item_id"].view(B, 1), b["item_seq"]], 1).reshape(-1)
+    slot = (torch.arange(n, device=hip_device) % (L + 1) > 0).long()
+    vec = gvec[torch.arange(n, device=hip_device) // (L + 1), slot]           # entry e's vector
+    valid = (ids > 0) & (ids < V)
+    ref = torch.zeros((V, d), dtype=torch.float64, device=hip_device)
+    ref.index_add_(0, ids[valid], vec[valid].double())
+    claimers = (slot_row != -1).nonzero().view(-1)
+    rows = (slot_row[claimers] & 0x3FFFFFFF).long()
+    flagged = (slot_row[claimers] & 0x40000000) != 0
+    got = vec[claimers].double() + torch.where(flagged[:, None], extra[claimers].double(), torch.zeros_like(ref[:1]))
+    assert torch.equal(torch.sort(rows).values, torch.unique(ids[valid]))      # each touched row claimed once
+    scale = ref[rows].abs().max(1, keepdim=True).values.clamp_min(1.0)
+    err = ((got - ref[rows]).abs() / scale).max().item()
+    assert err <= 1e-5, err
+    if zipf > 0:
+        assert int((dup >= 0).sum()) > n // 10       # the case is really duplicate-heavy
