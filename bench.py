@@ -145,6 +145,7 @@ def _initial_state(cfg, V, world, rank, dev):
 def measure(args, dtype, world, rank, dev, rehearsal, backend):
     """Build a trainer for `dtype`, bring it to steady state, time K steps; returns the result dict."""
     from ctr_recommendation_amd.data import make_device_batches
+    from ctr_recommendation_amd import ops
     from ctr_recommendation_amd.trainer import FiBiNETTrainer
 
     d, B, L = args.dim, args.batch, 20
@@ -252,8 +253,19 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
         tr.step(b, y, probe=probe, next_batch=batches[i % nb][0] if world == 1 else None)
     torch.cuda.synchronize()
 
-    def avg_ms(name):
-        ev = probe.get(name, [])
+    # the gather alone: eval-mode forwards of the same batches with nothing on the side stream (the
+    # probe above times it inside the step, beside the table-Adam passes)
+    iso = {}
+    if world == 1:
+        cfg_iso = ops.FwdConfig(**{**tr.fcfg.__dict__, "training": False})
+        cfg_iso.L = L
+        for j in range(12):
+            torch.cuda._sleep(2_000_000)
+            ops.forward(tr.p, batches[j % nb][0], cfg_iso, None, err=tr.err, probe=iso)
+        torch.cuda.synchronize()
+
+    def avg_ms(name, src=None):
+        ev = (probe if src is None else src).get(name, [])[2 if src is not None else 0:]
         return sum(a.elapsed_time(e) for a, e in ev) / max(1, len(ev))
 
     touched = int(uniq.numel())
@@ -281,6 +293,9 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
 
     add("fields_fwd", "fields_fwd (fused gather + history mean + LN + SENET)", avg_ms("fields_fwd"),
         gather_bytes_per_sample(d) * B, "GB/s", HBM_PEAK_GBS, "hbm", "SURVEY 8(d) 12,984 B/sample x batch")
+    if iso:
+        add("fields_fwd", "fields_fwd alone (eval-mode forward, no side-stream work)", avg_ms("fields_fwd", iso),
+            gather_bytes_per_sample(d) * B, "GB/s", HBM_PEAK_GBS, "hbm", "SURVEY 8(d) 12,984 B/sample x batch")
     dfr = getattr(tr, "deferred", False)
     # claimed-row catch-up: every entry's id, claim, slot and last (20 B) + the rows it replays
     crit = stale if prefetch else touched
