@@ -85,8 +85,8 @@ SIGNATURES = {
     "fbn_adam_prefetch_rows": (I, [P, I, I, LL, P, P, P, P, I, P, P, P, F, F, F, P, P, P, LL, I, I, P]),
     "fbn_adam_prefetch": (I, [P, P, I, I, LL, P, P, P, P, P, I, P, P, P, F, F, F, P, P, P, LL, I, I, P]),
     "fbn_adam_selftest": (I, [I, ctypes.c_uint, P, P]),
-    "fbn_adam_step_tail": (I, [P, P, P, P, LL, P, F, P, P, P, P, P, I, P, P, P, P, I, I, P, P, F, F, F, P, P, P, P, I, I,
-                               P, P, P, P, I, P, P]),
+    "fbn_adam_step_tail": (I, [P, P, P, P, LL, P, F, P, P, P, P, P, I, P, P, P, P, I, I, P, P, F, F, F, P, P, P, P, I,
+                               LL, I, P, P, P, P, I, P, P]),
     "fbn_adam_commit": (I, [P, P, P, I, P, P, P, P, I, I, P, P, P, F, F, F, P, P, P, P, I, I, P]),
     "fbn_claim_rows": (I, [P, P, I, I, LL, P, P, P, P, P]),
     "fbn_pack_extras": (I, [P, P, P, P]),

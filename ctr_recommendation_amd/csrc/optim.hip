@@ -1207,11 +1207,14 @@ __device__ __forceinline__ void adam_commit_body(float* __restrict__ p, float* _
                                                  int* __restrict__ last, const PendSrc& ps, int B, long long bid,
                                                  long long nblk) {
   constexpr int G = D / 4, RPW = 64 / G;
-  // ring copy of this step's per-sample vectors
-  float* dst = const_cast<float*>(ps.ring) + (size_t)(t % ps.ring_n) * ps.ring_stride;
-  const long long n4 = (long long)B * 2 * D / 4;
-  for (long long i = bid * blockDim.x + threadIdx.x; i < n4; i += nblk * blockDim.x)
-    reinterpret_cast<f32x4*>(dst)[i] = reinterpret_cast<const f32x4*>(gs.vec)[i];
+  // ring copy of this step's per-sample vectors (N > 1, per-entry rows: the rows were received
+  // straight into the ring slot -- nothing to copy)
+  if (gs.Lp1 > 1) {
+    float* dst = const_cast<float*>(ps.ring) + (size_t)(t % ps.ring_n) * ps.ring_stride;
+    const long long n4 = (long long)B * 2 * D / 4;
+    for (long long i = bid * blockDim.x + threadIdx.x; i < n4; i += nblk * blockDim.x)
+      reinterpret_cast<f32x4*>(dst)[i] = reinterpret_cast<const f32x4*>(gs.vec)[i];
+  }
   // one entry per lane: an unflagged claimer records its vector in pend; flagged claimers (rare)
   // are updated by the wave's G-lane groups afterwards
   const int lane = threadIdx.x & 63, q = lane % G;
@@ -1220,8 +1223,12 @@ __device__ __forceinline__ void adam_commit_body(float* __restrict__ p, float* _
     const int sr = e < n ? gs.slot_row[e] : -1;
     const bool flag = sr != -1 && (sr & FBN_SLOT_FLAG);
     if (sr != -1 && !flag) {
-      const int b = (int)(e / gs.Lp1), tt = (int)(e - (long long)b * gs.Lp1);
-      ps.pend[sr] = b * 2 + (tt ? 1 : 0);
+      if (gs.Lp1 == 1) {   // per-entry rows (N > 1 owner): the entry's own row of the ring slot
+        ps.pend[sr] = (int)e;
+      } else {
+        const int b = (int)(e / gs.Lp1), tt = (int)(e - (long long)b * gs.Lp1);
+        ps.pend[sr] = b * 2 + (tt ? 1 : 0);
+      }
       map[sr] = -1;
       gs.slot_row[e] = -1;
     }
@@ -1560,17 +1567,20 @@ extern "C" int fbn_adam_step_tail(float* dp, const float* dg, float* dm, float* 
                                   const double* sumsq, float max_norm, float* coef_out, float* norm_out, float* p,
                                   float* m, float* v, int D, int* map, const float* gvec, float* extra, int* slot_row,
                                   int Lp1, int n, const void* consts_table, int* step, float wd, float beta2, float eps,
-                                  int* last, int* pend, float* ring, float* coef_hist, int ring_n, int B,
-                                  unsigned long long* rng, long long* nbt0, long long* nbt1, unsigned* ticket,
+                                  int* last, int* pend, float* ring, float* coef_hist, int ring_n, long long ring_stride,
+                                  int B, unsigned long long* rng, long long* nbt0, long long* nbt1, unsigned* ticket,
                                   int max_step, int* err, void* stream) {
-  if (!pend || !ring || !coef_hist || !extra || !sumsq || !ticket || ring_n < 2 || (Lp1 & 0xffff) < 2) {
-    fbn_set_error("fbn_adam_step_tail: pend, ring, coef_hist, extra, sumsq and ticket are required");
+  const int lp = Lp1 & 0xffff;
+  if (!pend || !ring || !coef_hist || !sumsq || !ticket || ring_n < 2 || lp < 1 || (lp >= 2 && !extra) ||
+      (lp >= 2 && ring_stride != (long long)B * 2 * D)) {
+    fbn_set_error("fbn_adam_step_tail: pend, ring, coef_hist, sumsq, ticket (and extra with per-sample vectors, "
+                  "ring_stride = B*2*D) are required");
     return FBN_ERR_ARG;
   }
   hipStream_t st = (hipStream_t)stream;
   const float omb2 = (float)(1.0 - (double)beta2);
   const GradSrc s = make_src(gvec, extra, slot_row, Lp1);
-  const PendSrc ps{pend, ring, coef_hist, (long long)B * 2 * D, ring_n};
+  const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
   const StepEnd se{step, rng, (double*)sumsq, nbt0, nbt1, ticket, max_step, err};
   long long nd = (n_dense / 4 + 255) / 256;
   // few, fat blocks: every block draws the step-end ticket (one returning atomic on one word,

@@ -204,10 +204,12 @@ class RowExchange:
     def make_sendbuf(self) -> torch.Tensor:
         return torch.empty((sum(self.send_counts), self.d), dtype=self.row_dtype, device=self.device)
 
-    def backward(self, sendbuf: torch.Tensor) -> torch.Tensor:
-        """Returns the owner's received gradient rows [n_recv, d] f32 (entry i <-> recv_ids[i])."""
+    def backward(self, sendbuf: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Returns the owner's received gradient rows [n_recv, d] f32 (entry i <-> recv_ids[i]),
+        written into `out` (>= n_recv rows, e.g. a deferred-gradient ring slot) when given."""
         n_recv = sum(self.recv_counts)
-        grad = torch.empty((n_recv, self.d), dtype=torch.float32, device=sendbuf.device)
+        grad = out[:n_recv] if out is not None else \
+            torch.empty((n_recv, self.d), dtype=torch.float32, device=sendbuf.device)
         if sendbuf.dtype == torch.float32:
             self._a2a(grad, sendbuf, self.recv_counts, self.send_counts)
             return grad

@@ -200,14 +200,18 @@ class FiBiNETTrainer:
             raise ValueError(f"table_adam must be 'lazy', 'eager' or 'sparse', not {self.table_adam!r}")
         self.lazy_window = int(lazy_window)
         self.last = torch.zeros(max(1, self.rows_local), **i32)     # Adam steps applied per table row
-        # single GPU, lazy: deferred table gradients (fbn_adam_commit) -- pend[r] = per-sample vector
-        # row r received at step last[r]; the vectors of the last F+1 steps stay in a ring
-        self.deferred = self.table_adam == "lazy" and world == 1 and defer_table_grads
+        # lazy: deferred table gradients (the step tail's commit) -- pend[r] = the gradient row r
+        # received at step last[r], applied at the row's next replay; the last F+1 steps' gradients
+        # stay in a ring: single GPU, the per-sample vectors [B][2][d]; N > 1, the owner's received
+        # per-entry rows, up to ring_cap per step (a step receiving more applies its rows at once)
+        self.deferred = self.table_adam == "lazy" and defer_table_grads
         self.pend = self.ring = self.coef_hist = None
         self.ring_n = self.lazy_window + 1
+        self.ring_cap = self.B * (max_len + 1) if world > 1 else 0
         if self.deferred:
             self.pend = torch.full((max(1, self.rows_local),), -1, **i32)
-            self.ring = torch.zeros((self.ring_n, self.B, 2, d), dtype=torch.float32, device=dev)
+            shape = (self.ring_n, self.B, 2, d) if world == 1 else (self.ring_n, self.ring_cap, d)
+            self.ring = torch.zeros(shape, dtype=torch.float32, device=dev)
             self.coef_hist = torch.ones(total_steps + 1, dtype=torch.float32, device=dev)
             self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)     # fbn_adam_step_tail
         self.side = torch.cuda.Stream(device=dev)      # eager untouched pass / lazy rolling window
@@ -357,7 +361,13 @@ class FiBiNETTrainer:
                 call("fbn_sparse_fixup_dup", ptr(self.dup), n_ent, ptr(self.gvec), ptr(self.extra),
                      ptr(self.slot_row), L + 1, d, st)
         else:
-            grows = self.xchg.backward(sendbuf)              # owner: one received row per entry
+            # owner: one received row per entry -- straight into this step's deferred-gradient ring
+            # slot when it fits, else a buffer of its own and the rows applied at the step end
+            slot = None
+            if self.deferred and sum(self.xchg.recv_counts) <= self.ring_cap:
+                slot = self.ring[self.host_step % self.ring_n]
+            defer_now = slot is not None
+            grows = self.xchg.backward(sendbuf, out=slot)
             n_ent = grows.shape[0]
             gsrc = (grows, None, 1)
             call("fbn_sparse_fixup", None, None, ptr(self.xchg.recv_ids), n_ent, 0, self.V, self.rank, ptr(self.map),
@@ -378,7 +388,9 @@ class FiBiNETTrainer:
             call("fbn_unpack_extras", ptr(self.flat_g_ext[o:]), ptr(self.loss), ptr(self.sumsq), st)
         call("fbn_sumsq", ptr(self.flat_g), self.n_dense, None, 0, ptr(self.sumsq), st)
         main.wait_stream(self.side)   # side-stream table pass done before map entries are reset
-        if self.deferred:
+        if self.xchg is None:
+            defer_now = self.deferred
+        if defer_now:
             # ONE launch: dense Adam with clip_grad_norm_(10), the table step (deferred to each row's
             # next replay; rows with duplicates now), map/slot_row reset, step end
             ev = _events(probe, "adam_tail")
@@ -386,7 +398,8 @@ class FiBiNETTrainer:
                  self.n_dense, ptr(self.sumsq), self.max_norm, ptr(self.coef), ptr(self.norm), ptr(self.E),
                  ptr(self.Em), ptr(self.Ev), d, ptr(self.map), ptr(gsrc[0]), ptr(gsrc[1]), ptr(self.slot_row), gsrc[2],
                  n_ent, ptr(self.sched), ptr(self.step_dev), self.wd_g, self.beta2, self.eps, ptr(self.last),
-                 ptr(self.pend), ptr(self.ring), ptr(self.coef_hist), self.ring_n, self.B, ptr(self.rng),
+                 ptr(self.pend), ptr(self.ring), ptr(self.coef_hist), self.ring_n, self._ring_stride(), self.B,
+                 ptr(self.rng),
                  ptr(self.p["mlp.1.num_batches_tracked"]), ptr(self.p["mlp.5.num_batches_tracked"]), ptr(self.ticket),
                  self.total_steps, ptr(self.err), st)
             _events_end(ev)
@@ -407,11 +420,14 @@ class FiBiNETTrainer:
         self.host_step += 1
         return self.loss
 
+    def _ring_stride(self) -> int:
+        return self.B * 2 * self.d if self.world == 1 else self.ring_cap * self.d
+
     def _pend_args(self):
         """(pend, ring, coef_hist, ring_stride, ring_n) of the deferred table gradients (NULLs when off)."""
         if not self.deferred:
             return (None, None, None, 0, 0)
-        return (ptr(self.pend), ptr(self.ring), ptr(self.coef_hist), self.B * 2 * self.d, self.ring_n)
+        return (ptr(self.pend), ptr(self.ring), ptr(self.coef_hist), self._ring_stride(), self.ring_n)
 
     # ------------------------------------------------------------------ inference
     def flush(self) -> None:

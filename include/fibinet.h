@@ -302,8 +302,11 @@ int fbn_adam_step_tail(float* dp, const float* dg, float* dm, float* dv, long lo
                        float max_norm, float* coef_out, float* norm_out, float* p, float* m, float* v, int D, int* map,
                        const float* gvec, float* extra, int* slot_row, int Lp1, int n, const void* consts_table,
                        int* step, float wd, float beta2, float eps, int* last, int* pend, float* ring,
-                       float* coef_hist, int ring_n, int B, unsigned long long* rng, long long* nbt0, long long* nbt1,
-                       unsigned* ticket, int max_step, int* err, void* stream);
+                       float* coef_hist, int ring_n, long long ring_stride, int B, unsigned long long* rng,
+                       long long* nbt0, long long* nbt1, unsigned* ticket, int max_step, int* err, void* stream);
+/* (step tail) Lp1 >= 2: per-sample vectors gvec [B][2][D] copied into ring slot step % ring_n
+ * (ring_stride = B*2*D); Lp1 == 1 (N > 1 owner): per-entry rows gvec [n][D] already received into
+ * that ring slot (ring_stride = the slot's row capacity x D), pend[r] = the claiming entry. */
 /* Self-test of the table-row Adam step (hardware sqrt / rcp, fused moment updates; used by every
  * item_emb.weight kernel) against the IEEE element step of fbn_adam_dense: n x 4 random operands
  * in training ranges; dev[0..2] = max deviation of m, v, p in 1/16 ulp of each update's largest

@@ -145,11 +145,11 @@ def _prefetch_worker(rank, world, port, q, out):
             bs.append(({k: v[rank * per:(rank + 1) * per].to(dev) for k, v in b.items()},
                        y[rank * per:(rank + 1) * per].to(dev)))
         res = []
-        for pf in (False, True):
+        for pf, defer in ((False, False), (False, True), (True, True)):
             tr = FiBiNETTrainer(cfg, total_steps=20, batch_size=per, device=dev, rank=rank, world=world,
                                 init_state={k: v.clone() for k, v in init.items()}, stage_on_cpu=True,
-                                prefetch_rows=pf)
-            assert tr.prefetch_owner == pf
+                                prefetch_rows=pf, defer_table_grads=defer)
+            assert tr.prefetch_owner == pf and tr.deferred == defer
             losses = [tr.step(bs[s][0], bs[s][1], next_batch=bs[s + 1][0]).item() for s in range(steps)]
             torch.cuda.synchronize()
             # before the flush: the rows the unused last next batch names were caught up ahead
@@ -157,8 +157,8 @@ def _prefetch_worker(rank, world, port, q, out):
             tr.flush()
             res.append((losses, tr.E.cpu().clone(), tr.Em.cpu().clone(), tr.Ev.cpu().clone(), tr.flat_p.cpu().clone(),
                         lead))
-        ok = res[0][0] == res[1][0] and all(torch.equal(a, b) for a, b in zip(res[0][1:5], res[1][1:5]))
-        q.put((rank, "ok" if ok else f"mismatch losses {res[0][0]} vs {res[1][0]}", res[1][5]))
+        ok = all(r[0] == res[0][0] and all(torch.equal(a, b) for a, b in zip(res[0][1:5], r[1:5])) for r in res[1:])
+        q.put((rank, "ok" if ok else f"mismatch losses {[r[0] for r in res]}", res[2][5]))
     except Exception as e:
         q.put((rank, repr(e), 0))
         raise
@@ -167,9 +167,11 @@ def _prefetch_worker(rank, world, port, q, out):
 
 
 def test_owner_prefetch_bit_identical(hip_device, tmp_path):
-    """N > 1 owner-side prefetch (RowExchange.prepare's padded id exchange + fbn_adam_prefetch_rows):
-    2 ranks on one MI355X (gloo, host-staged), ids unique within a step and recurring across steps:
-    losses and every table / moment / dense tensor bit-identical to the run without it."""
+    """N > 1 owner-side prefetch (RowExchange.prepare's padded id exchange + fbn_adam_prefetch_rows)
+    and deferred table gradients (received rows kept in a ring slot, applied at the row's next
+    replay; a step receiving more than the slot holds applies them at once): 2 ranks on one MI355X
+    (gloo, host-staged), ids unique within a step and recurring across steps: losses and every
+    table / moment / dense tensor bit-identical across immediate, deferred, deferred + prefetch."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
