@@ -15,7 +15,12 @@ One JSON line on rank 0 with the contract keys plus
                  ones), HIP events around its launches inside an eager probe pass (same stream),
                  algorithmic work per launch (bytes or FLOPs) / that time, against the HBM or
                  MFMA peak; traffic = PMC-measured HBM bytes per launch when committed;
-  rooflines:     the same for every probed kernel (gather, lazy table-Adam catch-up, MLP GEMM);
+  rooflines:     the same for every probed kernel (gather, lazy table-Adam catch-up, MLP GEMM),
+                 plus the gather and the layer-1 GEMM "alone" (eval-mode forwards with nothing on
+                 the side stream: the in-step launches share the GPU with the table-Adam side work,
+                 which is why a rocprof per-name average -- graph replays + probes + these -- sits
+                 between the two; tools/step_launches.py lists one step's launches);
+  host_enqueue_ms_per_step: host time to issue the K timed steps (graph replays or eager launches);
   cpu_baseline:  the oracle's torch-CPU restatement of the reference train step (rank 0, N=1).
 """
 from __future__ import annotations
@@ -142,6 +147,11 @@ def _initial_state(cfg, V, world, rank, dev):
     return init
 
 
+# FBN_BENCH_SHARD=1 (under torch.distributed.run, one rank): the row-sharded N > 1 step at N = 1
+# over RCCL -- the per-GPU cost of the sharded path without any peer (scaling diagnostics)
+FORCE_SHARD = os.environ.get("FBN_BENCH_SHARD") == "1"
+
+
 def measure(args, dtype, world, rank, dev, rehearsal, backend):
     """Build a trainer for `dtype`, bring it to steady state, time K steps; returns the result dict."""
     from ctr_recommendation_amd.data import make_device_batches
@@ -160,22 +170,15 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
     # steady state of the lazy table Adam whatever --warmup says: a row's replay length settles
     # only after ~2F steps; warm-up steps are < 1 ms each
     prime = max(0, 2 * F - W) if args.prime < 0 else args.prime
-    use_graph = world == 1 and not args.no_graph
+    sharded = world > 1 or FORCE_SHARD
+    use_graph = not sharded and not args.no_graph
     total = 1 + (nb if use_graph else 0) + prime + W + K + args.probe_steps + 16
     init = _initial_state(cfg, V, world, rank, dev)
     tr = FiBiNETTrainer(cfg, total_steps=total, batch_size=B, device=dev, rank=rank, world=world,
-                        init_state=init, stage_on_cpu=rehearsal, lazy_window=F, prefetch_rows=args.prefetch)
+                        init_state=init, stage_on_cpu=rehearsal, lazy_window=F, prefetch_rows=args.prefetch,
+                        shard=sharded)
     del init
     batches = make_device_batches(nb, B, V, L, dev, seed=2025 + rank, zipf=args.zipf)
-    sb = {k: v.clone() for k, v in batches[0][0].items()}
-    sl = batches[0][1].clone()
-
-    def load(i):
-        b, y = batches[i % nb]
-        for k in sb:
-            sb[k].copy_(b[k], non_blocking=True)
-        sl.copy_(y, non_blocking=True)
-
     graphs = []
     if use_graph:
         torch.cuda.synchronize()
@@ -197,13 +200,11 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
     def run_step(i):
         if graphs:
             graphs[i % nb].replay()
-        elif world > 1:
-            # N > 1: the next batch is routed during this step (no mid-step host sync)
+        else:
+            # the HBM-resident batch itself: N > 1 routes the next batch during this step (no
+            # mid-step host sync); N = 1 catches its rows up ahead and pre-claims them
             b, y = batches[i % nb]
             tr.step(b, y, next_batch=batches[(i + 1) % nb][0])
-        else:
-            load(i)
-            tr.step(sb, sl, next_batch=batches[(i + 1) % nb][0])
 
     i = 0
     for j in range(prime + W):
@@ -218,6 +219,7 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
     for _ in range(K):
         run_step(i)
         i += 1
+    t_host = time.perf_counter() - t0            # host enqueue time of the K steps
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -314,12 +316,16 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
     add("gemm_mlp0", f"gemm MLP layer 1 (B x 15d -> 512, {dtype} MFMA)", avg_ms("gemm_mlp0"),
         2.0 * B * 512 * 15 * d, "TFLOP/s", MFMA_PEAK_TFS if dtype == "bf16" else FP32_MFMA_PEAK_TFS, "mfma",
         "2 x B x 512 x 15d")
+    if iso:
+        add("gemm_mlp0", f"gemm MLP layer 1 alone (eval-mode forward, no side-stream work, {dtype} MFMA)",
+            avg_ms("gemm_mlp0", iso), 2.0 * B * 512 * 15 * d, "TFLOP/s",
+            MFMA_PEAK_TFS if dtype == "bf16" else FP32_MFMA_PEAK_TFS, "mfma", "2 x B x 512 x 15d")
     if tr.table_adam == "eager":
         add("adam_table", "adam_table (eager: every untouched row each step)", avg_ms("adam_table"),
             24 * tr.rows_local * d + 4 * tr.rows_local, "GB/s", HBM_PEAK_GBS, "hbm", "24 B x rows x d + 4 B x rows")
-    main_k = [r for r in rooflines if "side stream" not in r["kernel"]]
+    main_k = [r for r in rooflines if "side stream" not in r["kernel"] and " alone " not in r["kernel"]]
     dominant = max(main_k, key=lambda r: r["avg_launch_ms"]) if main_k else None
-    out = {"dt": dt, "K": K, "W": W, "B": B, "L": L, "V": V, "d": d, "rows_local": tr.rows_local, "loss": loss,
+    out = {"dt": dt, "t_host": t_host, "K": K, "W": W, "B": B, "L": L, "V": V, "d": d, "rows_local": tr.rows_local, "loss": loss,
            "rooflines": rooflines, "roofline": dominant, "table_adam": tr.table_adam, "graphs": bool(graphs),
            "prime": prime, "batches": nb, "lag": lag, "stale": stale, "touched": touched, "prefetch": prefetch}
     del graphs, tr, batches
@@ -344,7 +350,7 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if world > 1 or FORCE_SHARD:
         if rehearsal:
             dist.init_process_group(backend)
         else:
@@ -379,8 +385,9 @@ def main():
                                       if args.dtype == "bf16" else "fp32 throughout"),
                        "model": "MM_FiBiNET", "global_batch": B * world, "seq_len": r["L"],
                        "item_rows": r["V"], "item_rows_per_gpu": r["rows_local"], "emb_dim": r["d"],
-                       "parallelism": f"row-shard{world}" if world > 1 else "single",
+                       "parallelism": f"row-shard{world}" if world > 1 or FORCE_SHARD else "single",
                        "hipgraph": r["graphs"], **({"rehearsal": backend} if rehearsal else {})},
+            "host_enqueue_ms_per_step": round(r["t_host"] / K * 1e3, 4),
             "roofline": r["roofline"],
             "rooflines": r["rooflines"],
             "table_adam": r["table_adam"],
@@ -403,7 +410,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, world)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if world > 1 or FORCE_SHARD:
         dist.barrier()
         dist.destroy_process_group()
 

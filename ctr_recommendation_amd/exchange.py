@@ -79,7 +79,7 @@ class RowExchange:
         self.cur = 0
         self.side = None
         self.route_group = group
-        if torch.device(device).type == "cuda" and world > 1 and dist.is_initialized():
+        if torch.device(device).type == "cuda" and dist.is_initialized():
             self.side = torch.cuda.Stream(device=device)
             # a communicator of its own: the next batch's counts exchange runs beside this step's
             # collectives instead of queueing between them (every rank creates it here, in order)

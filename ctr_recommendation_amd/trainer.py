@@ -56,6 +56,27 @@ def _events_end(e, stream=None):
         e.record(stream)
 
 
+def _side_stream(dev):
+    """The side stream; FBN_SIDE_CU_MASK=<hex word>[,<hex word>...] (32 CUs per word, repeated to
+    cover the device) restricts it to a CU subset (hipExtStreamCreateWithCUMask) -- tuning knob
+    (measured: restricting the table-Adam side work to 64 or 32 CUs doubles the step time)."""
+    mask = os.environ.get("FBN_SIDE_CU_MASK")
+    if not mask:
+        return torch.cuda.Stream(device=dev)
+    import ctypes
+    words = [int(w, 16) for w in mask.split(",")]
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    n = (ncu + 31) // 32
+    arr = (ctypes.c_uint32 * n)(*[words[i % len(words)] for i in range(n)])
+    hip = ctypes.CDLL("libamdhip64.so")
+    s = ctypes.c_void_p()
+    with torch.cuda.device(dev):
+        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(s), n, arr)
+    if rc != 0:
+        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
+    return torch.cuda.ExternalStream(s.value, device=dev)
+
+
 def _pad4(n: int) -> int:
     return (n + 3) // 4 * 4
 
@@ -67,7 +88,7 @@ class FiBiNETTrainer:
                  stage_on_cpu: bool = False, dropout_seed: Optional[int] = None, table_adam: str = "lazy",
                  lazy_window: int = 128, defer_table_grads: bool = True, max_norm: float = 10.0,
                  optimizer: Optional[str] = None, deterministic: Optional[bool] = None,
-                 prefetch_rows: bool = True):
+                 prefetch_rows: bool = True, shard: Optional[bool] = None):
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise RuntimeError("FiBiNETTrainer runs on a HIP device only (no CPU fallback)")
@@ -88,6 +109,10 @@ class FiBiNETTrainer:
         self.decoupled = self.optimizer == "adamw"
         self.wd_g = 0.0 if self.decoupled else self.wd           # weight decay inside the gradient
         self.rank, self.world, self.group = rank, world, group
+        # the row-sharded path (exchange, owner-side table Adam); shard=True runs it at world = 1 too
+        # (an RCCL smoke test of the N > 1 code on a one-GPU box: every collective has one rank)
+        self.sharded = world > 1 if shard is None else bool(shard)
+        sharded = self.sharded
         self.B = batch_size                     # per-rank batch
         self.L = max_len
         if init_state is None:
@@ -141,26 +166,26 @@ class FiBiNETTrainer:
         if world == 1:
             self.p[TABLE] = self.E
         i32 = dict(dtype=torch.int32, device=dev)
-        self.n_entries = self.B * (max_len + 1) if world == 1 else world * self.B * (max_len + 1)
+        self.n_entries = self.B * (max_len + 1) if not sharded else world * self.B * (max_len + 1)
         self.map = torch.full((max(1, self.rows_local),), -1, **i32)         # row -> claiming entry
         self.slot_row = torch.full((self.n_entries,), -1, **i32)              # entry -> claimed row
-        self.gvec = torch.zeros((self.B, 2, d), dtype=torch.float32, device=dev) if world == 1 else None
-        self.extra = torch.zeros((self.n_entries, d), dtype=torch.float32, device=dev) if world == 1 else None
+        self.gvec = torch.zeros((self.B, 2, d), dtype=torch.float32, device=dev) if not sharded else None
+        self.extra = torch.zeros((self.n_entries, d), dtype=torch.float32, device=dev) if not sharded else None
         # single GPU: claim-time duplicate list (entry -> claiming entry) and per-sample gradient norms
-        self.dup = torch.full((self.n_entries,), -1, **i32) if world == 1 else None
-        self.gnorm = torch.zeros((self.B, 2), dtype=torch.float64, device=dev) if world == 1 else None
+        self.dup = torch.full((self.n_entries,), -1, **i32) if not sharded else None
+        self.gnorm = torch.zeros((self.B, 2), dtype=torch.float64, device=dev) if not sharded else None
         # deterministic mode (single GPU): rows hit by several entries are folded by
         # order-independent int64 fixed-point sums (fbn_sparse_fold_fx) instead of float atomics, so
         # two runs from the same state produce bit-identical table gradients and weights
         if deterministic is None:
             deterministic = bool(model_cfg.get("deterministic", False)) or os.environ.get("FBN_DETERMINISTIC") == "1"
-        self.deterministic = bool(deterministic) and world == 1
+        self.deterministic = bool(deterministic) and not sharded
         # lazy table Adam, single GPU, d = 128 / 256: step(..., next_batch=...) brings the next
         # batch's rows up to date on the side stream during this step (fbn_adam_prefetch)
-        self.prefetch_rows = bool(prefetch_rows) and world == 1 and self.d in (128, 256)
+        self.prefetch_rows = bool(prefetch_rows) and not sharded and self.d in (128, 256)
         # N > 1, the owner's side: the next step's requested rows arrive during this step (the
         # padded id exchange of RowExchange.prepare) and are caught up ahead (fbn_adam_prefetch_rows)
-        self.prefetch_owner = bool(prefetch_rows) and world > 1 and self.d in (128, 256)
+        self.prefetch_owner = bool(prefetch_rows) and sharded and self.d in (128, 256)
         # the prefetch also decides the next batch's row claims (tagged, no CAS at claim time);
         # they are used only by a step given the very id tensors they were made for
         self.preclaim = torch.zeros(self.V, dtype=torch.int64, device=dev) if self.prefetch_rows else None
@@ -186,7 +211,7 @@ class FiBiNETTrainer:
         self.acts: Dict[str, torch.Tensor] = {}
         self.coll = DistCollective(world, group, stage_on_cpu)
         self.xchg = RowExchange(rank, world, self.V, d, self.B, max_len, dev, group, stage_on_cpu=stage_on_cpu,
-                                rows_bf16=self.fcfg.bf16) if world > 1 else None
+                                rows_bf16=self.fcfg.bf16) if sharded else None
         self.stage_on_cpu = stage_on_cpu
         # item-table Adam: "lazy" (default) replays the zero-gradient steps of a row when the row
         # is next claimed or its rolling window comes round (bit-identical to eager; see
@@ -207,14 +232,14 @@ class FiBiNETTrainer:
         self.deferred = self.table_adam == "lazy" and defer_table_grads
         self.pend = self.ring = self.coef_hist = None
         self.ring_n = self.lazy_window + 1
-        self.ring_cap = self.B * (max_len + 1) if world > 1 else 0
+        self.ring_cap = self.B * (max_len + 1) if sharded else 0
         if self.deferred:
             self.pend = torch.full((max(1, self.rows_local),), -1, **i32)
-            shape = (self.ring_n, self.B, 2, d) if world == 1 else (self.ring_n, self.ring_cap, d)
+            shape = (self.ring_n, self.B, 2, d) if not sharded else (self.ring_n, self.ring_cap, d)
             self.ring = torch.zeros(shape, dtype=torch.float32, device=dev)
             self.coef_hist = torch.ones(total_steps + 1, dtype=torch.float32, device=dev)
             self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)     # fbn_adam_step_tail
-        self.side = torch.cuda.Stream(device=dev)      # eager untouched pass / lazy rolling window
+        self.side = _side_stream(dev)      # eager untouched pass / lazy rolling window
 
     # ------------------------------------------------------------------ one training step
     def step(self, batch: Dict[str, torch.Tensor], labels: torch.Tensor,
@@ -373,14 +398,14 @@ class FiBiNETTrainer:
             call("fbn_sparse_fixup", None, None, ptr(self.xchg.recv_ids), n_ent, 0, self.V, self.rank, ptr(self.map),
                  ptr(grows), None, ptr(self.slot_row), 1, d, st)
         # clip_grad_norm_(10): dense grads (identical on every rank) + disjoint table shards
-        tab_acc = self.sumsq_tab if self.world > 1 else self.sumsq
+        tab_acc = self.sumsq_tab if self.sharded else self.sumsq
         if self.xchg is None and L > 0:
             call("fbn_sumsq_sparse_norms", ptr(self.gnorm), ptr(gsrc[0]), ptr(gsrc[1]), ptr(self.slot_row), gsrc[2],
                  n_ent, d, ptr(tab_acc), ptr(self.fx), st)
         else:
             call("fbn_sumsq_sparse", ptr(gsrc[0]), ptr(gsrc[1]), ptr(self.slot_row), gsrc[2], n_ent, d, ptr(tab_acc),
                  st)
-        if self.world > 1:
+        if self.sharded:
             # ONE all-reduce: dense grads + the loss + this shard's table-gradient sumsq
             o = self.n_dense
             call("fbn_pack_extras", ptr(self.loss), ptr(self.sumsq_tab), ptr(self.flat_g_ext[o:]), st)
@@ -421,7 +446,7 @@ class FiBiNETTrainer:
         return self.loss
 
     def _ring_stride(self) -> int:
-        return self.B * 2 * self.d if self.world == 1 else self.ring_cap * self.d
+        return self.B * 2 * self.d if not self.sharded else self.ring_cap * self.d
 
     def _pend_args(self):
         """(pend, ring, coef_hist, ring_stride, ring_n) of the deferred table gradients (NULLs when off)."""

@@ -1,0 +1,57 @@
+"""fbn_route (the requester's routing of a step's ids to their owners) against the oracle's
+restatement (oracle/exchange_ref.py, entry order): the same per-owner counts and offsets, each
+owner's segment holding the same multiset of local rows, pos[b][t] a bijection from the routed
+entries onto the send buffer with send_ids[pos[b][t]] == the entry's local row, and -1 exactly
+for the entries that are not routed (history padding).  The HIP kernel hands out positions per
+256-entry round, so the order inside a segment is not the oracle's entry order."""
+import pytest
+import torch
+
+from ctr_recommendation_amd.exchange import HipExchangeKernels
+from oracle.exchange_ref import CpuExchangeKernels
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("world,B,L,zipf", [(1, 8192, 20, False), (3, 4096, 20, False), (8, 8192, 20, True),
+                                            (64, 2048, 7, False), (5, 300, 0, False)])
+def test_route_matches_oracle(hip_device, world, B, L, zipf):
+    dev = hip_device
+    V = 250_007
+    Vl = (V + world - 1) // world
+    g = torch.Generator().manual_seed(world * 1000 + B)
+    if zipf:   # a few hot ids: many entries of one owner in every round
+        ids = (torch.rand(B, L + 1, generator=g) ** 6 * V).long()
+    else:
+        ids = torch.randint(0, V, (B, L + 1), generator=g)
+    ids[:, 1:][torch.rand(B, L, generator=g) < 0.4] = 0           # history padding (not routed)
+    ids[: B // 7, 0] = 0                                            # item id 0 is routed (row 0)
+    item, seq = ids[:, 0].contiguous(), (ids[:, 1:].contiguous() if L else None)
+
+    def bufs(device):
+        i32 = dict(dtype=torch.int32, device=device)
+        return dict(counts=torch.zeros(world, **i32), offsets=torch.zeros(world + 1, **i32),
+                    cursor=torch.zeros(world, **i32), send_ids=torch.full((B * (L + 1),), -7, **i32),
+                    pos=torch.full((B, L + 1), -7, **i32), err=torch.zeros(1, **i32))
+
+    ref = bufs("cpu")
+    CpuExchangeKernels().route(item, seq, B, L, V, Vl, world, ref["counts"], ref["offsets"], ref["cursor"],
+                               ref["send_ids"], ref["pos"], ref["err"])
+    out = bufs(dev)
+    HipExchangeKernels().route(item.to(dev), seq.to(dev) if L else None, B, L, V, Vl, world, out["counts"],
+                               out["offsets"], out["cursor"], out["send_ids"], out["pos"], out["err"])
+    out = {k: v.cpu() for k, v in out.items()}
+    assert int(out["err"]) == 0
+    assert torch.equal(out["counts"], ref["counts"]) and torch.equal(out["offsets"], ref["offsets"])
+    n = int(ref["offsets"][-1])
+    for o in range(world):
+        a, b = int(ref["offsets"][o]), int(ref["offsets"][o + 1])
+        assert torch.equal(out["send_ids"][a:b].sort().values, ref["send_ids"][a:b].sort().values), o
+    routed = ref["pos"] >= 0
+    assert torch.equal(out["pos"] >= 0, routed)
+    p = out["pos"][routed].long()
+    assert torch.equal(p.sort().values, torch.arange(n))             # a bijection onto the buffer
+    local = (ids - (ids // Vl) * Vl)[routed].int()
+    assert torch.equal(out["send_ids"][p], local)
+    owner = (ids // Vl)[routed]
+    assert bool(((p >= ref["offsets"][owner]) & (p < ref["offsets"][owner + 1])).all())

@@ -1,0 +1,90 @@
+"""The row-sharded (N > 1) trainer over RCCL, as a one-rank job on one MI355X.
+
+RCCL refuses two ranks on one device, so the multi-rank rehearsals (test_gpu_multirank.py)
+run their collectives over gloo.  This test runs the sharded code path itself -- RowExchange's
+all-to-alls with host split lists, the route-ahead communicator and its side-stream
+all-to-all (prepare), the owner-side prefetch, deferred gradient rows in a ring slot, the
+packed dense all-reduce -- over the "nccl" backend (RCCL) with world = 1 (FiBiNETTrainer
+shard=True), in a child process, and checks it against the single-GPU trainer on the same
+batches: fp32 losses within 1e-5 (relative), the table within 1e-5 after the flush and the dense
+parameters within 1e-3 of their displacement (norm; as test_gpu_trainer.py); with the bf16 wire
+format (rows and gradient rows as bf16) the losses agree within 5e-3 over the 6 steps.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        from ctr_recommendation_amd.data import make_batch
+        from ctr_recommendation_amd.trainer import FiBiNETTrainer
+        from oracle.fibinet_oracle import build_model
+        V, B, steps = 60000, 1024, 6
+        out = {}
+        for dtype in ("fp32", "bf16"):
+            cfg = {"embedding_dim": 128, "vocab_size": V, "honour_config": True, "net_dropout": 0.0,
+                   "compute_dtype": dtype}
+            torch.manual_seed(0)
+            init = build_model(None, cfg, honour_config=True).state_dict()
+            bs = [make_batch(500 + s, B, V, device=dev) for s in range(steps + 1)]
+            res = []
+            for shard in (False, True):
+                tr = FiBiNETTrainer(cfg, total_steps=20, batch_size=B, device=dev, init_state=
+                                    {k: v.clone() for k, v in init.items()}, shard=shard)
+                assert (tr.xchg is not None) == shard
+                p_init = tr.flat_p.cpu().clone()
+                if shard:
+                    assert tr.xchg.side is not None and tr.prefetch_owner and tr.deferred
+                losses = [tr.step(bs[s][0], bs[s][1], next_batch=bs[s + 1][0]).item() for s in range(steps)]
+                tr.flush()
+                tr.check_ids()
+                res.append((losses, tr.E.cpu().clone(), tr.flat_p.cpu().clone(), p_init))
+            (l0, e0, p0, q0), (l1, e1, p1, _) = res
+            # dense parameters: the difference relative to the 6 steps' displacement (Adam's
+            # normalised step turns last-bit gradient differences into small absolute ones)
+            out[dtype] = (l0, l1, float((e0 - e1).abs().max()), float((p0 - p1).norm() / (p0 - q0).norm()),
+                          float(e0.abs().max()))
+        q.put(("ok", out))
+    except Exception as e:   # report, then re-raise in the child
+        q.put((repr(e), None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_path_over_rccl_matches_single_gpu(hip_device):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(_port(), q))
+    p.start()
+    status, out = q.get(timeout=300)
+    p.join(timeout=60)
+    assert status == "ok", status
+    l0, l1, de, dp, e_max = out["fp32"]
+    for a, b in zip(l0, l1):
+        assert abs(a - b) <= 1e-5 * max(1.0, abs(a)), (l0, l1)
+    assert de <= 1e-5 * max(1.0, e_max) and dp <= 1e-3, (de, dp)
+    l0, l1, de, dp, _ = out["bf16"]
+    # bf16 wire: the looked-up rows are rounded to bf16 before the fields kernel (the single-GPU
+    # bf16 path reads f32 rows), so the two agree to bf16 rounding, not bit for bit
+    for a, b in zip(l0, l1):
+        assert abs(a - b) <= 5e-3, (l0, l1)
