@@ -215,11 +215,14 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if tr.xchg is not None:
+        tr.xchg.host_wait_s = 0.0
     t0 = time.perf_counter()
     for _ in range(K):
         run_step(i)
         i += 1
     t_host = time.perf_counter() - t0            # host enqueue time of the K steps
+    t_wait = tr.xchg.host_wait_s if tr.xchg is not None else 0.0   # of which blocked on routed counts
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -325,7 +328,7 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
             24 * tr.rows_local * d + 4 * tr.rows_local, "GB/s", HBM_PEAK_GBS, "hbm", "24 B x rows x d + 4 B x rows")
     main_k = [r for r in rooflines if "side stream" not in r["kernel"] and " alone " not in r["kernel"]]
     dominant = max(main_k, key=lambda r: r["avg_launch_ms"]) if main_k else None
-    out = {"dt": dt, "t_host": t_host, "K": K, "W": W, "B": B, "L": L, "V": V, "d": d, "rows_local": tr.rows_local, "loss": loss,
+    out = {"dt": dt, "t_host": t_host, "t_wait": t_wait, "K": K, "W": W, "B": B, "L": L, "V": V, "d": d, "rows_local": tr.rows_local, "loss": loss,
            "rooflines": rooflines, "roofline": dominant, "table_adam": tr.table_adam, "graphs": bool(graphs),
            "prime": prime, "batches": nb, "lag": lag, "stale": stale, "touched": touched, "prefetch": prefetch}
     del graphs, tr, batches
@@ -388,6 +391,7 @@ def main():
                        "parallelism": f"row-shard{world}" if world > 1 or FORCE_SHARD else "single",
                        "hipgraph": r["graphs"], **({"rehearsal": backend} if rehearsal else {})},
             "host_enqueue_ms_per_step": round(r["t_host"] / K * 1e3, 4),
+            **({"host_blocked_ms_per_step": round(r["t_wait"] / K * 1e3, 4)} if r["t_wait"] else {}),
             "roofline": r["roofline"],
             "rooflines": r["rooflines"],
             "table_adam": r["table_adam"],

@@ -241,12 +241,19 @@ extern "C" int fbn_widen_bf16(const void* in, float* out, long long n, void* str
 // Padded copy of a routing: out[o][j] = the j-th id routed to owner o (send_ids[offsets[o] + j]) for
 // j < counts[o], else -1 -- an all-to-all with equal splits of `cap` then needs no host-side counts
 // (RowExchange.prepare: the next step's requests reach their owners during this step)
+// The next step's routing as ONE equal-split all-to-all (RowExchange.prepare): destination o
+// gets a block of cap + 1 ints -- its routed local rows padded with -1 to cap, then -2 - count in
+// the last slot.  Negative slots read as "no row" (fbn_adam_prefetch_rows takes the received
+// blocks as they are); fbn_compact_routes recovers the counts and the packed ids at the owner,
+// so the next forward needs neither a counts nor an ids all-to-all.
 __global__ void pad_routes_kernel(const int* __restrict__ send_ids, const int* __restrict__ offsets,
                                   const int* __restrict__ counts, int world, int cap, int* __restrict__ out) {
-  const long long total = (long long)world * cap;
+  const int cap1 = cap + 1;
+  const long long total = (long long)world * cap1;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
-    const int o = (int)(i / cap), j = (int)(i - (long long)o * cap);
-    out[i] = j < counts[o] ? send_ids[offsets[o] + j] : -1;
+    const int o = (int)(i / cap1), j = (int)(i - (long long)o * cap1);
+    const int c = counts[o];
+    out[i] = j == cap ? -2 - c : (j < c ? send_ids[offsets[o] + j] : -1);
   }
 }
 
@@ -254,10 +261,42 @@ extern "C" int fbn_pad_routes(const int* send_ids, const int* offsets, const int
                               void* stream) {
   if (world <= 0 || cap <= 0) return FBN_OK;
   if (!send_ids || !offsets || !counts || !out) { fbn_set_error("fbn_pad_routes: null buffer"); return FBN_ERR_ARG; }
-  long long blocks = ((long long)world * cap + 255) / 256;
+  long long blocks = ((long long)world * (cap + 1) + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(pad_routes_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, send_ids, offsets,
                      counts, world, cap, out);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+// owner side of the padded exchange: counts[r] = entries requested by rank r, ids = the requests
+// packed in rank order (what the host-split ids all-to-all would have delivered)
+__global__ void compact_routes_kernel(const int* __restrict__ padded, int world, int cap, int* __restrict__ ids,
+                                      int* __restrict__ counts) {
+  __shared__ int cnt[64], off[64];
+  const int cap1 = cap + 1;
+  if (threadIdx.x < world) cnt[threadIdx.x] = -2 - padded[(long long)threadIdx.x * cap1 + cap];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int r = 0; r < world; ++r) { off[r] = s; s += cnt[r]; }
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x < world) counts[threadIdx.x] = cnt[threadIdx.x];
+  const long long total = (long long)world * cap1;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int r = (int)(i / cap1), j = (int)(i - (long long)r * cap1);
+    if (j < cnt[r]) ids[off[r] + j] = padded[i];
+  }
+}
+
+extern "C" int fbn_compact_routes(const int* padded, int world, int cap, int* ids, int* counts, void* stream) {
+  if (world < 1 || world > 64 || cap <= 0) { fbn_set_error("fbn_compact_routes: 1 <= world <= 64, cap > 0"); return FBN_ERR_ARG; }
+  if (!padded || !ids || !counts) { fbn_set_error("fbn_compact_routes: null buffer"); return FBN_ERR_ARG; }
+  long long blocks = ((long long)world * (cap + 1) + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(compact_routes_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, padded, world,
+                     cap, ids, counts);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

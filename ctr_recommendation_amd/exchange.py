@@ -14,13 +14,17 @@ Backward (the sparse reduce-scatter):
   rows are the owner's sparse gradient (slot = received entry; fbn_sparse_fixup folds rows hit
   by several entries into the entry that claimed the row in the forward).
 Split sizes need a host read of the N routed counts per step (all_to_all_single takes host
-split lists).  ``prepare(next_batch)`` takes that read off the critical path: the next batch is
-routed and its counts exchanged on a side stream while the current step runs, and the counts
-land in pinned host memory -- the next forward reads them without waiting on the main stream
-(two routing buffer sets alternate).  Without it the forward reads them inline (one sync).
+split lists).  ``prepare(next_batch)`` takes that read and the ids all-to-all off the critical
+path: the next batch is routed on a side stream while the current step runs and sent to the
+owners as ONE equal-split all-to-all of padded per-owner blocks that carry their counts; the
+owners pack the ids on device and both count vectors land in pinned host memory -- the next
+forward starts at the owner's claims with no collective before them (two routing buffer sets
+alternate).  Without it the forward routes inline: a counts all-to-all, one host sync, an ids
+all-to-all.
 """
 from __future__ import annotations
 
+import time
 from typing import Optional
 
 import torch
@@ -49,6 +53,9 @@ class HipExchangeKernels:
              int(out.dtype == torch.bfloat16),
              _lib.stream_handle(E.device))
 
+    def compact_routes(self, padded, world, cap, ids, counts):
+        call("fbn_compact_routes", ptr(padded), world, cap, ptr(ids), ptr(counts), _lib.stream_handle(ids.device))
+
     def widen(self, inp, out):
         call("fbn_widen_bf16", ptr(inp), ptr(out), inp.numel(), _lib.stream_handle(out.device))
 
@@ -73,6 +80,7 @@ class RowExchange:
             self.sets.append({"counts": torch.zeros(world, **i32), "offsets": torch.zeros(world + 1, **i32),
                               "cursor": torch.zeros(world, **i32), "send_ids": torch.empty(B * (L + 1), **i32),
                               "pos": torch.empty((B, L + 1), **i32), "recv_counts": torch.zeros(world, **i32),
+                              "recv_ids": None,
                               "host": torch.zeros(2 * world, dtype=torch.int32,
                                                   pin_memory=torch.device(device).type == "cuda"),
                               "event": None, "key": None})
@@ -88,6 +96,7 @@ class RowExchange:
         self.recv_counts = None
         self.recv_ids = None
         self.next_lids = None
+        self.host_wait_s = 0.0      # host time blocked on the routed-ahead counts (bench diagnostics)
 
     @property
     def rows_lo(self) -> int:
@@ -111,7 +120,7 @@ class RowExchange:
     def pos(self):
         return self.sets[self.cur]["pos"]
 
-    def _route(self, st, item, seq, err, group=None):
+    def _route(self, st, item, seq, err, group=None, exchange_counts=True):
         B = item.shape[0]
         L = 0 if seq is None else seq.shape[1]
         if L != self.L:
@@ -119,7 +128,8 @@ class RowExchange:
         pos = st["pos"][:B, :L + 1]
         self.k.route(item, seq, B, L, self.V, self.Vl, self.world, st["counts"], st["offsets"], st["cursor"],
                      st["send_ids"], pos, err)
-        self._a2a(st["recv_counts"], st["counts"], None, None, group)
+        if exchange_counts:
+            self._a2a(st["recv_counts"], st["counts"], None, None, group)
         return pos
 
     @staticmethod
@@ -128,32 +138,38 @@ class RowExchange:
         return (item.data_ptr(), item.shape[0], 0 if seq is None else seq.data_ptr(), 0 if seq is None else seq.shape[1])
 
     def prepare(self, item, seq, err, send_rows: bool = False) -> None:
-        """Route the NEXT step's batch now, on a side stream (HIP device only): its forward then
-        reads the counts from pinned host memory without a sync on the main stream.  It is used by
-        the next forward() only if that forward gets the same (unmodified) id tensors; otherwise
-        that forward routes inline.  send_rows: also deliver each owner the local rows the next
-        step's requests will name, as an equal-split all-to-all of the padded routing (no host
-        counts): self.next_lids [world * cap] (-1 = none), ready on self.side -- the owner's
-        table-Adam prefetch (fbn_adam_prefetch_rows) reads them."""
+        """Route the NEXT step's batch now, on a side stream (HIP device only), and deliver it to the
+        owners as ONE equal-split all-to-all of the padded routing (fbn_pad_routes: each
+        destination's ids padded to cap, its count in the last slot): the owner recovers the counts
+        and the packed ids on device (fbn_compact_routes), and both count vectors land in pinned
+        host memory -- the next forward reads them without a sync on the main stream and runs no
+        counts / ids all-to-all.  Used by the next forward() only if it gets the same
+        (unmodified) id tensors; otherwise that forward routes inline.  send_rows: also expose the
+        received padded blocks as self.next_lids [world * (cap + 1)] (negative = no row), ready on
+        self.side -- the owner's table-Adam prefetch (fbn_adam_prefetch_rows) reads them."""
         self.next_lids = None
         if self.side is None:
             return
         st = self.sets[1 - self.cur]
         main = torch.cuda.current_stream(item.device)
         self.side.wait_stream(main)                 # the ids and the buffer set are free
+        B = item.shape[0]
+        cap = B * (1 + (0 if seq is None else seq.shape[1]))
         with torch.cuda.stream(self.side):
-            st["pos_view"] = self._route(st, item, seq, err, self.route_group)
+            st["pos_view"] = self._route(st, item, seq, err, exchange_counts=False)
+            padded = torch.empty(self.world * (cap + 1), dtype=torch.int32, device=item.device)
+            self.k.pad_routes(st["send_ids"], st["offsets"], st["counts"], self.world, cap, padded)
+            recv = torch.empty_like(padded)
+            self._a2a(recv, padded, None, None, self.route_group)
+            if st["recv_ids"] is None or st["recv_ids"].numel() < self.world * cap:
+                st["recv_ids"] = torch.empty(self.world * cap, dtype=torch.int32, device=item.device)
+            self.k.compact_routes(recv, self.world, cap, st["recv_ids"], st["recv_counts"])
             st["host"][:self.world].copy_(st["counts"], non_blocking=True)
             st["host"][self.world:].copy_(st["recv_counts"], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self.side)
             if send_rows:
-                B = item.shape[0]
-                cap = B * (1 + (0 if seq is None else seq.shape[1]))
-                padded = torch.empty(self.world * cap, dtype=torch.int32, device=item.device)
-                self.k.pad_routes(st["send_ids"], st["offsets"], st["counts"], self.world, cap, padded)
-                self.next_lids = torch.empty_like(padded)
-                self._a2a(self.next_lids, padded, None, None, self.route_group)
+                self.next_lids = recv
         for t in (item, seq, err):
             if t is not None:
                 t.record_stream(self.side)
@@ -171,12 +187,15 @@ class RowExchange:
             # main stream after the side stream's routing work
             self.cur = 1 - self.cur
             st = self.sets[self.cur]
+            t0 = time.perf_counter()
             st["event"].synchronize()
+            self.host_wait_s += time.perf_counter() - t0
             torch.cuda.current_stream(item.device).wait_event(st["event"])
             st["event"] = None
             h = st["host"].tolist()
             sc, rc = h[:self.world], h[self.world:]
             pos = st["pos_view"]
+            prepared = True
         else:
             if nxt["event"] is not None:              # prepared for other tensors: drop it
                 nxt["event"].synchronize()
@@ -185,11 +204,15 @@ class RowExchange:
             pos = self._route(st, item, seq, err)
             sc = st["counts"].tolist()
             rc = st["recv_counts"].tolist()       # the one host sync of the step
+            prepared = False
         self.cur_pos = pos.contiguous()
         self.send_counts, self.recv_counts = sc, rc
         n_send, n_recv = sum(sc), sum(rc)
-        self.recv_ids = torch.empty(n_recv, dtype=torch.int32, device=item.device)
-        self._a2a(self.recv_ids, st["send_ids"][:n_send], rc, sc)
+        if prepared:          # the requests arrived with the routing (prepare): packed on the owner
+            self.recv_ids = st["recv_ids"][:n_recv]
+        else:
+            self.recv_ids = torch.empty(n_recv, dtype=torch.int32, device=item.device)
+            self._a2a(self.recv_ids, st["send_ids"][:n_send], rc, sc)
         reply = torch.empty((n_recv, self.d), dtype=self.row_dtype, device=item.device)
         if before_gather is not None and sparse.get("map") is not None:
             self.k.owner_claim(self.recv_ids, sparse["map"], sparse["slot_row"], self.rank)

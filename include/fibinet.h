@@ -353,10 +353,16 @@ int fbn_owner_gather(const int* ids, int n, const float* E, void* out, int* map,
                      int out_bf16, void* stream);
 /* bf16 -> f32 (n % 8 == 0, 16-B aligned): the owner's received bf16 gradient rows (bf16 mode). */
 int fbn_widen_bf16(const void* in, float* out, long long n, void* stream);
-/* out[o][j] = send_ids[offsets[o] + j] for j < counts[o], else -1 ([world][cap]): the routing of a
- * NEXT batch as an equal-split all-to-all (no host-side counts), for fbn_adam_prefetch_rows. */
+/* out [world][cap + 1]: out[o][j] = send_ids[offsets[o] + j] for j < counts[o], else -1, and
+ * out[o][cap] = -2 - counts[o] -- the routing of the NEXT batch as ONE equal-split all-to-all (no
+ * host-side counts, no counts all-to-all); negative slots read as "no row" in
+ * fbn_adam_prefetch_rows (n = world * (cap + 1)). */
 int fbn_pad_routes(const int* send_ids, const int* offsets, const int* counts, int world, int cap, int* out,
                    void* stream);
+/* The owner's side of that exchange (padded [world][cap + 1] as received): counts[r] = entries rank r
+ * requests, ids = the requests packed in rank order (= the host-split ids all-to-all's result);
+ * 1 <= world <= 64. */
+int fbn_compact_routes(const int* padded, int world, int cap, int* ids, int* counts, void* stream);
 
 /* ---------------------------------------------------------------- fused bilinear (bf16 mode, "all")
  * Replaces BilinearInteraction "all" (src/model_fibinet.py:60-79,89) and its autograd in ONE launch

@@ -54,11 +54,21 @@ class CpuExchangeKernels:
                 slot_row[i] = r
 
     def pad_routes(self, send_ids, offsets, counts, world, cap, out):
-        """Restates fbn_pad_routes: owner o's routed ids padded with -1 to cap."""
+        """Restates fbn_pad_routes: owner o's routed ids padded with -1 to cap, then -2 - count."""
         out.fill_(-1)
         for o in range(world):
             c, off = int(counts[o]), int(offsets[o])
-            out[o * cap:o * cap + c] = send_ids[off:off + c]
+            out[o * (cap + 1):o * (cap + 1) + c] = send_ids[off:off + c]
+            out[o * (cap + 1) + cap] = -2 - c
+
+    def compact_routes(self, padded, world, cap, ids, counts):
+        """Restates fbn_compact_routes: counts from the last slot of each block, ids packed in rank order."""
+        s = 0
+        for r in range(world):
+            c = -2 - int(padded[r * (cap + 1) + cap])
+            counts[r] = c
+            ids[s:s + c] = padded[r * (cap + 1):r * (cap + 1) + c]
+            s += c
 
     def widen(self, inp, out):
         """Restates fbn_widen_bf16: the owner's bf16 wire gradient rows to f32 (exact)."""

@@ -55,3 +55,33 @@ def test_route_matches_oracle(hip_device, world, B, L, zipf):
     assert torch.equal(out["send_ids"][p], local)
     owner = (ids // Vl)[routed]
     assert bool(((p >= ref["offsets"][owner]) & (p < ref["offsets"][owner + 1])).all())
+
+
+@pytest.mark.parametrize("world", [1, 4, 8])
+def test_padded_routes_roundtrip(hip_device, world):
+    """fbn_pad_routes -> (the equal-split all-to-all, here the identity of a one-sided view: block r
+    of rank s lands at rank r) -> fbn_compact_routes: the counts and the packed ids equal the
+    oracle's restatement, and equal what the host-split ids all-to-all would deliver."""
+    dev = hip_device
+    cap = 1000
+    g = torch.Generator().manual_seed(world)
+    counts = torch.randint(0, cap + 1, (world,), generator=g, dtype=torch.int32)
+    counts[0] = cap                                                  # a full block
+    offsets = torch.zeros(world + 1, dtype=torch.int32)
+    offsets[1:] = torch.cumsum(counts, 0)
+    send_ids = torch.randint(0, 10**6, (int(offsets[-1]),), generator=g, dtype=torch.int32)
+    ref, out = CpuExchangeKernels(), HipExchangeKernels()
+    pad_ref = torch.empty(world * (cap + 1), dtype=torch.int32)
+    ref.pad_routes(send_ids, offsets, counts, world, cap, pad_ref)
+    pad = torch.empty(world * (cap + 1), dtype=torch.int32, device=dev)
+    out.pad_routes(send_ids.to(dev), offsets.to(dev), counts.to(dev), world, cap, pad)
+    assert torch.equal(pad.cpu(), pad_ref)
+    ids = torch.full((world * cap,), -9, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(world, dtype=torch.int32, device=dev)
+    out.compact_routes(pad, world, cap, ids, cnt)
+    ids_ref = torch.full((world * cap,), -9, dtype=torch.int32)
+    cnt_ref = torch.zeros(world, dtype=torch.int32)
+    ref.compact_routes(pad_ref, world, cap, ids_ref, cnt_ref)
+    assert torch.equal(cnt.cpu(), counts) and torch.equal(cnt_ref, counts)
+    n = int(offsets[-1])
+    assert torch.equal(ids.cpu()[:n], send_ids) and torch.equal(ids_ref[:n], send_ids)
