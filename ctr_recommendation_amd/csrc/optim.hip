@@ -505,17 +505,27 @@ __global__ void __launch_bounds__(256) sumsq_sparse_kernel(GradSrc s, int n, dou
   const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
   double acc = 0.0;
-  for (long long e0 = gw * RPW; e0 < n; e0 += nw * RPW) {
-    const long long e = e0 + lane / G;
-    if (e >= n) continue;
-    const int sr = s.slot_row[e];
-    if (sr == -1) continue;
-    f32x4 v = *reinterpret_cast<const f32x4*>(grad_base<D>(s, (int)e) + 4 * q);
-    if (sr & FBN_SLOT_FLAG) {
-      const f32x4 x = *reinterpret_cast<const f32x4*>(s.extra + (size_t)e * D + 4 * q);
-      v = s.full ? x : v + x;
+  // two entries per group and round, each row loaded beside its slot_row (the row address does
+  // not depend on it: one round trip per round instead of two dependent ones per entry)
+  for (long long e0 = gw * RPW * 2; e0 < n; e0 += nw * RPW * 2) {
+    const long long ea = e0 + lane / G, eb = ea + RPW;
+    const bool oka = ea < n, okb = eb < n;
+    const int sra = oka ? s.slot_row[ea] : -1, srb = okb ? s.slot_row[eb] : -1;
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    f32x4 va = oka ? *reinterpret_cast<const f32x4*>(grad_base<D>(s, (int)ea) + 4 * q) : z;
+    f32x4 vb = okb ? *reinterpret_cast<const f32x4*>(grad_base<D>(s, (int)eb) + 4 * q) : z;
+    if (sra != -1 && (sra & FBN_SLOT_FLAG)) {
+      const f32x4 x = *reinterpret_cast<const f32x4*>(s.extra + (size_t)ea * D + 4 * q);
+      va = s.full ? x : va + x;
     }
-    acc += (double)(v[0] * v[0]) + (double)(v[1] * v[1]) + (double)(v[2] * v[2]) + (double)(v[3] * v[3]);
+    if (srb != -1 && (srb & FBN_SLOT_FLAG)) {
+      const f32x4 x = *reinterpret_cast<const f32x4*>(s.extra + (size_t)eb * D + 4 * q);
+      vb = s.full ? x : vb + x;
+    }
+    if (sra != -1)
+      acc += (double)(va[0] * va[0]) + (double)(va[1] * va[1]) + (double)(va[2] * va[2]) + (double)(va[3] * va[3]);
+    if (srb != -1)
+      acc += (double)(vb[0] * vb[0]) + (double)(vb[1] * vb[1]) + (double)(vb[2] * vb[2]) + (double)(vb[3] * vb[3]);
   }
   red[threadIdx.x] = acc;
   __syncthreads();
