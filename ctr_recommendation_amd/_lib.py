@@ -98,6 +98,7 @@ SIGNATURES = {
     "fbn_widen_bf16": (I, [P, P, LL, P]),
     "fbn_pad_routes": (I, [P, P, P, I, I, P, P]),
     "fbn_compact_routes": (I, [P, I, I, P, P, P]),
+    "fbn_copy_jobs": (I, [P, P, P, I, P]),
     "fbn_bilinear_supported": (I, [I]),
     "fbn_bilinear_fwd": (I, [P, P, P, I, I, I, P]),
     "fbn_bilinear_bwd": (I, [P, I, I, P, P, P, P, P, I, I, P]),

@@ -300,3 +300,47 @@ extern "C" int fbn_compact_routes(const int* padded, int world, int cap, int* id
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
+
+// ------------------------------------------------------------------ step inputs -> static buffers
+// Up to 8 device-to-device copies in ONE launch (16-B granules; sizes and pointers 16-B aligned):
+// the batch fields, labels and pos of a step copied into the addresses the trainer's captured
+// compute segments read (each copy_ alone is a ~5 us blit launch).
+struct CopyJobs {
+  const int4* src[8];
+  int4* dst[8];
+  long long n16[8];
+  long long first[9];   // first granule of each job (prefix sum)
+};
+__global__ void __launch_bounds__(256) copy_jobs_kernel(CopyJobs J, int njobs) {
+  const long long total = J.first[njobs];
+  for (long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x; g < total; g += (long long)gridDim.x * blockDim.x) {
+    int j = 0;
+    while (j + 1 < njobs && g >= J.first[j + 1]) ++j;
+    const long long k = g - J.first[j];
+    J.dst[j][k] = J.src[j][k];
+  }
+}
+
+extern "C" int fbn_copy_jobs(const void* const* src, void* const* dst, const long long* bytes, int n, void* stream) {
+  if (n <= 0) return FBN_OK;
+  if (n > 8) { fbn_set_error("fbn_copy_jobs: at most 8 copies"); return FBN_ERR_ARG; }
+  CopyJobs J;
+  J.first[0] = 0;
+  for (int i = 0; i < 8; ++i) {
+    const int k = i < n ? i : 0;
+    if (i < n && ((bytes[i] & 15) || (((uintptr_t)src[i] | (uintptr_t)dst[i]) & 15))) {
+      fbn_set_error("fbn_copy_jobs: sizes and addresses must be 16-byte multiples");
+      return FBN_ERR_ARG;
+    }
+    J.src[i] = (const int4*)src[k];
+    J.dst[i] = (int4*)dst[k];
+    J.n16[i] = i < n ? bytes[i] / 16 : 0;
+    J.first[i + 1] = J.first[i] + J.n16[i];
+  }
+  if (J.first[n] <= 0) return FBN_OK;
+  long long blocks = (J.first[n] + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(copy_jobs_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, J, n);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}

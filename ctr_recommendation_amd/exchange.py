@@ -62,8 +62,8 @@ class HipExchangeKernels:
 
 class RowExchange:
     def __init__(self, rank: int, world: int, V: int, d: int, B: int, L: int, device, group=None, kernels=None,
-                 stage_on_cpu: bool = False, rows_bf16: bool = False):
-        self.rank, self.world, self.V, self.d, self.L = rank, world, V, d, L
+                 stage_on_cpu: bool = False, rows_bf16: bool = False, side=None):
+        self.rank, self.world, self.V, self.d, self.L, self.B = rank, world, V, d, L, B
         self.Vl = (V + world - 1) // world
         self.group = group
         self.k = kernels or HipExchangeKernels()
@@ -88,7 +88,10 @@ class RowExchange:
         self.side = None
         self.route_group = group
         if torch.device(device).type == "cuda" and dist.is_initialized():
-            self.side = torch.cuda.Stream(device=device)
+            # the caller's side stream when given (the trainer's: a process has 4 hardware queues,
+            # GPU_MAX_HW_QUEUES, and a stream of its own here landed on the main stream's queue,
+            # serialising the next batch's routing with this step's compute)
+            self.side = side if side is not None else torch.cuda.Stream(device=device)
             # a communicator of its own: the next batch's counts exchange runs beside this step's
             # collectives instead of queueing between them (every rank creates it here, in order)
             self.route_group = dist.new_group(ranks=list(range(world)))
@@ -97,6 +100,10 @@ class RowExchange:
         self.recv_ids = None
         self.next_lids = None
         self.host_wait_s = 0.0      # host time blocked on the routed-ahead counts (bench diagnostics)
+        # looked-up rows and per-entry gradient rows live in buffers that only grow (each step uses a
+        # prefix): fixed addresses, so the trainer's compute between the exchanges can be a hipGraph
+        self.rows_buf = None
+        self.send_buf = None
 
     @property
     def rows_lo(self) -> int:
@@ -220,12 +227,20 @@ class RowExchange:
             self.k.owner_gather(self.recv_ids, E_local, reply, None, None, self.rank, self.d)
         else:
             self.k.owner_gather(self.recv_ids, E_local, reply, sparse["map"], sparse["slot_row"], self.rank, self.d)
-        rows = torch.empty((n_send, self.d), dtype=self.row_dtype, device=item.device)
+        self.rows_buf = self._grow(self.rows_buf, n_send)
+        rows = self.rows_buf[:n_send]
         self._a2a(rows, reply, sc, rc)
         return rows
 
+    def _grow(self, buf, n):
+        if buf is None or buf.shape[0] < n:
+            cap = max(n, self.B * (self.L + 1))
+            buf = torch.empty((cap, self.d), dtype=self.row_dtype, device=self.device)
+        return buf
+
     def make_sendbuf(self) -> torch.Tensor:
-        return torch.empty((sum(self.send_counts), self.d), dtype=self.row_dtype, device=self.device)
+        self.send_buf = self._grow(self.send_buf, sum(self.send_counts))
+        return self.send_buf[:sum(self.send_counts)]
 
     def backward(self, sendbuf: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Returns the owner's received gradient rows [n_recv, d] f32 (entry i <-> recv_ids[i]),

@@ -22,6 +22,7 @@ reference computes), dense gradients are all-reduced, the clip norm sums the tab
 """
 from __future__ import annotations
 
+import ctypes
 import os
 from typing import Dict, List, Optional
 
@@ -63,7 +64,6 @@ def _side_stream(dev):
     mask = os.environ.get("FBN_SIDE_CU_MASK")
     if not mask:
         return torch.cuda.Stream(device=dev)
-    import ctypes
     words = [int(w, 16) for w in mask.split(",")]
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     n = (ncu + 31) // 32
@@ -75,6 +75,61 @@ def _side_stream(dev):
     if rc != 0:
         raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
     return torch.cuda.ExternalStream(s.value, device=dev)
+
+
+class _Segments:
+    """The collective hook of a captured compute region: ops.forward / ops.backward run once
+    under capture with this object as their `coll`; every allreduce_ (the SyncBN moments) closes
+    the hipGraph segment being captured and opens the next, so a replay is segment, all-reduce,
+    segment, ... -- the all-reduces stay eager RCCL calls with host-side arguments (nothing
+    collective is captured), the ~45 kernel launches between them become a handful of graph
+    launches."""
+
+    def __init__(self, base, pool):
+        self.base, self.world, self.pool = base, base.world, pool
+        self.prog: list = []
+        self.cur = None
+
+    def begin(self) -> None:
+        self.cur = torch.cuda.CUDAGraph()
+        # thread-local: the process group's watchdog thread keeps querying its events meanwhile
+        self.cur.capture_begin(pool=self.pool, capture_error_mode="thread_local")
+
+    def allreduce_(self, t: torch.Tensor) -> None:
+        self.cur.capture_end()
+        self.prog += [("graph", self.cur), ("allreduce", t)]
+        self.begin()
+
+    def end(self) -> None:
+        self.cur.capture_end()
+        self.prog.append(("graph", self.cur))
+        self.cur = None
+
+    def replay(self) -> None:
+        for kind, x in self.prog:
+            if kind == "graph":
+                x.replay()
+            else:
+                self.base.allreduce_(x)
+
+
+def _copy_many(pairs, stream) -> None:
+    """dst.copy_(src) for every (src, dst) pair, same shapes and dtypes: the 16-byte-aligned
+    contiguous ones in fbn_copy_jobs launches of up to 8, any other with copy_."""
+    fused = []
+    for src, dst in pairs:
+        nb = src.numel() * src.element_size()
+        if (src.is_contiguous() and dst.is_contiguous() and nb % 16 == 0 and src.data_ptr() % 16 == 0
+                and dst.data_ptr() % 16 == 0):
+            fused.append((src.data_ptr(), dst.data_ptr(), nb))
+        else:
+            dst.copy_(src, non_blocking=True)
+    for i in range(0, len(fused), 8):
+        chunk = fused[i:i + 8]
+        n = len(chunk)
+        call("fbn_copy_jobs", (ctypes.c_void_p * n)(*[c[0] for c in chunk]),
+             (ctypes.c_void_p * n)(*[c[1] for c in chunk]), (ctypes.c_longlong * n)(*[c[2] for c in chunk]), n,
+             stream)
 
 
 def _pad4(n: int) -> int:
@@ -210,8 +265,9 @@ class FiBiNETTrainer:
         self.host_step = 0
         self.acts: Dict[str, torch.Tensor] = {}
         self.coll = DistCollective(world, group, stage_on_cpu)
+        self.side = _side_stream(dev)      # eager untouched pass / lazy rolling window / routing ahead
         self.xchg = RowExchange(rank, world, self.V, d, self.B, max_len, dev, group, stage_on_cpu=stage_on_cpu,
-                                rows_bf16=self.fcfg.bf16) if sharded else None
+                                rows_bf16=self.fcfg.bf16, side=self.side) if sharded else None
         self.stage_on_cpu = stage_on_cpu
         # item-table Adam: "lazy" (default) replays the zero-gradient steps of a row when the row
         # is next claimed or its rolling window comes round (bit-identical to eager; see
@@ -239,7 +295,11 @@ class FiBiNETTrainer:
             self.ring = torch.zeros(shape, dtype=torch.float32, device=dev)
             self.coef_hist = torch.ones(total_steps + 1, dtype=torch.float32, device=dev)
             self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)     # fbn_adam_step_tail
-        self.side = _side_stream(dev)      # eager untouched pass / lazy rolling window
+        # N > 1: forward + backward between the row exchanges replayed as hipGraph segments split at
+        # the SyncBN all-reduces (_Segments), after two eager steps; FBN_SHARD_GRAPH=0 keeps it eager
+        self.shard_graph = self.sharded and os.environ.get("FBN_SHARD_GRAPH", "1") != "0"
+        self._sg = None
+        self._sg_eager = 0
 
     # ------------------------------------------------------------------ one training step
     def step(self, batch: Dict[str, torch.Tensor], labels: torch.Tensor,
@@ -361,16 +421,22 @@ class FiBiNETTrainer:
                  ptr(self.slot_row), ptr(self.dup), ptr(self.hasdup), st)
         if w16_ev is not None:
             main.wait_event(w16_ev)
-        a = ops.forward(self.p, batch, cfg, self.rng, table_rows=rows, pos=pos, err=self.err, labels=labels,
-                        w16_ready=w16_ev is not None,
-                        loss_denom=float(ntot), coll=self.coll, ntot=ntot, acts=self.acts, masks_out=masks_out,
-                        probe=probe, count_batches=False,     # num_batches_tracked: fbn_step_end
-                        after_gather=start_untouched_adam if self.table_adam == "eager" else None)
-        sendbuf = self.xchg.make_sendbuf() if self.xchg is not None else None
-        ops.backward(self.p, batch, a, a["gout"], self.g, cfg, gvec=self.gvec if self.xchg is None else None,
-                     gnorm=self.gnorm if self.xchg is None else None,
-                     pos=pos, sendbuf=sendbuf, coll=self.coll, ntot=ntot,
-                     extra_sums=[(a["loss_terms"], B, 1, self.loss, 1.0 / ntot)], probe=probe)
+        graphed = False
+        if (self.xchg is not None and self.shard_graph and probe is None and masks_out is None
+                and self.table_adam != "eager"):
+            sendbuf = self.xchg.make_sendbuf()
+            graphed = self._sharded_compute(batch, labels, pos, cfg, ntot, B, L)
+        if not graphed:
+            a = ops.forward(self.p, batch, cfg, self.rng, table_rows=rows, pos=pos, err=self.err, labels=labels,
+                            w16_ready=w16_ev is not None,
+                            loss_denom=float(ntot), coll=self.coll, ntot=ntot, acts=self.acts, masks_out=masks_out,
+                            probe=probe, count_batches=False,     # num_batches_tracked: fbn_step_end
+                            after_gather=start_untouched_adam if self.table_adam == "eager" else None)
+            sendbuf = self.xchg.make_sendbuf() if self.xchg is not None else None
+            ops.backward(self.p, batch, a, a["gout"], self.g, cfg, gvec=self.gvec if self.xchg is None else None,
+                         gnorm=self.gnorm if self.xchg is None else None,
+                         pos=pos, sendbuf=sendbuf, coll=self.coll, ntot=ntot,
+                         extra_sums=[(a["loss_terms"], B, 1, self.loss, 1.0 / ntot)], probe=probe)
         if self.xchg is None:
             # single GPU: per-sample vectors; entry e = b*(L+1)+t; duplicates -> extra[claimer]
             n_ent = B * (L + 1)
@@ -447,6 +513,47 @@ class FiBiNETTrainer:
 
     def _ring_stride(self) -> int:
         return self.B * 2 * self.d if not self.sharded else self.ring_cap * self.d
+
+    def _sharded_compute(self, batch, labels, pos, cfg, ntot: int, B: int, L: int) -> bool:
+        """N > 1: this step's forward + backward (looked-up rows -> per-entry gradient rows in the
+        exchange's send buffer) as a replay of the captured segments; False = run it eagerly (the
+        first two steps, and once whenever the shapes or the exchange buffers change)."""
+        x = self.xchg
+        key = (B, L, x.rows_buf.data_ptr(), x.send_buf.data_ptr(),
+               tuple((k, tuple(v.shape), v.dtype) for k, v in sorted(batch.items())))
+        sg = self._sg
+        if sg is None or sg["key"] != key:
+            self._sg_eager += 1
+            if self._sg_eager <= 2:
+                return False
+            sg = self._capture(key, batch, labels, pos, cfg, ntot, B)
+        pairs = [(v, sg["batch"][k]) for k, v in batch.items()] + [(labels, sg["labels"]), (pos, sg["pos"])]
+        _copy_many(pairs, _lib.stream_handle(self.device))
+        sg["seg"].replay()
+        return True
+
+    def _capture(self, key, batch, labels, pos, cfg, ntot: int, B: int):
+        x = self.xchg
+        main = torch.cuda.current_stream(self.device)
+        sb = {k: v.clone() for k, v in batch.items()}
+        sl, sp = labels.clone(), pos.clone()
+        self._sg = None
+        torch.cuda.synchronize(self.device)
+        seg = _Segments(self.coll, torch.cuda.graph_pool_handle())
+        cap = torch.cuda.Stream(device=self.device)
+        cap.wait_stream(main)
+        with torch.cuda.stream(cap):
+            seg.begin()
+            a = ops.forward(self.p, sb, cfg, self.rng, table_rows=x.rows_buf, pos=sp, err=self.err, labels=sl,
+                            loss_denom=float(ntot), coll=seg, ntot=ntot, acts=self.acts, count_batches=False)
+            ops.backward(self.p, sb, a, a["gout"], self.g, cfg, pos=sp, sendbuf=x.send_buf, coll=seg, ntot=ntot,
+                         extra_sums=[(a["loss_terms"], B, 1, self.loss, 1.0 / ntot)])
+            seg.end()
+        main.wait_stream(cap)
+        # every tensor the segments address stays referenced as long as they live
+        self._sg = {"key": key, "seg": seg, "batch": sb, "labels": sl, "pos": sp, "a": a, "acts": dict(self.acts),
+                    "bufs": (x.rows_buf, x.send_buf)}
+        return self._sg
 
     def _pend_args(self):
         """(pend, ring, coef_hist, ring_stride, ring_n) of the deferred table gradients (NULLs when off)."""

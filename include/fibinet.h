@@ -363,6 +363,9 @@ int fbn_pad_routes(const int* send_ids, const int* offsets, const int* counts, i
  * requests, ids = the requests packed in rank order (= the host-split ids all-to-all's result);
  * 1 <= world <= 64. */
 int fbn_compact_routes(const int* padded, int world, int cap, int* ids, int* counts, void* stream);
+/* Up to 8 device-to-device copies in one launch (bytes and addresses multiples of 16): a step's
+ * inputs into the static buffers of the trainer's captured compute segments (N > 1). */
+int fbn_copy_jobs(const void* const* src, void* const* dst, const long long* bytes, int n, void* stream);
 
 /* ---------------------------------------------------------------- fused bilinear (bf16 mode, "all")
  * Replaces BilinearInteraction "all" (src/model_fibinet.py:60-79,89) and its autograd in ONE launch

@@ -145,11 +145,12 @@ def _prefetch_worker(rank, world, port, q, out):
             bs.append(({k: v[rank * per:(rank + 1) * per].to(dev) for k, v in b.items()},
                        y[rank * per:(rank + 1) * per].to(dev)))
         res = []
-        for pf, defer in ((False, False), (False, True), (True, True)):
+        for pf, defer, graph in ((False, False, True), (False, True, True), (True, True, True), (True, True, False)):
             tr = FiBiNETTrainer(cfg, total_steps=20, batch_size=per, device=dev, rank=rank, world=world,
                                 init_state={k: v.clone() for k, v in init.items()}, stage_on_cpu=True,
                                 prefetch_rows=pf, defer_table_grads=defer)
-            assert tr.prefetch_owner == pf and tr.deferred == defer
+            assert tr.prefetch_owner == pf and tr.deferred == defer and tr.shard_graph
+            tr.shard_graph = graph     # steps 3.. replay the captured segments (split at the SyncBN all-reduces)
             losses = [tr.step(bs[s][0], bs[s][1], next_batch=bs[s + 1][0]).item() for s in range(steps)]
             torch.cuda.synchronize()
             # before the flush: the rows the unused last next batch names were caught up ahead
@@ -171,7 +172,8 @@ def test_owner_prefetch_bit_identical(hip_device, tmp_path):
     and deferred table gradients (received rows kept in a ring slot, applied at the row's next
     replay; a step receiving more than the slot holds applies them at once): 2 ranks on one MI355X
     (gloo, host-staged), ids unique within a step and recurring across steps: losses and every
-    table / moment / dense tensor bit-identical across immediate, deferred, deferred + prefetch."""
+    table / moment / dense tensor bit-identical across immediate, deferred, deferred + prefetch, and
+    with the forward + backward replayed as hipGraph segments (from step 3) or run eagerly."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
