@@ -39,7 +39,7 @@ SIGNATURES = {
     "fbn_bn_colpart_size": (SZ, [I, I]),
     "fbn_row_chunks": (I, [I]),
     "fbn_bn_bwd_chunks": (I, [I, I]),
-    "fbn_bn_bwd_fused": (I, [P, P, P, P, F, P, P, P, P, I, I, D, P, P, P, P, P, P, P, P]),
+    "fbn_bn_bwd_fused": (I, [P, P, P, P, P, F, P, P, P, P, I, I, D, P, P, P, P, P, P, P, P]),
     "fbn_colsum_partial": (I, [P, I, I, I, P, P]),
     "fbn_sum_jobs": (I, [P, I, P]),
     "fbn_fields_fwd": (I, [P, P, P, P, P, P, P, F, P, I, P, LL, P, P, P, P, P, I, P, P, P, P, I, I, P, P, P, P, P, I, I, I, I,

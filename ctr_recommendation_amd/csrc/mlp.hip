@@ -280,7 +280,7 @@ __global__ void __launch_bounds__(256) bn_act_fwd2_kernel(const float* __restric
       }
       y[e] = v;
     }
-    *reinterpret_cast<f32x4*>(Y + i) = y;
+    if (Y) *reinterpret_cast<f32x4*>(Y + i) = y;
     if (Y16) store4(Y16 + i, y);
     if (HEAD) {
       const f32x4 ww = *reinterpret_cast<const f32x4*>(head.w + c);
@@ -298,7 +298,17 @@ struct BnBwdSrc {
   const float* w;      // [C]
   const float* hact;   // [B][C]
   float scale;
+  const short* hact16; // [B][C] bf16 image of the activation, read instead of hact when hact is null
+                       // (matrix source only: the mask needs just the sign, bf16 keeps it)
 };
+// the activation's "> 0" test on 4 columns, from the f32 activation or its bf16 image (a bf16
+// bit pattern read as a signed short is > 0 exactly when the value is > +0)
+__device__ __forceinline__ f32x4 bn_act4(const BnBwdSrc& s, size_t i) {
+  if (s.hact) return *reinterpret_cast<const f32x4*>(s.hact + i);
+  const uint2 u = *reinterpret_cast<const uint2*>(s.hact16 + i);
+  return (f32x4){(short)(u.x & 0xffffu) > 0 ? 1.f : 0.f, (short)(u.x >> 16) > 0 ? 1.f : 0.f,
+                 (short)(u.y & 0xffffu) > 0 ? 1.f : 0.f, (short)(u.y >> 16) > 0 ? 1.f : 0.f};
+}
 __device__ __forceinline__ float bn_dy(const BnBwdSrc& s, int b, int c, int C) {
   const size_t i = (size_t)b * C + c;
   const float d = s.G ? s.G[i] : s.gvec[b] * s.w[c];
@@ -351,7 +361,7 @@ __global__ void __launch_bounds__(256) bn_bwd_partial4_kernel(BnBwdSrc s, const 
 #pragma unroll 4
     for (int r = r0 + rl; r < r1; r += 4) {
       const size_t i = (size_t)r * C + c;
-      const f32x4 h = *reinterpret_cast<const f32x4*>(s.hact + i);
+      const f32x4 h = bn_act4(s, i);
       const f32x4 x = *reinterpret_cast<const f32x4*>(Xpre + i);
       f32x4 d;
       float gv = 0.f;
@@ -564,11 +574,13 @@ __global__ void __launch_bounds__(1024) bn_bwd_reduce_finalize16_kernel(const do
                                                                         const float* __restrict__ invstd, float* coef,
                                                                         float* dgamma, float* dbeta, float* dw) {
   __shared__ double red[64][3][16];
+  __shared__ double red2[16][3][16];
   __shared__ double tot[3][16];
   const int col = threadIdx.x & 15, str = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + col;
   double r0 = 0.0, r1 = 0.0, r2 = 0.0;
   if (c < C) {
+#pragma unroll 4
     for (int k = str; k < nchunk; k += 64) {
       const double* pk = part + (size_t)k * 3 * C + c;
       r0 += pk[0];
@@ -580,10 +592,17 @@ __global__ void __launch_bounds__(1024) bn_bwd_reduce_finalize16_kernel(const do
   red[str][1][col] = r1;
   red[str][2][col] = r2;
   __syncthreads();
+  // fixed-order two-level fold of the 64 chunk-stride partials: 16 groups of 4, then the 16
+  if (threadIdx.x < 768) {
+    const int j = threadIdx.x / 48, qc = threadIdx.x % 48, q = qc >> 4, cc = qc & 15;
+    red2[j][q][cc] = ((red[4 * j][q][cc] + red[4 * j + 1][q][cc]) + red[4 * j + 2][q][cc]) + red[4 * j + 3][q][cc];
+  }
+  __syncthreads();
   if (threadIdx.x < 48) {
     const int q = threadIdx.x >> 4, cc = threadIdx.x & 15;
     double r = 0.0;
-    for (int k = 0; k < 64; ++k) r += red[k][q][cc];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) r += red2[k][q][cc];
     tot[q][cc] = r;
   }
   __syncthreads();
@@ -622,7 +641,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply4_kernel(BnBwdSrc s, const fl
     const f32x4 ww = s.G ? (f32x4){0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(s.w + c);
     for (int r = r0 + rl; r < r1; r += 4) {
       const size_t i = (size_t)r * C + c;
-      const f32x4 h = *reinterpret_cast<const f32x4*>(s.hact + i);
+      const f32x4 h = bn_act4(s, i);
       const f32x4 x = *reinterpret_cast<const f32x4*>(Xpre + i);
       f32x4 d;
       if (s.G) d = *reinterpret_cast<const f32x4*>(s.G + i);
@@ -633,7 +652,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply4_kernel(BnBwdSrc s, const fl
         const float dy = h[e] > 0.f ? d[e] * s.scale : 0.f;
         v[e] = (dy - c0[e] - (x[e] - mu[e]) * c1[e]) * is[e] * gg[e];
       }
-      *reinterpret_cast<f32x4*>(dX + i) = v;
+      if (dX) *reinterpret_cast<f32x4*>(dX + i) = v;
       if (dX16) store4(dX16 + i, v);
       acc += v;
     }
@@ -845,6 +864,18 @@ extern "C" int fbn_bn_eval_params(const float* run_mean, const float* run_var, f
   return FBN_OK;
 }
 
+// Rows per workgroup of the BN-apply kernels: 4 = one row per wave, so every row of the batch is
+// in flight at once (the fused head reduces a whole row per wave and then runs a serial sigmoid /
+// BCE tail: with 16 rows per workgroup each wave walked 4 rows one after the other).
+static int bn_act_rows_per_chunk() {
+  static const int rpc = [] {
+    const char* e = getenv("FBN_BN_ACT_RPC");
+    const int v = e ? atoi(e) : 4;
+    return v >= 4 && v % 4 == 0 ? v : 4;
+  }();
+  return rpc;
+}
+
 // rng: device [seed, offset] (uint64 x2) or null; mask_out (optional, u8 [B][C]) receives the keep-mask;
 // mask_in (optional, u8 [B][C]) replaces the RNG (parity tests against injected masks)
 extern "C" int fbn_bn_act_fwd(const float* X, float* Y, int B, int C, const float* mean, const float* invstd,
@@ -854,7 +885,8 @@ extern "C" int fbn_bn_act_fwd(const float* X, float* Y, int B, int C, const floa
   if (B <= 0) return FBN_OK;
   if (C & 3) { fbn_set_error("bn_act: C % 4"); return FBN_ERR_ARG; }
   if (p_drop > 0.f && !rng && !mask_in) { fbn_set_error("bn_act: dropout needs an rng state or a mask"); return FBN_ERR_ARG; }
-  const int rpc = 16;
+  if (!Y && !Y16) { fbn_set_error("bn_act: no output"); return FBN_ERR_ARG; }
+  const int rpc = bn_act_rows_per_chunk();
   hipLaunchKernelGGL(bn_act_fwd2_kernel<false>, dim3(fbn_cdiv(C, 256), fbn_cdiv(B, rpc)), dim3(256), 0,
                      (hipStream_t)stream, X, Y, B, C, rpc, mean, invstd, g, b, p_drop, rng, stream_id, mask_out, mask_in,
                      Y16, HeadArgs{});
@@ -871,7 +903,7 @@ extern "C" int fbn_bn_act_head_fwd(const float* X, float* Y, int B, int C, const
   if (B <= 0) return FBN_OK;
   if (C != 256) { fbn_set_error("bn_act_head: the fused head needs C == 256"); return FBN_ERR_UNSUPPORTED; }
   if (p_drop > 0.f && !rng && !mask_in) { fbn_set_error("bn_act: dropout needs an rng state or a mask"); return FBN_ERR_ARG; }
-  const int rpc = 16;
+  const int rpc = bn_act_rows_per_chunk();
   hipLaunchKernelGGL(bn_act_fwd2_kernel<true>, dim3(1, fbn_cdiv(B, rpc)), dim3(256), 0, (hipStream_t)stream, X, Y, B,
                      C, rpc, mean, invstd, g, b, p_drop, rng, stream_id, mask_out, mask_in, nullptr,
                      HeadArgs{hw, hbias, logits, probs, labels, loss_terms, gout, denom});
@@ -885,7 +917,7 @@ extern "C" int fbn_bn_bwd_reduce(const float* G, const float* gvec, const float*
                                  const float* Xpre, const float* mean, int B, int C, double* red_d, void* ws,
                                  void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  BnBwdSrc s{G, gvec, w, hact, scale};
+  BnBwdSrc s{G, gvec, w, hact, scale, nullptr};
   const int nch = row_chunks(B), rpc = B > 0 ? (B + nch - 1) / nch : 1;
   double* part = (double*)ws;
   hipLaunchKernelGGL(bn_bwd_partial_kernel, dim3(fbn_cdiv(C, 64), nch), dim3(256), 0, st, s, Xpre, mean, B, C, rpc, part);
@@ -900,7 +932,7 @@ extern "C" int fbn_bn_bwd_apply(const float* G, const float* gvec, const float* 
                                 int C, const double* red_d, double ntot, float* dXpre, short* dXpre16, float* dgamma,
                                 float* dbeta, float* dw, void* ws, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  BnBwdSrc s{G, gvec, w, hact, scale};
+  BnBwdSrc s{G, gvec, w, hact, scale, nullptr};
   float* coef = (float*)((double*)ws + (size_t)row_chunks(B) * 3 * C + 3 * (size_t)C);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(fbn_cdiv(C, 256)), dim3(256), 0, st, red_d, C, ntot, invstd, coef,
                      dgamma, dbeta, G ? nullptr : dw);
@@ -1086,14 +1118,20 @@ extern "C" int fbn_bn_tile_finalize(const float* part, int M, int C, double ntot
 
 extern "C" size_t fbn_bn_colpart_size(int B, int C) { return (size_t)bn_bwd_chunks(B, C) * C * sizeof(float); }
 
-extern "C" int fbn_bn_bwd_fused(const float* G, const float* gvec, const float* w, const float* hact, float scale,
-                                const float* Xpre, const float* mean, const float* invstd, const float* gamma, int B,
-                                int C, double ntot, float* dXpre, short* dXpre16, float* dgamma, float* dbeta,
-                                float* dw, float* colpart, void* ws, void* stream) {
+extern "C" int fbn_bn_bwd_fused(const float* G, const float* gvec, const float* w, const float* hact,
+                                const short* hact16, float scale, const float* Xpre, const float* mean,
+                                const float* invstd, const float* gamma, int B, int C, double ntot, float* dXpre,
+                                short* dXpre16, float* dgamma, float* dbeta, float* dw, float* colpart, void* ws,
+                                void* stream) {
   if (B <= 0) return FBN_OK;
   if (C & 3) { fbn_set_error("fbn_bn_bwd_fused: C % 4"); return FBN_ERR_ARG; }
+  if (!hact && !(hact16 && G)) {
+    fbn_set_error("fbn_bn_bwd_fused: the bf16 activation image stands in only for a matrix source");
+    return FBN_ERR_ARG;
+  }
+  if (!dXpre && !dXpre16) { fbn_set_error("fbn_bn_bwd_fused: no output"); return FBN_ERR_ARG; }
   hipStream_t st = (hipStream_t)stream;
-  BnBwdSrc s{G, gvec, w, hact, scale};
+  BnBwdSrc s{G, gvec, w, hact, scale, hact16};
   const int nch = bn_bwd_chunks(B, C), rpc = (B + nch - 1) / nch;
   double* part = (double*)ws;
   float* coef = (float*)((double*)ws + (size_t)nch * 3 * C + 3 * (size_t)C);

@@ -204,9 +204,13 @@ def bn_train_stats(h, B, C, mean, invstd, run_mean, run_var, ntot, coll: Collect
 
 
 def bn_backward(G, gvec, w, hact, scale, hpre, mean, invstd, gamma, B, C, ntot, dpre, dgamma, dbeta, dw,
-                coll: Collective, stream, dpre16=None, bias_grad=None, sums: Optional[DeferredSums] = None):
+                coll: Collective, stream, dpre16=None, bias_grad=None, sums: Optional[DeferredSums] = None,
+                hact16=None):
     """BN (+ReLU/dropout) backward; bias_grad (with sums): the preceding Linear's bias gradient
-    = column sums of dpre, finalised later by sums.flush()."""
+    = column sums of dpre, finalised later by sums.flush().
+    Single process only: hact may be None with hact16 (the bf16 activation image; a matrix source
+    G needs only its sign) and dpre may be None when dpre16 is given (bf16 mode: nothing reads the
+    f32 gradient, the bias gradient comes from the apply's column partials)."""
     dev = hpre.device
     ws = _ws(_lib.lib().fbn_bn_workspace_size(B, C), dev)
     if coll.world <= 1:
@@ -215,10 +219,11 @@ def bn_backward(G, gvec, w, hact, scale, hpre, mean, invstd, gamma, B, C, ntot, 
             nch = _lib.lib().fbn_bn_bwd_chunks(B, C)
             part = torch.empty((nch, C), dtype=torch.float32, device=dev)
             sums.add(part, nch, C, bias_grad)
-        call("fbn_bn_bwd_fused", ptr(G), ptr(gvec), ptr(w), ptr(hact), float(scale), ptr(hpre), ptr(mean),
-             ptr(invstd), ptr(gamma), B, C, float(ntot), ptr(dpre), ptr(dpre16), ptr(dgamma), ptr(dbeta), ptr(dw),
-             ptr(part), ptr(ws), stream)
+        call("fbn_bn_bwd_fused", ptr(G), ptr(gvec), ptr(w), ptr(hact), ptr(hact16), float(scale), ptr(hpre),
+             ptr(mean), ptr(invstd), ptr(gamma), B, C, float(ntot), ptr(dpre), ptr(dpre16), ptr(dgamma), ptr(dbeta),
+             ptr(dw), ptr(part), ptr(ws), stream)
         return
+    assert hact is not None and dpre is not None, "SyncBN backward reads the f32 activation and gradient"
     red = torch.empty(3 * C, dtype=torch.float64, device=dev)
     call("fbn_bn_bwd_reduce", ptr(G), ptr(gvec), ptr(w), ptr(hact), float(scale), ptr(hpre), ptr(mean), B, C,
          ptr(red), ptr(ws), stream)
@@ -246,7 +251,8 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
             loss_denom: Optional[float] = None, coll: Collective = NO_COLLECTIVE, ntot: Optional[int] = None,
             masks_out: Optional[Dict[str, torch.Tensor]] = None, acts: Optional[Dict[str, torch.Tensor]] = None,
             probe: Optional[Dict[str, list]] = None, masks_in: Optional[Dict[str, torch.Tensor]] = None,
-            after_gather=None, count_batches: bool = True, w16_ready: bool = False) -> Dict[str, torch.Tensor]:
+            after_gather=None, count_batches: bool = True, w16_ready: bool = False,
+            hooks: Optional[Dict[str, object]] = None) -> Dict[str, torch.Tensor]:
     """Run the forward; returns the activation dict (probs, logits and what backward needs).
 
     p: parameter tensors keyed like the reference state_dict (fp32, contiguous, on device).
@@ -358,6 +364,8 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
              rB=wa_remap(d), stream=st, stats=t1)
     if ev1 is not None:
         ev1[1].record()
+    if hooks and "after_mlp0" in hooks:           # trainer: side-stream work forked here
+        hooks["after_mlp0"]()
     mean1, inv1 = buf("mean1", (H1,)), buf("inv1", (H1,))
     mean2, inv2 = buf("mean2", (H2,)), buf("inv2", (H2,))
     h1 = buf("h1", (B, H1))
@@ -375,7 +383,11 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     else:
         call("fbn_bn_eval_params", ptr(p["mlp.1.running_mean"]), ptr(p["mlp.1.running_var"]), ptr(mean1), ptr(inv1),
              H1, BN_EPS, st)
-    call("fbn_bn_act_fwd", ptr(h1pre), ptr(h1), B, H1, ptr(mean1), ptr(inv1), ptr(p["mlp.1.weight"]),
+    # bf16, one process: the f32 activation has no reader (layer 2 and its weight gradient take
+    # the bf16 image, the BN backward only its sign), so it is not written
+    lean = bf and coll.world <= 1
+    a["lean_h1"] = lean
+    call("fbn_bn_act_fwd", ptr(h1pre), None if lean else ptr(h1), B, H1, ptr(mean1), ptr(inv1), ptr(p["mlp.1.weight"]),
          ptr(p["mlp.1.bias"]), float(p_drop), ptr(rng), 1, ptr(m1), ptr(mi1), ptr(h1_16), st)
     if bf:
         gemm(h1_16, w16["Wb"], h2pre, B, H2, H1, H1, H1, H2, False, True, bias=p["mlp.4.bias"], bf16=True, stream=st,
@@ -462,7 +474,8 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     bf = cfg.bf16
     w16 = a.get("w16")
     bf16_ = dict(dtype=torch.bfloat16, device=dev)
-    dh2pre = torch.empty((B, H2), **f32)
+    lean = bf and coll.world <= 1             # f32 copies of dh2pre / dh1pre have no reader
+    dh2pre = None if lean else torch.empty((B, H2), **f32)
     dh2pre16 = torch.empty((B, H2), **bf16_) if bf else None
     sums = DeferredSums()
     wg = _SideWork(side, dev)
@@ -477,11 +490,12 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     else:
         wg.run(lambda s: gemm(dh2pre, a["h1"], g["mlp.4.weight"], H2, H1, B, H2, H1, H1, True, False, stream=s))
         gemm(dh2pre, p["mlp.4.weight"], dh1, B, H1, H2, H2, H1, H1, False, False, stream=st)
-    dh1pre = torch.empty((B, H1), **f32)
+    dh1pre = None if lean else torch.empty((B, H1), **f32)
     dh1pre16 = torch.empty((B, H1), **bf16_) if bf else None
-    bn_backward(dh1, None, None, a["h1"], scale, a["h1pre"], a["mean1"], a["inv1"], p["mlp.1.weight"], B, H1, ntot,
-                dh1pre, g["mlp.1.weight"], g["mlp.1.bias"], None, coll, st, dpre16=dh1pre16,
-                bias_grad=g["mlp.0.bias"], sums=sums)
+    lean_h1 = a.get("lean_h1", False)
+    bn_backward(dh1, None, None, None if lean_h1 else a["h1"], scale, a["h1pre"], a["mean1"], a["inv1"],
+                p["mlp.1.weight"], B, H1, ntot, dh1pre, g["mlp.1.weight"], g["mlp.1.bias"], None, coll, st,
+                dpre16=dh1pre16, bias_grad=g["mlp.0.bias"], sums=sums, hact16=a["h1_16"] if lean_h1 else None)
     # weight gradient of the MLP input layer (side work), then its dgrad dc
     if a.get("split_c"):
         wg.run(lambda s: gemm_split(dh1pre16, a["Vc16"], g["mlp.0.weight"], H1, KC, B, H1, 5 * d, 21 * d, True,

@@ -33,6 +33,14 @@ from . import _lib, ops
 from ._lib import call, ptr
 from .exchange import DistCollective, RowExchange
 from .model_fibinet import build_model
+
+# single GPU, bf16: where the step's bf16 weight images are made (A/B knob) -- "main": on the
+# main stream before the row claims; "side": on the side stream beside them; "late": on the side
+# stream, captured after the claimed-row catch-up
+_W16_MODE = os.environ.get("FBN_W16", "main")
+# single GPU: the side-stream table-Adam passes (window + next-batch prefetch) forked after the
+# MLP's first GEMM instead of right after the row claims (A/B knob)
+_SIDE_AFTER_MLP0 = os.environ.get("FBN_SIDE_AFTER_MLP0", "0") == "1"
 from .schedule import OneCycle, adam_table
 
 TABLE = "item_emb.weight"
@@ -143,7 +151,7 @@ class FiBiNETTrainer:
                  stage_on_cpu: bool = False, dropout_seed: Optional[int] = None, table_adam: str = "lazy",
                  lazy_window: int = 128, defer_table_grads: bool = True, max_norm: float = 10.0,
                  optimizer: Optional[str] = None, deterministic: Optional[bool] = None,
-                 prefetch_rows: bool = True, shard: Optional[bool] = None):
+                 prefetch_rows: bool = True, shard: Optional[bool] = None, sync_bn: Optional[bool] = None):
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise RuntimeError("FiBiNETTrainer runs on a HIP device only (no CPU fallback)")
@@ -265,6 +273,15 @@ class FiBiNETTrainer:
         self.host_step = 0
         self.acts: Dict[str, torch.Tensor] = {}
         self.coll = DistCollective(world, group, stage_on_cpu)
+        # BatchNorm at N > 1.  sync_bn (default): statistics over the GLOBAL batch (one f64
+        # all-reduce per BN layer and direction) -- the single-process reference run on the
+        # global batch.  sync_bn=False: every rank normalises its own slice, which is what the
+        # reference script itself does on a multi-GPU box (nn.DataParallel, train_fibinet.py:69-70:
+        # each replica's BatchNorm1d sees its scattered slice; running statistics survive from the
+        # device-0 replica only -> here each rank keeps its own and rank 0's are checkpointed).
+        # No collective inside the forward / backward then: the captured compute is ONE segment.
+        self.sync_bn = bool(model_cfg.get("sync_bn", True) if sync_bn is None else sync_bn)
+        self.bn_coll = self.coll if self.sync_bn else ops.NO_COLLECTIVE
         self.side = _side_stream(dev)      # eager untouched pass / lazy rolling window / routing ahead
         self.xchg = RowExchange(rank, world, self.V, d, self.B, max_len, dev, group, stage_on_cpu=stage_on_cpu,
                                 rows_bf16=self.fcfg.bf16, side=self.side) if sharded else None
@@ -335,7 +352,9 @@ class FiBiNETTrainer:
 
         lazy = self.table_adam == "lazy"
 
-        def catch_up(n_ent, claim=False):
+        side_hooks = {}
+
+        def catch_up(n_ent, claim=False, before_side=None):
             # lazy table Adam: the rows claimed this step are brought to `step` Adam steps before
             # anything reads them; the rolling window (step % F; unclaimed rows, read by nothing
             # this step) replays on the side stream beside the rest of the step.  claim (single
@@ -356,6 +375,14 @@ class FiBiNETTrainer:
                      ptr(self.slot_row), n_ent, ptr(self.map), self.lazy_window, 1, ptr(self.last), ptr(self.sched),
                      ptr(self.step_dev), self.wd_g, self.beta2, self.eps, *self._pend_args(), int(self.decoupled), st)
             _events_end(ev)
+            if before_side is not None:
+                self._w16_ev = start_w16(before_side)   # the side stream: images first, then the window
+            if claim and _SIDE_AFTER_MLP0:
+                side_hooks["after_mlp0"] = side_pass     # forked after the MLP's first GEMM instead
+                return
+            side_pass()
+
+        def side_pass():
             self.side.wait_stream(main)
             ev = _events(probe, "adam_window", self.side)
             call("fbn_adam_catchup", ptr(self.E), ptr(self.Em), ptr(self.Ev), self.rows_local, d, None, 0,
@@ -363,7 +390,7 @@ class FiBiNETTrainer:
                  self.beta2, self.eps, *self._pend_args(), int(self.decoupled), self.side.cuda_stream)
             _events_end(ev, self.side)
             nb = next_batch
-            if (claim and nb is not None and self.prefetch_rows and nb["item_id"].dtype == torch.int64
+            if (self.xchg is None and nb is not None and self.prefetch_rows and nb["item_id"].dtype == torch.int64
                     and nb["item_id"].device == self.device):
                 nseq = nb.get("item_seq")
                 nL = nseq.shape[1] if nseq is not None else 0
@@ -388,15 +415,29 @@ class FiBiNETTrainer:
             _events_end(ev, self.side)
 
         w16_ev = None
-        if cfg.bf16 and self.xchg is None:
+
+        def start_w16(after=None):
             # bf16 weight images (they depend only on the weights the previous step wrote) on the side
             # stream, beside the row claims and the claimed-row catch-up
-            self.side.wait_stream(main)
+            if after is None:
+                self.side.wait_stream(main)
+            else:
+                self.side.wait_event(after)
             with torch.cuda.stream(self.side):
                 self.acts["w16"] = ops.bf16_weights(self.p, d, self.acts, self.side.cuda_stream,
                                                     x=batch["item_emb_d128"])
-            w16_ev = torch.cuda.Event()
-            w16_ev.record(self.side)
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+            return ev
+
+        w16_main = cfg.bf16 and self.xchg is None and _W16_MODE == "main"
+        w16_late = cfg.bf16 and self.xchg is None and lazy and _W16_MODE == "late"
+        if w16_main:
+            # on the main stream ahead of the claims: a cross-queue wait inside a replayed graph
+            # costs ~10 us, about what the conversion itself takes
+            self.acts["w16"] = ops.bf16_weights(self.p, d, self.acts, st, x=batch["item_emb_d128"])
+        elif cfg.bf16 and self.xchg is None and not w16_late:
+            w16_ev = start_w16()
         if self.xchg is not None:
             rows = self.xchg.forward(batch["item_id"], seq, self.E, {"map": self.map, "slot_row": self.slot_row},
                                      self.err, before_gather=catch_up if lazy else None)
@@ -415,7 +456,16 @@ class FiBiNETTrainer:
                     _events_end(ev, self.side)
                     self.xchg.next_lids.record_stream(self.side)
         elif lazy:
-            catch_up(B * (L + 1), claim=True)
+            if w16_late:
+                # captured after the claimed-row catch-up's launch, so a graph replay starts the
+                # catch-up first; the images follow on the side stream, still beside it (they wait
+                # only for what preceded the catch-up)
+                step_start = torch.cuda.Event()
+                step_start.record(main)
+                catch_up(B * (L + 1), claim=True, before_side=step_start)
+                w16_ev = self._w16_ev
+            else:
+                catch_up(B * (L + 1), claim=True)
         else:
             call("fbn_claim_rows", ptr(batch["item_id"]), ptr(seq) if L else None, B, L, self.V, ptr(self.map),
                  ptr(self.slot_row), ptr(self.dup), ptr(self.hasdup), st)
@@ -428,14 +478,16 @@ class FiBiNETTrainer:
             graphed = self._sharded_compute(batch, labels, pos, cfg, ntot, B, L)
         if not graphed:
             a = ops.forward(self.p, batch, cfg, self.rng, table_rows=rows, pos=pos, err=self.err, labels=labels,
-                            w16_ready=w16_ev is not None,
-                            loss_denom=float(ntot), coll=self.coll, ntot=ntot, acts=self.acts, masks_out=masks_out,
+                            w16_ready=w16_ev is not None or w16_main,
+                            loss_denom=float(ntot), coll=self.bn_coll, ntot=self._bn_n(ntot, B), acts=self.acts,
+                            masks_out=masks_out,
                             probe=probe, count_batches=False,     # num_batches_tracked: fbn_step_end
-                            after_gather=start_untouched_adam if self.table_adam == "eager" else None)
+                            after_gather=start_untouched_adam if self.table_adam == "eager" else None,
+                            hooks=side_hooks)
             sendbuf = self.xchg.make_sendbuf() if self.xchg is not None else None
             ops.backward(self.p, batch, a, a["gout"], self.g, cfg, gvec=self.gvec if self.xchg is None else None,
                          gnorm=self.gnorm if self.xchg is None else None,
-                         pos=pos, sendbuf=sendbuf, coll=self.coll, ntot=ntot,
+                         pos=pos, sendbuf=sendbuf, coll=self.bn_coll, ntot=self._bn_n(ntot, B),
                          extra_sums=[(a["loss_terms"], B, 1, self.loss, 1.0 / ntot)], probe=probe)
         if self.xchg is None:
             # single GPU: per-sample vectors; entry e = b*(L+1)+t; duplicates -> extra[claimer]
@@ -540,20 +592,26 @@ class FiBiNETTrainer:
         self._sg = None
         torch.cuda.synchronize(self.device)
         seg = _Segments(self.coll, torch.cuda.graph_pool_handle())
+        bn = seg if self.sync_bn else ops.NO_COLLECTIVE      # local BN: one segment
         cap = torch.cuda.Stream(device=self.device)
         cap.wait_stream(main)
         with torch.cuda.stream(cap):
             seg.begin()
             a = ops.forward(self.p, sb, cfg, self.rng, table_rows=x.rows_buf, pos=sp, err=self.err, labels=sl,
-                            loss_denom=float(ntot), coll=seg, ntot=ntot, acts=self.acts, count_batches=False)
-            ops.backward(self.p, sb, a, a["gout"], self.g, cfg, pos=sp, sendbuf=x.send_buf, coll=seg, ntot=ntot,
-                         extra_sums=[(a["loss_terms"], B, 1, self.loss, 1.0 / ntot)])
+                            loss_denom=float(ntot), coll=bn, ntot=self._bn_n(ntot, B), acts=self.acts,
+                            count_batches=False)
+            ops.backward(self.p, sb, a, a["gout"], self.g, cfg, pos=sp, sendbuf=x.send_buf, coll=bn,
+                         ntot=self._bn_n(ntot, B), extra_sums=[(a["loss_terms"], B, 1, self.loss, 1.0 / ntot)])
             seg.end()
         main.wait_stream(cap)
         # every tensor the segments address stays referenced as long as they live
         self._sg = {"key": key, "seg": seg, "batch": sb, "labels": sl, "pos": sp, "a": a, "acts": dict(self.acts),
                     "bufs": (x.rows_buf, x.send_buf)}
         return self._sg
+
+    def _bn_n(self, ntot: int, B: int) -> int:
+        """Samples one BatchNorm normalises over: the global batch (SyncBN) or this rank's slice."""
+        return ntot if self.sync_bn else B
 
     def _pend_args(self):
         """(pend, ring, coef_hist, ring_stride, ring_n) of the deferred table gradients (NULLs when off)."""

@@ -141,6 +141,7 @@ int fbn_bn_tile_finalize(const float* part, int M, int C, double ntot, float* me
                          float* run_var, float momentum, float eps, int update_running, void* stream);
 int fbn_bn_eval_params(const float* run_mean, const float* run_var, float* mean, float* invstd, int C, float eps,
                        void* stream);
+/* Y (f32) or Y16 (bf16) may be null (not both). */
 int fbn_bn_act_fwd(const float* X, float* Y, int B, int C, const float* mean, const float* invstd, const float* g,
                    const float* b, float p_drop, const unsigned long long* rng, unsigned stream_id,
                    unsigned char* mask_out, const unsigned char* mask_in, short* Y16, void* stream);
@@ -166,9 +167,11 @@ size_t fbn_bn_colpart_size(int B, int C);
 int fbn_row_chunks(int B);
 /* row chunks of fbn_bn_bwd_fused (its colpart is [fbn_bn_bwd_chunks(B, C)][C]) */
 int fbn_bn_bwd_chunks(int B, int C);
-int fbn_bn_bwd_fused(const float* G, const float* gvec, const float* w, const float* hact, float scale,
-                     const float* Xpre, const float* mean, const float* invstd, const float* gamma, int B, int C,
-                     double ntot, float* dXpre, short* dXpre16, float* dgamma, float* dbeta, float* dw,
+/* hact16 (bf16 image of the activation) may replace hact (null) for a matrix source G: the ReLU /
+ * dropout mask needs only the sign.  dXpre or dXpre16 may be null (not both). */
+int fbn_bn_bwd_fused(const float* G, const float* gvec, const float* w, const float* hact, const short* hact16,
+                     float scale, const float* Xpre, const float* mean, const float* invstd, const float* gamma, int B,
+                     int C, double ntot, float* dXpre, short* dXpre16, float* dgamma, float* dbeta, float* dw,
                      float* colpart, void* ws, void* stream);
 /* bf16 weight images: jobs = host array of n <= 8 records
  * {const float* src; short* dst; int rows, cols, ld, trans, seg, off0, off1;}

@@ -243,12 +243,32 @@ class OracleTrainer:
             self.Em[rows] = m
             self.Ev[rows] = v
 
-    def step(self, batch, labels, masks=None) -> Tuple[float, torch.Tensor]:
+    def _replicated_forward(self, batch, replicas: int) -> torch.Tensor:
+        """nn.DataParallel's forward over `replicas` devices (train_fibinet.py:69-70): the batch is
+        scattered in equal contiguous slices, each replica's BatchNorm1d normalises its own slice,
+        the outputs are gathered in order; running statistics (and num_batches_tracked) keep
+        only the device-0 replica's update -- the other replicas update broadcast copies."""
+        n = next(iter(batch.values())).shape[0]
+        per = n // replicas
+        bufs = {k: v.clone() for k, v in self.model.named_buffers()}
+        outs = [None] * replicas
+        for r in list(range(1, replicas)) + [0]:
+            if r == 0:
+                with torch.no_grad():
+                    for k, v in self.model.named_buffers():
+                        v.copy_(bufs[k])
+            outs[r] = self.model({k: v[r * per:(r + 1) * per] for k, v in batch.items()})
+        return torch.cat(outs)
+
+    def step(self, batch, labels, masks=None, replicas: int = 1) -> Tuple[float, torch.Tensor]:
         self.model.train()
         self.opt.zero_grad()
         if self.sparse_table:
             self.model.item_emb.weight.grad = None
-        y = self.model(batch, masks=masks)
+        if replicas > 1:
+            y = self._replicated_forward(batch, replicas)
+        else:
+            y = self.model(batch, masks=masks)
         loss = self.loss_fn(y, labels)
         loss.backward()
         self.last_total_norm = float(torch.nn.utils.clip_grad_norm_(self.model.parameters(), max_norm=self.max_norm))

@@ -30,7 +30,7 @@ def _cfg(D=16, dtype="fp32"):
     return {"embedding_dim": D, "vocab_size": V, "honour_config": True, "net_dropout": 0.0, "compute_dtype": dtype}
 
 
-def _worker(rank, world, port, q, D, dtype):
+def _worker(rank, world, port, q, D, dtype, sync_bn=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -41,7 +41,7 @@ def _worker(rank, world, port, q, D, dtype):
         torch.manual_seed(0)
         init = build_model(None, _cfg(D), honour_config=True).state_dict()
         tr = FiBiNETTrainer(_cfg(D, dtype), total_steps=TOTAL, batch_size=B // world, device=dev, rank=rank, world=world,
-                            init_state=init, stage_on_cpu=True)
+                            init_state=init, stage_on_cpu=True, sync_bn=sync_bn)
         losses = []
         per = B // world
         bs = []
@@ -67,10 +67,15 @@ def _worker(rank, world, port, q, D, dtype):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,D,dtype", [(2, 16, "fp32"), (4, 16, "fp32"), (2, 128, "bf16")])
-def test_sharded_trainer_equals_single_process_reference(hip_device, world, D, dtype, tmp_path):
+@pytest.mark.parametrize("world,D,dtype,sync_bn", [(2, 16, "fp32", True), (4, 16, "fp32", True),
+                                                   (2, 128, "bf16", True), (2, 16, "fp32", False),
+                                                   (4, 16, "fp32", False), (2, 128, "bf16", False)])
+def test_sharded_trainer_equals_single_process_reference(hip_device, world, D, dtype, sync_bn, tmp_path):
     """fp32: the bars above.  bf16 (C3's mode, bf16 GEMM operands and bf16 forward rows on the
-    wire): losses within 2 %, rank 0's eval probabilities within 1e-2 of the fp32 oracle."""
+    wire): losses within 2 %, rank 0's eval probabilities within 1e-2 of the fp32 oracle.
+    sync_bn=False: per-rank BatchNorm against the oracle run as nn.DataParallel over `world`
+    replicas (per-slice statistics, device-0 running statistics) -- the reference script's own
+    multi-GPU semantics."""
     from ctr_recommendation_amd.data import make_batch
     from oracle.fibinet_oracle import OracleTrainer, build_model
     out = str(tmp_path / "rank0.pt")
@@ -78,7 +83,7 @@ def test_sharded_trainer_equals_single_process_reference(hip_device, world, D, d
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, D, dtype)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, D, dtype, sync_bn)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=600) for _ in range(world)]
@@ -92,7 +97,7 @@ def test_sharded_trainer_equals_single_process_reference(hip_device, world, D, d
     otr = OracleTrainer(ref, total_steps=TOTAL)
     for s in range(STEPS):
         b, y = make_batch(200 + s, B, V)
-        lr_, _ = otr.step(b, y)
+        lr_, _ = otr.step(b, y, replicas=1 if sync_bn else world)
         if dtype == "bf16":
             assert abs(got["losses"][s] - lr_) <= 0.02 * lr_, (s, got["losses"][s], lr_)
         else:
