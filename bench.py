@@ -65,6 +65,10 @@ def parse():
                     help="N = 1: no ahead-of-time catch-up of the next batch's rows (fbn_adam_prefetch)")
     ap.add_argument("--prime", type=int, default=-1,
                     help="untimed priming steps before the warm-up (default: top the warm-up up to 2F)")
+    ap.add_argument("--bn", default="local", choices=["local", "sync"],
+                    help="N > 1 BatchNorm statistics: 'local' = per GPU, what the reference script does on a "
+                         "multi-GPU box (nn.DataParallel, train_fibinet.py:69-70); 'sync' = over the global "
+                         "batch (parity with one process on the global batch; 4 all-reduces per step)")
     ap.add_argument("--no-fp32", dest="also_fp32", action="store_false",
                     help="skip the second (fp32) C3 measurement embedded in the line")
     return ap.parse_args()
@@ -176,7 +180,7 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
     init = _initial_state(cfg, V, world, rank, dev)
     tr = FiBiNETTrainer(cfg, total_steps=total, batch_size=B, device=dev, rank=rank, world=world,
                         init_state=init, stage_on_cpu=rehearsal, lazy_window=F, prefetch_rows=args.prefetch,
-                        shard=sharded)
+                        shard=sharded, sync_bn=args.bn == "sync")
     del init
     batches = make_device_batches(nb, B, V, L, dev, seed=2025 + rank, zipf=args.zipf)
     graphs = []
@@ -389,7 +393,10 @@ def main():
                        "model": "MM_FiBiNET", "global_batch": B * world, "seq_len": r["L"],
                        "item_rows": r["V"], "item_rows_per_gpu": r["rows_local"], "emb_dim": r["d"],
                        "parallelism": f"row-shard{world}" if world > 1 or FORCE_SHARD else "single",
-                       "hipgraph": r["graphs"], **({"rehearsal": backend} if rehearsal else {})},
+                       "hipgraph": r["graphs"], **({"rehearsal": backend} if rehearsal else {}),
+                       **({"batchnorm": "per-GPU statistics (nn.DataParallel semantics, train_fibinet.py:69-70)"
+                           if args.bn == "local" else "SyncBN (global-batch statistics)"}
+                          if world > 1 or FORCE_SHARD else {})},
             "host_enqueue_ms_per_step": round(r["t_host"] / K * 1e3, 4),
             **({"host_blocked_ms_per_step": round(r["t_wait"] / K * 1e3, 4)} if r["t_wait"] else {}),
             "roofline": r["roofline"],

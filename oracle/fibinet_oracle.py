@@ -250,14 +250,18 @@ class OracleTrainer:
         only the device-0 replica's update -- the other replicas update broadcast copies."""
         n = next(iter(batch.values())).shape[0]
         per = n // replicas
-        bufs = {k: v.clone() for k, v in self.model.named_buffers()}
+        bns = [mod for mod in self.model.modules() if isinstance(mod, nn.BatchNorm1d)]
+        keep = [(mod, dict(mod._buffers)) for mod in bns]
         outs = [None] * replicas
-        for r in list(range(1, replicas)) + [0]:
-            if r == 0:
-                with torch.no_grad():
-                    for k, v in self.model.named_buffers():
-                        v.copy_(bufs[k])
+        for r in range(1, replicas):
+            for mod, b in keep:                 # a replica's own copies (autograd keeps them)
+                for name, t in b.items():
+                    setattr(mod, name, t.clone())
             outs[r] = self.model({k: v[r * per:(r + 1) * per] for k, v in batch.items()})
+        for mod, b in keep:
+            for name, t in b.items():
+                setattr(mod, name, t)
+        outs[0] = self.model({k: v[:per] for k, v in batch.items()})
         return torch.cat(outs)
 
     def step(self, batch, labels, masks=None, replicas: int = 1) -> Tuple[float, torch.Tensor]:

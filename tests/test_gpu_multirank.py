@@ -15,7 +15,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
-V, B, STEPS, TOTAL = 3001, 128, 3, 20
+V, B, STEPS, TOTAL = 3001, int(os.environ.get("FBN_TEST_B", "128")), 3, 20
 
 
 def _port():
@@ -42,6 +42,8 @@ def _worker(rank, world, port, q, D, dtype, sync_bn=True):
         init = build_model(None, _cfg(D), honour_config=True).state_dict()
         tr = FiBiNETTrainer(_cfg(D, dtype), total_steps=TOTAL, batch_size=B // world, device=dev, rank=rank, world=world,
                             init_state=init, stage_on_cpu=True, sync_bn=sync_bn)
+        if os.environ.get("FBN_TEST_EAGER") == "1":
+            tr.shard_graph = False
         losses = []
         per = B // world
         bs = []
@@ -94,9 +96,17 @@ def test_sharded_trainer_equals_single_process_reference(hip_device, world, D, d
     torch.manual_seed(0)
     ref = build_model(None, _cfg(D), honour_config=True)
     init = {k: v.clone() for k, v in ref.state_dict().items()}
+    # per-GPU BatchNorm normalises slices of only B / world samples: on this seed a 32-sample slice
+    # has near-constant columns, where the fp32 CPU oracle itself moves 1.1 % away from its float64
+    # run -- the per-slice cases are held to the float64 oracle
+    f64 = not sync_bn
+    if f64:
+        ref = ref.double()
+    cast = (lambda t: t.double() if t.is_floating_point() else t) if f64 else (lambda t: t)
     otr = OracleTrainer(ref, total_steps=TOTAL)
     for s in range(STEPS):
         b, y = make_batch(200 + s, B, V)
+        b, y = {k: cast(v) for k, v in b.items()}, cast(y)
         lr_, _ = otr.step(b, y, replicas=1 if sync_bn else world)
         if dtype == "bf16":
             assert abs(got["losses"][s] - lr_) <= 0.02 * lr_, (s, got["losses"][s], lr_)
@@ -105,22 +115,29 @@ def test_sharded_trainer_equals_single_process_reference(hip_device, world, D, d
     ref.eval()
     be, _ = make_batch(777, B, V)
     with torch.no_grad():
-        pr = ref(be)[:B // world]
+        pr = ref({k: cast(v) for k, v in be.items()})[:B // world].float()
     assert (got["pe"] - pr).abs().max().item() < (1e-2 if dtype == "bf16" else 2e-3)
     if dtype == "bf16":
         return
     rsd = ref.state_dict()
+    bad = []
     for k, v in rsd.items():
         h = got["sd"][k]
         if v.dtype == torch.int64:
-            assert torch.equal(h, v), k
+            if not torch.equal(h, v):
+                bad.append((k, h.tolist(), v.tolist()))
             continue
         if "running" in k:
-            assert (h - v).abs().max().item() < 1e-4 * max(1.0, v.abs().max().item()), k
+            dev_ = (h - v).abs().max().item()
+            if dev_ >= 1e-4 * max(1.0, v.abs().max().item()):
+                bad.append((k, dev_))
             continue
         dr, dh = (v - init[k]).double(), (h - init[k]).double()
         tol = 5e-2 if k in ("mlp.0.bias", "mlp.4.bias") else 1e-3
-        assert (dh - dr).norm().item() <= tol * dr.norm().item() + 1e-9, k
+        rel = (dh - dr).norm().item() / (dr.norm().item() + 1e-30)
+        if rel > tol:
+            bad.append((k, rel))
+    assert not bad, bad
 
 
 def _prefetch_worker(rank, world, port, q, out):
