@@ -144,7 +144,7 @@ class RowExchange:
         # the prepared routing is used only for the very tensors it was computed from
         return (item.data_ptr(), item.shape[0], 0 if seq is None else seq.data_ptr(), 0 if seq is None else seq.shape[1])
 
-    def prepare(self, item, seq, err, send_rows: bool = False) -> None:
+    def prepare(self, item, seq, err, send_rows: bool = False, after=None) -> None:
         """Route the NEXT step's batch now, on a side stream (HIP device only), and deliver it to the
         owners as ONE equal-split all-to-all of the padded routing (fbn_pad_routes: each
         destination's ids padded to cap, its count in the last slot): the owner recovers the counts
@@ -159,7 +159,12 @@ class RowExchange:
             return
         st = self.sets[1 - self.cur]
         main = torch.cuda.current_stream(item.device)
-        self.side.wait_stream(main)                 # the ids and the buffer set are free
+        # the ids and the buffer set are free: after everything on the main stream so far, or after
+        # `after` (an event the caller recorded once this step's row exchange was enqueued)
+        if after is None:
+            self.side.wait_stream(main)
+        else:
+            self.side.wait_event(after)
         B = item.shape[0]
         cap = B * (1 + (0 if seq is None else seq.shape[1]))
         with torch.cuda.stream(self.side):

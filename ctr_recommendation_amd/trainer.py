@@ -41,6 +41,8 @@ _W16_MODE = os.environ.get("FBN_W16", "main")
 # single GPU: the side-stream table-Adam passes (window + next-batch prefetch) forked after the
 # MLP's first GEMM instead of right after the row claims (A/B knob)
 _SIDE_AFTER_MLP0 = os.environ.get("FBN_SIDE_AFTER_MLP0", "0") == "1"
+# N > 1: the next batch's routing enqueued after this step's compute (A/B knob)
+_ROUTE_AFTER_COMPUTE = os.environ.get("FBN_ROUTE_AFTER_COMPUTE", "1") == "1"
 from .schedule import OneCycle, adam_table
 
 TABLE = "item_emb.weight"
@@ -442,9 +444,14 @@ class FiBiNETTrainer:
             rows = self.xchg.forward(batch["item_id"], seq, self.E, {"map": self.map, "slot_row": self.slot_row},
                                      self.err, before_gather=catch_up if lazy else None)
             pos = self.xchg.cur_pos
-            if next_batch is not None:
+            fwd_ev = torch.cuda.Event()
+            fwd_ev.record(main)
+        route_ahead = None
+        if self.xchg is not None and next_batch is not None:
+            def route_ahead():
                 own = self.prefetch_owner and lazy
-                self.xchg.prepare(next_batch["item_id"], next_batch.get("item_seq"), self.err, send_rows=own)
+                self.xchg.prepare(next_batch["item_id"], next_batch.get("item_seq"), self.err, send_rows=own,
+                                  after=fwd_ev)
                 if own and self.xchg.next_lids is not None:
                     # after this step's claims and window (self.side), once the requests arrived
                     self.side.wait_stream(self.xchg.side)
@@ -455,7 +462,10 @@ class FiBiNETTrainer:
                          self.eps, *self._pend_args(), int(self.decoupled), self.side.cuda_stream)
                     _events_end(ev, self.side)
                     self.xchg.next_lids.record_stream(self.side)
-        elif lazy:
+            if not _ROUTE_AFTER_COMPUTE:
+                route_ahead()
+                route_ahead = None
+        elif self.xchg is None and lazy:
             if w16_late:
                 # captured after the claimed-row catch-up's launch, so a graph replay starts the
                 # catch-up first; the images follow on the side stream, still beside it (they wait
@@ -466,7 +476,7 @@ class FiBiNETTrainer:
                 w16_ev = self._w16_ev
             else:
                 catch_up(B * (L + 1), claim=True)
-        else:
+        elif self.xchg is None:
             call("fbn_claim_rows", ptr(batch["item_id"]), ptr(seq) if L else None, B, L, self.V, ptr(self.map),
                  ptr(self.slot_row), ptr(self.dup), ptr(self.hasdup), st)
         if w16_ev is not None:
@@ -489,6 +499,12 @@ class FiBiNETTrainer:
                          gnorm=self.gnorm if self.xchg is None else None,
                          pos=pos, sendbuf=sendbuf, coll=self.bn_coll, ntot=self._bn_n(ntot, B),
                          extra_sums=[(a["loss_terms"], B, 1, self.loss, 1.0 / ntot)], probe=probe)
+        if route_ahead is not None:
+            # the host enqueues the next batch's routing (and the owner-side prefetch) only after
+            # this step's compute: on the GPU it still starts right after this step's row exchange
+            # (it waits on fwd_ev only), but the compute no longer waits for the host to get
+            # through ~10 side-stream launches and a collective first
+            route_ahead()
         if self.xchg is None:
             # single GPU: per-sample vectors; entry e = b*(L+1)+t; duplicates -> extra[claimer]
             n_ent = B * (L + 1)
