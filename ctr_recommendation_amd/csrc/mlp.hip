@@ -1031,9 +1031,17 @@ __global__ void __launch_bounds__(256) convert_bf16_kernel(ConvJobs jobs, int nj
     const int j = j0 + tx;
     if (j < J.cols) {
       const int b = j + (j < J.seg ? J.off0 : J.off1);
-      for (int r = ty; r < 64; r += 4) {
-        const int i = i0 + r;
-        if (i < J.rows) J.dst[(size_t)i * J.cols + j] = f2bf(J.src[(size_t)i * J.ld + b]);
+      // all 16 loads in flight before the first store (the loop is unrolled)
+      float val[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int i = i0 + ty + 4 * k;
+        val[k] = i < J.rows ? J.src[(size_t)i * J.ld + b] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int i = i0 + ty + 4 * k;
+        if (i < J.rows) J.dst[(size_t)i * J.cols + j] = f2bf(val[k]);
       }
     }
     return;
@@ -1042,6 +1050,7 @@ __global__ void __launch_bounds__(256) convert_bf16_kernel(ConvJobs jobs, int nj
   {
     const int i = i0 + tx;
     const int b = i + (i < J.seg ? J.off0 : J.off1);
+#pragma unroll
     for (int r = ty; r < 64; r += 4) {
       const int j = j0 + r;
       tile[r][tx] = (i < J.rows && j < J.cols) ? J.src[(size_t)j * J.ld + b] : 0.f;
@@ -1049,6 +1058,7 @@ __global__ void __launch_bounds__(256) convert_bf16_kernel(ConvJobs jobs, int nj
   }
   __syncthreads();
   const int j = j0 + tx;
+#pragma unroll
   for (int r = ty; r < 64; r += 4) {
     const int i = i0 + r;
     if (i < J.rows && j < J.cols) J.dst[(size_t)i * J.cols + j] = f2bf(tile[tx][r]);
