@@ -104,6 +104,7 @@ class RowExchange:
         # prefix): fixed addresses, so the trainer's compute between the exchanges can be a hipGraph
         self.rows_buf = None
         self.send_buf = None
+        self._pending = None        # gradient-row all-to-all issued by backward_start()
 
     @property
     def rows_lo(self) -> int:
@@ -250,15 +251,33 @@ class RowExchange:
     def backward(self, sendbuf: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Returns the owner's received gradient rows [n_recv, d] f32 (entry i <-> recv_ids[i]),
         written into `out` (>= n_recv rows, e.g. a deferred-gradient ring slot) when given."""
+        self.backward_start(sendbuf, out)
+        return self.backward_finish()
+
+    def backward_start(self, sendbuf: torch.Tensor, out: Optional[torch.Tensor] = None) -> None:
+        """Issue the gradient-row all-to-all now, asynchronously on the process group's own stream
+        (the caller's stream goes on with other work); backward_finish() makes the caller's stream
+        wait for it and widens bf16 wire rows."""
         n_recv = sum(self.recv_counts)
         grad = out[:n_recv] if out is not None else \
             torch.empty((n_recv, self.d), dtype=torch.float32, device=sendbuf.device)
-        if sendbuf.dtype == torch.float32:
-            self._a2a(grad, sendbuf, self.recv_counts, self.send_counts)
-            return grad
-        wire = torch.empty((n_recv, self.d), dtype=sendbuf.dtype, device=sendbuf.device)
-        self._a2a(wire, sendbuf, self.recv_counts, self.send_counts)
-        self.k.widen(wire, grad)
+        wire = grad if sendbuf.dtype == torch.float32 else \
+            torch.empty((n_recv, self.d), dtype=sendbuf.dtype, device=sendbuf.device)
+        work = None
+        if self.stage_on_cpu:
+            self._a2a(wire, sendbuf, self.recv_counts, self.send_counts)
+        else:
+            work = dist.all_to_all_single(wire, sendbuf, self.recv_counts, self.send_counts, group=self.group,
+                                          async_op=True)
+        self._pending = (work, wire, grad)
+
+    def backward_finish(self) -> torch.Tensor:
+        work, wire, grad = self._pending
+        self._pending = None
+        if work is not None:
+            work.wait()
+        if wire is not grad:
+            self.k.widen(wire, grad)
         return grad
 
 

@@ -448,7 +448,7 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
              pos: Optional[torch.Tensor] = None,
              sendbuf: Optional[torch.Tensor] = None, coll: Collective = NO_COLLECTIVE,
              ntot: Optional[int] = None, extra_sums=(), side: Optional["torch.cuda.Stream"] = None,
-             probe: Optional[Dict[str, list]] = None) -> None:
+             probe: Optional[Dict[str, list]] = None, hooks: Optional[Dict[str, object]] = None) -> None:
     """Backward from dL/dlogit (gout [B]) into the gradient buffers ``g`` (same keys as ``p``).
 
     table_grad: dense [V, d] (drop-in, accumulated by atomics); or gvec [B, 2, d] (native
@@ -573,6 +573,8 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
          int(sendbuf is not None and sendbuf.dtype == torch.bfloat16), B, Lr, d, st)
     if evb is not None:
         evb[1].record()
+    if hooks and "after_fields_bwd" in hooks:     # N > 1: the gradient rows are complete -> exchange
+        hooks["after_fields_bwd"]()
     if bf:
         wg.run(lambda s: gemm(dhmm16, w16["x"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True, False, stream=s))
     else:

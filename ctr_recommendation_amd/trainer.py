@@ -43,6 +43,11 @@ _W16_MODE = os.environ.get("FBN_W16", "main")
 _SIDE_AFTER_MLP0 = os.environ.get("FBN_SIDE_AFTER_MLP0", "0") == "1"
 # N > 1: the next batch's routing enqueued after this step's compute (A/B knob)
 _ROUTE_AFTER_COMPUTE = os.environ.get("FBN_ROUTE_AFTER_COMPUTE", "1") == "1"
+# N > 1 (RCCL): the gradient-row all-to-all issued right after the fields backward -- default on
+# for world > 1; at world = 1 (one-rank rehearsal) the "all-to-all" is a local copy that only
+# competes with the compute for HBM (0.68-0.71 vs 0.68 ms/step), so default off there (A/B knob:
+# FBN_EARLY_GRAD_XCHG=0 / 1)
+_EARLY_GRAD_XCHG = os.environ.get("FBN_EARLY_GRAD_XCHG")
 from .schedule import OneCycle, adam_table
 
 TABLE = "item_emb.weight"
@@ -110,6 +115,12 @@ class _Segments:
         self.prog += [("graph", self.cur), ("allreduce", t)]
         self.begin()
 
+    def call(self, fn) -> None:
+        """Close the segment; a replay runs fn() (host code: e.g. an asynchronous collective) here."""
+        self.cur.capture_end()
+        self.prog += [("graph", self.cur), ("call", fn)]
+        self.begin()
+
     def end(self) -> None:
         self.cur.capture_end()
         self.prog.append(("graph", self.cur))
@@ -119,6 +130,8 @@ class _Segments:
         for kind, x in self.prog:
             if kind == "graph":
                 x.replay()
+            elif kind == "call":
+                x()
             else:
                 self.base.allreduce_(x)
 
@@ -288,6 +301,7 @@ class FiBiNETTrainer:
         self.xchg = RowExchange(rank, world, self.V, d, self.B, max_len, dev, group, stage_on_cpu=stage_on_cpu,
                                 rows_bf16=self.fcfg.bf16, side=self.side) if sharded else None
         self.stage_on_cpu = stage_on_cpu
+        self.early_grad_xchg = (world > 1) if _EARLY_GRAD_XCHG is None else _EARLY_GRAD_XCHG == "1"
         # item-table Adam: "lazy" (default) replays the zero-gradient steps of a row when the row
         # is next claimed or its rolling window comes round (bit-identical to eager; see
         # fbn_adam_catchup) -- "eager" streams every untouched row each step on a side stream (the
@@ -498,7 +512,8 @@ class FiBiNETTrainer:
             ops.backward(self.p, batch, a, a["gout"], self.g, cfg, gvec=self.gvec if self.xchg is None else None,
                          gnorm=self.gnorm if self.xchg is None else None,
                          pos=pos, sendbuf=sendbuf, coll=self.bn_coll, ntot=self._bn_n(ntot, B),
-                         extra_sums=[(a["loss_terms"], B, 1, self.loss, 1.0 / ntot)], probe=probe)
+                         extra_sums=[(a["loss_terms"], B, 1, self.loss, 1.0 / ntot)], probe=probe,
+                         hooks={"after_fields_bwd": self._grad_xchg_start} if self._early_grad_xchg() else None)
         if route_ahead is not None:
             # the host enqueues the next batch's routing (and the owner-side prefetch) only after
             # this step's compute: on the GPU it still starts right after this step's row exchange
@@ -522,11 +537,12 @@ class FiBiNETTrainer:
         else:
             # owner: one received row per entry -- straight into this step's deferred-gradient ring
             # slot when it fits, else a buffer of its own and the rows applied at the step end
-            slot = None
-            if self.deferred and sum(self.xchg.recv_counts) <= self.ring_cap:
-                slot = self.ring[self.host_step % self.ring_n]
+            slot = self._grad_slot()
             defer_now = slot is not None
-            grows = self.xchg.backward(sendbuf, out=slot)
+            if self.xchg._pending is not None:      # issued right after the fields backward
+                grows = self.xchg.backward_finish()
+            else:
+                grows = self.xchg.backward(sendbuf, out=slot)
             n_ent = grows.shape[0]
             gsrc = (grows, None, 1)
             call("fbn_sparse_fixup", None, None, ptr(self.xchg.recv_ids), n_ent, 0, self.V, self.rank, ptr(self.map),
@@ -616,14 +632,32 @@ class FiBiNETTrainer:
             a = ops.forward(self.p, sb, cfg, self.rng, table_rows=x.rows_buf, pos=sp, err=self.err, labels=sl,
                             loss_denom=float(ntot), coll=bn, ntot=self._bn_n(ntot, B), acts=self.acts,
                             count_batches=False)
+            hooks = {"after_fields_bwd": lambda: seg.call(self._grad_xchg_start)} if self._early_grad_xchg() else None
             ops.backward(self.p, sb, a, a["gout"], self.g, cfg, pos=sp, sendbuf=x.send_buf, coll=bn,
-                         ntot=self._bn_n(ntot, B), extra_sums=[(a["loss_terms"], B, 1, self.loss, 1.0 / ntot)])
+                         ntot=self._bn_n(ntot, B), extra_sums=[(a["loss_terms"], B, 1, self.loss, 1.0 / ntot)],
+                         hooks=hooks)
             seg.end()
         main.wait_stream(cap)
         # every tensor the segments address stays referenced as long as they live
         self._sg = {"key": key, "seg": seg, "batch": sb, "labels": sl, "pos": sp, "a": a, "acts": dict(self.acts),
                     "bufs": (x.rows_buf, x.send_buf)}
         return self._sg
+
+    def _grad_slot(self):
+        """This step's deferred-gradient ring slot, or None (rows applied at once)."""
+        if self.deferred and sum(self.xchg.recv_counts) <= self.ring_cap:
+            return self.ring[self.host_step % self.ring_n]
+        return None
+
+    def _early_grad_xchg(self) -> bool:
+        return self.early_grad_xchg and self.xchg is not None and not self.stage_on_cpu
+
+    def _grad_xchg_start(self) -> None:
+        """N > 1: the per-entry gradient rows are complete once the fields backward has run: their
+        all-to-all starts there, on the process group's stream, beside the rest of the backward
+        (the last parameter reductions and the mm_proj weight gradient)."""
+        x = self.xchg
+        x.backward_start(x.send_buf[:sum(x.send_counts)], out=self._grad_slot())
 
     def _bn_n(self, ntot: int, B: int) -> int:
         """Samples one BatchNorm normalises over: the global batch (SyncBN) or this rank's slice."""
