@@ -119,6 +119,7 @@ constexpr int PJ[10] = {1, 2, 3, 4, 2, 3, 4, 3, 4, 4};
 template <int D>
 __global__ void __launch_bounds__(2 * D) bilinear_fwd_kernel(const short* __restrict__ V16, const short* __restrict__ WT16,
                                                             short* __restrict__ c, int B, int ldc) {
+  FBN_MAIN_PRIO();
   constexpr int NT = 2 * D;   // D/32 waves
   __shared__ __attribute__((aligned(16))) short sV[5 * TS * D];
   __shared__ __attribute__((aligned(16))) short sW[D * D];
@@ -159,6 +160,7 @@ __global__ void __launch_bounds__(2 * D, 2) bilinear_bwd_kernel(const void* __re
                                                             const short* __restrict__ V16, const short* __restrict__ WT16,
                                                             const short* __restrict__ W16, float* __restrict__ dV,
                                                             short* __restrict__ dU16, int B) {
+  FBN_MAIN_PRIO();
   constexpr int NT = 2 * D;
   __shared__ __attribute__((aligned(16))) short sV[5 * TS * D];   // V tile, then dU tile
   __shared__ __attribute__((aligned(16))) short sW[D * D];        // W^T image, then W image

@@ -62,6 +62,19 @@ __device__ __forceinline__ Philox4 philox4x32_10(uint32_t c0, uint32_t c1, uint3
 }
 __device__ __forceinline__ float u01(uint32_t r) { return (float)(r >> 8) * (1.0f / 16777216.0f); }
 
+// Wave priority of the main-stream step kernels (GEMMs, gathers, BN, bilinear).  The lazy
+// table-Adam passes run beside them on the side stream as long-lived, VALU-heavy waves; a SIMD
+// arbitrates issue by priority, then AGE, so at equal priority the older side waves win and the
+// main-stream kernel that shares the SIMD takes the leftover slots.  s_setprio > 0 here makes the
+// side stream the background (it keeps priority 0).  -DFBN_MAIN_PRIO_LEVEL=0: off (A/B).
+#ifndef FBN_MAIN_PRIO_LEVEL
+#define FBN_MAIN_PRIO_LEVEL 2
+#endif
+#define FBN_MAIN_PRIO()                                                   \
+  do {                                                                    \
+    if (FBN_MAIN_PRIO_LEVEL > 0) __builtin_amdgcn_s_setprio(FBN_MAIN_PRIO_LEVEL); \
+  } while (0)
+
 // ---------------------------------------------------------------- host helpers
 #define FBN_CHECK_LAUNCH()                                       \
   do {                                                           \

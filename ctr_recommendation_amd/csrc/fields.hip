@@ -113,6 +113,7 @@ __device__ __forceinline__ f32x4 load_row(const FieldArgs& p, size_t r, int q) {
 
 template <int D, int MODE>
 __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
+  FBN_MAIN_PRIO();
   constexpr int G = D / 4;                  // lanes per sample
   constexpr int SPW = 64 / G;               // samples per wave
   constexpr int HCH = FBN_HCH;
@@ -293,6 +294,7 @@ __device__ __forceinline__ void atomic_add_row_t(float* row, const f32x4& t, int
 // partial row (same layout as before).
 template <int D, int MODE, int RMAX>
 __global__ void __launch_bounds__(256) fields_bwd_kernel(FieldBwdArgs p) {
+  FBN_MAIN_PRIO();
   constexpr int G = D / 4;
   constexpr int SPW = 64 / G;
   constexpr int NPMAX = 13 * RMAX + 6;

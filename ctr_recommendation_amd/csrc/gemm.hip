@@ -335,6 +335,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[T
 
 template <int BM, int BN, bool TA, bool TB, bool BF16, bool A16, bool B16>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int remap_xcd) {
+  FBN_MAIN_PRIO();
   typedef GemmTraits<BF16> Tr;
   typedef typename Tr::T T;
   constexpr int BK = Tr::BK, LDK = Tr::LDK;
@@ -434,6 +435,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
 }
 
 __global__ void gemm_splitk_reduce(GemmArgs g, int nsplit) {
+  FBN_MAIN_PRIO();
   const size_t total = (size_t)g.M * g.N;
   for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (size_t)gridDim.x * blockDim.x) {
@@ -519,6 +521,7 @@ __device__ __forceinline__ int xcd_tile(int bid, int nb) {
 // 3 fragment reads (4 waves on 64x64 tiles: 1 MFMA per 2 reads).
 template <int BM, int BN, bool AKM, bool BKM, int S, int WGM = 2, int WGN = 2>
 __global__ void __launch_bounds__(64 * WGM * WGN) gemm_dma16_kernel(GemmArgs g, int tiles_n, int remap_xcd) {
+  FBN_MAIN_PRIO();
   constexpr int NW = WGM * WGN;
   constexpr int BK = 64;
   constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 32, TN = WN / 32;
@@ -643,6 +646,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_dma16_kernel(GemmArgs g, 
 // vectorised split-K reduce: 4 consecutive columns per thread (N, ldc and the C remap in
 // multiples of 4, C 16-B aligned); same slab order as gemm_splitk_reduce (bit-identical)
 __global__ void gemm_splitk_reduce4(GemmArgs g, int nsplit) {
+  FBN_MAIN_PRIO();
   const int N4 = g.N >> 2;
   const size_t total4 = (size_t)g.M * N4, total = (size_t)g.M * g.N;
   for (size_t i4 = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i4 < total4; i4 += (size_t)gridDim.x * blockDim.x) {
@@ -661,6 +665,7 @@ __global__ void gemm_splitk_reduce4(GemmArgs g, int nsplit) {
 // 16 column quads x 16 slab groups; slab group zg sums slabs zg, zg+16, ...; the 16 partials are
 // combined in a fixed order (deterministic)
 __global__ void __launch_bounds__(256) gemm_splitk_reduce4_wide(GemmArgs g, int nsplit) {
+  FBN_MAIN_PRIO();
   __shared__ f32x4 red[16][16];
   const int qd = threadIdx.x & 15, zg = threadIdx.x >> 4;
   const int N4 = g.N >> 2;
@@ -692,6 +697,7 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce4_wide(GemmArgs g, int 
 // K-slabs in the same order as gemm_splitk_reduce (so C is bit-identical with or without stats),
 // then (sum, M2 about the tile mean) of each column from registers.
 __global__ __launch_bounds__(256) void gemm_splitk_reduce_stats(GemmArgs g, int nsplit) {
+  FBN_MAIN_PRIO();
   __shared__ float red[4][64];
   const int c = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int n = blockIdx.x * 64 + c, m0 = blockIdx.y * 64;

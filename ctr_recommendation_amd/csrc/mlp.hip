@@ -247,6 +247,7 @@ __global__ void __launch_bounds__(256) bn_act_fwd2_kernel(const float* __restric
                                                           unsigned stream_id, unsigned char* __restrict__ mask_out,
                                                           const unsigned char* __restrict__ mask_in,
                                                           short* __restrict__ Y16, HeadArgs head) {
+  FBN_MAIN_PRIO();
   const int q = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 256 + q * 4;
   if (c >= C) return;
@@ -350,6 +351,7 @@ __global__ void bn_bwd_partial_kernel(BnBwdSrc s, const float* __restrict__ Xpre
 __global__ void __launch_bounds__(256) bn_bwd_partial4_kernel(BnBwdSrc s, const float* __restrict__ Xpre,
                                                               const float* __restrict__ mean, int B, int C,
                                                               int rows_per_chunk, double* __restrict__ part) {
+  FBN_MAIN_PRIO();
   __shared__ double red[3][4][256];
   const int q = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 256 + q * 4;
@@ -456,6 +458,7 @@ __global__ void colsum_final_kernel(const float* part, int nchunk, int C, float*
 __global__ void bn_tile_finalize_kernel(const float* __restrict__ part, int T, int C, int M, int tile_rows,
                                         double ntot, float* mean, float* invstd, float* run_mean, float* run_var,
                                         float momentum, float eps, int update_running) {
+  FBN_MAIN_PRIO();
   const int c = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (c >= C) return;
@@ -573,6 +576,7 @@ __global__ void __launch_bounds__(1024) bn_bwd_reduce_finalize16_kernel(const do
                                                                         int C, double ntot,
                                                                         const float* __restrict__ invstd, float* coef,
                                                                         float* dgamma, float* dbeta, float* dw) {
+  FBN_MAIN_PRIO();
   __shared__ double red[64][3][16];
   __shared__ double red2[16][3][16];
   __shared__ double tot[3][16];
@@ -627,6 +631,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply4_kernel(BnBwdSrc s, const fl
                                                             const float* __restrict__ coef, float* __restrict__ dX,
                                                             short* __restrict__ dX16, int B, int C,
                                                             int rows_per_chunk, float* __restrict__ colpart) {
+  FBN_MAIN_PRIO();
   __shared__ f32x4 red[4][64];
   const int q = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 256 + q * 4;
