@@ -286,6 +286,8 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     hmm = buf("hmm", (B, d))
     gemm(w16["x"] if bf else x_mm, w16["Wp"] if bf else p["mm_proj.0.weight"], hmm, B, d, 128, 128, 128, d, False,
          True, bias=p["mm_proj.0.bias"], bf16=bf, stream=st)
+    if hooks and "after_mmproj" in hooks:         # trainer: side-stream work forked here
+        hooks["after_mmproj"]()
     X = buf("X", (B, 2, d))                     # fields 3 and 5 (the backward recomputes 1, 2, 4)
     # bf16 mode: the fields after SENET exist only as bf16 (GEMM operand and pair-kernel input)
     v16 = bf and not cfg.bilinear_each

@@ -41,6 +41,9 @@ _W16_MODE = os.environ.get("FBN_W16", "main")
 # single GPU: the side-stream table-Adam passes (window + next-batch prefetch) forked after the
 # MLP's first GEMM instead of right after the row claims (A/B knob)
 _SIDE_AFTER_MLP0 = os.environ.get("FBN_SIDE_AFTER_MLP0", "0") == "1"
+# ... or after the step's first GEMM (mm_proj), so a replayed graph launches that GEMM before the
+# side-stream branch (A/B knob)
+_SIDE_AFTER_MMPROJ = os.environ.get("FBN_SIDE_AFTER_MMPROJ", "0") == "1"
 # N > 1: the next batch's routing enqueued after this step's compute (A/B knob)
 _ROUTE_AFTER_COMPUTE = os.environ.get("FBN_ROUTE_AFTER_COMPUTE", "1") == "1"
 # N > 1 (RCCL): the gradient-row all-to-all issued right after the fields backward -- default on
@@ -395,6 +398,9 @@ class FiBiNETTrainer:
                 self._w16_ev = start_w16(before_side)   # the side stream: images first, then the window
             if claim and _SIDE_AFTER_MLP0:
                 side_hooks["after_mlp0"] = side_pass     # forked after the MLP's first GEMM instead
+                return
+            if claim and _SIDE_AFTER_MMPROJ:
+                side_hooks["after_mmproj"] = side_pass   # forked after the step's first GEMM
                 return
             side_pass()
 
