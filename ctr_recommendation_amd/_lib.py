@@ -39,7 +39,7 @@ SIGNATURES = {
     "fbn_bn_colpart_size": (SZ, [I, I]),
     "fbn_row_chunks": (I, [I]),
     "fbn_bn_bwd_chunks": (I, [I, I]),
-    "fbn_bn_bwd_fused": (I, [P, P, P, P, P, F, P, P, P, P, I, I, D, P, P, P, P, P, P, P, P]),
+    "fbn_bn_bwd_fused": (I, [P, P, P, P, P, F, P, P, P, P, I, I, D, P, P, P, P, P, P, P, P, P]),
     "fbn_colsum_partial": (I, [P, I, I, I, P, P]),
     "fbn_sum_jobs": (I, [P, I, P]),
     "fbn_fields_fwd": (I, [P, P, P, P, P, P, P, F, P, I, P, LL, P, P, P, P, P, I, P, P, P, P, I, I, P, P, P, P, P, I, I, I, I,
@@ -57,7 +57,7 @@ SIGNATURES = {
     "fbn_bn_stats": (I, [P, I, I, P, P, P, P, F, F, I, P, P]),
     "fbn_bn_eval_params": (I, [P, P, P, P, I, F, P]),
     "fbn_bn_act_fwd": (I, [P, P, I, I, P, P, P, P, F, P, U, P, P, P, P]),
-    "fbn_bn_act_head_fwd": (I, [P, P, I, I, P, P, P, P, F, P, U, P, P, P, P, P, P, P, P, P, F, P]),
+    "fbn_bn_act_head_fwd": (I, [P, P, I, I, P, P, P, P, F, P, U, P, P, P, P, P, P, P, P, P, F, P, F, P]),
     "fbn_bn_bwd_reduce": (I, [P, P, P, P, F, P, P, I, I, P, P, P]),
     "fbn_bn_bwd_apply": (I, [P, P, P, P, F, P, P, P, P, I, I, P, D, P, P, P, P, P, P, P]),
     "fbn_convert_bf16": (I, [P, I, P]),

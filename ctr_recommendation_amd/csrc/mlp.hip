@@ -213,8 +213,9 @@ struct HeadArgs {
 };
 // Linear(C,1) + sigmoid + BCE terms + dL/dlogit of one row from the wave's lane partials
 // (lane q holds columns 4q..4q+3): shared by head_fwd_kernel and the fused BN2 + head kernel
-__device__ __forceinline__ void head_row(float s, int row, int lane, const HeadArgs& h) {
+__device__ __forceinline__ float head_row(float s, int row, int lane, const HeadArgs& h) {
   s = wave_sum(s);
+  float go = 0.f;
   if (lane == 0) {
     const float o = s + h.bias[0];
     const float pr = 1.f / (1.f + expf(-o));
@@ -226,10 +227,12 @@ __device__ __forceinline__ void head_row(float s, int row, int lane, const HeadA
       if (h.loss_terms) h.loss_terms[row] = -(t * lp + (1.f - t) * l1p);
       if (h.gout) {
         const float gp = ((pr - t) / fmaxf((1.f - pr) * pr, 1e-12f)) / h.denom;
-        h.gout[row] = gp * (1.f - pr) * pr;
+        go = gp * (1.f - pr) * pr;
+        h.gout[row] = go;
       }
     }
   }
+  return go;   // dL/dlogit of the row on lane 0
 }
 
 // Column-blocked form: block = 64 column quads (256 columns) x 4 row lanes over a chunk of rows,
@@ -238,16 +241,23 @@ __device__ __forceinline__ void head_row(float s, int row, int lane, const HeadA
 // HEAD (C == 256, one column block): each wave holds whole rows, so the head Linear(256,1) +
 // sigmoid + BCE of src/model_fibinet.py:134,136 runs on the activations still in registers
 // (the same lane partials and reduction as head_fwd_kernel: bit-identical, one launch fewer).
-template <bool HEAD>
-__global__ void __launch_bounds__(256) bn_act_fwd2_kernel(const float* __restrict__ X, float* __restrict__ Y, int B,
-                                                          int C, int rows_per_chunk, const float* __restrict__ mean,
-                                                          const float* __restrict__ invstd,
-                                                          const float* __restrict__ g, const float* __restrict__ bta,
-                                                          float p_drop, const unsigned long long* __restrict__ rng,
-                                                          unsigned stream_id, unsigned char* __restrict__ mask_out,
-                                                          const unsigned char* __restrict__ mask_in,
-                                                          short* __restrict__ Y16, HeadArgs head) {
+// BWD (HEAD, 1024 threads, one row per wave): the BN2 backward's column partials of the rank-1
+// source (fbn_bn_bwd_fused's first pass, bn_bwd_partial4) from the row's dL/dlogit, activation
+// and input while they are in registers: bpart[chunk][3][C] = {sum dy, sum (x-mean) dy,
+// sum gout*h}, dy = gout*w*(h > 0)*bscale, the same float products and f64 sums; waves folded in
+// a fixed order (deterministic).
+template <bool HEAD, int NT = 256, bool BWD = false>
+__global__ void __launch_bounds__(NT) bn_act_fwd2_kernel(const float* __restrict__ X, float* __restrict__ Y, int B,
+                                                         int C, int rows_per_chunk, const float* __restrict__ mean,
+                                                         const float* __restrict__ invstd,
+                                                         const float* __restrict__ g, const float* __restrict__ bta,
+                                                         float p_drop, const unsigned long long* __restrict__ rng,
+                                                         unsigned stream_id, unsigned char* __restrict__ mask_out,
+                                                         const unsigned char* __restrict__ mask_in,
+                                                         short* __restrict__ Y16, HeadArgs head,
+                                                         double* __restrict__ bpart = nullptr, float bscale = 1.f) {
   FBN_MAIN_PRIO();
+  constexpr int NWV = NT / 64;
   const int q = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 256 + q * 4;
   if (c >= C) return;
@@ -262,7 +272,8 @@ __global__ void __launch_bounds__(256) bn_act_fwd2_kernel(const float* __restric
     alpha[e] = invstd[c + e] * g[c + e];
     bp[e] = bta[c + e] - mean[c + e] * alpha[e];
   }
-  for (int r = r0 + rl; r < r1; r += 4) {
+  double s0[4] = {0.0, 0.0, 0.0, 0.0}, s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int r = r0 + rl; r < r1; r += NWV) {
     const size_t i = (size_t)r * C + c, i4 = i >> 2;
     const f32x4 x = *reinterpret_cast<const f32x4*>(X + i);
     float um[4] = {1.f, 1.f, 1.f, 1.f};
@@ -285,7 +296,37 @@ __global__ void __launch_bounds__(256) bn_act_fwd2_kernel(const float* __restric
     if (Y16) store4(Y16 + i, y);
     if (HEAD) {
       const f32x4 ww = *reinterpret_cast<const f32x4*>(head.w + c);
-      head_row(y[0] * ww[0] + y[1] * ww[1] + y[2] * ww[2] + y[3] * ww[3], r, q, head);
+      const float go = head_row(y[0] * ww[0] + y[1] * ww[1] + y[2] * ww[2] + y[3] * ww[3], r, q, head);
+      if (BWD) {
+        const float gv = __shfl(go, 0, 64);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = gv * ww[e];
+          const float dy = y[e] > 0.f ? d * bscale : 0.f;
+          s0[e] += dy;
+          s1[e] += (double)((x[e] - mean[c + e]) * dy);
+          s2[e] += (double)(gv * y[e]);
+        }
+      }
+    }
+  }
+  if (BWD) {
+    // C == 256: lane q holds columns 4q..4q+3; fold the NWV waves per quantity through LDS
+    __shared__ double red[NWV][256];
+    double* pp = bpart + (size_t)blockIdx.y * 3 * C;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const double* sk = k == 0 ? s0 : (k == 1 ? s1 : s2);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[rl][q * 4 + e] = sk[e];
+      __syncthreads();
+      if (threadIdx.x < 256) {
+        double t = 0.0;
+#pragma unroll
+        for (int w = 0; w < NWV; ++w) t += red[w][threadIdx.x];
+        pp[(size_t)k * C + threadIdx.x] = t;
+      }
+      __syncthreads();
     }
   }
 }
@@ -904,10 +945,22 @@ extern "C" int fbn_bn_act_head_fwd(const float* X, float* Y, int B, int C, const
                                    const float* g, const float* b, float p_drop, const unsigned long long* rng,
                                    unsigned stream_id, unsigned char* mask_out, const unsigned char* mask_in,
                                    const float* hw, const float* hbias, float* logits, float* probs,
-                                   const float* labels, float* loss_terms, float* gout, float denom, void* stream) {
+                                   const float* labels, float* loss_terms, float* gout, float denom,
+                                   double* bwd_part, float bwd_scale, void* stream) {
   if (B <= 0) return FBN_OK;
   if (C != 256) { fbn_set_error("bn_act_head: the fused head needs C == 256"); return FBN_ERR_UNSUPPORTED; }
   if (p_drop > 0.f && !rng && !mask_in) { fbn_set_error("bn_act: dropout needs an rng state or a mask"); return FBN_ERR_ARG; }
+  if (bwd_part && !gout) { fbn_set_error("bn_act_head: backward partials need labels / gout"); return FBN_ERR_ARG; }
+  if (bwd_part) {
+    // the row chunks of fbn_bn_bwd_fused, so its reduce reads these partials as its own
+    const int nch = bn_bwd_chunks(B, C), rpc = (B + nch - 1) / nch;
+    hipLaunchKernelGGL((bn_act_fwd2_kernel<true, 1024, true>), dim3(1, fbn_cdiv(B, rpc)), dim3(1024), 0,
+                       (hipStream_t)stream, X, Y, B, C, rpc, mean, invstd, g, b, p_drop, rng, stream_id, mask_out,
+                       mask_in, nullptr, HeadArgs{hw, hbias, logits, probs, labels, loss_terms, gout, denom}, bwd_part,
+                       bwd_scale);
+    FBN_CHECK_LAUNCH();
+    return FBN_OK;
+  }
   const int rpc = bn_act_rows_per_chunk();
   hipLaunchKernelGGL(bn_act_fwd2_kernel<true>, dim3(1, fbn_cdiv(B, rpc)), dim3(256), 0, (hipStream_t)stream, X, Y, B,
                      C, rpc, mean, invstd, g, b, p_drop, rng, stream_id, mask_out, mask_in, nullptr,
@@ -1136,8 +1189,8 @@ extern "C" size_t fbn_bn_colpart_size(int B, int C) { return (size_t)bn_bwd_chun
 extern "C" int fbn_bn_bwd_fused(const float* G, const float* gvec, const float* w, const float* hact,
                                 const short* hact16, float scale, const float* Xpre, const float* mean,
                                 const float* invstd, const float* gamma, int B, int C, double ntot, float* dXpre,
-                                short* dXpre16, float* dgamma, float* dbeta, float* dw, float* colpart, void* ws,
-                                void* stream) {
+                                short* dXpre16, float* dgamma, float* dbeta, float* dw, float* colpart,
+                                const double* part_pre, void* ws, void* stream) {
   if (B <= 0) return FBN_OK;
   if (C & 3) { fbn_set_error("fbn_bn_bwd_fused: C % 4"); return FBN_ERR_ARG; }
   if (!hact && !(hact16 && G)) {
@@ -1150,8 +1203,11 @@ extern "C" int fbn_bn_bwd_fused(const float* G, const float* gvec, const float* 
   const int nch = bn_bwd_chunks(B, C), rpc = (B + nch - 1) / nch;
   double* part = (double*)ws;
   float* coef = (float*)((double*)ws + (size_t)nch * 3 * C + 3 * (size_t)C);
-  hipLaunchKernelGGL(bn_bwd_partial4_kernel, dim3(fbn_cdiv(C, 256), nch), dim3(256), 0, st, s, Xpre, mean, B, C, rpc,
-                     part);
+  if (part_pre)   // the first pass already ran inside the forward (fbn_bn_act_head_fwd's bwd_part)
+    part = const_cast<double*>(part_pre);
+  else
+    hipLaunchKernelGGL(bn_bwd_partial4_kernel, dim3(fbn_cdiv(C, 256), nch), dim3(256), 0, st, s, Xpre, mean, B, C, rpc,
+                       part);
   static const bool wide = !getenv("FBN_BN_REDUCE64");   // A/B knob: 64 columns per workgroup
   if (wide)
     hipLaunchKernelGGL(bn_bwd_reduce_finalize16_kernel, dim3(fbn_cdiv(C, 16)), dim3(1024), 0, st, part, nch, C, ntot,

@@ -33,6 +33,10 @@ BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
 
 
+# the trainer's BN2 backward first pass inside the forward head kernel (A/B knob)
+_BN2_BWD_IN_FWD = os.environ.get("FBN_BN2_BWD_IN_FWD", "1") == "1"
+
+
 def wa_remap(d: int):
     """compact MLP-input column -> mlp.0.weight column (skips V_0 and the five (0,j) pairs)."""
     return (5 * d, d, 6 * d)
@@ -205,7 +209,7 @@ def bn_train_stats(h, B, C, mean, invstd, run_mean, run_var, ntot, coll: Collect
 
 def bn_backward(G, gvec, w, hact, scale, hpre, mean, invstd, gamma, B, C, ntot, dpre, dgamma, dbeta, dw,
                 coll: Collective, stream, dpre16=None, bias_grad=None, sums: Optional[DeferredSums] = None,
-                hact16=None):
+                hact16=None, part_pre=None):
     """BN (+ReLU/dropout) backward; bias_grad (with sums): the preceding Linear's bias gradient
     = column sums of dpre, finalised later by sums.flush().
     Single process only: hact may be None with hact16 (the bf16 activation image; a matrix source
@@ -221,7 +225,7 @@ def bn_backward(G, gvec, w, hact, scale, hpre, mean, invstd, gamma, B, C, ntot, 
             sums.add(part, nch, C, bias_grad)
         call("fbn_bn_bwd_fused", ptr(G), ptr(gvec), ptr(w), ptr(hact), ptr(hact16), float(scale), ptr(hpre),
              ptr(mean), ptr(invstd), ptr(gamma), B, C, float(ntot), ptr(dpre), ptr(dpre16), ptr(dgamma), ptr(dbeta),
-             ptr(dw), ptr(part), ptr(ws), stream)
+             ptr(dw), ptr(part), ptr(part_pre), ptr(ws), stream)
         return
     assert hact is not None and dpre is not None, "SyncBN backward reads the f32 activation and gradient"
     red = torch.empty(3 * C, dtype=torch.float64, device=dev)
@@ -406,11 +410,17 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     logits, probs = buf("logits", (B,)), buf("probs", (B,))
     lt = buf("loss_terms", (B,)) if labels is not None else None
     go = buf("gout", (B,)) if labels is not None else None
-    # BN2 + ReLU + dropout with the head Linear(256,1) + sigmoid + BCE in the same launch
+    # BN2 + ReLU + dropout with the head Linear(256,1) + sigmoid + BCE in the same launch; with the
+    # labels (trainer, one BN group) also the first pass of the BN2 backward (its column partials)
+    bpart = None
+    if labels is not None and cfg.training and coll.world <= 1 and _BN2_BWD_IN_FWD:
+        bpart = buf("bn2_bwd_part", (_lib.lib().fbn_bn_bwd_chunks(B, H2) * 3 * H2,), torch.float64)
+    a["bn2_bwd_part"] = bpart
+    bscale = 1.0 / (1.0 - cfg.p_drop) if (cfg.training and cfg.p_drop > 0) else 1.0   # = backward()'s scale
     call("fbn_bn_act_head_fwd", ptr(h2pre), ptr(h2), B, H2, ptr(mean2), ptr(inv2), ptr(p["mlp.5.weight"]),
          ptr(p["mlp.5.bias"]), float(p_drop), ptr(rng), 2, ptr(m2), ptr(mi2), ptr(p["mlp.8.weight"]),
          ptr(p["mlp.8.bias"]), ptr(logits), ptr(probs), ptr(labels), ptr(lt), ptr(go),
-         float(loss_denom if loss_denom is not None else ntot), st)
+         float(loss_denom if loss_denom is not None else ntot), ptr(bpart), float(bscale), st)
     if cfg.training and count_batches and "mlp.1.num_batches_tracked" in p:
         p["mlp.1.num_batches_tracked"].add_(1)
         p["mlp.5.num_batches_tracked"].add_(1)
@@ -483,7 +493,8 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     wg = _SideWork(side, dev)
     bn_backward(None, gout, p["mlp.8.weight"], a["h2"], scale, a["h2pre"], a["mean2"], a["inv2"],
                 p["mlp.5.weight"], B, H2, ntot, dh2pre, g["mlp.5.weight"], g["mlp.5.bias"], g["mlp.8.weight"],
-                coll, st, dpre16=dh2pre16, bias_grad=g["mlp.4.bias"], sums=sums)
+                coll, st, dpre16=dh2pre16, bias_grad=g["mlp.4.bias"], sums=sums,
+                part_pre=a.get("bn2_bwd_part") if (gout is a.get("gout")) else None)
     sums.add(gout, B, 1, g["mlp.8.bias"])
     dh1 = torch.empty((B, H1), **f32)
     if bf:

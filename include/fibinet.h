@@ -145,12 +145,15 @@ int fbn_bn_eval_params(const float* run_mean, const float* run_var, float* mean,
 int fbn_bn_act_fwd(const float* X, float* Y, int B, int C, const float* mean, const float* invstd, const float* g,
                    const float* b, float p_drop, const unsigned long long* rng, unsigned stream_id,
                    unsigned char* mask_out, const unsigned char* mask_in, short* Y16, void* stream);
-/* fbn_bn_act_fwd of the last hidden layer (C = 256) fused with fbn_head_fwd (same outputs). */
+/* fbn_bn_act_fwd of the last hidden layer (C = 256) fused with fbn_head_fwd (same outputs).
+ * bwd_part (optional, with labels / gout; fbn_bn_bwd_chunks(B, C) * 3 * C doubles): the first pass
+ * of this layer's BN backward (rank-1 source gout x hw, dropout scale bwd_scale), handed to
+ * fbn_bn_bwd_fused as part_pre. */
 int fbn_bn_act_head_fwd(const float* X, float* Y, int B, int C, const float* mean, const float* invstd, const float* g,
                         const float* b, float p_drop, const unsigned long long* rng, unsigned stream_id,
                         unsigned char* mask_out, const unsigned char* mask_in, const float* hw, const float* hbias,
                         float* logits, float* probs, const float* labels, float* loss_terms, float* gout, float denom,
-                        void* stream);
+                        double* bwd_part, float bwd_scale, void* stream);
 int fbn_bn_bwd_reduce(const float* G, const float* gvec, const float* w, const float* hact, float scale,
                       const float* Xpre, const float* mean, int B, int C, double* red_d, void* ws, void* stream);
 int fbn_bn_bwd_apply(const float* G, const float* gvec, const float* w, const float* hact, float scale,
@@ -172,7 +175,7 @@ int fbn_bn_bwd_chunks(int B, int C);
 int fbn_bn_bwd_fused(const float* G, const float* gvec, const float* w, const float* hact, const short* hact16,
                      float scale, const float* Xpre, const float* mean, const float* invstd, const float* gamma, int B,
                      int C, double ntot, float* dXpre, short* dXpre16, float* dgamma, float* dbeta, float* dw,
-                     float* colpart, void* ws, void* stream);
+                     float* colpart, const double* part_pre, void* ws, void* stream);
 /* bf16 weight images: jobs = host array of n <= 8 records
  * {const float* src; short* dst; int rows, cols, ld, trans, seg, off0, off1;}
  * out[i][j] = bf16(trans ? src[j*ld + rm(i)] : src[i*ld + rm(j)]), rm(x) = x + (x < seg ? off0 : off1). */
