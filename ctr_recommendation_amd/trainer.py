@@ -28,6 +28,7 @@ from typing import Dict, List, Optional
 
 import numpy as np
 import torch
+import torch.distributed as dist
 
 from . import _lib, ops
 from ._lib import call, ptr
@@ -46,10 +47,12 @@ _SIDE_AFTER_MLP0 = os.environ.get("FBN_SIDE_AFTER_MLP0", "0") == "1"
 _SIDE_AFTER_MMPROJ = os.environ.get("FBN_SIDE_AFTER_MMPROJ", "0") == "1"
 # N > 1: the next batch's routing enqueued after this step's compute (A/B knob)
 _ROUTE_AFTER_COMPUTE = os.environ.get("FBN_ROUTE_AFTER_COMPUTE", "1") == "1"
-# N > 1 (RCCL): the gradient-row all-to-all issued right after the fields backward -- default on
-# for world > 1; at world = 1 (one-rank rehearsal) the "all-to-all" is a local copy that only
-# competes with the compute for HBM (0.68-0.71 vs 0.68 ms/step), so default off there (A/B knob:
-# FBN_EARLY_GRAD_XCHG=0 / 1)
+# N > 1 (RCCL), opt-in (FBN_EARLY_GRAD_XCHG=1): the gradient-row all-to-all issued right after the
+# fields backward and the dense-gradient all-reduce right after the compute, both asynchronous on
+# the process group's stream beside the remaining work (the loss + table sum of squares then take
+# a small all-reduce of their own).  Off by default: as a one-rank RCCL job it measured 0.73-0.74
+# vs 0.69-0.72 ms/step (extra launches, a local-copy "all-to-all" competing for HBM) and the
+# overlap it buys at N > 1 could not be measured on a one-GPU box
 _EARLY_GRAD_XCHG = os.environ.get("FBN_EARLY_GRAD_XCHG")
 from .schedule import OneCycle, adam_table
 
@@ -304,7 +307,7 @@ class FiBiNETTrainer:
         self.xchg = RowExchange(rank, world, self.V, d, self.B, max_len, dev, group, stage_on_cpu=stage_on_cpu,
                                 rows_bf16=self.fcfg.bf16, side=self.side) if sharded else None
         self.stage_on_cpu = stage_on_cpu
-        self.early_grad_xchg = (world > 1) if _EARLY_GRAD_XCHG is None else _EARLY_GRAD_XCHG == "1"
+        self.early_grad_xchg = _EARLY_GRAD_XCHG == "1"
         # item-table Adam: "lazy" (default) replays the zero-gradient steps of a row when the row
         # is next claimed or its rolling window comes round (bit-identical to eager; see
         # fbn_adam_catchup) -- "eager" streams every untouched row each step on a side stream (the
@@ -520,6 +523,13 @@ class FiBiNETTrainer:
                          pos=pos, sendbuf=sendbuf, coll=self.bn_coll, ntot=self._bn_n(ntot, B),
                          extra_sums=[(a["loss_terms"], B, 1, self.loss, 1.0 / ntot)], probe=probe,
                          hooks={"after_fields_bwd": self._grad_xchg_start} if self._early_grad_xchg() else None)
+        dense_work = None
+        if self.sharded and self._early_grad_xchg():
+            # the dense gradients are final once the compute is: their all-reduce goes out now,
+            # asynchronously behind the gradient-row all-to-all on the process group's stream,
+            # beside the owner's widen / fold / norm; only the loss and the table-gradient sum of
+            # squares (known after those) travel at the end
+            dense_work = dist.all_reduce(self.flat_g, group=self.coll.group, async_op=True)
         if route_ahead is not None:
             # the host enqueues the next batch's routing (and the owner-side prefetch) only after
             # this step's compute: on the GPU it still starts right after this step's row exchange
@@ -565,7 +575,11 @@ class FiBiNETTrainer:
             # ONE all-reduce: dense grads + the loss + this shard's table-gradient sumsq
             o = self.n_dense
             call("fbn_pack_extras", ptr(self.loss), ptr(self.sumsq_tab), ptr(self.flat_g_ext[o:]), st)
-            self.coll.allreduce_(self.flat_g_ext[:o + 2])
+            if dense_work is not None:
+                dist.all_reduce(self.flat_g_ext[o:o + 2], group=self.coll.group)
+                dense_work.wait()
+            else:
+                self.coll.allreduce_(self.flat_g_ext[:o + 2])
             call("fbn_unpack_extras", ptr(self.flat_g_ext[o:]), ptr(self.loss), ptr(self.sumsq), st)
         call("fbn_sumsq", ptr(self.flat_g), self.n_dense, None, 0, ptr(self.sumsq), st)
         main.wait_stream(self.side)   # side-stream table pass done before map entries are reset
