@@ -74,7 +74,7 @@ SIGNATURES = {
     "fbn_sparse_fixup": (I, [P, P, P, I, I, LL, I, P, P, P, P, I, I, P]),
     "fbn_sumsq_sparse": (I, [P, P, P, I, I, I, P, P]),
     "fbn_sparse_fixup_dup": (I, [P, I, P, P, P, I, I, P]),
-    "fbn_sumsq_sparse_norms": (I, [P, P, P, P, I, I, I, P, P, P]),
+    "fbn_sumsq_sparse_norms": (I, [P, P, P, P, I, I, I, P, P, P, LL, P]),
     "fbn_sparse_fold_fx": (I, [P, P, I, P, P, I, I, P, P]),
     "fbn_adam_table": (I, [P, P, P, LL, I, P, P, P, P, I, P, P, P, F, F, F, I, P]),
     "fbn_adam_touched": (I, [P, P, P, I, P, P, P, P, I, I, P, P, P, F, F, F, P, P]),

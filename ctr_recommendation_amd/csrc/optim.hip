@@ -455,10 +455,17 @@ __global__ void __launch_bounds__(256) sparse_fold_fx_kernel(const int* __restri
 // (FLAG, rare) sums vector + extra explicitly, cooperatively across the wave.  One entry per lane.
 template <int D>
 __global__ void __launch_bounds__(256) sumsq_norms_kernel(GradSrc s, const double* __restrict__ gnorm, int n,
-                                                          double* __restrict__ out, unsigned long long* __restrict__ fx) {
+                                                          double* __restrict__ out, unsigned long long* __restrict__ fx,
+                                                          const float* __restrict__ dense, long long n_dense) {
   __shared__ double red[4];
   const int lane = threadIdx.x & 63;
   double acc = 0.0;
+  // the dense gradients' squares too (fbn_sumsq's work, one launch fewer): n_dense % 4 == 0
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n_dense / 4;
+       i += (long long)gridDim.x * blockDim.x) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(dense + 4 * i);
+    acc += (double)(v[0] * v[0]) + (double)(v[1] * v[1]) + (double)(v[2] * v[2]) + (double)(v[3] * v[3]);
+  }
   for (long long e0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) - lane; e0 < n;
        e0 += (long long)gridDim.x * blockDim.x) {
     const long long e = e0 + lane;
@@ -1490,14 +1497,19 @@ extern "C" int fbn_sparse_fold_fx(const int* dup, int* hasdup, int n, const floa
 }
 
 extern "C" int fbn_sumsq_sparse_norms(const double* gnorm, const float* gvec, float* extra, int* slot_row, int Lp1,
-                                      int n, int D, double* out, unsigned long long* fx, void* stream) {
+                                      int n, int D, double* out, unsigned long long* fx, const float* dense,
+                                      long long n_dense, void* stream) {
   if (n <= 0) return FBN_OK;
+  if (dense ? (n_dense < 0 || (n_dense & 3) || ((uintptr_t)dense & 15)) : n_dense != 0) {
+    fbn_set_error("fbn_sumsq_sparse_norms: dense needs n_dense % 4 == 0 and 16-byte alignment");
+    return FBN_ERR_ARG;
+  }
   if ((Lp1 & 0xffff) < 2) { fbn_set_error("fbn_sumsq_sparse_norms: per-sample vectors only (Lp1 >= 2)"); return FBN_ERR_ARG; }
   hipStream_t st = (hipStream_t)stream;
   const GradSrc s = make_src(gvec, extra, slot_row, Lp1);
   int blocks = (n + 255) / 256;
   if (blocks > 1024) blocks = 1024;
-  FBN_DISPATCH_D(sumsq_norms_kernel, D, dim3(blocks), s, gnorm, n, out, fx);
+  FBN_DISPATCH_D(sumsq_norms_kernel, D, dim3(blocks), s, gnorm, n, out, fx, dense, dense ? n_dense : 0);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

@@ -47,6 +47,8 @@ _SIDE_AFTER_MLP0 = os.environ.get("FBN_SIDE_AFTER_MLP0", "0") == "1"
 _SIDE_AFTER_MMPROJ = os.environ.get("FBN_SIDE_AFTER_MMPROJ", "0") == "1"
 # N > 1: the next batch's routing enqueued after this step's compute (A/B knob)
 _ROUTE_AFTER_COMPUTE = os.environ.get("FBN_ROUTE_AFTER_COMPUTE", "1") == "1"
+# single GPU: the dense gradients' sum of squares inside the table-gradient norm launch (A/B knob)
+_DENSE_SUMSQ_FOLD = os.environ.get("FBN_DENSE_SUMSQ_FOLD", "1") == "1"
 # N > 1 (RCCL), opt-in (FBN_EARLY_GRAD_XCHG=1): the gradient-row all-to-all issued right after the
 # fields backward and the dense-gradient all-reduce right after the compute, both asynchronous on
 # the process group's stream beside the remaining work (the loss + table sum of squares then take
@@ -565,9 +567,14 @@ class FiBiNETTrainer:
                  ptr(grows), None, ptr(self.slot_row), 1, d, st)
         # clip_grad_norm_(10): dense grads (identical on every rank) + disjoint table shards
         tab_acc = self.sumsq_tab if self.sharded else self.sumsq
+        dense_done = False
         if self.xchg is None and L > 0:
+            # one process: the dense gradients are final here, so their squares ride along
+            fold = not self.sharded and _DENSE_SUMSQ_FOLD
             call("fbn_sumsq_sparse_norms", ptr(self.gnorm), ptr(gsrc[0]), ptr(gsrc[1]), ptr(self.slot_row), gsrc[2],
-                 n_ent, d, ptr(tab_acc), ptr(self.fx), st)
+                 n_ent, d, ptr(tab_acc), ptr(self.fx), ptr(self.flat_g) if fold else None,
+                 self.n_dense if fold else 0, st)
+            dense_done = fold
         else:
             call("fbn_sumsq_sparse", ptr(gsrc[0]), ptr(gsrc[1]), ptr(self.slot_row), gsrc[2], n_ent, d, ptr(tab_acc),
                  st)
@@ -581,7 +588,8 @@ class FiBiNETTrainer:
             else:
                 self.coll.allreduce_(self.flat_g_ext[:o + 2])
             call("fbn_unpack_extras", ptr(self.flat_g_ext[o:]), ptr(self.loss), ptr(self.sumsq), st)
-        call("fbn_sumsq", ptr(self.flat_g), self.n_dense, None, 0, ptr(self.sumsq), st)
+        if not dense_done:
+            call("fbn_sumsq", ptr(self.flat_g), self.n_dense, None, 0, ptr(self.sumsq), st)
         main.wait_stream(self.side)   # side-stream table pass done before map entries are reset
         if self.xchg is None:
             defer_now = self.deferred

@@ -226,8 +226,10 @@ int fbn_sumsq_sparse(const float* gvec, float* extra, int* slot_row, int Lp1, in
  * per-sample norms gnorm[B][2] (vectors re-read only for rows with duplicates). */
 int fbn_sparse_fixup_dup(const int* dup, int n, const float* gvec, float* extra, int* slot_row, int Lp1, int D,
                          void* stream);
+/* dense (optional, n_dense % 4 == 0, 16-B aligned): also adds the squares of a dense gradient
+ * vector to out (fbn_sumsq's work in the same launch). */
 int fbn_sumsq_sparse_norms(const double* gnorm, const float* gvec, float* extra, int* slot_row, int Lp1, int n, int D,
-                           double* out, unsigned long long* fx, void* stream);
+                           double* out, unsigned long long* fx, const float* dense, long long n_dense, void* stream);
 /* Deterministic mode (no float atomics on the table gradient): every entry of a row several
  * entries hit -- claimer included -- adds its vector into acc[claimer] ([n][D] int64 fixed point,
  * scale 2^40: order-independent sums); claimers are flagged.  fbn_sumsq_sparse_norms(fx = acc)
