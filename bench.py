@@ -52,7 +52,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=8192, help="per-GPU batch")
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--rows-per-gpu", type=int, default=ROWS_PER_GPU)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "bf16_fwd", "fp32"],
+                    help="bf16: every GEMM operand bf16; bf16_fwd: forward GEMM operands bf16, backward fp32; fp32")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=20)
@@ -70,7 +71,7 @@ def parse():
                          "multi-GPU box (nn.DataParallel, train_fibinet.py:69-70); 'sync' = over the global "
                          "batch (parity with one process on the global batch; 4 all-reduces per step)")
     ap.add_argument("--no-fp32", dest="also_fp32", action="store_false",
-                    help="skip the second (fp32) C3 measurement embedded in the line")
+                    help="skip the fp32 and bf16_fwd C3 measurements embedded in the line")
     return ap.parse_args()
 
 
@@ -261,6 +262,18 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
         torch.cuda._sleep(20_000_000)
         tr.step(b, y, probe=probe, next_batch=batches[i % nb][0] if world == 1 else None)
     torch.cuda.synchronize()
+    # the same steps with the side-stream passes on the main stream: every kernel alone
+    serial = {}
+    if world == 1 and tr.xchg is None:
+        side = tr.side
+        tr.side = torch.cuda.current_stream(dev)
+        for _ in range(max(4, args.probe_steps // 2)):
+            b, y = batches[i % nb]
+            i += 1
+            torch.cuda._sleep(20_000_000)
+            tr.step(b, y, probe=serial, next_batch=batches[i % nb][0])
+        torch.cuda.synchronize()
+        tr.side = side
 
     # the gather alone: eval-mode forwards of the same batches with nothing on the side stream (the
     # probe above times it inside the step, beside the table-Adam passes)
@@ -274,7 +287,7 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
         torch.cuda.synchronize()
 
     def avg_ms(name, src=None):
-        ev = (probe if src is None else src).get(name, [])[2 if src is not None else 0:]
+        ev = (probe if src is None else src).get(name, [])[2 if src is iso else 0:]
         return sum(a.elapsed_time(e) for a, e in ev) / max(1, len(ev))
 
     touched = int(uniq.numel())
@@ -314,12 +327,20 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
         f"{' + 4 B x d + 8 B deferred gradient' if dfr else ''}); mean lag {lag:.1f} steps over the {touched} rows")
     if prefetch:
         ahead = max(0, touched - stale)
+        pf_work = catchup_bytes(ahead, d, 5 * B * (L + 1)) + (ahead * (4 * d + 8) if dfr else 0)
+        pf_basis = f"~{ahead} rows x (24 B x d + 8 B + deferred gradient) + {B * (L + 1)} entries x 20 B"
         add("adam_prefetch", "adam_prefetch (next batch's rows caught up ahead, side stream)", avg_ms("adam_prefetch"),
-            catchup_bytes(ahead, d, 5 * B * (L + 1)) + (ahead * (4 * d + 8) if dfr else 0), "GB/s", HBM_PEAK_GBS,
-            "hbm", f"~{ahead} rows x (24 B x d + 8 B + deferred gradient) + {B * (L + 1)} entries x 20 B")
+            pf_work, "GB/s", HBM_PEAK_GBS, "hbm", pf_basis)
+        if serial:
+            add("adam_prefetch", "adam_prefetch alone (serialised probe step, nothing beside it)",
+                avg_ms("adam_prefetch", serial), pf_work, "GB/s", HBM_PEAK_GBS, "hbm", pf_basis)
     add("adam_window", "adam_catchup (lazy table Adam: rolling window, side stream)", avg_ms("adam_window"),
         catchup_bytes(window, d, 0), "GB/s", HBM_PEAK_GBS, "hbm",
         f"window {window} rows x (24 B x d + 8 B); VALU-bound replay of up to F steps per row")
+    if serial:
+        add("adam_window", "adam_catchup rolling window alone (serialised probe step)", avg_ms("adam_window", serial),
+            catchup_bytes(window, d, 0), "GB/s", HBM_PEAK_GBS, "hbm",
+            f"window {window} rows x (24 B x d + 8 B); VALU-bound replay of up to F steps per row")
     add("gemm_mlp0", f"gemm MLP layer 1 (B x 15d -> 512, {dtype} MFMA)", avg_ms("gemm_mlp0"),
         2.0 * B * 512 * 15 * d, "TFLOP/s", MFMA_PEAK_TFS if dtype == "bf16" else FP32_MFMA_PEAK_TFS, "mfma",
         "2 x B x 512 x 15d")
@@ -339,6 +360,25 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     return out
+
+
+def _workload(args, r) -> str:
+    """config.workload: which BASELINE config this line measures, and in which precision."""
+    prec = {"bf16": "every GEMM operand bf16 (forward and backward) / fp32 accumulation + fp32 master weights, "
+                    "gradients and Adam",
+            "bf16_fwd": "forward GEMM operands bf16 / fp32 accumulation, backward GEMMs and everything else fp32",
+            "fp32": "fp32 throughout"}[args.dtype]
+    d, B, rows = r["d"], r["B"], r["rows_local"]
+    if d == 16 and B == 4096:
+        name = f"C2: FiBiNET emb_dim=16, {rows} item rows, batch 4096/GPU, history 20 (item_emb_d128 input)"
+    elif d == 128 and rows >= 10_000_000:
+        name = (f"C5 per-GPU shard: FiBiNET emb_dim=128 + item_emb_d128, {rows} item rows on this GPU "
+                f"(100 M / 8), batch {B}/GPU, history 20")
+    elif d == 128:
+        name = f"C3: FiBiNET emb_dim=128 + item_emb_d128, batch {B}/GPU, history 20"
+    else:
+        name = f"FiBiNET emb_dim={d}, batch {B}/GPU, {rows} item rows/GPU, history 20"
+    return f"{name}, {prec}"
 
 
 def main():
@@ -364,15 +404,17 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
 
     r = measure(args, args.dtype, world, rank, dev, rehearsal, backend)
-    alt = None
+    alt = alt16 = None
     if args.also_fp32 and args.dtype == "bf16" and world == 1:
         # the reference computes in fp32 throughout: the same C3 step with fp32 GEMM operands
         alt = measure(args, "fp32", world, rank, dev, rehearsal, backend)
+        # C3's literal wording ("bf16 fwd / fp32 grad accum"): bf16 forward GEMMs, fp32 backward
+        alt16 = measure(args, "bf16_fwd", world, rank, dev, rehearsal, backend)
 
     if rank == 0:
         K, B, dt = r["K"], r["B"], r["dt"]
         out = {
-            "metric": "training samples/sec (FiBiNET d=128, MicroLens-shaped synthetic, full train step)",
+            "metric": f"training samples/sec (FiBiNET d={r['d']}, MicroLens-shaped synthetic, full train step)",
             "value": round(K * B * world / dt, 1),
             "unit": "samples/s",
             "n_gpus": world,
@@ -387,9 +429,7 @@ def main():
                     f"fresh ids every step, "
                     + (f"Zipf({args.zipf}) item / history ids" if args.zipf > 0 else "uniform ids")
                     + "; random-init weights)",
-            "config": {"workload": "C3: FiBiNET emb_dim=128 + item_emb_d128, batch 8192/GPU, history 20, "
-                                   + ("bf16 GEMM operands / fp32 accumulation + fp32 master weights and Adam"
-                                      if args.dtype == "bf16" else "fp32 throughout"),
+            "config": {"workload": _workload(args, r),
                        "model": "MM_FiBiNET", "global_batch": B * world, "seq_len": r["L"],
                        "item_rows": r["V"], "item_rows_per_gpu": r["rows_local"], "emb_dim": r["d"],
                        "parallelism": f"row-shard{world}" if world > 1 or FORCE_SHARD else "single",
@@ -418,6 +458,16 @@ def main():
             out["fp32"] = {"value": round(alt["K"] * B / alt["dt"], 1), "unit": "samples/s",
                            "ms_per_step": round(alt["dt"] / alt["K"] * 1e3, 4), "steps": alt["K"],
                            "roofline": alt["roofline"], "final_loss": round(alt["loss"], 5)}
+        if alt16 is not None:
+            out["c3_bf16_fwd"] = {
+                "value": round(alt16["K"] * B / alt16["dt"], 1), "unit": "samples/s",
+                "ms_per_step": round(alt16["dt"] / alt16["K"] * 1e3, 4), "steps": alt16["K"],
+                "dtype": "bf16 forward GEMMs / fp32 backward",
+                "gemm_precision": {"bf16 operands (fp32 accumulation)": [
+                    "mm_proj x W_p", "bilinear U = V W", "MLP layer 1 c W_a", "MLP layer 2 h1 W_b"],
+                    "fp32 operands": ["every backward GEMM: dh2 W_b, dW_b, dh1 W_a (dc), dW_a, dU W^T, dW, dW_p",
+                                      "all non-GEMM arithmetic, master weights, Adam"]},
+                "roofline": alt16["roofline"], "final_loss": round(alt16["loss"], 5)}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, world)
         print(json.dumps(out), flush=True)

@@ -1139,6 +1139,229 @@ __global__ void __launch_bounds__(256) adam_prefetch_kernel(float* __restrict__ 
   }
 }
 
+// ---- The same ahead-of-time catch-up in two passes (single GPU, with pre-claims: the bench and
+// every trainer step given a next batch of its own shape).  The one-pass kernel above is a chain
+// of dependent round trips per 16-entry scan (id -> map -> last -> returning CAS -> pend -> row
+// loads) replayed two rows at a time by ONE wave per SIMD: it measured 20 % VALU issue over
+// 190-257 us.  Here:
+//   pass 1 (adam_pretag_kernel): every entry posts its tagged claim with one non-returning
+//     atomic max -- the smallest entry index of an id wins, as the claim at step t + 1 expects;
+//   pass 2 (adam_prefetch2_kernel): one entry per lane and no atomics: the winning entry of a row
+//     this batch does not touch takes the row (last[r] = T, pend[r] consumed), a wave sorts its
+//     rows by replay start and replays them FOUR at a time (eight independent update chains per
+//     lane at D = 128) while the next four rows' loads are in flight; the schedule constants of
+//     the last FBN_PF_WIN steps sit in LDS and each step's are read one step ahead.
+// Same operations in the same order per row: bit-identical to the one-pass kernel and to eager.
+#define FBN_PF_WIN 256
+
+__global__ void __launch_bounds__(256) adam_pretag_kernel(ClaimSrc cs, int n, const int* __restrict__ step) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const unsigned long long T = (unsigned long long)(*step + 1);
+  const long long b = i / (cs.L + 1), tt = i - b * (cs.L + 1);
+  const long long id = tt == 0 ? cs.item[b] : cs.seq[b * cs.L + (tt - 1)];
+  if (id > 0 && id < cs.V) atomicMax(cs.pre + id, (T << 32) | (0xFFFFFFFFull - (unsigned long long)i));
+}
+
+// adam_tab1 with the step's constants as (w1, nss, rbc2s, dmul): the same operations, same order
+template <bool DW, int N>
+__device__ __forceinline__ void adam_tabk(typename FVec<N>::T& pp, typename FVec<N>::T& mm, typename FVec<N>::T& vv,
+                                          typename FVec<N>::T gg, float wd, float b2, float omb2, float eps,
+                                          f32x4 k) {
+#pragma unroll
+  for (int e = 0; e < N; ++e) {
+    const float g = __builtin_fmaf(wd, pp[e], gg[e]);
+    float p = pp[e];
+    if (DW) p = p * k[3];
+    mm[e] = __builtin_fmaf(k[0], g - mm[e], mm[e]);
+    vv[e] = __builtin_fmaf(omb2 * g, g, vv[e] * b2);
+    const float den = __builtin_fmaf(__builtin_amdgcn_sqrtf(vv[e]), k[2], eps);
+    pp[e] = __builtin_fmaf(k[1] * mm[e], __builtin_amdgcn_rcpf(den), p);
+  }
+}
+__device__ __forceinline__ f32x4 consts4(const AdamConsts& k) { return (f32x4){k.w1, k.nss, k.rbc2s, k.dmul}; }
+
+// The replay engine of the two-pass prefetch and the window pass: a wave's rows (one per lane:
+// row r, first zero-gradient step key -- INT_MAX = none --, deferred vector pe), sorted by key,
+// brought to T steps four at a time.  win: LDS constants of steps [w0, T] (w0 = max(0, T - FBN_PF_WIN)).
+template <int D, bool DW>
+__device__ __forceinline__ void replay4_sorted(int r, int key, int pe, int cnt, int T, int w0,
+                                               const f32x4* __restrict__ win, float* __restrict__ p,
+                                               float* __restrict__ m, float* __restrict__ v,
+                                               const AdamConsts* __restrict__ table, float wd, float b2,
+                                               float omb2, float eps, const PendSrc& ps, int lane) {
+  typedef typename WideRow<D>::V V;
+  constexpr int N = WideRow<D>::N;
+  // ascending replay start (descending replay length); rows past cnt last
+#pragma unroll
+  for (int kk = 2; kk <= 64; kk <<= 1)
+#pragma unroll
+    for (int j = kk >> 1; j > 0; j >>= 1) {
+      const int ok = __shfl_xor(key, j, 64), orr = __shfl_xor(r, j, 64), ope = __shfl_xor(pe, j, 64);
+      const bool up = (lane & kk) == 0, lower = (lane & j) == 0;
+      if (lower == up ? ok < key : ok > key) {
+        key = ok;
+        r = orr;
+        pe = ope;
+      }
+    }
+  // group slot x of the rows at j0: (row, first zero step, deferred vector); past cnt: row 0, no steps
+  auto get = [&](int idx, int& rr, int& kk, int& pp) {   // idx wave-uniform
+    const int sl = idx < cnt ? idx : 0;
+    rr = __builtin_amdgcn_readlane(r, sl);
+    kk = __builtin_amdgcn_readlane(key, sl);
+    pp = __builtin_amdgcn_readlane(pe, sl);
+    if (idx >= cnt) { rr = 0; kk = T; pp = -1; }
+  };
+  auto load = [&](WideRow<D>& x, int rr, int kk, int pp) {
+    wide_load<D>(x, p, m, v, rr, pp >= 0 ? kk - 1 : kk, pp, ps, lane);
+  };
+  WideRow<D> cur[4];
+  int cr[4], ck[4], cp[4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    get(x, cr[x], ck[x], cp[x]);
+    load(cur[x], cr[x], ck[x], cp[x]);
+  }
+  const V zero = {};
+  for (int j0 = 0; j0 < cnt; j0 += 4) {
+    WideRow<D> nxt[4];
+    int nr[4], nk[4], np[4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      get(j0 + 4 + x, nr[x], nk[x], np[x]);
+      load(nxt[x], nr[x], nk[x], np[x]);   // past the last group: row 0, discarded
+    }
+    // deferred-gradient steps (step ck - 1 with its stored vector and clip coefficient)
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+      if (cp[x] >= 0) {
+        const int s = ck[x] - 1;
+        adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, cur[x].g * cur[x].c, wd, b2, omb2, eps,
+                         s >= w0 ? win[s - w0] : consts4(table[s]));
+      }
+    // steps older than the LDS window (a row lagging more than FBN_PF_WIN steps): global table
+    int s0[4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      s0[x] = ck[x];
+      for (; s0[x] < w0; ++s0[x])
+        adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, zero, wd, b2, omb2, eps, consts4(table[s0[x]]));
+    }
+    // all four rows side by side for the steps they all still need, constants read a step ahead
+    const int n0 = T - s0[0], n1 = T - s0[1], n2 = T - s0[2], n3 = T - s0[3];
+    const int common = min(min(n0, n1), min(n2, n3));
+    const int most = max(max(n0, n1), max(n2, n3));
+    f32x4 kc[4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) kc[x] = win[s0[x] - w0];
+    for (int it = 0; it < common; ++it) {
+      f32x4 kn[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) kn[x] = win[s0[x] - w0 + it + 1];   // <= T - w0: in the window
+#pragma unroll
+      for (int x = 0; x < 4; ++x) adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, zero, wd, b2, omb2, eps, kc[x]);
+#pragma unroll
+      for (int x = 0; x < 4; ++x) kc[x] = kn[x];
+    }
+    // the longer rows' remaining steps (short after the sort)
+    for (int it = common; it < most; ++it) {
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+        if (it < T - s0[x])
+          adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, zero, wd, b2, omb2, eps, win[s0[x] - w0 + it]);
+    }
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+      if (j0 + x < cnt) wide_store<D>(cur[x], p, m, v, cr[x], lane);
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      cur[x] = nxt[x];
+      cr[x] = nr[x];
+      ck[x] = nk[x];
+      cp[x] = np[x];
+    }
+  }
+}
+
+
+template <int D, bool DW>
+__global__ void __launch_bounds__(256) adam_prefetch2_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                             float* __restrict__ v, ClaimSrc cs, int n,
+                                                             int* __restrict__ last,
+                                                             const AdamConsts* __restrict__ table,
+                                                             const int* __restrict__ step, float wd, float b2,
+                                                             float omb2, float eps, PendSrc ps) {
+  __shared__ f32x4 win[FBN_PF_WIN + 1];   // constants of steps [w0, T]
+  const int T = *step + 1;
+  const int w0 = T > FBN_PF_WIN ? T - FBN_PF_WIN : 0;
+  for (int s = threadIdx.x; s <= T - w0; s += blockDim.x) win[s] = consts4(table[w0 + s]);
+  const int lane = threadIdx.x & 63;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  int r = 0, key = 0x7fffffff, pe = -1;
+  if (i < n) {
+    const long long b = i / (cs.L + 1), tt = i - b * (cs.L + 1);
+    const long long id = tt == 0 ? cs.item[b] : cs.seq[b * cs.L + (tt - 1)];
+    if (id > 0 && id < cs.V) {
+      const unsigned long long pv = cs.pre[id];
+      if ((int)(pv >> 32) == T && (0xFFFFFFFFu - (unsigned)pv) == (unsigned)i && cs.map[id] == -1) {
+        const int k0 = last[id];
+        if (k0 < T) {   // this entry owns the row: its replay through step T - 1
+          r = (int)id;
+          if (ps.pend) pe = ps.pend[id];
+          key = k0 + (pe >= 0 ? 1 : 0);   // first zero-gradient step (after the deferred one)
+          last[id] = T;
+          if (pe >= 0) ps.pend[id] = -1;
+        }
+      }
+    }
+  }
+  __syncthreads();   // the LDS window (no barrier after this point)
+  const int cnt = __popcll(__ballot(key != 0x7fffffff));
+  if (cnt == 0) return;
+  replay4_sorted<D, DW>(r, key, pe, cnt, T, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
+}
+
+// The rolling window (step mod F) with the replay engine (D >= 128): FBN_WIN_ROWS rows per wave
+// (one per lane), so a window of ~1e5 rows (C5's 12.5 M-row shard: 97.7 K rows replaying up to F
+// steps each) spreads over thousands of waves instead of one wave per SIMD; claimed rows are left
+// to their claiming entry, as in adam_catchup_kernel.
+#define FBN_WIN_ROWS 16
+template <int D, bool DW>
+__global__ void __launch_bounds__(256) adam_window2_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                           float* __restrict__ v, const int* __restrict__ map,
+                                                           long long nrows, int F, long long chunk,
+                                                           int* __restrict__ last, const AdamConsts* __restrict__ table,
+                                                           const int* __restrict__ step, float wd, float b2,
+                                                           float omb2, float eps, PendSrc ps) {
+  __shared__ f32x4 win[FBN_PF_WIN + 1];   // constants of steps [w0, t]
+  const int t = *step;
+  const int w0 = t > FBN_PF_WIN ? t - FBN_PF_WIN : 0;
+  for (int s = threadIdx.x; s <= t - w0; s += blockDim.x) win[s] = consts4(table[w0 + s]);
+  const long long roll0 = (long long)(t % F) * chunk;
+  const long long nroll = roll0 < nrows ? min(chunk, nrows - roll0) : 0;
+  const int lane = threadIdx.x & 63;
+  const long long j = ((((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * FBN_WIN_ROWS) + lane;
+  int r = 0, key = 0x7fffffff, pe = -1;
+  if (lane < FBN_WIN_ROWS && j < nroll) {
+    const long long rr = roll0 + j;
+    if (!map || map[rr] == -1) {
+      const int k0 = last[rr];
+      if (k0 < t) {
+        r = (int)rr;
+        if (ps.pend) pe = ps.pend[rr];
+        key = k0 + (pe >= 0 ? 1 : 0);
+        last[rr] = t;
+        if (pe >= 0) ps.pend[rr] = -1;
+      }
+    }
+  }
+  __syncthreads();   // the LDS window (no barrier after this point)
+  const int cnt = __popcll(__ballot(key != 0x7fffffff));
+  if (cnt == 0) return;
+  replay4_sorted<D, DW>(r, key, pe, cnt, t, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
+}
+
 // every row up to `step` (checkpoint / evaluation)
 template <int D, bool DW>
 __global__ void __launch_bounds__(256) adam_flush_kernel(float* __restrict__ p, float* __restrict__ m,
@@ -1664,6 +1887,30 @@ extern "C" int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, i
     return FBN_ERR_ARG;
   }
   const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
+  // the window alone at D >= 128: the replay engine over FBN_WIN_ROWS rows per wave
+  // (FBN_WINDOW_ONEPASS=1 keeps adam_catchup_kernel, A/B)
+  static const bool wone = getenv("FBN_WINDOW_ONEPASS") && atoi(getenv("FBN_WINDOW_ONEPASS")) == 1;
+  if (parts == 2 && (D == 128 || D == 256) && !wone) {
+    const long long waves = (chunk + FBN_WIN_ROWS - 1) / FBN_WIN_ROWS;
+    const dim3 g2((unsigned)((waves + 3) / 4));
+    if (D == 128) {
+      if (decoupled)
+        hipLaunchKernelGGL((adam_window2_kernel<128, true>), g2, dim3(256), 0, st, p, m, v, map, nrows, F, chunk, last,
+                           (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+      else
+        hipLaunchKernelGGL((adam_window2_kernel<128, false>), g2, dim3(256), 0, st, p, m, v, map, nrows, F, chunk, last,
+                           (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+    } else {
+      if (decoupled)
+        hipLaunchKernelGGL((adam_window2_kernel<256, true>), g2, dim3(256), 0, st, p, m, v, map, nrows, F, chunk, last,
+                           (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+      else
+        hipLaunchKernelGGL((adam_window2_kernel<256, false>), g2, dim3(256), 0, st, p, m, v, map, nrows, F, chunk, last,
+                           (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+    }
+    FBN_CHECK_LAUNCH();
+    return FBN_OK;
+  }
   // one wave per SCAN items (16 at D >= 64, else 64; sorted and compacted inside the kernel)
   const long long scan = D >= 64 ? 16 : 64;
   const dim3 grid((unsigned)std::min<long long>(cap, (items + 4 * scan - 1) / (4 * scan)));
@@ -1700,6 +1947,30 @@ extern "C" int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B,
   static const int pcap = getenv("FBN_PREFETCH_BLOCKS") ? atoi(getenv("FBN_PREFETCH_BLOCKS")) : 256;   // tools/ab_prefetch.sh
   const dim3 grid((unsigned)std::min<long long>(pcap, (n + 63) / 64));
   hipStream_t st = (hipStream_t)stream;
+  // with pre-claims: the two-pass form (FBN_PREFETCH_ONEPASS=1 keeps the one-pass kernel, A/B)
+  static const bool onepass = getenv("FBN_PREFETCH_ONEPASS") && atoi(getenv("FBN_PREFETCH_ONEPASS")) == 1;
+  if (preclaim && !onepass) {
+    const dim3 g2((unsigned)((n + 255) / 256));
+    hipLaunchKernelGGL(adam_pretag_kernel, g2, dim3(256), 0, st, cs, (int)n, step);
+    FBN_CHECK_LAUNCH();
+    if (D == 128) {
+      if (decoupled)
+        hipLaunchKernelGGL((adam_prefetch2_kernel<128, true>), g2, dim3(256), 0, st, p, m, v, cs, (int)n, last,
+                           (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+      else
+        hipLaunchKernelGGL((adam_prefetch2_kernel<128, false>), g2, dim3(256), 0, st, p, m, v, cs, (int)n, last,
+                           (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+    } else {
+      if (decoupled)
+        hipLaunchKernelGGL((adam_prefetch2_kernel<256, true>), g2, dim3(256), 0, st, p, m, v, cs, (int)n, last,
+                           (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+      else
+        hipLaunchKernelGGL((adam_prefetch2_kernel<256, false>), g2, dim3(256), 0, st, p, m, v, cs, (int)n, last,
+                           (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+    }
+    FBN_CHECK_LAUNCH();
+    return FBN_OK;
+  }
   if (D == 128) {
     if (decoupled)
       hipLaunchKernelGGL((adam_prefetch_kernel<128, true>), grid, dim3(256), 0, st, p, m, v, cs, (int)n, last,

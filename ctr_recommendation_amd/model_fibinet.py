@@ -17,8 +17,9 @@ reference ``train_fibinet.py`` (torch Adam, clip_grad_norm_) drives it as-is.
 
 Opt-in extensions the reference's config names but its code ignores (off unless
 ``honour_config: true`` is set in model_cfg): ``vocab_size``, ``bilinear_type``,
-``senet_reduction``, ``net_dropout``.  ``compute_dtype: bf16`` runs the GEMMs with bf16
-operands and fp32 accumulation (config C3).
+``senet_reduction``, ``net_dropout``.  ``compute_dtype: bf16`` runs every GEMM with bf16
+operands and fp32 accumulation; ``compute_dtype: bf16_fwd`` only the forward GEMMs, the backward
+in fp32 (config C3's "bf16 fwd / fp32 grad accum").
 """
 from __future__ import annotations
 
@@ -118,7 +119,13 @@ class MM_FiBiNET(nn.Module):
         btype = model_cfg.get("bilinear_type", "all") if honour else "all"
         red = int(model_cfg.get("senet_reduction", 2)) if honour else 2
         self.dropout_p = float(model_cfg.get("net_dropout", 0.2)) if honour else 0.2
-        self.compute_bf16 = str(model_cfg.get("compute_dtype", "fp32")).lower() in ("bf16", "bfloat16")
+        cdt = str(model_cfg.get("compute_dtype", "fp32")).lower()
+        if cdt not in ("fp32", "float32", "bf16", "bfloat16", "bf16_fwd"):
+            raise ValueError(f"compute_dtype must be 'fp32', 'bf16' or 'bf16_fwd', not {cdt!r}")
+        # bf16: every GEMM operand bf16 (forward and backward); bf16_fwd: the forward GEMMs take bf16
+        # operands, the backward runs in fp32 from fp32 activations (C3's "bf16 fwd / fp32 grad")
+        self.compute_bf16 = cdt in ("bf16", "bfloat16")
+        self.compute_fwd16 = cdt == "bf16_fwd"
         d = self.emb_dim
         # creation order == reference (:100-136)
         self.item_emb = nn.Embedding(vocab, d, padding_idx=0)
@@ -148,7 +155,8 @@ class MM_FiBiNET(nn.Module):
 
     def _fwd_cfg(self) -> ops.FwdConfig:
         return ops.FwdConfig(d=self.emb_dim, L=0, training=self.training, p_drop=self.dropout_p,
-                             bf16=self.compute_bf16, bilinear_each=self.bilinear.bilinear_type == "each",
+                             bf16=self.compute_bf16, fwd16=self.compute_fwd16,
+                             bilinear_each=self.bilinear.bilinear_type == "each",
                              R=self.senet.excitation[0].out_features)
 
     def _rng_state(self, device) -> torch.Tensor:

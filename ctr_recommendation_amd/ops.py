@@ -162,6 +162,9 @@ class FwdConfig:
     training: bool
     p_drop: float
     bf16: bool = False
+    # forward GEMM operands rounded to bf16 (fp32 accumulation), the rest of the forward and the
+    # whole backward fp32 from fp32 activations (bf16 must be False)
+    fwd16: bool = False
     bilinear_each: bool = False
     R: int = 3
 
@@ -284,12 +287,14 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     Lr = 0 if seq is None else L
     x_mm = batch["item_emb_d128"]
     bf = cfg.bf16
+    f16 = cfg.fwd16 and not bf            # bf16 forward GEMM operands only
+    g16 = bf or f16                       # the forward GEMMs take bf16 operands
     # w16_ready: the caller already converted this step's bf16 images (a["w16"]) on another stream
-    w16 = (a["w16"] if w16_ready else bf16_weights(p, d, a, st, x=x_mm)) if bf else None
+    w16 = (a["w16"] if w16_ready else bf16_weights(p, d, a, st, x=x_mm)) if g16 else None
     a["w16"] = w16
     hmm = buf("hmm", (B, d))
-    gemm(w16["x"] if bf else x_mm, w16["Wp"] if bf else p["mm_proj.0.weight"], hmm, B, d, 128, 128, 128, d, False,
-         True, bias=p["mm_proj.0.bias"], bf16=bf, stream=st)
+    gemm(w16["x"] if g16 else x_mm, w16["Wp"] if g16 else p["mm_proj.0.weight"], hmm, B, d, 128, 128, 128, d, False,
+         True, bias=p["mm_proj.0.bias"], bf16=g16, stream=st)
     if hooks and "after_mmproj" in hooks:         # trainer: side-stream work forked here
         hooks["after_mmproj"]()
     X = buf("X", (B, 2, d))                     # fields 3 and 5 (the backward recomputes 1, 2, 4)
@@ -339,6 +344,8 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     elif not cfg.bilinear_each:
         if bf:   # B(k,n) = W[k][n]: K-contiguous image is W^T
             gemm(Vc16, w16["WT"], U, 5 * B, d, d, d, d, d, False, True, bf16=True, stream=st)
+        elif f16:   # the fp32 fields rounded to bf16 on load
+            gemm(Vc, w16["WT"], U, 5 * B, d, d, d, d, d, False, True, bf16=True, stream=st)
         else:
             gemm(Vc, p["bilinear.W"], U, 5 * B, d, d, d, d, d, False, False, stream=st)
     else:
@@ -362,7 +369,7 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     if split_c:
         gemm_split(Vc16, w16["Wa"], h1pre, B, H1, KC, 5 * d, KC, H1, False, True, bias=p["mlp.0.bias"], stream=st,
                    stats=t1, A2=c[:, 5 * d:], lda2=KC, kseg=5 * d)
-    elif bf:
+    elif bf or f16:   # bf16_fwd: the fp32 MLP input rounded to bf16 on load
         gemm(c, w16["Wa"], h1pre, B, H1, KC, KC, KC, H1, False, True, bias=p["mlp.0.bias"], bf16=True, stream=st,
              stats=t1)
     else:
@@ -375,7 +382,7 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     mean1, inv1 = buf("mean1", (H1,)), buf("inv1", (H1,))
     mean2, inv2 = buf("mean2", (H2,)), buf("inv2", (H2,))
     h1 = buf("h1", (B, H1))
-    h1_16 = buf("h1_16", (B, H1), torch.bfloat16) if bf else None
+    h1_16 = buf("h1_16", (B, H1), torch.bfloat16) if g16 else None
     h2pre = buf("h2pre", (B, H2))
     h2 = buf("h2", (B, H2))
     p_drop = cfg.p_drop if cfg.training else 0.0
@@ -395,7 +402,7 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     a["lean_h1"] = lean
     call("fbn_bn_act_fwd", ptr(h1pre), None if lean else ptr(h1), B, H1, ptr(mean1), ptr(inv1), ptr(p["mlp.1.weight"]),
          ptr(p["mlp.1.bias"]), float(p_drop), ptr(rng), 1, ptr(m1), ptr(mi1), ptr(h1_16), st)
-    if bf:
+    if g16:
         gemm(h1_16, w16["Wb"], h2pre, B, H2, H1, H1, H1, H2, False, True, bias=p["mlp.4.bias"], bf16=True, stream=st,
              stats=t2)
     else:

@@ -210,7 +210,7 @@ class FiBiNETTrainer:
         self.d = shape_model.emb_dim
         self.p_drop = shape_model.dropout_p
         self.fcfg = ops.FwdConfig(d=self.d, L=max_len, training=True, p_drop=self.p_drop,
-                                  bf16=shape_model.compute_bf16,
+                                  bf16=shape_model.compute_bf16, fwd16=shape_model.compute_fwd16,
                                   bilinear_each=shape_model.bilinear.bilinear_type == "each",
                                   R=shape_model.senet.excitation[0].out_features)
         self.V = init_state[TABLE].shape[0]

@@ -4,7 +4,8 @@
   and deferred table gradients -- and in the drop-in under the reference loop verbatim
   (torch Adam + clip_grad_norm_ + OneCycleLR, src/train_fibinet.py:78-92,113-123);
 * AUC of the HIP path vs the oracle on the same 65 536-sample eval set after training steps
-  (north star: |dAUC| <= 1e-4 fp32; the bf16 dAUC is recorded and held to 2e-3);
+  (north star: |dAUC| <= 1e-4 for fp32 and bf16_fwd; the all-bf16 dAUC is recorded and held to
+  its measured value plus margin);
 * the BCE log clamp (p rounding to exactly 0 or 1, src/train_fibinet.py:79 BCELoss);
 * the configs' full shapes: C2 (d=16, V=1M, B=4096) and C3 (d=128, V=1.25M, B=8192) through
   the drop-in forward + backward and one native-trainer step, against the oracle;
@@ -213,21 +214,38 @@ def test_auc_parity_after_training(hip_device, d):
     assert abs(compute_auc(y, p_hip) - oracle_auc(y, p_twin)) <= 1e-5
 
 
-def test_auc_bf16_mode_vs_oracle(hip_device):
-    """C3's bf16 GEMM-operand mode vs the fp32 oracle, same steps and eval set as above.  bf16
-    operands carry 8 significant bits, so the 1e-4 bar is the fp32 path's; this records the
-    bf16 dAUC and holds it to 2e-3."""
-    d, V, B = 128, 20000, 1024
+# measured bars of the reduced-precision modes (profiles/r03_auc_parity.json holds the values)
+PRECISION_AUC_BAR = {"fp32": 1e-4, "bf16_fwd": 1e-4, "bf16": 3e-4}
+
+
+@pytest.mark.parametrize("shape", ["small", "C3"])
+def test_auc_precision_modes_vs_oracle(hip_device, shape):
+    """The three compute modes vs ONE fp32 oracle trajectory: 8 training steps from the same init
+    (OneCycle over 40), then eval-mode probabilities on the 65 536-sample eval set.
+      fp32      -- the reference's precision;
+      bf16_fwd  -- C3's "bf16 fwd / fp32 grad accum": forward GEMM operands bf16, backward fp32;
+      bf16      -- the benched headline mode: every GEMM operand bf16 (forward and backward).
+    small: d 128, V 20 000, B 1024; C3: d 128, V 1.25 M, B 8192 (the config's own shape).
+    |dAUC| and max |dp| are written to $FBN_PARITY_OUT/auc_parity_<shape>.json (default
+    gpurun_out/parity/) and held to PRECISION_AUC_BAR (north star 1e-4 for fp32 and bf16_fwd; the
+    all-bf16 mode to its measured value plus margin)."""
+    import json
+    import os
+    d = 128
+    V, B = (20000, 1024) if shape == "small" else (1_250_000, 8192)
     cfg = dict({"embedding_dim": d, "vocab_size": V}, **NO_DROP)
     torch.manual_seed(0)
     ref = oracle_build(None, cfg, honour_config=True)
     init = {k: v.clone() for k, v in ref.state_dict().items()}
     otr = OracleTrainer(ref, total_steps=40)
-    htr = FiBiNETTrainer(dict(cfg, compute_dtype="bf16"), total_steps=40, batch_size=B, device=hip_device,
-                         init_state=init)
+    htrs = {m: FiBiNETTrainer(dict(cfg, compute_dtype=m), total_steps=40, batch_size=B, device=hip_device,
+                              init_state=init) for m in PRECISION_AUC_BAR}
+    del init
     for s in range(8):
         b, y = make_batch(800 + s, B, V, signal="fields")
-        htr.step(_to(b, hip_device), y.to(hip_device))
+        db, dy = _to(b, hip_device), y.to(hip_device)
+        for htr in htrs.values():
+            htr.step(db, dy)
         otr.step(b, y)
     ref.eval()
 
@@ -235,10 +253,23 @@ def test_auc_bf16_mode_vs_oracle(hip_device):
         with torch.no_grad():
             return ref(b).numpy()
     y, p_ref = _eval_auc(pr, V)
-    _, p_hip = _eval_auc(lambda b: htr.predict(_to(b, hip_device)).cpu().numpy(), V)
-    da = abs(compute_auc(y, p_hip) - oracle_auc(y, p_ref))
-    print(f"bf16 mode dAUC vs fp32 oracle: {da:.2e}")
-    assert da <= 2e-3, da
+    a_ref = oracle_auc(y, p_ref)
+    rec = {"shape": {"d": d, "V": V, "B": B, "train_steps": 8, "eval_samples": int(y.size)},
+           "oracle_auc": a_ref, "modes": {}}
+    for mode, htr in htrs.items():
+        _, p_hip = _eval_auc(lambda b: htr.predict(_to(b, hip_device)).cpu().numpy(), V)
+        rec["modes"][mode] = {"auc": compute_auc(y, p_hip), "dAUC": abs(compute_auc(y, p_hip) - a_ref),
+                              "max_abs_dp": float(np.abs(p_hip - p_ref).max()),
+                              "mean_abs_dp": float(np.abs(p_hip - p_ref).mean()),
+                              "bar": PRECISION_AUC_BAR[mode]}
+    out = os.environ.get("FBN_PARITY_OUT", os.path.join("gpurun_out", "parity"))
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, f"auc_parity_{shape}.json"), "w") as f:
+        json.dump(rec, f, indent=1)
+    print(json.dumps(rec))
+    assert a_ref > 0.55, a_ref
+    for mode, r in rec["modes"].items():
+        assert r["dAUC"] <= r["bar"], (mode, r)
 
 
 # ---------------------------------------------------------------- BCE clamp
@@ -382,37 +413,49 @@ def test_config_size_dropin_fwd_bwd(hip_device, cfgname, d, V, B):
 
 @pytest.mark.parametrize("cfgname,d,V,B,dtype", [("C2", 16, 1_000_000, 4096, "fp32"),
                                                  ("C3", 128, 1_250_000, 8192, "fp32"),
+                                                 ("C3", 128, 1_250_000, 8192, "bf16_fwd"),
                                                  ("C3", 128, 1_250_000, 8192, "bf16")])
 def test_config_size_trainer_step(hip_device, cfgname, d, V, B, dtype):
     """One native-trainer step + eval forward at the config's shape vs one oracle step.  fp32:
     loss 2e-5, eval probabilities after the step 2e-3 (Adam's first step is sign(g)*lr per
-    element), AUC of those probabilities 1e-4.  bf16 (C3's benched mode): loss 2 %, AUC 2e-3."""
+    element), AUC of those probabilities 1e-4.  bf16_fwd / bf16: loss 1e-3 / 2e-3 relative,
+    AUC 1e-4 / 3e-4 (the values are printed and written to $FBN_PARITY_OUT)."""
+    import json
+    import os
     cfg = dict({"embedding_dim": d, "vocab_size": V}, **NO_DROP)
     torch.manual_seed(0)
     ref = oracle_build(None, cfg, honour_config=True)
     init = {k: v.clone() for k, v in ref.state_dict().items()}
     otr = OracleTrainer(ref, total_steps=100)
-    hcfg = dict(cfg, compute_dtype="bf16") if dtype == "bf16" else cfg
+    hcfg = dict(cfg, compute_dtype=dtype)
     htr = FiBiNETTrainer(hcfg, total_steps=100, batch_size=B, device=hip_device, init_state=init)
     del init
     b, y = make_batch(21, B, V)
     lh = htr.step(_to(b, hip_device), y.to(hip_device)).item()
     lr_, _ = otr.step(b, y)
-    if dtype == "fp32":
-        assert abs(lh - lr_) < 2e-5, (lh, lr_)
-    else:
-        assert abs(lh - lr_) <= 0.02 * lr_, (lh, lr_)
     be, ye = make_batch(22, B, V)
     ref.eval()
     with torch.no_grad():
         pr = ref(be).numpy()
     ph = htr.predict(_to(be, hip_device)).cpu().numpy()
     da = abs(compute_auc(ye.numpy(), ph) - oracle_auc(ye.numpy(), pr))
+    rec = {"config": cfgname, "dtype": dtype, "loss_hip": lh, "loss_oracle": lr_, "rel_dloss": abs(lh - lr_) / lr_,
+           "dAUC": da, "max_abs_dp": float(np.abs(ph - pr).max())}
+    print(json.dumps(rec))
+    out = os.environ.get("FBN_PARITY_OUT", os.path.join("gpurun_out", "parity"))
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, f"one_step_{cfgname}_{dtype}.json"), "w") as f:
+        json.dump(rec, f, indent=1)
     if dtype == "fp32":
+        assert abs(lh - lr_) < 2e-5, (lh, lr_)
         assert np.abs(ph - pr).max() < 2e-3
         assert da <= 1e-4, da
+    elif dtype == "bf16_fwd":
+        assert abs(lh - lr_) <= 1e-3 * lr_, (lh, lr_)
+        assert da <= 1e-4, da
     else:
-        assert da <= 2e-3, da
+        assert abs(lh - lr_) <= 2e-3 * lr_, (lh, lr_)
+        assert da <= 3e-4, da
 
 
 # ---------------------------------------------------------------- opt-in config surface

@@ -227,29 +227,37 @@ def test_deferred_table_grads_bit_identical(hip_device):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("defer", [True, False])
-def test_next_batch_prefetch_bit_identical(hip_device, defer):
+@pytest.mark.parametrize("defer,dups,d", [(True, False, 128), (False, False, 128), (True, True, 128),
+                                          (True, True, 256)])
+def test_next_batch_prefetch_bit_identical(hip_device, defer, dups, d):
     """fbn_adam_prefetch: with step(..., next_batch=...) the next batch's rows that this batch does
     not touch are brought up to date on the side stream during this step.  Against the same run
     without prefetch: losses, table, Adam moments, dense parameters and last[] bit-identical (ids
-    unique within a step, recurring across steps, so prefetched rows also carry deferred gradients
-    and meet rolling windows).  The last step's next_batch is never used: rows prefetched for it
-    are simply up to date early."""
+    recurring across steps, so prefetched rows also carry deferred gradients and meet rolling
+    windows).  dups: ids drawn with replacement from a small pool, so one row is named by several
+    entries of a batch -- the two-pass prefetch gives it to the entry whose tagged pre-claim won
+    (no CAS); both runs fold duplicates deterministically (fixed-point sums), as float atomics
+    would round in arrival order.  The last step's next_batch is never used: rows prefetched for it are simply up to
+    date early."""
     V, B, L, steps = 40000, 64, 20, 14
-    cfg = {"embedding_dim": 128, "vocab_size": V}
+    cfg = {"embedding_dim": d, "vocab_size": V}
     torch.manual_seed(0)
     init = oracle_build(None, cfg).state_dict()
+    # duplicates are folded by float atomics (order-dependent rounding) unless deterministic
     kw = dict(total_steps=20, batch_size=B, device=hip_device, init_state=init, table_adam="lazy", lazy_window=4,
-              defer_table_grads=defer)
+              defer_table_grads=defer, deterministic=dups)
     ref = FiBiNETTrainer(cfg, prefetch_rows=False, **kw)
     pre = FiBiNETTrainer(cfg, prefetch_rows=True, **kw)
     assert pre.prefetch_rows
     g = torch.Generator().manual_seed(7)
-    pool = torch.randperm(V - 1, generator=g)[:3000] + 1
+    pool = torch.randperm(V - 1, generator=g)[:3000 if not dups else 700] + 1
     batches = []
     for s in range(steps + 1):
         b, y = make_batch(300 + s, B, V)
-        ids = pool[torch.randperm(len(pool), generator=g)[:B * (L + 1)]].view(B, L + 1)
+        if dups:
+            ids = pool[torch.randint(0, len(pool), (B, L + 1), generator=g)]
+        else:
+            ids = pool[torch.randperm(len(pool), generator=g)[:B * (L + 1)]].view(B, L + 1)
         b["item_id"] = ids[:, 0].clone()
         seq = ids[:, 1:].clone()
         seq[b["item_seq"] == 0] = 0
