@@ -62,6 +62,9 @@ def parse():
     ap.add_argument("--lazy-window", type=int, default=128, help="lazy table-Adam window F (rows per step: V/F)")
     ap.add_argument("--zipf", type=float, default=0.0,
                     help="item / history ids ~ Zipf(s) (SURVEY 8(d): 1.05) instead of uniform")
+    ap.add_argument("--table-adam", default="lazy", choices=["lazy", "eager", "sparse"],
+                    help="item-table Adam: lazy (exact replay, default), eager (every row each step), sparse "
+                         "(opt-in non-parity C5 variant: touched rows only)")
     ap.add_argument("--no-prefetch", dest="prefetch", action="store_false",
                     help="N = 1: no ahead-of-time catch-up of the next batch's rows (fbn_adam_prefetch)")
     ap.add_argument("--prime", type=int, default=-1,
@@ -70,6 +73,8 @@ def parse():
                     help="N > 1 BatchNorm statistics: 'local' = per GPU, what the reference script does on a "
                          "multi-GPU box (nn.DataParallel, train_fibinet.py:69-70); 'sync' = over the global "
                          "batch (parity with one process on the global batch; 4 all-reduces per step)")
+    ap.add_argument("--no-other-bn", action="store_true",
+                    help="N > 1: skip the second measurement in the other BatchNorm mode")
     ap.add_argument("--no-fp32", dest="also_fp32", action="store_false",
                     help="skip the fp32 and bf16_fwd C3 measurements embedded in the line")
     return ap.parse_args()
@@ -157,7 +162,7 @@ def _initial_state(cfg, V, world, rank, dev):
 FORCE_SHARD = os.environ.get("FBN_BENCH_SHARD") == "1"
 
 
-def measure(args, dtype, world, rank, dev, rehearsal, backend):
+def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
     """Build a trainer for `dtype`, bring it to steady state, time K steps; returns the result dict."""
     from ctr_recommendation_amd.data import make_device_batches
     from ctr_recommendation_amd import ops
@@ -181,7 +186,8 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend):
     init = _initial_state(cfg, V, world, rank, dev)
     tr = FiBiNETTrainer(cfg, total_steps=total, batch_size=B, device=dev, rank=rank, world=world,
                         init_state=init, stage_on_cpu=rehearsal, lazy_window=F, prefetch_rows=args.prefetch,
-                        shard=sharded, sync_bn=args.bn == "sync")
+                        table_adam=args.table_adam,
+                        shard=sharded, sync_bn=(bn or args.bn) == "sync")
     del init
     batches = make_device_batches(nb, B, V, L, dev, seed=2025 + rank, zipf=args.zipf)
     graphs = []
@@ -410,6 +416,11 @@ def main():
         alt = measure(args, "fp32", world, rank, dev, rehearsal, backend)
         # C3's literal wording ("bf16 fwd / fp32 grad accum"): bf16 forward GEMMs, fp32 backward
         alt16 = measure(args, "bf16_fwd", world, rank, dev, rehearsal, backend)
+    other_bn = None
+    if world > 1 and not args.no_other_bn:
+        # both BatchNorm modes at N > 1: the other one as an embedded line (SyncBN = the parity mode)
+        other_bn = measure(args, args.dtype, world, rank, dev, rehearsal, backend,
+                           bn="sync" if args.bn == "local" else "local")
 
     if rank == 0:
         K, B, dt = r["K"], r["B"], r["dt"]
@@ -435,7 +446,7 @@ def main():
                        "parallelism": f"row-shard{world}" if world > 1 or FORCE_SHARD else "single",
                        "hipgraph": r["graphs"], **({"rehearsal": backend} if rehearsal else {}),
                        **({"batchnorm": "per-GPU statistics (nn.DataParallel semantics, train_fibinet.py:69-70)"
-                           if args.bn == "local" else "SyncBN (global-batch statistics)"}
+                           if args.bn == "local" else "SyncBN (global-batch statistics; the parity mode)"}
                           if world > 1 or FORCE_SHARD else {})},
             "host_enqueue_ms_per_step": round(r["t_host"] / K * 1e3, 4),
             **({"host_blocked_ms_per_step": round(r["t_wait"] / K * 1e3, 4)} if r["t_wait"] else {}),
@@ -468,6 +479,15 @@ def main():
                     "fp32 operands": ["every backward GEMM: dh2 W_b, dW_b, dh1 W_a (dc), dW_a, dU W^T, dW, dW_p",
                                       "all non-GEMM arithmetic, master weights, Adam"]},
                 "roofline": alt16["roofline"], "final_loss": round(alt16["loss"], 5)}
+        if other_bn is not None:
+            mode = "sync" if args.bn == "local" else "local"
+            out["syncbn" if mode == "sync" else "local_bn"] = {
+                "value": round(other_bn["K"] * B * world / other_bn["dt"], 1), "unit": "samples/s",
+                "ms_per_step": round(other_bn["dt"] / other_bn["K"] * 1e3, 4), "steps": other_bn["K"],
+                "batchnorm": ("SyncBN: statistics over the global batch -- the PARITY mode (one process on the "
+                              "global batch); 4 extra all-reduces per step") if mode == "sync" else
+                             "per-GPU statistics (nn.DataParallel semantics, train_fibinet.py:69-70)",
+                "final_loss": round(other_bn["loss"], 5)}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, world)
         print(json.dumps(out), flush=True)

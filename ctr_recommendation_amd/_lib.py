@@ -102,7 +102,7 @@ SIGNATURES = {
     "fbn_bilinear_supported": (I, [I]),
     "fbn_bilinear_fwd": (I, [P, P, P, I, I, I, P]),
     "fbn_bilinear_bwd": (I, [P, I, I, P, P, P, P, P, I, I, P]),
-    "fbn_collate": (I, [P, I, P, P, I, I, P, P, P, P, P, LL, P, I, P, P, P, P, P, P, P, P, P]),
+    "fbn_collate": (I, [P, I, P, P, I, I, P, P, P, P, P, LL, P, P, I, P, P, P, P, P, P, P, P, P]),
     "fbn_collate_zero_if": (I, [P, LL, P, P]),
 }
 

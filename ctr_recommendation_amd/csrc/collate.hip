@@ -29,8 +29,10 @@ struct CollateArgs {
   const int64_t* views;
   const int64_t* user;
   const float* label;         // [N] or null
-  const int* slot_of_id;      // [n_ids] row of emb, -1 = no item_info row
+  const int* slot_of_id;      // [n_ids] row of emb, -1 = no item_info row (dense index by id), or
+                              // with sorted_ids: [n_ids] row of emb of the k-th sorted id
   long long n_ids;
+  const int64_t* sorted_ids;  // null: dense index; else [n_ids] ascending ids (sparse / hashed ids)
   const float* emb;           // [rows][E] or null
   int E;                      // multiple of 4
   int64_t* o_item;
@@ -60,7 +62,17 @@ __global__ void __launch_bounds__(256) collate_kernel(CollateArgs a) {
     if (a.seq)
       for (int t = lane; t < a.L; t += 64) a.o_seq[b * a.L + t] = a.seq[r * a.Ls + a.seq_off + t];
     if (a.emb) {
-      const int row = (id >= 0 && id < a.n_ids) ? a.slot_of_id[id] : -1;
+      int row = -1;
+      if (!a.sorted_ids) {
+        row = (id >= 0 && id < a.n_ids) ? a.slot_of_id[id] : -1;
+      } else {   // lower bound over the sorted ids (wave-uniform: every lane takes the same path)
+        long long lo = 0, hi = a.n_ids;
+        while (lo < hi) {
+          const long long mid = (lo + hi) >> 1;
+          if (a.sorted_ids[mid] < id) lo = mid + 1; else hi = mid;
+        }
+        row = (lo < a.n_ids && a.sorted_ids[lo] == id) ? a.slot_of_id[lo] : -1;
+      }
       if (row < 0 && lane == 0) *a.missing = 1;
       for (int c = lane * 4; c < a.E; c += 256) {
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
@@ -79,7 +91,8 @@ __global__ void zero_if_kernel(float* x, long long n, const int* flag) {
 
 extern "C" int fbn_collate(const int64_t* perm, int B, const int64_t* item, const int64_t* seq, int Ls, int L,
                            const int64_t* likes, const int64_t* views, const int64_t* user, const float* label,
-                           const int* slot_of_id, long long n_ids, const float* emb, int E, int64_t* o_item,
+                           const int* slot_of_id, long long n_ids, const int64_t* sorted_ids, const float* emb,
+                           int E, int64_t* o_item,
                            int64_t* o_seq, int64_t* o_likes, int64_t* o_views, int64_t* o_user, float* o_label,
                            float* o_emb, int* missing, void* stream) {
   if (B <= 0) return FBN_OK;
@@ -93,7 +106,7 @@ extern "C" int fbn_collate(const int64_t* perm, int B, const int64_t* item, cons
     fbn_set_error("fbn_collate: every input column needs its output");
     return FBN_ERR_ARG;
   }
-  CollateArgs a{perm, B, item, seq, Ls, L, Ls - L, likes, views, user, label, slot_of_id, n_ids, emb, E,
+  CollateArgs a{perm, B, item, seq, Ls, L, Ls - L, likes, views, user, label, slot_of_id, n_ids, sorted_ids, emb, E,
                 o_item, o_seq, o_likes, o_views, o_user, o_label, o_emb, missing};
   const int blocks = (int)std::min<long long>(2048, ((long long)B + 3) / 4);
   hipLaunchKernelGGL(collate_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);

@@ -22,7 +22,7 @@
 #define FBN_MAXR 8   // max SENET reduced width supported (reference: 3)
 #define FBN_MAX_L 32 // max history length (the reference keeps the last 20)
 #ifndef FBN_HCH
-#define FBN_HCH 5    // history rows in flight per sample before they are summed (tools/time_fields.py)
+#define FBN_HCH 20   // history rows in flight per sample before they are summed (tools/time_fields.py)
 #endif
 
 struct FieldArgs {
@@ -171,21 +171,26 @@ __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
     }
     const int gbase = lane - q;
     for (int t0 = 0; t0 < L; t0 += HCH) {
+      // branch-free: every slot of the chunk issues its load (a padding or past-L slot reads row
+      // 0, an L2-resident line, and contributes +0 by a select) -- a load under a branch makes
+      // hipcc drain vmcnt(0) before the next, which serialised the chunk's round trips
       f32x4 hist[HCH];
+      bool live[HCH];
 #pragma unroll
       for (int u = 0; u < HCH; ++u) {
-        hist[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
         const int t = t0 + u;
-        if (t < L) {
-          int r = -1;
+        int r = -1;
 #pragma unroll
-          for (int j = 0; j < IPL; ++j)
-            if ((t / G) == j) r = __shfl(sid[j], gbase + (t % G), 64);
-          if (r >= 0) { hist[u] = load_row<D, MODE>(p, r, q); ++nnz; }
-        }
+        for (int j = 0; j < IPL; ++j)
+          if ((t / G) == j) r = __shfl(sid[j], gbase + (t % G), 64);
+        live[u] = t < L && r >= 0;
+        hist[u] = load_row<D, MODE>(p, live[u] ? r : 0, q);
       }
 #pragma unroll
-      for (int u = 0; u < HCH; ++u) hs += hist[u];
+      for (int u = 0; u < HCH; ++u) {
+        hs += live[u] ? hist[u] : (f32x4){0.f, 0.f, 0.f, 0.f};
+        nnz += live[u] ? 1 : 0;
+      }
     }
     if (bad) atomicOr(p.err, 1);        // any lane: history ids are validated by the lane holding them
 

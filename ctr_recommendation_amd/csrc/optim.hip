@@ -1322,6 +1322,75 @@ __global__ void __launch_bounds__(256) adam_prefetch2_kernel(float* __restrict__
   replay4_sorted<D, DW>(r, key, pe, cnt, T, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
 }
 
+// Single GPU, D >= 128: the step's row claims + the claimed rows' catch-up (fbn_adam_claim_catchup)
+// with one entry per lane.  A lane's row state -- its pre-claim tag, last[] and pend[] -- is loaded
+// in ONE round trip right after the id (they depend on the id only; nothing else writes them while
+// this kernel runs: the previous step's side work was joined before its step tail, this step's starts
+// after the claims), instead of id -> tag -> claim -> last -> pend one after another; the rows that
+// are behind are replayed by the four-row engine.  Claims are those of adam_catchup_kernel (tagged
+// pre-claim, else plain load + CAS; dup / hasdup written the same way).
+template <int D, bool DW>
+__global__ void __launch_bounds__(256) adam_claim2_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                          float* __restrict__ v, ClaimSrc cs, int n,
+                                                          int* __restrict__ last, const AdamConsts* __restrict__ table,
+                                                          const int* __restrict__ step, float wd, float b2,
+                                                          float omb2, float eps, PendSrc ps) {
+  __shared__ f32x4 win[FBN_PF_WIN + 1];
+  const int t = *step;
+  const int w0 = t > FBN_PF_WIN ? t - FBN_PF_WIN : 0;
+  const int lane = threadIdx.x & 63;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  int r = 0, key = 0x7fffffff, pe = -1;
+  if (i < n) {
+    const long long b = i / (cs.L + 1), tt = i - b * (cs.L + 1);
+    const long long id = tt == 0 ? cs.item[b] : cs.seq[b * cs.L + (tt - 1)];
+    int owner = -1, mine = -1;
+    if (id > 0 && id < cs.V) {
+      const unsigned long long pv = cs.pre ? cs.pre[id] : 0ull;
+      const int k0 = last[id];
+      const int pe0 = ps.pend ? ps.pend[id] : -1;
+      if ((int)(pv >> 32) == t && t > 0) {   // pre-claimed: the smallest entry index claims
+        owner = (int)(0xFFFFFFFFu - (unsigned)pv);
+        if (owner == (int)i) {
+          cs.map[id] = (int)i;
+          cs.slot_row[i] = (int)id;
+          mine = (int)id;
+          owner = -1;
+        }
+      } else {
+        owner = __hip_atomic_load(cs.map + id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (owner == -1) {
+          int expected = -1;
+          if (__hip_atomic_compare_exchange_strong(cs.map + id, &expected, (int)i, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)) {
+            cs.slot_row[i] = (int)id;
+            mine = (int)id;
+          } else {
+            owner = expected;
+          }
+        }
+      }
+      if (mine >= 0 && k0 < t) {
+        r = mine;
+        pe = pe0;
+        key = k0 + (pe0 >= 0 ? 1 : 0);
+        last[mine] = t;
+        if (pe0 >= 0) ps.pend[mine] = -1;
+      }
+    }
+    if (cs.dup) cs.dup[i] = owner;
+    if (cs.hasdup && owner >= 0) cs.hasdup[owner] = 1;
+  }
+  // stage the constants only where some wave of the block has rows to replay (block-uniform)
+  const int any = __syncthreads_or(key != 0x7fffffff);
+  if (!any) return;
+  for (int s = threadIdx.x; s <= t - w0; s += blockDim.x) win[s] = consts4(table[w0 + s]);
+  __syncthreads();
+  const int cnt = __popcll(__ballot(key != 0x7fffffff));
+  if (cnt == 0) return;
+  replay4_sorted<D, DW>(r, key, pe, cnt, t, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
+}
+
 // The rolling window (step mod F) with the replay engine (D >= 128): FBN_WIN_ROWS rows per wave
 // (one per lane), so a window of ~1e5 rows (C5's 12.5 M-row shard: 97.7 K rows replaying up to F
 // steps each) spreads over thousands of waves instead of one wave per SIMD; claimed rows are left
@@ -2055,6 +2124,29 @@ extern "C" int fbn_adam_claim_catchup(const int64_t* item, const int64_t* seq, i
   const long long chunk = (nrows + F - 1) / F;
   const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
   const ClaimSrc cs{item, L > 0 ? seq : nullptr, L, V, map, slot_row, dup, hasdup, preclaim};
+  // D >= 128: one entry per lane, row state in one round trip, four-row replay (adam_claim2_kernel);
+  // FBN_CLAIM_ONEPASS=1 keeps the 16-entry scan of adam_catchup_kernel (A/B)
+  static const bool cone = getenv("FBN_CLAIM_ONEPASS") && atoi(getenv("FBN_CLAIM_ONEPASS")) == 1;
+  if ((D == 128 || D == 256) && !cone) {
+    const dim3 g2((unsigned)((n + 255) / 256));
+    if (D == 128) {
+      if (decoupled)
+        hipLaunchKernelGGL((adam_claim2_kernel<128, true>), g2, dim3(256), 0, st, p, m, v, cs, (int)n, last,
+                           (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+      else
+        hipLaunchKernelGGL((adam_claim2_kernel<128, false>), g2, dim3(256), 0, st, p, m, v, cs, (int)n, last,
+                           (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+    } else {
+      if (decoupled)
+        hipLaunchKernelGGL((adam_claim2_kernel<256, true>), g2, dim3(256), 0, st, p, m, v, cs, (int)n, last,
+                           (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+      else
+        hipLaunchKernelGGL((adam_claim2_kernel<256, false>), g2, dim3(256), 0, st, p, m, v, cs, (int)n, last,
+                           (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+    }
+    FBN_CHECK_LAUNCH();
+    return FBN_OK;
+  }
   const long long scan = D >= 64 ? 16 : 64;
   const dim3 grid((unsigned)std::min<long long>(8192, (n + 4 * scan - 1) / (4 * scan)));
   if (decoupled) {

@@ -142,8 +142,10 @@ class RowExchange:
 
     @staticmethod
     def _key(item, seq):
-        # the prepared routing is used only for the very tensors it was computed from
-        return (item.data_ptr(), item.shape[0], 0 if seq is None else seq.data_ptr(), 0 if seq is None else seq.shape[1])
+        # the prepared routing is used only for the very tensors it was computed from, unmodified
+        # since (a copy_ into the same buffer bumps the version counter)
+        return (item.data_ptr(), item.shape[0], item._version, 0 if seq is None else seq.data_ptr(),
+                0 if seq is None else seq.shape[1], 0 if seq is None else seq._version)
 
     def prepare(self, item, seq, err, send_rows: bool = False, after=None) -> None:
         """Route the NEXT step's batch now, on a side stream (HIP device only), and deliver it to the
@@ -152,7 +154,8 @@ class RowExchange:
         and the packed ids on device (fbn_compact_routes), and both count vectors land in pinned
         host memory -- the next forward reads them without a sync on the main stream and runs no
         counts / ids all-to-all.  Used by the next forward() only if it gets the same
-        (unmodified) id tensors; otherwise that forward routes inline.  send_rows: also expose the
+        id tensors, unmodified (address, shape and version counter); otherwise that forward routes
+        inline.  send_rows: also expose the
         received padded blocks as self.next_lids [world * (cap + 1)] (negative = no row), ready on
         self.side -- the owner's table-Adam prefetch (fbn_adam_prefetch_rows) reads them."""
         self.next_lids = None

@@ -67,7 +67,11 @@ def read_parquet_columns(path: str) -> Dict[str, np.ndarray]:
 
 class ItemInfoTable:
     """item_info (``item_id`` -> ``item_emb_d128``) in HBM behind a dense id -> row index
-    (BatchCollator.__init__, src/dataloader.py:54-65: ``read_parquet(...).set_index("item_id")``)."""
+    (BatchCollator.__init__, src/dataloader.py:54-65: ``read_parquet(...).set_index("item_id")``),
+    or, when the ids are sparse (largest id > DENSE_FACTOR x rows + 2^20), behind the sorted ids."""
+
+    DENSE_FACTOR = 8
+    DENSE_SLACK = 1 << 20
 
     def __init__(self, item_ids: np.ndarray, emb: np.ndarray, device):
         item_ids = np.asarray(item_ids, dtype=np.int64)
@@ -81,11 +85,21 @@ class ItemInfoTable:
             # no longer lines up with the batch
             raise ValueError("item_info: duplicate item_id")
         n_ids = int(item_ids.max()) + 1 if len(item_ids) else 0
-        slot = np.full(max(1, n_ids), -1, dtype=np.int32)
-        slot[item_ids] = np.arange(len(item_ids), dtype=np.int32)
         self.device = torch.device(device)
-        self.n_ids = n_ids
         self.dim = emb.shape[1]
+        if n_ids <= self.DENSE_FACTOR * len(item_ids) + self.DENSE_SLACK:
+            # dense id -> row index (MicroLens: ids 1..91 718, 0.4 MB)
+            slot = np.full(max(1, n_ids), -1, dtype=np.int32)
+            slot[item_ids] = np.arange(len(item_ids), dtype=np.int32)
+            self.n_ids = n_ids
+            self.sorted_ids = None
+        else:
+            # sparse / hashed ids: a dense index would be sized by the largest id -- the ids sorted
+            # instead, and the collator binary-searches them
+            order = np.argsort(item_ids, kind="stable")
+            slot = order.astype(np.int32)
+            self.n_ids = len(item_ids)
+            self.sorted_ids = torch.from_numpy(np.ascontiguousarray(item_ids[order])).to(self.device)
         self.slot_of_id = torch.from_numpy(slot).to(self.device)
         self.emb = torch.from_numpy(emb).to(self.device)
 
@@ -190,7 +204,8 @@ class DeviceLoader:
         flag = flag if flag is not None else self.missing
         call("fbn_collate", ptr(rows), B, ptr(c["item_id"]), ptr(seq), Ls, L, ptr(c.get("likes_level")),
              ptr(c.get("views_level")), ptr(c.get("user_id")), ptr(c["label"]) if lab is not None else None,
-             ptr(info.slot_of_id) if info else None, info.n_ids if info else 0, ptr(info.emb) if info else None,
+             ptr(info.slot_of_id) if info else None, info.n_ids if info else 0,
+             ptr(info.sorted_ids) if info else None, ptr(info.emb) if info else None,
              info.dim if info else 0, ptr(out["item_id"]), ptr(out.get("item_seq")), ptr(out.get("likes_level")),
              ptr(out.get("views_level")), ptr(out.get("user_id")), ptr(lab), ptr(out.get("item_emb_d128")),
              ptr(flag), _lib.stream_handle(dev))

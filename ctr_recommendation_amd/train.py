@@ -9,7 +9,8 @@ Same surface and loop as the reference script:
 * the YAML config (src/train_fibinet.py:18-28) -- the keys it reads: ``dataset_id``,
   ``base_expid``, ``dataset_config[id].{train_data, valid_data, item_info}`` and
   ``model_cfg.{embedding_dim, batch_size, max_len, learning_rate, weight_decay, epochs, seed}``;
-  optional keys this build adds: ``compute_dtype`` ("fp32" default, "bf16" = C3's mode),
+  optional keys this build adds: ``compute_dtype`` ("fp32" default; "bf16": every GEMM operand bf16;
+  "bf16_fwd": forward GEMMs bf16, backward fp32 -- C3's "bf16 fwd / fp32 grad accum"),
   ``table_adam`` ("lazy" default: exact), and ``honour_config`` (see model_fibinet.build_model);
 * ``set_seed(seed)`` then ``build_model`` (:33, :67): the seeded init of the reference;
 * Adam(lr, weight_decay) + BCELoss + clip_grad_norm_(10) + OneCycleLR(max_lr = 10 lr,
@@ -122,6 +123,9 @@ def run(config: Optional[str] = None, *, epochs: Optional[int] = None, checkpoin
             steps += 1
             if steps % 200 == 0:
                 log0(f"Epoch {epoch + 1} | Step {steps} | Loss: {loss.item():.4f} | LR: {trainer.current_lr():.6f}")
+                # the print's sync anyway: an item_id without item_info raises here, within 200
+                # steps of the batch (the reference raises at that batch, src/dataloader.py:104-106)
+                train_loader.check()
         trainer.check_ids()
         train_loader.check()
         avg_loss = float(total.item()) / steps if steps else 0.0
@@ -142,7 +146,7 @@ def run(config: Optional[str] = None, *, epochs: Optional[int] = None, checkpoin
              f"{steps * train_loader.batch_size / dt:.0f} samples/s")
         if auc is not None and auc > best_auc:
             best_auc = auc
-            sd = trainer.state_dict()                     # collective at N > 1 (table shards gathered)
+            sd = trainer.state_dict()                     # collective at N > 1 (table on rank 0 only)
             if rank == 0:
                 os.makedirs(os.path.dirname(os.path.abspath(ckpt)), exist_ok=True)
                 torch.save(sd, ckpt)

@@ -163,6 +163,15 @@ def _copy_many(pairs, stream) -> None:
              stream)
 
 
+def _batch_key(item: torch.Tensor, seq: Optional[torch.Tensor]):
+    """Identity of a batch's id tensors for work prepared one step ahead (pre-claims, routing):
+    address, shape AND version counter, so a caller that copies the next batch into the same
+    static buffer (copy_ bumps _version) gets a fresh claim instead of the previous batch's."""
+    return (item.data_ptr(), item.shape[0], item._version,
+            0 if seq is None else seq.data_ptr(), 0 if seq is None else tuple(seq.shape),
+            0 if seq is None else seq._version)
+
+
 def _pad4(n: int) -> int:
     return (n + 3) // 4 * 4
 
@@ -385,7 +394,7 @@ class FiBiNETTrainer:
             # GPU): the row claims are made inside the same launch (fbn_adam_claim_catchup)
             ev = _events(probe, "adam_catchup")
             if claim:
-                key = (batch["item_id"].data_ptr(), seq.data_ptr() if L else 0)
+                key = _batch_key(batch["item_id"], seq if L else None)
                 pre = self.preclaim if (self.preclaim is not None and key == self._pre_key) else None
                 self._pre_key = None
                 call("fbn_adam_claim_catchup", ptr(batch["item_id"]), ptr(seq) if L else None, B, L, self.V,
@@ -423,7 +432,7 @@ class FiBiNETTrainer:
                 nL = nseq.shape[1] if nseq is not None else 0
                 ev = _events(probe, "adam_prefetch", self.side)
                 if nb["item_id"].shape[0] == B and nL == L:   # claims made now are valid for that step
-                    self._pre_key = (nb["item_id"].data_ptr(), nseq.data_ptr() if nL else 0)
+                    self._pre_key = _batch_key(nb["item_id"], nseq if nL else None)
                 call("fbn_adam_prefetch", ptr(nb["item_id"]), ptr(nseq) if nL else None, nb["item_id"].shape[0], nL,
                      self.V, ptr(self.map), ptr(self.preclaim if self._pre_key is not None else None), ptr(self.E),
                      ptr(self.Em), ptr(self.Ev), d, ptr(self.last),
@@ -705,16 +714,39 @@ class FiBiNETTrainer:
                  ptr(self.sched), ptr(self.step_dev), self.wd_g, self.beta2, self.eps, *self._pend_args(),
                  int(self.decoupled), _lib.stream_handle(self.device))
 
+    def _bn_from_rank0(self) -> None:
+        """Per-rank BatchNorm (sync_bn=False) at N > 1: evaluation uses rank 0's running statistics
+        on every rank.  That is nn.DataParallel's behaviour (train_fibinet.py:69-70: each forward
+        replicates the module, buffers included, from device 0, and only device 0's updates are
+        kept), and they are the statistics the checkpoint holds."""
+        if self.world <= 1 or self.sync_bn:
+            return
+        for n in ("mlp.1.running_mean", "mlp.1.running_var", "mlp.5.running_mean", "mlp.5.running_var"):
+            t = self.p[n]
+            if self.stage_on_cpu:
+                c = t.cpu()
+                dist.broadcast(c, src=0, group=self.group)
+                t.copy_(c)
+            else:
+                dist.broadcast(t, src=0, group=self.group)
+
     @torch.no_grad()
     def predict(self, batch: Dict[str, torch.Tensor], logits: bool = False) -> torch.Tensor:
+        """Eval-mode probabilities (or logits) of this rank's batch.  N > 1: collective (the row
+        exchange, and rank 0's BatchNorm statistics when sync_bn is off); a rank with an empty slice
+        (a last batch smaller than the world) still joins them and returns an empty tensor."""
         self.flush()
+        self._bn_from_rank0()
         cfg = ops.FwdConfig(**{**self.fcfg.__dict__, "training": False})
         cfg.L = batch["item_seq"].shape[1] if "item_seq" in batch else 0
+        B = batch["item_id"].shape[0]
         rows = pos = None
         if self.xchg is not None:
             rows = self.xchg.forward(batch["item_id"], batch.get("item_seq"), self.E, {"map": None, "slot_row": None},
                                      self.err)
             pos = self.xchg.cur_pos
+        if B == 0:
+            return torch.empty(0, dtype=torch.float32, device=self.device)
         a = ops.forward(self.p, batch, cfg, None, table_rows=rows, pos=pos, err=self.err)
         return (a["logits"] if logits else a["probs"]).clone()
 
@@ -738,32 +770,58 @@ class FiBiNETTrainer:
         return self.lrs[min(self.device_step(), self.total_steps - 1)]
 
     # ------------------------------------------------------------------ checkpoint (App. B keys)
-    def state_dict(self) -> Dict[str, torch.Tensor]:
-        """Reference state_dict (CPU tensors).  Multi-GPU: collective; the full table on every rank."""
-        import torch.distributed as dist
+    def state_dict(self, all_ranks: bool = False) -> Dict[str, torch.Tensor]:
+        """Reference state_dict (App. B keys, CPU tensors).  N > 1: collective; the full table is
+        assembled on rank 0 only (the rank that saves the checkpoint, train_fibinet.py:148-152) --
+        every other rank gets the same dict without ``item_emb.weight`` -- unless all_ranks.  The
+        shards travel to rank 0 in chunks of <= 256 MB through one device staging buffer, straight
+        into one host tensor, so a C5 shard (12.5 M rows x 128, 6.4 GB) never needs a second full
+        copy on any GPU."""
         self.flush()
         out = {}
         if self.world > 1:
-            local = torch.zeros((self.Vl, self.d), dtype=torch.float32, device=self.device)
-            local[:self.rows_local] = self.E
-            if self.stage_on_cpu:
-                parts = [torch.zeros((self.Vl, self.d)) for _ in range(self.world)]
-                dist.all_gather(parts, local.cpu(), group=self.group)
-                full = torch.cat(parts)[:self.V]
-            else:
-                parts = [torch.zeros_like(local) for _ in range(self.world)]
-                dist.all_gather(parts, local, group=self.group)
-                full = torch.cat(parts)[:self.V].cpu()
+            full = self._gather_table(all_ranks)
         else:
             full = self.E.detach().cpu().clone()
         for k in self.key_order:
-            out[k] = full if k == TABLE else self.p[k].detach().cpu().clone()
+            if k == TABLE:
+                if full is not None:
+                    out[k] = full
+            else:
+                out[k] = self.p[k].detach().cpu().clone()
         return out
 
+    def _gather_table(self, all_ranks: bool) -> Optional[torch.Tensor]:
+        d, Vl = self.d, self.Vl
+        chunk = max(1, (256 << 20) // (d * 4))
+        dev = "cpu" if self.stage_on_cpu else self.device
+        me = all_ranks or self.rank == 0
+        full = torch.empty((self.V, d), dtype=torch.float32) if me else None
+        stage = torch.empty((min(chunk, Vl), d), dtype=torch.float32, device=dev)
+        for src in range(self.world):
+            lo = src * Vl
+            n = max(0, min(self.V, lo + Vl) - lo)
+            for c0 in range(0, n, chunk):
+                c1 = min(n, c0 + chunk)
+                buf = stage[:c1 - c0]
+                if src == self.rank:
+                    buf.copy_(self.E[c0:c1])
+                if all_ranks:
+                    dist.broadcast(buf, src=src, group=self.group)
+                elif src != 0:
+                    if self.rank == src:
+                        dist.send(buf, dst=0, group=self.group)
+                    elif self.rank == 0:
+                        dist.recv(buf, src=src, group=self.group)
+                if me:
+                    full[lo + c0:lo + c1].copy_(buf)
+        return full
+
     def load_state_dict(self, sd: Dict[str, torch.Tensor]) -> None:
-        """Load reference-format weights (App. B keys).  Like ``model.load_state_dict`` under the
-        reference's loop, the optimizer state (Adam moments, step count, schedule position) is
-        kept: only the weights and BatchNorm buffers change."""
+        """Load reference-format weights (App. B keys; every rank needs the full dict at N > 1).
+        Like ``model.load_state_dict`` under the reference's loop, the optimizer state (Adam
+        moments, step count, schedule position) is kept: only the weights and BatchNorm buffers
+        change."""
         self.flush()
         for k in self.key_order:
             if k == TABLE:

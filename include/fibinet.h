@@ -395,10 +395,14 @@ int fbn_bilinear_bwd(const void* dc, int ldc, int dc_bf16, const short* V16, con
  * seq [N][Ls] (the last L columns are kept: src/dataloader.py:111-116), likes, views, user [N]
  * int64 and label [N] f32 (any of those may be NULL), and o_emb[b] = emb[slot_of_id[item]] (the
  * item_info lookup of :91-95; E floats per row).  An item id without an item_info row gets a zero
- * row and sets *missing (the training collator's KeyError, raised by the host when it checks). */
+ * row and sets *missing (the training collator's KeyError, raised by the host when it checks).
+ * sorted_ids == NULL: slot_of_id is a dense index [n_ids] by id; else sorted_ids [n_ids] holds the
+ * item_info ids ascending and slot_of_id[k] the row of sorted_ids[k] (sparse or hashed ids, where a
+ * dense index would be sized by the largest id): a binary search per sample. */
 int fbn_collate(const int64_t* perm, int B, const int64_t* item, const int64_t* seq, int Ls, int L,
                 const int64_t* likes, const int64_t* views, const int64_t* user, const float* label,
-                const int* slot_of_id, long long n_ids, const float* emb, int E, int64_t* o_item, int64_t* o_seq,
+                const int* slot_of_id, long long n_ids, const int64_t* sorted_ids, const float* emb, int E,
+                int64_t* o_item, int64_t* o_seq,
                 int64_t* o_likes, int64_t* o_views, int64_t* o_user, float* o_label, float* o_emb, int* missing,
                 void* stream);
 /* x[0:n] = 0 when *flag != 0: the inference collator's whole-batch zero fallback

@@ -25,7 +25,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, V, d, B, L, q, hook=False, bf16=False):
+def _worker(rank, world, port, V, d, B, L, q, hook=False, bf16=False, padded=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -60,6 +60,22 @@ def _worker(rank, world, port, V, d, B, L, q, hook=False, bf16=False):
 
         rows = xg.forward(item, seq, E_local, sparse, err, before_gather=before_gather if hook else None)
         pos = xg.cur_pos
+        ok_pad = True
+        if padded:
+            # the routed-ahead form of the same requests (RowExchange.prepare on a GPU): every
+            # destination's ids padded to cap with -1 and its count in the last slot, ONE
+            # equal-split all-to-all, the owner packs them -> the inline path's counts and ids
+            st = xg.sets[xg.cur]
+            cap = B * (L + 1)
+            pad = torch.empty(world * (cap + 1), dtype=torch.int32)
+            xg.k.pad_routes(st["send_ids"], st["offsets"], st["counts"], world, cap, pad)
+            recv = torch.empty_like(pad)
+            dist.all_to_all_single(recv, pad)
+            ids2 = torch.empty(world * cap, dtype=torch.int32)
+            cnt2 = torch.zeros(world, dtype=torch.int32)
+            xg.k.compact_routes(recv, world, cap, ids2, cnt2)
+            n_recv = sum(xg.recv_counts)
+            ok_pad = cnt2.tolist() == list(xg.recv_counts) and torch.equal(ids2[:n_recv], xg.recv_ids)
         ids = torch.cat([item.view(B, 1), seq], dim=1)
         ok_fwd = True
         for b in range(B):
@@ -96,21 +112,26 @@ def _worker(rank, world, port, V, d, B, L, q, hook=False, bf16=False):
         c = DistCollective(world)
         t = torch.full((3,), float(rank + 1), dtype=torch.float64)
         c.allreduce_(t)
-        q.put((rank, bool(ok_fwd), bwd_err, nu, touched, t.tolist(), int(err[0])))
+        q.put((rank, bool(ok_fwd and ok_pad), bwd_err, nu, touched, t.tolist(), int(err[0])))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,hook,bf16", [(2, False, False), (3, False, False), (2, True, False),
-                                             (4, False, False), (4, True, False), (4, False, True)])
-def test_row_exchange_protocol(world, hook, bf16):
+@pytest.mark.parametrize("world,hook,bf16,padded", [(2, False, False, False), (3, False, False, False),
+                                                    (2, True, False, False), (4, False, False, True),
+                                                    (4, True, False, False), (4, False, True, True),
+                                                    (8, True, True, True)])
+def test_row_exchange_protocol(world, hook, bf16, padded):
     """hook: the owner-side claim -> before_gather -> gather split used by the lazy table Adam.
-    bf16: the bf16 mode's wire rows (each delivered row == E[id] rounded to bf16)."""
-    V, d, B, L = 101, 8, 12, 6
+    bf16: the bf16 mode's wire rows (each delivered row == E[id] rounded to bf16).  padded: the
+    routed-ahead padded blocks deliver the same counts and ids.  world 8: C4's split (eight
+    owners, blocks of B * (L + 1) + 1 ints per destination), bf16 rows, history length 20."""
+    V, d, B, L = (101, 8, 12, 6) if world < 8 else (1001, 8, 12, 20)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, V, d, B, L, q, hook, bf16)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, V, d, B, L, q, hook, bf16, padded))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]

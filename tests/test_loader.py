@@ -156,6 +156,37 @@ def test_device_collator_matches_reference_train(files, hip_device, bs):
 
 
 @pytest.mark.gpu
+def test_device_collator_sorted_id_index(files, hip_device, monkeypatch):
+    """The sparse-id item_info index (ids sorted, binary search per sample -- what a table of
+    hashed ids gets instead of a dense index sized by the largest id): the same batches,
+    bit-identical to BatchCollator's."""
+    monkeypatch.setattr(ItemInfoTable, "DENSE_FACTOR", 0)
+    monkeypatch.setattr(ItemInfoTable, "DENSE_SLACK", 0)
+    darray, ci = load_data(files["train_data"])
+    ref = list(batches(darray, BatchCollatorRef(20, ci, files["item_info"]), 128))
+    ours = _ours(files, hip_device, "train", "train", 128)
+    assert ours.info.sorted_ids is not None
+    for (rb, ry), (hb, hy) in zip(ref, ours):
+        assert torch.equal(rb["item_emb_d128"], hb["item_emb_d128"].cpu())
+        assert torch.equal(rb["item_id"].long(), hb["item_id"].cpu())
+    ours.check()
+
+
+def test_item_info_index_choice():
+    """Dense id -> row index for compact ids; sorted ids for sparse ones (largest id far beyond
+    the row count): the index never scales with the largest id."""
+    ids = np.array([3, 1, 7, 2], dtype=np.int64)
+    emb = np.arange(16, dtype=np.float32).reshape(4, 4)
+    t = ItemInfoTable(ids, emb, "cpu")
+    assert t.sorted_ids is None and t.n_ids == 8 and t.slot_of_id[7].item() == 2
+    big = np.array([5, 1 << 40, 17, 1 << 33], dtype=np.int64)
+    t = ItemInfoTable(big, emb, "cpu")
+    assert t.sorted_ids is not None and t.n_ids == 4
+    assert t.sorted_ids.tolist() == sorted(big.tolist())
+    assert [int(big[k]) for k in t.slot_of_id.tolist()] == sorted(big.tolist())
+
+
+@pytest.mark.gpu
 def test_device_collator_unknown_ids(files_missing, hip_device):
     """Training: the reference's KeyError (raised by check()); inference: the whole batch of an
     unknown id gets zero mm vectors, every other batch its item_info rows."""
