@@ -22,7 +22,7 @@
 #define FBN_MAXR 8   // max SENET reduced width supported (reference: 3)
 #define FBN_MAX_L 32 // max history length (the reference keeps the last 20)
 #ifndef FBN_HCH
-#define FBN_HCH 20   // history rows in flight per sample before they are summed (tools/time_fields.py)
+#define FBN_HCH 10   // default history rows in flight per sample before they are summed (FBN_FIELDS_HCH: 5 / 10 / 20)
 #endif
 
 struct FieldArgs {
@@ -111,12 +111,11 @@ __device__ __forceinline__ f32x4 load_row(const FieldArgs& p, size_t r, int q) {
   }
 }
 
-template <int D, int MODE>
+template <int D, int MODE, int HCH>
 __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
   FBN_MAIN_PRIO();
   constexpr int G = D / 4;                  // lanes per sample
   constexpr int SPW = 64 / G;               // samples per wave
-  constexpr int HCH = FBN_HCH;
   const int lane = threadIdx.x & 63;
   const int q = lane % G;
   const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -594,19 +593,29 @@ static int fields_grid(int B, int D, int cap = 1024) {
   return blocks < 1 ? 1 : (blocks > cap ? cap : blocks);
 }
 
-template <int MODE>
-static int launch_fields_fwd(const FieldArgs& a, int D, hipStream_t st) {
+// history rows per chunk: every row of a chunk is in flight at once (branch-free issue); more rows
+// per chunk = fewer dependent round trips but more registers (fewer waves resident)
+template <int MODE, int HCH>
+static int launch_fields_fwd_h(const FieldArgs& a, int D, hipStream_t st) {
   const int grid = fields_grid(a.B, D);
   switch (D) {
-    case 16: hipLaunchKernelGGL((fields_fwd_kernel<16, MODE>), dim3(grid), dim3(256), 0, st, a); break;
-    case 32: hipLaunchKernelGGL((fields_fwd_kernel<32, MODE>), dim3(grid), dim3(256), 0, st, a); break;
-    case 64: hipLaunchKernelGGL((fields_fwd_kernel<64, MODE>), dim3(grid), dim3(256), 0, st, a); break;
-    case 128: hipLaunchKernelGGL((fields_fwd_kernel<128, MODE>), dim3(grid), dim3(256), 0, st, a); break;
-    case 256: hipLaunchKernelGGL((fields_fwd_kernel<256, MODE>), dim3(grid), dim3(256), 0, st, a); break;
+    case 16: hipLaunchKernelGGL((fields_fwd_kernel<16, MODE, HCH>), dim3(grid), dim3(256), 0, st, a); break;
+    case 32: hipLaunchKernelGGL((fields_fwd_kernel<32, MODE, HCH>), dim3(grid), dim3(256), 0, st, a); break;
+    case 64: hipLaunchKernelGGL((fields_fwd_kernel<64, MODE, HCH>), dim3(grid), dim3(256), 0, st, a); break;
+    case 128: hipLaunchKernelGGL((fields_fwd_kernel<128, MODE, HCH>), dim3(grid), dim3(256), 0, st, a); break;
+    case 256: hipLaunchKernelGGL((fields_fwd_kernel<256, MODE, HCH>), dim3(grid), dim3(256), 0, st, a); break;
     default: fbn_set_error("fields: embedding_dim must be one of 16,32,64,128,256"); return FBN_ERR_UNSUPPORTED;
   }
   FBN_CHECK_LAUNCH();
   return FBN_OK;
+}
+
+template <int MODE>
+static int launch_fields_fwd(const FieldArgs& a, int D, hipStream_t st) {
+  static const int hch = getenv("FBN_FIELDS_HCH") ? atoi(getenv("FBN_FIELDS_HCH")) : FBN_HCH;
+  if (hch == 20) return launch_fields_fwd_h<MODE, 20>(a, D, st);
+  if (hch == 5) return launch_fields_fwd_h<MODE, 5>(a, D, st);
+  return launch_fields_fwd_h<MODE, 10>(a, D, st);
 }
 
 extern "C" int fbn_fields_fwd(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes,

@@ -1164,20 +1164,26 @@ __global__ void __launch_bounds__(256) adam_pretag_kernel(ClaimSrc cs, int n, co
 }
 
 // adam_tab1 with the step's constants as (w1, nss, rbc2s, dmul): the same operations, same order
+// written on whole vectors so every non-transcendental step is a packed v_pk_* instruction (the
+// element-wise fmas round exactly as adam_tab1's scalar ones)
 template <bool DW, int N>
 __device__ __forceinline__ void adam_tabk(typename FVec<N>::T& pp, typename FVec<N>::T& mm, typename FVec<N>::T& vv,
                                           typename FVec<N>::T gg, float wd, float b2, float omb2, float eps,
                                           f32x4 k) {
+  typedef typename FVec<N>::T V;
+  const V vwd = wd, vb2 = b2, vomb2 = omb2, veps = eps, w1 = k[0], nss = k[1], rb = k[2];
+  const V g = __builtin_elementwise_fma(vwd, pp, gg);
+  V p = pp;
+  if (DW) p = p * (V)k[3];
+  mm = __builtin_elementwise_fma(w1, g - mm, mm);
+  vv = __builtin_elementwise_fma(vomb2 * g, g, vv * vb2);
+  V sq, rc;
 #pragma unroll
-  for (int e = 0; e < N; ++e) {
-    const float g = __builtin_fmaf(wd, pp[e], gg[e]);
-    float p = pp[e];
-    if (DW) p = p * k[3];
-    mm[e] = __builtin_fmaf(k[0], g - mm[e], mm[e]);
-    vv[e] = __builtin_fmaf(omb2 * g, g, vv[e] * b2);
-    const float den = __builtin_fmaf(__builtin_amdgcn_sqrtf(vv[e]), k[2], eps);
-    pp[e] = __builtin_fmaf(k[1] * mm[e], __builtin_amdgcn_rcpf(den), p);
-  }
+  for (int e = 0; e < N; ++e) sq[e] = __builtin_amdgcn_sqrtf(vv[e]);
+  const V den = __builtin_elementwise_fma(sq, rb, veps);
+#pragma unroll
+  for (int e = 0; e < N; ++e) rc[e] = __builtin_amdgcn_rcpf(den[e]);
+  pp = __builtin_elementwise_fma(nss * mm, rc, p);
 }
 __device__ __forceinline__ f32x4 consts4(const AdamConsts& k) { return (f32x4){k.w1, k.nss, k.rbc2s, k.dmul}; }
 

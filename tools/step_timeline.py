@@ -20,7 +20,7 @@ def main():
     rows = list(csv.DictReader(open(path)))
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"],
                  int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0)) for r in rows)
-    starts = [i for i, e in enumerate(ev) if "claim_rows" in e[2]]
+    starts = [i for i, e in enumerate(ev) if "claim_rows" in e[2] or "adam_claim2" in e[2]]
     if not starts:
         # fused claim + catch-up (lazy single GPU): steps start at the claimed-row catch-up, the
         # adam_catchup launch with the largest grid
@@ -33,7 +33,7 @@ def main():
     def is_window(k, ks):
         # side stream: the rolling-window replay (the adam_catchup launch of the step with the
         # smaller grid) and the next batch's ahead-of-time catch-up (adam_prefetch)
-        if "adam_prefetch" in k[2]:
+        if "adam_prefetch" in k[2] or "adam_pretag" in k[2] or "adam_window2" in k[2]:
             return True
         cs = [c[3] for c in ks if "adam_catchup" in c[2]]
         return "adam_catchup" in k[2] and len(cs) > 1 and k[3] == min(cs)
