@@ -1290,6 +1290,97 @@ __device__ __forceinline__ void replay4_sorted(int r, int key, int pe, int cnt, 
   }
 }
 
+// The same engine for d < 128 (C2's d = 16): a row is G = d/4 lanes of 4 elements, so a wave replays
+// 64/G sorted rows per round, each lane group stepping its own row (the sort keeps a round's replay
+// lengths alike); the next round's rows are loaded before this round's arithmetic, and each step's
+// constants are read from the LDS window one step ahead.
+template <int D, bool DW>
+__device__ __forceinline__ void replay_narrow_sorted(int r, int key, int pe, int cnt, int T, int w0,
+                                                     const f32x4* __restrict__ win, float* __restrict__ p,
+                                                     float* __restrict__ m, float* __restrict__ v,
+                                                     const AdamConsts* __restrict__ table, float wd, float b2,
+                                                     float omb2, float eps, const PendSrc& ps, int lane) {
+  constexpr int G = D / 4, RPW = 64 / G;
+#pragma unroll
+  for (int kk = 2; kk <= 64; kk <<= 1)
+#pragma unroll
+    for (int j = kk >> 1; j > 0; j >>= 1) {
+      const int ok = __shfl_xor(key, j, 64), orr = __shfl_xor(r, j, 64), ope = __shfl_xor(pe, j, 64);
+      const bool up = (lane & kk) == 0, lower = (lane & j) == 0;
+      if (lower == up ? ok < key : ok > key) {
+        key = ok;
+        r = orr;
+        pe = ope;
+      }
+    }
+  const int q = lane % G, grp = lane / G;
+  auto fetch = [&](int j0, int& rr, int& kk, int& pp) {
+    const int src = j0 + grp;
+    const int sl = src < 64 ? src : 0;
+    rr = __shfl(r, sl, 64);
+    kk = __shfl(key, sl, 64);
+    pp = __shfl(pe, sl, 64);
+    if (src >= cnt) { rr = 0; kk = T; pp = -1; }
+  };
+  struct Row { f32x4 p, m, v, g; float c; };
+  auto load = [&](Row& x, int rr, int kk, int pp) {
+    const size_t off = (size_t)rr * D + 4 * q;
+    x.p = *reinterpret_cast<const f32x4*>(p + off);
+    x.m = *reinterpret_cast<const f32x4*>(m + off);
+    x.v = *reinterpret_cast<const f32x4*>(v + off);
+    const int k0 = pp >= 0 ? kk - 1 : kk;   // the deferred gradient's step
+    const float* ring = ps.ring ? ps.ring : p;   // branch-free, as row_load
+    const float* coef = ps.coef_hist ? ps.coef_hist : p;
+    const size_t go = pp >= 0 ? (size_t)(k0 % ps.ring_n) * ps.ring_stride + (size_t)pp * D : 0;
+    x.g = *reinterpret_cast<const f32x4*>(ring + go + 4 * q);
+    x.c = coef[pp >= 0 ? k0 : 0];
+  };
+  int rc, kc, pc;
+  fetch(0, rc, kc, pc);
+  Row cur;
+  load(cur, rc, kc, pc);
+  const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+  for (int j0 = 0; j0 < cnt; j0 += RPW) {
+    int rn, kn, pn;
+    fetch(j0 + RPW, rn, kn, pn);
+    Row nxt;
+    load(nxt, rn, kn, pn);   // past the last round: row 0, discarded
+    if (pc >= 0) {
+      const int s = kc - 1;
+      adam_tabk<DW, 4>(cur.p, cur.m, cur.v, cur.g * cur.c, wd, b2, omb2, eps, s >= w0 ? win[s - w0] : consts4(table[s]));
+    }
+    int s = kc;
+    for (; s < T && s < w0; ++s) adam_tabk<DW, 4>(cur.p, cur.m, cur.v, zero, wd, b2, omb2, eps, consts4(table[s]));
+    if (s < T) {
+      f32x4 k = win[s - w0];
+      for (; s < T; ++s) {
+        const f32x4 kx = win[s + 1 - w0];   // <= T - w0: in the window
+        adam_tabk<DW, 4>(cur.p, cur.m, cur.v, zero, wd, b2, omb2, eps, k);
+        k = kx;
+      }
+    }
+    if (j0 + grp < cnt) {
+      const size_t off = (size_t)rc * D + 4 * q;
+      *reinterpret_cast<f32x4*>(p + off) = cur.p;
+      *reinterpret_cast<f32x4*>(m + off) = cur.m;
+      *reinterpret_cast<f32x4*>(v + off) = cur.v;
+    }
+    cur = nxt;
+    rc = rn;
+    kc = kn;
+    pc = pn;
+  }
+}
+
+template <int D, bool DW>
+__device__ __forceinline__ void replay_sorted(int r, int key, int pe, int cnt, int T, int w0,
+                                              const f32x4* __restrict__ win, float* __restrict__ p,
+                                              float* __restrict__ m, float* __restrict__ v,
+                                              const AdamConsts* __restrict__ table, float wd, float b2, float omb2,
+                                              float eps, const PendSrc& ps, int lane) {
+  if constexpr (D >= 128) replay4_sorted<D, DW>(r, key, pe, cnt, T, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
+  else replay_narrow_sorted<D, DW>(r, key, pe, cnt, T, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
+}
 
 template <int D, bool DW>
 __global__ void __launch_bounds__(256) adam_prefetch2_kernel(float* __restrict__ p, float* __restrict__ m,
@@ -1325,7 +1416,7 @@ __global__ void __launch_bounds__(256) adam_prefetch2_kernel(float* __restrict__
   __syncthreads();   // the LDS window (no barrier after this point)
   const int cnt = __popcll(__ballot(key != 0x7fffffff));
   if (cnt == 0) return;
-  replay4_sorted<D, DW>(r, key, pe, cnt, T, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
+  replay_sorted<D, DW>(r, key, pe, cnt, T, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
 }
 
 // Single GPU, D >= 128: the step's row claims + the claimed rows' catch-up (fbn_adam_claim_catchup)
@@ -1394,7 +1485,7 @@ __global__ void __launch_bounds__(256) adam_claim2_kernel(float* __restrict__ p,
   __syncthreads();
   const int cnt = __popcll(__ballot(key != 0x7fffffff));
   if (cnt == 0) return;
-  replay4_sorted<D, DW>(r, key, pe, cnt, t, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
+  replay_sorted<D, DW>(r, key, pe, cnt, t, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
 }
 
 // The rolling window (step mod F) with the replay engine (D >= 128): FBN_WIN_ROWS rows per wave
@@ -1434,7 +1525,7 @@ __global__ void __launch_bounds__(256) adam_window2_kernel(float* __restrict__ p
   __syncthreads();   // the LDS window (no barrier after this point)
   const int cnt = __popcll(__ballot(key != 0x7fffffff));
   if (cnt == 0) return;
-  replay4_sorted<D, DW>(r, key, pe, cnt, t, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
+  replay_sorted<D, DW>(r, key, pe, cnt, t, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
 }
 
 // every row up to `step` (checkpoint / evaluation)
@@ -1962,26 +2053,18 @@ extern "C" int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, i
     return FBN_ERR_ARG;
   }
   const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
-  // the window alone at D >= 128: the replay engine over FBN_WIN_ROWS rows per wave
-  // (FBN_WINDOW_ONEPASS=1 keeps adam_catchup_kernel, A/B)
+  // the window alone: the replay engine over FBN_WIN_ROWS rows per wave (FBN_WINDOW_ONEPASS=1 keeps
+  // adam_catchup_kernel, A/B)
   static const bool wone = getenv("FBN_WINDOW_ONEPASS") && atoi(getenv("FBN_WINDOW_ONEPASS")) == 1;
-  if (parts == 2 && (D == 128 || D == 256) && !wone) {
+  if (parts == 2 && !wone) {
     const long long waves = (chunk + FBN_WIN_ROWS - 1) / FBN_WIN_ROWS;
     const dim3 g2((unsigned)((waves + 3) / 4));
-    if (D == 128) {
-      if (decoupled)
-        hipLaunchKernelGGL((adam_window2_kernel<128, true>), g2, dim3(256), 0, st, p, m, v, map, nrows, F, chunk, last,
-                           (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
-      else
-        hipLaunchKernelGGL((adam_window2_kernel<128, false>), g2, dim3(256), 0, st, p, m, v, map, nrows, F, chunk, last,
-                           (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+    if (decoupled) {
+      FBN_DISPATCH_D_B(adam_window2_kernel, true, D, g2, p, m, v, map, nrows, F, chunk, last,
+                       (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
     } else {
-      if (decoupled)
-        hipLaunchKernelGGL((adam_window2_kernel<256, true>), g2, dim3(256), 0, st, p, m, v, map, nrows, F, chunk, last,
-                           (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
-      else
-        hipLaunchKernelGGL((adam_window2_kernel<256, false>), g2, dim3(256), 0, st, p, m, v, map, nrows, F, chunk, last,
-                           (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+      FBN_DISPATCH_D_B(adam_window2_kernel, false, D, g2, p, m, v, map, nrows, F, chunk, last,
+                       (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
     }
     FBN_CHECK_LAUNCH();
     return FBN_OK;
@@ -2010,7 +2093,14 @@ extern "C" int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B,
                                  int decoupled, void* stream) {
   const long long n = (long long)B * (L + 1);
   if (n <= 0) return FBN_OK;
-  if (D < 128 || (D != 128 && D != 256)) { fbn_set_error("fbn_adam_prefetch: D = 128 or 256"); return FBN_ERR_ARG; }
+  if (D != 16 && D != 32 && D != 64 && D != 128 && D != 256) {
+    fbn_set_error("fbn_adam_prefetch: D = 16 / 32 / 64 / 128 / 256");
+    return FBN_ERR_ARG;
+  }
+  if (D < 128 && !preclaim) {   // the one-pass kernel replays wave-wide rows only
+    fbn_set_error("fbn_adam_prefetch: d < 128 needs the pre-claims (a next batch of this batch's shape)");
+    return FBN_ERR_ARG;
+  }
   if (!item || (L > 0 && !seq) || !map || !last) {
     fbn_set_error("fbn_adam_prefetch: item, seq (L > 0), map and last are required");
     return FBN_ERR_ARG;
@@ -2024,24 +2114,16 @@ extern "C" int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B,
   hipStream_t st = (hipStream_t)stream;
   // with pre-claims: the two-pass form (FBN_PREFETCH_ONEPASS=1 keeps the one-pass kernel, A/B)
   static const bool onepass = getenv("FBN_PREFETCH_ONEPASS") && atoi(getenv("FBN_PREFETCH_ONEPASS")) == 1;
-  if (preclaim && !onepass) {
+  if (preclaim && (!onepass || D < 128)) {
     const dim3 g2((unsigned)((n + 255) / 256));
     hipLaunchKernelGGL(adam_pretag_kernel, g2, dim3(256), 0, st, cs, (int)n, step);
     FBN_CHECK_LAUNCH();
-    if (D == 128) {
-      if (decoupled)
-        hipLaunchKernelGGL((adam_prefetch2_kernel<128, true>), g2, dim3(256), 0, st, p, m, v, cs, (int)n, last,
-                           (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
-      else
-        hipLaunchKernelGGL((adam_prefetch2_kernel<128, false>), g2, dim3(256), 0, st, p, m, v, cs, (int)n, last,
-                           (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+    if (decoupled) {
+      FBN_DISPATCH_D_B(adam_prefetch2_kernel, true, D, g2, p, m, v, cs, (int)n, last, (const AdamConsts*)consts_table,
+                       step, wd, beta2, omb2, eps, ps);
     } else {
-      if (decoupled)
-        hipLaunchKernelGGL((adam_prefetch2_kernel<256, true>), g2, dim3(256), 0, st, p, m, v, cs, (int)n, last,
-                           (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
-      else
-        hipLaunchKernelGGL((adam_prefetch2_kernel<256, false>), g2, dim3(256), 0, st, p, m, v, cs, (int)n, last,
-                           (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+      FBN_DISPATCH_D_B(adam_prefetch2_kernel, false, D, g2, p, m, v, cs, (int)n, last, (const AdamConsts*)consts_table,
+                       step, wd, beta2, omb2, eps, ps);
     }
     FBN_CHECK_LAUNCH();
     return FBN_OK;
@@ -2130,25 +2212,17 @@ extern "C" int fbn_adam_claim_catchup(const int64_t* item, const int64_t* seq, i
   const long long chunk = (nrows + F - 1) / F;
   const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
   const ClaimSrc cs{item, L > 0 ? seq : nullptr, L, V, map, slot_row, dup, hasdup, preclaim};
-  // D >= 128: one entry per lane, row state in one round trip, four-row replay (adam_claim2_kernel);
-  // FBN_CLAIM_ONEPASS=1 keeps the 16-entry scan of adam_catchup_kernel (A/B)
+  // one entry per lane, row state in one round trip, the replay engine (adam_claim2_kernel);
+  // FBN_CLAIM_ONEPASS=1 keeps the scans of adam_catchup_kernel (A/B)
   static const bool cone = getenv("FBN_CLAIM_ONEPASS") && atoi(getenv("FBN_CLAIM_ONEPASS")) == 1;
-  if ((D == 128 || D == 256) && !cone) {
+  if (!cone) {
     const dim3 g2((unsigned)((n + 255) / 256));
-    if (D == 128) {
-      if (decoupled)
-        hipLaunchKernelGGL((adam_claim2_kernel<128, true>), g2, dim3(256), 0, st, p, m, v, cs, (int)n, last,
-                           (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
-      else
-        hipLaunchKernelGGL((adam_claim2_kernel<128, false>), g2, dim3(256), 0, st, p, m, v, cs, (int)n, last,
-                           (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+    if (decoupled) {
+      FBN_DISPATCH_D_B(adam_claim2_kernel, true, D, g2, p, m, v, cs, (int)n, last, (const AdamConsts*)consts_table,
+                       step, wd, beta2, omb2, eps, ps);
     } else {
-      if (decoupled)
-        hipLaunchKernelGGL((adam_claim2_kernel<256, true>), g2, dim3(256), 0, st, p, m, v, cs, (int)n, last,
-                           (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
-      else
-        hipLaunchKernelGGL((adam_claim2_kernel<256, false>), g2, dim3(256), 0, st, p, m, v, cs, (int)n, last,
-                           (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+      FBN_DISPATCH_D_B(adam_claim2_kernel, false, D, g2, p, m, v, cs, (int)n, last, (const AdamConsts*)consts_table,
+                       step, wd, beta2, omb2, eps, ps);
     }
     FBN_CHECK_LAUNCH();
     return FBN_OK;

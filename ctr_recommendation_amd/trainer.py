@@ -275,9 +275,10 @@ class FiBiNETTrainer:
         if deterministic is None:
             deterministic = bool(model_cfg.get("deterministic", False)) or os.environ.get("FBN_DETERMINISTIC") == "1"
         self.deterministic = bool(deterministic) and not sharded
-        # lazy table Adam, single GPU, d = 128 / 256: step(..., next_batch=...) brings the next
-        # batch's rows up to date on the side stream during this step (fbn_adam_prefetch)
-        self.prefetch_rows = bool(prefetch_rows) and not sharded and self.d in (128, 256)
+        # lazy table Adam, single GPU: step(..., next_batch=...) brings the next batch's rows up to
+        # date on the side stream during this step (fbn_adam_prefetch; d < 128 needs the next batch
+        # to have this batch's shape -- its pre-claims drive the two-pass form)
+        self.prefetch_rows = bool(prefetch_rows) and not sharded and self.d in (16, 32, 64, 128, 256)
         # N > 1, the owner's side: the next step's requested rows arrive during this step (the
         # padded id exchange of RowExchange.prepare) and are caught up ahead (fbn_adam_prefetch_rows)
         self.prefetch_owner = bool(prefetch_rows) and sharded and self.d in (128, 256)
@@ -430,9 +431,11 @@ class FiBiNETTrainer:
                     and nb["item_id"].device == self.device):
                 nseq = nb.get("item_seq")
                 nL = nseq.shape[1] if nseq is not None else 0
-                ev = _events(probe, "adam_prefetch", self.side)
                 if nb["item_id"].shape[0] == B and nL == L:   # claims made now are valid for that step
                     self._pre_key = _batch_key(nb["item_id"], nseq if nL else None)
+                elif d < 128:
+                    return                                    # the one-pass form needs wave-wide rows
+                ev = _events(probe, "adam_prefetch", self.side)
                 call("fbn_adam_prefetch", ptr(nb["item_id"]), ptr(nseq) if nL else None, nb["item_id"].shape[0], nL,
                      self.V, ptr(self.map), ptr(self.preclaim if self._pre_key is not None else None), ptr(self.E),
                      ptr(self.Em), ptr(self.Ev), d, ptr(self.last),

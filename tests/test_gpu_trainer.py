@@ -148,8 +148,34 @@ def test_bf16_mode_tracks_fp32(hip_device):
     assert abs(a32 - a16) < 5e-3, (a32, a16)
 
 
-@pytest.mark.parametrize("window", [4, 128, "8->2"])
-def test_lazy_table_adam_matches_eager(hip_device, window):
+@pytest.mark.parametrize("d", [128, 16])
+def test_lazy_replay_beyond_lds_window(hip_device, d):
+    """The replay engine stages the schedule constants of the last 256 steps in LDS; a row lagging
+    further (window F = 512 over 300 steps: rows the window first reaches after step 256) replays
+    its oldest steps from the global table.  Untouched rows bit-identical to the eager pass."""
+    V, B, steps = 3000, 4, 300
+    cfg = {"embedding_dim": d, "vocab_size": V}
+    torch.manual_seed(0)
+    init = oracle_build(None, cfg).state_dict()
+    eager = FiBiNETTrainer(cfg, total_steps=steps, batch_size=B, device=hip_device, init_state=init,
+                           table_adam="eager", max_len=2)
+    lazy = FiBiNETTrainer(cfg, total_steps=steps, batch_size=B, device=hip_device, init_state=init,
+                          table_adam="lazy", lazy_window=512, max_len=2)
+    touched = torch.zeros(V, dtype=torch.bool)
+    for s in range(steps):
+        b, y = make_batch(5000 + s, B, V, L=2)
+        touched[b["item_id"]] = True
+        touched[b["item_seq"].flatten()] = True
+        db = {k: v.to(hip_device) for k, v in b.items()}
+        eager.step(db, y.to(hip_device))
+        lazy.step(db, y.to(hip_device))
+    assert int((steps - lazy.last).max()) > 256           # some rows lag past the LDS window
+    E_e, E_l = eager.state_dict()["item_emb.weight"], lazy.state_dict()["item_emb.weight"]
+    assert torch.equal(E_e[~touched], E_l[~touched])
+
+
+@pytest.mark.parametrize("window,d", [(4, 128), (128, 128), ("8->2", 128), (4, 16), ("8->2", 16)])
+def test_lazy_table_adam_matches_eager(hip_device, window, d):
     """Lazy table Adam (zero-gradient steps replayed when a row is claimed, its rolling window
     comes round, or at flush) against the eager per-step pass over every row.  Rows no batch
     touched are written by the replay alone: bit-identical.  Touched rows and dense params may
@@ -161,7 +187,7 @@ def test_lazy_table_adam_matches_eager(hip_device, window):
     shrink = window == "8->2"
     if shrink:
         window = 8
-    cfg = {"embedding_dim": 128, "vocab_size": V}
+    cfg = {"embedding_dim": d, "vocab_size": V}
     torch.manual_seed(0)
     init = oracle_build(None, cfg).state_dict()
     eager = FiBiNETTrainer(cfg, total_steps=20, batch_size=B, device=hip_device, init_state=init, table_adam="eager")
@@ -228,7 +254,8 @@ def test_deferred_table_grads_bit_identical(hip_device):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("defer,dups,d", [(True, False, 128), (False, False, 128), (True, True, 128),
-                                          (True, True, 256)])
+                                          (True, True, 256), (True, False, 16), (True, True, 16),
+                                          (False, False, 64)])
 def test_next_batch_prefetch_bit_identical(hip_device, defer, dups, d):
     """fbn_adam_prefetch: with step(..., next_batch=...) the next batch's rows that this batch does
     not touch are brought up to date on the side stream during this step.  Against the same run
