@@ -54,7 +54,10 @@ def parse():
     ap.add_argument("--rows-per-gpu", type=int, default=ROWS_PER_GPU)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "bf16_fwd", "fp32"],
                     help="bf16: every GEMM operand bf16; bf16_fwd: forward GEMM operands bf16, backward fp32; fp32")
-    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="N = 1: eager steps only (same as --mode eager)")
+    ap.add_argument("--mode", default="auto", choices=["auto", "graph", "eager"],
+                    help="N = 1: replay one hipGraph per batch, launch eagerly, or (auto) time both for a few "
+                         "steps after priming and run the timed steps in the faster mode")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=20)
     ap.add_argument("--probe-steps", type=int, default=10)
@@ -181,8 +184,9 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
     # only after ~2F steps; warm-up steps are < 1 ms each
     prime = max(0, 2 * F - W) if args.prime < 0 else args.prime
     sharded = world > 1 or FORCE_SHARD
-    use_graph = not sharded and not args.no_graph
-    total = 1 + (nb if use_graph else 0) + prime + W + K + args.probe_steps + 16
+    use_graph = not sharded and not args.no_graph and args.mode != "eager"
+    trial_n = 16 if (use_graph and args.mode == "auto") else 0
+    total = 1 + (nb if use_graph else 0) + prime + W + K + args.probe_steps + 16 + 4 * trial_n
     init = _initial_state(cfg, V, world, rank, dev)
     tr = FiBiNETTrainer(cfg, total_steps=total, batch_size=B, device=dev, rank=rank, world=world,
                         init_state=init, stage_on_cpu=rehearsal, lazy_window=F, prefetch_rows=args.prefetch,
@@ -208,8 +212,10 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
             graphs.append(gr)
         torch.cuda.synchronize()
 
+    eager_now = [False]
+
     def run_step(i):
-        if graphs:
+        if graphs and not eager_now[0]:
             graphs[i % nb].replay()
         else:
             # the HBM-resident batch itself: N > 1 routes the next batch during this step (no
@@ -223,6 +229,22 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
         i += 1
         if (j + 1) % 64 == 0 and rank == 0:
             print(f"[bench] {dtype}: {j + 1}/{prime + W} untimed steps", file=sys.stderr, flush=True)
+    # auto: a timed trial of both launch modes at steady state (graph replays and eager steps share
+    # every persistent buffer -- table, moments, deferred-gradient ring, pre-claims -- so the modes
+    # interleave freely: tests/test_gpu_trainer.py::test_graph_eager_interleave_bit_identical)
+    trial = {}
+    if trial_n:
+        for rnd in range(2):
+            for mode in ("graph", "eager"):
+                eager_now[0] = mode == "eager"
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(trial_n):
+                    run_step(i)
+                    i += 1
+                torch.cuda.synchronize()
+                trial.setdefault(mode, []).append((time.perf_counter() - t0) / trial_n * 1e3)
+        eager_now[0] = min(trial["eager"]) < min(trial["graph"])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -360,7 +382,9 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
     main_k = [r for r in rooflines if "side stream" not in r["kernel"] and " alone " not in r["kernel"]]
     dominant = max(main_k, key=lambda r: r["avg_launch_ms"]) if main_k else None
     out = {"dt": dt, "t_host": t_host, "t_wait": t_wait, "K": K, "W": W, "B": B, "L": L, "V": V, "d": d, "rows_local": tr.rows_local, "loss": loss,
-           "rooflines": rooflines, "roofline": dominant, "table_adam": tr.table_adam, "graphs": bool(graphs),
+           "rooflines": rooflines, "roofline": dominant, "table_adam": tr.table_adam,
+           "graphs": bool(graphs) and not eager_now[0],
+           "mode_trial_ms_per_step": {k: [round(x, 4) for x in v] for k, v in trial.items()} if trial else None,
            "prime": prime, "batches": nb, "lag": lag, "stale": stale, "touched": touched, "prefetch": prefetch}
     del graphs, tr, batches
     torch.cuda.synchronize()
@@ -445,6 +469,8 @@ def main():
                        "item_rows": r["V"], "item_rows_per_gpu": r["rows_local"], "emb_dim": r["d"],
                        "parallelism": f"row-shard{world}" if world > 1 or FORCE_SHARD else "single",
                        "hipgraph": r["graphs"], **({"rehearsal": backend} if rehearsal else {}),
+                       **({"launch_mode_trial_ms_per_step": r["mode_trial_ms_per_step"]}
+                          if r.get("mode_trial_ms_per_step") else {}),
                        **({"batchnorm": "per-GPU statistics (nn.DataParallel semantics, train_fibinet.py:69-70)"
                            if args.bn == "local" else "SyncBN (global-batch statistics; the parity mode)"}
                           if world > 1 or FORCE_SHARD else {})},

@@ -57,6 +57,15 @@ struct GemmArgs {
   const void* B2;
   int lda2, kseg, ldb2, nseg;
   int c16;      // C is bf16 (short*, ldc in elements): split == 1, no stats / beta (fbn_gemm_bf16out)
+  // BatchNorm backward first pass fused into a dgrad epilogue (fbn_gemm_bn_bwd_part): C is the
+  // gradient G wrt the BN output's activation; per row chunk of bnb_rpc rows (one wave's rows) and
+  // column: part[chunk][0][n] = sum dy, [1][n] = sum (x - mean) dy, [2][n] = 0, dy = (act > 0) * G * scale
+  const short* bnb_hact16;   // [M][N] bf16 activation image (its sign is the ReLU / dropout mask)
+  const float* bnb_xpre;     // [M][N] BN input
+  const float* bnb_mean;     // [N]
+  float bnb_scale;
+  double* bnb_part;          // null = off
+  int bnb_rpc;
 };
 
 template <bool BF16> struct GemmTraits;
@@ -253,8 +262,32 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[T
   constexpr int WM = BM / WGM, WN = BN / WGN;
   // C/D map of the 32x32 MFMA tile: col = lane&31, row = (e&3) + 8*(e>>2) + 4*(lane>>5)
   const bool split = gridDim.z > 1;
+  // common case, decided per workgroup (uniform): a whole tile of an unremapped f32 or bf16 C with no
+  // beta -- straight-line stores from one row base per (i, j), 32-bit offsets, no per-element tests
+  const bool fast = !split && g.beta == 0.f && g.rC.seg == 0x7fffffff && g.rC.off0 == 0 && m0 + BM <= g.M &&
+                    n0 + BN <= g.N;
+  if (fast) {
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * WN + j * 32 + lr;
+      const float bv = g.bias ? g.bias[n] : 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r0 = m0 + wm * WM + i * 32 + 4 * lh;
+        if (g.c16) {
+          short* base = reinterpret_cast<short*>(g.C) + (size_t)r0 * g.ldc + n;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) base[((e & 3) + 8 * (e >> 2)) * g.ldc] = f2bf(acc[i][j][e] + bv);
+        } else {
+          float* base = g.C + (size_t)r0 * g.ldc + n;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) base[((e & 3) + 8 * (e >> 2)) * g.ldc] = acc[i][j][e] + bv;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < TM && !fast; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int n = n0 + wn * WN + j * 32 + lr;
@@ -277,6 +310,38 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[T
         }
       }
     }
+  if (g.bnb_part && !split) {
+    // BatchNorm backward first pass (bn_bwd_partial4_kernel's sums) from the accumulators: this
+    // wave's WM rows are exactly one row chunk (the host checks WM == bnb_rpc)
+    const int chunk = (m0 + wm * WM) / g.bnb_rpc;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * WN + j * 32 + lr;
+      const bool nok = n < g.N;
+      const float mu = nok ? g.bnb_mean[n] : 0.f;
+      double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int m = m0 + wm * WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+          if (nok && m < g.M) {
+            const size_t idx = (size_t)m * g.N + n;
+            const float dy = g.bnb_hact16[idx] > 0 ? acc[i][j][e] * g.bnb_scale : 0.f;
+            s0 += dy;
+            s1 += (double)((g.bnb_xpre[idx] - mu) * dy);
+          }
+        }
+      s0 += __shfl_xor(s0, 32, 64);
+      s1 += __shfl_xor(s1, 32, 64);
+      if (lh == 0 && nok) {
+        double* pp = g.bnb_part + (size_t)chunk * 3 * g.N;
+        pp[n] = s0;
+        pp[g.N + n] = s1;
+        pp[2 * (size_t)g.N + n] = 0.0;
+      }
+    }
+  }
   if (g.stats && !split) {
     // BatchNorm fusion: exact two-pass (sum, M2) of each 64-row tile's column values from
     // registers; the BN finalize merges tiles in f64 (Chan) -- no extra pass over C.
@@ -869,7 +934,7 @@ static int gemm_impl(const void* A, const void* B, float* C, const float* bias, 
                      int ldb, int ldc, int transA, int transB, int rB_seg, int rB_off0, int rB_off1, int rC_seg,
                      int rC_off0, int rC_off1, float beta, int bf16, int a16, int b16, float* stats, float* ws,
                      size_t ws_bytes, const void* A2, int lda2, int kseg, const void* B2, int ldb2, int nseg,
-                     void* stream, int c16 = 0);
+                     void* stream, int c16 = 0, const GemmArgs* bnb = nullptr);
 
 extern "C" int fbn_gemm(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, int lda,
                         int ldb, int ldc, int transA, int transB, int rB_seg, int rB_off0, int rB_off1, int rC_seg,
@@ -910,7 +975,7 @@ static int gemm_impl(const void* A, const void* B, float* C, const float* bias, 
                      int ldb, int ldc, int transA, int transB, int rB_seg, int rB_off0, int rB_off1, int rC_seg,
                      int rC_off0, int rC_off1, float beta, int bf16, int a16, int b16, float* stats, float* ws,
                      size_t ws_bytes, const void* A2, int lda2, int kseg, const void* B2, int ldb2, int nseg,
-                     void* stream, int c16) {
+                     void* stream, int c16, const GemmArgs* bnb) {
   if (M <= 0 || N <= 0) return FBN_OK;
   if (!A || !B || !C) { fbn_set_error("fbn_gemm: null operand"); return FBN_ERR_ARG; }
   // 16-B vector loads along the contiguous dimension of every operand
@@ -932,6 +997,12 @@ static int gemm_impl(const void* A, const void* B, float* C, const float* bias, 
   g.A2 = A2; g.lda2 = lda2; g.kseg = kseg;
   g.B2 = B2; g.ldb2 = ldb2; g.nseg = nseg;
   g.c16 = c16;
+  g.bnb_hact16 = bnb ? bnb->bnb_hact16 : nullptr;
+  g.bnb_xpre = bnb ? bnb->bnb_xpre : nullptr;
+  g.bnb_mean = bnb ? bnb->bnb_mean : nullptr;
+  g.bnb_scale = bnb ? bnb->bnb_scale : 1.f;
+  g.bnb_part = bnb ? bnb->bnb_part : nullptr;
+  g.bnb_rpc = bnb ? bnb->bnb_rpc : 1;
   const int bk = bf16 ? 64 : 32;
   // LDS-DMA path: bf16 operands, K % 64 == 0, 16-B rows; k-major operands need their
   // M / N extent in whole 8-element chunks
@@ -989,4 +1060,42 @@ static int gemm_impl(const void* A, const void* B, float* C, const float* bias, 
     FBN_CHECK_LAUNCH();
   }
   return FBN_OK;
+}
+
+// The BatchNorm backward's first pass fused into its dgrad GEMM (bf16 mode, one process): C = op(A)
+// op(B) (bf16 operands, f32 C, no bias) and, from the accumulators, part = the column partials of
+// fbn_bn_bwd_fused ([fbn_bn_bwd_chunks(M, N)][3][N] doubles) for the matrix source G = C, the
+// activation's bf16 image `hact16` (mask = its sign), the BN input `xpre` and mean -- pass part to
+// fbn_bn_bwd_fused as part_pre.  Needs the plan whose waves cover exactly one row chunk each:
+// fbn_gemm_bn_bwd_part_supported(M, N, K, lda, ldb, transA, transB) says whether it applies.
+extern "C" int fbn_bn_bwd_chunks(int B, int C);
+extern "C" int fbn_gemm_bn_bwd_part_supported(int M, int N, int K, int lda, int ldb, int transA, int transB) {
+  if (M <= 0 || N <= 0 || K <= 0 || K % 64 || (lda & 7) || (ldb & 7) || (transA && (M & 7)) || (!transB && (N & 7)))
+    return 0;
+  const GemmPlan p = plan_dma16(M, N, K);
+  if (p.split != 1 || p.waves != 8 || p.bm != 64 || p.bn != 128) return 0;   // 2 x 4 waves: 32 rows each
+  const int nch = fbn_bn_bwd_chunks(M, N);
+  return (N % 4 == 0 && M % 32 == 0 && M / 32 == nch) ? 1 : 0;
+}
+
+extern "C" int fbn_gemm_bn_bwd_part(const void* A, const void* B, float* C, int M, int N, int K, int lda, int ldb,
+                                    int ldc, int transA, int transB, const short* hact16, const float* xpre,
+                                    const float* mean, float scale, double* part, void* stream) {
+  if (!fbn_gemm_bn_bwd_part_supported(M, N, K, lda, ldb, transA, transB)) {
+    fbn_set_error("fbn_gemm_bn_bwd_part: no plan with one row chunk per wave for this shape");
+    return FBN_ERR_UNSUPPORTED;
+  }
+  if (!hact16 || !xpre || !mean || !part || ldc != N) {
+    fbn_set_error("fbn_gemm_bn_bwd_part: hact16, xpre, mean and part are required, ldc == N");
+    return FBN_ERR_ARG;
+  }
+  GemmArgs x;
+  x.bnb_hact16 = hact16;
+  x.bnb_xpre = xpre;
+  x.bnb_mean = mean;
+  x.bnb_scale = scale;
+  x.bnb_part = part;
+  x.bnb_rpc = 32;
+  return gemm_impl(A, B, C, nullptr, M, N, K, lda, ldb, ldc, transA, transB, 0x7fffffff, 0, 0, 0x7fffffff, 0, 0, 0.f,
+                   1, 1, 1, nullptr, nullptr, 0, nullptr, 0, 0x7fffffff, nullptr, 0, 0x7fffffff, stream, 0, &x);
 }

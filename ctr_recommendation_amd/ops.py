@@ -35,6 +35,8 @@ BN_MOMENTUM = 0.1
 
 # the trainer's BN2 backward first pass inside the forward head kernel (A/B knob)
 _BN2_BWD_IN_FWD = os.environ.get("FBN_BN2_BWD_IN_FWD", "1") == "1"
+# bf16, one process: the BN1 backward first pass inside the epilogue of its dgrad GEMM (A/B knob)
+_BN1_BWD_IN_GEMM = os.environ.get("FBN_BN1_BWD_IN_GEMM", "1") == "1"
 
 
 def wa_remap(d: int):
@@ -504,18 +506,28 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
                 part_pre=a.get("bn2_bwd_part") if (gout is a.get("gout")) else None)
     sums.add(gout, B, 1, g["mlp.8.bias"])
     dh1 = torch.empty((B, H1), **f32)
+    part1 = None
+    lean_h1 = a.get("lean_h1", False)
     if bf:
         wg.run(lambda s: gemm(dh2pre16, a["h1_16"], g["mlp.4.weight"], H2, H1, B, H2, H1, H1, True, False, stream=s))
-        gemm(dh2pre16, w16["WbT"], dh1, B, H1, H2, H2, H2, H1, False, True, stream=st)
+        if (_BN1_BWD_IN_GEMM and lean_h1 and coll.world <= 1
+                and _lib.lib().fbn_gemm_bn_bwd_part_supported(B, H1, H2, H2, H2, 0, 1)):
+            # dh1 = dh2 Wb and, from its accumulators, the BN1 backward's column partials (no pass
+            # over dh1 to compute them)
+            part1 = torch.empty(_lib.lib().fbn_bn_bwd_chunks(B, H1) * 3 * H1, dtype=torch.float64, device=dev)
+            call("fbn_gemm_bn_bwd_part", ptr(dh2pre16), ptr(w16["WbT"]), ptr(dh1), B, H1, H2, H2, H2, H1, 0, 1,
+                 ptr(a["h1_16"]), ptr(a["h1pre"]), ptr(a["mean1"]), float(scale), ptr(part1), st)
+        else:
+            gemm(dh2pre16, w16["WbT"], dh1, B, H1, H2, H2, H2, H1, False, True, stream=st)
     else:
         wg.run(lambda s: gemm(dh2pre, a["h1"], g["mlp.4.weight"], H2, H1, B, H2, H1, H1, True, False, stream=s))
         gemm(dh2pre, p["mlp.4.weight"], dh1, B, H1, H2, H2, H1, H1, False, False, stream=st)
     dh1pre = None if lean else torch.empty((B, H1), **f32)
     dh1pre16 = torch.empty((B, H1), **bf16_) if bf else None
-    lean_h1 = a.get("lean_h1", False)
     bn_backward(dh1, None, None, None if lean_h1 else a["h1"], scale, a["h1pre"], a["mean1"], a["inv1"],
                 p["mlp.1.weight"], B, H1, ntot, dh1pre, g["mlp.1.weight"], g["mlp.1.bias"], None, coll, st,
-                dpre16=dh1pre16, bias_grad=g["mlp.0.bias"], sums=sums, hact16=a["h1_16"] if lean_h1 else None)
+                dpre16=dh1pre16, bias_grad=g["mlp.0.bias"], sums=sums, hact16=a["h1_16"] if lean_h1 else None,
+                part_pre=part1)
     # weight gradient of the MLP input layer (side work), then its dgrad dc
     if a.get("split_c"):
         wg.run(lambda s: gemm_split(dh1pre16, a["Vc16"], g["mlp.0.weight"], H1, KC, B, H1, 5 * d, 21 * d, True,

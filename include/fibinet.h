@@ -63,6 +63,17 @@ int fbn_gemm(const void* A, const void* B, float* C, const float* bias, int M, i
  * fbn_bilinear_bwd. */
 int fbn_gemm_bf16out(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                      int transA, int transB, void* stream);
+/* bf16 dgrad GEMM C = op(A) op(B) (f32 C, no bias) whose epilogue also computes the first pass of
+ * the BatchNorm backward that follows it (src/model_fibinet.py:127-129 autograd: the BN1 backward
+ * of the MLP, whose input gradient source G is this C): part = fbn_bn_bwd_fused's column partials
+ * ([fbn_bn_bwd_chunks(M, N)][3][N] doubles) from the accumulators, the activation's bf16 image
+ * hact16 (its sign is the ReLU / dropout mask), the BN input xpre and mean; hand part to
+ * fbn_bn_bwd_fused as part_pre.  _supported: 1 when the shape's tiling gives one row chunk per
+ * wave (else FBN_ERR_UNSUPPORTED: run fbn_gemm and the fused BN backward's own pass). */
+int fbn_gemm_bn_bwd_part_supported(int M, int N, int K, int lda, int ldb, int transA, int transB);
+int fbn_gemm_bn_bwd_part(const void* A, const void* B, float* C, int M, int N, int K, int lda, int ldb, int ldc,
+                         int transA, int transB, const short* hact16, const float* xpre, const float* mean, float scale,
+                         double* part, void* stream);
 int fbn_gemm_split(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, int lda, int ldb,
                    int ldc, int transA, int transB, int rC_seg, int rC_off0, int rC_off1, float beta, float* stats,
                    float* ws, size_t ws_bytes, const void* A2, int lda2, int kseg, const void* B2, int ldb2, int nseg,

@@ -342,3 +342,50 @@ def test_deterministic_mode_bit_identical_runs(hip_device):
                                                 ("m", tr.flat_m))})
     for n in runs[0]:
         assert torch.equal(runs[0][n], runs[1][n]), n
+
+
+@pytest.mark.gpu
+def test_graph_eager_interleave_bit_identical(hip_device):
+    """bench.py's launch-mode trial switches between hipGraph replays (one captured step per batch)
+    and eager steps mid-run: every buffer that carries state across steps (table, moments, last[],
+    the deferred-gradient ring and pend[], pre-claims, dense Adam state, step counter) is persistent
+    and shared by both.  A run mixing replays and eager steps equals an all-eager run bit for bit."""
+    V, B, n = 40000, 64, 9
+    cfg = {"embedding_dim": 128, "vocab_size": V, "compute_dtype": "bf16"}
+    torch.manual_seed(0)
+    init = oracle_build(None, {"embedding_dim": 128, "vocab_size": V}).state_dict()
+    batches = []
+    for s in range(n + 1):
+        b, y = make_batch(900 + s, B, V)
+        batches.append(({k: v.to(hip_device) for k, v in b.items()}, y.to(hip_device)))
+    kw = dict(total_steps=40, batch_size=B, device=hip_device, init_state=init, lazy_window=4)
+    ref = FiBiNETTrainer(cfg, **kw)
+    for s in range(n):
+        ref.step(*batches[s], next_batch=batches[s + 1][0])
+    mix = FiBiNETTrainer(cfg, **kw)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        mix.step(*batches[0], next_batch=batches[1][0])        # the warm-up step before capture
+    torch.cuda.current_stream().wait_stream(side)
+    graphs, pool = {}, None
+    for s in range(1, n):
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, pool=pool):
+            mix.step(*batches[s], next_batch=batches[s + 1][0])
+        pool = gr.pool()
+        graphs[s] = gr
+    torch.cuda.synchronize()
+    for s in range(1, n):
+        if s in (1, 2, 5, 8):
+            graphs[s].replay()
+        else:
+            mix.step(*batches[s], next_batch=batches[s + 1][0])
+    torch.cuda.synchronize()
+    assert mix.device_step() == ref.device_step() == n
+    for a, c in ((ref.E, mix.E), (ref.Em, mix.Em), (ref.Ev, mix.Ev), (ref.flat_p, mix.flat_p), (ref.flat_m, mix.flat_m),
+                 (ref.last, mix.last), (ref.pend, mix.pend)):
+        assert torch.equal(a, c)
+    ref.flush()
+    mix.flush()
+    assert torch.equal(ref.E, mix.E)

@@ -19,11 +19,12 @@ import sys
 # is at least half the largest (MLP layer 1 forward shares its grid with MLP layer 2's dgrad)
 KERNELS = {
     "fields_fwd": ("fields_fwd_kernel<128", None, None),
-    # the claimed-row catch-up (fused with the row claims) is the adam_catchup launch with the
-    # largest grid, the rolling window (side stream) the one with the smallest
-    "adam_catchup": ("adam_catchup_kernel<128", "max", None),
-    "adam_window": ("adam_catchup_kernel<128", "min", None),
-    "adam_prefetch": ("adam_prefetch_kernel<128", None, None),
+    # the claimed-row catch-up (fused with the row claims), the rolling window and the next-batch
+    # prefetch's two passes (the bench's events bracket both; summed below)
+    "adam_catchup": ("adam_claim2_kernel<128", None, None),
+    "adam_window": ("adam_window2_kernel<128", None, None),
+    "adam_prefetch": ("adam_prefetch2_kernel<128", None, None),
+    "adam_pretag": ("adam_pretag_kernel", None, None),
     "gemm_mlp0": ("gemm_dma16_kernel<64, 128, false, false", "262144", "max"),
     "adam_touched": ("adam_touched_kernel<128", None, None),
     "adam_commit": ("adam_commit_kernel<128", None, None),
@@ -74,6 +75,10 @@ def main():
         res[key] = {"kernel": sub, "fetch_bytes": round(fb), "write_bytes": round(wb),
                     "bytes_per_launch": round(fb + wb), "dispatches": len(f),
                     "note": "FETCH_SIZE KiB x 2 (gfx950 16-B-lane reads) + WRITE_SIZE KiB"}
+    if "adam_prefetch" in res and "adam_pretag" in res:   # one fbn_adam_prefetch call = both passes
+        for k in ("fetch_bytes", "write_bytes", "bytes_per_launch"):
+            res["adam_prefetch"][k] += res["adam_pretag"][k]
+        res["adam_prefetch"]["kernel"] += " + adam_pretag_kernel"
     json.dump(res, open(outp, "w"), indent=1)
     for k, v in res.items():
         print(f"{k:14s} fetch {v['fetch_bytes'] / 1e6:9.2f} MB  write {v['write_bytes'] / 1e6:9.2f} MB  "
