@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--mode", default="auto", choices=["auto", "graph", "eager"],
                     help="N = 1: replay one hipGraph per batch, launch eagerly, or (auto) time both for a few "
                          "steps after priming and run the timed steps in the faster mode")
+    ap.add_argument("--main-priority", action="store_true",
+                    help="run the step on a high-priority stream (the side stream stays at normal priority)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=20)
     ap.add_argument("--probe-steps", type=int, default=10)
@@ -187,6 +189,10 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
     use_graph = not sharded and not args.no_graph and args.mode != "eager"
     trial_n = 16 if (use_graph and args.mode == "auto") else 0
     total = 1 + (nb if use_graph else 0) + prime + W + K + args.probe_steps + 16 + 4 * trial_n
+    if args.main_priority:
+        # the step's own stream at high priority: the hardware queue arbiter then dispatches its
+        # workgroups ahead of the table-Adam side stream's when both have work pending
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
     init = _initial_state(cfg, V, world, rank, dev)
     tr = FiBiNETTrainer(cfg, total_steps=total, batch_size=B, device=dev, rank=rank, world=world,
                         init_state=init, stage_on_cpu=rehearsal, lazy_window=F, prefetch_rows=args.prefetch,

@@ -44,8 +44,14 @@ SIGNATURES = {
     "fbn_bn_bwd_fused": (I, [P, P, P, P, P, F, P, P, P, P, I, I, D, P, P, P, P, P, P, P, P, P]),
     "fbn_colsum_partial": (I, [P, I, I, I, P, P]),
     "fbn_sum_jobs": (I, [P, I, P]),
+    "fbn_sum_jobs2": (I, [P, I, P, I, P]),
+    "fbn_gemm_slabs_size": (SZ, [I, I, I]),
+    "fbn_gemm_slabs": (I, [P, P, I, I, I, I, I, I, I, P, SZ, P, I, I, P, I, I, P, P]),
     "fbn_fields_fwd": (I, [P, P, P, P, P, P, P, F, P, I, P, LL, P, P, P, P, P, I, P, P, P, P, I, I, P, P, P, P, P, I, I, I, I,
                            P]),
+    "fbn_fields_fwd_hot": (I, [P, P, P, P, P, P, P, F, P, I, P, LL, P, P, P, P, I, P, P, P, P, I, I, P, P, P, P, P,
+                               I, I, I, P, P, I, P]),
+    "fbn_hot_rows": (I, [P, P, I, I, LL, P, P, P, I, I, I, P]),
     "fbn_fields_bwd_partials_size": (I, [I, I, I]),
     "fbn_fields_bwd_grid": (I, [I, I]),
     "fbn_fields_bwd": (I, [P, P, P, P, P, P, P, F, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P, P, P, LL, P, P, I, I,

@@ -51,7 +51,15 @@ struct FieldArgs {
   long long V;              // rows of the table (mode 0)
   int B, L, ldc, R, n_cate, c16;
   float ln_eps;
+  const int* hot;           // optional hot-row list (fbn_hot_rows) staged in LDS: [H] row ids
+  const int* hot_n;         // its length (entries past H ignored)
+  int H;
 };
+
+// hot-row staging (fbn_fields_fwd_hot, an A/B variant of the gather): up to FBN_HOT_ROWS(D) rows
+// (32 KB of f32) sit in LDS, found through an open-addressed id table of twice that size
+#define FBN_HOT_ROWS(D) ((8192 / (D)) < 256 ? (8192 / (D)) : 256)
+__device__ __forceinline__ unsigned hot_hash(int r) { return (unsigned)r * 0x9E3779B1u; }
 
 // Sparse-gradient registration: the first entry e = b*(L+1)+t that touches row r claims it
 // (map[r] = e, slot_row[e] = r).  Slots are entry indices, so no shared counter is needed:
@@ -111,9 +119,41 @@ __device__ __forceinline__ f32x4 load_row(const FieldArgs& p, size_t r, int q) {
   }
 }
 
-template <int D, int MODE, int HCH>
+// BUF (MODE 0, tables under 4 GB): the history rows are read through a buffer resource over the
+// table, and a padding / past-L slot's load gets an out-of-range offset -- the buffer unit returns
+// zeros without a memory request, so dead slots stay off the fetch path (the global-load form
+// reads row 0 for them: an L2 hit, but L2 bandwidth and TA cycles all the same)
+#define FBN_BUF_FLAGS 0x00020000   // gfx9 buffer descriptor word 3 (raw, 32-bit dwords)
+template <int D, int MODE, int HCH, bool BUF = false, bool HOT = false>
 __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
   FBN_MAIN_PRIO();
+  // (unused, and dropped, unless BUF)
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(p.table), 0, (int)((unsigned long long)p.V * D * 4), FBN_BUF_FLAGS);
+  constexpr int HR = HOT ? FBN_HOT_ROWS(D) : 1, HT = 2 * HR;   // staged rows, id-table slots
+  __shared__ f32x4 hrow[HOT ? HR * (D / 4) : 1];
+  __shared__ int hkey[HOT ? HT : 1];   // staged row id (-1 = empty)
+  __shared__ int hval[HOT ? HT : 1];   // its index in hrow
+  int nh = 0;
+  if constexpr (HOT) {
+    nh = min(*p.hot_n, min(p.H, HR));
+    for (int i = threadIdx.x; i < HT; i += blockDim.x) hkey[i] = -1;
+    __syncthreads();
+    for (int i = threadIdx.x; i < nh; i += blockDim.x) {   // insert (linear probing, CAS in LDS)
+      const int r = p.hot[i];
+      unsigned h = hot_hash(r) >> (32 - __builtin_ctz(HT));
+      for (int k = 0; k < HT; ++k, h = (h + 1) & (HT - 1))
+        if (atomicCAS(&hkey[h], -1, r) == -1) {
+          hval[h] = i;
+          break;
+        }
+    }
+    for (int i = threadIdx.x; i < nh * (D / 4); i += blockDim.x) {
+      const int j = i / (D / 4), c = i - j * (D / 4);
+      hrow[i] = *reinterpret_cast<const f32x4*>(p.table + (size_t)p.hot[j] * D + 4 * c);
+    }
+    __syncthreads();
+  }
   constexpr int G = D / 4;                  // lanes per sample
   constexpr int SPW = 64 / G;               // samples per wave
   const int lane = threadIdx.x & 63;
@@ -183,7 +223,27 @@ __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
         for (int j = 0; j < IPL; ++j)
           if ((t / G) == j) r = __shfl(sid[j], gbase + (t % G), 64);
         live[u] = t < L && r >= 0;
-        hist[u] = load_row<D, MODE>(p, live[u] ? r : 0, q);
+        if constexpr (HOT) {
+          // two probes of the id table (slot -> list index): a staged row is read from LDS and
+          // its global load is sent out of range (no fetch)
+          int hi = -1;
+          if (live[u] && nh > 0) {
+            const unsigned h = hot_hash(r) >> (32 - __builtin_ctz(HT));
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+              const unsigned hk = (h + k) & (HT - 1);
+              if (hi < 0 && hkey[hk] == r) hi = hval[hk];
+            }
+          }
+          const unsigned off = (live[u] && hi < 0) ? ((unsigned)r * D + 4 * q) * 4u : 0xFFFFFFF0u;
+          hist[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+          if (hi >= 0) hist[u] = hrow[hi * (D / 4) + q];
+        } else if constexpr (BUF) {
+          const unsigned off = live[u] ? ((unsigned)r * D + 4 * q) * 4u : 0xFFFFFFF0u;
+          hist[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+        } else {
+          hist[u] = load_row<D, MODE>(p, live[u] ? r : 0, q);
+        }
       }
 #pragma unroll
       for (int u = 0; u < HCH; ++u) {
@@ -595,19 +655,31 @@ static int fields_grid(int B, int D, int cap = 1024) {
 
 // history rows per chunk: every row of a chunk is in flight at once (branch-free issue); more rows
 // per chunk = fewer dependent round trips but more registers (fewer waves resident)
-template <int MODE, int HCH>
-static int launch_fields_fwd_h(const FieldArgs& a, int D, hipStream_t st) {
-  const int grid = fields_grid(a.B, D);
+template <int MODE, int HCH, bool BUF, bool HOT = false>
+static int launch_fields_fwd_hb(const FieldArgs& a, int D, hipStream_t st) {
+  // hot staging: fewer, longer-lived workgroups (each stages the hot rows once)
+  const int grid = fields_grid(a.B, D, HOT ? 256 : 1024);
   switch (D) {
-    case 16: hipLaunchKernelGGL((fields_fwd_kernel<16, MODE, HCH>), dim3(grid), dim3(256), 0, st, a); break;
-    case 32: hipLaunchKernelGGL((fields_fwd_kernel<32, MODE, HCH>), dim3(grid), dim3(256), 0, st, a); break;
-    case 64: hipLaunchKernelGGL((fields_fwd_kernel<64, MODE, HCH>), dim3(grid), dim3(256), 0, st, a); break;
-    case 128: hipLaunchKernelGGL((fields_fwd_kernel<128, MODE, HCH>), dim3(grid), dim3(256), 0, st, a); break;
-    case 256: hipLaunchKernelGGL((fields_fwd_kernel<256, MODE, HCH>), dim3(grid), dim3(256), 0, st, a); break;
+    case 16: hipLaunchKernelGGL((fields_fwd_kernel<16, MODE, HCH, BUF, HOT>), dim3(grid), dim3(256), 0, st, a); break;
+    case 32: hipLaunchKernelGGL((fields_fwd_kernel<32, MODE, HCH, BUF, HOT>), dim3(grid), dim3(256), 0, st, a); break;
+    case 64: hipLaunchKernelGGL((fields_fwd_kernel<64, MODE, HCH, BUF, HOT>), dim3(grid), dim3(256), 0, st, a); break;
+    case 128: hipLaunchKernelGGL((fields_fwd_kernel<128, MODE, HCH, BUF, HOT>), dim3(grid), dim3(256), 0, st, a); break;
+    case 256: hipLaunchKernelGGL((fields_fwd_kernel<256, MODE, HCH, BUF, HOT>), dim3(grid), dim3(256), 0, st, a); break;
     default: fbn_set_error("fields: embedding_dim must be one of 16,32,64,128,256"); return FBN_ERR_UNSUPPORTED;
   }
   FBN_CHECK_LAUNCH();
   return FBN_OK;
+}
+
+template <int MODE, int HCH>
+static int launch_fields_fwd_h(const FieldArgs& a, int D, hipStream_t st) {
+  if constexpr (MODE == 0) {
+    if (a.hot) return launch_fields_fwd_hb<0, HCH, true, true>(a, D, st);
+    // buffer-resource history loads while the table's byte extent fits the descriptor's 32 bits
+    static const bool nobuf = getenv("FBN_FIELDS_NOBUF") != nullptr;   // A/B knob
+    if (!nobuf && (unsigned long long)a.V * D * 4 < 0xFFFFFF00ull) return launch_fields_fwd_hb<0, HCH, true>(a, D, st);
+  }
+  return launch_fields_fwd_hb<MODE, HCH, false>(a, D, st);
 }
 
 template <int MODE>
@@ -618,6 +690,14 @@ static int launch_fields_fwd(const FieldArgs& a, int D, hipStream_t st) {
   return launch_fields_fwd_h<MODE, 10>(a, D, st);
 }
 
+static int fields_fwd_impl(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes,
+                           const int64_t* views, const float* hmm, const float* ln_g, const float* ln_b,
+                           float ln_eps, const float* cate, int n_cate, const float* table, long long V,
+                           const int* pos, const float* w1, const float* b1, const float* w2,
+                           const float* b2, int R, float* X, float* Vc, short* Vc16, void* c, int ldc, int c_bf16,
+                           float* a_out, float* cnt_out, int* err, int* map, int* slot_row, int B, int L,
+                           int D, int rows_bf16, const int* hot, const int* hot_n, int H, void* stream);
+
 extern "C" int fbn_fields_fwd(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes,
                               const int64_t* views, const float* hmm, const float* ln_g, const float* ln_b,
                               float ln_eps, const float* cate, int n_cate, const float* table, long long V,
@@ -626,6 +706,67 @@ extern "C" int fbn_fields_fwd(const int64_t* item_id, const int64_t* item_seq, c
                               float* a_out,
                               float* cnt_out, int* err, int* map, int* slot_row, int B, int L,
                               int D, int rows_bf16, void* stream) {
+  return fields_fwd_impl(item_id, item_seq, likes, views, hmm, ln_g, ln_b, ln_eps, cate, n_cate, table, V, pos, w1,
+                         b1, w2, b2, R, X, Vc, Vc16, c, ldc, c_bf16, a_out, cnt_out, err, map, slot_row, B, L, D,
+                         rows_bf16, nullptr, nullptr, 0, stream);
+}
+
+// the gather with the batch's hot rows (fbn_hot_rows) staged in LDS (single GPU, f32 table < 4 GB)
+extern "C" int fbn_fields_fwd_hot(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes,
+                                  const int64_t* views, const float* hmm, const float* ln_g, const float* ln_b,
+                                  float ln_eps, const float* cate, int n_cate, const float* table, long long V,
+                                  const float* w1, const float* b1, const float* w2, const float* b2, int R, float* X,
+                                  float* Vc, short* Vc16, void* c, int ldc, int c_bf16, float* a_out, float* cnt_out,
+                                  int* err, int* map, int* slot_row, int B, int L, int D, const int* hot,
+                                  const int* hot_n, int H, void* stream) {
+  if (!hot || !hot_n || (unsigned long long)V * D * 4 >= 0xFFFFFF00ull) {
+    fbn_set_error("fbn_fields_fwd_hot: needs the hot list and a table under 4 GB");
+    return FBN_ERR_ARG;
+  }
+  return fields_fwd_impl(item_id, item_seq, likes, views, hmm, ln_g, ln_b, ln_eps, cate, n_cate, table, V, nullptr,
+                         w1, b1, w2, b2, R, X, Vc, Vc16, c, ldc, c_bf16, a_out, cnt_out, err, map, slot_row, B, L, D, 0,
+                         hot, hot_n, H, stream);
+}
+
+// Hot rows of a batch (clear = 0): every entry counts its row (cnt [V] int32, zero on entry); the
+// entry that brings a row's count to tau appends it to hot[] (hot_n: length, may exceed H).
+// clear = 1: the same entries zero their counts and hot_n (after the gather has read the list).
+__global__ void hot_rows_kernel(const int64_t* __restrict__ item, const int64_t* __restrict__ seq, int B, int L,
+                                long long V, int* __restrict__ cnt, int* __restrict__ hot, int* __restrict__ hot_n,
+                                int H, int tau, int clear) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (clear && i == 0) *hot_n = 0;
+  if (i >= (long long)B * (L + 1)) return;
+  const long long b = i / (L + 1), t = i - b * (L + 1);
+  const long long id = t == 0 ? item[b] : seq[b * L + (t - 1)];
+  if (id <= 0 || id >= V) return;
+  if (clear) {
+    cnt[id] = 0;
+    return;
+  }
+  if (atomicAdd(cnt + id, 1) == tau - 1) {
+    const int s = atomicAdd(hot_n, 1);
+    if (s < H) hot[s] = (int)id;
+  }
+}
+
+extern "C" int fbn_hot_rows(const int64_t* item, const int64_t* seq, int B, int L, long long V, int* cnt, int* hot,
+                            int* hot_n, int H, int tau, int clear, void* stream) {
+  const long long n = (long long)B * (L + 1);
+  if (n <= 0) return FBN_OK;
+  hipLaunchKernelGGL(hot_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, item,
+                     L > 0 ? seq : nullptr, B, L, V, cnt, hot, hot_n, H, tau < 1 ? 1 : tau, clear);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+static int fields_fwd_impl(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes,
+                           const int64_t* views, const float* hmm, const float* ln_g, const float* ln_b,
+                           float ln_eps, const float* cate, int n_cate, const float* table, long long V,
+                           const int* pos, const float* w1, const float* b1, const float* w2,
+                           const float* b2, int R, float* X, float* Vc, short* Vc16, void* c, int ldc, int c_bf16,
+                           float* a_out, float* cnt_out, int* err, int* map, int* slot_row, int B, int L,
+                           int D, int rows_bf16, const int* hot, const int* hot_n, int H, void* stream) {
   if (B <= 0) return FBN_OK;
   if (L < 0 || L > 32 || R < 1 || R > FBN_MAXR || (ldc & 3)) {
     fbn_set_error("fbn_fields_fwd: need 0 <= L <= 32, 1 <= R <= 8, ldc % 4 == 0");
@@ -638,6 +779,7 @@ extern "C" int fbn_fields_fwd(const int64_t* item_id, const int64_t* item_seq, c
   a.X = X; a.Vc = Vc; a.Vc16 = Vc16; a.c = c; a.a_out = a_out; a.cnt_out = cnt_out; a.err = err;
   a.map = map; a.slot_row = slot_row;
   a.V = V; a.B = B; a.L = L; a.ldc = ldc; a.R = R; a.n_cate = n_cate; a.ln_eps = ln_eps; a.c16 = c_bf16;
+  a.hot = hot; a.hot_n = hot_n; a.H = H;
   if (pos && rows_bf16) return launch_fields_fwd<2>(a, D, (hipStream_t)stream);
   if (pos) return launch_fields_fwd<1>(a, D, (hipStream_t)stream);
   return launch_fields_fwd<0>(a, D, (hipStream_t)stream);
@@ -670,9 +812,10 @@ static int launch_fields_bwd(const FieldBwdArgs& a, int D, hipStream_t st) {
   return a.R <= 3 ? launch_fields_bwd_r<MODE, 3>(a, D, st) : launch_fields_bwd_r<MODE, FBN_MAXR>(a, D, st);
 }
 
-// partials: [fbn_fields_bwd_grid(B,D)][fbn_fields_bwd_partials_size(D,R,n_cate)] scratch;
-// partials: [fbn_fields_bwd_grid(B,D)][P] scratch; param_grads: host array of 8 device
-// pointers receiving the gradients of w1, b1, w2, b2, ln_g, ln_b, cate.
+// partials: [fbn_fields_bwd_grid(B,D)][P] scratch (P = fbn_fields_bwd_partials_size(D,R,n_cate));
+// param_grads: host array of 8 device pointers receiving the gradients of w1, b1, w2, b2, ln_g,
+// ln_b, cate, mm_proj bias (segments of 6R, R, 6R, 6, D, D, n_cate*D, D columns of a partial row),
+// or NULL: the partial rows are left for the caller to sum (the trainer's one fbn_sum_jobs2 launch).
 extern "C" int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes,
                               const int64_t* views, const float* hmm, const float* ln_g, const float* ln_b,
                               float ln_eps, const float* w1, const float* b1, const float* w2, int R, int n_cate,
@@ -692,6 +835,7 @@ extern "C" int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, c
   int rc = !pos ? launch_fields_bwd<0>(p, D, st) : send_bf16 ? launch_fields_bwd<2>(p, D, st)
                                                                : launch_fields_bwd<1>(p, D, st);
   if (rc) return rc;
+  if (!param_grads) return FBN_OK;   // deferred: the caller sums the partial rows (fbn_sum_jobs2, ld = P)
   const int P = 13 * R + 6 + 3 * D + n_cate * D;
   const int nblk = fields_grid(B, D, FBN_FB_MAXBLK);
 

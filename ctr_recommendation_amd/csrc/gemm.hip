@@ -860,6 +860,14 @@ static GemmPlan plan_dma16(int M, int N, int K) {
   return p;
 }
 
+// K-slabs of the LDS-DMA plan after the K-per-split rounding gemm_impl applies (slab mode)
+static int slab_split(int M, int N, int K) {
+  const GemmPlan p = plan_dma16(M, N, K);
+  int per = fbn_cdiv(K, p.split);
+  per = fbn_cdiv(per, 64) * 64;
+  return K > 0 ? fbn_cdiv(K, per) : 1;
+}
+
 template <int BM, int BN, bool TA, bool TB, bool BF16, bool A16, bool B16>
 static void launch_tile(const GemmArgs& g, int nsplit, hipStream_t st) {
   const int tn = fbn_cdiv(g.N, BN), tm = fbn_cdiv(g.M, BM);
@@ -934,7 +942,7 @@ static int gemm_impl(const void* A, const void* B, float* C, const float* bias, 
                      int ldb, int ldc, int transA, int transB, int rB_seg, int rB_off0, int rB_off1, int rC_seg,
                      int rC_off0, int rC_off1, float beta, int bf16, int a16, int b16, float* stats, float* ws,
                      size_t ws_bytes, const void* A2, int lda2, int kseg, const void* B2, int ldb2, int nseg,
-                     void* stream, int c16 = 0, const GemmArgs* bnb = nullptr);
+                     void* stream, int c16 = 0, const GemmArgs* bnb = nullptr, int* slabs = nullptr);
 
 extern "C" int fbn_gemm(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, int lda,
                         int ldb, int ldc, int transA, int transB, int rB_seg, int rB_off0, int rB_off1, int rC_seg,
@@ -971,11 +979,33 @@ extern "C" int fbn_gemm_bf16out(const void* A, const void* B, void* C, int M, in
                    stream, 1);
 }
 
+// Slab mode (bf16 LDS-DMA path; the wgrad GEMMs of the trainer): op(A) op(B) with the split-K
+// partial products left in ws as nsplit slabs [nsplit][M][N] (f32) -- no reduce launch; the
+// caller sums them in the step's fbn_sum_jobs2 launch with the other deferred reductions (slab
+// order, deterministic).  A2/kseg, B2/nseg as fbn_gemm_split.  Returns FBN_OK and *nsplit.
+extern "C" size_t fbn_gemm_slabs_size(int M, int N, int K) {
+  return (M > 0 && N > 0) ? (size_t)slab_split(M, N, K) * M * N * sizeof(float) : 0;
+}
+extern "C" int fbn_gemm_slabs(const void* A, const void* B, int M, int N, int K, int lda, int ldb, int transA,
+                              int transB, float* ws, size_t ws_bytes, const void* A2, int lda2, int kseg,
+                              const void* B2, int ldb2, int nseg, int* nsplit, void* stream) {
+  if (!nsplit) { fbn_set_error("fbn_gemm_slabs: null nsplit"); return FBN_ERR_ARG; }
+  if ((A2 && (transA || (kseg & 127) || (lda2 & 7) || ((uintptr_t)A2 & 15))) ||
+      (B2 && (transB || (nseg & 127) || (ldb2 & 7) || ((uintptr_t)B2 & 15)))) {
+    fbn_set_error("fbn_gemm_slabs: A2 needs a k-contiguous A, B2 a k-major B; segments % 128, ld % 8, 16-B aligned");
+    return FBN_ERR_ARG;
+  }
+  return gemm_impl(A, B, ws, nullptr, M, N, K, lda, ldb, N, transA, transB, 0x7fffffff, 0, 0, 0x7fffffff, 0, 0, 0.f,
+                   1, 1, 1, nullptr, ws, ws_bytes, A2, lda2, A2 ? kseg : 0x7fffffff, B2, ldb2,
+                   B2 ? nseg : 0x7fffffff, stream, 0, nullptr, nsplit);
+}
+
 static int gemm_impl(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, int lda,
                      int ldb, int ldc, int transA, int transB, int rB_seg, int rB_off0, int rB_off1, int rC_seg,
                      int rC_off0, int rC_off1, float beta, int bf16, int a16, int b16, float* stats, float* ws,
                      size_t ws_bytes, const void* A2, int lda2, int kseg, const void* B2, int ldb2, int nseg,
-                     void* stream, int c16, const GemmArgs* bnb) {
+                     void* stream, int c16, const GemmArgs* bnb, int* slabs) {
+  if (slabs) *slabs = 0;
   if (M <= 0 || N <= 0) return FBN_OK;
   if (!A || !B || !C) { fbn_set_error("fbn_gemm: null operand"); return FBN_ERR_ARG; }
   // 16-B vector loads along the contiguous dimension of every operand
@@ -1013,7 +1043,16 @@ static int gemm_impl(const void* A, const void* B, float* C, const float* bias, 
     return FBN_ERR_ARG;
   }
   GemmPlan p = dma16 ? plan_dma16(M, N, K) : plan_gemm(M, N, K, bk);
-  if (const char* f = getenv("FBN_GEMM_FORCE")) {      // tuning sweeps only: "bm,bn,split[,waves[,stages]]"
+  if (slabs) {
+    // slab mode (fbn_gemm_slabs): the K-slabs stay in ws for a later fbn_sum_jobs2 launch; a plan
+    // with one split writes its single slab there too
+    if (!dma16 || bias || stats || c16 || bnb || beta != 0.f || !ws ||
+        ws_bytes < (size_t)slab_split(M, N, K) * M * N * sizeof(float)) {
+      fbn_set_error("fbn_gemm_slabs: needs the bf16 LDS-DMA path, no bias / beta / stats, ws >= fbn_gemm_slabs_size");
+      return FBN_ERR_ARG;
+    }
+    p.split = slab_split(M, N, K);
+  } else if (const char* f = getenv("FBN_GEMM_FORCE")) {   // tuning sweeps only: "bm,bn,split[,waves[,stages]]"
     int a = 0, b = 0, c = 0, w = 4, sg = 0;
     if (sscanf(f, "%d,%d,%d,%d,%d", &a, &b, &c, &w, &sg) >= 3) p = {a, b, c, w, sg};
   }
@@ -1027,6 +1066,10 @@ static int gemm_impl(const void* A, const void* B, float* C, const float* bias, 
   if (stats && p.split == 1 && !(dma16 && p.waves == 8 && p.bm == 128)) p.bm = 64;
   g.kchunk = K > 0 ? per : 0;
   g.ws = ws;
+  if (slabs && p.split == 1) {   // one slab: the kernel's plain C store into ws
+    g.C = ws; g.ldc = N;
+    g.rC = {0x7fffffff, 0, 0};
+  }
   hipStream_t st = (hipStream_t)stream;
   const int key = (transA ? 2 : 0) | (transB ? 1 : 0);
   if (dma16) {
@@ -1043,6 +1086,10 @@ static int gemm_impl(const void* A, const void* B, float* C, const float* bias, 
     default: launch_types<true, true>(g, p, bf16, a16, b16, st); break;
   }
   FBN_CHECK_LAUNCH();
+  if (slabs) {
+    *slabs = p.split;
+    return FBN_OK;
+  }
   if (p.split > 1 && stats) {
     hipLaunchKernelGGL(gemm_splitk_reduce_stats, dim3(fbn_cdiv(N, 64), fbn_cdiv(M, 64)), dim3(256), 0, st, g,
                        p.split);

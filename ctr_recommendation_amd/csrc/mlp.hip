@@ -714,34 +714,90 @@ __global__ void __launch_bounds__(256) bn_bwd_apply4_kernel(BnBwdSrc s, const fl
 // partials, the head-bias gradient and the loss from [B] vectors):
 //   out[c] = beta * out[c] + scale * sum_{k < nch} part[k * C + c]
 // one 256-thread block per output column, fixed-order tree (deterministic).
+//   (ld = row stride of part; 0 = C)
+// and, in the same launch (fbn_sum_jobs2), the split-K slabs of the step's weight-gradient GEMMs
+// (fbn_gemm_slabs): out[m * ldc + rm(n)] = beta * out + sum_{z < nsplit} ws[z][m][n] (slab groups
+// then a fixed-order fold: deterministic), rm(n) = n + (n < seg ? off0 : off1).
 struct SumJob {
   const float* part;
   float* out;
   int nch, C;
   float scale, beta;
+  int ld;
+  int pad_;
 };
-#define FBN_MAX_SUM_JOBS 8
+struct SlabJob {
+  const float* ws;
+  float* out;
+  int M, N, ldc, nsplit, seg, off0, off1;
+  float beta;
+};
+#define FBN_MAX_SUM_JOBS 16
+#define FBN_MAX_SLAB_JOBS 8
+#define FBN_SLAB_GROUPS 4      // slab groups per output quad (256 threads = 64 quads x 4 groups)
 struct SumJobs {
   SumJob j[FBN_MAX_SUM_JOBS];
   int col0[FBN_MAX_SUM_JOBS + 1];
   int n;
+  SlabJob s[FBN_MAX_SLAB_JOBS];
+  int blk0[FBN_MAX_SLAB_JOBS + 1];   // first block of each slab job (after the column blocks)
+  int ns;
 };
+__device__ __forceinline__ void slab_block(const SumJobs& J, int gb) {
+  __shared__ f32x4 red[FBN_SLAB_GROUPS][64];
+  int u = 0;
+  while (u + 1 < J.ns && gb >= J.blk0[u + 1]) ++u;
+  const SlabJob sj = J.s[u];
+  const int qd = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const size_t total = (size_t)sj.M * sj.N;
+  const size_t i4 = (size_t)(gb - J.blk0[u]) * 64 + qd;   // output quad
+  const bool ok = i4 < total / 4;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (ok) {
+    const float* src = sj.ws + i4 * 4;
+    int z = grp;
+    for (; z + 3 * FBN_SLAB_GROUPS < sj.nsplit; z += 4 * FBN_SLAB_GROUPS) {   // 4 slabs in flight
+      const f32x4 a = *reinterpret_cast<const f32x4*>(src + (size_t)z * total);
+      const f32x4 b = *reinterpret_cast<const f32x4*>(src + (size_t)(z + FBN_SLAB_GROUPS) * total);
+      const f32x4 c = *reinterpret_cast<const f32x4*>(src + (size_t)(z + 2 * FBN_SLAB_GROUPS) * total);
+      const f32x4 d = *reinterpret_cast<const f32x4*>(src + (size_t)(z + 3 * FBN_SLAB_GROUPS) * total);
+      acc += a; acc += b; acc += c; acc += d;
+    }
+    for (; z < sj.nsplit; z += FBN_SLAB_GROUPS) acc += *reinterpret_cast<const f32x4*>(src + (size_t)z * total);
+  }
+  red[grp][qd] = acc;
+  __syncthreads();
+  if (grp == 0 && ok) {
+    f32x4 t = red[0][qd];
+#pragma unroll
+    for (int k = 1; k < FBN_SLAB_GROUPS; ++k) t += red[k][qd];
+    const int m = (int)(i4 * 4 / sj.N), n = (int)(i4 * 4 - (size_t)m * sj.N);
+    float* cp = sj.out + (size_t)m * sj.ldc + n + (n < sj.seg ? sj.off0 : sj.off1);
+    if (sj.beta != 0.f) t += sj.beta * *reinterpret_cast<const f32x4*>(cp);
+    *reinterpret_cast<f32x4*>(cp) = t;
+  }
+}
 __global__ void __launch_bounds__(256) sum_jobs_kernel(SumJobs J) {
   __shared__ float red[4];
   const int gc = blockIdx.x;
+  if (gc >= J.col0[J.n]) {
+    slab_block(J, gc - J.col0[J.n]);
+    return;
+  }
   int u = 0;
   while (u + 1 < J.n && gc >= J.col0[u + 1]) ++u;
   const SumJob jb = J.j[u];
   const int c = gc - J.col0[u];
+  const size_t ld = jb.ld > 0 ? jb.ld : jb.C;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   int k = threadIdx.x;
   for (; k + 768 < jb.nch; k += 1024) {
-    a0 += jb.part[(size_t)k * jb.C + c];
-    a1 += jb.part[(size_t)(k + 256) * jb.C + c];
-    a2 += jb.part[(size_t)(k + 512) * jb.C + c];
-    a3 += jb.part[(size_t)(k + 768) * jb.C + c];
+    a0 += jb.part[(size_t)k * ld + c];
+    a1 += jb.part[(size_t)(k + 256) * ld + c];
+    a2 += jb.part[(size_t)(k + 512) * ld + c];
+    a3 += jb.part[(size_t)(k + 768) * ld + c];
   }
-  for (; k < jb.nch; k += 256) a0 += jb.part[(size_t)k * jb.C + c];
+  for (; k < jb.nch; k += 256) a0 += jb.part[(size_t)k * ld + c];
   float v = wave_sum((a0 + a1) + (a2 + a3));
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
@@ -1232,10 +1288,14 @@ extern "C" int fbn_colsum_partial(const float* X, int B, int C, int ldx, float* 
 
 extern "C" int fbn_row_chunks(int B) { return row_chunks(B); }
 
-// jobs: host array of n (<= 8) {part, out, nch, C, scale, beta} (copied into the kernel argument)
-extern "C" int fbn_sum_jobs(const SumJob* jobs, int n, void* stream) {
-  if (n <= 0) return FBN_OK;
-  if (n > FBN_MAX_SUM_JOBS) { fbn_set_error("fbn_sum_jobs: too many jobs"); return FBN_ERR_ARG; }
+// jobs: host array of n (<= 16) {part, out, nch, C, scale, beta, ld, pad} (copied into the kernel
+// argument); slabs: host array of ns (<= 8) {ws, out, M, N, ldc, nsplit, seg, off0, off1, beta}
+// (N, ldc, seg, off0, off1 multiples of 4; out 16-B aligned).  One launch for both.
+extern "C" int fbn_sum_jobs2(const SumJob* jobs, int n, const SlabJob* slabs, int ns, void* stream) {
+  if (n < 0 || ns < 0 || n > FBN_MAX_SUM_JOBS || ns > FBN_MAX_SLAB_JOBS) {
+    fbn_set_error("fbn_sum_jobs2: too many jobs");
+    return FBN_ERR_ARG;
+  }
   SumJobs J;
   J.n = n;
   J.col0[0] = 0;
@@ -1243,10 +1303,28 @@ extern "C" int fbn_sum_jobs(const SumJob* jobs, int n, void* stream) {
     J.j[i] = jobs[i];
     J.col0[i + 1] = J.col0[i] + jobs[i].C;
   }
-  if (J.col0[n] <= 0) return FBN_OK;
-  hipLaunchKernelGGL(sum_jobs_kernel, dim3(J.col0[n]), dim3(256), 0, (hipStream_t)stream, J);
+  J.ns = ns;
+  J.blk0[0] = 0;
+  for (int i = 0; i < ns; ++i) {
+    const SlabJob& sj = slabs[i];
+    if ((sj.N & 3) || (sj.ldc & 3) || (sj.off0 & 3) || (sj.off1 & 3) || (sj.seg != 0x7fffffff && (sj.seg & 3)) ||
+        ((uintptr_t)sj.out & 15) || ((uintptr_t)sj.ws & 15) || sj.nsplit < 1) {
+      fbn_set_error("fbn_sum_jobs2: slab job needs N, ldc, remap % 4, 16-B aligned buffers, nsplit >= 1");
+      return FBN_ERR_ARG;
+    }
+    J.s[i] = sj;
+    J.blk0[i + 1] = J.blk0[i] + (int)fbn_cdiv((long long)sj.M * sj.N / 4, 64);
+  }
+  const int blocks = J.col0[n] + J.blk0[ns];
+  if (blocks <= 0) return FBN_OK;
+  hipLaunchKernelGGL(sum_jobs_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, J);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
+}
+
+extern "C" int fbn_sum_jobs(const SumJob* jobs, int n, void* stream) {
+  if (n <= 0) return FBN_OK;
+  return fbn_sum_jobs2(jobs, n, nullptr, 0, stream);
 }
 
 extern "C" int fbn_bn_tile_moments(const float* part, int M, int C, double* out_d, void* stream) {

@@ -714,6 +714,17 @@ extern "C" int fbn_adam_selftest(int n, unsigned seed, unsigned long long* dev, 
 // constants of the last W <= FBN_LAZY_MAX_LAG steps sit in LDS.
 #define FBN_LAZY_MAX_LAG 512
 
+// Row state: ONE 16-B record per table row, {u64 pre-claim tag, i32 last, i32 pend}, so a claim
+// that needs all three (the critical-path adam_claim2, the prefetch) pulls one sector per row
+// instead of three.  The C ABI keeps field pointers: preclaim = record base, last = base + 8 B,
+// pend = base + 12 B; each field is indexed with the record stride below.
+#define FBN_RS_I 4   // record stride in ints
+#define FBN_RS_Q 2   // in u64
+// the whole record of row r from its `last` field pointer: {tag lo, tag hi, last, pend}
+__device__ __forceinline__ int4 row_state(const int* last, long long r) {
+  return *reinterpret_cast<const int4*>(last + (size_t)r * FBN_RS_I - 2);
+}
+
 // deferred gradients: pend[r] = index (b*2 + slot) of the per-sample vector row r received at step
 // last[r] (-1 = none); ring[(s % ring_n) * ring_stride + idx * D] holds step s's vectors
 struct PendSrc {
@@ -735,7 +746,7 @@ __device__ __forceinline__ void replay_rows(float* __restrict__ p, float* __rest
   f32x4 vv = *reinterpret_cast<f32x4*>(v + off);
   int s = k0;
   if (ps.pend) {
-    const int pe = ps.pend[r];
+    const int pe = ps.pend[(size_t)(r) * FBN_RS_I];
     if (pe >= 0) {   // step k0 with the deferred gradient (what fbn_adam_touched would have applied)
       const f32x4 gg = *reinterpret_cast<const f32x4*>(ps.ring + (size_t)(k0 % ps.ring_n) * ps.ring_stride +
                                                        (size_t)pe * D + 4 * q);
@@ -910,12 +921,12 @@ __device__ __forceinline__ void wide_rows(int r, int key, int pe, int cnt, int T
     wide_load<D>(nb, p, m, v, rnb, knb, pnb, ps, lane);
     wide_replay_pair<D, DW>(xa, ka, pa, xb, kb, pb, T, table, wd, b2, omb2, eps);
     wide_store<D>(xa, p, m, v, ra, lane);
-    last[ra] = T;   // every lane, one address
-    if (ps.pend) ps.pend[ra] = -1;
+    last[(size_t)(ra) * FBN_RS_I] = T;   // every lane, one address
+    if (ps.pend) ps.pend[(size_t)(ra) * FBN_RS_I] = -1;
     if (j0 + 1 < cnt) {
       wide_store<D>(xb, p, m, v, rb, lane);
-      last[rb] = T;
-      if (ps.pend) ps.pend[rb] = -1;
+      last[(size_t)(rb) * FBN_RS_I] = T;
+      if (ps.pend) ps.pend[(size_t)(rb) * FBN_RS_I] = -1;
     }
     xa = na; ra = rna; ka = kna; pa = pna;
     xb = nb; rb = rnb; kb = knb; pb = pnb;
@@ -986,7 +997,7 @@ __global__ void __launch_bounds__(256) adam_catchup_kernel(float* __restrict__ p
         const long long b = i / (cs.L + 1), tt = i - b * (cs.L + 1);
         const long long id = tt == 0 ? cs.item[b] : cs.seq[b * cs.L + (tt - 1)];
         int owner = -1;
-        const unsigned long long pv = (cs.pre && id > 0 && id < cs.V) ? cs.pre[id] : 0ull;
+        const unsigned long long pv = (cs.pre && id > 0 && id < cs.V) ? cs.pre[(size_t)(id) * FBN_RS_Q] : 0ull;
         if ((int)(pv >> 32) == t && t > 0) {   // pre-claimed: the smallest entry index claims
           owner = (int)(0xFFFFFFFFu - (unsigned)pv);
           if (owner == (int)i) {
@@ -1019,10 +1030,10 @@ __global__ void __launch_bounds__(256) adam_catchup_kernel(float* __restrict__ p
         if (!map || map[rr] == -1) r = (int)rr;   // claimed rows are replayed by their claiming entry
       }
       if (r >= 0) {
-        const int k0 = last[r];
+        const int k0 = last[(size_t)(r) * FBN_RS_I];
         if (k0 < t) {
           key = k0;
-          if (ps.pend) pe = ps.pend[r];
+          if (ps.pend) pe = ps.pend[(size_t)(r) * FBN_RS_I];
         }
       }
     }
@@ -1066,8 +1077,8 @@ __global__ void __launch_bounds__(256) adam_catchup_kernel(float* __restrict__ p
       if (j0 + grp < cnt) {
         row_replay_store<D, DW>(cur, p, m, v, rc, q, kc, pc >= 0, t, win, w0, table, wd, b2, omb2, eps);
         if (q == 0) {
-          last[rc] = t;
-          if (ps.pend) ps.pend[rc] = -1;
+          last[(size_t)(rc) * FBN_RS_I] = t;
+          if (ps.pend) ps.pend[(size_t)(rc) * FBN_RS_I] = -1;
         }
       }
       cur = nxt;
@@ -1111,13 +1122,13 @@ __global__ void __launch_bounds__(256) adam_prefetch_kernel(float* __restrict__ 
         ok = id > 0 && id < cs.V;
       }
       if (cs.pre && ok)   // next step's claim, decided now (non-returning, tagged)
-        atomicMax(cs.pre + id, ((unsigned long long)T << 32) | (0xFFFFFFFFull - (unsigned long long)i));
+        atomicMax(cs.pre + (size_t)id * FBN_RS_Q, ((unsigned long long)T << 32) | (0xFFFFFFFFull - (unsigned long long)i));
       if (ok && cs.map[id] == -1) {
-        const int k0 = last[id];
-        if (k0 < T && atomicCAS(last + id, k0, T) == k0) {
+        const int k0 = last[(size_t)(id) * FBN_RS_I];
+        if (k0 < T && atomicCAS(last + (size_t)id * FBN_RS_I, k0, T) == k0) {
           r = (int)id;
           key = k0;
-          if (ps.pend) pe = ps.pend[id];
+          if (ps.pend) pe = ps.pend[(size_t)(id) * FBN_RS_I];
         }
       }
     }
@@ -1160,7 +1171,7 @@ __global__ void __launch_bounds__(256) adam_pretag_kernel(ClaimSrc cs, int n, co
   const unsigned long long T = (unsigned long long)(*step + 1);
   const long long b = i / (cs.L + 1), tt = i - b * (cs.L + 1);
   const long long id = tt == 0 ? cs.item[b] : cs.seq[b * cs.L + (tt - 1)];
-  if (id > 0 && id < cs.V) atomicMax(cs.pre + id, (T << 32) | (0xFFFFFFFFull - (unsigned long long)i));
+  if (id > 0 && id < cs.V) atomicMax(cs.pre + (size_t)id * FBN_RS_Q, (T << 32) | (0xFFFFFFFFull - (unsigned long long)i));
 }
 
 // adam_tab1 with the step's constants as (w1, nss, rbc2s, dmul): the same operations, same order
@@ -1400,15 +1411,16 @@ __global__ void __launch_bounds__(256) adam_prefetch2_kernel(float* __restrict__
     const long long b = i / (cs.L + 1), tt = i - b * (cs.L + 1);
     const long long id = tt == 0 ? cs.item[b] : cs.seq[b * cs.L + (tt - 1)];
     if (id > 0 && id < cs.V) {
-      const unsigned long long pv = cs.pre[id];
+      const int4 rs = row_state(last, id);   // tag, last, pend: one 16-B load
+      const unsigned long long pv = ((unsigned long long)(unsigned)rs.y << 32) | (unsigned)rs.x;
       if ((int)(pv >> 32) == T && (0xFFFFFFFFu - (unsigned)pv) == (unsigned)i && cs.map[id] == -1) {
-        const int k0 = last[id];
+        const int k0 = rs.z;
         if (k0 < T) {   // this entry owns the row: its replay through step T - 1
           r = (int)id;
-          if (ps.pend) pe = ps.pend[id];
+          if (ps.pend) pe = rs.w;
           key = k0 + (pe >= 0 ? 1 : 0);   // first zero-gradient step (after the deferred one)
-          last[id] = T;
-          if (pe >= 0) ps.pend[id] = -1;
+          last[(size_t)(id) * FBN_RS_I] = T;
+          if (pe >= 0) ps.pend[(size_t)(id) * FBN_RS_I] = -1;
         }
       }
     }
@@ -1443,9 +1455,10 @@ __global__ void __launch_bounds__(256) adam_claim2_kernel(float* __restrict__ p,
     const long long id = tt == 0 ? cs.item[b] : cs.seq[b * cs.L + (tt - 1)];
     int owner = -1, mine = -1;
     if (id > 0 && id < cs.V) {
-      const unsigned long long pv = cs.pre ? cs.pre[id] : 0ull;
-      const int k0 = last[id];
-      const int pe0 = ps.pend ? ps.pend[id] : -1;
+      const int4 rs = row_state(last, id);   // tag, last, pend: one 16-B load
+      const unsigned long long pv = cs.pre ? (((unsigned long long)(unsigned)rs.y << 32) | (unsigned)rs.x) : 0ull;
+      const int k0 = rs.z;
+      const int pe0 = ps.pend ? rs.w : -1;
       if ((int)(pv >> 32) == t && t > 0) {   // pre-claimed: the smallest entry index claims
         owner = (int)(0xFFFFFFFFu - (unsigned)pv);
         if (owner == (int)i) {
@@ -1471,8 +1484,8 @@ __global__ void __launch_bounds__(256) adam_claim2_kernel(float* __restrict__ p,
         r = mine;
         pe = pe0;
         key = k0 + (pe0 >= 0 ? 1 : 0);
-        last[mine] = t;
-        if (pe0 >= 0) ps.pend[mine] = -1;
+        last[(size_t)(mine) * FBN_RS_I] = t;
+        if (pe0 >= 0) ps.pend[(size_t)(mine) * FBN_RS_I] = -1;
       }
     }
     if (cs.dup) cs.dup[i] = owner;
@@ -1511,14 +1524,15 @@ __global__ void __launch_bounds__(256) adam_window2_kernel(float* __restrict__ p
   int r = 0, key = 0x7fffffff, pe = -1;
   if (lane < FBN_WIN_ROWS && j < nroll) {
     const long long rr = roll0 + j;
+    const int4 rs = row_state(last, rr);
     if (!map || map[rr] == -1) {
-      const int k0 = last[rr];
+      const int k0 = rs.z;
       if (k0 < t) {
         r = (int)rr;
-        if (ps.pend) pe = ps.pend[rr];
+        if (ps.pend) pe = rs.w;
         key = k0 + (pe >= 0 ? 1 : 0);
-        last[rr] = t;
-        if (pe >= 0) ps.pend[rr] = -1;
+        last[(size_t)(rr) * FBN_RS_I] = t;
+        if (pe >= 0) ps.pend[(size_t)(rr) * FBN_RS_I] = -1;
       }
     }
   }
@@ -1549,12 +1563,12 @@ __global__ void __launch_bounds__(256) adam_flush_kernel(float* __restrict__ p, 
   for (long long r0 = gw * RPW; r0 < nrows; r0 += nw * RPW) {
     const long long r = r0 + lane / G;
     if (r >= nrows) continue;
-    const int k0 = last[r];
+    const int k0 = last[(size_t)(r) * FBN_RS_I];
     if (k0 >= t) continue;
     replay_rows<D, DW>(p, m, v, r, q, k0, t, win, w0, table, wd, b2, omb2, eps, ps);
     if (q == 0) {
-      last[r] = t;
-      if (ps.pend) ps.pend[r] = -1;
+      last[(size_t)(r) * FBN_RS_I] = t;
+      if (ps.pend) ps.pend[(size_t)(r) * FBN_RS_I] = -1;
     }
   }
 }
@@ -1596,7 +1610,7 @@ __global__ void __launch_bounds__(256) adam_touched_kernel(float* __restrict__ p
     *reinterpret_cast<f32x4*>(v + off) = vv;
     if (q == 0) {
       map[r] = -1;
-      if (last) last[r] = *step_ptr + 1;
+      if (last) last[(size_t)(r) * FBN_RS_I] = *step_ptr + 1;
     }
   }
 }
@@ -1630,10 +1644,10 @@ __device__ __forceinline__ void adam_commit_body(float* __restrict__ p, float* _
     const bool flag = sr != -1 && (sr & FBN_SLOT_FLAG);
     if (sr != -1 && !flag) {
       if (gs.Lp1 == 1) {   // per-entry rows (N > 1 owner): the entry's own row of the ring slot
-        ps.pend[sr] = (int)e;
+        ps.pend[(size_t)(sr) * FBN_RS_I] = (int)e;
       } else {
         const int b = (int)(e / gs.Lp1), tt = (int)(e - (long long)b * gs.Lp1);
-        ps.pend[sr] = b * 2 + (tt ? 1 : 0);
+        ps.pend[(size_t)(sr) * FBN_RS_I] = b * 2 + (tt ? 1 : 0);
       }
       map[sr] = -1;
       gs.slot_row[e] = -1;
@@ -1667,7 +1681,7 @@ __device__ __forceinline__ void adam_commit_body(float* __restrict__ p, float* _
       *reinterpret_cast<f32x4*>(v + off) = vv;
       if (q == 0) {
         map[r] = -1;
-        last[r] = t + 1;
+        last[(size_t)(r) * FBN_RS_I] = t + 1;
         gs.slot_row[ee] = -1;
       }
     }

@@ -122,20 +122,55 @@ def bf16_weights(p: Dict[str, torch.Tensor], d: int, a: Dict[str, torch.Tensor],
 
 class _SumJob(ctypes.Structure):
     _fields_ = [("part", ctypes.c_void_p), ("out", ctypes.c_void_p), ("nch", ctypes.c_int), ("C", ctypes.c_int),
-                ("scale", ctypes.c_float), ("beta", ctypes.c_float)]
+                ("scale", ctypes.c_float), ("beta", ctypes.c_float), ("ld", ctypes.c_int), ("pad", ctypes.c_int)]
+
+
+class _SlabJob(ctypes.Structure):
+    _fields_ = [("ws", ctypes.c_void_p), ("out", ctypes.c_void_p), ("M", ctypes.c_int), ("N", ctypes.c_int),
+                ("ldc", ctypes.c_int), ("nsplit", ctypes.c_int), ("seg", ctypes.c_int), ("off0", ctypes.c_int),
+                ("off1", ctypes.c_int), ("beta", ctypes.c_float)]
+
+
+# the weight-gradient GEMMs leave their split-K slabs for the step's one fbn_sum_jobs2 launch, and
+# the fields backward its partial rows (FBN_DEFER_REDUCE=0: a reduce launch after each, A/B)
+_DEFER_REDUCE = os.environ.get("FBN_DEFER_REDUCE", "1") != "0"
+_nsplit = ctypes.c_int(0)
+# FBN_GATHER_HOT=<tau> (A/B variant of the gather, N1): rows a batch draws >= tau times staged in
+# LDS per workgroup (fbn_hot_rows + fbn_fields_fwd_hot); 0 = off (default: measured slower)
+_GATHER_HOT = int(os.environ.get("FBN_GATHER_HOT", "0"))
 
 
 class DeferredSums:
-    """Small reductions of one step, finalised together by ONE fbn_sum_jobs launch:
-    out[c] = beta*out[c] + scale * sum_k part[k][c].  Partials must stay alive until flush()."""
+    """Small reductions of one step, finalised together by ONE fbn_sum_jobs2 launch:
+    out[c] = beta*out[c] + scale * sum_k part[k*ld + c], and the weight-gradient GEMMs' split-K
+    slabs (gemm_slabs).  Partials must stay alive until flush()."""
 
     def __init__(self):
         self.jobs = []
+        self.slabs = []
         self.keep = []
 
-    def add(self, part, nch, C, out, scale=1.0, beta=0.0):
-        self.jobs.append((part.data_ptr(), out.data_ptr(), int(nch), int(C), float(scale), float(beta)))
+    def add(self, part, nch, C, out, scale=1.0, beta=0.0, ld=0):
+        self.jobs.append((part.data_ptr(), out.data_ptr(), int(nch), int(C), float(scale), float(beta), int(ld), 0))
         self.keep.append(part)
+
+    def gemm_slabs(self, A, B, out, M, N, K, lda, ldb, ldc, transA, transB, rC=NO_REMAP, beta=0.0, stream=None,
+                   A2=None, lda2=0, kseg=INT_MAX, B2=None, ldb2=0, nseg=INT_MAX) -> bool:
+        """out (+)= op(A) op(B) through fbn_gemm_slabs, its slabs summed at flush(); False (nothing
+        launched) when the shape is outside the slab path's bf16 LDS-DMA conditions."""
+        if not (_DEFER_REDUCE and A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16 and K % 64 == 0
+                and lda % 8 == 0 and ldb % 8 == 0 and (not transA or M % 8 == 0) and (transB or N % 8 == 0)
+                and N % 4 == 0 and ldc % 4 == 0 and all(x % 4 == 0 for x in rC[1:])
+                and (rC[0] == INT_MAX or rC[0] % 4 == 0)):
+            return False
+        nbytes = _lib.lib().fbn_gemm_slabs_size(M, N, K)
+        ws = _ws(nbytes, out.device)
+        call("fbn_gemm_slabs", ptr(A), ptr(B), M, N, K, lda, ldb, int(transA), int(transB), ptr(ws), nbytes,
+             ptr(A2), lda2, kseg, ptr(B2), ldb2, nseg, ctypes.byref(_nsplit),
+             stream if stream is not None else _lib.stream_handle())
+        self.slabs.append((ws.data_ptr(), out.data_ptr(), M, N, ldc, _nsplit.value, rC[0], rC[1], rC[2], float(beta)))
+        self.keep.append(ws)
+        return True
 
     def colsum(self, X, B, C, ldx, out, stream):
         nch = _lib.lib().fbn_row_chunks(B)
@@ -144,11 +179,14 @@ class DeferredSums:
         self.add(part, nch, C, out)
 
     def flush(self, stream):
-        for i in range(0, len(self.jobs), 8):
-            chunk = self.jobs[i:i + 8]
-            arr = (_SumJob * len(chunk))(*[_SumJob(*j) for j in chunk])
-            call("fbn_sum_jobs", ctypes.addressof(arr), len(chunk), stream)
-        self.jobs, self.keep = [], []
+        jobs, slabs = self.jobs, self.slabs
+        while jobs or slabs:
+            jc, sc = jobs[:16], slabs[:8]
+            jobs, slabs = jobs[16:], slabs[8:]
+            arr = (_SumJob * max(1, len(jc)))(*[_SumJob(*j) for j in jc])
+            sarr = (_SlabJob * max(1, len(sc)))(*[_SlabJob(*j) for j in sc])
+            call("fbn_sum_jobs2", ctypes.addressof(arr), len(jc), ctypes.addressof(sarr), len(sc), stream)
+        self.jobs, self.slabs, self.keep = [], [], []
 
 
 def colsum(X, B, C, ldx, out, beta=0.0, stream=None):
@@ -322,14 +360,34 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record()
         probe.setdefault("fields_fwd", []).append(ev)
-    call("fbn_fields_fwd", ptr(item_id), ptr(seq) if Lr else None, ptr(batch["likes_level"]),
-         ptr(batch["views_level"]), ptr(hmm), ptr(p["mm_proj.1.weight"]), ptr(p["mm_proj.1.bias"]), LN_EPS,
-         ptr(p["cate_emb.weight"]), p["cate_emb.weight"].shape[0], ptr(E), V, ptr(pos),
-         ptr(p["senet.excitation.0.weight"]), ptr(p["senet.excitation.0.bias"]),
-         ptr(p["senet.excitation.2.weight"]), ptr(p["senet.excitation.2.bias"]), cfg.R, ptr(X), ptr(Vc), ptr(Vc16),
-         None if split_c else ptr(c), KC,
-         int(bf), ptr(av), ptr(cnt), ptr(err), ptr(sm.get("map")), ptr(sm.get("slot_row")), B, Lr, d,
-         int(table_rows is not None and table_rows.dtype == torch.bfloat16), st)
+    if _GATHER_HOT and table_rows is None and V * d * 4 < 0xFFFFFF00:
+        # A/B variant: the batch's rows drawn >= _GATHER_HOT times are staged in LDS per workgroup
+        hc = a.get("hot_cnt")
+        if hc is None or hc.numel() != V:
+            hc = a["hot_cnt"] = torch.zeros(V, dtype=torch.int32, device=dev)
+            a["hot_list"] = torch.zeros(256, dtype=torch.int32, device=dev)
+            a["hot_n"] = torch.zeros(1, dtype=torch.int32, device=dev)
+        H = 8192 // d
+        call("fbn_hot_rows", ptr(item_id), ptr(seq) if Lr else None, B, Lr, V, ptr(hc), ptr(a["hot_list"]),
+             ptr(a["hot_n"]), H, _GATHER_HOT, 0, st)
+        call("fbn_fields_fwd_hot", ptr(item_id), ptr(seq) if Lr else None, ptr(batch["likes_level"]),
+             ptr(batch["views_level"]), ptr(hmm), ptr(p["mm_proj.1.weight"]), ptr(p["mm_proj.1.bias"]), LN_EPS,
+             ptr(p["cate_emb.weight"]), p["cate_emb.weight"].shape[0], ptr(E), V,
+             ptr(p["senet.excitation.0.weight"]), ptr(p["senet.excitation.0.bias"]),
+             ptr(p["senet.excitation.2.weight"]), ptr(p["senet.excitation.2.bias"]), cfg.R, ptr(X), ptr(Vc),
+             ptr(Vc16), None if split_c else ptr(c), KC, int(bf), ptr(av), ptr(cnt), ptr(err), ptr(sm.get("map")),
+             ptr(sm.get("slot_row")), B, Lr, d, ptr(a["hot_list"]), ptr(a["hot_n"]), H, st)
+        call("fbn_hot_rows", ptr(item_id), ptr(seq) if Lr else None, B, Lr, V, ptr(hc), None, ptr(a["hot_n"]), H,
+             _GATHER_HOT, 1, st)
+    else:
+        call("fbn_fields_fwd", ptr(item_id), ptr(seq) if Lr else None, ptr(batch["likes_level"]),
+             ptr(batch["views_level"]), ptr(hmm), ptr(p["mm_proj.1.weight"]), ptr(p["mm_proj.1.bias"]), LN_EPS,
+             ptr(p["cate_emb.weight"]), p["cate_emb.weight"].shape[0], ptr(E), V, ptr(pos),
+             ptr(p["senet.excitation.0.weight"]), ptr(p["senet.excitation.0.bias"]),
+             ptr(p["senet.excitation.2.weight"]), ptr(p["senet.excitation.2.bias"]), cfg.R, ptr(X), ptr(Vc),
+             ptr(Vc16), None if split_c else ptr(c), KC,
+             int(bf), ptr(av), ptr(cnt), ptr(err), ptr(sm.get("map")), ptr(sm.get("slot_row")), B, Lr, d,
+             int(table_rows is not None and table_rows.dtype == torch.bfloat16), st)
     if ev is not None:
         ev[1].record()
     if after_gather is not None:
@@ -509,7 +567,10 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     part1 = None
     lean_h1 = a.get("lean_h1", False)
     if bf:
-        wg.run(lambda s: gemm(dh2pre16, a["h1_16"], g["mlp.4.weight"], H2, H1, B, H2, H1, H1, True, False, stream=s))
+        if not sums.gemm_slabs(dh2pre16, a["h1_16"], g["mlp.4.weight"], H2, H1, B, H2, H1, H1, True, False,
+                               stream=st):
+            wg.run(lambda s: gemm(dh2pre16, a["h1_16"], g["mlp.4.weight"], H2, H1, B, H2, H1, H1, True, False,
+                                  stream=s))
         if (_BN1_BWD_IN_GEMM and lean_h1 and coll.world <= 1
                 and _lib.lib().fbn_gemm_bn_bwd_part_supported(B, H1, H2, H2, H2, 0, 1)):
             # dh1 = dh2 Wb and, from its accumulators, the BN1 backward's column partials (no pass
@@ -530,8 +591,10 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
                 part_pre=part1)
     # weight gradient of the MLP input layer (side work), then its dgrad dc
     if a.get("split_c"):
-        wg.run(lambda s: gemm_split(dh1pre16, a["Vc16"], g["mlp.0.weight"], H1, KC, B, H1, 5 * d, 21 * d, True,
-                                    False, rC=wa_remap(d), stream=s, B2=a["c"][:, 5 * d:], ldb2=KC, nseg=5 * d))
+        if not sums.gemm_slabs(dh1pre16, a["Vc16"], g["mlp.0.weight"], H1, KC, B, H1, 5 * d, 21 * d, True, False,
+                               rC=wa_remap(d), stream=st, B2=a["c"][:, 5 * d:], ldb2=KC, nseg=5 * d):
+            wg.run(lambda s: gemm_split(dh1pre16, a["Vc16"], g["mlp.0.weight"], H1, KC, B, H1, 5 * d, 21 * d, True,
+                                        False, rC=wa_remap(d), stream=s, B2=a["c"][:, 5 * d:], ldb2=KC, nseg=5 * d))
     elif bf:
         wg.run(lambda s: gemm(dh1pre16, a["c"], g["mlp.0.weight"], H1, KC, B, H1, KC, 21 * d, True, False,
                               rC=wa_remap(d), stream=s))
@@ -556,7 +619,8 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
         # one launch: dU and dV = dc_V + pair terms + dU W^T (U recomputed on the MFMA)
         call("fbn_bilinear_bwd", ptr(dc), KC, int(dc.dtype == torch.bfloat16), ptr(a["Vc16"]), ptr(w16["WT"]),
              ptr(w16["W"]), ptr(dV), ptr(dU16), B, d, st)
-        wg.run(lambda s: gemm(a["Vc16"], dU16, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=s))
+        if not sums.gemm_slabs(a["Vc16"], dU16, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=st):
+            wg.run(lambda s: gemm(a["Vc16"], dU16, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=s))
     else:
         dU = torch.empty((B, 5, d), **f32)
         call("fbn_pairs_bwd", ptr(dc), None if v16 else ptr(a["Vc"]), ptr(a["Vc16"]) if v16 else None, ptr(a["U"]),
@@ -590,8 +654,15 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     V = p["item_emb.weight"].shape[0] if pos is None else 0
     keys = ("senet.excitation.0.weight", "senet.excitation.0.bias", "senet.excitation.2.weight",
             "senet.excitation.2.bias", "mm_proj.1.weight", "mm_proj.1.bias", "cate_emb.weight", "mm_proj.0.bias")
-    outs_arr = (ctypes.c_void_p * 8)(*[g[k].data_ptr() for k in keys])   # host array of device pointers
-    outs = ctypes.cast(outs_arr, ctypes.c_void_p).value
+    if _DEFER_REDUCE:
+        outs = None       # the partial rows' segments are summed in the step's sum_jobs launch
+        o = 0
+        for k, n in zip(keys, (6 * R, R, 6 * R, 6, d, d, ncate * d, d)):
+            sums.add(partials[:, o:], nblk, n, g[k], ld=P)
+            o += n
+    else:
+        outs_arr = (ctypes.c_void_p * 8)(*[g[k].data_ptr() for k in keys])   # host array of device pointers
+        outs = ctypes.cast(outs_arr, ctypes.c_void_p).value
     evb = None
     if probe is not None:                       # bench / tools: events around the fields backward
         evb = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -608,7 +679,10 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     if hooks and "after_fields_bwd" in hooks:     # N > 1: the gradient rows are complete -> exchange
         hooks["after_fields_bwd"]()
     if bf:
-        wg.run(lambda s: gemm(dhmm16, w16["x"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True, False, stream=s))
+        if not sums.gemm_slabs(dhmm16, w16["x"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True, False,
+                               stream=st):
+            wg.run(lambda s: gemm(dhmm16, w16["x"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True, False,
+                                  stream=s))
     else:
         wg.run(lambda s: gemm(dhmm, batch["item_emb_d128"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True,
                               False, stream=s))

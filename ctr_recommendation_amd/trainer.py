@@ -284,7 +284,11 @@ class FiBiNETTrainer:
         self.prefetch_owner = bool(prefetch_rows) and sharded and self.d in (128, 256)
         # the prefetch also decides the next batch's row claims (tagged, no CAS at claim time);
         # they are used only by a step given the very id tensors they were made for
-        self.preclaim = torch.zeros(self.V, dtype=torch.int64, device=dev) if self.prefetch_rows else None
+        # per-row table-Adam state: ONE 16-B record per row {i64 pre-claim tag, i32 last, i32 pend}
+        # (include/fibinet.h FBN_ROW_STATE_BYTES); .preclaim / .last / .pend are strided views of it
+        self.row_state = torch.zeros((max(1, self.rows_local), 4), **i32)
+        self.row_state[:, 3] = -1
+        self.preclaim = self.row_state.view(torch.int64)[:, 0] if self.prefetch_rows else None
         self._pre_key = None
         self.hasdup = torch.zeros((self.n_entries,), **i32) if self.deterministic else None
         self.fx = torch.zeros((self.n_entries, d), dtype=torch.int64, device=dev) if self.deterministic else None
@@ -331,7 +335,7 @@ class FiBiNETTrainer:
         if self.table_adam not in ("lazy", "eager", "sparse"):
             raise ValueError(f"table_adam must be 'lazy', 'eager' or 'sparse', not {self.table_adam!r}")
         self.lazy_window = int(lazy_window)
-        self.last = torch.zeros(max(1, self.rows_local), **i32)     # Adam steps applied per table row
+        self.last = self.row_state[:, 2]     # Adam steps applied per table row
         # lazy: deferred table gradients (the step tail's commit) -- pend[r] = the gradient row r
         # received at step last[r], applied at the row's next replay; the last F+1 steps' gradients
         # stay in a ring: single GPU, the per-sample vectors [B][2][d]; N > 1, the owner's received
@@ -341,7 +345,7 @@ class FiBiNETTrainer:
         self.ring_n = self.lazy_window + 1
         self.ring_cap = self.B * (max_len + 1) if sharded else 0
         if self.deferred:
-            self.pend = torch.full((max(1, self.rows_local),), -1, **i32)
+            self.pend = self.row_state[:, 3]
             shape = (self.ring_n, self.B, 2, d) if not sharded else (self.ring_n, self.ring_cap, d)
             self.ring = torch.zeros(shape, dtype=torch.float32, device=dev)
             self.coef_hist = torch.ones(total_steps + 1, dtype=torch.float32, device=dev)

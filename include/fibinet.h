@@ -57,6 +57,15 @@ int fbn_gemm(const void* A, const void* B, float* C, const float* bias, int M, i
  * (A(m,k), k >= kseg, at A2[m*lda2 + k - kseg]); B2/nseg -- a k-major B is [B | B2] along N
  * (B(k,n), n >= nseg, at B2[k*ldb2 + n - nseg]); segments multiples of 128.  The MLP input
  * [V_1..V_5 | pairs] is read from the bf16 fields (Vc16) and the pair block of c without a copy. */
+/* Slab mode (bf16 LDS-DMA path): op(A) op(B) whose split-K partial products stay in ws as
+ * *nsplit slabs [nsplit][M][N] f32 (ws >= fbn_gemm_slabs_size(M, N, K) bytes) -- no reduce launch;
+ * the caller sums them with fbn_sum_jobs2 beside the step's other deferred reductions (the
+ * trainer's weight-gradient GEMMs, autograd of src/model_fibinet.py:72,105,126,130).  No bias,
+ * beta, remap or statistics; A2/kseg, B2/nseg as fbn_gemm_split. */
+size_t fbn_gemm_slabs_size(int M, int N, int K);
+int fbn_gemm_slabs(const void* A, const void* B, int M, int N, int K, int lda, int ldb, int transA, int transB,
+                   float* ws, size_t ws_bytes, const void* A2, int lda2, int kseg, const void* B2, int ldb2, int nseg,
+                   int* nsplit, void* stream);
 /* bf16 operands (as fbn_gemm with bf16 = a16 = b16 = 1), C stored in bf16 (C[m * ldc + n], rounded
  * once from the f32 accumulators); no bias, beta, remap or statistics.  The bf16-mode dgrad
  * dc = dh1 Wa of the MLP input (src/model_fibinet.py:126-130 autograd), read only by
@@ -92,6 +101,20 @@ int fbn_fields_fwd(const int64_t* item_id, const int64_t* item_seq, const int64_
                    const float* b2, int R, float* X, float* Vc, short* Vc16, void* c, int ldc, int c_bf16, float* a_out,
                    float* cnt_out,
                    int* err, int* map, int* slot_row, int B, int L, int D, int rows_bf16, void* stream);
+/* Hot-row LDS staging (A/B variant of the gather; single GPU, f32 table under 4 GB).
+ * fbn_hot_rows(clear = 0): each batch entry counts its row in cnt [V] (int32, zero on entry) and
+ * the entry that brings a row's count to tau appends it to hot [H] (hot_n: count, may exceed H);
+ * clear = 1 zeroes those counts and hot_n again.  fbn_fields_fwd_hot = fbn_fields_fwd (pos = NULL,
+ * f32 rows) whose workgroups first stage min(hot_n, H, 8192/D) listed rows in LDS and read those
+ * from there. */
+int fbn_hot_rows(const int64_t* item, const int64_t* seq, int B, int L, long long V, int* cnt, int* hot, int* hot_n,
+                 int H, int tau, int clear, void* stream);
+int fbn_fields_fwd_hot(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes, const int64_t* views,
+                       const float* hmm, const float* ln_g, const float* ln_b, float ln_eps, const float* cate,
+                       int n_cate, const float* table, long long V, const float* w1, const float* b1, const float* w2,
+                       const float* b2, int R, float* X, float* Vc, short* Vc16, void* c, int ldc, int c_bf16,
+                       float* a_out, float* cnt_out, int* err, int* map, int* slot_row, int B, int L, int D,
+                       const int* hot, const int* hot_n, int H, void* stream);
 
 /* ---------------------------------------------------------------- K2 + K4 backward
  * Replaces the autograd of the lines above, including embedding_dense_backward with
@@ -101,7 +124,8 @@ int fbn_fields_fwd(const int64_t* item_id, const int64_t* item_seq, const int64_
  * entry into sendbuf at pos (multi-GPU).
  * param_grads: host array of 8 device pointers that receive the gradients of {senet W1, b1,
  * W2, b2, LN gamma, beta, cate table, mm_proj bias (may be NULL)}; partials: [fbn_fields_bwd_grid(B,D)][P] scratch with
- * P = fbn_fields_bwd_partials_size. */
+ * P = fbn_fields_bwd_partials_size.  param_grads == NULL: no reduction launch -- the caller sums
+ * the partial rows' segments (6R, R, 6R, 6, D, D, n_cate*D, D columns) with fbn_sum_jobs2 (ld = P). */
 int fbn_fields_bwd_partials_size(int D, int R, int n_cate);
 int fbn_fields_bwd_grid(int B, int D);
 /* Vc16 / dhmm16 / dU16 (optional, may be NULL): bf16 copies written beside the fp32 outputs,
@@ -195,12 +219,17 @@ size_t fbn_colsum_workspace_size(int B, int C);
 int fbn_colsum(const float* X, int B, int C, int ldx, float* out, float beta, void* ws, void* stream);
 /* column partials only: part[fbn_row_chunks(B)][C] (finalised by fbn_sum_jobs) */
 int fbn_colsum_partial(const float* X, int B, int C, int ldx, float* part, void* stream);
-/* Deferred sums of one step in ONE launch: jobs = host array of n <= 8 records
- * {const float* part; float* out; int nch, C; float scale, beta;}:
- * out[c] = beta * out[c] + scale * sum_{k < nch} part[k * C + c]   (fixed-order tree).
- * Used for the bias gradients (sum over the batch, autograd of src/model_fibinet.py:105,126,130,134)
- * and the mean BCE loss (src/train_fibinet.py:115). */
+/* Deferred sums of one step in ONE launch: jobs = host array of n <= 16 records
+ * {const float* part; float* out; int nch, C; float scale, beta; int ld, pad;}:
+ * out[c] = beta * out[c] + scale * sum_{k < nch} part[k * ld + c]   (ld 0 = C; fixed-order tree).
+ * Used for the bias gradients (sum over the batch, autograd of src/model_fibinet.py:105,126,130,134),
+ * the fields' small parameter gradients and the mean BCE loss (src/train_fibinet.py:115).
+ * fbn_sum_jobs2 adds, in the same launch, ns <= 8 slab jobs {const float* ws; float* out; int M, N,
+ * ldc, nsplit, seg, off0, off1; float beta;}: out[m*ldc + n + (n < seg ? off0 : off1)] =
+ * beta*out + sum_{z < nsplit} ws[z][m][n] -- the split-K slabs fbn_gemm_slabs left (N, ldc and the
+ * remap multiples of 4, buffers 16-B aligned). */
 int fbn_sum_jobs(const void* jobs, int n, void* stream);
+int fbn_sum_jobs2(const void* jobs, int n, const void* slabs, int ns, void* stream);
 
 /* ---------------------------------------------------------------- K7 head: Linear(256,1)+sigmoid+BCE
  * Replaces src/model_fibinet.py:134,136,199 and nn.BCELoss fwd/bwd (src/train_fibinet.py:79,115). */
@@ -260,6 +289,11 @@ int fbn_adam_table(float* p, float* m, float* v, long long nrows, int D, int* ma
 int fbn_adam_touched(float* p, float* m, float* v, int D, int* map, const float* gvec, float* extra, int* slot_row,
                      int Lp1, int n, const float* coef, const void* consts_table, const int* step, float wd,
                      float beta2, float eps, int* last, void* stream);
+/* Row-state record.  Every `last`, `pend` and `preclaim` argument below is a FIELD of one 16-B
+ * record per table row, {uint64 preclaim; int32 last; int32 pend} (FBN_ROW_STATE_BYTES): pass the
+ * record array's base as preclaim, base + 8 B as last, base + 12 B as pend; the kernels index each
+ * field with the 16-B record stride, so a claim reads a row's whole state in one sector. */
+#define FBN_ROW_STATE_BYTES 16
 /* Lazy table Adam (bit-identical to the eager table pass): last[r] = Adam steps applied to row r.  fbn_adam_catchup replays the
  * zero-loss-gradient steps (coupled L2 decay only: g = 0*coef + wd*p) of the rows claimed in
  * slot_row and of rolling window (step mod F) (ceil(nrows/F) rows) up to *step, with the same

@@ -82,6 +82,38 @@ def test_gemm_bf16_all_layouts(hip_device, transA, transB, M, N, K):
     assert err < 2e-5 * K ** 0.5 * 4, err
 
 
+@pytest.mark.parametrize("M,N,K,remap", [(256, 512, 8192, False), (512, 1920, 8192, True), (128, 128, 40960, False),
+                                          (16, 16, 20480, False), (128, 128, 8192, False)])
+def test_gemm_slabs_deferred_sum(hip_device, M, N, K, remap):
+    """The weight-gradient GEMMs' slab mode (fbn_gemm_slabs: split-K slabs left in ws) summed by
+    the step's fbn_sum_jobs2 launch beside ordinary column-sum jobs (one with a row stride ld):
+    C == torch's op(A) op(B) of the same bf16 operands, written through the mlp.0.weight remap."""
+    g = torch.Generator(device="cpu").manual_seed(5)
+    A = torch.randn((K, M), generator=g).to(hip_device).bfloat16()      # k-major A (the wgrads' dY)
+    Bm = torch.randn((K, N), generator=g).to(hip_device).bfloat16()     # k-major B (activations)
+    rc = ops.wa_remap(128) if remap else ops.NO_REMAP
+    ldc = 21 * 128 if remap else N
+    C = torch.full((M, ldc), float("nan"), device=hip_device)
+    part = torch.randn((300, 40), generator=g).to(hip_device)
+    out1 = torch.empty(24, device=hip_device)
+    out2 = torch.empty(16, device=hip_device)
+    sums = ops.DeferredSums()
+    assert sums.gemm_slabs(A, Bm, C, M, N, K, M, N, ldc, True, False, rC=rc)
+    sums.add(part, 300, 24, out1, ld=40)
+    sums.add(part[:, 24:], 300, 16, out2, scale=0.5, ld=40)
+    sums.flush(ops._lib.stream_handle(hip_device))
+    torch.cuda.synchronize()
+    ref = A.double().T @ Bm.double()
+    cols = torch.arange(N, device=hip_device)
+    if remap:
+        cols = cols + torch.where(cols < rc[0], rc[1], rc[2])
+    err = (C[:, cols].double() - ref).abs().max().item()
+    assert err < 2e-5 * K ** 0.5 * 4, err
+    pd = part.double().sum(0)
+    assert torch.allclose(out1.double(), pd[:24], rtol=1e-5, atol=1e-4)
+    assert torch.allclose(out2.double(), 0.5 * pd[24:], rtol=1e-5, atol=1e-4)
+
+
 @pytest.mark.gpu
 def test_table_adam_step_vs_ieee(hip_device):
     """The table-row Adam step (v_sqrt_f32 / v_rcp_f32, fused moment updates) that every

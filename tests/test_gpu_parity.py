@@ -183,3 +183,22 @@ def test_hip_matches_committed_golden_vectors(hip_device, d):
         n = key[9:]
         ref = torch.from_numpy(z[key])
         _grad_close(g[n][:ref.shape[0]].cpu(), ref, n)
+
+
+@pytest.mark.parametrize("d,zipf,tau", [(128, 1.05, 2), (16, 1.2, 3), (128, 0.0, 2)])
+def test_hot_row_staging_is_bit_identical(hip_device, d, zipf, tau, monkeypatch):
+    """The gather's hot-row LDS staging (FBN_GATHER_HOT, the north star's 'LDS staging of hot
+    rows' measured as an A/B variant): a staged row read from LDS is the same f32 row, summed in
+    the same slot order, so the forward is bit-identical to the plain gather -- under Zipf ids
+    (many staged rows), a steeper skew at d = 16, and uniform ids (few or none)."""
+    from ctr_recommendation_amd.data import make_device_batches
+    V, B = 20000, 2048
+    torch.manual_seed(0)
+    hip = build_model(None, {"embedding_dim": d, "vocab_size": V}).to(hip_device).eval()
+    (batch, _), = make_device_batches(1, B, V, 20, hip_device, seed=9, zipf=zipf)
+    with torch.no_grad():
+        p0 = hip(batch)
+        monkeypatch.setattr(ops, "_GATHER_HOT", tau)
+        p1 = hip(batch)
+        p2 = hip(batch)          # counts and the list were cleared after the first staged pass
+    assert torch.equal(p0, p1) and torch.equal(p0, p2)

@@ -363,9 +363,15 @@ static void modes(const Shape& sh, const short* A, const short* B, float* C, con
   run<BM, BN, S, WGM, WGN, 2>(sh, A, B, C, nullptr);
 }
 
-int main() {
-  const Shape shapes[] = {{"F3", 8192, 512, 1920}, {"dc", 8192, 1920, 512}};
-  for (const Shape& sh : shapes) {
+int main(int argc, char** argv) {
+  // "wide": 128x256 / 256x128 tiles; F3h = one K-half of F3 on twice the rows, i.e. the per-workgroup
+  // work of F3 split-K 2 on 256 workgroups (its split fix-up is not in the time)
+  const bool wide = argc > 1 && !strcmp(argv[1], "wide");
+  const Shape shapes_all[] = {{"F3", 8192, 512, 1920}, {"dc", 8192, 1920, 512}};
+  const Shape shapes_wide[] = {{"F3", 8192, 512, 1920}, {"F3h", 16384, 512, 960}};
+  const Shape* shapes = wide ? shapes_wide : shapes_all;
+  for (int si = 0; si < 2; ++si) {
+    const Shape& sh = shapes[si];
     const size_t na = (size_t)sh.M * sh.K, nbb = (size_t)sh.N * sh.K;
     std::vector<unsigned short> ha(na), hb(nbb);
     std::vector<float> fa(na), fb(nbb);
@@ -387,6 +393,18 @@ int main() {
     CK(hipMalloc(&C, (size_t)sh.M * sh.N * 4));
     CK(hipMemcpy(A, ha.data(), na * 2, hipMemcpyHostToDevice));
     CK(hipMemcpy(B, hb.data(), nbb * 2, hipMemcpyHostToDevice));
+    if (wide) {
+      modes<64, 128, 2, 2, 4>(sh, A, B, C, &ref);
+      modes<128, 256, 2, 2, 4>(sh, A, B, C, &ref);
+      modes<128, 256, 3, 2, 4>(sh, A, B, C, &ref);
+      modes<128, 256, 2, 4, 4>(sh, A, B, C, &ref);
+      modes<256, 128, 2, 4, 2>(sh, A, B, C, &ref);
+      modes<256, 128, 2, 4, 4>(sh, A, B, C, &ref);
+      CK(hipFree(A));
+      CK(hipFree(B));
+      CK(hipFree(C));
+      continue;
+    }
     modes2<128, 128, 3, 2, 2>(sh, A, B, C, &ref);
     modes2<128, 128, 4, 2, 2>(sh, A, B, C, &ref);
     modes2<128, 128, 3, 2, 4>(sh, A, B, C, &ref);
