@@ -143,15 +143,28 @@ __device__ __forceinline__ void adam_dense_body(float* __restrict__ p, const flo
                                                 const AdamConsts& k, float wd, float b2, float omb2, float eps,
                                                 long long bid, long long nblk) {
   const long long n4 = n / 4;
-  for (long long i = bid * blockDim.x + threadIdx.x; i < n4; i += nblk * blockDim.x) {
-    f32x4 pp = *reinterpret_cast<f32x4*>(p + 4 * i);
-    f32x4 mm = *reinterpret_cast<f32x4*>(m + 4 * i);
-    f32x4 vv = *reinterpret_cast<f32x4*>(v + 4 * i);
-    const f32x4 gg = *reinterpret_cast<const f32x4*>(g + 4 * i);
-    adam_tab4<true>(pp, mm, vv, gg * coef, wd, b2, omb2, eps, k);
-    *reinterpret_cast<f32x4*>(p + 4 * i) = pp;
-    *reinterpret_cast<f32x4*>(m + 4 * i) = mm;
-    *reinterpret_cast<f32x4*>(v + 4 * i) = vv;
+  const long long st = nblk * blockDim.x;
+  // four vectors per thread per round, every load of the round in flight before the first
+  // update (the pass is latency-bound otherwise: a few blocks per CU, one round trip per vector)
+  for (long long i0 = bid * blockDim.x + threadIdx.x; i0 < n4; i0 += 4 * st) {
+    f32x4 pp[4], mm[4], vv[4], gg[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long long i = i0 + u * st < n4 ? i0 + u * st : i0;
+      pp[u] = *reinterpret_cast<f32x4*>(p + 4 * i);
+      mm[u] = *reinterpret_cast<f32x4*>(m + 4 * i);
+      vv[u] = *reinterpret_cast<f32x4*>(v + 4 * i);
+      gg[u] = *reinterpret_cast<const f32x4*>(g + 4 * i);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long long i = i0 + u * st;
+      if (i >= n4) break;
+      adam_tab4<true>(pp[u], mm[u], vv[u], gg[u] * coef, wd, b2, omb2, eps, k);
+      *reinterpret_cast<f32x4*>(p + 4 * i) = pp[u];
+      *reinterpret_cast<f32x4*>(m + 4 * i) = mm[u];
+      *reinterpret_cast<f32x4*>(v + 4 * i) = vv[u];
+    }
   }
   for (long long i = n4 * 4 + bid * blockDim.x + threadIdx.x; i < n; i += nblk * blockDim.x) {
     float mm = m[i], vv = v[i];
@@ -1249,44 +1262,33 @@ __device__ __forceinline__ void replay4_sorted(int r, int key, int pe, int cnt, 
       get(j0 + 4 + x, nr[x], nk[x], np[x]);
       load(nxt[x], nr[x], nk[x], np[x]);   // past the last group: row 0, discarded
     }
+    // A row spans the whole wave, so its step -- and the step's schedule constants -- are
+    // wave-uniform: scalar loads from the table (no LDS staging, no vector registers for them).
     // deferred-gradient steps (step ck - 1 with its stored vector and clip coefficient)
 #pragma unroll
     for (int x = 0; x < 4; ++x)
-      if (cp[x] >= 0) {
-        const int s = ck[x] - 1;
-        adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, cur[x].g * cur[x].c, wd, b2, omb2, eps,
-                         s >= w0 ? win[s - w0] : consts4(table[s]));
+      if (cp[x] >= 0) adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, cur[x].g * cur[x].c, wd, b2, omb2, eps,
+                                       consts4(table[ck[x] - 1]));
+    // END-aligned: every row replays up to T, so from the group's latest start on, all four rows
+    // are at the SAME step and share one set of constants; before it, the earlier-starting rows
+    // catch up to that start one by one (short after the sort)
+    int smax = ck[0];
+#pragma unroll
+    for (int x = 1; x < 4; ++x)
+      if (j0 + x < cnt) smax = max(smax, ck[x]);
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+      if (j0 + x < cnt)
+        for (int s = ck[x]; s < smax; ++s)
+          adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, zero, wd, b2, omb2, eps, consts4(table[s]));
+    if (smax < T) {
+      f32x4 kc = consts4(table[smax]);
+      for (int s = smax; s < T; ++s) {
+        const f32x4 kn = consts4(table[s + 1]);   // a step ahead (table row T exists)
+#pragma unroll
+        for (int x = 0; x < 4; ++x) adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, zero, wd, b2, omb2, eps, kc);
+        kc = kn;
       }
-    // steps older than the LDS window (a row lagging more than FBN_PF_WIN steps): global table
-    int s0[4];
-#pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      s0[x] = ck[x];
-      for (; s0[x] < w0; ++s0[x])
-        adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, zero, wd, b2, omb2, eps, consts4(table[s0[x]]));
-    }
-    // all four rows side by side for the steps they all still need, constants read a step ahead
-    const int n0 = T - s0[0], n1 = T - s0[1], n2 = T - s0[2], n3 = T - s0[3];
-    const int common = min(min(n0, n1), min(n2, n3));
-    const int most = max(max(n0, n1), max(n2, n3));
-    f32x4 kc[4];
-#pragma unroll
-    for (int x = 0; x < 4; ++x) kc[x] = win[s0[x] - w0];
-    for (int it = 0; it < common; ++it) {
-      f32x4 kn[4];
-#pragma unroll
-      for (int x = 0; x < 4; ++x) kn[x] = win[s0[x] - w0 + it + 1];   // <= T - w0: in the window
-#pragma unroll
-      for (int x = 0; x < 4; ++x) adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, zero, wd, b2, omb2, eps, kc[x]);
-#pragma unroll
-      for (int x = 0; x < 4; ++x) kc[x] = kn[x];
-    }
-    // the longer rows' remaining steps (short after the sort)
-    for (int it = common; it < most; ++it) {
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-        if (it < T - s0[x])
-          adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, zero, wd, b2, omb2, eps, win[s0[x] - w0 + it]);
     }
 #pragma unroll
     for (int x = 0; x < 4; ++x)
@@ -1399,13 +1401,16 @@ __global__ void __launch_bounds__(256) adam_prefetch2_kernel(float* __restrict__
                                                              int* __restrict__ last,
                                                              const AdamConsts* __restrict__ table,
                                                              const int* __restrict__ step, float wd, float b2,
-                                                             float omb2, float eps, PendSrc ps) {
+                                                             float omb2, float eps, PendSrc ps, int epw) {
   __shared__ f32x4 win[FBN_PF_WIN + 1];   // constants of steps [w0, T]
   const int T = *step + 1;
   const int w0 = T > FBN_PF_WIN ? T - FBN_PF_WIN : 0;
-  for (int s = threadIdx.x; s <= T - w0; s += blockDim.x) win[s] = consts4(table[w0 + s]);
+  if constexpr (D < 128)   // the narrow engine's LDS constants (wave-wide rows read the table directly)
+    for (int s = threadIdx.x; s <= T - w0; s += blockDim.x) win[s] = consts4(table[w0 + s]);
   const int lane = threadIdx.x & 63;
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  // epw entries per wave (lanes past epw hold none): fewer rows per wave, more waves per SIMD
+  // replaying side by side -- the engine's row loads are latency-bound, not its arithmetic
+  const long long i = lane < epw ? (((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * epw + lane : n;
   int r = 0, key = 0x7fffffff, pe = -1;
   if (i < n) {
     const long long b = i / (cs.L + 1), tt = i - b * (cs.L + 1);
@@ -1425,7 +1430,7 @@ __global__ void __launch_bounds__(256) adam_prefetch2_kernel(float* __restrict__
       }
     }
   }
-  __syncthreads();   // the LDS window (no barrier after this point)
+  if constexpr (D < 128) __syncthreads();   // the LDS window (no barrier after this point)
   const int cnt = __popcll(__ballot(key != 0x7fffffff));
   if (cnt == 0) return;
   replay_sorted<D, DW>(r, key, pe, cnt, T, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
@@ -1492,16 +1497,18 @@ __global__ void __launch_bounds__(256) adam_claim2_kernel(float* __restrict__ p,
     if (cs.hasdup && owner >= 0) cs.hasdup[owner] = 1;
   }
   // stage the constants only where some wave of the block has rows to replay (block-uniform)
-  const int any = __syncthreads_or(key != 0x7fffffff);
-  if (!any) return;
-  for (int s = threadIdx.x; s <= t - w0; s += blockDim.x) win[s] = consts4(table[w0 + s]);
-  __syncthreads();
+  if constexpr (D < 128) {
+    const int any = __syncthreads_or(key != 0x7fffffff);
+    if (!any) return;
+    for (int s = threadIdx.x; s <= t - w0; s += blockDim.x) win[s] = consts4(table[w0 + s]);
+    __syncthreads();
+  }
   const int cnt = __popcll(__ballot(key != 0x7fffffff));
   if (cnt == 0) return;
   replay_sorted<D, DW>(r, key, pe, cnt, t, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
 }
 
-// The rolling window (step mod F) with the replay engine (D >= 128): FBN_WIN_ROWS rows per wave
+// The rolling window (step mod F) with the replay engine: rpw rows per wave
 // (one per lane), so a window of ~1e5 rows (C5's 12.5 M-row shard: 97.7 K rows replaying up to F
 // steps each) spreads over thousands of waves instead of one wave per SIMD; claimed rows are left
 // to their claiming entry, as in adam_catchup_kernel.
@@ -1512,17 +1519,18 @@ __global__ void __launch_bounds__(256) adam_window2_kernel(float* __restrict__ p
                                                            long long nrows, int F, long long chunk,
                                                            int* __restrict__ last, const AdamConsts* __restrict__ table,
                                                            const int* __restrict__ step, float wd, float b2,
-                                                           float omb2, float eps, PendSrc ps) {
+                                                           float omb2, float eps, PendSrc ps, int rpw) {
   __shared__ f32x4 win[FBN_PF_WIN + 1];   // constants of steps [w0, t]
   const int t = *step;
   const int w0 = t > FBN_PF_WIN ? t - FBN_PF_WIN : 0;
-  for (int s = threadIdx.x; s <= t - w0; s += blockDim.x) win[s] = consts4(table[w0 + s]);
+  if constexpr (D < 128)
+    for (int s = threadIdx.x; s <= t - w0; s += blockDim.x) win[s] = consts4(table[w0 + s]);
   const long long roll0 = (long long)(t % F) * chunk;
   const long long nroll = roll0 < nrows ? min(chunk, nrows - roll0) : 0;
   const int lane = threadIdx.x & 63;
-  const long long j = ((((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * FBN_WIN_ROWS) + lane;
+  const long long j = ((((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * rpw) + lane;
   int r = 0, key = 0x7fffffff, pe = -1;
-  if (lane < FBN_WIN_ROWS && j < nroll) {
+  if (lane < rpw && j < nroll) {
     const long long rr = roll0 + j;
     const int4 rs = row_state(last, rr);
     if (!map || map[rr] == -1) {
@@ -1536,7 +1544,7 @@ __global__ void __launch_bounds__(256) adam_window2_kernel(float* __restrict__ p
       }
     }
   }
-  __syncthreads();   // the LDS window (no barrier after this point)
+  if constexpr (D < 128) __syncthreads();   // the LDS window (no barrier after this point)
   const int cnt = __popcll(__ballot(key != 0x7fffffff));
   if (cnt == 0) return;
   replay_sorted<D, DW>(r, key, pe, cnt, t, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
@@ -1631,9 +1639,16 @@ __device__ __forceinline__ void adam_commit_body(float* __restrict__ p, float* _
   // straight into the ring slot -- nothing to copy)
   if (gs.Lp1 > 1) {
     float* dst = const_cast<float*>(ps.ring) + (size_t)(t % ps.ring_n) * ps.ring_stride;
-    const long long n4 = (long long)B * 2 * D / 4;
-    for (long long i = bid * blockDim.x + threadIdx.x; i < n4; i += nblk * blockDim.x)
-      reinterpret_cast<f32x4*>(dst)[i] = reinterpret_cast<const f32x4*>(gs.vec)[i];
+    const long long n4 = (long long)B * 2 * D / 4, st = nblk * blockDim.x;
+    for (long long i0 = bid * blockDim.x + threadIdx.x; i0 < n4; i0 += 8 * st) {   // 8 loads in flight
+      f32x4 x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        x[u] = reinterpret_cast<const f32x4*>(gs.vec)[i0 + u * st < n4 ? i0 + u * st : i0];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (i0 + u * st < n4) reinterpret_cast<f32x4*>(dst)[i0 + u * st] = x[u];
+    }
   }
   // one entry per lane: an unflagged claimer records its vector in pend; flagged claimers (rare)
   // are updated by the wave's G-lane groups afterwards
@@ -1712,13 +1727,14 @@ __global__ void __launch_bounds__(256) adam_commit_kernel(float* __restrict__ p,
 // blocks [0, ndense) run the dense Adam (clip coefficient from the norm slots, as adam_dense),
 // the rest the deferred-gradient commit; the last block to finish (ticket counter) advances the
 // step, the dropout offset and num_batches_tracked and clears the norm slots (fbn_step_end).
+#define FBN_TICKET_GROUPS 16   // fbn_adam_step_tail: ticket is [1 + FBN_TICKET_GROUPS] words
 struct StepEnd {
   int* step;
   unsigned long long* rng;
   double* sumsq;
   long long* nbt0;
   long long* nbt1;
-  unsigned* ticket;   // zero at rest; the last block resets it
+  unsigned* ticket;   // [1 + FBN_TICKET_GROUPS], zero at rest; the last block of each level resets its word
   int max_step;       // total_steps: the counter saturates there (schedule table / coef_hist bounds)
   int* err;           // bit 2 set on a step past max_step (graph replays cannot raise on the host)
 };
@@ -1756,9 +1772,20 @@ __global__ void __launch_bounds__(256) adam_tail_kernel(float* __restrict__ dp, 
   // and the last block publishes nothing another block of this launch reads: a relaxed ticket
   // needs no release/acquire fences (an agent-scope release writes back the XCD's L2 -- in every
   // block that costs tens of microseconds).  The next launch sees the stores at the kernel boundary.
+  // Two-level ticket (ticket[1 + g] for the blocks with blockIdx % FBN_TICKET_GROUPS == g, then
+  // ticket[0] once per group): a returning atomic on one word serialises at ~88 per microsecond,
+  // so hundreds of blocks on one word alone would add microseconds to the tail.
   __syncthreads();
-  if (threadIdx.x == 0)
-    is_last = __hip_atomic_fetch_add(se.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  if (threadIdx.x == 0) {
+    const unsigned ng = min((unsigned)FBN_TICKET_GROUPS, gridDim.x), g = blockIdx.x % ng;
+    const unsigned in_g = (gridDim.x - g + ng - 1) / ng;   // blocks of group g
+    bool last = false;
+    if (__hip_atomic_fetch_add(se.ticket + 1 + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_g - 1) {
+      se.ticket[1 + g] = 0u;
+      last = __hip_atomic_fetch_add(se.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+    }
+    is_last = last;
+  }
   __syncthreads();
   if (is_last && threadIdx.x == 0) {
     if (t + 1 <= se.max_step) se.step[0] = t + 1;
@@ -2071,14 +2098,19 @@ extern "C" int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, i
   // adam_catchup_kernel, A/B)
   static const bool wone = getenv("FBN_WINDOW_ONEPASS") && atoi(getenv("FBN_WINDOW_ONEPASS")) == 1;
   if (parts == 2 && !wone) {
-    const long long waves = (chunk + FBN_WIN_ROWS - 1) / FBN_WIN_ROWS;
+    // rows per wave: 16 below d = 128 (one round of the narrow engine); wave-wide rows take fewer
+    // (FBN_WIN_RPW, default 8) so more waves replay side by side
+    const char* we = getenv("FBN_WIN_RPW");
+    const int wr = we ? std::max(1, std::min(64, atoi(we))) : 8;
+    const int rpw = D >= 128 ? wr : FBN_WIN_ROWS;
+    const long long waves = (chunk + rpw - 1) / rpw;
     const dim3 g2((unsigned)((waves + 3) / 4));
     if (decoupled) {
       FBN_DISPATCH_D_B(adam_window2_kernel, true, D, g2, p, m, v, map, nrows, F, chunk, last,
-                       (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+                       (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, rpw);
     } else {
       FBN_DISPATCH_D_B(adam_window2_kernel, false, D, g2, p, m, v, map, nrows, F, chunk, last,
-                       (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
+                       (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, rpw);
     }
     FBN_CHECK_LAUNCH();
     return FBN_OK;
@@ -2132,12 +2164,15 @@ extern "C" int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B,
     const dim3 g2((unsigned)((n + 255) / 256));
     hipLaunchKernelGGL(adam_pretag_kernel, g2, dim3(256), 0, st, cs, (int)n, step);
     FBN_CHECK_LAUNCH();
+    const char* ee = getenv("FBN_PF_EPW");   // A/B knob, read per call (tools/ab_step.py flips it in-process)
+    const int epw = ee ? std::max(1, std::min(64, atoi(ee))) : 64;
+    const dim3 g3((unsigned)(((n + epw - 1) / epw + 3) / 4));   // 4 waves per block
     if (decoupled) {
-      FBN_DISPATCH_D_B(adam_prefetch2_kernel, true, D, g2, p, m, v, cs, (int)n, last, (const AdamConsts*)consts_table,
-                       step, wd, beta2, omb2, eps, ps);
+      FBN_DISPATCH_D_B(adam_prefetch2_kernel, true, D, g3, p, m, v, cs, (int)n, last, (const AdamConsts*)consts_table,
+                       step, wd, beta2, omb2, eps, ps, epw);
     } else {
-      FBN_DISPATCH_D_B(adam_prefetch2_kernel, false, D, g2, p, m, v, cs, (int)n, last, (const AdamConsts*)consts_table,
-                       step, wd, beta2, omb2, eps, ps);
+      FBN_DISPATCH_D_B(adam_prefetch2_kernel, false, D, g3, p, m, v, cs, (int)n, last, (const AdamConsts*)consts_table,
+                       step, wd, beta2, omb2, eps, ps, epw);
     }
     FBN_CHECK_LAUNCH();
     return FBN_OK;

@@ -337,6 +337,8 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
          True, bias=p["mm_proj.0.bias"], bf16=g16, stream=st)
     if hooks and "after_mmproj" in hooks:         # trainer: side-stream work forked here
         hooks["after_mmproj"]()
+    if hooks and "before_gather" in hooks:        # trainer: the table rows' claims ran on the side stream
+        hooks["before_gather"]()
     X = buf("X", (B, 2, d))                     # fields 3 and 5 (the backward recomputes 1, 2, 4)
     # bf16 mode: the fields after SENET exist only as bf16 (GEMM operand and pair-kernel input)
     v16 = bf and not cfg.bilinear_each
@@ -392,6 +394,8 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
         ev[1].record()
     if after_gather is not None:
         after_gather()
+    if hooks and "after_fields" in hooks:         # trainer: side-stream work forked here
+        hooks["after_fields"]()
     # bilinear: U = V W  ("all")  or  U_i = V_i W_i ("each"), then pair products into c
     fused_bil = bf and not cfg.bilinear_each and fused_bilinear(d)
     a["fused_bilinear"] = fused_bil

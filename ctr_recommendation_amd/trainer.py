@@ -45,6 +45,18 @@ _SIDE_AFTER_MLP0 = os.environ.get("FBN_SIDE_AFTER_MLP0", "0") == "1"
 # ... or after the step's first GEMM (mm_proj), so a replayed graph launches that GEMM before the
 # side-stream branch (A/B knob)
 _SIDE_AFTER_MMPROJ = os.environ.get("FBN_SIDE_AFTER_MMPROJ", "0") == "1"
+# single GPU, A/B knobs of the stream placement (tools/ab_step.py, in-process: each measured SLOWER
+# than the default, profiles/r03_stream_placement_ab.txt):
+#   FBN_CLAIM_ON_SIDE=1  the row claims + claimed-row catch-up on the side stream from the step's
+#                        start, beside the bf16 weight images and the mm_proj GEMM (+15 us/step)
+#   FBN_FIXUP_ON_SIDE=1  the duplicate-gradient fold on the side stream after the fields backward
+#                        (+2-3 us/step)
+#   FBN_SIDE_SERIAL=1    the rolling window + next-batch prefetch on the main stream, in sequence
+_CLAIM_ON_SIDE = os.environ.get("FBN_CLAIM_ON_SIDE", "0") == "1"
+_SIDE_SERIAL = os.environ.get("FBN_SIDE_SERIAL", "0") == "1"
+_FIXUP_ON_SIDE = os.environ.get("FBN_FIXUP_ON_SIDE", "0") == "1"
+# ... or after the gather (fields_fwd then runs with the chip to itself; A/B knob)
+_SIDE_AFTER_GATHER = os.environ.get("FBN_SIDE_AFTER_GATHER", "0") == "1"
 # N > 1: the next batch's routing enqueued after this step's compute (A/B knob)
 _ROUTE_AFTER_COMPUTE = os.environ.get("FBN_ROUTE_AFTER_COMPUTE", "1") == "1"
 # single GPU: the dense gradients' sum of squares inside the table-gradient norm launch (A/B knob)
@@ -349,7 +361,7 @@ class FiBiNETTrainer:
             shape = (self.ring_n, self.B, 2, d) if not sharded else (self.ring_n, self.ring_cap, d)
             self.ring = torch.zeros(shape, dtype=torch.float32, device=dev)
             self.coef_hist = torch.ones(total_steps + 1, dtype=torch.float32, device=dev)
-            self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)     # fbn_adam_step_tail
+            self.ticket = torch.zeros(17, dtype=torch.int32, device=dev)    # fbn_adam_step_tail (FBN_TICKET_WORDS)
         # N > 1: forward + backward between the row exchanges replayed as hipGraph segments split at
         # the SyncBN all-reduces (_Segments), after two eager steps; FBN_SHARD_GRAPH=0 keeps it eager
         self.shard_graph = self.sharded and os.environ.get("FBN_SHARD_GRAPH", "1") != "0"
@@ -392,11 +404,30 @@ class FiBiNETTrainer:
 
         side_hooks = {}
 
-        def catch_up(n_ent, claim=False, before_side=None):
+        def catch_up(n_ent, claim=False, before_side=None, on_side=None):
             # lazy table Adam: the rows claimed this step are brought to `step` Adam steps before
             # anything reads them; the rolling window (step % F; unclaimed rows, read by nothing
             # this step) replays on the side stream beside the rest of the step.  claim (single
-            # GPU): the row claims are made inside the same launch (fbn_adam_claim_catchup)
+            # GPU): the row claims are made inside the same launch (fbn_adam_claim_catchup).
+            # on_side (an event on main at the step's start): the claims run on the side stream,
+            # and the main stream waits for them just before the gather
+            if on_side is not None:
+                self.side.wait_event(on_side)
+                ev = _events(probe, "adam_catchup", self.side)
+                key = _batch_key(batch["item_id"], seq if L else None)
+                pre = self.preclaim if (self.preclaim is not None and key == self._pre_key) else None
+                self._pre_key = None
+                call("fbn_adam_claim_catchup", ptr(batch["item_id"]), ptr(seq) if L else None, B, L, self.V,
+                     ptr(self.map), ptr(self.slot_row), ptr(self.dup), ptr(self.hasdup), ptr(pre), ptr(self.E),
+                     ptr(self.Em), ptr(self.Ev), self.rows_local, d, self.lazy_window, ptr(self.last),
+                     ptr(self.sched), ptr(self.step_dev), self.wd_g, self.beta2, self.eps, *self._pend_args(),
+                     int(self.decoupled), self.side.cuda_stream)
+                _events_end(ev, self.side)
+                claim_ev = torch.cuda.Event()
+                claim_ev.record(self.side)
+                side_hooks["before_gather"] = lambda: main.wait_event(claim_ev)
+                side_pass(wait_main=False)
+                return
             ev = _events(probe, "adam_catchup")
             if claim:
                 key = _batch_key(batch["item_id"], seq if L else None)
@@ -421,15 +452,20 @@ class FiBiNETTrainer:
             if claim and _SIDE_AFTER_MMPROJ:
                 side_hooks["after_mmproj"] = side_pass   # forked after the step's first GEMM
                 return
+            if claim and _SIDE_AFTER_GATHER:
+                side_hooks["after_fields"] = side_pass   # forked after the gather
+                return
             side_pass()
 
-        def side_pass():
-            self.side.wait_stream(main)
-            ev = _events(probe, "adam_window", self.side)
+        def side_pass(wait_main=True):
+            sst = self.side if not _SIDE_SERIAL else main      # FBN_SIDE_SERIAL: in sequence on main
+            if wait_main and not _SIDE_SERIAL:
+                self.side.wait_stream(main)
+            ev = _events(probe, "adam_window", sst)
             call("fbn_adam_catchup", ptr(self.E), ptr(self.Em), ptr(self.Ev), self.rows_local, d, None, 0,
                  ptr(self.map), self.lazy_window, 2, ptr(self.last), ptr(self.sched), ptr(self.step_dev), self.wd_g,
-                 self.beta2, self.eps, *self._pend_args(), int(self.decoupled), self.side.cuda_stream)
-            _events_end(ev, self.side)
+                 self.beta2, self.eps, *self._pend_args(), int(self.decoupled), sst.cuda_stream)
+            _events_end(ev, sst)
             nb = next_batch
             if (self.xchg is None and nb is not None and self.prefetch_rows and nb["item_id"].dtype == torch.int64
                     and nb["item_id"].device == self.device):
@@ -439,13 +475,13 @@ class FiBiNETTrainer:
                     self._pre_key = _batch_key(nb["item_id"], nseq if nL else None)
                 elif d < 128:
                     return                                    # the one-pass form needs wave-wide rows
-                ev = _events(probe, "adam_prefetch", self.side)
+                ev = _events(probe, "adam_prefetch", sst)
                 call("fbn_adam_prefetch", ptr(nb["item_id"]), ptr(nseq) if nL else None, nb["item_id"].shape[0], nL,
                      self.V, ptr(self.map), ptr(self.preclaim if self._pre_key is not None else None), ptr(self.E),
                      ptr(self.Em), ptr(self.Ev), d, ptr(self.last),
                      ptr(self.sched), ptr(self.step_dev), self.wd_g, self.beta2, self.eps, *self._pend_args(),
-                     int(self.decoupled), self.side.cuda_stream)
-                _events_end(ev, self.side)
+                     int(self.decoupled), sst.cuda_stream)
+                _events_end(ev, sst)
 
         def start_untouched_adam():
             # eager mode: every row this shard's batch does not touch gets g = wd * p, independent
@@ -475,6 +511,11 @@ class FiBiNETTrainer:
 
         w16_main = cfg.bf16 and self.xchg is None and _W16_MODE == "main"
         w16_late = cfg.bf16 and self.xchg is None and lazy and _W16_MODE == "late"
+        claim_side = None
+        if (self.xchg is None and lazy and _CLAIM_ON_SIDE and not w16_late and not _SIDE_AFTER_MLP0
+                and not _SIDE_AFTER_MMPROJ and not _SIDE_AFTER_GATHER):
+            claim_side = torch.cuda.Event()          # the step's start: the claims wait for nothing later
+            claim_side.record(main)
         if w16_main:
             # on the main stream ahead of the claims: a cross-queue wait inside a replayed graph
             # costs ~10 us, about what the conversion itself takes
@@ -516,13 +557,15 @@ class FiBiNETTrainer:
                 catch_up(B * (L + 1), claim=True, before_side=step_start)
                 w16_ev = self._w16_ev
             else:
-                catch_up(B * (L + 1), claim=True)
+                catch_up(B * (L + 1), claim=True, on_side=claim_side)
         elif self.xchg is None:
             call("fbn_claim_rows", ptr(batch["item_id"]), ptr(seq) if L else None, B, L, self.V, ptr(self.map),
                  ptr(self.slot_row), ptr(self.dup), ptr(self.hasdup), st)
         if w16_ev is not None:
             main.wait_event(w16_ev)
         graphed = False
+        fixup_side = (self.xchg is None and _FIXUP_ON_SIDE and not self.deterministic and L > 0
+                      and not self._early_grad_xchg())
         if (self.xchg is not None and self.shard_graph and probe is None and masks_out is None
                 and self.table_adam != "eager"):
             sendbuf = self.xchg.make_sendbuf()
@@ -536,11 +579,18 @@ class FiBiNETTrainer:
                             after_gather=start_untouched_adam if self.table_adam == "eager" else None,
                             hooks=side_hooks)
             sendbuf = self.xchg.make_sendbuf() if self.xchg is not None else None
+            bhooks = {"after_fields_bwd": self._grad_xchg_start} if self._early_grad_xchg() else None
+            if fixup_side:
+                def fork_fixup():
+                    self.side.wait_stream(main)
+                    call("fbn_sparse_fixup_dup", ptr(self.dup), B * (L + 1), ptr(self.gvec), ptr(self.extra),
+                         ptr(self.slot_row), L + 1, d, self.side.cuda_stream)
+                bhooks = {"after_fields_bwd": fork_fixup}
             ops.backward(self.p, batch, a, a["gout"], self.g, cfg, gvec=self.gvec if self.xchg is None else None,
                          gnorm=self.gnorm if self.xchg is None else None,
                          pos=pos, sendbuf=sendbuf, coll=self.bn_coll, ntot=self._bn_n(ntot, B),
                          extra_sums=[(a["loss_terms"], B, 1, self.loss, 1.0 / ntot)], probe=probe,
-                         hooks={"after_fields_bwd": self._grad_xchg_start} if self._early_grad_xchg() else None)
+                         hooks=bhooks)
         dense_work = None
         if self.sharded and self._early_grad_xchg():
             # the dense gradients are final once the compute is: their all-reduce goes out now,
@@ -566,8 +616,11 @@ class FiBiNETTrainer:
                      gsrc[2], d, ptr(self.fx), st)
             else:
                 gsrc = (self.gvec, self.extra, L + 1)
-                call("fbn_sparse_fixup_dup", ptr(self.dup), n_ent, ptr(self.gvec), ptr(self.extra),
-                     ptr(self.slot_row), L + 1, d, st)
+                if fixup_side:
+                    main.wait_stream(self.side)     # the fold (and the side's table passes) done
+                else:
+                    call("fbn_sparse_fixup_dup", ptr(self.dup), n_ent, ptr(self.gvec), ptr(self.extra),
+                         ptr(self.slot_row), L + 1, d, st)
         else:
             # owner: one received row per entry -- straight into this step's deferred-gradient ring
             # slot when it fits, else a buffer of its own and the rows applied at the step end

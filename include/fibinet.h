@@ -349,8 +349,9 @@ int fbn_adam_flush(float* p, float* m, float* v, long long nrows, int D, int* la
                    const int* step, float wd, float beta2, float eps, int* pend, const float* ring,
                    const float* coef_hist, long long ring_stride, int ring_n, int decoupled, void* stream);
 /* Single-GPU step tail in ONE launch: fbn_adam_dense (clip from the sumsq slots) on the flat dense
- * parameters + fbn_adam_commit on the table + fbn_step_end; ticket = one device unsigned, zero
- * before the first call (the kernel's last block resets it); max_step / err as fbn_step_end. */
+ * parameters + fbn_adam_commit on the table + fbn_step_end; ticket = FBN_TICKET_WORDS device
+ * unsigneds, zero before the first call (the kernel resets them); max_step / err as fbn_step_end. */
+#define FBN_TICKET_WORDS 17
 int fbn_adam_step_tail(float* dp, const float* dg, float* dm, float* dv, long long n_dense, const double* sumsq,
                        float max_norm, float* coef_out, float* norm_out, float* p, float* m, float* v, int D, int* map,
                        const float* gvec, float* extra, int* slot_row, int Lp1, int n, const void* consts_table,
