@@ -684,7 +684,8 @@ static int launch_fields_fwd_h(const FieldArgs& a, int D, hipStream_t st) {
 
 template <int MODE>
 static int launch_fields_fwd(const FieldArgs& a, int D, hipStream_t st) {
-  static const int hch = getenv("FBN_FIELDS_HCH") ? atoi(getenv("FBN_FIELDS_HCH")) : FBN_HCH;
+  const char* he = getenv("FBN_FIELDS_HCH");   // A/B knob, read per call
+  const int hch = he ? atoi(he) : FBN_HCH;
   if (hch == 20) return launch_fields_fwd_h<MODE, 20>(a, D, st);
   if (hch == 5) return launch_fields_fwd_h<MODE, 5>(a, D, st);
   return launch_fields_fwd_h<MODE, 10>(a, D, st);

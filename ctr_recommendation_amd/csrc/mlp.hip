@@ -733,6 +733,7 @@ struct SlabJob {
   float beta;
 };
 #define FBN_MAX_SUM_JOBS 16
+#define FBN_SUM_WIDE 32        // jobs with at least this many columns take 64 columns per block
 #define FBN_MAX_SLAB_JOBS 8
 #define FBN_SLAB_GROUPS 4      // slab groups per output quad (256 threads = 64 quads x 4 groups)
 struct SumJobs {
@@ -777,6 +778,28 @@ __device__ __forceinline__ void slab_block(const SumJobs& J, int gb) {
     *reinterpret_cast<f32x4*>(cp) = t;
   }
 }
+// wide jobs (C >= FBN_SUM_WIDE): a block takes 64 consecutive columns, its 4 waves stride over the
+// rows (64 lanes read one 256-B run of a row: coalesced), then a fixed-order fold of the 4
+__device__ __forceinline__ void sum_wide_block(const SumJob& jb, int c0) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = c0 + lane;
+  const size_t ld = jb.ld > 0 ? jb.ld : jb.C;
+  float a0 = 0.f, a1 = 0.f;
+  if (c < jb.C) {
+    int k = w;
+    for (; k + 4 < jb.nch; k += 8) {
+      a0 += jb.part[(size_t)k * ld + c];
+      a1 += jb.part[(size_t)(k + 4) * ld + c];
+    }
+    for (; k < jb.nch; k += 4) a0 += jb.part[(size_t)k * ld + c];
+  }
+  red[w][lane] = a0 + a1;
+  __syncthreads();
+  if (w == 0 && c < jb.C) {
+    const float t = jb.scale * ((red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]));
+    jb.out[c] = jb.beta != 0.f ? jb.beta * jb.out[c] + t : t;
+  }
+}
 __global__ void __launch_bounds__(256) sum_jobs_kernel(SumJobs J) {
   __shared__ float red[4];
   const int gc = blockIdx.x;
@@ -787,6 +810,10 @@ __global__ void __launch_bounds__(256) sum_jobs_kernel(SumJobs J) {
   int u = 0;
   while (u + 1 < J.n && gc >= J.col0[u + 1]) ++u;
   const SumJob jb = J.j[u];
+  if (jb.C >= FBN_SUM_WIDE) {
+    sum_wide_block(jb, (gc - J.col0[u]) * 64);
+    return;
+  }
   const int c = gc - J.col0[u];
   const size_t ld = jb.ld > 0 ? jb.ld : jb.C;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
@@ -970,11 +997,9 @@ extern "C" int fbn_bn_eval_params(const float* run_mean, const float* run_var, f
 // in flight at once (the fused head reduces a whole row per wave and then runs a serial sigmoid /
 // BCE tail: with 16 rows per workgroup each wave walked 4 rows one after the other).
 static int bn_act_rows_per_chunk() {
-  static const int rpc = [] {
-    const char* e = getenv("FBN_BN_ACT_RPC");
-    const int v = e ? atoi(e) : 4;
-    return v >= 4 && v % 4 == 0 ? v : 4;
-  }();
+  const char* e = getenv("FBN_BN_ACT_RPC");   // A/B knob, read per call
+  const int v = e ? atoi(e) : 4;
+  const int rpc = v >= 4 && v % 4 == 0 ? v : 4;
   return rpc;
 }
 
@@ -1130,7 +1155,9 @@ struct ConvJobs {
   ConvJob j[8];
   int tile0[9];   // first 64x64 output tile of each job (prefix sum)
 };
-// One 64x64 output tile per workgroup.  A transposed job reads its source tile along the
+// One 64x64 output tile per workgroup, four consecutive outputs per thread (one 8-B bf16x4 store):
+// a plain job reads four source columns at once (16-B load when they are contiguous and aligned:
+// the remap offsets and seg are multiples of 4); a transposed job reads its source tile along the
 // source's contiguous dimension into LDS (coalesced) and writes the output rows from LDS.
 __global__ void __launch_bounds__(256) convert_bf16_kernel(ConvJobs jobs, int njobs) {
   __shared__ float tile[64][65];
@@ -1140,28 +1167,47 @@ __global__ void __launch_bounds__(256) convert_bf16_kernel(ConvJobs jobs, int nj
   const int t = blockIdx.x - jobs.tile0[jb];
   const int tcols = (J.cols + 63) / 64;
   const int i0 = (t / tcols) * 64, j0 = (t % tcols) * 64;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int tq = threadIdx.x & 15, tr = threadIdx.x >> 4;   // column quad, row of 16
   if (!J.trans) {
-    const int j = j0 + tx;
-    if (j < J.cols) {
-      const int b = j + (j < J.seg ? J.off0 : J.off1);
-      // all 16 loads in flight before the first store (the loop is unrolled)
-      float val[16];
+    const int j = j0 + 4 * tq;
+    if (j >= J.cols) return;
+    const bool full = j + 4 <= J.cols;
+    const int b = j + (j < J.seg ? J.off0 : J.off1);
+    const bool vec = full && !(J.ld & 3) && !(b & 3) && (J.seg == 0x7fffffff || !(J.seg & 3) || j + 4 <= J.seg ||
+                                                         j >= J.seg);
+    f32x4 val[4];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int i = i0 + ty + 4 * k;
-        val[k] = i < J.rows ? J.src[(size_t)i * J.ld + b] : 0.f;
+    for (int k = 0; k < 4; ++k) {   // all loads in flight before the first store
+      const int i = i0 + tr + 16 * k;
+      if (i >= J.rows) { val[k] = (f32x4){0.f, 0.f, 0.f, 0.f}; continue; }
+      if (vec) {
+        val[k] = *reinterpret_cast<const f32x4*>(J.src + (size_t)i * J.ld + b);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int jj = j + e;
+          val[k][e] = jj < J.cols ? J.src[(size_t)i * J.ld + jj + (jj < J.seg ? J.off0 : J.off1)] : 0.f;
+        }
       }
+    }
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int i = i0 + ty + 4 * k;
-        if (i < J.rows) J.dst[(size_t)i * J.cols + j] = f2bf(val[k]);
+    for (int k = 0; k < 4; ++k) {
+      const int i = i0 + tr + 16 * k;
+      if (i >= J.rows) continue;
+      short* d = J.dst + (size_t)i * J.cols + j;
+      if (full && !(J.cols & 3)) {
+        *reinterpret_cast<bf16x4*>(d) = (bf16x4){f2bf(val[k][0]), f2bf(val[k][1]), f2bf(val[k][2]), f2bf(val[k][3])};
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (j + e < J.cols) d[e] = f2bf(val[k][e]);
       }
     }
     return;
   }
   // out[i][j] = src[j][rm(i)]: lanes run along i, the source's contiguous dimension
   {
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     const int i = i0 + tx;
     const int b = i + (i < J.seg ? J.off0 : J.off1);
 #pragma unroll
@@ -1171,11 +1217,22 @@ __global__ void __launch_bounds__(256) convert_bf16_kernel(ConvJobs jobs, int nj
     }
   }
   __syncthreads();
-  const int j = j0 + tx;
+  const int j = j0 + 4 * tq;
+  if (j >= J.cols) return;
 #pragma unroll
-  for (int r = ty; r < 64; r += 4) {
-    const int i = i0 + r;
-    if (i < J.rows && j < J.cols) J.dst[(size_t)i * J.cols + j] = f2bf(tile[tx][r]);
+  for (int k = 0; k < 4; ++k) {
+    const int r = tr + 16 * k, i = i0 + r;
+    if (i >= J.rows) continue;
+    short* d = J.dst + (size_t)i * J.cols + j;
+    const bf16x4 v = {f2bf(tile[4 * tq][r]), f2bf(tile[4 * tq + 1][r]), f2bf(tile[4 * tq + 2][r]),
+                      f2bf(tile[4 * tq + 3][r])};
+    if (j + 4 <= J.cols && !(J.cols & 3)) {
+      *reinterpret_cast<bf16x4*>(d) = v;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (j + e < J.cols) d[e] = v[e];
+    }
   }
 }
 
@@ -1301,7 +1358,8 @@ extern "C" int fbn_sum_jobs2(const SumJob* jobs, int n, const SlabJob* slabs, in
   J.col0[0] = 0;
   for (int i = 0; i < n; ++i) {
     J.j[i] = jobs[i];
-    J.col0[i + 1] = J.col0[i] + jobs[i].C;
+    // blocks of job i: one per column, or one per 64 columns for a wide job
+    J.col0[i + 1] = J.col0[i] + (jobs[i].C >= FBN_SUM_WIDE ? fbn_cdiv(jobs[i].C, 64) : jobs[i].C);
   }
   J.ns = ns;
   J.blk0[0] = 0;

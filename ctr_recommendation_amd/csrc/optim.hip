@@ -489,12 +489,12 @@ __global__ void __launch_bounds__(256) sumsq_norms_kernel(GradSrc s, const doubl
       acc += gnorm[(size_t)b * 2 + (t ? 1 : 0)];
     }
     unsigned long long mask = __ballot(flag);
-    while (mask) {
-      const int l = __ffsll((long long)mask) - 1;
-      mask &= mask - 1;
-      const float* v = grad_base<D>(s, (int)(e0 + l));
-      float* x = s.extra + (size_t)(e0 + l) * D;
-      if (fx) {   // deterministic fold: the full row gradient from the fixed-point total
+    if (fx) {
+      while (mask) {
+        const int l = __ffsll((long long)mask) - 1;
+        mask &= mask - 1;
+        float* x = s.extra + (size_t)(e0 + l) * D;
+        // deterministic fold: the full row gradient from the fixed-point total
         unsigned long long* a = fx + (size_t)(e0 + l) * D;
         for (int k = lane; k < D; k += 64) {
           const float y = (float)((double)(long long)a[k] * (1.0 / 1099511627776.0));
@@ -502,11 +502,29 @@ __global__ void __launch_bounds__(256) sumsq_norms_kernel(GradSrc s, const doubl
           a[k] = 0ull;
           acc += (double)(y * y);
         }
-        continue;
       }
-      for (int k = lane; k < D; k += 64) {
-        const float y = v[k] + x[k];
-        acc += (double)(y * y);
+    } else {
+      // the wave's flagged claimers RPR at a time, D/8 lanes per row (8 elements each): a wave
+      // with up to RPR of them pays one round trip, not one per claimer
+      constexpr int LPR = D / 8, RPR = 64 / LPR;
+      while (mask) {
+        int mine = -1;
+#pragma unroll
+        for (int gi = 0; gi < RPR; ++gi) {
+          if (!mask) break;
+          const int l = __ffsll((long long)mask) - 1;
+          mask &= mask - 1;
+          if (lane / LPR == gi) mine = l;
+        }
+        if (mine < 0) continue;
+        const int c = (lane % LPR) * 8;
+        const float* v = grad_base<D>(s, (int)(e0 + mine)) + c;
+        const float* x = s.extra + (size_t)(e0 + mine) * D + c;
+        const f32x4 v0 = *reinterpret_cast<const f32x4*>(v), v1 = *reinterpret_cast<const f32x4*>(v + 4);
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(x), x1 = *reinterpret_cast<const f32x4*>(x + 4);
+        const f32x4 y0 = v0 + x0, y1 = v1 + x1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc += (double)(y0[k] * y0[k]) + (double)(y1[k] * y1[k]);
       }
     }
   }
@@ -1651,23 +1669,31 @@ __device__ __forceinline__ void adam_commit_body(float* __restrict__ p, float* _
     }
   }
   // one entry per lane: an unflagged claimer records its vector in pend; flagged claimers (rare)
-  // are updated by the wave's G-lane groups afterwards
+  // and rows the next batch reads are updated by the wave's G-lane groups afterwards
   const int lane = threadIdx.x & 63, q = lane % G;
   for (long long e0 = (bid * blockDim.x + threadIdx.x) - lane; e0 < n; e0 += nblk * blockDim.x) {
     const long long e = e0 + lane;
     const int sr = e < n ? gs.slot_row[e] : -1;
     const bool flag = sr != -1 && (sr & FBN_SLOT_FLAG);
+    bool imm = flag;
     if (sr != -1 && !flag) {
-      if (gs.Lp1 == 1) {   // per-entry rows (N > 1 owner): the entry's own row of the ring slot
-        ps.pend[(size_t)(sr) * FBN_RS_I] = (int)e;
+      // a row the NEXT batch also reads (its pre-claim tag is step t + 1: fbn_adam_prefetch's
+      // pass for that batch ran during this step) takes step t now, so the next step's claims
+      // find it current and replay nothing; the others defer it to their next replay
+      if (last && (unsigned)row_state(last, sr).y == (unsigned)(t + 1)) {
+        imm = true;
       } else {
-        const int b = (int)(e / gs.Lp1), tt = (int)(e - (long long)b * gs.Lp1);
-        ps.pend[(size_t)(sr) * FBN_RS_I] = b * 2 + (tt ? 1 : 0);
+        if (gs.Lp1 == 1) {   // per-entry rows (N > 1 owner): the entry's own row of the ring slot
+          ps.pend[(size_t)(sr) * FBN_RS_I] = (int)e;
+        } else {
+          const int b = (int)(e / gs.Lp1), tt = (int)(e - (long long)b * gs.Lp1);
+          ps.pend[(size_t)(sr) * FBN_RS_I] = b * 2 + (tt ? 1 : 0);
+        }
+        map[sr] = -1;
+        gs.slot_row[e] = -1;
       }
-      map[sr] = -1;
-      gs.slot_row[e] = -1;
     }
-    unsigned long long mask = __ballot(flag);
+    unsigned long long mask = __ballot(imm);
     while (mask) {
       // up to RPW flagged entries per round, one per G-lane group
       int mine = -1;
@@ -1683,9 +1709,11 @@ __device__ __forceinline__ void adam_commit_body(float* __restrict__ p, float* _
       const long long ee = e0 + mine;
       const long long r = sr_l & ~FBN_SLOT_FLAG;
       f32x4 gg = *reinterpret_cast<const f32x4*>(grad_base<D>(gs, (int)ee) + 4 * q);
-      float* ex = gs.extra + (size_t)ee * D + 4 * q;
-      gg = gs.full ? *reinterpret_cast<const f32x4*>(ex) : gg + *reinterpret_cast<const f32x4*>(ex);
-      *reinterpret_cast<f32x4*>(ex) = (f32x4){0.f, 0.f, 0.f, 0.f};
+      if (sr_l & FBN_SLOT_FLAG) {   // duplicates folded into extra (the only claimers with one)
+        float* ex = gs.extra + (size_t)ee * D + 4 * q;
+        gg = gs.full ? *reinterpret_cast<const f32x4*>(ex) : gg + *reinterpret_cast<const f32x4*>(ex);
+        *reinterpret_cast<f32x4*>(ex) = (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
       const size_t off = (size_t)r * D + 4 * q;
       f32x4 pp = *reinterpret_cast<f32x4*>(p + off);
       f32x4 mm = *reinterpret_cast<f32x4*>(m + off);
@@ -2035,12 +2063,16 @@ extern "C" int fbn_adam_step_tail(float* dp, const float* dg, float* dm, float* 
   const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
   const StepEnd se{step, rng, (double*)sumsq, nbt0, nbt1, ticket, max_step, err};
   long long nd = (n_dense / 4 + 255) / 256;
-  // few, fat blocks: every block draws the step-end ticket (one returning atomic on one word,
-  // ~88 per microsecond chip-wide), so the block count, not the work, sets the tail's floor
-  if (nd > 256) nd = 256;
+  // block caps (every block draws the step-end ticket; two-level, so ~16x less contention than
+  // one word): FBN_TAIL_ND / FBN_TAIL_NC, A/B knobs read per call
+  const char* ndc = getenv("FBN_TAIL_ND");
+  const char* ncc = getenv("FBN_TAIL_NC");
+  const long long cap_d = ndc ? atoll(ndc) : 256, cap_c = ncc ? atoll(ncc) : 1024;   // A/B: nc 1024 -5 us
+  if (nd > cap_d) nd = cap_d;
   if (nd < 1) nd = 1;
   long long nc = ((long long)(n > 0 ? n : 1) + 255) / 256;
-  if (nc > 256) nc = 256;
+  if (nc > cap_c) nc = cap_c;
+  if (nc < 1) nc = 1;
   FBN_DISPATCH_D(adam_tail_kernel, D, dim3((unsigned)(nd + nc)), dp, dg, dm, dv, n_dense, (int)nd, max_norm, coef_out,
                  norm_out, p, m, v, map, s, n, (const AdamConsts*)consts_table, wd, beta2, omb2, eps, last, ps,
                  coef_hist, B, se);

@@ -101,6 +101,8 @@ def test_gemm_slabs_deferred_sum(hip_device, M, N, K, remap):
     assert sums.gemm_slabs(A, Bm, C, M, N, K, M, N, ldc, True, False, rC=rc)
     sums.add(part, 300, 24, out1, ld=40)
     sums.add(part[:, 24:], 300, 16, out2, scale=0.5, ld=40)
+    out3 = torch.ones(40, device=hip_device)
+    sums.add(part, 300, 40, out3, beta=2.0, ld=40)           # a wide job (64 columns per block)
     sums.flush(ops._lib.stream_handle(hip_device))
     torch.cuda.synchronize()
     ref = A.double().T @ Bm.double()
@@ -112,6 +114,7 @@ def test_gemm_slabs_deferred_sum(hip_device, M, N, K, remap):
     pd = part.double().sum(0)
     assert torch.allclose(out1.double(), pd[:24], rtol=1e-5, atol=1e-4)
     assert torch.allclose(out2.double(), 0.5 * pd[24:], rtol=1e-5, atol=1e-4)
+    assert torch.allclose(out3.double(), 2.0 + pd, rtol=1e-5, atol=1e-4)
 
 
 @pytest.mark.gpu
@@ -245,3 +248,22 @@ def test_duplicate_fold_matches_scatter_add(hip_device, d, zipf):
     assert err <= 1e-5, err
     if zipf > 0:
         assert int((dup >= 0).sum()) > n // 10       # the case is really duplicate-heavy
+
+
+@pytest.mark.parametrize("d", [128, 16, 64])
+def test_bf16_weight_images_match_torch(hip_device, d):
+    """fbn_convert_bf16 (the step's bf16 GEMM operand images, four outputs per thread): every
+    image equals torch's round-to-nearest-even bf16 of the same f32 weights, remapped / transposed
+    as the GEMMs read them (mlp.0.weight without its V_0 and (0, j) pair columns)."""
+    from ctr_recommendation_amd.model_fibinet import build_model
+    torch.manual_seed(3)
+    p = {k: v.to(hip_device) for k, v in build_model(None, {"embedding_dim": d, "vocab_size": 50}).state_dict().items()}
+    x = torch.randn((300, 128), device=hip_device)
+    out = ops.bf16_weights(p, d, {}, ops._lib.stream_handle(hip_device), x=x)
+    torch.cuda.synchronize()
+    w0 = p["mlp.0.weight"]
+    cols = torch.cat([torch.arange(d, 6 * d), torch.arange(11 * d, 21 * d)]).to(hip_device)
+    ref = {"Wa": w0[:, cols], "WaT": w0[:, cols].T, "Wb": p["mlp.4.weight"], "WbT": p["mlp.4.weight"].T,
+           "Wp": p["mm_proj.0.weight"], "W": p["bilinear.W"], "WT": p["bilinear.W"].T, "x": x}
+    for k, r in ref.items():
+        assert torch.equal(out[k], r.contiguous().bfloat16()), k

@@ -1,7 +1,7 @@
 """In-process A/B of the eager C3 step over Python-level switches (module globals of trainer /
 ops), alternating blocks of K steps per arm for R rounds on one trainer at steady state; prints
-the median ms/step per arm.  Usage: python tools/ab_step.py ARM [ARM ...] with ARM =
-name:module.GLOBAL=value[,module.GLOBAL=value...] ('base' = no change; module env = an
+the median ms/step per arm (AB_ZIPF=s: Zipf(s) ids).  Usage: python tools/ab_step.py ARM [ARM ...] with ARM =
+name:module.GLOBAL=value[;module.GLOBAL=value...] ('base' = no change; module env = an
 environment variable the library reads per call), e.g.
   python tools/ab_step.py base claim_main:trainer._CLAIM_ON_SIDE=False"""
 import os
@@ -32,7 +32,7 @@ arms = []
 for a in sys.argv[1:] or ["base"]:
     name, _, spec = a.partition(":")
     sets = []
-    for kv in filter(None, spec.split(",")):
+    for kv in filter(None, spec.split(";")):
         k, v = kv.split("=")
         m, g = k.split(".")
         sets.append((mods[m], g, eval(v)))
@@ -42,7 +42,7 @@ V, B, K, R = 1_250_000, 8192, int(os.environ.get("AB_K", 40)), int(os.environ.ge
 tr = FiBiNETTrainer({"embedding_dim": 128, "vocab_size": V, "compute_dtype": "bf16"}, total_steps=300 + 2 * R * K * len(arms),
                     batch_size=B, device=dev)
 nb = 160
-batches = make_device_batches(nb, B, V, 20, dev, seed=2025)
+batches = make_device_batches(nb, B, V, 20, dev, seed=2025, zipf=float(os.environ.get("AB_ZIPF", "0")))
 i = 0
 for _ in range(280):
     tr.step(*batches[i % nb], next_batch=batches[(i + 1) % nb][0])
