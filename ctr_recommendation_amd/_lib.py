@@ -133,10 +133,16 @@ def lib() -> ctypes.CDLL:
     return _lib
 
 
+_fns = {}
+_UNCHECKED = ("fbn_version", "fbn_device_ok")
+
+
 def call(name: str, *args) -> int:
-    rc = getattr(lib(), name)(*args)
-    if isinstance(rc, int) and rc != 0 and name not in ("fbn_version", "fbn_device_ok") and not name.endswith(
-            ("_size", "_grid")):
+    f = _fns.get(name)
+    if f is None:                  # bound ctypes function, looked up once (host time per step)
+        f = _fns[name] = getattr(lib(), name)
+    rc = f(*args)
+    if rc and isinstance(rc, int) and name not in _UNCHECKED and not name.endswith(("_size", "_grid")):
         msg = lib().fbn_last_error().decode(errors="replace")
         raise RuntimeError(f"{name} failed (code {rc}): {msg}")
     return rc

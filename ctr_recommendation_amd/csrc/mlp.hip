@@ -733,7 +733,7 @@ struct SlabJob {
   float beta;
 };
 #define FBN_MAX_SUM_JOBS 16
-#define FBN_SUM_WIDE 32        // jobs with at least this many columns take 64 columns per block
+#define FBN_SUM_WIDE 32        // jobs with at least this many columns take 16 columns per block
 #define FBN_MAX_SLAB_JOBS 8
 #define FBN_SLAB_GROUPS 4      // slab groups per output quad (256 threads = 64 quads x 4 groups)
 struct SumJobs {
@@ -778,25 +778,29 @@ __device__ __forceinline__ void slab_block(const SumJobs& J, int gb) {
     *reinterpret_cast<f32x4*>(cp) = t;
   }
 }
-// wide jobs (C >= FBN_SUM_WIDE): a block takes 64 consecutive columns, its 4 waves stride over the
-// rows (64 lanes read one 256-B run of a row: coalesced), then a fixed-order fold of the 4
+// wide jobs (C >= FBN_SUM_WIDE): a block takes 16 consecutive columns and 16 row streams (16 lanes
+// read one 64-B run of a row: coalesced; every row stream has nch/16 rows), then a fixed-order fold
+// of the 16 streams
 __device__ __forceinline__ void sum_wide_block(const SumJob& jb, int c0) {
-  __shared__ float red[4][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, c = c0 + lane;
+  __shared__ float red[16][17];
+  const int col = threadIdx.x & 15, str = threadIdx.x >> 4, c = c0 + col;
   const size_t ld = jb.ld > 0 ? jb.ld : jb.C;
   float a0 = 0.f, a1 = 0.f;
   if (c < jb.C) {
-    int k = w;
-    for (; k + 4 < jb.nch; k += 8) {
+    int k = str;
+    for (; k + 16 < jb.nch; k += 32) {
       a0 += jb.part[(size_t)k * ld + c];
-      a1 += jb.part[(size_t)(k + 4) * ld + c];
+      a1 += jb.part[(size_t)(k + 16) * ld + c];
     }
-    for (; k < jb.nch; k += 4) a0 += jb.part[(size_t)k * ld + c];
+    for (; k < jb.nch; k += 16) a0 += jb.part[(size_t)k * ld + c];
   }
-  red[w][lane] = a0 + a1;
+  red[str][col] = a0 + a1;
   __syncthreads();
-  if (w == 0 && c < jb.C) {
-    const float t = jb.scale * ((red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]));
+  if (str == 0 && c < jb.C) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][col];
+    t *= jb.scale;
     jb.out[c] = jb.beta != 0.f ? jb.beta * jb.out[c] + t : t;
   }
 }
@@ -811,7 +815,7 @@ __global__ void __launch_bounds__(256) sum_jobs_kernel(SumJobs J) {
   while (u + 1 < J.n && gc >= J.col0[u + 1]) ++u;
   const SumJob jb = J.j[u];
   if (jb.C >= FBN_SUM_WIDE) {
-    sum_wide_block(jb, (gc - J.col0[u]) * 64);
+    sum_wide_block(jb, (gc - J.col0[u]) * 16);
     return;
   }
   const int c = gc - J.col0[u];
@@ -1359,7 +1363,7 @@ extern "C" int fbn_sum_jobs2(const SumJob* jobs, int n, const SlabJob* slabs, in
   for (int i = 0; i < n; ++i) {
     J.j[i] = jobs[i];
     // blocks of job i: one per column, or one per 64 columns for a wide job
-    J.col0[i + 1] = J.col0[i] + (jobs[i].C >= FBN_SUM_WIDE ? fbn_cdiv(jobs[i].C, 64) : jobs[i].C);
+    J.col0[i + 1] = J.col0[i] + (jobs[i].C >= FBN_SUM_WIDE ? fbn_cdiv(jobs[i].C, 16) : jobs[i].C);
   }
   J.ns = ns;
   J.blk0[0] = 0;

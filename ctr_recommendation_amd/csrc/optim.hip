@@ -1694,35 +1694,43 @@ __device__ __forceinline__ void adam_commit_body(float* __restrict__ p, float* _
       }
     }
     unsigned long long mask = __ballot(imm);
+    // up to RPW8 of them per round, one per group of D/8 lanes (8 elements each: every load of a
+    // round in flight at once)
+    constexpr int G8 = D / 8 > 0 ? D / 8 : 1, RPW8 = 64 / G8;
+    const int q8 = lane % G8;
     while (mask) {
-      // up to RPW flagged entries per round, one per G-lane group
       int mine = -1;
 #pragma unroll
-      for (int gi = 0; gi < RPW; ++gi) {
+      for (int gi = 0; gi < RPW8; ++gi) {
         if (!mask) break;
         const int l = __ffsll((long long)mask) - 1;
         mask &= mask - 1;
-        if (lane / G == gi) mine = l;
+        if (lane / G8 == gi) mine = l;
       }
       const int sr_l = __shfl(sr, mine < 0 ? 0 : mine, 64);
       if (mine < 0) continue;
       const long long ee = e0 + mine;
       const long long r = sr_l & ~FBN_SLOT_FLAG;
-      f32x4 gg = *reinterpret_cast<const f32x4*>(grad_base<D>(gs, (int)ee) + 4 * q);
-      if (sr_l & FBN_SLOT_FLAG) {   // duplicates folded into extra (the only claimers with one)
-        float* ex = gs.extra + (size_t)ee * D + 4 * q;
-        gg = gs.full ? *reinterpret_cast<const f32x4*>(ex) : gg + *reinterpret_cast<const f32x4*>(ex);
-        *reinterpret_cast<f32x4*>(ex) = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = 8 * q8 + 4 * h;
+        if (D < 8 && c >= D) break;
+        f32x4 gg = *reinterpret_cast<const f32x4*>(grad_base<D>(gs, (int)ee) + c);
+        if (sr_l & FBN_SLOT_FLAG) {   // duplicates folded into extra (the only claimers with one)
+          float* ex = gs.extra + (size_t)ee * D + c;
+          gg = gs.full ? *reinterpret_cast<const f32x4*>(ex) : gg + *reinterpret_cast<const f32x4*>(ex);
+          *reinterpret_cast<f32x4*>(ex) = (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+        const size_t off = (size_t)r * D + c;
+        f32x4 pp = *reinterpret_cast<f32x4*>(p + off);
+        f32x4 mm = *reinterpret_cast<f32x4*>(m + off);
+        f32x4 vv = *reinterpret_cast<f32x4*>(v + off);
+        adam_tab4<true>(pp, mm, vv, gg * coef, wd, b2, omb2, eps, k);
+        *reinterpret_cast<f32x4*>(p + off) = pp;
+        *reinterpret_cast<f32x4*>(m + off) = mm;
+        *reinterpret_cast<f32x4*>(v + off) = vv;
       }
-      const size_t off = (size_t)r * D + 4 * q;
-      f32x4 pp = *reinterpret_cast<f32x4*>(p + off);
-      f32x4 mm = *reinterpret_cast<f32x4*>(m + off);
-      f32x4 vv = *reinterpret_cast<f32x4*>(v + off);
-      adam_tab4<true>(pp, mm, vv, gg * coef, wd, b2, omb2, eps, k);
-      *reinterpret_cast<f32x4*>(p + off) = pp;
-      *reinterpret_cast<f32x4*>(m + off) = mm;
-      *reinterpret_cast<f32x4*>(v + off) = vv;
-      if (q == 0) {
+      if (q8 == 0) {
         map[r] = -1;
         last[(size_t)(r) * FBN_RS_I] = t + 1;
         gs.slot_row[ee] = -1;

@@ -145,10 +145,12 @@ class DeferredSums:
     out[c] = beta*out[c] + scale * sum_k part[k*ld + c], and the weight-gradient GEMMs' split-K
     slabs (gemm_slabs).  Partials must stay alive until flush()."""
 
-    def __init__(self):
+    def __init__(self, cache: Optional[Dict[str, torch.Tensor]] = None):
         self.jobs = []
         self.slabs = []
         self.keep = []
+        self.cache = cache      # slab workspaces kept across steps (one per GEMM shape)
+        self.used = set()
 
     def add(self, part, nch, C, out, scale=1.0, beta=0.0, ld=0):
         self.jobs.append((part.data_ptr(), out.data_ptr(), int(nch), int(C), float(scale), float(beta), int(ld), 0))
@@ -164,7 +166,15 @@ class DeferredSums:
                 and (rC[0] == INT_MAX or rC[0] % 4 == 0)):
             return False
         nbytes = _lib.lib().fbn_gemm_slabs_size(M, N, K)
-        ws = _ws(nbytes, out.device)
+        key = f"slab_ws_{M}_{N}_{K}"
+        while key in self.used:       # two slab GEMMs of one shape in a step: separate workspaces
+            key += "'"
+        self.used.add(key)
+        ws = self.cache.get(key) if self.cache is not None else None
+        if ws is None or ws.numel() * 8 < nbytes:
+            ws = _ws(nbytes, out.device)
+            if self.cache is not None:
+                self.cache[key] = ws
         call("fbn_gemm_slabs", ptr(A), ptr(B), M, N, K, lda, ldb, int(transA), int(transB), ptr(ws), nbytes,
              ptr(A2), lda2, kseg, ptr(B2), ldb2, nseg, ctypes.byref(_nsplit),
              stream if stream is not None else _lib.stream_handle())
@@ -187,6 +197,7 @@ class DeferredSums:
             sarr = (_SlabJob * max(1, len(sc)))(*[_SlabJob(*j) for j in sc])
             call("fbn_sum_jobs2", ctypes.addressof(arr), len(jc), ctypes.addressof(sarr), len(sc), stream)
         self.jobs, self.slabs, self.keep = [], [], []
+        self.used = set()
 
 
 def colsum(X, B, C, ldx, out, beta=0.0, stream=None):
@@ -225,12 +236,12 @@ def bn_train_stats(h, B, C, mean, invstd, run_mean, run_var, ntot, coll: Collect
     """Training-mode BatchNorm statistics over the GLOBAL batch (SyncBN when coll.world > 1).
     tiles: per-64-row-tile (sum, M2) partials written by the producing GEMM (no pass over h)."""
     dev = h.device
-    s = torch.empty(C, dtype=torch.float64, device=dev)
-    mean_d = torch.empty(C, dtype=torch.float64, device=dev)
     if tiles is not None and coll.world <= 1:
         call("fbn_bn_tile_finalize", ptr(tiles), B, C, float(ntot), ptr(mean), ptr(invstd), ptr(run_mean),
              ptr(run_var), BN_MOMENTUM, BN_EPS, 1 if run_mean is not None else 0, stream)
         return
+    s = torch.empty(C, dtype=torch.float64, device=dev)
+    mean_d = torch.empty(C, dtype=torch.float64, device=dev)
     if tiles is not None:
         # SyncBN: raw f64 moments, ONE all-reduce per layer
         mom = torch.empty(2 * C, dtype=torch.float64, device=dev)
@@ -259,12 +270,18 @@ def bn_backward(G, gvec, w, hact, scale, hpre, mean, invstd, gamma, B, C, ntot, 
     G needs only its sign) and dpre may be None when dpre16 is given (bf16 mode: nothing reads the
     f32 gradient, the bias gradient comes from the apply's column partials)."""
     dev = hpre.device
-    ws = _ws(_lib.lib().fbn_bn_workspace_size(B, C), dev)
+    cache = sums.cache if sums is not None and sums.cache is not None else {}
+    nws = _lib.lib().fbn_bn_workspace_size(B, C)
+    ws = cache.get(f"bn_ws_{C}") if nws > 0 else None
+    if nws > 0 and (ws is None or ws.numel() * 8 < nws):
+        ws = cache[f"bn_ws_{C}"] = _ws(nws, dev)
     if coll.world <= 1:
         part = None
         if bias_grad is not None:
             nch = _lib.lib().fbn_bn_bwd_chunks(B, C)
-            part = torch.empty((nch, C), dtype=torch.float32, device=dev)
+            part = cache.get(f"bn_part_{C}")
+            if part is None or tuple(part.shape) != (nch, C):
+                part = cache[f"bn_part_{C}"] = torch.empty((nch, C), dtype=torch.float32, device=dev)
             sums.add(part, nch, C, bias_grad)
         call("fbn_bn_bwd_fused", ptr(G), ptr(gvec), ptr(w), ptr(hact), ptr(hact16), float(scale), ptr(hpre),
              ptr(mean), ptr(invstd), ptr(gamma), B, C, float(ntot), ptr(dpre), ptr(dpre16), ptr(dgamma), ptr(dbeta),
@@ -558,16 +575,26 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     w16 = a.get("w16")
     bf16_ = dict(dtype=torch.bfloat16, device=dev)
     lean = bf and coll.world <= 1             # f32 copies of dh2pre / dh1pre have no reader
-    dh2pre = None if lean else torch.empty((B, H2), **f32)
-    dh2pre16 = torch.empty((B, H2), **bf16_) if bf else None
-    sums = DeferredSums()
+
+    def tmp(name, shape, dtype=torch.float32):
+        # the backward's scratch, kept in the activation dict: the native trainer's dict lives
+        # across steps, so a step allocates nothing (host time); stream order keeps reuse safe
+        t = a.get("bwd_" + name)
+        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
+            t = torch.empty(shape, dtype=dtype, device=dev)
+            a["bwd_" + name] = t
+        return t
+
+    dh2pre = None if lean else tmp("dh2pre", (B, H2))
+    dh2pre16 = tmp("dh2pre16", (B, H2), torch.bfloat16) if bf else None
+    sums = DeferredSums(a)
     wg = _SideWork(side, dev)
     bn_backward(None, gout, p["mlp.8.weight"], a["h2"], scale, a["h2pre"], a["mean2"], a["inv2"],
                 p["mlp.5.weight"], B, H2, ntot, dh2pre, g["mlp.5.weight"], g["mlp.5.bias"], g["mlp.8.weight"],
                 coll, st, dpre16=dh2pre16, bias_grad=g["mlp.4.bias"], sums=sums,
                 part_pre=a.get("bn2_bwd_part") if (gout is a.get("gout")) else None)
     sums.add(gout, B, 1, g["mlp.8.bias"])
-    dh1 = torch.empty((B, H1), **f32)
+    dh1 = tmp("dh1", (B, H1))
     part1 = None
     lean_h1 = a.get("lean_h1", False)
     if bf:
@@ -579,7 +606,7 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
                 and _lib.lib().fbn_gemm_bn_bwd_part_supported(B, H1, H2, H2, H2, 0, 1)):
             # dh1 = dh2 Wb and, from its accumulators, the BN1 backward's column partials (no pass
             # over dh1 to compute them)
-            part1 = torch.empty(_lib.lib().fbn_bn_bwd_chunks(B, H1) * 3 * H1, dtype=torch.float64, device=dev)
+            part1 = tmp("part1", (_lib.lib().fbn_bn_bwd_chunks(B, H1) * 3 * H1,), torch.float64)
             call("fbn_gemm_bn_bwd_part", ptr(dh2pre16), ptr(w16["WbT"]), ptr(dh1), B, H1, H2, H2, H2, H1, 0, 1,
                  ptr(a["h1_16"]), ptr(a["h1pre"]), ptr(a["mean1"]), float(scale), ptr(part1), st)
         else:
@@ -587,8 +614,8 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     else:
         wg.run(lambda s: gemm(dh2pre, a["h1"], g["mlp.4.weight"], H2, H1, B, H2, H1, H1, True, False, stream=s))
         gemm(dh2pre, p["mlp.4.weight"], dh1, B, H1, H2, H2, H1, H1, False, False, stream=st)
-    dh1pre = None if lean else torch.empty((B, H1), **f32)
-    dh1pre16 = torch.empty((B, H1), **bf16_) if bf else None
+    dh1pre = None if lean else tmp("dh1pre", (B, H1))
+    dh1pre16 = tmp("dh1pre16", (B, H1), torch.bfloat16) if bf else None
     bn_backward(dh1, None, None, None if lean_h1 else a["h1"], scale, a["h1pre"], a["mean1"], a["inv1"],
                 p["mlp.1.weight"], B, H1, ntot, dh1pre, g["mlp.1.weight"], g["mlp.1.bias"], None, coll, st,
                 dpre16=dh1pre16, bias_grad=g["mlp.0.bias"], sums=sums, hact16=a["h1_16"] if lean_h1 else None,
@@ -607,7 +634,7 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
                               rC=wa_remap(d), stream=s))
     if a.get("fused_bilinear"):
         # dc in bf16: its one reader, the fused bilinear backward, widens it on load
-        dc = torch.empty((B, KC), **bf16_)
+        dc = tmp("dc16", (B, KC), torch.bfloat16)
         call("fbn_gemm_bf16out", ptr(dh1pre16), ptr(w16["WaT"]), ptr(dc), B, KC, H1, H1, H1, KC, 0, 1, st)
     elif bf:
         dc = torch.empty((B, KC), **f32)
@@ -616,9 +643,9 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
         dc = torch.empty((B, KC), **f32)
         gemm(dh1pre, p["mlp.0.weight"], dc, B, KC, H1, H1, 21 * d, KC, False, False, rB=wa_remap(d), stream=st)
     # bilinear backward
-    dV = torch.empty((B, 5, d), **f32)
+    dV = tmp("dV", (B, 5, d))
     v16 = bf and not cfg.bilinear_each
-    dU16 = torch.empty((B, 5, d), dtype=torch.bfloat16, device=dev) if v16 else None
+    dU16 = tmp("dU16", (B, 5, d), torch.bfloat16) if v16 else None
     if a.get("fused_bilinear"):
         # one launch: dU and dV = dc_V + pair terms + dU W^T (U recomputed on the MFMA)
         call("fbn_bilinear_bwd", ptr(dc), KC, int(dc.dtype == torch.bfloat16), ptr(a["Vc16"]), ptr(w16["WT"]),
@@ -650,9 +677,9 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     ncate = p["cate_emb.weight"].shape[0]
     P = _lib.lib().fbn_fields_bwd_partials_size(d, R, ncate)
     nblk = _lib.lib().fbn_fields_bwd_grid(B, d)
-    partials = torch.empty((nblk, P), **f32)
-    dhmm = torch.empty((B, d), **f32)
-    dhmm16 = torch.empty((B, d), dtype=torch.bfloat16, device=dev) if bf else None
+    partials = tmp("partials", (nblk, P))
+    dhmm = tmp("dhmm", (B, d))
+    dhmm16 = tmp("dhmm16", (B, d), torch.bfloat16) if bf else None
     seq = batch.get("item_seq", None)
     Lr = 0 if seq is None else L
     V = p["item_emb.weight"].shape[0] if pos is None else 0

@@ -102,7 +102,7 @@ def test_gemm_slabs_deferred_sum(hip_device, M, N, K, remap):
     sums.add(part, 300, 24, out1, ld=40)
     sums.add(part[:, 24:], 300, 16, out2, scale=0.5, ld=40)
     out3 = torch.ones(40, device=hip_device)
-    sums.add(part, 300, 40, out3, beta=2.0, ld=40)           # a wide job (64 columns per block)
+    sums.add(part, 300, 40, out3, beta=2.0, ld=40)           # a wide job (16 columns x 16 row streams per block)
     sums.flush(ops._lib.stream_handle(hip_device))
     torch.cuda.synchronize()
     ref = A.double().T @ Bm.double()

@@ -1,4 +1,4 @@
-"""GPU-bound time of an eager C3 step: the host enqueues 20 steps while the GPU is held by a
+"""GPU-bound time of an eager C3 (or EG_D/EG_V/EG_B) step: the host enqueues 20 steps while the GPU is held by a
 sleep kernel, so the steps then run back to back whatever the host's enqueue rate; compared
 with the same 20 steps enqueued live (host and GPU racing) and with their host enqueue time."""
 import os
@@ -12,8 +12,10 @@ from ctr_recommendation_amd.data import make_device_batches
 from ctr_recommendation_amd.trainer import FiBiNETTrainer
 
 dev = torch.device("cuda", 0)
-V, B, K = 1_250_000, 8192, 20
-tr = FiBiNETTrainer({"embedding_dim": 128, "vocab_size": V, "compute_dtype": "bf16"}, total_steps=2000,
+# C3 by default; EG_D / EG_V / EG_B for another config (C2: 16 / 1000000 / 4096)
+d, V, B, K = (int(os.environ.get("EG_D", 128)), int(os.environ.get("EG_V", 1_250_000)),
+              int(os.environ.get("EG_B", 8192)), 20)
+tr = FiBiNETTrainer({"embedding_dim": d, "vocab_size": V, "compute_dtype": "bf16"}, total_steps=2000,
                     batch_size=B, device=dev)
 nb = 160
 batches = make_device_batches(nb, B, V, 20, dev, seed=2025)
