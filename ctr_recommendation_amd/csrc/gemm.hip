@@ -856,7 +856,13 @@ static GemmPlan plan_dma16(int M, int N, int K) {
   GemmPlan p = (M >= 512 && N >= 512) ? GemmPlan{128, 128, 1, 8} : GemmPlan{64, 64, 1};
   const long long tiles = (long long)fbn_cdiv(M, p.bm) * fbn_cdiv(N, p.bn);
   const long long target = p.bm == 128 ? 512 : 256;
-  while (p.split < 64 && tiles * p.split * 2 <= target && K / (p.split * 2) >= 256) p.split *= 2;
+  // a tiny output (the d x d / d x 128 weight gradients: 4 tiles) is latency-bound, not feed-bound:
+  // split K down to 2 K-steps per workgroup and keep a 4-deep ring (FBN_GEMM_TINY=0: the old rule)
+  const char* te = getenv("FBN_GEMM_TINY");
+  const bool tiny = tiles <= 16 && !(te && atoi(te) == 0);
+  const int min_k = tiny ? 128 : 256;
+  while (p.split < 64 && tiles * p.split * 2 <= target && K / (p.split * 2) >= min_k) p.split *= 2;
+  if (tiny) p.stages = 4;
   return p;
 }
 

@@ -1426,9 +1426,13 @@ __global__ void __launch_bounds__(256) adam_prefetch2_kernel(float* __restrict__
   if constexpr (D < 128)   // the narrow engine's LDS constants (wave-wide rows read the table directly)
     for (int s = threadIdx.x; s <= T - w0; s += blockDim.x) win[s] = consts4(table[w0 + s]);
   const int lane = threadIdx.x & 63;
-  // epw entries per wave (lanes past epw hold none): fewer rows per wave, more waves per SIMD
-  // replaying side by side -- the engine's row loads are latency-bound, not its arithmetic
-  const long long i = lane < epw ? (((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * epw + lane : n;
+  if constexpr (D < 128) __syncthreads();   // the LDS window (no barrier after this point)
+  // epw entries per wave (lanes past epw hold none); a capped grid (FBN_PF_WAVES) walks the
+  // entry chunks wave-strided, so the side stream holds few wave slots per SIMD at a time
+  const long long nchunk = ((long long)n + epw - 1) / epw;
+  const long long wstride = ((long long)gridDim.x * blockDim.x) >> 6;
+  for (long long ch = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6; ch < nchunk; ch += wstride) {
+  const long long i = lane < epw ? ch * epw + lane : n;
   int r = 0, key = 0x7fffffff, pe = -1;
   if (i < n) {
     const long long b = i / (cs.L + 1), tt = i - b * (cs.L + 1);
@@ -1448,10 +1452,10 @@ __global__ void __launch_bounds__(256) adam_prefetch2_kernel(float* __restrict__
       }
     }
   }
-  if constexpr (D < 128) __syncthreads();   // the LDS window (no barrier after this point)
   const int cnt = __popcll(__ballot(key != 0x7fffffff));
-  if (cnt == 0) return;
+  if (cnt == 0) continue;
   replay_sorted<D, DW>(r, key, pe, cnt, T, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
+  }
 }
 
 // Single GPU, D >= 128: the step's row claims + the claimed rows' catch-up (fbn_adam_claim_catchup)
@@ -1546,7 +1550,12 @@ __global__ void __launch_bounds__(256) adam_window2_kernel(float* __restrict__ p
   const long long roll0 = (long long)(t % F) * chunk;
   const long long nroll = roll0 < nrows ? min(chunk, nrows - roll0) : 0;
   const int lane = threadIdx.x & 63;
-  const long long j = ((((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * rpw) + lane;
+  if constexpr (D < 128) __syncthreads();   // the LDS window (no barrier after this point)
+  // rpw rows per wave; a capped grid (FBN_WIN_WAVES) walks the row groups wave-strided
+  const long long ngrp = (nroll + rpw - 1) / rpw;
+  const long long wstride = ((long long)gridDim.x * blockDim.x) >> 6;
+  for (long long gq = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6; gq < ngrp; gq += wstride) {
+  const long long j = gq * rpw + lane;
   int r = 0, key = 0x7fffffff, pe = -1;
   if (lane < rpw && j < nroll) {
     const long long rr = roll0 + j;
@@ -1562,10 +1571,10 @@ __global__ void __launch_bounds__(256) adam_window2_kernel(float* __restrict__ p
       }
     }
   }
-  if constexpr (D < 128) __syncthreads();   // the LDS window (no barrier after this point)
   const int cnt = __popcll(__ballot(key != 0x7fffffff));
-  if (cnt == 0) return;
+  if (cnt == 0) continue;
   replay_sorted<D, DW>(r, key, pe, cnt, t, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
+  }
 }
 
 // every row up to `step` (checkpoint / evaluation)
@@ -2143,7 +2152,9 @@ extern "C" int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, i
     const char* we = getenv("FBN_WIN_RPW");
     const int wr = we ? std::max(1, std::min(64, atoi(we))) : 8;
     const int rpw = D >= 128 ? wr : FBN_WIN_ROWS;
-    const long long waves = (chunk + rpw - 1) / rpw;
+    long long waves = (chunk + rpw - 1) / rpw;
+    const char* wc = getenv("FBN_WIN_WAVES");   // cap on the grid's waves (A/B knob; 0 = none)
+    if (wc && atoll(wc) > 0) waves = std::min(waves, atoll(wc));
     const dim3 g2((unsigned)((waves + 3) / 4));
     if (decoupled) {
       FBN_DISPATCH_D_B(adam_window2_kernel, true, D, g2, p, m, v, map, nrows, F, chunk, last,
@@ -2206,7 +2217,11 @@ extern "C" int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B,
     FBN_CHECK_LAUNCH();
     const char* ee = getenv("FBN_PF_EPW");   // A/B knob, read per call (tools/ab_step.py flips it in-process)
     const int epw = ee ? std::max(1, std::min(64, atoi(ee))) : 64;
-    const dim3 g3((unsigned)(((n + epw - 1) / epw + 3) / 4));   // 4 waves per block
+    // FBN_PF_WAVES: cap on the grid's waves (0 = one wave per entry chunk); A/B knob
+    const char* wc = getenv("FBN_PF_WAVES");
+    long long waves = (n + epw - 1) / epw;
+    if (wc && atoll(wc) > 0) waves = std::min(waves, atoll(wc));
+    const dim3 g3((unsigned)((waves + 3) / 4));   // 4 waves per block
     if (decoupled) {
       FBN_DISPATCH_D_B(adam_prefetch2_kernel, true, D, g3, p, m, v, cs, (int)n, last, (const AdamConsts*)consts_table,
                        step, wd, beta2, omb2, eps, ps, epw);

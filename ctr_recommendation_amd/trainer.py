@@ -54,6 +54,10 @@ _SIDE_AFTER_MMPROJ = os.environ.get("FBN_SIDE_AFTER_MMPROJ", "0") == "1"
 #   FBN_SIDE_SERIAL=1    the rolling window + next-batch prefetch on the main stream, in sequence
 _CLAIM_ON_SIDE = os.environ.get("FBN_CLAIM_ON_SIDE", "0") == "1"
 _SIDE_SERIAL = os.environ.get("FBN_SIDE_SERIAL", "0") == "1"
+# order of the side stream's two table-Adam passes (A/B knob): "wp" window then next-batch
+# prefetch (default), "pw" the prefetch first, "p_w" the prefetch at the fork and the window only
+# once the backward starts (the side stream waits for the forward)
+_SIDE_ORDER = os.environ.get("FBN_SIDE_ORDER", "wp")
 _FIXUP_ON_SIDE = os.environ.get("FBN_FIXUP_ON_SIDE", "0") == "1"
 # ... or after the gather (fields_fwd then runs with the chip to itself; A/B knob)
 _SIDE_AFTER_GATHER = os.environ.get("FBN_SIDE_AFTER_GATHER", "0") == "1"
@@ -365,6 +369,7 @@ class FiBiNETTrainer:
         # N > 1: forward + backward between the row exchanges replayed as hipGraph segments split at
         # the SyncBN all-reduces (_Segments), after two eager steps; FBN_SHARD_GRAPH=0 keeps it eager
         self.shard_graph = self.sharded and os.environ.get("FBN_SHARD_GRAPH", "1") != "0"
+        self._late_side = None
         self._sg = None
         self._sg_eager = 0
 
@@ -461,11 +466,27 @@ class FiBiNETTrainer:
             sst = self.side if not _SIDE_SERIAL else main      # FBN_SIDE_SERIAL: in sequence on main
             if wait_main and not _SIDE_SERIAL:
                 self.side.wait_stream(main)
-            ev = _events(probe, "adam_window", sst)
-            call("fbn_adam_catchup", ptr(self.E), ptr(self.Em), ptr(self.Ev), self.rows_local, d, None, 0,
-                 ptr(self.map), self.lazy_window, 2, ptr(self.last), ptr(self.sched), ptr(self.step_dev), self.wd_g,
-                 self.beta2, self.eps, *self._pend_args(), int(self.decoupled), sst.cuda_stream)
-            _events_end(ev, sst)
+
+            def window():
+                ev = _events(probe, "adam_window", sst)
+                call("fbn_adam_catchup", ptr(self.E), ptr(self.Em), ptr(self.Ev), self.rows_local, d, None, 0,
+                     ptr(self.map), self.lazy_window, 2, ptr(self.last), ptr(self.sched), ptr(self.step_dev),
+                     self.wd_g, self.beta2, self.eps, *self._pend_args(), int(self.decoupled), sst.cuda_stream)
+                _events_end(ev, sst)
+
+            order = _SIDE_ORDER if not _SIDE_SERIAL else "wp"
+            if order == "wp":
+                window()
+            prefetch_pass(sst)
+            if order == "pw":
+                window()
+            elif order == "p_w":
+                def late_window():
+                    self.side.wait_stream(main)      # the forward is done: the window beside the backward
+                    window()
+                self._late_side = late_window
+
+        def prefetch_pass(sst):
             nb = next_batch
             if (self.xchg is None and nb is not None and self.prefetch_rows and nb["item_id"].dtype == torch.int64
                     and nb["item_id"].device == self.device):
@@ -578,6 +599,9 @@ class FiBiNETTrainer:
                             probe=probe, count_batches=False,     # num_batches_tracked: fbn_step_end
                             after_gather=start_untouched_adam if self.table_adam == "eager" else None,
                             hooks=side_hooks)
+            if self._late_side is not None:
+                self._late_side()
+                self._late_side = None
             sendbuf = self.xchg.make_sendbuf() if self.xchg is not None else None
             bhooks = {"after_fields_bwd": self._grad_xchg_start} if self._early_grad_xchg() else None
             if fixup_side:
