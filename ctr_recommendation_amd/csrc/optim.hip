@@ -1229,17 +1229,61 @@ __device__ __forceinline__ void adam_tabk(typename FVec<N>::T& pp, typename FVec
 }
 __device__ __forceinline__ f32x4 consts4(const AdamConsts& k) { return (f32x4){k.w1, k.nss, k.rbc2s, k.dmul}; }
 
+// One group of the replay engine: G wave-wide rows (cur, rows cr, replay starts ck, deferred
+// vectors cp; slots past cnt carry row 0 and no steps) brought to T, then stored.
+template <int D, bool DW, int G>
+__device__ __forceinline__ void replay_group(WideRow<D> (&cur)[G], const int (&cr)[G], const int (&ck)[G],
+                                             const int (&cp)[G], int j0, int cnt, int T, float* __restrict__ p,
+                                             float* __restrict__ m, float* __restrict__ v,
+                                             const AdamConsts* __restrict__ table, float wd, float b2, float omb2,
+                                             float eps, int lane) {
+  typedef typename WideRow<D>::V V;
+  constexpr int N = WideRow<D>::N;
+  const V zero = {};
+  // A row spans the whole wave, so its step -- and the step's schedule constants -- are
+  // wave-uniform: scalar loads from the table (no LDS staging, no vector registers for them).
+  // deferred-gradient steps (step ck - 1 with its stored vector and clip coefficient)
+#pragma unroll
+  for (int x = 0; x < G; ++x)
+    if (cp[x] >= 0) adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, cur[x].g * cur[x].c, wd, b2, omb2, eps,
+                                     consts4(table[ck[x] - 1]));
+  // END-aligned: every row replays up to T, so from the group's latest start on, all G rows
+  // are at the SAME step and share one set of constants; before it, the earlier-starting rows
+  // catch up to that start one by one (short after the sort)
+  int smax = ck[0];
+#pragma unroll
+  for (int x = 1; x < G; ++x)
+    if (j0 + x < cnt) smax = max(smax, ck[x]);
+#pragma unroll
+  for (int x = 0; x < G; ++x)
+    if (j0 + x < cnt)
+      for (int s = ck[x]; s < smax; ++s)
+        adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, zero, wd, b2, omb2, eps, consts4(table[s]));
+  if (smax < T) {
+    f32x4 kc = consts4(table[smax]);
+    for (int s = smax; s < T; ++s) {
+      const f32x4 kn = consts4(table[s + 1]);   // a step ahead (table row T exists)
+#pragma unroll
+      for (int x = 0; x < G; ++x) adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, zero, wd, b2, omb2, eps, kc);
+      kc = kn;
+    }
+  }
+#pragma unroll
+  for (int x = 0; x < G; ++x)
+    if (j0 + x < cnt) wide_store<D>(cur[x], p, m, v, cr[x], lane);
+}
+
 // The replay engine of the two-pass prefetch and the window pass: a wave's rows (one per lane:
 // row r, first zero-gradient step key -- INT_MAX = none --, deferred vector pe), sorted by key,
-// brought to T steps four at a time.  win: LDS constants of steps [w0, T] (w0 = max(0, T - FBN_PF_WIN)).
-template <int D, bool DW>
+// brought to T steps G at a time, the next group's loads in flight while one replays.
+// G = 4 by default; G = 2 holds half the rows' registers (a smaller footprint beside the main
+// stream's kernels, fewer independent update chains per lane).
+template <int D, bool DW, int G = 4>
 __device__ __forceinline__ void replay4_sorted(int r, int key, int pe, int cnt, int T, int w0,
                                                const f32x4* __restrict__ win, float* __restrict__ p,
                                                float* __restrict__ m, float* __restrict__ v,
                                                const AdamConsts* __restrict__ table, float wd, float b2,
                                                float omb2, float eps, const PendSrc& ps, int lane) {
-  typedef typename WideRow<D>::V V;
-  constexpr int N = WideRow<D>::N;
   // ascending replay start (descending replay length); rows past cnt last
 #pragma unroll
   for (int kk = 2; kk <= 64; kk <<= 1)
@@ -1261,63 +1305,23 @@ __device__ __forceinline__ void replay4_sorted(int r, int key, int pe, int cnt, 
     pp = __builtin_amdgcn_readlane(pe, sl);
     if (idx >= cnt) { rr = 0; kk = T; pp = -1; }
   };
-  auto load = [&](WideRow<D>& x, int rr, int kk, int pp) {
-    wide_load<D>(x, p, m, v, rr, pp >= 0 ? kk - 1 : kk, pp, ps, lane);
+  struct Grp {
+    WideRow<D> w[G];
+    int r[G], k[G], p[G];
   };
-  WideRow<D> cur[4];
-  int cr[4], ck[4], cp[4];
+  auto fill = [&](Grp& g, int j) {   // past the last group: row 0, discarded
 #pragma unroll
-  for (int x = 0; x < 4; ++x) {
-    get(x, cr[x], ck[x], cp[x]);
-    load(cur[x], cr[x], ck[x], cp[x]);
-  }
-  const V zero = {};
-  for (int j0 = 0; j0 < cnt; j0 += 4) {
-    WideRow<D> nxt[4];
-    int nr[4], nk[4], np[4];
-#pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      get(j0 + 4 + x, nr[x], nk[x], np[x]);
-      load(nxt[x], nr[x], nk[x], np[x]);   // past the last group: row 0, discarded
+    for (int x = 0; x < G; ++x) {
+      get(j + x, g.r[x], g.k[x], g.p[x]);
+      wide_load<D>(g.w[x], p, m, v, g.r[x], g.p[x] >= 0 ? g.k[x] - 1 : g.k[x], g.p[x], ps, lane);
     }
-    // A row spans the whole wave, so its step -- and the step's schedule constants -- are
-    // wave-uniform: scalar loads from the table (no LDS staging, no vector registers for them).
-    // deferred-gradient steps (step ck - 1 with its stored vector and clip coefficient)
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-      if (cp[x] >= 0) adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, cur[x].g * cur[x].c, wd, b2, omb2, eps,
-                                       consts4(table[ck[x] - 1]));
-    // END-aligned: every row replays up to T, so from the group's latest start on, all four rows
-    // are at the SAME step and share one set of constants; before it, the earlier-starting rows
-    // catch up to that start one by one (short after the sort)
-    int smax = ck[0];
-#pragma unroll
-    for (int x = 1; x < 4; ++x)
-      if (j0 + x < cnt) smax = max(smax, ck[x]);
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-      if (j0 + x < cnt)
-        for (int s = ck[x]; s < smax; ++s)
-          adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, zero, wd, b2, omb2, eps, consts4(table[s]));
-    if (smax < T) {
-      f32x4 kc = consts4(table[smax]);
-      for (int s = smax; s < T; ++s) {
-        const f32x4 kn = consts4(table[s + 1]);   // a step ahead (table row T exists)
-#pragma unroll
-        for (int x = 0; x < 4; ++x) adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, zero, wd, b2, omb2, eps, kc);
-        kc = kn;
-      }
-    }
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-      if (j0 + x < cnt) wide_store<D>(cur[x], p, m, v, cr[x], lane);
-#pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      cur[x] = nxt[x];
-      cr[x] = nr[x];
-      ck[x] = nk[x];
-      cp[x] = np[x];
-    }
+  };
+  Grp a, b;
+  fill(a, 0);
+  for (int j0 = 0; j0 < cnt; j0 += G) {
+    fill(b, j0 + G);
+    replay_group<D, DW, G>(a.w, a.r, a.k, a.p, j0, cnt, T, p, m, v, table, wd, b2, omb2, eps, lane);
+    a = b;
   }
 }
 
@@ -1403,17 +1407,17 @@ __device__ __forceinline__ void replay_narrow_sorted(int r, int key, int pe, int
   }
 }
 
-template <int D, bool DW>
+template <int D, bool DW, int G = 4>
 __device__ __forceinline__ void replay_sorted(int r, int key, int pe, int cnt, int T, int w0,
                                               const f32x4* __restrict__ win, float* __restrict__ p,
                                               float* __restrict__ m, float* __restrict__ v,
                                               const AdamConsts* __restrict__ table, float wd, float b2, float omb2,
                                               float eps, const PendSrc& ps, int lane) {
-  if constexpr (D >= 128) replay4_sorted<D, DW>(r, key, pe, cnt, T, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
+  if constexpr (D >= 128) replay4_sorted<D, DW, G>(r, key, pe, cnt, T, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
   else replay_narrow_sorted<D, DW>(r, key, pe, cnt, T, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
 }
 
-template <int D, bool DW>
+template <int D, bool DW, int G = 4>
 __global__ void __launch_bounds__(256) adam_prefetch2_kernel(float* __restrict__ p, float* __restrict__ m,
                                                              float* __restrict__ v, ClaimSrc cs, int n,
                                                              int* __restrict__ last,
@@ -1454,7 +1458,7 @@ __global__ void __launch_bounds__(256) adam_prefetch2_kernel(float* __restrict__
   }
   const int cnt = __popcll(__ballot(key != 0x7fffffff));
   if (cnt == 0) continue;
-  replay_sorted<D, DW>(r, key, pe, cnt, T, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
+  replay_sorted<D, DW, G>(r, key, pe, cnt, T, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
   }
 }
 
@@ -1535,7 +1539,7 @@ __global__ void __launch_bounds__(256) adam_claim2_kernel(float* __restrict__ p,
 // steps each) spreads over thousands of waves instead of one wave per SIMD; claimed rows are left
 // to their claiming entry, as in adam_catchup_kernel.
 #define FBN_WIN_ROWS 16
-template <int D, bool DW>
+template <int D, bool DW, int G = 4>
 __global__ void __launch_bounds__(256) adam_window2_kernel(float* __restrict__ p, float* __restrict__ m,
                                                            float* __restrict__ v, const int* __restrict__ map,
                                                            long long nrows, int F, long long chunk,
@@ -1573,7 +1577,7 @@ __global__ void __launch_bounds__(256) adam_window2_kernel(float* __restrict__ p
   }
   const int cnt = __popcll(__ballot(key != 0x7fffffff));
   if (cnt == 0) continue;
-  replay_sorted<D, DW>(r, key, pe, cnt, t, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
+  replay_sorted<D, DW, G>(r, key, pe, cnt, t, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
   }
 }
 
@@ -2136,7 +2140,7 @@ extern "C" int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, i
   if (items <= 0) return FBN_OK;
   // the window-only pass runs beside the step: a few workgroups per CU leave the CUs' wave
   // slots to the main stream while its four-chain replay keeps the VALU busy
-  static const int wcap = getenv("FBN_WINDOW_BLOCKS") ? atoi(getenv("FBN_WINDOW_BLOCKS")) : 256;   // tools/window_sweep.sh
+  static const int wcap = getenv("FBN_WINDOW_BLOCKS") ? atoi(getenv("FBN_WINDOW_BLOCKS")) : 256;
   const long long cap = parts == 2 ? wcap : 8192;
   if (pend && (!ring || !coef_hist || ring_n <= F)) {
     fbn_set_error("fbn_adam_catchup: deferred gradients need ring, coef_hist and ring_n > F");
@@ -2156,6 +2160,24 @@ extern "C" int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, i
     const char* wc = getenv("FBN_WIN_WAVES");   // cap on the grid's waves (A/B knob; 0 = none)
     if (wc && atoll(wc) > 0) waves = std::min(waves, atoll(wc));
     const dim3 g2((unsigned)((waves + 3) / 4));
+    const char* ge = getenv("FBN_WIN_G");   // rows per replay group (4, or 2; A/B knob)
+    if (D >= 128 && ge && atoi(ge) == 2) {
+#define FBN_WIN2_G2(DW_)                                                                                       \
+  if (D == 128)                                                                                                \
+    hipLaunchKernelGGL((adam_window2_kernel<128, DW_, 2>), g2, dim3(256), 0, st, p, m, v, map, nrows, F, chunk, \
+                       last, (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, rpw);             \
+  else                                                                                                         \
+    hipLaunchKernelGGL((adam_window2_kernel<256, DW_, 2>), g2, dim3(256), 0, st, p, m, v, map, nrows, F, chunk, \
+                       last, (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, rpw);
+      if (decoupled) {
+        FBN_WIN2_G2(true)
+      } else {
+        FBN_WIN2_G2(false)
+      }
+#undef FBN_WIN2_G2
+      FBN_CHECK_LAUNCH();
+      return FBN_OK;
+    }
     if (decoupled) {
       FBN_DISPATCH_D_B(adam_window2_kernel, true, D, g2, p, m, v, map, nrows, F, chunk, last,
                        (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, rpw);
@@ -2206,7 +2228,7 @@ extern "C" int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B,
   const float omb2 = (float)(1.0 - (double)beta2);
   const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
   const ClaimSrc cs{item, L > 0 ? seq : nullptr, L, V, const_cast<int*>(map), nullptr, nullptr, nullptr, preclaim};
-  static const int pcap = getenv("FBN_PREFETCH_BLOCKS") ? atoi(getenv("FBN_PREFETCH_BLOCKS")) : 256;   // tools/ab_prefetch.sh
+  static const int pcap = getenv("FBN_PREFETCH_BLOCKS") ? atoi(getenv("FBN_PREFETCH_BLOCKS")) : 256;
   const dim3 grid((unsigned)std::min<long long>(pcap, (n + 63) / 64));
   hipStream_t st = (hipStream_t)stream;
   // with pre-claims: the two-pass form (FBN_PREFETCH_ONEPASS=1 keeps the one-pass kernel, A/B)
@@ -2222,6 +2244,25 @@ extern "C" int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B,
     long long waves = (n + epw - 1) / epw;
     if (wc && atoll(wc) > 0) waves = std::min(waves, atoll(wc));
     const dim3 g3((unsigned)((waves + 3) / 4));   // 4 waves per block
+    // FBN_PF_G: rows per replay group (4, or 2 for half the register footprint; A/B knob)
+    const char* ge = getenv("FBN_PF_G");
+    if (D >= 128 && ge && atoi(ge) == 2) {
+#define FBN_PF2_G2(DW_)                                                                                        \
+  if (D == 128)                                                                                                \
+    hipLaunchKernelGGL((adam_prefetch2_kernel<128, DW_, 2>), g3, dim3(256), 0, st, p, m, v, cs, (int)n, last, \
+                       (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, epw);                  \
+  else                                                                                                         \
+    hipLaunchKernelGGL((adam_prefetch2_kernel<256, DW_, 2>), g3, dim3(256), 0, st, p, m, v, cs, (int)n, last, \
+                       (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, epw);
+      if (decoupled) {
+        FBN_PF2_G2(true)
+      } else {
+        FBN_PF2_G2(false)
+      }
+#undef FBN_PF2_G2
+      FBN_CHECK_LAUNCH();
+      return FBN_OK;
+    }
     if (decoupled) {
       FBN_DISPATCH_D_B(adam_prefetch2_kernel, true, D, g3, p, m, v, cs, (int)n, last, (const AdamConsts*)consts_table,
                        step, wd, beta2, omb2, eps, ps, epw);

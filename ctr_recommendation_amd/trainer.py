@@ -52,8 +52,13 @@ _SIDE_AFTER_MMPROJ = os.environ.get("FBN_SIDE_AFTER_MMPROJ", "0") == "1"
 #   FBN_FIXUP_ON_SIDE=1  the duplicate-gradient fold on the side stream after the fields backward
 #                        (+2-3 us/step)
 #   FBN_SIDE_SERIAL=1    the rolling window + next-batch prefetch on the main stream, in sequence
+#                        (0.5128 vs 0.4629 ms/step at C3: the overlap is worth 50 us there)
+# FBN_SIDE_SERIAL defaults to "auto": in sequence on the main stream below d = 128, where the side
+# work is small and the cross-queue edges cost more than the overlap saves (C2, graph-replayed:
+# 0.2833-0.2844 vs 0.2934-0.2952 ms/step; eager 0.30 vs 0.45-0.50, the host's event waits gone;
+# profiles/r03s2_side_serial_ab.txt), on the side stream from d = 128 on
 _CLAIM_ON_SIDE = os.environ.get("FBN_CLAIM_ON_SIDE", "0") == "1"
-_SIDE_SERIAL = os.environ.get("FBN_SIDE_SERIAL", "0") == "1"
+_SIDE_SERIAL = os.environ.get("FBN_SIDE_SERIAL", "auto")
 # order of the side stream's two table-Adam passes (A/B knob): "wp" window then next-batch
 # prefetch (default), "pw" the prefetch first, "p_w" the prefetch at the fork and the window only
 # once the backward starts (the side stream waits for the forward)
@@ -351,6 +356,8 @@ class FiBiNETTrainer:
         if self.table_adam not in ("lazy", "eager", "sparse"):
             raise ValueError(f"table_adam must be 'lazy', 'eager' or 'sparse', not {self.table_adam!r}")
         self.lazy_window = int(lazy_window)
+        # single GPU: the side-stream table-Adam passes in sequence on the main stream (see _SIDE_SERIAL)
+        self.side_serial = _SIDE_SERIAL == "1" or (_SIDE_SERIAL == "auto" and d < 128)
         self.last = self.row_state[:, 2]     # Adam steps applied per table row
         # lazy: deferred table gradients (the step tail's commit) -- pend[r] = the gradient row r
         # received at step last[r], applied at the row's next replay; the last F+1 steps' gradients
@@ -463,8 +470,9 @@ class FiBiNETTrainer:
             side_pass()
 
         def side_pass(wait_main=True):
-            sst = self.side if not _SIDE_SERIAL else main      # FBN_SIDE_SERIAL: in sequence on main
-            if wait_main and not _SIDE_SERIAL:
+            serial = self.side_serial
+            sst = self.side if not serial else main      # in sequence on main (FBN_SIDE_SERIAL)
+            if wait_main and not serial:
                 self.side.wait_stream(main)
 
             def window():
@@ -474,7 +482,7 @@ class FiBiNETTrainer:
                      self.wd_g, self.beta2, self.eps, *self._pend_args(), int(self.decoupled), sst.cuda_stream)
                 _events_end(ev, sst)
 
-            order = _SIDE_ORDER if not _SIDE_SERIAL else "wp"
+            order = _SIDE_ORDER if not serial else "wp"
             if order == "wp":
                 window()
             prefetch_pass(sst)
