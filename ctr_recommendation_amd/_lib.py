@@ -47,6 +47,8 @@ SIGNATURES = {
     "fbn_sum_jobs2": (I, [P, I, P, I, P]),
     "fbn_gemm_slabs_size": (SZ, [I, I, I]),
     "fbn_gemm_slabs": (I, [P, P, I, I, I, I, I, I, I, P, SZ, P, I, I, P, I, I, P, P]),
+    "fbn_gemm_slabs_split": (I, [I, I, I]),
+    "fbn_gemm_slabs_group": (I, [P, I, P]),
     "fbn_fields_fwd": (I, [P, P, P, P, P, P, P, F, P, I, P, LL, P, P, P, P, P, I, P, P, P, P, I, I, P, P, P, P, P, I, I, I, I,
                            P]),
     "fbn_fields_fwd_hot": (I, [P, P, P, P, P, P, P, F, P, I, P, LL, P, P, P, P, I, P, P, P, P, I, I, P, P, P, P, P,
@@ -89,6 +91,8 @@ SIGNATURES = {
     "fbn_adam_catchup": (I, [P, P, P, LL, I, P, I, P, I, I, P, P, P, F, F, F, P, P, P, LL, I, I, P]),
     "fbn_adam_claim_catchup": (I, [P, P, I, I, LL, P, P, P, P, P, P, P, P, LL, I, I, P, P, P, F, F, F, P, P, P, LL, I,
                                    I, P]),
+    "fbn_adam_claim_catchup_conv": (I, [P, P, I, I, LL, P, P, P, P, P, P, P, P, LL, I, I, P, P, P, F, F, F, P, P, P,
+                                        LL, I, I, P, I, P]),
     "fbn_adam_flush": (I, [P, P, P, LL, I, P, P, P, F, F, F, P, P, P, LL, I, I, P]),
     "fbn_adam_prefetch_rows": (I, [P, I, I, LL, P, P, P, P, I, P, P, P, F, F, F, P, P, P, LL, I, I, P]),
     "fbn_adam_prefetch": (I, [P, P, I, I, LL, P, P, P, P, P, I, P, P, P, F, F, F, P, P, P, LL, I, I, P]),

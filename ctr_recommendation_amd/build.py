@@ -26,7 +26,7 @@ FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-re
 def _compile(src: str) -> str:
     path = os.path.join(CSRC, src)
     obj = os.path.join(BUILD, src + ".o")
-    deps = [path, os.path.join(CSRC, "common.h")]
+    deps = [path] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
         return obj
     cmd = [HIPCC] + FLAGS + ["-c", path, "-o", obj]

@@ -1,0 +1,106 @@
+// bf16 images of fp32 matrices (the GEMM weight operands, the batch's item_emb_d128): the tile
+// body shared by fbn_convert_bf16 (mlp.hip) and the step-head launch that runs it beside the row
+// claims (fbn_adam_claim_catchup_conv, optim.hip).
+#pragma once
+#include "common.h"
+
+struct ConvJob {
+  const float* src;
+  short* dst;
+  int rows, cols, ld, trans, seg, off0, off1;
+};
+struct ConvJobs {
+  ConvJob j[8];
+  int tile0[9];   // first 64x64 output tile of each job (prefix sum)
+};
+// One 64x64 output tile per workgroup, four consecutive outputs per thread (one 8-B bf16x4 store):
+// a plain job reads four source columns at once (16-B load when they are contiguous and aligned:
+// the remap offsets and seg are multiples of 4); a transposed job reads its source tile along the
+// source's contiguous dimension into LDS (coalesced) and writes the output rows from LDS.
+__device__ __forceinline__ void convert_tile(const ConvJobs& jobs, int njobs, int blk) {
+  __shared__ float tile[64][65];
+  int jb = 0;
+  while (jb + 1 < njobs && blk >= jobs.tile0[jb + 1]) ++jb;
+  const ConvJob J = jobs.j[jb];
+  const int t = blk - jobs.tile0[jb];
+  const int tcols = (J.cols + 63) / 64;
+  const int i0 = (t / tcols) * 64, j0 = (t % tcols) * 64;
+  const int tq = threadIdx.x & 15, tr = threadIdx.x >> 4;   // column quad, row of 16
+  if (!J.trans) {
+    const int j = j0 + 4 * tq;
+    if (j >= J.cols) return;
+    const bool full = j + 4 <= J.cols;
+    const int b = j + (j < J.seg ? J.off0 : J.off1);
+    const bool vec = full && !(J.ld & 3) && !(b & 3) && (J.seg == 0x7fffffff || !(J.seg & 3) || j + 4 <= J.seg ||
+                                                         j >= J.seg);
+    f32x4 val[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {   // all loads in flight before the first store
+      const int i = i0 + tr + 16 * k;
+      if (i >= J.rows) { val[k] = (f32x4){0.f, 0.f, 0.f, 0.f}; continue; }
+      if (vec) {
+        val[k] = *reinterpret_cast<const f32x4*>(J.src + (size_t)i * J.ld + b);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int jj = j + e;
+          val[k][e] = jj < J.cols ? J.src[(size_t)i * J.ld + jj + (jj < J.seg ? J.off0 : J.off1)] : 0.f;
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = i0 + tr + 16 * k;
+      if (i >= J.rows) continue;
+      short* d = J.dst + (size_t)i * J.cols + j;
+      if (full && !(J.cols & 3)) {
+        *reinterpret_cast<bf16x4*>(d) = (bf16x4){f2bf(val[k][0]), f2bf(val[k][1]), f2bf(val[k][2]), f2bf(val[k][3])};
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (j + e < J.cols) d[e] = f2bf(val[k][e]);
+      }
+    }
+    return;
+  }
+  // out[i][j] = src[j][rm(i)]: lanes run along i, the source's contiguous dimension
+  {
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const int i = i0 + tx;
+    const int b = i + (i < J.seg ? J.off0 : J.off1);
+#pragma unroll
+    for (int r = ty; r < 64; r += 4) {
+      const int j = j0 + r;
+      tile[r][tx] = (i < J.rows && j < J.cols) ? J.src[(size_t)j * J.ld + b] : 0.f;
+    }
+  }
+  __syncthreads();
+  const int j = j0 + 4 * tq;
+  if (j >= J.cols) return;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int r = tr + 16 * k, i = i0 + r;
+    if (i >= J.rows) continue;
+    short* d = J.dst + (size_t)i * J.cols + j;
+    const bf16x4 v = {f2bf(tile[4 * tq][r]), f2bf(tile[4 * tq + 1][r]), f2bf(tile[4 * tq + 2][r]),
+                      f2bf(tile[4 * tq + 3][r])};
+    if (j + 4 <= J.cols && !(J.cols & 3)) {
+      *reinterpret_cast<bf16x4*>(d) = v;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (j + e < J.cols) d[e] = v[e];
+    }
+  }
+}
+
+
+// host: pack n <= 8 ConvJob records into the kernel argument; returns the 64 x 64 tile count
+static inline int conv_jobs_pack(const void* jobs, int n, ConvJobs& J) {
+  J.tile0[0] = 0;
+  for (int i = 0; i < 8; ++i) {
+    J.j[i] = ((const ConvJob*)jobs)[i < n ? i : 0];
+    J.tile0[i + 1] = J.tile0[i] + (i < n ? fbn_cdiv(J.j[i].rows, 64) * fbn_cdiv(J.j[i].cols, 64) : 0);
+  }
+  return J.tile0[n];
+}

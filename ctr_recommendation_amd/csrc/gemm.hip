@@ -258,10 +258,10 @@ template <int ROWS, int BK, bool KC, bool MAP> struct OpLoader<ROWS, BK, KC, MAP
 // past the main loop).
 template <int BM, int BN, int WGM, int WGN, int TM, int TN>
 __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[TM][TN], int m0, int n0, int wm,
-                                              int wn, int lr, int lh, float* red) {
+                                              int wn, int lr, int lh, float* red, bool split, int z) {
   constexpr int WM = BM / WGM, WN = BN / WGN;
   // C/D map of the 32x32 MFMA tile: col = lane&31, row = (e&3) + 8*(e>>2) + 4*(lane>>5)
-  const bool split = gridDim.z > 1;
+  // split: this workgroup's K range z is one slab of ws (split-K), not C
   // common case, decided per workgroup (uniform): a whole tile of an unremapped f32 or bf16 C with no
   // beta -- straight-line stores from one row base per (i, j), 32-bit offsets, no per-element tests
   const bool fast = !split && g.beta == 0.f && g.rC.seg == 0x7fffffff && g.rC.off0 == 0 && m0 + BM <= g.M &&
@@ -299,7 +299,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[T
         const int m = m0 + wm * WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
         if (m >= g.M) continue;
         if (split) {
-          g.ws[((size_t)blockIdx.z * g.M + m) * g.N + n] = acc[i][j][e];
+          g.ws[((size_t)z * g.M + m) * g.N + n] = acc[i][j][e];
         } else if (g.c16) {
           reinterpret_cast<short*>(g.C)[(size_t)m * g.ldc + nc] = f2bf(acc[i][j][e] + bv);
         } else {
@@ -496,7 +496,8 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
     __syncthreads();
   }
 
-  gemm_epilogue<BM, BN, 2, 2>(g, acc, m0, n0, wm, wn, lr, lh, reinterpret_cast<float*>(&sA[0][0]));
+  gemm_epilogue<BM, BN, 2, 2>(g, acc, m0, n0, wm, wn, lr, lh, reinterpret_cast<float*>(&sA[0][0]), gridDim.z > 1,
+                              blockIdx.z);
 }
 
 __global__ void gemm_splitk_reduce(GemmArgs g, int nsplit) {
@@ -585,8 +586,7 @@ __device__ __forceinline__ int xcd_tile(int bid, int nb) {
 // of 32x32 MFMA blocks.  8 waves on a 128x128 tile: two waves per SIMD, each with 2 MFMAs per
 // 3 fragment reads (4 waves on 64x64 tiles: 1 MFMA per 2 reads).
 template <int BM, int BN, bool AKM, bool BKM, int S, int WGM = 2, int WGN = 2>
-__global__ void __launch_bounds__(64 * WGM * WGN) gemm_dma16_kernel(GemmArgs g, int tiles_n, int remap_xcd) {
-  FBN_MAIN_PRIO();
+__device__ __forceinline__ void gemm_dma16_tile(const GemmArgs& g, int m0, int n0, int z, bool split) {
   constexpr int NW = WGM * WGN;
   constexpr int BK = 64;
   constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 32, TN = WN / 32;
@@ -596,12 +596,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_dma16_kernel(GemmArgs g, 
   static_assert(S >= 2 && S <= 4, "stages");
   __shared__ __attribute__((aligned(1024))) char smem[S * STAGE];
 
-  int bid = blockIdx.x;
-  const int nb = gridDim.x;
-  if (remap_xcd) bid = xcd_tile(bid, nb);
-  const int tm = bid / tiles_n, tn = bid % tiles_n;
-  const int n0 = tn * BN, m0 = tm * BM;
-  const int kbeg = blockIdx.z * g.kchunk;
+  const int kbeg = z * g.kchunk;
   const int kend = min(g.K, kbeg + g.kchunk);
   const int nk = kend > kbeg ? (kend - kbeg) / BK : 0;
 
@@ -705,7 +700,42 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_dma16_kernel(GemmArgs g, 
     }
   }
   __syncthreads();   // the stats epilogue reuses the staging LDS
-  gemm_epilogue<BM, BN, WGM, WGN>(g, acc, m0, n0, wm, wn, lr, lh, reinterpret_cast<float*>(smem));
+  gemm_epilogue<BM, BN, WGM, WGN>(g, acc, m0, n0, wm, wn, lr, lh, reinterpret_cast<float*>(smem), split, z);
+}
+
+template <int BM, int BN, bool AKM, bool BKM, int S, int WGM = 2, int WGN = 2>
+__global__ void __launch_bounds__(64 * WGM * WGN) gemm_dma16_kernel(GemmArgs g, int tiles_n, int remap_xcd) {
+  FBN_MAIN_PRIO();
+  int bid = blockIdx.x;
+  const int nb = gridDim.x;
+  if (remap_xcd) bid = xcd_tile(bid, nb);
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  gemm_dma16_tile<BM, BN, AKM, BKM, S, WGM, WGN>(g, tm * BM, tn * BN, blockIdx.z, gridDim.z > 1);
+}
+
+// Several slab-mode GEMMs (fbn_gemm_slabs_group: the step's weight gradients) in ONE launch: the
+// flat block index runs over problem p's tiles x K-slabs in [start[p], start[p+1]), slab-major
+// (the order of a separate launch's (x, z) grid).  Every problem writes its K-slabs into its own
+// ws exactly as a separate fbn_gemm_slabs launch would: each output element's K-chunk is summed by
+// the same 32x32x16 MFMA sequence whatever the tile shape, so the slabs are bit-identical.
+#define FBN_GEMM_GROUP_MAX 6
+struct GemmGroup {
+  GemmArgs g[FBN_GEMM_GROUP_MAX];
+  int tiles_n[FBN_GEMM_GROUP_MAX], tiles[FBN_GEMM_GROUP_MAX], start[FBN_GEMM_GROUP_MAX + 1];
+  int n;
+};
+template <int BM, int BN, bool AKM, bool BKM, int S, int WGM, int WGN>
+__global__ void __launch_bounds__(64 * WGM * WGN) gemm_dma16_group_kernel(GemmGroup G) {
+  FBN_MAIN_PRIO();
+  const int b = blockIdx.x;
+  int p = 0;
+#pragma unroll
+  for (int q = 1; q < FBN_GEMM_GROUP_MAX; ++q)
+    if (q < G.n && b >= G.start[q]) p = q;
+  const int local = b - G.start[p];
+  const int z = local / G.tiles[p], t = local - z * G.tiles[p];
+  const int tm = t / G.tiles_n[p], tn = t - tm * G.tiles_n[p];
+  gemm_dma16_tile<BM, BN, AKM, BKM, S, WGM, WGN>(G.g[p], tm * BM, tn * BN, z, true);
 }
 
 // vectorised split-K reduce: 4 consecutive columns per thread (N, ldc and the C remap in
@@ -1004,6 +1034,83 @@ extern "C" int fbn_gemm_slabs(const void* A, const void* B, int M, int N, int K,
   return gemm_impl(A, B, ws, nullptr, M, N, K, lda, ldb, N, transA, transB, 0x7fffffff, 0, 0, 0x7fffffff, 0, 0, 0.f,
                    1, 1, 1, nullptr, ws, ws_bytes, A2, lda2, A2 ? kseg : 0x7fffffff, B2, ldb2,
                    B2 ? nseg : 0x7fffffff, stream, 0, nullptr, nsplit);
+}
+
+extern "C" int fbn_gemm_slabs_split(int M, int N, int K) { return (M > 0 && N > 0) ? slab_split(M, N, K) : 0; }
+
+// n <= FBN_GEMM_GROUP_MAX slab-mode GEMMs (each exactly what fbn_gemm_slabs(d[i]...) would compute
+// into d[i].ws: fbn_gemm_slabs_split(M, N, K) K-slabs) in one launch, on the tile shape the
+// largest problem's own plan takes.  Every problem: k-major A and B (transA = 1, transB = 0, the
+// weight-gradient form), bf16, K % 64 == 0.
+struct FbnSlabGemm {   // one record of fbn_gemm_slabs_group (include/fibinet.h)
+  const void* A;
+  const void* B;
+  float* ws;
+  size_t ws_bytes;
+  const void* A2;
+  const void* B2;
+  int M, N, K, lda, ldb, transA, transB, lda2, kseg, ldb2, nseg, pad;
+};
+extern "C" int fbn_gemm_slabs_group(const void* descs, int n, void* stream) {
+  const FbnSlabGemm* d = static_cast<const FbnSlabGemm*>(descs);
+  if (n <= 0) return FBN_OK;
+  if (!d || n > FBN_GEMM_GROUP_MAX) { fbn_set_error("fbn_gemm_slabs_group: 1 <= n <= 6 descriptors"); return FBN_ERR_ARG; }
+  GemmGroup G;
+  G.n = n;
+  int big = 0;
+  double fl = -1.0;
+  for (int i = 0; i < n; ++i) {
+    const FbnSlabGemm& x = d[i];
+    const bool ok = x.A && x.B && x.ws && x.M > 0 && x.N > 0 && x.K > 0 && x.transA && !x.transB && x.K % 64 == 0 &&
+                    !(x.lda & 7) && !(x.ldb & 7) && !(x.M & 7) && !(x.N & 7) && !((uintptr_t)x.A & 15) &&
+                    !((uintptr_t)x.B & 15) && !x.A2 &&
+                    (!x.B2 || (!(x.nseg & 127) && !(x.ldb2 & 7) && !((uintptr_t)x.B2 & 15))) &&
+                    x.ws_bytes >= (size_t)slab_split(x.M, x.N, x.K) * x.M * x.N * sizeof(float);
+    if (!ok) {
+      fbn_set_error("fbn_gemm_slabs_group: each problem needs transA = 1, transB = 0, K % 64 == 0, M, N, ld % 8 == 0, "
+                    "16-B aligned operands, no A2, ws >= fbn_gemm_slabs_size");
+      return FBN_ERR_ARG;
+    }
+    const double f = (double)x.M * x.N * x.K;
+    if (f > fl) { fl = f; big = i; }
+  }
+  const GemmPlan bp = plan_dma16(d[big].M, d[big].N, d[big].K);
+  const bool wide = bp.waves == 8 && bp.bm == 128 && bp.bn == 128;
+  const int BM = wide ? 128 : 64, BN = wide ? 128 : 64;
+  long long total = 0;
+  for (int i = 0; i < n; ++i) {
+    const FbnSlabGemm& x = d[i];
+    GemmArgs& g = G.g[i];
+    g = GemmArgs{};
+    g.A = x.A; g.B = x.B; g.C = x.ws; g.bias = nullptr;
+    g.M = x.M; g.N = x.N; g.K = x.K; g.lda = x.lda; g.ldb = x.ldb; g.ldc = x.N;
+    g.rB = {0x7fffffff, 0, 0};
+    g.rC = {0x7fffffff, 0, 0};
+    g.beta = 0.f;
+    g.A2 = nullptr; g.lda2 = 0; g.kseg = 0x7fffffff;
+    g.B2 = x.B2; g.ldb2 = x.ldb2; g.nseg = x.B2 ? x.nseg : 0x7fffffff;
+    g.c16 = 0;
+    g.bnb_hact16 = nullptr; g.bnb_xpre = nullptr; g.bnb_mean = nullptr; g.bnb_scale = 1.f; g.bnb_part = nullptr;
+    g.bnb_rpc = 1;
+    g.stats = nullptr;
+    g.ws = x.ws;
+    const int split = slab_split(x.M, x.N, x.K);
+    g.kchunk = fbn_cdiv(fbn_cdiv(x.K, split), 64) * 64;
+    G.tiles_n[i] = fbn_cdiv(x.N, BN);
+    G.tiles[i] = G.tiles_n[i] * fbn_cdiv(x.M, BM);
+    G.start[i] = (int)total;
+    total += (long long)G.tiles[i] * split;
+  }
+  G.start[n] = (int)total;
+  hipStream_t st = (hipStream_t)stream;
+  if (wide)
+    hipLaunchKernelGGL((gemm_dma16_group_kernel<128, 128, true, true, 2, 2, 4>), dim3((unsigned)total), dim3(512), 0,
+                       st, G);
+  else
+    hipLaunchKernelGGL((gemm_dma16_group_kernel<64, 64, true, true, 2, 2, 2>), dim3((unsigned)total), dim3(256), 0,
+                       st, G);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
 }
 
 static int gemm_impl(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, int lda,

@@ -15,6 +15,7 @@
 // Philox4x32-10 stream keyed by (seed, offset) so the backward never stores them: the
 // backward factor is recovered from the stored activation (h_act > 0 <=> kept and positive).
 #include "common.h"
+#include "convert.h"
 
 // ------------------------------------------------------------------ bilinear pairs
 // pair index k enumerates (i,j), 1<=i<j<=5 lexicographically: (1,2)(1,3)(1,4)(1,5)(2,3)...(4,5)
@@ -1150,94 +1151,8 @@ extern "C" int fbn_sum(const float* x, int n, float* out, float scale, void* str
 // out[i][j] = bf16( T ? src[j*ld + rm(i)] : src[i*ld + rm(j)] ),  i < rows, j < cols,
 // rm(x) = x + (x < seg ? off0 : off1).  Up to 8 jobs per launch (one per blockIdx.y): the
 // compacted / transposed bf16 weight images the bf16 GEMMs read (made once per step).
-struct ConvJob {
-  const float* src;
-  short* dst;
-  int rows, cols, ld, trans, seg, off0, off1;
-};
-struct ConvJobs {
-  ConvJob j[8];
-  int tile0[9];   // first 64x64 output tile of each job (prefix sum)
-};
-// One 64x64 output tile per workgroup, four consecutive outputs per thread (one 8-B bf16x4 store):
-// a plain job reads four source columns at once (16-B load when they are contiguous and aligned:
-// the remap offsets and seg are multiples of 4); a transposed job reads its source tile along the
-// source's contiguous dimension into LDS (coalesced) and writes the output rows from LDS.
 __global__ void __launch_bounds__(256) convert_bf16_kernel(ConvJobs jobs, int njobs) {
-  __shared__ float tile[64][65];
-  int jb = 0;
-  while (jb + 1 < njobs && (int)blockIdx.x >= jobs.tile0[jb + 1]) ++jb;
-  const ConvJob J = jobs.j[jb];
-  const int t = blockIdx.x - jobs.tile0[jb];
-  const int tcols = (J.cols + 63) / 64;
-  const int i0 = (t / tcols) * 64, j0 = (t % tcols) * 64;
-  const int tq = threadIdx.x & 15, tr = threadIdx.x >> 4;   // column quad, row of 16
-  if (!J.trans) {
-    const int j = j0 + 4 * tq;
-    if (j >= J.cols) return;
-    const bool full = j + 4 <= J.cols;
-    const int b = j + (j < J.seg ? J.off0 : J.off1);
-    const bool vec = full && !(J.ld & 3) && !(b & 3) && (J.seg == 0x7fffffff || !(J.seg & 3) || j + 4 <= J.seg ||
-                                                         j >= J.seg);
-    f32x4 val[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {   // all loads in flight before the first store
-      const int i = i0 + tr + 16 * k;
-      if (i >= J.rows) { val[k] = (f32x4){0.f, 0.f, 0.f, 0.f}; continue; }
-      if (vec) {
-        val[k] = *reinterpret_cast<const f32x4*>(J.src + (size_t)i * J.ld + b);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int jj = j + e;
-          val[k][e] = jj < J.cols ? J.src[(size_t)i * J.ld + jj + (jj < J.seg ? J.off0 : J.off1)] : 0.f;
-        }
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int i = i0 + tr + 16 * k;
-      if (i >= J.rows) continue;
-      short* d = J.dst + (size_t)i * J.cols + j;
-      if (full && !(J.cols & 3)) {
-        *reinterpret_cast<bf16x4*>(d) = (bf16x4){f2bf(val[k][0]), f2bf(val[k][1]), f2bf(val[k][2]), f2bf(val[k][3])};
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (j + e < J.cols) d[e] = f2bf(val[k][e]);
-      }
-    }
-    return;
-  }
-  // out[i][j] = src[j][rm(i)]: lanes run along i, the source's contiguous dimension
-  {
-    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-    const int i = i0 + tx;
-    const int b = i + (i < J.seg ? J.off0 : J.off1);
-#pragma unroll
-    for (int r = ty; r < 64; r += 4) {
-      const int j = j0 + r;
-      tile[r][tx] = (i < J.rows && j < J.cols) ? J.src[(size_t)j * J.ld + b] : 0.f;
-    }
-  }
-  __syncthreads();
-  const int j = j0 + 4 * tq;
-  if (j >= J.cols) return;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int r = tr + 16 * k, i = i0 + r;
-    if (i >= J.rows) continue;
-    short* d = J.dst + (size_t)i * J.cols + j;
-    const bf16x4 v = {f2bf(tile[4 * tq][r]), f2bf(tile[4 * tq + 1][r]), f2bf(tile[4 * tq + 2][r]),
-                      f2bf(tile[4 * tq + 3][r])};
-    if (j + 4 <= J.cols && !(J.cols & 3)) {
-      *reinterpret_cast<bf16x4*>(d) = v;
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (j + e < J.cols) d[e] = v[e];
-    }
-  }
+  convert_tile(jobs, njobs, blockIdx.x);
 }
 
 // jobs: host array of n (<= 8) ConvJob records {src, dst, rows, cols, ld, trans, seg, off0, off1}
@@ -1245,13 +1160,9 @@ extern "C" int fbn_convert_bf16(const void* jobs, int n, void* stream) {
   if (n <= 0) return FBN_OK;
   if (n > 8) { fbn_set_error("convert_bf16: at most 8 jobs"); return FBN_ERR_ARG; }
   ConvJobs J;
-  J.tile0[0] = 0;
-  for (int i = 0; i < 8; ++i) {
-    J.j[i] = ((const ConvJob*)jobs)[i < n ? i : 0];
-    J.tile0[i + 1] = J.tile0[i] + (i < n ? fbn_cdiv(J.j[i].rows, 64) * fbn_cdiv(J.j[i].cols, 64) : 0);
-  }
-  if (J.tile0[n] <= 0) return FBN_OK;
-  hipLaunchKernelGGL(convert_bf16_kernel, dim3(J.tile0[n]), dim3(256), 0, (hipStream_t)stream, J, n);
+  const int tiles = conv_jobs_pack(jobs, n, J);
+  if (tiles <= 0) return FBN_OK;
+  hipLaunchKernelGGL(convert_bf16_kernel, dim3(tiles), dim3(256), 0, (hipStream_t)stream, J, n);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

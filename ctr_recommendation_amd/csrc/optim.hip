@@ -15,6 +15,7 @@
 // the gradient only through the row->slot map (4 B/row); untouched rows get g = 0 + wd*p.
 // The map entries of touched rows are reset in the same pass.
 #include "common.h"
+#include "convert.h"
 #include <cstdlib>
 #include <algorithm>
 
@@ -1470,16 +1471,16 @@ __global__ void __launch_bounds__(256) adam_prefetch2_kernel(float* __restrict__
 // are behind are replayed by the four-row engine.  Claims are those of adam_catchup_kernel (tagged
 // pre-claim, else plain load + CAS; dup / hasdup written the same way).
 template <int D, bool DW>
-__global__ void __launch_bounds__(256) adam_claim2_kernel(float* __restrict__ p, float* __restrict__ m,
-                                                          float* __restrict__ v, ClaimSrc cs, int n,
-                                                          int* __restrict__ last, const AdamConsts* __restrict__ table,
-                                                          const int* __restrict__ step, float wd, float b2,
-                                                          float omb2, float eps, PendSrc ps) {
+__device__ __forceinline__ void adam_claim2_body(float* __restrict__ p, float* __restrict__ m,
+                                                 float* __restrict__ v, const ClaimSrc& cs, int n,
+                                                 int* __restrict__ last, const AdamConsts* __restrict__ table,
+                                                 const int* __restrict__ step, float wd, float b2,
+                                                 float omb2, float eps, const PendSrc& ps, int blk) {
   __shared__ f32x4 win[FBN_PF_WIN + 1];
   const int t = *step;
   const int w0 = t > FBN_PF_WIN ? t - FBN_PF_WIN : 0;
   const int lane = threadIdx.x & 63;
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long i = (long long)blk * blockDim.x + threadIdx.x;
   int r = 0, key = 0x7fffffff, pe = -1;
   if (i < n) {
     const long long b = i / (cs.L + 1), tt = i - b * (cs.L + 1);
@@ -1532,6 +1533,35 @@ __global__ void __launch_bounds__(256) adam_claim2_kernel(float* __restrict__ p,
   const int cnt = __popcll(__ballot(key != 0x7fffffff));
   if (cnt == 0) return;
   replay_sorted<D, DW>(r, key, pe, cnt, t, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
+}
+template <int D, bool DW>
+__global__ void __launch_bounds__(256) adam_claim2_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                          float* __restrict__ v, ClaimSrc cs, int n,
+                                                          int* __restrict__ last, const AdamConsts* __restrict__ table,
+                                                          const int* __restrict__ step, float wd, float b2,
+                                                          float omb2, float eps, PendSrc ps) {
+  adam_claim2_body<D, DW>(p, m, v, cs, n, last, table, step, wd, b2, omb2, eps, ps, blockIdx.x);
+}
+// The step's head in one launch: blocks [0, nclaim) make the row claims + claimed-row catch-up
+// (adam_claim2_kernel), the rest convert the bf16 images (fbn_convert_bf16: the weights the previous
+// step's tail wrote, this batch's item_emb_d128) -- independent work, side by side instead of one
+// launch after the other.
+template <int D, bool DW>
+__global__ void __launch_bounds__(256) adam_claim2_conv_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                               float* __restrict__ v, ClaimSrc cs, int n,
+                                                               int* __restrict__ last,
+                                                               const AdamConsts* __restrict__ table,
+                                                               const int* __restrict__ step, float wd, float b2,
+                                                               float omb2, float eps, PendSrc ps, ConvJobs cj,
+                                                               int njobs, int nclaim) {
+  if ((int)blockIdx.x < nclaim)
+    adam_claim2_body<D, DW>(p, m, v, cs, n, last, table, step, wd, b2, omb2, eps, ps, blockIdx.x);
+  else
+    convert_tile(cj, njobs, blockIdx.x - nclaim);
+}
+
+__global__ void __launch_bounds__(256) convert_bf16_kernel_o(ConvJobs jobs, int njobs) {
+  convert_tile(jobs, njobs, blockIdx.x);
 }
 
 // The rolling window (step mod F) with the replay engine: rpw rows per wave
@@ -2335,13 +2365,54 @@ extern "C" int fbn_adam_prefetch_rows(const int* lids, int n, int skip0, long lo
 }
 
 // single GPU: fbn_claim_rows + fbn_adam_catchup(parts = 1) in one launch (see ClaimSrc)
+static int claim_catchup_impl(const int64_t* item, const int64_t* seq, int B, int L, long long V, int* map,
+                              int* slot_row, int* dup, int* hasdup, unsigned long long* preclaim, float* p, float* m,
+                              float* v, long long nrows, int D, int F, int* last, const void* consts_table,
+                              const int* step, float wd, float beta2, float eps, int* pend, const float* ring,
+                              const float* coef_hist, long long ring_stride, int ring_n, int decoupled,
+                              const void* conv_jobs, int n_conv, void* stream);
+
 extern "C" int fbn_adam_claim_catchup(const int64_t* item, const int64_t* seq, int B, int L, long long V, int* map,
                                       int* slot_row, int* dup, int* hasdup, unsigned long long* preclaim, float* p,
                                       float* m, float* v, long long nrows, int D,
                                       int F, int* last, const void* consts_table, const int* step, float wd,
                                       float beta2, float eps, int* pend, const float* ring, const float* coef_hist,
                                       long long ring_stride, int ring_n, int decoupled, void* stream) {
+  return claim_catchup_impl(item, seq, B, L, V, map, slot_row, dup, hasdup, preclaim, p, m, v, nrows, D, F, last,
+                            consts_table, step, wd, beta2, eps, pend, ring, coef_hist, ring_stride, ring_n, decoupled,
+                            nullptr, 0, stream);
+}
+
+extern "C" int fbn_adam_claim_catchup_conv(const int64_t* item, const int64_t* seq, int B, int L, long long V,
+                                           int* map, int* slot_row, int* dup, int* hasdup,
+                                           unsigned long long* preclaim, float* p, float* m, float* v,
+                                           long long nrows, int D, int F, int* last, const void* consts_table,
+                                           const int* step, float wd, float beta2, float eps, int* pend,
+                                           const float* ring, const float* coef_hist, long long ring_stride,
+                                           int ring_n, int decoupled, const void* conv_jobs, int n_conv,
+                                           void* stream) {
+  if (n_conv < 0 || n_conv > 8 || (n_conv > 0 && !conv_jobs)) {
+    fbn_set_error("fbn_adam_claim_catchup_conv: 0 <= n_conv <= 8 conversion jobs");
+    return FBN_ERR_ARG;
+  }
+  return claim_catchup_impl(item, seq, B, L, V, map, slot_row, dup, hasdup, preclaim, p, m, v, nrows, D, F, last,
+                            consts_table, step, wd, beta2, eps, pend, ring, coef_hist, ring_stride, ring_n, decoupled,
+                            conv_jobs, n_conv, stream);
+}
+
+static int claim_catchup_impl(const int64_t* item, const int64_t* seq, int B, int L, long long V, int* map,
+                              int* slot_row, int* dup, int* hasdup, unsigned long long* preclaim, float* p, float* m,
+                              float* v, long long nrows, int D, int F, int* last, const void* consts_table,
+                              const int* step, float wd, float beta2, float eps, int* pend, const float* ring,
+                              const float* coef_hist, long long ring_stride, int ring_n, int decoupled,
+                              const void* conv_jobs, int n_conv, void* stream) {
   const long long n = (long long)B * (L + 1);
+  ConvJobs cj;
+  const int conv_tiles = n_conv > 0 ? conv_jobs_pack(conv_jobs, n_conv, cj) : 0;
+  if (conv_tiles > 0 && (n <= 0 || nrows <= 0 || D < 128)) {   // no claim launch to ride on: convert alone
+    hipLaunchKernelGGL(convert_bf16_kernel_o, dim3(conv_tiles), dim3(256), 0, (hipStream_t)stream, cj, n_conv);
+    FBN_CHECK_LAUNCH();
+  }
   if (n <= 0 || nrows <= 0) return FBN_OK;
   if (!item || (L > 0 && !seq) || !map || !slot_row) {
     fbn_set_error("fbn_adam_claim_catchup: item, seq (L > 0), map and slot_row are required");
@@ -2360,6 +2431,25 @@ extern "C" int fbn_adam_claim_catchup(const int64_t* item, const int64_t* seq, i
   // one entry per lane, row state in one round trip, the replay engine (adam_claim2_kernel);
   // FBN_CLAIM_ONEPASS=1 keeps the scans of adam_catchup_kernel (A/B)
   static const bool cone = getenv("FBN_CLAIM_ONEPASS") && atoi(getenv("FBN_CLAIM_ONEPASS")) == 1;
+  if (conv_tiles > 0 && D >= 128 && !cone) {
+    const int nclaim = (int)((n + 255) / 256);
+    const dim3 g2((unsigned)(nclaim + conv_tiles));
+#define FBN_CLAIM_CONV(DD, DW_)                                                                                  \
+  hipLaunchKernelGGL((adam_claim2_conv_kernel<DD, DW_>), g2, dim3(256), 0, st, p, m, v, cs, (int)n, last,        \
+                     (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, cj, n_conv, nclaim)
+    if (D == 128) {
+      if (decoupled) FBN_CLAIM_CONV(128, true); else FBN_CLAIM_CONV(128, false);
+    } else {
+      if (decoupled) FBN_CLAIM_CONV(256, true); else FBN_CLAIM_CONV(256, false);
+    }
+#undef FBN_CLAIM_CONV
+    FBN_CHECK_LAUNCH();
+    return FBN_OK;
+  }
+  if (conv_tiles > 0 && D >= 128) {   // FBN_CLAIM_ONEPASS: the images in their own launch first
+    hipLaunchKernelGGL(convert_bf16_kernel_o, dim3(conv_tiles), dim3(256), 0, st, cj, n_conv);
+    FBN_CHECK_LAUNCH();
+  }
   if (!cone) {
     const dim3 g2((unsigned)((n + 255) / 256));
     if (decoupled) {

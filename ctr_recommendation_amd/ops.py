@@ -95,6 +95,15 @@ def bf16_weights(p: Dict[str, torch.Tensor], d: int, a: Dict[str, torch.Tensor],
     """bf16 images of the GEMM weights, laid out so every bf16 GEMM operand is K-contiguous:
     Wa_nz [512,15d] (zero columns dropped) and its transpose, Wb and Wb^T, W and W^T, Wp;
     plus x (the batch's item_emb_d128, [B,128]) when given -- all in one launch."""
+    jobs, n, out = bf16_weight_jobs(p, d, a, x)
+    call("fbn_convert_bf16", ctypes.cast(jobs, ctypes.c_void_p).value, n, stream)
+    return out
+
+
+def bf16_weight_jobs(p: Dict[str, torch.Tensor], d: int, a: Dict[str, torch.Tensor],
+                     x: Optional[torch.Tensor] = None):
+    """(job records, count, images) of bf16_weights, for a launch that carries the conversion
+    (fbn_convert_bf16, or the step head fbn_adam_claim_catchup_conv); the records live in a["_conv_jobs"]."""
     dev = p["mlp.0.weight"].device
     KC = 15 * d
     spec = [("Wa", p["mlp.0.weight"], H1, KC, 21 * d, 0, wa_remap(d)),
@@ -107,6 +116,7 @@ def bf16_weights(p: Dict[str, torch.Tensor], d: int, a: Dict[str, torch.Tensor],
     if x is not None:
         spec.append(("x", x, x.shape[0], x.shape[1], x.shape[1], 0, NO_REMAP))
     jobs = (_ConvJob * 8)()
+    a["_conv_jobs"] = jobs
     out = {}
     for i, (name, src, rows, cols, ld, trans, rm) in enumerate(spec):
         key = "w16_" + name
@@ -116,8 +126,7 @@ def bf16_weights(p: Dict[str, torch.Tensor], d: int, a: Dict[str, torch.Tensor],
             a[key] = t
         out[name] = t
         jobs[i] = _ConvJob(src.data_ptr(), t.data_ptr(), rows, cols, ld, trans, rm[0], rm[1], rm[2])
-    call("fbn_convert_bf16", ctypes.cast(jobs, ctypes.c_void_p).value, len(spec), stream)
-    return out
+    return jobs, len(spec), out
 
 
 class _SumJob(ctypes.Structure):
@@ -134,6 +143,18 @@ class _SlabJob(ctypes.Structure):
 # the weight-gradient GEMMs leave their split-K slabs for the step's one fbn_sum_jobs2 launch, and
 # the fields backward its partial rows (FBN_DEFER_REDUCE=0: a reduce launch after each, A/B)
 _DEFER_REDUCE = os.environ.get("FBN_DEFER_REDUCE", "1") != "0"
+# ... and those GEMMs themselves wait for the end of the backward, where they run as ONE grouped
+# launch (fbn_gemm_slabs_group) right before that sum launch (FBN_WGRAD_GROUP=0: each launched in
+# place, A/B)
+_WGRAD_GROUP = os.environ.get("FBN_WGRAD_GROUP", "1") != "0"
+
+
+class _SlabGemm(ctypes.Structure):
+    _fields_ = [("A", ctypes.c_void_p), ("B", ctypes.c_void_p), ("ws", ctypes.c_void_p), ("ws_bytes", ctypes.c_size_t),
+                ("A2", ctypes.c_void_p), ("B2", ctypes.c_void_p), ("M", ctypes.c_int), ("N", ctypes.c_int),
+                ("K", ctypes.c_int), ("lda", ctypes.c_int), ("ldb", ctypes.c_int), ("transA", ctypes.c_int),
+                ("transB", ctypes.c_int), ("lda2", ctypes.c_int), ("kseg", ctypes.c_int), ("ldb2", ctypes.c_int),
+                ("nseg", ctypes.c_int), ("pad", ctypes.c_int)]
 _nsplit = ctypes.c_int(0)
 # FBN_GATHER_HOT=<tau> (A/B variant of the gather, N1): rows a batch draws >= tau times staged in
 # LDS per workgroup (fbn_hot_rows + fbn_fields_fwd_hot); 0 = off (default: measured slower)
@@ -151,6 +172,7 @@ class DeferredSums:
         self.keep = []
         self.cache = cache      # slab workspaces kept across steps (one per GEMM shape)
         self.used = set()
+        self.group = []         # slab GEMMs deferred to one fbn_gemm_slabs_group launch at flush()
 
     def add(self, part, nch, C, out, scale=1.0, beta=0.0, ld=0):
         self.jobs.append((part.data_ptr(), out.data_ptr(), int(nch), int(C), float(scale), float(beta), int(ld), 0))
@@ -175,10 +197,19 @@ class DeferredSums:
             ws = _ws(nbytes, out.device)
             if self.cache is not None:
                 self.cache[key] = ws
-        call("fbn_gemm_slabs", ptr(A), ptr(B), M, N, K, lda, ldb, int(transA), int(transB), ptr(ws), nbytes,
-             ptr(A2), lda2, kseg, ptr(B2), ldb2, nseg, ctypes.byref(_nsplit),
-             stream if stream is not None else _lib.stream_handle())
-        self.slabs.append((ws.data_ptr(), out.data_ptr(), M, N, ldc, _nsplit.value, rC[0], rC[1], rC[2], float(beta)))
+        st = stream if stream is not None else _lib.stream_handle()
+        if _WGRAD_GROUP and transA and not transB and A2 is None and M % 8 == 0 and N % 8 == 0:
+            # deferred to flush(): the step's weight gradients in one fbn_gemm_slabs_group launch
+            # (their operands are not rewritten before it: stream order, buffers of this step)
+            nsplit = _lib.lib().fbn_gemm_slabs_split(M, N, K)
+            self.group.append((A.data_ptr(), B.data_ptr(), ws.data_ptr(), nbytes, 0, ptr(B2) or 0, M, N, K, lda,
+                               ldb, 1, 0, 0, 0, ldb2, nseg if B2 is not None else INT_MAX, 0))
+            self.keep += [A, B] + ([B2] if B2 is not None else [])
+        else:
+            call("fbn_gemm_slabs", ptr(A), ptr(B), M, N, K, lda, ldb, int(transA), int(transB), ptr(ws), nbytes,
+                 ptr(A2), lda2, kseg, ptr(B2), ldb2, nseg, ctypes.byref(_nsplit), st)
+            nsplit = _nsplit.value
+        self.slabs.append((ws.data_ptr(), out.data_ptr(), M, N, ldc, nsplit, rC[0], rC[1], rC[2], float(beta)))
         self.keep.append(ws)
         return True
 
@@ -189,6 +220,12 @@ class DeferredSums:
         self.add(part, nch, C, out)
 
     def flush(self, stream):
+        group = self.group
+        while group:
+            gc, group = group[:6], group[6:]
+            garr = (_SlabGemm * len(gc))(*[_SlabGemm(*x) for x in gc])
+            call("fbn_gemm_slabs_group", ctypes.addressof(garr), len(gc), stream)
+        self.group = []
         jobs, slabs = self.jobs, self.slabs
         while jobs or slabs:
             jc, sc = jobs[:16], slabs[:8]

@@ -58,6 +58,9 @@ _SIDE_AFTER_MMPROJ = os.environ.get("FBN_SIDE_AFTER_MMPROJ", "0") == "1"
 # 0.2833-0.2844 vs 0.2934-0.2952 ms/step; eager 0.30 vs 0.45-0.50, the host's event waits gone;
 # profiles/r03s2_side_serial_ab.txt), on the side stream from d = 128 on
 _CLAIM_ON_SIDE = os.environ.get("FBN_CLAIM_ON_SIDE", "0") == "1"
+# single GPU, lazy table Adam, images on main: the bf16 image conversion rides in the row claims'
+# launch (FBN_HEAD_CONV=0: its own launch ahead of the claims, A/B)
+_HEAD_CONV = os.environ.get("FBN_HEAD_CONV", "1") != "0"
 _SIDE_SERIAL = os.environ.get("FBN_SIDE_SERIAL", "auto")
 # order of the side stream's two table-Adam passes (A/B knob): "wp" window then next-batch
 # prefetch (default), "pw" the prefetch first, "p_w" the prefetch at the fork and the window only
@@ -445,12 +448,15 @@ class FiBiNETTrainer:
                 key = _batch_key(batch["item_id"], seq if L else None)
                 pre = self.preclaim if (self.preclaim is not None and key == self._pre_key) else None
                 self._pre_key = None
-                call("fbn_adam_claim_catchup", ptr(batch["item_id"]), ptr(seq) if L else None, B, L, self.V,
-                     ptr(self.map), ptr(self.slot_row), ptr(self.dup), ptr(self.hasdup), ptr(pre), ptr(self.E),
-                     ptr(self.Em),
-                     ptr(self.Ev),
-                     self.rows_local, d, self.lazy_window, ptr(self.last), ptr(self.sched), ptr(self.step_dev),
-                     self.wd_g, self.beta2, self.eps, *self._pend_args(), int(self.decoupled), st)
+                args = (ptr(batch["item_id"]), ptr(seq) if L else None, B, L, self.V, ptr(self.map),
+                        ptr(self.slot_row), ptr(self.dup), ptr(self.hasdup), ptr(pre), ptr(self.E), ptr(self.Em),
+                        ptr(self.Ev), self.rows_local, d, self.lazy_window, ptr(self.last), ptr(self.sched),
+                        ptr(self.step_dev), self.wd_g, self.beta2, self.eps, *self._pend_args(), int(self.decoupled))
+                if head_conv:
+                    # the step head: the bf16 images converted in the same launch as the claims
+                    call("fbn_adam_claim_catchup_conv", *args, *head_conv, st)
+                else:
+                    call("fbn_adam_claim_catchup", *args, st)
             else:
                 call("fbn_adam_catchup", ptr(self.E), ptr(self.Em), ptr(self.Ev), self.rows_local, d,
                      ptr(self.slot_row), n_ent, ptr(self.map), self.lazy_window, 1, ptr(self.last), ptr(self.sched),
@@ -545,7 +551,13 @@ class FiBiNETTrainer:
                 and not _SIDE_AFTER_MMPROJ and not _SIDE_AFTER_GATHER):
             claim_side = torch.cuda.Event()          # the step's start: the claims wait for nothing later
             claim_side.record(main)
-        if w16_main:
+        head_conv = None
+        if w16_main and self.xchg is None and lazy and claim_side is None and _HEAD_CONV:
+            # on the main stream, in the claims' launch (fbn_adam_claim_catchup_conv): the two are
+            # independent, so they run side by side instead of one launch after the other
+            jobs, njobs, self.acts["w16"] = ops.bf16_weight_jobs(self.p, d, self.acts, x=batch["item_emb_d128"])
+            head_conv = (ctypes.cast(jobs, ctypes.c_void_p).value, njobs)
+        elif w16_main:
             # on the main stream ahead of the claims: a cross-queue wait inside a replayed graph
             # costs ~10 us, about what the conversion itself takes
             self.acts["w16"] = ops.bf16_weights(self.p, d, self.acts, st, x=batch["item_emb_d128"])

@@ -66,6 +66,16 @@ size_t fbn_gemm_slabs_size(int M, int N, int K);
 int fbn_gemm_slabs(const void* A, const void* B, int M, int N, int K, int lda, int ldb, int transA, int transB,
                    float* ws, size_t ws_bytes, const void* A2, int lda2, int kseg, const void* B2, int ldb2, int nseg,
                    int* nsplit, void* stream);
+/* The K-slab count fbn_gemm_slabs takes for an M x N x K product (its *nsplit), host-only. */
+int fbn_gemm_slabs_split(int M, int N, int K);
+/* n <= 6 slab-mode GEMMs in ONE launch (the step's weight gradients, deferred to the end of the
+ * backward: one tail instead of one per GEMM).  descs = host array of n records
+ * {const void* A, *B; float* ws; size_t ws_bytes; const void* A2, *B2;
+ *  int M, N, K, lda, ldb, transA, transB, lda2, kseg, ldb2, nseg, pad;}
+ * with the meaning of fbn_gemm_slabs's arguments; each ws receives exactly the
+ * fbn_gemm_slabs_split(M, N, K) slabs fbn_gemm_slabs would write (bit-identical).  Every problem:
+ * transA = 1, transB = 0, K % 64 == 0, M, N, lda, ldb % 8 == 0, no A2. */
+int fbn_gemm_slabs_group(const void* descs, int n, void* stream);
 /* bf16 operands (as fbn_gemm with bf16 = a16 = b16 = 1), C stored in bf16 (C[m * ldc + n], rounded
  * once from the f32 accumulators); no bias, beta, remap or statistics.  The bf16-mode dgrad
  * dc = dh1 Wa of the MLP input (src/model_fibinet.py:126-130 autograd), read only by
@@ -325,6 +335,16 @@ int fbn_adam_claim_catchup(const int64_t* item, const int64_t* seq, int B, int L
                            const void* consts_table, const int* step, float wd, float beta2, float eps, int* pend,
                            const float* ring, const float* coef_hist, long long ring_stride, int ring_n, int decoupled,
                            void* stream);
+/* fbn_adam_claim_catchup with the step's bf16 image conversion (fbn_convert_bf16's n_conv <= 8
+ * job records) in the same launch (D >= 128: claim blocks, then conversion blocks; otherwise the
+ * conversion's own launch first) -- the two are independent: the images are of the weights the
+ * previous step's tail wrote and of this batch's item_emb_d128 (src/model_fibinet.py:162). */
+int fbn_adam_claim_catchup_conv(const int64_t* item, const int64_t* seq, int B, int L, long long V, int* map,
+                                int* slot_row, int* dup, int* hasdup, unsigned long long* preclaim, float* p,
+                                float* m, float* v, long long nrows, int D, int F, int* last,
+                                const void* consts_table, const int* step, float wd, float beta2, float eps,
+                                int* pend, const float* ring, const float* coef_hist, long long ring_stride,
+                                int ring_n, int decoupled, const void* conv_jobs, int n_conv, void* stream);
 /* Single GPU, D = 128 / 256: ahead-of-time catch-up of the NEXT batch's rows during this step, on
  * the rolling window's stream after this step's claims and before its step tail.  A next-batch row
  * that this batch does not touch (map == -1) takes only zero-gradient steps through the current

@@ -267,3 +267,43 @@ def test_bf16_weight_images_match_torch(hip_device, d):
            "Wp": p["mm_proj.0.weight"], "W": p["bilinear.W"], "WT": p["bilinear.W"].T, "x": x}
     for k, r in ref.items():
         assert torch.equal(out[k], r.contiguous().bfloat16()), k
+
+
+@pytest.mark.gpu
+def test_gemm_slabs_group_matches_separate_launches(hip_device):
+    """fbn_gemm_slabs_group writes exactly the K-slabs separate fbn_gemm_slabs launches write, for
+    the step's weight-gradient shapes (C3 at B = 1024 and C2), the split-operand [B | B2] form of
+    the MLP input's included."""
+    import ctypes
+    from ctr_recommendation_amd import _lib
+    st = _lib.stream_handle(hip_device)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    lib = _lib.lib()
+    for probs in ([(256, 512, 1024, 0), (512, 1920, 1024, 640), (128, 128, 5120, 0), (128, 128, 1024, 0)],
+                  [(256, 512, 512, 0), (512, 240, 512, 0), (16, 16, 2560, 0), (16, 128, 512, 0)]):
+        descs, refs, outs = [], [], []
+        for (M, N, K, nseg) in probs:
+            A = torch.randn(K, M, generator=g).to(hip_device, torch.bfloat16)     # k-major A (transA)
+            Bm = torch.randn(K, N, generator=g).to(hip_device, torch.bfloat16)    # k-major B
+            B1, B2 = (Bm[:, :nseg].contiguous(), Bm[:, nseg:].contiguous()) if nseg else (Bm, None)
+            nbytes = lib.fbn_gemm_slabs_size(M, N, K)
+            ns = lib.fbn_gemm_slabs_split(M, N, K)
+            ws_ref = torch.full((nbytes // 4,), float("nan"), device=hip_device)
+            ws_grp = torch.full((nbytes // 4,), float("nan"), device=hip_device)
+            nsp = ctypes.c_int(0)
+            ldb = nseg if nseg else N
+            _lib.call("fbn_gemm_slabs", _lib.ptr(A), _lib.ptr(B1), M, N, K, M, ldb, 1, 0, _lib.ptr(ws_ref), nbytes, None,
+                      0, 0x7FFFFFFF, _lib.ptr(B2) if nseg else None, N - nseg if nseg else 0,
+                      nseg if nseg else 0x7FFFFFFF, ctypes.byref(nsp), st)
+            assert nsp.value == ns
+            descs.append(ops._SlabGemm(A.data_ptr(), B1.data_ptr(), ws_grp.data_ptr(), nbytes, 0,
+                                       B2.data_ptr() if nseg else 0, M, N, K, M, ldb, 1, 0, 0, 0,
+                                       N - nseg if nseg else 0, nseg if nseg else 0x7FFFFFFF, 0))
+            refs.append((ws_ref, ns * M * N))
+            outs.append((ws_grp, A, B1, B2))
+        arr = (ops._SlabGemm * len(descs))(*descs)
+        _lib.call("fbn_gemm_slabs_group", ctypes.addressof(arr), len(descs), st)
+        torch.cuda.synchronize()
+        for (ref, n), (grp, *_), pr in zip(refs, outs, probs):
+            assert torch.equal(ref[:n], grp[:n]), (pr, (ref[:n] - grp[:n]).abs().max().item(),
+                                                   torch.isnan(grp[:n]).sum().item())

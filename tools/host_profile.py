@@ -1,4 +1,4 @@
-"""Where the host time of one eager C3 trainer step goes (cProfile over 40 steps with next_batch,
+"""Where the host time of one eager C3 (or EG_D/EG_V/EG_B) trainer step goes (cProfile over 40 steps with next_batch,
 the bench's eager form).  Prints the median enqueue time per step and the top functions."""
 import cProfile
 import os
@@ -13,8 +13,9 @@ from ctr_recommendation_amd.data import make_device_batches
 from ctr_recommendation_amd.trainer import FiBiNETTrainer
 
 dev = torch.device("cuda", 0)
-V, B = 1_250_000, 8192
-cfg = {"embedding_dim": 128, "vocab_size": V, "compute_dtype": "bf16"}
+# C3 by default; EG_D / EG_V / EG_B for another config (C2: 16 / 1000000 / 4096)
+d, V, B = int(os.environ.get("EG_D", 128)), int(os.environ.get("EG_V", 1_250_000)), int(os.environ.get("EG_B", 8192))
+cfg = {"embedding_dim": d, "vocab_size": V, "compute_dtype": "bf16"}
 tr = FiBiNETTrainer(cfg, total_steps=400, batch_size=B, device=dev)
 nb = 8
 batches = make_device_batches(nb, B, V, 20, dev, seed=1)
@@ -29,6 +30,8 @@ for i in range(20):
     host.append(time.perf_counter() - t0)
     torch.cuda.synchronize()
 print(f"median host enqueue {sorted(host)[len(host) // 2] * 1e3:.3f} ms per step")
+if os.environ.get("HP_NOPROF") == "1":
+    sys.exit(0)
 pr = cProfile.Profile()
 pr.enable()
 for i in range(40):
