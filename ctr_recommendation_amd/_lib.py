@@ -49,6 +49,7 @@ SIGNATURES = {
     "fbn_gemm_slabs": (I, [P, P, I, I, I, I, I, I, I, P, SZ, P, I, I, P, I, I, P, P]),
     "fbn_gemm_slabs_split": (I, [I, I, I]),
     "fbn_gemm_slabs_group": (I, [P, I, P]),
+    "fbn_gemm_slabs_group_split": (I, [I, I, I]),
     "fbn_fields_fwd": (I, [P, P, P, P, P, P, P, F, P, I, P, LL, P, P, P, P, P, I, P, P, P, P, I, I, P, P, P, P, P, I, I, I, I,
                            P]),
     "fbn_fields_fwd_hot": (I, [P, P, P, P, P, P, P, F, P, I, P, LL, P, P, P, P, I, P, P, P, P, I, I, P, P, P, P, P,

@@ -28,6 +28,7 @@
 // order (deterministic).
 #include "common.h"
 #include <cstdlib>
+#include <algorithm>
 #include <cstdio>
 
 #ifndef FBN_DMA_STAGES
@@ -1038,9 +1039,29 @@ extern "C" int fbn_gemm_slabs(const void* A, const void* B, int M, int N, int K,
 
 extern "C" int fbn_gemm_slabs_split(int M, int N, int K) { return (M > 0 && N > 0) ? slab_split(M, N, K) : 0; }
 
-// n <= FBN_GEMM_GROUP_MAX slab-mode GEMMs (each exactly what fbn_gemm_slabs(d[i]...) would compute
-// into d[i].ws: fbn_gemm_slabs_split(M, N, K) K-slabs) in one launch, on the tile shape the
-// largest problem's own plan takes.  Every problem: k-major A and B (transA = 1, transB = 0, the
+// K-slabs of a problem inside fbn_gemm_slabs_group: half fbn_gemm_slabs_split's -- the grouped
+// problems fill the chip together, so each needs fewer workgroups, and half the slabs are written
+// and summed (C3: 0.4407 -> 0.4327 ms/step; a quarter: 0.4617; profiles/r03s2_group_knobs_ab.txt).
+// FBN_GROUP_SPLIT_DIV overrides the divisor (1: fbn_gemm_slabs's own partition, whose sums the
+// group then reproduces bit for bit; tests/test_gpu_trainer.py::test_wgrad_group_bit_identical).
+static int group_split(int M, int N, int K) {
+  int s = slab_split(M, N, K);
+  const char* e = getenv("FBN_GROUP_SPLIT_DIV");
+  const int div = e ? atoi(e) : 2;
+  if (div > 1) {
+    s = std::max(1, s / div);
+    const int per = fbn_cdiv(fbn_cdiv(K, s), 64) * 64;
+    s = fbn_cdiv(K, per);
+  }
+  return s;
+}
+extern "C" int fbn_gemm_slabs_group_split(int M, int N, int K) {
+  return (M > 0 && N > 0 && K > 0) ? group_split(M, N, K) : 0;
+}
+
+// n <= FBN_GEMM_GROUP_MAX slab-mode GEMMs (each what fbn_gemm_slabs(d[i]...) computes, into d[i].ws
+// as fbn_gemm_slabs_group_split(M, N, K) K-slabs) in one launch, on the tile shape the largest
+// problem's own plan takes.  Every problem: k-major A and B (transA = 1, transB = 0, the
 // weight-gradient form), bf16, K % 64 == 0.
 struct FbnSlabGemm {   // one record of fbn_gemm_slabs_group (include/fibinet.h)
   const void* A;
@@ -1065,7 +1086,7 @@ extern "C" int fbn_gemm_slabs_group(const void* descs, int n, void* stream) {
                     !(x.lda & 7) && !(x.ldb & 7) && !(x.M & 7) && !(x.N & 7) && !((uintptr_t)x.A & 15) &&
                     !((uintptr_t)x.B & 15) && !x.A2 &&
                     (!x.B2 || (!(x.nseg & 127) && !(x.ldb2 & 7) && !((uintptr_t)x.B2 & 15))) &&
-                    x.ws_bytes >= (size_t)slab_split(x.M, x.N, x.K) * x.M * x.N * sizeof(float);
+                    x.ws_bytes >= (size_t)group_split(x.M, x.N, x.K) * x.M * x.N * sizeof(float);
     if (!ok) {
       fbn_set_error("fbn_gemm_slabs_group: each problem needs transA = 1, transB = 0, K % 64 == 0, M, N, ld % 8 == 0, "
                     "16-B aligned operands, no A2, ws >= fbn_gemm_slabs_size");
@@ -1094,7 +1115,7 @@ extern "C" int fbn_gemm_slabs_group(const void* descs, int n, void* stream) {
     g.bnb_rpc = 1;
     g.stats = nullptr;
     g.ws = x.ws;
-    const int split = slab_split(x.M, x.N, x.K);
+    const int split = group_split(x.M, x.N, x.K);
     g.kchunk = fbn_cdiv(fbn_cdiv(x.K, split), 64) * 64;
     G.tiles_n[i] = fbn_cdiv(x.N, BN);
     G.tiles[i] = G.tiles_n[i] * fbn_cdiv(x.M, BM);
@@ -1103,7 +1124,11 @@ extern "C" int fbn_gemm_slabs_group(const void* descs, int n, void* stream) {
   }
   G.start[n] = (int)total;
   hipStream_t st = (hipStream_t)stream;
-  if (wide)
+  const char* se = getenv("FBN_GROUP_STAGES");   // A/B knob: LDS-DMA ring depth of the group (2 or 3)
+  if (wide && se && atoi(se) == 3)
+    hipLaunchKernelGGL((gemm_dma16_group_kernel<128, 128, true, true, 3, 2, 4>), dim3((unsigned)total), dim3(512), 0,
+                       st, G);
+  else if (wide)
     hipLaunchKernelGGL((gemm_dma16_group_kernel<128, 128, true, true, 2, 2, 4>), dim3((unsigned)total), dim3(512), 0,
                        st, G);
   else

@@ -1419,12 +1419,11 @@ __device__ __forceinline__ void replay_sorted(int r, int key, int pe, int cnt, i
 }
 
 template <int D, bool DW, int G = 4>
-__global__ void __launch_bounds__(256) adam_prefetch2_kernel(float* __restrict__ p, float* __restrict__ m,
-                                                             float* __restrict__ v, ClaimSrc cs, int n,
-                                                             int* __restrict__ last,
-                                                             const AdamConsts* __restrict__ table,
-                                                             const int* __restrict__ step, float wd, float b2,
-                                                             float omb2, float eps, PendSrc ps, int epw) {
+__device__ __forceinline__ void adam_prefetch2_body(float* __restrict__ p, float* __restrict__ m,
+                                                    float* __restrict__ v, const ClaimSrc& cs, int n,
+                                                    int* __restrict__ last, const AdamConsts* __restrict__ table,
+                                                    const int* __restrict__ step, float wd, float b2, float omb2,
+                                                    float eps, const PendSrc& ps, int epw, int blk, int nblk) {
   __shared__ f32x4 win[FBN_PF_WIN + 1];   // constants of steps [w0, T]
   const int T = *step + 1;
   const int w0 = T > FBN_PF_WIN ? T - FBN_PF_WIN : 0;
@@ -1435,8 +1434,8 @@ __global__ void __launch_bounds__(256) adam_prefetch2_kernel(float* __restrict__
   // epw entries per wave (lanes past epw hold none); a capped grid (FBN_PF_WAVES) walks the
   // entry chunks wave-strided, so the side stream holds few wave slots per SIMD at a time
   const long long nchunk = ((long long)n + epw - 1) / epw;
-  const long long wstride = ((long long)gridDim.x * blockDim.x) >> 6;
-  for (long long ch = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6; ch < nchunk; ch += wstride) {
+  const long long wstride = ((long long)nblk * blockDim.x) >> 6;
+  for (long long ch = ((long long)blk * blockDim.x + threadIdx.x) >> 6; ch < nchunk; ch += wstride) {
   const long long i = lane < epw ? ch * epw + lane : n;
   int r = 0, key = 0x7fffffff, pe = -1;
   if (i < n) {
@@ -1461,6 +1460,16 @@ __global__ void __launch_bounds__(256) adam_prefetch2_kernel(float* __restrict__
   if (cnt == 0) continue;
   replay_sorted<D, DW, G>(r, key, pe, cnt, T, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
   }
+}
+template <int D, bool DW, int G = 4>
+__global__ void __launch_bounds__(256) adam_prefetch2_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                             float* __restrict__ v, ClaimSrc cs, int n,
+                                                             int* __restrict__ last,
+                                                             const AdamConsts* __restrict__ table,
+                                                             const int* __restrict__ step, float wd, float b2,
+                                                             float omb2, float eps, PendSrc ps, int epw) {
+  adam_prefetch2_body<D, DW, G>(p, m, v, cs, n, last, table, step, wd, b2, omb2, eps, ps, epw, blockIdx.x,
+                                gridDim.x);
 }
 
 // Single GPU, D >= 128: the step's row claims + the claimed rows' catch-up (fbn_adam_claim_catchup)
@@ -1569,13 +1578,16 @@ __global__ void __launch_bounds__(256) convert_bf16_kernel_o(ConvJobs jobs, int 
 // steps each) spreads over thousands of waves instead of one wave per SIMD; claimed rows are left
 // to their claiming entry, as in adam_catchup_kernel.
 #define FBN_WIN_ROWS 16
+// tagged: leave the rows pre-claimed for the next step to a prefetch running in the same launch
+// (which brings them one step further; measured slower as one launch, profiles/r03s2_wgrad_group_head_ab.txt)
 template <int D, bool DW, int G = 4>
-__global__ void __launch_bounds__(256) adam_window2_kernel(float* __restrict__ p, float* __restrict__ m,
-                                                           float* __restrict__ v, const int* __restrict__ map,
-                                                           long long nrows, int F, long long chunk,
-                                                           int* __restrict__ last, const AdamConsts* __restrict__ table,
-                                                           const int* __restrict__ step, float wd, float b2,
-                                                           float omb2, float eps, PendSrc ps, int rpw) {
+__device__ __forceinline__ void adam_window2_body(float* __restrict__ p, float* __restrict__ m,
+                                                  float* __restrict__ v, const int* __restrict__ map,
+                                                  long long nrows, int F, long long chunk, int* __restrict__ last,
+                                                  const AdamConsts* __restrict__ table,
+                                                  const int* __restrict__ step, float wd, float b2, float omb2,
+                                                  float eps, const PendSrc& ps, int rpw, int blk, int nblk,
+                                                  bool tagged) {
   __shared__ f32x4 win[FBN_PF_WIN + 1];   // constants of steps [w0, t]
   const int t = *step;
   const int w0 = t > FBN_PF_WIN ? t - FBN_PF_WIN : 0;
@@ -1587,14 +1599,14 @@ __global__ void __launch_bounds__(256) adam_window2_kernel(float* __restrict__ p
   if constexpr (D < 128) __syncthreads();   // the LDS window (no barrier after this point)
   // rpw rows per wave; a capped grid (FBN_WIN_WAVES) walks the row groups wave-strided
   const long long ngrp = (nroll + rpw - 1) / rpw;
-  const long long wstride = ((long long)gridDim.x * blockDim.x) >> 6;
-  for (long long gq = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6; gq < ngrp; gq += wstride) {
+  const long long wstride = ((long long)nblk * blockDim.x) >> 6;
+  for (long long gq = ((long long)blk * blockDim.x + threadIdx.x) >> 6; gq < ngrp; gq += wstride) {
   const long long j = gq * rpw + lane;
   int r = 0, key = 0x7fffffff, pe = -1;
   if (lane < rpw && j < nroll) {
     const long long rr = roll0 + j;
     const int4 rs = row_state(last, rr);
-    if (!map || map[rr] == -1) {
+    if ((!map || map[rr] == -1) && !(tagged && rs.y == t + 1)) {
       const int k0 = rs.z;
       if (k0 < t) {
         r = (int)rr;
@@ -1609,6 +1621,16 @@ __global__ void __launch_bounds__(256) adam_window2_kernel(float* __restrict__ p
   if (cnt == 0) continue;
   replay_sorted<D, DW, G>(r, key, pe, cnt, t, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
   }
+}
+template <int D, bool DW, int G = 4>
+__global__ void __launch_bounds__(256) adam_window2_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                           float* __restrict__ v, const int* __restrict__ map,
+                                                           long long nrows, int F, long long chunk,
+                                                           int* __restrict__ last, const AdamConsts* __restrict__ table,
+                                                           const int* __restrict__ step, float wd, float b2,
+                                                           float omb2, float eps, PendSrc ps, int rpw) {
+  adam_window2_body<D, DW, G>(p, m, v, map, nrows, F, chunk, last, table, step, wd, b2, omb2, eps, ps, rpw,
+                              blockIdx.x, gridDim.x, false);
 }
 
 // every row up to `step` (checkpoint / evaluation)

@@ -201,7 +201,7 @@ class DeferredSums:
         if _WGRAD_GROUP and transA and not transB and A2 is None and M % 8 == 0 and N % 8 == 0:
             # deferred to flush(): the step's weight gradients in one fbn_gemm_slabs_group launch
             # (their operands are not rewritten before it: stream order, buffers of this step)
-            nsplit = _lib.lib().fbn_gemm_slabs_split(M, N, K)
+            nsplit = _lib.lib().fbn_gemm_slabs_group_split(M, N, K)
             self.group.append((A.data_ptr(), B.data_ptr(), ws.data_ptr(), nbytes, 0, ptr(B2) or 0, M, N, K, lda,
                                ldb, 1, 0, 0, 0, ldb2, nseg if B2 is not None else INT_MAX, 0))
             self.keep += [A, B] + ([B2] if B2 is not None else [])

@@ -72,10 +72,13 @@ int fbn_gemm_slabs_split(int M, int N, int K);
  * backward: one tail instead of one per GEMM).  descs = host array of n records
  * {const void* A, *B; float* ws; size_t ws_bytes; const void* A2, *B2;
  *  int M, N, K, lda, ldb, transA, transB, lda2, kseg, ldb2, nseg, pad;}
- * with the meaning of fbn_gemm_slabs's arguments; each ws receives exactly the
- * fbn_gemm_slabs_split(M, N, K) slabs fbn_gemm_slabs would write (bit-identical).  Every problem:
- * transA = 1, transB = 0, K % 64 == 0, M, N, lda, ldb % 8 == 0, no A2. */
+ * with the meaning of fbn_gemm_slabs's arguments; each ws receives fbn_gemm_slabs_group_split(M, N, K)
+ * K-slabs (half fbn_gemm_slabs_split's by default; with FBN_GROUP_SPLIT_DIV=1 exactly the slabs
+ * fbn_gemm_slabs writes, bit for bit).  Every problem: transA = 1, transB = 0, K % 64 == 0,
+ * M, N, lda, ldb % 8 == 0, no A2. */
 int fbn_gemm_slabs_group(const void* descs, int n, void* stream);
+/* The K-slab count a problem takes inside fbn_gemm_slabs_group, host-only. */
+int fbn_gemm_slabs_group_split(int M, int N, int K);
 /* bf16 operands (as fbn_gemm with bf16 = a16 = b16 = 1), C stored in bf16 (C[m * ldc + n], rounded
  * once from the f32 accumulators); no bias, beta, remap or statistics.  The bf16-mode dgrad
  * dc = dh1 Wa of the MLP input (src/model_fibinet.py:126-130 autograd), read only by

@@ -276,9 +276,23 @@ def test_gemm_slabs_group_matches_separate_launches(hip_device):
     the MLP input's included."""
     import ctypes
     from ctr_recommendation_amd import _lib
+    import os
     st = _lib.stream_handle(hip_device)
     g = torch.Generator(device="cpu").manual_seed(5)
     lib = _lib.lib()
+    saved_div = os.environ.get("FBN_GROUP_SPLIT_DIV")
+    os.environ["FBN_GROUP_SPLIT_DIV"] = "1"     # the group on fbn_gemm_slabs's K partition
+    try:
+        _slabs_group_cases(hip_device, st, g, lib, _lib)
+    finally:
+        if saved_div is None:
+            os.environ.pop("FBN_GROUP_SPLIT_DIV", None)
+        else:
+            os.environ["FBN_GROUP_SPLIT_DIV"] = saved_div
+
+
+def _slabs_group_cases(hip_device, st, g, lib, _lib):
+    import ctypes
     for probs in ([(256, 512, 1024, 0), (512, 1920, 1024, 640), (128, 128, 5120, 0), (128, 128, 1024, 0)],
                   [(256, 512, 512, 0), (512, 240, 512, 0), (16, 16, 2560, 0), (16, 128, 512, 0)]):
         descs, refs, outs = [], [], []
@@ -307,3 +321,36 @@ def test_gemm_slabs_group_matches_separate_launches(hip_device):
         for (ref, n), (grp, *_), pr in zip(refs, outs, probs):
             assert torch.equal(ref[:n], grp[:n]), (pr, (ref[:n] - grp[:n]).abs().max().item(),
                                                    torch.isnan(grp[:n]).sum().item())
+
+
+@pytest.mark.gpu
+def test_gemm_slabs_group_default_partition_sums(hip_device):
+    """With its default K partition (half fbn_gemm_slabs's slabs) the group's slab SUM -- what the
+    step's sum launch turns into the weight gradient -- equals the separate launch's within fp32
+    rounding of a K-long dot product (1e-5 relative to the largest entry)."""
+    import ctypes
+    import os
+    from ctr_recommendation_amd import _lib
+    assert "FBN_GROUP_SPLIT_DIV" not in os.environ
+    st = _lib.stream_handle(hip_device)
+    g = torch.Generator(device="cpu").manual_seed(9)
+    lib = _lib.lib()
+    for (M, N, K) in ((512, 1920, 8192), (256, 512, 8192), (128, 128, 40960), (128, 128, 8192)):
+        A = torch.randn(K, M, generator=g).to(hip_device, torch.bfloat16)
+        Bm = torch.randn(K, N, generator=g).to(hip_device, torch.bfloat16)
+        nbytes = lib.fbn_gemm_slabs_size(M, N, K)
+        ns, ng = lib.fbn_gemm_slabs_split(M, N, K), lib.fbn_gemm_slabs_group_split(M, N, K)
+        assert 1 <= ng <= ns
+        ws_ref = torch.zeros((nbytes // 4,), device=hip_device)
+        ws_grp = torch.zeros((nbytes // 4,), device=hip_device)
+        nsp = ctypes.c_int(0)
+        _lib.call("fbn_gemm_slabs", _lib.ptr(A), _lib.ptr(Bm), M, N, K, M, N, 1, 0, _lib.ptr(ws_ref), nbytes, None, 0,
+                  0x7FFFFFFF, None, 0, 0x7FFFFFFF, ctypes.byref(nsp), st)
+        arr = (ops._SlabGemm * 1)(ops._SlabGemm(A.data_ptr(), Bm.data_ptr(), ws_grp.data_ptr(), nbytes, 0, 0, M, N, K,
+                                                M, N, 1, 0, 0, 0, 0, 0x7FFFFFFF, 0))
+        _lib.call("fbn_gemm_slabs_group", ctypes.addressof(arr), 1, st)
+        torch.cuda.synchronize()
+        ref = ws_ref[:ns * M * N].view(ns, M, N).sum(0)
+        grp = ws_grp[:ng * M * N].view(ng, M, N).sum(0)
+        exact = A.float().t() @ Bm.float()
+        assert (grp - ref).abs().max().item() <= 1e-5 * exact.abs().max().item(), (M, N, K)

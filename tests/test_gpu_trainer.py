@@ -395,10 +395,13 @@ def test_graph_eager_interleave_bit_identical(hip_device):
 @pytest.mark.parametrize("d,B", [(128, 1024), (16, 512)])
 def test_wgrad_group_bit_identical(hip_device, d, B):
     """The step's weight-gradient GEMMs deferred to ONE grouped launch at the end of the backward
-    (fbn_gemm_slabs_group, ops._WGRAD_GROUP) write the same K-slabs as launching each in place:
+    (fbn_gemm_slabs_group, ops._WGRAD_GROUP), on fbn_gemm_slabs's K partition
+    (FBN_GROUP_SPLIT_DIV=1; the default halves the slab count), write the same K-slabs as
+    launching each in place:
     every output element's K-chunk goes through the same 32x32x16 MFMA sequence whatever the
     group's tile shape.  Three bf16 steps with and without grouping: losses, dense parameters and
     moments, table and its moments bit-identical."""
+    import os
     from ctr_recommendation_amd import ops
     V = 30000
     cfg = {"embedding_dim": d, "vocab_size": V, "compute_dtype": "bf16"}
@@ -410,6 +413,8 @@ def test_wgrad_group_bit_identical(hip_device, d, B):
         batches.append(({k: v.to(hip_device) for k, v in b.items()}, y.to(hip_device)))
     runs = []
     saved = ops._WGRAD_GROUP
+    saved_div = os.environ.get("FBN_GROUP_SPLIT_DIV")
+    os.environ["FBN_GROUP_SPLIT_DIV"] = "1"     # fbn_gemm_slabs's own K partition (read per call)
     try:
         for grouped in (False, True):
             ops._WGRAD_GROUP = grouped
@@ -421,6 +426,10 @@ def test_wgrad_group_bit_identical(hip_device, d, B):
             runs.append((losses, [t.clone() for t in (tr.flat_p, tr.flat_m, tr.E, tr.Em, tr.Ev)]))
     finally:
         ops._WGRAD_GROUP = saved
+        if saved_div is None:
+            os.environ.pop("FBN_GROUP_SPLIT_DIV", None)
+        else:
+            os.environ["FBN_GROUP_SPLIT_DIV"] = saved_div
     assert runs[0][0] == runs[1][0]
     for name, a, c in zip(("p", "m", "E", "Em", "Ev"), runs[0][1], runs[1][1]):
         bad = (a != c).nonzero()
