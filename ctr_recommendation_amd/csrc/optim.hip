@@ -1232,12 +1232,20 @@ __device__ __forceinline__ f32x4 consts4(const AdamConsts& k) { return (f32x4){k
 
 // One group of the replay engine: G wave-wide rows (cur, rows cr, replay starts ck, deferred
 // vectors cp; slots past cnt carry row 0 and no steps) brought to T, then stored.
-template <int D, bool DW, int G>
+// ABL (measurement only, tools/pf_ablation.py): 1 = no arithmetic (rows loaded and stored as they
+// are), 2 = no row traffic (zero rows, stores behind a run-time false flag); 0 = the real replay
+template <int D, bool DW, int G, int ABL = 0>
 __device__ __forceinline__ void replay_group(WideRow<D> (&cur)[G], const int (&cr)[G], const int (&ck)[G],
                                              const int (&cp)[G], int j0, int cnt, int T, float* __restrict__ p,
                                              float* __restrict__ m, float* __restrict__ v,
                                              const AdamConsts* __restrict__ table, float wd, float b2, float omb2,
-                                             float eps, int lane) {
+                                             float eps, int lane, bool sink = true) {
+  if constexpr (ABL == 1) {
+#pragma unroll
+    for (int x = 0; x < G; ++x)
+      if (j0 + x < cnt) wide_store<D>(cur[x], p, m, v, cr[x], lane);
+    return;
+  }
   typedef typename WideRow<D>::V V;
   constexpr int N = WideRow<D>::N;
   const V zero = {};
@@ -1248,30 +1256,26 @@ __device__ __forceinline__ void replay_group(WideRow<D> (&cur)[G], const int (&c
   for (int x = 0; x < G; ++x)
     if (cp[x] >= 0) adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, cur[x].g * cur[x].c, wd, b2, omb2, eps,
                                      consts4(table[ck[x] - 1]));
-  // END-aligned: every row replays up to T, so from the group's latest start on, all G rows
-  // are at the SAME step and share one set of constants; before it, the earlier-starting rows
-  // catch up to that start one by one (short after the sort)
-  int smax = ck[0];
+  // END-aligned staircase: every row replays up to T and the rows are sorted by start (ck
+  // ascending; slots past cnt start at T), so at step s the rows x with ck[x] <= s are all at the
+  // SAME step and share one set of constants -- read by a scalar load one step ahead.  Phase k runs
+  // rows 0..k from ck[k] to ck[k+1] (ck[G] = T): the longest row never replays alone while a later
+  // row could join it, and no step waits on its own constants' load.
+  int s = ck[0] < T ? ck[0] : T;
+  f32x4 kc = consts4(table[s]);   // table row T exists
 #pragma unroll
-  for (int x = 1; x < G; ++x)
-    if (j0 + x < cnt) smax = max(smax, ck[x]);
+  for (int k = 0; k < G; ++k) {
+    const int send = k + 1 < G ? min(ck[k + 1], T) : T;
+    for (; s < send; ++s) {
+      const f32x4 kn = consts4(table[s + 1]);   // a step ahead
 #pragma unroll
-  for (int x = 0; x < G; ++x)
-    if (j0 + x < cnt)
-      for (int s = ck[x]; s < smax; ++s)
-        adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, zero, wd, b2, omb2, eps, consts4(table[s]));
-  if (smax < T) {
-    f32x4 kc = consts4(table[smax]);
-    for (int s = smax; s < T; ++s) {
-      const f32x4 kn = consts4(table[s + 1]);   // a step ahead (table row T exists)
-#pragma unroll
-      for (int x = 0; x < G; ++x) adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, zero, wd, b2, omb2, eps, kc);
+      for (int x = 0; x <= k; ++x) adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, zero, wd, b2, omb2, eps, kc);
       kc = kn;
     }
   }
 #pragma unroll
   for (int x = 0; x < G; ++x)
-    if (j0 + x < cnt) wide_store<D>(cur[x], p, m, v, cr[x], lane);
+    if (j0 + x < cnt && (ABL != 2 || sink)) wide_store<D>(cur[x], p, m, v, cr[x], lane);
 }
 
 // The replay engine of the two-pass prefetch and the window pass: a wave's rows (one per lane:
@@ -1279,7 +1283,7 @@ __device__ __forceinline__ void replay_group(WideRow<D> (&cur)[G], const int (&c
 // brought to T steps G at a time, the next group's loads in flight while one replays.
 // G = 4 by default; G = 2 holds half the rows' registers (a smaller footprint beside the main
 // stream's kernels, fewer independent update chains per lane).
-template <int D, bool DW, int G = 4>
+template <int D, bool DW, int G = 4, int ABL = 0>
 __device__ __forceinline__ void replay4_sorted(int r, int key, int pe, int cnt, int T, int w0,
                                                const f32x4* __restrict__ win, float* __restrict__ p,
                                                float* __restrict__ m, float* __restrict__ v,
@@ -1314,14 +1318,20 @@ __device__ __forceinline__ void replay4_sorted(int r, int key, int pe, int cnt, 
 #pragma unroll
     for (int x = 0; x < G; ++x) {
       get(j + x, g.r[x], g.k[x], g.p[x]);
-      wide_load<D>(g.w[x], p, m, v, g.r[x], g.p[x] >= 0 ? g.k[x] - 1 : g.k[x], g.p[x], ps, lane);
+      if constexpr (ABL == 2) {
+        g.w[x].p = g.w[x].m = g.w[x].v = g.w[x].g = (typename WideRow<D>::V){};
+        g.w[x].c = 1.f;
+      } else {
+        wide_load<D>(g.w[x], p, m, v, g.r[x], g.p[x] >= 0 ? g.k[x] - 1 : g.k[x], g.p[x], ps, lane);
+      }
     }
   };
   Grp a, b;
   fill(a, 0);
   for (int j0 = 0; j0 < cnt; j0 += G) {
     fill(b, j0 + G);
-    replay_group<D, DW, G>(a.w, a.r, a.k, a.p, j0, cnt, T, p, m, v, table, wd, b2, omb2, eps, lane);
+    replay_group<D, DW, G, ABL>(a.w, a.r, a.k, a.p, j0, cnt, T, p, m, v, table, wd, b2, omb2, eps, lane,
+                                ABL != 2 || wd == 12345.f);
     a = b;
   }
 }
@@ -1408,17 +1418,17 @@ __device__ __forceinline__ void replay_narrow_sorted(int r, int key, int pe, int
   }
 }
 
-template <int D, bool DW, int G = 4>
+template <int D, bool DW, int G = 4, int ABL = 0>
 __device__ __forceinline__ void replay_sorted(int r, int key, int pe, int cnt, int T, int w0,
                                               const f32x4* __restrict__ win, float* __restrict__ p,
                                               float* __restrict__ m, float* __restrict__ v,
                                               const AdamConsts* __restrict__ table, float wd, float b2, float omb2,
                                               float eps, const PendSrc& ps, int lane) {
-  if constexpr (D >= 128) replay4_sorted<D, DW, G>(r, key, pe, cnt, T, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
+  if constexpr (D >= 128) replay4_sorted<D, DW, G, ABL>(r, key, pe, cnt, T, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
   else replay_narrow_sorted<D, DW>(r, key, pe, cnt, T, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
 }
 
-template <int D, bool DW, int G = 4>
+template <int D, bool DW, int G = 4, int ABL = 0>
 __device__ __forceinline__ void adam_prefetch2_body(float* __restrict__ p, float* __restrict__ m,
                                                     float* __restrict__ v, const ClaimSrc& cs, int n,
                                                     int* __restrict__ last, const AdamConsts* __restrict__ table,
@@ -1458,18 +1468,18 @@ __device__ __forceinline__ void adam_prefetch2_body(float* __restrict__ p, float
   }
   const int cnt = __popcll(__ballot(key != 0x7fffffff));
   if (cnt == 0) continue;
-  replay_sorted<D, DW, G>(r, key, pe, cnt, T, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
+  replay_sorted<D, DW, G, ABL>(r, key, pe, cnt, T, w0, win, p, m, v, table, wd, b2, omb2, eps, ps, lane);
   }
 }
-template <int D, bool DW, int G = 4>
+template <int D, bool DW, int G = 4, int ABL = 0>
 __global__ void __launch_bounds__(256) adam_prefetch2_kernel(float* __restrict__ p, float* __restrict__ m,
                                                              float* __restrict__ v, ClaimSrc cs, int n,
                                                              int* __restrict__ last,
                                                              const AdamConsts* __restrict__ table,
                                                              const int* __restrict__ step, float wd, float b2,
                                                              float omb2, float eps, PendSrc ps, int epw) {
-  adam_prefetch2_body<D, DW, G>(p, m, v, cs, n, last, table, step, wd, b2, omb2, eps, ps, epw, blockIdx.x,
-                                gridDim.x);
+  adam_prefetch2_body<D, DW, G, ABL>(p, m, v, cs, n, last, table, step, wd, b2, omb2, eps, ps, epw, blockIdx.x,
+                                     gridDim.x);
 }
 
 // Single GPU, D >= 128: the step's row claims + the claimed rows' catch-up (fbn_adam_claim_catchup)
@@ -2296,6 +2306,19 @@ extern "C" int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B,
     long long waves = (n + epw - 1) / epw;
     if (wc && atoll(wc) > 0) waves = std::min(waves, atoll(wc));
     const dim3 g3((unsigned)((waves + 3) / 4));   // 4 waves per block
+    // FBN_PF_ABL (measurement only, tools/pf_ablation.py; results are NOT a valid Adam step):
+    // 1 = the replay without its arithmetic, 2 = without its row traffic
+    const char* ab = getenv("FBN_PF_ABL");
+    if (D == 128 && !decoupled && ab && (atoi(ab) == 1 || atoi(ab) == 2)) {
+      if (atoi(ab) == 1)
+        hipLaunchKernelGGL((adam_prefetch2_kernel<128, false, 4, 1>), g3, dim3(256), 0, st, p, m, v, cs, (int)n,
+                           last, (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, epw);
+      else
+        hipLaunchKernelGGL((adam_prefetch2_kernel<128, false, 4, 2>), g3, dim3(256), 0, st, p, m, v, cs, (int)n,
+                           last, (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, epw);
+      FBN_CHECK_LAUNCH();
+      return FBN_OK;
+    }
     // FBN_PF_G: rows per replay group (4, or 2 for half the register footprint; A/B knob)
     const char* ge = getenv("FBN_PF_G");
     if (D >= 128 && ge && atoi(ge) == 2) {
