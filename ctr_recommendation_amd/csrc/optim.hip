@@ -2306,11 +2306,18 @@ extern "C" int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B,
     long long waves = (n + epw - 1) / epw;
     if (wc && atoll(wc) > 0) waves = std::min(waves, atoll(wc));
     const dim3 g3((unsigned)((waves + 3) / 4));   // 4 waves per block
-    // FBN_PF_ABL (measurement only, tools/pf_ablation.py; results are NOT a valid Adam step):
-    // 1 = the replay without its arithmetic, 2 = without its row traffic
+    // FBN_PF_ABL (measurement only, tools/pf_ablation.py; 1 and 2 are NOT a valid Adam step):
+    // 1 = the replay without its arithmetic, 2 = without its row traffic; 3 = groups of 8 rows
+    // (valid), 4 = groups of 8 without row traffic
     const char* ab = getenv("FBN_PF_ABL");
-    if (D == 128 && !decoupled && ab && (atoi(ab) == 1 || atoi(ab) == 2)) {
-      if (atoi(ab) == 1)
+    if (D == 128 && !decoupled && ab && (atoi(ab) == 1 || atoi(ab) == 2 || atoi(ab) == 3 || atoi(ab) == 4)) {
+      if (atoi(ab) == 3)   // groups of 8 rows (diagnosis: more independent update chains per wave)
+        hipLaunchKernelGGL((adam_prefetch2_kernel<128, false, 8, 0>), g3, dim3(256), 0, st, p, m, v, cs, (int)n,
+                           last, (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, epw);
+      else if (atoi(ab) == 4)   // groups of 8 rows without row traffic
+        hipLaunchKernelGGL((adam_prefetch2_kernel<128, false, 8, 2>), g3, dim3(256), 0, st, p, m, v, cs, (int)n,
+                           last, (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, epw);
+      else if (atoi(ab) == 1)
         hipLaunchKernelGGL((adam_prefetch2_kernel<128, false, 4, 1>), g3, dim3(256), 0, st, p, m, v, cs, (int)n,
                            last, (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, epw);
       else

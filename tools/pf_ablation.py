@@ -1,7 +1,8 @@
 """What bounds the next-batch prefetch (adam_prefetch2_kernel, C3, uniform ids, steady state):
 its launch timed alone (serialised probe steps: side work on the main stream behind a GPU sleep)
 as is, without its arithmetic (FBN_PF_ABL=1: rows loaded and stored unchanged) and without its
-row traffic (FBN_PF_ABL=2: the replay on zero rows, nothing stored).  The ablations leave the
+row traffic (FBN_PF_ABL=2: the replay on zero rows, nothing stored), and with groups of 8 rows
+(3; 4 = that without row traffic).  The ablations leave the
 table wrong: only their launch times mean anything.  Prints the median launch time per arm."""
 import os
 import sys
@@ -27,7 +28,7 @@ side = tr.side
 tr.side = torch.cuda.current_stream(dev)
 res = {}
 for rnd in range(3):
-    for arm in ("real", "1", "2"):
+    for arm in ("real", "1", "2", "3", "4"):
         if arm == "real":
             os.environ.pop("FBN_PF_ABL", None)
         else:
@@ -42,7 +43,8 @@ for rnd in range(3):
         res.setdefault(arm, []).extend(ts)
 os.environ.pop("FBN_PF_ABL", None)
 tr.side = side
-names = {"real": "prefetch as is", "1": "no arithmetic (rows in / out)", "2": "no row traffic (arithmetic)"}
+names = {"real": "prefetch as is", "1": "no arithmetic (rows in / out)", "2": "no row traffic (arithmetic)",
+         "3": "groups of 8 rows", "4": "groups of 8, no row traffic"}
 for arm, v in res.items():
     v = sorted(v)
     print(f"{names[arm]:32s} median {v[len(v) // 2]:.1f} us  min {v[0]:.1f}  n {len(v)}")
