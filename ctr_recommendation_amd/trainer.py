@@ -50,6 +50,10 @@ _SIDE_AFTER_MMPROJ = os.environ.get("FBN_SIDE_AFTER_MMPROJ", "0") == "1"
 #   FBN_CLAIM_ON_SIDE=1  the row claims + claimed-row catch-up on the side stream from the step's
 #                        start, beside the bf16 weight images and the mm_proj GEMM (+15 us/step)
 #   FBN_FIXUP_ON_SIDE=1  the duplicate-gradient fold on the side stream after the fields backward
+#                        (round 3's first half: +2-3 us; since the weight gradients run as one grouped
+#                        launch after the fields backward the fold hides beside it: 0.4290 vs 0.4321
+#                        ms/step, profiles/r03s2_group_knobs_ab.txt -- so "auto", the default, puts it
+#                        there whenever the side stream is in use)
 #                        (+2-3 us/step)
 #   FBN_SIDE_SERIAL=1    the rolling window + next-batch prefetch on the main stream, in sequence
 #                        (0.5128 vs 0.4629 ms/step at C3: the overlap is worth 50 us there)
@@ -66,7 +70,7 @@ _SIDE_SERIAL = os.environ.get("FBN_SIDE_SERIAL", "auto")
 # prefetch (default), "pw" the prefetch first, "p_w" the prefetch at the fork and the window only
 # once the backward starts (the side stream waits for the forward)
 _SIDE_ORDER = os.environ.get("FBN_SIDE_ORDER", "wp")
-_FIXUP_ON_SIDE = os.environ.get("FBN_FIXUP_ON_SIDE", "0") == "1"
+_FIXUP_ON_SIDE = os.environ.get("FBN_FIXUP_ON_SIDE", "auto")
 # ... or after the gather (fields_fwd then runs with the chip to itself; A/B knob)
 _SIDE_AFTER_GATHER = os.environ.get("FBN_SIDE_AFTER_GATHER", "0") == "1"
 # N > 1: the next batch's routing enqueued after this step's compute (A/B knob)
@@ -605,7 +609,8 @@ class FiBiNETTrainer:
         if w16_ev is not None:
             main.wait_event(w16_ev)
         graphed = False
-        fixup_side = (self.xchg is None and _FIXUP_ON_SIDE and not self.deterministic and L > 0
+        fixup_side = (self.xchg is None and (_FIXUP_ON_SIDE == "1" or (_FIXUP_ON_SIDE == "auto" and not self.side_serial))
+                      and not self.deterministic and L > 0
                       and not self._early_grad_xchg())
         if (self.xchg is not None and self.shard_graph and probe is None and masks_out is None
                 and self.table_adam != "eager"):
