@@ -172,6 +172,7 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
     from ctr_recommendation_amd.data import make_device_batches
     from ctr_recommendation_amd import ops
     from ctr_recommendation_amd.trainer import FiBiNETTrainer
+    from ctr_recommendation_amd import trainer as trmod
 
     d, B, L = args.dim, args.batch, 20
     V = args.rows_per_gpu * world
@@ -358,10 +359,17 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
     dfr = getattr(tr, "deferred", False)
     # claimed-row catch-up: every entry's id, claim, slot and last (20 B) + the rows it replays
     crit = stale if prefetch else touched
-    add("adam_catchup", "adam_catchup (lazy table Adam: rows claimed this step)", avg_ms("adam_catchup"),
-        catchup_bytes(crit, d, 5 * B * (L + 1)) + (crit * (4 * d + 8) if dfr else 0), "GB/s", HBM_PEAK_GBS, "hbm",
+    # the step head: the claims' launch also converts the bf16 operand images (fbn_adam_claim_catchup_conv):
+    # Wa, Wa^T (512 x 15d), Wb, Wb^T (256 x 512), W, W^T (d x d), Wp (d x 128), x (B x 128); 4 B in, 2 B out
+    head_conv = world == 1 and dtype == "bf16" and trmod._HEAD_CONV and trmod._W16_MODE == "main"
+    conv_bytes = 6 * (2 * 512 * 15 * d + 2 * 256 * 512 + 2 * d * d + d * 128 + B * 128) if head_conv else 0
+    add("adam_catchup", "adam_catchup (lazy table Adam: rows claimed this step"
+        + ("; the bf16 image conversion in the same launch)" if head_conv else ")"), avg_ms("adam_catchup"),
+        catchup_bytes(crit, d, 5 * B * (L + 1)) + (crit * (4 * d + 8) if dfr else 0) + conv_bytes, "GB/s",
+        HBM_PEAK_GBS, "hbm",
         f"{B * (L + 1)} entries x 20 B + {crit} replayed rows x (24 B x d + 8 B"
-        f"{' + 4 B x d + 8 B deferred gradient' if dfr else ''}); mean lag {lag:.1f} steps over the {touched} rows")
+        f"{' + 4 B x d + 8 B deferred gradient' if dfr else ''}); mean lag {lag:.1f} steps over the {touched} rows"
+        + (f" + {conv_bytes} B of bf16 images (6 B per element)" if head_conv else ""))
     if prefetch:
         ahead = max(0, touched - stale)
         pf_work = catchup_bytes(ahead, d, 5 * B * (L + 1)) + (ahead * (4 * d + 8) if dfr else 0)
