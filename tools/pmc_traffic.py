@@ -21,7 +21,7 @@ KERNELS = {
     "fields_fwd": ("fields_fwd_kernel<128", None, None),
     # the claimed-row catch-up (fused with the row claims), the rolling window and the next-batch
     # prefetch's two passes (the bench's events bracket both; summed below)
-    "adam_catchup": ("adam_claim2_kernel<128", None, None),
+    "adam_catchup": ("adam_claim2_conv_kernel<128", None, None),   # the step head (claims + bf16 images)
     "adam_window": ("adam_window2_kernel<128", None, None),
     "adam_prefetch": ("adam_prefetch2_kernel<128", None, None),
     "adam_pretag": ("adam_pretag_kernel", None, None),
@@ -29,6 +29,8 @@ KERNELS = {
     "adam_touched": ("adam_touched_kernel<128", None, None),
     "adam_commit": ("adam_commit_kernel<128", None, None),
     "adam_tail": ("adam_tail_kernel<128", None, None),
+    "wgrad_group": ("gemm_dma16_group_kernel<128, 128", None, None),
+    "sum_jobs": ("sum_jobs_kernel", None, None),
 }
 
 
