@@ -744,12 +744,38 @@ struct SumJobs {
   SlabJob s[FBN_MAX_SLAB_JOBS];
   int blk0[FBN_MAX_SLAB_JOBS + 1];   // first block of each slab job (after the column blocks)
   int ns;
+  int direct;                        // slab jobs of <= FBN_SLAB_DIRECT slabs: slab_direct
 };
+// slab jobs of at most FBN_SLAB_DIRECT slabs: one output quad per thread, every slab's load in
+// flight at once, summed in slab order (no LDS fold; a quarter of the blocks)
+#define FBN_SLAB_DIRECT 8
+__device__ __forceinline__ void slab_direct(const SlabJob& sj, int lb) {
+  const size_t total = (size_t)sj.M * sj.N;
+  const size_t i4 = (size_t)lb * 256 + threadIdx.x;
+  if (i4 >= total / 4) return;
+  const float* src = sj.ws + i4 * 4;
+  f32x4 x[FBN_SLAB_DIRECT];
+#pragma unroll
+  for (int z = 0; z < FBN_SLAB_DIRECT; ++z)
+    if (z < sj.nsplit) x[z] = *reinterpret_cast<const f32x4*>(src + (size_t)z * total);
+  f32x4 t = x[0];
+#pragma unroll
+  for (int z = 1; z < FBN_SLAB_DIRECT; ++z)
+    if (z < sj.nsplit) t += x[z];
+  const int m = (int)(i4 * 4 / sj.N), n = (int)(i4 * 4 - (size_t)m * sj.N);
+  float* cp = sj.out + (size_t)m * sj.ldc + n + (n < sj.seg ? sj.off0 : sj.off1);
+  if (sj.beta != 0.f) t += sj.beta * *reinterpret_cast<const f32x4*>(cp);
+  *reinterpret_cast<f32x4*>(cp) = t;
+}
 __device__ __forceinline__ void slab_block(const SumJobs& J, int gb) {
   __shared__ f32x4 red[FBN_SLAB_GROUPS][64];
   int u = 0;
   while (u + 1 < J.ns && gb >= J.blk0[u + 1]) ++u;
   const SlabJob sj = J.s[u];
+  if (J.direct && sj.nsplit <= FBN_SLAB_DIRECT) {
+    slab_direct(sj, gb - J.blk0[u]);
+    return;
+  }
   const int qd = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const size_t total = (size_t)sj.M * sj.N;
   const size_t i4 = (size_t)(gb - J.blk0[u]) * 64 + qd;   // output quad
@@ -1277,6 +1303,8 @@ extern "C" int fbn_sum_jobs2(const SumJob* jobs, int n, const SlabJob* slabs, in
     J.col0[i + 1] = J.col0[i] + (jobs[i].C >= FBN_SUM_WIDE ? fbn_cdiv(jobs[i].C, 16) : jobs[i].C);
   }
   J.ns = ns;
+  const char* de = getenv("FBN_SLAB_DIRECT");   // A/B knob (0: the 4-group LDS fold for every slab job)
+  J.direct = !(de && atoi(de) == 0);
   J.blk0[0] = 0;
   for (int i = 0; i < ns; ++i) {
     const SlabJob& sj = slabs[i];
@@ -1286,7 +1314,8 @@ extern "C" int fbn_sum_jobs2(const SumJob* jobs, int n, const SlabJob* slabs, in
       return FBN_ERR_ARG;
     }
     J.s[i] = sj;
-    J.blk0[i + 1] = J.blk0[i] + (int)fbn_cdiv((long long)sj.M * sj.N / 4, 64);
+    const int qpb = (J.direct && sj.nsplit <= FBN_SLAB_DIRECT) ? 256 : 64;   // output quads per block
+    J.blk0[i + 1] = J.blk0[i] + (int)fbn_cdiv((long long)sj.M * sj.N / 4, qpb);
   }
   const int blocks = J.col0[n] + J.blk0[ns];
   if (blocks <= 0) return FBN_OK;
