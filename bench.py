@@ -64,7 +64,8 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=20)
     ap.add_argument("--probe-steps", type=int, default=10)
     ap.add_argument("--batches", type=int, default=0, help="distinct HBM-resident batches (default F + 32)")
-    ap.add_argument("--lazy-window", type=int, default=128, help="lazy table-Adam window F (rows per step: V/F)")
+    ap.add_argument("--lazy-window", type=int, default=0,
+                    help="lazy table-Adam window F (rows per step: V/F; default: the trainer's, 128 at d >= 128, else 32)")
     ap.add_argument("--zipf", type=float, default=0.0,
                     help="item / history ids ~ Zipf(s) (SURVEY 8(d): 1.05) instead of uniform")
     ap.add_argument("--table-adam", default="lazy", choices=["lazy", "eager", "sparse"],
@@ -178,7 +179,8 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
     V = args.rows_per_gpu * world
     cfg = {"embedding_dim": d, "vocab_size": V, "compute_dtype": dtype}
     K, W = args.steps, args.warmup
-    F = args.lazy_window                      # lazy table-Adam window (FiBiNETTrainer default 128)
+    from ctr_recommendation_amd.trainer import default_lazy_window
+    F = args.lazy_window or default_lazy_window(d)   # lazy table-Adam window (the trainer's default)
     # fresh ids every step: more distinct HBM-resident batches than the window F, so every row a
     # timed step claims was last touched at the lag fresh uniform ids give (bounded by F), never
     # replayed from a batch seen a few steps earlier
@@ -393,6 +395,10 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
         add("gemm_mlp0", f"gemm MLP layer 1 alone (eval-mode forward, no side-stream work, {dtype} MFMA)",
             avg_ms("gemm_mlp0", iso), 2.0 * B * 512 * 15 * d, "TFLOP/s",
             MFMA_PEAK_TFS if dtype == "bf16" else FP32_MFMA_PEAK_TFS, "mfma", "2 x B x 512 x 15d")
+    # the four weight-gradient GEMMs in their one grouped launch (bf16 mode): dWa, dWb, dW, dWp
+    add("wgrad_group", "gemm weight gradients, grouped launch (dWa + dWb + dW + dWp, bf16 MFMA)",
+        avg_ms("wgrad_group"), 2.0 * B * (512 * 15 * d + 256 * 512 + 5 * d * d + 128 * d), "TFLOP/s", MFMA_PEAK_TFS,
+        "mfma", "2 x B x (512 x 15d + 256 x 512 + 5 d^2 + 128 d)")
     if tr.table_adam == "eager":
         add("adam_table", "adam_table (eager: every untouched row each step)", avg_ms("adam_table"),
             24 * tr.rows_local * d + 4 * tr.rows_local, "GB/s", HBM_PEAK_GBS, "hbm", "24 B x rows x d + 4 B x rows")

@@ -219,12 +219,19 @@ class DeferredSums:
         call("fbn_colsum_partial", ptr(X), B, C, ldx, ptr(part), stream)
         self.add(part, nch, C, out)
 
-    def flush(self, stream):
+    def flush(self, stream, probe: Optional[Dict[str, list]] = None):
         group = self.group
+        ev = None
+        if group and probe is not None:             # bench: HIP events around the grouped launch
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+            probe.setdefault("wgrad_group", []).append(ev)
         while group:
             gc, group = group[:6], group[6:]
             garr = (_SlabGemm * len(gc))(*[_SlabGemm(*x) for x in gc])
             call("fbn_gemm_slabs_group", ctypes.addressof(garr), len(gc), stream)
+        if ev is not None:
+            ev[1].record()
         self.group = []
         jobs, slabs = self.jobs, self.slabs
         while jobs or slabs:
@@ -756,5 +763,5 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
                               False, stream=s))
     for job in extra_sums:              # e.g. the trainer's mean loss
         sums.add(*job)
-    sums.flush(st)
+    sums.flush(st, probe)
     wg.join()

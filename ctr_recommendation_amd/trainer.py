@@ -108,6 +108,15 @@ def _events_end(e, stream=None):
         e.record(stream)
 
 
+def default_lazy_window(d: int) -> int:
+    """The rolling window F of the lazy table Adam (every row is visited at least once per F steps;
+    the deferred-gradient ring holds F + 1 steps).  The window pass is bound by its longest replay
+    chain (lags up to F), not by its rows: at C3 (d = 128) F = 128 measured best (64 / 32: +9 / +22
+    us per step), at C2 (d = 16, the side passes in sequence on the main stream) F = 32 (0.264 vs
+    0.287 ms/step at 128; 16 / 8 within noise of 32) -- profiles/r03s2_lazy_window_sweep.txt."""
+    return 128 if d >= 128 else 32
+
+
 def _side_stream(dev):
     """The side stream; FBN_SIDE_CU_MASK=<hex word>[,<hex word>...] (32 CUs per word, repeated to
     cover the device) restricts it to a CU subset (hipExtStreamCreateWithCUMask) -- tuning knob
@@ -209,7 +218,7 @@ class FiBiNETTrainer:
                  lr: Optional[float] = None, weight_decay: Optional[float] = None, rank: int = 0, world: int = 1,
                  group=None, init_state: Optional[Dict[str, torch.Tensor]] = None, seed: int = 2025,
                  stage_on_cpu: bool = False, dropout_seed: Optional[int] = None, table_adam: str = "lazy",
-                 lazy_window: int = 128, defer_table_grads: bool = True, max_norm: float = 10.0,
+                 lazy_window: Optional[int] = None, defer_table_grads: bool = True, max_norm: float = 10.0,
                  optimizer: Optional[str] = None, deterministic: Optional[bool] = None,
                  prefetch_rows: bool = True, shard: Optional[bool] = None, sync_bn: Optional[bool] = None):
         self.device = torch.device(device if device is not None else "cuda")
@@ -362,7 +371,7 @@ class FiBiNETTrainer:
         self.table_adam = os.environ.get("FBN_TABLE_ADAM", table_adam)
         if self.table_adam not in ("lazy", "eager", "sparse"):
             raise ValueError(f"table_adam must be 'lazy', 'eager' or 'sparse', not {self.table_adam!r}")
-        self.lazy_window = int(lazy_window)
+        self.lazy_window = int(lazy_window) if lazy_window is not None else default_lazy_window(d)
         # single GPU: the side-stream table-Adam passes in sequence on the main stream (see _SIDE_SERIAL)
         self.side_serial = _SIDE_SERIAL == "1" or (_SIDE_SERIAL == "auto" and d < 128)
         self.last = self.row_state[:, 2]     # Adam steps applied per table row
