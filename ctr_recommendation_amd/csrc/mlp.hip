@@ -504,17 +504,42 @@ __global__ void bn_tile_finalize_kernel(const float* __restrict__ part, int T, i
   const int c = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (c >= C) return;
-  double s = 0.0;
-  for (int t = lane; t < T; t += 64) s += (double)part[((size_t)t * C + c) * 2];
+  double s = 0.0, q = 0.0, mu;
+  if (T <= 256) {
+    // one round trip: every (sum, M2) pair of this lane's tiles loaded at once and kept in
+    // registers for both passes (same operations, same order as the loop below)
+    float2 sm[4];
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-  const double mu = s / ntot;
-  double q = 0.0;
-  for (int t = lane; t < T; t += 64) {
-    const float S = part[((size_t)t * C + c) * 2], M2 = part[((size_t)t * C + c) * 2 + 1];
-    const int nt = min(tile_rows, M - t * tile_rows);
-    const double dm = (double)S / nt - mu;
-    q += (double)M2 + nt * dm * dm;
+    for (int j = 0; j < 4; ++j) {
+      const int t = lane + 64 * j;
+      sm[j] = t < T ? *reinterpret_cast<const float2*>(part + ((size_t)t * C + c) * 2) : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (lane + 64 * j < T) s += (double)sm[j].x;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    mu = s / ntot;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = lane + 64 * j;
+      if (t < T) {
+        const int nt = min(tile_rows, M - t * tile_rows);
+        const double dm = (double)sm[j].x / nt - mu;
+        q += (double)sm[j].y + nt * dm * dm;
+      }
+    }
+  } else {
+    for (int t = lane; t < T; t += 64) s += (double)part[((size_t)t * C + c) * 2];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    mu = s / ntot;
+    for (int t = lane; t < T; t += 64) {
+      const float S = part[((size_t)t * C + c) * 2], M2 = part[((size_t)t * C + c) * 2 + 1];
+      const int nt = min(tile_rows, M - t * tile_rows);
+      const double dm = (double)S / nt - mu;
+      q += (double)M2 + nt * dm * dm;
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
