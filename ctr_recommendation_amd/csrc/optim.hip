@@ -2461,7 +2461,7 @@ static int claim_catchup_impl(const int64_t* item, const int64_t* seq, int B, in
   const long long n = (long long)B * (L + 1);
   ConvJobs cj;
   const int conv_tiles = n_conv > 0 ? conv_jobs_pack(conv_jobs, n_conv, cj) : 0;
-  if (conv_tiles > 0 && (n <= 0 || nrows <= 0 || D < 128)) {   // no claim launch to ride on: convert alone
+  if (conv_tiles > 0 && (n <= 0 || nrows <= 0)) {   // no claim launch to ride on: convert alone
     hipLaunchKernelGGL(convert_bf16_kernel_o, dim3(conv_tiles), dim3(256), 0, (hipStream_t)stream, cj, n_conv);
     FBN_CHECK_LAUNCH();
   }
@@ -2483,22 +2483,20 @@ static int claim_catchup_impl(const int64_t* item, const int64_t* seq, int B, in
   // one entry per lane, row state in one round trip, the replay engine (adam_claim2_kernel);
   // FBN_CLAIM_ONEPASS=1 keeps the scans of adam_catchup_kernel (A/B)
   static const bool cone = getenv("FBN_CLAIM_ONEPASS") && atoi(getenv("FBN_CLAIM_ONEPASS")) == 1;
-  if (conv_tiles > 0 && D >= 128 && !cone) {
+  if (conv_tiles > 0 && !cone) {
     const int nclaim = (int)((n + 255) / 256);
     const dim3 g2((unsigned)(nclaim + conv_tiles));
-#define FBN_CLAIM_CONV(DD, DW_)                                                                                  \
-  hipLaunchKernelGGL((adam_claim2_conv_kernel<DD, DW_>), g2, dim3(256), 0, st, p, m, v, cs, (int)n, last,        \
-                     (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, cj, n_conv, nclaim)
-    if (D == 128) {
-      if (decoupled) FBN_CLAIM_CONV(128, true); else FBN_CLAIM_CONV(128, false);
+    if (decoupled) {
+      FBN_DISPATCH_D_B(adam_claim2_conv_kernel, true, D, g2, p, m, v, cs, (int)n, last,
+                       (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, cj, n_conv, nclaim);
     } else {
-      if (decoupled) FBN_CLAIM_CONV(256, true); else FBN_CLAIM_CONV(256, false);
+      FBN_DISPATCH_D_B(adam_claim2_conv_kernel, false, D, g2, p, m, v, cs, (int)n, last,
+                       (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, cj, n_conv, nclaim);
     }
-#undef FBN_CLAIM_CONV
     FBN_CHECK_LAUNCH();
     return FBN_OK;
   }
-  if (conv_tiles > 0 && D >= 128) {   // FBN_CLAIM_ONEPASS: the images in their own launch first
+  if (conv_tiles > 0) {   // FBN_CLAIM_ONEPASS: the images in their own launch first
     hipLaunchKernelGGL(convert_bf16_kernel_o, dim3(conv_tiles), dim3(256), 0, st, cj, n_conv);
     FBN_CHECK_LAUNCH();
   }

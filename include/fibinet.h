@@ -339,9 +339,9 @@ int fbn_adam_claim_catchup(const int64_t* item, const int64_t* seq, int B, int L
                            const float* ring, const float* coef_hist, long long ring_stride, int ring_n, int decoupled,
                            void* stream);
 /* fbn_adam_claim_catchup with the step's bf16 image conversion (fbn_convert_bf16's n_conv <= 8
- * job records) in the same launch (D >= 128: claim blocks, then conversion blocks; otherwise the
- * conversion's own launch first) -- the two are independent: the images are of the weights the
- * previous step's tail wrote and of this batch's item_emb_d128 (src/model_fibinet.py:162). */
+ * job records) in the same launch (claim blocks, then conversion blocks) -- the two are
+ * independent: the images are of the weights the previous step's tail wrote and of this batch's
+ * item_emb_d128 (src/model_fibinet.py:162). */
 int fbn_adam_claim_catchup_conv(const int64_t* item, const int64_t* seq, int B, int L, long long V, int* map,
                                 int* slot_row, int* dup, int* hasdup, unsigned long long* preclaim, float* p,
                                 float* m, float* v, long long nrows, int D, int F, int* last,
