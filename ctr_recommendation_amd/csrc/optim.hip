@@ -1588,16 +1588,13 @@ __global__ void __launch_bounds__(256) convert_bf16_kernel_o(ConvJobs jobs, int 
 // steps each) spreads over thousands of waves instead of one wave per SIMD; claimed rows are left
 // to their claiming entry, as in adam_catchup_kernel.
 #define FBN_WIN_ROWS 16
-// tagged: leave the rows pre-claimed for the next step to a prefetch running in the same launch
-// (which brings them one step further; measured slower as one launch, profiles/r03s2_wgrad_group_head_ab.txt)
 template <int D, bool DW, int G = 4>
 __device__ __forceinline__ void adam_window2_body(float* __restrict__ p, float* __restrict__ m,
                                                   float* __restrict__ v, const int* __restrict__ map,
                                                   long long nrows, int F, long long chunk, int* __restrict__ last,
                                                   const AdamConsts* __restrict__ table,
                                                   const int* __restrict__ step, float wd, float b2, float omb2,
-                                                  float eps, const PendSrc& ps, int rpw, int blk, int nblk,
-                                                  bool tagged) {
+                                                  float eps, const PendSrc& ps, int rpw, int blk, int nblk) {
   __shared__ f32x4 win[FBN_PF_WIN + 1];   // constants of steps [w0, t]
   const int t = *step;
   const int w0 = t > FBN_PF_WIN ? t - FBN_PF_WIN : 0;
@@ -1616,7 +1613,7 @@ __device__ __forceinline__ void adam_window2_body(float* __restrict__ p, float* 
   if (lane < rpw && j < nroll) {
     const long long rr = roll0 + j;
     const int4 rs = row_state(last, rr);
-    if ((!map || map[rr] == -1) && !(tagged && rs.y == t + 1)) {
+    if (!map || map[rr] == -1) {
       const int k0 = rs.z;
       if (k0 < t) {
         r = (int)rr;
@@ -1640,7 +1637,7 @@ __global__ void __launch_bounds__(256) adam_window2_kernel(float* __restrict__ p
                                                            const int* __restrict__ step, float wd, float b2,
                                                            float omb2, float eps, PendSrc ps, int rpw) {
   adam_window2_body<D, DW, G>(p, m, v, map, nrows, F, chunk, last, table, step, wd, b2, omb2, eps, ps, rpw,
-                              blockIdx.x, gridDim.x, false);
+                              blockIdx.x, gridDim.x);
 }
 
 // every row up to `step` (checkpoint / evaluation)
