@@ -618,7 +618,9 @@ class FiBiNETTrainer:
         if w16_ev is not None:
             main.wait_event(w16_ev)
         graphed = False
-        fixup_side = (self.xchg is None and (_FIXUP_ON_SIDE == "1" or (_FIXUP_ON_SIDE == "auto" and not self.side_serial))
+        # (not inside a graph capture: there each cross-queue edge costs ~10 us of the replay)
+        fixup_side = (self.xchg is None and (_FIXUP_ON_SIDE == "1" or (_FIXUP_ON_SIDE == "auto" and not self.side_serial
+                                                                        and not torch.cuda.is_current_stream_capturing()))
                       and not self.deterministic and L > 0
                       and not self._early_grad_xchg())
         if (self.xchg is not None and self.shard_graph and probe is None and masks_out is None
