@@ -22,7 +22,10 @@
 #define FBN_MAXR 8   // max SENET reduced width supported (reference: 3)
 #define FBN_MAX_L 32 // max history length (the reference keeps the last 20)
 #ifndef FBN_HCH
-#define FBN_HCH 10   // default history rows in flight per sample before they are summed (FBN_FIELDS_HCH: 5 / 10 / 20)
+// default history rows in flight per sample before they are summed (FBN_FIELDS_HCH: 5 / 10 / 20):
+// 5 -- in the step, beside the side-stream table-Adam passes, the lighter waves win (C3 in-process,
+// 10 rounds: 0.4184 vs 0.4203 (10) vs 0.4212 ms/step (20), profiles/r03s2_group_knobs_ab.txt)
+#define FBN_HCH 5
 #endif
 
 struct FieldArgs {

@@ -1,4 +1,5 @@
-# gather history rows in flight per chunk (FBN_FIELDS_HCH, default 10): a longer in-process A/B
+# the final tree: the gather tests, then the default bench line
 set -o pipefail
 mkdir -p gpurun_out
-AB_R=10 timeout -k 10 800 python -u tools/ab_step.py base hch5:env.FBN_FIELDS_HCH=5 hch20:env.FBN_FIELDS_HCH=20 > gpurun_out/s2s_ab.txt 2>&1
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_coverage.py tests/test_gpu_trainer.py > gpurun_out/s2t_tests.log 2>&1 &&
+timeout -k 10 600 python -u bench.py > gpurun_out/s2t_bench.json 2> gpurun_out/s2t_bench.err
