@@ -54,14 +54,21 @@ def parse():
     ap.add_argument("--rows-per-gpu", type=int, default=ROWS_PER_GPU)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "bf16_fwd", "fp32"],
                     help="bf16: every GEMM operand bf16; bf16_fwd: forward GEMM operands bf16, backward fp32; fp32")
-    ap.add_argument("--no-graph", action="store_true", help="N = 1: eager steps only (same as --mode eager)")
-    ap.add_argument("--mode", default="auto", choices=["auto", "graph", "eager"],
-                    help="N = 1: replay one hipGraph per batch, launch eagerly, or (auto) time both for a few "
-                         "steps after priming and run the timed steps in the faster mode")
+    ap.add_argument("--no-graph", action="store_true", help="N = 1: no hipGraph capture (auto picks program / eager)")
+    ap.add_argument("--mode", default="auto", choices=["auto", "program", "graph", "eager"],
+                    help="N = 1: replay one recorded step program per batch (the native step driver, "
+                         "csrc/plan.cpp), replay one hipGraph per batch, launch eagerly from Python, or (auto) "
+                         "time all three for a few steps after priming and run the timed steps in the fastest")
     ap.add_argument("--main-priority", action="store_true",
                     help="run the step on a high-priority stream (the side stream stays at normal priority)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=20)
+    ap.add_argument("--no-cpu-plan", dest="cpu_plan", action="store_false",
+                    help="skip BASELINE.md 2's CPU-baseline plan (C1 / C2 shapes, 20 warm-up + 200 timed steps)")
+    ap.add_argument("--cpu-plan-steps", type=int, default=200)
+    ap.add_argument("--no-inference", dest="inference", action="store_false",
+                    help="skip the inference leg (eval-mode drop-in forwards at batch 8192, src/Prediction.py:95-113)")
+    ap.add_argument("--infer-batches", type=int, default=96)
     ap.add_argument("--probe-steps", type=int, default=10)
     ap.add_argument("--batches", type=int, default=0, help="distinct HBM-resident batches (default F + 32)")
     ap.add_argument("--lazy-window", type=int, default=0,
@@ -135,6 +142,90 @@ def cpu_baseline(args, world):
                       f"fp32) at d={d}, batch {B}, {V} item rows, history 20 -- the same per-GPU workload"}
 
 
+def cpu_baseline_plan(args):
+    """BASELINE.md 2 / SURVEY 8(d)'s CPU-baseline plan: the oracle's train step (torch CPU restatement of
+    src/train_fibinet.py:113-123) at the C1 shape (d 16, batch 256, the reference's 91 718-row vocab) and
+    the C2 shape (d 16, batch 4096, 1 M rows), 20 warm-up + 200 timed steps each, on this host's cores."""
+    from ctr_recommendation_amd.data import make_batch
+    from oracle.fibinet_oracle import OracleTrainer, build_model
+    threads = torch.get_num_threads()
+    out = []
+    for name, d, B, V in (("C1", 16, 256, 91_718), ("C2", 16, 4096, 1_000_000)):
+        torch.manual_seed(2025)
+        tr = OracleTrainer(build_model(None, {"embedding_dim": d, "vocab_size": V}), lr=1e-3, weight_decay=1e-5,
+                           total_steps=1000)
+        batches = [make_batch(7 + i, B, V) for i in range(4)]
+        for i in range(20):
+            tr.step(*batches[i % 4])
+        n = args.cpu_plan_steps
+        t0 = time.perf_counter()
+        for i in range(n):
+            tr.step(*batches[i % 4])
+        dt = time.perf_counter() - t0
+        out.append({"config": name, "value": round(n * B / dt, 1), "unit": "samples/s",
+                    "ms_per_step": round(dt / n * 1e3, 3), "cores": threads, "kind": "port",
+                    "sample": f"20 warm-up + {n} timed oracle train steps, d={d}, batch {B}, {V} item rows (fp32)"})
+        del tr, batches
+    return out
+
+
+def inference_leg(args, dev, dtype):
+    """Inference throughput (SURVEY 6's other derived figure, src/Prediction.py:95-113): the drop-in
+    MM_FiBiNET in eval mode, batch 8192, d = 128, `model(batch_dict)` then `y_pred.cpu()` per batch --
+    the reference loop (ctr_recommendation_amd.predict.predict) over HBM-resident synthetic batches, so
+    the host collate (pandas, 4 workers) is out of the timed region.  Also the gather's roofline inside
+    those forwards (HIP events around fields_fwd, same stream)."""
+    from ctr_recommendation_amd import ops
+    from ctr_recommendation_amd.data import make_device_batches
+    from ctr_recommendation_amd.model_fibinet import build_model
+    from ctr_recommendation_amd.predict import predict
+    d, B, V, L = args.dim, args.batch, args.rows_per_gpu, 20
+    torch.manual_seed(2025)
+    model = build_model(None, {"embedding_dim": d, "vocab_size": 4, "compute_dtype": dtype})
+    g = torch.Generator(device=dev)
+    g.manual_seed(2025)
+    table = torch.randn((V, d), generator=g, device=dev)
+    table[0].zero_()
+    model.item_emb.weight = torch.nn.Parameter(table)
+    model.to(dev).eval()
+    nb = 32
+    xs = [b for b, _ in make_device_batches(nb, B, V, L, dev, seed=4242)]
+    predict(model, xs[:4])                              # warm-up
+    torch.cuda.synchronize()
+    n = max(nb, args.infer_batches)
+    t0 = time.perf_counter()
+    preds = predict(model, [xs[i % nb] for i in range(n)])
+    dt = time.perf_counter() - t0
+    assert preds.shape == (n * B,)
+    # the gather inside the same eval-mode forwards, timed by events on its stream
+    p = {k: t for k, t in model.named_parameters()}
+    p.update(model._buffers_dict())
+    cfg = model._fwd_cfg()
+    cfg.L = L
+    probe = {}
+    with torch.no_grad():
+        for j in range(12):
+            torch.cuda._sleep(2_000_000)
+            ops.forward(p, xs[j % nb], cfg, None, probe=probe)
+    torch.cuda.synchronize()
+    ev = probe["fields_fwd"][2:]
+    ms = sum(a.elapsed_time(e) for a, e in ev) / len(ev)
+    work = gather_bytes_per_sample(d) * B
+    ach = work / (ms * 1e-3) / 1e9
+    out = {"value": round(n * B / dt, 1), "unit": "samples/s", "ms_per_batch": round(dt / n * 1e3, 4),
+           "batches": n, "batch": B, "dtype": dtype, "emb_dim": d, "item_rows": V,
+           "loop": "src/Prediction.py:106-113 (model(batch_dict); y_pred.cpu().numpy() per batch) through the drop-in "
+                   "MM_FiBiNET, eval mode; batches HBM-resident (no host collate)",
+           "roofline": {"kernel": "fields_fwd (eval-mode forward)", "bound": "hbm", "achieved": round(ach, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                        "traffic": None, "avg_launch_ms": round(ms, 4), "work_per_launch": work,
+                        "work_basis": "SURVEY 8(d) 12,984 B/sample x batch"}}
+    del model, xs, table
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
+
+
 def _initial_state(cfg, V, world, rank, dev):
     """Seeded init: small params from build_model; the N(0,1) table (row 0 = padding = 0) built on the
     device -- each rank only materialises its own shard (the trainer slices init[...][lo:hi])."""
@@ -189,9 +280,13 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
     # only after ~2F steps; warm-up steps are < 1 ms each
     prime = max(0, 2 * F - W) if args.prime < 0 else args.prime
     sharded = world > 1 or FORCE_SHARD
-    use_graph = not sharded and not args.no_graph and args.mode != "eager"
-    trial_n = 16 if (use_graph and args.mode == "auto") else 0
-    total = 1 + (nb if use_graph else 0) + prime + W + K + args.probe_steps + 16 + 4 * trial_n
+    use_graph = not sharded and not args.no_graph and args.mode in ("auto", "graph")
+    use_prog = not sharded and args.mode in ("auto", "program") and args.table_adam == "lazy"
+    if use_prog:
+        prime = max(prime, nb)            # every batch's program is recorded (a real step each) while priming
+    modes = [m for m, ok in (("program", use_prog), ("graph", use_graph), ("eager", True)) if ok]
+    trial_n = 16 if (args.mode == "auto" and len(modes) > 1) else 0
+    total = 1 + (nb if use_graph else 0) + prime + W + K + args.probe_steps + 16 + 2 * len(modes) * trial_n
     if args.main_priority:
         # the step's own stream at high priority: the hardware queue arbiter then dispatches its
         # workgroups ahead of the table-Adam side stream's when both have work pending
@@ -221,15 +316,24 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
             graphs.append(gr)
         torch.cuda.synchronize()
 
-    eager_now = [False]
+    mode_now = [modes[0]]
+    progs = [None] * nb
+    prog_pool = torch.cuda.MemPool() if use_prog else None     # one private pool for every program
 
     def run_step(i):
-        if graphs and not eager_now[0]:
-            graphs[i % nb].replay()
+        j = i % nb
+        if mode_now[0] == "graph":
+            graphs[j].replay()
+        elif mode_now[0] == "program" and progs[j] is not None:
+            tr.run_program(progs[j])
+        elif mode_now[0] == "program":
+            # first visit of this batch: a real step, recorded (the program replays it from now on)
+            b, y = batches[j]
+            progs[j] = tr.record_program(b, y, next_batch=batches[(i + 1) % nb][0], pool=prog_pool)
         else:
             # the HBM-resident batch itself: N > 1 routes the next batch during this step (no
             # mid-step host sync); N = 1 catches its rows up ahead and pre-claims them
-            b, y = batches[i % nb]
+            b, y = batches[j]
             tr.step(b, y, next_batch=batches[(i + 1) % nb][0])
 
     i = 0
@@ -244,8 +348,8 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
     trial = {}
     if trial_n:
         for rnd in range(2):
-            for mode in ("graph", "eager"):
-                eager_now[0] = mode == "eager"
+            for mode in modes:
+                mode_now[0] = mode
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 for _ in range(trial_n):
@@ -253,7 +357,7 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
                     i += 1
                 torch.cuda.synchronize()
                 trial.setdefault(mode, []).append((time.perf_counter() - t0) / trial_n * 1e3)
-        eager_now[0] = min(trial["eager"]) < min(trial["graph"])
+        mode_now[0] = min(modes, key=lambda m: min(trial[m]))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -324,7 +428,9 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
         torch.cuda.synchronize()
 
     def avg_ms(name, src=None):
-        ev = (probe if src is None else src).get(name, [])[2 if src is iso else 0:]
+        # the first two launches of an explicit source (the eval-mode forwards, the serialised probe
+        # steps) carry first-iteration warm-up; the in-step probe follows the timed steps (warm)
+        ev = (probe if src is None else src).get(name, [])[2 if src is not None else 0:]
         return sum(a.elapsed_time(e) for a, e in ev) / max(1, len(ev))
 
     touched = int(uniq.numel())
@@ -388,13 +494,15 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
         add("adam_window", "adam_catchup rolling window alone (serialised probe step)", avg_ms("adam_window", serial),
             catchup_bytes(window, d, 0), "GB/s", HBM_PEAK_GBS, "hbm",
             f"window {window} rows x (24 B x d + 8 B); VALU-bound replay of up to F steps per row")
-    add("gemm_mlp0", f"gemm MLP layer 1 (B x 15d -> 512, {dtype} MFMA)", avg_ms("gemm_mlp0"),
-        2.0 * B * 512 * 15 * d, "TFLOP/s", MFMA_PEAK_TFS if dtype == "bf16" else FP32_MFMA_PEAK_TFS, "mfma",
-        "2 x B x 512 x 15d")
+    # the layer-1 forward GEMM takes bf16 operands in bf16 AND bf16_fwd mode (priced against the bf16
+    # peak), fp32 operands (v_mfma_f32_32x32x2_f32) only in fp32 mode
+    fwd_peak = FP32_MFMA_PEAK_TFS if dtype == "fp32" else MFMA_PEAK_TFS
+    fwd_isa = "fp32 MFMA" if dtype == "fp32" else "bf16 MFMA"
+    add("gemm_mlp0", f"gemm MLP layer 1 (B x 15d -> 512, {fwd_isa})", avg_ms("gemm_mlp0"),
+        2.0 * B * 512 * 15 * d, "TFLOP/s", fwd_peak, "mfma", "2 x B x 512 x 15d")
     if iso:
-        add("gemm_mlp0", f"gemm MLP layer 1 alone (eval-mode forward, no side-stream work, {dtype} MFMA)",
-            avg_ms("gemm_mlp0", iso), 2.0 * B * 512 * 15 * d, "TFLOP/s",
-            MFMA_PEAK_TFS if dtype == "bf16" else FP32_MFMA_PEAK_TFS, "mfma", "2 x B x 512 x 15d")
+        add("gemm_mlp0", f"gemm MLP layer 1 alone (eval-mode forward, no side-stream work, {fwd_isa})",
+            avg_ms("gemm_mlp0", iso), 2.0 * B * 512 * 15 * d, "TFLOP/s", fwd_peak, "mfma", "2 x B x 512 x 15d")
     # the four weight-gradient GEMMs in their one grouped launch (bf16 mode): dWa, dWb, dW, dWp
     add("wgrad_group", "gemm weight gradients, grouped launch (dWa + dWb + dW + dWp, bf16 MFMA)",
         avg_ms("wgrad_group"), 2.0 * B * (512 * 15 * d + 256 * 512 + 5 * d * d + 128 * d), "TFLOP/s", MFMA_PEAK_TFS,
@@ -406,10 +514,10 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
     dominant = max(main_k, key=lambda r: r["avg_launch_ms"]) if main_k else None
     out = {"dt": dt, "t_host": t_host, "t_wait": t_wait, "K": K, "W": W, "B": B, "L": L, "V": V, "d": d, "rows_local": tr.rows_local, "loss": loss,
            "rooflines": rooflines, "roofline": dominant, "table_adam": tr.table_adam,
-           "graphs": bool(graphs) and not eager_now[0],
+           "graphs": mode_now[0] == "graph", "launch_mode": mode_now[0] if not sharded else "eager",
            "mode_trial_ms_per_step": {k: [round(x, 4) for x in v] for k, v in trial.items()} if trial else None,
            "prime": prime, "batches": nb, "lag": lag, "stale": stale, "touched": touched, "prefetch": prefetch}
-    del graphs, tr, batches
+    del graphs, progs, tr, batches
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     return out
@@ -463,6 +571,9 @@ def main():
         alt = measure(args, "fp32", world, rank, dev, rehearsal, backend)
         # C3's literal wording ("bf16 fwd / fp32 grad accum"): bf16 forward GEMMs, fp32 backward
         alt16 = measure(args, "bf16_fwd", world, rank, dev, rehearsal, backend)
+    inf = None
+    if world == 1 and args.inference and not FORCE_SHARD:
+        inf = {m: inference_leg(args, dev, m) for m in ("fp32", "bf16")}
     other_bn = None
     if world > 1 and not args.no_other_bn:
         # both BatchNorm modes at N > 1: the other one as an embedded line (SyncBN = the parity mode)
@@ -482,7 +593,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16" if args.dtype == "bf16" else "fp32",
+            "dtype": args.dtype,
             "data": f"synthetic (MicroLens-shaped, seeded, HBM-resident, {r['batches']} distinct batches cycled: "
                     f"fresh ids every step, "
                     + (f"Zipf({args.zipf}) item / history ids" if args.zipf > 0 else "uniform ids")
@@ -491,7 +602,8 @@ def main():
                        "model": "MM_FiBiNET", "global_batch": B * world, "seq_len": r["L"],
                        "item_rows": r["V"], "item_rows_per_gpu": r["rows_local"], "emb_dim": r["d"],
                        "parallelism": f"row-shard{world}" if world > 1 or FORCE_SHARD else "single",
-                       "hipgraph": r["graphs"], **({"rehearsal": backend} if rehearsal else {}),
+                       "hipgraph": r["graphs"], "launch_mode": r["launch_mode"],
+                       **({"rehearsal": backend} if rehearsal else {}),
                        **({"launch_mode_trial_ms_per_step": r["mode_trial_ms_per_step"]}
                           if r.get("mode_trial_ms_per_step") else {}),
                        **({"batchnorm": "per-GPU statistics (nn.DataParallel semantics, train_fibinet.py:69-70)"
@@ -537,8 +649,12 @@ def main():
                               "global batch); 4 extra all-reduces per step") if mode == "sync" else
                              "per-GPU statistics (nn.DataParallel semantics, train_fibinet.py:69-70)",
                 "final_loss": round(other_bn["loss"], 5)}
+        if inf is not None:
+            out["inference"] = inf
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, world)
+            if args.cpu_plan:
+                out["cpu_baseline_plan"] = cpu_baseline_plan(args)
         print(json.dumps(out), flush=True)
     if world > 1 or FORCE_SHARD:
         dist.barrier()

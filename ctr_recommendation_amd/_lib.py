@@ -6,8 +6,11 @@ raises ``RuntimeError`` with ``fbn_last_error()`` on a non-zero return code.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
+import struct
+import threading
 from typing import Optional
 
 import torch
@@ -117,6 +120,13 @@ SIGNATURES = {
     "fbn_bilinear_bwd": (I, [P, I, I, P, P, P, P, P, I, I, P]),
     "fbn_collate": (I, [P, I, P, P, I, I, P, P, P, P, P, LL, P, P, I, P, P, P, P, P, P, P, P, P]),
     "fbn_collate_zero_if": (I, [P, LL, P, P]),
+    "fbn_plan_create": (I, [P]),
+    "fbn_plan_destroy": (I, [P]),
+    "fbn_plan_size": (I, [P]),
+    "fbn_plan_add_call": (I, [P, P, P, I, P, I]),
+    "fbn_plan_add_record": (I, [P, I, P]),
+    "fbn_plan_add_wait": (I, [P, P, I]),
+    "fbn_plan_run": (I, [P, P]),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -140,6 +150,7 @@ def lib() -> ctypes.CDLL:
 
 _fns = {}
 _UNCHECKED = ("fbn_version", "fbn_device_ok")
+_tls = threading.local()           # .prog: the StepProgram recording on this thread (or None)
 
 
 def call(name: str, *args) -> int:
@@ -150,7 +161,162 @@ def call(name: str, *args) -> int:
     if rc and isinstance(rc, int) and name not in _UNCHECKED and not name.endswith(("_size", "_grid")):
         msg = lib().fbn_last_error().decode(errors="replace")
         raise RuntimeError(f"{name} failed (code {rc}): {msg}")
+    prog = getattr(_tls, "prog", None)
+    if prog is not None:
+        prog.add_call(name, f, args)
     return rc
+
+
+def keep(obj) -> None:
+    """A host object whose address was passed to a call as an integer (a job array): kept alive
+    by the step program being recorded, whose replays pass the same address again."""
+    prog = getattr(_tls, "prog", None)
+    if prog is not None:
+        prog.keep.append(obj)
+
+
+def recording() -> bool:
+    return getattr(_tls, "prog", None) is not None
+
+
+def wait_stream(dst, src) -> None:
+    """dst.wait_stream(src), recorded as a stream edge while a step program is being recorded."""
+    dst.wait_stream(src)
+    prog = getattr(_tls, "prog", None)
+    if prog is not None and dst.cuda_stream != src.cuda_stream:
+        prog.edge(src.cuda_stream, dst.cuda_stream)
+
+
+def record_event(ev, stream) -> None:
+    """ev.record(stream) (recorded: the program's event slot of ev)."""
+    ev.record(stream)
+    prog = getattr(_tls, "prog", None)
+    if prog is not None:
+        call_raw("fbn_plan_add_record", prog.h, prog.slot_of(ev), stream.cuda_stream)
+
+
+def wait_event(stream, ev) -> None:
+    """stream.wait_event(ev) (recorded: a wait on the program's event slot of ev)."""
+    stream.wait_event(ev)
+    prog = getattr(_tls, "prog", None)
+    if prog is not None:
+        call_raw("fbn_plan_add_wait", prog.h, stream.cuda_stream, prog.slot_of(ev))
+
+
+def call_raw(name: str, *args) -> int:
+    """A call that is never recorded (the step-program API itself)."""
+    f = _fns.get(name)
+    if f is None:
+        f = _fns[name] = getattr(lib(), name)
+    rc = f(*args)
+    if rc:
+        msg = lib().fbn_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed (code {rc}): {msg}")
+    return rc
+
+
+_INT_TYPES = (P, I, LL, SZ, U)
+_MASK64 = (1 << 64) - 1
+
+
+def _as_u64(v) -> int:
+    if v is None:
+        return 0
+    if isinstance(v, bool):
+        return int(v)
+    if isinstance(v, int):
+        return v & _MASK64
+    if isinstance(v, ctypes.c_void_p):
+        return (v.value or 0) & _MASK64
+    if isinstance(v, (ctypes.Array, ctypes.Structure)):
+        return ctypes.addressof(v)
+    if isinstance(v, ctypes._SimpleCData):
+        return int(v.value) & _MASK64
+    raise TypeError(f"step program: cannot record an argument of type {type(v).__name__} (pass an address)")
+
+
+def _f32_in_f64(x: float) -> float:
+    """The double whose low 32 bits are the float32 bits of x (a float argument in an xmm register)."""
+    bits = struct.unpack("<I", struct.pack("<f", x))[0]
+    return struct.unpack("<d", struct.pack("<Q", bits))[0]
+
+
+class StepProgram:
+    """A recorded training step replayed by the native step driver (csrc/plan.cpp, include/fibinet.h
+    "step programs").  Record with ``with prog.recording(): <run the step eagerly>``; every call()
+    on this thread is appended (after it ran), wait_stream / record_event / wait_event become the
+    program's stream edges, and every device allocation goes to the program's private memory pool,
+    so the addresses the recorded calls name stay owned by the program (the pool is used by
+    recordings only; steps never overlap, so programs may share its freed blocks, as torch's graphs
+    share a pool).  run() replays the whole step with one host call."""
+
+    def __init__(self, device=None):
+        h = ctypes.c_void_p()
+        call_raw("fbn_plan_create", ctypes.byref(h))
+        self.h = h.value
+        self.device = torch.device(device if device is not None else "cuda")
+        self.keep = []
+        self._slots = {}
+        self._nslot = 0
+        self.pool = None
+        self._failed = ctypes.c_int(-1)
+        self._run = lib().fbn_plan_run
+
+    def add_call(self, name, f, args) -> None:
+        types = SIGNATURES[name][1]
+        ints, flts = [], []
+        for t, v in zip(types, args):
+            if t is F:
+                flts.append(_f32_in_f64(float(v)))
+            elif t is D:
+                flts.append(float(v))
+            else:
+                ints.append(_as_u64(v))
+                if isinstance(v, (ctypes.Array, ctypes.Structure, ctypes.c_void_p)):
+                    self.keep.append(v)
+        ia = (ctypes.c_ulonglong * max(1, len(ints)))(*ints)
+        fa = (ctypes.c_double * max(1, len(flts)))(*flts)
+        call_raw("fbn_plan_add_call", self.h, ctypes.cast(f, ctypes.c_void_p), ia, len(ints), fa, len(flts))
+
+    def slot_of(self, ev) -> int:
+        k = id(ev)
+        if k not in self._slots:
+            self._slots[k] = self._nslot
+            self._nslot += 1
+            self.keep.append(ev)           # id() stays unique while the event lives
+        return self._slots[k]
+
+    def edge(self, src_stream: int, dst_stream: int) -> None:
+        slot = self._nslot
+        self._nslot += 1
+        call_raw("fbn_plan_add_record", self.h, slot, src_stream)
+        call_raw("fbn_plan_add_wait", self.h, dst_stream, slot)
+
+    @contextlib.contextmanager
+    def recording(self, pool=None):
+        if getattr(_tls, "prog", None) is not None:
+            raise RuntimeError("a step program is already being recorded on this thread")
+        self.pool = pool if pool is not None else torch.cuda.MemPool()
+        _tls.prog = self
+        try:
+            with torch.cuda.use_mem_pool(self.pool, device=self.device):
+                yield self
+        finally:
+            _tls.prog = None
+
+    def __len__(self) -> int:
+        return call_raw("fbn_plan_size", self.h) if False else lib().fbn_plan_size(self.h)
+
+    def run(self) -> None:
+        rc = self._run(self.h, ctypes.byref(self._failed))
+        if rc:
+            msg = lib().fbn_last_error().decode(errors="replace")
+            raise RuntimeError(f"step program op {self._failed.value} failed (code {rc}): {msg}")
+
+    def __del__(self):
+        h, self.h = getattr(self, "h", None), None
+        if h and _lib is not None:
+            _lib.fbn_plan_destroy(h)
 
 
 def ptr(t: Optional[torch.Tensor]) -> Optional[int]:

@@ -16,7 +16,7 @@ CSRC = os.path.join(HERE, "csrc")
 ROOT = os.path.dirname(HERE)
 BUILD = os.path.join(ROOT, "build", "fibinet_hip")
 LIB = os.path.join(HERE, "libfibinet_hip.so")
-SOURCES = ["capi.cpp", "gemm.hip", "fields.hip", "mlp.hip", "optim.hip", "exchange.hip", "collate.hip", "bilinear.hip"]
+SOURCES = ["capi.cpp", "gemm.hip", "fields.hip", "mlp.hip", "optim.hip", "exchange.hip", "collate.hip", "bilinear.hip", "plan.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result",

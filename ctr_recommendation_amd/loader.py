@@ -233,9 +233,18 @@ class DeviceLoader:
             else:
                 yield self.collate(rows)
 
-    def check(self) -> None:
-        """Raise the KeyError the reference's collator would have raised (one 4-byte read)."""
-        if int(self.missing.item()):
+    def check(self, group=None, world: int = 1) -> None:
+        """Raise the KeyError the reference's collator would have raised (one 4-byte read).
+
+        world > 1: collective -- the flag is MAX-all-reduced first, so every rank raises at the same
+        step (a rank that raised alone would leave the others blocked in the next step's
+        collectives until the communicator's timeout)."""
+        flag = self.missing
+        if world > 1:
+            import torch.distributed as dist
+            flag = self.missing.clone()
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+        if int(flag.item()):
             raise KeyError("item_id(s) of a batch are not in item_info (src/dataloader.py:104-106)")
 
 

@@ -117,6 +117,7 @@ def bf16_weight_jobs(p: Dict[str, torch.Tensor], d: int, a: Dict[str, torch.Tens
         spec.append(("x", x, x.shape[0], x.shape[1], x.shape[1], 0, NO_REMAP))
     jobs = (_ConvJob * 8)()
     a["_conv_jobs"] = jobs
+    _lib.keep(jobs)               # its address is passed as an integer (step programs keep it alive)
     out = {}
     for i, (name, src, rows, cols, ld, trans, rm) in enumerate(spec):
         key = "w16_" + name
@@ -207,7 +208,7 @@ class DeferredSums:
             self.keep += [A, B] + ([B2] if B2 is not None else [])
         else:
             call("fbn_gemm_slabs", ptr(A), ptr(B), M, N, K, lda, ldb, int(transA), int(transB), ptr(ws), nbytes,
-                 ptr(A2), lda2, kseg, ptr(B2), ldb2, nseg, ctypes.byref(_nsplit), st)
+                 ptr(A2), lda2, kseg, ptr(B2), ldb2, nseg, ctypes.addressof(_nsplit), st)
             nsplit = _nsplit.value
         self.slabs.append((ws.data_ptr(), out.data_ptr(), M, N, ldc, nsplit, rC[0], rC[1], rC[2], float(beta)))
         self.keep.append(ws)
@@ -229,6 +230,7 @@ class DeferredSums:
         while group:
             gc, group = group[:6], group[6:]
             garr = (_SlabGemm * len(gc))(*[_SlabGemm(*x) for x in gc])
+            _lib.keep(garr)
             call("fbn_gemm_slabs_group", ctypes.addressof(garr), len(gc), stream)
         if ev is not None:
             ev[1].record()
@@ -239,6 +241,7 @@ class DeferredSums:
             jobs, slabs = jobs[16:], slabs[8:]
             arr = (_SumJob * max(1, len(jc)))(*[_SumJob(*j) for j in jc])
             sarr = (_SlabJob * max(1, len(sc)))(*[_SlabJob(*j) for j in sc])
+            _lib.keep((arr, sarr))
             call("fbn_sum_jobs2", ctypes.addressof(arr), len(jc), ctypes.addressof(sarr), len(sc), stream)
         self.jobs, self.slabs, self.keep = [], [], []
         self.used = set()
@@ -307,25 +310,29 @@ def bn_train_stats(h, B, C, mean, invstd, run_mean, run_var, ntot, coll: Collect
 
 def bn_backward(G, gvec, w, hact, scale, hpre, mean, invstd, gamma, B, C, ntot, dpre, dgamma, dbeta, dw,
                 coll: Collective, stream, dpre16=None, bias_grad=None, sums: Optional[DeferredSums] = None,
-                hact16=None, part_pre=None):
+                hact16=None, part_pre=None, tag: str = ""):
     """BN (+ReLU/dropout) backward; bias_grad (with sums): the preceding Linear's bias gradient
-    = column sums of dpre, finalised later by sums.flush().
+    = column sums of dpre, finalised later by sums.flush().  tag names the layer ("bn1" / "bn2"):
+    its cached workspace and bias-gradient partials are the layer's own, so two BatchNorm layers of
+    one width never share the partial slab that sums.flush() reads at the end of the backward.
+
     Single process only: hact may be None with hact16 (the bf16 activation image; a matrix source
     G needs only its sign) and dpre may be None when dpre16 is given (bf16 mode: nothing reads the
     f32 gradient, the bias gradient comes from the apply's column partials)."""
     dev = hpre.device
     cache = sums.cache if sums is not None and sums.cache is not None else {}
     nws = _lib.lib().fbn_bn_workspace_size(B, C)
-    ws = cache.get(f"bn_ws_{C}") if nws > 0 else None
+    key = tag or str(C)
+    ws = cache.get(f"bn_ws_{key}") if nws > 0 else None
     if nws > 0 and (ws is None or ws.numel() * 8 < nws):
-        ws = cache[f"bn_ws_{C}"] = _ws(nws, dev)
+        ws = cache[f"bn_ws_{key}"] = _ws(nws, dev)
     if coll.world <= 1:
         part = None
         if bias_grad is not None:
             nch = _lib.lib().fbn_bn_bwd_chunks(B, C)
-            part = cache.get(f"bn_part_{C}")
+            part = cache.get(f"bn_part_{key}")
             if part is None or tuple(part.shape) != (nch, C):
-                part = cache[f"bn_part_{C}"] = torch.empty((nch, C), dtype=torch.float32, device=dev)
+                part = cache[f"bn_part_{key}"] = torch.empty((nch, C), dtype=torch.float32, device=dev)
             sums.add(part, nch, C, bias_grad)
         call("fbn_bn_bwd_fused", ptr(G), ptr(gvec), ptr(w), ptr(hact), ptr(hact16), float(scale), ptr(hpre),
              ptr(mean), ptr(invstd), ptr(gamma), B, C, float(ntot), ptr(dpre), ptr(dpre16), ptr(dgamma), ptr(dbeta),
@@ -576,13 +583,13 @@ class _SideWork:
         if self.side is None:
             fn(_lib.stream_handle(self.dev))
             return
-        self.side.wait_stream(self.main)
+        _lib.wait_stream(self.side, self.main)
         with torch.cuda.stream(self.side):
             fn(self.side.cuda_stream)
 
     def join(self):
         if self.side is not None:
-            self.main.wait_stream(self.side)
+            _lib.wait_stream(self.main, self.side)
 
 
 def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict[str, torch.Tensor],
@@ -636,7 +643,7 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     bn_backward(None, gout, p["mlp.8.weight"], a["h2"], scale, a["h2pre"], a["mean2"], a["inv2"],
                 p["mlp.5.weight"], B, H2, ntot, dh2pre, g["mlp.5.weight"], g["mlp.5.bias"], g["mlp.8.weight"],
                 coll, st, dpre16=dh2pre16, bias_grad=g["mlp.4.bias"], sums=sums,
-                part_pre=a.get("bn2_bwd_part") if (gout is a.get("gout")) else None)
+                part_pre=a.get("bn2_bwd_part") if (gout is a.get("gout")) else None, tag="bn2")
     sums.add(gout, B, 1, g["mlp.8.bias"])
     dh1 = tmp("dh1", (B, H1))
     part1 = None
@@ -663,7 +670,7 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     bn_backward(dh1, None, None, None if lean_h1 else a["h1"], scale, a["h1pre"], a["mean1"], a["inv1"],
                 p["mlp.1.weight"], B, H1, ntot, dh1pre, g["mlp.1.weight"], g["mlp.1.bias"], None, coll, st,
                 dpre16=dh1pre16, bias_grad=g["mlp.0.bias"], sums=sums, hact16=a["h1_16"] if lean_h1 else None,
-                part_pre=part1)
+                part_pre=part1, tag="bn1")
     # weight gradient of the MLP input layer (side work), then its dgrad dc
     if a.get("split_c"):
         if not sums.gemm_slabs(dh1pre16, a["Vc16"], g["mlp.0.weight"], H1, KC, B, H1, 5 * d, 21 * d, True, False,
@@ -737,6 +744,7 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
             o += n
     else:
         outs_arr = (ctypes.c_void_p * 8)(*[g[k].data_ptr() for k in keys])   # host array of device pointers
+        _lib.keep(outs_arr)
         outs = ctypes.cast(outs_arr, ctypes.c_void_p).value
     evb = None
     if probe is not None:                       # bench / tools: events around the fields backward

@@ -125,9 +125,9 @@ def run(config: Optional[str] = None, *, epochs: Optional[int] = None, checkpoin
                 log0(f"Epoch {epoch + 1} | Step {steps} | Loss: {loss.item():.4f} | LR: {trainer.current_lr():.6f}")
                 # the print's sync anyway: an item_id without item_info raises here, within 200
                 # steps of the batch (the reference raises at that batch, src/dataloader.py:104-106)
-                train_loader.check()
+                train_loader.check(world=world)
         trainer.check_ids()
-        train_loader.check()
+        train_loader.check(world=world)
         avg_loss = float(total.item()) / steps if steps else 0.0
         dt = time.perf_counter() - t0
         # validation (:133-146): eval-mode probabilities of the whole split, AUC on the host
@@ -135,7 +135,7 @@ def run(config: Optional[str] = None, *, epochs: Optional[int] = None, checkpoin
         for batch, labels in valid_loader:
             ps.append(trainer.predict(batch).cpu().numpy())
             ys.append(labels.cpu().numpy())
-        valid_loader.check()
+        valid_loader.check(world=world)
         auc = None
         if ys:
             y = _gather_host(np.concatenate(ys), world)

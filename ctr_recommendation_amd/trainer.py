@@ -395,6 +395,7 @@ class FiBiNETTrainer:
         self._late_side = None
         self._sg = None
         self._sg_eager = 0
+        self._bn_synced_at = -1     # host step of the last rank-0 BatchNorm broadcast (_bn_from_rank0)
 
     # ------------------------------------------------------------------ one training step
     def step(self, batch: Dict[str, torch.Tensor], labels: torch.Tensor,
@@ -440,7 +441,7 @@ class FiBiNETTrainer:
             # on_side (an event on main at the step's start): the claims run on the side stream,
             # and the main stream waits for them just before the gather
             if on_side is not None:
-                self.side.wait_event(on_side)
+                _lib.wait_event(self.side, on_side)
                 ev = _events(probe, "adam_catchup", self.side)
                 key = _batch_key(batch["item_id"], seq if L else None)
                 pre = self.preclaim if (self.preclaim is not None and key == self._pre_key) else None
@@ -452,8 +453,8 @@ class FiBiNETTrainer:
                      int(self.decoupled), self.side.cuda_stream)
                 _events_end(ev, self.side)
                 claim_ev = torch.cuda.Event()
-                claim_ev.record(self.side)
-                side_hooks["before_gather"] = lambda: main.wait_event(claim_ev)
+                _lib.record_event(claim_ev, self.side)
+                side_hooks["before_gather"] = lambda: _lib.wait_event(main, claim_ev)
                 side_pass(wait_main=False)
                 return
             ev = _events(probe, "adam_catchup")
@@ -492,7 +493,7 @@ class FiBiNETTrainer:
             serial = self.side_serial
             sst = self.side if not serial else main      # in sequence on main (FBN_SIDE_SERIAL)
             if wait_main and not serial:
-                self.side.wait_stream(main)
+                _lib.wait_stream(self.side, main)
 
             def window():
                 ev = _events(probe, "adam_window", sst)
@@ -509,7 +510,7 @@ class FiBiNETTrainer:
                 window()
             elif order == "p_w":
                 def late_window():
-                    self.side.wait_stream(main)      # the forward is done: the window beside the backward
+                    _lib.wait_stream(self.side, main)      # the forward is done: the window beside the backward
                     window()
                 self._late_side = late_window
 
@@ -534,7 +535,7 @@ class FiBiNETTrainer:
         def start_untouched_adam():
             # eager mode: every row this shard's batch does not touch gets g = wd * p, independent
             # of the backward -> concurrently on the side stream
-            self.side.wait_stream(main)
+            _lib.wait_stream(self.side, main)
             ev = _events(probe, "adam_table", self.side)
             call("fbn_adam_table", ptr(self.E), ptr(self.Em), ptr(self.Ev), self.rows_local, d, ptr(self.map),
                  None, None, None, 1, None, ptr(self.sched), ptr(self.step_dev), self.wd_g, self.beta2, self.eps, 1,
@@ -547,14 +548,14 @@ class FiBiNETTrainer:
             # bf16 weight images (they depend only on the weights the previous step wrote) on the side
             # stream, beside the row claims and the claimed-row catch-up
             if after is None:
-                self.side.wait_stream(main)
+                _lib.wait_stream(self.side, main)
             else:
-                self.side.wait_event(after)
+                _lib.wait_event(self.side, after)
             with torch.cuda.stream(self.side):
                 self.acts["w16"] = ops.bf16_weights(self.p, d, self.acts, self.side.cuda_stream,
                                                     x=batch["item_emb_d128"])
             ev = torch.cuda.Event()
-            ev.record(self.side)
+            _lib.record_event(ev, self.side)
             return ev
 
         w16_main = cfg.bf16 and self.xchg is None and _W16_MODE == "main"
@@ -563,7 +564,7 @@ class FiBiNETTrainer:
         if (self.xchg is None and lazy and _CLAIM_ON_SIDE and not w16_late and not _SIDE_AFTER_MLP0
                 and not _SIDE_AFTER_MMPROJ and not _SIDE_AFTER_GATHER):
             claim_side = torch.cuda.Event()          # the step's start: the claims wait for nothing later
-            claim_side.record(main)
+            _lib.record_event(claim_side, main)
         head_conv = None
         if w16_main and self.xchg is None and lazy and claim_side is None and _HEAD_CONV:
             # on the main stream, in the claims' launch (fbn_adam_claim_catchup_conv): the two are
@@ -607,7 +608,7 @@ class FiBiNETTrainer:
                 # catch-up first; the images follow on the side stream, still beside it (they wait
                 # only for what preceded the catch-up)
                 step_start = torch.cuda.Event()
-                step_start.record(main)
+                _lib.record_event(step_start, main)
                 catch_up(B * (L + 1), claim=True, before_side=step_start)
                 w16_ev = self._w16_ev
             else:
@@ -616,7 +617,7 @@ class FiBiNETTrainer:
             call("fbn_claim_rows", ptr(batch["item_id"]), ptr(seq) if L else None, B, L, self.V, ptr(self.map),
                  ptr(self.slot_row), ptr(self.dup), ptr(self.hasdup), st)
         if w16_ev is not None:
-            main.wait_event(w16_ev)
+            _lib.wait_event(main, w16_ev)
         graphed = False
         # (not inside a graph capture: there each cross-queue edge costs ~10 us of the replay)
         fixup_side = (self.xchg is None and (_FIXUP_ON_SIDE == "1" or (_FIXUP_ON_SIDE == "auto" and not self.side_serial
@@ -642,7 +643,7 @@ class FiBiNETTrainer:
             bhooks = {"after_fields_bwd": self._grad_xchg_start} if self._early_grad_xchg() else None
             if fixup_side:
                 def fork_fixup():
-                    self.side.wait_stream(main)
+                    _lib.wait_stream(self.side, main)
                     call("fbn_sparse_fixup_dup", ptr(self.dup), B * (L + 1), ptr(self.gvec), ptr(self.extra),
                          ptr(self.slot_row), L + 1, d, self.side.cuda_stream)
                 bhooks = {"after_fields_bwd": fork_fixup}
@@ -677,7 +678,7 @@ class FiBiNETTrainer:
             else:
                 gsrc = (self.gvec, self.extra, L + 1)
                 if fixup_side:
-                    main.wait_stream(self.side)     # the fold (and the side's table passes) done
+                    _lib.wait_stream(main, self.side)     # the fold (and the side's table passes) done
                 else:
                     call("fbn_sparse_fixup_dup", ptr(self.dup), n_ent, ptr(self.gvec), ptr(self.extra),
                          ptr(self.slot_row), L + 1, d, st)
@@ -719,7 +720,7 @@ class FiBiNETTrainer:
             call("fbn_unpack_extras", ptr(self.flat_g_ext[o:]), ptr(self.loss), ptr(self.sumsq), st)
         if not dense_done:
             call("fbn_sumsq", ptr(self.flat_g), self.n_dense, None, 0, ptr(self.sumsq), st)
-        main.wait_stream(self.side)   # side-stream table pass done before map entries are reset
+        _lib.wait_stream(main, self.side)   # side-stream table pass done before map entries are reset
         if self.xchg is None:
             defer_now = self.deferred
         if defer_now:
@@ -749,6 +750,42 @@ class FiBiNETTrainer:
             call("fbn_step_end", ptr(self.step_dev), ptr(self.rng), ptr(self.sumsq),
                  ptr(self.p["mlp.1.num_batches_tracked"]), ptr(self.p["mlp.5.num_batches_tracked"]), self.total_steps,
                  ptr(self.err), st)
+        self.host_step += 1
+        return self.loss
+
+    # ------------------------------------------------------------------ step programs (native step driver)
+    def record_program(self, batch: Dict[str, torch.Tensor], labels: torch.Tensor,
+                       next_batch: Optional[Dict[str, torch.Tensor]] = None, pool=None) -> "_lib.StepProgram":
+        """Run ONE training step on (batch, labels[, next_batch]) -- a real step, counted -- and record
+        it as a step program (csrc/plan.cpp): its ~25 library calls and stream edges, replayed later
+        by run_program() with one host call instead of ~0.4 ms of Python per step.
+
+        A replay repeats the recorded step exactly: the same batch tensors (their CURRENT contents
+        at replay time), the same next batch for the table-Adam prefetch, the same streams.  Valid
+        replays follow the conditions of a hipGraph capture of the step: the step's schedule
+        position, dropout stream, claims and deferred gradients are device state (the device step
+        counter), nothing host-side changes between replays; pre-claims carry their step in the
+        tag, so a replay in another order than recorded still claims correctly.  One GPU, lazy table
+        Adam with deferred gradients, "all" bilinear (the paths whose step is library calls only)."""
+        if self.xchg is not None:
+            raise ValueError("step programs record the single-GPU step (the sharded step has host-side "
+                             "split sizes and collectives between its kernels)")
+        if not (self.table_adam == "lazy" and self.deferred) or self.fcfg.bilinear_each:
+            raise ValueError("step programs need the lazy table Adam with deferred gradients and the 'all' "
+                             "bilinear interaction")
+        prog = _lib.StepProgram(self.device)
+        with prog.recording(pool):
+            self.step(batch, labels, next_batch=next_batch)
+        # the tensors the recorded calls address
+        prog.keep += [batch, labels, next_batch, dict(self.acts)]
+        return prog
+
+    def run_program(self, prog: "_lib.StepProgram") -> torch.Tensor:
+        """One training step by replaying a recorded step program (see record_program)."""
+        if self.host_step >= self.total_steps:
+            raise ValueError(f"Tried to step {self.host_step + 1} times. The specified number of total steps is "
+                             f"{self.total_steps}")
+        prog.run()
         self.host_step += 1
         return self.loss
 
@@ -838,9 +875,16 @@ class FiBiNETTrainer:
         """Per-rank BatchNorm (sync_bn=False) at N > 1: evaluation uses rank 0's running statistics
         on every rank.  That is nn.DataParallel's behaviour (train_fibinet.py:69-70: each forward
         replicates the module, buffers included, from device 0, and only device 0's updates are
-        kept), and they are the statistics the checkpoint holds."""
+        kept), and they are the statistics the checkpoint holds.  Side effect: the other ranks'
+        running statistics are REPLACED by rank 0's (they keep training from those values; only
+        rank 0's are ever evaluated or saved).  Broadcast once per evaluation pass: skipped while
+        the host step count is unchanged since the last broadcast (4 broadcasts per pass, not per
+        batch)."""
         if self.world <= 1 or self.sync_bn:
             return
+        if self._bn_synced_at == self.host_step:
+            return
+        self._bn_synced_at = self.host_step
         for n in ("mlp.1.running_mean", "mlp.1.running_var", "mlp.5.running_mean", "mlp.5.running_var"):
             t = self.p[n]
             if self.stage_on_cpu:
@@ -911,6 +955,35 @@ class FiBiNETTrainer:
                 out[k] = self.p[k].detach().cpu().clone()
         return out
 
+    _loaded_table = None
+
+    def _scatter_table(self, full: Optional[torch.Tensor]) -> None:
+        """Rank 0's full table -> every rank's row block (the inverse of _gather_table; chunks of
+        <= 256 MB through one staging buffer)."""
+        if self.rank == 0 and full is None:
+            raise KeyError(f"load_state_dict at N > 1: rank 0's dict must hold {TABLE!r} (state_dict() "
+                           f"gives it to rank 0; state_dict(all_ranks=True) to every rank)")
+        d, Vl = self.d, self.Vl
+        chunk = max(1, (256 << 20) // (d * 4))
+        dev = "cpu" if self.stage_on_cpu else self.device
+        stage = torch.empty((min(chunk, Vl), d), dtype=torch.float32, device=dev)
+        for dst in range(self.world):
+            lo = dst * Vl
+            n = max(0, min(self.V, lo + Vl) - lo)
+            for c0 in range(0, n, chunk):
+                c1 = min(n, c0 + chunk)
+                buf = stage[:c1 - c0]
+                if self.rank == 0:
+                    buf.copy_(full[lo + c0:lo + c1])
+                if dst != 0:
+                    if self.rank == 0:
+                        dist.send(buf, dst=dst, group=self.group)
+                    elif self.rank == dst:
+                        dist.recv(buf, src=0, group=self.group)
+                if self.rank == dst:
+                    self.E[c0:c1].copy_(buf)
+        self._loaded_table = True
+
     def _gather_table(self, all_ranks: bool) -> Optional[torch.Tensor]:
         d, Vl = self.d, self.Vl
         chunk = max(1, (256 << 20) // (d * 4))
@@ -938,14 +1011,26 @@ class FiBiNETTrainer:
         return full
 
     def load_state_dict(self, sd: Dict[str, torch.Tensor]) -> None:
-        """Load reference-format weights (App. B keys; every rank needs the full dict at N > 1).
-        Like ``model.load_state_dict`` under the reference's loop, the optimizer state (Adam
-        moments, step count, schedule position) is kept: only the weights and BatchNorm buffers
-        change."""
+        """Load reference-format weights (App. B keys).  Like ``model.load_state_dict`` under the
+        reference's loop, the optimizer state (Adam moments, step count, schedule position) is kept:
+        only the weights and BatchNorm buffers change.
+
+        N > 1: collective when any rank's dict lacks ``item_emb.weight`` -- the form state_dict()
+        returns on ranks above 0 -- so ``load_state_dict(state_dict())`` round-trips on every rank:
+        rank 0 (which must hold the table) sends each rank its row block; ranks whose dict holds the
+        full table take their block from it."""
         self.flush()
+        if self.world > 1:
+            have = torch.tensor([int(TABLE in sd)], dtype=torch.int32,
+                                device="cpu" if self.stage_on_cpu else self.device)
+            dist.all_reduce(have, op=dist.ReduceOp.MIN, group=self.group)
+            if not int(have.item()):
+                self._scatter_table(sd.get(TABLE) if self.rank == 0 else None)
         for k in self.key_order:
             if k == TABLE:
-                self.E.copy_(sd[k][self.rows_lo:self.rows_lo + self.rows_local].to(self.device))
+                if self.world == 1 or TABLE in sd and self._loaded_table is None:
+                    self.E.copy_(sd[k][self.rows_lo:self.rows_lo + self.rows_local].to(self.device))
+                self._loaded_table = None
             else:
                 self.p[k].copy_(sd[k].to(self.device))
         self.last.copy_(self.step_dev.expand_as(self.last))     # loaded rows are current (device step)

@@ -478,6 +478,28 @@ int fbn_collate(const int64_t* perm, int B, const int64_t* item, const int64_t* 
  * (src/Prediction.py:39-42) on the batch's own missing flag, with no host round trip. */
 int fbn_collate_zero_if(float* x, long long n, const int* flag, void* stream);
 
+/* ---------------------------------------------------------------- step programs (native step driver)
+ * Replaces the Python loop body that issues one training step (src/train_fibinet.py:113-123): the
+ * host records a step's calls of this library -- entry point, arguments, and the cross-stream
+ * edges (event record + stream wait) -- once while running the step, and replays them natively
+ * (the same launches, streams and order: a replay is bit-identical to the eager step).  Replay calls
+ * each recorded entry point through one generic signature under the x86-64 System V convention
+ * (integer-class arguments in order, float / double arguments in xmm0-7), so every fbn_* entry point
+ * with <= 48 integer-class and <= 8 floating arguments can be recorded (csrc/plan.cpp).
+ *   fbn_plan_create(&plan); fbn_plan_add_call(plan, fn, iargs, ni, fargs, nf)  -- iargs: the integer
+ *   arguments in order (pointers / ints as 64-bit, sign-extended); fargs: the float / double
+ *   arguments in order as doubles (a float argument: a double whose low 32 bits are the float's);
+ *   fbn_plan_add_record(plan, slot, stream) / fbn_plan_add_wait(plan, stream, slot): a stream edge
+ *   through the program's event `slot`; fbn_plan_run(plan, &failed_op): 0, or the failing entry
+ *   point's code (message in fbn_last_error). */
+int fbn_plan_create(void** plan);
+int fbn_plan_destroy(void* plan);
+int fbn_plan_size(void* plan);
+int fbn_plan_add_call(void* plan, void* fn, const unsigned long long* iargs, int ni, const double* fargs, int nf);
+int fbn_plan_add_record(void* plan, int slot, void* stream);
+int fbn_plan_add_wait(void* plan, void* stream, int slot);
+int fbn_plan_run(void* plan, int* failed);
+
 #ifdef __cplusplus
 }
 #endif

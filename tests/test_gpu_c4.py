@@ -1,0 +1,294 @@
+"""Config C4 (BASELINE.json configs[3]): 10 M item rows row-sharded over 8 ranks, global batch
+65 536 -- the row-sharded trainer (replacing src/train_fibinet.py:69-70's nn.DataParallel over the
+table of src/model_fibinet.py:100) at C4's per-rank shape: 1.25 M rows and 8 192 samples per rank.
+
+The 8 ranks share the one MI355X of a test box: every rank runs the real HIP kernels (owner claims,
+lazy table Adam, exchange-mode gather, SyncBN, sparse reduce-scatter) on cuda:0 and the collectives
+run over gloo on host copies (stage_on_cpu=True), because RCCL refuses two ranks on one device.
+SyncBN (statistics over the global batch) is the parity mode: the 8 ranks must equal ONE process on
+the global batch.
+
+* d = 16, fp32: against the single-process fp32 oracle (src/train_fibinet.py:113-123 restated) on
+  the global batch -- per-step loss within 2e-5 (5e-4 after an Adam update) and every parameter's
+  displacement within the bars of tests/test_gpu_multirank.py (1e-3 relative; 5e-2 for the two
+  biases that precede a BatchNorm, whose true gradient is ~0).
+* d = 128, bf16 (the benched mode: bf16 GEMM operands, bf16 rows and gradient rows on the wire):
+  against the single-GPU trainer at B = 65 536 (same init, same batches) and against the fp32
+  oracle: eval |dAUC| (the 8-rank weights through the 8-rank forward vs through the fp32 oracle
+  forward) and 4-step trajectory |dAUC| (the 8-rank model vs the fp32 oracle's) <= 1e-4 on a
+  65 536-sample eval set (tests/test_gpu_coverage.py's protocol).  The values are written to
+  $FBN_PARITY_OUT/auc_parity_n8.json (default gpurun_out/parity/; committed as
+  profiles/r04_auc_parity_n8.json).
+
+The item table: 8 blocks of 1.25 M rows, block b drawn N(0,1) from a device generator seeded
+1000 + b (row 0 zeroed: padding_idx), so each rank materialises only its own block and the
+single-process references concatenate the same 8 blocks.
+"""
+import json
+import os
+import socket
+import time
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+WORLD = 8
+V = 10_000_000
+PER = 8192
+GB = WORLD * PER
+EVAL_N, EVAL_CHUNK = 65536, 8192
+AUC_BAR = 1e-4
+TABLE = "item_emb.weight"
+
+
+def _out_dir():
+    out = os.environ.get("FBN_PARITY_OUT", os.path.join("gpurun_out", "parity"))
+    os.makedirs(out, exist_ok=True)
+    return out
+
+
+def _progress(msg):
+    # long test: progress lines on disk (a run with no output for minutes looks hung)
+    with open(os.path.join(_out_dir(), "c4_progress.log"), "a") as f:
+        f.write(f"{time.strftime('%H:%M:%S')} {msg}\n")
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _cfg(d, dtype="fp32", vocab=V):
+    return {"embedding_dim": d, "vocab_size": vocab, "honour_config": True, "net_dropout": 0.0,
+            "compute_dtype": dtype}
+
+
+def _dense_init(d):
+    """Every parameter but the table, from the oracle's build (same creation order as the drop-in)."""
+    from oracle.fibinet_oracle import build_model
+    torch.manual_seed(0)
+    sd = build_model(None, _cfg(d, vocab=4), honour_config=True).state_dict()
+    return {k: v for k, v in sd.items() if k != TABLE}
+
+
+def _block(b, d, dev):
+    Vl = V // WORLD
+    g = torch.Generator(device=dev)
+    g.manual_seed(1000 + b)
+    t = torch.randn((Vl, d), generator=g, device=dev)
+    if b == 0:
+        t[0].zero_()
+    return t
+
+
+class _Shard:
+    """init_state[TABLE] for a rank: the trainer slices [lo:hi] of its own block only."""
+
+    def __init__(self, d, dev):
+        self.shape, self.d, self.dev = (V, d), d, dev
+
+    def __getitem__(self, sl):
+        Vl = V // WORLD
+        assert sl.start % Vl == 0 and sl.stop - sl.start == Vl, sl
+        return _block(sl.start // Vl, self.d, self.dev)
+
+
+def _full_table(d, dev):
+    return torch.cat([_block(b, d, dev) for b in range(WORLD)])
+
+
+def _batches(steps):
+    from ctr_recommendation_amd.data import make_batch
+    return [make_batch(900 + s, GB, V, signal="fields") for s in range(steps)]
+
+
+def _eval_chunks():
+    from ctr_recommendation_amd.data import make_batch
+    return [make_batch(4242 + i, EVAL_CHUNK, V, signal="fields") for i in range(EVAL_N // EVAL_CHUNK)]
+
+
+def _worker(rank, port, q, d, dtype, steps, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        from ctr_recommendation_amd.trainer import FiBiNETTrainer
+        dev = torch.device("cuda:0")
+        init = dict(_dense_init(d))
+        init[TABLE] = _Shard(d, dev)
+        tr = FiBiNETTrainer(_cfg(d, dtype), total_steps=40, batch_size=PER, device=dev, rank=rank, world=WORLD,
+                            init_state=init, stage_on_cpu=True, sync_bn=True, lazy_window=16)
+        del init
+        sl = slice(rank * PER, (rank + 1) * PER)
+        bs = [({k: v[sl].to(dev) for k, v in b.items()}, y[sl].to(dev)) for b, y in _batches(steps)]
+        losses = []
+        for s in range(steps):
+            nxt = bs[s + 1][0] if s + 1 < steps else None      # routed ahead, as the bench does
+            losses.append(tr.step(bs[s][0], bs[s][1], next_batch=nxt).item())
+            if rank == 0:
+                _progress(f"n8 d={d} {dtype} step {s} loss {losses[-1]:.6f}")
+        tr.check_ids()
+        per = EVAL_CHUNK // WORLD
+        preds = [tr.predict({k: v[rank * per:(rank + 1) * per].to(dev) for k, v in b.items()}).cpu()
+                 for b, _ in _eval_chunks()]
+        res = {"losses": losses, "pe": torch.cat(preds)}
+        sd = tr.state_dict()                                    # the table gathered on rank 0 only
+        if rank == 0:
+            if d == 16:
+                res["sd"] = sd
+            else:
+                # the fp32 oracle's forward with these weights (the eval-parity twin), here: the 5 GB
+                # state never crosses a file
+                from oracle.fibinet_oracle import build_model
+                twin = build_model(None, _cfg(d), honour_config=True)
+                twin.load_state_dict(sd)
+                twin.eval()
+                torch.set_num_threads(16)
+                with torch.no_grad():
+                    res["p_twin"] = torch.cat([twin(b) for b, _ in _eval_chunks()])
+                res["dense"] = {k: v for k, v in sd.items() if k != TABLE}
+        torch.save(res, f"{out}.{rank}")
+        q.put((rank, "ok"))
+    except Exception as e:  # surface worker failures in the test
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_ranks(d, dtype, steps, tmp_path):
+    out = str(tmp_path / "c4")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, port, q, d, dtype, steps, out)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=900) for _ in range(WORLD)]
+    for p in procs:
+        p.join(timeout=120)
+    assert all(r[1] == "ok" for r in res), res
+    got = [torch.load(f"{out}.{r}", weights_only=True) for r in range(WORLD)]
+    # eval chunk i: rank r predicted samples [r*per, (r+1)*per) of it -> reassemble in sample order
+    per = EVAL_CHUNK // WORLD
+    n_chunks = EVAL_N // EVAL_CHUNK
+    pe = torch.stack([g["pe"].view(n_chunks, per) for g in got], 1).reshape(-1)
+    return got, pe.numpy()
+
+
+def _oracle(d, steps):
+    from oracle.fibinet_oracle import OracleTrainer, build_model
+    ref = build_model(None, _cfg(d), honour_config=True)
+    sd = ref.state_dict()
+    sd.update(_dense_init(d))
+    sd[TABLE] = _full_table(d, torch.device("cuda:0")).cpu()
+    ref.load_state_dict(sd)
+    del sd
+    return ref, OracleTrainer(ref, total_steps=40)
+
+
+def test_c4_fp32_syncbn_8_ranks_vs_oracle(hip_device, tmp_path):
+    """C4 at d = 16, fp32, SyncBN: 8 ranks x (1.25 M rows, 8 192 samples) against one process on
+    the 65 536-sample global batch over the 10 M-row table."""
+    d, steps = 16, 3
+    _progress("C4 fp32 d=16: 8 ranks start")
+    got, _ = _run_ranks(d, "fp32", steps, tmp_path)
+    _progress("C4 fp32 d=16: ranks done, oracle")
+    ref, otr = _oracle(d, steps)
+    init = {k: v.clone() for k, v in ref.state_dict().items()}
+    for s, (b, y) in enumerate(_batches(steps)):
+        lr_, _ = otr.step(b, y)
+        for r in range(WORLD):                      # every rank reports the global-mean loss
+            assert abs(got[r]["losses"][s] - lr_) < (2e-5 if s == 0 else 5e-4), (r, s, got[r]["losses"][s], lr_)
+    bad = []
+    sd = got[0]["sd"]
+    for k, v in ref.state_dict().items():
+        h = sd[k]
+        if v.dtype == torch.int64:
+            if not torch.equal(h, v):
+                bad.append((k, h.tolist(), v.tolist()))
+            continue
+        if "running" in k:
+            dev_ = (h - v).abs().max().item()
+            if dev_ >= 1e-4 * max(1.0, v.abs().max().item()):
+                bad.append((k, dev_))
+            continue
+        dr, dh = (v - init[k]).double(), (h - init[k]).double()
+        tol = 5e-2 if k in ("mlp.0.bias", "mlp.4.bias") else 1e-3
+        rel = (dh - dr).norm().item() / (dr.norm().item() + 1e-30)
+        if rel > tol:
+            bad.append((k, rel))
+    assert not bad, bad
+    _progress("C4 fp32 d=16: passed")
+
+
+def test_c4_bf16_8_ranks_auc_parity(hip_device, tmp_path):
+    """C4 at d = 128 in the benched bf16 mode (bf16 rows and gradient rows on the wire), SyncBN:
+    8 ranks against the single-GPU trainer at B = 65 536 and against the fp32 oracle (AUC bars in
+    the module docstring); the record goes to auc_parity_n8.json."""
+    from ctr_recommendation_amd.trainer import FiBiNETTrainer
+    from ctr_recommendation_amd.utils import compute_auc
+    from oracle.fibinet_oracle import compute_auc as oracle_auc
+    d, steps = 128, 4
+    t0 = time.time()
+    _progress("C4 bf16 d=128: 8 ranks start")
+    got, p_n8 = _run_ranks(d, "bf16", steps, tmp_path)
+    t_ranks = time.time() - t0
+    _progress(f"C4 bf16 d=128: ranks done in {t_ranks:.0f}s; single-GPU trainer at B={GB}")
+    chunks = _eval_chunks()
+    y = np.concatenate([c[1].numpy() for c in chunks])
+    # the same global step on ONE GPU (bf16, f32 rows: nothing crosses a wire)
+    init = dict(_dense_init(d))
+    init[TABLE] = _full_table(d, hip_device)
+    n1 = FiBiNETTrainer(_cfg(d, "bf16"), total_steps=40, batch_size=GB, device=hip_device, init_state=init,
+                        lazy_window=16)
+    del init
+    n1_losses = [n1.step({k: v.to(hip_device) for k, v in b.items()}, t.to(hip_device)).item()
+                 for b, t in _batches(steps)]
+    p_n1 = np.concatenate([n1.predict({k: v.to(hip_device) for k, v in b.items()}).cpu().numpy() for b, _ in chunks])
+    n1_dense = {k: n1.p[k].detach().cpu() for k in got[0]["dense"]}
+    del n1
+    torch.cuda.empty_cache()
+    _progress("C4 bf16 d=128: fp32 oracle (CPU) on the global batch")
+    torch.set_num_threads(max(1, min(16, len(os.sched_getaffinity(0)))))
+    ref, otr = _oracle(d, steps)
+    o_losses = [otr.step(b, t)[0] for b, t in _batches(steps)]
+    ref.eval()
+    with torch.no_grad():
+        p_ref = torch.cat([ref(b) for b, _ in chunks]).numpy()
+    del ref, otr
+    p_twin = got[0]["p_twin"].numpy()
+    a_ref, a_n8, a_n1 = oracle_auc(y, p_ref), compute_auc(y, p_n8), compute_auc(y, p_n1)
+    dense_rel = max((got[0]["dense"][k] - n1_dense[k]).norm().item() / (n1_dense[k].norm().item() + 1e-30)
+                    for k in n1_dense if n1_dense[k].is_floating_point())
+    rec = {"config": "C4: 10 M item rows row-sharded over 8 ranks (1.25 M each), global batch 65 536 (8 192 per "
+                     "rank), d 128, bf16 GEMM operands, bf16 looked-up rows and gradient rows on the wire, SyncBN; "
+                     "8 ranks on one MI355X with host-staged gloo collectives",
+           "steps": steps, "eval_samples": EVAL_N, "eval_bar": AUC_BAR, "trajectory_bar": AUC_BAR,
+           "oracle_auc": a_ref,
+           "n8": {"auc": a_n8, "trajectory_dAUC": abs(a_n8 - a_ref), "eval_dAUC": abs(a_n8 - oracle_auc(y, p_twin)),
+                  "eval_max_abs_dp": float(np.abs(p_n8 - p_twin).max()),
+                  "trajectory_max_abs_dp": float(np.abs(p_n8 - p_ref).max()),
+                  "losses": got[0]["losses"]},
+           "n1_bf16": {"auc": a_n1, "trajectory_dAUC": abs(a_n1 - a_ref), "losses": n1_losses},
+           "n8_vs_n1": {"dAUC": abs(a_n8 - a_n1), "max_abs_dp": float(np.abs(p_n8 - p_n1).max()),
+                        "max_rel_loss": max(abs(a - b) / b for a, b in zip(got[0]["losses"], n1_losses)),
+                        "max_rel_dense_param_diff": dense_rel},
+           "oracle_losses": o_losses, "ranks_wall_s": round(t_ranks, 1)}
+    with open(os.path.join(_out_dir(), "auc_parity_n8.json"), "w") as f:
+        json.dump(rec, f, indent=1)
+    _progress("C4 bf16 d=128: " + json.dumps({k: rec[k] for k in ("oracle_auc", "n8", "n1_bf16", "n8_vs_n1")}))
+    assert a_ref > 0.55, a_ref
+    for r in range(WORLD):                          # every rank reports the same global-mean loss
+        assert np.allclose(got[r]["losses"], got[0]["losses"], rtol=1e-6, atol=0), r
+    for s in range(steps):                          # the bf16 wire rows: within 1e-3 of one GPU
+        assert abs(got[0]["losses"][s] - n1_losses[s]) <= 1e-3 * n1_losses[s], (s, got[0]["losses"], n1_losses)
+    assert rec["n8"]["eval_dAUC"] <= AUC_BAR, rec["n8"]
+    assert rec["n8"]["trajectory_dAUC"] <= AUC_BAR, rec["n8"]

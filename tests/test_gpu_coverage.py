@@ -223,7 +223,8 @@ TRAJ_AUC_BAR = {"fp32": 1e-4, "bf16_fwd": 1e-4, "bf16": 1e-4}   # 4 training ste
 @pytest.mark.parametrize("shape", ["small", "C3"])
 def test_auc_precision_modes_vs_oracle(hip_device, shape):
     """The three compute modes against the oracle (north star: AUC within 1e-4 of the CPU path on
-    the same synthetic batch).
+    the same synthetic batch), each trainer driven by the bench's own call: step(b, y,
+    next_batch=...) with eager launches.
       fp32      -- the reference's precision;
       bf16_fwd  -- C3's "bf16 fwd / fp32 grad accum": forward GEMM operands bf16, backward fp32;
       bf16      -- the benched headline mode: every GEMM operand bf16 (forward and backward).
@@ -260,12 +261,20 @@ def test_auc_precision_modes_vs_oracle(hip_device, shape):
                 return m(bb).float().numpy()
         return f
     rec = {"shape": {"d": d, "V": V, "B": B, "eval_samples": 65536}, "eval_bar": EVAL_AUC_BAR,
+           "call": "FiBiNETTrainer.step(b, y, next_batch=<following batch>), eager launches (bench.py's timed "
+                   "call: next-batch prefetch + pre-claims, side-stream window / prefetch, duplicate fold on the "
+                   "side stream)",
            "trajectory_bar": TRAJ_AUC_BAR, "steps": {}}
+    # the bench's own call (bench.py run_step, eager): step(b, y, next_batch=<the following batch>), so
+    # the next-batch table-Adam prefetch with its tagged pre-claims, the side-stream passes and the
+    # duplicate-gradient fold on the side stream all run inside the parity check
+    host = [make_batch(800 + s, B, V, signal="fields") for s in range(9)]
+    dev_b = [(_to(b, hip_device), y.to(hip_device)) for b, y in host]
     for s in range(8):
-        b, y = make_batch(800 + s, B, V, signal="fields")
-        db, dy = _to(b, hip_device), y.to(hip_device)
+        b, y = host[s]
+        db, dy = dev_b[s]
         for htr in htrs.values():
-            htr.step(db, dy)
+            htr.step(db, dy, next_batch=dev_b[s + 1][0])
         otr.step(b, y)
         o64.step({k: v.double() if v.is_floating_point() else v for k, v in b.items()}, y.double())
         print(f"[{shape}] step {s} done", flush=True)

@@ -57,6 +57,10 @@ def _worker(rank, world, port, q, D, dtype, sync_bn=True):
             losses.append(tr.step(bs[s][0], bs[s][1], next_batch=nxt).item())
         sd = tr.state_dict()          # the table on rank 0 only
         assert ("item_emb.weight" in sd) == (rank == 0)
+        # ... and it round-trips on every rank (rank 0 sends each rank its row block)
+        E0 = tr.E.clone()
+        tr.load_state_dict(sd)
+        assert torch.equal(tr.E, E0)
         tr.check_ids()
         be, _ = make_batch(777, B, V)
         pe = tr.predict({k: v[rank * per:(rank + 1) * per].to(dev) for k, v in be.items()}).cpu()

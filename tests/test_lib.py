@@ -61,3 +61,35 @@ def test_kernels_are_gfx950_code_objects():
     so = os.path.join(ROOT, "ctr_recommendation_amd", "libfibinet_hip.so")
     data = open(so, "rb").read()
     assert b"gfx950" in data
+
+
+def test_step_program_argument_encoding():
+    """Step programs pass recorded arguments through the x86-64 System V convention
+    (csrc/plan.cpp): integer-class values as 64-bit two's complement, a float as the double whose
+    low 32 bits are its bits (read from the low half of its xmm register by the callee)."""
+    import ctypes
+    import struct
+    from ctr_recommendation_amd import _lib
+    assert _lib._as_u64(None) == 0
+    assert _lib._as_u64(-1) == (1 << 64) - 1              # an int -1: low 32 bits 0xFFFFFFFF
+    assert _lib._as_u64(7) == 7
+    arr = (ctypes.c_int * 4)()
+    assert _lib._as_u64(arr) == ctypes.addressof(arr)
+    for x in (1.0, -2.5, 1e-8, 0.999, 3.4e38):
+        d = _lib._f32_in_f64(x)
+        bits = struct.unpack("<Q", struct.pack("<d", d))[0]
+        assert bits >> 32 == 0
+        assert struct.unpack("<f", struct.pack("<I", bits))[0] == struct.unpack("<f", struct.pack("<f", x))[0]
+    with pytest.raises(TypeError):
+        _lib._as_u64(ctypes.byref(ctypes.c_int(0)))
+    h = _lib.lib()
+    # every signature the recorder may meet fits the generic replay signature (<= 48 integer-class,
+    # <= 8 floating arguments)
+    for name, (_, args) in _lib.SIGNATURES.items():
+        nf = sum(1 for a in args if a in (_lib.F, _lib.D))
+        assert len(args) - nf <= 48 and nf <= 8, name
+    # an empty program runs (host only: no launches)
+    prog = _lib.StepProgram("cpu")
+    assert len(prog) == 0
+    prog.run()
+    del prog, h
