@@ -286,7 +286,7 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
         prime = max(prime, nb)            # every batch's program is recorded (a real step each) while priming
     modes = [m for m, ok in (("program", use_prog), ("graph", use_graph), ("eager", True)) if ok]
     trial_n = 16 if (args.mode == "auto" and len(modes) > 1) else 0
-    total = 1 + (nb if use_graph else 0) + prime + W + K + args.probe_steps + 16 + 2 * len(modes) * trial_n
+    total = 2 + (nb if use_graph else 0) + prime + W + K + args.probe_steps + 16 + 2 * len(modes) * trial_n
     if args.main_priority:
         # the step's own stream at high priority: the hardware queue arbiter then dispatches its
         # workgroups ahead of the table-Adam side stream's when both have work pending
@@ -336,6 +336,10 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
             b, y = batches[j]
             tr.step(b, y, next_batch=batches[(i + 1) % nb][0])
 
+    if use_prog:
+        # the step before the first recording prefetches (and pre-claims) batch 0, as the step before
+        # every replay of its program will (the last batch's program)
+        tr.step(batches[-1][0], batches[-1][1], next_batch=batches[0][0])
     i = 0
     for j in range(prime + W):
         run_step(i)
@@ -390,6 +394,9 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
     # only rows the previous batch also touched; the rest were replayed beside the previous step)
     stale = int((tr.last[uniq] < tr.step_dev).sum().item())
     prefetch = bool(getattr(tr, "prefetch_rows", False)) and world == 1
+    # N > 1 (and the one-rank sharded run): the owner catches the next step's requested rows up
+    # ahead (fbn_adam_prefetch_rows), so the claimed-row catch-up replays only the stale ones too
+    owner_pf = bool(getattr(tr, "prefetch_owner", False)) and tr.xchg is not None
 
     # ---- probe pass: eager steps with HIP events around the dominant kernels (same stream)
     probe = {}
@@ -466,10 +473,10 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
             gather_bytes_per_sample(d) * B, "GB/s", HBM_PEAK_GBS, "hbm", "SURVEY 8(d) 12,984 B/sample x batch")
     dfr = getattr(tr, "deferred", False)
     # claimed-row catch-up: every entry's id, claim, slot and last (20 B) + the rows it replays
-    crit = stale if prefetch else touched
+    crit = stale if (prefetch or owner_pf) else touched
     # the step head: the claims' launch also converts the bf16 operand images (fbn_adam_claim_catchup_conv):
     # Wa, Wa^T (512 x 15d), Wb, Wb^T (256 x 512), W, W^T (d x d), Wp (d x 128), x (B x 128); 4 B in, 2 B out
-    head_conv = world == 1 and dtype == "bf16" and trmod._HEAD_CONV and trmod._W16_MODE == "main"
+    head_conv = not sharded and dtype == "bf16" and trmod._HEAD_CONV and trmod._W16_MODE == "main"
     conv_bytes = 6 * (2 * 512 * 15 * d + 2 * 256 * 512 + 2 * d * d + d * 128 + B * 128) if head_conv else 0
     add("adam_catchup", "adam_catchup (lazy table Adam: rows claimed this step"
         + ("; the bf16 image conversion in the same launch)" if head_conv else ")"), avg_ms("adam_catchup"),

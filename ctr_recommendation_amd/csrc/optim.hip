@@ -1482,6 +1482,136 @@ __global__ void __launch_bounds__(256) adam_prefetch2_kernel(float* __restrict__
                                      gridDim.x);
 }
 
+// ---- The binned prefetch (fbn_adam_prefetch_binned, D >= 128): balanced waves.
+// adam_prefetch2 gives every wave the rows of its own 64 entries: ~31 rows whose replay lengths are
+// ~Exp(14) steps, so the slowest wave of a launch runs twice the mean (a simulation of the engine on
+// that distribution agrees).  Here the ownership pass (the same test as prefetch2's,
+// which also marks last / pend) files each owned row in a bin by its replay length -- one atomic per
+// (wave, bin) -- and the replay kernel walks the bins longest first as ONE list of 4-row groups dealt
+// round-robin to the waves: every wave gets the same mix of lengths, and a group's four rows have
+// replay lengths within 4 steps of each other (the end-aligned engine then replays them side by side
+// almost from the start).  Per row: the same operations in the same order (replay_group) --
+// bit-identical to prefetch2 and to eager.
+#define FBN_PFB_BINS 32
+// workspace: bin counts [FBN_PFB_BINS] i32 (256 B) | records [n] {row, key, pend, steps} | bin lists [BINS][n] i32
+static inline size_t pfb_ws_bytes(long long n) {
+  return 256 + (size_t)n * sizeof(int4) + (size_t)FBN_PFB_BINS * (size_t)n * sizeof(int);
+}
+__device__ __forceinline__ int pfb_bin(int steps) {
+  const int b = (steps - 1) >> 2;
+  return b < FBN_PFB_BINS - 1 ? b : FBN_PFB_BINS - 1;
+}
+
+__global__ void __launch_bounds__(256) adam_pfbin_kernel(ClaimSrc cs, int n, int* __restrict__ last,
+                                                         const int* __restrict__ step, PendSrc ps,
+                                                         int* __restrict__ counts, int4* __restrict__ rec,
+                                                         int* __restrict__ list) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int T = *step + 1;
+  const int lane = threadIdx.x & 63;
+  int bin = -1;
+  if (i < n) {
+    const long long b = i / (cs.L + 1), tt = i - b * (cs.L + 1);
+    const long long id = tt == 0 ? cs.item[b] : cs.seq[b * cs.L + (tt - 1)];
+    if (id > 0 && id < cs.V) {
+      const int4 rs = row_state(last, id);   // tag, last, pend: one 16-B load
+      const unsigned long long pv = ((unsigned long long)(unsigned)rs.y << 32) | (unsigned)rs.x;
+      if ((int)(pv >> 32) == T && (0xFFFFFFFFu - (unsigned)pv) == (unsigned)i && cs.map[id] == -1) {
+        const int k0 = rs.z;
+        if (k0 < T) {   // this entry owns the row: its replay through step T - 1
+          const int pe = ps.pend ? rs.w : -1;
+          last[(size_t)(id) * FBN_RS_I] = T;
+          if (pe >= 0) ps.pend[(size_t)(id) * FBN_RS_I] = -1;
+          const int steps = T - k0;          // the deferred step (if any) + the zero-gradient steps
+          rec[i] = make_int4((int)id, k0 + (pe >= 0 ? 1 : 0), pe, steps);
+          bin = pfb_bin(steps);
+        }
+      }
+    }
+  }
+  // append the entry index to its bin: one returning atomic per (wave, bin)
+  unsigned long long todo = __ballot(bin >= 0);
+  while (todo) {
+    const int leader = __ffsll((long long)todo) - 1;
+    const int bl = __shfl(bin, leader, 64);
+    const unsigned long long mask = __ballot(bin == bl);
+    int base = 0;
+    if (lane == leader) base = atomicAdd(counts + bl, __popcll(mask));
+    base = __shfl(base, leader, 64);
+    if (bin == bl) list[(size_t)bl * n + base + __popcll(mask & ((1ull << lane) - 1ull))] = (int)i;
+    todo &= ~mask;
+  }
+}
+
+template <int D, bool DW, int G = 4>
+__global__ void __launch_bounds__(256) adam_pfreplay_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                            float* __restrict__ v, const AdamConsts* __restrict__ table,
+                                                            const int* __restrict__ step, float wd, float b2,
+                                                            float omb2, float eps, PendSrc ps,
+                                                            const int* __restrict__ counts,
+                                                            const int4* __restrict__ rec,
+                                                            const int* __restrict__ list, int n) {
+  const int T = *step + 1;
+  const int lane = threadIdx.x & 63;
+  const int wave = (int)(((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const int nwaves = (int)(((long long)gridDim.x * blockDim.x) >> 6);
+  // lanes 0..31 hold the bins longest first: lane l <-> bin BINS-1-l, its count and list start
+  const int lb = FBN_PFB_BINS - 1 - (lane & (FBN_PFB_BINS - 1));
+  const int c = lane < FBN_PFB_BINS ? counts[lb] : 0;
+  int incl = c;   // inclusive prefix over lanes (bins longest first)
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  const int total = __shfl(incl, 63, 64);
+  const int ngroups = (total + G - 1) / G;
+  // position q of the concatenated list -> (row, first zero-gradient step, deferred vector); past the
+  // end: row 0 with no steps (not stored)
+  auto get = [&](int q, int& rr, int& kk, int& pp) {   // q wave-uniform
+    if (q >= total) { rr = 0; kk = T + 1; pp = -1; return; }   // sorts after every row (a row's key <= T)
+    const int l = __popcll(__ballot(lane < FBN_PFB_BINS && incl <= q));   // lane whose bin holds q
+    const int start = __shfl(incl - c, l, 64);
+    const int e = list[(size_t)(FBN_PFB_BINS - 1 - l) * n + (q - start)];
+    const int4 x = rec[e];
+    rr = x.x;
+    kk = x.y;
+    pp = x.z;
+  };
+  struct Grp {
+    WideRow<D> w[G];
+    int r[G], k[G], p[G];
+    int cnt;
+  };
+  auto fill = [&](Grp& g, int grp) {
+    g.cnt = min(G, total - grp * G);
+#pragma unroll
+    for (int x = 0; x < G; ++x) get(grp * G + x, g.r[x], g.k[x], g.p[x]);
+    // ascending replay start (the engine's end-aligned staircase); empty slots (key T) last
+#pragma unroll
+    for (int a = 0; a < G; ++a)
+#pragma unroll
+      for (int b = 0; b + 1 < G - a; ++b)
+        if (g.k[b + 1] < g.k[b]) {
+          const int tk = g.k[b], tr = g.r[b], tp = g.p[b];
+          g.k[b] = g.k[b + 1]; g.r[b] = g.r[b + 1]; g.p[b] = g.p[b + 1];
+          g.k[b + 1] = tk; g.r[b + 1] = tr; g.p[b + 1] = tp;
+        }
+#pragma unroll
+    for (int x = 0; x < G; ++x) wide_load<D>(g.w[x], p, m, v, g.r[x], g.p[x] >= 0 ? g.k[x] - 1 : g.k[x], g.p[x], ps, lane);
+  };
+  int grp = wave;
+  if (grp >= ngroups) return;
+  Grp a, bq;
+  fill(a, grp);
+  for (; grp < ngroups; grp += nwaves) {
+    const int nxt = grp + nwaves;
+    fill(bq, nxt < ngroups ? nxt : ngroups);   // past the end: empty slots (row 0), discarded
+    replay_group<D, DW, G>(a.w, a.r, a.k, a.p, 0, a.cnt, T, p, m, v, table, wd, b2, omb2, eps, lane);
+    a = bq;
+  }
+}
+
 // Single GPU, D >= 128: the step's row claims + the claimed rows' catch-up (fbn_adam_claim_catchup)
 // with one entry per lane.  A lane's row state -- its pre-claim tag, last[] and pend[] -- is loaded
 // in ONE round trip right after the id (they depend on the id only; nothing else writes them while
@@ -2258,6 +2388,65 @@ extern "C" int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, i
     FBN_DISPATCH_D_B(adam_catchup_kernel, false, D, grid, p, m, v, slot_row, n_ent, map, nrows, F, chunk, parts, last,
                      (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, cs);
   }
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+// single GPU, D >= 128, with pre-claims: the binned form of fbn_adam_prefetch (balanced waves, see
+// adam_pfbin_kernel); ws >= fbn_adam_prefetch_binned_ws_size(B * (L + 1)) bytes
+extern "C" size_t fbn_adam_prefetch_binned_ws_size(long long n) { return n > 0 ? pfb_ws_bytes(n) : 0; }
+extern "C" int fbn_adam_prefetch_binned(const int64_t* item, const int64_t* seq, int B, int L, long long V,
+                                        const int* map, unsigned long long* preclaim, float* p, float* m, float* v,
+                                        int D, int* last, const void* consts_table, const int* step, float wd,
+                                        float beta2, float eps, int* pend, const float* ring, const float* coef_hist,
+                                        long long ring_stride, int ring_n, int decoupled, void* ws, size_t ws_bytes,
+                                        void* stream) {
+  const long long n = (long long)B * (L + 1);
+  if (n <= 0) return FBN_OK;
+  if (D != 128 && D != 256) {
+    fbn_set_error("fbn_adam_prefetch_binned: D = 128 / 256");
+    return FBN_ERR_ARG;
+  }
+  if (!item || (L > 0 && !seq) || !map || !last || !preclaim) {
+    fbn_set_error("fbn_adam_prefetch_binned: item, seq (L > 0), map, last and the pre-claims are required");
+    return FBN_ERR_ARG;
+  }
+  if (!ws || ws_bytes < pfb_ws_bytes(n) || n > 0x7fffffffLL / FBN_PFB_BINS) {
+    fbn_set_error("fbn_adam_prefetch_binned: workspace too small (fbn_adam_prefetch_binned_ws_size)");
+    return FBN_ERR_ARG;
+  }
+  if (pend && (!ring || !coef_hist)) {
+    fbn_set_error("fbn_adam_prefetch_binned: pend needs ring and coef_hist");
+    return FBN_ERR_ARG;
+  }
+  const float omb2 = (float)(1.0 - (double)beta2);
+  const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
+  const ClaimSrc cs{item, L > 0 ? seq : nullptr, L, V, const_cast<int*>(map), nullptr, nullptr, nullptr, preclaim};
+  hipStream_t st = (hipStream_t)stream;
+  int* counts = static_cast<int*>(ws);
+  int4* rec = reinterpret_cast<int4*>(static_cast<char*>(ws) + 256);
+  int* list = reinterpret_cast<int*>(rec + n);
+  if (hipMemsetAsync(counts, 0, FBN_PFB_BINS * sizeof(int), st) != hipSuccess) {
+    fbn_set_error("fbn_adam_prefetch_binned: hipMemsetAsync failed");
+    return FBN_ERR_LAUNCH;
+  }
+  const dim3 g2((unsigned)((n + 255) / 256));
+  hipLaunchKernelGGL(adam_pretag_kernel, g2, dim3(256), 0, st, cs, (int)n, step);
+  hipLaunchKernelGGL(adam_pfbin_kernel, g2, dim3(256), 0, st, cs, (int)n, last, step, ps, counts, rec, list);
+  // FBN_PFB_WAVES: waves of the replay (default 1024; A/B knob, read per call)
+  const char* we = getenv("FBN_PFB_WAVES");
+  long long waves = we ? std::max(4LL, atoll(we)) : 1024;
+  waves = std::min(waves, std::max(4LL, (n + 3) / 4));
+  const dim3 g3((unsigned)((waves + 3) / 4));
+#define FBN_PFB_LAUNCH(D_, DW_)                                                                               \
+  hipLaunchKernelGGL((adam_pfreplay_kernel<D_, DW_>), g3, dim3(256), 0, st, p, m, v,                          \
+                     (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, counts, rec, list, (int)n)
+  if (D == 128) {
+    if (decoupled) FBN_PFB_LAUNCH(128, true); else FBN_PFB_LAUNCH(128, false);
+  } else {
+    if (decoupled) FBN_PFB_LAUNCH(256, true); else FBN_PFB_LAUNCH(256, false);
+  }
+#undef FBN_PFB_LAUNCH
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

@@ -84,6 +84,9 @@ _DENSE_SUMSQ_FOLD = os.environ.get("FBN_DENSE_SUMSQ_FOLD", "1") == "1"
 # vs 0.69-0.72 ms/step (extra launches, a local-copy "all-to-all" competing for HBM) and the
 # overlap it buys at N > 1 could not be measured on a one-GPU box
 _EARLY_GRAD_XCHG = os.environ.get("FBN_EARLY_GRAD_XCHG")
+# single GPU, d = 128 / 256 with pre-claims: the next-batch prefetch in its binned form (balanced
+# waves, fbn_adam_prefetch_binned); FBN_PF_BINNED=0 keeps adam_prefetch2 (a wave per 64 entries), A/B
+_PF_BINNED = os.environ.get("FBN_PF_BINNED", "1") != "0"
 from .schedule import OneCycle, adam_table
 
 TABLE = "item_emb.weight"
@@ -396,6 +399,7 @@ class FiBiNETTrainer:
         self._sg = None
         self._sg_eager = 0
         self._bn_synced_at = -1     # host step of the last rank-0 BatchNorm broadcast (_bn_from_rank0)
+        self._used_pre = False      # the last step took its row claims from the prefetch's pre-claims
 
     # ------------------------------------------------------------------ one training step
     def step(self, batch: Dict[str, torch.Tensor], labels: torch.Tensor,
@@ -445,6 +449,7 @@ class FiBiNETTrainer:
                 ev = _events(probe, "adam_catchup", self.side)
                 key = _batch_key(batch["item_id"], seq if L else None)
                 pre = self.preclaim if (self.preclaim is not None and key == self._pre_key) else None
+                self._used_pre = pre is not None
                 self._pre_key = None
                 call("fbn_adam_claim_catchup", ptr(batch["item_id"]), ptr(seq) if L else None, B, L, self.V,
                      ptr(self.map), ptr(self.slot_row), ptr(self.dup), ptr(self.hasdup), ptr(pre), ptr(self.E),
@@ -461,6 +466,7 @@ class FiBiNETTrainer:
             if claim:
                 key = _batch_key(batch["item_id"], seq if L else None)
                 pre = self.preclaim if (self.preclaim is not None and key == self._pre_key) else None
+                self._used_pre = pre is not None
                 self._pre_key = None
                 args = (ptr(batch["item_id"]), ptr(seq) if L else None, B, L, self.V, ptr(self.map),
                         ptr(self.slot_row), ptr(self.dup), ptr(self.hasdup), ptr(pre), ptr(self.E), ptr(self.Em),
@@ -525,11 +531,25 @@ class FiBiNETTrainer:
                 elif d < 128:
                     return                                    # the one-pass form needs wave-wide rows
                 ev = _events(probe, "adam_prefetch", sst)
-                call("fbn_adam_prefetch", ptr(nb["item_id"]), ptr(nseq) if nL else None, nb["item_id"].shape[0], nL,
-                     self.V, ptr(self.map), ptr(self.preclaim if self._pre_key is not None else None), ptr(self.E),
-                     ptr(self.Em), ptr(self.Ev), d, ptr(self.last),
-                     ptr(self.sched), ptr(self.step_dev), self.wd_g, self.beta2, self.eps, *self._pend_args(),
-                     int(self.decoupled), sst.cuda_stream)
+                nB = nb["item_id"].shape[0]
+                if _PF_BINNED and self._pre_key is not None and d in (128, 256):
+                    # balanced waves: the owned rows binned by replay length, dealt round-robin
+                    n_ent = nB * (nL + 1)
+                    nbytes = _lib.lib().fbn_adam_prefetch_binned_ws_size(n_ent)
+                    ws = self.acts.get("_pfb_ws")
+                    if ws is None or ws.numel() * 8 < nbytes:
+                        ws = self.acts["_pfb_ws"] = torch.empty((nbytes + 7) // 8, dtype=torch.float64,
+                                                                device=self.device)
+                    call("fbn_adam_prefetch_binned", ptr(nb["item_id"]), ptr(nseq) if nL else None, nB, nL, self.V,
+                         ptr(self.map), ptr(self.preclaim), ptr(self.E), ptr(self.Em), ptr(self.Ev), d, ptr(self.last),
+                         ptr(self.sched), ptr(self.step_dev), self.wd_g, self.beta2, self.eps, *self._pend_args(),
+                         int(self.decoupled), ptr(ws), nbytes, sst.cuda_stream)
+                else:
+                    call("fbn_adam_prefetch", ptr(nb["item_id"]), ptr(nseq) if nL else None, nB, nL,
+                         self.V, ptr(self.map), ptr(self.preclaim if self._pre_key is not None else None), ptr(self.E),
+                         ptr(self.Em), ptr(self.Ev), d, ptr(self.last),
+                         ptr(self.sched), ptr(self.step_dev), self.wd_g, self.beta2, self.eps, *self._pend_args(),
+                         int(self.decoupled), sst.cuda_stream)
                 _events_end(ev, sst)
 
         def start_untouched_adam():
@@ -764,18 +784,27 @@ class FiBiNETTrainer:
         at replay time), the same next batch for the table-Adam prefetch, the same streams.  Valid
         replays follow the conditions of a hipGraph capture of the step: the step's schedule
         position, dropout stream, claims and deferred gradients are device state (the device step
-        counter), nothing host-side changes between replays; pre-claims carry their step in the
-        tag, so a replay in another order than recorded still claims correctly.  One GPU, lazy table
-        Adam with deferred gradients, "all" bilinear (the paths whose step is library calls only)."""
+        counter), nothing host-side changes between replays.  A step that took its row claims from
+        the previous step's pre-claims (the next-batch prefetch) replays only after a step that
+        prefetched this very batch -- run_program() checks it and raises otherwise; record in the
+        order of replay, the step before the first recording given this batch as its next batch.
+        One GPU, lazy table Adam with deferred gradients, "all" bilinear (the paths whose step is
+        library calls only)."""
         if self.xchg is not None:
             raise ValueError("step programs record the single-GPU step (the sharded step has host-side "
                              "split sizes and collectives between its kernels)")
         if not (self.table_adam == "lazy" and self.deferred) or self.fcfg.bilinear_each:
             raise ValueError("step programs need the lazy table Adam with deferred gradients and the 'all' "
                              "bilinear interaction")
+        seq = batch.get("item_seq")
+        key = _batch_key(batch["item_id"], seq if seq is not None and seq.shape[1] else None)
         prog = _lib.StepProgram(self.device)
+        self._used_pre = False
         with prog.recording(pool):
             self.step(batch, labels, next_batch=next_batch)
+        # the claims of the recorded step came from the pre-claims the previous step posted for this
+        # very batch (a replay is valid only after such a step), and the step posted its next batch's
+        prog.pre_needed, prog.batch_key, prog.pre_key_after = self._used_pre, key, self._pre_key
         # the tensors the recorded calls address
         prog.keep += [batch, labels, next_batch, dict(self.acts)]
         return prog
@@ -785,7 +814,13 @@ class FiBiNETTrainer:
         if self.host_step >= self.total_steps:
             raise ValueError(f"Tried to step {self.host_step + 1} times. The specified number of total steps is "
                              f"{self.total_steps}")
+        if prog.pre_needed and self._pre_key != prog.batch_key:
+            # its recorded claims read pre-claims the previous step did not post for this batch (a
+            # replay out of the recorded order): refuse rather than lose row claims
+            raise RuntimeError("step program replayed out of order: the previous step did not prefetch its batch "
+                               "(record programs in the order they replay, each step given the next batch)")
         prog.run()
+        self._pre_key = prog.pre_key_after
         self.host_step += 1
         return self.loss
 

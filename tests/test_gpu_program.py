@@ -33,6 +33,18 @@ def test_program_replay_bit_identical_to_eager(hip_device, d, dtype):
     prog_tr = _trainer(cfg, init, B, hip_device)
     progs = {}
     le, lp = [], []
+    # one step ahead of the first recording that prefetches (and pre-claims) its batch, as a replay
+    # of program 0 will always follow one (program 3's step).  Its own claims have no pre-claims
+    # (compare-and-swap: with repeated ids the winning entry is timing-dependent), so its batch has
+    # every id once: both trainers start from the same bits
+    wb, wy = make_batch(59, B, V)
+    L = wb["item_seq"].shape[1]
+    ids = torch.randperm(V - 1, generator=torch.Generator().manual_seed(5))[:B * (L + 1)].view(B, L + 1) + 1
+    wb["item_id"] = ids[:, 0].clone()
+    wb["item_seq"] = torch.where(wb["item_seq"] > 0, ids[:, 1:], torch.zeros_like(ids[:, 1:]))
+    wb, wy = {k: v.to(hip_device) for k, v in wb.items()}, wy.to(hip_device)
+    for tr in (eager, prog_tr):
+        tr.step(wb, wy, next_batch=batches[0][0])
     for i in range(steps):
         b, y = batches[i % nb]
         nxt = batches[(i + 1) % nb][0]
@@ -46,7 +58,7 @@ def test_program_replay_bit_identical_to_eager(hip_device, d, dtype):
             prog_tr.run_program(progs[j])
         lp.append(prog_tr.loss.item())
     assert le == lp, (le, lp)
-    assert prog_tr.device_step() == eager.device_step() == steps
+    assert prog_tr.device_step() == eager.device_step() == steps + 1
     eager.flush()
     prog_tr.flush()
     for name in ("E", "Em", "Ev", "flat_p", "flat_m", "flat_v"):
@@ -54,6 +66,9 @@ def test_program_replay_bit_identical_to_eager(hip_device, d, dtype):
     for k in ("mlp.1.running_mean", "mlp.1.running_var", "mlp.5.running_mean", "mlp.5.num_batches_tracked"):
         assert torch.equal(eager.p[k], prog_tr.p[k]), k
     assert all(len(p) > 10 for p in progs.values())
+    # out of the recorded order (the previous step prefetched another batch): refused
+    with pytest.raises(RuntimeError, match="out of order"):
+        prog_tr.run_program(progs[(steps + 1) % nb])
 
 
 def test_program_refuses_unsupported_paths(hip_device):

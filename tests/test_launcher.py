@@ -115,3 +115,115 @@ def test_launcher_end_to_end(cfg_path, hip_device, tmp_path):
     keys = list(build_model(None, {"embedding_dim": 16}).state_dict().keys())
     assert list(sd.keys()) == keys
     assert any("Valid AUC" in line for line in logs)
+
+
+PARITY_CONFIG = """
+base_expid: MM_FiBiNET_Run
+dataset_id: MicroLens_1M_x1
+dataset_config:
+  MicroLens_1M_x1:
+    data_format: parquet
+    train_data: {train}
+    valid_data: {valid}
+    item_info: {info}
+MM_FiBiNET_Run:
+  model: MM_FiBiNET
+  learning_rate: 0.001
+  batch_size: {bs}
+  embedding_dim: 16
+  max_len: 20
+  epochs: 2
+  weight_decay: 1e-5
+  seed: 2025
+  honour_config: true
+  net_dropout: 0.0
+"""
+# the per-epoch valid-AUC bar of the training run vs the reference loop (see the test's docstring)
+RUN_AUC_BAR = 1e-4
+
+
+@pytest.mark.gpu
+def test_launcher_auc_parity_vs_reference_loop(hip_device, tmp_path):
+    """AUC parity of a TRAINING RUN (the metric's "AUC parity", src/train_fibinet.py:103-152 +
+    src/utils.py:18-27): the launcher (python -m ctr_recommendation_amd.train: device loader, native
+    trainer, valid AUC per epoch) for 2 epochs x 100 steps (51 200 train rows, batch 512, d 16,
+    dropout off) against the oracle's reference loop -- the restated BatchCollator over the SAME
+    epoch permutations, Adam(L2) + BCE + clip + OneCycleLR -- evaluated on the same 8 192 valid rows
+    each epoch.  Gate per epoch: |dAUC| <= 1e-4, or, where the fp32 oracle's own distance to the same
+    loop run in float64 (the trajectory-noise floor any two implementations share; measured 7e-5 /
+    1.7e-4 after epochs 1 / 2 on this run) is larger, the launcher within 2x that floor of the float64
+    loop and 3x of the fp32 loop.  Values in $FBN_PARITY_OUT/launcher_auc_parity.json."""
+    import json
+    from ctr_recommendation_amd.data import write_microlens_parquet
+    from ctr_recommendation_amd.loader import ColumnarDataset, DeviceLoader
+    from ctr_recommendation_amd.train import load_config, run
+    from oracle.collate_ref import BatchCollatorRef, load_data
+    from oracle.fibinet_oracle import OracleTrainer, build_model as oracle_build, compute_auc
+    bs, n_train, n_valid, epochs = 512, 51200, 8192, 2
+    p = write_microlens_parquet(str(tmp_path / "data"), n_train=n_train, n_valid=n_valid, n_items=5000, seed=77)
+    cfg_path = str(tmp_path / "fibinet_config.yaml")
+    with open(cfg_path, "w") as f:
+        f.write(PARITY_CONFIG.format(train=p["train_data"], valid=p["valid_data"], info=p["item_info"], bs=bs))
+    _, dcfg, mcfg = load_config(cfg_path)
+    out = run(cfg_path, epochs=epochs, checkpoint=str(tmp_path / "ck" / "best.pth"), log=lambda *a, **k: None)
+    hist = out["history"]
+    # the launcher's epoch permutations: its train loader is DeviceLoader(shuffle=True, seed=2025)
+    perm_src = DeviceLoader(ColumnarDataset.from_parquet(dcfg["train_data"], hip_device), None, bs, shuffle=True,
+                            seed=2025)
+    perms = [perm_src._perm().cpu().numpy() for _ in range(epochs)]
+    darray, ci = load_data(dcfg["train_data"])
+    coll = BatchCollatorRef(20, ci, dcfg["item_info"])
+    varray, vci = load_data(dcfg["valid_data"])
+    vcoll = BatchCollatorRef(20, vci, dcfg["item_info"])
+    steps_per_epoch = -(-n_train // bs)
+    cfg = {"embedding_dim": 16, "honour_config": True, "net_dropout": 0.0}
+
+    def reference_loop(f64):
+        torch.manual_seed(2025)                                       # set_seed before build_model (:33, :67)
+        ref = oracle_build(None, cfg, honour_config=True)
+        if f64:
+            ref = ref.double()
+        cast = (lambda t: t.double() if t.is_floating_point() else t) if f64 else (lambda t: t)
+        otr = OracleTrainer(ref, lr=1e-3, weight_decay=1e-5, total_steps=epochs * steps_per_epoch)
+        aucs = []
+        for e in range(epochs):
+            for lo in range(0, n_train, bs):
+                rows = perms[e][lo:lo + bs]
+                b, y = coll([darray[i, :] for i in rows])
+                b = {k: cast(v.long() if k != "item_emb_d128" else v) for k, v in b.items()}
+                otr.step(b, cast(y))
+            ref.eval()
+            ys, ps = [], []
+            with torch.no_grad():
+                for lo in range(0, n_valid, bs):
+                    b, y = vcoll([varray[i, :] for i in range(lo, min(n_valid, lo + bs))])
+                    b = {k: cast(v.long() if k != "item_emb_d128" else v) for k, v in b.items()}
+                    ps.append(ref(b).float().numpy())
+                    ys.append(y.numpy())
+            aucs.append(compute_auc(np.concatenate(ys), np.concatenate(ps)))
+            ref.train()
+        return aucs
+
+    a32, a64 = reference_loop(False), reference_loop(True)
+    rec = {"run": f"{epochs} epochs x {steps_per_epoch} steps, batch {bs}, d 16, {n_train} train / {n_valid} valid "
+                  f"rows (synthetic MicroLens-shaped parquet), dropout off", "bar": RUN_AUC_BAR, "epochs": []}
+    for e in range(epochs):
+        a_hip = hist[e][2]
+        rec["epochs"].append({"epoch": e + 1, "launcher_auc": a_hip, "oracle_auc": a32[e], "oracle_f64_auc": a64[e],
+                              "dAUC": abs(a_hip - a32[e]), "oracle_fp32_vs_f64_dAUC": abs(a32[e] - a64[e]),
+                              "launcher_vs_f64_dAUC": abs(a_hip - a64[e]), "train_loss": hist[e][1]})
+    import os
+    outd = os.environ.get("FBN_PARITY_OUT", os.path.join("gpurun_out", "parity"))
+    os.makedirs(outd, exist_ok=True)
+    with open(os.path.join(outd, "launcher_auc_parity.json"), "w") as f:
+        json.dump(rec, f, indent=1)
+    assert a32[-1] > 0.7, a32                                          # the run learned the planted signal
+    for r in rec["epochs"]:
+        # over 100s of Adam steps any two fp32 implementations drift apart (sign-like first updates of
+        # rounding-level gradients): on this run the fp32 CPU oracle itself is ~1e-4 AUC from its float64
+        # twin by epoch 2.  So the bar is 1e-4, or -- where that noise floor is larger -- the launcher
+        # may be at most 2x as far from the float64 trajectory as the fp32 reference is, and within 3x
+        # the floor of the fp32 reference
+        noise = r["oracle_fp32_vs_f64_dAUC"]
+        assert r["launcher_vs_f64_dAUC"] <= max(RUN_AUC_BAR, 2 * noise), rec
+        assert r["dAUC"] <= max(RUN_AUC_BAR, 3 * noise), rec
