@@ -9,9 +9,9 @@ SyncBN (statistics over the global batch) is the parity mode: the 8 ranks must e
 the global batch.
 
 * d = 16, fp32: against the single-process fp32 oracle (src/train_fibinet.py:113-123 restated) on
-  the global batch -- per-step loss within 2e-5 (5e-4 after an Adam update) and every parameter's
-  displacement within the bars of tests/test_gpu_multirank.py (1e-3 relative; 5e-2 for the two
-  biases that precede a BatchNorm, whose true gradient is ~0).
+  the global batch -- per-step loss within 2e-5 (5e-4 after an Adam update); every parameter's
+  displacement held to the float64 oracle: within max(1e-3, 3x the fp32 oracle's own distance to it)
+  (the test's docstring says why).
 * d = 128, bf16 (the benched mode: bf16 GEMM operands, bf16 rows and gradient rows on the wire):
   against the single-GPU trainer at B = 65 536 (same init, same batches) and against the fp32
   oracle: eval |dAUC| (the 8-rank weights through the 8-rank forward vs through the fp32 oracle
@@ -196,20 +196,33 @@ def _oracle(d, steps):
 
 def test_c4_fp32_syncbn_8_ranks_vs_oracle(hip_device, tmp_path):
     """C4 at d = 16, fp32, SyncBN: 8 ranks x (1.25 M rows, 8 192 samples) against one process on
-    the 65 536-sample global batch over the 10 M-row table."""
+    the 65 536-sample global batch over the 10 M-row table.
+
+    Losses: within 2e-5 (5e-4 after an Adam update) of the fp32 oracle, on every rank.
+    Parameters: Adam's first updates are sign(g) * lr per element, and at a 65 536-sample batch many
+    gradient elements sit at rounding level, so ANY two fp32 implementations flip some of them -- the
+    fp32 CPU oracle itself moves up to ~1e-2 (relative displacement norm) from its float64 twin here.
+    So each parameter's displacement is held to the float64 oracle: the 8 ranks' distance to it within
+    max(1e-3, 3x the fp32 oracle's own distance), recorded in $FBN_PARITY_OUT/c4_fp32_parity.json."""
     d, steps = 16, 3
     _progress("C4 fp32 d=16: 8 ranks start")
     got, _ = _run_ranks(d, "fp32", steps, tmp_path)
-    _progress("C4 fp32 d=16: ranks done, oracle")
+    _progress("C4 fp32 d=16: ranks done, oracles (fp32, float64)")
     ref, otr = _oracle(d, steps)
     init = {k: v.clone() for k, v in ref.state_dict().items()}
+    r64 = _oracle(d, steps)[0].double()
+    r64.load_state_dict({k: v.double() if v.is_floating_point() else v for k, v in init.items()})
+    from oracle.fibinet_oracle import OracleTrainer
+    o64 = OracleTrainer(r64, total_steps=40)
     for s, (b, y) in enumerate(_batches(steps)):
         lr_, _ = otr.step(b, y)
+        o64.step({k: v.double() if v.is_floating_point() else v for k, v in b.items()}, y.double())
         for r in range(WORLD):                      # every rank reports the global-mean loss
             assert abs(got[r]["losses"][s] - lr_) < (2e-5 if s == 0 else 5e-4), (r, s, got[r]["losses"][s], lr_)
-    bad = []
-    sd = got[0]["sd"]
-    for k, v in ref.state_dict().items():
+    sd, s32, s64 = got[0]["sd"], ref.state_dict(), r64.state_dict()
+    rec, bad = {"config": "C4: 10 M rows over 8 ranks, global batch 65 536, d 16, fp32, SyncBN", "steps": steps,
+                "params": {}}, []
+    for k, v in s32.items():
         h = sd[k]
         if v.dtype == torch.int64:
             if not torch.equal(h, v):
@@ -220,11 +233,15 @@ def test_c4_fp32_syncbn_8_ranks_vs_oracle(hip_device, tmp_path):
             if dev_ >= 1e-4 * max(1.0, v.abs().max().item()):
                 bad.append((k, dev_))
             continue
-        dr, dh = (v - init[k]).double(), (h - init[k]).double()
-        tol = 5e-2 if k in ("mlp.0.bias", "mlp.4.bias") else 1e-3
-        rel = (dh - dr).norm().item() / (dr.norm().item() + 1e-30)
-        if rel > tol:
-            bad.append((k, rel))
+        d64 = (s64[k] - init[k].double())
+        den = d64.norm().item() + 1e-30
+        rel_hip = ((h - init[k]).double() - d64).norm().item() / den
+        rel_32 = ((v - init[k]).double() - d64).norm().item() / den
+        rec["params"][k] = {"hip_vs_f64": rel_hip, "fp32_oracle_vs_f64": rel_32}
+        if rel_hip > max(1e-3, 3 * rel_32):
+            bad.append((k, rel_hip, rel_32))
+    with open(os.path.join(_out_dir(), "c4_fp32_parity.json"), "w") as f:
+        json.dump(rec, f, indent=1)
     assert not bad, bad
     _progress("C4 fp32 d=16: passed")
 

@@ -14,23 +14,42 @@ from oracle.fibinet_oracle import build_model as oracle_build
 pytestmark = pytest.mark.gpu
 
 
-def _trainer(cfg, init, B, dev):
-    return FiBiNETTrainer(cfg, total_steps=60, batch_size=B, device=dev,
+def _trainer(cfg, init, B, dev, det=False):
+    return FiBiNETTrainer(cfg, total_steps=60, batch_size=B, device=dev, deterministic=det,
                           init_state={k: v.clone() for k, v in init.items()})
 
 
-@pytest.mark.parametrize("d,dtype", [(128, "bf16"), (128, "fp32"), (16, "fp32"), (128, "bf16_fwd")])
-def test_program_replay_bit_identical_to_eager(hip_device, d, dtype):
+def _unique_ids(b, V, g, pool):
+    """The batch's ids redrawn without repetition from `pool` (ids recur ACROSS batches, never within
+    one: a row named twice in a batch is folded by float atomics, whose rounding follows arrival order
+    -- two runs of the same step differ there unless the trainer is deterministic)."""
+    B, L = b["item_seq"].shape
+    ids = pool[torch.randperm(len(pool), generator=g)[:B * (L + 1)]].view(B, L + 1)
+    b["item_id"] = ids[:, 0].clone()
+    b["item_seq"] = torch.where(b["item_seq"] > 0, ids[:, 1:], torch.zeros_like(ids[:, 1:]))
+    return b
+
+
+@pytest.mark.parametrize("d,dtype,det", [(128, "bf16", False), (128, "fp32", False), (16, "fp32", False),
+                                         (128, "bf16_fwd", False), (128, "bf16", True)])
+def test_program_replay_bit_identical_to_eager(hip_device, d, dtype, det):
+    """det=False: the bench's stream structure (duplicate fold on the side stream, float atomics),
+    ids unique within a batch; det=True: deterministic mode (fixed-point fold on the main stream)
+    with ids repeated inside batches."""
     V, B, nb, steps = 40000, 512, 4, 14
     cfg = {"embedding_dim": d, "vocab_size": V, "compute_dtype": dtype}
     torch.manual_seed(0)
     init = oracle_build(None, dict(cfg, honour_config=False)).state_dict()
+    g = torch.Generator().manual_seed(7)
+    pool = torch.randperm(V - 1, generator=g)[:20000] + 1
     batches = []
     for j in range(nb):
         b, y = make_batch(60 + j, B, V)
+        if not det:
+            b = _unique_ids(b, V, g, pool)
         batches.append(({k: v.to(hip_device) for k, v in b.items()}, y.to(hip_device)))
-    eager = _trainer(cfg, init, B, hip_device)
-    prog_tr = _trainer(cfg, init, B, hip_device)
+    eager = _trainer(cfg, init, B, hip_device, det)
+    prog_tr = _trainer(cfg, init, B, hip_device, det)
     progs = {}
     le, lp = [], []
     # one step ahead of the first recording that prefetches (and pre-claims) its batch, as a replay
@@ -38,10 +57,7 @@ def test_program_replay_bit_identical_to_eager(hip_device, d, dtype):
     # (compare-and-swap: with repeated ids the winning entry is timing-dependent), so its batch has
     # every id once: both trainers start from the same bits
     wb, wy = make_batch(59, B, V)
-    L = wb["item_seq"].shape[1]
-    ids = torch.randperm(V - 1, generator=torch.Generator().manual_seed(5))[:B * (L + 1)].view(B, L + 1) + 1
-    wb["item_id"] = ids[:, 0].clone()
-    wb["item_seq"] = torch.where(wb["item_seq"] > 0, ids[:, 1:], torch.zeros_like(ids[:, 1:]))
+    wb = _unique_ids(wb, V, g, pool)
     wb, wy = {k: v.to(hip_device) for k, v in wb.items()}, wy.to(hip_device)
     for tr in (eager, prog_tr):
         tr.step(wb, wy, next_batch=batches[0][0])
