@@ -4,15 +4,23 @@
 #pragma once
 #include "common.h"
 
+// part: 0 = the value rounded to bf16 ("hi"), 1 = the rounding residual x - hi rounded to bf16 ("lo"):
+// hi + lo carries 16 significant bits of x (the split-bf16 images of the bf16_fwd backward GEMMs);
+// dld: the destination's row stride in elements (0 = cols), so images can be laid side by side
 struct ConvJob {
   const float* src;
   short* dst;
-  int rows, cols, ld, trans, seg, off0, off1;
+  int rows, cols, ld, trans, seg, off0, off1, part, dld;
 };
+#define FBN_CONV_MAX 16
 struct ConvJobs {
-  ConvJob j[8];
-  int tile0[9];   // first 64x64 output tile of each job (prefix sum)
+  ConvJob j[FBN_CONV_MAX];
+  int tile0[FBN_CONV_MAX + 1];   // first 64x64 output tile of each job (prefix sum)
 };
+__device__ __forceinline__ short conv_bf(float x, int part) {
+  const short h = f2bf(x);
+  return part ? f2bf(x - bf2f(h)) : h;
+}
 // One 64x64 output tile per workgroup, four consecutive outputs per thread (one 8-B bf16x4 store):
 // a plain job reads four source columns at once (16-B load when they are contiguous and aligned:
 // the remap offsets and seg are multiples of 4); a transposed job reads its source tile along the
@@ -29,6 +37,7 @@ __device__ __forceinline__ void convert_tile(const ConvJobs& jobs, int njobs, in
   if (!J.trans) {
     const int j = j0 + 4 * tq;
     if (j >= J.cols) return;
+    const int dld = J.dld ? J.dld : J.cols;
     const bool full = j + 4 <= J.cols;
     const int b = j + (j < J.seg ? J.off0 : J.off1);
     const bool vec = full && !(J.ld & 3) && !(b & 3) && (J.seg == 0x7fffffff || !(J.seg & 3) || j + 4 <= J.seg ||
@@ -52,13 +61,14 @@ __device__ __forceinline__ void convert_tile(const ConvJobs& jobs, int njobs, in
     for (int k = 0; k < 4; ++k) {
       const int i = i0 + tr + 16 * k;
       if (i >= J.rows) continue;
-      short* d = J.dst + (size_t)i * J.cols + j;
-      if (full && !(J.cols & 3)) {
-        *reinterpret_cast<bf16x4*>(d) = (bf16x4){f2bf(val[k][0]), f2bf(val[k][1]), f2bf(val[k][2]), f2bf(val[k][3])};
+      short* d = J.dst + (size_t)i * dld + j;
+      if (full && !(dld & 3)) {
+        *reinterpret_cast<bf16x4*>(d) = (bf16x4){conv_bf(val[k][0], J.part), conv_bf(val[k][1], J.part),
+                                                 conv_bf(val[k][2], J.part), conv_bf(val[k][3], J.part)};
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          if (j + e < J.cols) d[e] = f2bf(val[k][e]);
+          if (j + e < J.cols) d[e] = conv_bf(val[k][e], J.part);
       }
     }
     return;
@@ -77,14 +87,15 @@ __device__ __forceinline__ void convert_tile(const ConvJobs& jobs, int njobs, in
   __syncthreads();
   const int j = j0 + 4 * tq;
   if (j >= J.cols) return;
+  const int dld = J.dld ? J.dld : J.cols;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int r = tr + 16 * k, i = i0 + r;
     if (i >= J.rows) continue;
-    short* d = J.dst + (size_t)i * J.cols + j;
-    const bf16x4 v = {f2bf(tile[4 * tq][r]), f2bf(tile[4 * tq + 1][r]), f2bf(tile[4 * tq + 2][r]),
-                      f2bf(tile[4 * tq + 3][r])};
-    if (j + 4 <= J.cols && !(J.cols & 3)) {
+    short* d = J.dst + (size_t)i * dld + j;
+    const bf16x4 v = {conv_bf(tile[4 * tq][r], J.part), conv_bf(tile[4 * tq + 1][r], J.part),
+                      conv_bf(tile[4 * tq + 2][r], J.part), conv_bf(tile[4 * tq + 3][r], J.part)};
+    if (j + 4 <= J.cols && !(dld & 3)) {
       *reinterpret_cast<bf16x4*>(d) = v;
     } else {
 #pragma unroll
@@ -95,10 +106,10 @@ __device__ __forceinline__ void convert_tile(const ConvJobs& jobs, int njobs, in
 }
 
 
-// host: pack n <= 8 ConvJob records into the kernel argument; returns the 64 x 64 tile count
+// host: pack n <= FBN_CONV_MAX ConvJob records into the kernel argument; returns the 64 x 64 tile count
 static inline int conv_jobs_pack(const void* jobs, int n, ConvJobs& J) {
   J.tile0[0] = 0;
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < FBN_CONV_MAX; ++i) {
     J.j[i] = ((const ConvJob*)jobs)[i < n ? i : 0];
     J.tile0[i + 1] = J.tile0[i] + (i < n ? fbn_cdiv(J.j[i].rows, 64) * fbn_cdiv(J.j[i].cols, 64) : 0);
   }

@@ -1199,17 +1199,17 @@ extern "C" int fbn_sum(const float* x, int n, float* out, float scale, void* str
 }
 
 // ------------------------------------------------------------------ bf16 weight copies
-// out[i][j] = bf16( T ? src[j*ld + rm(i)] : src[i*ld + rm(j)] ),  i < rows, j < cols,
-// rm(x) = x + (x < seg ? off0 : off1).  Up to 8 jobs per launch (one per blockIdx.y): the
-// compacted / transposed bf16 weight images the bf16 GEMMs read (made once per step).
+// out[i*dld + j] = bf16( T ? src[j*ld + rm(i)] : src[i*ld + rm(j)] ) (or its rounding residual, part 1),
+// i < rows, j < cols, rm(x) = x + (x < seg ? off0 : off1).  Up to 16 jobs per launch: the compacted /
+// transposed bf16 weight images the bf16 GEMMs read (made once per step), the split-bf16 operand images.
 __global__ void __launch_bounds__(256) convert_bf16_kernel(ConvJobs jobs, int njobs) {
   convert_tile(jobs, njobs, blockIdx.x);
 }
 
-// jobs: host array of n (<= 8) ConvJob records {src, dst, rows, cols, ld, trans, seg, off0, off1}
+// jobs: host array of n (<= 16) ConvJob records {src, dst, rows, cols, ld, trans, seg, off0, off1, part, dld}
 extern "C" int fbn_convert_bf16(const void* jobs, int n, void* stream) {
   if (n <= 0) return FBN_OK;
-  if (n > 8) { fbn_set_error("convert_bf16: at most 8 jobs"); return FBN_ERR_ARG; }
+  if (n > FBN_CONV_MAX) { fbn_set_error("convert_bf16: at most 16 jobs"); return FBN_ERR_ARG; }
   ConvJobs J;
   const int tiles = conv_jobs_pack(jobs, n, J);
   if (tiles <= 0) return FBN_OK;

@@ -1493,9 +1493,9 @@ __global__ void __launch_bounds__(256) adam_prefetch2_kernel(float* __restrict__
 // almost from the start).  Per row: the same operations in the same order (replay_group) --
 // bit-identical to prefetch2 and to eager.
 #define FBN_PFB_BINS 32
-// workspace: bin counts [FBN_PFB_BINS] i32 (256 B) | records [n] {row, key, pend, steps} | bin lists [BINS][n] i32
+// workspace: bin counts [FBN_PFB_BINS] i32 (256 B) | bin lists [BINS][n] of records {row, key, pend, steps}
 static inline size_t pfb_ws_bytes(long long n) {
-  return 256 + (size_t)n * sizeof(int4) + (size_t)FBN_PFB_BINS * (size_t)n * sizeof(int);
+  return 256 + (size_t)FBN_PFB_BINS * (size_t)n * sizeof(int4);
 }
 __device__ __forceinline__ int pfb_bin(int steps) {
   const int b = (steps - 1) >> 2;
@@ -1504,12 +1504,12 @@ __device__ __forceinline__ int pfb_bin(int steps) {
 
 __global__ void __launch_bounds__(256) adam_pfbin_kernel(ClaimSrc cs, int n, int* __restrict__ last,
                                                          const int* __restrict__ step, PendSrc ps,
-                                                         int* __restrict__ counts, int4* __restrict__ rec,
-                                                         int* __restrict__ list) {
+                                                         int* __restrict__ counts, int4* __restrict__ list) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int T = *step + 1;
   const int lane = threadIdx.x & 63;
   int bin = -1;
+  int4 rec = make_int4(0, 0, -1, 0);
   if (i < n) {
     const long long b = i / (cs.L + 1), tt = i - b * (cs.L + 1);
     const long long id = tt == 0 ? cs.item[b] : cs.seq[b * cs.L + (tt - 1)];
@@ -1523,13 +1523,13 @@ __global__ void __launch_bounds__(256) adam_pfbin_kernel(ClaimSrc cs, int n, int
           last[(size_t)(id) * FBN_RS_I] = T;
           if (pe >= 0) ps.pend[(size_t)(id) * FBN_RS_I] = -1;
           const int steps = T - k0;          // the deferred step (if any) + the zero-gradient steps
-          rec[i] = make_int4((int)id, k0 + (pe >= 0 ? 1 : 0), pe, steps);
+          rec = make_int4((int)id, k0 + (pe >= 0 ? 1 : 0), pe, steps);
           bin = pfb_bin(steps);
         }
       }
     }
   }
-  // append the entry index to its bin: one returning atomic per (wave, bin)
+  // append the record to its bin: one returning atomic per (wave, bin)
   unsigned long long todo = __ballot(bin >= 0);
   while (todo) {
     const int leader = __ffsll((long long)todo) - 1;
@@ -1538,27 +1538,30 @@ __global__ void __launch_bounds__(256) adam_pfbin_kernel(ClaimSrc cs, int n, int
     int base = 0;
     if (lane == leader) base = atomicAdd(counts + bl, __popcll(mask));
     base = __shfl(base, leader, 64);
-    if (bin == bl) list[(size_t)bl * n + base + __popcll(mask & ((1ull << lane) - 1ull))] = (int)i;
+    if (bin == bl) list[(size_t)bl * n + base + __popcll(mask & ((1ull << lane) - 1ull))] = rec;
     todo &= ~mask;
   }
 }
 
+// The binned list, longest bins first, as G-row groups; wave w takes groups w, w + W, w + 2W, ...
+// (at most 64 / G of them: the grid is sized so), loading all its records in ONE round trip (lane
+// G*k + x holds slot x of its k-th group), then replays the groups with the next group's rows in
+// flight.  Empty slots past the list: row 0, key T + 1 (sorted last), no steps, not stored.
 template <int D, bool DW, int G = 4>
 __global__ void __launch_bounds__(256) adam_pfreplay_kernel(float* __restrict__ p, float* __restrict__ m,
                                                             float* __restrict__ v, const AdamConsts* __restrict__ table,
                                                             const int* __restrict__ step, float wd, float b2,
                                                             float omb2, float eps, PendSrc ps,
                                                             const int* __restrict__ counts,
-                                                            const int4* __restrict__ rec,
-                                                            const int* __restrict__ list, int n) {
+                                                            const int4* __restrict__ list, int n) {
   const int T = *step + 1;
   const int lane = threadIdx.x & 63;
   const int wave = (int)(((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   const int nwaves = (int)(((long long)gridDim.x * blockDim.x) >> 6);
-  // lanes 0..31 hold the bins longest first: lane l <-> bin BINS-1-l, its count and list start
+  // lanes 0..31 hold the bins longest first: lane l <-> bin BINS-1-l, its count; inclusive prefix
   const int lb = FBN_PFB_BINS - 1 - (lane & (FBN_PFB_BINS - 1));
   const int c = lane < FBN_PFB_BINS ? counts[lb] : 0;
-  int incl = c;   // inclusive prefix over lanes (bins longest first)
+  int incl = c;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const int y = __shfl_up(incl, o, 64);
@@ -1566,28 +1569,40 @@ __global__ void __launch_bounds__(256) adam_pfreplay_kernel(float* __restrict__ 
   }
   const int total = __shfl(incl, 63, 64);
   const int ngroups = (total + G - 1) / G;
-  // position q of the concatenated list -> (row, first zero-gradient step, deferred vector); past the
-  // end: row 0 with no steps (not stored)
-  auto get = [&](int q, int& rr, int& kk, int& pp) {   // q wave-uniform
-    if (q >= total) { rr = 0; kk = T + 1; pp = -1; return; }   // sorts after every row (a row's key <= T)
-    const int l = __popcll(__ballot(lane < FBN_PFB_BINS && incl <= q));   // lane whose bin holds q
-    const int start = __shfl(incl - c, l, 64);
-    const int e = list[(size_t)(FBN_PFB_BINS - 1 - l) * n + (q - start)];
-    const int4 x = rec[e];
-    rr = x.x;
-    kk = x.y;
-    pp = x.z;
-  };
+  if (wave >= ngroups) return;
+  // this lane's record: slot x = lane % G of group wave + (lane / G) * nwaves
+  const int q = (wave + (lane / G) * nwaves) * G + lane % G;
+  int4 rec = make_int4(0, T + 1, -1, 0);
+  {
+    int l = 0;   // the bin (in longest-first order) holding position q: first lane with incl > q
+#pragma unroll
+    for (int bit = 16; bit > 0; bit >>= 1) {
+      const int cand = l + bit;
+      const int e = __shfl(incl, (cand - 1) & 63, 64);   // end of bins 0 .. cand-1
+      if (cand <= FBN_PFB_BINS && e <= q) l = cand;
+    }
+    if (q < total) {
+      const int start = __shfl(incl - c, l & 63, 64);
+      rec = list[(size_t)(FBN_PFB_BINS - 1 - l) * n + (q - start)];
+    }
+  }
   struct Grp {
     WideRow<D> w[G];
     int r[G], k[G], p[G];
     int cnt;
   };
-  auto fill = [&](Grp& g, int grp) {
-    g.cnt = min(G, total - grp * G);
+  auto fill = [&](Grp& g, int k) {   // this wave's k-th group (k wave-uniform)
+    g.cnt = 0;
 #pragma unroll
-    for (int x = 0; x < G; ++x) get(grp * G + x, g.r[x], g.k[x], g.p[x]);
-    // ascending replay start (the engine's end-aligned staircase); empty slots (key T) last
+    for (int x = 0; x < G; ++x) {
+      const int src = (k * G + x) & 63;
+      g.r[x] = __builtin_amdgcn_readlane(rec.x, src);
+      g.k[x] = __builtin_amdgcn_readlane(rec.y, src);
+      g.p[x] = __builtin_amdgcn_readlane(rec.z, src);
+      if (k * G + x >= 64) { g.r[x] = 0; g.k[x] = T + 1; g.p[x] = -1; }
+      g.cnt += g.k[x] <= T ? 1 : 0;
+    }
+    // ascending replay start (the engine's end-aligned staircase); empty slots (key T + 1) last
 #pragma unroll
     for (int a = 0; a < G; ++a)
 #pragma unroll
@@ -1600,13 +1615,11 @@ __global__ void __launch_bounds__(256) adam_pfreplay_kernel(float* __restrict__ 
 #pragma unroll
     for (int x = 0; x < G; ++x) wide_load<D>(g.w[x], p, m, v, g.r[x], g.p[x] >= 0 ? g.k[x] - 1 : g.k[x], g.p[x], ps, lane);
   };
-  int grp = wave;
-  if (grp >= ngroups) return;
+  const int mine = min(64 / G, (ngroups - wave + nwaves - 1) / nwaves);   // groups of this wave
   Grp a, bq;
-  fill(a, grp);
-  for (; grp < ngroups; grp += nwaves) {
-    const int nxt = grp + nwaves;
-    fill(bq, nxt < ngroups ? nxt : ngroups);   // past the end: empty slots (row 0), discarded
+  fill(a, 0);
+  for (int k = 0; k < mine; ++k) {
+    fill(bq, k + 1 < mine ? k + 1 : 64 / G);   // past this wave's last group: empty slots, discarded
     replay_group<D, DW, G>(a.w, a.r, a.k, a.p, 0, a.cnt, T, p, m, v, table, wd, b2, omb2, eps, lane);
     a = bq;
   }
@@ -2424,23 +2437,24 @@ extern "C" int fbn_adam_prefetch_binned(const int64_t* item, const int64_t* seq,
   const ClaimSrc cs{item, L > 0 ? seq : nullptr, L, V, const_cast<int*>(map), nullptr, nullptr, nullptr, preclaim};
   hipStream_t st = (hipStream_t)stream;
   int* counts = static_cast<int*>(ws);
-  int4* rec = reinterpret_cast<int4*>(static_cast<char*>(ws) + 256);
-  int* list = reinterpret_cast<int*>(rec + n);
+  int4* list = reinterpret_cast<int4*>(static_cast<char*>(ws) + 256);
   if (hipMemsetAsync(counts, 0, FBN_PFB_BINS * sizeof(int), st) != hipSuccess) {
     fbn_set_error("fbn_adam_prefetch_binned: hipMemsetAsync failed");
     return FBN_ERR_LAUNCH;
   }
   const dim3 g2((unsigned)((n + 255) / 256));
   hipLaunchKernelGGL(adam_pretag_kernel, g2, dim3(256), 0, st, cs, (int)n, step);
-  hipLaunchKernelGGL(adam_pfbin_kernel, g2, dim3(256), 0, st, cs, (int)n, last, step, ps, counts, rec, list);
-  // FBN_PFB_WAVES: waves of the replay (default 1024; A/B knob, read per call)
+  hipLaunchKernelGGL(adam_pfbin_kernel, g2, dim3(256), 0, st, cs, (int)n, last, step, ps, counts, list);
+  // waves of the replay: every wave holds at most 16 four-row groups (one record per lane), so at
+  // least ceil(n / 64) waves; FBN_PFB_WAVES (A/B knob, read per call) raises the count -- default
+  // 4096 (16 per CU: the groups' row loads overlap the replay of other waves)
   const char* we = getenv("FBN_PFB_WAVES");
-  long long waves = we ? std::max(4LL, atoll(we)) : 1024;
-  waves = std::min(waves, std::max(4LL, (n + 3) / 4));
+  long long waves = we ? atoll(we) : 4096;
+  waves = std::max(waves, (n + 63) / 64);
   const dim3 g3((unsigned)((waves + 3) / 4));
 #define FBN_PFB_LAUNCH(D_, DW_)                                                                               \
   hipLaunchKernelGGL((adam_pfreplay_kernel<D_, DW_>), g3, dim3(256), 0, st, p, m, v,                          \
-                     (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, counts, rec, list, (int)n)
+                     (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, counts, list, (int)n)
   if (D == 128) {
     if (decoupled) FBN_PFB_LAUNCH(128, true); else FBN_PFB_LAUNCH(128, false);
   } else {
@@ -2629,7 +2643,7 @@ extern "C" int fbn_adam_claim_catchup_conv(const int64_t* item, const int64_t* s
                                            const float* ring, const float* coef_hist, long long ring_stride,
                                            int ring_n, int decoupled, const void* conv_jobs, int n_conv,
                                            void* stream) {
-  if (n_conv < 0 || n_conv > 8 || (n_conv > 0 && !conv_jobs)) {
+  if (n_conv < 0 || n_conv > FBN_CONV_MAX || (n_conv > 0 && !conv_jobs)) {
     fbn_set_error("fbn_adam_claim_catchup_conv: 0 <= n_conv <= 8 conversion jobs");
     return FBN_ERR_ARG;
   }

@@ -87,7 +87,8 @@ def gemm_split(A, B, C, M, N, K, lda, ldb, ldc, transA, transB, bias=None, rC=NO
 class _ConvJob(ctypes.Structure):
     _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("rows", ctypes.c_int), ("cols", ctypes.c_int),
                 ("ld", ctypes.c_int), ("trans", ctypes.c_int), ("seg", ctypes.c_int), ("off0", ctypes.c_int),
-                ("off1", ctypes.c_int)]
+                ("off1", ctypes.c_int), ("part", ctypes.c_int), ("dld", ctypes.c_int)]
+CONV_MAX = 16   # include/fibinet.h: jobs per fbn_convert_bf16 launch
 
 
 def bf16_weights(p: Dict[str, torch.Tensor], d: int, a: Dict[str, torch.Tensor], stream,
@@ -115,7 +116,7 @@ def bf16_weight_jobs(p: Dict[str, torch.Tensor], d: int, a: Dict[str, torch.Tens
         spec += [("W", p["bilinear.W"], d, d, d, 0, NO_REMAP), ("WT", p["bilinear.W"], d, d, d, 1, NO_REMAP)]
     if x is not None:
         spec.append(("x", x, x.shape[0], x.shape[1], x.shape[1], 0, NO_REMAP))
-    jobs = (_ConvJob * 8)()
+    jobs = (_ConvJob * CONV_MAX)()
     a["_conv_jobs"] = jobs
     _lib.keep(jobs)               # its address is passed as an integer (step programs keep it alive)
     out = {}

@@ -224,9 +224,11 @@ int fbn_bn_bwd_fused(const float* G, const float* gvec, const float* w, const fl
                      float scale, const float* Xpre, const float* mean, const float* invstd, const float* gamma, int B,
                      int C, double ntot, float* dXpre, short* dXpre16, float* dgamma, float* dbeta, float* dw,
                      float* colpart, const double* part_pre, void* ws, void* stream);
-/* bf16 weight images: jobs = host array of n <= 8 records
- * {const float* src; short* dst; int rows, cols, ld, trans, seg, off0, off1;}
- * out[i][j] = bf16(trans ? src[j*ld + rm(i)] : src[i*ld + rm(j)]), rm(x) = x + (x < seg ? off0 : off1). */
+/* bf16 images: jobs = host array of n <= 16 records
+ * {const float* src; short* dst; int rows, cols, ld, trans, seg, off0, off1, part, dld;}
+ * x = trans ? src[j*ld + rm(i)] : src[i*ld + rm(j)], rm(x) = x + (x < seg ? off0 : off1);
+ * dst[i*dld + j] = part ? bf16(x - float(bf16(x))) : bf16(x)  (dld = 0: cols).  part 1 is the rounding
+ * residual: hi + lo images carry 16 significant bits (the split-bf16 backward GEMMs of bf16_fwd mode). */
 int fbn_convert_bf16(const void* jobs, int n, void* stream);
 size_t fbn_colsum_workspace_size(int B, int C);
 int fbn_colsum(const float* X, int B, int C, int ldx, float* out, float beta, void* ws, void* stream);
@@ -338,7 +340,7 @@ int fbn_adam_claim_catchup(const int64_t* item, const int64_t* seq, int B, int L
                            const void* consts_table, const int* step, float wd, float beta2, float eps, int* pend,
                            const float* ring, const float* coef_hist, long long ring_stride, int ring_n, int decoupled,
                            void* stream);
-/* fbn_adam_claim_catchup with the step's bf16 image conversion (fbn_convert_bf16's n_conv <= 8
+/* fbn_adam_claim_catchup with the step's bf16 image conversion (fbn_convert_bf16's n_conv <= 16
  * job records) in the same launch (claim blocks, then conversion blocks) -- the two are
  * independent: the images are of the weights the previous step's tail wrote and of this batch's
  * item_emb_d128 (src/model_fibinet.py:162). */

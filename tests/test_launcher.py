@@ -143,7 +143,7 @@ RUN_AUC_BAR = 1e-4
 
 
 @pytest.mark.gpu
-def test_launcher_auc_parity_vs_reference_loop(hip_device, tmp_path):
+def test_launcher_auc_parity_vs_reference_loop(hip_device, tmp_path, monkeypatch):
     """AUC parity of a TRAINING RUN (the metric's "AUC parity", src/train_fibinet.py:103-152 +
     src/utils.py:18-27): the launcher (python -m ctr_recommendation_amd.train: device loader, native
     trainer, valid AUC per epoch) for 2 epochs x 100 steps (51 200 train rows, batch 512, d 16,
@@ -165,12 +165,25 @@ def test_launcher_auc_parity_vs_reference_loop(hip_device, tmp_path):
     with open(cfg_path, "w") as f:
         f.write(PARITY_CONFIG.format(train=p["train_data"], valid=p["valid_data"], info=p["item_info"], bs=bs))
     _, dcfg, mcfg = load_config(cfg_path)
+    # the launcher's epoch permutations, as its train loader draws them (the valid loader's are aranges)
+    drawn = []
+    orig_perm = DeviceLoader._perm
+
+    def rec_perm(self):
+        p = orig_perm(self)
+        if self.shuffle:
+            drawn.append(p.cpu().numpy())
+        return p
+    monkeypatch.setattr(DeviceLoader, "_perm", rec_perm)
     out = run(cfg_path, epochs=epochs, checkpoint=str(tmp_path / "ck" / "best.pth"), log=lambda *a, **k: None)
     hist = out["history"]
-    # the launcher's epoch permutations: its train loader is DeviceLoader(shuffle=True, seed=2025)
-    perm_src = DeviceLoader(ColumnarDataset.from_parquet(dcfg["train_data"], hip_device), None, bs, shuffle=True,
-                            seed=2025)
-    perms = [perm_src._perm().cpu().numpy() for _ in range(epochs)]
+    perms = drawn
+    assert len(perms) == epochs
+    # the launcher's trained model on the valid rows (after the last epoch)
+    from ctr_recommendation_amd.loader import ItemInfoTable
+    vl = DeviceLoader(ColumnarDataset.from_parquet(dcfg["valid_data"], hip_device),
+                      ItemInfoTable.from_parquet(dcfg["item_info"], hip_device), bs, shuffle=False)
+    p_hip = np.concatenate([out["trainer"].predict(b).cpu().numpy() for b, _ in vl])
     darray, ci = load_data(dcfg["train_data"])
     coll = BatchCollatorRef(20, ci, dcfg["item_info"])
     varray, vci = load_data(dcfg["valid_data"])
@@ -185,13 +198,15 @@ def test_launcher_auc_parity_vs_reference_loop(hip_device, tmp_path):
             ref = ref.double()
         cast = (lambda t: t.double() if t.is_floating_point() else t) if f64 else (lambda t: t)
         otr = OracleTrainer(ref, lr=1e-3, weight_decay=1e-5, total_steps=epochs * steps_per_epoch)
-        aucs = []
+        aucs, losses = [], []
         for e in range(epochs):
+            tot = 0.0
             for lo in range(0, n_train, bs):
                 rows = perms[e][lo:lo + bs]
                 b, y = coll([darray[i, :] for i in rows])
                 b = {k: cast(v.long() if k != "item_emb_d128" else v) for k, v in b.items()}
-                otr.step(b, cast(y))
+                tot += otr.step(b, cast(y))[0]
+            losses.append(tot / steps_per_epoch)
             ref.eval()
             ys, ps = [], []
             with torch.no_grad():
@@ -202,16 +217,19 @@ def test_launcher_auc_parity_vs_reference_loop(hip_device, tmp_path):
                     ys.append(y.numpy())
             aucs.append(compute_auc(np.concatenate(ys), np.concatenate(ps)))
             ref.train()
-        return aucs
+        return aucs, losses, np.concatenate(ps)
 
-    a32, a64 = reference_loop(False), reference_loop(True)
+    (a32, l32, p32), (a64, l64, _) = reference_loop(False), reference_loop(True)
     rec = {"run": f"{epochs} epochs x {steps_per_epoch} steps, batch {bs}, d 16, {n_train} train / {n_valid} valid "
                   f"rows (synthetic MicroLens-shaped parquet), dropout off", "bar": RUN_AUC_BAR, "epochs": []}
     for e in range(epochs):
         a_hip = hist[e][2]
         rec["epochs"].append({"epoch": e + 1, "launcher_auc": a_hip, "oracle_auc": a32[e], "oracle_f64_auc": a64[e],
                               "dAUC": abs(a_hip - a32[e]), "oracle_fp32_vs_f64_dAUC": abs(a32[e] - a64[e]),
-                              "launcher_vs_f64_dAUC": abs(a_hip - a64[e]), "train_loss": hist[e][1]})
+                              "launcher_vs_f64_dAUC": abs(a_hip - a64[e]), "train_loss": hist[e][1],
+                              "oracle_train_loss": l32[e], "oracle_f64_train_loss": l64[e]})
+    rec["final_valid_max_abs_dp"] = float(np.abs(p_hip - p32).max())
+    rec["final_valid_mean_abs_dp"] = float(np.abs(p_hip - p32).mean())
     import os
     outd = os.environ.get("FBN_PARITY_OUT", os.path.join("gpurun_out", "parity"))
     os.makedirs(outd, exist_ok=True)

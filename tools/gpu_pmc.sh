@@ -7,7 +7,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/pmc_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-BENCH="python $R/bench.py --steps 3 --warmup 1 --prime ${PMC_PRIME:-64} --probe-steps 0 --no-graph --no-cpu-baseline --no-fp32"
+BENCH="python $R/bench.py --steps 3 --warmup 1 --prime ${PMC_PRIME:-64} --probe-steps 0 --mode eager --no-cpu-baseline --no-cpu-plan --no-inference --no-fp32"
 i=0
 PASSES=${PMC_PASSES:-"SQ_WAVES,SQ_INSTS_VALU,SQ_ACTIVE_INST_VALU,GRBM_GUI_ACTIVE;SQ_VALU_MFMA_BUSY_CYCLES,SQ_INSTS_VALU_MFMA_MOPS_BF16,SQ_WAVE_CYCLES,GRBM_GUI_ACTIVE;FETCH_SIZE;WRITE_SIZE;SQ_WAIT_ANY,SQ_BUSY_CYCLES,SQ_LDS_BANK_CONFLICT,SQ_ACTIVE_INST_LDS"}
 IFS=';' read -ra PS <<< "$PASSES"
