@@ -85,8 +85,8 @@ _DENSE_SUMSQ_FOLD = os.environ.get("FBN_DENSE_SUMSQ_FOLD", "1") == "1"
 # overlap it buys at N > 1 could not be measured on a one-GPU box
 _EARLY_GRAD_XCHG = os.environ.get("FBN_EARLY_GRAD_XCHG")
 # single GPU, d = 128 / 256 with pre-claims: the next-batch prefetch in its binned form (balanced
-# waves, fbn_adam_prefetch_binned); FBN_PF_BINNED=0 keeps adam_prefetch2 (a wave per 64 entries), A/B
-_PF_BINNED = os.environ.get("FBN_PF_BINNED", "1") != "0"
+# waves, fbn_adam_prefetch_binned) with FBN_PF_BINNED=1; default adam_prefetch2 (a wave per 64 entries)
+_PF_BINNED = os.environ.get("FBN_PF_BINNED", "0") == "1"
 from .schedule import OneCycle, adam_table
 
 TABLE = "item_emb.weight"
