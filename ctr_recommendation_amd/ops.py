@@ -221,12 +221,14 @@ class DeferredSums:
         call("fbn_colsum_partial", ptr(X), B, C, ldx, ptr(part), stream)
         self.add(part, nch, C, out)
 
-    def flush(self, stream, probe: Optional[Dict[str, list]] = None):
+    def launch_group(self, stream, probe: Optional[Dict[str, list]] = None, tstream=None) -> None:
+        """The slab GEMMs recorded so far, in ONE fbn_gemm_slabs_group launch on `stream` (tstream: the
+        torch stream of that handle, for the bench's events); their slabs are summed at flush()."""
         group = self.group
         ev = None
         if group and probe is not None:             # bench: HIP events around the grouped launch
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            ev[0].record()
+            ev[0].record(tstream)
             probe.setdefault("wgrad_group", []).append(ev)
         while group:
             gc, group = group[:6], group[6:]
@@ -234,8 +236,16 @@ class DeferredSums:
             _lib.keep(garr)
             call("fbn_gemm_slabs_group", ctypes.addressof(garr), len(gc), stream)
         if ev is not None:
-            ev[1].record()
+            ev[1].record(tstream)
+            self.timed_group = True
         self.group = []
+
+    timed_group = False
+
+    def flush(self, stream, probe: Optional[Dict[str, list]] = None):
+        # the bench's "wgrad_group" events time the launch of the step's weight gradients: the early one
+        # when the trainer launched it beside the fields backward, else this one
+        self.launch_group(stream, None if self.timed_group else probe)
         jobs, slabs = self.jobs, self.slabs
         while jobs or slabs:
             jc, sc = jobs[:16], slabs[:8]
@@ -724,6 +734,8 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
                  beta=1.0, bf16=cfg.bf16, stream=st)
             gemm(a["Vc"][:, f - 1], dU[:, f - 1], g[f"bilinear.W_list.{f}"], d, d, B, 5 * d, 5 * d, d, True, False,
                  bf16=cfg.bf16, stream=st)
+    if hooks and "after_bilinear_bwd" in hooks:   # trainer: the weight gradients so far launched early
+        hooks["after_bilinear_bwd"](sums)
     # fields backward: SENET, LN, cate + item-table scatter
     R = cfg.R
     ncate = p["cate_emb.weight"].shape[0]
@@ -772,5 +784,7 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
                               False, stream=s))
     for job in extra_sums:              # e.g. the trainer's mean loss
         sums.add(*job)
+    if hooks and "before_flush" in hooks:         # trainer: join the early weight-gradient launch
+        hooks["before_flush"]()
     sums.flush(st, probe)
     wg.join()

@@ -87,6 +87,11 @@ _EARLY_GRAD_XCHG = os.environ.get("FBN_EARLY_GRAD_XCHG")
 # single GPU, d = 128 / 256 with pre-claims: the next-batch prefetch in its binned form (balanced
 # waves, fbn_adam_prefetch_binned) with FBN_PF_BINNED=1; default adam_prefetch2 (a wave per 64 entries)
 _PF_BINNED = os.environ.get("FBN_PF_BINNED", "0") == "1"
+# single GPU, eager steps with the side stream (A/B knob, FBN_WGRAD_EARLY=1): the grouped weight-
+# gradient GEMMs of the MLP and the bilinear W (dWa, dWb, dW) launched on the side stream right after
+# the bilinear backward, beside the fields backward (HBM-bound) on the main stream; dW_p stays in the
+# flush's launch on main, which waits for the side stream before the slab sums
+_WGRAD_EARLY = os.environ.get("FBN_WGRAD_EARLY", "0") == "1"
 from .schedule import OneCycle, adam_table
 
 TABLE = "item_emb.weight"
@@ -667,6 +672,12 @@ class FiBiNETTrainer:
                     call("fbn_sparse_fixup_dup", ptr(self.dup), B * (L + 1), ptr(self.gvec), ptr(self.extra),
                          ptr(self.slot_row), L + 1, d, self.side.cuda_stream)
                 bhooks = {"after_fields_bwd": fork_fixup}
+                if _WGRAD_EARLY and cfg.bf16:
+                    def early_wgrad(sums):
+                        _lib.wait_stream(self.side, main)
+                        sums.launch_group(self.side.cuda_stream, probe, tstream=self.side)
+                    bhooks["after_bilinear_bwd"] = early_wgrad
+                    bhooks["before_flush"] = lambda: _lib.wait_stream(main, self.side)
             ops.backward(self.p, batch, a, a["gout"], self.g, cfg, gvec=self.gvec if self.xchg is None else None,
                          gnorm=self.gnorm if self.xchg is None else None,
                          pos=pos, sendbuf=sendbuf, coll=self.bn_coll, ntot=self._bn_n(ntot, B),

@@ -94,3 +94,28 @@ def test_program_refuses_unsupported_paths(hip_device):
     b, y = make_batch(1, 64, 3000)
     with pytest.raises(ValueError, match="lazy table Adam"):
         tr.record_program({k: v.to(hip_device) for k, v in b.items()}, y.to(hip_device))
+
+
+def test_early_wgrad_launch_bit_identical(hip_device, monkeypatch):
+    """FBN_WGRAD_EARLY (A/B knob): the grouped weight-gradient GEMMs launched on the side stream beside
+    the fields backward give the same slabs, hence bit-identical steps."""
+    from ctr_recommendation_amd import trainer as trmod
+    V, B, nb, steps, d = 40000, 512, 3, 6, 128
+    cfg = {"embedding_dim": d, "vocab_size": V, "compute_dtype": "bf16"}
+    torch.manual_seed(0)
+    init = oracle_build(None, dict(cfg, honour_config=False)).state_dict()
+    g = torch.Generator().manual_seed(7)
+    pool = torch.randperm(V - 1, generator=g)[:20000] + 1
+    batches = []
+    for j in range(nb):
+        b, y = make_batch(70 + j, B, V)
+        batches.append(({k: v.to(hip_device) for k, v in _unique_ids(b, V, g, pool).items()}, y.to(hip_device)))
+    res = []
+    for early in (False, True):
+        monkeypatch.setattr(trmod, "_WGRAD_EARLY", early)
+        tr = _trainer(cfg, init, B, hip_device)
+        losses = [tr.step(*batches[i % nb], next_batch=batches[(i + 1) % nb][0]).item() for i in range(steps)]
+        tr.flush()
+        res.append((losses, tr.E.clone(), tr.flat_p.clone()))
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
