@@ -1197,13 +1197,25 @@ __global__ void __launch_bounds__(256) adam_prefetch_kernel(float* __restrict__ 
 // Same operations in the same order per row: bit-identical to the one-pass kernel and to eager.
 #define FBN_PF_WIN 256
 
+// entry i's row, or -1: the batch's ids (item, then history slots; 0 = padding), or in owner mode
+// (cs.lids, N > 1) the local rows the next step's requests name (-1 = none; rank 0's row 0 is the
+// padding id)
+__device__ __forceinline__ long long entry_row(const ClaimSrc& cs, long long i) {
+  if (cs.lids) {
+    const long long id = cs.lids[i];
+    return (id >= 0 && id < cs.V && !(cs.skip0 && id == 0)) ? id : -1;
+  }
+  const long long b = i / (cs.L + 1), tt = i - b * (cs.L + 1);
+  const long long id = tt == 0 ? cs.item[b] : cs.seq[b * cs.L + (tt - 1)];
+  return (id > 0 && id < cs.V) ? id : -1;
+}
+
 __global__ void __launch_bounds__(256) adam_pretag_kernel(ClaimSrc cs, int n, const int* __restrict__ step) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const unsigned long long T = (unsigned long long)(*step + 1);
-  const long long b = i / (cs.L + 1), tt = i - b * (cs.L + 1);
-  const long long id = tt == 0 ? cs.item[b] : cs.seq[b * cs.L + (tt - 1)];
-  if (id > 0 && id < cs.V) atomicMax(cs.pre + (size_t)id * FBN_RS_Q, (T << 32) | (0xFFFFFFFFull - (unsigned long long)i));
+  const long long id = entry_row(cs, i);
+  if (id >= 0) atomicMax(cs.pre + (size_t)id * FBN_RS_Q, (T << 32) | (0xFFFFFFFFull - (unsigned long long)i));
 }
 
 // adam_tab1 with the step's constants as (w1, nss, rbc2s, dmul): the same operations, same order
@@ -1449,9 +1461,8 @@ __device__ __forceinline__ void adam_prefetch2_body(float* __restrict__ p, float
   const long long i = lane < epw ? ch * epw + lane : n;
   int r = 0, key = 0x7fffffff, pe = -1;
   if (i < n) {
-    const long long b = i / (cs.L + 1), tt = i - b * (cs.L + 1);
-    const long long id = tt == 0 ? cs.item[b] : cs.seq[b * cs.L + (tt - 1)];
-    if (id > 0 && id < cs.V) {
+    const long long id = entry_row(cs, i);
+    if (id >= 0) {
       const int4 rs = row_state(last, id);   // tag, last, pend: one 16-B load
       const unsigned long long pv = ((unsigned long long)(unsigned)rs.y << 32) | (unsigned)rs.x;
       if ((int)(pv >> 32) == T && (0xFFFFFFFFu - (unsigned)pv) == (unsigned)i && cs.map[id] == -1) {
@@ -1480,149 +1491,6 @@ __global__ void __launch_bounds__(256) adam_prefetch2_kernel(float* __restrict__
                                                              float omb2, float eps, PendSrc ps, int epw) {
   adam_prefetch2_body<D, DW, G, ABL>(p, m, v, cs, n, last, table, step, wd, b2, omb2, eps, ps, epw, blockIdx.x,
                                      gridDim.x);
-}
-
-// ---- The binned prefetch (fbn_adam_prefetch_binned, D >= 128): balanced waves.
-// adam_prefetch2 gives every wave the rows of its own 64 entries: ~31 rows whose replay lengths are
-// ~Exp(14) steps, so the slowest wave of a launch runs twice the mean (a simulation of the engine on
-// that distribution agrees).  Here the ownership pass (the same test as prefetch2's,
-// which also marks last / pend) files each owned row in a bin by its replay length -- one atomic per
-// (wave, bin) -- and the replay kernel walks the bins longest first as ONE list of 4-row groups dealt
-// round-robin to the waves: every wave gets the same mix of lengths, and a group's four rows have
-// replay lengths within 4 steps of each other (the end-aligned engine then replays them side by side
-// almost from the start).  Per row: the same operations in the same order (replay_group) --
-// bit-identical to prefetch2 and to eager.
-#define FBN_PFB_BINS 32
-// workspace: bin counts [FBN_PFB_BINS] i32 (256 B) | bin lists [BINS][n] of records {row, key, pend, steps}
-static inline size_t pfb_ws_bytes(long long n) {
-  return 256 + (size_t)FBN_PFB_BINS * (size_t)n * sizeof(int4);
-}
-__device__ __forceinline__ int pfb_bin(int steps) {
-  const int b = (steps - 1) >> 2;
-  return b < FBN_PFB_BINS - 1 ? b : FBN_PFB_BINS - 1;
-}
-
-__global__ void __launch_bounds__(256) adam_pfbin_kernel(ClaimSrc cs, int n, int* __restrict__ last,
-                                                         const int* __restrict__ step, PendSrc ps,
-                                                         int* __restrict__ counts, int4* __restrict__ list) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int T = *step + 1;
-  const int lane = threadIdx.x & 63;
-  int bin = -1;
-  int4 rec = make_int4(0, 0, -1, 0);
-  if (i < n) {
-    const long long b = i / (cs.L + 1), tt = i - b * (cs.L + 1);
-    const long long id = tt == 0 ? cs.item[b] : cs.seq[b * cs.L + (tt - 1)];
-    if (id > 0 && id < cs.V) {
-      const int4 rs = row_state(last, id);   // tag, last, pend: one 16-B load
-      const unsigned long long pv = ((unsigned long long)(unsigned)rs.y << 32) | (unsigned)rs.x;
-      if ((int)(pv >> 32) == T && (0xFFFFFFFFu - (unsigned)pv) == (unsigned)i && cs.map[id] == -1) {
-        const int k0 = rs.z;
-        if (k0 < T) {   // this entry owns the row: its replay through step T - 1
-          const int pe = ps.pend ? rs.w : -1;
-          last[(size_t)(id) * FBN_RS_I] = T;
-          if (pe >= 0) ps.pend[(size_t)(id) * FBN_RS_I] = -1;
-          const int steps = T - k0;          // the deferred step (if any) + the zero-gradient steps
-          rec = make_int4((int)id, k0 + (pe >= 0 ? 1 : 0), pe, steps);
-          bin = pfb_bin(steps);
-        }
-      }
-    }
-  }
-  // append the record to its bin: one returning atomic per (wave, bin)
-  unsigned long long todo = __ballot(bin >= 0);
-  while (todo) {
-    const int leader = __ffsll((long long)todo) - 1;
-    const int bl = __shfl(bin, leader, 64);
-    const unsigned long long mask = __ballot(bin == bl);
-    int base = 0;
-    if (lane == leader) base = atomicAdd(counts + bl, __popcll(mask));
-    base = __shfl(base, leader, 64);
-    if (bin == bl) list[(size_t)bl * n + base + __popcll(mask & ((1ull << lane) - 1ull))] = rec;
-    todo &= ~mask;
-  }
-}
-
-// The binned list, longest bins first, as G-row groups; wave w takes groups w, w + W, w + 2W, ...
-// (at most 64 / G of them: the grid is sized so), loading all its records in ONE round trip (lane
-// G*k + x holds slot x of its k-th group), then replays the groups with the next group's rows in
-// flight.  Empty slots past the list: row 0, key T + 1 (sorted last), no steps, not stored.
-template <int D, bool DW, int G = 4>
-__global__ void __launch_bounds__(256) adam_pfreplay_kernel(float* __restrict__ p, float* __restrict__ m,
-                                                            float* __restrict__ v, const AdamConsts* __restrict__ table,
-                                                            const int* __restrict__ step, float wd, float b2,
-                                                            float omb2, float eps, PendSrc ps,
-                                                            const int* __restrict__ counts,
-                                                            const int4* __restrict__ list, int n) {
-  const int T = *step + 1;
-  const int lane = threadIdx.x & 63;
-  const int wave = (int)(((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-  const int nwaves = (int)(((long long)gridDim.x * blockDim.x) >> 6);
-  // lanes 0..31 hold the bins longest first: lane l <-> bin BINS-1-l, its count; inclusive prefix
-  const int lb = FBN_PFB_BINS - 1 - (lane & (FBN_PFB_BINS - 1));
-  const int c = lane < FBN_PFB_BINS ? counts[lb] : 0;
-  int incl = c;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += y;
-  }
-  const int total = __shfl(incl, 63, 64);
-  const int ngroups = (total + G - 1) / G;
-  if (wave >= ngroups) return;
-  // this lane's record: slot x = lane % G of group wave + (lane / G) * nwaves
-  const int q = (wave + (lane / G) * nwaves) * G + lane % G;
-  int4 rec = make_int4(0, T + 1, -1, 0);
-  {
-    int l = 0;   // the bin (in longest-first order) holding position q: first lane with incl > q
-#pragma unroll
-    for (int bit = 16; bit > 0; bit >>= 1) {
-      const int cand = l + bit;
-      const int e = __shfl(incl, (cand - 1) & 63, 64);   // end of bins 0 .. cand-1
-      if (cand <= FBN_PFB_BINS && e <= q) l = cand;
-    }
-    if (q < total) {
-      const int start = __shfl(incl - c, l & 63, 64);
-      rec = list[(size_t)(FBN_PFB_BINS - 1 - l) * n + (q - start)];
-    }
-  }
-  struct Grp {
-    WideRow<D> w[G];
-    int r[G], k[G], p[G];
-    int cnt;
-  };
-  auto fill = [&](Grp& g, int k) {   // this wave's k-th group (k wave-uniform)
-    g.cnt = 0;
-#pragma unroll
-    for (int x = 0; x < G; ++x) {
-      const int src = (k * G + x) & 63;
-      g.r[x] = __builtin_amdgcn_readlane(rec.x, src);
-      g.k[x] = __builtin_amdgcn_readlane(rec.y, src);
-      g.p[x] = __builtin_amdgcn_readlane(rec.z, src);
-      if (k * G + x >= 64) { g.r[x] = 0; g.k[x] = T + 1; g.p[x] = -1; }
-      g.cnt += g.k[x] <= T ? 1 : 0;
-    }
-    // ascending replay start (the engine's end-aligned staircase); empty slots (key T + 1) last
-#pragma unroll
-    for (int a = 0; a < G; ++a)
-#pragma unroll
-      for (int b = 0; b + 1 < G - a; ++b)
-        if (g.k[b + 1] < g.k[b]) {
-          const int tk = g.k[b], tr = g.r[b], tp = g.p[b];
-          g.k[b] = g.k[b + 1]; g.r[b] = g.r[b + 1]; g.p[b] = g.p[b + 1];
-          g.k[b + 1] = tk; g.r[b + 1] = tr; g.p[b + 1] = tp;
-        }
-#pragma unroll
-    for (int x = 0; x < G; ++x) wide_load<D>(g.w[x], p, m, v, g.r[x], g.p[x] >= 0 ? g.k[x] - 1 : g.k[x], g.p[x], ps, lane);
-  };
-  const int mine = min(64 / G, (ngroups - wave + nwaves - 1) / nwaves);   // groups of this wave
-  Grp a, bq;
-  fill(a, 0);
-  for (int k = 0; k < mine; ++k) {
-    fill(bq, k + 1 < mine ? k + 1 : 64 / G);   // past this wave's last group: empty slots, discarded
-    replay_group<D, DW, G>(a.w, a.r, a.k, a.p, 0, a.cnt, T, p, m, v, table, wd, b2, omb2, eps, lane);
-    a = bq;
-  }
 }
 
 // Single GPU, D >= 128: the step's row claims + the claimed rows' catch-up (fbn_adam_claim_catchup)
@@ -2405,66 +2273,6 @@ extern "C" int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, i
   return FBN_OK;
 }
 
-// single GPU, D >= 128, with pre-claims: the binned form of fbn_adam_prefetch (balanced waves, see
-// adam_pfbin_kernel); ws >= fbn_adam_prefetch_binned_ws_size(B * (L + 1)) bytes
-extern "C" size_t fbn_adam_prefetch_binned_ws_size(long long n) { return n > 0 ? pfb_ws_bytes(n) : 0; }
-extern "C" int fbn_adam_prefetch_binned(const int64_t* item, const int64_t* seq, int B, int L, long long V,
-                                        const int* map, unsigned long long* preclaim, float* p, float* m, float* v,
-                                        int D, int* last, const void* consts_table, const int* step, float wd,
-                                        float beta2, float eps, int* pend, const float* ring, const float* coef_hist,
-                                        long long ring_stride, int ring_n, int decoupled, void* ws, size_t ws_bytes,
-                                        void* stream) {
-  const long long n = (long long)B * (L + 1);
-  if (n <= 0) return FBN_OK;
-  if (D != 128 && D != 256) {
-    fbn_set_error("fbn_adam_prefetch_binned: D = 128 / 256");
-    return FBN_ERR_ARG;
-  }
-  if (!item || (L > 0 && !seq) || !map || !last || !preclaim) {
-    fbn_set_error("fbn_adam_prefetch_binned: item, seq (L > 0), map, last and the pre-claims are required");
-    return FBN_ERR_ARG;
-  }
-  if (!ws || ws_bytes < pfb_ws_bytes(n) || n > 0x7fffffffLL / FBN_PFB_BINS) {
-    fbn_set_error("fbn_adam_prefetch_binned: workspace too small (fbn_adam_prefetch_binned_ws_size)");
-    return FBN_ERR_ARG;
-  }
-  if (pend && (!ring || !coef_hist)) {
-    fbn_set_error("fbn_adam_prefetch_binned: pend needs ring and coef_hist");
-    return FBN_ERR_ARG;
-  }
-  const float omb2 = (float)(1.0 - (double)beta2);
-  const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
-  const ClaimSrc cs{item, L > 0 ? seq : nullptr, L, V, const_cast<int*>(map), nullptr, nullptr, nullptr, preclaim};
-  hipStream_t st = (hipStream_t)stream;
-  int* counts = static_cast<int*>(ws);
-  int4* list = reinterpret_cast<int4*>(static_cast<char*>(ws) + 256);
-  if (hipMemsetAsync(counts, 0, FBN_PFB_BINS * sizeof(int), st) != hipSuccess) {
-    fbn_set_error("fbn_adam_prefetch_binned: hipMemsetAsync failed");
-    return FBN_ERR_LAUNCH;
-  }
-  const dim3 g2((unsigned)((n + 255) / 256));
-  hipLaunchKernelGGL(adam_pretag_kernel, g2, dim3(256), 0, st, cs, (int)n, step);
-  hipLaunchKernelGGL(adam_pfbin_kernel, g2, dim3(256), 0, st, cs, (int)n, last, step, ps, counts, list);
-  // waves of the replay: every wave holds at most 16 four-row groups (one record per lane), so at
-  // least ceil(n / 64) waves; FBN_PFB_WAVES (A/B knob, read per call) raises the count -- default
-  // 4096 (16 per CU: the groups' row loads overlap the replay of other waves)
-  const char* we = getenv("FBN_PFB_WAVES");
-  long long waves = we ? atoll(we) : 4096;
-  waves = std::max(waves, (n + 63) / 64);
-  const dim3 g3((unsigned)((waves + 3) / 4));
-#define FBN_PFB_LAUNCH(D_, DW_)                                                                               \
-  hipLaunchKernelGGL((adam_pfreplay_kernel<D_, DW_>), g3, dim3(256), 0, st, p, m, v,                          \
-                     (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, counts, list, (int)n)
-  if (D == 128) {
-    if (decoupled) FBN_PFB_LAUNCH(128, true); else FBN_PFB_LAUNCH(128, false);
-  } else {
-    if (decoupled) FBN_PFB_LAUNCH(256, true); else FBN_PFB_LAUNCH(256, false);
-  }
-#undef FBN_PFB_LAUNCH
-  FBN_CHECK_LAUNCH();
-  return FBN_OK;
-}
-
 // single GPU, D >= 128: ahead-of-time catch-up of the next batch's rows (adam_prefetch_kernel);
 // call on the stream of the rolling window, after this step's claims and before its step tail
 extern "C" int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B, int L, long long V, const int* map,
@@ -2577,11 +2385,11 @@ extern "C" int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B,
 // N > 1 (the owner's side): the same ahead-of-time catch-up over the local rows the NEXT step's
 // requests name (lids [n], -1 = none: the padded id exchange of RowExchange.prepare); rows this
 // step's requests claimed (map != -1) are left to the next step's claimed-row catch-up
-extern "C" int fbn_adam_prefetch_rows(const int* lids, int n, int skip0, long long nrows, const int* map, float* p,
-                                      float* m, float* v, int D, int* last, const void* consts_table, const int* step,
-                                      float wd, float beta2, float eps, int* pend, const float* ring,
-                                      const float* coef_hist, long long ring_stride, int ring_n, int decoupled,
-                                      void* stream) {
+extern "C" int fbn_adam_prefetch_rows(const int* lids, int n, int skip0, long long nrows, const int* map,
+                                      unsigned long long* preclaim, float* p, float* m, float* v, int D, int* last,
+                                      const void* consts_table, const int* step, float wd, float beta2, float eps,
+                                      int* pend, const float* ring, const float* coef_hist, long long ring_stride,
+                                      int ring_n, int decoupled, void* stream) {
   if (n <= 0 || nrows <= 0) return FBN_OK;
   if (D != 128 && D != 256) { fbn_set_error("fbn_adam_prefetch_rows: D = 128 or 256"); return FBN_ERR_ARG; }
   if (!lids || !map || !last) { fbn_set_error("fbn_adam_prefetch_rows: lids, map and last are required"); return FBN_ERR_ARG; }
@@ -2594,9 +2402,29 @@ extern "C" int fbn_adam_prefetch_rows(const int* lids, int n, int skip0, long lo
   ClaimSrc cs{nullptr, nullptr, 0, nrows, const_cast<int*>(map), nullptr, nullptr, nullptr, nullptr};
   cs.lids = lids;
   cs.skip0 = skip0;
+  hipStream_t st = (hipStream_t)stream;
+  if (preclaim) {
+    // the two passes of the single-GPU prefetch (adam_pretag + adam_prefetch2): tagged pre-claims
+    // decide each row's owning entry with one non-returning atomic, the four-row engine replays
+    // (round 3's one-pass kernel: a returning CAS per entry and 16-entry scans, ~174 us per step at
+    // one rank).  The tags only decide this pass: the next step's owner claims do not read them.
+    cs.pre = preclaim;
+    const dim3 g2((unsigned)((n + 255) / 256));
+    hipLaunchKernelGGL(adam_pretag_kernel, g2, dim3(256), 0, st, cs, n, step);
+    const int epw = 64;
+    const dim3 g3((unsigned)(((n + epw - 1) / epw + 3) / 4));
+    if (decoupled) {
+      FBN_DISPATCH_D_B(adam_prefetch2_kernel, true, D, g3, p, m, v, cs, n, last, (const AdamConsts*)consts_table,
+                       step, wd, beta2, omb2, eps, ps, epw);
+    } else {
+      FBN_DISPATCH_D_B(adam_prefetch2_kernel, false, D, g3, p, m, v, cs, n, last, (const AdamConsts*)consts_table,
+                       step, wd, beta2, omb2, eps, ps, epw);
+    }
+    FBN_CHECK_LAUNCH();
+    return FBN_OK;
+  }
   static const int pcap = getenv("FBN_PREFETCH_BLOCKS") ? atoi(getenv("FBN_PREFETCH_BLOCKS")) : 256;
   const dim3 grid((unsigned)std::min<long long>(pcap, ((long long)n + 63) / 64));
-  hipStream_t st = (hipStream_t)stream;
   if (D == 128) {
     if (decoupled)
       hipLaunchKernelGGL((adam_prefetch_kernel<128, true>), grid, dim3(256), 0, st, p, m, v, cs, n, last,

@@ -84,14 +84,14 @@ _DENSE_SUMSQ_FOLD = os.environ.get("FBN_DENSE_SUMSQ_FOLD", "1") == "1"
 # vs 0.69-0.72 ms/step (extra launches, a local-copy "all-to-all" competing for HBM) and the
 # overlap it buys at N > 1 could not be measured on a one-GPU box
 _EARLY_GRAD_XCHG = os.environ.get("FBN_EARLY_GRAD_XCHG")
-# single GPU, d = 128 / 256 with pre-claims: the next-batch prefetch in its binned form (balanced
-# waves, fbn_adam_prefetch_binned) with FBN_PF_BINNED=1; default adam_prefetch2 (a wave per 64 entries)
-_PF_BINNED = os.environ.get("FBN_PF_BINNED", "0") == "1"
 # single GPU, eager steps with the side stream (A/B knob, FBN_WGRAD_EARLY=1): the grouped weight-
 # gradient GEMMs of the MLP and the bilinear W (dWa, dWb, dW) launched on the side stream right after
 # the bilinear backward, beside the fields backward (HBM-bound) on the main stream; dW_p stays in the
 # flush's launch on main, which waits for the side stream before the slab sums
 _WGRAD_EARLY = os.environ.get("FBN_WGRAD_EARLY", "0") == "1"
+# N > 1, the owner's ahead-of-time catch-up of the next step's requested rows in two passes (tagged
+# pre-claims + the four-row replay engine); FBN_OWNER_PF2=0 keeps the one-pass kernel (A/B)
+_OWNER_PF2 = os.environ.get("FBN_OWNER_PF2", "1") != "0"
 from .schedule import OneCycle, adam_table
 
 TABLE = "item_emb.weight"
@@ -537,24 +537,11 @@ class FiBiNETTrainer:
                     return                                    # the one-pass form needs wave-wide rows
                 ev = _events(probe, "adam_prefetch", sst)
                 nB = nb["item_id"].shape[0]
-                if _PF_BINNED and self._pre_key is not None and d in (128, 256):
-                    # balanced waves: the owned rows binned by replay length, dealt round-robin
-                    n_ent = nB * (nL + 1)
-                    nbytes = _lib.lib().fbn_adam_prefetch_binned_ws_size(n_ent)
-                    ws = self.acts.get("_pfb_ws")
-                    if ws is None or ws.numel() * 8 < nbytes:
-                        ws = self.acts["_pfb_ws"] = torch.empty((nbytes + 7) // 8, dtype=torch.float64,
-                                                                device=self.device)
-                    call("fbn_adam_prefetch_binned", ptr(nb["item_id"]), ptr(nseq) if nL else None, nB, nL, self.V,
-                         ptr(self.map), ptr(self.preclaim), ptr(self.E), ptr(self.Em), ptr(self.Ev), d, ptr(self.last),
-                         ptr(self.sched), ptr(self.step_dev), self.wd_g, self.beta2, self.eps, *self._pend_args(),
-                         int(self.decoupled), ptr(ws), nbytes, sst.cuda_stream)
-                else:
-                    call("fbn_adam_prefetch", ptr(nb["item_id"]), ptr(nseq) if nL else None, nB, nL,
-                         self.V, ptr(self.map), ptr(self.preclaim if self._pre_key is not None else None), ptr(self.E),
-                         ptr(self.Em), ptr(self.Ev), d, ptr(self.last),
-                         ptr(self.sched), ptr(self.step_dev), self.wd_g, self.beta2, self.eps, *self._pend_args(),
-                         int(self.decoupled), sst.cuda_stream)
+                call("fbn_adam_prefetch", ptr(nb["item_id"]), ptr(nseq) if nL else None, nB, nL,
+                     self.V, ptr(self.map), ptr(self.preclaim if self._pre_key is not None else None), ptr(self.E),
+                     ptr(self.Em), ptr(self.Ev), d, ptr(self.last),
+                     ptr(self.sched), ptr(self.step_dev), self.wd_g, self.beta2, self.eps, *self._pend_args(),
+                     int(self.decoupled), sst.cuda_stream)
                 _events_end(ev, sst)
 
         def start_untouched_adam():
@@ -619,7 +606,8 @@ class FiBiNETTrainer:
                     self.side.wait_stream(self.xchg.side)
                     ev = _events(probe, "adam_prefetch", self.side)
                     call("fbn_adam_prefetch_rows", ptr(self.xchg.next_lids), self.xchg.next_lids.numel(),
-                         int(self.rank == 0), self.rows_local, ptr(self.map), ptr(self.E), ptr(self.Em),
+                         int(self.rank == 0), self.rows_local, ptr(self.map),
+                         ptr(self.row_state.view(torch.int64)[:, 0]) if _OWNER_PF2 else None, ptr(self.E), ptr(self.Em),
                          ptr(self.Ev), d, ptr(self.last), ptr(self.sched), ptr(self.step_dev), self.wd_g, self.beta2,
                          self.eps, *self._pend_args(), int(self.decoupled), self.side.cuda_stream)
                     _events_end(ev, self.side)

@@ -363,25 +363,17 @@ int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B, int L, lon
                       const void* consts_table, const int* step, float wd, float beta2, float eps, int* pend,
                       const float* ring, const float* coef_hist, long long ring_stride, int ring_n, int decoupled,
                       void* stream);
-/* The binned form of fbn_adam_prefetch (D = 128 / 256, pre-claims required): the same rows caught
- * up with the same operations (bit-identical), but the owned rows are filed in bins by replay length
- * and replayed as one list of 4-row groups dealt round-robin to the waves (balanced waves instead of
- * a wave per 64 entries).  Replaces the same reference lines as fbn_adam_prefetch.
- * ws: >= fbn_adam_prefetch_binned_ws_size(B * (L + 1)) bytes of scratch (caller-owned). */
-size_t fbn_adam_prefetch_binned_ws_size(long long n);
-int fbn_adam_prefetch_binned(const int64_t* item, const int64_t* seq, int B, int L, long long V, const int* map,
-                             unsigned long long* preclaim, float* p, float* m, float* v, int D, int* last,
-                             const void* consts_table, const int* step, float wd, float beta2, float eps, int* pend,
-                             const float* ring, const float* coef_hist, long long ring_stride, int ring_n,
-                             int decoupled, void* ws, size_t ws_bytes, void* stream);
 
 /* N > 1, the owner's side, D = 128 / 256: fbn_adam_prefetch over local rows lids [n] (-1 = none;
  * skip0: row 0 is the padding id, rank 0) -- the rows the NEXT step's requests name, received
- * through fbn_pad_routes + an equal-split all-to-all during this step. */
-int fbn_adam_prefetch_rows(const int* lids, int n, int skip0, long long nrows, const int* map, float* p, float* m,
-                           float* v, int D, int* last, const void* consts_table, const int* step, float wd,
-                           float beta2, float eps, int* pend, const float* ring, const float* coef_hist,
-                           long long ring_stride, int ring_n, int decoupled, void* stream);
+ * through fbn_pad_routes + an equal-split all-to-all during this step.  preclaim (the row-state
+ * records' tag field, optional): the two-pass form -- tagged pre-claims decide each row's entry with
+ * one non-returning atomic, the four-row engine replays; NULL: the one-pass kernel. */
+int fbn_adam_prefetch_rows(const int* lids, int n, int skip0, long long nrows, const int* map,
+                           unsigned long long* preclaim, float* p, float* m, float* v, int D, int* last,
+                           const void* consts_table, const int* step, float wd, float beta2, float eps, int* pend,
+                           const float* ring, const float* coef_hist, long long ring_stride, int ring_n,
+                           int decoupled, void* stream);
 int fbn_adam_flush(float* p, float* m, float* v, long long nrows, int D, int* last, const void* consts_table,
                    const int* step, float wd, float beta2, float eps, int* pend, const float* ring,
                    const float* coef_hist, long long ring_stride, int ring_n, int decoupled, void* stream);

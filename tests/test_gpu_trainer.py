@@ -253,13 +253,10 @@ def test_deferred_table_grads_bit_identical(hip_device):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("defer,dups,d,binned", [(True, False, 128, False), (False, False, 128, False),
-                                                 (True, True, 128, False), (True, True, 256, False),
-                                                 (True, False, 16, False), (True, True, 16, False),
-                                                 (False, False, 64, False), (True, False, 128, True),
-                                                 (False, False, 128, True), (True, True, 128, True),
-                                                 (True, True, 256, True)])
-def test_next_batch_prefetch_bit_identical(hip_device, defer, dups, d, binned, monkeypatch):
+@pytest.mark.parametrize("defer,dups,d", [(True, False, 128), (False, False, 128), (True, True, 128),
+                                          (True, True, 256), (True, False, 16), (True, True, 16),
+                                          (False, False, 64)])
+def test_next_batch_prefetch_bit_identical(hip_device, defer, dups, d):
     """fbn_adam_prefetch: with step(..., next_batch=...) the next batch's rows that this batch does
     not touch are brought up to date on the side stream during this step.  Against the same run
     without prefetch: losses, table, Adam moments, dense parameters and last[] bit-identical (ids
@@ -270,8 +267,6 @@ def test_next_batch_prefetch_bit_identical(hip_device, defer, dups, d, binned, m
     would round in arrival order.  The last step's next_batch is never used: rows prefetched for it are simply up to
     date early."""
     V, B, L, steps = 40000, 64, 20, 14
-    from ctr_recommendation_amd import trainer as trmod
-    monkeypatch.setattr(trmod, "_PF_BINNED", binned)     # binned: fbn_adam_prefetch_binned (d >= 128)
     cfg = {"embedding_dim": d, "vocab_size": V}
     torch.manual_seed(0)
     init = oracle_build(None, cfg).state_dict()

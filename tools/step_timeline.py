@@ -33,7 +33,7 @@ def main():
     def is_window(k, ks):
         # side stream: the rolling-window replay (the adam_catchup launch of the step with the
         # smaller grid) and the next batch's ahead-of-time catch-up (adam_prefetch)
-        if any(s in k[2] for s in ("adam_prefetch", "adam_pretag", "adam_window2", "adam_pfbin", "adam_pfreplay",
+        if any(s in k[2] for s in ("adam_prefetch", "adam_pretag", "adam_window2",
                                    "sparse_fixup_dup")):
             return True
         cs = [c[3] for c in ks if "adam_catchup" in c[2]]
