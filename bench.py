@@ -522,6 +522,8 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
     out = {"dt": dt, "t_host": t_host, "t_wait": t_wait, "K": K, "W": W, "B": B, "L": L, "V": V, "d": d, "rows_local": tr.rows_local, "loss": loss,
            "rooflines": rooflines, "roofline": dominant, "table_adam": tr.table_adam,
            "graphs": mode_now[0] == "graph", "launch_mode": mode_now[0] if not sharded else "eager",
+           "collectives": (None if not sharded else "RCCL on the step's stream (csrc/comm.cpp)"
+                           if tr.native_comm is not None else "torch.distributed process group"),
            "mode_trial_ms_per_step": {k: [round(x, 4) for x in v] for k, v in trial.items()} if trial else None,
            "prime": prime, "batches": nb, "lag": lag, "stale": stale, "touched": touched, "prefetch": prefetch}
     del graphs, progs, tr, batches
@@ -610,6 +612,7 @@ def main():
                        "item_rows": r["V"], "item_rows_per_gpu": r["rows_local"], "emb_dim": r["d"],
                        "parallelism": f"row-shard{world}" if world > 1 or FORCE_SHARD else "single",
                        "hipgraph": r["graphs"], "launch_mode": r["launch_mode"],
+                       **({"collectives": r["collectives"]} if r.get("collectives") else {}),
                        **({"rehearsal": backend} if rehearsal else {}),
                        **({"launch_mode_trial_ms_per_step": r["mode_trial_ms_per_step"]}
                           if r.get("mode_trial_ms_per_step") else {}),

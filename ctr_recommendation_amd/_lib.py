@@ -127,6 +127,14 @@ SIGNATURES = {
     "fbn_plan_add_record": (I, [P, I, P]),
     "fbn_plan_add_wait": (I, [P, P, I]),
     "fbn_plan_run": (I, [P, P]),
+    "fbn_comm_load": (I, [ctypes.c_char_p]),
+    "fbn_comm_id_bytes": (I, []),
+    "fbn_comm_unique_id": (I, [P]),
+    "fbn_comm_init": (I, [P, P, I, I]),
+    "fbn_comm_destroy": (I, [P]),
+    "fbn_comm_alltoallv": (I, [P, P, P, P, P, LL, P]),
+    "fbn_comm_alltoall": (I, [P, P, P, LL, P]),
+    "fbn_comm_allreduce": (I, [P, P, LL, I, P]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

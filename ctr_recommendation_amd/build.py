@@ -16,7 +16,7 @@ CSRC = os.path.join(HERE, "csrc")
 ROOT = os.path.dirname(HERE)
 BUILD = os.path.join(ROOT, "build", "fibinet_hip")
 LIB = os.path.join(HERE, "libfibinet_hip.so")
-SOURCES = ["capi.cpp", "gemm.hip", "fields.hip", "mlp.hip", "optim.hip", "exchange.hip", "collate.hip", "bilinear.hip", "plan.cpp"]
+SOURCES = ["capi.cpp", "gemm.hip", "fields.hip", "mlp.hip", "optim.hip", "exchange.hip", "collate.hip", "bilinear.hip", "plan.cpp", "comm.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result",
@@ -44,7 +44,7 @@ def build(verbose: bool = True) -> str:
         objs = list(ex.map(_compile, SOURCES))
     newest = max(os.path.getmtime(o) for o in objs)
     if not os.path.exists(LIB) or os.path.getmtime(LIB) < newest:
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + ["-ldl"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")

@@ -1,0 +1,204 @@
+// RCCL communicators of the row-sharded step (N > 1), enqueued on the CALLER's stream.
+//
+// The row exchange (route ids -> owner gather -> rows back; per-entry gradient rows -> owner)
+// and the dense-gradient all-reduce are collectives between kernels of the same step.  Issued
+// through torch.distributed they run on the process group's internal stream, and every one of
+// them costs two cross-queue event edges (compute -> collective -> compute): ~10-20 us each on
+// MI355X, ~55 us of idle GPU per step at one rank (profiles/r04_shard_gaps.txt).  Here the
+// collectives are RCCL calls on the stream the step's kernels run on -- no edges at all.
+//
+// RCCL is the one torch already loaded (its librccl.so, passed to fbn_comm_load by path and
+// bound with dlopen/dlsym): one RCCL runtime per process, whatever rccl the system also has.
+// The unique id travels over torch.distributed (exchange.py NativeComm); only the data path is
+// here.  All-to-all with per-peer counts = grouped ncclSend/ncclRecv (the counts are host ints,
+// read at call time); equal-split all-to-all = ncclAllToAll; sum all-reduce in place.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdio.h>
+#include <string.h>
+
+void fbn_set_error(const char* msg);
+
+namespace {
+
+struct Rccl {
+  void* handle = nullptr;
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclSend) send = nullptr;
+  decltype(&ncclRecv) recv = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclAllToAll) all_to_all = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+};
+
+Rccl g_rccl;
+
+struct Comm {
+  ncclComm_t comm;
+  int world;
+  int rank;
+};
+
+int fail(const char* where, ncclResult_t r) {
+  char msg[256];
+  snprintf(msg, sizeof(msg), "%s: %s", where, g_rccl.error_string ? g_rccl.error_string(r) : "rccl error");
+  fbn_set_error(msg);
+  return 3;
+}
+
+int need_loaded(const char* where) {
+  if (g_rccl.handle) return 0;
+  char msg[160];
+  snprintf(msg, sizeof(msg), "%s: RCCL not loaded (fbn_comm_load first)", where);
+  fbn_set_error(msg);
+  return 1;
+}
+
+template <typename F>
+bool bind(void* h, const char* name, F* out) {
+  *out = reinterpret_cast<F>(dlsym(h, name));
+  return *out != nullptr;
+}
+
+}  // namespace
+
+// Bind the RCCL library at `path` (torch's own librccl.so: already mapped, so no second copy).
+extern "C" int fbn_comm_load(const char* path) {
+  if (g_rccl.handle) return 0;
+  if (!path) {
+    fbn_set_error("fbn_comm_load: null path");
+    return 1;
+  }
+  void* h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+  if (!h) {
+    char msg[512];
+    snprintf(msg, sizeof(msg), "fbn_comm_load: dlopen(%s) failed: %s", path, dlerror());
+    fbn_set_error(msg);
+    return 1;
+  }
+  Rccl r;
+  r.handle = h;
+  bool ok = bind(h, "ncclGetUniqueId", &r.get_unique_id) && bind(h, "ncclCommInitRank", &r.comm_init_rank) &&
+            bind(h, "ncclCommDestroy", &r.comm_destroy) && bind(h, "ncclSend", &r.send) &&
+            bind(h, "ncclRecv", &r.recv) && bind(h, "ncclGroupStart", &r.group_start) &&
+            bind(h, "ncclGroupEnd", &r.group_end) && bind(h, "ncclAllReduce", &r.all_reduce) &&
+            bind(h, "ncclAllToAll", &r.all_to_all) && bind(h, "ncclGetErrorString", &r.error_string);
+  if (!ok) {
+    fbn_set_error("fbn_comm_load: the library lacks an RCCL entry point");
+    dlclose(h);
+    return 1;
+  }
+  g_rccl = r;
+  return 0;
+}
+
+extern "C" int fbn_comm_id_bytes() { return (int)sizeof(ncclUniqueId); }
+
+// rank 0: a fresh unique id (NCCL_UNIQUE_ID_BYTES bytes into `out`) for every rank's fbn_comm_init
+extern "C" int fbn_comm_unique_id(void* out) {
+  if (int rc = need_loaded("fbn_comm_unique_id")) return rc;
+  if (!out) {
+    fbn_set_error("fbn_comm_unique_id: null out");
+    return 1;
+  }
+  ncclUniqueId id;
+  ncclResult_t r = g_rccl.get_unique_id(&id);
+  if (r != ncclSuccess) return fail("fbn_comm_unique_id", r);
+  memcpy(out, &id, sizeof(id));
+  return 0;
+}
+
+// collective over the `world` ranks: every rank calls it with the same id, on its own device
+extern "C" int fbn_comm_init(void** out, const void* id, int world, int rank) {
+  if (int rc = need_loaded("fbn_comm_init")) return rc;
+  if (!out || !id || world < 1 || rank < 0 || rank >= world) {
+    fbn_set_error("fbn_comm_init: bad arguments");
+    return 1;
+  }
+  ncclUniqueId uid;
+  memcpy(&uid, id, sizeof(uid));
+  Comm* c = new Comm{nullptr, world, rank};
+  ncclResult_t r = g_rccl.comm_init_rank(&c->comm, world, uid, rank);
+  if (r != ncclSuccess) {
+    delete c;
+    return fail("fbn_comm_init", r);
+  }
+  *out = c;
+  return 0;
+}
+
+extern "C" int fbn_comm_destroy(void* comm) {
+  Comm* c = static_cast<Comm*>(comm);
+  if (!c) return 0;
+  if (g_rccl.handle && c->comm) (void)g_rccl.comm_destroy(c->comm);
+  delete c;
+  return 0;
+}
+
+// All-to-all with per-peer counts (rows of `row_bytes` bytes; send_counts / recv_counts: host
+// int arrays of `world` entries, read now).  Blocks are packed in rank order on both sides.
+extern "C" int fbn_comm_alltoallv(void* comm, const void* send, const int* send_counts, void* recv,
+                                  const int* recv_counts, long long row_bytes, void* stream) {
+  if (int rc = need_loaded("fbn_comm_alltoallv")) return rc;
+  Comm* c = static_cast<Comm*>(comm);
+  if (!c || !send_counts || !recv_counts || row_bytes <= 0) {
+    fbn_set_error("fbn_comm_alltoallv: bad arguments");
+    return 1;
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const char* sp = static_cast<const char*>(send);
+  char* rp = static_cast<char*>(recv);
+  for (int p = 0; p < c->world; ++p) {
+    if (send_counts[p] < 0 || recv_counts[p] < 0) {
+      fbn_set_error("fbn_comm_alltoallv: negative count");
+      return 1;
+    }
+  }
+  ncclResult_t r = g_rccl.group_start();
+  if (r != ncclSuccess) return fail("fbn_comm_alltoallv", r);
+  size_t so = 0, ro = 0;
+  for (int p = 0; p < c->world && r == ncclSuccess; ++p) {
+    size_t sb = (size_t)send_counts[p] * (size_t)row_bytes, rb = (size_t)recv_counts[p] * (size_t)row_bytes;
+    if (sb) r = g_rccl.send(sp + so, sb, ncclUint8, p, c->comm, s);
+    if (r == ncclSuccess && rb) r = g_rccl.recv(rp + ro, rb, ncclUint8, p, c->comm, s);
+    so += sb;
+    ro += rb;
+  }
+  ncclResult_t e = g_rccl.group_end();
+  if (r != ncclSuccess) return fail("fbn_comm_alltoallv", r);
+  if (e != ncclSuccess) return fail("fbn_comm_alltoallv", e);
+  return 0;
+}
+
+// Equal-split all-to-all: `bytes_per_peer` bytes to and from every rank.
+extern "C" int fbn_comm_alltoall(void* comm, const void* send, void* recv, long long bytes_per_peer, void* stream) {
+  if (int rc = need_loaded("fbn_comm_alltoall")) return rc;
+  Comm* c = static_cast<Comm*>(comm);
+  if (!c || bytes_per_peer < 0) {
+    fbn_set_error("fbn_comm_alltoall: bad arguments");
+    return 1;
+  }
+  if (bytes_per_peer == 0) return 0;
+  ncclResult_t r = g_rccl.all_to_all(send, recv, (size_t)bytes_per_peer, ncclUint8, c->comm,
+                                     static_cast<hipStream_t>(stream));
+  return r == ncclSuccess ? 0 : fail("fbn_comm_alltoall", r);
+}
+
+// In-place sum all-reduce of n elements: dtype 0 = f32, 1 = f64, 2 = i32.
+extern "C" int fbn_comm_allreduce(void* comm, void* buf, long long n, int dtype, void* stream) {
+  if (int rc = need_loaded("fbn_comm_allreduce")) return rc;
+  Comm* c = static_cast<Comm*>(comm);
+  if (!c || n < 0 || dtype < 0 || dtype > 2) {
+    fbn_set_error("fbn_comm_allreduce: bad arguments");
+    return 1;
+  }
+  if (n == 0) return 0;
+  ncclDataType_t t = dtype == 0 ? ncclFloat32 : (dtype == 1 ? ncclFloat64 : ncclInt32);
+  ncclResult_t r = g_rccl.all_reduce(buf, buf, (size_t)n, t, ncclSum, c->comm, static_cast<hipStream_t>(stream));
+  return r == ncclSuccess ? 0 : fail("fbn_comm_allreduce", r);
+}

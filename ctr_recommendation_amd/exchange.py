@@ -24,6 +24,8 @@ all-to-all.
 """
 from __future__ import annotations
 
+import ctypes
+import os
 import time
 from typing import Optional
 
@@ -32,6 +34,65 @@ import torch.distributed as dist
 
 from . import _lib
 from ._lib import call, ptr
+
+
+def _torch_rccl() -> str:
+    """The RCCL library torch's process groups use (torch/lib/librccl.so), so the native
+    communicators share its runtime; the system one if torch carries none."""
+    p = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    return p if os.path.exists(p) else "librccl.so.1"
+
+
+_DTYPE_CODE = {torch.float32: 0, torch.float64: 1, torch.int32: 2}
+
+
+class NativeComm:
+    """An RCCL communicator driven through the C-ABI (csrc/comm.cpp): collectives enqueued on the
+    CALLER's stream, between the step's kernels, with no cross-queue edges (torch.distributed runs
+    each collective on its process group's own stream behind two event edges, ~10-20 us apiece).
+    Creation is collective over `group` (rank 0's unique id is broadcast through it)."""
+
+    def __init__(self, world: int, rank: int, group=None, device=None):
+        call("fbn_comm_load", _torch_rccl().encode())
+        n = _lib.lib().fbn_comm_id_bytes()
+        uid = (ctypes.c_char * n)()
+        if rank == 0:
+            call("fbn_comm_unique_id", uid)
+        obj = [bytes(uid) if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0 if group is None else dist.get_global_rank(group, 0), group=group)
+        uid = (ctypes.c_char * n).from_buffer_copy(obj[0])
+        h = ctypes.c_void_p()
+        with torch.cuda.device(device if device is not None else torch.cuda.current_device()):
+            call("fbn_comm_init", ctypes.byref(h), uid, world, rank)
+        self.handle, self.world, self.rank = h.value, world, rank
+
+    def alltoallv(self, out: torch.Tensor, inp: torch.Tensor, recv_counts, send_counts) -> None:
+        """Rows (dim 0) of inp to the ranks, send_counts[r] to rank r; recv_counts[r] rows from r."""
+        row_bytes = inp.element_size() * (inp[0].numel() if inp.dim() > 1 else 1)
+        sc = (ctypes.c_int * self.world)(*send_counts)
+        rc = (ctypes.c_int * self.world)(*recv_counts)
+        call("fbn_comm_alltoallv", self.handle, ptr(inp), sc, ptr(out), rc, row_bytes,
+             _lib.stream_handle(out.device))
+
+    def alltoall(self, out: torch.Tensor, inp: torch.Tensor) -> None:
+        """Equal split: inp.numel() / world elements to every rank."""
+        call("fbn_comm_alltoall", self.handle, ptr(inp), ptr(out), inp.numel() * inp.element_size() // self.world,
+             _lib.stream_handle(out.device))
+
+    def allreduce_(self, t: torch.Tensor) -> None:
+        call("fbn_comm_allreduce", self.handle, ptr(t), t.numel(), _DTYPE_CODE[t.dtype], _lib.stream_handle(t.device))
+
+    def close(self) -> None:
+        if self.handle:
+            call("fbn_comm_destroy", self.handle)
+            self.handle = None
+
+
+def native_comm_wanted(device, group=None, stage_on_cpu: bool = False) -> bool:
+    """RCCL on the step's stream: a HIP device, an nccl (= RCCL) process group, unless
+    FBN_NATIVE_COMM=0 (then torch.distributed's collectives, on its own stream)."""
+    return (torch.device(device).type == "cuda" and not stage_on_cpu and dist.is_initialized()
+            and dist.get_backend(group) == "nccl" and os.environ.get("FBN_NATIVE_COMM", "1") != "0")
 
 
 class HipExchangeKernels:
@@ -62,13 +123,15 @@ class HipExchangeKernels:
 
 class RowExchange:
     def __init__(self, rank: int, world: int, V: int, d: int, B: int, L: int, device, group=None, kernels=None,
-                 stage_on_cpu: bool = False, rows_bf16: bool = False, side=None):
+                 stage_on_cpu: bool = False, rows_bf16: bool = False, side=None, comm: Optional[NativeComm] = None):
         self.rank, self.world, self.V, self.d, self.L, self.B = rank, world, V, d, L, B
         self.Vl = (V + world - 1) // world
         self.group = group
         self.k = kernels or HipExchangeKernels()
         self.device = device
         self.stage_on_cpu = stage_on_cpu          # gloo on a GPU box: collectives on host copies
+        self.comm = comm                          # RCCL on the caller's stream (NativeComm) or None
+        self.route_comm = None
         # bf16 mode: looked-up rows AND per-entry gradient rows cross the wire as bf16 (half the
         # bytes of both all-to-alls; the fields kernel widens the rows on load, the owner widens the
         # gradient rows on receipt and folds them in f32)
@@ -94,7 +157,10 @@ class RowExchange:
             self.side = side if side is not None else torch.cuda.Stream(device=device)
             # a communicator of its own: the next batch's counts exchange runs beside this step's
             # collectives instead of queueing between them (every rank creates it here, in order)
-            self.route_group = dist.new_group(ranks=list(range(world)))
+            if comm is not None:
+                self.route_comm = NativeComm(world, rank, group, device)
+            else:
+                self.route_group = dist.new_group(ranks=list(range(world)))
         self.send_counts = None
         self.recv_counts = None
         self.recv_ids = None
@@ -114,7 +180,15 @@ class RowExchange:
     def rows_local(self) -> int:
         return max(0, min(self.V, (self.rank + 1) * self.Vl) - self.rows_lo)
 
-    def _a2a(self, out, inp, out_splits, in_splits, group=None):
+    def _a2a(self, out, inp, out_splits, in_splits, group=None, route=False):
+        """out <- all-to-all of inp (rows; splits None = equal) on the current stream."""
+        if self.comm is not None:
+            comm = self.route_comm if route else self.comm
+            if out_splits is None:
+                comm.alltoall(out, inp)
+            else:
+                comm.alltoallv(out, inp, out_splits, in_splits)
+            return out
         group = group if group is not None else self.group
         if not self.stage_on_cpu:
             dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
@@ -176,7 +250,7 @@ class RowExchange:
             padded = torch.empty(self.world * (cap + 1), dtype=torch.int32, device=item.device)
             self.k.pad_routes(st["send_ids"], st["offsets"], st["counts"], self.world, cap, padded)
             recv = torch.empty_like(padded)
-            self._a2a(recv, padded, None, None, self.route_group)
+            self._a2a(recv, padded, None, None, self.route_group, route=True)
             if st["recv_ids"] is None or st["recv_ids"].numel() < self.world * cap:
                 st["recv_ids"] = torch.empty(self.world * cap, dtype=torch.int32, device=item.device)
             self.k.compact_routes(recv, self.world, cap, st["recv_ids"], st["recv_counts"])
@@ -267,7 +341,7 @@ class RowExchange:
         wire = grad if sendbuf.dtype == torch.float32 else \
             torch.empty((n_recv, self.d), dtype=sendbuf.dtype, device=sendbuf.device)
         work = None
-        if self.stage_on_cpu:
+        if self.stage_on_cpu or self.comm is not None:       # host-staged, or on this stream
             self._a2a(wire, sendbuf, self.recv_counts, self.send_counts)
         else:
             work = dist.all_to_all_single(wire, sendbuf, self.recv_counts, self.send_counts, group=self.group,
@@ -287,15 +361,18 @@ class RowExchange:
 class DistCollective:
     """SyncBN / gradient all-reduce hook for ops.forward/backward (sum over ranks)."""
 
-    def __init__(self, world: int, group=None, stage_on_cpu: bool = False):
+    def __init__(self, world: int, group=None, stage_on_cpu: bool = False, comm: Optional[NativeComm] = None):
         self.world = world
         self.group = group
         self.stage_on_cpu = stage_on_cpu
+        self.comm = comm
 
     def allreduce_(self, t: torch.Tensor) -> None:
         if self.world <= 1:
             return
-        if self.stage_on_cpu:
+        if self.comm is not None:
+            self.comm.allreduce_(t)
+        elif self.stage_on_cpu:
             c = t.cpu()
             dist.all_reduce(c, group=self.group)
             t.copy_(c)

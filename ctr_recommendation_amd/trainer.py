@@ -32,7 +32,7 @@ import torch.distributed as dist
 
 from . import _lib, ops
 from ._lib import call, ptr
-from .exchange import DistCollective, RowExchange
+from .exchange import DistCollective, NativeComm, RowExchange, native_comm_wanted
 from .model_fibinet import build_model
 
 # single GPU, bf16: where the step's bf16 weight images are made (A/B knob) -- "main": on the
@@ -354,7 +354,10 @@ class FiBiNETTrainer:
         self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
         self.host_step = 0
         self.acts: Dict[str, torch.Tensor] = {}
-        self.coll = DistCollective(world, group, stage_on_cpu)
+        # RCCL on the step's own stream (exchange.NativeComm) when the process group is RCCL
+        self.native_comm = NativeComm(world, rank, group, dev) \
+            if (sharded or world > 1) and native_comm_wanted(dev, group, stage_on_cpu) else None
+        self.coll = DistCollective(world, group, stage_on_cpu, comm=self.native_comm)
         # BatchNorm at N > 1.  sync_bn (default): statistics over the GLOBAL batch (one f64
         # all-reduce per BN layer and direction) -- the single-process reference run on the
         # global batch.  sync_bn=False: every rank normalises its own slice, which is what the
@@ -366,7 +369,7 @@ class FiBiNETTrainer:
         self.bn_coll = self.coll if self.sync_bn else ops.NO_COLLECTIVE
         self.side = _side_stream(dev)      # eager untouched pass / lazy rolling window / routing ahead
         self.xchg = RowExchange(rank, world, self.V, d, self.B, max_len, dev, group, stage_on_cpu=stage_on_cpu,
-                                rows_bf16=self.fcfg.bf16, side=self.side) if sharded else None
+                                rows_bf16=self.fcfg.bf16, side=self.side, comm=self.native_comm) if sharded else None
         self.stage_on_cpu = stage_on_cpu
         self.early_grad_xchg = _EARLY_GRAD_XCHG == "1"
         # item-table Adam: "lazy" (default) replays the zero-gradient steps of a row when the row
@@ -878,7 +881,9 @@ class FiBiNETTrainer:
         return None
 
     def _early_grad_xchg(self) -> bool:
-        return self.early_grad_xchg and self.xchg is not None and not self.stage_on_cpu
+        # torch.distributed's asynchronous collectives only: with RCCL on the step's stream the
+        # gradient rows already leave in stream order, right after the backward
+        return self.early_grad_xchg and self.xchg is not None and not self.stage_on_cpu and self.native_comm is None
 
     def _grad_xchg_start(self) -> None:
         """N > 1: the per-entry gradient rows are complete once the fields backward has run: their

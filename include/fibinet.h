@@ -506,6 +506,26 @@ int fbn_plan_add_record(void* plan, int slot, void* stream);
 int fbn_plan_add_wait(void* plan, void* stream, int slot);
 int fbn_plan_run(void* plan, int* failed);
 
+/* ---------------------------------------------------------------- RCCL on the step's stream (N > 1)
+ * The row exchange's all-to-alls and the dense all-reduce as RCCL calls on the stream the step's
+ * kernels run on (csrc/comm.cpp) instead of torch.distributed's internal stream -- replaces the
+ * process-group collectives the reference gets from nn.DataParallel (src/train_fibinet.py:69-70).
+ *   fbn_comm_load(path): bind torch's own librccl.so (dlopen + dlsym; one RCCL runtime per process)
+ *   fbn_comm_unique_id(out[fbn_comm_id_bytes()]) on rank 0, broadcast by the host, then
+ *   fbn_comm_init(&comm, id, world, rank) on every rank (collective).
+ *   fbn_comm_alltoallv: rows of row_bytes bytes, host int counts per peer (read at call time),
+ *   blocks packed in rank order; fbn_comm_alltoall: equal split; fbn_comm_allreduce: in-place sum,
+ *   dtype 0 f32 / 1 f64 / 2 i32.  Errors: 1 bad arguments / not loaded, 3 an RCCL error. */
+int fbn_comm_load(const char* path);
+int fbn_comm_id_bytes(void);
+int fbn_comm_unique_id(void* out);
+int fbn_comm_init(void** comm, const void* id, int world, int rank);
+int fbn_comm_destroy(void* comm);
+int fbn_comm_alltoallv(void* comm, const void* send, const int* send_counts, void* recv, const int* recv_counts,
+                       long long row_bytes, void* stream);
+int fbn_comm_alltoall(void* comm, const void* send, void* recv, long long bytes_per_peer, void* stream);
+int fbn_comm_allreduce(void* comm, void* buf, long long n, int dtype, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

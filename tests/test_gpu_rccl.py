@@ -4,7 +4,9 @@ RCCL refuses two ranks on one device, so the multi-rank rehearsals (test_gpu_mul
 run their collectives over gloo.  This test runs the sharded code path itself -- RowExchange's
 all-to-alls with host split lists, the route-ahead communicator and its side-stream
 all-to-all (prepare), the owner-side prefetch, deferred gradient rows in a ring slot, the
-packed dense all-reduce -- over the "nccl" backend (RCCL) with world = 1 (FiBiNETTrainer
+packed dense all-reduce -- over the "nccl" backend (RCCL) with world = 1, both with RCCL called
+on the step's own stream (csrc/comm.cpp, the default) and through torch.distributed's process
+group (FiBiNETTrainer
 shard=True), in a child process, and checks it against the single-GPU trainer on the same
 batches: fp32 losses within 1e-5 (relative), the table within 1e-5 after the flush and the dense
 parameters within 1e-3 of their displacement (norm; as test_gpu_trainer.py); with the bf16 wire
@@ -47,11 +49,17 @@ def _worker(port, q):
             init = build_model(None, cfg, honour_config=True).state_dict()
             bs = [make_batch(500 + s, B, V, device=dev) for s in range(steps + 1)]
             res = []
+            # (shard, early): the single GPU; the sharded step with RCCL on the step's stream (the
+            # default, exchange.NativeComm); torch.distributed's collectives with the early
+            # (asynchronous) gradient all-to-all issued after the fields backward
             for shard, early in ((False, False), (True, False), (True, True)):
+                os.environ["FBN_NATIVE_COMM"] = "0" if early else "1"
                 tr = FiBiNETTrainer(cfg, total_steps=20, batch_size=B, device=dev, init_state=
                                     {k: v.clone() for k, v in init.items()}, shard=shard)
-                tr.early_grad_xchg = early      # the gradient all-to-all issued after the fields backward
+                tr.early_grad_xchg = early
                 assert (tr.xchg is not None) == shard
+                assert (tr.native_comm is not None) == (shard and not early)
+                assert tr._early_grad_xchg() == early
                 p_init = tr.flat_p.cpu().clone()
                 if shard:
                     assert tr.xchg.side is not None and tr.prefetch_owner and tr.deferred
