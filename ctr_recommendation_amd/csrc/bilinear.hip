@@ -36,23 +36,28 @@ __device__ __forceinline__ int swz(int r, int k) {   // element offset of (row r
   return r * D + ((((k >> 3) ^ (r % CH))) << 3) + (k & 7);
 }
 
+// threads per workgroup and 16-row blocks of n per wave: D/32 waves of two blocks each; at D = 16
+// one wave with one block
+template <int D> constexpr int nthreads() { return D >= 32 ? 2 * D : 64; }
+template <int D> constexpr int row_blocks() { return D >= 32 ? 2 : 1; }
+
 // 16-B chunk loads of a [D][D] bf16 image into the swizzled LDS image.  Every load of a thread is
 // issued before any LDS store (register-staged batch): one HBM/L2 round trip per stage, not one
 // per chunk.
 template <int D, int NT>
 struct WStage {
-  static constexpr int CH = D / 8, N = D * CH / NT;
-  static_assert((D * CH) % NT == 0, "W image / thread mismatch");
+  static constexpr int CH = D / 8, TOT = D * CH, N = (TOT + NT - 1) / NT;
   bf16x8 v[N];
   __device__ __forceinline__ void load(const short* __restrict__ src, int tid) {
 #pragma unroll
-    for (int j = 0; j < N; ++j) v[j] = *reinterpret_cast<const bf16x8*>(src + (size_t)(tid + j * NT) * 8);
+    for (int j = 0; j < N; ++j)
+      if (TOT % NT == 0 || tid + j * NT < TOT) v[j] = *reinterpret_cast<const bf16x8*>(src + (size_t)(tid + j * NT) * 8);
   }
   __device__ __forceinline__ void store(short* __restrict__ img, int tid) const {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       const int i = tid + j * NT, r = i / CH, c = i % CH;
-      *reinterpret_cast<bf16x8*>(img + swz<D>(r, c * 8)) = v[j];
+      if (TOT % NT == 0 || i < TOT) *reinterpret_cast<bf16x8*>(img + swz<D>(r, c * 8)) = v[j];
     }
   }
 };
@@ -67,20 +72,19 @@ __device__ __forceinline__ void stage_w(short* __restrict__ img, const short* __
 template <int D, int NT>
 __device__ __forceinline__ void stage_v(short* __restrict__ img, const short* __restrict__ V16, int b0, int ns,
                                         int tid) {
-  constexpr int CH = D / 8, N = TS * 5 * CH / NT;
-  static_assert((TS * 5 * CH) % NT == 0, "V tile / thread mismatch");
+  constexpr int CH = D / 8, TOT = TS * 5 * CH, N = (TOT + NT - 1) / NT;
   const short* src = V16 + (size_t)b0 * 5 * D;
   bf16x8 v[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) {
     const int i = tid + j * NT, m = i / CH;          // m = s*5 + f
     v[j] = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-    if (m / 5 < ns) v[j] = *reinterpret_cast<const bf16x8*>(src + (size_t)i * 8);
+    if ((TOT % NT == 0 || i < TOT) && m / 5 < ns) v[j] = *reinterpret_cast<const bf16x8*>(src + (size_t)i * 8);
   }
 #pragma unroll
   for (int j = 0; j < N; ++j) {
     const int i = tid + j * NT, m = i / CH, c = i % CH;
-    *reinterpret_cast<bf16x8*>(img + swz<D>((m % 5) * TS + m / 5, c * 8)) = v[j];
+    if (TOT % NT == 0 || i < TOT) *reinterpret_cast<bf16x8*>(img + swz<D>((m % 5) * TS + m / 5, c * 8)) = v[j];
   }
 }
 
@@ -90,9 +94,20 @@ __device__ __forceinline__ bf16x8 frag(const short* img, int row, int k) {
 }
 
 // acc[rb][f][i] += sum_k A[n][k] * Bt[f*16 + s][k], n = 32w + 16rb + 4(lane>>4) + i, s = lane & 15
+// (D = 16: K = 16, one v_mfma_f32_16x16x16_bf16 per field, 4 k per lane)
 template <int D>
-__device__ __forceinline__ void mfma_5(f32x4 (&acc)[2][5], const short* A, const short* Bt, int w, int lane) {
+__device__ __forceinline__ void mfma_5(f32x4 (&acc)[row_blocks<D>()][5], const short* A, const short* Bt, int w,
+                                       int lane) {
   const int lr = lane & 15, lq = lane >> 4;
+  if constexpr (D == 16) {
+    const bf16x4 a = *reinterpret_cast<const bf16x4*>(A + swz<D>(lr, 4 * lq));
+#pragma unroll
+    for (int f = 0; f < 5; ++f) {
+      const bf16x4 b = *reinterpret_cast<const bf16x4*>(Bt + swz<D>(f * TS + lr, 4 * lq));
+      acc[0][f] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, acc[0][f], 0, 0, 0);
+    }
+    return;
+  }
 #pragma unroll
   for (int ks = 0; ks < D / 32; ++ks) {
     bf16x8 b[5];
@@ -117,10 +132,11 @@ constexpr int PI[10] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3};
 constexpr int PJ[10] = {1, 2, 3, 4, 2, 3, 4, 3, 4, 4};
 
 template <int D>
-__global__ void __launch_bounds__(2 * D) bilinear_fwd_kernel(const short* __restrict__ V16, const short* __restrict__ WT16,
-                                                            short* __restrict__ c, int B, int ldc) {
+__global__ void __launch_bounds__(nthreads<D>()) bilinear_fwd_kernel(const short* __restrict__ V16,
+                                                                    const short* __restrict__ WT16,
+                                                                    short* __restrict__ c, int B, int ldc) {
   FBN_MAIN_PRIO();
-  constexpr int NT = 2 * D;   // D/32 waves
+  constexpr int NT = nthreads<D>(), RB = row_blocks<D>();
   __shared__ __attribute__((aligned(16))) short sV[5 * TS * D];
   __shared__ __attribute__((aligned(16))) short sW[D * D];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -128,9 +144,9 @@ __global__ void __launch_bounds__(2 * D) bilinear_fwd_kernel(const short* __rest
   stage_v<D, NT>(sV, V16, b0, ns, tid);
   stage_w<D, NT>(sW, WT16, tid);
   __syncthreads();
-  f32x4 acc[2][5];
+  f32x4 acc[RB][5];
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb)
+  for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
     for (int f = 0; f < 5; ++f) acc[rb][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
   mfma_5<D>(acc, sW, sV, w, lane);          // acc[rb][f] = U_f^T[n0..n0+3][s]
@@ -138,7 +154,7 @@ __global__ void __launch_bounds__(2 * D) bilinear_fwd_kernel(const short* __rest
   if (s >= ns) return;
   short* crow = c + (size_t)(b0 + s) * ldc + 5 * D;
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb) {
+  for (int rb = 0; rb < RB; ++rb) {
     const int n0 = 32 * w + 16 * rb + 4 * lq;
     f32x4 v[4];
 #pragma unroll
@@ -156,12 +172,14 @@ __device__ __forceinline__ f32x4 ld_dc4(const void* __restrict__ row, int off) {
 }
 
 template <int D, bool DC16>
-__global__ void __launch_bounds__(2 * D, 2) bilinear_bwd_kernel(const void* __restrict__ dc, int ldc,
-                                                            const short* __restrict__ V16, const short* __restrict__ WT16,
-                                                            const short* __restrict__ W16, float* __restrict__ dV,
-                                                            short* __restrict__ dU16, int B) {
+__global__ void __launch_bounds__(nthreads<D>(), 2) bilinear_bwd_kernel(const void* __restrict__ dc, int ldc,
+                                                                       const short* __restrict__ V16,
+                                                                       const short* __restrict__ WT16,
+                                                                       const short* __restrict__ W16,
+                                                                       float* __restrict__ dV,
+                                                                       short* __restrict__ dU16, int B) {
   FBN_MAIN_PRIO();
-  constexpr int NT = 2 * D;
+  constexpr int NT = nthreads<D>(), RB = row_blocks<D>();
   __shared__ __attribute__((aligned(16))) short sV[5 * TS * D];   // V tile, then dU tile
   __shared__ __attribute__((aligned(16))) short sW[D * D];        // W^T image, then W image
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -171,9 +189,9 @@ __global__ void __launch_bounds__(2 * D, 2) bilinear_bwd_kernel(const void* __re
   __syncthreads();
   WStage<D, NT> wnext;
   wnext.load(W16, tid);                     // the W image for dV += dU W^T: in flight meanwhile
-  f32x4 acc[2][5];
+  f32x4 acc[RB][5];
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb)
+  for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
     for (int f = 0; f < 5; ++f) acc[rb][f] = (f32x4){0.f, 0.f, 0.f, 0.f};
   mfma_5<D>(acc, sW, sV, w, lane);          // acc = U^T (recomputed: never stored)
@@ -182,7 +200,7 @@ __global__ void __launch_bounds__(2 * D, 2) bilinear_bwd_kernel(const void* __re
   const bool live = s < ns;
   const char* dcr = reinterpret_cast<const char*>(dc) + (size_t)(b0 + (live ? s : 0)) * ldc * (DC16 ? 2 : 4);
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb) {
+  for (int rb = 0; rb < RB; ++rb) {
     const int n0 = 32 * w + 16 * rb + 4 * lq;
     f32x4 v[5], gv[5], gu[5];
 #pragma unroll
@@ -213,7 +231,7 @@ __global__ void __launch_bounds__(2 * D, 2) bilinear_bwd_kernel(const void* __re
   mfma_5<D>(acc, sW, sV, w, lane);          // acc = dV^T = elementwise part + W dU^T
   if (!live) return;
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb) {
+  for (int rb = 0; rb < RB; ++rb) {
     const int k0 = 32 * w + 16 * rb + 4 * lq;
 #pragma unroll
     for (int f = 0; f < 5; ++f) *reinterpret_cast<f32x4*>(dV + ((size_t)(b0 + s) * 5 + f) * D + k0) = acc[rb][f];
@@ -222,7 +240,7 @@ __global__ void __launch_bounds__(2 * D, 2) bilinear_bwd_kernel(const void* __re
 
 }  // namespace
 
-extern "C" int fbn_bilinear_supported(int D) { return D == 64 || D == 128; }
+extern "C" int fbn_bilinear_supported(int D) { return D == 16 || D == 32 || D == 64 || D == 128; }
 
 extern "C" int fbn_bilinear_fwd(const short* V16, const short* WT16, short* c, int B, int D, int ldc, void* stream) {
   if (B <= 0) return FBN_OK;
@@ -232,9 +250,13 @@ extern "C" int fbn_bilinear_fwd(const short* V16, const short* WT16, short* c, i
   }
   const dim3 grid((unsigned)((B + TS - 1) / TS));
   hipStream_t st = (hipStream_t)stream;
-  if (D == 128) hipLaunchKernelGGL(bilinear_fwd_kernel<128>, grid, dim3(256), 0, st, V16, WT16, c, B, ldc);
-  else if (D == 64) hipLaunchKernelGGL(bilinear_fwd_kernel<64>, grid, dim3(128), 0, st, V16, WT16, c, B, ldc);
-  else { fbn_set_error("fbn_bilinear_fwd: D must be 64 or 128"); return FBN_ERR_UNSUPPORTED; }
+  switch (D) {
+    case 128: hipLaunchKernelGGL(bilinear_fwd_kernel<128>, grid, dim3(256), 0, st, V16, WT16, c, B, ldc); break;
+    case 64: hipLaunchKernelGGL(bilinear_fwd_kernel<64>, grid, dim3(128), 0, st, V16, WT16, c, B, ldc); break;
+    case 32: hipLaunchKernelGGL(bilinear_fwd_kernel<32>, grid, dim3(64), 0, st, V16, WT16, c, B, ldc); break;
+    case 16: hipLaunchKernelGGL(bilinear_fwd_kernel<16>, grid, dim3(64), 0, st, V16, WT16, c, B, ldc); break;
+    default: fbn_set_error("fbn_bilinear_fwd: D must be 16, 32, 64 or 128"); return FBN_ERR_UNSUPPORTED;
+  }
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -250,15 +272,19 @@ extern "C" int fbn_bilinear_bwd(const void* dc, int ldc, int dc_bf16, const shor
   const dim3 grid((unsigned)((B + TS - 1) / TS));
   hipStream_t st = (hipStream_t)stream;
   if (!dc_bf16 && ((uintptr_t)dc & 15)) { fbn_set_error("fbn_bilinear_bwd: f32 dc must be 16-B aligned"); return FBN_ERR_ARG; }
-  if (D == 128 && dc_bf16)
-    hipLaunchKernelGGL((bilinear_bwd_kernel<128, true>), grid, dim3(256), 0, st, dc, ldc, V16, WT16, W16, dV, dU16, B);
-  else if (D == 128)
-    hipLaunchKernelGGL((bilinear_bwd_kernel<128, false>), grid, dim3(256), 0, st, dc, ldc, V16, WT16, W16, dV, dU16, B);
-  else if (D == 64 && dc_bf16)
-    hipLaunchKernelGGL((bilinear_bwd_kernel<64, true>), grid, dim3(128), 0, st, dc, ldc, V16, WT16, W16, dV, dU16, B);
-  else if (D == 64)
-    hipLaunchKernelGGL((bilinear_bwd_kernel<64, false>), grid, dim3(128), 0, st, dc, ldc, V16, WT16, W16, dV, dU16, B);
-  else { fbn_set_error("fbn_bilinear_bwd: D must be 64 or 128"); return FBN_ERR_UNSUPPORTED; }
+#define FBN_BILINEAR_BWD(DD, NTH)                                                                              \
+  if (dc_bf16)                                                                                               \
+    hipLaunchKernelGGL((bilinear_bwd_kernel<DD, true>), grid, dim3(NTH), 0, st, dc, ldc, V16, WT16, W16, dV, dU16, B); \
+  else                                                                                                       \
+    hipLaunchKernelGGL((bilinear_bwd_kernel<DD, false>), grid, dim3(NTH), 0, st, dc, ldc, V16, WT16, W16, dV, dU16, B)
+  switch (D) {
+    case 128: FBN_BILINEAR_BWD(128, 256); break;
+    case 64: FBN_BILINEAR_BWD(64, 128); break;
+    case 32: FBN_BILINEAR_BWD(32, 64); break;
+    case 16: FBN_BILINEAR_BWD(16, 64); break;
+    default: fbn_set_error("fbn_bilinear_bwd: D must be 16, 32, 64 or 128"); return FBN_ERR_UNSUPPORTED;
+  }
+#undef FBN_BILINEAR_BWD
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

@@ -155,6 +155,32 @@ struct TileLoader {
       }
     }
   }
+
+  // split-bf16: x = hi + lo with hi = bf16(x), lo = bf16(x - hi); the hi tile at S, the lo tile at
+  // S + PLANE (fp32 operands of the split-bf16 x3 GEMM)
+  template <int LDK, int PLANE>
+  __device__ __forceinline__ void store_split(short* __restrict__ S) const {
+    auto put = [&](short* dst, float a, float b, float c, float d) {
+      const short ha = f2bf(a), hb = f2bf(b), hc = f2bf(c), hd = f2bf(d);
+      *reinterpret_cast<bf16x4*>(dst) = (bf16x4){ha, hb, hc, hd};
+      *reinterpret_cast<bf16x4*>(dst + PLANE) =
+          (bf16x4){f2bf(a - bf2f(ha)), f2bf(b - bf2f(hb)), f2bf(c - bf2f(hc)), f2bf(d - bf2f(hd))};
+    };
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      if (UNITS < 256 && c >= UNITS) continue;
+      if (KC) {
+        const int r = c / (BK / 4), kk = (c % (BK / 4)) * 4;
+        put(S + r * LDK + kk, v[i][0], v[i][1], v[i][2], v[i][3]);
+      } else {
+        const int r = (c % (ROWS / 4)) * 4, kk = (c / (ROWS / 4)) * 4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          put(S + (r + e) * LDK + kk, v[i * 4 + 0][e], v[i * 4 + 1][e], v[i * 4 + 2][e], v[i * 4 + 3][e]);
+      }
+    }
+  }
 };
 
 // bf16-source variant (bf16 compute only; no remap: the host passes compacted operands).
@@ -241,6 +267,9 @@ template <int ROWS, int BK, bool KC, bool MAP> struct OpLoader<ROWS, BK, KC, MAP
     t.load(reinterpret_cast<const float*>(P), ld, row0, nrows, k0, kend, rm);
   }
   template <typename T, int LDK> __device__ __forceinline__ void store(T* S) const { t.template store<T, LDK>(S); }
+  template <int LDK, int PLANE> __device__ __forceinline__ void store_split(short* S) const {
+    t.template store_split<LDK, PLANE>(S);
+  }
 };
 template <int ROWS, int BK, bool KC, bool MAP> struct OpLoader<ROWS, BK, KC, MAP, true> {
   TileLoaderBf16<ROWS, BK, KC> t;
@@ -399,15 +428,23 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[T
   }
 }
 
-template <int BM, int BN, bool TA, bool TB, bool BF16, bool A16, bool B16>
+// SPLIT (BF16, fp32 operands in memory): split-bf16 x3 -- each operand tile is staged in LDS as a hi
+// and a lo bf16 plane (x = hi + lo to ~16 mantissa bits) and C += Ahi Bhi + Ahi Blo + Alo Bhi on the
+// bf16 MFMA with fp32 accumulation: the fp32 GEMMs of the bf16-forward / fp32-backward mode at
+// three bf16 MFMA passes instead of the 8x slower fp32 MFMA (the dropped Alo Blo term is 2^-16
+// relative).
+template <int BM, int BN, bool TA, bool TB, bool BF16, bool A16, bool B16, bool SPLIT = false>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int remap_xcd) {
   FBN_MAIN_PRIO();
   typedef GemmTraits<BF16> Tr;
   typedef typename Tr::T T;
-  constexpr int BK = Tr::BK, LDK = Tr::LDK;
+  static_assert(!SPLIT || (BF16 && !A16 && !B16), "split-bf16 stages fp32 operands");
+  // split: K tiles of 32 (two LDS planes per operand at half the depth: the LDS of a plain bf16 tile)
+  constexpr int BK = SPLIT ? 32 : Tr::BK, LDK = SPLIT ? 40 : Tr::LDK;
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
-  __shared__ __attribute__((aligned(16))) T sA[2][BM * LDK];
-  __shared__ __attribute__((aligned(16))) T sB[2][BN * LDK];
+  constexpr int PL = SPLIT ? 2 : 1;                 // LDS planes per operand tile (hi, lo)
+  __shared__ __attribute__((aligned(16))) T sA[2][PL * BM * LDK];
+  __shared__ __attribute__((aligned(16))) T sB[2][PL * BN * LDK];
 
   // XCD-aware tile order: dispatch deals blocks round-robin over 8 XCDs, so block b runs on
   // XCD b % 8; give each XCD a contiguous run of tiles (neighbours share the A row panel).
@@ -436,11 +473,19 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
+  auto stage = [&](int b) {
+    if constexpr (SPLIT) {
+      la.template store_split<LDK, BM * LDK>(reinterpret_cast<short*>(sA[b]));
+      lb.template store_split<LDK, BN * LDK>(reinterpret_cast<short*>(sB[b]));
+    } else {
+      la.template store<T, LDK>(sA[b]);
+      lb.template store<T, LDK>(sB[b]);
+    }
+  };
   if (ntiles > 0) {
     la.load(g.A, g.lda, m0, g.M, kbeg, kend, none);
     lb.load(g.B, g.ldb, n0, g.N, kbeg, kend, g.rB);
-    la.template store<T, LDK>(sA[0]);
-    lb.template store<T, LDK>(sB[0]);
+    stage(0);
   }
   __syncthreads();
 
@@ -488,12 +533,25 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g, int tiles_n, int 
 #pragma unroll
           for (int j = 0; j < TN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        if constexpr (SPLIT) {
+          bf16x8 al[TM], bl[TN];
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            al[i] = *reinterpret_cast<const bf16x8*>(A_ + BM * LDK + (wm * WM + i * 32 + lr) * LDK + s * 16 + lh * 8);
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            bl[j] = *reinterpret_cast<const bf16x8*>(B_ + BN * LDK + (wn * WN + j * 32 + lr) * LDK + s * 16 + lh * 8);
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bl[j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bfr[j], acc[i][j], 0, 0, 0);
+            }
+        }
       }
     }
-    if (more) {
-      la.template store<T, LDK>(sA[buf ^ 1]);
-      lb.template store<T, LDK>(sB[buf ^ 1]);
-    }
+    if (more) stage(buf ^ 1);
     __syncthreads();
   }
 
@@ -910,12 +968,12 @@ static int slab_split(int M, int N, int K) {
   return K > 0 ? fbn_cdiv(K, per) : 1;
 }
 
-template <int BM, int BN, bool TA, bool TB, bool BF16, bool A16, bool B16>
+template <int BM, int BN, bool TA, bool TB, bool BF16, bool A16, bool B16, bool SPLIT = false>
 static void launch_tile(const GemmArgs& g, int nsplit, hipStream_t st) {
   const int tn = fbn_cdiv(g.N, BN), tm = fbn_cdiv(g.M, BM);
   const int nb = tn * tm;
   dim3 grid(nb, 1, nsplit);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, TA, TB, BF16, A16, B16>), grid, dim3(256), 0, st, g, tn,
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, TA, TB, BF16, A16, B16, SPLIT>), grid, dim3(256), 0, st, g, tn,
                      (nb % 8 == 0) ? 1 : 0);
 }
 
@@ -959,8 +1017,17 @@ static void launch_sel(const GemmArgs& g, const GemmPlan& p, hipStream_t st) {
 }
 
 template <bool TA, bool TB>
+static void launch_split(const GemmArgs& g, const GemmPlan& p, hipStream_t st) {
+  if (p.bm == 128 && p.bn == 128) launch_tile<128, 128, TA, TB, true, false, false, true>(g, p.split, st);
+  else if (p.bm == 128) launch_tile<128, 64, TA, TB, true, false, false, true>(g, p.split, st);
+  else if (p.bn == 128) launch_tile<64, 128, TA, TB, true, false, false, true>(g, p.split, st);
+  else launch_tile<64, 64, TA, TB, true, false, false, true>(g, p.split, st);
+}
+
+template <bool TA, bool TB>
 static void launch_types(const GemmArgs& g, const GemmPlan& p, int bf16, int a16, int b16, hipStream_t st) {
-  if (!bf16) launch_sel<TA, TB, false, false, false>(g, p, st);
+  if (bf16 == 2) launch_split<TA, TB>(g, p, st);
+  else if (!bf16) launch_sel<TA, TB, false, false, false>(g, p, st);
   else if (a16 && b16) launch_sel<TA, TB, true, true, true>(g, p, st);
   else if (a16) launch_sel<TA, TB, true, true, false>(g, p, st);
   else if (b16) launch_sel<TA, TB, true, false, true>(g, p, st);
@@ -969,7 +1036,7 @@ static void launch_types(const GemmArgs& g, const GemmPlan& p, int bf16, int a16
 
 // upper bound over both kernels' plans (the caller does not say whether the DMA path applies)
 extern "C" size_t fbn_gemm_workspace_size(int M, int N, int K, int bf16) {
-  GemmPlan p = plan_gemm(M, N, K, bf16 ? 64 : 32);
+  GemmPlan p = plan_gemm(M, N, K, bf16 == 1 ? 64 : 32);
   if (bf16) {
     const GemmPlan q = plan_dma16(M, N, K);
     if (q.split > p.split) p = q;
@@ -1163,6 +1230,10 @@ static int gemm_impl(const void* A, const void* B, float* C, const float* bias, 
     fbn_set_error("fbn_gemm: bf16 operands need bf16 compute, ld % 8 == 0 and no B remap");
     return FBN_ERR_ARG;
   }
+  if (bf16 == 2 && (a16 || b16 || A2 || B2 || c16 || bnb)) {
+    fbn_set_error("fbn_gemm: split-bf16 (bf16 = 2) takes fp32 operands only");
+    return FBN_ERR_ARG;
+  }
   GemmArgs g;
   g.A = A; g.B = B; g.C = C; g.bias = bias;
   g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = ldc;
@@ -1178,7 +1249,7 @@ static int gemm_impl(const void* A, const void* B, float* C, const float* bias, 
   g.bnb_scale = bnb ? bnb->bnb_scale : 1.f;
   g.bnb_part = bnb ? bnb->bnb_part : nullptr;
   g.bnb_rpc = bnb ? bnb->bnb_rpc : 1;
-  const int bk = bf16 ? 64 : 32;
+  const int bk = bf16 == 1 ? 64 : 32;     // fp32 and split-bf16 (bf16 = 2) tiles are 32 deep
   // LDS-DMA path: bf16 operands, K % 64 == 0, 16-B rows; k-major operands need their
   // M / N extent in whole 8-element chunks
   const bool dma16 = bf16 && a16 && b16 && rB_seg == 0x7fffffff && K % 64 == 0 && !(lda & 7) && !(ldb & 7) &&

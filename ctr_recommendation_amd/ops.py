@@ -35,6 +35,8 @@ BN_MOMENTUM = 0.1
 
 # the trainer's BN2 backward first pass inside the forward head kernel (A/B knob)
 _BN2_BWD_IN_FWD = os.environ.get("FBN_BN2_BWD_IN_FWD", "1") == "1"
+# bf16_fwd: the backward's fp32 GEMMs as split-bf16 x3 (fbn_gemm bf16 = 2) with FBN_SPLIT_BWD=1 (A/B knob)
+_SPLIT_BWD = os.environ.get("FBN_SPLIT_BWD", "0") == "1"
 # bf16, one process: the BN1 backward first pass inside the epilogue of its dgrad GEMM (A/B knob)
 _BN1_BWD_IN_GEMM = os.environ.get("FBN_BN1_BWD_IN_GEMM", "1") == "1"
 
@@ -647,6 +649,9 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
             a["bwd_" + name] = t
         return t
 
+    # bf16_fwd: the fp32 gradient GEMMs as split-bf16 x3 on the bf16 MFMA (fbn_gemm bf16 = 2;
+    # FBN_SPLIT_BWD=0: fp32 MFMA)
+    sb = 2 if (cfg.fwd16 and _SPLIT_BWD) else False
     dh2pre = None if lean else tmp("dh2pre", (B, H2))
     dh2pre16 = tmp("dh2pre16", (B, H2), torch.bfloat16) if bf else None
     sums = DeferredSums(a)
@@ -674,8 +679,9 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
         else:
             gemm(dh2pre16, w16["WbT"], dh1, B, H1, H2, H2, H2, H1, False, True, stream=st)
     else:
-        wg.run(lambda s: gemm(dh2pre, a["h1"], g["mlp.4.weight"], H2, H1, B, H2, H1, H1, True, False, stream=s))
-        gemm(dh2pre, p["mlp.4.weight"], dh1, B, H1, H2, H2, H1, H1, False, False, stream=st)
+        wg.run(lambda s: gemm(dh2pre, a["h1"], g["mlp.4.weight"], H2, H1, B, H2, H1, H1, True, False, bf16=sb,
+                              stream=s))
+        gemm(dh2pre, p["mlp.4.weight"], dh1, B, H1, H2, H2, H1, H1, False, False, bf16=sb, stream=st)
     dh1pre = None if lean else tmp("dh1pre", (B, H1))
     dh1pre16 = tmp("dh1pre16", (B, H1), torch.bfloat16) if bf else None
     bn_backward(dh1, None, None, None if lean_h1 else a["h1"], scale, a["h1pre"], a["mean1"], a["inv1"],
@@ -689,11 +695,15 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
             wg.run(lambda s: gemm_split(dh1pre16, a["Vc16"], g["mlp.0.weight"], H1, KC, B, H1, 5 * d, 21 * d, True,
                                         False, rC=wa_remap(d), stream=s, B2=a["c"][:, 5 * d:], ldb2=KC, nseg=5 * d))
     elif bf:
-        wg.run(lambda s: gemm(dh1pre16, a["c"], g["mlp.0.weight"], H1, KC, B, H1, KC, 21 * d, True, False,
-                              rC=wa_remap(d), stream=s))
+        # (d < 128: the MLP input c is one bf16 operand) slabs in the step's grouped launch when the
+        # shape allows, else a launch of its own with its split-K reduce
+        if not sums.gemm_slabs(dh1pre16, a["c"], g["mlp.0.weight"], H1, KC, B, H1, KC, 21 * d, True, False,
+                               rC=wa_remap(d), stream=st):
+            wg.run(lambda s: gemm(dh1pre16, a["c"], g["mlp.0.weight"], H1, KC, B, H1, KC, 21 * d, True, False,
+                                  rC=wa_remap(d), stream=s))
     else:
         wg.run(lambda s: gemm(dh1pre, a["c"], g["mlp.0.weight"], H1, KC, B, H1, KC, 21 * d, True, False,
-                              rC=wa_remap(d), stream=s))
+                              rC=wa_remap(d), bf16=sb, stream=s))
     if a.get("fused_bilinear"):
         # dc in bf16: its one reader, the fused bilinear backward, widens it on load
         dc = tmp("dc16", (B, KC), torch.bfloat16)
@@ -703,7 +713,8 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
         gemm(dh1pre16, w16["WaT"], dc, B, KC, H1, H1, H1, KC, False, True, stream=st)
     else:
         dc = torch.empty((B, KC), **f32)
-        gemm(dh1pre, p["mlp.0.weight"], dc, B, KC, H1, H1, 21 * d, KC, False, False, rB=wa_remap(d), stream=st)
+        gemm(dh1pre, p["mlp.0.weight"], dc, B, KC, H1, H1, 21 * d, KC, False, False, rB=wa_remap(d), bf16=sb,
+             stream=st)
     # bilinear backward
     dV = tmp("dV", (B, 5, d))
     v16 = bf and not cfg.bilinear_each
@@ -722,11 +733,13 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
         pass
     elif not cfg.bilinear_each:
         if bf:
-            wg.run(lambda s: gemm(a["Vc16"], dU16, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=s))
+            if not sums.gemm_slabs(a["Vc16"], dU16, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=st):
+                wg.run(lambda s: gemm(a["Vc16"], dU16, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=s))
             gemm(dU16, w16["W"], dV, 5 * B, d, d, d, d, d, False, True, beta=1.0, stream=st)
         else:
-            wg.run(lambda s: gemm(a["Vc"], dU, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=s))
-            gemm(dU, p["bilinear.W"], dV, 5 * B, d, d, d, d, d, False, True, beta=1.0, stream=st)
+            wg.run(lambda s: gemm(a["Vc"], dU, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, bf16=sb,
+                                  stream=s))
+            gemm(dU, p["bilinear.W"], dV, 5 * B, d, d, d, d, d, False, True, beta=1.0, bf16=sb, stream=st)
     else:
         g["bilinear.W_list.0"].zero_()
         for f in range(1, 5):
@@ -781,7 +794,7 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
                                   stream=s))
     else:
         wg.run(lambda s: gemm(dhmm, batch["item_emb_d128"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True,
-                              False, stream=s))
+                              False, bf16=sb, stream=s))
     for job in extra_sums:              # e.g. the trainer's mean loss
         sums.add(*job)
     if hooks and "before_flush" in hooks:         # trainer: join the early weight-gradient launch

@@ -46,6 +46,9 @@ int fbn_device_ok(void); /* 1 if the current HIP device is gfx950 */
  * and all of their autograd backward GEMMs.  Split-K slabs need ws >= fbn_gemm_workspace_size. */
 size_t fbn_gemm_workspace_size(int M, int N, int K, int bf16);
 /* a16 / b16: operand A / B is bf16 in memory (bf16 = 1, ld % 8 == 0, no rB remap); otherwise fp32.
+ * bf16 = 2: split-bf16 x3 over fp32 operands (a16 = b16 = 0): each operand x = hi + lo, hi = bf16(x),
+ * lo = bf16(x - hi), and C = Ahi Bhi + Ahi Blo + Alo Bhi on the bf16 MFMA with fp32 accumulation
+ * (~2^-16 relative per product) -- the fp32-gradient GEMMs of the bf16-forward mode.
  * stats (optional): [ceil(M/64)][N][2] per-64-row-tile column (sum, M2) of C for the fused
  * BatchNorm statistics, from the MFMA epilogue (no split-K: 64-row tiles) or the split-K reduce;
  * C is bit-identical with or without it. */

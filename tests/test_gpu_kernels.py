@@ -82,6 +82,32 @@ def test_gemm_bf16_all_layouts(hip_device, transA, transB, M, N, K):
     assert err < 2e-5 * K ** 0.5 * 4, err
 
 
+@pytest.mark.parametrize("transA,transB", [(False, True), (False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(8192, 1920, 512), (512, 1920, 8192), (200, 136, 256), (128, 128, 40960),
+                                   (1000, 72, 100)])
+def test_gemm_split_bf16x3(hip_device, transA, transB, M, N, K):
+    """fbn_gemm bf16 = 2 (split-bf16 x3 over fp32 operands, the bf16_fwd backward's GEMMs) against
+    float64: ~2^-16 relative per product (the dropped lo x lo term and the lo rounding), so the
+    error bar is 4e-5 x sqrt(K) x |a||b| -- 100x tighter than a plain bf16 GEMM on the same fp32
+    inputs (checked beside it), and within 30x of the fp32 MFMA GEMM's."""
+    g = torch.Generator(device="cpu").manual_seed(5)
+    A = torch.randn((K, M) if transA else (M, K), generator=g).to(hip_device)
+    Bm = torch.randn((N, K) if transB else (K, N), generator=g).to(hip_device)
+    lda = M if transA else K
+    ldb = K if transB else N
+    a = A.double().T if transA else A.double()
+    b = Bm.double().T if transB else Bm.double()
+    ref = a @ b
+    errs = {}
+    for mode in (2, True, False):
+        C = torch.full((M, N), float("nan"), device=hip_device)
+        ops.gemm(A, Bm, C, M, N, K, lda, ldb, N, transA, transB, bf16=mode)
+        errs[mode] = (C.double() - ref).abs().max().item()
+    assert errs[2] < 4e-5 * K ** 0.5, errs
+    assert errs[2] * 20 < errs[True], errs            # far better than bf16 operands
+    assert errs[2] < 30 * errs[False] + 1e-6, errs    # near fp32
+
+
 @pytest.mark.parametrize("M,N,K,remap", [(256, 512, 8192, False), (512, 1920, 8192, True), (128, 128, 40960, False),
                                           (16, 16, 20480, False), (128, 128, 8192, False)])
 def test_gemm_slabs_deferred_sum(hip_device, M, N, K, remap):
@@ -138,13 +164,14 @@ def test_table_adam_step_vs_ieee(hip_device):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("d,B,dc16", [(128, 8192, 1), (128, 8192, 0), (128, 100, 1), (64, 333, 0)])
+@pytest.mark.parametrize("d,B,dc16", [(128, 8192, 1), (128, 8192, 0), (128, 100, 1), (64, 333, 0), (32, 1000, 1),
+                                      (16, 4096, 1), (16, 333, 0)])
 def test_fused_bilinear_matches_unfused_math(hip_device, d, B, dc16):
     """fbn_bilinear_fwd / _bwd (one MFMA + pair-product launch each way, U never stored) against
     the same arithmetic in torch on the same bf16 operands: pairs and dU16 within 1 bf16 ulp (U's
     f32 sums may round differently), dV within 2e-5 x max|dV|.  B = 100 / 333: a partial last
     tile of samples.  dc16: the incoming gradient dc in bf16 (fbn_gemm_bf16out's output, the
-    trainer's bf16 mode) or f32."""
+    trainer's bf16 mode) or f32.  d = 16 (config C2): one wave per 16 samples on the 16x16x16 MFMA."""
     from ctr_recommendation_amd import _lib
     g = torch.Generator(device=hip_device).manual_seed(3)
     V16 = (torch.randn((B, 5, d), generator=g, device=hip_device) * 0.5).to(torch.bfloat16)

@@ -20,4 +20,7 @@ timeout -k 10 400 python $R/bench.py --rows-per-gpu 12500000 --no-cpu-baseline -
 rc=$?; echo "c5 rc=$rc $(grep -o '"ms_per_step": [0-9.]*' $OUT/c5.json | head -1)"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python $R/bench.py --rows-per-gpu 12500000 --table-adam sparse --no-cpu-baseline --no-fp32 --no-inference \
   > $OUT/c5s.json 2> $OUT/c5s.err
-rc=$?; echo "c5 sparse rc=$rc $(grep -o '"ms_per_step": [0-9.]*' $OUT/c5s.json | head -1)"; exit $rc
+rc=$?; echo "c5 sparse rc=$rc $(grep -o '"ms_per_step": [0-9.]*' $OUT/c5s.json | head -1)"; [ $rc -eq 0 ] || exit $rc
+FBN_BENCH_SHARD=1 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29541 timeout -k 10 400 \
+  python $R/bench.py --no-cpu-baseline --no-fp32 --no-inference --no-cpu-plan > $OUT/shard.json 2> $OUT/shard.err
+rc=$?; echo "shard rc=$rc $(grep -o '"ms_per_step": [0-9.]*' $OUT/shard.json | head -1)"; exit $rc
