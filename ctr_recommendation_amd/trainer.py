@@ -60,7 +60,7 @@ _SIDE_AFTER_MMPROJ = os.environ.get("FBN_SIDE_AFTER_MMPROJ", "0") == "1"
 # FBN_SIDE_SERIAL defaults to "auto": in sequence on the main stream below d = 128, where the side
 # work is small and the cross-queue edges cost more than the overlap saves (C2, graph-replayed:
 # 0.2833-0.2844 vs 0.2934-0.2952 ms/step; eager 0.30 vs 0.45-0.50, the host's event waits gone;
-# profiles/r03s2_side_serial_ab.txt), on the side stream from d = 128 on
+# profiles/r03s2_side_serial_ab.txt), on the side stream from d = 128 on and in step programs
 _CLAIM_ON_SIDE = os.environ.get("FBN_CLAIM_ON_SIDE", "0") == "1"
 # single GPU, lazy table Adam, images on main: the bf16 image conversion rides in the row claims'
 # launch (FBN_HEAD_CONV=0: its own launch ahead of the claims, A/B)
@@ -408,6 +408,7 @@ class FiBiNETTrainer:
         self._sg_eager = 0
         self._bn_synced_at = -1     # host step of the last rank-0 BatchNorm broadcast (_bn_from_rank0)
         self._used_pre = False      # the last step took its row claims from the prefetch's pre-claims
+        self._recording = False     # inside record_program()
 
     # ------------------------------------------------------------------ one training step
     def step(self, batch: Dict[str, torch.Tensor], labels: torch.Tensor,
@@ -504,7 +505,10 @@ class FiBiNETTrainer:
             side_pass()
 
         def side_pass(wait_main=True):
-            serial = self.side_serial
+            # a step being recorded as a step program runs its side passes on the side stream at every
+            # d: replayed natively, the two edges cost less than the overlap saves (C2: 0.2071-0.2082
+            # vs 0.2176-0.2190 ms/step, profiles/r04_c2_stream_placement.txt)
+            serial = self.side_serial and not (self._recording and _SIDE_SERIAL == "auto")
             sst = self.side if not serial else main      # in sequence on main (FBN_SIDE_SERIAL)
             if wait_main and not serial:
                 _lib.wait_stream(self.side, main)
@@ -802,8 +806,12 @@ class FiBiNETTrainer:
         key = _batch_key(batch["item_id"], seq if seq is not None and seq.shape[1] else None)
         prog = _lib.StepProgram(self.device)
         self._used_pre = False
-        with prog.recording(pool):
-            self.step(batch, labels, next_batch=next_batch)
+        self._recording = True
+        try:
+            with prog.recording(pool):
+                self.step(batch, labels, next_batch=next_batch)
+        finally:
+            self._recording = False
         # the claims of the recorded step came from the pre-claims the previous step posted for this
         # very batch (a replay is valid only after such a step), and the step posted its next batch's
         prog.pre_needed, prog.batch_key, prog.pre_key_after = self._used_pre, key, self._pre_key

@@ -2,8 +2,9 @@
 host call must be bit-identical to running the step eagerly (src/train_fibinet.py:113-123's loop
 body), in every mode the bench times -- bf16 at d 128 (two streams, the next-batch prefetch, the
 duplicate fold on the side stream), fp32 at d 128 (per-step temporaries from the program's private
-memory pool), d 16 (the side passes in sequence on the main stream) -- and when replays interleave
-with eager steps (the bench's probe steps run eagerly between replays)."""
+memory pool), d 16 (eager steps run the side passes in sequence on the main stream, a recorded step
+on the side stream: the replays must still match the eager run bit for bit) -- and when replays
+interleave with eager steps (the bench's probe steps run eagerly between replays)."""
 import pytest
 import torch
 
@@ -31,7 +32,7 @@ def _unique_ids(b, V, g, pool):
 
 
 @pytest.mark.parametrize("d,dtype,det", [(128, "bf16", False), (128, "fp32", False), (16, "fp32", False),
-                                         (128, "bf16_fwd", False), (128, "bf16", True)])
+                                         (16, "bf16", False), (128, "bf16_fwd", False), (128, "bf16", True)])
 def test_program_replay_bit_identical_to_eager(hip_device, d, dtype, det):
     """det=False: the bench's stream structure (duplicate fold on the side stream, float atomics),
     ids unique within a batch; det=True: deterministic mode (fixed-point fold on the main stream)
