@@ -12,7 +12,9 @@ per-GPU table shard are fixed as N grows.
 
 One JSON line on rank 0 with the contract keys plus
   roofline:      the dominant kernel of the step (largest average launch time among the probed
-                 ones), HIP events around its launches inside an eager probe pass (same stream),
+                 ones), its launches timed by their own start / end events inside an eager probe
+                 pass (the library launches every kernel with hipExtLaunchKernelGGL; armed per call
+                 by _lib.KernelProbe: the kernel span rocprofv3 reports, no marker packets around it),
                  algorithmic work per launch (bytes or FLOPs) / that time, against the HBM or
                  MFMA peak; traffic = PMC-measured HBM bytes per launch when committed;
   rooflines:     the same for every probed kernel (gather, lazy table-Adam catch-up, MLP GEMM),
@@ -169,6 +171,15 @@ def cpu_baseline_plan(args):
     return out
 
 
+def _mean_ms(pairs) -> float:
+    """Mean kernel span (ms) of a probe list: _lib.KernelProbe entries (the library's kernels, timed by
+    their own start / end events: what rocprofv3 reports) or torch event pairs; probes whose call
+    launched nothing are skipped."""
+    vals = [a.elapsed_time(e) for a, e in pairs]
+    vals = [v for v in vals if v >= 0]
+    return sum(vals) / len(vals) if vals else 0.0
+
+
 def inference_leg(args, dev, dtype):
     """Inference throughput (SURVEY 6's other derived figure, src/Prediction.py:95-113): the drop-in
     MM_FiBiNET in eval mode, batch 8192, d = 128, `model(batch_dict)` then `y_pred.cpu()` per batch --
@@ -208,8 +219,7 @@ def inference_leg(args, dev, dtype):
             torch.cuda._sleep(2_000_000)
             ops.forward(p, xs[j % nb], cfg, None, probe=probe)
     torch.cuda.synchronize()
-    ev = probe["fields_fwd"][2:]
-    ms = sum(a.elapsed_time(e) for a, e in ev) / len(ev)
+    ms = _mean_ms(probe["fields_fwd"][2:])
     work = gather_bytes_per_sample(d) * B
     ach = work / (ms * 1e-3) / 1e9
     out = {"value": round(n * B / dt, 1), "unit": "samples/s", "ms_per_batch": round(dt / n * 1e3, 4),
@@ -398,13 +408,13 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
     # ahead (fbn_adam_prefetch_rows), so the claimed-row catch-up replays only the stale ones too
     owner_pf = bool(getattr(tr, "prefetch_owner", False)) and tr.xchg is not None
 
-    # ---- probe pass: eager steps with HIP events around the dominant kernels (same stream)
+    # ---- probe pass: eager steps with the dominant kernels' spans probed (_lib.KernelProbe)
     probe = {}
     for _ in range(args.probe_steps):
         b, y = batches[i % nb]
         i += 1
-        # a ~10 ms spin ahead of the step keeps the GPU behind the host's launches, so each event
-        # pair brackets only its kernel (as in the graph replays), not host enqueue gaps; the
+        # a ~10 ms spin ahead of the step keeps the GPU behind the host's launches, so the step's
+        # kernels run back to back as in the timed replays, not at the host's pace; the
         # HBM-resident batches themselves are passed (as in the graphs), so the next-batch
         # prefetch's claims are taken up exactly as in the timed replays
         torch.cuda._sleep(20_000_000)
@@ -437,8 +447,7 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
     def avg_ms(name, src=None):
         # the first two launches of an explicit source (the eval-mode forwards, the serialised probe
         # steps) carry first-iteration warm-up; the in-step probe follows the timed steps (warm)
-        ev = (probe if src is None else src).get(name, [])[2 if src is not None else 0:]
-        return sum(a.elapsed_time(e) for a, e in ev) / max(1, len(ev))
+        return _mean_ms((probe if src is None else src).get(name, [])[2 if src is not None else 0:])
 
     touched = int(uniq.numel())
     if world > 1:

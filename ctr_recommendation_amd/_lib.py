@@ -127,6 +127,9 @@ SIGNATURES = {
     "fbn_plan_add_record": (I, [P, I, P]),
     "fbn_plan_add_wait": (I, [P, P, I]),
     "fbn_plan_run": (I, [P, P]),
+    "fbn_probe_arm": (I, [I]),
+    "fbn_probe_disarm": (I, []),
+    "fbn_probe_elapsed": (F, [I]),
     "fbn_comm_load": (I, [ctypes.c_char_p]),
     "fbn_comm_id_bytes": (I, []),
     "fbn_comm_unique_id": (I, [P]),
@@ -157,7 +160,7 @@ def lib() -> ctypes.CDLL:
 
 
 _fns = {}
-_UNCHECKED = ("fbn_version", "fbn_device_ok")
+_UNCHECKED = ("fbn_version", "fbn_device_ok", "fbn_probe_disarm", "fbn_probe_elapsed")
 _tls = threading.local()           # .prog: the StepProgram recording on this thread (or None)
 
 
@@ -247,6 +250,27 @@ def _f32_in_f64(x: float) -> float:
     """The double whose low 32 bits are the float32 bits of x (a float argument in an xmm register)."""
     bits = struct.unpack("<I", struct.pack("<f", x))[0]
     return struct.unpack("<d", struct.pack("<Q", bits))[0]
+
+
+class KernelProbe:
+    """The kernels of one entry-point call, timed on the device (bench.py's rooflines): construct it
+    right before the call (fbn_probe_arm), done() right after (fbn_probe_disarm); elapsed_time() is
+    the span from the first kernel's start to the last one's end, as rocprofv3 sees them (the
+    library launches every kernel with hipExtLaunchKernelGGL and the probe's event pair), or -1 when
+    the call launched nothing.  Same interface as a torch.cuda.Event pair's start.elapsed_time(end)."""
+    _next = 0
+
+    def __init__(self):
+        self.slot = KernelProbe._next
+        KernelProbe._next += 1
+        self.taken = False
+        call_raw("fbn_probe_arm", self.slot)
+
+    def done(self) -> None:
+        self.taken = bool(lib().fbn_probe_disarm())
+
+    def elapsed_time(self, _end=None) -> float:
+        return float(lib().fbn_probe_elapsed(self.slot)) if self.taken else -1.0
 
 
 class StepProgram:

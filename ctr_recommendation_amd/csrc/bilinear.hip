@@ -251,10 +251,10 @@ extern "C" int fbn_bilinear_fwd(const short* V16, const short* WT16, short* c, i
   const dim3 grid((unsigned)((B + TS - 1) / TS));
   hipStream_t st = (hipStream_t)stream;
   switch (D) {
-    case 128: hipLaunchKernelGGL(bilinear_fwd_kernel<128>, grid, dim3(256), 0, st, V16, WT16, c, B, ldc); break;
-    case 64: hipLaunchKernelGGL(bilinear_fwd_kernel<64>, grid, dim3(128), 0, st, V16, WT16, c, B, ldc); break;
-    case 32: hipLaunchKernelGGL(bilinear_fwd_kernel<32>, grid, dim3(64), 0, st, V16, WT16, c, B, ldc); break;
-    case 16: hipLaunchKernelGGL(bilinear_fwd_kernel<16>, grid, dim3(64), 0, st, V16, WT16, c, B, ldc); break;
+    case 128: fbn_launch(bilinear_fwd_kernel<128>, grid, dim3(256), 0, st, V16, WT16, c, B, ldc); break;
+    case 64: fbn_launch(bilinear_fwd_kernel<64>, grid, dim3(128), 0, st, V16, WT16, c, B, ldc); break;
+    case 32: fbn_launch(bilinear_fwd_kernel<32>, grid, dim3(64), 0, st, V16, WT16, c, B, ldc); break;
+    case 16: fbn_launch(bilinear_fwd_kernel<16>, grid, dim3(64), 0, st, V16, WT16, c, B, ldc); break;
     default: fbn_set_error("fbn_bilinear_fwd: D must be 16, 32, 64 or 128"); return FBN_ERR_UNSUPPORTED;
   }
   FBN_CHECK_LAUNCH();
@@ -274,9 +274,9 @@ extern "C" int fbn_bilinear_bwd(const void* dc, int ldc, int dc_bf16, const shor
   if (!dc_bf16 && ((uintptr_t)dc & 15)) { fbn_set_error("fbn_bilinear_bwd: f32 dc must be 16-B aligned"); return FBN_ERR_ARG; }
 #define FBN_BILINEAR_BWD(DD, NTH)                                                                              \
   if (dc_bf16)                                                                                               \
-    hipLaunchKernelGGL((bilinear_bwd_kernel<DD, true>), grid, dim3(NTH), 0, st, dc, ldc, V16, WT16, W16, dV, dU16, B); \
+    fbn_launch((bilinear_bwd_kernel<DD, true>), grid, dim3(NTH), 0, st, dc, ldc, V16, WT16, W16, dV, dU16, B); \
   else                                                                                                       \
-    hipLaunchKernelGGL((bilinear_bwd_kernel<DD, false>), grid, dim3(NTH), 0, st, dc, ldc, V16, WT16, W16, dV, dU16, B)
+    fbn_launch((bilinear_bwd_kernel<DD, false>), grid, dim3(NTH), 0, st, dc, ldc, V16, WT16, W16, dV, dU16, B)
   switch (D) {
     case 128: FBN_BILINEAR_BWD(128, 256); break;
     case 64: FBN_BILINEAR_BWD(64, 128); break;

@@ -109,7 +109,7 @@ extern "C" int fbn_collate(const int64_t* perm, int B, const int64_t* item, cons
   CollateArgs a{perm, B, item, seq, Ls, L, Ls - L, likes, views, user, label, slot_of_id, n_ids, sorted_ids, emb, E,
                 o_item, o_seq, o_likes, o_views, o_user, o_label, o_emb, missing};
   const int blocks = (int)std::min<long long>(2048, ((long long)B + 3) / 4);
-  hipLaunchKernelGGL(collate_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
+  fbn_launch(collate_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -118,7 +118,7 @@ extern "C" int fbn_collate_zero_if(float* x, long long n, const int* flag, void*
   if (n <= 0) return FBN_OK;
   if (!x || !flag) { fbn_set_error("fbn_collate_zero_if: x and flag are required"); return FBN_ERR_ARG; }
   const int blocks = (int)std::min<long long>(1024, (n + 255) / 256);
-  hipLaunchKernelGGL(zero_if_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, n, flag);
+  fbn_launch(zero_if_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, n, flag);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

@@ -1,8 +1,23 @@
 // Shared device helpers for the FiBiNET gfx950 kernels.
 // Wave width is 64 on CDNA4; every cross-lane idiom below assumes it.
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+// Every kernel of the library is launched through fbn_launch: while the host has a probe armed
+// (fbn_probe_arm .. fbn_probe_disarm around one entry-point call, bench.py's roofline timings) the
+// launch records the probe's start event at the first kernel's start and its stop event at every
+// kernel's end (hipExtLaunchKernelGGL): the call's kernel span as rocprofv3 sees it, with no
+// marker packets or dispatch gaps around it.
+bool fbn_probe_take(hipEvent_t* start, hipEvent_t* stop);
+template <typename F, typename... Args>
+inline void fbn_launch(F kernel, const dim3& grid, const dim3& block, unsigned shmem, hipStream_t stream,
+                       Args... args) {
+  hipEvent_t start = nullptr, stop = nullptr;
+  fbn_probe_take(&start, &stop);
+  hipExtLaunchKernelGGL(kernel, grid, block, shmem, stream, start, stop, 0, args...);
+}
 
 #define FBN_WAVE 64
 

@@ -154,7 +154,7 @@ extern "C" int fbn_owner_claim(const int* ids, int n, int* map, int* slot_row, i
   if (n <= 0) return FBN_OK;
   int blocks = (n + 255) / 256;
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(owner_claim_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, ids, n, map, slot_row, rank);
+  fbn_launch(owner_claim_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, ids, n, map, slot_row, rank);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -170,10 +170,10 @@ extern "C" int fbn_route(const int64_t* item, const int64_t* seq, int B, int L, 
   if (blocks < 1) blocks = 1;
   // the count's per-workgroup histograms meet in one global atomic per (workgroup, owner): keep
   // the workgroups few (grid-stride) so the nranks counters see <= 256 atomics each
-  hipLaunchKernelGGL(route_count_kernel, dim3(std::min(blocks, 256)), dim3(256), 0, st, item, L > 0 ? seq : nullptr,
+  fbn_launch(route_count_kernel, dim3(std::min(blocks, 256)), dim3(256), 0, st, item, L > 0 ? seq : nullptr,
                      B, L, V, Vl, nranks, counts, err);
-  hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(1), 0, st, counts, nranks, offsets, cursor);
-  hipLaunchKernelGGL(route_fill_kernel, dim3(blocks), dim3(256), 0, st, item, L > 0 ? seq : nullptr, B, L, V, Vl,
+  fbn_launch(route_scan_kernel, dim3(1), dim3(1), 0, st, counts, nranks, offsets, cursor);
+  fbn_launch(route_fill_kernel, dim3(blocks), dim3(256), 0, st, item, L > 0 ? seq : nullptr, B, L, V, Vl,
                      nranks, offsets, cursor, send_ids, pos);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
@@ -181,11 +181,11 @@ extern "C" int fbn_route(const int64_t* item, const int64_t* seq, int B, int L, 
 
 #define FBN_DISPATCH_D(KERNEL, D, GRID, ...)                                                         \
   switch (D) {                                                                                      \
-    case 16: hipLaunchKernelGGL((KERNEL<16>), GRID, dim3(256), 0, st, __VA_ARGS__); break;          \
-    case 32: hipLaunchKernelGGL((KERNEL<32>), GRID, dim3(256), 0, st, __VA_ARGS__); break;          \
-    case 64: hipLaunchKernelGGL((KERNEL<64>), GRID, dim3(256), 0, st, __VA_ARGS__); break;          \
-    case 128: hipLaunchKernelGGL((KERNEL<128>), GRID, dim3(256), 0, st, __VA_ARGS__); break;        \
-    case 256: hipLaunchKernelGGL((KERNEL<256>), GRID, dim3(256), 0, st, __VA_ARGS__); break;        \
+    case 16: fbn_launch((KERNEL<16>), GRID, dim3(256), 0, st, __VA_ARGS__); break;          \
+    case 32: fbn_launch((KERNEL<32>), GRID, dim3(256), 0, st, __VA_ARGS__); break;          \
+    case 64: fbn_launch((KERNEL<64>), GRID, dim3(256), 0, st, __VA_ARGS__); break;          \
+    case 128: fbn_launch((KERNEL<128>), GRID, dim3(256), 0, st, __VA_ARGS__); break;        \
+    case 256: fbn_launch((KERNEL<256>), GRID, dim3(256), 0, st, __VA_ARGS__); break;        \
     default: fbn_set_error("exchange: D must be 16/32/64/128/256"); return FBN_ERR_UNSUPPORTED;      \
   }
 
@@ -232,7 +232,7 @@ extern "C" int fbn_widen_bf16(const void* in, float* out, long long n, void* str
   const long long n8 = n / 8;
   long long blocks = (n8 + 255) / 256;
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(widen_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+  fbn_launch(widen_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
                      reinterpret_cast<const short*>(in), out, n8);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
@@ -263,7 +263,7 @@ extern "C" int fbn_pad_routes(const int* send_ids, const int* offsets, const int
   if (!send_ids || !offsets || !counts || !out) { fbn_set_error("fbn_pad_routes: null buffer"); return FBN_ERR_ARG; }
   long long blocks = ((long long)world * (cap + 1) + 255) / 256;
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(pad_routes_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, send_ids, offsets,
+  fbn_launch(pad_routes_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, send_ids, offsets,
                      counts, world, cap, out);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
@@ -295,7 +295,7 @@ extern "C" int fbn_compact_routes(const int* padded, int world, int cap, int* id
   if (!padded || !ids || !counts) { fbn_set_error("fbn_compact_routes: null buffer"); return FBN_ERR_ARG; }
   long long blocks = ((long long)world * (cap + 1) + 255) / 256;
   if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(compact_routes_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, padded, world,
+  fbn_launch(compact_routes_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, padded, world,
                      cap, ids, counts);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
@@ -340,7 +340,7 @@ extern "C" int fbn_copy_jobs(const void* const* src, void* const* dst, const lon
   if (J.first[n] <= 0) return FBN_OK;
   long long blocks = (J.first[n] + 255) / 256;
   if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(copy_jobs_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, J, n);
+  fbn_launch(copy_jobs_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, J, n);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

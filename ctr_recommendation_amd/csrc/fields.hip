@@ -663,11 +663,11 @@ static int launch_fields_fwd_hb(const FieldArgs& a, int D, hipStream_t st) {
   // hot staging: fewer, longer-lived workgroups (each stages the hot rows once)
   const int grid = fields_grid(a.B, D, HOT ? 256 : 1024);
   switch (D) {
-    case 16: hipLaunchKernelGGL((fields_fwd_kernel<16, MODE, HCH, BUF, HOT>), dim3(grid), dim3(256), 0, st, a); break;
-    case 32: hipLaunchKernelGGL((fields_fwd_kernel<32, MODE, HCH, BUF, HOT>), dim3(grid), dim3(256), 0, st, a); break;
-    case 64: hipLaunchKernelGGL((fields_fwd_kernel<64, MODE, HCH, BUF, HOT>), dim3(grid), dim3(256), 0, st, a); break;
-    case 128: hipLaunchKernelGGL((fields_fwd_kernel<128, MODE, HCH, BUF, HOT>), dim3(grid), dim3(256), 0, st, a); break;
-    case 256: hipLaunchKernelGGL((fields_fwd_kernel<256, MODE, HCH, BUF, HOT>), dim3(grid), dim3(256), 0, st, a); break;
+    case 16: fbn_launch((fields_fwd_kernel<16, MODE, HCH, BUF, HOT>), dim3(grid), dim3(256), 0, st, a); break;
+    case 32: fbn_launch((fields_fwd_kernel<32, MODE, HCH, BUF, HOT>), dim3(grid), dim3(256), 0, st, a); break;
+    case 64: fbn_launch((fields_fwd_kernel<64, MODE, HCH, BUF, HOT>), dim3(grid), dim3(256), 0, st, a); break;
+    case 128: fbn_launch((fields_fwd_kernel<128, MODE, HCH, BUF, HOT>), dim3(grid), dim3(256), 0, st, a); break;
+    case 256: fbn_launch((fields_fwd_kernel<256, MODE, HCH, BUF, HOT>), dim3(grid), dim3(256), 0, st, a); break;
     default: fbn_set_error("fields: embedding_dim must be one of 16,32,64,128,256"); return FBN_ERR_UNSUPPORTED;
   }
   FBN_CHECK_LAUNCH();
@@ -758,7 +758,7 @@ extern "C" int fbn_hot_rows(const int64_t* item, const int64_t* seq, int B, int 
                             int* hot_n, int H, int tau, int clear, void* stream) {
   const long long n = (long long)B * (L + 1);
   if (n <= 0) return FBN_OK;
-  hipLaunchKernelGGL(hot_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, item,
+  fbn_launch(hot_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, item,
                      L > 0 ? seq : nullptr, B, L, V, cnt, hot, hot_n, H, tau < 1 ? 1 : tau, clear);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
@@ -799,11 +799,11 @@ static int launch_fields_bwd_r(const FieldBwdArgs& a, int D, hipStream_t st) {
   const size_t lds = (4 * (size_t)(13 * a.R + 6 + 3 * D + a.n_cate * D) + 4 * (64 / (D / 4)) * (12 + 2 * RMAX)) *
                      sizeof(float);   // 4 wave slices + SENET staging
   switch (D) {
-    case 16: hipLaunchKernelGGL((fields_bwd_kernel<16, MODE, RMAX>), dim3(grid), dim3(256), lds, st, a); break;
-    case 32: hipLaunchKernelGGL((fields_bwd_kernel<32, MODE, RMAX>), dim3(grid), dim3(256), lds, st, a); break;
-    case 64: hipLaunchKernelGGL((fields_bwd_kernel<64, MODE, RMAX>), dim3(grid), dim3(256), lds, st, a); break;
-    case 128: hipLaunchKernelGGL((fields_bwd_kernel<128, MODE, RMAX>), dim3(grid), dim3(256), lds, st, a); break;
-    case 256: hipLaunchKernelGGL((fields_bwd_kernel<256, MODE, RMAX>), dim3(grid), dim3(256), lds, st, a); break;
+    case 16: fbn_launch((fields_bwd_kernel<16, MODE, RMAX>), dim3(grid), dim3(256), lds, st, a); break;
+    case 32: fbn_launch((fields_bwd_kernel<32, MODE, RMAX>), dim3(grid), dim3(256), lds, st, a); break;
+    case 64: fbn_launch((fields_bwd_kernel<64, MODE, RMAX>), dim3(grid), dim3(256), lds, st, a); break;
+    case 128: fbn_launch((fields_bwd_kernel<128, MODE, RMAX>), dim3(grid), dim3(256), lds, st, a); break;
+    case 256: fbn_launch((fields_bwd_kernel<256, MODE, RMAX>), dim3(grid), dim3(256), lds, st, a); break;
     default: fbn_set_error("fields: embedding_dim must be one of 16,32,64,128,256"); return FBN_ERR_UNSUPPORTED;
   }
   FBN_CHECK_LAUNCH();
@@ -856,9 +856,9 @@ extern "C" int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, c
   }
   static const bool narrow = getenv("FBN_PARTIALS64") != nullptr;   // A/B knob: 64 columns per workgroup
   if (narrow)
-    hipLaunchKernelGGL(reduce_partials_one, dim3(fbn_cdiv(P, 64)), dim3(1024), 0, st, (const float*)partials, nblk, P, o);
+    fbn_launch(reduce_partials_one, dim3(fbn_cdiv(P, 64)), dim3(1024), 0, st, (const float*)partials, nblk, P, o);
   else
-    hipLaunchKernelGGL(reduce_partials_one16, dim3(fbn_cdiv(P, 16)), dim3(1024), 0, st, (const float*)partials, nblk, P,
+    fbn_launch(reduce_partials_one16, dim3(fbn_cdiv(P, 16)), dim3(1024), 0, st, (const float*)partials, nblk, P,
                        o);
   FBN_CHECK_LAUNCH();
   return FBN_OK;

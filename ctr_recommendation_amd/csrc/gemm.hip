@@ -973,7 +973,7 @@ static void launch_tile(const GemmArgs& g, int nsplit, hipStream_t st) {
   const int tn = fbn_cdiv(g.N, BN), tm = fbn_cdiv(g.M, BM);
   const int nb = tn * tm;
   dim3 grid(nb, 1, nsplit);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, TA, TB, BF16, A16, B16, SPLIT>), grid, dim3(256), 0, st, g, tn,
+  fbn_launch((gemm_kernel<BM, BN, TA, TB, BF16, A16, B16, SPLIT>), grid, dim3(256), 0, st, g, tn,
                      (nb % 8 == 0) ? 1 : 0);
 }
 
@@ -986,11 +986,11 @@ static void launch_dma16(const GemmArgs& g, const GemmPlan& p, hipStream_t st) {
   const int S = e ? atoi(e) : (p.stages ? p.stages : FBN_DMA_STAGES);
   const dim3 grid(nb, 1, p.split), blk(64 * WGM * WGN);
   if (S <= 2)
-    hipLaunchKernelGGL((gemm_dma16_kernel<BM, BN, AKM, BKM, 2, WGM, WGN>), grid, blk, 0, st, g, tn, rx);
+    fbn_launch((gemm_dma16_kernel<BM, BN, AKM, BKM, 2, WGM, WGN>), grid, blk, 0, st, g, tn, rx);
   else if (S == 3)
-    hipLaunchKernelGGL((gemm_dma16_kernel<BM, BN, AKM, BKM, 3, WGM, WGN>), grid, blk, 0, st, g, tn, rx);
+    fbn_launch((gemm_dma16_kernel<BM, BN, AKM, BKM, 3, WGM, WGN>), grid, blk, 0, st, g, tn, rx);
   else
-    hipLaunchKernelGGL((gemm_dma16_kernel<BM, BN, AKM, BKM, 4, WGM, WGN>), grid, blk, 0, st, g, tn, rx);
+    fbn_launch((gemm_dma16_kernel<BM, BN, AKM, BKM, 4, WGM, WGN>), grid, blk, 0, st, g, tn, rx);
 }
 
 template <bool AKM, bool BKM>
@@ -1200,13 +1200,13 @@ extern "C" int fbn_gemm_slabs_group(const void* descs, int n, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const char* se = getenv("FBN_GROUP_STAGES");   // A/B knob: LDS-DMA ring depth of the group (2 or 3)
   if (wide && se && atoi(se) == 3)
-    hipLaunchKernelGGL((gemm_dma16_group_kernel<128, 128, true, true, 3, 2, 4>), dim3((unsigned)total), dim3(512), 0,
+    fbn_launch((gemm_dma16_group_kernel<128, 128, true, true, 3, 2, 4>), dim3((unsigned)total), dim3(512), 0,
                        st, G);
   else if (wide)
-    hipLaunchKernelGGL((gemm_dma16_group_kernel<128, 128, true, true, 2, 2, 4>), dim3((unsigned)total), dim3(512), 0,
+    fbn_launch((gemm_dma16_group_kernel<128, 128, true, true, 2, 2, 4>), dim3((unsigned)total), dim3(512), 0,
                        st, G);
   else
-    hipLaunchKernelGGL((gemm_dma16_group_kernel<64, 64, true, true, 2, 2, 2>), dim3((unsigned)total), dim3(256), 0,
+    fbn_launch((gemm_dma16_group_kernel<64, 64, true, true, 2, 2, 2>), dim3((unsigned)total), dim3(256), 0,
                        st, G);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
@@ -1307,7 +1307,7 @@ static int gemm_impl(const void* A, const void* B, float* C, const float* bias, 
     return FBN_OK;
   }
   if (p.split > 1 && stats) {
-    hipLaunchKernelGGL(gemm_splitk_reduce_stats, dim3(fbn_cdiv(N, 64), fbn_cdiv(M, 64)), dim3(256), 0, st, g,
+    fbn_launch(gemm_splitk_reduce_stats, dim3(fbn_cdiv(N, 64), fbn_cdiv(M, 64)), dim3(256), 0, st, g,
                        p.split);
     FBN_CHECK_LAUNCH();
   } else if (p.split > 1) {
@@ -1317,9 +1317,9 @@ static int gemm_impl(const void* A, const void* B, float* C, const float* bias, 
     int blocks = (int)((total + 255) / 256);
     if (blocks > 4096) blocks = 4096;
     if (v4 && p.split >= 16 && total < (size_t)65536)
-      hipLaunchKernelGGL(gemm_splitk_reduce4_wide, dim3((unsigned)((total + 15) / 16)), dim3(256), 0, st, g, p.split);
-    else if (v4) hipLaunchKernelGGL(gemm_splitk_reduce4, dim3(blocks), dim3(256), 0, st, g, p.split);
-    else hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, st, g, p.split);
+      fbn_launch(gemm_splitk_reduce4_wide, dim3((unsigned)((total + 15) / 16)), dim3(256), 0, st, g, p.split);
+    else if (v4) fbn_launch(gemm_splitk_reduce4, dim3(blocks), dim3(256), 0, st, g, p.split);
+    else fbn_launch(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, st, g, p.split);
     FBN_CHECK_LAUNCH();
   }
   return FBN_OK;

@@ -968,10 +968,10 @@ extern "C" int fbn_pairs_fwd(const float* Vc, const short* Vc16, const float* U,
   if (B <= 0) return FBN_OK;
   if ((D & 3) || (ldc & 3)) { fbn_set_error("pairs: D and ldc must be multiples of 4"); return FBN_ERR_ARG; }
   if (c_bf16)
-    hipLaunchKernelGGL(pairs_fwd_kernel<short>, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream,
+    fbn_launch(pairs_fwd_kernel<short>, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream,
                        Vc, Vc16, U, (short*)c, B, D, ldc, mode);
   else
-    hipLaunchKernelGGL(pairs_fwd_kernel<float>, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream,
+    fbn_launch(pairs_fwd_kernel<float>, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream,
                        Vc, Vc16, U, (float*)c, B, D, ldc, mode);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
@@ -981,10 +981,10 @@ extern "C" int fbn_pairs_bwd(const float* dc, const float* Vc, const short* Vc16
                              float* dU, short* dU16, int B, int D, int ldc, int mode, void* stream) {
   if (B <= 0) return FBN_OK;
   if (mode == 0)
-    hipLaunchKernelGGL(pairs_bwd_kernel<0>, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream, dc, Vc,
+    fbn_launch(pairs_bwd_kernel<0>, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream, dc, Vc,
                        Vc16, U, dV, dU, dU16, B, D, ldc);
   else
-    hipLaunchKernelGGL(pairs_bwd_kernel<1>, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream, dc, Vc,
+    fbn_launch(pairs_bwd_kernel<1>, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream, dc, Vc,
                        Vc16, U, dV, dU, dU16, B, D, ldc);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
@@ -1004,15 +1004,15 @@ extern "C" int fbn_bn_stats_pass(const float* X, int B, int C, const double* mea
   hipStream_t st = (hipStream_t)stream;
   const int nch = row_chunks(B), rpc = B > 0 ? (B + nch - 1) / nch : 1;
   double* part = (double*)ws;
-  hipLaunchKernelGGL(colstat_partial_kernel, dim3(fbn_cdiv(C, 64), nch), dim3(256), 0, st, X, B, C, C, rpc, mean_d,
+  fbn_launch(colstat_partial_kernel, dim3(fbn_cdiv(C, 64), nch), dim3(256), 0, st, X, B, C, C, rpc, mean_d,
                      part, mean_d ? 1 : 0);
-  hipLaunchKernelGGL(chunk_reduce_kernel, dim3(fbn_cdiv(C, 4)), dim3(256), 0, st, part, nch, C, out_d);
+  fbn_launch(chunk_reduce_kernel, dim3(fbn_cdiv(C, 4)), dim3(256), 0, st, part, nch, C, out_d);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
 
 extern "C" int fbn_bn_mean(const double* sum_d, double ntot, int C, double* mean_d, void* stream) {
-  hipLaunchKernelGGL(bn_mean_kernel, dim3(fbn_cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, sum_d, ntot, C, mean_d);
+  fbn_launch(bn_mean_kernel, dim3(fbn_cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, sum_d, ntot, C, mean_d);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -1020,7 +1020,7 @@ extern "C" int fbn_bn_mean(const double* sum_d, double ntot, int C, double* mean
 extern "C" int fbn_bn_finalize(const double* m2_d, const double* mean_d, double ntot, int C, float* mean,
                                float* invstd, float* run_mean, float* run_var, float momentum, float eps,
                                int update_running, void* stream) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(fbn_cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, m2_d, mean_d, ntot,
+  fbn_launch(bn_finalize_kernel, dim3(fbn_cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, m2_d, mean_d, ntot,
                      C, mean, invstd, run_mean, run_var, momentum, eps, update_running);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
@@ -1043,7 +1043,7 @@ extern "C" int fbn_bn_stats(const float* X, int B, int C, float* mean, float* in
 
 extern "C" int fbn_bn_eval_params(const float* run_mean, const float* run_var, float* mean, float* invstd, int C,
                                   float eps, void* stream) {
-  hipLaunchKernelGGL(bn_eval_params_kernel, dim3(fbn_cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, run_mean,
+  fbn_launch(bn_eval_params_kernel, dim3(fbn_cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, run_mean,
                      run_var, mean, invstd, C, eps);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
@@ -1070,9 +1070,9 @@ extern "C" int fbn_bn_act_fwd(const float* X, float* Y, int B, int C, const floa
   if (p_drop > 0.f && !rng && !mask_in) { fbn_set_error("bn_act: dropout needs an rng state or a mask"); return FBN_ERR_ARG; }
   if (!Y && !Y16) { fbn_set_error("bn_act: no output"); return FBN_ERR_ARG; }
   const int rpc = bn_act_rows_per_chunk();
-  hipLaunchKernelGGL(bn_act_fwd2_kernel<false>, dim3(fbn_cdiv(C, 256), fbn_cdiv(B, rpc)), dim3(256), 0,
+  fbn_launch(bn_act_fwd2_kernel<false>, dim3(fbn_cdiv(C, 256), fbn_cdiv(B, rpc)), dim3(256), 0,
                      (hipStream_t)stream, X, Y, B, C, rpc, mean, invstd, g, b, p_drop, rng, stream_id, mask_out, mask_in,
-                     Y16, HeadArgs{});
+                     Y16, HeadArgs{}, nullptr, 1.f);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -1091,7 +1091,7 @@ extern "C" int fbn_bn_act_head_fwd(const float* X, float* Y, int B, int C, const
   if (bwd_part) {
     // the row chunks of fbn_bn_bwd_fused, so its reduce reads these partials as its own
     const int nch = bn_bwd_chunks(B, C), rpc = (B + nch - 1) / nch;
-    hipLaunchKernelGGL((bn_act_fwd2_kernel<true, 1024, true>), dim3(1, fbn_cdiv(B, rpc)), dim3(1024), 0,
+    fbn_launch((bn_act_fwd2_kernel<true, 1024, true>), dim3(1, fbn_cdiv(B, rpc)), dim3(1024), 0,
                        (hipStream_t)stream, X, Y, B, C, rpc, mean, invstd, g, b, p_drop, rng, stream_id, mask_out,
                        mask_in, nullptr, HeadArgs{hw, hbias, logits, probs, labels, loss_terms, gout, denom}, bwd_part,
                        bwd_scale);
@@ -1099,9 +1099,9 @@ extern "C" int fbn_bn_act_head_fwd(const float* X, float* Y, int B, int C, const
     return FBN_OK;
   }
   const int rpc = bn_act_rows_per_chunk();
-  hipLaunchKernelGGL(bn_act_fwd2_kernel<true>, dim3(1, fbn_cdiv(B, rpc)), dim3(256), 0, (hipStream_t)stream, X, Y, B,
-                     C, rpc, mean, invstd, g, b, p_drop, rng, stream_id, mask_out, mask_in, nullptr,
-                     HeadArgs{hw, hbias, logits, probs, labels, loss_terms, gout, denom});
+  fbn_launch(bn_act_fwd2_kernel<true>, dim3(1, fbn_cdiv(B, rpc)), dim3(256), 0, (hipStream_t)stream, X, Y, B,
+                     C, rpc, mean, invstd, g, b, p_drop, rng, stream_id, mask_out, mask_in, (short*)nullptr,
+                     HeadArgs{hw, hbias, logits, probs, labels, loss_terms, gout, denom}, nullptr, 1.f);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -1115,8 +1115,8 @@ extern "C" int fbn_bn_bwd_reduce(const float* G, const float* gvec, const float*
   BnBwdSrc s{G, gvec, w, hact, scale, nullptr};
   const int nch = row_chunks(B), rpc = B > 0 ? (B + nch - 1) / nch : 1;
   double* part = (double*)ws;
-  hipLaunchKernelGGL(bn_bwd_partial_kernel, dim3(fbn_cdiv(C, 64), nch), dim3(256), 0, st, s, Xpre, mean, B, C, rpc, part);
-  hipLaunchKernelGGL(chunk_reduce_kernel, dim3(fbn_cdiv(3 * C, 4)), dim3(256), 0, st, part, nch, 3 * C, red_d);
+  fbn_launch(bn_bwd_partial_kernel, dim3(fbn_cdiv(C, 64), nch), dim3(256), 0, st, s, Xpre, mean, B, C, rpc, part);
+  fbn_launch(chunk_reduce_kernel, dim3(fbn_cdiv(3 * C, 4)), dim3(256), 0, st, part, nch, 3 * C, red_d);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -1129,14 +1129,14 @@ extern "C" int fbn_bn_bwd_apply(const float* G, const float* gvec, const float* 
   hipStream_t st = (hipStream_t)stream;
   BnBwdSrc s{G, gvec, w, hact, scale, nullptr};
   float* coef = (float*)((double*)ws + (size_t)row_chunks(B) * 3 * C + 3 * (size_t)C);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(fbn_cdiv(C, 256)), dim3(256), 0, st, red_d, C, ntot, invstd, coef,
+  fbn_launch(bn_bwd_finalize_kernel, dim3(fbn_cdiv(C, 256)), dim3(256), 0, st, red_d, C, ntot, invstd, coef,
                      dgamma, dbeta, G ? nullptr : dw);
   if (B > 0 && !(C & 3)) {
     const int nch = row_chunks(B), rpc = (B + nch - 1) / nch;
-    hipLaunchKernelGGL(bn_bwd_apply4_kernel, dim3(fbn_cdiv(C, 256), nch), dim3(256), 0, st, s, Xpre, mean, invstd,
+    fbn_launch(bn_bwd_apply4_kernel, dim3(fbn_cdiv(C, 256), nch), dim3(256), 0, st, s, Xpre, mean, invstd,
                        gamma, coef, dXpre, dXpre16, B, C, rpc, nullptr);
   } else if (B > 0) {
-    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ew_grid((size_t)B * C)), dim3(256), 0, st, s, Xpre, mean, invstd,
+    fbn_launch(bn_bwd_apply_kernel, dim3(ew_grid((size_t)B * C)), dim3(256), 0, st, s, Xpre, mean, invstd,
                        gamma, coef, dXpre, dXpre16, B, C);
   }
   FBN_CHECK_LAUNCH();
@@ -1161,8 +1161,8 @@ extern "C" int fbn_colsum(const float* X, int B, int C, int ldx, float* out, flo
   if (B <= 0) return FBN_OK;
   hipStream_t st = (hipStream_t)stream;
   const int nch = row_chunks(B), rpc = (B + nch - 1) / nch;
-  hipLaunchKernelGGL(colsum_partial_kernel, dim3(fbn_cdiv(C, 64), nch), dim3(256), 0, st, X, B, C, ldx, rpc, (float*)ws);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3(fbn_cdiv(C, 4)), dim3(256), 0, st, (const float*)ws, nch, C, out, beta);
+  fbn_launch(colsum_partial_kernel, dim3(fbn_cdiv(C, 64), nch), dim3(256), 0, st, X, B, C, ldx, rpc, (float*)ws);
+  fbn_launch(colsum_final_kernel, dim3(fbn_cdiv(C, 4)), dim3(256), 0, st, (const float*)ws, nch, C, out, beta);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -1172,7 +1172,7 @@ extern "C" int fbn_head_fwd(const float* H, const float* w, const float* bias, i
                             void* stream) {
   if (B <= 0) return FBN_OK;
   if (C & 3) { fbn_set_error("head: C % 4"); return FBN_ERR_ARG; }
-  hipLaunchKernelGGL(head_fwd_kernel, dim3(fbn_cdiv((long long)B * 64, 256)), dim3(256), 0, (hipStream_t)stream, H, w,
+  fbn_launch(head_fwd_kernel, dim3(fbn_cdiv((long long)B * 64, 256)), dim3(256), 0, (hipStream_t)stream, H, w,
                      bias, B, C, logits, probs, labels, loss_terms, gout, denom);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
@@ -1180,20 +1180,20 @@ extern "C" int fbn_head_fwd(const float* H, const float* w, const float* bias, i
 
 extern "C" int fbn_sigmoid_bwd(const float* gp, const float* probs, float* gout, int B, void* stream) {
   if (B <= 0) return FBN_OK;
-  hipLaunchKernelGGL(sigmoid_bwd_kernel, dim3(fbn_cdiv(B, 256)), dim3(256), 0, (hipStream_t)stream, gp, probs, gout, B);
+  fbn_launch(sigmoid_bwd_kernel, dim3(fbn_cdiv(B, 256)), dim3(256), 0, (hipStream_t)stream, gp, probs, gout, B);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
 
 extern "C" int fbn_outer(const float* g, const float* w, float* out, int B, int C, void* stream) {
   if (B <= 0) return FBN_OK;
-  hipLaunchKernelGGL(outer_kernel, dim3(ew_grid((size_t)B * C)), dim3(256), 0, (hipStream_t)stream, g, w, out, B, C);
+  fbn_launch(outer_kernel, dim3(ew_grid((size_t)B * C)), dim3(256), 0, (hipStream_t)stream, g, w, out, B, C);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
 
 extern "C" int fbn_sum(const float* x, int n, float* out, float scale, void* stream) {
-  hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, x, n, out, scale);
+  fbn_launch(sum_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, x, n, out, scale);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -1213,7 +1213,7 @@ extern "C" int fbn_convert_bf16(const void* jobs, int n, void* stream) {
   ConvJobs J;
   const int tiles = conv_jobs_pack(jobs, n, J);
   if (tiles <= 0) return FBN_OK;
-  hipLaunchKernelGGL(convert_bf16_kernel, dim3(tiles), dim3(256), 0, (hipStream_t)stream, J, n);
+  fbn_launch(convert_bf16_kernel, dim3(tiles), dim3(256), 0, (hipStream_t)stream, J, n);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -1246,7 +1246,7 @@ __global__ void bn_tile_stats_kernel(const float* __restrict__ part, int T, int 
 
 extern "C" int fbn_bn_tile_stats(const float* part, int M, int C, const double* mean_d, double* out_d, void* stream) {
   const int T = (M + 63) / 64;
-  hipLaunchKernelGGL(bn_tile_stats_kernel, dim3(fbn_cdiv(C, 4)), dim3(256), 0, (hipStream_t)stream, part, T, C, M, 64,
+  fbn_launch(bn_tile_stats_kernel, dim3(fbn_cdiv(C, 4)), dim3(256), 0, (hipStream_t)stream, part, T, C, M, 64,
                      mean_d, out_d);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
@@ -1257,7 +1257,7 @@ extern "C" int fbn_bn_tile_finalize(const float* part, int M, int C, double ntot
                                     float* run_mean, float* run_var, float momentum, float eps, int update_running,
                                     void* stream) {
   if (M <= 0) return FBN_OK;
-  hipLaunchKernelGGL(bn_tile_finalize_kernel, dim3(fbn_cdiv(C, 4)), dim3(256), 0, (hipStream_t)stream, part,
+  fbn_launch(bn_tile_finalize_kernel, dim3(fbn_cdiv(C, 4)), dim3(256), 0, (hipStream_t)stream, part,
                      (M + 63) / 64, C, M, 64, ntot, mean, invstd, run_mean, run_var, momentum, eps, update_running);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
@@ -1285,16 +1285,16 @@ extern "C" int fbn_bn_bwd_fused(const float* G, const float* gvec, const float* 
   if (part_pre)   // the first pass already ran inside the forward (fbn_bn_act_head_fwd's bwd_part)
     part = const_cast<double*>(part_pre);
   else
-    hipLaunchKernelGGL(bn_bwd_partial4_kernel, dim3(fbn_cdiv(C, 256), nch), dim3(256), 0, st, s, Xpre, mean, B, C, rpc,
+    fbn_launch(bn_bwd_partial4_kernel, dim3(fbn_cdiv(C, 256), nch), dim3(256), 0, st, s, Xpre, mean, B, C, rpc,
                        part);
   static const bool wide = !getenv("FBN_BN_REDUCE64");   // A/B knob: 64 columns per workgroup
   if (wide)
-    hipLaunchKernelGGL(bn_bwd_reduce_finalize16_kernel, dim3(fbn_cdiv(C, 16)), dim3(1024), 0, st, part, nch, C, ntot,
+    fbn_launch(bn_bwd_reduce_finalize16_kernel, dim3(fbn_cdiv(C, 16)), dim3(1024), 0, st, part, nch, C, ntot,
                        invstd, coef, dgamma, dbeta, dw);
   else
-    hipLaunchKernelGGL(bn_bwd_reduce_finalize_kernel, dim3(fbn_cdiv(C, 64)), dim3(1024), 0, st, part, nch, C, ntot,
+    fbn_launch(bn_bwd_reduce_finalize_kernel, dim3(fbn_cdiv(C, 64)), dim3(1024), 0, st, part, nch, C, ntot,
                        invstd, coef, dgamma, dbeta, dw);
-  hipLaunchKernelGGL(bn_bwd_apply4_kernel, dim3(fbn_cdiv(C, 256), nch), dim3(256), 0, st, s, Xpre, mean, invstd, gamma,
+  fbn_launch(bn_bwd_apply4_kernel, dim3(fbn_cdiv(C, 256), nch), dim3(256), 0, st, s, Xpre, mean, invstd, gamma,
                      coef, dXpre, dXpre16, B, C, rpc, colpart);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
@@ -1303,7 +1303,7 @@ extern "C" int fbn_bn_bwd_fused(const float* G, const float* gvec, const float* 
 extern "C" int fbn_colsum_partial(const float* X, int B, int C, int ldx, float* part, void* stream) {
   if (B <= 0) return FBN_OK;
   const int nch = row_chunks(B), rpc = (B + nch - 1) / nch;
-  hipLaunchKernelGGL(colsum_partial_kernel, dim3(fbn_cdiv(C, 64), nch), dim3(256), 0, (hipStream_t)stream, X, B, C,
+  fbn_launch(colsum_partial_kernel, dim3(fbn_cdiv(C, 64), nch), dim3(256), 0, (hipStream_t)stream, X, B, C,
                      ldx, rpc, part);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
@@ -1344,7 +1344,7 @@ extern "C" int fbn_sum_jobs2(const SumJob* jobs, int n, const SlabJob* slabs, in
   }
   const int blocks = J.col0[n] + J.blk0[ns];
   if (blocks <= 0) return FBN_OK;
-  hipLaunchKernelGGL(sum_jobs_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, J);
+  fbn_launch(sum_jobs_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, J);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -1356,7 +1356,7 @@ extern "C" int fbn_sum_jobs(const SumJob* jobs, int n, void* stream) {
 
 extern "C" int fbn_bn_tile_moments(const float* part, int M, int C, double* out_d, void* stream) {
   if (M <= 0) { (void)hipMemsetAsync(out_d, 0, 2 * sizeof(double) * C, (hipStream_t)stream); return FBN_OK; }
-  hipLaunchKernelGGL(bn_tile_moments_kernel, dim3(fbn_cdiv(C, 4)), dim3(256), 0, (hipStream_t)stream, part,
+  fbn_launch(bn_tile_moments_kernel, dim3(fbn_cdiv(C, 4)), dim3(256), 0, (hipStream_t)stream, part,
                      (M + 63) / 64, C, M, 64, out_d);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
@@ -1365,7 +1365,7 @@ extern "C" int fbn_bn_tile_moments(const float* part, int M, int C, double* out_
 extern "C" int fbn_bn_moments_finalize(const double* mom_d, double ntot, int C, float* mean, float* invstd,
                                        float* run_mean, float* run_var, float momentum, float eps, int update_running,
                                        void* stream) {
-  hipLaunchKernelGGL(bn_moments_finalize_kernel, dim3(fbn_cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, mom_d, ntot,
+  fbn_launch(bn_moments_finalize_kernel, dim3(fbn_cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, mom_d, ntot,
                      C, mean, invstd, run_mean, run_var, momentum, eps, update_running);
   FBN_CHECK_LAUNCH();
   return FBN_OK;

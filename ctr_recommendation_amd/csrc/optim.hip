@@ -724,7 +724,7 @@ __global__ void adam_selftest_kernel(int n, unsigned seed, unsigned long long* d
 
 extern "C" int fbn_adam_selftest(int n, unsigned seed, unsigned long long* dev, void* stream) {
   if (n <= 0) return FBN_OK;
-  hipLaunchKernelGGL(adam_selftest_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, n, seed, dev);
+  fbn_launch(adam_selftest_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, n, seed, dev);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -1932,13 +1932,13 @@ __global__ void step_end_kernel(int* step, unsigned long long* rng, double* sums
 // ------------------------------------------------------------------ C ABI
 extern "C" int fbn_sumsq(const float* x, long long n, const int* n_rows, int row_len, double* out, void* stream) {
   if (n <= 0 && !n_rows) return FBN_OK;
-  hipLaunchKernelGGL(sumsq_kernel, dim3(512), dim3(256), 0, (hipStream_t)stream, x, n, n_rows, row_len, out);
+  fbn_launch(sumsq_kernel, dim3(512), dim3(256), 0, (hipStream_t)stream, x, n, n_rows, row_len, out);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
 
 extern "C" int fbn_clip_coef(const double* sumsq, float max_norm, float* coef, float* norm, void* stream) {
-  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, sumsq, max_norm, coef, norm);
+  fbn_launch(clip_coef_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, sumsq, max_norm, coef, norm);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -1954,7 +1954,7 @@ extern "C" int fbn_adam_dense(float* p, const float* g, float* m, float* v, long
   long long blocks = (n / 4 + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(adam_dense_kernel, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, coef,
+  fbn_launch(adam_dense_kernel, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, coef,
                      (const AdamConsts*)consts_table, step, wd, beta2, (float)(1.0 - (double)beta2), eps, sumsq,
                      max_norm, coef_out, norm_out);
   FBN_CHECK_LAUNCH();
@@ -1963,33 +1963,33 @@ extern "C" int fbn_adam_dense(float* p, const float* g, float* m, float* v, long
 
 #define FBN_DISPATCH_D(KERNEL, D, GRID, ...)                                                         \
   switch (D) {                                                                                      \
-    case 16: hipLaunchKernelGGL((KERNEL<16>), GRID, dim3(256), 0, st, __VA_ARGS__); break;          \
-    case 32: hipLaunchKernelGGL((KERNEL<32>), GRID, dim3(256), 0, st, __VA_ARGS__); break;          \
-    case 64: hipLaunchKernelGGL((KERNEL<64>), GRID, dim3(256), 0, st, __VA_ARGS__); break;          \
-    case 128: hipLaunchKernelGGL((KERNEL<128>), GRID, dim3(256), 0, st, __VA_ARGS__); break;        \
-    case 256: hipLaunchKernelGGL((KERNEL<256>), GRID, dim3(256), 0, st, __VA_ARGS__); break;        \
+    case 16: fbn_launch((KERNEL<16>), GRID, dim3(256), 0, st, __VA_ARGS__); break;          \
+    case 32: fbn_launch((KERNEL<32>), GRID, dim3(256), 0, st, __VA_ARGS__); break;          \
+    case 64: fbn_launch((KERNEL<64>), GRID, dim3(256), 0, st, __VA_ARGS__); break;          \
+    case 128: fbn_launch((KERNEL<128>), GRID, dim3(256), 0, st, __VA_ARGS__); break;        \
+    case 256: fbn_launch((KERNEL<256>), GRID, dim3(256), 0, st, __VA_ARGS__); break;        \
     default: fbn_set_error("D must be 16/32/64/128/256"); return FBN_ERR_UNSUPPORTED;              \
   }
 
 // the same with a block size of T threads
 #define FBN_DISPATCH_D_T(KERNEL, D, GRID, T, ...)                                                    \
   switch (D) {                                                                                      \
-    case 16: hipLaunchKernelGGL((KERNEL<16>), GRID, dim3(T), 0, st, __VA_ARGS__); break;            \
-    case 32: hipLaunchKernelGGL((KERNEL<32>), GRID, dim3(T), 0, st, __VA_ARGS__); break;            \
-    case 64: hipLaunchKernelGGL((KERNEL<64>), GRID, dim3(T), 0, st, __VA_ARGS__); break;            \
-    case 128: hipLaunchKernelGGL((KERNEL<128>), GRID, dim3(T), 0, st, __VA_ARGS__); break;          \
-    case 256: hipLaunchKernelGGL((KERNEL<256>), GRID, dim3(T), 0, st, __VA_ARGS__); break;          \
+    case 16: fbn_launch((KERNEL<16>), GRID, dim3(T), 0, st, __VA_ARGS__); break;            \
+    case 32: fbn_launch((KERNEL<32>), GRID, dim3(T), 0, st, __VA_ARGS__); break;            \
+    case 64: fbn_launch((KERNEL<64>), GRID, dim3(T), 0, st, __VA_ARGS__); break;            \
+    case 128: fbn_launch((KERNEL<128>), GRID, dim3(T), 0, st, __VA_ARGS__); break;          \
+    case 256: fbn_launch((KERNEL<256>), GRID, dim3(T), 0, st, __VA_ARGS__); break;          \
     default: fbn_set_error("D must be 16/32/64/128/256"); return FBN_ERR_UNSUPPORTED;              \
   }
 
 // the same for a kernel templated on <D, bool>
 #define FBN_DISPATCH_D_B(KERNEL, B, D, GRID, ...)                                                    \
   switch (D) {                                                                                      \
-    case 16: hipLaunchKernelGGL((KERNEL<16, B>), GRID, dim3(256), 0, st, __VA_ARGS__); break;       \
-    case 32: hipLaunchKernelGGL((KERNEL<32, B>), GRID, dim3(256), 0, st, __VA_ARGS__); break;       \
-    case 64: hipLaunchKernelGGL((KERNEL<64, B>), GRID, dim3(256), 0, st, __VA_ARGS__); break;       \
-    case 128: hipLaunchKernelGGL((KERNEL<128, B>), GRID, dim3(256), 0, st, __VA_ARGS__); break;     \
-    case 256: hipLaunchKernelGGL((KERNEL<256, B>), GRID, dim3(256), 0, st, __VA_ARGS__); break;     \
+    case 16: fbn_launch((KERNEL<16, B>), GRID, dim3(256), 0, st, __VA_ARGS__); break;       \
+    case 32: fbn_launch((KERNEL<32, B>), GRID, dim3(256), 0, st, __VA_ARGS__); break;       \
+    case 64: fbn_launch((KERNEL<64, B>), GRID, dim3(256), 0, st, __VA_ARGS__); break;       \
+    case 128: fbn_launch((KERNEL<128, B>), GRID, dim3(256), 0, st, __VA_ARGS__); break;     \
+    case 256: fbn_launch((KERNEL<256, B>), GRID, dim3(256), 0, st, __VA_ARGS__); break;     \
     default: fbn_set_error("D must be 16/32/64/128/256"); return FBN_ERR_UNSUPPORTED;              \
   }
 
@@ -2177,7 +2177,7 @@ extern "C" int fbn_claim_rows(const int64_t* item, const int64_t* seq, int B, in
   if (n <= 0) return FBN_OK;
   int blocks = (int)((n + 255) / 256);
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(claim_rows_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, item, L > 0 ? seq : nullptr,
+  fbn_launch(claim_rows_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, item, L > 0 ? seq : nullptr,
                      B, L, V, map, slot_row, dup, hasdup);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
@@ -2185,7 +2185,7 @@ extern "C" int fbn_claim_rows(const int64_t* item, const int64_t* seq, int B, in
 
 extern "C" int fbn_step_end(int* step, unsigned long long* rng, double* sumsq, long long* nbt0, long long* nbt1,
                             int max_step, int* err, void* stream) {
-  hipLaunchKernelGGL(step_end_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step, rng, sumsq, nbt0, nbt1,
+  fbn_launch(step_end_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step, rng, sumsq, nbt0, nbt1,
                      max_step, err);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
@@ -2234,10 +2234,10 @@ extern "C" int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, i
     if (D >= 128 && ge && atoi(ge) == 2) {
 #define FBN_WIN2_G2(DW_)                                                                                       \
   if (D == 128)                                                                                                \
-    hipLaunchKernelGGL((adam_window2_kernel<128, DW_, 2>), g2, dim3(256), 0, st, p, m, v, map, nrows, F, chunk, \
+    fbn_launch((adam_window2_kernel<128, DW_, 2>), g2, dim3(256), 0, st, p, m, v, map, nrows, F, chunk, \
                        last, (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, rpw);             \
   else                                                                                                         \
-    hipLaunchKernelGGL((adam_window2_kernel<256, DW_, 2>), g2, dim3(256), 0, st, p, m, v, map, nrows, F, chunk, \
+    fbn_launch((adam_window2_kernel<256, DW_, 2>), g2, dim3(256), 0, st, p, m, v, map, nrows, F, chunk, \
                        last, (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, rpw);
       if (decoupled) {
         FBN_WIN2_G2(true)
@@ -2305,7 +2305,7 @@ extern "C" int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B,
   static const bool onepass = getenv("FBN_PREFETCH_ONEPASS") && atoi(getenv("FBN_PREFETCH_ONEPASS")) == 1;
   if (preclaim && (!onepass || D < 128)) {
     const dim3 g2((unsigned)((n + 255) / 256));
-    hipLaunchKernelGGL(adam_pretag_kernel, g2, dim3(256), 0, st, cs, (int)n, step);
+    fbn_launch(adam_pretag_kernel, g2, dim3(256), 0, st, cs, (int)n, step);
     FBN_CHECK_LAUNCH();
     const char* ee = getenv("FBN_PF_EPW");   // A/B knob, read per call (tools/ab_step.py flips it in-process)
     const int epw = ee ? std::max(1, std::min(64, atoi(ee))) : 64;
@@ -2320,16 +2320,16 @@ extern "C" int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B,
     const char* ab = getenv("FBN_PF_ABL");
     if (D == 128 && !decoupled && ab && (atoi(ab) == 1 || atoi(ab) == 2 || atoi(ab) == 3 || atoi(ab) == 4)) {
       if (atoi(ab) == 3)   // groups of 8 rows (diagnosis: more independent update chains per wave)
-        hipLaunchKernelGGL((adam_prefetch2_kernel<128, false, 8, 0>), g3, dim3(256), 0, st, p, m, v, cs, (int)n,
+        fbn_launch((adam_prefetch2_kernel<128, false, 8, 0>), g3, dim3(256), 0, st, p, m, v, cs, (int)n,
                            last, (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, epw);
       else if (atoi(ab) == 4)   // groups of 8 rows without row traffic
-        hipLaunchKernelGGL((adam_prefetch2_kernel<128, false, 8, 2>), g3, dim3(256), 0, st, p, m, v, cs, (int)n,
+        fbn_launch((adam_prefetch2_kernel<128, false, 8, 2>), g3, dim3(256), 0, st, p, m, v, cs, (int)n,
                            last, (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, epw);
       else if (atoi(ab) == 1)
-        hipLaunchKernelGGL((adam_prefetch2_kernel<128, false, 4, 1>), g3, dim3(256), 0, st, p, m, v, cs, (int)n,
+        fbn_launch((adam_prefetch2_kernel<128, false, 4, 1>), g3, dim3(256), 0, st, p, m, v, cs, (int)n,
                            last, (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, epw);
       else
-        hipLaunchKernelGGL((adam_prefetch2_kernel<128, false, 4, 2>), g3, dim3(256), 0, st, p, m, v, cs, (int)n,
+        fbn_launch((adam_prefetch2_kernel<128, false, 4, 2>), g3, dim3(256), 0, st, p, m, v, cs, (int)n,
                            last, (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, epw);
       FBN_CHECK_LAUNCH();
       return FBN_OK;
@@ -2339,10 +2339,10 @@ extern "C" int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B,
     if (D >= 128 && ge && atoi(ge) == 2) {
 #define FBN_PF2_G2(DW_)                                                                                        \
   if (D == 128)                                                                                                \
-    hipLaunchKernelGGL((adam_prefetch2_kernel<128, DW_, 2>), g3, dim3(256), 0, st, p, m, v, cs, (int)n, last, \
+    fbn_launch((adam_prefetch2_kernel<128, DW_, 2>), g3, dim3(256), 0, st, p, m, v, cs, (int)n, last, \
                        (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, epw);                  \
   else                                                                                                         \
-    hipLaunchKernelGGL((adam_prefetch2_kernel<256, DW_, 2>), g3, dim3(256), 0, st, p, m, v, cs, (int)n, last, \
+    fbn_launch((adam_prefetch2_kernel<256, DW_, 2>), g3, dim3(256), 0, st, p, m, v, cs, (int)n, last, \
                        (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps, epw);
       if (decoupled) {
         FBN_PF2_G2(true)
@@ -2365,17 +2365,17 @@ extern "C" int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B,
   }
   if (D == 128) {
     if (decoupled)
-      hipLaunchKernelGGL((adam_prefetch_kernel<128, true>), grid, dim3(256), 0, st, p, m, v, cs, (int)n, last,
+      fbn_launch((adam_prefetch_kernel<128, true>), grid, dim3(256), 0, st, p, m, v, cs, (int)n, last,
                          (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
     else
-      hipLaunchKernelGGL((adam_prefetch_kernel<128, false>), grid, dim3(256), 0, st, p, m, v, cs, (int)n, last,
+      fbn_launch((adam_prefetch_kernel<128, false>), grid, dim3(256), 0, st, p, m, v, cs, (int)n, last,
                          (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
   } else {
     if (decoupled)
-      hipLaunchKernelGGL((adam_prefetch_kernel<256, true>), grid, dim3(256), 0, st, p, m, v, cs, (int)n, last,
+      fbn_launch((adam_prefetch_kernel<256, true>), grid, dim3(256), 0, st, p, m, v, cs, (int)n, last,
                          (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
     else
-      hipLaunchKernelGGL((adam_prefetch_kernel<256, false>), grid, dim3(256), 0, st, p, m, v, cs, (int)n, last,
+      fbn_launch((adam_prefetch_kernel<256, false>), grid, dim3(256), 0, st, p, m, v, cs, (int)n, last,
                          (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
   }
   FBN_CHECK_LAUNCH();
@@ -2410,7 +2410,7 @@ extern "C" int fbn_adam_prefetch_rows(const int* lids, int n, int skip0, long lo
     // one rank).  The tags only decide this pass: the next step's owner claims do not read them.
     cs.pre = preclaim;
     const dim3 g2((unsigned)((n + 255) / 256));
-    hipLaunchKernelGGL(adam_pretag_kernel, g2, dim3(256), 0, st, cs, n, step);
+    fbn_launch(adam_pretag_kernel, g2, dim3(256), 0, st, cs, n, step);
     const int epw = 64;
     const dim3 g3((unsigned)(((n + epw - 1) / epw + 3) / 4));
     if (decoupled) {
@@ -2427,17 +2427,17 @@ extern "C" int fbn_adam_prefetch_rows(const int* lids, int n, int skip0, long lo
   const dim3 grid((unsigned)std::min<long long>(pcap, ((long long)n + 63) / 64));
   if (D == 128) {
     if (decoupled)
-      hipLaunchKernelGGL((adam_prefetch_kernel<128, true>), grid, dim3(256), 0, st, p, m, v, cs, n, last,
+      fbn_launch((adam_prefetch_kernel<128, true>), grid, dim3(256), 0, st, p, m, v, cs, n, last,
                          (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
     else
-      hipLaunchKernelGGL((adam_prefetch_kernel<128, false>), grid, dim3(256), 0, st, p, m, v, cs, n, last,
+      fbn_launch((adam_prefetch_kernel<128, false>), grid, dim3(256), 0, st, p, m, v, cs, n, last,
                          (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
   } else {
     if (decoupled)
-      hipLaunchKernelGGL((adam_prefetch_kernel<256, true>), grid, dim3(256), 0, st, p, m, v, cs, n, last,
+      fbn_launch((adam_prefetch_kernel<256, true>), grid, dim3(256), 0, st, p, m, v, cs, n, last,
                          (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
     else
-      hipLaunchKernelGGL((adam_prefetch_kernel<256, false>), grid, dim3(256), 0, st, p, m, v, cs, n, last,
+      fbn_launch((adam_prefetch_kernel<256, false>), grid, dim3(256), 0, st, p, m, v, cs, n, last,
                          (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);
   }
   FBN_CHECK_LAUNCH();
@@ -2490,7 +2490,7 @@ static int claim_catchup_impl(const int64_t* item, const int64_t* seq, int B, in
   ConvJobs cj;
   const int conv_tiles = n_conv > 0 ? conv_jobs_pack(conv_jobs, n_conv, cj) : 0;
   if (conv_tiles > 0 && (n <= 0 || nrows <= 0)) {   // no claim launch to ride on: convert alone
-    hipLaunchKernelGGL(convert_bf16_kernel_o, dim3(conv_tiles), dim3(256), 0, (hipStream_t)stream, cj, n_conv);
+    fbn_launch(convert_bf16_kernel_o, dim3(conv_tiles), dim3(256), 0, (hipStream_t)stream, cj, n_conv);
     FBN_CHECK_LAUNCH();
   }
   if (n <= 0 || nrows <= 0) return FBN_OK;
@@ -2525,7 +2525,7 @@ static int claim_catchup_impl(const int64_t* item, const int64_t* seq, int B, in
     return FBN_OK;
   }
   if (conv_tiles > 0) {   // FBN_CLAIM_ONEPASS: the images in their own launch first
-    hipLaunchKernelGGL(convert_bf16_kernel_o, dim3(conv_tiles), dim3(256), 0, st, cj, n_conv);
+    fbn_launch(convert_bf16_kernel_o, dim3(conv_tiles), dim3(256), 0, st, cj, n_conv);
     FBN_CHECK_LAUNCH();
   }
   if (!cone) {
@@ -2589,12 +2589,12 @@ __global__ void unpack_extras_kernel(const float* in, float* loss, double* sumsq
   sumsq[0] += (double)in[1];
 }
 extern "C" int fbn_pack_extras(const float* loss, double* tab_slots, float* out, void* stream) {
-  hipLaunchKernelGGL(pack_extras_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, loss, tab_slots, out);
+  fbn_launch(pack_extras_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, loss, tab_slots, out);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
 extern "C" int fbn_unpack_extras(const float* in, float* loss, double* sumsq, void* stream) {
-  hipLaunchKernelGGL(unpack_extras_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, in, loss, sumsq);
+  fbn_launch(unpack_extras_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, in, loss, sumsq);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

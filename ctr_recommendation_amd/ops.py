@@ -64,6 +64,20 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, transA, transB, bias=None, rB=NO_REMAP
          stream if stream is not None else _lib.stream_handle())
 
 
+def _probe_start(probe, name):
+    """bench probes: a kernel-span probe (_lib.KernelProbe) armed for the next library call."""
+    if probe is None:
+        return None
+    kp = _lib.KernelProbe()
+    probe.setdefault(name, []).append((kp, None))
+    return kp
+
+
+def _probe_end(kp) -> None:
+    if kp is not None:
+        kp.done()
+
+
 def fused_bilinear(d: int) -> bool:
     """bf16 "all" bilinear as one fused MFMA + pair-product launch each way (csrc/bilinear.hip);
     FBN_NO_FUSED_BILINEAR=1 selects the GEMM + pair-kernel path (A/B measurements)."""
@@ -227,18 +241,14 @@ class DeferredSums:
         """The slab GEMMs recorded so far, in ONE fbn_gemm_slabs_group launch on `stream` (tstream: the
         torch stream of that handle, for the bench's events); their slabs are summed at flush()."""
         group = self.group
-        ev = None
-        if group and probe is not None:             # bench: HIP events around the grouped launch
-            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            ev[0].record(tstream)
-            probe.setdefault("wgrad_group", []).append(ev)
+        ev = _probe_start(probe, "wgrad_group") if group else None    # bench: the grouped launch
         while group:
             gc, group = group[:6], group[6:]
             garr = (_SlabGemm * len(gc))(*[_SlabGemm(*x) for x in gc])
             _lib.keep(garr)
             call("fbn_gemm_slabs_group", ctypes.addressof(garr), len(gc), stream)
         if ev is not None:
-            ev[1].record(tstream)
+            _probe_end(ev)
             self.timed_group = True
         self.group = []
 
@@ -438,11 +448,7 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     E = p["item_emb.weight"] if table_rows is None else table_rows
     V = p["item_emb.weight"].shape[0] if table_rows is None else 0
     sm = sparse or {}
-    ev = None
-    if probe is not None:                       # bench: HIP events around the gather kernel
-        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-        ev[0].record()
-        probe.setdefault("fields_fwd", []).append(ev)
+    ev = _probe_start(probe, "fields_fwd")      # bench: the gather kernel's span
     if _GATHER_HOT and table_rows is None and V * d * 4 < 0xFFFFFF00:
         # A/B variant: the batch's rows drawn >= _GATHER_HOT times are staged in LDS per workgroup
         hc = a.get("hot_cnt")
@@ -471,8 +477,7 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
              ptr(Vc16), None if split_c else ptr(c), KC,
              int(bf), ptr(av), ptr(cnt), ptr(err), ptr(sm.get("map")), ptr(sm.get("slot_row")), B, Lr, d,
              int(table_rows is not None and table_rows.dtype == torch.bfloat16), st)
-    if ev is not None:
-        ev[1].record()
+    _probe_end(ev)
     if after_gather is not None:
         after_gather()
     if hooks and "after_fields" in hooks:         # trainer: side-stream work forked here
@@ -506,11 +511,7 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     fuse = cfg.training
     t1 = buf("tiles1", (nt, H1, 2)) if fuse else None      # fused BN statistics (GEMM epilogue)
     t2 = buf("tiles2", (nt, H2, 2)) if fuse else None
-    ev1 = None
-    if probe is not None:                       # bench: HIP events around the MLP's first GEMM
-        ev1 = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-        ev1[0].record()
-        probe.setdefault("gemm_mlp0", []).append(ev1)
+    ev1 = _probe_start(probe, "gemm_mlp0")      # bench: the MLP's first GEMM
     if split_c:
         gemm_split(Vc16, w16["Wa"], h1pre, B, H1, KC, 5 * d, KC, H1, False, True, bias=p["mlp.0.bias"], stream=st,
                    stats=t1, A2=c[:, 5 * d:], lda2=KC, kseg=5 * d)
@@ -520,8 +521,7 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     else:
         gemm(c, p["mlp.0.weight"], h1pre, B, H1, KC, KC, 21 * d, H1, False, True, bias=p["mlp.0.bias"],
              rB=wa_remap(d), stream=st, stats=t1)
-    if ev1 is not None:
-        ev1[1].record()
+    _probe_end(ev1)
     if hooks and "after_mlp0" in hooks:           # trainer: side-stream work forked here
         hooks["after_mlp0"]()
     mean1, inv1 = buf("mean1", (H1,)), buf("inv1", (H1,))
@@ -772,19 +772,14 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
         outs_arr = (ctypes.c_void_p * 8)(*[g[k].data_ptr() for k in keys])   # host array of device pointers
         _lib.keep(outs_arr)
         outs = ctypes.cast(outs_arr, ctypes.c_void_p).value
-    evb = None
-    if probe is not None:                       # bench / tools: events around the fields backward
-        evb = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-        evb[0].record()
-        probe.setdefault("fields_bwd", []).append(evb)
+    evb = _probe_start(probe, "fields_bwd")     # bench / tools: the fields backward
     call("fbn_fields_bwd", ptr(batch["item_id"]), ptr(seq) if Lr else None, ptr(batch["likes_level"]),
          ptr(batch["views_level"]), ptr(a["hmm"]), ptr(p["mm_proj.1.weight"]), ptr(p["mm_proj.1.bias"]), LN_EPS,
          ptr(p["senet.excitation.0.weight"]), ptr(p["senet.excitation.0.bias"]), ptr(p["senet.excitation.2.weight"]),
          R, ncate, ptr(p["cate_emb.weight"]), ptr(a["X"]), ptr(a["a"]), ptr(a["cnt"]), ptr(dV), ptr(dhmm), ptr(dhmm16), ptr(partials), outs,
          ptr(table_grad), ptr(gvec), ptr(gnorm), V, ptr(pos), ptr(sendbuf),
          int(sendbuf is not None and sendbuf.dtype == torch.bfloat16), B, Lr, d, st)
-    if evb is not None:
-        evb[1].record()
+    _probe_end(evb)
     if hooks and "after_fields_bwd" in hooks:     # N > 1: the gradient rows are complete -> exchange
         hooks["after_fields_bwd"]()
     if bf:

@@ -102,18 +102,18 @@ BUFFERS = ("mlp.1.running_mean", "mlp.1.running_var", "mlp.1.num_batches_tracked
 
 
 def _events(probe, name, stream=None):
-    """Start a (start, end) HIP-event pair on `stream` (default: current) for kernel `name` (bench probes)."""
+    """Arm a kernel-span probe (_lib.KernelProbe) for the next library call, recorded under `name`
+    (bench probes); _events_end() right after that call."""
     if probe is None:
         return None
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record(stream)
-    probe.setdefault(name, []).append((s, e))
-    return e
+    kp = _lib.KernelProbe()
+    probe.setdefault(name, []).append((kp, None))
+    return kp
 
 
-def _events_end(e, stream=None):
-    if e is not None:
-        e.record(stream)
+def _events_end(kp, stream=None):
+    if kp is not None:
+        kp.done()
 
 
 def default_lazy_window(d: int) -> int:

@@ -34,6 +34,13 @@ extern "C" {
 #define FBN_ERR_UNSUPPORTED 3
 
 const char* fbn_last_error(void);
+/* Kernel-span probes (bench.py's rooflines): between fbn_probe_arm(slot) and fbn_probe_disarm() the
+ * library's kernel launches record slot's event pair -- start at the first kernel's start, stop at
+ * each kernel's end (hipExtLaunchKernelGGL).  fbn_probe_disarm: 1 if a kernel took the slot;
+ * fbn_probe_elapsed(slot): the span in ms once those kernels completed, or -1. */
+int fbn_probe_arm(int slot);
+int fbn_probe_disarm(void);
+float fbn_probe_elapsed(int slot);
 int fbn_version(void);
 int fbn_device_ok(void); /* 1 if the current HIP device is gfx950 */
 
