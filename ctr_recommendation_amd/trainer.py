@@ -71,6 +71,8 @@ _SIDE_SERIAL = os.environ.get("FBN_SIDE_SERIAL", "auto")
 # once the backward starts (the side stream waits for the forward)
 _SIDE_ORDER = os.environ.get("FBN_SIDE_ORDER", "wp")
 _FIXUP_ON_SIDE = os.environ.get("FBN_FIXUP_ON_SIDE", "auto")
+# one join of the side stream per step after the fold (A/B knob: False joins again before the tail)
+_JOIN_ONCE = True
 # ... or after the gather (fields_fwd then runs with the chip to itself; A/B knob)
 _SIDE_AFTER_GATHER = os.environ.get("FBN_SIDE_AFTER_GATHER", "0") == "1"
 # N > 1: the next batch's routing enqueued after this step's compute (A/B knob)
@@ -691,6 +693,7 @@ class FiBiNETTrainer:
             # (it waits on fwd_ev only), but the compute no longer waits for the host to get
             # through ~10 side-stream launches and a collective first
             route_ahead()
+        joined = False
         if self.xchg is None:
             # single GPU: per-sample vectors; entry e = b*(L+1)+t; duplicates -> extra[claimer]
             n_ent = B * (L + 1)
@@ -705,6 +708,7 @@ class FiBiNETTrainer:
                 gsrc = (self.gvec, self.extra, L + 1)
                 if fixup_side:
                     _lib.wait_stream(main, self.side)     # the fold (and the side's table passes) done
+                    joined = True
                 else:
                     call("fbn_sparse_fixup_dup", ptr(self.dup), n_ent, ptr(self.gvec), ptr(self.extra),
                          ptr(self.slot_row), L + 1, d, st)
@@ -746,7 +750,10 @@ class FiBiNETTrainer:
             call("fbn_unpack_extras", ptr(self.flat_g_ext[o:]), ptr(self.loss), ptr(self.sumsq), st)
         if not dense_done:
             call("fbn_sumsq", ptr(self.flat_g), self.n_dense, None, 0, ptr(self.sumsq), st)
-        _lib.wait_stream(main, self.side)   # side-stream table pass done before map entries are reset
+        if not (joined and _JOIN_ONCE):
+            # side-stream table pass done before map entries are reset (already joined after the
+            # fold: nothing went to the side stream since, and each join costs ~6 us of main-stream idle)
+            _lib.wait_stream(main, self.side)
         if self.xchg is None:
             defer_now = self.deferred
         if defer_now:
