@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <vector>
@@ -69,10 +70,22 @@ int call_op(const Op& o) {
             a[46], a[47], f[0], f[1], f[2], f[3], f[4], f[5], f[6], f[7]);
 }
 
+// The program's events only order work between streams of one device, so their release need not be
+// system scope (the default: an L2 writeback + invalidate at every record, ~6 us of idle on the
+// recording stream before its next kernel).  FBN_PLAN_EVENT_SCOPE (A/B knob, read at event creation):
+// "device" (default) -- hipEventDisableSystemFence; "release_device" -- hipEventReleaseToDevice;
+// "system" -- the runtime's default fence.
+unsigned event_flags() {
+  const char* e = getenv("FBN_PLAN_EVENT_SCOPE");
+  if (e && !strcmp(e, "system")) return hipEventDisableTiming;
+  if (e && !strcmp(e, "release_device")) return hipEventDisableTiming | hipEventReleaseToDevice;
+  return hipEventDisableTiming | hipEventDisableSystemFence;
+}
+
 int ensure_event(Plan* p, int slot) {
   while ((int)p->events.size() <= slot) {
     hipEvent_t e;
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+    if (hipEventCreateWithFlags(&e, event_flags()) != hipSuccess) {
       fbn_set_error("fbn_plan: hipEventCreateWithFlags failed");
       return 2;
     }
