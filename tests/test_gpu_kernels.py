@@ -381,3 +381,37 @@ def test_gemm_slabs_group_default_partition_sums(hip_device):
         grp = ws_grp[:ng * M * N].view(ng, M, N).sum(0)
         exact = A.float().t() @ Bm.float()
         assert (grp - ref).abs().max().item() <= 1e-5 * exact.abs().max().item(), (M, N, K)
+
+
+@pytest.mark.gpu
+def test_kernel_span_probe(hip_device):
+    """fbn_probe_arm / _disarm / _elapsed (bench.py's roofline timings): a probed call's span is its
+    kernels' own start-to-end time -- positive, and no longer than host-side events around the same
+    call (which add marker packets and dispatch latency); a call that launches nothing leaves the
+    probe untaken (-1); an unarmed launch records nothing."""
+    from ctr_recommendation_amd import _lib
+    M, N, K = 8192, 512, 1920
+    A = torch.randn((M, K), device=hip_device).bfloat16()
+    W = torch.randn((N, K), device=hip_device).bfloat16()
+    C = torch.empty((M, N), device=hip_device)
+    ops.gemm(A, W, C, M, N, K, K, K, N, False, True)          # warm-up
+    spans, outer = [], []
+    for _ in range(5):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        kp = _lib.KernelProbe()
+        ops.gemm(A, W, C, M, N, K, K, K, N, False, True)
+        kp.done()
+        e1.record()
+        torch.cuda.synchronize()
+        assert kp.taken
+        spans.append(kp.elapsed_time())
+        outer.append(e0.elapsed_time(e1))
+    assert all(0 < s <= o for s, o in zip(spans, outer)), (spans, outer)
+    empty = _lib.KernelProbe()
+    ops.gemm(A, W, C, 0, N, K, K, K, N, False, True)          # M = 0: no launch
+    empty.done()
+    assert not empty.taken and empty.elapsed_time() == -1.0
+    ops.gemm(A, W, C, M, N, K, K, K, N, False, True)          # unarmed: the last slot stays as it was
+    torch.cuda.synchronize()
+    assert kp.elapsed_time() == spans[-1]
