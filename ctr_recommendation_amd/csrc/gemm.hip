@@ -342,14 +342,16 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[T
     }
   if (g.bnb_part && !split) {
     // BatchNorm backward first pass (bn_bwd_partial4_kernel's sums) from the accumulators: this
-    // wave's WM rows are exactly one row chunk (the host checks WM == bnb_rpc)
+    // wave's WM (= 32, TM = 1) rows are one row chunk (bnb_rpc 32) or two (bnb_rpc 16: rows 0-15 of
+    // the 32x32 tile are its elements e < 8, rows 16-31 e >= 8); the host checks the plan
     const int chunk = (m0 + wm * WM) / g.bnb_rpc;
+    const bool two = g.bnb_rpc == 16;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int n = n0 + wn * WN + j * 32 + lr;
       const bool nok = n < g.N;
       const float mu = nok ? g.bnb_mean[n] : 0.f;
-      double s0 = 0.0, s1 = 0.0;
+      double s0[2] = {0.0, 0.0}, s1[2] = {0.0, 0.0};
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -358,18 +360,24 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, f32x16 (&acc)[T
           if (nok && m < g.M) {
             const size_t idx = (size_t)m * g.N + n;
             const float dy = g.bnb_hact16[idx] > 0 ? acc[i][j][e] * g.bnb_scale : 0.f;
-            s0 += dy;
-            s1 += (double)((g.bnb_xpre[idx] - mu) * dy);
+            const int h = (two && e >= 8) ? 1 : 0;
+            s0[h] += dy;
+            s1[h] += (double)((g.bnb_xpre[idx] - mu) * dy);
           }
         }
-      s0 += __shfl_xor(s0, 32, 64);
-      s1 += __shfl_xor(s1, 32, 64);
-      if (lh == 0 && nok) {
-        double* pp = g.bnb_part + (size_t)chunk * 3 * g.N;
-        pp[n] = s0;
-        pp[g.N + n] = s1;
-        pp[2 * (size_t)g.N + n] = 0.0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        s0[h] += __shfl_xor(s0[h], 32, 64);
+        s1[h] += __shfl_xor(s1[h], 32, 64);
       }
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (lh == 0 && nok && (h == 0 || two)) {
+          double* pp = g.bnb_part + (size_t)(chunk + h) * 3 * g.N;
+          pp[n] = s0[h];
+          pp[g.N + n] = s1[h];
+          pp[2 * (size_t)g.N + n] = 0.0;
+        }
     }
   }
   if (g.stats && !split) {
@@ -1338,7 +1346,8 @@ extern "C" int fbn_gemm_bn_bwd_part_supported(int M, int N, int K, int lda, int 
   const GemmPlan p = plan_dma16(M, N, K);
   if (p.split != 1 || p.waves != 8 || p.bm != 64 || p.bn != 128) return 0;   // 2 x 4 waves: 32 rows each
   const int nch = fbn_bn_bwd_chunks(M, N);
-  return (N % 4 == 0 && M % 32 == 0 && M / 32 == nch) ? 1 : 0;
+  // one row chunk per wave (32 rows) or two (16 rows each)
+  return (N % 4 == 0 && M % 32 == 0 && (M / 32 == nch || M / 16 == nch)) ? 1 : 0;
 }
 
 extern "C" int fbn_gemm_bn_bwd_part(const void* A, const void* B, float* C, int M, int N, int K, int lda, int ldb,
@@ -1358,7 +1367,7 @@ extern "C" int fbn_gemm_bn_bwd_part(const void* A, const void* B, float* C, int 
   x.bnb_mean = mean;
   x.bnb_scale = scale;
   x.bnb_part = part;
-  x.bnb_rpc = 32;
+  x.bnb_rpc = M / fbn_bn_bwd_chunks(M, N);     // 32 or 16 (fbn_gemm_bn_bwd_part_supported)
   return gemm_impl(A, B, C, nullptr, M, N, K, lda, ldb, ldc, transA, transB, 0x7fffffff, 0, 0, 0x7fffffff, 0, 0, 0.f,
                    1, 1, 1, nullptr, nullptr, 0, nullptr, 0, 0x7fffffff, nullptr, 0, 0x7fffffff, stream, 0, &x);
 }

@@ -456,6 +456,7 @@ def test_config_size_dropin_fwd_bwd(hip_device, cfgname, d, V, B):
 
 
 @pytest.mark.parametrize("cfgname,d,V,B,dtype", [("C2", 16, 1_000_000, 4096, "fp32"),
+                                                 ("C2", 16, 1_000_000, 4096, "bf16"),
                                                  ("C3", 128, 1_250_000, 8192, "fp32"),
                                                  ("C3", 128, 1_250_000, 8192, "bf16_fwd"),
                                                  ("C3", 128, 1_250_000, 8192, "bf16")])

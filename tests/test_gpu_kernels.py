@@ -415,3 +415,38 @@ def test_kernel_span_probe(hip_device):
     ops.gemm(A, W, C, M, N, K, K, K, N, False, True)          # unarmed: the last slot stays as it was
     torch.cuda.synchronize()
     assert kp.elapsed_time() == spans[-1]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [8192, 4096])
+def test_gemm_bn_bwd_part_epilogue(hip_device, M):
+    """fbn_gemm_bn_bwd_part (the BN1 backward's first pass in the epilogue of its dgrad GEMM): C is the
+    plain bf16 GEMM, and part[chunk][0 / 1][n] = the chunk's sum of dy / (x - mean) dy with
+    dy = (hact > 0) C scale, against torch in float64.  M = 8192 (C3): one 32-row chunk per wave;
+    M = 4096 (C2): two 16-row chunks per wave."""
+    from ctr_recommendation_amd import _lib
+    N, K = 512, 256
+    assert _lib.lib().fbn_gemm_bn_bwd_part_supported(M, N, K, K, K, 0, 1)
+    g = torch.Generator(device="cpu").manual_seed(9)
+    A = torch.randn((M, K), generator=g).to(hip_device).bfloat16()
+    W = torch.randn((N, K), generator=g).to(hip_device).bfloat16()
+    hact16 = torch.randn((M, N), generator=g).to(hip_device).bfloat16()
+    xpre = torch.randn((M, N), generator=g).to(hip_device)
+    mean = torch.randn((N,), generator=g).to(hip_device) * 0.1
+    nch = _lib.lib().fbn_bn_bwd_chunks(M, N)
+    part = torch.full((nch, 3, N), float("nan"), dtype=torch.float64, device=hip_device)
+    C = torch.empty((M, N), device=hip_device)
+    scale = 1.25
+    _lib.call("fbn_gemm_bn_bwd_part", _lib.ptr(A), _lib.ptr(W), _lib.ptr(C), M, N, K, K, K, N, 0, 1,
+              _lib.ptr(hact16), _lib.ptr(xpre), _lib.ptr(mean), scale, _lib.ptr(part), _lib.stream_handle(hip_device))
+    C0 = torch.empty_like(C)
+    ops.gemm(A, W, C0, M, N, K, K, K, N, False, True)
+    torch.cuda.synchronize()
+    assert torch.equal(C, C0)
+    dy = torch.where(hact16.float() > 0, C.double() * scale, torch.zeros_like(C, dtype=torch.float64))
+    rpc = M // nch
+    s0 = dy.view(nch, rpc, N).sum(1)
+    s1 = ((xpre.double() - mean.double()) * dy).view(nch, rpc, N).sum(1)
+    assert torch.allclose(part[:, 0], s0, rtol=1e-5, atol=1e-3)
+    assert torch.allclose(part[:, 1], s1, rtol=1e-5, atol=1e-3)
+    assert bool((part[:, 2] == 0).all())
