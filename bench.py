@@ -43,6 +43,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 MFMA_PEAK_TFS = 2500.0         # dense bf16 MFMA (2.5 PFLOP/s, no sparsity)
 FP32_MFMA_PEAK_TFS = 157.0     # fp32 matrix
 ROWS_PER_GPU = 1_250_000
+LIVE_EVERY = 8       # one step program in 8 carries the recorded kernel-span probes (bench rooflines)
 
 
 def parse():
@@ -72,6 +73,9 @@ def parse():
                     help="skip the inference leg (eval-mode drop-in forwards at batch 8192, src/Prediction.py:95-113)")
     ap.add_argument("--infer-batches", type=int, default=96)
     ap.add_argument("--probe-steps", type=int, default=10)
+    ap.add_argument("--no-live-probes", dest="live_probes", action="store_false",
+                    help="step programs without the kernel-span probes recorded into them (the in-step "
+                         "rooflines then come from the eager probe pass)")
     ap.add_argument("--batches", type=int, default=0, help="distinct HBM-resident batches (default F + 32)")
     ap.add_argument("--lazy-window", type=int, default=0,
                     help="lazy table-Adam window F (rows per step: V/F; default: the trainer's, 128 at d >= 128, else 32)")
@@ -328,6 +332,11 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
 
     mode_now = [modes[0]]
     progs = [None] * nb
+    # kernel-span probes recorded into every program: each replay re-arms them, so right after the timed
+    # steps the programs replayed there hold the spans of THOSE launches (rooflines of the timed region)
+    # (one program in LIVE_EVERY carries them: a probed kernel launch costs ~2 us, so probing every
+    # step would slow the very steps it times)
+    live = [({} if j % LIVE_EVERY == 0 else None) for j in range(nb)] if (use_prog and args.live_probes) else None
     prog_pool = torch.cuda.MemPool() if use_prog else None     # one private pool for every program
 
     def run_step(i):
@@ -339,7 +348,8 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
         elif mode_now[0] == "program":
             # first visit of this batch: a real step, recorded (the program replays it from now on)
             b, y = batches[j]
-            progs[j] = tr.record_program(b, y, next_batch=batches[(i + 1) % nb][0], pool=prog_pool)
+            progs[j] = tr.record_program(b, y, next_batch=batches[(i + 1) % nb][0], pool=prog_pool,
+                                         probe=live[j] if live else None)   # None: unprobed program
         else:
             # the HBM-resident batch itself: N > 1 routes the next batch during this step (no
             # mid-step host sync); N = 1 catches its rows up ahead and pre-claims them
@@ -378,6 +388,7 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
     if tr.xchg is not None:
         tr.xchg.host_wait_s = 0.0
     t0 = time.perf_counter()
+    i_timed = i
     for _ in range(K):
         run_step(i)
         i += 1
@@ -443,6 +454,17 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
             torch.cuda._sleep(2_000_000)
             ops.forward(tr.p, batches[j % nb][0], cfg_iso, None, err=tr.err, probe=iso)
         torch.cuda.synchronize()
+
+    # the in-step rooflines from the timed replays themselves (step programs with recorded probes): the
+    # programs of the timed steps (each replayed once when K <= the number of batches) hold their spans
+    timed_src = None
+    if live and mode_now[0] == "program":
+        timed_src = {}
+        for jj in sorted({t % nb for t in range(i_timed, i_timed + K)}):
+            for name, pairs in (live[jj] or {}).items():
+                timed_src.setdefault(name, []).extend(pairs)
+        for name, pairs in timed_src.items():
+            probe[name] = pairs            # replaces the eager probe steps' in-step values
 
     def avg_ms(name, src=None):
         # the first two launches of an explicit source (the eval-mode forwards, the serialised probe
@@ -531,6 +553,8 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
     out = {"dt": dt, "t_host": t_host, "t_wait": t_wait, "K": K, "W": W, "B": B, "L": L, "V": V, "d": d, "rows_local": tr.rows_local, "loss": loss,
            "rooflines": rooflines, "roofline": dominant, "table_adam": tr.table_adam,
            "graphs": mode_now[0] == "graph", "launch_mode": mode_now[0] if not sharded else "eager",
+           "probe_source": ("the timed step-program replays (kernel-span probes recorded into the programs)"
+                            if timed_src else "eager probe steps after the timed region"),
            "collectives": (None if not sharded else "RCCL on the step's stream (csrc/comm.cpp)"
                            if tr.native_comm is not None else "torch.distributed process group"),
            "mode_trial_ms_per_step": {k: [round(x, 4) for x in v] for k, v in trial.items()} if trial else None,
@@ -632,6 +656,7 @@ def main():
             **({"host_blocked_ms_per_step": round(r["t_wait"] / K * 1e3, 4)} if r["t_wait"] else {}),
             "roofline": r["roofline"],
             "rooflines": r["rooflines"],
+            "rooflines_in_step_from": r["probe_source"],
             "table_adam": r["table_adam"],
             "steady_state": {"priming_steps": r["prime"], "warmup_steps": args.warmup,
                              "mean_replay_steps_per_claimed_row": round(r["lag"], 2),

@@ -160,7 +160,7 @@ def lib() -> ctypes.CDLL:
 
 
 _fns = {}
-_UNCHECKED = ("fbn_version", "fbn_device_ok", "fbn_probe_disarm", "fbn_probe_elapsed")
+_UNCHECKED = ("fbn_version", "fbn_device_ok", "fbn_probe_elapsed")
 _tls = threading.local()           # .prog: the StepProgram recording on this thread (or None)
 
 
@@ -253,24 +253,25 @@ def _f32_in_f64(x: float) -> float:
 
 
 class KernelProbe:
-    """The kernels of one entry-point call, timed on the device (bench.py's rooflines): construct it
-    right before the call (fbn_probe_arm), done() right after (fbn_probe_disarm); elapsed_time() is
-    the span from the first kernel's start to the last one's end, as rocprofv3 sees them (the
-    library launches every kernel with hipExtLaunchKernelGGL and the probe's event pair), or -1 when
-    the call launched nothing.  Same interface as a torch.cuda.Event pair's start.elapsed_time(end)."""
+    """The kernels of one entry-point call, timed on the device (bench.py's rooflines): opened right
+    before the call (fbn_probe_arm), closed right after (fbn_probe_disarm); elapsed_time() is the
+    span from the first kernel's start to the last one's end, as rocprofv3 sees them (the library
+    launches every kernel with hipExtLaunchKernelGGL and the probe's event pair), or -1 when the call
+    launched nothing.  While a step program is being recorded the arm / disarm are recorded calls:
+    every replay re-arms the slot, so after a replay the slot holds that replay's span.  Same
+    interface as a torch.cuda.Event pair's start.elapsed_time(end)."""
     _next = 0
 
     def __init__(self):
         self.slot = KernelProbe._next
         KernelProbe._next += 1
-        self.taken = False
-        call_raw("fbn_probe_arm", self.slot)
+        (call if recording() else call_raw)("fbn_probe_arm", self.slot)
 
     def done(self) -> None:
-        self.taken = bool(lib().fbn_probe_disarm())
+        (call if recording() else call_raw)("fbn_probe_disarm")
 
     def elapsed_time(self, _end=None) -> float:
-        return float(lib().fbn_probe_elapsed(self.slot)) if self.taken else -1.0
+        return float(lib().fbn_probe_elapsed(self.slot))
 
 
 class StepProgram:

@@ -18,19 +18,22 @@ extern "C" int fbn_version(void) { return 1; }
 // ---- bench probes: slot k is an event pair.  fbn_probe_arm(k) .. fbn_probe_disarm() brackets one
 // entry-point call: the first kernel the library launches in between records the start event at its
 // own start, every one records the stop event at its end (fbn_launch -> hipExtLaunchKernelGGL), so the
-// pair spans exactly the call's kernels -- no marker packets or dispatch latency around them.
+// pair spans exactly the call's kernels -- no marker packets or dispatch latency around them.  The
+// events carry no system-scope fence (timing only), so probes inside timed steps (recorded into step
+// programs) cost no cache writeback.
 #include <vector>
 namespace {
 std::vector<hipEvent_t> g_probe_ev;      // [2k] start, [2k + 1] stop
+std::vector<char> g_probe_taken;         // [k]: a launch recorded slot k since its last arm
 int g_probe_armed = -1;
-bool g_probe_first = false;
 }  // namespace
 
 bool fbn_probe_take(hipEvent_t* start, hipEvent_t* stop) {
   if (g_probe_armed < 0) return false;
-  *start = g_probe_first ? g_probe_ev[2 * g_probe_armed] : nullptr;
+  const bool first = !g_probe_taken[g_probe_armed];
+  *start = first ? g_probe_ev[2 * g_probe_armed] : nullptr;
   *stop = g_probe_ev[2 * g_probe_armed + 1];
-  g_probe_first = false;
+  g_probe_taken[g_probe_armed] = 1;
   return true;
 }
 
@@ -41,27 +44,26 @@ extern "C" int fbn_probe_arm(int slot) {
   }
   while ((int)g_probe_ev.size() < 2 * (slot + 1)) {
     hipEvent_t e;
-    if (hipEventCreate(&e) != hipSuccess) {
-      fbn_set_error("fbn_probe_arm: hipEventCreate failed");
+    if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) {
+      fbn_set_error("fbn_probe_arm: hipEventCreateWithFlags failed");
       return 2;
     }
     g_probe_ev.push_back(e);
   }
+  if ((int)g_probe_taken.size() <= slot) g_probe_taken.resize(slot + 1, 0);
   g_probe_armed = slot;
-  g_probe_first = true;
+  g_probe_taken[slot] = 0;
   return 0;
 }
 
-// 1 if a kernel launch took the armed slot (0: the call launched nothing); disarms it
 extern "C" int fbn_probe_disarm(void) {
-  const int taken = (g_probe_armed >= 0 && !g_probe_first) ? 1 : 0;
   g_probe_armed = -1;
-  return taken;
+  return 0;
 }
 
-// span of slot k's kernels in ms (after they completed), or -1
+// span of slot k's kernels in ms (after they completed), or -1 when no launch took the slot
 extern "C" float fbn_probe_elapsed(int slot) {
-  if (slot < 0 || 2 * slot + 1 >= (int)g_probe_ev.size()) return -1.f;
+  if (slot < 0 || slot >= (int)g_probe_taken.size() || !g_probe_taken[slot]) return -1.f;
   float ms = -1.f;
   if (hipEventElapsedTime(&ms, g_probe_ev[2 * slot], g_probe_ev[2 * slot + 1]) != hipSuccess) return -1.f;
   return ms;

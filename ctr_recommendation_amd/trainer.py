@@ -788,7 +788,8 @@ class FiBiNETTrainer:
 
     # ------------------------------------------------------------------ step programs (native step driver)
     def record_program(self, batch: Dict[str, torch.Tensor], labels: torch.Tensor,
-                       next_batch: Optional[Dict[str, torch.Tensor]] = None, pool=None) -> "_lib.StepProgram":
+                       next_batch: Optional[Dict[str, torch.Tensor]] = None, pool=None,
+                       probe: Optional[Dict[str, list]] = None) -> "_lib.StepProgram":
         """Run ONE training step on (batch, labels[, next_batch]) -- a real step, counted -- and record
         it as a step program (csrc/plan.cpp): its ~25 library calls and stream edges, replayed later
         by run_program() with one host call instead of ~0.4 ms of Python per step.
@@ -816,7 +817,9 @@ class FiBiNETTrainer:
         self._recording = True
         try:
             with prog.recording(pool):
-                self.step(batch, labels, next_batch=next_batch)
+                # probe (bench): kernel-span probes recorded into the program -- every replay re-arms
+                # them, so after a replay each holds that replay's kernel span
+                self.step(batch, labels, next_batch=next_batch, probe=probe)
         finally:
             self._recording = False
         # the claims of the recorded step came from the pre-claims the previous step posted for this

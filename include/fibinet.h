@@ -36,8 +36,9 @@ extern "C" {
 const char* fbn_last_error(void);
 /* Kernel-span probes (bench.py's rooflines): between fbn_probe_arm(slot) and fbn_probe_disarm() the
  * library's kernel launches record slot's event pair -- start at the first kernel's start, stop at
- * each kernel's end (hipExtLaunchKernelGGL).  fbn_probe_disarm: 1 if a kernel took the slot;
- * fbn_probe_elapsed(slot): the span in ms once those kernels completed, or -1. */
+ * each kernel's end (hipExtLaunchKernelGGL; timing events without the system-scope fence).  Both are
+ * ordinary entry points, so a step program can record them (probes inside the timed replays).
+ * fbn_probe_elapsed(slot): the span in ms once those kernels completed, -1 if none took the slot. */
 int fbn_probe_arm(int slot);
 int fbn_probe_disarm(void);
 float fbn_probe_elapsed(int slot);

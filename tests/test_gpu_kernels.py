@@ -404,14 +404,14 @@ def test_kernel_span_probe(hip_device):
         kp.done()
         e1.record()
         torch.cuda.synchronize()
-        assert kp.taken
+        assert kp.elapsed_time() > 0
         spans.append(kp.elapsed_time())
         outer.append(e0.elapsed_time(e1))
     assert all(0 < s <= o for s, o in zip(spans, outer)), (spans, outer)
     empty = _lib.KernelProbe()
     ops.gemm(A, W, C, 0, N, K, K, K, N, False, True)          # M = 0: no launch
     empty.done()
-    assert not empty.taken and empty.elapsed_time() == -1.0
+    assert empty.elapsed_time() == -1.0
     ops.gemm(A, W, C, M, N, K, K, K, N, False, True)          # unarmed: the last slot stays as it was
     torch.cuda.synchronize()
     assert kp.elapsed_time() == spans[-1]
