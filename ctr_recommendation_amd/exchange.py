@@ -68,7 +68,9 @@ class NativeComm:
 
     def alltoallv(self, out: torch.Tensor, inp: torch.Tensor, recv_counts, send_counts) -> None:
         """Rows (dim 0) of inp to the ranks, send_counts[r] to rank r; recv_counts[r] rows from r."""
-        row_bytes = inp.element_size() * (inp[0].numel() if inp.dim() > 1 else 1)
+        row_bytes = inp.element_size()
+        for n in inp.shape[1:]:          # (an empty inp -- a rank asked for no rows -- has shape (0, d))
+            row_bytes *= n
         sc = (ctypes.c_int * self.world)(*send_counts)
         rc = (ctypes.c_int * self.world)(*recv_counts)
         call("fbn_comm_alltoallv", self.handle, ptr(inp), sc, ptr(out), rc, row_bytes,
