@@ -173,6 +173,7 @@ class RowExchange:
         self.rows_buf = None
         self.send_buf = None
         self._pending = None        # gradient-row all-to-all issued by backward_start()
+        self._comm_stream = None    # native RCCL, early gradient exchange: its stream
 
     @property
     def rows_lo(self) -> int:
@@ -333,7 +334,7 @@ class RowExchange:
         self.backward_start(sendbuf, out)
         return self.backward_finish()
 
-    def backward_start(self, sendbuf: torch.Tensor, out: Optional[torch.Tensor] = None) -> None:
+    def backward_start(self, sendbuf: torch.Tensor, out: Optional[torch.Tensor] = None, early: bool = False) -> None:
         """Issue the gradient-row all-to-all now, asynchronously on the process group's own stream
         (the caller's stream goes on with other work); backward_finish() makes the caller's stream
         wait for it and widens bf16 wire rows."""
@@ -343,7 +344,21 @@ class RowExchange:
         wire = grad if sendbuf.dtype == torch.float32 else \
             torch.empty((n_recv, self.d), dtype=sendbuf.dtype, device=sendbuf.device)
         work = None
-        if self.stage_on_cpu or self.comm is not None:       # host-staged, or on this stream
+        if self.comm is not None and early:
+            # RCCL on a stream of its own, right after the fields backward: the exchange runs beside
+            # the rest of the backward (the grouped weight gradients); backward_finish() joins it
+            cur = torch.cuda.current_stream(sendbuf.device)
+            if self._comm_stream is None:
+                self._comm_stream = torch.cuda.Stream(device=sendbuf.device)
+            cs = self._comm_stream
+            cs.wait_stream(cur)
+            with torch.cuda.stream(cs):
+                self._a2a(wire, sendbuf, self.recv_counts, self.send_counts)
+            work = torch.cuda.Event()
+            work.record(cs)
+            for t in (wire, grad, sendbuf):
+                t.record_stream(cs)
+        elif self.stage_on_cpu or self.comm is not None:       # host-staged, or on this stream
             self._a2a(wire, sendbuf, self.recv_counts, self.send_counts)
         else:
             work = dist.all_to_all_single(wire, sendbuf, self.recv_counts, self.send_counts, group=self.group,
@@ -353,7 +368,9 @@ class RowExchange:
     def backward_finish(self) -> torch.Tensor:
         work, wire, grad = self._pending
         self._pending = None
-        if work is not None:
+        if isinstance(work, torch.cuda.Event):              # native RCCL on the exchange's own stream
+            torch.cuda.current_stream(grad.device).wait_event(work)
+        elif work is not None:
             work.wait()
         if wire is not grad:
             self.k.widen(wire, grad)

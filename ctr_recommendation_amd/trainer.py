@@ -681,7 +681,7 @@ class FiBiNETTrainer:
                          extra_sums=[(a["loss_terms"], B, 1, self.loss, 1.0 / ntot)], probe=probe,
                          hooks=bhooks)
         dense_work = None
-        if self.sharded and self._early_grad_xchg():
+        if self.sharded and self._early_grad_xchg() and self.native_comm is None:
             # the dense gradients are final once the compute is: their all-reduce goes out now,
             # asynchronously behind the gradient-row all-to-all on the process group's stream,
             # beside the owner's widen / fold / norm; only the loss and the table-gradient sum of
@@ -899,16 +899,16 @@ class FiBiNETTrainer:
         return None
 
     def _early_grad_xchg(self) -> bool:
-        # torch.distributed's asynchronous collectives only: with RCCL on the step's stream the
-        # gradient rows already leave in stream order, right after the backward
-        return self.early_grad_xchg and self.xchg is not None and not self.stage_on_cpu and self.native_comm is None
+        # the gradient-row all-to-all issued right after the fields backward: native RCCL on the
+        # exchange's own stream; torch.distributed asynchronous on its stream (+ the dense all-reduce)
+        return self.early_grad_xchg and self.xchg is not None and not self.stage_on_cpu
 
     def _grad_xchg_start(self) -> None:
         """N > 1: the per-entry gradient rows are complete once the fields backward has run: their
         all-to-all starts there, on the process group's stream, beside the rest of the backward
         (the last parameter reductions and the mm_proj weight gradient)."""
         x = self.xchg
-        x.backward_start(x.send_buf[:sum(x.send_counts)], out=self._grad_slot())
+        x.backward_start(x.send_buf[:sum(x.send_counts)], out=self._grad_slot(), early=True)
 
     def _bn_n(self, ntot: int, B: int) -> int:
         """Samples one BatchNorm normalises over: the global batch (SyncBN) or this rank's slice."""

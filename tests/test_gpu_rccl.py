@@ -52,13 +52,15 @@ def _worker(port, q):
             # (shard, early): the single GPU; the sharded step with RCCL on the step's stream (the
             # default, exchange.NativeComm); torch.distributed's collectives with the early
             # (asynchronous) gradient all-to-all issued after the fields backward
-            for shard, early in ((False, False), (True, False), (True, True)):
-                os.environ["FBN_NATIVE_COMM"] = "0" if early else "1"
+            # (and the early gradient exchange with native RCCL on the exchange's own stream)
+            for shard, early, native in ((False, False, True), (True, False, True), (True, True, False),
+                                         (True, True, True)):
+                os.environ["FBN_NATIVE_COMM"] = "1" if native else "0"
                 tr = FiBiNETTrainer(cfg, total_steps=20, batch_size=B, device=dev, init_state=
                                     {k: v.clone() for k, v in init.items()}, shard=shard)
                 tr.early_grad_xchg = early
                 assert (tr.xchg is not None) == shard
-                assert (tr.native_comm is not None) == (shard and not early)
+                assert (tr.native_comm is not None) == (shard and native)
                 assert tr._early_grad_xchg() == early
                 p_init = tr.flat_p.cpu().clone()
                 if shard:
@@ -67,7 +69,7 @@ def _worker(port, q):
                 tr.flush()
                 tr.check_ids()
                 res.append((losses, tr.E.cpu().clone(), tr.flat_p.cpu().clone(), p_init))
-            (l0, e0, p0, q0), (l1, e1, p1, _), (l2, e2, p2, _) = res
+            (l0, e0, p0, q0), (l1, e1, p1, _), (l2, e2, p2, _), (l3, e3, p3, _) = res
             # dense parameters: the difference relative to the 6 steps' displacement (Adam's
             # normalised step turns last-bit gradient differences into small absolute ones)
             out[dtype] = (l0, l1, float((e0 - e1).abs().max()), float((p0 - p1).norm() / (p0 - q0).norm()),
@@ -76,6 +78,8 @@ def _worker(port, q):
             # duplicate fold's float atomics make two sharded runs differ in the last bits anyway)
             out[dtype + "_early"] = (l0, l2, float((e0 - e2).abs().max()), float((p0 - p2).norm() / (p0 - q0).norm()),
                                      float(e0.abs().max()))
+            out[dtype + "_early_native"] = (l0, l3, float((e0 - e3).abs().max()),
+                                            float((p0 - p3).norm() / (p0 - q0).norm()), float(e0.abs().max()))
         q.put(("ok", out))
     except Exception as e:   # report, then re-raise in the child
         q.put((repr(e), None))
@@ -96,11 +100,12 @@ def test_sharded_path_over_rccl_matches_single_gpu(hip_device):
     for a, b in zip(l0, l1):
         assert abs(a - b) <= 1e-5 * max(1.0, abs(a)), (l0, l1)
     assert de <= 1e-5 * max(1.0, e_max) and dp <= 1e-3, (de, dp)
-    l0, l1, de, dp, e_max = out["fp32_early"]
-    for a, b in zip(l0, l1):
-        assert abs(a - b) <= 1e-5 * max(1.0, abs(a)), (l0, l1)
-    assert de <= 1e-5 * max(1.0, e_max) and dp <= 1e-3, (de, dp)
-    for key in ("bf16", "bf16_early"):
+    for key in ("fp32_early", "fp32_early_native"):
+        l0, l1, de, dp, e_max = out[key]
+        for a, b in zip(l0, l1):
+            assert abs(a - b) <= 1e-5 * max(1.0, abs(a)), (key, l0, l1)
+        assert de <= 1e-5 * max(1.0, e_max) and dp <= 1e-3, (key, de, dp)
+    for key in ("bf16", "bf16_early", "bf16_early_native"):
         l0, l1, de, dp, _ = out[key]
         # bf16 wire: the looked-up rows are rounded to bf16 before the fields kernel (the single-GPU
         # bf16 path reads f32 rows), so the two agree to bf16 rounding, not bit for bit
