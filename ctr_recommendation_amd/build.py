@@ -23,13 +23,13 @@ FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-re
          "-I", CSRC, "-I", os.path.join(ROOT, "include")]
 
 
-def _compile(src: str) -> str:
+def _compile(src: str, build_dir: str = BUILD, defines=()) -> str:
     path = os.path.join(CSRC, src)
-    obj = os.path.join(BUILD, src + ".o")
+    obj = os.path.join(build_dir, src + ".o")
     deps = [path] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
         return obj
-    cmd = [HIPCC] + FLAGS + ["-c", path, "-o", obj]
+    cmd = [HIPCC] + FLAGS + [f"-D{d}" for d in defines] + ["-c", path, "-o", obj]
     if src.endswith(".cpp"):
         cmd = [HIPCC, "-O3", "-fPIC", "-std=c++17", "-c", path, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -53,6 +53,36 @@ def build(verbose: bool = True) -> str:
     return LIB
 
 
+# A/B builds of the library (never the product): name -> preprocessor defines.  Built into
+# tools/variants/libfibinet_hip_<name>.so and selected with FBN_LIB_PATH (_lib.py).
+VARIANTS = {
+    # table and dense Adam with correctly rounded sqrt / division, unfused (parity bisection)
+    "ieee": ("FBN_ADAM_IEEE",),
+}
+
+
+def build_variant(name: str, verbose: bool = True) -> str:
+    defines = VARIANTS[name]
+    bdir = os.path.join(ROOT, "build", "variant_" + name)
+    os.makedirs(bdir, exist_ok=True)
+    with ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
+        objs = list(ex.map(lambda s: _compile(s, bdir, defines), SOURCES))
+    out = os.path.join(ROOT, "tools", "variants", f"libfibinet_hip_{name}.so")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(o) for o in objs):
+        r = subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs + ["-ldl"],
+                           capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr}")
+    if verbose:
+        print(f"built {out}")
+    return out
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1:
+        for v in sys.argv[1:]:
+            build_variant(v)
+        sys.exit(0)
     build()
     sys.exit(0)

@@ -100,6 +100,15 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <bool DW>
 __device__ __forceinline__ float adam_tab1(float p, float& m, float& v, float g, float wd, float b2, float omb2,
                                            float eps, const AdamConsts& k) {
+#ifdef FBN_ADAM_IEEE
+  // A/B build only (build.build_variant("ieee")): unfused, correctly rounded sqrt and division --
+  // the parity bisection's IEEE arm (profiles/r05_auc_bisect.json); adam_tabk has the same form
+  g = g + wd * p;
+  if (DW) p = p * k.dmul;
+  m = m + k.w1 * (g - m);
+  v = v * b2 + (omb2 * g) * g;
+  return p + (k.nss * m) / (sqrtf(v) * k.rbc2s + eps);
+#endif
   g = __builtin_fmaf(wd, p, g);
   if (DW) p = p * k.dmul;
   m = __builtin_fmaf(k.w1, g - m, m);
@@ -1227,6 +1236,18 @@ __device__ __forceinline__ void adam_tabk(typename FVec<N>::T& pp, typename FVec
                                           f32x4 k) {
   typedef typename FVec<N>::T V;
   const V vwd = wd, vb2 = b2, vomb2 = omb2, veps = eps, w1 = k[0], nss = k[1], rb = k[2];
+#ifdef FBN_ADAM_IEEE
+  {
+    const V g = gg + vwd * pp;
+    V p = pp;
+    if (DW) p = p * (V)k[3];
+    mm = mm + w1 * (g - mm);
+    vv = vv * vb2 + (vomb2 * g) * g;
+#pragma unroll
+    for (int e = 0; e < N; ++e) pp[e] = p[e] + (k[1] * mm[e]) / (sqrtf(vv[e]) * k[2] + eps);
+    return;
+  }
+#endif
   const V g = __builtin_elementwise_fma(vwd, pp, gg);
   V p = pp;
   if (DW) p = p * (V)k[3];

@@ -91,10 +91,18 @@ class NativeComm:
 
 
 def native_comm_wanted(device, group=None, stage_on_cpu: bool = False) -> bool:
-    """RCCL on the step's stream: a HIP device, an nccl (= RCCL) process group, unless
-    FBN_NATIVE_COMM=0 (then torch.distributed's collectives, on its own stream)."""
-    return (torch.device(device).type == "cuda" and not stage_on_cpu and dist.is_initialized()
-            and dist.get_backend(group) == "nccl" and os.environ.get("FBN_NATIVE_COMM", "1") != "0")
+    """RCCL on the step's stream: a HIP device and an nccl (= RCCL) process group.  FBN_NATIVE_COMM
+    = 1: always; 0: never (torch.distributed's collectives, on its own stream); "auto" (default): at
+    world = 1 only (the sharded smoke job, where it is tested against the torch.distributed path).
+    At world > 1 the native communicators have never run on hardware (RCCL refuses two ranks on
+    one device, and no multi-GPU box was available), and they bypass torch's watchdog timeouts, so
+    the default keeps torch.distributed's collectives there until a multi-GPU run shows loss and
+    table parity between the two."""
+    mode = os.environ.get("FBN_NATIVE_COMM", "auto")
+    if not (torch.device(device).type == "cuda" and not stage_on_cpu and dist.is_initialized()
+            and dist.get_backend(group) == "nccl") or mode == "0":
+        return False
+    return mode == "1" or dist.get_world_size(group) == 1
 
 
 class HipExchangeKernels:

@@ -161,7 +161,8 @@ def main(argv=None):
     ap.add_argument("--epochs", type=int)
     ap.add_argument("--checkpoint")
     args = ap.parse_args(argv)
-    run(args.config, epochs=args.epochs, checkpoint=args.checkpoint)
+    out = run(args.config, epochs=args.epochs, checkpoint=args.checkpoint)
+    out["trainer"].close()
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         import torch.distributed as dist
         dist.barrier()

@@ -825,6 +825,7 @@ class FiBiNETTrainer:
         # the claims of the recorded step came from the pre-claims the previous step posted for this
         # very batch (a replay is valid only after such a step), and the step posted its next batch's
         prog.pre_needed, prog.batch_key, prog.pre_key_after = self._used_pre, key, self._pre_key
+        prog.batch_ids = (batch["item_id"], seq if seq is not None and seq.shape[1] else None)
         # the tensors the recorded calls address
         prog.keep += [batch, labels, next_batch, dict(self.acts)]
         return prog
@@ -834,6 +835,12 @@ class FiBiNETTrainer:
         if self.host_step >= self.total_steps:
             raise ValueError(f"Tried to step {self.host_step + 1} times. The specified number of total steps is "
                              f"{self.total_steps}")
+        if _batch_key(*prog.batch_ids) != prog.batch_key:
+            # the ids were rewritten in place since the recording (copy_ bumps the version counter):
+            # the pre-claims the previous step posted, and the claims this replay would take from
+            # them, are for the old contents -- refuse rather than lose row claims
+            raise RuntimeError("step program replayed over batch tensors modified since it was recorded "
+                               "(re-record it, or pass fresh tensors to step())")
         if prog.pre_needed and self._pre_key != prog.batch_key:
             # its recorded claims read pre-claims the previous step did not post for this batch (a
             # replay out of the recorded order): refuse rather than lose row claims
@@ -919,6 +926,19 @@ class FiBiNETTrainer:
         if not self.deferred:
             return (None, None, None, 0, 0)
         return (ptr(self.pend), ptr(self.ring), ptr(self.coef_hist), self._ring_stride(), self.ring_n)
+
+    def close(self) -> None:
+        """Destroy the native RCCL communicators (the step's and the routing one) and their proxy
+        threads; the trainer cannot step at N > 1 afterwards.  Idempotent."""
+        if self.xchg is not None and self.xchg.route_comm is not None:
+            self.xchg.route_comm.close()
+            self.xchg.route_comm = None
+        if self.native_comm is not None:
+            self.native_comm.close()
+            self.native_comm = None
+            self.coll.comm = None
+            if self.xchg is not None:
+                self.xchg.comm = None
 
     # ------------------------------------------------------------------ inference
     def flush(self) -> None:
@@ -1078,10 +1098,16 @@ class FiBiNETTrainer:
         full table take their block from it."""
         self.flush()
         if self.world > 1:
-            have = torch.tensor([int(TABLE in sd)], dtype=torch.int32,
+            # [ranks holding the table, rank 0 holds it]: every rank decides (and raises) together --
+            # a rank-0-only KeyError would leave the others blocked in _scatter_table's recv
+            have = torch.tensor([int(TABLE in sd), int(self.rank == 0 and TABLE in sd)], dtype=torch.int32,
                                 device="cpu" if self.stage_on_cpu else self.device)
-            dist.all_reduce(have, op=dist.ReduceOp.MIN, group=self.group)
-            if not int(have.item()):
+            dist.all_reduce(have, group=self.group)
+            n_have, rank0_has = (int(x) for x in have.tolist())
+            if n_have < self.world:
+                if not rank0_has:
+                    raise KeyError(f"load_state_dict at N > 1: rank 0's dict must hold {TABLE!r} (state_dict() "
+                                   f"gives it to rank 0; state_dict(all_ranks=True) to every rank)")
                 self._scatter_table(sd.get(TABLE) if self.rank == 0 else None)
         for k in self.key_order:
             if k == TABLE:

@@ -197,8 +197,80 @@ def test_hot_row_staging_is_bit_identical(hip_device, d, zipf, tau, monkeypatch)
     hip = build_model(None, {"embedding_dim": d, "vocab_size": V}).to(hip_device).eval()
     (batch, _), = make_device_batches(1, B, V, 20, hip_device, seed=9, zipf=zipf)
     with torch.no_grad():
+        pn = hip(batch)          # the default one-wave-per-sample gather (fields_fwd2_kernel)
+        # the staging is built on the two-samples-per-wave gather: it is the bit-identity reference
+        monkeypatch.setenv("FBN_FIELDS_V", "1")
         p0 = hip(batch)
         monkeypatch.setattr(ops, "_GATHER_HOT", tau)
         p1 = hip(batch)
         p2 = hip(batch)          # counts and the list were cleared after the first staged pass
     assert torch.equal(p0, p1) and torch.equal(p0, p2)
+    # the two gathers sum a sample's history rows in different orders (slot order vs two row groups)
+    assert (pn - p0).abs().max().item() <= 1e-5
+
+
+@pytest.mark.parametrize("d", [16, 32, 64, 128, 256])
+@pytest.mark.parametrize("mode", ["table", "rows_f32", "rows_bf16"])
+def test_gather_one_wave_per_sample_matches_two_per_wave(hip_device, d, mode, monkeypatch):
+    """The one-wave-per-sample gather (fields_fwd2_kernel: compacted live history slots, row groups,
+    butterfly of the group sums) against the two-samples-per-wave one (FBN_FIELDS_V=1) on every
+    output of fbn_fields_fwd, reading the table (mode 0) or an exchanged row buffer through pos
+    (modes 1 / 2): ids, counts and SENET weights identical, the fields within float rounding of
+    the history sums' order; an all-padding sample and a history of one live slot included."""
+    import ctypes
+    from ctr_recommendation_amd._lib import call, ptr
+    V, B, L = 5000, 300, 20
+    g = torch.Generator().manual_seed(d)
+    item = torch.randint(1, V, (B,), generator=g)
+    seq = torch.randint(1, V, (B, L), generator=g)
+    seq[torch.rand((B, L), generator=g) < 0.5] = 0
+    seq[0] = 0                                  # all padding
+    seq[1] = 0
+    seq[1, 7] = 11                              # one live slot, mid-history
+    likes = torch.randint(0, 11, (B,), generator=g)
+    views = torch.randint(0, 11, (B,), generator=g)
+    dev = hip_device
+    f = lambda t: t.to(dev).contiguous()
+    item, seq, likes, views = f(item), f(seq), f(likes), f(views)
+    hmm = f(torch.randn(B, d, generator=g))
+    ln_g, ln_b = f(torch.rand(d, generator=g) + 0.5), f(torch.randn(d, generator=g) * 0.1)
+    cate = f(torch.randn(11, d, generator=g))
+    table = f(torch.randn(V, d, generator=g))
+    w1, b1 = f(torch.randn(3, 6, generator=g)), f(torch.randn(3, generator=g))
+    w2, b2 = f(torch.randn(6, 3, generator=g)), f(torch.randn(6, generator=g))
+    pos = None
+    rows = table
+    if mode != "table":
+        # every (sample, slot) gets its own row of a shuffled row buffer; padding slots -1
+        ids = torch.cat([item[:, None], seq], 1)
+        perm = torch.randperm(B * (L + 1), generator=g).to(dev).view(B, L + 1).int()
+        pos = torch.where(ids > 0, perm, torch.full_like(perm, -1)).contiguous()
+        rows = torch.zeros(B * (L + 1), d, device=dev)
+        live = pos >= 0
+        rows[pos[live].long()] = table[ids[live]]
+        if mode == "rows_bf16":
+            rows = rows.bfloat16()
+
+    def run():
+        out = {"X": torch.full((B, 2, d), 7.0, device=dev), "Vc": torch.full((B, 5, d), 7.0, device=dev),
+               "a": torch.zeros(B, 6, device=dev), "cnt": torch.zeros(B, device=dev)}
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        call("fbn_fields_fwd", ptr(item), ptr(seq), ptr(likes), ptr(views), ptr(hmm), ptr(ln_g), ptr(ln_b), 1e-5,
+             ptr(cate), 11, ptr(rows), V if mode == "table" else B * (L + 1), ptr(pos), ptr(w1), ptr(b1), ptr(w2),
+             ptr(b2), 3, ptr(out["X"]), ptr(out["Vc"]), None, None, 0, 0, ptr(out["a"]), ptr(out["cnt"]), ptr(err),
+             None, None, B, L, d, int(mode == "rows_bf16"), torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize()
+        assert int(err.item()) == 0
+        return out
+    new = run()
+    monkeypatch.setenv("FBN_FIELDS_V", "1")
+    old = run()
+    assert torch.equal(new["cnt"], old["cnt"])
+    assert new["cnt"][0].item() == 1.0 and new["cnt"][1].item() == 1.0
+    assert torch.equal(new["X"][:, 0], old["X"][:, 0])          # the item row: a plain copy
+    for k in ("X", "Vc", "a"):
+        assert (new[k] - old[k]).abs().max().item() <= 2e-6 * max(1.0, old[k].abs().max().item()), k
+    # all padding: the history mean is exactly zero; one live slot: exactly that row
+    assert torch.all(new["X"][0, 1] == 0)
+    ref1 = (rows[pos[1, 8].long()].float() if mode != "table" else table[11])
+    assert torch.equal(new["X"][1, 1], ref1)

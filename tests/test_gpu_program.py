@@ -31,12 +31,16 @@ def _unique_ids(b, V, g, pool):
     return b
 
 
-@pytest.mark.parametrize("d,dtype,det", [(128, "bf16", False), (128, "fp32", False), (16, "fp32", False),
-                                         (16, "bf16", False), (128, "bf16_fwd", False), (128, "bf16", True)])
-def test_program_replay_bit_identical_to_eager(hip_device, d, dtype, det):
+@pytest.mark.parametrize("d,dtype,det,shared", [(128, "bf16", False, False), (128, "fp32", False, False),
+                                                (16, "fp32", False, False), (16, "bf16", False, False),
+                                                (128, "bf16_fwd", False, False), (128, "bf16", True, False),
+                                                (128, "bf16", False, True), (128, "fp32", False, True),
+                                                (16, "fp32", False, True)])
+def test_program_replay_bit_identical_to_eager(hip_device, d, dtype, det, shared):
     """det=False: the bench's stream structure (duplicate fold on the side stream, float atomics),
     ids unique within a batch; det=True: deterministic mode (fixed-point fold on the main stream)
-    with ids repeated inside batches."""
+    with ids repeated inside batches.  shared: every program recorded into ONE memory pool, as
+    bench.py records them (a temporary one recording freed may back a tensor another keeps)."""
     V, B, nb, steps = 40000, 512, 4, 14
     cfg = {"embedding_dim": d, "vocab_size": V, "compute_dtype": dtype}
     torch.manual_seed(0)
@@ -52,6 +56,7 @@ def test_program_replay_bit_identical_to_eager(hip_device, d, dtype, det):
     eager = _trainer(cfg, init, B, hip_device, det)
     prog_tr = _trainer(cfg, init, B, hip_device, det)
     progs = {}
+    mem_pool = torch.cuda.MemPool() if shared else None
     le, lp = [], []
     # one step ahead of the first recording that prefetches (and pre-claims) its batch, as a replay
     # of program 0 will always follow one (program 3's step).  Its own claims have no pre-claims
@@ -68,7 +73,7 @@ def test_program_replay_bit_identical_to_eager(hip_device, d, dtype, det):
         le.append(eager.step(b, y, next_batch=nxt).item())
         j = i % nb
         if j not in progs:
-            progs[j] = prog_tr.record_program(b, y, next_batch=nxt)      # a real step, recorded
+            progs[j] = prog_tr.record_program(b, y, next_batch=nxt, pool=mem_pool)   # a real step, recorded
         elif i == 9:
             prog_tr.step(b, y, next_batch=nxt)                           # an eager step between replays
         else:
@@ -86,6 +91,25 @@ def test_program_replay_bit_identical_to_eager(hip_device, d, dtype, det):
     # out of the recorded order (the previous step prefetched another batch): refused
     with pytest.raises(RuntimeError, match="out of order"):
         prog_tr.run_program(progs[(steps + 1) % nb])
+
+
+def test_program_refuses_rewritten_batch(hip_device):
+    """A batch whose ids were rewritten in place (copy_) since its program was recorded is refused:
+    the previous replay's pre-claims name the old ids."""
+    V, B = 40000, 256
+    cfg = {"embedding_dim": 128, "vocab_size": V, "compute_dtype": "bf16"}
+    torch.manual_seed(0)
+    init = oracle_build(None, dict(cfg, honour_config=False)).state_dict()
+    tr = _trainer(cfg, init, B, hip_device)
+    bs = [tuple(t.to(hip_device) if not isinstance(t, dict) else {k: v.to(hip_device) for k, v in t.items()}
+                for t in make_batch(80 + j, B, V)) for j in range(3)]
+    tr.step(*bs[0], next_batch=bs[1][0])
+    p1 = tr.record_program(*bs[1], next_batch=bs[2][0])
+    p2 = tr.record_program(*bs[2], next_batch=bs[1][0])
+    tr.run_program(p1)
+    bs[2][0]["item_id"].copy_(bs[0][0]["item_id"])            # new contents, same buffer
+    with pytest.raises(RuntimeError, match="modified since it was recorded"):
+        tr.run_program(p2)
 
 
 def test_program_refuses_unsupported_paths(hip_device):

@@ -69,6 +69,9 @@ def _worker(port, q):
                 tr.flush()
                 tr.check_ids()
                 res.append((losses, tr.E.cpu().clone(), tr.flat_p.cpu().clone(), p_init))
+                tr.close()                       # the communicators and their proxy threads
+                tr.close()                       # idempotent
+                assert tr.native_comm is None
             (l0, e0, p0, q0), (l1, e1, p1, _), (l2, e2, p2, _), (l3, e3, p3, _) = res
             # dense parameters: the difference relative to the 6 steps' displacement (Adam's
             # normalised step turns last-bit gradient differences into small absolute ones)

@@ -117,133 +117,49 @@ def test_launcher_end_to_end(cfg_path, hip_device, tmp_path):
     assert any("Valid AUC" in line for line in logs)
 
 
-PARITY_CONFIG = """
-base_expid: MM_FiBiNET_Run
-dataset_id: MicroLens_1M_x1
-dataset_config:
-  MicroLens_1M_x1:
-    data_format: parquet
-    train_data: {train}
-    valid_data: {valid}
-    item_info: {info}
-MM_FiBiNET_Run:
-  model: MM_FiBiNET
-  learning_rate: 0.001
-  batch_size: {bs}
-  embedding_dim: 16
-  max_len: 20
-  epochs: 2
-  weight_decay: 1e-5
-  seed: 2025
-  honour_config: true
-  net_dropout: 0.0
-  deterministic: true
-"""
-# the per-epoch valid-AUC bar of the training run vs the reference loop (see the test's docstring)
-RUN_AUC_BAR = 1e-4
-RUN_AUC_CAP = 1e-3
-
-
 @pytest.mark.gpu
-def test_launcher_auc_parity_vs_reference_loop(hip_device, tmp_path, monkeypatch):
+def test_launcher_auc_parity_vs_reference_loop(hip_device, tmp_path):
     """AUC parity of a TRAINING RUN (the metric's "AUC parity", src/train_fibinet.py:103-152 +
     src/utils.py:18-27): the launcher (python -m ctr_recommendation_amd.train: device loader, native
     trainer, valid AUC per epoch) for 2 epochs x 100 steps (51 200 train rows, batch 512, d 16,
-    dropout off) against the oracle's reference loop -- the restated BatchCollator over the SAME
-    epoch permutations, Adam(L2) + BCE + clip + OneCycleLR -- evaluated on the same 8 192 valid rows
-    each epoch (deterministic mode: fixed-point duplicate folds, so the run is reproducible).  Gate per
-    epoch: train loss within 1e-3 relative, |dAUC| <= 1e-3 against the fp32 and float64 loops; the
-    measured values sit beside the noise floors of equally valid fp32 implementations in
-    $FBN_PARITY_OUT/launcher_auc_parity.json."""
+    dropout off, deterministic duplicate folds) against the oracle's reference loop -- the restated
+    BatchCollator over the SAME epoch permutations, Adam(L2) + BCE + clip + OneCycleLR -- evaluated
+    on the same 8 192 valid rows each epoch.
+
+    Over 200 Adam steps any two correct fp32 implementations drift apart: Adam's first updates are
+    sign(g) * lr per element, so rounding-level gradient differences become lr-sized steps.  The
+    float64 loop is the arbiter and an ENSEMBLE of equally valid fp32 loops (torch's default Adam on
+    the default / 1 / 2 CPU threads, torch's fused Adam) measures the noise floor on this very data:
+    gate per epoch |AUC_hip - AUC_f64| <= max(1e-4, 2 x max over the ensemble of |AUC_k - AUC_f64|),
+    train loss within 1e-3 relative.  The committed record (tests/parity_bisect.py)
+    holds the gate it asserted."""
     import json
-    from ctr_recommendation_amd.data import write_microlens_parquet
-    from ctr_recommendation_amd.loader import ColumnarDataset, DeviceLoader
-    from ctr_recommendation_amd.train import load_config, run
-    from oracle.collate_ref import BatchCollatorRef, load_data
-    from oracle.fibinet_oracle import OracleTrainer, build_model as oracle_build, compute_auc
-    bs, n_train, n_valid, epochs = 512, 51200, 8192, 2
-    p = write_microlens_parquet(str(tmp_path / "data"), n_train=n_train, n_valid=n_valid, n_items=5000, seed=77)
-    cfg_path = str(tmp_path / "fibinet_config.yaml")
-    with open(cfg_path, "w") as f:
-        f.write(PARITY_CONFIG.format(train=p["train_data"], valid=p["valid_data"], info=p["item_info"], bs=bs))
-    _, dcfg, mcfg = load_config(cfg_path)
-    # the launcher's epoch permutations, as its train loader draws them (the valid loader's are aranges)
-    drawn = []
-    orig_perm = DeviceLoader._perm
-
-    def rec_perm(self):
-        p = orig_perm(self)
-        if self.shuffle:
-            drawn.append(p.cpu().numpy())
-        return p
-    monkeypatch.setattr(DeviceLoader, "_perm", rec_perm)
-    out = run(cfg_path, epochs=epochs, checkpoint=str(tmp_path / "ck" / "best.pth"), log=lambda *a, **k: None)
-    hist = out["history"]
-    perms = drawn
-    assert len(perms) == epochs
-    # the launcher's trained model on the valid rows (after the last epoch)
-    from ctr_recommendation_amd.loader import ItemInfoTable
-    vl = DeviceLoader(ColumnarDataset.from_parquet(dcfg["valid_data"], hip_device),
-                      ItemInfoTable.from_parquet(dcfg["item_info"], hip_device), bs, shuffle=False)
-    p_hip = np.concatenate([out["trainer"].predict(b).cpu().numpy() for b, _ in vl])
-    darray, ci = load_data(dcfg["train_data"])
-    coll = BatchCollatorRef(20, ci, dcfg["item_info"])
-    varray, vci = load_data(dcfg["valid_data"])
-    vcoll = BatchCollatorRef(20, vci, dcfg["item_info"])
-    steps_per_epoch = -(-n_train // bs)
-    cfg = {"embedding_dim": 16, "honour_config": True, "net_dropout": 0.0}
-
-    def reference_loop(f64):
-        torch.manual_seed(2025)                                       # set_seed before build_model (:33, :67)
-        ref = oracle_build(None, cfg, honour_config=True)
-        if f64:
-            ref = ref.double()
-        cast = (lambda t: t.double() if t.is_floating_point() else t) if f64 else (lambda t: t)
-        otr = OracleTrainer(ref, lr=1e-3, weight_decay=1e-5, total_steps=epochs * steps_per_epoch)
-        aucs, losses = [], []
-        for e in range(epochs):
-            tot = 0.0
-            for lo in range(0, n_train, bs):
-                rows = perms[e][lo:lo + bs]
-                b, y = coll([darray[i, :] for i in rows])
-                b = {k: cast(v.long() if k != "item_emb_d128" else v) for k, v in b.items()}
-                tot += otr.step(b, cast(y))[0]
-            losses.append(tot / steps_per_epoch)
-            ref.eval()
-            ys, ps = [], []
-            with torch.no_grad():
-                for lo in range(0, n_valid, bs):
-                    b, y = vcoll([varray[i, :] for i in range(lo, min(n_valid, lo + bs))])
-                    b = {k: cast(v.long() if k != "item_emb_d128" else v) for k, v in b.items()}
-                    ps.append(ref(b).float().numpy())
-                    ys.append(y.numpy())
-            aucs.append(compute_auc(np.concatenate(ys), np.concatenate(ps)))
-            ref.train()
-        return aucs, losses, np.concatenate(ps)
-
-    (a32, l32, p32), (a64, l64, _) = reference_loop(False), reference_loop(True)
-    rec = {"run": f"{epochs} epochs x {steps_per_epoch} steps, batch {bs}, d 16, {n_train} train / {n_valid} valid "
-                  f"rows (synthetic MicroLens-shaped parquet), dropout off", "bar": RUN_AUC_BAR, "epochs": []}
-    for e in range(epochs):
-        a_hip = hist[e][2]
-        rec["epochs"].append({"epoch": e + 1, "launcher_auc": a_hip, "oracle_auc": a32[e], "oracle_f64_auc": a64[e],
-                              "dAUC": abs(a_hip - a32[e]), "oracle_fp32_vs_f64_dAUC": abs(a32[e] - a64[e]),
-                              "launcher_vs_f64_dAUC": abs(a_hip - a64[e]), "train_loss": hist[e][1],
-                              "oracle_train_loss": l32[e], "oracle_f64_train_loss": l64[e]})
-    rec["final_valid_max_abs_dp"] = float(np.abs(p_hip - p32).max())
-    rec["final_valid_mean_abs_dp"] = float(np.abs(p_hip - p32).mean())
-    import os
+    from tests.parity_bisect import distances, ensemble, oracle_data, run_launcher, write_data
+    root = str(tmp_path)
+    p = write_data(root)
+    hip = run_launcher(p, root, deterministic=True)
+    assert len(hip["perms"]) == 2
+    res = ensemble(oracle_data(p), hip["perms"])
+    base = res["f64"]
+    members = [n for n in res if n != "f64"]
+    floor = [max(abs(res[n]["auc"][e] - base["auc"][e]) for n in members) for e in range(2)]
+    gate = [max(1e-4, 2 * f) for f in floor]
+    rec = {"run": "2 epochs x 100 steps, batch 512, d 16, 51 200 train / 8 192 valid rows (synthetic "
+                  "MicroLens-shaped parquet), dropout off, deterministic folds",
+           "bar": gate, "bar_rule": "max(1e-4, 2 x max_k |AUC_k - AUC_f64|) over the fp32 ensemble", "epochs": [],
+           "hip_vs_f64": distances(hip, base),
+           "oracle_vs_f64": {n: distances(res[n], base) for n in members}}
+    for e in range(2):
+        rec["epochs"].append({"epoch": e + 1, "launcher_auc": hip["auc"][e], "oracle_f64_auc": base["auc"][e],
+                              "oracle_auc": {n: res[n]["auc"][e] for n in members},
+                              "launcher_vs_f64_dAUC": abs(hip["auc"][e] - base["auc"][e]),
+                              "ensemble_max_dAUC_vs_f64": floor[e], "gate": gate[e],
+                              "train_loss": hip["loss"][e], "oracle_f64_train_loss": base["loss"][e]})
     outd = os.environ.get("FBN_PARITY_OUT", os.path.join("gpurun_out", "parity"))
     os.makedirs(outd, exist_ok=True)
     with open(os.path.join(outd, "launcher_auc_parity.json"), "w") as f:
         json.dump(rec, f, indent=1)
-    assert a32[-1] > 0.7, a32                                          # the run learned the planted signal
+    assert base["auc"][-1] > 0.7, base["auc"]                           # the run learned the planted signal
     for r in rec["epochs"]:
-        # over 100s of Adam steps any two fp32 implementations drift apart (sign-like updates of
-        # rounding-level gradients): the fp32 CPU oracle is 1.0e-4 / 1.4e-4 AUC from its float64 twin
-        # after epochs 1 / 2, torch's fused Adam 1.4e-4 / 7e-5 from the default one, and this launcher
-        # (deterministic mode) sits a few times further from the float64 loop (DESIGN.md §3a).  Gate:
-        # the train loss of every epoch within 1e-3 relative of the oracle's (same data, same learning),
-        # |dAUC| <= 1e-3 against both oracles; the values and the floors are recorded
-        assert abs(r["train_loss"] - r["oracle_train_loss"]) <= 1e-3 * r["oracle_train_loss"], rec
-        assert r["dAUC"] <= RUN_AUC_CAP and r["launcher_vs_f64_dAUC"] <= RUN_AUC_CAP, rec
+        assert abs(r["train_loss"] - r["oracle_f64_train_loss"]) <= 1e-3 * r["oracle_f64_train_loss"], rec
+        assert r["launcher_vs_f64_dAUC"] <= r["gate"], rec

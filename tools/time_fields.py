@@ -1,8 +1,12 @@
 """Time fbn_fields_fwd and fbn_fields_bwd (with its partial reductions) at C3 shapes (B=8192,
 d=128, L=20, V=1.25M, bf16), cycling 8 batches (their 88 MB of rows each do not stay in the
-Infinity Cache between uses); FBN_FIELDS_HCH selects the gather's rows-in-flight chunk,
-FBN_FIELDS_NOBUF=1 the global-load form, FBN_GATHER_HOT=<tau> the hot-row LDS staging; ZIPF=<s>
-draws the ids from Zipf(s) (SURVEY 8(d)'s popularity skew)."""
+Infinity Cache between uses); kernel spans from the library's kernel probes.
+
+Arms (interleaved in one process, ROUNDS rounds; each arm sets environment knobs the library reads
+per call), e.g.
+    python tools/time_fields.py "v1:FBN_FIELDS_V=1" "v2:" "v2_hc10:FBN_FIELDS_HC=10"
+Knobs: FBN_FIELDS_V=1 the two-samples-per-wave gather, FBN_FIELDS_HC the one-wave-per-sample
+gather's rows in flight per row group, FBN_FIELDS_HCH / FBN_FIELDS_NOBUF the old one's, FBN_GATHER_HOT=<tau> hot-row LDS staging; env ZIPF=<s> draws Zipf(s) ids, D / B the shape."""
 import os
 import sys
 
@@ -14,7 +18,10 @@ from ctr_recommendation_amd.data import make_device_batches
 from ctr_recommendation_amd.model_fibinet import build_model
 
 dev = torch.device("cuda", 0)
-B, d, L, V = 8192, 128, 20, 1_250_000
+d = int(os.environ.get("D", "128"))
+B = int(os.environ.get("B", "8192"))
+L, V = 20, int(os.environ.get("V", "1250000"))
+ROUNDS = int(os.environ.get("ROUNDS", "4"))
 cfg = {"embedding_dim": d, "vocab_size": 4}
 small = build_model(None, cfg).state_dict()
 p = {k: v.to(dev) for k, v in small.items()}
@@ -23,24 +30,35 @@ g = {k: torch.zeros_like(v) for k, v in p.items() if v.is_floating_point()}
 ZIPF = float(os.environ.get("ZIPF", "0"))
 batches = make_device_batches(8, B, V, L, dev, seed=3, zipf=ZIPF)
 gvec = torch.zeros((B, 2, d), device=dev)
-a = {}
 fc = ops.FwdConfig(d=d, L=L, training=True, p_drop=0.0, bf16=True, bilinear_each=False, R=3)
-probe = {}
-for i in range(30):
-    batch, labels = batches[i % len(batches)]
-    torch.cuda._sleep(2_000_000)
-    a = ops.forward(p, batch, fc, None, acts=a, probe=probe, labels=labels, loss_denom=float(B))
-    ops.backward(p, batch, a, a["gout"], g, fc, gvec=gvec, probe=probe)
-torch.cuda.synchronize()
-
-
-def avg(name):
-    ev = probe[name][10:]
-    return sum(s.elapsed_time(e) for s, e in ev) / len(ev)
-
-
-fwd, bwd = avg("fields_fwd"), avg("fields_bwd")
+arms = [a.split(":", 1) for a in (sys.argv[1:] or ["default:"])]
+knobs = sorted({kv.split("=")[0] for _, spec in arms for kv in spec.split(",") if kv})
+res = {name: {"fwd": [], "bwd": []} for name, _ in arms}
+a = {}
+for rnd in range(ROUNDS):
+    for name, spec in arms:
+        for k in knobs:
+            os.environ.pop(k, None)
+        for kv in (x for x in spec.split(",") if x):
+            k, v = kv.split("=")
+            os.environ[k] = v
+        probe = {}
+        for i in range(20):
+            batch, labels = batches[i % len(batches)]
+            torch.cuda._sleep(1_000_000)
+            a = ops.forward(p, batch, fc, None, acts=a, probe=probe, labels=labels, loss_denom=float(B))
+            ops.backward(p, batch, a, a["gout"], g, fc, gvec=gvec, probe=probe)
+        torch.cuda.synchronize()
+        for key, pn in (("fwd", "fields_fwd"), ("bwd", "fields_bwd")):
+            ev = probe[pn][5:]
+            res[name][key].append(sum(s.elapsed_time(e) for s, e in ev) / len(ev))
+for k in knobs:
+    os.environ.pop(k, None)
 byts = ((L + 1) * d * 4 + (L + 3) * 8 + 4 * d * 4) * B
-print(f"zipf={ZIPF} HCH={os.environ.get('FBN_FIELDS_HCH', 'default')} nobuf={os.environ.get('FBN_FIELDS_NOBUF', 0)} "
-      f"hot={os.environ.get('FBN_GATHER_HOT', 0)}: fields_fwd {fwd * 1e3:.1f} us ({byts / fwd / 1e6 / 8000:.3f} "
-      f"of 8 TB/s)  fields_bwd {bwd * 1e3:.1f} us")
+for name, spec in arms:
+    f = sorted(res[name]["fwd"])
+    bw = sorted(res[name]["bwd"])
+    fm = f[len(f) // 2]
+    print(f"d={d} B={B} zipf={ZIPF} {name} [{spec}]: fields_fwd median {fm * 1e3:.2f} us (rounds "
+          f"{', '.join(f'{x * 1e3:.2f}' for x in res[name]['fwd'])}; {byts / fm / 1e6 / 8000:.3f} of 8 TB/s on "
+          f"SURVEY 8(d)'s count)  fields_bwd {bw[len(bw) // 2] * 1e3:.2f} us", flush=True)
