@@ -100,6 +100,8 @@ SIGNATURES = {
     "fbn_adam_flush": (I, [P, P, P, LL, I, P, P, P, F, F, F, P, P, P, LL, I, I, P]),
     "fbn_adam_prefetch_rows": (I, [P, I, I, LL, P, P, P, P, P, I, P, P, P, F, F, F, P, P, P, LL, I, I, P]),
     "fbn_adam_prefetch": (I, [P, P, I, I, LL, P, P, P, P, P, I, P, P, P, F, F, F, P, P, P, LL, I, I, P]),
+    "fbn_adam_prefetch_binned_ws_size": (SZ, [LL]),
+    "fbn_adam_prefetch_binned": (I, [P, P, I, I, LL, P, P, P, P, P, I, P, P, P, F, F, F, P, P, P, LL, I, I, P, SZ, P]),
     "fbn_adam_selftest": (I, [I, ctypes.c_uint, P, P]),
     "fbn_adam_step_tail": (I, [P, P, P, P, LL, P, F, P, P, P, P, P, I, P, P, P, P, I, I, P, P, F, F, F, P, P, P, P, I,
                                LL, I, P, P, P, P, I, P, P]),

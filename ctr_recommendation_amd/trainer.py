@@ -91,6 +91,9 @@ _EARLY_GRAD_XCHG = os.environ.get("FBN_EARLY_GRAD_XCHG")
 # the bilinear backward, beside the fields backward (HBM-bound) on the main stream; dW_p stays in the
 # flush's launch on main, which waits for the side stream before the slab sums
 _WGRAD_EARLY = os.environ.get("FBN_WGRAD_EARLY", "0") == "1"
+# single GPU, d >= 128: the next-batch prefetch's replay balanced longest-first (fbn_adam_prefetch_binned);
+# FBN_PF_BINNED=0 keeps adam_prefetch2's 64-entries-per-wave replay (A/B)
+_PF_BINNED = os.environ.get("FBN_PF_BINNED", "1") != "0"
 # N > 1, the owner's ahead-of-time catch-up of the next step's requested rows in two passes (tagged
 # pre-claims + the four-row replay engine); FBN_OWNER_PF2=0 keeps the one-pass kernel (A/B)
 _OWNER_PF2 = os.environ.get("FBN_OWNER_PF2", "1") != "0"
@@ -336,6 +339,11 @@ class FiBiNETTrainer:
         self.row_state = torch.zeros((max(1, self.rows_local), 4), **i32)
         self.row_state[:, 3] = -1
         self.preclaim = self.row_state.view(torch.int64)[:, 0] if self.prefetch_rows else None
+        # scratch of the binned prefetch (bins of replay records), d >= 128
+        self.pf_ws = None
+        if self.prefetch_rows and self.d >= 128:
+            nb = _lib.lib().fbn_adam_prefetch_binned_ws_size(self.B * (max_len + 1))
+            self.pf_ws = torch.empty(nb, dtype=torch.uint8, device=dev)
         self._pre_key = None
         self.hasdup = torch.zeros((self.n_entries,), **i32) if self.deterministic else None
         self.fx = torch.zeros((self.n_entries, d), dtype=torch.int64, device=dev) if self.deterministic else None
@@ -546,6 +554,15 @@ class FiBiNETTrainer:
                     return                                    # the one-pass form needs wave-wide rows
                 ev = _events(probe, "adam_prefetch", sst)
                 nB = nb["item_id"].shape[0]
+                if (_PF_BINNED and self._pre_key is not None and self.pf_ws is not None
+                        and nB * (nL + 1) <= self.B * (self.L + 1)):
+                    call("fbn_adam_prefetch_binned", ptr(nb["item_id"]), ptr(nseq) if nL else None, nB, nL,
+                         self.V, ptr(self.map), ptr(self.preclaim), ptr(self.E), ptr(self.Em), ptr(self.Ev), d,
+                         ptr(self.last), ptr(self.sched), ptr(self.step_dev), self.wd_g, self.beta2, self.eps,
+                         *self._pend_args(), int(self.decoupled), ptr(self.pf_ws), self.pf_ws.numel(),
+                         sst.cuda_stream)
+                    _events_end(ev, sst)
+                    return
                 call("fbn_adam_prefetch", ptr(nb["item_id"]), ptr(nseq) if nL else None, nB, nL,
                      self.V, ptr(self.map), ptr(self.preclaim if self._pre_key is not None else None), ptr(self.E),
                      ptr(self.Em), ptr(self.Ev), d, ptr(self.last),

@@ -375,6 +375,18 @@ int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B, int L, lon
                       const float* ring, const float* coef_hist, long long ring_stride, int ring_n, int decoupled,
                       void* stream);
 
+/* fbn_adam_prefetch (two-pass form: preclaim required; D = 128 / 256) with the replay balanced
+ * longest-first: a binning pass makes the same claims and appends each owned row's record to a bin
+ * by replay length (one 128-B counter line per (bin, block % 8)); the replay pass hands every wave a
+ * chunk of 64 records of one bin, longest bins first.  Bit-identical to fbn_adam_prefetch.
+ * ws: fbn_adam_prefetch_binned_ws_size(B * (L + 1)) bytes of device scratch (reused every call). */
+size_t fbn_adam_prefetch_binned_ws_size(long long n);
+int fbn_adam_prefetch_binned(const int64_t* item, const int64_t* seq, int B, int L, long long V, const int* map,
+                             unsigned long long* preclaim, float* p, float* m, float* v, int D, int* last,
+                             const void* consts_table, const int* step, float wd, float beta2, float eps, int* pend,
+                             const float* ring, const float* coef_hist, long long ring_stride, int ring_n,
+                             int decoupled, void* ws, size_t ws_bytes, void* stream);
+
 /* N > 1, the owner's side, D = 128 / 256: fbn_adam_prefetch over local rows lids [n] (-1 = none;
  * skip0: row 0 is the padding id, rank 0) -- the rows the NEXT step's requests name, received
  * through fbn_pad_routes + an equal-split all-to-all during this step.  preclaim (the row-state

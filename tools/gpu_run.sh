@@ -14,6 +14,7 @@
 #   gather     the gather arms (tools/time_fields.py) at C3 and C2 shapes
 #   prof       rocprofv3 kernel trace + stats of the quick bench
 #   pmc        the PMC passes (tools/gpu_pmc.sh)
+#   ab:R:ARM1|ARM2|...   interleaved bench arms (tools/ab_arms.sh; an arm is "VAR=x VAR2=y", "-" = default)
 TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$TAG
@@ -58,6 +59,9 @@ for step in "$@"; do
              -d $O/prof -o run -- python $R/bench.py --no-cpu-baseline --no-cpu-plan --no-inference --no-fp32 \
              > $O/prof.log 2>&1); rc=$?; [ -f $O/prof/run_kernel_trace.csv ] && gzip -f $O/prof/run_kernel_trace.csv ;;
     pmc) bash tools/gpu_pmc.sh $TAG > $O/pmc.txt 2>&1; rc=$?; tail -40 $O/pmc.txt ;;
+    ab:*) IFS=: read -r _ nr arms <<< "$step"; IFS='|' read -ra A <<< "$arms"
+          for i in "${!A[@]}"; do [ "${A[$i]}" = "-" ] && A[$i]=""; done
+          timeout -k 10 1100 bash tools/ab_arms.sh $nr "${A[@]}" > $O/ab.txt 2>&1; rc=$?; cat $O/ab.txt ;;
     *) echo "unknown step $step"; rc=2 ;;
   esac
   echo "== $step rc=$rc $(date +%T)"

@@ -7,7 +7,12 @@ Each PASS_DIR holds run_counter_collection.csv (+ run_kernel_trace.csv) of one
 Kernels are grouped by (name, grid); per group the median over its steady dispatches (the first
 is dropped) of every counter, and derived figures:
 
-* cycles       = GRBM_GUI_ACTIVE / 8 (rocprofv3 sums the 8 XCDs; MI355X_MICROARCH.md, DVFS note)
+* cycles       = the kernel's duration (its --kernel-trace span) x F_CLK = 2.4 GHz, the MI355X peak
+                 engine clock: a ratio over these cycles is a LOWER bound on the kernel's utilisation
+                 (round 4 divided by GRBM_GUI_ACTIVE / 8, which counts the counter window around a
+                 dispatch, not the dispatch: it derived 2.5-4.95 GHz clocks for kernels under ~30 us
+                 and mis-scaled every ratio of theirs); grbm_clock_ghz keeps that derivation as a
+                 diagnostic
 * mfma_busy    = SQ_VALU_MFMA_BUSY_CYCLES / (cycles x 1024 SIMDs): fraction of the chip's matrix-
                  pipe cycles busy (a 32x32x16 bf16 MFMA keeps its SIMD busy 32 cycles);
                  mfma_tflops_at_busy = the bf16 rate those busy cycles imply at the kernel's clock
@@ -21,6 +26,8 @@ import os
 import statistics
 import sys
 from collections import defaultdict
+
+F_CLK_GHZ = 2.4       # MI355X peak engine clock (MI355X_MICROARCH.md)
 
 
 def load_pass(d):
@@ -57,15 +64,16 @@ def main():
     for (name, grid), ctrs in merged.items():
         m = {c: statistics.median(v) for c, v in ctrs.items()}
         d = {"kernel": name, "grid": grid, **{k: round(v, 3) for k, v in m.items()}}
-        cyc = m.get("GRBM_GUI_ACTIVE", 0) / 8.0
+        grbm = m.get("GRBM_GUI_ACTIVE", 0) / 8.0
+        dur = m.get("duration_us", 0.0)
+        if grbm > 0 and dur > 0:
+            d["grbm_clock_ghz"] = round(grbm / (dur * 1e3), 3)
+        cyc = dur * 1e3 * F_CLK_GHZ
         if cyc > 0:
             d["cycles"] = round(cyc)
-            if "duration_us" in m and m["duration_us"] > 0:
-                d["clock_ghz"] = round(cyc / (m["duration_us"] * 1e3), 3)
             if "SQ_VALU_MFMA_BUSY_CYCLES" in m:
                 d["mfma_busy"] = round(m["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * 1024), 4)
-                if "clock_ghz" in d:
-                    d["mfma_tflops_at_busy"] = round(d["mfma_busy"] * 1024 * 1024 * d["clock_ghz"] * 1e9 / 1e12, 1)
+                d["mfma_tflops_at_busy"] = round(d["mfma_busy"] * 1024 * 1024 * F_CLK_GHZ * 1e9 / 1e12, 1)
             if "SQ_ACTIVE_INST_VALU" in m:
                 d["valu_issue"] = round(4 * m["SQ_ACTIVE_INST_VALU"] / (cyc * 1024), 4)
         if "FETCH_SIZE" in m or "WRITE_SIZE" in m:
@@ -74,7 +82,7 @@ def main():
     res.sort(key=lambda r: -r.get("duration_us", 0))
     json.dump(res, open(out, "w"), indent=1)
     for r in res[:30]:
-        extra = "  ".join(f"{k} {r[k]}" for k in ("duration_us", "clock_ghz", "mfma_busy", "mfma_tflops_at_busy",
+        extra = "  ".join(f"{k} {r[k]}" for k in ("duration_us", "grbm_clock_ghz", "mfma_busy", "mfma_tflops_at_busy",
                                                  "valu_issue", "SQ_INSTS_VALU", "hbm_bytes") if k in r)
         print(f"{r['kernel'][:60]:60s} grid {r['grid']:8d}  {extra}")
 
