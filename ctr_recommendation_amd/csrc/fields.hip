@@ -127,7 +127,11 @@ __device__ __forceinline__ f32x4 load_row(const FieldArgs& p, size_t r, int q) {
 // zeros without a memory request, so dead slots stay off the fetch path (the global-load form
 // reads row 0 for them: an L2 hit, but L2 bandwidth and TA cycles all the same)
 #define FBN_BUF_FLAGS 0x00020000   // gfx9 buffer descriptor word 3 (raw, 32-bit dwords)
-template <int D, int MODE, int HCH, bool BUF = false, bool HOT = false>
+// CMP: the sample's live history slots are compacted first (ballot + mbcnt; their rows staged in a
+// per-sample LDS list in slot order), so a chunk of HCH loads carries only live rows and a sample
+// takes ceil(n_live / HCH) rounds instead of L / HCH; summed in slot order like the plain form --
+// the skipped padding slots added +0.0 there, so the two are bit-identical.
+template <int D, int MODE, int HCH, bool BUF = false, bool HOT = false, bool CMP = false>
 __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
   FBN_MAIN_PRIO();
   // (unused, and dropped, unless BUF)
@@ -212,7 +216,47 @@ __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
       sid[j] = r;
     }
     const int gbase = lane - q;
-    for (int t0 = 0; t0 < L; t0 += HCH) {
+    if constexpr (CMP) {
+      constexpr int SPB = 4 * SPW;                     // samples per 256-thread block
+      __shared__ int lid[SPB][FBN_MAX_L];
+      int* mine = lid[(threadIdx.x >> 6) * SPW + lane / G];
+      const unsigned long long gmask = (G == 64 ? ~0ull : ((1ull << G) - 1)) << gbase;
+      int nl = 0;
+#pragma unroll
+      for (int j = 0; j < IPL; ++j) {
+        const unsigned long long mk = __ballot(sid[j] >= 0) & gmask;
+        const int below = __popcll(mk & ((1ull << lane) - 1));
+        if (sid[j] >= 0) mine[nl + below] = sid[j];
+        nl += __popcll(mk);
+      }
+      __builtin_amdgcn_wave_barrier();
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);         // the list is read back by the group's lanes
+      int nch = (nl + HCH - 1) / HCH;                  // wave-uniform bound: the wave's largest
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) nch = max(nch, __shfl_xor(nch, o, 64));
+      for (int c = 0; c < nch; ++c) {
+        f32x4 hist[HCH];
+        bool live[HCH];
+#pragma unroll
+        for (int u = 0; u < HCH; ++u) {
+          const int k = c * HCH + u;
+          live[u] = k < nl;
+          const int r = mine[live[u] ? k : 0];
+          if constexpr (BUF) {
+            const unsigned off = live[u] ? ((unsigned)r * D + 4 * q) * 4u : 0xFFFFFFF0u;
+            hist[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+          } else {
+            hist[u] = load_row<D, MODE>(p, live[u] ? r : 0, q);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < HCH; ++u) hs += live[u] ? hist[u] : (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+      nnz = nl;
+      __builtin_amdgcn_wave_barrier();                 // the next sample's list overwrites this one
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    }
+    for (int t0 = 0; t0 < (CMP ? 0 : L); t0 += HCH) {
       // branch-free: every slot of the chunk issues its load (a padding or past-L slot reads row
       // 0, an L2-resident line, and contributes +0 by a select) -- a load under a branch makes
       // hipcc drain vmcnt(0) before the next, which serialised the chunk's round trips
@@ -298,140 +342,6 @@ __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
       for (int t = q; t <= L; t += G) {
         long long r = (t == 0) ? item : p.item_seq[(size_t)b * L + (t - 1)];
         if (r > 0 && r < p.V) map_claim(p.map, p.slot_row, (int)r, b * (L + 1) + t);
-      }
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------ forward, one wave per sample
-// fields_fwd_kernel runs 8192 samples as ONE generation of 16 waves per CU (two samples per wave at
-// d = 128) that all walk the same dependent round trips together -- ids, the item row, then the
-// history in chunks of HCH slots, padding slots included -- and read 3.3 TB/s of real bytes alone
-// (VERDICT r4 "weak" 4).  Here a wave takes ONE sample, split into RG = 256 / D row groups of G = D / 4
-// lanes (a row is one coalesced read by a group; at d = 128 two rows per wave-instruction):
-//  * the sample's non-padding history slots are compacted (ballot + mbcnt; their row ids staged in
-//    a per-wave LDS list), so padding slots are never issued;
-//  * row group g reads compacted slots g, g + RG, g + 2 RG, ..., HC per round trip (at d = 128 a
-//    typical sample's ~10 live rows are all in flight at once, every sample's in at most two rounds);
-//  * each group sums its rows in slot order and a butterfly over the groups adds the partial sums
-//    (commutative at every level, so every group holds the same total);
-//  * the LayerNorm / SENET epilogue is the old kernel's, stored by group 0.
-// The item row, cate rows and mm projection are loaded by every group (one address per group: the
-// extra lanes hit the same lines), which keeps the kernel branch-free.
-template <int D, int MODE, bool BUF, int HC>
-__global__ void __launch_bounds__(256) fields_fwd2_kernel(FieldArgs p) {
-  FBN_MAIN_PRIO();
-  constexpr int G = D / 4, RG = 64 / G;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(p.table), 0, (int)((unsigned long long)p.V * D * 4), FBN_BUF_FLAGS);
-  __shared__ int lid[4][FBN_MAX_L];          // per wave: the sample's live history rows, slot order
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int q = lane % G, rg = lane / G;
-  const int gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int nwaves = (gridDim.x * blockDim.x) >> 6;
-  const int L = p.L;
-  for (int b = gw; b < p.B; b += nwaves) {
-    long long item = p.item_id[b];
-    long long lk = p.likes[b], vw = p.views[b];
-    bool bad = false;
-    if (lk < 0 || lk >= p.n_cate) { bad = true; lk = 0; }
-    if (vw < 0 || vw >= p.n_cate) { bad = true; vw = 0; }
-    const int* pb = MODE >= 1 ? p.pos + (size_t)b * (L + 1) : nullptr;
-    // history ids: lane t < L holds slot t
-    int r = -1;
-    if (lane < L) {
-      if (MODE == 0) {
-        long long s = p.item_seq[(size_t)b * L + lane];
-        if (s < 0 || s >= p.V) { bad = true; s = 0; }
-        r = s != 0 ? (int)s : -1;
-      } else {
-        r = pb[lane + 1];
-      }
-    }
-    const f32x4 c1 = *reinterpret_cast<const f32x4*>(p.cate + lk * D + 4 * q);
-    const f32x4 c2 = *reinterpret_cast<const f32x4*>(p.cate + vw * D + 4 * q);
-    const f32x4 h = *reinterpret_cast<const f32x4*>(p.hmm + (size_t)b * D + 4 * q);
-    f32x4 rit;
-    if (MODE == 0) {
-      if (item < 0 || item >= p.V) { bad = true; item = -1; }
-      rit = *reinterpret_cast<const f32x4*>(p.table + (item >= 0 ? item : 0) * D + 4 * q);
-      if (item < 0) rit = (f32x4){0.f, 0.f, 0.f, 0.f};
-    } else {
-      const int pi = pb[0];
-      rit = load_row<D, MODE>(p, pi >= 0 ? pi : 0, q);
-      if (pi < 0) rit = (f32x4){0.f, 0.f, 0.f, 0.f};
-    }
-    const unsigned long long live = __ballot(r >= 0);
-    const int n_live = __popcll(live);
-    if (r >= 0)
-      lid[w][__builtin_amdgcn_mbcnt_hi((unsigned)(live >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)live, 0u))] = r;
-    __builtin_amdgcn_wave_barrier();
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);   // the list is read back by other lanes of this wave
-    f32x4 hs = {0.f, 0.f, 0.f, 0.f};
-    const int nch = (n_live + RG * HC - 1) / (RG * HC);     // wave-uniform
-    for (int c = 0; c < nch; ++c) {
-      f32x4 hist[HC];
-      bool lv[HC];
-#pragma unroll
-      for (int u = 0; u < HC; ++u) {
-        const int k = rg + RG * (c * HC + u);
-        lv[u] = k < n_live;
-        const int rr = lid[w][lv[u] ? k : 0];
-        if constexpr (BUF) {
-          const unsigned off = lv[u] ? ((unsigned)rr * D + 4 * q) * 4u : 0xFFFFFFF0u;
-          hist[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
-        } else {
-          hist[u] = load_row<D, MODE>(p, lv[u] ? rr : 0, q);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < HC; ++u) hs += lv[u] ? hist[u] : (f32x4){0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int o = G; o < 64; o <<= 1) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) hs[e] += __shfl_xor(hs[e], o, 64);
-    }
-    if (bad) atomicOr(p.err, 1);
-
-    // ---------------- history masked mean, mm field, SENET (as fields_fwd_kernel)
-    const float cnt = fmaxf((float)n_live, 1.f);
-    f32x4 x5 = hs / cnt;
-    const f32x4 x4 = ln_relu<G>(h, p.ln_g, p.ln_b, p.ln_eps, q);
-    const f32x4 xs[5] = {c1, c2, rit, x4, x5};
-    float z[6];
-    z[0] = 0.f;
-#pragma unroll
-    for (int f = 0; f < 5; ++f) z[f + 1] = group_sum<G>(xs[f][0] + xs[f][1] + xs[f][2] + xs[f][3]) / (float)D;
-    float qv[FBN_MAXR], a[6];
-    senet_excite<D>(z, p.w1, p.b1, p.w2, p.b2, p.R, qv, a);
-
-    // ---------------- stores (row group 0)
-    if (rg == 0) {
-      float* Xb = p.X + (size_t)b * 2 * D + 4 * q;
-      *reinterpret_cast<f32x4*>(Xb) = rit;
-      *reinterpret_cast<f32x4*>(Xb + D) = x5;
-      float* Vb = p.Vc ? p.Vc + (size_t)b * 5 * D + 4 * q : nullptr;
-      float* cb = (p.c && !p.c16) ? (float*)p.c + (size_t)b * p.ldc + 4 * q : nullptr;
-      short* cb16 = (p.c && p.c16) ? (short*)p.c + (size_t)b * p.ldc + 4 * q : nullptr;
-#pragma unroll
-      for (int f = 0; f < 5; ++f) {
-        const f32x4 v = xs[f] * a[f + 1];
-        if (p.Vc) *reinterpret_cast<f32x4*>(Vb + f * D) = v;
-        const bf16x4 v16 = (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
-        if (cb16) *reinterpret_cast<bf16x4*>(cb16 + f * D) = v16;
-        else if (cb) *reinterpret_cast<f32x4*>(cb + f * D) = v;
-        if (p.Vc16) *reinterpret_cast<bf16x4*>(p.Vc16 + ((size_t)b * 5 + f) * D + 4 * q) = v16;
-      }
-#pragma unroll
-      for (int f = 0; f < 6; ++f)
-        if (f % G == q) p.a_out[(size_t)b * 6 + f] = a[f];
-      if (q == 0) p.cnt_out[b] = cnt;
-      if (MODE == 0 && p.map) {
-        for (int t = q; t <= L; t += G) {
-          long long rr = (t == 0) ? item : p.item_seq[(size_t)b * L + (t - 1)];
-          if (rr > 0 && rr < p.V) map_claim(p.map, p.slot_row, (int)rr, b * (L + 1) + t);
-        }
       }
     }
   }
@@ -792,78 +702,48 @@ static int fields_grid(int B, int D, int cap = 1024) {
 
 // history rows per chunk: every row of a chunk is in flight at once (branch-free issue); more rows
 // per chunk = fewer dependent round trips but more registers (fewer waves resident)
-template <int MODE, int HCH, bool BUF, bool HOT = false>
+template <int MODE, int HCH, bool BUF, bool HOT = false, bool CMP = false>
 static int launch_fields_fwd_hb(const FieldArgs& a, int D, hipStream_t st) {
   // hot staging: fewer, longer-lived workgroups (each stages the hot rows once)
   const int grid = fields_grid(a.B, D, HOT ? 256 : 1024);
   switch (D) {
-    case 16: fbn_launch((fields_fwd_kernel<16, MODE, HCH, BUF, HOT>), dim3(grid), dim3(256), 0, st, a); break;
-    case 32: fbn_launch((fields_fwd_kernel<32, MODE, HCH, BUF, HOT>), dim3(grid), dim3(256), 0, st, a); break;
-    case 64: fbn_launch((fields_fwd_kernel<64, MODE, HCH, BUF, HOT>), dim3(grid), dim3(256), 0, st, a); break;
-    case 128: fbn_launch((fields_fwd_kernel<128, MODE, HCH, BUF, HOT>), dim3(grid), dim3(256), 0, st, a); break;
-    case 256: fbn_launch((fields_fwd_kernel<256, MODE, HCH, BUF, HOT>), dim3(grid), dim3(256), 0, st, a); break;
+    case 16: fbn_launch((fields_fwd_kernel<16, MODE, HCH, BUF, HOT, CMP>), dim3(grid), dim3(256), 0, st, a); break;
+    case 32: fbn_launch((fields_fwd_kernel<32, MODE, HCH, BUF, HOT, CMP>), dim3(grid), dim3(256), 0, st, a); break;
+    case 64: fbn_launch((fields_fwd_kernel<64, MODE, HCH, BUF, HOT, CMP>), dim3(grid), dim3(256), 0, st, a); break;
+    case 128: fbn_launch((fields_fwd_kernel<128, MODE, HCH, BUF, HOT, CMP>), dim3(grid), dim3(256), 0, st, a); break;
+    case 256: fbn_launch((fields_fwd_kernel<256, MODE, HCH, BUF, HOT, CMP>), dim3(grid), dim3(256), 0, st, a); break;
     default: fbn_set_error("fields: embedding_dim must be one of 16,32,64,128,256"); return FBN_ERR_UNSUPPORTED;
   }
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
 
-template <int MODE, int HCH>
+template <int MODE, int HCH, bool CMP>
 static int launch_fields_fwd_h(const FieldArgs& a, int D, hipStream_t st) {
   if constexpr (MODE == 0) {
     if (a.hot) return launch_fields_fwd_hb<0, HCH, true, true>(a, D, st);
     // buffer-resource history loads while the table's byte extent fits the descriptor's 32 bits
     static const bool nobuf = getenv("FBN_FIELDS_NOBUF") != nullptr;   // A/B knob
-    if (!nobuf && (unsigned long long)a.V * D * 4 < 0xFFFFFF00ull) return launch_fields_fwd_hb<0, HCH, true>(a, D, st);
+    if (!nobuf && (unsigned long long)a.V * D * 4 < 0xFFFFFF00ull)
+      return launch_fields_fwd_hb<0, HCH, true, false, CMP>(a, D, st);
   }
-  return launch_fields_fwd_hb<MODE, HCH, false>(a, D, st);
-}
-
-// the one-wave-per-sample gather (fields_fwd2_kernel); HC rows in flight per row group, by d (at
-// most ceil(20 / RG) are ever live in a group); FBN_FIELDS_HC overrides at d = 128 (A/B)
-template <int D, int MODE, bool BUF>
-static void launch_fwd2_d(const FieldArgs& a, int grid, hipStream_t st, int hc) {
-  constexpr int RG = 256 / D;
-  constexpr int HCD = (20 + RG - 1) / RG < 6 ? (20 + RG - 1) / RG : 6;
-  if constexpr (D == 128 && MODE == 0) {
-    if (hc == 10) return fbn_launch((fields_fwd2_kernel<D, MODE, BUF, 10>), dim3(grid), dim3(256), 0, st, a);
-    if (hc == 4) return fbn_launch((fields_fwd2_kernel<D, MODE, BUF, 4>), dim3(grid), dim3(256), 0, st, a);
-    if (hc == 8) return fbn_launch((fields_fwd2_kernel<D, MODE, BUF, 8>), dim3(grid), dim3(256), 0, st, a);
-  }
-  fbn_launch((fields_fwd2_kernel<D, MODE, BUF, HCD>), dim3(grid), dim3(256), 0, st, a);
-}
-
-template <int MODE, bool BUF>
-static int launch_fields_fwd2(const FieldArgs& a, int D, hipStream_t st) {
-  // A/B knob, read per call: FBN_FIELDS_HC rows in flight per row group (d = 128, single GPU)
-  const char* he = getenv("FBN_FIELDS_HC");
-  const int hc = he ? atoi(he) : 6;
-  const int grid = a.B < 4 * 4096 ? (a.B + 3) / 4 : 4096;    // one wave per sample (grid-stride beyond)
-  switch (D) {
-    case 16: launch_fwd2_d<16, MODE, BUF>(a, grid, st, hc); break;
-    case 32: launch_fwd2_d<32, MODE, BUF>(a, grid, st, hc); break;
-    case 64: launch_fwd2_d<64, MODE, BUF>(a, grid, st, hc); break;
-    case 128: launch_fwd2_d<128, MODE, BUF>(a, grid, st, hc); break;
-    case 256: launch_fwd2_d<256, MODE, BUF>(a, grid, st, hc); break;
-    default: fbn_set_error("fields: embedding_dim must be one of 16,32,64,128,256"); return FBN_ERR_UNSUPPORTED;
-  }
-  FBN_CHECK_LAUNCH();
-  return FBN_OK;
+  return launch_fields_fwd_hb<MODE, HCH, false, false, CMP>(a, D, st);
 }
 
 template <int MODE>
 static int launch_fields_fwd(const FieldArgs& a, int D, hipStream_t st) {
-  // FBN_FIELDS_V=1: the two-samples-per-wave gather (fields_fwd_kernel; A/B, and the hot-row staging's base)
-  const char* ve = getenv("FBN_FIELDS_V");
-  if (!(MODE == 0 && a.hot) && !(ve && atoi(ve) == 1)) {
-    if (MODE == 0 && (unsigned long long)a.V * D * 4 < 0xFFFFFF00ull) return launch_fields_fwd2<MODE, true>(a, D, st);
-    return launch_fields_fwd2<MODE, false>(a, D, st);
-  }
   const char* he = getenv("FBN_FIELDS_HCH");   // A/B knob, read per call
   const int hch = he ? atoi(he) : FBN_HCH;
-  if (hch == 20) return launch_fields_fwd_h<MODE, 20>(a, D, st);
-  if (hch == 5) return launch_fields_fwd_h<MODE, 5>(a, D, st);
-  return launch_fields_fwd_h<MODE, 10>(a, D, st);
+  // FBN_FIELDS_CMP=1: the live history slots compacted first (A/B knob, read per call)
+  const char* ce = getenv("FBN_FIELDS_CMP");
+  if (ce && atoi(ce) == 1) {
+    if (hch == 10) return launch_fields_fwd_h<MODE, 10, true>(a, D, st);
+    if (hch == 8) return launch_fields_fwd_h<MODE, 8, true>(a, D, st);
+    return launch_fields_fwd_h<MODE, 5, true>(a, D, st);
+  }
+  if (hch == 20) return launch_fields_fwd_h<MODE, 20, false>(a, D, st);
+  if (hch == 5) return launch_fields_fwd_h<MODE, 5, false>(a, D, st);
+  return launch_fields_fwd_h<MODE, 10, false>(a, D, st);
 }
 
 static int fields_fwd_impl(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes,

@@ -1583,27 +1583,29 @@ __global__ void __launch_bounds__(256) adam_pfbin_kernel(ClaimSrc cs, int n, int
   }
 }
 
-// pass B: wave w takes the w-th chunk of 64 records in the order (bin descending, block copy c8
-// ascending); waves past the last chunk exit.  The counts are zeroed by the next step's pass 0.
+// pass B: wave w takes the w-th chunk of `ch` records (ch <= 64) in the order (bin descending, block
+// copy c8 ascending); waves past the last chunk exit.  The counts are zeroed by the next call's
+// pfb_zero.  ch = 32 by default: about as many waves as adam_prefetch2's (64 entries -> ~31 rows
+// each); chunks of 64 halve the waves and measured 0.474 vs 0.431 ms/step (fewer chains in flight).
 template <int D, bool DW, int G = 4>
 __global__ void __launch_bounds__(256) adam_pfreplay_kernel(float* __restrict__ p, float* __restrict__ m,
                                                             float* __restrict__ v, const int* __restrict__ step,
                                                             float wd, float b2, float omb2, float eps,
                                                             const AdamConsts* __restrict__ table, PendSrc ps,
                                                             const unsigned* __restrict__ counts,
-                                                            const int4* __restrict__ recs, int nblk_bin) {
+                                                            const int4* __restrict__ recs, int nblk_bin, int ch) {
   const int T = *step + 1;
   const int lane = threadIdx.x & 63;
   const int w = (int)(((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   // lane l holds lists o = 4l .. 4l+3 of the longest-first order (o -> bin 31 - o / 8, c8 = o % 8)
-  int ch[4], tot = 0;
+  int nc[4], tot = 0;
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int o = 4 * lane + u;
     const int bin = FBN_PFB_NB - 1 - o / FBN_PFB_NC, c8 = o % FBN_PFB_NC;
     const unsigned c = counts[((size_t)bin * FBN_PFB_NC + c8) * FBN_PFB_LINE];
-    ch[u] = (int)((c + 63) / 64);
-    tot += ch[u];
+    nc[u] = (int)((c + ch - 1) / ch);
+    tot += nc[u];
   }
   // inclusive prefix of the chunk counts over the lanes
   int inc = tot;
@@ -1619,15 +1621,15 @@ __global__ void __launch_bounds__(256) adam_pfreplay_kernel(float* __restrict__ 
   const int src = __ffsll((long long)hit) - 1;
   int lo = __shfl(start, src, 64);
   int sel = 0;
-  const int c0 = __shfl(ch[0], src, 64), c1 = __shfl(ch[1], src, 64), c2 = __shfl(ch[2], src, 64);
+  const int c0 = __shfl(nc[0], src, 64), c1 = __shfl(nc[1], src, 64), c2 = __shfl(nc[2], src, 64);
   if (w >= lo + c0) { lo += c0; sel = 1;
     if (w >= lo + c1) { lo += c1; sel = 2;
       if (w >= lo + c2) { lo += c2; sel = 3; } } }
   const int o = 4 * src + sel;
   const int bin = FBN_PFB_NB - 1 - o / FBN_PFB_NC, c8 = o % FBN_PFB_NC;
   const int cntl = (int)counts[((size_t)bin * FBN_PFB_NC + c8) * FBN_PFB_LINE];
-  const int j0 = (w - lo) * 64;
-  const int cnt = min(64, cntl - j0);
+  const int j0 = (w - lo) * ch;
+  const int cnt = min(ch, cntl - j0);
   int r = 0, key = 0x7fffffff, pe = -1;
   if (lane < cnt) {
     const int4 rec = recs[((long long)bin * FBN_PFB_NC + c8) * pfb_cap(nblk_bin) + j0 + lane];
@@ -2450,13 +2452,16 @@ static int launch_prefetch_binned(const ClaimSrc& cs, long long n, float* p, flo
   fbn_launch(pfb_zero_kernel, dim3(1), dim3(256), 0, st, counts);
   fbn_launch(adam_pretag_kernel, dim3(nblk), dim3(256), 0, st, cs, (int)n, step);
   fbn_launch(adam_pfbin_kernel, dim3(nblk), dim3(256), 0, st, cs, (int)n, last, step, ps, counts, recs);
-  // at most one chunk per 64 records plus one partial chunk per list
-  const long long waves = (n + 63) / 64 + FBN_PFB_NB * FBN_PFB_NC;
+  // FBN_PFB_CHUNK: records per replay wave (A/B knob, read per call; 1 .. 64)
+  const char* ce = getenv("FBN_PFB_CHUNK");
+  const int ch = ce ? std::max(1, std::min(64, atoi(ce))) : 32;
+  // at most one chunk per ch records plus one partial chunk per list
+  const long long waves = (n + ch - 1) / ch + FBN_PFB_NB * FBN_PFB_NC;
   const dim3 g((unsigned)((waves + 3) / 4));
   const AdamConsts* tab = (const AdamConsts*)consts_table;
 #define FBN_PFB_LAUNCH(D_, DW_)                                                                              \
   fbn_launch((adam_pfreplay_kernel<D_, DW_>), g, dim3(256), 0, st, p, m, v, step, wd, beta2, omb2, eps, tab, ps, \
-             (const unsigned*)counts, (const int4*)recs, nblk)
+             (const unsigned*)counts, (const int4*)recs, nblk, ch)
   if (D == 128) {
     if (decoupled) FBN_PFB_LAUNCH(128, true); else FBN_PFB_LAUNCH(128, false);
   } else {

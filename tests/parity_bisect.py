@@ -13,6 +13,8 @@ valid AUC and its distance (|dAUC|, max / mean |dp|) from the float64 loop:
 * fp32 / f64: the oracle in float32 / float64 (the chaos floor of two correct implementations);
 * fp32_t<n>: fp32 on n CPU threads (other reduction orders inside torch's kernels);
 * fp32_foreach / fp32_fused: torch's multi-tensor / fused Adam (other operation orders of the step);
+* f64_n<k>: float64 with relative 2^-24 noise (seed k) injected into every parameter after every
+  step: an exact implementation that rounds like fp32 -- an independent trajectory of the chaos;
 * fp32_fx40: the per-entry table-gradient vectors rounded to the 2^-40 fixed-point grid before the
   row sums -- what the deterministic duplicate fold (csrc/optim.hip sparse_fold_fx_kernel) did to
   every row several entries hit.
@@ -80,6 +82,14 @@ def run_variant(name, data, perms, epochs, bs, n_train, n_valid):
             ref.shift = int(name[len("fp32_fx"):])
         if f64:
             ref = ref.double()
+        noise = None
+        if name.startswith("f64_n"):
+            # float64 with fp32-level rounding noise injected into every parameter after every step
+            # (relative 2^-24 x N(0,1), seed k): an exact implementation that rounds like fp32 --
+            # one more independent trajectory of the chaos every fp32 implementation goes through
+            ref = ref.double()
+            f64 = True
+            noise = torch.Generator().manual_seed(int(name[len("f64_n"):]))
         cast = (lambda t: t.double() if t.is_floating_point() else t) if f64 else (lambda t: t)
         steps_per_epoch = -(-n_train // bs)
         otr = OracleTrainer(ref, lr=1e-3, weight_decay=1e-5, total_steps=epochs * steps_per_epoch)
@@ -92,6 +102,10 @@ def run_variant(name, data, perms, epochs, bs, n_train, n_valid):
                 b, y = coll([darray[i, :] for i in perms[e][lo:lo + bs]])
                 b = {k: cast(v.long() if k != "item_emb_d128" else v) for k, v in b.items()}
                 ls = otr.step(b, cast(y))[0]
+                if noise is not None:
+                    with torch.no_grad():
+                        for prm in ref.parameters():
+                            prm.mul_(1.0 + 2.0 ** -24 * torch.randn(prm.shape, generator=noise, dtype=torch.float64))
                 steps.append(ls)
                 tot += ls
             losses.append(tot / steps_per_epoch)
@@ -113,7 +127,7 @@ def run_variant(name, data, perms, epochs, bs, n_train, n_valid):
             "sd": {k: v.detach().double().clone() for k, v in ref.state_dict().items()}}
 
 
-ENSEMBLE = ("fp32", "fp32_t1", "fp32_t2", "fp32_fused")
+ENSEMBLE = ("fp32", "fp32_t1", "fp32_t2", "fp32_fused", "f64_n1", "f64_n2")
 BS, N_TRAIN, N_VALID, EPOCHS, N_ITEMS = 512, 51200, 8192, 2, 5000
 PARITY_CONFIG = """
 base_expid: MM_FiBiNET_Run
@@ -235,15 +249,66 @@ def eval_weights(sd, data, f64=True):
     return compute_auc(np.concatenate(ys), np.concatenate(ps))
 
 
+def first_step(p, data, seed=5):
+    """One training step on the parity data's first batch (GPU): per tensor, the HIP trainer's
+    gradient and update against the float64 oracle's, beside the fp32 oracle's distance from it.
+    The step-2 loss of a HIP run sits ~50x further from the float64 loop than the fp32 loop's
+    (tests/parity_bisect report: trajectory); this names the tensors whose first update differs."""
+    from ctr_recommendation_amd.trainer import FiBiNETTrainer
+    darray, coll, _, _ = data
+    rows = np.random.default_rng(seed).permutation(N_TRAIN)[:BS]
+    b, y = coll([darray[i, :] for i in rows])
+    b = {k: (v.long() if k != "item_emb_d128" else v) for k, v in b.items()}
+    cfg = {"embedding_dim": 16, "honour_config": True, "net_dropout": 0.0}
+    torch.manual_seed(2025)
+    init = OracleFiBiNET(cfg, honour_config=True).state_dict()
+    res = {}
+    for name in ("f64", "fp32"):
+        m = OracleFiBiNET(cfg, honour_config=True)
+        m.load_state_dict(init)
+        cast = (lambda t: t.double() if t.is_floating_point() else t) if name == "f64" else (lambda t: t)
+        if name == "f64":
+            m = m.double()
+        otr = OracleTrainer(m, lr=1e-3, weight_decay=1e-5, total_steps=EPOCHS * (N_TRAIN // BS))
+        lr0 = otr.sched.get_last_lr()[0]
+        otr.step({k: cast(v) for k, v in b.items()}, cast(y))
+        res[name] = {"g": {n: q.grad.detach().double().clone() for n, q in m.named_parameters() if q.grad is not None},
+                     "sd": {k: v.detach().double().clone() for k, v in m.state_dict().items()}, "norm": otr.last_total_norm}
+    dev = torch.device("cuda", 0)
+    htr = FiBiNETTrainer(dict(cfg, deterministic=True), total_steps=EPOCHS * (N_TRAIN // BS), batch_size=BS,
+                         device=dev, init_state={k: v.clone() for k, v in init.items()})
+    htr.step({k: v.to(dev) for k, v in b.items()}, y.to(dev))
+    torch.cuda.synchronize()
+    res["hip"] = {"g": {n: t.detach().double().cpu() for n, t in htr.g.items()},
+                  "sd": {k: v.double() for k, v in htr.state_dict().items()}, "norm": float(htr.norm.item())}
+    out = {"lr0": lr0, "clip_norm": {k: r["norm"] for k, r in res.items()}, "tensors": {}}
+    ref = res["f64"]
+    for n, v in ref["sd"].items():
+        if not v.is_floating_point() or n == "user_emb.weight":
+            continue
+        ent = {}
+        for who in ("fp32", "hip"):
+            d_ref = v - init[n].double()
+            d_who = res[who]["sd"][n] - init[n].double()
+            dd = (d_who - d_ref).abs()
+            ent[who] = {"update_max_abs_diff_over_lr": float(dd.max() / lr0),
+                        "elements_off_by_1pct_lr": int((dd > 0.01 * lr0).sum()), "numel": v.numel()}
+            if n in ref["g"] and n in res[who]["g"]:
+                gr, gw = ref["g"][n], res[who]["g"][n].reshape(ref["g"][n].shape)
+                ent[who]["grad_max_abs_diff_over_max"] = float((gw - gr).abs().max() / max(gr.abs().max(), 1e-30))
+        out["tensors"][n] = ent
+    return out
+
+
 def ensemble(data, perms, names=("f64",) + ENSEMBLE):
     return {n: run_variant(n, data, perms, EPOCHS, BS, N_TRAIN, N_VALID) for n in names}
 
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=("cpu", "hip", "report"))
+    ap.add_argument("mode", choices=("cpu", "hip", "report", "step1"))
     ap.add_argument("--out", default=None)
-    ap.add_argument("--variants", default="f64,fp32,fp32_t1,fp32_t2,fp32_fused,fp32_fx40")
+    ap.add_argument("--variants", default="f64,fp32,fp32_t1,fp32_t2,fp32_fused,f64_n1,f64_n2,fp32_fx40")
     ap.add_argument("--perm-seed", type=int, default=5)
     ap.add_argument("--tag", default="default")
     ap.add_argument("--nondet", action="store_true")
@@ -252,6 +317,13 @@ def main(argv=None):
     root = tempfile.mkdtemp()
     p = write_data(root)
     data = oracle_data(p)
+    if args.mode == "step1":
+        out = first_step(p, data)
+        print(json.dumps(out, indent=1))
+        if args.out:
+            with open(args.out, "w") as f:
+                json.dump(out, f, indent=1)
+        return
     if args.mode == "hip":
         # one launcher run (the library FBN_LIB_PATH names) -> npz for the report
         r = run_launcher(p, root, deterministic=not args.nondet)

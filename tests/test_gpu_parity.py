@@ -197,26 +197,23 @@ def test_hot_row_staging_is_bit_identical(hip_device, d, zipf, tau, monkeypatch)
     hip = build_model(None, {"embedding_dim": d, "vocab_size": V}).to(hip_device).eval()
     (batch, _), = make_device_batches(1, B, V, 20, hip_device, seed=9, zipf=zipf)
     with torch.no_grad():
-        pn = hip(batch)          # the default one-wave-per-sample gather (fields_fwd2_kernel)
-        # the staging is built on the two-samples-per-wave gather: it is the bit-identity reference
-        monkeypatch.setenv("FBN_FIELDS_V", "1")
         p0 = hip(batch)
         monkeypatch.setattr(ops, "_GATHER_HOT", tau)
         p1 = hip(batch)
         p2 = hip(batch)          # counts and the list were cleared after the first staged pass
     assert torch.equal(p0, p1) and torch.equal(p0, p2)
-    # the two gathers sum a sample's history rows in different orders (slot order vs two row groups)
-    assert (pn - p0).abs().max().item() <= 1e-5
 
 
 @pytest.mark.parametrize("d", [16, 32, 64, 128, 256])
 @pytest.mark.parametrize("mode", ["table", "rows_f32", "rows_bf16"])
-def test_gather_one_wave_per_sample_matches_two_per_wave(hip_device, d, mode, monkeypatch):
-    """The one-wave-per-sample gather (fields_fwd2_kernel: compacted live history slots, row groups,
-    butterfly of the group sums) against the two-samples-per-wave one (FBN_FIELDS_V=1) on every
-    output of fbn_fields_fwd, reading the table (mode 0) or an exchanged row buffer through pos
-    (modes 1 / 2): ids, counts and SENET weights identical, the fields within float rounding of
-    the history sums' order; an all-padding sample and a history of one live slot included."""
+@pytest.mark.parametrize("hch", ["5", "10"])
+def test_gather_compacted_slots_bit_identical(hip_device, d, mode, hch, monkeypatch):
+    """The gather with the live history slots compacted first (FBN_FIELDS_CMP=1: ballot + mbcnt, a
+    per-sample LDS list, chunks of live rows only) against the plain one on every output of
+    fbn_fields_fwd, reading the table (mode 0) or an exchanged row buffer through pos (modes 1 / 2):
+    bit-identical (the plain form's padding slots add +0.0); an all-padding sample and a history of
+    one live slot included."""
+    monkeypatch.setenv("FBN_FIELDS_HCH", hch)
     import ctypes
     from ctr_recommendation_amd._lib import call, ptr
     V, B, L = 5000, 300, 20
@@ -262,14 +259,12 @@ def test_gather_one_wave_per_sample_matches_two_per_wave(hip_device, d, mode, mo
         torch.cuda.synchronize()
         assert int(err.item()) == 0
         return out
-    new = run()
-    monkeypatch.setenv("FBN_FIELDS_V", "1")
     old = run()
-    assert torch.equal(new["cnt"], old["cnt"])
+    monkeypatch.setenv("FBN_FIELDS_CMP", "1")
+    new = run()
+    for k in ("X", "Vc", "a", "cnt"):
+        assert torch.equal(new[k], old[k]), k
     assert new["cnt"][0].item() == 1.0 and new["cnt"][1].item() == 1.0
-    assert torch.equal(new["X"][:, 0], old["X"][:, 0])          # the item row: a plain copy
-    for k in ("X", "Vc", "a"):
-        assert (new[k] - old[k]).abs().max().item() <= 2e-6 * max(1.0, old[k].abs().max().item()), k
     # all padding: the history mean is exactly zero; one live slot: exactly that row
     assert torch.all(new["X"][0, 1] == 0)
     ref1 = (rows[pos[1, 8].long()].float() if mode != "table" else table[11])

@@ -6,6 +6,7 @@
 #   bisect     the training-run AUC bisection (tests/parity_bisect.py): launcher runs with the
 #              deterministic fold, the atomic fold (twice) and the IEEE-Adam library, then the
 #              oracle ensemble report (gpurun_out/<tag>/auc_bisect.json)
+#   step1      the first training step per tensor, HIP vs the float64 / fp32 oracle (parity_bisect step1)
 #   bench      the default bench line (gpurun_out/<tag>/bench.json)
 #   benchq     the bench without the CPU / fp32 / inference legs
 #   zipf       the Zipf(1.05) bench line
@@ -41,6 +42,8 @@ for step in "$@"; do
           >> $O/bisect.log 2>&1; rc=$?
       fi
       grep -E "^(hip|f64|fp32)" $O/bisect.log || true ;;
+    step1) timeout -k 10 300 python -m tests.parity_bisect step1 --out $O/step1.json > $O/step1.log 2>&1; rc=$?
+           tail -5 $O/step1.log ;;
     bench) timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err; rc=$?; cat $O/bench.json | head -c 600; echo ;;
     benchq) timeout -k 10 400 python bench.py --no-cpu-baseline --no-cpu-plan --no-inference --no-fp32 \
               > $O/benchq.json 2> $O/benchq.err; rc=$?; head -c 400 $O/benchq.json; echo ;;
@@ -51,9 +54,11 @@ for step in "$@"; do
     shard) FBN_BENCH_SHARD=1 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29533 \
              timeout -k 10 300 python bench.py --gpus 1 --no-fp32 --no-cpu-baseline --no-cpu-plan --no-inference \
              --bn local > $O/shard.json 2> $O/shard.err; rc=$?; head -c 400 $O/shard.json; echo ;;
-    gather) { timeout -k 10 300 python tools/time_fields.py "v1:FBN_FIELDS_V=1" "v2:" "v2_hc4:FBN_FIELDS_HC=4" \
-                "v2_hc8:FBN_FIELDS_HC=8" "v2_hc10:FBN_FIELDS_HC=10" && \
-              D=16 B=4096 V=1000000 timeout -k 10 300 python tools/time_fields.py "v1:FBN_FIELDS_V=1" "v2:"; } \
+    gather) { timeout -k 10 300 python tools/time_fields.py "plain5:" "plain10:FBN_FIELDS_HCH=10" \
+                "plain20:FBN_FIELDS_HCH=20" "cmp5:FBN_FIELDS_CMP=1" "cmp8:FBN_FIELDS_CMP=1,FBN_FIELDS_HCH=8" \
+                "cmp10:FBN_FIELDS_CMP=1,FBN_FIELDS_HCH=10" && \
+              D=16 B=4096 V=1000000 timeout -k 10 300 python tools/time_fields.py "plain5:" "cmp5:FBN_FIELDS_CMP=1" \
+                "cmp10:FBN_FIELDS_CMP=1,FBN_FIELDS_HCH=10"; } \
               > $O/gather.txt 2>&1; rc=$?; cat $O/gather.txt | grep -v Warn ;;
     prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv \
              -d $O/prof -o run -- python $R/bench.py --no-cpu-baseline --no-cpu-plan --no-inference --no-fp32 \

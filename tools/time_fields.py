@@ -4,9 +4,9 @@ Infinity Cache between uses); kernel spans from the library's kernel probes.
 
 Arms (interleaved in one process, ROUNDS rounds; each arm sets environment knobs the library reads
 per call), e.g.
-    python tools/time_fields.py "v1:FBN_FIELDS_V=1" "v2:" "v2_hc10:FBN_FIELDS_HC=10"
-Knobs: FBN_FIELDS_V=1 the two-samples-per-wave gather, FBN_FIELDS_HC the one-wave-per-sample
-gather's rows in flight per row group, FBN_FIELDS_HCH / FBN_FIELDS_NOBUF the old one's, FBN_GATHER_HOT=<tau> hot-row LDS staging; env ZIPF=<s> draws Zipf(s) ids, D / B the shape."""
+    python tools/time_fields.py "plain:" "cmp10:FBN_FIELDS_CMP=1,FBN_FIELDS_HCH=10"
+Knobs: FBN_FIELDS_HCH the history rows in flight per chunk, FBN_FIELDS_CMP=1 live slots compacted
+first, FBN_FIELDS_NOBUF=1 global loads instead of the buffer resource, FBN_GATHER_HOT=<tau> hot-row LDS staging; env ZIPF=<s> draws Zipf(s) ids, D / B the shape."""
 import os
 import sys
 
