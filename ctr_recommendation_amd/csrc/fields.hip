@@ -57,6 +57,8 @@ struct FieldArgs {
   const int* hot;           // optional hot-row list (fbn_hot_rows) staged in LDS: [H] row ids
   const int* hot_n;         // its length (entries past H ignored)
   int H;
+  int abl;                  // measurement only (FBN_FIELDS_ABL, tools/time_fields.py): 1 = no history
+                            // loads, 2 = no field stores, 4 = no item / cate / mm loads; 0 = the real kernel
 };
 
 // hot-row staging (fbn_fields_fwd_hot, an A/B variant of the gather): up to FBN_HOT_ROWS(D) rows
@@ -181,16 +183,17 @@ __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
     // history rows are issued in chunks of HCH slots (all loads of a chunk in flight before
     // any is consumed) and summed in slot order like the reference's sum over dim 1
     // independent loads first (they overlap the row gather below)
-    const f32x4 c1 = *reinterpret_cast<const f32x4*>(p.cate + lk * D + 4 * q);
-    const f32x4 c2 = *reinterpret_cast<const f32x4*>(p.cate + vw * D + 4 * q);
-    const f32x4 h = *reinterpret_cast<const f32x4*>(p.hmm + (size_t)b * D + 4 * q);
+    const bool ld3 = !(p.abl & 4);
+    const f32x4 c1 = ld3 ? *reinterpret_cast<const f32x4*>(p.cate + lk * D + 4 * q) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    const f32x4 c2 = ld3 ? *reinterpret_cast<const f32x4*>(p.cate + vw * D + 4 * q) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    const f32x4 h = ld3 ? *reinterpret_cast<const f32x4*>(p.hmm + (size_t)b * D + 4 * q) : (f32x4){1.f, 2.f, 3.f, 4.f};
     f32x4 rit = {0.f, 0.f, 0.f, 0.f};
     f32x4 hs = {0.f, 0.f, 0.f, 0.f};
     int nnz = 0;
     const int* pb = MODE >= 1 ? p.pos + (size_t)b * (L + 1) : nullptr;
     if (MODE == 0) {
       if (item < 0 || item >= p.V) { bad = true; item = -1; }
-      if (item >= 0) rit = *reinterpret_cast<const f32x4*>(p.table + item * D + 4 * q);
+      if (item >= 0 && ld3) rit = *reinterpret_cast<const f32x4*>(p.table + item * D + 4 * q);
     } else {
       const int pi = pb[0];
       if (pi >= 0) rit = load_row<D, MODE>(p, pi, q);
@@ -256,7 +259,7 @@ __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
       __builtin_amdgcn_wave_barrier();                 // the next sample's list overwrites this one
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
     }
-    for (int t0 = 0; t0 < (CMP ? 0 : L); t0 += HCH) {
+    for (int t0 = 0; t0 < ((CMP || (p.abl & 1)) ? 0 : L); t0 += HCH) {
       // branch-free: every slot of the chunk issues its load (a padding or past-L slot reads row
       // 0, an L2-resident line, and contributes +0 by a select) -- a load under a branch makes
       // hipcc drain vmcnt(0) before the next, which serialised the chunk's round trips
@@ -318,13 +321,15 @@ __global__ void __launch_bounds__(256) fields_fwd_kernel(FieldArgs p) {
 
     // ---------------- stores
     float* Xb = p.X + (size_t)b * 2 * D + 4 * q;
-    *reinterpret_cast<f32x4*>(Xb) = rit;
-    *reinterpret_cast<f32x4*>(Xb + D) = x5;
+    if (!(p.abl & 2)) {
+      *reinterpret_cast<f32x4*>(Xb) = rit;
+      *reinterpret_cast<f32x4*>(Xb + D) = x5;
+    }
     float* Vb = p.Vc ? p.Vc + (size_t)b * 5 * D + 4 * q : nullptr;
     float* cb = (p.c && !p.c16) ? (float*)p.c + (size_t)b * p.ldc + 4 * q : nullptr;
     short* cb16 = (p.c && p.c16) ? (short*)p.c + (size_t)b * p.ldc + 4 * q : nullptr;
 #pragma unroll
-    for (int f = 0; f < 5; ++f) {
+    for (int f = 0; f < 5 && !(p.abl & 2); ++f) {
       const f32x4 v = xs[f] * a[f + 1];
       if (p.Vc) *reinterpret_cast<f32x4*>(Vb + f * D) = v;   // bf16 mode: only the bf16 copies
       const bf16x4 v16 = (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
@@ -836,6 +841,8 @@ static int fields_fwd_impl(const int64_t* item_id, const int64_t* item_seq, cons
   a.map = map; a.slot_row = slot_row;
   a.V = V; a.B = B; a.L = L; a.ldc = ldc; a.R = R; a.n_cate = n_cate; a.ln_eps = ln_eps; a.c16 = c_bf16;
   a.hot = hot; a.hot_n = hot_n; a.H = H;
+  const char* ae = getenv("FBN_FIELDS_ABL");   // measurement only (NOT a valid forward when set)
+  a.abl = ae ? atoi(ae) : 0;
   if (pos && rows_bf16) return launch_fields_fwd<2>(a, D, (hipStream_t)stream);
   if (pos) return launch_fields_fwd<1>(a, D, (hipStream_t)stream);
   return launch_fields_fwd<0>(a, D, (hipStream_t)stream);

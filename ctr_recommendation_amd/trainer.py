@@ -91,9 +91,10 @@ _EARLY_GRAD_XCHG = os.environ.get("FBN_EARLY_GRAD_XCHG")
 # the bilinear backward, beside the fields backward (HBM-bound) on the main stream; dW_p stays in the
 # flush's launch on main, which waits for the side stream before the slab sums
 _WGRAD_EARLY = os.environ.get("FBN_WGRAD_EARLY", "0") == "1"
-# single GPU, d >= 128: the next-batch prefetch's replay balanced longest-first (fbn_adam_prefetch_binned);
-# FBN_PF_BINNED=0 keeps adam_prefetch2's 64-entries-per-wave replay (A/B)
-_PF_BINNED = os.environ.get("FBN_PF_BINNED", "1") != "0"
+# single GPU, d >= 128, A/B knob FBN_PF_BINNED=1: the next-batch prefetch's replay balanced longest-first
+# (fbn_adam_prefetch_binned).  Bit-identical, measured slower (0.443 vs 0.421 ms/step at C3),
+# so adam_prefetch2's 64-entries-per-wave replay stays the default
+_PF_BINNED = os.environ.get("FBN_PF_BINNED", "0") == "1"
 # N > 1, the owner's ahead-of-time catch-up of the next step's requested rows in two passes (tagged
 # pre-claims + the four-row replay engine); FBN_OWNER_PF2=0 keeps the one-pass kernel (A/B)
 _OWNER_PF2 = os.environ.get("FBN_OWNER_PF2", "1") != "0"

@@ -13,8 +13,11 @@ valid AUC and its distance (|dAUC|, max / mean |dp|) from the float64 loop:
 * fp32 / f64: the oracle in float32 / float64 (the chaos floor of two correct implementations);
 * fp32_t<n>: fp32 on n CPU threads (other reduction orders inside torch's kernels);
 * fp32_foreach / fp32_fused: torch's multi-tensor / fused Adam (other operation orders of the step);
-* f64_n<k>: float64 with relative 2^-24 noise (seed k) injected into every parameter after every
-  step: an exact implementation that rounds like fp32 -- an independent trajectory of the chaos;
+* f64_n<k> / fp32_n<k>: float64 (fp32) with relative 2^-24 noise (seed k) injected into every
+  parameter after every step: an implementation that rounds like fp32 -- an independent trajectory
+  of the chaos (the torch variants above share torch's kernels and stay correlated);
+* fp32_g<k>: fp32 with gradient noise 10^-k x max |g| per tensor (does rounding-level gradient noise
+  shift the learned AUC systematically?);
 * fp32_fx40: the per-entry table-gradient vectors rounded to the 2^-40 fixed-point grid before the
   row sums -- what the deterministic duplicate fold (csrc/optim.hip sparse_fold_fx_kernel) did to
   every row several entries hit.
@@ -82,17 +85,35 @@ def run_variant(name, data, perms, epochs, bs, n_train, n_valid):
             ref.shift = int(name[len("fp32_fx"):])
         if f64:
             ref = ref.double()
+        gnoise = None
+        if name.startswith("fp32_g"):
+            # fp32 with relative gradient noise 10^-k of each tensor's max |g| injected before the
+            # clip (diagnosis: does rounding-level gradient noise degrade the learned AUC?)
+            gnoise = (float(10.0 ** -int(name[len("fp32_g"):])), torch.Generator().manual_seed(17))
         noise = None
-        if name.startswith("f64_n"):
-            # float64 with fp32-level rounding noise injected into every parameter after every step
-            # (relative 2^-24 x N(0,1), seed k): an exact implementation that rounds like fp32 --
+        if name.startswith(("f64_n", "fp32_n")):
+            # fp32-level rounding noise (relative 2^-24 x N(0,1), seed k) injected into every parameter
+            # after every step, in float64 (an exact implementation that rounds like fp32) or fp32:
             # one more independent trajectory of the chaos every fp32 implementation goes through
-            ref = ref.double()
-            f64 = True
-            noise = torch.Generator().manual_seed(int(name[len("f64_n"):]))
+            if name.startswith("f64_n"):
+                ref = ref.double()
+                f64 = True
+            noise = torch.Generator().manual_seed(int(name.split("_n")[1]))
         cast = (lambda t: t.double() if t.is_floating_point() else t) if f64 else (lambda t: t)
         steps_per_epoch = -(-n_train // bs)
         otr = OracleTrainer(ref, lr=1e-3, weight_decay=1e-5, total_steps=epochs * steps_per_epoch)
+        if gnoise is not None:
+            amp, gen_ = gnoise
+
+            def noisy_clip(params, max_norm, _orig=torch.nn.utils.clip_grad_norm_):
+                params = list(params)
+                with torch.no_grad():
+                    for prm in params:
+                        if prm.grad is not None:
+                            prm.grad.add_(amp * prm.grad.abs().max() * torch.randn(prm.grad.shape, generator=gen_))
+                return _orig(params, max_norm=max_norm)
+            import oracle.fibinet_oracle as ofo
+            ofo.torch.nn.utils.clip_grad_norm_ = noisy_clip
         if name in ("fp32_foreach", "fp32_fused"):
             otr.opt.param_groups[0]["foreach" if name == "fp32_foreach" else "fused"] = True
         aucs, losses, probs, steps = [], [], [], []
@@ -105,7 +126,8 @@ def run_variant(name, data, perms, epochs, bs, n_train, n_valid):
                 if noise is not None:
                     with torch.no_grad():
                         for prm in ref.parameters():
-                            prm.mul_(1.0 + 2.0 ** -24 * torch.randn(prm.shape, generator=noise, dtype=torch.float64))
+                            prm.mul_((1.0 + 2.0 ** -24 * torch.randn(prm.shape, generator=noise,
+                                                                     dtype=torch.float64)).to(prm.dtype))
                 steps.append(ls)
                 tot += ls
             losses.append(tot / steps_per_epoch)
@@ -123,11 +145,14 @@ def run_variant(name, data, perms, epochs, bs, n_train, n_valid):
             ref.train()
     finally:
         torch.set_num_threads(nthreads)
+        if gnoise is not None:
+            import oracle.fibinet_oracle as ofo
+            ofo.torch.nn.utils.clip_grad_norm_ = noisy_clip.__defaults__[0]
     return {"auc": aucs, "loss": losses, "probs": probs, "step_loss": steps,
             "sd": {k: v.detach().double().clone() for k, v in ref.state_dict().items()}}
 
 
-ENSEMBLE = ("fp32", "fp32_t1", "fp32_t2", "fp32_fused", "f64_n1", "f64_n2")
+ENSEMBLE = ("fp32", "fp32_t1", "fp32_t2", "fp32_fused", "f64_n1", "f64_n2", "f64_n3", "f64_n4")
 BS, N_TRAIN, N_VALID, EPOCHS, N_ITEMS = 512, 51200, 8192, 2, 5000
 PARITY_CONFIG = """
 base_expid: MM_FiBiNET_Run
@@ -308,7 +333,7 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("mode", choices=("cpu", "hip", "report", "step1"))
     ap.add_argument("--out", default=None)
-    ap.add_argument("--variants", default="f64,fp32,fp32_t1,fp32_t2,fp32_fused,f64_n1,f64_n2,fp32_fx40")
+    ap.add_argument("--variants", default="f64,fp32,fp32_t1,fp32_t2,fp32_fused,f64_n1,f64_n2,f64_n3,f64_n4,fp32_fx40,fp32_g6")
     ap.add_argument("--perm-seed", type=int, default=5)
     ap.add_argument("--tag", default="default")
     ap.add_argument("--nondet", action="store_true")

@@ -13,6 +13,7 @@
 #   c2         the C2 bench line (d 16, B 4096, 1 M rows)
 #   shard      the sharded step as a one-rank RCCL job (per-GPU BatchNorm)
 #   gather     the gather arms (tools/time_fields.py) at C3 and C2 shapes
+#   gabl       the gather's ablations (FBN_FIELDS_ABL: no history loads / no stores / no other loads)
 #   prof       rocprofv3 kernel trace + stats of the quick bench
 #   pmc        the PMC passes (tools/gpu_pmc.sh)
 #   ab:R:ARM1|ARM2|...   interleaved bench arms (tools/ab_arms.sh; an arm is "VAR=x VAR2=y", "-" = default)
@@ -60,6 +61,9 @@ for step in "$@"; do
               D=16 B=4096 V=1000000 timeout -k 10 300 python tools/time_fields.py "plain5:" "cmp5:FBN_FIELDS_CMP=1" \
                 "cmp10:FBN_FIELDS_CMP=1,FBN_FIELDS_HCH=10"; } \
               > $O/gather.txt 2>&1; rc=$?; cat $O/gather.txt | grep -v Warn ;;
+    gabl) timeout -k 10 300 python tools/time_fields.py "real:" "nohist:FBN_FIELDS_ABL=1" "nostore:FBN_FIELDS_ABL=2" \
+            "noitem:FBN_FIELDS_ABL=4" "stores_only:FBN_FIELDS_ABL=5" "hist_only:FBN_FIELDS_ABL=6" "none:FBN_FIELDS_ABL=7" \
+            > $O/gabl.txt 2>&1; rc=$?; grep -v Warn $O/gabl.txt ;;
     prof) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv \
              -d $O/prof -o run -- python $R/bench.py --no-cpu-baseline --no-cpu-plan --no-inference --no-fp32 \
              > $O/prof.log 2>&1); rc=$?; [ -f $O/prof/run_kernel_trace.csv ] && gzip -f $O/prof/run_kernel_trace.csv ;;
