@@ -111,6 +111,9 @@ SIGNATURES = {
     "fbn_unpack_extras": (I, [P, P, P, P]),
     "fbn_step_end": (I, [P, P, P, P, P, I, P, P]),
     "fbn_route": (I, [P, P, I, I, LL, LL, I, P, P, P, P, P, P, P]),
+    "fbn_route_fc": (I, [P, P, I, I, LL, LL, I, I, P, P, P, P, P]),
+    "fbn_route_fc_status": (I, [P, I, I, P, P, P]),
+    "fbn_ring_slot": (I, [P, I, LL, P, P, P, I, LL, P]),
     "fbn_owner_claim": (I, [P, I, P, P, I, P]),
     "fbn_owner_gather": (I, [P, I, P, P, P, P, I, I, I, P]),
     "fbn_widen_bf16": (I, [P, P, LL, P]),
@@ -125,10 +128,11 @@ SIGNATURES = {
     "fbn_plan_create": (I, [P]),
     "fbn_plan_destroy": (I, [P]),
     "fbn_plan_size": (I, [P]),
-    "fbn_plan_add_call": (I, [P, P, P, I, P, I]),
+    "fbn_plan_add_call": (I, [P, ctypes.c_char_p, P, I, P, I]),
     "fbn_plan_add_record": (I, [P, I, P]),
     "fbn_plan_add_wait": (I, [P, P, I]),
     "fbn_plan_run": (I, [P, P]),
+    "fbn_plan_event_sync": (I, [P, I]),
     "fbn_probe_arm": (I, [I]),
     "fbn_probe_disarm": (I, []),
     "fbn_probe_elapsed": (F, [I]),
@@ -311,7 +315,7 @@ class StepProgram:
                     self.keep.append(v)
         ia = (ctypes.c_ulonglong * max(1, len(ints)))(*ints)
         fa = (ctypes.c_double * max(1, len(flts)))(*flts)
-        call_raw("fbn_plan_add_call", self.h, ctypes.cast(f, ctypes.c_void_p), ia, len(ints), fa, len(flts))
+        call_raw("fbn_plan_add_call", self.h, name.encode(), ia, len(ints), fa, len(flts))
 
     def slot_of(self, ev) -> int:
         k = id(ev)

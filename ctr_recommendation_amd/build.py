@@ -11,6 +11,8 @@ import subprocess
 import sys
 from concurrent.futures import ThreadPoolExecutor
 
+from . import gen_thunks
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 ROOT = os.path.dirname(HERE)
@@ -26,12 +28,13 @@ FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-re
 def _compile(src: str, build_dir: str = BUILD, defines=()) -> str:
     path = os.path.join(CSRC, src)
     obj = os.path.join(build_dir, src + ".o")
-    deps = [path] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
+    deps = [path] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith((".h", ".inc"))]
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
         return obj
     cmd = [HIPCC] + FLAGS + [f"-D{d}" for d in defines] + ["-c", path, "-o", obj]
     if src.endswith(".cpp"):
-        cmd = [HIPCC, "-O3", "-fPIC", "-std=c++17", "-c", path, "-o", obj]
+        cmd = [HIPCC, "-O3", "-fPIC", "-std=c++17", "-I", CSRC, "-I", os.path.join(ROOT, "include"), "-c", path,
+               "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed on {src}:\n{r.stderr}")
@@ -40,6 +43,7 @@ def _compile(src: str, build_dir: str = BUILD, defines=()) -> str:
 
 def build(verbose: bool = True) -> str:
     os.makedirs(BUILD, exist_ok=True)
+    gen_thunks.write_if_changed(verbose)     # the step programs' thunks follow include/fibinet.h
     with ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
         objs = list(ex.map(_compile, SOURCES))
     newest = max(os.path.getmtime(o) for o in objs)
@@ -64,6 +68,7 @@ VARIANTS = {
 def build_variant(name: str, verbose: bool = True) -> str:
     defines = VARIANTS[name]
     bdir = os.path.join(ROOT, "build", "variant_" + name)
+    gen_thunks.write_if_changed(verbose)
     os.makedirs(bdir, exist_ok=True)
     with ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
         objs = list(ex.map(lambda s: _compile(s, bdir, defines), SOURCES))

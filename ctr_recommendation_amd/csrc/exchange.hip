@@ -51,11 +51,17 @@ __global__ void route_scan_kernel(const int* counts, int nranks, int* offsets, i
 // per-owner totals take ONE global atomic each (a per-entry atomicAdd on cursor[o] serialised all
 // B*(L+1) entries of a step on nranks counters: ~1 ms per step at N = 1, ~0.25 ms at N = 8).
 // Order inside a round is deterministic (wave, lane); rounds of different workgroups race.
+// FC (the fixed-capacity exchange, fbn_route_fc): owner o's segment is block o of cap + 1 slots
+// (position o * (cap + 1) + k); an entry past k = cap - 1 is not routed (pos -1) and flags the
+// routing as overflowed -- *ovf = 1 and every block's last slot = -2 (the flag travels in-band
+// with the ids, so every owner learns that some requester overflowed)
+template <bool FC>
 __global__ void __launch_bounds__(256) route_fill_kernel(const int64_t* __restrict__ item,
                                                          const int64_t* __restrict__ seq, int B, int L, long long V,
                                                          long long Vl, int nranks, const int* __restrict__ offsets,
                                                          int* __restrict__ cursor, int* __restrict__ send_ids,
-                                                         int* __restrict__ pos) {
+                                                         int* __restrict__ pos, int cap, int* __restrict__ ovf,
+                                                         int* __restrict__ err) {
   __shared__ int wc[4][64];     // per wave, per owner: entries this round
   __shared__ int gb[4][64];     // per wave, per owner: first position
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -70,6 +76,8 @@ __global__ void __launch_bounds__(256) route_fill_kernel(const int64_t* __restri
       if (id >= 0 && id < V && !(t > 0 && id == 0)) {
         o = (int)(id / Vl);
         lid = (int)(id - (long long)o * Vl);
+      } else if (FC && (id < 0 || id >= V)) {
+        atomicOr(err, 1);                            // (the count pass flags them in the other form)
       }
     }
     __syncthreads();
@@ -86,7 +94,7 @@ __global__ void __launch_bounds__(256) route_fill_kernel(const int64_t* __restri
     if (threadIdx.x < nranks) {
       const int q = threadIdx.x;
       const int n = wc[0][q] + wc[1][q] + wc[2][q] + wc[3][q];
-      int base = n ? offsets[q] + atomicAdd(&cursor[q], n) : 0;
+      int base = n ? (FC ? 0 : offsets[q]) + atomicAdd(&cursor[q], n) : 0;
 #pragma unroll
       for (int w = 0; w < 4; ++w) { gb[w][q] = base; base += wc[w][q]; }
     }
@@ -95,12 +103,36 @@ __global__ void __launch_bounds__(256) route_fill_kernel(const int64_t* __restri
       int p = -1;
       if (o >= 0) {
         p = gb[wave][o] + rank;
-        send_ids[p] = lid;
+        if (FC) {
+          if (p >= cap) {
+            p = -1;
+            atomicOr(ovf, 1);
+            for (int k = 0; k < nranks; ++k) send_ids[(size_t)k * (cap + 1) + cap] = -2;
+          } else {
+            p += o * (cap + 1);
+          }
+        }
+        if (p >= 0) send_ids[p] = lid;
       }
       pos[e] = p;
     }
     __syncthreads();                                 // wc / gb are rewritten by the next round
   }
+}
+
+// the fixed-capacity routing's initial state: every slot "no row" (-1), counters and flag zero
+__global__ void route_fc_init_kernel(int* __restrict__ send_ids, long long n, int* __restrict__ stat, int nstat) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    send_ids[i] = -1;
+  if (blockIdx.x == 0 && threadIdx.x < nstat) stat[threadIdx.x] = 0;
+}
+
+// owner side of a fixed-capacity routing: stat[0] |= "some requester overflowed" (a block whose
+// last slot is -2) -- the same value on every rank, so all of them agree on a fallback
+__global__ void route_fc_status_kernel(const int* __restrict__ recv_ids, int world, int cap, int* __restrict__ stat) {
+  const int r = threadIdx.x;
+  const bool f = r < world && recv_ids[(size_t)r * (cap + 1) + cap] == -2;
+  if (__ballot(f) != 0ull && r == 0) stat[0] = 1;
 }
 
 // owner side: out[i] = E_local[ids[i]]; G = D/4 lanes per row.  Received entry i claims its
@@ -119,6 +151,7 @@ __global__ void __launch_bounds__(256) owner_gather_kernel(const int* __restrict
     const long long i = i0 + lane / G;
     if (i >= n) continue;
     const int r = ids[i];
+    if (r < 0) continue;   // a fixed-capacity block's empty slot: nothing requested
     const f32x4 row = *reinterpret_cast<const f32x4*>(E + (size_t)r * D + 4 * q);
     if (out_bf16)   // bf16 mode: the rows cross the wire as bf16 (half the all-to-all bytes)
       *reinterpret_cast<bf16x4*>(reinterpret_cast<short*>(out) + i * D + 4 * q) =
@@ -140,7 +173,7 @@ __global__ void __launch_bounds__(256) owner_gather_kernel(const int* __restrict
 __global__ void owner_claim_kernel(const int* __restrict__ ids, int n, int* map, int* slot_row, int rank) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const int r = ids[i];
-    if (rank == 0 && r == 0) continue;
+    if (r < 0 || (rank == 0 && r == 0)) continue;
     if (__hip_atomic_load(map + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != -1) continue;
     int expected = -1;
     if (__hip_atomic_compare_exchange_strong(map + r, &expected, i, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
@@ -173,9 +206,51 @@ extern "C" int fbn_route(const int64_t* item, const int64_t* seq, int B, int L, 
   fbn_launch(route_count_kernel, dim3(std::min(blocks, 256)), dim3(256), 0, st, item, L > 0 ? seq : nullptr,
                      B, L, V, Vl, nranks, counts, err);
   fbn_launch(route_scan_kernel, dim3(1), dim3(1), 0, st, counts, nranks, offsets, cursor);
-  fbn_launch(route_fill_kernel, dim3(blocks), dim3(256), 0, st, item, L > 0 ? seq : nullptr, B, L, V, Vl,
-                     nranks, offsets, cursor, send_ids, pos);
+  fbn_launch(route_fill_kernel<false>, dim3(blocks), dim3(256), 0, st, item, L > 0 ? seq : nullptr, B, L, V, Vl,
+                     nranks, offsets, cursor, send_ids, pos, 0, nullptr, nullptr);
   FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+// The fixed-capacity routing: entry positions o * (cap + 1) + k in owner o's block, blocks
+// pre-filled with -1, stat = [overflow flag, entries requested from owner 0 .. nranks-1] (the
+// requested counts include entries past cap).  No count pass and no host-side counts: the ids,
+// looked-up rows and gradient rows all cross as equal-split all-to-alls of cap + 1 slots.
+extern "C" int fbn_route_fc(const int64_t* item, const int64_t* seq, int B, int L, long long V, long long Vl, int nranks,
+                            int cap, int* send_ids, int* pos, int* stat, int* err, void* stream) {
+  if (nranks < 1 || nranks > 64 || cap < 1) { fbn_set_error("fbn_route_fc: 1 <= nranks <= 64, cap >= 1"); return FBN_ERR_ARG; }
+  if (!item || !send_ids || !pos || !stat || !err || (L > 0 && !seq)) { fbn_set_error("fbn_route_fc: null buffer"); return FBN_ERR_ARG; }
+  hipStream_t st = (hipStream_t)stream;
+  const long long nslots = (long long)nranks * (cap + 1);
+  long long iblocks = (nslots + 255) / 256;
+  if (iblocks > 1024) iblocks = 1024;
+  fbn_launch(route_fc_init_kernel, dim3((unsigned)iblocks), dim3(256), 0, st, send_ids, nslots, stat, nranks + 1);
+  const long long total = (long long)B * (L + 1);
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  fbn_launch(route_fill_kernel<true>, dim3(blocks), dim3(256), 0, st, item, L > 0 ? seq : nullptr, B, L, V, Vl,
+             nranks, nullptr, stat + 1, send_ids, pos, cap, stat, err);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+// After the ids all-to-all of a fixed-capacity routing: stat[0] becomes the GLOBAL overflow flag
+// (this rank's, or any requester's in-band flag), then stat[0 .. nranks] is copied to `host`
+// (pinned) on the stream -- the host reads it once the stream got there and, if set, every rank
+// exchanges that step with host-side split sizes instead (RowExchange).
+extern "C" int fbn_route_fc_status(const int* recv_ids, int nranks, int cap, int* stat, int* host, void* stream) {
+  if (nranks < 1 || nranks > 64 || cap < 1 || !recv_ids || !stat) {
+    fbn_set_error("fbn_route_fc_status: 1 <= nranks <= 64, cap >= 1, buffers");
+    return FBN_ERR_ARG;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  fbn_launch(route_fc_status_kernel, dim3(1), dim3(64), 0, st, recv_ids, nranks, cap, stat);
+  FBN_CHECK_LAUNCH();
+  if (host && hipMemcpyAsync(host, stat, sizeof(int) * (nranks + 1), hipMemcpyDeviceToHost, st) != hipSuccess) {
+    fbn_set_error("fbn_route_fc_status: hipMemcpyAsync failed");
+    return FBN_ERR_LAUNCH;
+  }
   return FBN_OK;
 }
 

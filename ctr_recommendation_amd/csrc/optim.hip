@@ -218,6 +218,10 @@ __global__ void adam_dense_kernel(float* __restrict__ p, const float* __restrict
 // Lp1 | FBN_GRAD_FULL (deterministic mode): extra[e] of a flagged claimer holds the row's FULL
 // gradient (fbn_sparse_fold_fx), not the sum of its duplicates
 #define FBN_GRAD_FULL 0x10000
+// Lp1 | FBN_GRAD_CELL: `vec` is the address of a device cell holding the row pointer (fbn_ring_slot:
+// the owner's received gradient rows in deferred-gradient ring slot step % ring_n, a slot chosen on
+// the device, so a recorded step program needs no host-side ring index)
+#define FBN_GRAD_CELL 0x20000
 #define FBN_FOLD_CHUNKS 1     // sparse_fixup_dup_kernel: 64-entry chunks per wave
 #define FBN_FOLD_THREADS 1024 // sparse_fixup_dup_kernel: 16 waves share one LDS table
 struct GradSrc {
@@ -226,9 +230,15 @@ struct GradSrc {
   int* slot_row;        // [n] claimed row | FLAG, or -1
   int Lp1;
   int full;             // extra of a flagged claimer = the whole row gradient
+  int cell;             // vec holds the address of a device cell with the row pointer (FBN_GRAD_CELL)
 };
 static inline GradSrc make_src(const float* vec, float* extra, int* slot_row, int lp1_flags) {
-  return GradSrc{vec, extra, slot_row, lp1_flags & 0xffff, (lp1_flags & FBN_GRAD_FULL) ? 1 : 0};
+  return GradSrc{vec, extra, slot_row, lp1_flags & 0xffff, (lp1_flags & FBN_GRAD_FULL) ? 1 : 0,
+                 (lp1_flags & FBN_GRAD_CELL) ? 1 : 0};
+}
+// a kernel's first step with a GradSrc: FBN_GRAD_CELL's pointer read from its cell
+__device__ __forceinline__ void resolve_src(GradSrc& s) {
+  if (s.cell) s.vec = *reinterpret_cast<const float* const*>(s.vec);
 }
 
 template <int D>
@@ -245,6 +255,7 @@ __global__ void __launch_bounds__(256) sparse_fixup_kernel(const int64_t* __rest
                                                            const int64_t* __restrict__ seq, const int* __restrict__ ids,
                                                            int n, int L, long long V, int rank,
                                                            const int* __restrict__ map, GradSrc s) {
+  resolve_src(s);
   constexpr int G = D / 4, RPW = 64 / G;
   const int lane = threadIdx.x & 63, q = lane % G;
   const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -255,7 +266,7 @@ __global__ void __launch_bounds__(256) sparse_fixup_kernel(const int64_t* __rest
     long long r;
     if (ids) {
       r = ids[e];
-      if (rank == 0 && r == 0) continue;
+      if (r < 0 || (rank == 0 && r == 0)) continue;   // r < 0: a fixed-capacity block's empty slot
     } else {
       const long long b = e / (L + 1), t = e - b * (L + 1);
       r = t == 0 ? item[b] : seq[b * L + (t - 1)];
@@ -269,7 +280,7 @@ __global__ void __launch_bounds__(256) sparse_fixup_kernel(const int64_t* __rest
       if (q == 0) atomicOr(&s.slot_row[u], FBN_SLOT_FLAG);
       dst = s.extra + (size_t)u * D;
     } else {
-      dst = const_cast<float*>(s.vec) + (size_t)u * D;
+      dst = const_cast<float*>(s.vec) + (size_t)u * D;   // (the resolved pointer under FBN_GRAD_CELL)
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) atomicAdd(dst + k * G + q, src[k * G + q]);
@@ -547,6 +558,7 @@ __global__ void __launch_bounds__(256) sumsq_norms_kernel(GradSrc s, const doubl
 // sum of squares of the clipped-to-be table gradient, over claiming entries only
 template <int D>
 __global__ void __launch_bounds__(256) sumsq_sparse_kernel(GradSrc s, int n, double* __restrict__ out) {
+  resolve_src(s);
   constexpr int G = D / 4, RPW = 64 / G;
   __shared__ double red[256];
   const int lane = threadIdx.x & 63, q = lane % G;
@@ -597,6 +609,7 @@ __device__ __forceinline__ void adam_table_body(float* __restrict__ p, float* __
                                                          const AdamConsts* __restrict__ table,
                                                          const int* __restrict__ step_ptr, float wd, float b2, float omb2,
                                                          float eps) {
+  resolve_src(gs);
   constexpr int G = D / 4;
   constexpr int RPW = 64 / G;
   const AdamConsts k = table[*step_ptr];
@@ -1843,6 +1856,7 @@ __global__ void __launch_bounds__(256) adam_touched_kernel(float* __restrict__ p
                                                            const AdamConsts* __restrict__ table,
                                                            const int* __restrict__ step_ptr, float wd, float b2,
                                                            float omb2, float eps, int* __restrict__ last) {
+  resolve_src(gs);
   constexpr int G = D / 4, RPW = 64 / G;
   const AdamConsts k = table[*step_ptr];
   const float coef = coef_ptr ? *coef_ptr : 1.f;
@@ -1987,6 +2001,7 @@ __global__ void __launch_bounds__(256) adam_commit_kernel(float* __restrict__ p,
                                                           const int* __restrict__ step_ptr, float wd, float b2,
                                                           float omb2, float eps, int* __restrict__ last, PendSrc ps,
                                                           float* __restrict__ coef_hist, int B) {
+  resolve_src(gs);
   const int t = *step_ptr;
   const AdamConsts k = table[t];
   const float coef = coef_ptr ? *coef_ptr : 1.f;
@@ -2019,6 +2034,7 @@ __global__ void __launch_bounds__(256) adam_tail_kernel(float* __restrict__ dp, 
                                                         const AdamConsts* __restrict__ table, float wd, float b2,
                                                         float omb2, float eps, int* __restrict__ last, PendSrc ps,
                                                         float* __restrict__ coef_hist, int B, StepEnd se) {
+  resolve_src(gs);
   __shared__ float sc;
   __shared__ unsigned is_last;
   const int t = *se.step;
@@ -2151,6 +2167,48 @@ static dim3 group_grid(long long n, int D, long long cap) {
   if (blocks < 1) blocks = 1;
   if (blocks > cap) blocks = cap;
   return dim3((unsigned)blocks);
+}
+
+// N > 1 owner, deferred table gradients: the received gradient rows (wire: n floats, bf16 or f32)
+// widened / copied into ring slot step % ring_n, whose address goes to *cell (read by the fold,
+// the norm and the step tail through FBN_GRAD_CELL)
+__global__ void __launch_bounds__(256) ring_slot_kernel(float* __restrict__ ring, int ring_n, long long stride,
+                                                        const int* __restrict__ step, float** __restrict__ cell,
+                                                        const void* __restrict__ wire, int wire_bf16, long long n8) {
+  float* dst = ring + (size_t)(*step % ring_n) * stride;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *cell = dst;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    f32x4 a, b;
+    if (wire_bf16) {
+      const bf16x8 v = reinterpret_cast<const bf16x8*>(wire)[i];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        a[k] = __uint_as_float((unsigned)(unsigned short)v[k] << 16);
+        b[k] = __uint_as_float((unsigned)(unsigned short)v[k + 4] << 16);
+      }
+    } else {
+      a = reinterpret_cast<const f32x4*>(wire)[2 * i];
+      b = reinterpret_cast<const f32x4*>(wire)[2 * i + 1];
+    }
+    reinterpret_cast<f32x4*>(dst)[2 * i] = a;
+    reinterpret_cast<f32x4*>(dst)[2 * i + 1] = b;
+  }
+}
+
+extern "C" int fbn_ring_slot(float* ring, int ring_n, long long stride, const int* step, void* cell, const void* wire,
+                             int wire_bf16, long long n, void* stream) {
+  if (!ring || !step || !cell || ring_n < 1 || n < 0 || n > stride || (n & 7) || (n > 0 && !wire) ||
+      ((uintptr_t)ring & 15) || (stride & 7) || ((uintptr_t)wire & 15)) {
+    fbn_set_error("fbn_ring_slot: ring, step, cell; n % 8 == 0, n <= stride, 16-B aligned buffers");
+    return FBN_ERR_ARG;
+  }
+  long long blocks = (n / 8 + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 8192) blocks = 8192;
+  fbn_launch(ring_slot_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, ring, ring_n, stride, step,
+             (float**)cell, wire, wire_bf16, n / 8);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
 }
 
 // gvec: single GPU per-sample vectors [B][2][D] (Lp1 = L+1) or owner per-entry rows [n][D] (Lp1 = 1)

@@ -8,17 +8,12 @@
 // edges) while running it, and replays them natively: the same launches on the same streams in
 // the same order, so a replay is bit-identical to the eager step it was recorded from.
 //
-// Replay calls each recorded entry point through one generic signature.  Every fbn_* entry
-// point takes only INTEGER-class arguments (pointers, int, long long, size_t, unsigned) and
-// SSE-class scalars (float, double), and returns int.  Under the x86-64 System V calling
-// convention integer-class arguments occupy rdi, rsi, rdx, rcx, r8, r9 and then 8-byte stack
-// slots in order, and SSE-class arguments occupy xmm0..xmm7 in order, independently of each
-// other.  So a call through `int (*)(u64 x 48, double x 8)` with the integer arguments in
-// order (int32 values sign-extended) and the float arguments as doubles whose low 32 bits
-// hold the float's bits (a float argument is read from the low 32 bits of its xmm register)
-// passes exactly what the real prototype expects; the callee ignores the unused tail, and the
-// caller pops the stack.  Entry points with more than 48 integer or 8 float arguments are
-// refused at record time.
+// Replay calls each recorded entry point through a packed-argument thunk generated from
+// include/fibinet.h (csrc/plan_thunks.inc, ctr_recommendation_amd/gen_thunks.py): the thunk
+// takes the recorded arguments as two arrays -- integer-class values (pointers, int, long long,
+// size_t) as 64-bit words, float / double values as doubles (a float in the low 32 bits of its
+// double) -- and makes an ordinary, well-typed call of the entry point's declared prototype.
+// A recording names the entry point; its argument counts are checked against the thunk's.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -27,9 +22,7 @@
 
 #include <vector>
 
-#if !defined(__x86_64__) || !defined(__linux__)
-#error "step programs rely on the x86-64 System V calling convention"
-#endif
+#include "fibinet.h"
 
 void fbn_set_error(const char* msg);
 
@@ -39,16 +32,44 @@ constexpr int kMaxInt = 48;
 constexpr int kMaxFlt = 8;
 
 typedef uint64_t U;
-typedef int (*GenericFn)(U, U, U, U, U, U, U, U, U, U, U, U, U, U, U, U, U, U, U, U, U, U, U, U, U, U, U, U,
-                         U, U, U, U, U, U, U, U, U, U, U, U, U, U, U, U, U, U, U, U, double, double, double,
-                         double, double, double, double, double);
+typedef int (*ThunkFn)(const U* i, const double* f);
+
+struct PlanThunk {
+  const char* name;
+  ThunkFn fn;
+  int ni, nf;
+};
+
+// a float argument: the low 32 bits of its double slot (the recorder's encoding)
+inline float plan_f32(double d) {
+  uint64_t b;
+  memcpy(&b, &d, sizeof(b));
+  const uint32_t lo = (uint32_t)b;
+  float x;
+  memcpy(&x, &lo, sizeof(x));
+  return x;
+}
+
+#include "plan_thunks.inc"
+
+const PlanThunk* find_thunk(const char* name) {
+  size_t lo = 0, hi = sizeof(kPlanThunks) / sizeof(kPlanThunks[0]);
+  while (lo < hi) {
+    const size_t mid = (lo + hi) / 2;
+    const int c = strcmp(kPlanThunks[mid].name, name);
+    if (c == 0) return &kPlanThunks[mid];
+    if (c < 0) lo = mid + 1;
+    else hi = mid;
+  }
+  return nullptr;
+}
 
 enum OpKind { kCall = 0, kRecord = 1, kWait = 2 };
 
 struct Op {
   int kind;
   int slot;                // kRecord / kWait: event slot
-  void* fn;                // kCall
+  ThunkFn fn;              // kCall
   hipStream_t stream;      // kRecord / kWait
   U i[kMaxInt];
   double f[kMaxFlt];
@@ -60,15 +81,7 @@ struct Plan {
   std::vector<hipEvent_t> events;
 };
 
-int call_op(const Op& o) {
-  GenericFn fn = reinterpret_cast<GenericFn>(o.fn);
-  const U* a = o.i;
-  const double* f = o.f;
-  return fn(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7], a[8], a[9], a[10], a[11], a[12], a[13], a[14], a[15],
-            a[16], a[17], a[18], a[19], a[20], a[21], a[22], a[23], a[24], a[25], a[26], a[27], a[28], a[29], a[30],
-            a[31], a[32], a[33], a[34], a[35], a[36], a[37], a[38], a[39], a[40], a[41], a[42], a[43], a[44], a[45],
-            a[46], a[47], f[0], f[1], f[2], f[3], f[4], f[5], f[6], f[7]);
-}
+int call_op(const Op& o) { return o.fn(o.i, o.f); }
 
 // The program's events only order work between streams of one device, so their release need not be
 // system scope (the default: an L2 writeback + invalidate at every record, ~6 us of idle on the
@@ -117,17 +130,26 @@ extern "C" int fbn_plan_destroy(void* plan) {
 
 extern "C" int fbn_plan_size(void* plan) { return plan ? (int)static_cast<Plan*>(plan)->ops.size() : 0; }
 
-extern "C" int fbn_plan_add_call(void* plan, void* fn, const unsigned long long* iargs, int ni, const double* fargs,
-                                 int nf) {
+extern "C" int fbn_plan_add_call(void* plan, const char* name, const unsigned long long* iargs, int ni,
+                                 const double* fargs, int nf) {
   Plan* p = static_cast<Plan*>(plan);
-  if (!p || !fn || ni < 0 || nf < 0 || ni > kMaxInt || nf > kMaxFlt || (ni && !iargs) || (nf && !fargs)) {
-    fbn_set_error("fbn_plan_add_call: bad arguments (at most 48 integer and 8 float arguments)");
+  if (!p || !name || ni < 0 || nf < 0 || ni > kMaxInt || nf > kMaxFlt || (ni && !iargs) || (nf && !fargs)) {
+    fbn_set_error("fbn_plan_add_call: bad arguments");
+    return 1;
+  }
+  const PlanThunk* t = find_thunk(name);
+  if (!t) {
+    fbn_set_error("fbn_plan_add_call: not a recordable entry point of fibinet.h");
+    return 1;
+  }
+  if (t->ni != ni || t->nf != nf) {
+    fbn_set_error("fbn_plan_add_call: argument counts differ from the entry point's prototype");
     return 1;
   }
   Op o;
   memset(&o, 0, sizeof(o));
   o.kind = kCall;
-  o.fn = fn;
+  o.fn = t->fn;
   for (int k = 0; k < ni; ++k) o.i[k] = iargs[k];
   for (int k = 0; k < nf; ++k) o.f[k] = fargs[k];
   p->ops.push_back(o);
@@ -165,6 +187,21 @@ extern "C" int fbn_plan_add_wait(void* plan, void* stream, int slot) {
   o.slot = slot;
   o.stream = static_cast<hipStream_t>(stream);
   p->ops.push_back(o);
+  return 0;
+}
+
+// Host wait for the program's event `slot` as its last replay (or the recording run) left it -- the
+// sharded step's host check of the routed-ahead overflow flag waits for the routing this way.
+extern "C" int fbn_plan_event_sync(void* plan, int slot) {
+  Plan* p = static_cast<Plan*>(plan);
+  if (!p || slot < 0 || slot >= (int)p->events.size()) {
+    fbn_set_error("fbn_plan_event_sync: bad arguments");
+    return 1;
+  }
+  if (hipEventSynchronize(p->events[slot]) != hipSuccess) {
+    fbn_set_error("fbn_plan_event_sync: hipEventSynchronize failed");
+    return 2;
+  }
   return 0;
 }
 

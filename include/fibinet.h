@@ -303,6 +303,9 @@ int fbn_sumsq_sparse_norms(const double* gnorm, const float* gvec, float* extra,
  * to the table-Adam entry points so they read it as the whole gradient.  hasdup [n]: set by the
  * row claims (fbn_claim_rows / fbn_adam_claim_catchup), cleared here. */
 #define FBN_GRAD_FULL 0x10000
+/* Lp1 | FBN_GRAD_CELL: the gradient-row pointer argument is the address of a device cell holding the
+ * row pointer (written by fbn_ring_slot) -- readers resolve it on the device */
+#define FBN_GRAD_CELL 0x20000
 int fbn_sparse_fold_fx(const int* dup, int* hasdup, int n, const float* gvec, int* slot_row, int Lp1, int D,
                        unsigned long long* acc, void* stream);
 /* adam_table mode 0: every row (touched rows read their gradient through map); mode 1: only the
@@ -452,11 +455,32 @@ int fbn_step_end(int* step, unsigned long long* rng, double* sumsq, long long* n
  * by routing ids to the owner of each row block; RCCL all-to-all runs between these calls. */
 int fbn_route(const int64_t* item, const int64_t* seq, int B, int L, long long V, long long Vl, int nranks,
               int* counts, int* offsets, int* cursor, int* send_ids, int* pos, int* err, void* stream);
+/* The fixed-capacity exchange (RowExchange, default at N > 1): every requester -> owner block has
+ * cap + 1 slots, so the ids, the looked-up rows and the gradient rows cross as equal-split
+ * all-to-alls and no split size ever reaches the host (the step can be recorded as a step program).
+ * send_ids [nranks][cap + 1]: owner o's block holds the local rows routed to o in slots 0..cap-1,
+ * -1 in unused slots; pos[b][t] = o * (cap + 1) + k (-1 = not routed).  An entry past slot cap - 1
+ * is not routed: stat[0] = 1 and every block's last slot is -2 (the flag travels in-band).
+ * stat [nranks + 1] = {overflow, entries requested from owner 0 .. nranks-1}.  Owner-side kernels
+ * (fbn_owner_claim / fbn_owner_gather / fbn_sparse_fixup / fbn_adam_prefetch_rows) skip negative ids.
+ * fbn_route_fc_status (after the ids all-to-all, recv_ids as received): stat[0] |= any requester's
+ * flag -- the same on every rank -- and stat[0 .. nranks] is copied to host (pinned, may be NULL) on
+ * the stream: a set flag makes every rank exchange that step with host-side split sizes instead. */
+int fbn_route_fc(const int64_t* item, const int64_t* seq, int B, int L, long long V, long long Vl, int nranks,
+                 int cap, int* send_ids, int* pos, int* stat, int* err, void* stream);
+int fbn_route_fc_status(const int* recv_ids, int nranks, int cap, int* stat, int* host, void* stream);
 /* claims only (the lazy table Adam replays the claimed rows before fbn_owner_gather(map = NULL)) */
 int fbn_owner_claim(const int* ids, int n, int* map, int* slot_row, int rank, void* stream);
 /* out_bf16: reply rows as bf16 (the bf16 mode's wire format; fbn_fields_fwd(rows_bf16 = 1) reads them) */
 int fbn_owner_gather(const int* ids, int n, const float* E, void* out, int* map, int* slot_row, int rank, int D,
                      int out_bf16, void* stream);
+/* N > 1 owner with deferred table gradients: the received gradient rows `wire` (n floats; bf16 when
+ * wire_bf16, else f32; n % 8 == 0, n <= stride) widened / copied into ring slot (*step % ring_n) of
+ * ring [ring_n][stride]; *cell = that slot's address (pass cell with Lp1 | FBN_GRAD_CELL to
+ * fbn_sparse_fixup / fbn_sumsq_sparse / fbn_adam_step_tail) -- the slot is chosen on the device, so
+ * a recorded step program replays with the right slot. */
+int fbn_ring_slot(float* ring, int ring_n, long long stride, const int* step, void* cell, const void* wire,
+                  int wire_bf16, long long n, void* stream);
 /* bf16 -> f32 (n % 8 == 0, 16-B aligned): the owner's received bf16 gradient rows (bf16 mode). */
 int fbn_widen_bf16(const void* in, float* out, long long n, void* stream);
 /* out [world][cap + 1]: out[o][j] = send_ids[offsets[o] + j] for j < counts[o], else -1, and
@@ -511,23 +535,28 @@ int fbn_collate_zero_if(float* x, long long n, const int* flag, void* stream);
  * Replaces the Python loop body that issues one training step (src/train_fibinet.py:113-123): the
  * host records a step's calls of this library -- entry point, arguments, and the cross-stream
  * edges (event record + stream wait) -- once while running the step, and replays them natively
- * (the same launches, streams and order: a replay is bit-identical to the eager step).  Replay calls
- * each recorded entry point through one generic signature under the x86-64 System V convention
- * (integer-class arguments in order, float / double arguments in xmm0-7), so every fbn_* entry point
- * with <= 48 integer-class and <= 8 floating arguments can be recorded (csrc/plan.cpp).
- *   fbn_plan_create(&plan); fbn_plan_add_call(plan, fn, iargs, ni, fargs, nf)  -- iargs: the integer
- *   arguments in order (pointers / ints as 64-bit, sign-extended); fargs: the float / double
- *   arguments in order as doubles (a float argument: a double whose low 32 bits are the float's);
+ * (the same launches, streams and order: a replay is bit-identical to the eager step).  A recorded
+ * call names its entry point; replay goes through a packed-argument thunk generated from this
+ * header (csrc/plan_thunks.inc) that makes a well-typed call of the declared prototype.  Every
+ * int-returning fbn_* entry point below (except the program and communicator set-up calls) with
+ * <= 48 integer-class and <= 8 floating arguments can be recorded.
+ *   fbn_plan_create(&plan); fbn_plan_add_call(plan, "fbn_...", iargs, ni, fargs, nf)  -- iargs: the
+ *   integer-class arguments in order (pointers / ints as 64-bit, sign-extended); fargs: the float /
+ *   double arguments in order as doubles (a float argument: a double whose low 32 bits are the
+ *   float's); ni / nf must match the prototype (else FBN_ERR_ARG);
  *   fbn_plan_add_record(plan, slot, stream) / fbn_plan_add_wait(plan, stream, slot): a stream edge
  *   through the program's event `slot`; fbn_plan_run(plan, &failed_op): 0, or the failing entry
  *   point's code (message in fbn_last_error). */
 int fbn_plan_create(void** plan);
 int fbn_plan_destroy(void* plan);
 int fbn_plan_size(void* plan);
-int fbn_plan_add_call(void* plan, void* fn, const unsigned long long* iargs, int ni, const double* fargs, int nf);
+int fbn_plan_add_call(void* plan, const char* name, const unsigned long long* iargs, int ni, const double* fargs,
+                      int nf);
 int fbn_plan_add_record(void* plan, int slot, void* stream);
 int fbn_plan_add_wait(void* plan, void* stream, int slot);
 int fbn_plan_run(void* plan, int* failed);
+/* host: wait for event `slot` of the program's last replay (hipEventSynchronize) */
+int fbn_plan_event_sync(void* plan, int slot);
 
 /* ---------------------------------------------------------------- RCCL on the step's stream (N > 1)
  * The row exchange's all-to-alls and the dense all-reduce as RCCL calls on the stream the step's

@@ -64,14 +64,17 @@ def test_kernels_are_gfx950_code_objects():
 
 
 def test_step_program_argument_encoding():
-    """Step programs pass recorded arguments through the x86-64 System V convention
-    (csrc/plan.cpp): integer-class values as 64-bit two's complement, a float as the double whose
-    low 32 bits are its bits (read from the low half of its xmm register by the callee)."""
+    """Step programs record each call's arguments as 64-bit integer words and doubles and replay it
+    through a packed-argument thunk generated from include/fibinet.h (csrc/plan_thunks.inc): an
+    int -1 is the word 0xFFFF...F (the thunk casts it back to int), a float the double whose low
+    32 bits are its bits.  The committed thunks are what the header generates, every recordable
+    SIGNATURES entry has one with the same integer / floating argument counts, and the library
+    refuses a recording whose counts differ or that names no entry point."""
     import ctypes
     import struct
-    from ctr_recommendation_amd import _lib
+    from ctr_recommendation_amd import _lib, gen_thunks
     assert _lib._as_u64(None) == 0
-    assert _lib._as_u64(-1) == (1 << 64) - 1              # an int -1: low 32 bits 0xFFFFFFFF
+    assert _lib._as_u64(-1) == (1 << 64) - 1
     assert _lib._as_u64(7) == 7
     arr = (ctypes.c_int * 4)()
     assert _lib._as_u64(arr) == ctypes.addressof(arr)
@@ -82,12 +85,24 @@ def test_step_program_argument_encoding():
         assert struct.unpack("<f", struct.pack("<I", bits))[0] == struct.unpack("<f", struct.pack("<f", x))[0]
     with pytest.raises(TypeError):
         _lib._as_u64(ctypes.byref(ctypes.c_int(0)))
-    h = _lib.lib()
-    # every signature the recorder may meet fits the generic replay signature (<= 48 integer-class,
-    # <= 8 floating arguments)
+    hdr = open(os.path.join(ROOT, "include", "fibinet.h")).read()
+    assert open(gen_thunks.OUT).read() == gen_thunks.generate(hdr), "run python -m ctr_recommendation_amd.gen_thunks"
+    thunks = {name: args for name, args in gen_thunks.declarations(hdr)}
     for name, (_, args) in _lib.SIGNATURES.items():
+        if name not in thunks:
+            continue
         nf = sum(1 for a in args if a in (_lib.F, _lib.D))
+        t = thunks[name]
+        assert (len(args) - nf, nf) == (sum(1 for a in t if not (a[1] or a[2])), sum(1 for a in t if a[1] or a[2])), name
         assert len(args) - nf <= 48 and nf <= 8, name
+    h = _lib.lib()
+    prog = _lib.StepProgram("cpu")
+    ia, fa = (ctypes.c_ulonglong * 4)(), (ctypes.c_double * 1)()
+    assert h.fbn_plan_add_call(ctypes.c_void_p(prog.h), b"fbn_widen_bf16", ia, 4, fa, 0) == 0     # counts match
+    assert h.fbn_plan_add_call(ctypes.c_void_p(prog.h), b"fbn_widen_bf16", ia, 3, fa, 0) != 0     # too few
+    assert h.fbn_plan_add_call(ctypes.c_void_p(prog.h), b"fbn_no_such_call", ia, 0, fa, 0) != 0
+    assert len(prog) == 1
+    del prog
     # an empty program runs (host only: no launches)
     prog = _lib.StepProgram("cpu")
     assert len(prog) == 0
