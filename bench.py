@@ -295,12 +295,16 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
     prime = max(0, 2 * F - W) if args.prime < 0 else args.prime
     sharded = world > 1 or FORCE_SHARD
     use_graph = not sharded and not args.no_graph and args.mode in ("auto", "graph")
-    use_prog = not sharded and args.mode in ("auto", "program") and args.table_adam == "lazy"
+    # step programs: the single-GPU step, and the sharded step in the fixed-capacity exchange form over
+    # RCCL on the step's stream (the one-rank job; N > 1 with FBN_NATIVE_COMM=1)
+    from ctr_recommendation_amd.exchange import native_comm_wanted
+    shard_prog = sharded and trmod._FC and native_comm_wanted(dev, None, rehearsal)
+    use_prog = (not sharded or shard_prog) and args.mode in ("auto", "program") and args.table_adam == "lazy"
     if use_prog:
         prime = max(prime, nb)            # every batch's program is recorded (a real step each) while priming
     modes = [m for m, ok in (("program", use_prog), ("graph", use_graph), ("eager", True)) if ok]
     trial_n = 16 if (args.mode == "auto" and len(modes) > 1) else 0
-    total = 2 + (nb if use_graph else 0) + prime + W + K + args.probe_steps + 16 + 2 * len(modes) * trial_n
+    total = 2 + trmod.FC_CALIB_STEPS + (nb if use_graph else 0) + prime + W + K + args.probe_steps + 16 + 2 * len(modes) * trial_n
     if args.main_priority:
         # the step's own stream at high priority: the hardware queue arbiter then dispatches its
         # workgroups ahead of the table-Adam side stream's when both have work pending
@@ -356,9 +360,13 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
             b, y = batches[j]
             tr.step(b, y, next_batch=batches[(i + 1) % nb][0])
 
+    if use_prog and sharded:
+        # the exchange's calibration steps (host split sizes), after which it is fixed-capacity
+        for k in range(trmod.FC_CALIB_STEPS):
+            tr.step(batches[nb - 2 - k][0], batches[nb - 2 - k][1], next_batch=batches[nb - 1 - k][0])
     if use_prog:
         # the step before the first recording prefetches (and pre-claims) batch 0, as the step before
-        # every replay of its program will (the last batch's program)
+        # every replay of its program will (the last batch's program); sharded: routes it ahead
         tr.step(batches[-1][0], batches[-1][1], next_batch=batches[0][0])
     i = 0
     for j in range(prime + W):
@@ -552,7 +560,7 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
     dominant = max(main_k, key=lambda r: r["avg_launch_ms"]) if main_k else None
     out = {"dt": dt, "t_host": t_host, "t_wait": t_wait, "K": K, "W": W, "B": B, "L": L, "V": V, "d": d, "rows_local": tr.rows_local, "loss": loss,
            "rooflines": rooflines, "roofline": dominant, "table_adam": tr.table_adam,
-           "graphs": mode_now[0] == "graph", "launch_mode": mode_now[0] if not sharded else "eager",
+           "graphs": mode_now[0] == "graph", "launch_mode": mode_now[0],
            "probe_source": ("the timed step-program replays (kernel-span probes recorded into the programs)"
                             if timed_src else "eager probe steps after the timed region"),
            "collectives": (None if not sharded else "RCCL on the step's stream (csrc/comm.cpp)"

@@ -170,11 +170,29 @@ _UNCHECKED = ("fbn_version", "fbn_device_ok", "fbn_probe_elapsed")
 _tls = threading.local()           # .prog: the StepProgram recording on this thread (or None)
 
 
+# FBN_DEBUG_SYNC=<path> (diagnostics only): every call is logged to <path> and followed by a device
+# synchronize, so an asynchronous kernel fault surfaces at -- and is attributed to -- its own call
+_DEBUG_SYNC = os.environ.get("FBN_DEBUG_SYNC")
+_debug_log = None
+
+
+def _debug_sync(name: str) -> None:
+    global _debug_log
+    if _debug_log is None:
+        _debug_log = open(_DEBUG_SYNC, "a", buffering=1)
+    _debug_log.write(name + "\n")
+    torch.cuda.synchronize()
+
+
 def call(name: str, *args) -> int:
     f = _fns.get(name)
     if f is None:                  # bound ctypes function, looked up once (host time per step)
         f = _fns[name] = getattr(lib(), name)
+    if _DEBUG_SYNC:
+        _debug_sync("> " + name)
     rc = f(*args)
+    if _DEBUG_SYNC:
+        _debug_sync("< " + name)
     if rc and isinstance(rc, int) and name not in _UNCHECKED and not name.endswith(("_size", "_grid")):
         msg = lib().fbn_last_error().decode(errors="replace")
         raise RuntimeError(f"{name} failed (code {rc}): {msg}")

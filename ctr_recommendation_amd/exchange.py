@@ -21,11 +21,21 @@ owners pack the ids on device and both count vectors land in pinned host memory 
 forward starts at the owner's claims with no collective before them (two routing buffer sets
 alternate).  Without it the forward routes inline: a counts all-to-all, one host sync, an ids
 all-to-all.
+
+Fixed-capacity form (enable_fixed(cap), the trainer's default once calibrated): requester r's
+block for owner o has cap + 1 slots, so the ids, the looked-up rows and the gradient rows all cross
+as EQUAL-split all-to-alls and no split size reaches the host; the owner works on the
+world * (cap + 1) slots as they arrive (negative id = empty slot) and a step is a fixed sequence
+of library calls -- recordable as a step program (trainer.record_program).  An entry past a block's
+capacity is not routed; the overflow travels in-band with the ids (every block's last slot), so
+every rank reads the same global flag before the step and all of them exchange that step with
+host-side split sizes instead (fbn_route_fc / fbn_route_fc_status).
 """
 from __future__ import annotations
 
 import ctypes
 import os
+import sys
 import time
 from typing import Optional
 
@@ -43,6 +53,7 @@ def _torch_rccl() -> str:
     return p if os.path.exists(p) else "librccl.so.1"
 
 
+_DEBUG_FC = os.environ.get("FBN_DEBUG_FC") == "1"     # diagnostics: trace the fixed-capacity routing
 _DTYPE_CODE = {torch.float32: 0, torch.float64: 1, torch.int32: 2}
 
 
@@ -130,6 +141,20 @@ class HipExchangeKernels:
     def widen(self, inp, out):
         call("fbn_widen_bf16", ptr(inp), ptr(out), inp.numel(), _lib.stream_handle(out.device))
 
+    def route_fc(self, item, seq, B, L, V, Vl, world, cap, send_ids, pos, stat, err):
+        call("fbn_route_fc", ptr(item), ptr(seq), B, L, V, Vl, world, cap, ptr(send_ids), ptr(pos), ptr(stat), ptr(err),
+             _lib.stream_handle(item.device))
+
+    def route_fc_status(self, recv_ids, world, cap, stat, host):
+        call("fbn_route_fc_status", ptr(recv_ids), world, cap, ptr(stat), ptr(host), _lib.stream_handle(recv_ids.device))
+
+
+def _pad4(n: int) -> int:
+    return (n + 3) // 4 * 4
+
+
+FC_MAX_SETS = 1024      # fixed-capacity routing sets kept (one per distinct batch; ~2 MB each at C3)
+
 
 class RowExchange:
     def __init__(self, rank: int, world: int, V: int, d: int, B: int, L: int, device, group=None, kernels=None,
@@ -182,6 +207,126 @@ class RowExchange:
         self.send_buf = None
         self._pending = None        # gradient-row all-to-all issued by backward_start()
         self._comm_stream = None    # native RCCL, early gradient exchange: its stream
+        # fixed-capacity form (enable_fixed): slots per requester -> owner block, 0 = off
+        self.cap = 0
+        self.fc_sets = {}           # batch key -> its routing buffers (kept: step programs address them)
+        self.fc_next = None         # (key, set): the next batch, routed ahead in the fixed-capacity form
+        self.fc_wait = None         # host wait for that routing (an event, or a step program's event slot)
+        self.fc_active = False      # this step exchanges in the fixed-capacity form
+        self.fc_set = None          # ... and this is its routing set
+        self.fc_fallbacks = 0       # steps exchanged with host split sizes after an overflow
+
+    # ------------------------------------------------------------------ fixed-capacity form
+    def enable_fixed(self, cap: int) -> None:
+        """Exchange in equal-split blocks of cap + 1 slots per (requester, owner) pair from the next
+        routed-ahead batch on (cap must be the same on every rank)."""
+        self.cap = int(cap)
+        n = self.fc_slots
+        self.fc_rows = torch.empty((n, self.d), dtype=self.row_dtype, device=self.device)    # requester: rows[pos]
+        self.fc_reply = torch.empty((n, self.d), dtype=self.row_dtype, device=self.device)   # owner: gathered rows
+        self.fc_send = torch.empty((n, self.d), dtype=self.row_dtype, device=self.device)    # requester: grad rows
+        self.fc_wire = torch.empty((n, self.d), dtype=self.row_dtype, device=self.device)    # owner: received grads
+        self.fc_sets = {}
+        self.fc_next = None
+
+    @property
+    def fc_slots(self) -> int:
+        return self.world * (self.cap + 1)
+
+    def _fc_routing_set(self, key):
+        st = self.fc_sets.get(key)
+        if st is None:
+            if len(self.fc_sets) >= FC_MAX_SETS:      # forget the oldest (a program holds its own)
+                self.fc_sets.pop(next(iter(self.fc_sets)))
+            n = self.fc_slots
+            i32 = dict(dtype=torch.int32, device=self.device)
+            st = {"send_ids": torch.empty(n, **i32), "recv_ids": torch.empty(n, **i32),
+                  "pos": torch.empty((self.B, self.L + 1), **i32), "stat": torch.zeros(_pad4(self.world + 1), **i32),
+                  "host": torch.zeros(_pad4(self.world + 1), dtype=torch.int32,
+                                      pin_memory=torch.device(self.device).type == "cuda"),
+                  "event": None, "key": key}
+            self.fc_sets[key] = st
+        return st
+
+    def _prepare_fc(self, item, seq, err, send_rows, after) -> None:
+        """prepare() in the fixed-capacity form: route, the ids all-to-all (equal split) and the
+        global overflow flag, all on the side stream with no host involvement; the flag lands in
+        pinned memory for the next forward's host check."""
+        B = item.shape[0]
+        L = 0 if seq is None else seq.shape[1]
+        key = self._key(item, seq)
+        if self.side is None:
+            st = self._fc_routing_set(key)
+        else:
+            # allocated on the side stream, which writes it while the main stream is still running
+            # this step's backward: a block the main stream freed earlier in the step (still in use
+            # by its queued kernels -- and by a step program's replays, at the recorded addresses)
+            # must not come back here
+            with torch.cuda.stream(self.side):
+                st = self._fc_routing_set(key)
+        if self.side is None:
+            # CPU ranks (gloo tests): routed inline, nothing to wait for
+            self.k.route_fc(item, seq if L else None, B, L, self.V, self.Vl, self.world, self.cap, st["send_ids"],
+                            st["pos"], st["stat"], err)
+            self._a2a(st["recv_ids"], st["send_ids"], None, None, self.route_group, route=True)
+            self.k.route_fc_status(st["recv_ids"], self.world, self.cap, st["stat"], st["host"])
+            self.fc_next, self.fc_wait = (key, st), (lambda: None)
+            if send_rows:
+                self.next_lids = st["recv_ids"]
+            return
+        main = torch.cuda.current_stream(item.device)
+        if after is None:
+            _lib.wait_stream(self.side, main)
+        else:
+            _lib.wait_event(self.side, after)
+        with torch.cuda.stream(self.side):
+            self.k.route_fc(item, seq if L else None, B, L, self.V, self.Vl, self.world, self.cap, st["send_ids"],
+                            st["pos"], st["stat"], err)
+            self._a2a(st["recv_ids"], st["send_ids"], None, None, self.route_group, route=True)
+            self.k.route_fc_status(st["recv_ids"], self.world, self.cap, st["stat"], st["host"])
+        ev = torch.cuda.Event()
+        _lib.record_event(ev, self.side)
+        st["event"] = ev
+        self.fc_next = (key, st)
+        self.fc_wait = ev.synchronize
+        if send_rows:
+            self.next_lids = st["recv_ids"]
+        if _DEBUG_FC:
+            print(f"[fc] prepare key {key[0] % 100000} set {id(st) % 100000}", file=sys.stderr, flush=True)
+
+    def fc_overflowed(self) -> bool:
+        """Host: wait for the routed-ahead batch's routing and read its global overflow flag (the
+        same value on every rank)."""
+        t0 = time.perf_counter()
+        self.fc_wait()
+        self.host_wait_s += time.perf_counter() - t0
+        return int(self.fc_next[1]["host"][0]) != 0
+
+    def _forward_fc(self, st, E_local, sparse, err, before_gather) -> torch.Tensor:
+        self.fc_active, self.fc_set = True, st
+        self.cur_pos = st["pos"]
+        self.recv_ids = st["recv_ids"]
+        self.send_counts = self.recv_counts = None
+        n = self.fc_slots
+        if before_gather is not None and sparse.get("map") is not None:
+            self.k.owner_claim(self.recv_ids, sparse["map"], sparse["slot_row"], self.rank)
+            before_gather(n)
+            self.k.owner_gather(self.recv_ids, E_local, self.fc_reply, None, None, self.rank, self.d)
+        else:
+            self.k.owner_gather(self.recv_ids, E_local, self.fc_reply, sparse["map"], sparse["slot_row"], self.rank,
+                                self.d)
+        self._a2a(self.fc_rows, self.fc_reply, None, None)
+        self.rows_buf = self.fc_rows
+        return self.fc_rows
+
+    @property
+    def n_recv(self) -> int:
+        """Owner-side entries of this step (received slots, empty ones included in the fixed form)."""
+        return self.fc_slots if self.fc_active else sum(self.recv_counts)
+
+    @property
+    def n_send(self) -> int:
+        return self.fc_slots if self.fc_active else sum(self.send_counts)
 
     @property
     def rows_lo(self) -> int:
@@ -244,6 +389,9 @@ class RowExchange:
         received padded blocks as self.next_lids [world * (cap + 1)] (negative = no row), ready on
         self.side -- the owner's table-Adam prefetch (fbn_adam_prefetch_rows) reads them."""
         self.next_lids = None
+        if self.cap and item.shape[0] == self.B and (0 if seq is None else seq.shape[1]) == self.L:
+            self._prepare_fc(item, seq, err, send_rows, after)
+            return
         if self.side is None:
             return
         st = self.sets[1 - self.cur]
@@ -282,6 +430,21 @@ class RowExchange:
         sparse map and gathering them (the lazy table Adam brings them up to date there)."""
         B = item.shape[0]
         L = 0 if seq is None else seq.shape[1]
+        self.fc_active = False
+        if _DEBUG_FC:
+            print(f"[fc] forward key {self._key(item, seq)[0] % 100000} next "
+                  f"{None if self.fc_next is None else (self.fc_next[0][0] % 100000, id(self.fc_next[1]) % 100000)}",
+                  file=sys.stderr, flush=True)
+        if self.fc_next is not None and self.fc_next[0] == self._key(item, seq):
+            st = self.fc_next[1]
+            if not self.fc_overflowed():
+                self.fc_next = None
+                if not _lib.recording() and item.device.type == "cuda":
+                    # (a recorded step relies on the previous step's closing join of the side stream)
+                    _lib.wait_event(torch.cuda.current_stream(item.device), st["event"])
+                return self._forward_fc(st, E_local, sparse, err, before_gather)
+            self.fc_fallbacks += 1                    # every rank read the same flag: all route inline
+        self.fc_next = None
         nxt = self.sets[1 - self.cur]
         if nxt["event"] is not None and nxt["key"] == self._key(item, seq):
             # routed ahead by prepare(): wait for the side stream's copy only, then order the
@@ -333,6 +496,9 @@ class RowExchange:
         return buf
 
     def make_sendbuf(self) -> torch.Tensor:
+        if self.fc_active:
+            self.send_buf = self.fc_send
+            return self.fc_send
         self.send_buf = self._grow(self.send_buf, sum(self.send_counts))
         return self.send_buf[:sum(self.send_counts)]
 
@@ -346,11 +512,17 @@ class RowExchange:
         """Issue the gradient-row all-to-all now, asynchronously on the process group's own stream
         (the caller's stream goes on with other work); backward_finish() makes the caller's stream
         wait for it and widens bf16 wire rows."""
-        n_recv = sum(self.recv_counts)
-        grad = out[:n_recv] if out is not None else \
-            torch.empty((n_recv, self.d), dtype=torch.float32, device=sendbuf.device)
-        wire = grad if sendbuf.dtype == torch.float32 else \
-            torch.empty((n_recv, self.d), dtype=sendbuf.dtype, device=sendbuf.device)
+        n_recv = self.n_recv
+        if self.fc_active and out is None:
+            # fixed-capacity form: the rows land in the fixed wire buffer (the caller moves them into
+            # a device-chosen ring slot, fbn_ring_slot, or widens them itself)
+            grad = wire = self.fc_wire
+        else:
+            grad = out[:n_recv] if out is not None else \
+                torch.empty((n_recv, self.d), dtype=torch.float32, device=sendbuf.device)
+            wire = grad if sendbuf.dtype == torch.float32 else \
+                (self.fc_wire if self.fc_active else
+                 torch.empty((n_recv, self.d), dtype=sendbuf.dtype, device=sendbuf.device))
         work = None
         if self.comm is not None and early:
             # RCCL on a stream of its own, right after the fields backward: the exchange runs beside
@@ -359,11 +531,11 @@ class RowExchange:
             if self._comm_stream is None:
                 self._comm_stream = torch.cuda.Stream(device=sendbuf.device)
             cs = self._comm_stream
-            cs.wait_stream(cur)
+            _lib.wait_stream(cs, cur)
             with torch.cuda.stream(cs):
                 self._a2a(wire, sendbuf, self.recv_counts, self.send_counts)
             work = torch.cuda.Event()
-            work.record(cs)
+            _lib.record_event(work, cs)
             for t in (wire, grad, sendbuf):
                 t.record_stream(cs)
         elif self.stage_on_cpu or self.comm is not None:       # host-staged, or on this stream
@@ -377,7 +549,7 @@ class RowExchange:
         work, wire, grad = self._pending
         self._pending = None
         if isinstance(work, torch.cuda.Event):              # native RCCL on the exchange's own stream
-            torch.cuda.current_stream(grad.device).wait_event(work)
+            _lib.wait_event(torch.cuda.current_stream(grad.device), work)
         elif work is not None:
             work.wait()
         if wire is not grad:

@@ -95,6 +95,16 @@ _WGRAD_EARLY = os.environ.get("FBN_WGRAD_EARLY", "0") == "1"
 # (fbn_adam_prefetch_binned).  Bit-identical, measured slower (0.443 vs 0.421 ms/step at C3),
 # so adam_prefetch2's 64-entries-per-wave replay stays the default
 _PF_BINNED = os.environ.get("FBN_PF_BINNED", "0") == "1"
+# N > 1 (and the one-rank sharded run): the fixed-capacity exchange (RowExchange.enable_fixed) once
+# FC_CALIB_STEPS steps measured the per-owner load -- equal-split all-to-alls, no host-side split
+# sizes, the step recordable as a step program.  FBN_FC=0 keeps the host-split exchange (A/B);
+# FBN_FC_CAP=<n> fixes the per-block capacity instead of calibrating it; FBN_FC_MARGIN (1.25) scales
+# the calibrated load
+_FC = os.environ.get("FBN_FC", "1") != "0"
+_FC_CAP = int(os.environ.get("FBN_FC_CAP", "0"))
+_FC_MARGIN = float(os.environ.get("FBN_FC_MARGIN", "1.25"))
+FC_CALIB_STEPS = 2
+FBN_GRAD_CELL = 0x20000      # include/fibinet.h: the gradient-row argument is a device cell (fbn_ring_slot)
 # N > 1, the owner's ahead-of-time catch-up of the next step's requested rows in two passes (tagged
 # pre-claims + the four-row replay engine); FBN_OWNER_PF2=0 keeps the one-pass kernel (A/B)
 _OWNER_PF2 = os.environ.get("FBN_OWNER_PF2", "1") != "0"
@@ -221,6 +231,12 @@ def _batch_key(item: torch.Tensor, seq: Optional[torch.Tensor]):
     return (item.data_ptr(), item.shape[0], item._version,
             0 if seq is None else seq.data_ptr(), 0 if seq is None else tuple(seq.shape),
             0 if seq is None else seq._version)
+
+
+def _lib_key(x, batch):
+    """RowExchange's routing key of a batch (the id tensors, their shapes and version counters)."""
+    seq = batch.get("item_seq")
+    return x._key(batch["item_id"], seq if seq is not None and seq.shape[1] else None)
 
 
 def _pad4(n: int) -> int:
@@ -420,6 +436,12 @@ class FiBiNETTrainer:
         self._bn_synced_at = -1     # host step of the last rank-0 BatchNorm broadcast (_bn_from_rank0)
         self._used_pre = False      # the last step took its row claims from the prefetch's pre-claims
         self._recording = False     # inside record_program()
+        # fixed-capacity exchange: calibration (largest per-owner block seen) and the ring-slot cell
+        self.fc_wanted = self.sharded and _FC and self.device.type == "cuda"
+        self._fc_seen = 0
+        self._fc_steps = 0
+        self.ring_cell = torch.zeros(2, dtype=torch.int64, device=dev)     # fbn_ring_slot's pointer cell
+        self._fc_grad = None        # fixed-capacity rows, f32, when they are not deferred
 
     # ------------------------------------------------------------------ one training step
     def step(self, batch: Dict[str, torch.Tensor], labels: torch.Tensor,
@@ -621,7 +643,7 @@ class FiBiNETTrainer:
                                      self.err, before_gather=catch_up if lazy else None)
             pos = self.xchg.cur_pos
             fwd_ev = torch.cuda.Event()
-            fwd_ev.record(main)
+            _lib.record_event(fwd_ev, main)
         route_ahead = None
         if self.xchg is not None and next_batch is not None:
             def route_ahead():
@@ -630,7 +652,7 @@ class FiBiNETTrainer:
                                   after=fwd_ev)
                 if own and self.xchg.next_lids is not None:
                     # after this step's claims and window (self.side), once the requests arrived
-                    self.side.wait_stream(self.xchg.side)
+                    _lib.wait_stream(self.side, self.xchg.side)
                     ev = _events(probe, "adam_prefetch", self.side)
                     call("fbn_adam_prefetch_rows", ptr(self.xchg.next_lids), self.xchg.next_lids.numel(),
                          int(self.rank == 0), self.rows_local, ptr(self.map),
@@ -665,7 +687,7 @@ class FiBiNETTrainer:
                       and not self.deterministic and L > 0
                       and not self._early_grad_xchg())
         if (self.xchg is not None and self.shard_graph and probe is None and masks_out is None
-                and self.table_adam != "eager"):
+                and self.table_adam != "eager" and not self._recording):
             sendbuf = self.xchg.make_sendbuf()
             graphed = self._sharded_compute(batch, labels, pos, cfg, ntot, B, L)
         if not graphed:
@@ -733,16 +755,35 @@ class FiBiNETTrainer:
         else:
             # owner: one received row per entry -- straight into this step's deferred-gradient ring
             # slot when it fits, else a buffer of its own and the rows applied at the step end
-            slot = self._grad_slot()
-            defer_now = slot is not None
-            if self.xchg._pending is not None:      # issued right after the fields backward
-                grows = self.xchg.backward_finish()
+            x = self.xchg
+            n_ent = x.n_recv
+            if x.fc_active:
+                # fixed-capacity form: the rows arrive in the fixed wire buffer; deferred, they move
+                # into ring slot step % ring_n chosen on the device (a replayed step program gets the
+                # right slot), and the readers take them through the slot's pointer cell
+                wire = x.backward_finish() if x._pending is not None else x.backward(sendbuf)
+                defer_now = self.deferred and n_ent <= self.ring_cap
+                if defer_now:
+                    call("fbn_ring_slot", ptr(self.ring), self.ring_n, self._ring_stride(), ptr(self.step_dev),
+                         ptr(self.ring_cell), ptr(wire), int(wire.dtype == torch.bfloat16), n_ent * d, st)
+                    gsrc = (self.ring_cell, None, 1 | FBN_GRAD_CELL)
+                else:
+                    if self._fc_grad is None or self._fc_grad.shape[0] < n_ent:
+                        self._fc_grad = torch.empty((n_ent, d), dtype=torch.float32, device=self.device)
+                    grows = self._fc_grad[:n_ent]
+                    call("fbn_ring_slot", ptr(grows), 1, n_ent * d, ptr(self.step_dev), ptr(self.ring_cell), ptr(wire),
+                         int(wire.dtype == torch.bfloat16), n_ent * d, st)
+                    gsrc = (grows, None, 1)
             else:
-                grows = self.xchg.backward(sendbuf, out=slot)
-            n_ent = grows.shape[0]
-            gsrc = (grows, None, 1)
-            call("fbn_sparse_fixup", None, None, ptr(self.xchg.recv_ids), n_ent, 0, self.V, self.rank, ptr(self.map),
-                 ptr(grows), None, ptr(self.slot_row), 1, d, st)
+                slot = self._grad_slot()
+                defer_now = slot is not None
+                if x._pending is not None:          # issued right after the fields backward
+                    grows = x.backward_finish()
+                else:
+                    grows = x.backward(sendbuf, out=slot)
+                gsrc = (grows, None, 1)
+            call("fbn_sparse_fixup", None, None, ptr(x.recv_ids), n_ent, 0, self.V, self.rank, ptr(self.map),
+                 ptr(gsrc[0]), None, ptr(self.slot_row), gsrc[2], d, st)
         # clip_grad_norm_(10): dense grads (identical on every rank) + disjoint table shards
         tab_acc = self.sumsq_tab if self.sharded else self.sumsq
         dense_done = False
@@ -801,6 +842,8 @@ class FiBiNETTrainer:
             call("fbn_step_end", ptr(self.step_dev), ptr(self.rng), ptr(self.sumsq),
                  ptr(self.p["mlp.1.num_batches_tracked"]), ptr(self.p["mlp.5.num_batches_tracked"]), self.total_steps,
                  ptr(self.err), st)
+        if self.fc_wanted and not self.xchg.cap and not self.xchg.fc_active:
+            self._fc_calibrate()
         self.host_step += 1
         return self.loss
 
@@ -822,14 +865,21 @@ class FiBiNETTrainer:
         order of replay, the step before the first recording given this batch as its next batch.
         One GPU, lazy table Adam with deferred gradients, "all" bilinear (the paths whose step is
         library calls only)."""
-        if self.xchg is not None:
-            raise ValueError("step programs record the single-GPU step (the sharded step has host-side "
-                             "split sizes and collectives between its kernels)")
         if not (self.table_adam == "lazy" and self.deferred) or self.fcfg.bilinear_each:
             raise ValueError("step programs need the lazy table Adam with deferred gradients and the 'all' "
                              "bilinear interaction")
         seq = batch.get("item_seq")
         key = _batch_key(batch["item_id"], seq if seq is not None and seq.shape[1] else None)
+        x = self.xchg
+        if x is not None:
+            # N > 1: the fixed-capacity exchange over RCCL on the step's stream, this batch routed
+            # ahead by the previous step -- then the step is library calls and stream edges only
+            if not (x.cap and self.native_comm is not None and next_batch is not None):
+                raise ValueError("the sharded step records with the fixed-capacity exchange (after its calibration "
+                                 "steps), native RCCL and a next batch")
+            if x.fc_next is None or x.fc_next[0] != _lib_key(x, batch):
+                raise ValueError("record the sharded step after a step that routed this batch ahead (given it as "
+                                 "its next_batch)")
         prog = _lib.StepProgram(self.device)
         self._used_pre = False
         self._recording = True
@@ -840,6 +890,16 @@ class FiBiNETTrainer:
                 self.step(batch, labels, next_batch=next_batch, probe=probe)
         finally:
             self._recording = False
+        if x is not None:
+            if not x.fc_active:
+                raise RuntimeError("the recorded step's routing overflowed its fixed capacity (it ran with host "
+                                   "split sizes): record another step")
+            # the routing set this step used, and the next batch's, routed ahead by this step (its
+            # event slot: the host waits there for the overflow flag before the next replay)
+            prog.fc_cur, prog.fc_after = x.fc_set, x.fc_next
+            prog.fc_slot = prog.slot_of(x.fc_next[1]["event"])
+            prog.args = (batch, labels, next_batch)
+            prog.keep += [x.fc_set, x.fc_next[1]]        # the routing buffers its calls address
         # the claims of the recorded step came from the pre-claims the previous step posted for this
         # very batch (a replay is valid only after such a step), and the step posted its next batch's
         prog.pre_needed, prog.batch_key, prog.pre_key_after = self._used_pre, key, self._pre_key
@@ -859,6 +919,23 @@ class FiBiNETTrainer:
             # them, are for the old contents -- refuse rather than lose row claims
             raise RuntimeError("step program replayed over batch tensors modified since it was recorded "
                                "(re-record it, or pass fresh tensors to step())")
+        x = self.xchg
+        if x is not None:
+            if x.fc_next is None or x.fc_next[1] is not prog.fc_cur:
+                got = "nothing" if x.fc_next is None else (
+                    "another batch" if x.fc_next[0] != prog.fc_cur["key"] else "this batch into other buffers")
+                raise RuntimeError(f"sharded step program replayed out of order: the previous step routed {got} "
+                                   "ahead (record programs in the order they replay, each step given the next batch)")
+            if x.fc_overflowed():
+                # the routed-ahead ids overflowed a block on some rank (every rank reads the same flag):
+                # this step runs eagerly with host-side split sizes, on every rank
+                batch, labels, next_batch = prog.args
+                return self.step(batch, labels, next_batch=next_batch)
+            prog.run()
+            x.fc_next = prog.fc_after
+            x.fc_wait = lambda: _lib.call_raw("fbn_plan_event_sync", prog.h, prog.fc_slot)
+            self.host_step += 1
+            return self.loss
         if prog.pre_needed and self._pre_key != prog.batch_key:
             # its recorded claims read pre-claims the previous step did not post for this batch (a
             # replay out of the recorded order): refuse rather than lose row claims
@@ -868,6 +945,39 @@ class FiBiNETTrainer:
         self._pre_key = prog.pre_key_after
         self.host_step += 1
         return self.loss
+
+    def _fc_calibrate(self) -> None:
+        """N > 1: after FC_CALIB_STEPS host-split steps, switch the exchange to the fixed-capacity form
+        with a per-block capacity of FBN_FC_MARGIN x the largest block seen on any rank (+ 256), capped
+        at B * (L + 1) -- a collective, at the same step on every rank."""
+        x = self.xchg
+        if x.send_counts is not None:
+            self._fc_seen = max(self._fc_seen, max(x.send_counts))
+        self._fc_steps += 1
+        if self._fc_steps < FC_CALIB_STEPS:
+            return
+        seen = torch.tensor([self._fc_seen], dtype=torch.int64,
+                            device="cpu" if self.stage_on_cpu else self.device)
+        if dist.is_initialized() and self.world > 1:
+            dist.all_reduce(seen, op=dist.ReduceOp.MAX, group=self.group)
+        full = self.B * (self.L + 1)
+        cap = _FC_CAP if _FC_CAP > 0 else min(full, (int(int(seen.item()) * _FC_MARGIN) + 256 + 63) // 64 * 64)
+        self.enable_fixed_exchange(cap)
+
+    def enable_fixed_exchange(self, cap: int) -> None:
+        """Exchange in equal-split blocks of cap + 1 slots from the next routed-ahead batch on (the same
+        cap on every rank).  Grows the deferred-gradient ring (after bringing every row up to date,
+        which clears the pending gradients it holds) and the claim slots when the blocks need more."""
+        x = self.xchg
+        x.enable_fixed(cap)
+        n = x.fc_slots
+        if n > self.slot_row.numel():
+            self.slot_row = torch.full((n,), -1, dtype=torch.int32, device=self.device)
+        if self.deferred and n > self.ring_cap:
+            self.flush()
+            self.ring_cap = n
+            self.ring = torch.zeros((self.ring_n, n, self.d), dtype=torch.float32, device=self.device)
+        self.fc_wanted = False
 
     def _ring_stride(self) -> int:
         return self.B * 2 * self.d if not self.sharded else self.ring_cap * self.d
@@ -919,7 +1029,7 @@ class FiBiNETTrainer:
 
     def _grad_slot(self):
         """This step's deferred-gradient ring slot, or None (rows applied at once)."""
-        if self.deferred and sum(self.xchg.recv_counts) <= self.ring_cap:
+        if self.deferred and self.xchg.n_recv <= self.ring_cap:
             return self.ring[self.host_step % self.ring_n]
         return None
 
@@ -933,7 +1043,10 @@ class FiBiNETTrainer:
         all-to-all starts there, on the process group's stream, beside the rest of the backward
         (the last parameter reductions and the mm_proj weight gradient)."""
         x = self.xchg
-        x.backward_start(x.send_buf[:sum(x.send_counts)], out=self._grad_slot(), early=True)
+        if x.fc_active:
+            x.backward_start(x.fc_send, out=None, early=True)
+        else:
+            x.backward_start(x.send_buf[:sum(x.send_counts)], out=self._grad_slot(), early=True)
 
     def _bn_n(self, ntot: int, B: int) -> int:
         """Samples one BatchNorm normalises over: the global batch (SyncBN) or this rank's slice."""

@@ -39,15 +39,56 @@ class CpuExchangeKernels:
                     send_ids[p] = int(ids[b, t] - o * Vl)
                     pos[b, t] = p
 
+    def route_fc(self, item, seq, B, L, V, Vl, world, cap, send_ids, pos, stat, err):
+        """Restates fbn_route_fc: owner o's block is slots [o * (cap + 1), o * (cap + 1) + cap), its
+        last slot -1 (or -2 in every block once any entry overflowed); pos = the entry's slot or -1;
+        stat = [overflow, entries requested per owner].  (The kernel's order inside a block depends
+        on workgroup timing; this one is entry order -- the tests compare sets, not orders.)"""
+        ids = item.view(B, 1) if seq is None or L == 0 else torch.cat([item.view(B, 1), seq.view(B, L)], dim=1)
+        valid = (ids >= 0) & (ids < V)
+        if not bool(valid.all()):
+            err.fill_(1)
+        send_ids.fill_(-1)
+        pos.fill_(-1)
+        cnt = [0] * world
+        ovf = 0
+        for b in range(B):
+            for t in range(ids.shape[1]):
+                i = int(ids[b, t])
+                if not (0 <= i < V) or (t > 0 and i == 0):
+                    continue
+                o = i // Vl
+                k = cnt[o]
+                cnt[o] += 1
+                if k >= cap:
+                    ovf = 1
+                    continue
+                send_ids[o * (cap + 1) + k] = i - o * Vl
+                pos[b, t] = o * (cap + 1) + k
+        if ovf:
+            for o in range(world):
+                send_ids[o * (cap + 1) + cap] = -2
+        stat[0] = ovf
+        stat[1:1 + world] = torch.tensor(cnt, dtype=stat.dtype)
+
+    def route_fc_status(self, recv_ids, world, cap, stat, host):
+        """Restates fbn_route_fc_status: stat[0] |= any requester's in-band flag; host <- stat."""
+        if any(int(recv_ids[r * (cap + 1) + cap]) == -2 for r in range(world)):
+            stat[0] = 1
+        host[:world + 1] = stat[:world + 1]
+
     def owner_claim(self, ids, map_, slot_row, rank):
-        """Restates fbn_owner_claim: first entry referencing a row claims it (padding row excluded)."""
+        """Restates fbn_owner_claim: first entry referencing a row claims it (padding row and empty
+        fixed-capacity slots excluded)."""
         for i, r in enumerate(ids.tolist()):
-            if not (rank == 0 and r == 0) and int(map_[r]) == -1:
+            if r >= 0 and not (rank == 0 and r == 0) and int(map_[r]) == -1:
                 map_[r] = i
                 slot_row[i] = r
 
     def owner_gather(self, ids, E, out, map_, slot_row, rank, d):
         for i, r in enumerate(ids.tolist()):
+            if r < 0:
+                continue                      # an empty fixed-capacity slot
             out[i] = E[r]                     # a bf16 `out` (the bf16 mode's wire rows) rounds here
             if map_ is not None and not (rank == 0 and r == 0) and int(map_[r]) == -1:
                 map_[r] = i
@@ -78,7 +119,7 @@ class CpuExchangeKernels:
     def sparse_fixup_owner(ids, grows, map_, rank):
         """Restates fbn_sparse_fixup's owner mode: fold duplicates into the claiming entry."""
         for i, r in enumerate(ids.tolist()):
-            if rank == 0 and r == 0:
+            if r < 0 or (rank == 0 and r == 0):
                 continue
             u = int(map_[r])
             if u != i:

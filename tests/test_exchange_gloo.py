@@ -25,7 +25,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, V, d, B, L, q, hook=False, bf16=False, padded=False):
+def _worker(rank, world, port, V, d, B, L, q, hook=False, bf16=False, padded=False, fc=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -44,7 +44,7 @@ def _worker(rank, world, port, V, d, B, L, q, hook=False, bf16=False, padded=Fal
         xg = RowExchange(rank, world, V, d, B, L, torch.device("cpu"), kernels=CpuExchangeKernels(), rows_bf16=bf16)
         lo, n_local = xg.rows_lo, xg.rows_local
         E_local = E_full[lo:lo + n_local].clone()
-        cap = world * B * (L + 1)
+        cap = world * (B * (L + 1) + 1)          # (>= the fixed form's world * (cap + 1) slots)
         sparse = {"map": torch.full((n_local,), -1, dtype=torch.int32),
                   "slot_row": torch.full((cap,), -1, dtype=torch.int32)}
         err = torch.zeros(1, dtype=torch.int32)
@@ -58,8 +58,14 @@ def _worker(rank, world, port, V, d, B, L, q, hook=False, bf16=False, padded=Fal
             seen["n"] = int(claimed.numel())
             E_local[claimed] += 1000.0
 
+        if fc is not None:
+            # the fixed-capacity form: blocks of cap + 1 slots, routed by prepare() (inline on CPU);
+            # "tiny" overflows on every rank's batch -> all ranks read the flag and fall back together
+            xg.enable_fixed(B * (L + 1) if fc == "fit" else 2)
+            xg.prepare(item, seq, err)
         rows = xg.forward(item, seq, E_local, sparse, err, before_gather=before_gather if hook else None)
         pos = xg.cur_pos
+        fc_state = (xg.fc_active, xg.fc_fallbacks)
         ok_pad = True
         if padded:
             # the routed-ahead form of the same requests (RowExchange.prepare on a GPU): every
@@ -89,7 +95,7 @@ def _worker(rank, world, port, V, d, B, L, q, hook=False, bf16=False, padded=Fal
         # backward: one random gradient row per routed entry
         sendbuf = xg.make_sendbuf()
         sendbuf.copy_(torch.randn(sendbuf.shape, generator=gb))
-        grows = xg.backward(sendbuf)
+        grows = xg.backward(sendbuf).float()        # (the fixed form hands back the wire rows)
         CpuExchangeKernels.sparse_fixup_owner(xg.recv_ids, grows, sparse["map"], rank)
         # dense reference: all ranks' scatter over the global table
         dense = torch.zeros((V, d), dtype=torch.float64)
@@ -112,25 +118,32 @@ def _worker(rank, world, port, V, d, B, L, q, hook=False, bf16=False, padded=Fal
         c = DistCollective(world)
         t = torch.full((3,), float(rank + 1), dtype=torch.float64)
         c.allreduce_(t)
-        q.put((rank, bool(ok_fwd and ok_pad), bwd_err, nu, touched, t.tolist(), int(err[0])))
+        q.put((rank, bool(ok_fwd and ok_pad), bwd_err, nu, touched, t.tolist(), int(err[0]),
+               fc_state if fc is not None else None))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,hook,bf16,padded", [(2, False, False, False), (3, False, False, False),
-                                                    (2, True, False, False), (4, False, False, True),
-                                                    (4, True, False, False), (4, False, True, True),
-                                                    (8, True, True, True)])
-def test_row_exchange_protocol(world, hook, bf16, padded):
+@pytest.mark.parametrize("world,hook,bf16,padded,fc", [(2, False, False, False, None), (3, False, False, False, None),
+                                                       (2, True, False, False, None), (4, False, False, True, None),
+                                                       (4, True, False, False, None), (4, False, True, True, None),
+                                                       (8, True, True, True, None),
+                                                       (2, True, False, False, "fit"), (3, False, True, False, "fit"),
+                                                       (4, True, True, False, "fit"), (3, True, False, False, "tiny"),
+                                                       (8, True, True, False, "fit")])
+def test_row_exchange_protocol(world, hook, bf16, padded, fc):
     """hook: the owner-side claim -> before_gather -> gather split used by the lazy table Adam.
     bf16: the bf16 mode's wire rows (each delivered row == E[id] rounded to bf16).  padded: the
     routed-ahead padded blocks deliver the same counts and ids.  world 8: C4's split (eight
-    owners, blocks of B * (L + 1) + 1 ints per destination), bf16 rows, history length 20."""
+    owners, blocks of B * (L + 1) + 1 ints per destination), bf16 rows, history length 20.
+    fc: the fixed-capacity form (equal-split all-to-alls of cap + 1 slots, empty slots negative):
+    "fit" -- every block fits, the step exchanges in that form; "tiny" -- cap 2 overflows, every rank
+    sees the in-band flag and the step falls back to host split sizes on all ranks together."""
     V, d, B, L = (101, 8, 12, 6) if world < 8 else (1001, 8, 12, 20)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, V, d, B, L, q, hook, bf16, padded))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, V, d, B, L, q, hook, bf16, padded, fc))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -139,7 +152,9 @@ def test_row_exchange_protocol(world, hook, bf16, padded):
         p.join(timeout=60)
         assert p.exitcode == 0
     tot = sum(range(1, world + 1))
-    for rank, ok_fwd, bwd_err, nu, touched, red, err in res:
+    for rank, ok_fwd, bwd_err, nu, touched, red, err, fc_state in res:
+        if fc is not None:
+            assert fc_state == ((True, 0) if fc == "fit" else (False, 1)), (rank, fc_state)
         assert ok_fwd, f"rank {rank}: wrong rows delivered"
         assert bwd_err < 1e-5, f"rank {rank}: sparse reduce-scatter error {bwd_err}"
         assert nu >= touched

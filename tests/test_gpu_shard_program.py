@@ -1,0 +1,134 @@
+"""The sharded step as a step program: the fixed-capacity exchange (equal-split all-to-alls, the
+overflow flag in-band with the ids) recorded once per batch and replayed natively, over RCCL as a
+one-rank job on one MI355X (RCCL refuses two ranks on one device).
+
+Two sharded trainers from the same state run the same batch sequence in lockstep -- one eagerly,
+one by recorded step programs -- through the exchange's calibration steps (host split sizes),
+the switch to the fixed-capacity form, the recording cycle and replay cycles.  Then one batch's
+history is rewritten in place (through the library, so the tensors keep their version counters:
+the programs stay valid) with full histories that overflow the calibrated block capacity: both
+trainers must read the routed-ahead overflow flag and run that step with host split sizes (the
+program trainer falls back to an eager step for it), and the replays after it go on.  Losses agree
+within 1e-5 (relative; the duplicate fold's float atomics and the routing's round order make two
+sharded runs differ in the last bits), the tables within 1e-5 after the flush, the dense parameters
+within 1e-3 of their displacement.
+"""
+import ctypes
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(port, dtype, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FBN_NATIVE_COMM="1",
+                      FBN_DEBUG_FC=os.environ.get("FBN_DEBUG_FC", "0"))
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        from ctr_recommendation_amd import _lib
+        from ctr_recommendation_amd.data import make_batch
+        from ctr_recommendation_amd.trainer import FC_CALIB_STEPS, FiBiNETTrainer
+        from oracle.fibinet_oracle import build_model
+        V, B, L = 60000, 1024, 20
+        cfg = {"embedding_dim": 128, "vocab_size": V, "honour_config": True, "net_dropout": 0.0,
+               "compute_dtype": dtype}
+        torch.manual_seed(0)
+        init = build_model(None, cfg, honour_config=True).state_dict()
+        nb = 4
+        bs = [make_batch(700 + s, B, V, device=dev) for s in range(nb + FC_CALIB_STEPS)]
+        # calibration batches, the step before the cycle (batch nb - 1, next batch 0), then cycles
+        order = [nb + k for k in range(FC_CALIB_STEPS)] + [nb - 1] + list(range(nb)) * 5
+        heavy_at = FC_CALIB_STEPS + 1 + 3 * nb           # the 4th cycle: batch 2 is rewritten before it
+        total = len(order) + 4
+        trs = [FiBiNETTrainer(cfg, total_steps=total, batch_size=B, device=dev,
+                              init_state={k: v.clone() for k, v in init.items()}, shard=True) for _ in range(2)]
+        eager, prog_tr = trs
+        p_init = eager.flat_p.clone()
+        assert all(t.native_comm is not None and t.fc_wanted for t in trs)
+        pool = torch.cuda.MemPool()
+        progs = {}
+        losses = ([], [])
+        caps = []
+        for i, j in enumerate(order):
+            if i == heavy_at:
+                # full histories (every slot a row): more entries than the calibrated capacity;
+                # written through the library so the batch tensors keep their version counters
+                g = torch.Generator(device="cpu").manual_seed(99)
+                full = torch.randint(1, V, (B, L), generator=g).to(dev)
+                seq = bs[2][0]["item_seq"]
+                src = (ctypes.c_void_p * 1)(full.data_ptr())
+                dst = (ctypes.c_void_p * 1)(seq.data_ptr())
+                nbytes = (ctypes.c_longlong * 1)(full.numel() * 8)
+                _lib.call("fbn_copy_jobs", src, dst, nbytes, 1, _lib.stream_handle(dev))
+                torch.cuda.synchronize()
+            nxt = bs[order[i + 1]][0] if i + 1 < len(order) else bs[order[0]][0]
+            b, y = bs[j]
+            if os.environ.get("FBN_DEBUG_FC") == "1":
+                print(f"[fc] ---- step {i} batch {j}", flush=True, file=sys.stderr)
+            losses[0].append(eager.step(b, y, next_batch=nxt).item())
+            if i < FC_CALIB_STEPS + 1:
+                losses[1].append(prog_tr.step(b, y, next_batch=nxt).item())
+                if i == FC_CALIB_STEPS - 1:
+                    caps.append(prog_tr.xchg.cap)
+            elif j not in progs:
+                progs[j] = prog_tr.record_program(b, y, next_batch=nxt, pool=pool)
+                losses[1].append(prog_tr.loss.item())
+            else:
+                try:
+                    losses[1].append(prog_tr.run_program(progs[j]).item())
+                except RuntimeError as e:
+                    raise RuntimeError(f"step {i} (batch {j}): {e}") from e
+        torch.cuda.synchronize()
+        res = {"caps": caps, "fallbacks": (eager.xchg.fc_fallbacks, prog_tr.xchg.fc_fallbacks),
+               "fc": (eager.xchg.cap, prog_tr.xchg.cap), "losses": losses}
+        for t in trs:
+            t.flush()
+            t.check_ids()
+        res["de"] = float((eager.E - prog_tr.E).abs().max())
+        res["e_max"] = float(eager.E.abs().max())
+        # dense parameters: relative to their displacement (Adam turns last-bit differences into
+        # small absolute ones)
+        res["dp"] = float((eager.flat_p - prog_tr.flat_p).norm() / (eager.flat_p - p_init).norm())
+        for t in trs:
+            t.close()
+        q.put(("ok", res))
+    except Exception as e:
+        q.put((repr(e), None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_sharded_step_program_matches_eager_with_overflow_fallback(hip_device, dtype):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(_port(), dtype, q))
+    p.start()
+    status, res = q.get(timeout=300)
+    p.join(timeout=60)
+    assert status == "ok", status
+    assert res["caps"][0] > 0 and res["fc"][0] == res["fc"][1] == res["caps"][0], (res["caps"], res["fc"])
+    # the rewritten batch overflowed once per pass over it (cycles 4 and 5), in both trainers
+    assert res["fallbacks"] == (2, 2), res["fallbacks"]
+    le, lp = res["losses"]
+    for a, b in zip(le, lp):
+        assert abs(a - b) <= 1e-5 * max(1.0, abs(a)), (le, lp)
+    assert res["de"] <= 1e-5 * max(1.0, res["e_max"]), res["de"]
+    assert res["dp"] <= 1e-3, res["dp"]
