@@ -112,8 +112,9 @@ SIGNATURES = {
     "fbn_step_end": (I, [P, P, P, P, P, I, P, P]),
     "fbn_route": (I, [P, P, I, I, LL, LL, I, P, P, P, P, P, P, P]),
     "fbn_route_fc": (I, [P, P, I, I, LL, LL, I, I, P, P, P, P, P]),
-    "fbn_route_fc_status": (I, [P, I, I, P, P, P]),
-    "fbn_ring_slot": (I, [P, I, LL, P, P, P, I, LL, P]),
+    "fbn_route_fc_status": (I, [P, P, I, I, I, P, P, P]),
+    "fbn_ring_slot": (I, [P, I, LL, P, P, P, I, LL, P, LL, LL, P]),
+    "fbn_owner_gather_self": (I, [P, I, P, P, P, P, I, I, I, P, I, I, P]),
     "fbn_owner_claim": (I, [P, I, P, P, I, P]),
     "fbn_owner_gather": (I, [P, I, P, P, P, P, I, I, I, P]),
     "fbn_widen_bf16": (I, [P, P, LL, P]),
@@ -142,6 +143,7 @@ SIGNATURES = {
     "fbn_comm_init": (I, [P, P, I, I]),
     "fbn_comm_destroy": (I, [P]),
     "fbn_comm_alltoallv": (I, [P, P, P, P, P, LL, P]),
+    "fbn_comm_alltoall_peers": (I, [P, P, P, LL, P]),
     "fbn_comm_alltoall": (I, [P, P, P, LL, P]),
     "fbn_comm_allreduce": (I, [P, P, LL, I, P]),
 }

@@ -189,6 +189,36 @@ extern "C" int fbn_comm_alltoall(void* comm, const void* send, void* recv, long 
   return r == ncclSuccess ? 0 : fail("fbn_comm_alltoall", r);
 }
 
+// Equal-split all-to-all WITHOUT the caller's own block (grouped ncclSend / ncclRecv to every
+// peer): the fixed-capacity exchange keeps a rank's requests to itself in place -- the owner side
+// reads / writes the requester's buffers for that block directly -- so no self copy crosses RCCL.
+// A one-rank communicator does nothing here.
+extern "C" int fbn_comm_alltoall_peers(void* comm, const void* send, void* recv, long long bytes_per_peer,
+                                       void* stream) {
+  if (int rc = need_loaded("fbn_comm_alltoall_peers")) return rc;
+  Comm* c = static_cast<Comm*>(comm);
+  if (!c || bytes_per_peer < 0) {
+    fbn_set_error("fbn_comm_alltoall_peers: bad arguments");
+    return 1;
+  }
+  if (bytes_per_peer == 0 || c->world <= 1) return 0;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  ncclResult_t r = g_rccl.group_start();
+  if (r != ncclSuccess) return fail("fbn_comm_alltoall_peers", r);
+  for (int p = 0; p < c->world && r == ncclSuccess; ++p) {
+    if (p == c->rank) continue;
+    r = g_rccl.send(static_cast<const char*>(send) + (size_t)p * bytes_per_peer, (size_t)bytes_per_peer, ncclUint8,
+                    p, c->comm, st);
+    if (r == ncclSuccess)
+      r = g_rccl.recv(static_cast<char*>(recv) + (size_t)p * bytes_per_peer, (size_t)bytes_per_peer, ncclUint8, p,
+                      c->comm, st);
+  }
+  ncclResult_t e = g_rccl.group_end();
+  if (r != ncclSuccess) return fail("fbn_comm_alltoall_peers", r);
+  if (e != ncclSuccess) return fail("fbn_comm_alltoall_peers", e);
+  return 0;
+}
+
 // In-place sum all-reduce of n elements: dtype 0 = f32, 1 = f64, 2 = i32.
 extern "C" int fbn_comm_allreduce(void* comm, void* buf, long long n, int dtype, void* stream) {
   if (int rc = need_loaded("fbn_comm_allreduce")) return rc;

@@ -128,21 +128,36 @@ __global__ void route_fc_init_kernel(int* __restrict__ send_ids, long long n, in
 }
 
 // owner side of a fixed-capacity routing: stat[0] |= "some requester overflowed" (a block whose
-// last slot is -2) -- the same value on every rank, so all of them agree on a fallback
-__global__ void route_fc_status_kernel(const int* __restrict__ recv_ids, int world, int cap, int* __restrict__ stat) {
-  const int r = threadIdx.x;
-  const bool f = r < world && recv_ids[(size_t)r * (cap + 1) + cap] == -2;
-  if (__ballot(f) != 0ull && r == 0) stat[0] = 1;
+// last slot is -2) -- the same value on every rank, so all of them agree on a fallback.  self_send
+// (an all-to-all that skipped the caller's own block): that block is copied from the caller's
+// send_ids first (its flag slot included).
+__global__ void __launch_bounds__(256) route_fc_status_kernel(const int* __restrict__ self_send,
+                                                              int* __restrict__ recv_ids, int world, int rank, int cap,
+                                                              int* __restrict__ stat) {
+  const size_t o = (size_t)rank * (cap + 1);
+  if (self_send)
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i <= cap; i += (long long)gridDim.x * blockDim.x)
+      reinterpret_cast<int*>(recv_ids)[o + i] = self_send[o + i];
+  if (blockIdx.x == 0 && threadIdx.x < 64) {
+    const int r = threadIdx.x;
+    // (the own block's flag read at its source: the copy above may not have reached it yet)
+    const int* blk = (self_send && r == rank) ? self_send : recv_ids;
+    const bool f = r < world && blk[(size_t)r * (cap + 1) + cap] == -2;
+    if (__ballot(f) != 0ull && r == 0) stat[0] = 1;
+  }
 }
 
 // owner side: out[i] = E_local[ids[i]]; G = D/4 lanes per row.  Received entry i claims its
 // row for the sparse gradient (map[r] = i, slot_row[i] = r) unless another entry did first.
 // Rows with global id 0 (rank 0, local row 0) are padding: gathered (the item lookup of id 0
 // reads row 0) but never registered for a gradient.
+// (self_out: entries [self_lo, self_lo + self_n) -- the caller's own requests in the fixed-capacity
+// exchange -- are written there instead, at the same index: the requester's row buffer itself)
 template <int D>
 __global__ void __launch_bounds__(256) owner_gather_kernel(const int* __restrict__ ids, int n, const float* __restrict__ E,
                                                            float* __restrict__ out, int* map, int* slot_row, int rank,
-                                                           int out_bf16) {
+                                                           int out_bf16, float* __restrict__ self_out, int self_lo,
+                                                           int self_n) {
   constexpr int G = D / 4, RPW = 64 / G;
   const int lane = threadIdx.x & 63, q = lane % G;
   const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -153,11 +168,12 @@ __global__ void __launch_bounds__(256) owner_gather_kernel(const int* __restrict
     const int r = ids[i];
     if (r < 0) continue;   // a fixed-capacity block's empty slot: nothing requested
     const f32x4 row = *reinterpret_cast<const f32x4*>(E + (size_t)r * D + 4 * q);
+    float* dst = (self_out && i >= self_lo && i < self_lo + self_n) ? self_out : out;
     if (out_bf16)   // bf16 mode: the rows cross the wire as bf16 (half the all-to-all bytes)
-      *reinterpret_cast<bf16x4*>(reinterpret_cast<short*>(out) + i * D + 4 * q) =
+      *reinterpret_cast<bf16x4*>(reinterpret_cast<short*>(dst) + i * D + 4 * q) =
           (bf16x4){f2bf(row[0]), f2bf(row[1]), f2bf(row[2]), f2bf(row[3])};
     else
-      *reinterpret_cast<f32x4*>(out + i * D + 4 * q) = row;
+      *reinterpret_cast<f32x4*>(dst + i * D + 4 * q) = row;
     if (map && q == 0 && !(rank == 0 && r == 0) &&
         __hip_atomic_load(map + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == -1) {
       int expected = -1;
@@ -239,13 +255,17 @@ extern "C" int fbn_route_fc(const int64_t* item, const int64_t* seq, int B, int 
 // (this rank's, or any requester's in-band flag), then stat[0 .. nranks] is copied to `host`
 // (pinned) on the stream -- the host reads it once the stream got there and, if set, every rank
 // exchanges that step with host-side split sizes instead (RowExchange).
-extern "C" int fbn_route_fc_status(const int* recv_ids, int nranks, int cap, int* stat, int* host, void* stream) {
-  if (nranks < 1 || nranks > 64 || cap < 1 || !recv_ids || !stat) {
-    fbn_set_error("fbn_route_fc_status: 1 <= nranks <= 64, cap >= 1, buffers");
+extern "C" int fbn_route_fc_status(const int* send_ids, int* recv_ids, int nranks, int rank, int cap, int* stat,
+                                   int* host, void* stream) {
+  if (nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks || cap < 1 || !recv_ids || !stat) {
+    fbn_set_error("fbn_route_fc_status: 1 <= nranks <= 64, 0 <= rank < nranks, cap >= 1, buffers");
     return FBN_ERR_ARG;
   }
   hipStream_t st = (hipStream_t)stream;
-  fbn_launch(route_fc_status_kernel, dim3(1), dim3(64), 0, st, recv_ids, nranks, cap, stat);
+  long long blocks = send_ids ? ((long long)cap + 1 + 255) / 256 : 1;
+  if (blocks > 1024) blocks = 1024;
+  fbn_launch(route_fc_status_kernel, dim3((unsigned)blocks), dim3(256), 0, st, send_ids, recv_ids, nranks, rank, cap,
+             stat);
   FBN_CHECK_LAUNCH();
   if (host && hipMemcpyAsync(host, stat, sizeof(int) * (nranks + 1), hipMemcpyDeviceToHost, st) != hipSuccess) {
     fbn_set_error("fbn_route_fc_status: hipMemcpyAsync failed");
@@ -276,7 +296,23 @@ extern "C" int fbn_owner_gather(const int* ids, int n, const float* E, void* out
                                 int D, int out_bf16, void* stream) {
   if (n <= 0) return FBN_OK;
   hipStream_t st = (hipStream_t)stream;
-  FBN_DISPATCH_D(owner_gather_kernel, D, rows_grid(n, D), ids, n, E, (float*)out, map, slot_row, rank, out_bf16);
+  FBN_DISPATCH_D(owner_gather_kernel, D, rows_grid(n, D), ids, n, E, (float*)out, map, slot_row, rank, out_bf16,
+                 nullptr, 0, 0);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+extern "C" int fbn_owner_gather_self(const int* ids, int n, const float* E, void* out, int* map, int* slot_row,
+                                     int rank, int D, int out_bf16, void* self_out, int self_lo, int self_n,
+                                     void* stream) {
+  if (n <= 0) return FBN_OK;
+  if (self_n < 0 || self_lo < 0 || (self_n > 0 && !self_out)) {
+    fbn_set_error("fbn_owner_gather_self: self block");
+    return FBN_ERR_ARG;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  FBN_DISPATCH_D(owner_gather_kernel, D, rows_grid(n, D), ids, n, E, (float*)out, map, slot_row, rank, out_bf16,
+                 (float*)self_out, self_lo, self_n);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

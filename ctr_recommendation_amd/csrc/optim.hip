@@ -2171,24 +2171,29 @@ static dim3 group_grid(long long n, int D, long long cap) {
 
 // N > 1 owner, deferred table gradients: the received gradient rows (wire: n floats, bf16 or f32)
 // widened / copied into ring slot step % ring_n, whose address goes to *cell (read by the fold,
-// the norm and the step tail through FBN_GRAD_CELL)
+// the norm and the step tail through FBN_GRAD_CELL).  Floats [self_lo, self_lo + self_n) come from
+// wire_self instead (the caller's own block of the fixed-capacity exchange: the requester's send
+// buffer, never sent through RCCL).
 __global__ void __launch_bounds__(256) ring_slot_kernel(float* __restrict__ ring, int ring_n, long long stride,
                                                         const int* __restrict__ step, float** __restrict__ cell,
-                                                        const void* __restrict__ wire, int wire_bf16, long long n8) {
+                                                        const void* __restrict__ wire, int wire_bf16, long long n8,
+                                                        const void* __restrict__ wire_self, long long self_lo8,
+                                                        long long self_n8) {
   float* dst = ring + (size_t)(*step % ring_n) * stride;
   if (blockIdx.x == 0 && threadIdx.x == 0) *cell = dst;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    const void* src = (wire_self && i >= self_lo8 && i < self_lo8 + self_n8) ? wire_self : wire;
     f32x4 a, b;
     if (wire_bf16) {
-      const bf16x8 v = reinterpret_cast<const bf16x8*>(wire)[i];
+      const bf16x8 v = reinterpret_cast<const bf16x8*>(src)[i];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         a[k] = __uint_as_float((unsigned)(unsigned short)v[k] << 16);
         b[k] = __uint_as_float((unsigned)(unsigned short)v[k + 4] << 16);
       }
     } else {
-      a = reinterpret_cast<const f32x4*>(wire)[2 * i];
-      b = reinterpret_cast<const f32x4*>(wire)[2 * i + 1];
+      a = reinterpret_cast<const f32x4*>(src)[2 * i];
+      b = reinterpret_cast<const f32x4*>(src)[2 * i + 1];
     }
     reinterpret_cast<f32x4*>(dst)[2 * i] = a;
     reinterpret_cast<f32x4*>(dst)[2 * i + 1] = b;
@@ -2196,17 +2201,20 @@ __global__ void __launch_bounds__(256) ring_slot_kernel(float* __restrict__ ring
 }
 
 extern "C" int fbn_ring_slot(float* ring, int ring_n, long long stride, const int* step, void* cell, const void* wire,
-                             int wire_bf16, long long n, void* stream) {
+                             int wire_bf16, long long n, const void* wire_self, long long self_lo, long long self_n,
+                             void* stream) {
   if (!ring || !step || !cell || ring_n < 1 || n < 0 || n > stride || (n & 7) || (n > 0 && !wire) ||
-      ((uintptr_t)ring & 15) || (stride & 7) || ((uintptr_t)wire & 15)) {
-    fbn_set_error("fbn_ring_slot: ring, step, cell; n % 8 == 0, n <= stride, 16-B aligned buffers");
+      ((uintptr_t)ring & 15) || (stride & 7) || ((uintptr_t)wire & 15) || ((uintptr_t)wire_self & 15) ||
+      (self_lo & 7) || (self_n & 7) || self_lo < 0 || self_n < 0 || self_lo + self_n > n ||
+      (self_n > 0 && !wire_self)) {
+    fbn_set_error("fbn_ring_slot: ring, step, cell; n, self_lo, self_n % 8 == 0, n <= stride, 16-B aligned buffers");
     return FBN_ERR_ARG;
   }
   long long blocks = (n / 8 + 255) / 256;
   if (blocks < 1) blocks = 1;
   if (blocks > 8192) blocks = 8192;
   fbn_launch(ring_slot_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, ring, ring_n, stride, step,
-             (float**)cell, wire, wire_bf16, n / 8);
+             (float**)cell, wire, wire_bf16, n / 8, self_n > 0 ? wire_self : nullptr, self_lo / 8, self_n / 8);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

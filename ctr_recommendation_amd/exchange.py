@@ -92,6 +92,11 @@ class NativeComm:
         call("fbn_comm_alltoall", self.handle, ptr(inp), ptr(out), inp.numel() * inp.element_size() // self.world,
              _lib.stream_handle(out.device))
 
+    def alltoall_peers(self, out: torch.Tensor, inp: torch.Tensor) -> None:
+        """Equal split without this rank's own block (it stays where it is; nothing at one rank)."""
+        call("fbn_comm_alltoall_peers", self.handle, ptr(inp), ptr(out),
+             inp.numel() * inp.element_size() // self.world, _lib.stream_handle(out.device))
+
     def allreduce_(self, t: torch.Tensor) -> None:
         call("fbn_comm_allreduce", self.handle, ptr(t), t.numel(), _DTYPE_CODE[t.dtype], _lib.stream_handle(t.device))
 
@@ -145,8 +150,13 @@ class HipExchangeKernels:
         call("fbn_route_fc", ptr(item), ptr(seq), B, L, V, Vl, world, cap, ptr(send_ids), ptr(pos), ptr(stat), ptr(err),
              _lib.stream_handle(item.device))
 
-    def route_fc_status(self, recv_ids, world, cap, stat, host):
-        call("fbn_route_fc_status", ptr(recv_ids), world, cap, ptr(stat), ptr(host), _lib.stream_handle(recv_ids.device))
+    def route_fc_status(self, send_ids, recv_ids, world, rank, cap, stat, host):
+        call("fbn_route_fc_status", ptr(send_ids), ptr(recv_ids), world, rank, cap, ptr(stat), ptr(host),
+             _lib.stream_handle(recv_ids.device))
+
+    def owner_gather_self(self, ids, E, out, map_, slot_row, rank, d, self_out, self_lo, self_n):
+        call("fbn_owner_gather_self", ptr(ids), ids.shape[0], ptr(E), ptr(out), ptr(map_), ptr(slot_row), rank, d,
+             int(out.dtype == torch.bfloat16), ptr(self_out), self_lo, self_n, _lib.stream_handle(E.device))
 
 
 def _pad4(n: int) -> int:
@@ -228,10 +238,26 @@ class RowExchange:
         self.fc_wire = torch.empty((n, self.d), dtype=self.row_dtype, device=self.device)    # owner: received grads
         self.fc_sets = {}
         self.fc_next = None
+        # native RCCL: this rank's own block never crosses the all-to-alls (fbn_comm_alltoall_peers) --
+        # the owner writes its looked-up rows straight into the requester's row buffer and reads the
+        # requester's gradient rows from its send buffer
+        self.fc_self = self.comm is not None
 
     @property
     def fc_slots(self) -> int:
         return self.world * (self.cap + 1)
+
+    @property
+    def fc_self_rows(self):
+        """(first row, rows) of this rank's own block when it stays in place, else (0, 0)."""
+        return (self.rank * (self.cap + 1), self.cap + 1) if self.fc_self else (0, 0)
+
+    def _a2a_fc(self, out, inp, route=False):
+        """Equal-split all-to-all of the fixed-capacity form (own block skipped when it stays in place)."""
+        if self.fc_self:
+            (self.route_comm if route else self.comm).alltoall_peers(out, inp)
+        else:
+            self._a2a(out, inp, None, None, self.route_group if route else None, route=route)
 
     def _fc_routing_set(self, key):
         st = self.fc_sets.get(key)
@@ -268,8 +294,9 @@ class RowExchange:
             # CPU ranks (gloo tests): routed inline, nothing to wait for
             self.k.route_fc(item, seq if L else None, B, L, self.V, self.Vl, self.world, self.cap, st["send_ids"],
                             st["pos"], st["stat"], err)
-            self._a2a(st["recv_ids"], st["send_ids"], None, None, self.route_group, route=True)
-            self.k.route_fc_status(st["recv_ids"], self.world, self.cap, st["stat"], st["host"])
+            self._a2a_fc(st["recv_ids"], st["send_ids"], route=True)
+            self.k.route_fc_status(st["send_ids"] if self.fc_self else None, st["recv_ids"], self.world, self.rank,
+                                   self.cap, st["stat"], st["host"])
             self.fc_next, self.fc_wait = (key, st), (lambda: None)
             if send_rows:
                 self.next_lids = st["recv_ids"]
@@ -282,8 +309,9 @@ class RowExchange:
         with torch.cuda.stream(self.side):
             self.k.route_fc(item, seq if L else None, B, L, self.V, self.Vl, self.world, self.cap, st["send_ids"],
                             st["pos"], st["stat"], err)
-            self._a2a(st["recv_ids"], st["send_ids"], None, None, self.route_group, route=True)
-            self.k.route_fc_status(st["recv_ids"], self.world, self.cap, st["stat"], st["host"])
+            self._a2a_fc(st["recv_ids"], st["send_ids"], route=True)
+            self.k.route_fc_status(st["send_ids"] if self.fc_self else None, st["recv_ids"], self.world, self.rank,
+                                   self.cap, st["stat"], st["host"])
         ev = torch.cuda.Event()
         _lib.record_event(ev, self.side)
         st["event"] = ev
@@ -308,14 +336,18 @@ class RowExchange:
         self.recv_ids = st["recv_ids"]
         self.send_counts = self.recv_counts = None
         n = self.fc_slots
-        if before_gather is not None and sparse.get("map") is not None:
+        claim = before_gather is not None and sparse.get("map") is not None
+        if claim:
             self.k.owner_claim(self.recv_ids, sparse["map"], sparse["slot_row"], self.rank)
             before_gather(n)
-            self.k.owner_gather(self.recv_ids, E_local, self.fc_reply, None, None, self.rank, self.d)
+        m, sr = (None, None) if claim else (sparse["map"], sparse["slot_row"])
+        if self.fc_self:
+            lo, cnt = self.fc_self_rows
+            self.k.owner_gather_self(self.recv_ids, E_local, self.fc_reply, m, sr, self.rank, self.d, self.fc_rows,
+                                     lo, cnt)
         else:
-            self.k.owner_gather(self.recv_ids, E_local, self.fc_reply, sparse["map"], sparse["slot_row"], self.rank,
-                                self.d)
-        self._a2a(self.fc_rows, self.fc_reply, None, None)
+            self.k.owner_gather(self.recv_ids, E_local, self.fc_reply, m, sr, self.rank, self.d)
+        self._a2a_fc(self.fc_rows, self.fc_reply)
         self.rows_buf = self.fc_rows
         return self.fc_rows
 
@@ -533,11 +565,16 @@ class RowExchange:
             cs = self._comm_stream
             _lib.wait_stream(cs, cur)
             with torch.cuda.stream(cs):
-                self._a2a(wire, sendbuf, self.recv_counts, self.send_counts)
+                if self.fc_active:
+                    self._a2a_fc(wire, sendbuf)
+                else:
+                    self._a2a(wire, sendbuf, self.recv_counts, self.send_counts)
             work = torch.cuda.Event()
             _lib.record_event(work, cs)
             for t in (wire, grad, sendbuf):
                 t.record_stream(cs)
+        elif self.fc_active:
+            self._a2a_fc(wire, sendbuf)
         elif self.stage_on_cpu or self.comm is not None:       # host-staged, or on this stream
             self._a2a(wire, sendbuf, self.recv_counts, self.send_counts)
         else:

@@ -636,7 +636,8 @@ class FiBiNETTrainer:
             # on the main stream ahead of the claims: a cross-queue wait inside a replayed graph
             # costs ~10 us, about what the conversion itself takes
             self.acts["w16"] = ops.bf16_weights(self.p, d, self.acts, st, x=batch["item_emb_d128"])
-        elif cfg.bf16 and self.xchg is None and not w16_late:
+        elif cfg.bf16 and not w16_late:
+            # (N > 1: beside the row exchange)
             w16_ev = start_w16()
         if self.xchg is not None:
             rows = self.xchg.forward(batch["item_id"], seq, self.E, {"map": self.map, "slot_row": self.slot_row},
@@ -763,16 +764,19 @@ class FiBiNETTrainer:
                 # right slot), and the readers take them through the slot's pointer cell
                 wire = x.backward_finish() if x._pending is not None else x.backward(sendbuf)
                 defer_now = self.deferred and n_ent <= self.ring_cap
+                # (this rank's own block was not sent: its rows are read from the send buffer itself)
+                lo, cnt = x.fc_self_rows
+                self_args = (ptr(x.fc_send) if cnt else None, lo * d, cnt * d)
                 if defer_now:
                     call("fbn_ring_slot", ptr(self.ring), self.ring_n, self._ring_stride(), ptr(self.step_dev),
-                         ptr(self.ring_cell), ptr(wire), int(wire.dtype == torch.bfloat16), n_ent * d, st)
+                         ptr(self.ring_cell), ptr(wire), int(wire.dtype == torch.bfloat16), n_ent * d, *self_args, st)
                     gsrc = (self.ring_cell, None, 1 | FBN_GRAD_CELL)
                 else:
                     if self._fc_grad is None or self._fc_grad.shape[0] < n_ent:
                         self._fc_grad = torch.empty((n_ent, d), dtype=torch.float32, device=self.device)
                     grows = self._fc_grad[:n_ent]
                     call("fbn_ring_slot", ptr(grows), 1, n_ent * d, ptr(self.step_dev), ptr(self.ring_cell), ptr(wire),
-                         int(wire.dtype == torch.bfloat16), n_ent * d, st)
+                         int(wire.dtype == torch.bfloat16), n_ent * d, *self_args, st)
                     gsrc = (grows, None, 1)
             else:
                 slot = self._grad_slot()

@@ -465,10 +465,18 @@ int fbn_route(const int64_t* item, const int64_t* seq, int B, int L, long long V
  * (fbn_owner_claim / fbn_owner_gather / fbn_sparse_fixup / fbn_adam_prefetch_rows) skip negative ids.
  * fbn_route_fc_status (after the ids all-to-all, recv_ids as received): stat[0] |= any requester's
  * flag -- the same on every rank -- and stat[0 .. nranks] is copied to host (pinned, may be NULL) on
- * the stream: a set flag makes every rank exchange that step with host-side split sizes instead. */
+ * the stream: a set flag makes every rank exchange that step with host-side split sizes instead.
+ * send_ids non-NULL: the all-to-all skipped the caller's own block (fbn_comm_alltoall_peers), which
+ * is copied from send_ids into recv_ids first. */
 int fbn_route_fc(const int64_t* item, const int64_t* seq, int B, int L, long long V, long long Vl, int nranks,
                  int cap, int* send_ids, int* pos, int* stat, int* err, void* stream);
-int fbn_route_fc_status(const int* recv_ids, int nranks, int cap, int* stat, int* host, void* stream);
+int fbn_route_fc_status(const int* send_ids, int* recv_ids, int nranks, int rank, int cap, int* stat, int* host,
+                        void* stream);
+/* fbn_owner_gather with the caller's own block redirected: entries [self_lo, self_lo + self_n) are
+ * written to self_out (same index) -- the requester's row buffer, so that block never crosses RCCL
+ * (the fixed-capacity exchange's all-to-alls skip it: fbn_comm_alltoall_peers). */
+int fbn_owner_gather_self(const int* ids, int n, const float* E, void* out, int* map, int* slot_row, int rank, int D,
+                          int out_bf16, void* self_out, int self_lo, int self_n, void* stream);
 /* claims only (the lazy table Adam replays the claimed rows before fbn_owner_gather(map = NULL)) */
 int fbn_owner_claim(const int* ids, int n, int* map, int* slot_row, int rank, void* stream);
 /* out_bf16: reply rows as bf16 (the bf16 mode's wire format; fbn_fields_fwd(rows_bf16 = 1) reads them) */
@@ -478,9 +486,11 @@ int fbn_owner_gather(const int* ids, int n, const float* E, void* out, int* map,
  * wire_bf16, else f32; n % 8 == 0, n <= stride) widened / copied into ring slot (*step % ring_n) of
  * ring [ring_n][stride]; *cell = that slot's address (pass cell with Lp1 | FBN_GRAD_CELL to
  * fbn_sparse_fixup / fbn_sumsq_sparse / fbn_adam_step_tail) -- the slot is chosen on the device, so
- * a recorded step program replays with the right slot. */
+ * a recorded step program replays with the right slot.  Elements [self_lo, self_lo + self_n) are read
+ * from wire_self instead (the caller's own block, never sent: the requester's gradient rows). */
 int fbn_ring_slot(float* ring, int ring_n, long long stride, const int* step, void* cell, const void* wire,
-                  int wire_bf16, long long n, void* stream);
+                  int wire_bf16, long long n, const void* wire_self, long long self_lo, long long self_n,
+                  void* stream);
 /* bf16 -> f32 (n % 8 == 0, 16-B aligned): the owner's received bf16 gradient rows (bf16 mode). */
 int fbn_widen_bf16(const void* in, float* out, long long n, void* stream);
 /* out [world][cap + 1]: out[o][j] = send_ids[offsets[o] + j] for j < counts[o], else -1, and
@@ -576,6 +586,9 @@ int fbn_comm_destroy(void* comm);
 int fbn_comm_alltoallv(void* comm, const void* send, const int* send_counts, void* recv, const int* recv_counts,
                        long long row_bytes, void* stream);
 int fbn_comm_alltoall(void* comm, const void* send, void* recv, long long bytes_per_peer, void* stream);
+/* the equal-split all-to-all WITHOUT the caller's own block (grouped send / recv to the peers; a
+ * no-op at one rank): the fixed-capacity exchange keeps a rank's requests to itself in place */
+int fbn_comm_alltoall_peers(void* comm, const void* send, void* recv, long long bytes_per_peer, void* stream);
 int fbn_comm_allreduce(void* comm, void* buf, long long n, int dtype, void* stream);
 
 #ifdef __cplusplus

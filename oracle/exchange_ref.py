@@ -71,8 +71,12 @@ class CpuExchangeKernels:
         stat[0] = ovf
         stat[1:1 + world] = torch.tensor(cnt, dtype=stat.dtype)
 
-    def route_fc_status(self, recv_ids, world, cap, stat, host):
-        """Restates fbn_route_fc_status: stat[0] |= any requester's in-band flag; host <- stat."""
+    def route_fc_status(self, send_ids, recv_ids, world, rank, cap, stat, host):
+        """Restates fbn_route_fc_status: (send_ids given: the own block copied first, the all-to-all
+        skipped it) stat[0] |= any requester's in-band flag; host <- stat."""
+        if send_ids is not None:
+            o = rank * (cap + 1)
+            recv_ids[o:o + cap + 1] = send_ids[o:o + cap + 1]
         if any(int(recv_ids[r * (cap + 1) + cap]) == -2 for r in range(world)):
             stat[0] = 1
         host[:world + 1] = stat[:world + 1]
