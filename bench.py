@@ -23,6 +23,10 @@ One JSON line on rank 0 with the contract keys plus
                  which is why a rocprof per-name average -- graph replays + probes + these -- sits
                  between the two; tools/step_launches.py lists one step's launches);
   host_enqueue_ms_per_step: host time to issue the K timed steps (graph replays or eager launches);
+  host_wait_ms_per_step (N > 1 / the sharded one-rank job): of that, the host's wait for the routed-ahead
+                 batch's overflow flag before each step -- back-pressure: the flag is ready ~1/3 into the
+                 step before, so the host waits while the GPU still has ~2/3 of a step queued;
+                 host_busy_ms_per_step = enqueue - wait (what the host needs per step);
   cpu_baseline:  the oracle's torch-CPU restatement of the reference train step (rank 0, N=1).
 """
 from __future__ import annotations
@@ -401,7 +405,7 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
         run_step(i)
         i += 1
     t_host = time.perf_counter() - t0            # host enqueue time of the K steps
-    t_wait = tr.xchg.host_wait_s if tr.xchg is not None else 0.0   # of which blocked on routed counts
+    t_wait = tr.xchg.host_wait_s if tr.xchg is not None else 0.0   # of which waiting for the routed-ahead batch
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -661,7 +665,8 @@ def main():
                            if args.bn == "local" else "SyncBN (global-batch statistics; the parity mode)"}
                           if world > 1 or FORCE_SHARD else {})},
             "host_enqueue_ms_per_step": round(r["t_host"] / K * 1e3, 4),
-            **({"host_blocked_ms_per_step": round(r["t_wait"] / K * 1e3, 4)} if r["t_wait"] else {}),
+            **({"host_wait_ms_per_step": round(r["t_wait"] / K * 1e3, 4),
+                "host_busy_ms_per_step": round((r["t_host"] - r["t_wait"]) / K * 1e3, 4)} if r["t_wait"] else {}),
             "roofline": r["roofline"],
             "rooflines": r["rooflines"],
             "rooflines_in_step_from": r["probe_source"],

@@ -115,6 +115,8 @@ SIGNATURES = {
     "fbn_route_fc_status": (I, [P, P, I, I, I, P, P, P]),
     "fbn_ring_slot": (I, [P, I, LL, P, P, P, I, LL, P, LL, LL, P]),
     "fbn_owner_gather_self": (I, [P, I, P, P, P, P, I, I, I, P, I, I, P]),
+    "fbn_adam_owner_claim_catchup": (I, [P, I, I, P, P, P, P, P, P, LL, I, I, P, P, P, F, F, F, P, P, P, LL, I, I,
+                                         P]),
     "fbn_owner_claim": (I, [P, I, P, P, I, P]),
     "fbn_owner_gather": (I, [P, I, P, P, P, P, I, I, I, P]),
     "fbn_widen_bf16": (I, [P, P, LL, P]),

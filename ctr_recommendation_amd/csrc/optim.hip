@@ -1678,10 +1678,18 @@ __device__ __forceinline__ void adam_claim2_body(float* __restrict__ p, float* _
   const long long i = (long long)blk * blockDim.x + threadIdx.x;
   int r = 0, key = 0x7fffffff, pe = -1;
   if (i < n) {
-    const long long b = i / (cs.L + 1), tt = i - b * (cs.L + 1);
-    const long long id = tt == 0 ? cs.item[b] : cs.seq[b * cs.L + (tt - 1)];
+    long long id;
+    bool ok;
+    if (cs.lids) {   // owner mode (N > 1): the received local rows (negative: an empty slot)
+      id = cs.lids[i];
+      ok = id >= 0 && id < cs.V && !(cs.skip0 && id == 0);
+    } else {
+      const long long b = i / (cs.L + 1), tt = i - b * (cs.L + 1);
+      id = tt == 0 ? cs.item[b] : cs.seq[b * cs.L + (tt - 1)];
+      ok = id > 0 && id < cs.V;
+    }
     int owner = -1, mine = -1;
-    if (id > 0 && id < cs.V) {
+    if (ok) {
       const int4 rs = row_state(last, id);   // tag, last, pend: one 16-B load
       const unsigned long long pv = cs.pre ? (((unsigned long long)(unsigned)rs.y << 32) | (unsigned)rs.x) : 0ull;
       const int k0 = rs.z;
@@ -2747,6 +2755,45 @@ extern "C" int fbn_adam_claim_catchup(const int64_t* item, const int64_t* seq, i
   return claim_catchup_impl(item, seq, B, L, V, map, slot_row, dup, hasdup, preclaim, p, m, v, nrows, D, F, last,
                             consts_table, step, wd, beta2, eps, pend, ring, coef_hist, ring_stride, ring_n, decoupled,
                             nullptr, 0, stream);
+}
+
+// N > 1 owner, the fixed-capacity exchange: the claims of the received local rows (lids [n], negative =
+// empty slot; rank 0's row 0 is padding when skip0) and the claimed-row catch-up in ONE launch, as
+// fbn_adam_claim_catchup does for the single GPU.  preclaim (optional): the tags
+// fbn_adam_prefetch_rows posted during the previous step for this very routing (its entry indices
+// are these slots): a row tagged for this step is claimed by its smallest slot without a CAS.
+extern "C" int fbn_adam_owner_claim_catchup(const int* lids, int n, int skip0, int* map, int* slot_row,
+                                            unsigned long long* preclaim, float* p, float* m, float* v,
+                                            long long nrows, int D, int F, int* last, const void* consts_table,
+                                            const int* step, float wd, float beta2, float eps, int* pend,
+                                            const float* ring, const float* coef_hist, long long ring_stride,
+                                            int ring_n, int decoupled, void* stream) {
+  if (n <= 0 || nrows <= 0) return FBN_OK;
+  if (!lids || !map || !slot_row || !last) {
+    fbn_set_error("fbn_adam_owner_claim_catchup: lids, map, slot_row and last are required");
+    return FBN_ERR_ARG;
+  }
+  if (F < 1 || F > FBN_LAZY_MAX_LAG) { fbn_set_error("fbn_adam_owner_claim_catchup: 1 <= F <= 512"); return FBN_ERR_ARG; }
+  if (pend && (!ring || !coef_hist || ring_n <= F)) {
+    fbn_set_error("fbn_adam_owner_claim_catchup: deferred gradients need ring, coef_hist and ring_n > F");
+    return FBN_ERR_ARG;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const float omb2 = (float)(1.0 - (double)beta2);
+  const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
+  ClaimSrc cs{nullptr, nullptr, 0, nrows, map, slot_row, nullptr, nullptr, preclaim};
+  cs.lids = lids;
+  cs.skip0 = skip0;
+  const dim3 g2((unsigned)((n + 255) / 256));
+  if (decoupled) {
+    FBN_DISPATCH_D_B(adam_claim2_kernel, true, D, g2, p, m, v, cs, n, last, (const AdamConsts*)consts_table, step, wd,
+                     beta2, omb2, eps, ps);
+  } else {
+    FBN_DISPATCH_D_B(adam_claim2_kernel, false, D, g2, p, m, v, cs, n, last, (const AdamConsts*)consts_table, step,
+                     wd, beta2, omb2, eps, ps);
+  }
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
 }
 
 extern "C" int fbn_adam_claim_catchup_conv(const int64_t* item, const int64_t* seq, int B, int L, long long V,

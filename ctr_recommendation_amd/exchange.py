@@ -337,7 +337,10 @@ class RowExchange:
         self.send_counts = self.recv_counts = None
         n = self.fc_slots
         claim = before_gather is not None and sparse.get("map") is not None
-        if claim:
+        if claim and sparse.get("claim_catchup") is not None:
+            # the claims and the claimed-row catch-up in one launch (the trainer's lazy table Adam)
+            sparse["claim_catchup"](self.recv_ids, n)
+        elif claim:
             self.k.owner_claim(self.recv_ids, sparse["map"], sparse["slot_row"], self.rank)
             before_gather(n)
         m, sr = (None, None) if claim else (sparse["map"], sparse["slot_row"])

@@ -108,6 +108,10 @@ FBN_GRAD_CELL = 0x20000      # include/fibinet.h: the gradient-row argument is a
 # N > 1, the owner's ahead-of-time catch-up of the next step's requested rows in two passes (tagged
 # pre-claims + the four-row replay engine); FBN_OWNER_PF2=0 keeps the one-pass kernel (A/B)
 _OWNER_PF2 = os.environ.get("FBN_OWNER_PF2", "1") != "0"
+# N > 1, the fixed-capacity exchange: the owner's claims and claimed-row catch-up in one launch
+# (fbn_adam_owner_claim_catchup, pre-claims from the owner prefetch); FBN_OWNER_CLAIM_FUSED=0 keeps
+# fbn_owner_claim + fbn_adam_catchup (A/B)
+_OWNER_CLAIM_FUSED = os.environ.get("FBN_OWNER_CLAIM_FUSED", "1") != "0"
 from .schedule import OneCycle, adam_table
 
 TABLE = "item_emb.weight"
@@ -640,8 +644,23 @@ class FiBiNETTrainer:
             # (N > 1: beside the row exchange)
             w16_ev = start_w16()
         if self.xchg is not None:
-            rows = self.xchg.forward(batch["item_id"], seq, self.E, {"map": self.map, "slot_row": self.slot_row},
-                                     self.err, before_gather=catch_up if lazy else None)
+            sparse = {"map": self.map, "slot_row": self.slot_row}
+            if lazy and _OWNER_CLAIM_FUSED:
+                def owner_claim_catchup(ids, n):
+                    # fixed-capacity form: claims + claimed-row catch-up in one launch, the claims
+                    # decided by the pre-claim tags the previous step's owner prefetch posted for
+                    # this very routing (those with a tag of this step; the rest by CAS)
+                    ev = _events(probe, "adam_catchup")
+                    pre = self.row_state.view(torch.int64)[:, 0] if (self.prefetch_owner and _OWNER_PF2) else None
+                    call("fbn_adam_owner_claim_catchup", ptr(ids), n, int(self.rank == 0), ptr(self.map),
+                         ptr(self.slot_row), ptr(pre), ptr(self.E), ptr(self.Em), ptr(self.Ev), self.rows_local, d,
+                         self.lazy_window, ptr(self.last), ptr(self.sched), ptr(self.step_dev), self.wd_g,
+                         self.beta2, self.eps, *self._pend_args(), int(self.decoupled), st)
+                    _events_end(ev)
+                    side_pass()
+                sparse["claim_catchup"] = owner_claim_catchup
+            rows = self.xchg.forward(batch["item_id"], seq, self.E, sparse, self.err,
+                                     before_gather=catch_up if lazy else None)
             pos = self.xchg.cur_pos
             fwd_ev = torch.cuda.Event()
             _lib.record_event(fwd_ev, main)

@@ -348,6 +348,15 @@ int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, int D, const
  * batch by the previous step's fbn_adam_prefetch -- an entry whose tag is the current step takes
  * the claim from it without a CAS (the smallest entry index of each row claims); pass it only when
  * that prefetch was given this very batch. */
+/* N > 1 owner (the fixed-capacity exchange): claims of the received local rows lids [n] (negative =
+ * empty slot; skip0: rank 0's row 0 is padding) + the claimed-row catch-up in one launch; preclaim
+ * (optional): fbn_adam_prefetch_rows' tags for this very routing -- a row tagged for this step is
+ * claimed by its smallest slot without a CAS. */
+int fbn_adam_owner_claim_catchup(const int* lids, int n, int skip0, int* map, int* slot_row,
+                                 unsigned long long* preclaim, float* p, float* m, float* v, long long nrows, int D,
+                                 int F, int* last, const void* consts_table, const int* step, float wd, float beta2,
+                                 float eps, int* pend, const float* ring, const float* coef_hist, long long ring_stride,
+                                 int ring_n, int decoupled, void* stream);
 int fbn_adam_claim_catchup(const int64_t* item, const int64_t* seq, int B, int L, long long V, int* map, int* slot_row,
                            int* dup, int* hasdup, unsigned long long* preclaim, float* p, float* m, float* v,
                            long long nrows, int D, int F, int* last,
