@@ -19,4 +19,5 @@ for P in "${PS[@]}"; do
   rc=$?; echo "pass $i ($C) rc=$rc"; [ $rc -eq 0 ] || exit $rc
   DIRS="$DIRS $OUT/p$i"
 done
-cd $R && python tools/pmc_sq.py $OUT/summary.json $DIRS
+cd $R && python tools/pmc_sq.py $OUT/summary.json $DIRS && \
+for d in $DIRS; do gzip -f $d/run_counter_collection.csv; rm -f $d/run_kernel_trace.csv $d/*agent_info.csv; done

@@ -66,9 +66,9 @@ def main():
         d = {"kernel": name, "grid": grid, **{k: round(v, 3) for k, v in m.items()}}
         grbm = m.get("GRBM_GUI_ACTIVE", 0) / 8.0
         dur = m.get("duration_us", 0.0)
-        if grbm > 0 and dur > 0:
-            d["grbm_clock_ghz"] = round(grbm / (dur * 1e3), 3)
         cyc = dur * 1e3 * F_CLK_GHZ
+        if grbm > 0 and cyc > 0:
+            d["grbm_window_ratio"] = round(grbm / cyc, 3)
         if cyc > 0:
             d["cycles"] = round(cyc)
             if "SQ_VALU_MFMA_BUSY_CYCLES" in m:
@@ -82,7 +82,7 @@ def main():
     res.sort(key=lambda r: -r.get("duration_us", 0))
     json.dump(res, open(out, "w"), indent=1)
     for r in res[:30]:
-        extra = "  ".join(f"{k} {r[k]}" for k in ("duration_us", "grbm_clock_ghz", "mfma_busy", "mfma_tflops_at_busy",
+        extra = "  ".join(f"{k} {r[k]}" for k in ("duration_us", "mfma_busy", "mfma_tflops_at_busy",
                                                  "valu_issue", "SQ_INSTS_VALU", "hbm_bytes") if k in r)
         print(f"{r['kernel'][:60]:60s} grid {r['grid']:8d}  {extra}")
 
