@@ -1232,12 +1232,55 @@ __device__ __forceinline__ long long entry_row(const ClaimSrc& cs, long long i) 
   return (id > 0 && id < cs.V) ? id : -1;
 }
 
-__global__ void __launch_bounds__(256) adam_pretag_kernel(ClaimSrc cs, int n, const int* __restrict__ step) {
+// One block of FBN_PRETAG_BLOCK entries folds its claims in an LDS table first (id -> smallest
+// entry index, LDS atomics) and posts ONE global atomic max per distinct id: with Zipf ids the
+// hottest row takes ~9 % of a batch's entries, and one same-address atomic per entry serialised
+// ~15 K of them at one L2 channel (~100 us, stalling every stream's traffic through it).  The
+// posted value is the same maximum as per-entry posting: bit-identical pre-claims.
+#define FBN_PRETAG_BLOCK 1024
+#define FBN_PRETAG_SLOTS 2048   // open addressing, load factor <= 1/2
+static int pretag_flat() {
+  static const int f = getenv("FBN_PRETAG_FLAT") && atoi(getenv("FBN_PRETAG_FLAT")) == 1;
+  return f;
+}
+__global__ void __launch_bounds__(FBN_PRETAG_BLOCK) adam_pretag_kernel(ClaimSrc cs, int n,
+                                                                        const int* __restrict__ step, int flat) {
+  __shared__ int hkey[FBN_PRETAG_SLOTS];
+  __shared__ int hval[FBN_PRETAG_SLOTS];
+  for (int k = threadIdx.x; k < FBN_PRETAG_SLOTS; k += blockDim.x) {
+    hkey[k] = -1;
+    hval[k] = 0x7fffffff;
+  }
+  __syncthreads();
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  const long long id = i < n ? entry_row(cs, i) : -1;
+  if (flat) {   // A/B (FBN_PRETAG_FLAT=1): round 4's one global atomic per entry
+    if (id >= 0)
+      atomicMax(cs.pre + (size_t)id * FBN_RS_Q, ((unsigned long long)(*step + 1) << 32) | (0xFFFFFFFFull - (unsigned long long)i));
+    return;
+  }
+  if (id >= 0) {   // (local rows and entry indices fit 31 bits: V, n < 2^31)
+    unsigned h = ((unsigned)id * 2654435761u) >> (32 - 11);
+    for (;;) {
+      int cur = hkey[h];
+      if (cur == -1) {
+        const int prev = atomicCAS(&hkey[h], -1, (int)id);
+        cur = prev == -1 ? (int)id : prev;
+      }
+      if (cur == (int)id) {
+        atomicMin(&hval[h], (int)i);
+        break;
+      }
+      h = (h + 1) & (FBN_PRETAG_SLOTS - 1);
+    }
+  }
+  __syncthreads();
   const unsigned long long T = (unsigned long long)(*step + 1);
-  const long long id = entry_row(cs, i);
-  if (id >= 0) atomicMax(cs.pre + (size_t)id * FBN_RS_Q, (T << 32) | (0xFFFFFFFFull - (unsigned long long)i));
+  for (int k = threadIdx.x; k < FBN_PRETAG_SLOTS; k += blockDim.x) {
+    const int r = hkey[k];
+    if (r >= 0)
+      atomicMax(cs.pre + (size_t)r * FBN_RS_Q, (T << 32) | (0xFFFFFFFFull - (unsigned long long)(unsigned)hval[k]));
+  }
 }
 
 // adam_tab1 with the step's constants as (w1, nss, rbc2s, dmul): the same operations, same order
@@ -2524,7 +2567,8 @@ static int launch_prefetch_binned(const ClaimSrc& cs, long long n, float* p, flo
   int4* recs = (int4*)((char*)ws + (size_t)FBN_PFB_NB * FBN_PFB_NC * FBN_PFB_LINE * sizeof(unsigned));
   const int nblk = (int)((n + 255) / 256);
   fbn_launch(pfb_zero_kernel, dim3(1), dim3(256), 0, st, counts);
-  fbn_launch(adam_pretag_kernel, dim3(nblk), dim3(256), 0, st, cs, (int)n, step);
+  fbn_launch(adam_pretag_kernel, dim3((unsigned)((n + FBN_PRETAG_BLOCK - 1) / FBN_PRETAG_BLOCK)),
+             dim3(FBN_PRETAG_BLOCK), 0, st, cs, (int)n, step, pretag_flat());
   fbn_launch(adam_pfbin_kernel, dim3(nblk), dim3(256), 0, st, cs, (int)n, last, step, ps, counts, recs);
   // FBN_PFB_CHUNK: records per replay wave (A/B knob, read per call; 1 .. 64)
   const char* ce = getenv("FBN_PFB_CHUNK");
@@ -2599,7 +2643,8 @@ extern "C" int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B,
   static const bool onepass = getenv("FBN_PREFETCH_ONEPASS") && atoi(getenv("FBN_PREFETCH_ONEPASS")) == 1;
   if (preclaim && (!onepass || D < 128)) {
     const dim3 g2((unsigned)((n + 255) / 256));
-    fbn_launch(adam_pretag_kernel, g2, dim3(256), 0, st, cs, (int)n, step);
+    fbn_launch(adam_pretag_kernel, dim3((unsigned)((n + FBN_PRETAG_BLOCK - 1) / FBN_PRETAG_BLOCK)),
+               dim3(FBN_PRETAG_BLOCK), 0, st, cs, (int)n, step, pretag_flat());
     FBN_CHECK_LAUNCH();
     const char* ee = getenv("FBN_PF_EPW");   // A/B knob, read per call (tools/ab_step.py flips it in-process)
     const int epw = ee ? std::max(1, std::min(64, atoi(ee))) : 64;
@@ -2704,7 +2749,8 @@ extern "C" int fbn_adam_prefetch_rows(const int* lids, int n, int skip0, long lo
     // one rank).  The tags only decide this pass: the next step's owner claims do not read them.
     cs.pre = preclaim;
     const dim3 g2((unsigned)((n + 255) / 256));
-    fbn_launch(adam_pretag_kernel, g2, dim3(256), 0, st, cs, n, step);
+    fbn_launch(adam_pretag_kernel, dim3((unsigned)((n + FBN_PRETAG_BLOCK - 1) / FBN_PRETAG_BLOCK)),
+               dim3(FBN_PRETAG_BLOCK), 0, st, cs, n, step, pretag_flat());
     const int epw = 64;
     const dim3 g3((unsigned)(((n + epw - 1) / epw + 3) / 4));
     if (decoupled) {
