@@ -2270,6 +2270,71 @@ extern "C" int fbn_ring_slot(float* ring, int ring_n, long long stride, const in
   return FBN_OK;
 }
 
+// N > 1 owner, the fixed-capacity exchange: the widen into the ring slot and the duplicate fold in ONE
+// pass.  Received slot e (local row ids[e]; negative = empty, rank 0's row 0 = padding: skipped):
+// the claimer of its row (map[row] == e) stores its widened row into ring slot step % ring_n (its
+// address to *cell, as fbn_ring_slot); a duplicate adds its row into extra[claimer] (zero at rest)
+// and flags the claimer (FBN_SLOT_FLAG), as the single-GPU fold does -- the norm and the step tail
+// read claimer + extra (Lp1 | FBN_GRAD_CELL with extra), and a flagged claimer's step is applied at
+// the tail, which zeroes its extra row.  Rows [self_lo, self_lo + self_n) come from wire_self.
+template <int D>
+__global__ void __launch_bounds__(256) owner_fold_kernel(const int* __restrict__ ids, int n, int rank,
+                                                         const int* __restrict__ map, int* __restrict__ slot_row,
+                                                         const void* __restrict__ wire, int wire_bf16,
+                                                         const void* __restrict__ wire_self, long long self_lo,
+                                                         long long self_n, float* __restrict__ ring, int ring_n,
+                                                         long long stride, const int* __restrict__ step,
+                                                         float** __restrict__ cell, float* __restrict__ extra) {
+  constexpr int G = D / 4, RPW = 64 / G;
+  float* dst = ring + (size_t)(*step % ring_n) * stride;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *cell = dst;
+  const int lane = threadIdx.x & 63, q = lane % G;
+  const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+  for (long long e0 = gw * RPW; e0 < n; e0 += nw * RPW) {
+    const long long e = e0 + lane / G;
+    if (e >= n) continue;
+    const int r = ids[e];
+    if (r < 0 || (rank == 0 && r == 0)) continue;
+    const int u = map[r];
+    if (u < 0) continue;
+    const void* src = (wire_self && e >= self_lo && e < self_lo + self_n) ? wire_self : wire;
+    f32x4 x;
+    if (wire_bf16) {
+      const bf16x4 h = reinterpret_cast<const bf16x4*>(src)[(size_t)e * (D / 4) + q];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) x[k] = __uint_as_float((unsigned)(unsigned short)h[k] << 16);
+    } else {
+      x = reinterpret_cast<const f32x4*>(src)[(size_t)e * (D / 4) + q];
+    }
+    if (u == (int)e) {
+      reinterpret_cast<f32x4*>(dst)[(size_t)e * (D / 4) + q] = x;
+    } else {
+      if (q == 0) atomicOr(&slot_row[u], FBN_SLOT_FLAG);
+      float* ex = extra + (size_t)u * D + 4 * q;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) atomicAdd(ex + k, x[k]);
+    }
+  }
+}
+
+extern "C" int fbn_owner_fold(const int* ids, int n, int rank, const int* map, int* slot_row, const void* wire,
+                              int wire_bf16, const void* wire_self, long long self_lo, long long self_n, float* ring,
+                              int ring_n, long long stride, const int* step, void* cell, float* extra, int D,
+                              void* stream) {
+  if (n <= 0) return FBN_OK;
+  if (!ids || !map || !slot_row || !wire || !ring || !step || !cell || !extra || ring_n < 1 ||
+      (long long)n * D > stride || self_lo < 0 || self_n < 0 || (self_n > 0 && !wire_self)) {
+    fbn_set_error("fbn_owner_fold: ids, map, slot_row, wire, ring, step, cell, extra; n * D <= stride");
+    return FBN_ERR_ARG;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  FBN_DISPATCH_D(owner_fold_kernel, D, group_grid(n, D, 8192), ids, n, rank, map, slot_row, wire, wire_bf16,
+                 self_n > 0 ? wire_self : nullptr, self_lo, self_n, ring, ring_n, stride, step, (float**)cell, extra);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
 // gvec: single GPU per-sample vectors [B][2][D] (Lp1 = L+1) or owner per-entry rows [n][D] (Lp1 = 1)
 extern "C" int fbn_sparse_fixup(const int64_t* item, const int64_t* seq, const int* ids, int n, int L, long long V,
                                 int rank, const int* map, const float* gvec, float* extra, int* slot_row, int Lp1,

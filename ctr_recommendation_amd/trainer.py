@@ -112,6 +112,10 @@ _OWNER_PF2 = os.environ.get("FBN_OWNER_PF2", "1") != "0"
 # (fbn_adam_owner_claim_catchup, pre-claims from the owner prefetch); FBN_OWNER_CLAIM_FUSED=0 keeps
 # fbn_owner_claim + fbn_adam_catchup (A/B)
 _OWNER_CLAIM_FUSED = os.environ.get("FBN_OWNER_CLAIM_FUSED", "1") != "0"
+# ... and the widen into the ring slot + the duplicate fold in one pass (fbn_owner_fold; duplicates
+# summed in extra[claimer], applied at the tail); FBN_OWNER_FOLD=0 keeps fbn_ring_slot +
+# fbn_sparse_fixup (A/B)
+_OWNER_FOLD = os.environ.get("FBN_OWNER_FOLD", "1") != "0"
 from .schedule import OneCycle, adam_table
 
 TABLE = "item_emb.weight"
@@ -446,6 +450,7 @@ class FiBiNETTrainer:
         self._fc_steps = 0
         self.ring_cell = torch.zeros(2, dtype=torch.int64, device=dev)     # fbn_ring_slot's pointer cell
         self._fc_grad = None        # fixed-capacity rows, f32, when they are not deferred
+        self._fc_extra = None       # fixed-capacity form: duplicates' sums per claimer (zero at rest)
 
     # ------------------------------------------------------------------ one training step
     def step(self, batch: Dict[str, torch.Tensor], labels: torch.Tensor,
@@ -777,6 +782,7 @@ class FiBiNETTrainer:
             # slot when it fits, else a buffer of its own and the rows applied at the step end
             x = self.xchg
             n_ent = x.n_recv
+            fold_done = False
             if x.fc_active:
                 # fixed-capacity form: the rows arrive in the fixed wire buffer; deferred, they move
                 # into ring slot step % ring_n chosen on the device (a replayed step program gets the
@@ -785,18 +791,28 @@ class FiBiNETTrainer:
                 defer_now = self.deferred and n_ent <= self.ring_cap
                 # (this rank's own block was not sent: its rows are read from the send buffer itself)
                 lo, cnt = x.fc_self_rows
-                self_args = (ptr(x.fc_send) if cnt else None, lo * d, cnt * d)
+                if self._fc_extra is None or self._fc_extra.shape[0] < n_ent:
+                    self._fc_extra = torch.zeros((n_ent, d), dtype=torch.float32, device=self.device)
                 if defer_now:
-                    call("fbn_ring_slot", ptr(self.ring), self.ring_n, self._ring_stride(), ptr(self.step_dev),
-                         ptr(self.ring_cell), ptr(wire), int(wire.dtype == torch.bfloat16), n_ent * d, *self_args, st)
-                    gsrc = (self.ring_cell, None, 1 | FBN_GRAD_CELL)
+                    ring, ring_n, stride = self.ring, self.ring_n, self._ring_stride()
                 else:
                     if self._fc_grad is None or self._fc_grad.shape[0] < n_ent:
                         self._fc_grad = torch.empty((n_ent, d), dtype=torch.float32, device=self.device)
-                    grows = self._fc_grad[:n_ent]
-                    call("fbn_ring_slot", ptr(grows), 1, n_ent * d, ptr(self.step_dev), ptr(self.ring_cell), ptr(wire),
-                         int(wire.dtype == torch.bfloat16), n_ent * d, *self_args, st)
-                    gsrc = (grows, None, 1)
+                    ring, ring_n, stride = self._fc_grad, 1, n_ent * d
+                if _OWNER_FOLD:
+                    # the widen into the ring slot and the duplicate fold in one pass: a claimer's row is
+                    # stored, a duplicate's added into extra[claimer] (flagged; applied at the tail)
+                    call("fbn_owner_fold", ptr(x.recv_ids), n_ent, self.rank, ptr(self.map), ptr(self.slot_row),
+                         ptr(wire), int(wire.dtype == torch.bfloat16), ptr(x.fc_send) if cnt else None, lo, cnt,
+                         ptr(ring), ring_n, stride, ptr(self.step_dev), ptr(self.ring_cell), ptr(self._fc_extra), d,
+                         st)
+                    gsrc = (self.ring_cell, self._fc_extra, 1 | FBN_GRAD_CELL)
+                    fold_done = True
+                else:
+                    call("fbn_ring_slot", ptr(ring), ring_n, stride, ptr(self.step_dev), ptr(self.ring_cell),
+                         ptr(wire), int(wire.dtype == torch.bfloat16), n_ent * d, ptr(x.fc_send) if cnt else None,
+                         lo * d, cnt * d, st)
+                    gsrc = (self.ring_cell, None, 1 | FBN_GRAD_CELL)
             else:
                 slot = self._grad_slot()
                 defer_now = slot is not None
@@ -805,8 +821,9 @@ class FiBiNETTrainer:
                 else:
                     grows = x.backward(sendbuf, out=slot)
                 gsrc = (grows, None, 1)
-            call("fbn_sparse_fixup", None, None, ptr(x.recv_ids), n_ent, 0, self.V, self.rank, ptr(self.map),
-                 ptr(gsrc[0]), None, ptr(self.slot_row), gsrc[2], d, st)
+            if not fold_done:
+                call("fbn_sparse_fixup", None, None, ptr(x.recv_ids), n_ent, 0, self.V, self.rank, ptr(self.map),
+                     ptr(gsrc[0]), None, ptr(self.slot_row), gsrc[2], d, st)
         # clip_grad_norm_(10): dense grads (identical on every rank) + disjoint table shards
         tab_acc = self.sumsq_tab if self.sharded else self.sumsq
         dense_done = False

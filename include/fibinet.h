@@ -500,6 +500,16 @@ int fbn_owner_gather(const int* ids, int n, const float* E, void* out, int* map,
 int fbn_ring_slot(float* ring, int ring_n, long long stride, const int* step, void* cell, const void* wire,
                   int wire_bf16, long long n, const void* wire_self, long long self_lo, long long self_n,
                   void* stream);
+/* N > 1 owner, the fixed-capacity exchange: fbn_ring_slot + the duplicate fold in one pass.  Slot e
+ * (local row ids[e]; negative = empty; rank 0's row 0 = padding): the claimer of its row
+ * (map[row] == e) stores its widened row into ring slot (*step % ring_n) [stride floats per slot;
+ * *cell = its address]; a duplicate adds its row into extra[claimer] (zero at rest) and flags the
+ * claimer in slot_row (FBN_SLOT_FLAG).  Readers take (cell, extra, Lp1 = 1 | FBN_GRAD_CELL); the step
+ * tail applies flagged claimers at once and zeroes their extra rows.  Rows [self_lo, self_lo +
+ * self_n) come from wire_self (the caller's own block, never sent). */
+int fbn_owner_fold(const int* ids, int n, int rank, const int* map, int* slot_row, const void* wire, int wire_bf16,
+                   const void* wire_self, long long self_lo, long long self_n, float* ring, int ring_n,
+                   long long stride, const int* step, void* cell, float* extra, int D, void* stream);
 /* bf16 -> f32 (n % 8 == 0, 16-B aligned): the owner's received bf16 gradient rows (bf16 mode). */
 int fbn_widen_bf16(const void* in, float* out, long long n, void* stream);
 /* out [world][cap + 1]: out[o][j] = send_ids[offsets[o] + j] for j < counts[o], else -1, and
