@@ -62,6 +62,8 @@ def build(verbose: bool = True) -> str:
 VARIANTS = {
     # table and dense Adam with correctly rounded sqrt / division, unfused (parity bisection)
     "ieee": ("FBN_ADAM_IEEE",),
+    # the replay engine's constants one step at a time (round 4's form; A/B of FBN_REPLAY_BLOCK4)
+    "rstep1": ("FBN_REPLAY_BLOCK4=0",),
 }
 
 

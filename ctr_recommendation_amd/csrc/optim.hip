@@ -1319,6 +1319,9 @@ __device__ __forceinline__ void adam_tabk(typename FVec<N>::T& pp, typename FVec
 }
 __device__ __forceinline__ f32x4 consts4(const AdamConsts& k) { return (f32x4){k.w1, k.nss, k.rbc2s, k.dmul}; }
 
+#ifndef FBN_REPLAY_BLOCK4
+#define FBN_REPLAY_BLOCK4 1   // build-time A/B (build.py VARIANTS "rstep1": 0 = one step per constant load)
+#endif
 // One group of the replay engine: G wave-wide rows (cur, rows cr, replay starts ck, deferred
 // vectors cp; slots past cnt carry row 0 and no steps) brought to T, then stored.
 // ABL (measurement only, tools/pf_ablation.py): 1 = no arithmetic (rows loaded and stored as they
@@ -1351,6 +1354,49 @@ __device__ __forceinline__ void replay_group(WideRow<D> (&cur)[G], const int (&c
   // rows 0..k from ck[k] to ck[k+1] (ck[G] = T): the longest row never replays alone while a later
   // row could join it, and no step waits on its own constants' load.
   int s = ck[0] < T ? ck[0] : T;
+#if FBN_REPLAY_BLOCK4
+  // steps in blocks of four: the next block's four constant sets are loaded while this block runs,
+  // so a scalar-cache miss (every other step: 32-B records) is hidden behind four steps of the
+  // update chains instead of one; the partial last block of a phase uses the block's own sets
+#pragma unroll
+  for (int k = 0; k < G; ++k) {
+    const int send = k + 1 < G ? min(ck[k + 1], T) : T;
+    if (s >= send) continue;
+    f32x4 k0 = consts4(table[s]), k1 = consts4(table[min(s + 1, T)]), k2 = consts4(table[min(s + 2, T)]),
+          k3 = consts4(table[min(s + 3, T)]);
+    for (; s + 4 <= send; s += 4) {
+      const f32x4 n0 = consts4(table[min(s + 4, T)]), n1 = consts4(table[min(s + 5, T)]),
+                  n2 = consts4(table[min(s + 6, T)]), n3 = consts4(table[min(s + 7, T)]);
+#pragma unroll
+      for (int x = 0; x <= k; ++x) adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, zero, wd, b2, omb2, eps, k0);
+#pragma unroll
+      for (int x = 0; x <= k; ++x) adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, zero, wd, b2, omb2, eps, k1);
+#pragma unroll
+      for (int x = 0; x <= k; ++x) adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, zero, wd, b2, omb2, eps, k2);
+#pragma unroll
+      for (int x = 0; x <= k; ++x) adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, zero, wd, b2, omb2, eps, k3);
+      k0 = n0;
+      k1 = n1;
+      k2 = n2;
+      k3 = n3;
+    }
+    if (s < send) {
+#pragma unroll
+      for (int x = 0; x <= k; ++x) adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, zero, wd, b2, omb2, eps, k0);
+      ++s;
+    }
+    if (s < send) {
+#pragma unroll
+      for (int x = 0; x <= k; ++x) adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, zero, wd, b2, omb2, eps, k1);
+      ++s;
+    }
+    if (s < send) {
+#pragma unroll
+      for (int x = 0; x <= k; ++x) adam_tabk<DW, N>(cur[x].p, cur[x].m, cur[x].v, zero, wd, b2, omb2, eps, k2);
+      ++s;
+    }
+  }
+#else
   f32x4 kc = consts4(table[s]);   // table row T exists
 #pragma unroll
   for (int k = 0; k < G; ++k) {
@@ -1362,6 +1408,7 @@ __device__ __forceinline__ void replay_group(WideRow<D> (&cur)[G], const int (&c
       kc = kn;
     }
   }
+#endif
 #pragma unroll
   for (int x = 0; x < G; ++x)
     if (j0 + x < cnt && (ABL != 2 || sink)) wide_store<D>(cur[x], p, m, v, cr[x], lane);
