@@ -219,6 +219,35 @@ def recording() -> bool:
     return getattr(_tls, "prog", None) is not None
 
 
+def persistent(fn):
+    """fn() -- allocations that outlive the step (cached scratch, activation buffers, routing sets,
+    state grown on first use) -- made OUTSIDE a step program's recording pool.  The pool holds the
+    step's temporaries, whose blocks programs share once freed (steps never overlap); a buffer that
+    lives on and took such a block would be overwritten by every replay of the program that recorded
+    the temporary there.  Pool routing is per thread (torch.cuda.use_mem_pool), so while recording
+    fn runs on a helper thread, on the caller's current stream."""
+    prog = getattr(_tls, "prog", None)
+    if prog is None:
+        return fn()
+    stream = torch.cuda.current_stream(prog.device)
+    box = {}
+
+    def run():
+        try:
+            torch.cuda.set_device(prog.device)
+            with torch.cuda.stream(stream):
+                box["out"] = fn()
+        except BaseException as e:          # re-raised on the caller's thread
+            box["err"] = e
+
+    t = threading.Thread(target=run, name="fbn-persistent-alloc")
+    t.start()
+    t.join()
+    if "err" in box:
+        raise box["err"]
+    return box["out"]
+
+
 def wait_stream(dst, src) -> None:
     """dst.wait_stream(src), recorded as a stream edge while a step program is being recorded."""
     dst.wait_stream(src)

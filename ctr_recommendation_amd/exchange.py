@@ -266,11 +266,13 @@ class RowExchange:
                 self.fc_sets.pop(next(iter(self.fc_sets)))
             n = self.fc_slots
             i32 = dict(dtype=torch.int32, device=self.device)
-            st = {"send_ids": torch.empty(n, **i32), "recv_ids": torch.empty(n, **i32),
-                  "pos": torch.empty((self.B, self.L + 1), **i32), "stat": torch.zeros(_pad4(self.world + 1), **i32),
-                  "host": torch.zeros(_pad4(self.world + 1), dtype=torch.int32,
-                                      pin_memory=torch.device(self.device).type == "cuda"),
-                  "event": None, "key": key}
+            # (a set outlives the step that routes into it: never from a program's recording pool)
+            st = _lib.persistent(lambda: {
+                "send_ids": torch.empty(n, **i32), "recv_ids": torch.empty(n, **i32),
+                "pos": torch.empty((self.B, self.L + 1), **i32), "stat": torch.zeros(_pad4(self.world + 1), **i32),
+                "host": torch.zeros(_pad4(self.world + 1), dtype=torch.int32,
+                                    pin_memory=torch.device(self.device).type == "cuda"),
+                "event": None, "key": key})
             self.fc_sets[key] = st
         return st
 
@@ -527,7 +529,7 @@ class RowExchange:
     def _grow(self, buf, n):
         if buf is None or buf.shape[0] < n:
             cap = max(n, self.B * (self.L + 1))
-            buf = torch.empty((cap, self.d), dtype=self.row_dtype, device=self.device)
+            buf = _lib.persistent(lambda: torch.empty((cap, self.d), dtype=self.row_dtype, device=self.device))
         return buf
 
     def make_sendbuf(self) -> torch.Tensor:

@@ -140,7 +140,7 @@ def bf16_weight_jobs(p: Dict[str, torch.Tensor], d: int, a: Dict[str, torch.Tens
         key = "w16_" + name
         t = a.get(key)
         if t is None or tuple(t.shape) != (rows, cols):
-            t = torch.empty((rows, cols), dtype=torch.bfloat16, device=dev)
+            t = _lib.persistent(lambda: torch.empty((rows, cols), dtype=torch.bfloat16, device=dev))
             a[key] = t
         out[name] = t
         jobs[i] = _ConvJob(src.data_ptr(), t.data_ptr(), rows, cols, ld, trans, rm[0], rm[1], rm[2])
@@ -212,9 +212,10 @@ class DeferredSums:
         self.used.add(key)
         ws = self.cache.get(key) if self.cache is not None else None
         if ws is None or ws.numel() * 8 < nbytes:
-            ws = _ws(nbytes, out.device)
             if self.cache is not None:
-                self.cache[key] = ws
+                ws = self.cache[key] = _lib.persistent(lambda: _ws(nbytes, out.device))
+            else:
+                ws = _ws(nbytes, out.device)
         st = stream if stream is not None else _lib.stream_handle()
         if _WGRAD_GROUP and transA and not transB and A2 is None and M % 8 == 0 and N % 8 == 0:
             # deferred to flush(): the step's weight gradients in one fbn_gemm_slabs_group launch
@@ -348,14 +349,15 @@ def bn_backward(G, gvec, w, hact, scale, hpre, mean, invstd, gamma, B, C, ntot, 
     key = tag or str(C)
     ws = cache.get(f"bn_ws_{key}") if nws > 0 else None
     if nws > 0 and (ws is None or ws.numel() * 8 < nws):
-        ws = cache[f"bn_ws_{key}"] = _ws(nws, dev)
+        ws = cache[f"bn_ws_{key}"] = _lib.persistent(lambda: _ws(nws, dev))
     if coll.world <= 1:
         part = None
         if bias_grad is not None:
             nch = _lib.lib().fbn_bn_bwd_chunks(B, C)
             part = cache.get(f"bn_part_{key}")
             if part is None or tuple(part.shape) != (nch, C):
-                part = cache[f"bn_part_{key}"] = torch.empty((nch, C), dtype=torch.float32, device=dev)
+                part = cache[f"bn_part_{key}"] = _lib.persistent(
+                    lambda: torch.empty((nch, C), dtype=torch.float32, device=dev))
             sums.add(part, nch, C, bias_grad)
         call("fbn_bn_bwd_fused", ptr(G), ptr(gvec), ptr(w), ptr(hact), ptr(hact16), float(scale), ptr(hpre),
              ptr(mean), ptr(invstd), ptr(gamma), B, C, float(ntot), ptr(dpre), ptr(dpre16), ptr(dgamma), ptr(dbeta),
@@ -410,7 +412,7 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     def buf(name, shape, dtype=torch.float32):
         t = a.get(name)
         if t is None or tuple(t.shape) != tuple(shape):
-            t = torch.empty(shape, dtype=dtype, device=dev)
+            t = _lib.persistent(lambda: torch.empty(shape, dtype=dtype, device=dev))
             a[name] = t
         return t
 
@@ -453,9 +455,9 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
         # A/B variant: the batch's rows drawn >= _GATHER_HOT times are staged in LDS per workgroup
         hc = a.get("hot_cnt")
         if hc is None or hc.numel() != V:
-            hc = a["hot_cnt"] = torch.zeros(V, dtype=torch.int32, device=dev)
-            a["hot_list"] = torch.zeros(256, dtype=torch.int32, device=dev)
-            a["hot_n"] = torch.zeros(1, dtype=torch.int32, device=dev)
+            hc = a["hot_cnt"] = _lib.persistent(lambda: torch.zeros(V, dtype=torch.int32, device=dev))
+            a["hot_list"] = _lib.persistent(lambda: torch.zeros(256, dtype=torch.int32, device=dev))
+            a["hot_n"] = _lib.persistent(lambda: torch.zeros(1, dtype=torch.int32, device=dev))
         H = 8192 // d
         call("fbn_hot_rows", ptr(item_id), ptr(seq) if Lr else None, B, Lr, V, ptr(hc), ptr(a["hot_list"]),
              ptr(a["hot_n"]), H, _GATHER_HOT, 0, st)
@@ -645,7 +647,7 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
         # across steps, so a step allocates nothing (host time); stream order keeps reuse safe
         t = a.get("bwd_" + name)
         if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
-            t = torch.empty(shape, dtype=dtype, device=dev)
+            t = _lib.persistent(lambda: torch.empty(shape, dtype=dtype, device=dev))
             a["bwd_" + name] = t
         return t
 

@@ -115,6 +115,7 @@ _OWNER_CLAIM_FUSED = os.environ.get("FBN_OWNER_CLAIM_FUSED", "1") != "0"
 # ... and the widen into the ring slot + the duplicate fold in one pass (fbn_owner_fold; duplicates
 # summed in extra[claimer], applied at the tail); FBN_OWNER_FOLD=0 keeps fbn_ring_slot +
 # fbn_sparse_fixup (A/B)
+_SHARD_W16_SIDE = os.environ.get("FBN_SHARD_W16_SIDE", "1") != "0"
 _OWNER_FOLD = os.environ.get("FBN_OWNER_FOLD", "1") != "0"
 from .schedule import OneCycle, adam_table
 
@@ -645,7 +646,7 @@ class FiBiNETTrainer:
             # on the main stream ahead of the claims: a cross-queue wait inside a replayed graph
             # costs ~10 us, about what the conversion itself takes
             self.acts["w16"] = ops.bf16_weights(self.p, d, self.acts, st, x=batch["item_emb_d128"])
-        elif cfg.bf16 and not w16_late:
+        elif cfg.bf16 and not w16_late and (self.xchg is None or _SHARD_W16_SIDE):
             # (N > 1: beside the row exchange)
             w16_ev = start_w16()
         if self.xchg is not None:
@@ -792,12 +793,14 @@ class FiBiNETTrainer:
                 # (this rank's own block was not sent: its rows are read from the send buffer itself)
                 lo, cnt = x.fc_self_rows
                 if self._fc_extra is None or self._fc_extra.shape[0] < n_ent:
-                    self._fc_extra = torch.zeros((n_ent, d), dtype=torch.float32, device=self.device)
+                    self._fc_extra = _lib.persistent(
+                        lambda: torch.zeros((n_ent, d), dtype=torch.float32, device=self.device))
                 if defer_now:
                     ring, ring_n, stride = self.ring, self.ring_n, self._ring_stride()
                 else:
                     if self._fc_grad is None or self._fc_grad.shape[0] < n_ent:
-                        self._fc_grad = torch.empty((n_ent, d), dtype=torch.float32, device=self.device)
+                        self._fc_grad = _lib.persistent(
+                            lambda: torch.empty((n_ent, d), dtype=torch.float32, device=self.device))
                     ring, ring_n, stride = self._fc_grad, 1, n_ent * d
                 if _OWNER_FOLD:
                     # the widen into the ring slot and the duplicate fold in one pass: a claimer's row is
@@ -1009,14 +1012,18 @@ class FiBiNETTrainer:
         cap on every rank).  Grows the deferred-gradient ring (after bringing every row up to date,
         which clears the pending gradients it holds) and the claim slots when the blocks need more."""
         x = self.xchg
-        x.enable_fixed(cap)
+        _lib.persistent(lambda: x.enable_fixed(cap))
         n = x.fc_slots
         if n > self.slot_row.numel():
-            self.slot_row = torch.full((n,), -1, dtype=torch.int32, device=self.device)
+            self.slot_row = _lib.persistent(lambda: torch.full((n,), -1, dtype=torch.int32, device=self.device))
         if self.deferred and n > self.ring_cap:
             self.flush()
             self.ring_cap = n
-            self.ring = torch.zeros((self.ring_n, n, self.d), dtype=torch.float32, device=self.device)
+            self.ring = _lib.persistent(
+                lambda: torch.zeros((self.ring_n, n, self.d), dtype=torch.float32, device=self.device))
+        # the duplicate fold's sums per claimer (zero at rest), made here rather than inside a step
+        if self._fc_extra is None or self._fc_extra.shape[0] < n:
+            self._fc_extra = _lib.persistent(lambda: torch.zeros((n, self.d), dtype=torch.float32, device=self.device))
         self.fc_wanted = False
 
     def _ring_stride(self) -> int:

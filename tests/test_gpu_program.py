@@ -112,6 +112,25 @@ def test_program_refuses_rewritten_batch(hip_device):
         tr.run_program(p2)
 
 
+def test_persistent_allocation_escapes_recording_pool(hip_device):
+    """A buffer that outlives the step, first allocated while a step is recorded, must not take a
+    block of the program's pool: a temporary the recording freed there is rewritten by every replay
+    (the sharded step's duplicate-fold buffer did, and every replay of its program clobbered it)."""
+    from ctr_recommendation_amd import _lib
+    prog = _lib.StepProgram(hip_device)
+    pool = torch.cuda.MemPool()
+    n = 1 << 20
+    with prog.recording(pool):
+        tmp = torch.empty(n, device=hip_device)
+        addr = tmp.data_ptr()
+        del tmp                                            # freed into the pool
+        kept = _lib.persistent(lambda: torch.zeros(n, device=hip_device))
+        again = torch.empty(n, device=hip_device)          # a temporary takes the freed block back
+    assert kept.data_ptr() != addr and again.data_ptr() == addr, (hex(kept.data_ptr()), hex(addr))
+    torch.cuda.synchronize()
+    assert float(kept.abs().max()) == 0.0
+
+
 def test_program_refuses_unsupported_paths(hip_device):
     cfg = {"embedding_dim": 16, "vocab_size": 3000}
     torch.manual_seed(0)

@@ -134,6 +134,8 @@ def test_sharded_step_program_matches_eager_with_overflow_fallback(hip_device, d
     # the two runs part in the last bits from the first float-atomic fold on, and Adam amplifies it
     # (measured: 6e-8 at step 5, ~8e-5 by step 11, ~1e-3 by step 23): 1e-5 up to the first
     # parting, 5e-3 to the end
-    assert max(diffs[:6]) <= 1e-5 and max(diffs) <= 5e-3, [f"{x:.1e}" for x in diffs]
+    worst = max(range(len(diffs)), key=lambda k: diffs[k])
+    print(f"[{dtype}] max loss diff {max(diffs):.3g} (first 6: {max(diffs[:6]):.3g}), de {res['de']:.3g}, dp {res['dp']:.3g}")
+    assert max(diffs[:6]) <= 1e-5 and max(diffs) <= 5e-3, (worst, " ".join(f"{a:.5f}/{b:.5f}" for a, b in zip(le, lp)))
     assert res["de"] <= 5e-2, res["de"]
     assert res["dp"] <= 5e-2, res["dp"]
