@@ -9,9 +9,11 @@ history is rewritten in place (through the library, so the tensors keep their ve
 the programs stay valid) with full histories that overflow the calibrated block capacity: both
 trainers must read the routed-ahead overflow flag and run that step with host split sizes (the
 program trainer falls back to an eager step for it), and the replays after it go on.  The duplicate
-fold's float atomics and the routing's round order make two sharded runs part in the last bits, which
-Adam amplifies over the 23 steps: losses agree within 1e-5 (relative) until they first part and 5e-3
-to the end, the tables (after the flush) and the dense parameters within 5e-2 of their displacement -- a wrong row or a lost gradient shows at once, far above these.
+fold's float atomics can part two fp32 runs in the last bits (measured: 6e-8 in the loss, 3e-7 / 1e-5
+of the table / dense displacement; bf16 bit-identical): losses within 1e-6 (relative), the tables
+(after the flush) within 1e-4 and the dense parameters within 1e-3 of their displacement.  (Under
+tolerances of 5e-3 / 5e-2 this test once passed in fp32 over a program whose every replay clobbered
+the fold buffer: a loose bar here hides real bugs.)
 """
 import ctypes
 import os
@@ -131,11 +133,8 @@ def test_sharded_step_program_matches_eager_with_overflow_fallback(hip_device, d
     assert res["fallbacks"] == (2, 2), res["fallbacks"]
     le, lp = res["losses"]
     diffs = [abs(a - b) / max(1.0, abs(a)) for a, b in zip(le, lp)]
-    # the two runs part in the last bits from the first float-atomic fold on, and Adam amplifies it
-    # (measured: 6e-8 at step 5, ~8e-5 by step 11, ~1e-3 by step 23): 1e-5 up to the first
-    # parting, 5e-3 to the end
     worst = max(range(len(diffs)), key=lambda k: diffs[k])
-    print(f"[{dtype}] max loss diff {max(diffs):.3g} (first 6: {max(diffs[:6]):.3g}), de {res['de']:.3g}, dp {res['dp']:.3g}")
-    assert max(diffs[:6]) <= 1e-5 and max(diffs) <= 5e-3, (worst, " ".join(f"{a:.5f}/{b:.5f}" for a, b in zip(le, lp)))
-    assert res["de"] <= 5e-2, res["de"]
-    assert res["dp"] <= 5e-2, res["dp"]
+    print(f"[{dtype}] max loss diff {max(diffs):.3g}, de {res['de']:.3g}, dp {res['dp']:.3g}")
+    assert max(diffs) <= 1e-6, (worst, " ".join(f"{a:.5f}/{b:.5f}" for a, b in zip(le, lp)))
+    assert res["de"] <= 1e-4, res["de"]
+    assert res["dp"] <= 1e-3, res["dp"]
