@@ -35,6 +35,7 @@ SIGNATURES = {
     "fbn_gemm": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, I, I, F, I, I, I, P, P, SZ, P]),
     "fbn_gemm_split": (I, [P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, F, P, P, SZ, P, I, I, P, I, I, P]),
     "fbn_gemm_bf16out": (I, [P, P, P, I, I, I, I, I, I, I, I, P]),
+    "fbn_gemm_s3": (I, [P, P, P, I, I, I, I, I, I, I, I, LL, LL, F, P, SZ, P]),
     "fbn_gemm_bn_bwd_part_supported": (I, [I, I, I, I, I, I, I]),
     "fbn_gemm_bn_bwd_part": (I, [P, P, P, I, I, I, I, I, I, I, I, P, P, P, F, P, P]),
     "fbn_bn_tile_stats": (I, [P, I, I, P, P, P]),

@@ -6,21 +6,54 @@
 
 // part: 0 = the value rounded to bf16 ("hi"), 1 = the rounding residual x - hi rounded to bf16 ("lo"):
 // hi + lo carries 16 significant bits of x (the split-bf16 images of the bf16_fwd backward GEMMs);
+// 2 = both images from one read, lo pst elements past hi (the operands of fbn_gemm_s3 and the
+// split-bf16 x3 slab GEMMs, which read A_hi B_hi + A_hi B_lo + A_lo B_hi from them);
 // dld: the destination's row stride in elements (0 = cols), so images can be laid side by side
+__device__ __forceinline__ short conv_bf(float x, int part) {
+  const short h = f2bf(x);
+  return part ? f2bf(x - bf2f(h)) : h;
+}
 struct ConvJob {
   const float* src;
   short* dst;
-  int rows, cols, ld, trans, seg, off0, off1, part, dld;
+  int rows, cols, ld, trans, seg, off0, off1, part, dld, pst;
 };
+// the images of four consecutive outputs: one 8-B store each (vec) or element stores
+__device__ __forceinline__ void conv_store4(short* d, const f32x4& x, int part, int pst, int n, bool vec) {
+  if (part < 2) {
+    if (vec) {
+      *reinterpret_cast<bf16x4*>(d) = (bf16x4){conv_bf(x[0], part), conv_bf(x[1], part), conv_bf(x[2], part),
+                                               conv_bf(x[3], part)};
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (e < n) d[e] = conv_bf(x[e], part);
+    }
+    return;
+  }
+  bf16x4 hi, lo;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    hi[e] = f2bf(x[e]);
+    lo[e] = f2bf(x[e] - bf2f(hi[e]));
+  }
+  if (vec) {
+    *reinterpret_cast<bf16x4*>(d) = hi;
+    *reinterpret_cast<bf16x4*>(d + pst) = lo;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (e < n) {
+        d[e] = hi[e];
+        d[e + pst] = lo[e];
+      }
+  }
+}
 #define FBN_CONV_MAX 16
 struct ConvJobs {
   ConvJob j[FBN_CONV_MAX];
   int tile0[FBN_CONV_MAX + 1];   // first 64x64 output tile of each job (prefix sum)
 };
-__device__ __forceinline__ short conv_bf(float x, int part) {
-  const short h = f2bf(x);
-  return part ? f2bf(x - bf2f(h)) : h;
-}
 // One 64x64 output tile per workgroup, four consecutive outputs per thread (one 8-B bf16x4 store):
 // a plain job reads four source columns at once (16-B load when they are contiguous and aligned:
 // the remap offsets and seg are multiples of 4); a transposed job reads its source tile along the
@@ -57,19 +90,12 @@ __device__ __forceinline__ void convert_tile(const ConvJobs& jobs, int njobs, in
         }
       }
     }
+    const bool vst = full && !(dld & 3) && !(J.pst & 3);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int i = i0 + tr + 16 * k;
       if (i >= J.rows) continue;
-      short* d = J.dst + (size_t)i * dld + j;
-      if (full && !(dld & 3)) {
-        *reinterpret_cast<bf16x4*>(d) = (bf16x4){conv_bf(val[k][0], J.part), conv_bf(val[k][1], J.part),
-                                                 conv_bf(val[k][2], J.part), conv_bf(val[k][3], J.part)};
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (j + e < J.cols) d[e] = conv_bf(val[k][e], J.part);
-      }
+      conv_store4(J.dst + (size_t)i * dld + j, val[k], J.part, J.pst, J.cols - j, vst);
     }
     return;
   }
@@ -88,20 +114,13 @@ __device__ __forceinline__ void convert_tile(const ConvJobs& jobs, int njobs, in
   const int j = j0 + 4 * tq;
   if (j >= J.cols) return;
   const int dld = J.dld ? J.dld : J.cols;
+  const bool vst = j + 4 <= J.cols && !(dld & 3) && !(J.pst & 3);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int r = tr + 16 * k, i = i0 + r;
     if (i >= J.rows) continue;
-    short* d = J.dst + (size_t)i * dld + j;
-    const bf16x4 v = {conv_bf(tile[4 * tq][r], J.part), conv_bf(tile[4 * tq + 1][r], J.part),
-                      conv_bf(tile[4 * tq + 2][r], J.part), conv_bf(tile[4 * tq + 3][r], J.part)};
-    if (j + 4 <= J.cols && !(dld & 3)) {
-      *reinterpret_cast<bf16x4*>(d) = v;
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (j + e < J.cols) d[e] = v[e];
-    }
+    const f32x4 x = {tile[4 * tq][r], tile[4 * tq + 1][r], tile[4 * tq + 2][r], tile[4 * tq + 3][r]};
+    conv_store4(J.dst + (size_t)i * dld + j, x, J.part, J.pst, J.cols - j, vst);
   }
 }
 

@@ -57,6 +57,11 @@ struct GemmArgs {
   const void* A2;
   const void* B2;
   int lda2, kseg, ldb2, nseg;
+  // split-bf16 x3 (LDS-DMA kernel, S3 instantiations): K = 3 s3k0 in three K-segments; segment s of A
+  // reads its hi image (s < 2) or its lo image (s == 2, s3_loa elements past hi), of B hi (s != 1)
+  // or lo (s == 1, s3_lob past hi): C = A_hi B_hi + A_hi B_lo + A_lo B_hi from two images each
+  int s3k0;
+  long long s3_loa, s3_lob;
   int c16;      // C is bf16 (short*, ldc in elements): split == 1, no stats / beta (fbn_gemm_bf16out)
   // BatchNorm backward first pass fused into a dgrad epilogue (fbn_gemm_bn_bwd_part): C is the
   // gradient G wrt the BN output's activation; per row chunk of bnb_rpc rows (one wave's rows) and
@@ -652,7 +657,7 @@ __device__ __forceinline__ int xcd_tile(int bid, int nb) {
 // WGM x WGN waves (64 * WGM * WGN threads); wave (wm, wn) owns a (BM/WGM) x (BN/WGN) sub-tile
 // of 32x32 MFMA blocks.  8 waves on a 128x128 tile: two waves per SIMD, each with 2 MFMAs per
 // 3 fragment reads (4 waves on 64x64 tiles: 1 MFMA per 2 reads).
-template <int BM, int BN, bool AKM, bool BKM, int S, int WGM = 2, int WGN = 2>
+template <int BM, int BN, bool AKM, bool BKM, int S, int WGM = 2, int WGN = 2, bool S3 = false>
 __device__ __forceinline__ void gemm_dma16_tile(const GemmArgs& g, int m0, int n0, int z, bool split) {
   constexpr int NW = WGM * WGN;
   constexpr int BK = 64;
@@ -677,6 +682,8 @@ __device__ __forceinline__ void gemm_dma16_tile(const GemmArgs& g, int m0, int n
   const short* src[GPW];
   const short* src2[GPW];   // split A ([A | A2] along K): the same lane's chunk in A2, k rebased to kseg
   long long adv[GPW];
+  long long loff[GPW];      // S3: the lo image's offset, read in K-segment sel[j]
+  int sel[GPW];
   const int t2 = kbeg < g.kseg ? (g.kseg - kbeg) / BK : 0;   // first K-step read from A2
 #pragma unroll
   for (int j = 0; j < GPW; ++j) {
@@ -688,10 +695,17 @@ __device__ __forceinline__ void gemm_dma16_tile(const GemmArgs& g, int m0, int n
     const bool km = isA ? AKM : BKM;
     const int rows = isA ? BM : BN;
     src2[j] = nullptr;
+    loff[j] = isA ? g.s3_loa : g.s3_lob;
+    sel[j] = isA ? 2 : 1;
     if (!km) {
       const int r = off >> 7, slot = (off >> 4) & 7;
       const int row = min(base + r, lim - 1);
       const int sw = (slot ^ ((r >> 1) & 7)) << 3;
+      if constexpr (S3) {   // k = 0 of the hi image; per element of k
+        src[j] = P + (size_t)row * ld + sw;
+        adv[j] = 1;
+        continue;
+      }
       src[j] = P + (size_t)row * ld + kbeg + sw;
       if (isA && g.A2) src2[j] = reinterpret_cast<const short*>(g.A2) + (size_t)row * g.lda2 + (kbeg - g.kseg) + sw;
       adv[j] = BK;
@@ -707,11 +721,27 @@ __device__ __forceinline__ void gemm_dma16_tile(const GemmArgs& g, int m0, int n
       const int f = RB == 128 ? (((k >> 1) & 1) << 2) : ((k & 3) << 2);
       int col = base + ((slot ^ f) << 3);
       if (col + 8 > lim) col = 0;
+      if constexpr (S3) {
+        src[j] = P + (size_t)k * ld + col;
+        adv[j] = ld;
+        continue;
+      }
       src[j] = P + (size_t)(kbeg + k) * ld + col;
       adv[j] = (long long)BK * ld;
     }
   }
   auto issue = [&](int t, int buf) {
+    if constexpr (S3) {
+      // K-step t reads k' = kbeg + t BK in segment s = k' / s3k0 (BK never straddles one)
+      const int kk = kbeg + t * BK, s = kk / g.s3k0, kl = kk - s * g.s3k0;
+#pragma unroll
+      for (int j = 0; j < GPW; ++j) {
+        const short* s0 = src[j] + (s == sel[j] ? loff[j] : 0) + (long long)kl * adv[j];
+        __builtin_amdgcn_global_load_lds((g_void*)s0, (l_void*)(smem + buf * STAGE + (wave * GPW + j) * 1024), 16, 0,
+                                         0);
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < GPW; ++j) {
       const short* s0 = (src2[j] && t >= t2) ? src2[j] : src[j];
@@ -770,14 +800,14 @@ __device__ __forceinline__ void gemm_dma16_tile(const GemmArgs& g, int m0, int n
   gemm_epilogue<BM, BN, WGM, WGN>(g, acc, m0, n0, wm, wn, lr, lh, reinterpret_cast<float*>(smem), split, z);
 }
 
-template <int BM, int BN, bool AKM, bool BKM, int S, int WGM = 2, int WGN = 2>
+template <int BM, int BN, bool AKM, bool BKM, int S, int WGM = 2, int WGN = 2, bool S3 = false>
 __global__ void __launch_bounds__(64 * WGM * WGN) gemm_dma16_kernel(GemmArgs g, int tiles_n, int remap_xcd) {
   FBN_MAIN_PRIO();
   int bid = blockIdx.x;
   const int nb = gridDim.x;
   if (remap_xcd) bid = xcd_tile(bid, nb);
   const int tm = bid / tiles_n, tn = bid % tiles_n;
-  gemm_dma16_tile<BM, BN, AKM, BKM, S, WGM, WGN>(g, tm * BM, tn * BN, blockIdx.z, gridDim.z > 1);
+  gemm_dma16_tile<BM, BN, AKM, BKM, S, WGM, WGN, S3>(g, tm * BM, tn * BN, blockIdx.z, gridDim.z > 1);
 }
 
 // Several slab-mode GEMMs (fbn_gemm_slabs_group: the step's weight gradients) in ONE launch: the
@@ -792,7 +822,7 @@ struct GemmGroup {
   int n;
   int remap;   // XCD-aware block order (FBN_GROUP_XCD=0: dispatch order, A/B)
 };
-template <int BM, int BN, bool AKM, bool BKM, int S, int WGM, int WGN>
+template <int BM, int BN, bool AKM, bool BKM, int S, int WGM, int WGN, bool S3 = false>
 __global__ void __launch_bounds__(64 * WGM * WGN) gemm_dma16_group_kernel(GemmGroup G) {
   FBN_MAIN_PRIO();
   // XCD-aware order over the whole flat grid: each XCD runs a contiguous run of (problem, slab,
@@ -807,7 +837,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_dma16_group_kernel(GemmGr
   const int local = b - G.start[p];
   const int z = local / G.tiles[p], t = local - z * G.tiles[p];
   const int tm = t / G.tiles_n[p], tn = t - tm * G.tiles_n[p];
-  gemm_dma16_tile<BM, BN, AKM, BKM, S, WGM, WGN>(G.g[p], tm * BM, tn * BN, z, true);
+  gemm_dma16_tile<BM, BN, AKM, BKM, S, WGM, WGN, S3>(G.g[p], tm * BM, tn * BN, z, true);
 }
 
 // vectorised split-K reduce: 4 consecutive columns per thread (N, ldc and the C remap in
@@ -993,6 +1023,10 @@ static void launch_dma16(const GemmArgs& g, const GemmPlan& p, hipStream_t st) {
   const char* e = getenv("FBN_GEMM_STAGES");   // tuning knob
   const int S = e ? atoi(e) : (p.stages ? p.stages : FBN_DMA_STAGES);
   const dim3 grid(nb, 1, p.split), blk(64 * WGM * WGN);
+  if (g.s3k0) {   // split-bf16 x3 over two images per operand (two-stage ring only)
+    fbn_launch((gemm_dma16_kernel<BM, BN, AKM, BKM, 2, WGM, WGN, true>), grid, blk, 0, st, g, tn, rx);
+    return;
+  }
   if (S <= 2)
     fbn_launch((gemm_dma16_kernel<BM, BN, AKM, BKM, 2, WGM, WGN>), grid, blk, 0, st, g, tn, rx);
   else if (S == 3)
@@ -1059,7 +1093,8 @@ static int gemm_impl(const void* A, const void* B, float* C, const float* bias, 
                      int ldb, int ldc, int transA, int transB, int rB_seg, int rB_off0, int rB_off1, int rC_seg,
                      int rC_off0, int rC_off1, float beta, int bf16, int a16, int b16, float* stats, float* ws,
                      size_t ws_bytes, const void* A2, int lda2, int kseg, const void* B2, int ldb2, int nseg,
-                     void* stream, int c16 = 0, const GemmArgs* bnb = nullptr, int* slabs = nullptr);
+                     void* stream, int c16 = 0, const GemmArgs* bnb = nullptr, int* slabs = nullptr,
+                     const long long* s3 = nullptr);
 
 extern "C" int fbn_gemm(const void* A, const void* B, float* C, const float* bias, int M, int N, int K, int lda,
                         int ldb, int ldc, int transA, int transB, int rB_seg, int rB_off0, int rB_off1, int rC_seg,
@@ -1094,6 +1129,18 @@ extern "C" int fbn_gemm_bf16out(const void* A, const void* B, void* C, int M, in
   return gemm_impl(A, B, reinterpret_cast<float*>(C), nullptr, M, N, K, lda, ldb, ldc, transA, transB, 0x7fffffff, 0, 0,
                    0x7fffffff, 0, 0, 0.f, 1, 1, 1, nullptr, nullptr, 0, nullptr, 0, 0x7fffffff, nullptr, 0, 0x7fffffff,
                    stream, 1);
+}
+
+// Split-bf16 x3 (the bf16_fwd backward): C = beta C + A_hi B_hi + A_hi B_lo + A_lo B_hi, as ONE bf16
+// GEMM over K = 3 K0 on the LDS-DMA path; A / B point at the hi image, their lo image lies lo_a /
+// lo_b elements further (same layout): hi + lo carry 16 significant bits of each fp32 operand.
+extern "C" int fbn_gemm_s3(const void* A, const void* B, float* C, int M, int N, int K0, int lda, int ldb, int ldc,
+                           int transA, int transB, long long lo_a, long long lo_b, float beta, float* ws,
+                           size_t ws_bytes, void* stream) {
+  const long long s3[3] = {K0, lo_a, lo_b};
+  return gemm_impl(A, B, C, nullptr, M, N, 3 * K0, lda, ldb, ldc, transA, transB, 0x7fffffff, 0, 0, 0x7fffffff, 0, 0,
+                   beta, 1, 1, 1, nullptr, ws, ws_bytes, nullptr, 0, 0x7fffffff, nullptr, 0, 0x7fffffff, stream, 0,
+                   nullptr, nullptr, s3);
 }
 
 // Slab mode (bf16 LDS-DMA path; the wgrad GEMMs of the trainer): op(A) op(B) with the split-K
@@ -1150,7 +1197,8 @@ struct FbnSlabGemm {   // one record of fbn_gemm_slabs_group (include/fibinet.h)
   size_t ws_bytes;
   const void* A2;
   const void* B2;
-  int M, N, K, lda, ldb, transA, transB, lda2, kseg, ldb2, nseg, pad;
+  int M, N, K, lda, ldb, transA, transB, lda2, kseg, ldb2, nseg, s3k0;
+  long long lo_a, lo_b;   // s3k0 > 0: split-bf16 x3 (GemmArgs::s3k0), K = 3 s3k0
 };
 extern "C" int fbn_gemm_slabs_group(const void* descs, int n, void* stream) {
   const FbnSlabGemm* d = static_cast<const FbnSlabGemm*>(descs);
@@ -1168,10 +1216,13 @@ extern "C" int fbn_gemm_slabs_group(const void* descs, int n, void* stream) {
                     !(x.lda & 7) && !(x.ldb & 7) && !(x.M & 7) && !(x.N & 7) && !((uintptr_t)x.A & 15) &&
                     !((uintptr_t)x.B & 15) && !x.A2 &&
                     (!x.B2 || (!(x.nseg & 127) && !(x.ldb2 & 7) && !((uintptr_t)x.B2 & 15))) &&
-                    x.ws_bytes >= (size_t)group_split(x.M, x.N, x.K) * x.M * x.N * sizeof(float);
+                    x.ws_bytes >= (size_t)group_split(x.M, x.N, x.K) * x.M * x.N * sizeof(float) &&
+                    (x.s3k0 == 0 || (!(x.s3k0 & 63) && x.K == 3 * x.s3k0 && !x.B2 && !(x.lo_a & 7) && !(x.lo_b & 7))) &&
+                    (x.s3k0 > 0) == (d[0].s3k0 > 0);
     if (!ok) {
       fbn_set_error("fbn_gemm_slabs_group: each problem needs transA = 1, transB = 0, K % 64 == 0, M, N, ld % 8 == 0, "
-                    "16-B aligned operands, no A2, ws >= fbn_gemm_slabs_size");
+                    "16-B aligned operands, no A2, ws >= fbn_gemm_slabs_size; split-bf16 x3 (s3k0 > 0) on every "
+                    "problem or none, K = 3 s3k0, s3k0 % 64 == 0, no B2");
       return FBN_ERR_ARG;
     }
     const double f = (double)x.M * x.N * x.K;
@@ -1192,6 +1243,7 @@ extern "C" int fbn_gemm_slabs_group(const void* descs, int n, void* stream) {
     g.beta = 0.f;
     g.A2 = nullptr; g.lda2 = 0; g.kseg = 0x7fffffff;
     g.B2 = x.B2; g.ldb2 = x.ldb2; g.nseg = x.B2 ? x.nseg : 0x7fffffff;
+    g.s3k0 = x.s3k0; g.s3_loa = x.lo_a; g.s3_lob = x.lo_b;
     g.c16 = 0;
     g.bnb_hact16 = nullptr; g.bnb_xpre = nullptr; g.bnb_mean = nullptr; g.bnb_scale = 1.f; g.bnb_part = nullptr;
     g.bnb_rpc = 1;
@@ -1207,7 +1259,13 @@ extern "C" int fbn_gemm_slabs_group(const void* descs, int n, void* stream) {
   G.start[n] = (int)total;
   hipStream_t st = (hipStream_t)stream;
   const char* se = getenv("FBN_GROUP_STAGES");   // A/B knob: LDS-DMA ring depth of the group (2 or 3)
-  if (wide && se && atoi(se) == 3)
+  if (d[0].s3k0 && wide)
+    fbn_launch((gemm_dma16_group_kernel<128, 128, true, true, 2, 2, 4, true>), dim3((unsigned)total), dim3(512), 0,
+                       st, G);
+  else if (d[0].s3k0)
+    fbn_launch((gemm_dma16_group_kernel<64, 64, true, true, 2, 2, 2, true>), dim3((unsigned)total), dim3(256), 0,
+                       st, G);
+  else if (wide && se && atoi(se) == 3)
     fbn_launch((gemm_dma16_group_kernel<128, 128, true, true, 3, 2, 4>), dim3((unsigned)total), dim3(512), 0,
                        st, G);
   else if (wide)
@@ -1224,7 +1282,7 @@ static int gemm_impl(const void* A, const void* B, float* C, const float* bias, 
                      int ldb, int ldc, int transA, int transB, int rB_seg, int rB_off0, int rB_off1, int rC_seg,
                      int rC_off0, int rC_off1, float beta, int bf16, int a16, int b16, float* stats, float* ws,
                      size_t ws_bytes, const void* A2, int lda2, int kseg, const void* B2, int ldb2, int nseg,
-                     void* stream, int c16, const GemmArgs* bnb, int* slabs) {
+                     void* stream, int c16, const GemmArgs* bnb, int* slabs, const long long* s3) {
   if (slabs) *slabs = 0;
   if (M <= 0 || N <= 0) return FBN_OK;
   if (!A || !B || !C) { fbn_set_error("fbn_gemm: null operand"); return FBN_ERR_ARG; }
@@ -1250,6 +1308,9 @@ static int gemm_impl(const void* A, const void* B, float* C, const float* bias, 
   g.beta = beta;
   g.A2 = A2; g.lda2 = lda2; g.kseg = kseg;
   g.B2 = B2; g.ldb2 = ldb2; g.nseg = nseg;
+  g.s3k0 = s3 ? (int)s3[0] : 0;
+  g.s3_loa = s3 ? s3[1] : 0;
+  g.s3_lob = s3 ? s3[2] : 0;
   g.c16 = c16;
   g.bnb_hact16 = bnb ? bnb->bnb_hact16 : nullptr;
   g.bnb_xpre = bnb ? bnb->bnb_xpre : nullptr;
@@ -1264,6 +1325,12 @@ static int gemm_impl(const void* A, const void* B, float* C, const float* bias, 
                      (!transA ? true : !(M & 7)) && (transB ? true : !(N & 7)) && !getenv("FBN_GEMM_NO_DMA16");
   if ((A2 || B2) && !dma16) {
     fbn_set_error("fbn_gemm_split: split operands need the bf16 LDS-DMA path (K % 64 == 0, bf16 operands)");
+    return FBN_ERR_ARG;
+  }
+  if (s3 && (!dma16 || A2 || B2 || c16 || bnb || stats || (s3[0] & 63) || K != 3 * s3[0] || (s3[1] & 7) ||
+             (s3[2] & 7))) {
+    fbn_set_error("fbn_gemm_s3: needs the bf16 LDS-DMA path (K0 % 64 == 0, ld % 8, k-major extents % 8), image "
+                  "offsets % 8, no split operands / stats");
     return FBN_ERR_ARG;
   }
   GemmPlan p = dma16 ? plan_dma16(M, N, K) : plan_gemm(M, N, K, bk);

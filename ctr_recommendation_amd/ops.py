@@ -37,6 +37,10 @@ BN_MOMENTUM = 0.1
 _BN2_BWD_IN_FWD = os.environ.get("FBN_BN2_BWD_IN_FWD", "1") == "1"
 # bf16_fwd: the backward's fp32 GEMMs as split-bf16 x3 (fbn_gemm bf16 = 2) with FBN_SPLIT_BWD=1 (A/B knob)
 _SPLIT_BWD = os.environ.get("FBN_SPLIT_BWD", "0") == "1"
+# bf16_fwd: the backward's GEMMs as ONE bf16 GEMM over 3 K each, on split operand images made once
+# (fbn_convert_bf16 part 2 / 3: [hi, hi, lo] x [hi, lo, hi]) -- the LDS-DMA bf16 path instead of the
+# fp32 MFMA (FBN_SPLIT3=0: fp32 MFMA, A/B)
+_SPLIT3 = os.environ.get("FBN_SPLIT3", "1") != "0"
 # bf16, one process: the BN1 backward first pass inside the epilogue of its dgrad GEMM (A/B knob)
 _BN1_BWD_IN_GEMM = os.environ.get("FBN_BN1_BWD_IN_GEMM", "1") == "1"
 
@@ -103,8 +107,33 @@ def gemm_split(A, B, C, M, N, K, lda, ldb, ldc, transA, transB, bias=None, rC=NO
 class _ConvJob(ctypes.Structure):
     _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("rows", ctypes.c_int), ("cols", ctypes.c_int),
                 ("ld", ctypes.c_int), ("trans", ctypes.c_int), ("seg", ctypes.c_int), ("off0", ctypes.c_int),
-                ("off1", ctypes.c_int), ("part", ctypes.c_int), ("dld", ctypes.c_int)]
+                ("off1", ctypes.c_int), ("part", ctypes.c_int), ("dld", ctypes.c_int), ("pst", ctypes.c_int)]
 CONV_MAX = 16   # include/fibinet.h: jobs per fbn_convert_bf16 launch
+
+
+def split_images(specs, stream) -> None:
+    """ONE fbn_convert_bf16 launch (part 2) of split-bf16 operand images: specs = [(src, dst, rows,
+    cols, ld, trans, remap)], dst [2, rows, cols] bf16 = (hi, lo) of the fp32 source (bf16_fwd
+    backward: fbn_gemm_s3 and the split-bf16 x3 slab GEMMs read A_hi B_hi + A_hi B_lo + A_lo B_hi)."""
+    jobs = (_ConvJob * CONV_MAX)()
+    _lib.keep(jobs)
+    for i, (src, dst, rows, cols, ld, trans, rm) in enumerate(specs):
+        jobs[i] = _ConvJob(src.data_ptr(), dst.data_ptr(), rows, cols, ld, trans, rm[0], rm[1], rm[2], 2, 0,
+                           rows * cols)
+    call("fbn_convert_bf16", ctypes.cast(jobs, ctypes.c_void_p).value, len(specs), stream)
+
+
+def s3_ok(M, N, K0, lda, ldb, transA, transB) -> bool:
+    """fbn_gemm_s3's LDS-DMA conditions."""
+    return K0 % 64 == 0 and lda % 8 == 0 and ldb % 8 == 0 and (not transA or M % 8 == 0) and (transB or N % 8 == 0)
+
+
+def gemm_s3(A, B, C, M, N, K0, lda, ldb, ldc, transA, transB, beta=0.0, stream=None):
+    """C (+)= split-bf16 x3 product of the (hi, lo) images A [2, ...] and B [2, ...] (fbn_gemm_s3)."""
+    nbytes = _lib.lib().fbn_gemm_workspace_size(M, N, 3 * K0, 1)
+    ws = _ws(nbytes, C.device)
+    call("fbn_gemm_s3", ptr(A), ptr(B), ptr(C), M, N, K0, lda, ldb, ldc, int(transA), int(transB), A[0].numel(),
+         B[0].numel(), float(beta), ptr(ws), nbytes, stream if stream is not None else _lib.stream_handle())
 
 
 def bf16_weights(p: Dict[str, torch.Tensor], d: int, a: Dict[str, torch.Tensor], stream,
@@ -172,7 +201,8 @@ class _SlabGemm(ctypes.Structure):
                 ("A2", ctypes.c_void_p), ("B2", ctypes.c_void_p), ("M", ctypes.c_int), ("N", ctypes.c_int),
                 ("K", ctypes.c_int), ("lda", ctypes.c_int), ("ldb", ctypes.c_int), ("transA", ctypes.c_int),
                 ("transB", ctypes.c_int), ("lda2", ctypes.c_int), ("kseg", ctypes.c_int), ("ldb2", ctypes.c_int),
-                ("nseg", ctypes.c_int), ("pad", ctypes.c_int)]
+                ("nseg", ctypes.c_int), ("s3k0", ctypes.c_int), ("lo_a", ctypes.c_longlong),
+                ("lo_b", ctypes.c_longlong)]
 _nsplit = ctypes.c_int(0)
 # FBN_GATHER_HOT=<tau> (A/B variant of the gather, N1): rows a batch draws >= tau times staged in
 # LDS per workgroup (fbn_hot_rows + fbn_fields_fwd_hot); 0 = off (default: measured slower)
@@ -197,9 +227,15 @@ class DeferredSums:
         self.keep.append(part)
 
     def gemm_slabs(self, A, B, out, M, N, K, lda, ldb, ldc, transA, transB, rC=NO_REMAP, beta=0.0, stream=None,
-                   A2=None, lda2=0, kseg=INT_MAX, B2=None, ldb2=0, nseg=INT_MAX) -> bool:
+                   A2=None, lda2=0, kseg=INT_MAX, B2=None, ldb2=0, nseg=INT_MAX, s3=False) -> bool:
         """out (+)= op(A) op(B) through fbn_gemm_slabs, its slabs summed at flush(); False (nothing
-        launched) when the shape is outside the slab path's bf16 LDS-DMA conditions."""
+        launched) when the shape is outside the slab path's bf16 LDS-DMA conditions.  s3: A and B are
+        (hi, lo) images [2, K, .] and the product is split-bf16 x3 over 3 K (grouped launch only)."""
+        grouped = _WGRAD_GROUP and transA and not transB and A2 is None and M % 8 == 0 and N % 8 == 0
+        if s3 and not (grouped and B2 is None and K % 64 == 0):
+            return False
+        lo_a, lo_b = (A[0].numel(), B[0].numel()) if s3 else (0, 0)
+        K0, K = (K, 3 * K) if s3 else (0, K)
         if not (_DEFER_REDUCE and A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16 and K % 64 == 0
                 and lda % 8 == 0 and ldb % 8 == 0 and (not transA or M % 8 == 0) and (transB or N % 8 == 0)
                 and N % 4 == 0 and ldc % 4 == 0 and all(x % 4 == 0 for x in rC[1:])
@@ -217,12 +253,12 @@ class DeferredSums:
             else:
                 ws = _ws(nbytes, out.device)
         st = stream if stream is not None else _lib.stream_handle()
-        if _WGRAD_GROUP and transA and not transB and A2 is None and M % 8 == 0 and N % 8 == 0:
+        if grouped:
             # deferred to flush(): the step's weight gradients in one fbn_gemm_slabs_group launch
             # (their operands are not rewritten before it: stream order, buffers of this step)
             nsplit = _lib.lib().fbn_gemm_slabs_group_split(M, N, K)
             self.group.append((A.data_ptr(), B.data_ptr(), ws.data_ptr(), nbytes, 0, ptr(B2) or 0, M, N, K, lda,
-                               ldb, 1, 0, 0, 0, ldb2, nseg if B2 is not None else INT_MAX, 0))
+                               ldb, 1, 0, 0, 0, ldb2, nseg if B2 is not None else INT_MAX, K0, lo_a, lo_b))
             self.keep += [A, B] + ([B2] if B2 is not None else [])
         else:
             call("fbn_gemm_slabs", ptr(A), ptr(B), M, N, K, lda, ldb, int(transA), int(transB), ptr(ws), nbytes,
@@ -241,10 +277,14 @@ class DeferredSums:
     def launch_group(self, stream, probe: Optional[Dict[str, list]] = None, tstream=None) -> None:
         """The slab GEMMs recorded so far, in ONE fbn_gemm_slabs_group launch on `stream` (tstream: the
         torch stream of that handle, for the bench's events); their slabs are summed at flush()."""
-        group = self.group
+        # (split-bf16 x3 problems and plain ones launch apart: a launch takes one kind)
+        group = [x for x in self.group if x[-3]] + [x for x in self.group if not x[-3]]
         ev = _probe_start(probe, "wgrad_group") if group else None    # bench: the grouped launch
         while group:
-            gc, group = group[:6], group[6:]
+            n = 0
+            while n < min(6, len(group)) and bool(group[n][-3]) == bool(group[0][-3]):
+                n += 1
+            gc, group = group[:n], group[n:]
             garr = (_SlabGemm * len(gc))(*[_SlabGemm(*x) for x in gc])
             _lib.keep(garr)
             call("fbn_gemm_slabs_group", ctypes.addressof(garr), len(gc), stream)
@@ -517,7 +557,16 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     if split_c:
         gemm_split(Vc16, w16["Wa"], h1pre, B, H1, KC, 5 * d, KC, H1, False, True, bias=p["mlp.0.bias"], stream=st,
                    stats=t1, A2=c[:, 5 * d:], lda2=KC, kseg=5 * d)
+    elif f16 and _SPLIT3 and cfg.training and not cfg.bilinear_each:
+        # bf16_fwd training: c's split images [hi; lo; hi] for the backward's GEMMs, made here -- the
+        # GEMM takes the hi image (c rounded to bf16, as on load) through the LDS-DMA path
+        c2 = buf("s3_c_fwd", (2, B, KC), torch.bfloat16)
+        split_images([(c, c2, B, KC, KC, 0, NO_REMAP)], st)
+        a["s3_c"] = c2
+        gemm(c2[0], w16["Wa"], h1pre, B, H1, KC, KC, KC, H1, False, True, bias=p["mlp.0.bias"], bf16=True, stream=st,
+             stats=t1)
     elif bf or f16:   # bf16_fwd: the fp32 MLP input rounded to bf16 on load
+        a["s3_c"] = None
         gemm(c, w16["Wa"], h1pre, B, H1, KC, KC, KC, H1, False, True, bias=p["mlp.0.bias"], bf16=True, stream=st,
              stats=t1)
     else:
@@ -654,6 +703,31 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     # bf16_fwd: the fp32 gradient GEMMs as split-bf16 x3 on the bf16 MFMA (fbn_gemm bf16 = 2;
     # FBN_SPLIT_BWD=0: fp32 MFMA)
     sb = 2 if (cfg.fwd16 and _SPLIT_BWD) else False
+    # bf16_fwd: every backward GEMM as ONE bf16 GEMM over 3 K on (hi, lo) images of its fp32 operands
+    # (split_images; fbn_gemm_s3 / split-bf16 x3 slabs) where the LDS-DMA path takes the shape, else
+    # the fp32 MFMA
+    s3 = cfg.fwd16 and _SPLIT3 and not bf and not cfg.bilinear_each
+    im = {}
+
+    def img(name, rows, cols):
+        return tmp("s3_" + name, (2, rows, cols), torch.bfloat16)
+
+    if s3:
+        # the operands the forward left and the weights: ONE launch
+        im = {"WbT": img("WbT", H1, H2), "WaT": img("WaT", KC, H1), "W": img("W", d, d),
+              "h1": img("h1", B, H1), "x": img("x", B, 128), "Vc": img("Vc", 5 * B, d)}
+        jobs = [(p["mlp.4.weight"], im["WbT"], H1, H2, H1, 1, NO_REMAP),
+                (p["mlp.0.weight"], im["WaT"], KC, H1, 21 * d, 1, wa_remap(d)),
+                (p["bilinear.W"], im["W"], d, d, d, 0, NO_REMAP),
+                (a["h1"], im["h1"], B, H1, H1, 0, NO_REMAP),
+                (batch["item_emb_d128"], im["x"], B, 128, 128, 0, NO_REMAP),
+                (a["Vc"], im["Vc"], 5 * B, d, d, 0, NO_REMAP)]
+        if a.get("s3_c") is not None and tuple(a["s3_c"].shape) == (2, B, KC):
+            im["c"] = a["s3_c"]                     # made by the forward (its layer-1 GEMM reads the hi image)
+        else:
+            im["c"] = img("c", B, KC)
+            jobs.append((a["c"], im["c"], B, KC, KC, 0, NO_REMAP))
+        split_images(jobs, st)
     dh2pre = None if lean else tmp("dh2pre", (B, H2))
     dh2pre16 = tmp("dh2pre16", (B, H2), torch.bfloat16) if bf else None
     sums = DeferredSums(a)
@@ -680,6 +754,21 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
                  ptr(a["h1_16"]), ptr(a["h1pre"]), ptr(a["mean1"]), float(scale), ptr(part1), st)
         else:
             gemm(dh2pre16, w16["WbT"], dh1, B, H1, H2, H2, H2, H1, False, True, stream=st)
+    elif s3:
+        dh2 = img("dh2", B, H2)
+        split_images([(dh2pre, dh2, B, H2, H2, 0, NO_REMAP)], st)
+        if not sums.gemm_slabs(dh2, im["h1"], g["mlp.4.weight"], H2, H1, B, H2, H1, H1, True, False, stream=st,
+                               s3=True):
+            if s3_ok(H2, H1, B, H2, H1, True, False):
+                wg.run(lambda s: gemm_s3(dh2, im["h1"], g["mlp.4.weight"], H2, H1, B, H2, H1, H1, True, False,
+                                         stream=s))
+            else:
+                wg.run(lambda s: gemm(dh2pre, a["h1"], g["mlp.4.weight"], H2, H1, B, H2, H1, H1, True, False,
+                                      stream=s))
+        if s3_ok(B, H1, H2, H2, H2, False, True):
+            gemm_s3(dh2, im["WbT"], dh1, B, H1, H2, H2, H2, H1, False, True, stream=st)
+        else:
+            gemm(dh2pre, p["mlp.4.weight"], dh1, B, H1, H2, H2, H1, H1, False, False, stream=st)
     else:
         wg.run(lambda s: gemm(dh2pre, a["h1"], g["mlp.4.weight"], H2, H1, B, H2, H1, H1, True, False, bf16=sb,
                               stream=s))
@@ -691,7 +780,14 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
                 dpre16=dh1pre16, bias_grad=g["mlp.0.bias"], sums=sums, hact16=a["h1_16"] if lean_h1 else None,
                 part_pre=part1, tag="bn1")
     # weight gradient of the MLP input layer (side work), then its dgrad dc
-    if a.get("split_c"):
+    if s3:
+        dh1i = img("dh1", B, H1)
+        split_images([(dh1pre, dh1i, B, H1, H1, 0, NO_REMAP)], st)
+        if not sums.gemm_slabs(dh1i, im["c"], g["mlp.0.weight"], H1, KC, B, H1, KC, 21 * d, True, False,
+                               rC=wa_remap(d), stream=st, s3=True):
+            wg.run(lambda s: gemm(dh1pre, a["c"], g["mlp.0.weight"], H1, KC, B, H1, KC, 21 * d, True, False,
+                                  rC=wa_remap(d), stream=s))
+    elif a.get("split_c"):
         if not sums.gemm_slabs(dh1pre16, a["Vc16"], g["mlp.0.weight"], H1, KC, B, H1, 5 * d, 21 * d, True, False,
                                rC=wa_remap(d), stream=st, B2=a["c"][:, 5 * d:], ldb2=KC, nseg=5 * d):
             wg.run(lambda s: gemm_split(dh1pre16, a["Vc16"], g["mlp.0.weight"], H1, KC, B, H1, 5 * d, 21 * d, True,
@@ -713,6 +809,9 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     elif bf:
         dc = torch.empty((B, KC), **f32)
         gemm(dh1pre16, w16["WaT"], dc, B, KC, H1, H1, H1, KC, False, True, stream=st)
+    elif s3 and s3_ok(B, KC, H1, H1, H1, False, True):
+        dc = torch.empty((B, KC), **f32)
+        gemm_s3(dh1i, im["WaT"], dc, B, KC, H1, H1, H1, KC, False, True, stream=st)
     else:
         dc = torch.empty((B, KC), **f32)
         gemm(dh1pre, p["mlp.0.weight"], dc, B, KC, H1, H1, 21 * d, KC, False, False, rB=wa_remap(d), bf16=sb,
@@ -738,6 +837,16 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
             if not sums.gemm_slabs(a["Vc16"], dU16, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=st):
                 wg.run(lambda s: gemm(a["Vc16"], dU16, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=s))
             gemm(dU16, w16["W"], dV, 5 * B, d, d, d, d, d, False, True, beta=1.0, stream=st)
+        elif s3:
+            dU2 = img("dU", 5 * B, d)
+            split_images([(dU, dU2, 5 * B, d, d, 0, NO_REMAP)], st)
+            if not sums.gemm_slabs(im["Vc"], dU2, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=st,
+                                   s3=True):
+                wg.run(lambda s: gemm(a["Vc"], dU, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=s))
+            if s3_ok(5 * B, d, d, d, d, False, True):
+                gemm_s3(dU2, im["W"], dV, 5 * B, d, d, d, d, d, False, True, beta=1.0, stream=st)
+            else:
+                gemm(dU, p["bilinear.W"], dV, 5 * B, d, d, d, d, d, False, True, beta=1.0, stream=st)
         else:
             wg.run(lambda s: gemm(a["Vc"], dU, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, bf16=sb,
                                   stream=s))
@@ -789,6 +898,13 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
                                stream=st):
             wg.run(lambda s: gemm(dhmm16, w16["x"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True, False,
                                   stream=s))
+    elif s3:
+        dhs = img("dhmm", B, d)
+        split_images([(dhmm, dhs, B, d, d, 0, NO_REMAP)], st)
+        if not sums.gemm_slabs(dhs, im["x"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True, False,
+                               stream=st, s3=True):
+            wg.run(lambda s: gemm(dhmm, batch["item_emb_d128"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True,
+                                  False, stream=s))
     else:
         wg.run(lambda s: gemm(dhmm, batch["item_emb_d128"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True,
                               False, bf16=sb, stream=s))

@@ -82,11 +82,12 @@ int fbn_gemm_slabs_split(int M, int N, int K);
 /* n <= 6 slab-mode GEMMs in ONE launch (the step's weight gradients, deferred to the end of the
  * backward: one tail instead of one per GEMM).  descs = host array of n records
  * {const void* A, *B; float* ws; size_t ws_bytes; const void* A2, *B2;
- *  int M, N, K, lda, ldb, transA, transB, lda2, kseg, ldb2, nseg, pad;}
+ *  int M, N, K, lda, ldb, transA, transB, lda2, kseg, ldb2, nseg, s3k0; long long lo_a, lo_b;}
  * with the meaning of fbn_gemm_slabs's arguments; each ws receives fbn_gemm_slabs_group_split(M, N, K)
  * K-slabs (half fbn_gemm_slabs_split's by default; with FBN_GROUP_SPLIT_DIV=1 exactly the slabs
  * fbn_gemm_slabs writes, bit for bit).  Every problem: transA = 1, transB = 0, K % 64 == 0,
- * M, N, lda, ldb % 8 == 0, no A2. */
+ * M, N, lda, ldb % 8 == 0, no A2.  s3k0 > 0 (on every problem or none): split-bf16 x3 as
+ * fbn_gemm_s3, K = 3 s3k0 over the hi images A / B and the lo images lo_a / lo_b elements past them. */
 int fbn_gemm_slabs_group(const void* descs, int n, void* stream);
 /* The K-slab count a problem takes inside fbn_gemm_slabs_group, host-only. */
 int fbn_gemm_slabs_group_split(int M, int N, int K);
@@ -96,6 +97,13 @@ int fbn_gemm_slabs_group_split(int M, int N, int K);
  * fbn_bilinear_bwd. */
 int fbn_gemm_bf16out(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                      int transA, int transB, void* stream);
+/* Split-bf16 x3 (the bf16_fwd backward GEMMs, src/model_fibinet.py:126-134 autograd at ~fp32 accuracy):
+ * C = beta C + A_hi B_hi + A_hi B_lo + A_lo B_hi as ONE bf16 MFMA GEMM over K = 3 K0 (LDS-DMA path).
+ * A / B are the hi images (bf16, layout as fbn_gemm's bf16 operands), the lo images (x - hi rounded to
+ * bf16: fbn_convert_bf16 part 2 writes both) lie lo_a / lo_b elements past them.  K0 % 64 == 0,
+ * lda, ldb % 8 == 0, k-major extents % 8; ws: fbn_gemm_workspace_size(M, N, 3 K0, 1) bytes. */
+int fbn_gemm_s3(const void* A, const void* B, float* C, int M, int N, int K0, int lda, int ldb, int ldc, int transA,
+                int transB, long long lo_a, long long lo_b, float beta, float* ws, size_t ws_bytes, void* stream);
 /* bf16 dgrad GEMM C = op(A) op(B) (f32 C, no bias) whose epilogue also computes the first pass of
  * the BatchNorm backward that follows it (src/model_fibinet.py:127-129 autograd: the BN1 backward
  * of the MLP, whose input gradient source G is this C): part = fbn_bn_bwd_fused's column partials
@@ -236,10 +244,11 @@ int fbn_bn_bwd_fused(const float* G, const float* gvec, const float* w, const fl
                      int C, double ntot, float* dXpre, short* dXpre16, float* dgamma, float* dbeta, float* dw,
                      float* colpart, const double* part_pre, void* ws, void* stream);
 /* bf16 images: jobs = host array of n <= 16 records
- * {const float* src; short* dst; int rows, cols, ld, trans, seg, off0, off1, part, dld;}
+ * {const float* src; short* dst; int rows, cols, ld, trans, seg, off0, off1, part, dld, pst;}
  * x = trans ? src[j*ld + rm(i)] : src[i*ld + rm(j)], rm(x) = x + (x < seg ? off0 : off1);
- * dst[i*dld + j] = part ? bf16(x - float(bf16(x))) : bf16(x)  (dld = 0: cols).  part 1 is the rounding
- * residual: hi + lo images carry 16 significant bits (the split-bf16 backward GEMMs of bf16_fwd mode). */
+ * hi = bf16(x), lo = bf16(x - float(hi));  dst[i*dld + j] = part ? lo : hi  (dld = 0: cols).  part 1
+ * is the rounding residual: hi + lo carry 16 significant bits.  part 2 writes both from one read,
+ * lo pst elements past hi: the operand images of fbn_gemm_s3 / split-bf16 x3 slab GEMMs. */
 int fbn_convert_bf16(const void* jobs, int n, void* stream);
 size_t fbn_colsum_workspace_size(int B, int C);
 int fbn_colsum(const float* X, int B, int C, int ldx, float* out, float beta, void* ws, void* stream);

@@ -8,7 +8,7 @@ reduce; C must be bit-identical with and without the statistics.  Tolerances: fp
 import pytest
 import torch
 
-from ctr_recommendation_amd import ops
+from ctr_recommendation_amd import _lib, ops
 
 pytestmark = pytest.mark.gpu
 
@@ -106,6 +106,41 @@ def test_gemm_split_bf16x3(hip_device, transA, transB, M, N, K):
     assert errs[2] < 4e-5 * K ** 0.5, errs
     assert errs[2] * 20 < errs[True], errs            # far better than bf16 operands
     assert errs[2] < 30 * errs[False] + 1e-6, errs    # near fp32
+
+
+@pytest.mark.parametrize("transA,transB", [(False, True), (False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(8192, 1920, 512), (512, 1920, 8192), (256, 136, 256), (128, 128, 40960)])
+def test_gemm_s3_images(hip_device, transA, transB, M, N, K):
+    """fbn_gemm_s3 (the bf16_fwd backward's GEMMs): ONE bf16 GEMM over 3 K on the (hi, lo) images
+    fbn_convert_bf16 part 2 writes, against float64 -- the same split-bf16 x3 error bar as
+    fbn_gemm bf16 = 2 (4e-5 x sqrt(K)); beta = 1 accumulates; and in slab mode (the grouped
+    weight-gradient launch, k-major A and B) the sum of its slabs matches the plain launch."""
+    g = torch.Generator(device="cpu").manual_seed(7)
+    A = torch.randn((K, M) if transA else (M, K), generator=g).to(hip_device)
+    Bm = torch.randn((N, K) if transB else (K, N), generator=g).to(hip_device)
+    lda = M if transA else K
+    ldb = K if transB else N
+    a = A.double().T if transA else A.double()
+    b = Bm.double().T if transB else Bm.double()
+    ref = a @ b
+    Ai = torch.empty((2,) + tuple(A.shape), dtype=torch.bfloat16, device=hip_device)
+    Bi = torch.empty((2,) + tuple(Bm.shape), dtype=torch.bfloat16, device=hip_device)
+    ops.split_images([(A, Ai, A.shape[0], A.shape[1], A.shape[1], 0, ops.NO_REMAP),
+                      (Bm, Bi, Bm.shape[0], Bm.shape[1], Bm.shape[1], 0, ops.NO_REMAP)], _lib.stream_handle())
+    assert torch.equal(Ai[0], A.bfloat16()) and torch.equal(Ai[1], (A - Ai[0].float()).bfloat16())
+    C = torch.full((M, N), float("nan"), device=hip_device)
+    ops.gemm_s3(Ai, Bi, C, M, N, K, lda, ldb, N, transA, transB)
+    err = (C.double() - ref).abs().max().item()
+    assert err < 4e-5 * K ** 0.5, err
+    C2 = C.clone()
+    ops.gemm_s3(Ai, Bi, C2, M, N, K, lda, ldb, N, transA, transB, beta=1.0)
+    assert (C2.double() - 2 * ref).abs().max().item() < 8e-5 * K ** 0.5
+    if transA and not transB:
+        C3 = torch.full((M, N), float("nan"), device=hip_device)
+        sums = ops.DeferredSums()
+        assert sums.gemm_slabs(Ai, Bi, C3, M, N, K, lda, ldb, N, True, False, s3=True)
+        sums.flush(_lib.stream_handle())
+        assert (C3.double() - ref).abs().max().item() < 4e-5 * K ** 0.5
 
 
 @pytest.mark.parametrize("M,N,K,remap", [(256, 512, 8192, False), (512, 1920, 8192, True), (128, 128, 40960, False),

@@ -439,3 +439,40 @@ def test_wgrad_group_bit_identical(hip_device, d, B):
     for name, a, c in zip(("p", "m", "E", "Em", "Ev"), runs[0][1], runs[1][1]):
         bad = (a != c).nonzero()
         assert bad.numel() == 0, (name, bad[:8].tolist(), (a - c).abs().max().item())
+
+
+@pytest.mark.parametrize("d,B", [(16, 256), (128, 512), (128, 200)])
+def test_split3_backward_matches_fp32_mfma(hip_device, d, B, monkeypatch):
+    """bf16_fwd's backward GEMMs as ONE bf16 GEMM over 3 K on split images ([hi, hi, lo] x [hi, lo,
+    hi], ops.split3_images) against the same backward on the fp32 MFMA (FBN_SPLIT3=0), from the same
+    bf16-forward activations: every gradient within 1e-4 of its tensor's largest entry (the split
+    keeps 16 of fp32's 24 significand bits per operand; measured ~1e-5).  B = 200: K = 3 B is not a
+    multiple of 64, so the weight gradients take the plain GEMM instead of the slab launch."""
+    from ctr_recommendation_amd import ops
+    cfg = {"embedding_dim": d, "vocab_size": V, "honour_config": True, "net_dropout": 0.0,
+           "compute_dtype": "bf16_fwd"}
+    torch.manual_seed(0)
+    init = oracle_build(None, cfg, honour_config=True).state_dict()
+    b, y = make_batch(5, B, V)
+    b = {k: v.to(hip_device) for k, v in b.items()}
+    y = y.to(hip_device)
+    out = {}
+    for s3 in (True, False):
+        monkeypatch.setattr(ops, "_SPLIT3", s3)
+        tr = FiBiNETTrainer(cfg, total_steps=4, batch_size=B, device=hip_device,
+                            init_state={k: v.clone() for k, v in init.items()})
+        loss = tr.step(b, y).item()
+        torch.cuda.synchronize()
+        out[s3] = (loss, {k: v.detach().clone().cpu() for k, v in tr.g.items()})
+        tr.close()
+    # the same forward math (the layer-1 GEMM reads c's hi image instead of rounding c on load: the
+    # same bf16 operands, another kernel's accumulation order)
+    assert abs(out[True][0] - out[False][0]) <= 1e-6 * abs(out[False][0]), (out[True][0], out[False][0])
+    for k, g0 in out[False][1].items():
+        g1 = out[True][1][k]
+        scale = g0.abs().max().item()
+        err = (g1 - g0).abs().max().item()
+        if k in NOISE_BIASES:                      # exactly cancelled by the BatchNorm: rounding noise
+            assert err <= 1e-5, (k, err)
+            continue
+        assert err <= 1e-4 * scale + 1e-8, f"{k}: max err {err:.3e} vs scale {scale:.3e}"
