@@ -65,6 +65,8 @@ SIGNATURES = {
                            I, I, P]),
     "fbn_pairs_fwd": (I, [P, P, P, P, I, I, I, I, I, P]),
     "fbn_pairs_bwd": (I, [P, P, P, P, P, P, P, I, I, I, I, P]),
+    "fbn_pairs_fwd_img": (I, [P, P, P, P, I, I, I, P]),
+    "fbn_pairs_bwd_img": (I, [P, P, P, P, P, I, I, I, P]),
     "fbn_bn_workspace_size": (SZ, [I, I]),
     "fbn_bn_stats_pass": (I, [P, I, I, P, P, P, P]),
     "fbn_bn_mean": (I, [P, D, I, P, P]),

@@ -30,6 +30,18 @@ __device__ __forceinline__ void store4(float* p, const f32x4& v) { *reinterpret_
 __device__ __forceinline__ void store4(short* p, const f32x4& v) {
   *reinterpret_cast<bf16x4*>(p) = (bf16x4){f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
 }
+// split-bf16 images (bf16_fwd training, fbn_gemm_s3 operands): hi = bf16(x) at p, lo = bf16(x - hi)
+// lo_off elements further
+__device__ __forceinline__ void store_img4(short* p, long long lo_off, const f32x4& v) {
+  bf16x4 h, l;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    h[e] = f2bf(v[e]);
+    l[e] = f2bf(v[e] - bf2f(h[e]));
+  }
+  *reinterpret_cast<bf16x4*>(p) = h;
+  *reinterpret_cast<bf16x4*>(p + lo_off) = l;
+}
 // V from the fp32 fields (fp32 mode) or from their bf16 copy (bf16 mode: the fp32 copy is not
 // written at all; U = V W is computed from the same bf16 V by the GEMM)
 __device__ __forceinline__ f32x4 load_v4(const float* __restrict__ V, const short* __restrict__ V16, size_t off) {
@@ -62,6 +74,33 @@ __global__ void pairs_fwd_kernel(const float* __restrict__ Vc, const short* __re
   }
 }
 
+// bf16_fwd training, bilinear "all": the MLP input c = [V | pairs] and the fields V written only as
+// split images (c: [B][ldc] hi + lo B ldc further; V: [B][5][D] hi + lo 5 B D further) -- the
+// layer-1 GEMM reads c's hi image, the backward's split-bf16 x3 GEMMs both
+__global__ void pairs_fwd_img_kernel(const float* __restrict__ Vc, const float* __restrict__ U, short* __restrict__ ci,
+                                     short* __restrict__ vi, int B, int D, int ldc) {
+  const int q4 = D / 4;
+  const size_t total = (size_t)B * q4;
+  const long long clo = (long long)B * ldc, vlo = 5LL * B * D;
+  for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
+    const int b = (int)(idx / q4), col = (int)(idx % q4) * 4;
+    f32x4 v[5], u[5];
+#pragma unroll
+    for (int f = 0; f < 5; ++f) {
+      v[f] = *reinterpret_cast<const f32x4*>(Vc + ((size_t)b * 5 + f) * D + col);
+      u[f] = *reinterpret_cast<const f32x4*>(U + ((size_t)b * 5 + f) * D + col);
+    }
+    short* out = ci + (size_t)b * ldc + col;
+#pragma unroll
+    for (int f = 0; f < 5; ++f) {
+      store_img4(out + f * D, clo, v[f]);
+      if (vi) store_img4(vi + ((size_t)b * 5 + f) * D + col, vlo, v[f]);
+    }
+#pragma unroll
+    for (int k = 0; k < 10; ++k) store_img4(out + (5 + k) * D, clo, v[c_pi[k]] * u[c_pj[k]]);
+  }
+}
+
 // dV (out) = dc_V + sum of pair-grad terms that land on V ; dU (out) = pair-grad terms that land on U
 // MODE (bilinear "all" = 0 / "each" = 1) is a template parameter and the pair loop is unrolled
 // with compile-time indices: with runtime indices the five-field register arrays go to scratch.
@@ -70,7 +109,7 @@ __global__ void __launch_bounds__(256) pairs_bwd_kernel(const float* __restrict_
                                                         const short* __restrict__ Vc16,
                                                         const float* __restrict__ U, float* __restrict__ dV,
                                                         float* __restrict__ dU, short* __restrict__ dU16, int B, int D,
-                                                        int ldc) {
+                                                        int ldc, short* __restrict__ dUi) {
   const int q4 = D / 4;
   const size_t total = (size_t)B * q4;
   for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
@@ -95,8 +134,9 @@ __global__ void __launch_bounds__(256) pairs_bwd_kernel(const float* __restrict_
 #pragma unroll
     for (int f = 0; f < 5; ++f) {
       *reinterpret_cast<f32x4*>(dV + ((size_t)b * 5 + f) * D + col) = gv[f];
-      *reinterpret_cast<f32x4*>(dU + ((size_t)b * 5 + f) * D + col) = gu[f];
+      if (dU) *reinterpret_cast<f32x4*>(dU + ((size_t)b * 5 + f) * D + col) = gu[f];
       if (dU16) store4(dU16 + ((size_t)b * 5 + f) * D + col, gu[f]);
+      if (dUi) store_img4(dUi + ((size_t)b * 5 + f) * D + col, 5LL * B * D, gu[f]);   // split images (bf16_fwd)
     }
   }
 }
@@ -977,15 +1017,41 @@ extern "C" int fbn_pairs_fwd(const float* Vc, const short* Vc16, const float* U,
   return FBN_OK;
 }
 
+extern "C" int fbn_pairs_fwd_img(const float* Vc, const float* U, void* c_img, void* vc_img, int B, int D, int ldc,
+                                 void* stream) {
+  if (B <= 0) return FBN_OK;
+  if ((D & 3) || (ldc & 3) || ldc < 15 * D || !Vc || !U || !c_img) {
+    fbn_set_error("fbn_pairs_fwd_img: Vc, U, c_img; D, ldc multiples of 4, ldc >= 15 D");
+    return FBN_ERR_ARG;
+  }
+  fbn_launch(pairs_fwd_img_kernel, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream, Vc, U,
+             (short*)c_img, (short*)vc_img, B, D, ldc);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+extern "C" int fbn_pairs_bwd_img(const float* dc, const float* Vc, const float* U, float* dV, void* dU_img, int B,
+                                 int D, int ldc, void* stream) {
+  if (B <= 0) return FBN_OK;
+  if ((D & 3) || (ldc & 3) || !dc || !Vc || !U || !dV || !dU_img) {
+    fbn_set_error("fbn_pairs_bwd_img: dc, Vc, U, dV, dU_img; D, ldc multiples of 4");
+    return FBN_ERR_ARG;
+  }
+  fbn_launch(pairs_bwd_kernel<0>, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream, dc, Vc,
+             (const short*)nullptr, U, dV, (float*)nullptr, (short*)nullptr, B, D, ldc, (short*)dU_img);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
 extern "C" int fbn_pairs_bwd(const float* dc, const float* Vc, const short* Vc16, const float* U, float* dV,
                              float* dU, short* dU16, int B, int D, int ldc, int mode, void* stream) {
   if (B <= 0) return FBN_OK;
   if (mode == 0)
     fbn_launch(pairs_bwd_kernel<0>, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream, dc, Vc,
-                       Vc16, U, dV, dU, dU16, B, D, ldc);
+                       Vc16, U, dV, dU, dU16, B, D, ldc, (short*)nullptr);
   else
     fbn_launch(pairs_bwd_kernel<1>, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream, dc, Vc,
-                       Vc16, U, dV, dU, dU16, B, D, ldc);
+                       Vc16, U, dV, dU, dU16, B, D, ldc, (short*)nullptr);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

@@ -482,6 +482,11 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     # bf16 LDS-DMA mode: c's V block is never written -- the MLP GEMMs read [Vc16 | c[:, 5d:]] (split operand)
     split_c = v16 and split_mlp_input(d)
     a["split_c"] = split_c
+    # bf16_fwd training whose split-bf16 x3 backward runs every GEMM on the LDS-DMA path: c and V exist
+    # only as split images (fbn_pairs_fwd_img) -- no fp32 c is written or converted
+    s3img = (f16 and _SPLIT3 and cfg.training and not cfg.bilinear_each and B % 64 == 0 and d % 64 == 0
+             and _WGRAD_GROUP and _DEFER_REDUCE)
+    a["s3img"] = s3img
     av = buf("a", (B, 6))
     cnt = buf("cnt", (B,))
     if err is None:
@@ -516,7 +521,7 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
              ptr(p["cate_emb.weight"]), p["cate_emb.weight"].shape[0], ptr(E), V, ptr(pos),
              ptr(p["senet.excitation.0.weight"]), ptr(p["senet.excitation.0.bias"]),
              ptr(p["senet.excitation.2.weight"]), ptr(p["senet.excitation.2.bias"]), cfg.R, ptr(X), ptr(Vc),
-             ptr(Vc16), None if split_c else ptr(c), KC,
+             ptr(Vc16), None if (split_c or s3img) else ptr(c), KC,
              int(bf), ptr(av), ptr(cnt), ptr(err), ptr(sm.get("map")), ptr(sm.get("slot_row")), B, Lr, d,
              int(table_rows is not None and table_rows.dtype == torch.bfloat16), st)
     _probe_end(ev)
@@ -545,7 +550,11 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
         for f in range(1, 5):   # field index in Vc: f-1 <-> reference field f; W_list[f]
             gemm(Vc[:, f - 1], p[f"bilinear.W_list.{f}"], U[:, f - 1], B, d, d, 5 * d, d, 5 * d, False, False,
                  bf16=bf, stream=st)
-    if not fused_bil:
+    if s3img:
+        a["s3_c"] = buf("s3_c_fwd", (2, B, KC), torch.bfloat16)
+        a["s3_vc"] = buf("s3_vc_fwd", (2, 5 * B, d), torch.bfloat16)
+        call("fbn_pairs_fwd_img", ptr(Vc), ptr(U), ptr(a["s3_c"]), ptr(a["s3_vc"]), B, d, KC, st)
+    elif not fused_bil:
         call("fbn_pairs_fwd", ptr(Vc), ptr(Vc16), ptr(U), ptr(c), B, d, KC, int(cfg.bilinear_each), int(bf), st)
     # MLP layer 1
     h1pre = buf("h1pre", (B, H1))
@@ -560,9 +569,12 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     elif f16 and _SPLIT3 and cfg.training and not cfg.bilinear_each:
         # bf16_fwd training: c's split images [hi; lo; hi] for the backward's GEMMs, made here -- the
         # GEMM takes the hi image (c rounded to bf16, as on load) through the LDS-DMA path
-        c2 = buf("s3_c_fwd", (2, B, KC), torch.bfloat16)
-        split_images([(c, c2, B, KC, KC, 0, NO_REMAP)], st)
-        a["s3_c"] = c2
+        if s3img:
+            c2 = a["s3_c"]                          # fbn_pairs_fwd_img
+        else:
+            c2 = buf("s3_c_fwd", (2, B, KC), torch.bfloat16)
+            split_images([(c, c2, B, KC, KC, 0, NO_REMAP)], st)
+            a["s3_c"] = c2
         gemm(c2[0], w16["Wa"], h1pre, B, H1, KC, KC, KC, H1, False, True, bias=p["mlp.0.bias"], bf16=True, stream=st,
              stats=t1)
     elif bf or f16:   # bf16_fwd: the fp32 MLP input rounded to bf16 on load
@@ -715,13 +727,17 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     if s3:
         # the operands the forward left and the weights: ONE launch
         im = {"WbT": img("WbT", H1, H2), "WaT": img("WaT", KC, H1), "W": img("W", d, d),
-              "h1": img("h1", B, H1), "x": img("x", B, 128), "Vc": img("Vc", 5 * B, d)}
+              "h1": img("h1", B, H1), "x": img("x", B, 128)}
         jobs = [(p["mlp.4.weight"], im["WbT"], H1, H2, H1, 1, NO_REMAP),
                 (p["mlp.0.weight"], im["WaT"], KC, H1, 21 * d, 1, wa_remap(d)),
                 (p["bilinear.W"], im["W"], d, d, d, 0, NO_REMAP),
                 (a["h1"], im["h1"], B, H1, H1, 0, NO_REMAP),
-                (batch["item_emb_d128"], im["x"], B, 128, 128, 0, NO_REMAP),
-                (a["Vc"], im["Vc"], 5 * B, d, d, 0, NO_REMAP)]
+                (batch["item_emb_d128"], im["x"], B, 128, 128, 0, NO_REMAP)]
+        if a.get("s3img"):
+            im["Vc"] = a["s3_vc"]                   # written by fbn_pairs_fwd_img
+        else:
+            im["Vc"] = img("Vc", 5 * B, d)
+            jobs.append((a["Vc"], im["Vc"], 5 * B, d, d, 0, NO_REMAP))
         if a.get("s3_c") is not None and tuple(a["s3_c"].shape) == (2, B, KC):
             im["c"] = a["s3_c"]                     # made by the forward (its layer-1 GEMM reads the hi image)
         else:
@@ -826,6 +842,10 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
              ptr(w16["W"]), ptr(dV), ptr(dU16), B, d, st)
         if not sums.gemm_slabs(a["Vc16"], dU16, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=st):
             wg.run(lambda s: gemm(a["Vc16"], dU16, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=s))
+    elif s3 and a.get("s3img"):
+        dU = None                                   # only its split images (every reader takes them)
+        dU2 = img("dU", 5 * B, d)
+        call("fbn_pairs_bwd_img", ptr(dc), ptr(a["Vc"]), ptr(a["U"]), ptr(dV), ptr(dU2), B, d, KC, st)
     else:
         dU = torch.empty((B, 5, d), **f32)
         call("fbn_pairs_bwd", ptr(dc), None if v16 else ptr(a["Vc"]), ptr(a["Vc16"]) if v16 else None, ptr(a["U"]),
@@ -838,8 +858,9 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
                 wg.run(lambda s: gemm(a["Vc16"], dU16, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=s))
             gemm(dU16, w16["W"], dV, 5 * B, d, d, d, d, d, False, True, beta=1.0, stream=st)
         elif s3:
-            dU2 = img("dU", 5 * B, d)
-            split_images([(dU, dU2, 5 * B, d, d, 0, NO_REMAP)], st)
+            if dU is not None:
+                dU2 = img("dU", 5 * B, d)
+                split_images([(dU, dU2, 5 * B, d, d, 0, NO_REMAP)], st)
             if not sums.gemm_slabs(im["Vc"], dU2, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=st,
                                    s3=True):
                 wg.run(lambda s: gemm(a["Vc"], dU, g["bilinear.W"], d, d, 5 * B, d, d, d, True, False, stream=s))
