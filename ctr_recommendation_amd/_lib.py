@@ -46,6 +46,7 @@ SIGNATURES = {
     "fbn_row_chunks": (I, [I]),
     "fbn_bn_bwd_chunks": (I, [I, I]),
     "fbn_bn_bwd_fused": (I, [P, P, P, P, P, F, P, P, P, P, I, I, D, P, P, P, P, P, P, P, P, P]),
+    "fbn_bn_bwd_fused_img": (I, [P, P, P, P, P, F, P, P, P, P, I, I, D, P, P, P, P, P, P, P, P, P]),
     "fbn_colsum_partial": (I, [P, I, I, I, P, P]),
     "fbn_sum_jobs": (I, [P, I, P]),
     "fbn_sum_jobs2": (I, [P, I, P, I, P]),
@@ -74,6 +75,7 @@ SIGNATURES = {
     "fbn_bn_stats": (I, [P, I, I, P, P, P, P, F, F, I, P, P]),
     "fbn_bn_eval_params": (I, [P, P, P, P, I, F, P]),
     "fbn_bn_act_fwd": (I, [P, P, I, I, P, P, P, P, F, P, U, P, P, P, P]),
+    "fbn_bn_act_fwd_img": (I, [P, P, I, I, P, P, P, P, F, P, U, P, P, P, P]),
     "fbn_bn_act_head_fwd": (I, [P, P, I, I, P, P, P, P, F, P, U, P, P, P, P, P, P, P, P, P, F, P, F, P]),
     "fbn_bn_bwd_reduce": (I, [P, P, P, P, F, P, P, I, I, P, P, P]),
     "fbn_bn_bwd_apply": (I, [P, P, P, P, F, P, P, P, P, I, I, P, D, P, P, P, P, P, P, P]),

@@ -296,7 +296,8 @@ __global__ void __launch_bounds__(NT) bn_act_fwd2_kernel(const float* __restrict
                                                          unsigned stream_id, unsigned char* __restrict__ mask_out,
                                                          const unsigned char* __restrict__ mask_in,
                                                          short* __restrict__ Y16, HeadArgs head,
-                                                         double* __restrict__ bpart = nullptr, float bscale = 1.f) {
+                                                         double* __restrict__ bpart = nullptr, float bscale = 1.f,
+                                                         long long y16_lo = 0) {
   FBN_MAIN_PRIO();
   constexpr int NWV = NT / 64;
   const int q = threadIdx.x & 63, rl = threadIdx.x >> 6;
@@ -334,7 +335,10 @@ __global__ void __launch_bounds__(NT) bn_act_fwd2_kernel(const float* __restrict
       y[e] = v;
     }
     if (Y) *reinterpret_cast<f32x4*>(Y + i) = y;
-    if (Y16) store4(Y16 + i, y);
+    if (Y16) {
+      if (y16_lo) store_img4(Y16 + i, y16_lo, y);   // split images (bf16_fwd): hi here, lo y16_lo further
+      else store4(Y16 + i, y);
+    }
     if (HEAD) {
       const f32x4 ww = *reinterpret_cast<const f32x4*>(head.w + c);
       const float go = head_row(y[0] * ww[0] + y[1] * ww[1] + y[2] * ww[2] + y[3] * ww[3], r, q, head);
@@ -383,6 +387,7 @@ struct BnBwdSrc {
   float scale;
   const short* hact16; // [B][C] bf16 image of the activation, read instead of hact when hact is null
                        // (matrix source only: the mask needs just the sign, bf16 keeps it)
+  long long dx16_lo;   // > 0: the bf16 output is split images (hi, lo this many elements further)
 };
 // the activation's "> 0" test on 4 columns, from the f32 activation or its bf16 image (a bf16
 // bit pattern read as a signed short is > 0 exactly when the value is > +0)
@@ -765,7 +770,10 @@ __global__ void __launch_bounds__(256) bn_bwd_apply4_kernel(BnBwdSrc s, const fl
         v[e] = (dy - c0[e] - (x[e] - mu[e]) * c1[e]) * is[e] * gg[e];
       }
       if (dX) *reinterpret_cast<f32x4*>(dX + i) = v;
-      if (dX16) store4(dX16 + i, v);
+      if (dX16) {
+        if (s.dx16_lo) store_img4(dX16 + i, s.dx16_lo, v);
+        else store4(dX16 + i, v);
+      }
       acc += v;
     }
   }
@@ -1138,7 +1146,24 @@ extern "C" int fbn_bn_act_fwd(const float* X, float* Y, int B, int C, const floa
   const int rpc = bn_act_rows_per_chunk();
   fbn_launch(bn_act_fwd2_kernel<false>, dim3(fbn_cdiv(C, 256), fbn_cdiv(B, rpc)), dim3(256), 0,
                      (hipStream_t)stream, X, Y, B, C, rpc, mean, invstd, g, b, p_drop, rng, stream_id, mask_out, mask_in,
-                     Y16, HeadArgs{}, nullptr, 1.f);
+                     Y16, HeadArgs{}, nullptr, 1.f, 0LL);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+// fbn_bn_act_fwd with the bf16 output as split images: Y_img = hi (the layer-2 GEMM operand), lo =
+// bf16(y - hi) B*C elements further (the bf16_fwd backward's split-bf16 x3 weight gradient)
+extern "C" int fbn_bn_act_fwd_img(const float* X, float* Y, int B, int C, const float* mean, const float* invstd,
+                                  const float* g, const float* b, float p_drop, const unsigned long long* rng,
+                                  unsigned stream_id, unsigned char* mask_out, const unsigned char* mask_in,
+                                  void* Y_img, void* stream) {
+  if (B <= 0) return FBN_OK;
+  if ((C & 3) || !Y_img) { fbn_set_error("bn_act_img: C % 4, Y_img"); return FBN_ERR_ARG; }
+  if (p_drop > 0.f && !rng && !mask_in) { fbn_set_error("bn_act: dropout needs an rng state or a mask"); return FBN_ERR_ARG; }
+  const int rpc = bn_act_rows_per_chunk();
+  fbn_launch(bn_act_fwd2_kernel<false>, dim3(fbn_cdiv(C, 256), fbn_cdiv(B, rpc)), dim3(256), 0,
+                     (hipStream_t)stream, X, Y, B, C, rpc, mean, invstd, g, b, p_drop, rng, stream_id, mask_out, mask_in,
+                     (short*)Y_img, HeadArgs{}, nullptr, 1.f, (long long)B * C);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -1160,14 +1185,14 @@ extern "C" int fbn_bn_act_head_fwd(const float* X, float* Y, int B, int C, const
     fbn_launch((bn_act_fwd2_kernel<true, 1024, true>), dim3(1, fbn_cdiv(B, rpc)), dim3(1024), 0,
                        (hipStream_t)stream, X, Y, B, C, rpc, mean, invstd, g, b, p_drop, rng, stream_id, mask_out,
                        mask_in, nullptr, HeadArgs{hw, hbias, logits, probs, labels, loss_terms, gout, denom}, bwd_part,
-                       bwd_scale);
+                       bwd_scale, 0LL);
     FBN_CHECK_LAUNCH();
     return FBN_OK;
   }
   const int rpc = bn_act_rows_per_chunk();
   fbn_launch(bn_act_fwd2_kernel<true>, dim3(1, fbn_cdiv(B, rpc)), dim3(256), 0, (hipStream_t)stream, X, Y, B,
                      C, rpc, mean, invstd, g, b, p_drop, rng, stream_id, mask_out, mask_in, (short*)nullptr,
-                     HeadArgs{hw, hbias, logits, probs, labels, loss_terms, gout, denom}, nullptr, 1.f);
+                     HeadArgs{hw, hbias, logits, probs, labels, loss_terms, gout, denom}, nullptr, 1.f, 0LL);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -1331,11 +1356,34 @@ extern "C" int fbn_bn_tile_finalize(const float* part, int M, int C, double ntot
 
 extern "C" size_t fbn_bn_colpart_size(int B, int C) { return (size_t)bn_bwd_chunks(B, C) * C * sizeof(float); }
 
+static int bn_bwd_fused_impl(const float* G, const float* gvec, const float* w, const float* hact,
+                             const short* hact16, float scale, const float* Xpre, const float* mean,
+                             const float* invstd, const float* gamma, int B, int C, double ntot, float* dXpre,
+                             short* dXpre16, float* dgamma, float* dbeta, float* dw, float* colpart,
+                             const double* part_pre, void* ws, void* stream, long long img_lo);
 extern "C" int fbn_bn_bwd_fused(const float* G, const float* gvec, const float* w, const float* hact,
                                 const short* hact16, float scale, const float* Xpre, const float* mean,
                                 const float* invstd, const float* gamma, int B, int C, double ntot, float* dXpre,
                                 short* dXpre16, float* dgamma, float* dbeta, float* dw, float* colpart,
                                 const double* part_pre, void* ws, void* stream) {
+  return bn_bwd_fused_impl(G, gvec, w, hact, hact16, scale, Xpre, mean, invstd, gamma, B, C, ntot, dXpre, dXpre16,
+                           dgamma, dbeta, dw, colpart, part_pre, ws, stream, 0);
+}
+// fbn_bn_bwd_fused with dXpre_img = split images of dXpre (hi, lo B*C elements further; bf16_fwd)
+extern "C" int fbn_bn_bwd_fused_img(const float* G, const float* gvec, const float* w, const float* hact,
+                                    const short* hact16, float scale, const float* Xpre, const float* mean,
+                                    const float* invstd, const float* gamma, int B, int C, double ntot, float* dXpre,
+                                    void* dXpre_img, float* dgamma, float* dbeta, float* dw, float* colpart,
+                                    const double* part_pre, void* ws, void* stream) {
+  if (!dXpre_img) { fbn_set_error("fbn_bn_bwd_fused_img: dXpre_img"); return FBN_ERR_ARG; }
+  return bn_bwd_fused_impl(G, gvec, w, hact, hact16, scale, Xpre, mean, invstd, gamma, B, C, ntot, dXpre,
+                           (short*)dXpre_img, dgamma, dbeta, dw, colpart, part_pre, ws, stream, (long long)B * C);
+}
+static int bn_bwd_fused_impl(const float* G, const float* gvec, const float* w, const float* hact,
+                             const short* hact16, float scale, const float* Xpre, const float* mean,
+                             const float* invstd, const float* gamma, int B, int C, double ntot, float* dXpre,
+                             short* dXpre16, float* dgamma, float* dbeta, float* dw, float* colpart,
+                             const double* part_pre, void* ws, void* stream, long long img_lo) {
   if (B <= 0) return FBN_OK;
   if (C & 3) { fbn_set_error("fbn_bn_bwd_fused: C % 4"); return FBN_ERR_ARG; }
   if (!hact && !(hact16 && G)) {
@@ -1344,7 +1392,7 @@ extern "C" int fbn_bn_bwd_fused(const float* G, const float* gvec, const float* 
   }
   if (!dXpre && !dXpre16) { fbn_set_error("fbn_bn_bwd_fused: no output"); return FBN_ERR_ARG; }
   hipStream_t st = (hipStream_t)stream;
-  BnBwdSrc s{G, gvec, w, hact, scale, hact16};
+  BnBwdSrc s{G, gvec, w, hact, scale, hact16, img_lo};
   const int nch = bn_bwd_chunks(B, C), rpc = (B + nch - 1) / nch;
   double* part = (double*)ws;
   float* coef = (float*)((double*)ws + (size_t)nch * 3 * C + 3 * (size_t)C);

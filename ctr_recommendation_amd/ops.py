@@ -137,17 +137,19 @@ def gemm_s3(A, B, C, M, N, K0, lda, ldb, ldc, transA, transB, beta=0.0, stream=N
 
 
 def bf16_weights(p: Dict[str, torch.Tensor], d: int, a: Dict[str, torch.Tensor], stream,
-                 x: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+                 x: Optional[torch.Tensor] = None, images: bool = False) -> Dict[str, torch.Tensor]:
     """bf16 images of the GEMM weights, laid out so every bf16 GEMM operand is K-contiguous:
     Wa_nz [512,15d] (zero columns dropped) and its transpose, Wb and Wb^T, W and W^T, Wp;
-    plus x (the batch's item_emb_d128, [B,128]) when given -- all in one launch."""
-    jobs, n, out = bf16_weight_jobs(p, d, a, x)
+    plus x (the batch's item_emb_d128, [B,128]) when given -- all in one launch.  images (bf16_fwd
+    training): Wa^T, Wb^T, W and x also get their lo image (a["s3w_<name>"] = [2, ...]: hi, lo), the
+    split-bf16 x3 backward's operands, from the same read."""
+    jobs, n, out = bf16_weight_jobs(p, d, a, x, images)
     call("fbn_convert_bf16", ctypes.cast(jobs, ctypes.c_void_p).value, n, stream)
     return out
 
 
 def bf16_weight_jobs(p: Dict[str, torch.Tensor], d: int, a: Dict[str, torch.Tensor],
-                     x: Optional[torch.Tensor] = None):
+                     x: Optional[torch.Tensor] = None, images: bool = False):
     """(job records, count, images) of bf16_weights, for a launch that carries the conversion
     (fbn_convert_bf16, or the step head fbn_adam_claim_catchup_conv); the records live in a["_conv_jobs"]."""
     dev = p["mlp.0.weight"].device
@@ -166,13 +168,16 @@ def bf16_weight_jobs(p: Dict[str, torch.Tensor], d: int, a: Dict[str, torch.Tens
     _lib.keep(jobs)               # its address is passed as an integer (step programs keep it alive)
     out = {}
     for i, (name, src, rows, cols, ld, trans, rm) in enumerate(spec):
-        key = "w16_" + name
+        img = images and name in ("WaT", "WbT", "W", "x")
+        key = ("s3w_" if img else "w16_") + name
+        shape = (2, rows, cols) if img else (rows, cols)
         t = a.get(key)
-        if t is None or tuple(t.shape) != (rows, cols):
-            t = _lib.persistent(lambda: torch.empty((rows, cols), dtype=torch.bfloat16, device=dev))
+        if t is None or tuple(t.shape) != shape:
+            t = _lib.persistent(lambda: torch.empty(shape, dtype=torch.bfloat16, device=dev))
             a[key] = t
-        out[name] = t
-        jobs[i] = _ConvJob(src.data_ptr(), t.data_ptr(), rows, cols, ld, trans, rm[0], rm[1], rm[2])
+        out[name] = t[0] if img else t
+        jobs[i] = _ConvJob(src.data_ptr(), t.data_ptr(), rows, cols, ld, trans, rm[0], rm[1], rm[2],
+                           2 if img else 0, 0, rows * cols if img else 0)
     return jobs, len(spec), out
 
 
@@ -374,7 +379,7 @@ def bn_train_stats(h, B, C, mean, invstd, run_mean, run_var, ntot, coll: Collect
 
 def bn_backward(G, gvec, w, hact, scale, hpre, mean, invstd, gamma, B, C, ntot, dpre, dgamma, dbeta, dw,
                 coll: Collective, stream, dpre16=None, bias_grad=None, sums: Optional[DeferredSums] = None,
-                hact16=None, part_pre=None, tag: str = ""):
+                hact16=None, part_pre=None, tag: str = "", dpre_img=None):
     """BN (+ReLU/dropout) backward; bias_grad (with sums): the preceding Linear's bias gradient
     = column sums of dpre, finalised later by sums.flush().  tag names the layer ("bn1" / "bn2"):
     its cached workspace and bias-gradient partials are the layer's own, so two BatchNorm layers of
@@ -382,7 +387,8 @@ def bn_backward(G, gvec, w, hact, scale, hpre, mean, invstd, gamma, B, C, ntot, 
 
     Single process only: hact may be None with hact16 (the bf16 activation image; a matrix source
     G needs only its sign) and dpre may be None when dpre16 is given (bf16 mode: nothing reads the
-    f32 gradient, the bias gradient comes from the apply's column partials)."""
+    f32 gradient, the bias gradient comes from the apply's column partials).  dpre_img (single process,
+    bf16_fwd): the bf16 output as split images [2, B, C] (hi, lo) instead of dpre16."""
     dev = hpre.device
     cache = sums.cache if sums is not None and sums.cache is not None else {}
     nws = _lib.lib().fbn_bn_workspace_size(B, C)
@@ -399,9 +405,10 @@ def bn_backward(G, gvec, w, hact, scale, hpre, mean, invstd, gamma, B, C, ntot, 
                 part = cache[f"bn_part_{key}"] = _lib.persistent(
                     lambda: torch.empty((nch, C), dtype=torch.float32, device=dev))
             sums.add(part, nch, C, bias_grad)
-        call("fbn_bn_bwd_fused", ptr(G), ptr(gvec), ptr(w), ptr(hact), ptr(hact16), float(scale), ptr(hpre),
-             ptr(mean), ptr(invstd), ptr(gamma), B, C, float(ntot), ptr(dpre), ptr(dpre16), ptr(dgamma), ptr(dbeta),
-             ptr(dw), ptr(part), ptr(part_pre), ptr(ws), stream)
+        call("fbn_bn_bwd_fused_img" if dpre_img is not None else "fbn_bn_bwd_fused", ptr(G), ptr(gvec), ptr(w),
+             ptr(hact), ptr(hact16), float(scale), ptr(hpre), ptr(mean), ptr(invstd), ptr(gamma), B, C, float(ntot),
+             ptr(dpre), ptr(dpre_img if dpre_img is not None else dpre16), ptr(dgamma), ptr(dbeta), ptr(dw), ptr(part),
+             ptr(part_pre), ptr(ws), stream)
         return
     assert hact is not None and dpre is not None, "SyncBN backward reads the f32 activation and gradient"
     red = torch.empty(3 * C, dtype=torch.float64, device=dev)
@@ -463,7 +470,10 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     f16 = cfg.fwd16 and not bf            # bf16 forward GEMM operands only
     g16 = bf or f16                       # the forward GEMMs take bf16 operands
     # w16_ready: the caller already converted this step's bf16 images (a["w16"]) on another stream
-    w16 = (a["w16"] if w16_ready else bf16_weights(p, d, a, st, x=x_mm)) if g16 else None
+    # bf16_fwd training: the weight images carry their lo image too (the split-bf16 x3 backward)
+    s3w = f16 and _SPLIT3 and cfg.training and not cfg.bilinear_each
+    a["s3w"] = s3w and not w16_ready
+    w16 = (a["w16"] if w16_ready else bf16_weights(p, d, a, st, x=x_mm, images=s3w)) if g16 else None
     a["w16"] = w16
     hmm = buf("hmm", (B, d))
     gemm(w16["x"] if g16 else x_mm, w16["Wp"] if g16 else p["mm_proj.0.weight"], hmm, B, d, 128, 128, 128, d, False,
@@ -485,7 +495,7 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     # bf16_fwd training whose split-bf16 x3 backward runs every GEMM on the LDS-DMA path: c and V exist
     # only as split images (fbn_pairs_fwd_img) -- no fp32 c is written or converted
     s3img = (f16 and _SPLIT3 and cfg.training and not cfg.bilinear_each and B % 64 == 0 and d % 64 == 0
-             and _WGRAD_GROUP and _DEFER_REDUCE)
+             and _WGRAD_GROUP and _DEFER_REDUCE and coll.world <= 1)
     a["s3img"] = s3img
     av = buf("a", (B, 6))
     cnt = buf("cnt", (B,))
@@ -606,10 +616,21 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
              H1, BN_EPS, st)
     # bf16, one process: the f32 activation has no reader (layer 2 and its weight gradient take
     # the bf16 image, the BN backward only its sign), so it is not written
-    lean = bf and coll.world <= 1
+    lean = (bf or s3img) and coll.world <= 1
     a["lean_h1"] = lean
-    call("fbn_bn_act_fwd", ptr(h1pre), None if lean else ptr(h1), B, H1, ptr(mean1), ptr(inv1), ptr(p["mlp.1.weight"]),
-         ptr(p["mlp.1.bias"]), float(p_drop), ptr(rng), 1, ptr(m1), ptr(mi1), ptr(h1_16), st)
+    if s3img:
+        # h1 only as split images: hi = the layer-2 GEMM operand, both = the split-bf16 x3 dWb operand;
+        # the BN1 backward takes the ReLU / dropout mask from hi's sign
+        a["s3_h1"] = buf("s3_h1_fwd", (2, B, H1), torch.bfloat16)
+        h1_16 = a["s3_h1"][0]
+        a["h1_16"] = h1_16
+        call("fbn_bn_act_fwd_img", ptr(h1pre), None if lean else ptr(h1), B, H1, ptr(mean1), ptr(inv1),
+             ptr(p["mlp.1.weight"]), ptr(p["mlp.1.bias"]), float(p_drop), ptr(rng), 1, ptr(m1), ptr(mi1),
+             ptr(a["s3_h1"]), st)
+    else:
+        call("fbn_bn_act_fwd", ptr(h1pre), None if lean else ptr(h1), B, H1, ptr(mean1), ptr(inv1),
+             ptr(p["mlp.1.weight"]), ptr(p["mlp.1.bias"]), float(p_drop), ptr(rng), 1, ptr(m1), ptr(mi1), ptr(h1_16),
+             st)
     if g16:
         gemm(h1_16, w16["Wb"], h2pre, B, H2, H1, H1, H1, H2, False, True, bias=p["mlp.4.bias"], bf16=True, stream=st,
              stats=t2)
@@ -719,20 +740,33 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     # (split_images; fbn_gemm_s3 / split-bf16 x3 slabs) where the LDS-DMA path takes the shape, else
     # the fp32 MFMA
     s3 = cfg.fwd16 and _SPLIT3 and not bf and not cfg.bilinear_each
+    # ... with every operand image made by its producing kernel (forward: fbn_pairs_fwd_img,
+    # fbn_bn_act_fwd_img, the weight conversion; here: the BN backward, fbn_pairs_bwd_img): no fp32
+    # dh2 / dh1 / dU and no conversion pass but dhmm's
+    s3img = s3 and bool(a.get("s3img"))
     im = {}
 
     def img(name, rows, cols):
         return tmp("s3_" + name, (2, rows, cols), torch.bfloat16)
 
     if s3:
-        # the operands the forward left and the weights: ONE launch
-        im = {"WbT": img("WbT", H1, H2), "WaT": img("WaT", KC, H1), "W": img("W", d, d),
-              "h1": img("h1", B, H1), "x": img("x", B, 128)}
-        jobs = [(p["mlp.4.weight"], im["WbT"], H1, H2, H1, 1, NO_REMAP),
-                (p["mlp.0.weight"], im["WaT"], KC, H1, 21 * d, 1, wa_remap(d)),
-                (p["bilinear.W"], im["W"], d, d, d, 0, NO_REMAP),
-                (a["h1"], im["h1"], B, H1, H1, 0, NO_REMAP),
-                (batch["item_emb_d128"], im["x"], B, 128, 128, 0, NO_REMAP)]
+        # the operands the forward left and the weights: ONE launch (none when the forward made them)
+        jobs = []
+        for name, src, rows, cols, ld, trans, rm in (("WbT", p["mlp.4.weight"], H1, H2, H1, 1, NO_REMAP),
+                                                     ("WaT", p["mlp.0.weight"], KC, H1, 21 * d, 1, wa_remap(d)),
+                                                     ("W", p["bilinear.W"], d, d, d, 0, NO_REMAP),
+                                                     ("x", batch["item_emb_d128"], B, 128, 128, 0, NO_REMAP)):
+            t = a.get("s3w_" + name) if a.get("s3w") else None
+            if t is not None and tuple(t.shape) == (2, rows, cols):
+                im[name] = t                        # the forward's weight conversion wrote both images
+            else:
+                im[name] = img(name, rows, cols)
+                jobs.append((src, im[name], rows, cols, ld, trans, rm))
+        if s3img:
+            im["h1"] = a["s3_h1"]                   # fbn_bn_act_fwd_img
+        else:
+            im["h1"] = img("h1", B, H1)
+            jobs.append((a["h1"], im["h1"], B, H1, H1, 0, NO_REMAP))
         if a.get("s3img"):
             im["Vc"] = a["s3_vc"]                   # written by fbn_pairs_fwd_img
         else:
@@ -743,15 +777,18 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
         else:
             im["c"] = img("c", B, KC)
             jobs.append((a["c"], im["c"], B, KC, KC, 0, NO_REMAP))
-        split_images(jobs, st)
-    dh2pre = None if lean else tmp("dh2pre", (B, H2))
+        if jobs:
+            split_images(jobs, st)
+    dh2pre = None if (lean or s3img) else tmp("dh2pre", (B, H2))
+    dh2 = img("dh2", B, H2) if s3 else None
     dh2pre16 = tmp("dh2pre16", (B, H2), torch.bfloat16) if bf else None
     sums = DeferredSums(a)
     wg = _SideWork(side, dev)
     bn_backward(None, gout, p["mlp.8.weight"], a["h2"], scale, a["h2pre"], a["mean2"], a["inv2"],
                 p["mlp.5.weight"], B, H2, ntot, dh2pre, g["mlp.5.weight"], g["mlp.5.bias"], g["mlp.8.weight"],
                 coll, st, dpre16=dh2pre16, bias_grad=g["mlp.4.bias"], sums=sums,
-                part_pre=a.get("bn2_bwd_part") if (gout is a.get("gout")) else None, tag="bn2")
+                part_pre=a.get("bn2_bwd_part") if (gout is a.get("gout")) else None, tag="bn2",
+                dpre_img=dh2 if s3img else None)
     sums.add(gout, B, 1, g["mlp.8.bias"])
     dh1 = tmp("dh1", (B, H1))
     part1 = None
@@ -771,8 +808,8 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
         else:
             gemm(dh2pre16, w16["WbT"], dh1, B, H1, H2, H2, H2, H1, False, True, stream=st)
     elif s3:
-        dh2 = img("dh2", B, H2)
-        split_images([(dh2pre, dh2, B, H2, H2, 0, NO_REMAP)], st)
+        if not s3img:
+            split_images([(dh2pre, dh2, B, H2, H2, 0, NO_REMAP)], st)
         if not sums.gemm_slabs(dh2, im["h1"], g["mlp.4.weight"], H2, H1, B, H2, H1, H1, True, False, stream=st,
                                s3=True):
             if s3_ok(H2, H1, B, H2, H1, True, False):
@@ -789,16 +826,17 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
         wg.run(lambda s: gemm(dh2pre, a["h1"], g["mlp.4.weight"], H2, H1, B, H2, H1, H1, True, False, bf16=sb,
                               stream=s))
         gemm(dh2pre, p["mlp.4.weight"], dh1, B, H1, H2, H2, H1, H1, False, False, bf16=sb, stream=st)
-    dh1pre = None if lean else tmp("dh1pre", (B, H1))
+    dh1pre = None if (lean or s3img) else tmp("dh1pre", (B, H1))
     dh1pre16 = tmp("dh1pre16", (B, H1), torch.bfloat16) if bf else None
+    dh1i = img("dh1", B, H1) if s3 else None
     bn_backward(dh1, None, None, None if lean_h1 else a["h1"], scale, a["h1pre"], a["mean1"], a["inv1"],
                 p["mlp.1.weight"], B, H1, ntot, dh1pre, g["mlp.1.weight"], g["mlp.1.bias"], None, coll, st,
                 dpre16=dh1pre16, bias_grad=g["mlp.0.bias"], sums=sums, hact16=a["h1_16"] if lean_h1 else None,
-                part_pre=part1, tag="bn1")
+                part_pre=part1, tag="bn1", dpre_img=dh1i if s3img else None)
     # weight gradient of the MLP input layer (side work), then its dgrad dc
     if s3:
-        dh1i = img("dh1", B, H1)
-        split_images([(dh1pre, dh1i, B, H1, H1, 0, NO_REMAP)], st)
+        if not s3img:
+            split_images([(dh1pre, dh1i, B, H1, H1, 0, NO_REMAP)], st)
         if not sums.gemm_slabs(dh1i, im["c"], g["mlp.0.weight"], H1, KC, B, H1, KC, 21 * d, True, False,
                                rC=wa_remap(d), stream=st, s3=True):
             wg.run(lambda s: gemm(dh1pre, a["c"], g["mlp.0.weight"], H1, KC, B, H1, KC, 21 * d, True, False,

@@ -221,6 +221,11 @@ int fbn_bn_eval_params(const float* run_mean, const float* run_var, float* mean,
 int fbn_bn_act_fwd(const float* X, float* Y, int B, int C, const float* mean, const float* invstd, const float* g,
                    const float* b, float p_drop, const unsigned long long* rng, unsigned stream_id,
                    unsigned char* mask_out, const unsigned char* mask_in, short* Y16, void* stream);
+/* fbn_bn_act_fwd with the bf16 output as split images (bf16_fwd training): Y_img = bf16(y) (the
+ * layer-2 GEMM operand), lo = bf16(y - hi) B*C elements further; Y (fp32) may be null. */
+int fbn_bn_act_fwd_img(const float* X, float* Y, int B, int C, const float* mean, const float* invstd, const float* g,
+                       const float* b, float p_drop, const unsigned long long* rng, unsigned stream_id,
+                       unsigned char* mask_out, const unsigned char* mask_in, void* Y_img, void* stream);
 /* fbn_bn_act_fwd of the last hidden layer (C = 256) fused with fbn_head_fwd (same outputs).
  * bwd_part (optional, with labels / gout; fbn_bn_bwd_chunks(B, C) * 3 * C doubles): the first pass
  * of this layer's BN backward (rank-1 source gout x hw, dropout scale bwd_scale), handed to
@@ -252,6 +257,12 @@ int fbn_bn_bwd_fused(const float* G, const float* gvec, const float* w, const fl
                      float scale, const float* Xpre, const float* mean, const float* invstd, const float* gamma, int B,
                      int C, double ntot, float* dXpre, short* dXpre16, float* dgamma, float* dbeta, float* dw,
                      float* colpart, const double* part_pre, void* ws, void* stream);
+/* fbn_bn_bwd_fused with the bf16 output as split images (bf16_fwd training): dXpre_img = bf16(dx),
+ * lo = bf16(dx - hi) B*C elements further -- the operands of the split-bf16 x3 backward GEMMs. */
+int fbn_bn_bwd_fused_img(const float* G, const float* gvec, const float* w, const float* hact, const short* hact16,
+                         float scale, const float* Xpre, const float* mean, const float* invstd, const float* gamma,
+                         int B, int C, double ntot, float* dXpre, void* dXpre_img, float* dgamma, float* dbeta,
+                         float* dw, float* colpart, const double* part_pre, void* ws, void* stream);
 /* bf16 images: jobs = host array of n <= 16 records
  * {const float* src; short* dst; int rows, cols, ld, trans, seg, off0, off1, part, dld, pst;}
  * x = trans ? src[j*ld + rm(i)] : src[i*ld + rm(j)], rm(x) = x + (x < seg ? off0 : off1);
