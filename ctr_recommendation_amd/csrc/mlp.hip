@@ -42,6 +42,13 @@ __device__ __forceinline__ void store_img4(short* p, long long lo_off, const f32
   *reinterpret_cast<bf16x4*>(p) = h;
   *reinterpret_cast<bf16x4*>(p + lo_off) = l;
 }
+// the lo image alone (its hi image written elsewhere)
+__device__ __forceinline__ void store_lo4(short* p, const f32x4& v) {
+  bf16x4 l;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) l[e] = f2bf(v[e] - bf2f(f2bf(v[e])));
+  *reinterpret_cast<bf16x4*>(p) = l;
+}
 // V from the fp32 fields (fp32 mode) or from their bf16 copy (bf16 mode: the fp32 copy is not
 // written at all; U = V W is computed from the same bf16 V by the GEMM)
 __device__ __forceinline__ f32x4 load_v4(const float* __restrict__ V, const short* __restrict__ V16, size_t off) {
@@ -74,9 +81,10 @@ __global__ void pairs_fwd_kernel(const float* __restrict__ Vc, const short* __re
   }
 }
 
-// bf16_fwd training, bilinear "all": the MLP input c = [V | pairs] and the fields V written only as
-// split images (c: [B][ldc] hi + lo B ldc further; V: [B][5][D] hi + lo 5 B D further) -- the
-// layer-1 GEMM reads c's hi image, the backward's split-bf16 x3 GEMMs both
+// bf16_fwd training, bilinear "all": the MLP input c = [V | pairs] written only as split images
+// (c: [B][ldc] hi + lo B ldc further) -- the layer-1 GEMM reads c's hi image, the backward's
+// split-bf16 x3 GEMMs both -- and the lo image of the fields V (vi: [B][5][D] hi, written by the
+// gather as its bf16 copy; lo 5 B D further, written here)
 __global__ void pairs_fwd_img_kernel(const float* __restrict__ Vc, const float* __restrict__ U, short* __restrict__ ci,
                                      short* __restrict__ vi, int B, int D, int ldc) {
   const int q4 = D / 4;
@@ -94,7 +102,7 @@ __global__ void pairs_fwd_img_kernel(const float* __restrict__ Vc, const float* 
 #pragma unroll
     for (int f = 0; f < 5; ++f) {
       store_img4(out + f * D, clo, v[f]);
-      if (vi) store_img4(vi + ((size_t)b * 5 + f) * D + col, vlo, v[f]);
+      if (vi) store_lo4(vi + vlo + ((size_t)b * 5 + f) * D + col, v[f]);
     }
 #pragma unroll
     for (int k = 0; k < 10; ++k) store_img4(out + (5 + k) * D, clo, v[c_pi[k]] * u[c_pj[k]]);

@@ -497,6 +497,11 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     s3img = (f16 and _SPLIT3 and cfg.training and not cfg.bilinear_each and B % 64 == 0 and d % 64 == 0
              and _WGRAD_GROUP and _DEFER_REDUCE and coll.world <= 1)
     a["s3img"] = s3img
+    if s3img:
+        # V's split images: hi = the gather's bf16 copy (the U = V W GEMM's operand), lo from the
+        # pair kernel
+        a["s3_vc"] = buf("s3_vc_fwd", (2, 5 * B, d), torch.bfloat16)
+        Vc16 = a["s3_vc"][0].view(B, 5, d)
     av = buf("a", (B, 6))
     cnt = buf("cnt", (B,))
     if err is None:
@@ -551,6 +556,8 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     elif not cfg.bilinear_each:
         if bf:   # B(k,n) = W[k][n]: K-contiguous image is W^T
             gemm(Vc16, w16["WT"], U, 5 * B, d, d, d, d, d, False, True, bf16=True, stream=st)
+        elif f16 and s3img:   # the gather's bf16 copy of the fields (= rounded on load), LDS-DMA path
+            gemm(Vc16, w16["WT"], U, 5 * B, d, d, d, d, d, False, True, bf16=True, stream=st)
         elif f16:   # the fp32 fields rounded to bf16 on load
             gemm(Vc, w16["WT"], U, 5 * B, d, d, d, d, d, False, True, bf16=True, stream=st)
         else:
@@ -562,7 +569,6 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
                  bf16=bf, stream=st)
     if s3img:
         a["s3_c"] = buf("s3_c_fwd", (2, B, KC), torch.bfloat16)
-        a["s3_vc"] = buf("s3_vc_fwd", (2, 5 * B, d), torch.bfloat16)
         call("fbn_pairs_fwd_img", ptr(Vc), ptr(U), ptr(a["s3_c"]), ptr(a["s3_vc"]), B, d, KC, st)
     elif not fused_bil:
         call("fbn_pairs_fwd", ptr(Vc), ptr(Vc16), ptr(U), ptr(c), B, d, KC, int(cfg.bilinear_each), int(bf), st)

@@ -181,9 +181,10 @@ int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, const int64_
 int fbn_pairs_fwd(const float* Vc, const short* Vc16, const float* U, void* c, int B, int D, int ldc, int mode,
                   int c_bf16, void* stream);
 /* bf16_fwd training, bilinear "all" (src/model_fibinet.py:60-66 pair products): the MLP input c =
- * [V | pairs] and the fields V written ONLY as split-bf16 images (bf16 hi at c_img[b*ldc + j], lo =
- * bf16(x - hi) B*ldc elements further; vc_img: [B][5][D] hi, lo 5*B*D further; vc_img may be null) --
- * the operands of the layer-1 GEMM (hi) and of fbn_gemm_s3 / the split-bf16 x3 slab GEMMs. */
+ * [V | pairs] written ONLY as split-bf16 images (bf16 hi at c_img[b*ldc + j], lo = bf16(x - hi)
+ * B*ldc elements further) -- the operands of the layer-1 GEMM (hi) and of fbn_gemm_s3 / the
+ * split-bf16 x3 slab GEMMs; and the lo image of V (vc_img: [B][5][D] hi = fbn_fields_fwd's Vc16,
+ * lo 5*B*D further, written here; vc_img may be null). */
 int fbn_pairs_fwd_img(const float* Vc, const float* U, void* c_img, void* vc_img, int B, int D, int ldc, void* stream);
 /* fbn_pairs_bwd (bilinear "all") with dU written only as split-bf16 images (hi [B][5][D], lo 5*B*D
  * elements further). */
