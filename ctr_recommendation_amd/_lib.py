@@ -64,6 +64,8 @@ SIGNATURES = {
     "fbn_fields_bwd_grid": (I, [I, I]),
     "fbn_fields_bwd": (I, [P, P, P, P, P, P, P, F, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P, P, P, LL, P, P, I, I,
                            I, I, P]),
+    "fbn_fields_bwd_img": (I, [P, P, P, P, P, P, P, F, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P, P, P, LL, P, P, I,
+                               I, I, I, P]),
     "fbn_pairs_fwd": (I, [P, P, P, P, I, I, I, I, I, P]),
     "fbn_pairs_bwd": (I, [P, P, P, P, P, P, P, I, I, I, I, P]),
     "fbn_pairs_fwd_img": (I, [P, P, P, P, I, I, I, P]),

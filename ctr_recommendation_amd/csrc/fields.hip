@@ -365,6 +365,7 @@ struct FieldBwdArgs {
   const float* dV;     // [B][5][D] total gradient wrt V_1..V_5
   float* dhmm;         // [B][D] gradient wrt the pre-LN projection
   short* dhmm16;       // optional bf16 copy (operand of the mm_proj weight-gradient GEMM)
+  long long dhmm16_lo; // > 0: dhmm16 is split images (hi, lo this many elements further; bf16_fwd)
   float* partials;     // [gridDim.x][P]; P = 6R + R + 6R + 6 + 2D + n_cate*D
   // table gradient, mode 0: dense gtab[V][D] (atomics) if gvec == null; otherwise the two
   // per-sample vectors gvec[b][0] = dX3 (item row), gvec[b][1] = dX5/count (each history row)
@@ -552,9 +553,14 @@ __global__ void __launch_bounds__(256) fields_bwd_kernel(FieldBwdArgs p) {
         for (int e = 0; e < 4; ++e) out[e] = rstd * (gx[e] - m1 - xh[e] * m2);
         *reinterpret_cast<f32x4*>(p.dhmm + (size_t)b * D + 4 * q) = out;
         acc_hb += out;                              // mm_proj.0.bias gradient (sum over the batch)
-        if (p.dhmm16)
-          *reinterpret_cast<bf16x4*>(p.dhmm16 + (size_t)b * D + 4 * q) = (bf16x4){f2bf(out[0]), f2bf(out[1]),
-                                                                                   f2bf(out[2]), f2bf(out[3])};
+        if (p.dhmm16) {
+          const bf16x4 hi = (bf16x4){f2bf(out[0]), f2bf(out[1]), f2bf(out[2]), f2bf(out[3])};
+          *reinterpret_cast<bf16x4*>(p.dhmm16 + (size_t)b * D + 4 * q) = hi;
+          if (p.dhmm16_lo)
+            *reinterpret_cast<bf16x4*>(p.dhmm16 + p.dhmm16_lo + (size_t)b * D + 4 * q) =
+                (bf16x4){f2bf(out[0] - bf2f(hi[0])), f2bf(out[1] - bf2f(hi[1])), f2bf(out[2] - bf2f(hi[2])),
+                         f2bf(out[3] - bf2f(hi[3]))};
+        }
       }
       // item table: dX3 -> row item_id, dX5 / count -> each non-padding history row
       const f32x4 gh = dx[4] / p.cnt[b];
@@ -879,6 +885,13 @@ static int launch_fields_bwd(const FieldBwdArgs& a, int D, hipStream_t st) {
 // param_grads: host array of 8 device pointers receiving the gradients of w1, b1, w2, b2, ln_g,
 // ln_b, cate, mm_proj bias (segments of 6R, R, 6R, 6, D, D, n_cate*D, D columns of a partial row),
 // or NULL: the partial rows are left for the caller to sum (the trainer's one fbn_sum_jobs2 launch).
+static int fields_bwd_impl(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes,
+                           const int64_t* views, const float* hmm, const float* ln_g, const float* ln_b,
+                           float ln_eps, const float* w1, const float* b1, const float* w2, int R, int n_cate,
+                           const float* cate, const float* X, const float* a, const float* cnt, const float* dV,
+                           float* dhmm, short* dhmm16, float* partials, float* const* param_grads, float* gtab,
+                           float* gvec, double* gnorm, long long V, const int* pos, void* sendbuf, int send_bf16,
+                           int B, int L, int D, void* stream, long long dhmm16_lo);
 extern "C" int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes,
                               const int64_t* views, const float* hmm, const float* ln_g, const float* ln_b,
                               float ln_eps, const float* w1, const float* b1, const float* w2, int R, int n_cate,
@@ -886,12 +899,37 @@ extern "C" int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, c
                               short* dhmm16, float* partials, float* const* param_grads, float* gtab, float* gvec,
                               double* gnorm, long long V, const int* pos, void* sendbuf, int send_bf16, int B,
                               int L, int D, void* stream) {
+  return fields_bwd_impl(item_id, item_seq, likes, views, hmm, ln_g, ln_b, ln_eps, w1, b1, w2, R, n_cate, cate, X, a,
+                         cnt, dV, dhmm, dhmm16, partials, param_grads, gtab, gvec, gnorm, V, pos, sendbuf, send_bf16, B,
+                         L, D, stream, 0);
+}
+// fbn_fields_bwd with dhmm_img = split images of dhmm (hi, lo B*D elements further; bf16_fwd training)
+extern "C" int fbn_fields_bwd_img(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes,
+                                  const int64_t* views, const float* hmm, const float* ln_g, const float* ln_b,
+                                  float ln_eps, const float* w1, const float* b1, const float* w2, int R, int n_cate,
+                                  const float* cate, const float* X, const float* a, const float* cnt, const float* dV,
+                                  float* dhmm, void* dhmm_img, float* partials, float* const* param_grads,
+                                  float* gtab, float* gvec, double* gnorm, long long V, const int* pos, void* sendbuf,
+                                  int send_bf16, int B, int L, int D, void* stream) {
+  if (!dhmm_img) { fbn_set_error("fbn_fields_bwd_img: dhmm_img"); return FBN_ERR_ARG; }
+  return fields_bwd_impl(item_id, item_seq, likes, views, hmm, ln_g, ln_b, ln_eps, w1, b1, w2, R, n_cate, cate, X, a,
+                         cnt, dV, dhmm, (short*)dhmm_img, partials, param_grads, gtab, gvec, gnorm, V, pos, sendbuf,
+                         send_bf16, B, L, D, stream, (long long)B * D);
+}
+static int fields_bwd_impl(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes,
+                           const int64_t* views, const float* hmm, const float* ln_g, const float* ln_b,
+                           float ln_eps, const float* w1, const float* b1, const float* w2, int R, int n_cate,
+                           const float* cate, const float* X, const float* a, const float* cnt, const float* dV,
+                           float* dhmm, short* dhmm16, float* partials, float* const* param_grads, float* gtab,
+                           float* gvec, double* gnorm, long long V, const int* pos, void* sendbuf, int send_bf16,
+                           int B, int L, int D, void* stream, long long dhmm16_lo) {
   if (B <= 0) return FBN_OK;
   if (L < 0 || L > 32 || R < 1 || R > FBN_MAXR) { fbn_set_error("fbn_fields_bwd: bad L/R"); return FBN_ERR_ARG; }
   FieldBwdArgs p;
   p.item_id = item_id; p.item_seq = L > 0 ? item_seq : nullptr; p.likes = likes; p.views = views;
   p.hmm = hmm; p.ln_g = ln_g; p.ln_b = ln_b; p.w1 = w1; p.b1 = b1; p.w2 = w2; p.cate = cate;
   p.X = X; p.a = a; p.cnt = cnt; p.dV = dV; p.dhmm = dhmm; p.dhmm16 = dhmm16; p.partials = partials;
+  p.dhmm16_lo = dhmm16_lo;
   p.gtab = gtab; p.gvec = gvec; p.gnorm = gvec ? gnorm : nullptr; p.pos = pos; p.sendbuf = sendbuf;
   p.V = V; p.B = B; p.L = L; p.R = R; p.n_cate = n_cate; p.ln_eps = ln_eps;
   hipStream_t st = (hipStream_t)stream;

@@ -933,6 +933,7 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     partials = tmp("partials", (nblk, P))
     dhmm = tmp("dhmm", (B, d))
     dhmm16 = tmp("dhmm16", (B, d), torch.bfloat16) if bf else None
+    dhs = img("dhmm", B, d) if s3 else None
     seq = batch.get("item_seq", None)
     Lr = 0 if seq is None else L
     V = p["item_emb.weight"].shape[0] if pos is None else 0
@@ -949,10 +950,12 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
         _lib.keep(outs_arr)
         outs = ctypes.cast(outs_arr, ctypes.c_void_p).value
     evb = _probe_start(probe, "fields_bwd")     # bench / tools: the fields backward
-    call("fbn_fields_bwd", ptr(batch["item_id"]), ptr(seq) if Lr else None, ptr(batch["likes_level"]),
+    call("fbn_fields_bwd_img" if s3img else "fbn_fields_bwd", ptr(batch["item_id"]), ptr(seq) if Lr else None,
+         ptr(batch["likes_level"]),
          ptr(batch["views_level"]), ptr(a["hmm"]), ptr(p["mm_proj.1.weight"]), ptr(p["mm_proj.1.bias"]), LN_EPS,
          ptr(p["senet.excitation.0.weight"]), ptr(p["senet.excitation.0.bias"]), ptr(p["senet.excitation.2.weight"]),
-         R, ncate, ptr(p["cate_emb.weight"]), ptr(a["X"]), ptr(a["a"]), ptr(a["cnt"]), ptr(dV), ptr(dhmm), ptr(dhmm16), ptr(partials), outs,
+         R, ncate, ptr(p["cate_emb.weight"]), ptr(a["X"]), ptr(a["a"]), ptr(a["cnt"]), ptr(dV), ptr(dhmm),
+         ptr(dhs if s3img else dhmm16), ptr(partials), outs,
          ptr(table_grad), ptr(gvec), ptr(gnorm), V, ptr(pos), ptr(sendbuf),
          int(sendbuf is not None and sendbuf.dtype == torch.bfloat16), B, Lr, d, st)
     _probe_end(evb)
@@ -964,8 +967,8 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
             wg.run(lambda s: gemm(dhmm16, w16["x"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True, False,
                                   stream=s))
     elif s3:
-        dhs = img("dhmm", B, d)
-        split_images([(dhmm, dhs, B, d, d, 0, NO_REMAP)], st)
+        if not s3img:
+            split_images([(dhmm, dhs, B, d, d, 0, NO_REMAP)], st)
         if not sums.gemm_slabs(dhs, im["x"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True, False,
                                stream=st, s3=True):
             wg.run(lambda s: gemm(dhmm, batch["item_emb_d128"], g["mm_proj.0.weight"], d, 128, B, d, 128, 128, True,

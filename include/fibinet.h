@@ -168,6 +168,14 @@ int fbn_fields_bwd(const int64_t* item_id, const int64_t* item_seq, const int64_
                    short* dhmm16, float* partials, float* const* param_grads, float* gtab, float* gvec,
                    double* gnorm, long long V, const int* pos, void* sendbuf, int send_bf16, int B, int L, int D,
                    void* stream);
+/* fbn_fields_bwd with the bf16 copy of dhmm as split images (bf16_fwd training): dhmm_img = bf16(dhmm),
+ * lo = bf16(dhmm - hi) B*D elements further (the split-bf16 x3 mm_proj weight gradient's operand). */
+int fbn_fields_bwd_img(const int64_t* item_id, const int64_t* item_seq, const int64_t* likes, const int64_t* views,
+                       const float* hmm, const float* ln_g, const float* ln_b, float ln_eps, const float* w1,
+                       const float* b1, const float* w2, int R, int n_cate, const float* cate, const float* X,
+                       const float* a, const float* cnt, const float* dV, float* dhmm, void* dhmm_img,
+                       float* partials, float* const* param_grads, float* gtab, float* gvec, double* gnorm,
+                       long long V, const int* pos, void* sendbuf, int send_bf16, int B, int L, int D, void* stream);
 /* gnorm (optional, with gvec): [B][2] float64 sums of squares of the two per-sample vectors,
  * read by fbn_sumsq_sparse_norms for the clip_grad_norm_ total (src/train_fibinet.py:119).
  * pos / sendbuf (N > 1): one gradient row per routed entry, f32, or bf16 when send_bf16 (the bf16
