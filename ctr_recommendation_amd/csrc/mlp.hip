@@ -85,27 +85,51 @@ __global__ void pairs_fwd_kernel(const float* __restrict__ Vc, const short* __re
 // (c: [B][ldc] hi + lo B ldc further) -- the layer-1 GEMM reads c's hi image, the backward's
 // split-bf16 x3 GEMMs both -- and the lo image of the fields V (vi: [B][5][D] hi, written by the
 // gather as its bf16 copy; lo 5 B D further, written here)
+// eight columns per thread: 16-byte image stores (half the store instructions of four)
+__device__ __forceinline__ void store_img8(short* p, long long lo_off, const f32x4& a, const f32x4& b) {
+  bf16x8 h, l;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    h[e] = f2bf(a[e]);
+    h[e + 4] = f2bf(b[e]);
+    l[e] = f2bf(a[e] - bf2f(h[e]));
+    l[e + 4] = f2bf(b[e] - bf2f(h[e + 4]));
+  }
+  *reinterpret_cast<bf16x8*>(p) = h;
+  if (lo_off >= 0) *reinterpret_cast<bf16x8*>(p + lo_off) = l;
+}
 __global__ void pairs_fwd_img_kernel(const float* __restrict__ Vc, const float* __restrict__ U, short* __restrict__ ci,
                                      short* __restrict__ vi, int B, int D, int ldc) {
-  const int q4 = D / 4;
-  const size_t total = (size_t)B * q4;
+  const int q8 = D / 8;
+  const size_t total = (size_t)B * q8;
   const long long clo = (long long)B * ldc, vlo = 5LL * B * D;
   for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
-    const int b = (int)(idx / q4), col = (int)(idx % q4) * 4;
-    f32x4 v[5], u[5];
+    const int b = (int)(idx / q8), col = (int)(idx % q8) * 8;
+    f32x4 v[5][2], u[5][2];
 #pragma unroll
-    for (int f = 0; f < 5; ++f) {
-      v[f] = *reinterpret_cast<const f32x4*>(Vc + ((size_t)b * 5 + f) * D + col);
-      u[f] = *reinterpret_cast<const f32x4*>(U + ((size_t)b * 5 + f) * D + col);
-    }
+    for (int f = 0; f < 5; ++f)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        v[f][h] = *reinterpret_cast<const f32x4*>(Vc + ((size_t)b * 5 + f) * D + col + 4 * h);
+        u[f][h] = *reinterpret_cast<const f32x4*>(U + ((size_t)b * 5 + f) * D + col + 4 * h);
+      }
     short* out = ci + (size_t)b * ldc + col;
 #pragma unroll
     for (int f = 0; f < 5; ++f) {
-      store_img4(out + f * D, clo, v[f]);
-      if (vi) store_lo4(vi + vlo + ((size_t)b * 5 + f) * D + col, v[f]);
+      store_img8(out + f * D, clo, v[f][0], v[f][1]);
+      if (vi) {   // V's lo image only (its hi image is the gather's bf16 copy)
+        bf16x8 l;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = v[f][e >> 2][e & 3];
+          l[e] = f2bf(x - bf2f(f2bf(x)));
+        }
+        *reinterpret_cast<bf16x8*>(vi + vlo + ((size_t)b * 5 + f) * D + col) = l;
+      }
     }
 #pragma unroll
-    for (int k = 0; k < 10; ++k) store_img4(out + (5 + k) * D, clo, v[c_pi[k]] * u[c_pj[k]]);
+    for (int k = 0; k < 10; ++k)
+      store_img8(out + (5 + k) * D, clo, v[c_pi[k]][0] * u[c_pj[k]][0], v[c_pi[k]][1] * u[c_pj[k]][1]);
   }
 }
 
@@ -1036,11 +1060,11 @@ extern "C" int fbn_pairs_fwd(const float* Vc, const short* Vc16, const float* U,
 extern "C" int fbn_pairs_fwd_img(const float* Vc, const float* U, void* c_img, void* vc_img, int B, int D, int ldc,
                                  void* stream) {
   if (B <= 0) return FBN_OK;
-  if ((D & 3) || (ldc & 3) || ldc < 15 * D || !Vc || !U || !c_img) {
-    fbn_set_error("fbn_pairs_fwd_img: Vc, U, c_img; D, ldc multiples of 4, ldc >= 15 D");
+  if ((D & 7) || (ldc & 7) || ldc < 15 * D || !Vc || !U || !c_img) {
+    fbn_set_error("fbn_pairs_fwd_img: Vc, U, c_img; D, ldc multiples of 8, ldc >= 15 D");
     return FBN_ERR_ARG;
   }
-  fbn_launch(pairs_fwd_img_kernel, dim3(ew_grid((size_t)B * D / 4)), dim3(256), 0, (hipStream_t)stream, Vc, U,
+  fbn_launch(pairs_fwd_img_kernel, dim3(ew_grid((size_t)B * D / 8)), dim3(256), 0, (hipStream_t)stream, Vc, U,
              (short*)c_img, (short*)vc_img, B, D, ldc);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
