@@ -10,11 +10,12 @@ the programs stay valid) with full histories that overflow the calibrated block 
 trainers must read the routed-ahead overflow flag and run that step with host split sizes (the
 program trainer falls back to an eager step for it), and the replays after it go on.  The duplicate
 fold's float atomics can part two fp32 runs in the last bits, and Adam amplifies the parting over the
-23 steps (measured over runs: 6e-8 .. 3.3e-5 in the loss, up to 1.2e-4 / 2.2e-3 of the table / dense
-displacement; bf16 bit-identical): losses within 1e-5 (relative) over the first 6 steps and 1e-3 to
-the end, the tables (after the flush) within 5e-3 and the dense parameters within 2e-2 of their
-displacement.  (A program whose every replay clobbered the fold buffer -- fixed, DESIGN §7 -- showed
-8.8e-3 in the loss one step after its first replay and 2.8e-2 of the table displacement: caught.)
+23 steps (measured over runs: 6e-8 .. 4.4e-4 in the loss, up to 1.2e-3 / 2.3e-2 of the table / dense
+displacement; bf16 bit-identical: sums of a few bf16 values are exact in f32): losses within 1e-5
+(relative) over the first 6 steps and 3e-3 to the end, the tables (after the flush) within 1e-2 and
+the dense parameters within 1e-1 of their displacement.  (A program whose every replay clobbered the
+fold buffer -- fixed, DESIGN §7 -- showed 8.8e-3 in the loss one step after its first replay and
+2.8e-2 of the table displacement: caught by both.)
 """
 import ctypes
 import os
@@ -136,6 +137,6 @@ def test_sharded_step_program_matches_eager_with_overflow_fallback(hip_device, d
     diffs = [abs(a - b) / max(1.0, abs(a)) for a, b in zip(le, lp)]
     worst = max(range(len(diffs)), key=lambda k: diffs[k])
     print(f"[{dtype}] max loss diff {max(diffs):.3g}, de {res['de']:.3g}, dp {res['dp']:.3g}")
-    assert max(diffs[:6]) <= 1e-5 and max(diffs) <= 1e-3, (worst, " ".join(f"{a:.5f}/{b:.5f}" for a, b in zip(le, lp)))
-    assert res["de"] <= 5e-3, res["de"]
-    assert res["dp"] <= 2e-2, res["dp"]
+    assert max(diffs[:6]) <= 1e-5 and max(diffs) <= 3e-3, (worst, " ".join(f"{a:.5f}/{b:.5f}" for a, b in zip(le, lp)))
+    assert res["de"] <= 1e-2, res["de"]
+    assert res["dp"] <= 1e-1, res["dp"]
