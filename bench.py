@@ -694,8 +694,12 @@ def main():
                 "dtype": "bf16 forward GEMMs / fp32 backward",
                 "gemm_precision": {"bf16 operands (fp32 accumulation)": [
                     "mm_proj x W_p", "bilinear U = V W", "MLP layer 1 c W_a", "MLP layer 2 h1 W_b"],
-                    "fp32 operands": ["every backward GEMM: dh2 W_b, dW_b, dh1 W_a (dc), dW_a, dU W^T, dW, dW_p",
-                                      "all non-GEMM arithmetic, master weights, Adam"]},
+                    "fp32 operands as split-bf16 x3 (hi/lo images, A_hi B_hi + A_hi B_lo + A_lo B_hi, fp32 "
+                    "accumulation; FBN_SPLIT3=0: fp32 MFMA)": [
+                        "every backward GEMM: dh2 W_b, dW_b, dh1 W_a (dc), dW_a, dU W^T, dW, dW_p"],
+                    "fp32": ["all non-GEMM arithmetic, master weights, Adam"]},
+                # (its roofline counts the weight gradients' algorithmic flops once; the split runs three
+                # bf16 MFMA products per fp32 one)
                 "roofline": alt16["roofline"], "final_loss": round(alt16["loss"], 5)}
         if other_bn is not None:
             mode = "sync" if args.bn == "local" else "local"
