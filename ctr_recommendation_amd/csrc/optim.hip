@@ -2331,11 +2331,14 @@ __global__ void __launch_bounds__(256) owner_fold_kernel(const int* __restrict__
                                                          const void* __restrict__ wire_self, long long self_lo,
                                                          long long self_n, float* __restrict__ ring, int ring_n,
                                                          long long stride, const int* __restrict__ step,
-                                                         float** __restrict__ cell, float* __restrict__ extra) {
+                                                         float** __restrict__ cell, float* __restrict__ extra,
+                                                         double* __restrict__ part) {
   constexpr int G = D / 4, RPW = 64 / G;
+  __shared__ double red[256];
   float* dst = ring + (size_t)(*step % ring_n) * stride;
   if (blockIdx.x == 0 && threadIdx.x == 0) *cell = dst;
   const int lane = threadIdx.x & 63, q = lane % G;
+  double acc = 0.0;   // sumsq: the claimers' own rows (a flagged claimer's duplicates: fbn_sumsq_flagged)
   const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
   for (long long e0 = gw * RPW; e0 < n; e0 += nw * RPW) {
@@ -2356,6 +2359,7 @@ __global__ void __launch_bounds__(256) owner_fold_kernel(const int* __restrict__
     }
     if (u == (int)e) {
       reinterpret_cast<f32x4*>(dst)[(size_t)e * (D / 4) + q] = x;
+      acc += (double)(x[0] * x[0]) + (double)(x[1] * x[1]) + (double)(x[2] * x[2]) + (double)(x[3] * x[3]);
     } else {
       if (q == 0) atomicOr(&slot_row[u], FBN_SLOT_FLAG);
       float* ex = extra + (size_t)u * D + 4 * q;
@@ -2363,12 +2367,70 @@ __global__ void __launch_bounds__(256) owner_fold_kernel(const int* __restrict__
       for (int k = 0; k < 4; ++k) atomicAdd(ex + k, x[k]);
     }
   }
+  if (!part) return;
+  // one partial per block (no atomics: thousands of blocks on 64 slots serialise at L2);
+  // fbn_sumsq_flagged folds them
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
 }
 
+// After fbn_owner_fold(sumsq): the flagged claimers' correction |x + extra|^2 - |x|^2 (x = the claimer's
+// own row in the ring slot, extra = its duplicates' sum): one lane per entry scans slot_row, the
+// (rare) flagged rows are read by D/4-lane groups.
+template <int D>
+__global__ void __launch_bounds__(256) sumsq_flagged_kernel(const int* __restrict__ slot_row, int n,
+                                                            float* const* __restrict__ cell,
+                                                            const float* __restrict__ extra,
+                                                            const double* __restrict__ part, int nparts,
+                                                            double* __restrict__ sumsq) {
+  constexpr int G = D / 4, RPW = 64 / G;
+  __shared__ double red[256];
+  const float* src = *cell;
+  const int lane = threadIdx.x & 63, q = lane % G;
+  double acc = 0.0;
+  if (part)
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nparts; i += gridDim.x * blockDim.x) acc += part[i];
+  for (long long e0 = (long long)blockIdx.x * blockDim.x + threadIdx.x - lane; e0 < n;
+       e0 += (long long)gridDim.x * blockDim.x) {
+    const long long e = e0 + lane;
+    const int sr = e < n ? slot_row[e] : -1;
+    unsigned long long mask = __ballot(sr != -1 && (sr & FBN_SLOT_FLAG));
+    while (mask) {
+      int mine = -1;
+#pragma unroll
+      for (int gi = 0; gi < RPW; ++gi) {
+        if (!mask) break;
+        const int l = __ffsll((long long)mask) - 1;
+        mask &= mask - 1;
+        if (lane / G == gi) mine = l;
+      }
+      if (mine < 0) continue;
+      const long long ee = e0 + mine;
+      const f32x4 x = *reinterpret_cast<const f32x4*>(src + (size_t)ee * D + 4 * q);
+      const f32x4 t = x + *reinterpret_cast<const f32x4*>(extra + (size_t)ee * D + 4 * q);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc += (double)(t[k] * t[k]) - (double)(x[k] * x[k]);
+    }
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) atomicAdd(sumsq + (blockIdx.x & (FBN_SUMSQ_SLOTS - 1)), red[0]);
+}
+
+#define FBN_FOLD_PARTS 8192   // fbn_owner_fold's block cap = its partial sums of squares
 extern "C" int fbn_owner_fold(const int* ids, int n, int rank, const int* map, int* slot_row, const void* wire,
                               int wire_bf16, const void* wire_self, long long self_lo, long long self_n, float* ring,
                               int ring_n, long long stride, const int* step, void* cell, float* extra, int D,
-                              void* stream) {
+                              double* part, void* stream) {
   if (n <= 0) return FBN_OK;
   if (!ids || !map || !slot_row || !wire || !ring || !step || !cell || !extra || ring_n < 1 ||
       (long long)n * D > stride || self_lo < 0 || self_n < 0 || (self_n > 0 && !wire_self)) {
@@ -2376,8 +2438,25 @@ extern "C" int fbn_owner_fold(const int* ids, int n, int rank, const int* map, i
     return FBN_ERR_ARG;
   }
   hipStream_t st = (hipStream_t)stream;
-  FBN_DISPATCH_D(owner_fold_kernel, D, group_grid(n, D, 8192), ids, n, rank, map, slot_row, wire, wire_bf16,
-                 self_n > 0 ? wire_self : nullptr, self_lo, self_n, ring, ring_n, stride, step, (float**)cell, extra);
+  FBN_DISPATCH_D(owner_fold_kernel, D, group_grid(n, D, FBN_FOLD_PARTS), ids, n, rank, map, slot_row, wire,
+                 wire_bf16, self_n > 0 ? wire_self : nullptr, self_lo, self_n, ring, ring_n, stride, step,
+                 (float**)cell, extra, part);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
+extern "C" int fbn_sumsq_flagged(const int* slot_row, int n, const void* cell, const float* extra, int D,
+                                 const double* part, double* sumsq, void* stream) {
+  if (n <= 0) return FBN_OK;
+  if (!slot_row || !cell || !extra || !sumsq) {
+    fbn_set_error("fbn_sumsq_flagged: slot_row, cell, extra, sumsq");
+    return FBN_ERR_ARG;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  int blocks = (n + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  const int nparts = part ? (int)group_grid(n, D, FBN_FOLD_PARTS).x : 0;   // fbn_owner_fold's grid on the same n
+  FBN_DISPATCH_D(sumsq_flagged_kernel, D, dim3(blocks), slot_row, n, (float* const*)cell, extra, part, nparts, sumsq);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -3066,21 +3145,60 @@ extern "C" int fbn_adam_flush(float* p, float* m, float* v, long long nrows, int
 // Multi-GPU: the loss and this rank's table-gradient sum of squares ride in the dense-gradient
 // all-reduce (two floats appended to it): pack before, unpack after (sumsq += all ranks' table
 // norms; the loss becomes the global mean).  One thread each.
+// one wave: every slot loaded at once, folded in a fixed order (deterministic), then cleared
 __global__ void pack_extras_kernel(const float* loss, double* tab_slots, float* out) {
-  double s = 0.0;
-  for (int i = 0; i < FBN_SUMSQ_SLOTS; ++i) {
-    s += tab_slots[i];
-    tab_slots[i] = 0.0;
+  static_assert(FBN_SUMSQ_SLOTS == 64, "one lane per slot");
+  const int lane = threadIdx.x;
+  double s = tab_slots[lane];
+  tab_slots[lane] = 0.0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+  if (lane == 0) {
+    out[0] = *loss;
+    out[1] = (float)s;
   }
-  out[0] = *loss;
-  out[1] = (float)s;
 }
 __global__ void unpack_extras_kernel(const float* in, float* loss, double* sumsq) {
   *loss = in[0];
   sumsq[0] += (double)in[1];
 }
+// N > 1, after the all-reduce: fbn_unpack_extras and the dense gradients' sum of squares (fbn_sumsq
+// over x[0, n)) in one launch -- block 0 adds the unpacked table sumsq into its slot atomically,
+// beside the other blocks' dense partials
+__global__ void unpack_sumsq_kernel(const float* __restrict__ in, float* __restrict__ loss,
+                                    const float* __restrict__ x, long long n, double* __restrict__ sumsq) {
+  __shared__ double red[256];
+  double s = 0.0;
+  const long long n4 = n / 4;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(x + 4 * i);
+    s += (double)(v[0] * v[0]) + (double)(v[1] * v[1]) + (double)(v[2] * v[2]) + (double)(v[3] * v[3]);
+  }
+  for (long long i = n4 * 4 + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    s += (double)(x[i] * x[i]);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    double t = red[0];
+    if (blockIdx.x == 0) {
+      *loss = in[0];
+      t += (double)in[1];
+    }
+    atomicAdd(sumsq + (blockIdx.x & (FBN_SUMSQ_SLOTS - 1)), t);
+  }
+}
 extern "C" int fbn_pack_extras(const float* loss, double* tab_slots, float* out, void* stream) {
-  fbn_launch(pack_extras_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, loss, tab_slots, out);
+  fbn_launch(pack_extras_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, loss, tab_slots, out);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+extern "C" int fbn_unpack_sumsq(const float* in, float* loss, const float* x, long long n, double* sumsq, void* stream) {
+  if (!in || !loss || !sumsq || (n > 0 && !x)) { fbn_set_error("fbn_unpack_sumsq: in, loss, x, sumsq"); return FBN_ERR_ARG; }
+  fbn_launch(unpack_sumsq_kernel, dim3(512), dim3(256), 0, (hipStream_t)stream, in, loss, x, n, sumsq);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

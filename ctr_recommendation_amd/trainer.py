@@ -452,6 +452,7 @@ class FiBiNETTrainer:
         self.ring_cell = torch.zeros(2, dtype=torch.int64, device=dev)     # fbn_ring_slot's pointer cell
         self._fc_grad = None        # fixed-capacity rows, f32, when they are not deferred
         self._fc_extra = None       # fixed-capacity form: duplicates' sums per claimer (zero at rest)
+        self._fc_part = None        # ... and fbn_owner_fold's per-workgroup sums of squares
 
     # ------------------------------------------------------------------ one training step
     def step(self, batch: Dict[str, torch.Tensor], labels: torch.Tensor,
@@ -760,6 +761,7 @@ class FiBiNETTrainer:
             # through ~10 side-stream launches and a collective first
             route_ahead()
         joined = False
+        fold_done = False
         if self.xchg is None:
             # single GPU: per-sample vectors; entry e = b*(L+1)+t; duplicates -> extra[claimer]
             n_ent = B * (L + 1)
@@ -804,11 +806,12 @@ class FiBiNETTrainer:
                     ring, ring_n, stride = self._fc_grad, 1, n_ent * d
                 if _OWNER_FOLD:
                     # the widen into the ring slot and the duplicate fold in one pass: a claimer's row is
-                    # stored, a duplicate's added into extra[claimer] (flagged; applied at the tail)
+                    # stored, a duplicate's added into extra[claimer] (flagged; applied at the tail); the
+                    # claimers' squares summed on the way (the flagged ones corrected below)
                     call("fbn_owner_fold", ptr(x.recv_ids), n_ent, self.rank, ptr(self.map), ptr(self.slot_row),
                          ptr(wire), int(wire.dtype == torch.bfloat16), ptr(x.fc_send) if cnt else None, lo, cnt,
                          ptr(ring), ring_n, stride, ptr(self.step_dev), ptr(self.ring_cell), ptr(self._fc_extra), d,
-                         st)
+                         ptr(self._fc_part), st)
                     gsrc = (self.ring_cell, self._fc_extra, 1 | FBN_GRAD_CELL)
                     fold_done = True
                 else:
@@ -837,6 +840,10 @@ class FiBiNETTrainer:
                  n_ent, d, ptr(tab_acc), ptr(self.fx), ptr(self.flat_g) if fold else None,
                  self.n_dense if fold else 0, st)
             dense_done = fold
+        elif fold_done:
+            # the fold summed the claimers' own rows; only the flagged ones (duplicates) remain
+            call("fbn_sumsq_flagged", ptr(self.slot_row), n_ent, ptr(self.ring_cell), ptr(self._fc_extra), d,
+                 ptr(self._fc_part), ptr(tab_acc), st)
         else:
             call("fbn_sumsq_sparse", ptr(gsrc[0]), ptr(gsrc[1]), ptr(self.slot_row), gsrc[2], n_ent, d, ptr(tab_acc),
                  st)
@@ -849,7 +856,13 @@ class FiBiNETTrainer:
                 dense_work.wait()
             else:
                 self.coll.allreduce_(self.flat_g_ext[:o + 2])
-            call("fbn_unpack_extras", ptr(self.flat_g_ext[o:]), ptr(self.loss), ptr(self.sumsq), st)
+            if not dense_done:
+                # the unpack and the dense gradients' squares in one launch
+                call("fbn_unpack_sumsq", ptr(self.flat_g_ext[o:]), ptr(self.loss), ptr(self.flat_g), self.n_dense,
+                     ptr(self.sumsq), st)
+                dense_done = True
+            else:
+                call("fbn_unpack_extras", ptr(self.flat_g_ext[o:]), ptr(self.loss), ptr(self.sumsq), st)
         if not dense_done:
             call("fbn_sumsq", ptr(self.flat_g), self.n_dense, None, 0, ptr(self.sumsq), st)
         if not (joined and _JOIN_ONCE):
@@ -1021,9 +1034,12 @@ class FiBiNETTrainer:
             self.ring_cap = n
             self.ring = _lib.persistent(
                 lambda: torch.zeros((self.ring_n, n, self.d), dtype=torch.float32, device=self.device))
-        # the duplicate fold's sums per claimer (zero at rest), made here rather than inside a step
+        # the duplicate fold's sums per claimer (zero at rest) and its per-workgroup sums of squares
+        # (fbn_owner_fold's 8192-block cap), made here rather than inside a step
         if self._fc_extra is None or self._fc_extra.shape[0] < n:
             self._fc_extra = _lib.persistent(lambda: torch.zeros((n, self.d), dtype=torch.float32, device=self.device))
+        if self._fc_part is None:
+            self._fc_part = _lib.persistent(lambda: torch.zeros(8192, dtype=torch.float64, device=self.device))
         self.fc_wanted = False
 
     def _ring_stride(self) -> int:

@@ -489,6 +489,9 @@ int fbn_claim_rows(const int64_t* item, const int64_t* seq, int B, int L, long l
  * appended to the dense-gradient all-reduce buffer; unpack after it (sumsq[0] += table norms). */
 int fbn_pack_extras(const float* loss, double* tab_slots, float* out, void* stream);
 int fbn_unpack_extras(const float* in, float* loss, double* sumsq, void* stream);
+/* fbn_unpack_extras + fbn_sumsq(x, n) in one launch (N > 1: after the all-reduce, the dense
+ * gradients' sum of squares beside the unpacked table sumsq). */
+int fbn_unpack_sumsq(const float* in, float* loss, const float* x, long long n, double* sumsq, void* stream);
 /* end of step: step counter, dropout counter, zero the sumsq slots, and the BatchNorm
  * num_batches_tracked buffers (nbt0 / nbt1 may be NULL; model_fibinet.py:127,131 BN1d).
  * max_step (= total_steps): the counter saturates there and sets bit 2 of *err (err may be NULL)
@@ -547,7 +550,14 @@ int fbn_ring_slot(float* ring, int ring_n, long long stride, const int* step, vo
  * self_n) come from wire_self (the caller's own block, never sent). */
 int fbn_owner_fold(const int* ids, int n, int rank, const int* map, int* slot_row, const void* wire, int wire_bf16,
                    const void* wire_self, long long self_lo, long long self_n, float* ring, int ring_n,
-                   long long stride, const int* step, void* cell, float* extra, int D, void* stream);
+                   long long stride, const int* step, void* cell, float* extra, int D, double* part, void* stream);
+/* part (optional, 8192 doubles): fbn_owner_fold leaves one partial sum of the claimers' own rows' squares
+ * per workgroup; fbn_sumsq_flagged (same n and D) folds them and adds each flagged claimer's
+ * |x + extra|^2 - |x|^2 (x read through the ring slot's pointer cell) into sumsq (FBN_SUMSQ_SLOTS
+ * doubles): together the table gradient's sum of squares (clip_grad_norm_, src/train_fibinet.py:119)
+ * without a pass over every row. */
+int fbn_sumsq_flagged(const int* slot_row, int n, const void* cell, const float* extra, int D, const double* part,
+                      double* sumsq, void* stream);
 /* bf16 -> f32 (n % 8 == 0, 16-B aligned): the owner's received bf16 gradient rows (bf16 mode). */
 int fbn_widen_bf16(const void* in, float* out, long long n, void* stream);
 /* out [world][cap + 1]: out[o][j] = send_ids[offsets[o] + j] for j < counts[o], else -1, and

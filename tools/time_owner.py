@@ -28,9 +28,13 @@ step = torch.zeros(1, dtype=torch.int32, device=dev)
 cell = torch.zeros(2, dtype=torch.int64, device=dev)
 extra = torch.zeros((n, D), device=dev)
 out = torch.zeros(64, dtype=torch.float64, device=dev)
+part = torch.zeros(8192, dtype=torch.float64, device=dev)
 E = torch.randn((V, D), device=dev)
 reply = torch.empty((n, D), device=dev).bfloat16()
 st = _lib.stream_handle()
+
+
+flush = torch.empty(1 << 28, device=dev)        # 1 GiB: evicts L2 and the MALL between cold launches
 
 
 def timeit(name, fn):
@@ -42,11 +46,22 @@ def timeit(name, fn):
         fn()
     b.record()
     torch.cuda.synchronize()
-    print(f"{name:28s} {a.elapsed_time(b) / R * 1e3:8.1f} us", flush=True)
+    hot = a.elapsed_time(b) / R * 1e3
+    cold = 0.0
+    for _ in range(10):
+        flush.fill_(1.0)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        cold += a.elapsed_time(b) * 1e3 / 10
+    print(f"{name:28s} hot {hot:8.1f} us   cold {cold:8.1f} us", flush=True)
 
 
 timeit("owner_fold", lambda: call("fbn_owner_fold", ptr(ids), n, 0, ptr(mp), ptr(slot_row), ptr(wire), 1, None, 0, 0,
-                                  ptr(ring), 2, n * D, ptr(step), ptr(cell), ptr(extra), D, st))
+                                  ptr(ring), 2, n * D, ptr(step), ptr(cell), ptr(extra), D, ptr(part), st))
+timeit("sumsq_flagged", lambda: call("fbn_sumsq_flagged", ptr(slot_row), n, ptr(cell), ptr(extra), D, ptr(part),
+                                     ptr(out), st))
 timeit("sumsq_sparse (cell)", lambda: call("fbn_sumsq_sparse", ptr(cell), ptr(extra), ptr(slot_row), 1 | 0x20000, n, D,
                                            ptr(out), st))
 timeit("sumsq_sparse (direct)", lambda: call("fbn_sumsq_sparse", ptr(ring), ptr(extra), ptr(slot_row), 1, n, D,
