@@ -94,6 +94,15 @@ def split_mlp_input(d: int) -> bool:
     return (5 * d) % 128 == 0
 
 
+def wa_ld(d: int) -> int:
+    """Row stride of the bf16 Wa image and of the bf16 MLP input c: 15d, or -- when 15d is not a
+    multiple of 64 and c is not a split operand (d = 16: 240) -- 15d rounded up to 64 with zero
+    columns, so the layer-1 GEMM takes the LDS-DMA path over K = 256 instead of the generic kernel
+    over K = 240 (C2)."""
+    kc = 15 * d
+    return kc if (kc % 64 == 0 or split_mlp_input(d)) else (kc + 63) // 64 * 64
+
+
 def gemm_split(A, B, C, M, N, K, lda, ldb, ldc, transA, transB, bias=None, rC=NO_REMAP, beta=0.0, stream=None,
                stats=None, A2=None, lda2=0, kseg=INT_MAX, B2=None, ldb2=0, nseg=INT_MAX):
     """bf16 C = op(A) op(B) with A = [A | A2] along K (k-contiguous A) or B = [B | B2] along N (k-major B)."""
@@ -170,14 +179,17 @@ def bf16_weight_jobs(p: Dict[str, torch.Tensor], d: int, a: Dict[str, torch.Tens
     for i, (name, src, rows, cols, ld, trans, rm) in enumerate(spec):
         img = images and name in ("WaT", "WbT", "W", "x")
         key = ("s3w_" if img else "w16_") + name
-        shape = (2, rows, cols) if img else (rows, cols)
+        dld = wa_ld(d) if name == "Wa" else cols          # Wa: zero columns up to the GEMM's K (wa_ld)
+        shape = (2, rows, cols) if img else (rows, dld)
         t = a.get(key)
         if t is None or tuple(t.shape) != shape:
-            t = _lib.persistent(lambda: torch.empty(shape, dtype=torch.bfloat16, device=dev))
+            t = _lib.persistent(lambda: torch.zeros(shape, dtype=torch.bfloat16, device=dev))
             a[key] = t
-        out[name] = t[0] if img else t
+        out[name] = t[0] if img else (t[:, :cols] if dld != cols else t)
+        if name == "Wa":
+            out["Wa_full"] = t                          # [H1, wa_ld(d)]: the layer-1 GEMM's operand
         jobs[i] = _ConvJob(src.data_ptr(), t.data_ptr(), rows, cols, ld, trans, rm[0], rm[1], rm[2],
-                           2 if img else 0, 0, rows * cols if img else 0)
+                           2 if img else 0, dld if dld != cols else 0, rows * cols if img else 0)
     return jobs, len(spec), out
 
 
@@ -488,7 +500,12 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     Vc = None if v16 else buf("Vc", (B, 5, d))
     Vc16 = buf("Vc16", (B, 5, d), torch.bfloat16) if v16 else None
     KC = 15 * d
-    c = buf("c", (B, KC), torch.bfloat16 if bf else torch.float32)     # bf16 mode: GEMM-only operand
+    # bf16 mode: GEMM-only operand, rows wa_ld(d) apart (zero columns past 15d at d = 16)
+    KCp = wa_ld(d) if bf else KC
+    c = a.get("c")
+    cdt = torch.bfloat16 if bf else torch.float32
+    if c is None or tuple(c.shape) != (B, KCp) or c.dtype != cdt:
+        c = a["c"] = _lib.persistent(lambda: torch.zeros((B, KCp), dtype=cdt, device=dev))
     # bf16 LDS-DMA mode: c's V block is never written -- the MLP GEMMs read [Vc16 | c[:, 5d:]] (split operand)
     split_c = v16 and split_mlp_input(d)
     a["split_c"] = split_c
@@ -526,7 +543,7 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
              ptr(p["cate_emb.weight"]), p["cate_emb.weight"].shape[0], ptr(E), V,
              ptr(p["senet.excitation.0.weight"]), ptr(p["senet.excitation.0.bias"]),
              ptr(p["senet.excitation.2.weight"]), ptr(p["senet.excitation.2.bias"]), cfg.R, ptr(X), ptr(Vc),
-             ptr(Vc16), None if split_c else ptr(c), KC, int(bf), ptr(av), ptr(cnt), ptr(err), ptr(sm.get("map")),
+             ptr(Vc16), None if split_c else ptr(c), KCp, int(bf), ptr(av), ptr(cnt), ptr(err), ptr(sm.get("map")),
              ptr(sm.get("slot_row")), B, Lr, d, ptr(a["hot_list"]), ptr(a["hot_n"]), H, st)
         call("fbn_hot_rows", ptr(item_id), ptr(seq) if Lr else None, B, Lr, V, ptr(hc), None, ptr(a["hot_n"]), H,
              _GATHER_HOT, 1, st)
@@ -536,7 +553,7 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
              ptr(p["cate_emb.weight"]), p["cate_emb.weight"].shape[0], ptr(E), V, ptr(pos),
              ptr(p["senet.excitation.0.weight"]), ptr(p["senet.excitation.0.bias"]),
              ptr(p["senet.excitation.2.weight"]), ptr(p["senet.excitation.2.bias"]), cfg.R, ptr(X), ptr(Vc),
-             ptr(Vc16), None if (split_c or s3img) else ptr(c), KC,
+             ptr(Vc16), None if (split_c or s3img) else ptr(c), KCp,
              int(bf), ptr(av), ptr(cnt), ptr(err), ptr(sm.get("map")), ptr(sm.get("slot_row")), B, Lr, d,
              int(table_rows is not None and table_rows.dtype == torch.bfloat16), st)
     _probe_end(ev)
@@ -549,7 +566,7 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     a["fused_bilinear"] = fused_bil
     if fused_bil:
         # one launch: MFMA U = V W in registers, pair products straight into c (U never stored)
-        call("fbn_bilinear_fwd", ptr(Vc16), ptr(w16["WT"]), ptr(c), B, d, KC, st)
+        call("fbn_bilinear_fwd", ptr(Vc16), ptr(w16["WT"]), ptr(c), B, d, KCp, st)
     U = None if fused_bil else buf("U", (B, 5, d))
     if fused_bil:
         pass
@@ -571,7 +588,7 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
         a["s3_c"] = buf("s3_c_fwd", (2, B, KC), torch.bfloat16)
         call("fbn_pairs_fwd_img", ptr(Vc), ptr(U), ptr(a["s3_c"]), ptr(a["s3_vc"]), B, d, KC, st)
     elif not fused_bil:
-        call("fbn_pairs_fwd", ptr(Vc), ptr(Vc16), ptr(U), ptr(c), B, d, KC, int(cfg.bilinear_each), int(bf), st)
+        call("fbn_pairs_fwd", ptr(Vc), ptr(Vc16), ptr(U), ptr(c), B, d, KCp, int(cfg.bilinear_each), int(bf), st)
     # MLP layer 1
     h1pre = buf("h1pre", (B, H1))
     nt = (B + 63) // 64
@@ -591,12 +608,13 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
             c2 = buf("s3_c_fwd", (2, B, KC), torch.bfloat16)
             split_images([(c, c2, B, KC, KC, 0, NO_REMAP)], st)
             a["s3_c"] = c2
-        gemm(c2[0], w16["Wa"], h1pre, B, H1, KC, KC, KC, H1, False, True, bias=p["mlp.0.bias"], bf16=True, stream=st,
-             stats=t1)
+        gemm(c2[0], w16["Wa_full"], h1pre, B, H1, KC, KC, wa_ld(d), H1, False, True, bias=p["mlp.0.bias"], bf16=True,
+             stream=st, stats=t1)
     elif bf or f16:   # bf16_fwd: the fp32 MLP input rounded to bf16 on load
         a["s3_c"] = None
-        gemm(c, w16["Wa"], h1pre, B, H1, KC, KC, KC, H1, False, True, bias=p["mlp.0.bias"], bf16=True, stream=st,
-             stats=t1)
+        # (bf16: K padded with zero columns to wa_ld(d) on both operands; bf16_fwd: fp32 c over K = 15d)
+        gemm(c, w16["Wa_full"], h1pre, B, H1, KCp, KCp, wa_ld(d), H1, False, True, bias=p["mlp.0.bias"], bf16=True,
+             stream=st, stats=t1)
     else:
         gemm(c, p["mlp.0.weight"], h1pre, B, H1, KC, KC, 21 * d, H1, False, True, bias=p["mlp.0.bias"],
              rB=wa_remap(d), stream=st, stats=t1)
@@ -855,9 +873,10 @@ def backward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], a: Dict
     elif bf:
         # (d < 128: the MLP input c is one bf16 operand) slabs in the step's grouped launch when the
         # shape allows, else a launch of its own with its split-K reduce
-        if not sums.gemm_slabs(dh1pre16, a["c"], g["mlp.0.weight"], H1, KC, B, H1, KC, 21 * d, True, False,
+        ldcc = a["c"].shape[1]                      # wa_ld(d): c's rows carry zero columns past 15d
+        if not sums.gemm_slabs(dh1pre16, a["c"], g["mlp.0.weight"], H1, KC, B, H1, ldcc, 21 * d, True, False,
                                rC=wa_remap(d), stream=st):
-            wg.run(lambda s: gemm(dh1pre16, a["c"], g["mlp.0.weight"], H1, KC, B, H1, KC, 21 * d, True, False,
+            wg.run(lambda s: gemm(dh1pre16, a["c"], g["mlp.0.weight"], H1, KC, B, H1, ldcc, 21 * d, True, False,
                                   rC=wa_remap(d), stream=s))
     else:
         wg.run(lambda s: gemm(dh1pre, a["c"], g["mlp.0.weight"], H1, KC, B, H1, KC, 21 * d, True, False,
