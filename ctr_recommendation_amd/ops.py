@@ -484,7 +484,7 @@ def forward(p: Dict[str, torch.Tensor], batch: Dict[str, torch.Tensor], cfg: Fwd
     # w16_ready: the caller already converted this step's bf16 images (a["w16"]) on another stream
     # bf16_fwd training: the weight images carry their lo image too (the split-bf16 x3 backward)
     s3w = f16 and _SPLIT3 and cfg.training and not cfg.bilinear_each
-    a["s3w"] = s3w and not w16_ready
+    a["s3w"] = s3w and (not w16_ready or bool(a.get("w16_images")))   # (the trainer's images carry lo too)
     w16 = (a["w16"] if w16_ready else bf16_weights(p, d, a, st, x=x_mm, images=s3w)) if g16 else None
     a["w16"] = w16
     hmm = buf("hmm", (B, d))

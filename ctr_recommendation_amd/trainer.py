@@ -630,7 +630,11 @@ class FiBiNETTrainer:
             _lib.record_event(ev, self.side)
             return ev
 
-        w16_main = cfg.bf16 and self.xchg is None and _W16_MODE == "main"
+        # bf16_fwd training on the split-bf16 x3 backward: the forward's weight images (and their lo
+        # images) made here too, in the claims' launch, instead of at the forward's start
+        w16_img = bool(cfg.fwd16 and not cfg.bf16 and ops._SPLIT3 and not cfg.bilinear_each and cfg.training)
+        w16_main = (cfg.bf16 or w16_img) and self.xchg is None and _W16_MODE == "main"
+        self.acts["w16_images"] = w16_main and w16_img
         w16_late = cfg.bf16 and self.xchg is None and lazy and _W16_MODE == "late"
         claim_side = None
         if (self.xchg is None and lazy and _CLAIM_ON_SIDE and not w16_late and not _SIDE_AFTER_MLP0
@@ -641,12 +645,13 @@ class FiBiNETTrainer:
         if w16_main and self.xchg is None and lazy and claim_side is None and _HEAD_CONV:
             # on the main stream, in the claims' launch (fbn_adam_claim_catchup_conv): the two are
             # independent, so they run side by side instead of one launch after the other
-            jobs, njobs, self.acts["w16"] = ops.bf16_weight_jobs(self.p, d, self.acts, x=batch["item_emb_d128"])
+            jobs, njobs, self.acts["w16"] = ops.bf16_weight_jobs(self.p, d, self.acts, x=batch["item_emb_d128"],
+                                                                 images=w16_img)
             head_conv = (ctypes.cast(jobs, ctypes.c_void_p).value, njobs)
         elif w16_main:
             # on the main stream ahead of the claims: a cross-queue wait inside a replayed graph
             # costs ~10 us, about what the conversion itself takes
-            self.acts["w16"] = ops.bf16_weights(self.p, d, self.acts, st, x=batch["item_emb_d128"])
+            self.acts["w16"] = ops.bf16_weights(self.p, d, self.acts, st, x=batch["item_emb_d128"], images=w16_img)
         elif cfg.bf16 and not w16_late and (self.xchg is None or _SHARD_W16_SIDE):
             # (N > 1: beside the row exchange)
             w16_ev = start_w16()
