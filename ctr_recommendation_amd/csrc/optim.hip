@@ -2332,7 +2332,8 @@ __global__ void __launch_bounds__(256) owner_fold_kernel(const int* __restrict__
                                                          long long self_n, float* __restrict__ ring, int ring_n,
                                                          long long stride, const int* __restrict__ step,
                                                          float** __restrict__ cell, float* __restrict__ extra,
-                                                         double* __restrict__ part) {
+                                                         double* __restrict__ part,
+                                                         unsigned long long* __restrict__ fx) {
   constexpr int G = D / 4, RPW = 64 / G;
   __shared__ double red[256];
   float* dst = ring + (size_t)(*step % ring_n) * stride;
@@ -2362,9 +2363,17 @@ __global__ void __launch_bounds__(256) owner_fold_kernel(const int* __restrict__
       acc += (double)(x[0] * x[0]) + (double)(x[1] * x[1]) + (double)(x[2] * x[2]) + (double)(x[3] * x[3]);
     } else {
       if (q == 0) atomicOr(&slot_row[u], FBN_SLOT_FLAG);
-      float* ex = extra + (size_t)u * D + 4 * q;
+      if (fx) {
+        // deterministic mode: int64 fixed-point sums (as fbn_sparse_fold_fx) -- the total depends
+        // neither on the order the atomics land in nor on which entry won the claim
+        unsigned long long* a = fx + (size_t)u * D + 4 * q;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) atomicAdd(ex + k, x[k]);
+        for (int k = 0; k < 4; ++k) atomicAdd(a + k, (unsigned long long)to_fx(x[k]));
+      } else {
+        float* ex = extra + (size_t)u * D + 4 * q;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) atomicAdd(ex + k, x[k]);
+      }
     }
   }
   if (!part) return;
@@ -2381,13 +2390,18 @@ __global__ void __launch_bounds__(256) owner_fold_kernel(const int* __restrict__
 
 // After fbn_owner_fold(sumsq): the flagged claimers' correction |x + extra|^2 - |x|^2 (x = the claimer's
 // own row in the ring slot, extra = its duplicates' sum): one lane per entry scans slot_row, the
-// (rare) flagged rows are read by D/4-lane groups.
+// (rare) flagged rows are read by D/4-lane groups.  fx (deterministic mode): the duplicates' sums are
+// in the fixed-point accumulator instead; the claimer's own row joins them there and extra[claimer]
+// becomes the row's FULL gradient, float(total) -- the same integer total, hence the same float, as the
+// single-GPU deterministic fold (fbn_sparse_fold_fx + fbn_sumsq_sparse_norms) on the same entries --
+// and the accumulator row is reset.
 template <int D>
 __global__ void __launch_bounds__(256) sumsq_flagged_kernel(const int* __restrict__ slot_row, int n,
                                                             float* const* __restrict__ cell,
-                                                            const float* __restrict__ extra,
+                                                            float* __restrict__ extra,
                                                             const double* __restrict__ part, int nparts,
-                                                            double* __restrict__ sumsq) {
+                                                            double* __restrict__ sumsq,
+                                                            unsigned long long* __restrict__ fx) {
   constexpr int G = D / 4, RPW = 64 / G;
   __shared__ double red[256];
   const float* src = *cell;
@@ -2412,7 +2426,19 @@ __global__ void __launch_bounds__(256) sumsq_flagged_kernel(const int* __restric
       if (mine < 0) continue;
       const long long ee = e0 + mine;
       const f32x4 x = *reinterpret_cast<const f32x4*>(src + (size_t)ee * D + 4 * q);
-      const f32x4 t = x + *reinterpret_cast<const f32x4*>(extra + (size_t)ee * D + 4 * q);
+      f32x4 t;
+      if (fx) {
+        unsigned long long* a = fx + (size_t)ee * D + 4 * q;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const long long tot = (long long)(a[k] + (unsigned long long)to_fx(x[k]));
+          t[k] = (float)((double)tot * (1.0 / 1099511627776.0));
+          a[k] = 0ull;
+        }
+        *reinterpret_cast<f32x4*>(extra + (size_t)ee * D + 4 * q) = t;
+      } else {
+        t = x + *reinterpret_cast<const f32x4*>(extra + (size_t)ee * D + 4 * q);
+      }
 #pragma unroll
       for (int k = 0; k < 4; ++k) acc += (double)(t[k] * t[k]) - (double)(x[k] * x[k]);
     }
@@ -2430,7 +2456,7 @@ __global__ void __launch_bounds__(256) sumsq_flagged_kernel(const int* __restric
 extern "C" int fbn_owner_fold(const int* ids, int n, int rank, const int* map, int* slot_row, const void* wire,
                               int wire_bf16, const void* wire_self, long long self_lo, long long self_n, float* ring,
                               int ring_n, long long stride, const int* step, void* cell, float* extra, int D,
-                              double* part, void* stream) {
+                              double* part, unsigned long long* fx, void* stream) {
   if (n <= 0) return FBN_OK;
   if (!ids || !map || !slot_row || !wire || !ring || !step || !cell || !extra || ring_n < 1 ||
       (long long)n * D > stride || self_lo < 0 || self_n < 0 || (self_n > 0 && !wire_self)) {
@@ -2440,13 +2466,13 @@ extern "C" int fbn_owner_fold(const int* ids, int n, int rank, const int* map, i
   hipStream_t st = (hipStream_t)stream;
   FBN_DISPATCH_D(owner_fold_kernel, D, group_grid(n, D, FBN_FOLD_PARTS), ids, n, rank, map, slot_row, wire,
                  wire_bf16, self_n > 0 ? wire_self : nullptr, self_lo, self_n, ring, ring_n, stride, step,
-                 (float**)cell, extra, part);
+                 (float**)cell, extra, part, fx);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
 
-extern "C" int fbn_sumsq_flagged(const int* slot_row, int n, const void* cell, const float* extra, int D,
-                                 const double* part, double* sumsq, void* stream) {
+extern "C" int fbn_sumsq_flagged(const int* slot_row, int n, const void* cell, float* extra, int D,
+                                 const double* part, double* sumsq, unsigned long long* fx, void* stream) {
   if (n <= 0) return FBN_OK;
   if (!slot_row || !cell || !extra || !sumsq) {
     fbn_set_error("fbn_sumsq_flagged: slot_row, cell, extra, sumsq");
@@ -2454,9 +2480,12 @@ extern "C" int fbn_sumsq_flagged(const int* slot_row, int n, const void* cell, c
   }
   hipStream_t st = (hipStream_t)stream;
   int blocks = (n + 255) / 256;
-  if (blocks > 1024) blocks = 1024;
+  // deterministic mode: at most one block per norm slot, so each slot takes one addition (onto the
+  // zero the previous step's pack left) and the f64 total does not depend on the blocks' order
+  if (blocks > (fx ? FBN_SUMSQ_SLOTS : 1024)) blocks = fx ? FBN_SUMSQ_SLOTS : 1024;
   const int nparts = part ? (int)group_grid(n, D, FBN_FOLD_PARTS).x : 0;   // fbn_owner_fold's grid on the same n
-  FBN_DISPATCH_D(sumsq_flagged_kernel, D, dim3(blocks), slot_row, n, (float* const*)cell, extra, part, nparts, sumsq);
+  FBN_DISPATCH_D(sumsq_flagged_kernel, D, dim3(blocks), slot_row, n, (float* const*)cell, extra, part, nparts, sumsq,
+                 fx);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }

@@ -345,12 +345,15 @@ class FiBiNETTrainer:
         # single GPU: claim-time duplicate list (entry -> claiming entry) and per-sample gradient norms
         self.dup = torch.full((self.n_entries,), -1, **i32) if not sharded else None
         self.gnorm = torch.zeros((self.B, 2), dtype=torch.float64, device=dev) if not sharded else None
-        # deterministic mode (single GPU): rows hit by several entries are folded by
-        # order-independent int64 fixed-point sums (fbn_sparse_fold_fx) instead of float atomics, so
-        # two runs from the same state produce bit-identical table gradients and weights
+        # deterministic mode (src/utils.py:15-16): rows hit by several entries are folded by
+        # order-independent int64 fixed-point sums instead of float atomics -- single GPU
+        # fbn_sparse_fold_fx, the sharded owner fbn_owner_fold(fx) + fbn_sumsq_flagged(fx) -- so two runs
+        # from the same state produce bit-identical table gradients and weights (and a one-rank sharded
+        # run the single-GPU run's)
         if deterministic is None:
             deterministic = bool(model_cfg.get("deterministic", False)) or os.environ.get("FBN_DETERMINISTIC") == "1"
-        self.deterministic = bool(deterministic) and not sharded
+        self.deterministic = bool(deterministic)
+        self._fx_sh = None          # sharded deterministic fold: fixed-point accumulator [n][d] (zero at rest)
         # lazy table Adam, single GPU: step(..., next_batch=...) brings the next batch's rows up to
         # date on the side stream during this step (fbn_adam_prefetch; d < 128 needs the next batch
         # to have this batch's shape -- its pre-claims drive the two-pass form)
@@ -371,8 +374,9 @@ class FiBiNETTrainer:
             nb = _lib.lib().fbn_adam_prefetch_binned_ws_size(self.B * (max_len + 1))
             self.pf_ws = torch.empty(nb, dtype=torch.uint8, device=dev)
         self._pre_key = None
-        self.hasdup = torch.zeros((self.n_entries,), **i32) if self.deterministic else None
-        self.fx = torch.zeros((self.n_entries, d), dtype=torch.int64, device=dev) if self.deterministic else None
+        self.hasdup = torch.zeros((self.n_entries,), **i32) if self.deterministic and not sharded else None
+        self.fx = torch.zeros((self.n_entries, d), dtype=torch.int64, device=dev) \
+            if self.deterministic and not sharded else None
         # ---------------- optimizer schedule + device step state
         self.total_steps = total_steps
         tab, self.lrs = adam_table(total_steps, self.lr, self.beta2, OneCycle(total_steps, self.lr),
@@ -809,15 +813,17 @@ class FiBiNETTrainer:
                         self._fc_grad = _lib.persistent(
                             lambda: torch.empty((n_ent, d), dtype=torch.float32, device=self.device))
                     ring, ring_n, stride = self._fc_grad, 1, n_ent * d
-                if _OWNER_FOLD:
+                if _OWNER_FOLD or self.deterministic:
                     # the widen into the ring slot and the duplicate fold in one pass: a claimer's row is
                     # stored, a duplicate's added into extra[claimer] (flagged; applied at the tail); the
-                    # claimers' squares summed on the way (the flagged ones corrected below)
+                    # claimers' squares summed on the way (the flagged ones corrected below).  Deterministic:
+                    # the duplicates go to the fixed-point accumulator, extra becomes the FULL row gradient
+                    fx = self._det_fx(n_ent)
                     call("fbn_owner_fold", ptr(x.recv_ids), n_ent, self.rank, ptr(self.map), ptr(self.slot_row),
                          ptr(wire), int(wire.dtype == torch.bfloat16), ptr(x.fc_send) if cnt else None, lo, cnt,
                          ptr(ring), ring_n, stride, ptr(self.step_dev), ptr(self.ring_cell), ptr(self._fc_extra), d,
-                         ptr(self._fc_part), st)
-                    gsrc = (self.ring_cell, self._fc_extra, 1 | FBN_GRAD_CELL)
+                         ptr(self._fc_part), ptr(fx), st)
+                    gsrc = (self.ring_cell, self._fc_extra, 1 | FBN_GRAD_CELL | (FBN_GRAD_FULL if fx is not None else 0))
                     fold_done = True
                 else:
                     call("fbn_ring_slot", ptr(ring), ring_n, stride, ptr(self.step_dev), ptr(self.ring_cell),
@@ -832,6 +838,16 @@ class FiBiNETTrainer:
                 else:
                     grows = x.backward(sendbuf, out=slot)
                 gsrc = (grows, None, 1)
+                if self.deterministic and n_ent > 0:
+                    # the host-split form (calibration steps, overflow fallbacks): the same
+                    # deterministic fold, in place over the received rows (the claimer's row is
+                    # rewritten with itself; ring_n 1, the cell -> grows)
+                    fx = self._det_fx(n_ent)
+                    call("fbn_owner_fold", ptr(x.recv_ids), n_ent, self.rank, ptr(self.map), ptr(self.slot_row),
+                         ptr(grows), 0, None, 0, 0, ptr(grows), 1, n_ent * d, ptr(self.step_dev), ptr(self.ring_cell),
+                         ptr(self._fc_extra), d, ptr(self._fc_part), ptr(fx), st)
+                    gsrc = (self.ring_cell, self._fc_extra, 1 | FBN_GRAD_CELL | FBN_GRAD_FULL)
+                    fold_done = True
             if not fold_done:
                 call("fbn_sparse_fixup", None, None, ptr(x.recv_ids), n_ent, 0, self.V, self.rank, ptr(self.map),
                      ptr(gsrc[0]), None, ptr(self.slot_row), gsrc[2], d, st)
@@ -848,7 +864,7 @@ class FiBiNETTrainer:
         elif fold_done:
             # the fold summed the claimers' own rows; only the flagged ones (duplicates) remain
             call("fbn_sumsq_flagged", ptr(self.slot_row), n_ent, ptr(self.ring_cell), ptr(self._fc_extra), d,
-                 ptr(self._fc_part), ptr(tab_acc), st)
+                 ptr(self._fc_part), ptr(tab_acc), ptr(self._fx_sh) if self.deterministic else None, st)
         else:
             call("fbn_sumsq_sparse", ptr(gsrc[0]), ptr(gsrc[1]), ptr(self.slot_row), gsrc[2], n_ent, d, ptr(tab_acc),
                  st)
@@ -1045,7 +1061,23 @@ class FiBiNETTrainer:
             self._fc_extra = _lib.persistent(lambda: torch.zeros((n, self.d), dtype=torch.float32, device=self.device))
         if self._fc_part is None:
             self._fc_part = _lib.persistent(lambda: torch.zeros(8192, dtype=torch.float64, device=self.device))
+        self._det_fx(n)
         self.fc_wanted = False
+
+    def _det_fx(self, n: int):
+        """Sharded, deterministic mode: the fold's fixed-point accumulator for n received slots (and
+        the extra rows and per-workgroup partials the fold writes), grown outside any recording pool;
+        None when not deterministic."""
+        if not self.deterministic:
+            return None
+        d = self.d
+        if self._fx_sh is None or self._fx_sh.shape[0] < n:
+            self._fx_sh = _lib.persistent(lambda: torch.zeros((n, d), dtype=torch.int64, device=self.device))
+        if self._fc_extra is None or self._fc_extra.shape[0] < n:
+            self._fc_extra = _lib.persistent(lambda: torch.zeros((n, d), dtype=torch.float32, device=self.device))
+        if self._fc_part is None:
+            self._fc_part = _lib.persistent(lambda: torch.zeros(8192, dtype=torch.float64, device=self.device))
+        return self._fx_sh
 
     def _ring_stride(self) -> int:
         return self.B * 2 * self.d if not self.sharded else self.ring_cap * self.d

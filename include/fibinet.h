@@ -550,14 +550,22 @@ int fbn_ring_slot(float* ring, int ring_n, long long stride, const int* step, vo
  * self_n) come from wire_self (the caller's own block, never sent). */
 int fbn_owner_fold(const int* ids, int n, int rank, const int* map, int* slot_row, const void* wire, int wire_bf16,
                    const void* wire_self, long long self_lo, long long self_n, float* ring, int ring_n,
-                   long long stride, const int* step, void* cell, float* extra, int D, double* part, void* stream);
+                   long long stride, const int* step, void* cell, float* extra, int D, double* part,
+                   unsigned long long* fx, void* stream);
 /* part (optional, 8192 doubles): fbn_owner_fold leaves one partial sum of the claimers' own rows' squares
  * per workgroup; fbn_sumsq_flagged (same n and D) folds them and adds each flagged claimer's
  * |x + extra|^2 - |x|^2 (x read through the ring slot's pointer cell) into sumsq (FBN_SUMSQ_SLOTS
  * doubles): together the table gradient's sum of squares (clip_grad_norm_, src/train_fibinet.py:119)
- * without a pass over every row. */
-int fbn_sumsq_flagged(const int* slot_row, int n, const void* cell, const float* extra, int D, const double* part,
-                      double* sumsq, void* stream);
+ * without a pass over every row.
+ * fx (optional, [n][D] int64, zero at rest): deterministic mode (src/utils.py:15-16).
+ * fbn_owner_fold adds each duplicate's row into fx[claimer] as fixed point (2^-40) instead of float
+ * atomics into extra; fbn_sumsq_flagged (same fx) adds the claimer's own row, writes the FULL row
+ * gradient float(total) to extra[claimer] and resets fx -- readers then take Lp1 = 1 | FBN_GRAD_CELL |
+ * FBN_GRAD_FULL.  The fold is bitwise reproducible and equal to the single-GPU deterministic fold on
+ * the same entries; with fx, fbn_sumsq_flagged runs on at most FBN_SUMSQ_SLOTS workgroups (one f64
+ * addition per norm slot). */
+int fbn_sumsq_flagged(const int* slot_row, int n, const void* cell, float* extra, int D, const double* part,
+                      double* sumsq, unsigned long long* fx, void* stream);
 /* bf16 -> f32 (n % 8 == 0, 16-B aligned): the owner's received bf16 gradient rows (bf16 mode). */
 int fbn_widen_bf16(const void* in, float* out, long long n, void* stream);
 /* out [world][cap + 1]: out[o][j] = send_ids[offsets[o] + j] for j < counts[o], else -1, and

@@ -41,6 +41,8 @@ def _worker(rank, world, port, V, d, B, L, q, hook=False, bf16=False, padded=Fal
         seq = torch.randint(0, V, (B, L), generator=gb)
         seq[0] = 0
         seq[1, :3] = 5
+        if fc == "one" and rank != 0:
+            seq.zero_()          # items only: at most B entries per block -- these ranks' blocks all fit
         xg = RowExchange(rank, world, V, d, B, L, torch.device("cpu"), kernels=CpuExchangeKernels(), rows_bf16=bf16)
         lo, n_local = xg.rows_lo, xg.rows_local
         E_local = E_full[lo:lo + n_local].clone()
@@ -60,8 +62,10 @@ def _worker(rank, world, port, V, d, B, L, q, hook=False, bf16=False, padded=Fal
 
         if fc is not None:
             # the fixed-capacity form: blocks of cap + 1 slots, routed by prepare() (inline on CPU);
-            # "tiny" overflows on every rank's batch -> all ranks read the flag and fall back together
-            xg.enable_fixed(B * (L + 1) if fc == "fit" else 2)
+            # "tiny" overflows on every rank's batch -> all ranks read the flag and fall back together;
+            # "one": cap B, only rank 0's batch (full histories) overflows -- the others learn it from
+            # the in-band flag in rank 0's blocks alone
+            xg.enable_fixed({"fit": B * (L + 1), "tiny": 2, "one": B}[fc])
             xg.prepare(item, seq, err)
         rows = xg.forward(item, seq, E_local, sparse, err, before_gather=before_gather if hook else None)
         pos = xg.cur_pos
@@ -118,8 +122,17 @@ def _worker(rank, world, port, V, d, B, L, q, hook=False, bf16=False, padded=Fal
         c = DistCollective(world)
         t = torch.full((3,), float(rank + 1), dtype=torch.float64)
         c.allreduce_(t)
+        own_ovf = None
+        if fc is not None:
+            # did THIS rank's own routing overflow? (stat[0] before the status kernel ORs the peers' flags)
+            st = {}
+            xg.k.route_fc(item, seq, B, L, V, xg.Vl, world, xg.cap, torch.empty(world * (xg.cap + 1), dtype=torch.int32),
+                          torch.empty((B, L + 1), dtype=torch.int32), st.setdefault("stat", torch.zeros(world + 1,
+                                                                                                     dtype=torch.int32)),
+                          torch.zeros(1, dtype=torch.int32))
+            own_ovf = int(st["stat"][0])
         q.put((rank, bool(ok_fwd and ok_pad), bwd_err, nu, touched, t.tolist(), int(err[0]),
-               fc_state if fc is not None else None))
+               (fc_state, own_ovf) if fc is not None else None))
     finally:
         dist.destroy_process_group()
 
@@ -130,7 +143,8 @@ def _worker(rank, world, port, V, d, B, L, q, hook=False, bf16=False, padded=Fal
                                                        (8, True, True, True, None),
                                                        (2, True, False, False, "fit"), (3, False, True, False, "fit"),
                                                        (4, True, True, False, "fit"), (3, True, False, False, "tiny"),
-                                                       (8, True, True, False, "fit")])
+                                                       (8, True, True, False, "fit"), (3, True, False, False, "one"),
+                                                       (4, False, True, False, "one")])
 def test_row_exchange_protocol(world, hook, bf16, padded, fc):
     """hook: the owner-side claim -> before_gather -> gather split used by the lazy table Adam.
     bf16: the bf16 mode's wire rows (each delivered row == E[id] rounded to bf16).  padded: the
@@ -138,7 +152,10 @@ def test_row_exchange_protocol(world, hook, bf16, padded, fc):
     owners, blocks of B * (L + 1) + 1 ints per destination), bf16 rows, history length 20.
     fc: the fixed-capacity form (equal-split all-to-alls of cap + 1 slots, empty slots negative):
     "fit" -- every block fits, the step exchanges in that form; "tiny" -- cap 2 overflows, every rank
-    sees the in-band flag and the step falls back to host split sizes on all ranks together."""
+    sees the in-band flag and the step falls back to host split sizes on all ranks together; "one" --
+    only rank 0's batch overflows: the ranks whose own routing fit must still fall back, from the flag
+    in rank 0's blocks (a rank that missed it would run the equal-split all-to-all against the others'
+    host-split one and deadlock)."""
     V, d, B, L = (101, 8, 12, 6) if world < 8 else (1001, 8, 12, 20)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -154,7 +171,10 @@ def test_row_exchange_protocol(world, hook, bf16, padded, fc):
     tot = sum(range(1, world + 1))
     for rank, ok_fwd, bwd_err, nu, touched, red, err, fc_state in res:
         if fc is not None:
+            fc_state, own_ovf = fc_state
             assert fc_state == ((True, 0) if fc == "fit" else (False, 1)), (rank, fc_state)
+            if fc == "one":
+                assert own_ovf == (1 if rank == 0 else 0), (rank, own_ovf)
         assert ok_fwd, f"rank {rank}: wrong rows delivered"
         assert bwd_err < 1e-5, f"rank {rank}: sparse reduce-scatter error {bwd_err}"
         assert nu >= touched

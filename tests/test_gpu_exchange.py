@@ -85,3 +85,100 @@ def test_padded_routes_roundtrip(hip_device, world):
     assert torch.equal(cnt.cpu(), counts) and torch.equal(cnt_ref, counts)
     n = int(offsets[-1])
     assert torch.equal(ids.cpu()[:n], send_ids) and torch.equal(ids_ref[:n], send_ids)
+
+
+@pytest.mark.parametrize("world,cap_kind,zipf", [(1, "fit", False), (3, "fit", False), (8, "fit", True),
+                                                 (4, "over", False), (8, "over", True)])
+def test_route_fc_matches_oracle(hip_device, world, cap_kind, zipf):
+    """fbn_route_fc (the fixed-capacity routing) against the oracle's restatement: the same per-owner
+    request counts and overflow flag in stat, every block holding the same multiset of local rows
+    (the kernel's order inside a block follows workgroup timing), pos a bijection from the routed
+    entries onto their owner's block with send_ids[pos] == the local row, and each block's last slot
+    -1, or -2 in EVERY block once any entry overflowed (the in-band flag)."""
+    dev = hip_device
+    V, B, L = 250_007, 2048, 20
+    Vl = (V + world - 1) // world
+    g = torch.Generator().manual_seed(world * 31 + B)
+    ids = (torch.rand(B, L + 1, generator=g) ** 6 * V).long() if zipf else torch.randint(0, V, (B, L + 1), generator=g)
+    ids[:, 1:][torch.rand(B, L, generator=g) < 0.4] = 0
+    item, seq = ids[:, 0].contiguous(), ids[:, 1:].contiguous()
+    per_owner = torch.bincount((ids[:, 0] // Vl), minlength=world) + \
+        torch.bincount((ids[:, 1:][ids[:, 1:] != 0] // Vl), minlength=world)
+    cap = int(per_owner.max()) + 64 if cap_kind == "fit" else max(1, int(per_owner.max()) // 2)
+    n = world * (cap + 1)
+    i32 = dict(dtype=torch.int32)
+    ref = dict(send_ids=torch.empty(n, **i32), pos=torch.empty((B, L + 1), **i32), stat=torch.zeros(world + 1, **i32),
+               err=torch.zeros(1, **i32))
+    CpuExchangeKernels().route_fc(item, seq, B, L, V, Vl, world, cap, ref["send_ids"], ref["pos"], ref["stat"], ref["err"])
+    out = dict(send_ids=torch.full((n,), -7, dtype=torch.int32, device=dev),
+               pos=torch.full((B, L + 1), -7, dtype=torch.int32, device=dev),
+               stat=torch.zeros(world + 4, dtype=torch.int32, device=dev), err=torch.zeros(1, dtype=torch.int32, device=dev))
+    HipExchangeKernels().route_fc(item.to(dev), seq.to(dev), B, L, V, Vl, world, cap, out["send_ids"], out["pos"],
+                                  out["stat"], out["err"])
+    out = {k: v.cpu() for k, v in out.items()}
+    assert int(out["err"]) == 0
+    assert torch.equal(out["stat"][:world + 1], ref["stat"]), (out["stat"], ref["stat"])
+    assert int(ref["stat"][0]) == (1 if cap_kind == "over" else 0)
+    last = torch.arange(world) * (cap + 1) + cap
+    assert torch.equal(out["send_ids"][last], ref["send_ids"][last])
+    routed = out["pos"] >= 0
+    if cap_kind == "fit":
+        assert torch.equal(routed, ref["pos"] >= 0)
+    else:   # which entries of an overflowing owner keep a slot depends on timing: only counts are fixed
+        assert int(routed.sum()) == int((ref["pos"] >= 0).sum())
+    for o in range(world):
+        a = o * (cap + 1)
+        blk, rblk = out["send_ids"][a:a + cap], ref["send_ids"][a:a + cap]
+        assert int((blk >= 0).sum()) == int((rblk >= 0).sum()), o
+        if cap_kind == "fit":
+            assert torch.equal(blk.sort().values, rblk.sort().values), o
+    p = out["pos"][routed].long()
+    assert p.unique().numel() == p.numel()                                   # one slot per routed entry
+    owner = (ids // Vl)[routed]
+    assert bool(((p >= owner * (cap + 1)) & (p < owner * (cap + 1) + cap)).all())
+    assert torch.equal(out["send_ids"][p], (ids - (ids // Vl) * Vl)[routed].int())
+
+
+@pytest.mark.parametrize("world,rank,self_send", [(4, 0, False), (4, 2, True), (8, 5, True), (8, 3, False),
+                                                  (1, 0, True)])
+@pytest.mark.parametrize("flagger", ["none", "peer", "self"])
+def test_route_fc_status_multirank_layout(hip_device, world, rank, self_send, flagger):
+    """fbn_route_fc_status on a synthetic received layout of `world` requester blocks (what the
+    equal-split all-to-all delivers): with self_send the own block is copied from send_ids first (the
+    native path never sends it); stat[0] becomes 1 when ANY block carries the in-band -2 -- a peer's
+    block while this rank's own routing fit ("peer"), or this rank's own ("self") -- and the host copy
+    equals the oracle's.  The received ids themselves are left as they are."""
+    dev = hip_device
+    cap = 37
+    n = world * (cap + 1)
+    g = torch.Generator().manual_seed(world * 7 + rank)
+    recv = torch.randint(-1, 1000, (n,), generator=g, dtype=torch.int32)
+    send = torch.randint(-1, 1000, (n,), generator=g, dtype=torch.int32)
+    for r in range(world):
+        recv[r * (cap + 1) + cap] = -1
+        send[r * (cap + 1) + cap] = -1
+    own_flag = flagger == "self"
+    if flagger == "peer" and world > 1:
+        peer = (rank + 1) % world
+        recv[peer * (cap + 1) + cap] = -2
+    if own_flag:
+        # this rank's own routing overflowed: -2 in every block it sends, its own block included
+        for r in range(world):
+            send[r * (cap + 1) + cap] = -2
+        if not self_send:
+            recv[rank * (cap + 1) + cap] = -2
+    stat0 = torch.zeros(world + 4, dtype=torch.int32)
+    stat0[0] = int(own_flag)
+    stat0[1:world + 1] = torch.arange(1, world + 1, dtype=torch.int32)
+    ref_recv, ref_stat = recv.clone(), stat0.clone()
+    ref_host = torch.zeros(world + 4, dtype=torch.int32)
+    CpuExchangeKernels().route_fc_status(send if self_send else None, ref_recv, world, rank, cap, ref_stat, ref_host)
+    d_recv, d_stat = recv.to(dev), stat0.to(dev)
+    host = torch.zeros(world + 4, dtype=torch.int32, pin_memory=True)
+    HipExchangeKernels().route_fc_status(send.to(dev) if self_send else None, d_recv, world, rank, cap, d_stat, host)
+    torch.cuda.synchronize()
+    want = 1 if (own_flag or (flagger == "peer" and world > 1)) else 0
+    assert int(ref_stat[0]) == want
+    assert torch.equal(d_stat.cpu()[:world + 1], ref_stat[:world + 1])
+    assert torch.equal(host[:world + 1], ref_host[:world + 1])
+    assert torch.equal(d_recv.cpu(), ref_recv)

@@ -114,3 +114,70 @@ def test_sharded_path_over_rccl_matches_single_gpu(hip_device):
         # bf16 path reads f32 rows), so the two agree to bf16 rounding, not bit for bit
         for a, b in zip(l0, l1):
             assert abs(a - b) <= 5e-3, (key, l0, l1)
+
+
+def _det_worker(port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FBN_NATIVE_COMM="1")
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        from ctr_recommendation_amd.data import make_batch
+        from ctr_recommendation_amd.trainer import FiBiNETTrainer
+        from oracle.fibinet_oracle import build_model
+        V, B, steps = 60000, 1024, 8
+        cfg = {"embedding_dim": 128, "vocab_size": V, "honour_config": True, "net_dropout": 0.0,
+               "compute_dtype": "fp32"}
+        torch.manual_seed(0)
+        init = build_model(None, cfg, honour_config=True).state_dict()
+        bs = [make_batch(900 + s, B, V, device=dev) for s in range(steps + 1)]
+        res = []
+        for shard in (False, True):
+            tr = FiBiNETTrainer(cfg, total_steps=20, batch_size=B, device=dev, deterministic=True,
+                                init_state={k: v.clone() for k, v in init.items()}, shard=shard)
+            assert tr.deterministic and (tr.native_comm is not None) == shard
+            losses = [tr.step(bs[s][0], bs[s][1], next_batch=bs[s + 1][0]).item() for s in range(steps)]
+            norms = float(tr.norm.item())
+            tr.flush()
+            tr.check_ids()
+            res.append((losses, {n: getattr(tr, n).cpu().clone() for n in ("E", "Em", "Ev", "flat_p", "flat_m",
+                                                                            "flat_v")}, norms,
+                        tr.xchg.fc_active if shard else None))
+            tr.close()
+        (l0, t0, n0, _), (l1, t1, n1, fc) = res
+        out = {"losses": (l0, l1), "norm": (n0, n1), "fc": fc,
+               "equal": {k: bool(torch.equal(t0[k], t1[k])) for k in t0},
+               "maxdiff": {k: float((t0[k] - t1[k]).abs().max()) for k in t0}}
+        q.put(("ok", out))
+    except Exception as e:
+        q.put((repr(e), None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_deterministic_matches_single_gpu_bitwise(hip_device):
+    """Deterministic mode (src/utils.py:15-16), fp32: the one-rank sharded step over RCCL
+    (route, owner claims and catch-up, exchange, per-entry gradient rows, the fixed-point owner fold,
+    deferred ring slots, the packed all-reduce; through the exchange's calibration steps and the switch
+    to the fixed-capacity form) against the single-GPU trainer's deterministic step on the same batches:
+    every loss and the table, its Adam moments, the dense parameters and moments BIT-IDENTICAL (the
+    fold's integer total is the same whichever entries carry the row, and the rest is the same
+    kernels on the same values).  Only the clip norm is summed in another order (per-sample vector
+    norms vs the rows' squares); it enters the update only when the clip engages, which it does not at
+    max_norm 10 here -- both norms are reported."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_det_worker, args=(_port(), q))
+    p.start()
+    status, out = q.get(timeout=300)
+    p.join(timeout=60)
+    assert status == "ok", status
+    print(f"det one-rank sharded vs single GPU: equal {out['equal']}, max |diff| {out['maxdiff']}, "
+          f"norms {out['norm']}, fc {out['fc']}")
+    assert out["fc"], "the sharded trainer never switched to the fixed-capacity exchange"
+    assert max(out["norm"]) < 10.0, out["norm"]          # the clip did not engage (see docstring)
+    l0, l1 = out["losses"]
+    assert l0 == l1, (l0, l1)
+    assert all(out["equal"].values()), (out["equal"], out["maxdiff"])

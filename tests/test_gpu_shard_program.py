@@ -9,13 +9,17 @@ history is rewritten in place (through the library, so the tensors keep their ve
 the programs stay valid) with full histories that overflow the calibrated block capacity: both
 trainers must read the routed-ahead overflow flag and run that step with host split sizes (the
 program trainer falls back to an eager step for it), and the replays after it go on.  The duplicate
-fold's float atomics can part two fp32 runs in the last bits, and Adam amplifies the parting over the
-23 steps (measured over runs: 6e-8 .. 4.4e-4 in the loss, up to 1.2e-3 / 2.3e-2 of the table / dense
-displacement; bf16 bit-identical: sums of a few bf16 values are exact in f32): losses within 1e-5
-(relative) over the first 6 steps and 3e-3 to the end, the tables (after the flush) within 1e-2 and
-the dense parameters within 1e-1 of their displacement.  (A program whose every replay clobbered the
-fold buffer -- fixed, DESIGN §7 -- showed 8.8e-3 in the loss one step after its first replay and
-2.8e-2 of the table displacement: caught by both.)
+fold is the one order-dependent reduction of the sharded step:
+  * deterministic mode (fp32 and bf16; the fold in int64 fixed point, fbn_owner_fold(fx)): replays
+    and eager steps are BIT-IDENTICAL -- every loss, the table and its Adam moments and row state, the
+    dense parameters and moments, the BatchNorm buffers (torch.equal);
+  * the default float-atomic fold (fp32): the atomics' order can part two runs in the last bits, and
+    Adam amplifies the parting over the 23 steps (measured over runs: 6e-8 .. 4.4e-4 in the loss, up to
+    1.2e-3 / 2.3e-2 of the table / dense displacement): losses within 1e-5 (relative) over the first 6
+    steps and 3e-3 to the end, the tables (after the flush) within 1e-2 and the dense parameters within
+    1e-1 of their displacement.  (A program whose every replay clobbered the fold buffer -- fixed,
+    DESIGN §7 -- showed 8.8e-3 in the loss one step after its first replay and 2.8e-2 of the table
+    displacement: caught by these bars, and by the deterministic cases' equality at once.)
 """
 import ctypes
 import os
@@ -37,7 +41,7 @@ def _port():
     return p
 
 
-def _worker(port, dtype, q):
+def _worker(port, dtype, det, q):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FBN_NATIVE_COMM="1",
                       FBN_DEBUG_FC=os.environ.get("FBN_DEBUG_FC", "0"))
@@ -61,7 +65,8 @@ def _worker(port, dtype, q):
         heavy_at = FC_CALIB_STEPS + 1 + 3 * nb           # the 4th cycle: batch 2 is rewritten before it
         total = len(order) + 4
         trs = [FiBiNETTrainer(cfg, total_steps=total, batch_size=B, device=dev,
-                              init_state={k: v.clone() for k, v in init.items()}, shard=True) for _ in range(2)]
+                              init_state={k: v.clone() for k, v in init.items()}, shard=True, deterministic=det)
+               for _ in range(2)]
         eager, prog_tr = trs
         p_init = eager.flat_p.clone()
         e_init = eager.E.clone()
@@ -111,6 +116,11 @@ def _worker(port, dtype, q):
         # dense parameters: relative to their displacement (Adam turns last-bit differences into
         # small absolute ones)
         res["dp"] = float((eager.flat_p - prog_tr.flat_p).norm() / (eager.flat_p - p_init).norm())
+        # bitwise: table, its moments and row state, dense parameters and moments, BatchNorm buffers
+        res["equal"] = {n: bool(torch.equal(getattr(eager, n), getattr(prog_tr, n)))
+                        for n in ("E", "Em", "Ev", "last", "flat_p", "flat_m", "flat_v")}
+        for n in ("mlp.1.running_mean", "mlp.1.running_var", "mlp.5.running_mean", "mlp.5.running_var"):
+            res["equal"][n] = bool(torch.equal(eager.p[n], prog_tr.p[n]))
         for t in trs:
             t.close()
         q.put(("ok", res))
@@ -121,11 +131,11 @@ def _worker(port, dtype, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_sharded_step_program_matches_eager_with_overflow_fallback(hip_device, dtype):
+@pytest.mark.parametrize("dtype,det", [("fp32", True), ("bf16", True), ("fp32", False)])
+def test_sharded_step_program_matches_eager_with_overflow_fallback(hip_device, dtype, det):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_worker, args=(_port(), dtype, q))
+    p = ctx.Process(target=_worker, args=(_port(), dtype, det, q))
     p.start()
     status, res = q.get(timeout=300)
     p.join(timeout=60)
@@ -136,7 +146,13 @@ def test_sharded_step_program_matches_eager_with_overflow_fallback(hip_device, d
     le, lp = res["losses"]
     diffs = [abs(a - b) / max(1.0, abs(a)) for a, b in zip(le, lp)]
     worst = max(range(len(diffs)), key=lambda k: diffs[k])
-    print(f"[{dtype}] max loss diff {max(diffs):.3g}, de {res['de']:.3g}, dp {res['dp']:.3g}")
+    print(f"[{dtype} det={det}] max loss diff {max(diffs):.3g}, de {res['de']:.3g}, dp {res['dp']:.3g}, "
+          f"equal {res['equal']}")
+    if det:
+        # deterministic mode (fixed-point owner fold): the replays ARE the eager steps, bit for bit
+        assert le == lp, (worst, " ".join(f"{a:.7f}/{b:.7f}" for a, b in zip(le, lp)))
+        assert all(res["equal"].values()), res["equal"]
+        return
     assert max(diffs[:6]) <= 1e-5 and max(diffs) <= 3e-3, (worst, " ".join(f"{a:.5f}/{b:.5f}" for a, b in zip(le, lp)))
     assert res["de"] <= 1e-2, res["de"]
     assert res["dp"] <= 1e-1, res["dp"]
