@@ -277,8 +277,114 @@ def _initial_state(cfg, V, world, rank, dev):
 FORCE_SHARD = os.environ.get("FBN_BENCH_SHARD") == "1"
 
 
-def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
-    """Build a trainer for `dtype`, bring it to steady state, time K steps; returns the result dict."""
+AB_CYCLES = 3      # native_ab: passes over its batches after the recording pass
+
+
+def _ab_agree(ok: bool, first_diff: int, dev) -> tuple:
+    """Every rank's verdict of the lockstep A/B -> the job's: valid only if valid on EVERY rank; the
+    first step that differed anywhere (-1: none).  One MIN all-reduce on the default group."""
+    t = torch.tensor([1 if ok else 0, first_diff if first_diff >= 0 else 1 << 30], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    fd = int(t[1])
+    return bool(t[0]), (-1 if fd >= 1 << 30 else fd)
+
+
+def native_ab(args, world, rank, dev):
+    """N > 1 (and the one-rank sharded job): validate the fast collective path before timing it.
+
+    The sharded step runs two ways from the same seeded state over the same batches, both in
+    deterministic mode (the fixed-point owner fold: no order-dependent reduction left in the step):
+      A  native RCCL on the step's stream (csrc/comm.cpp) + the fixed-capacity exchange recorded as
+         step programs -- the fast path, never run above one rank before this job;
+      B  torch.distributed's collectives, eager steps (the compute between exchanges as hipGraph
+         segments) -- the conservative path.
+    A runs first, through the exchange's calibration steps, the recording pass and AB_CYCLES replay
+    passes, under the native communicators' watchdog (FBN_AB_TIMEOUT_S, default 120 s: a rank whose
+    peer never posts aborts instead of hanging); its health is agreed over every rank; then B runs the
+    same steps.  Valid iff every step's loss and, after the flush, the table, its Adam moments and the
+    dense parameters and moments are bitwise equal on every rank.  Returns the verdict (and the first
+    differing step) for the headline's choice of path."""
+    from ctr_recommendation_amd import _lib
+    from ctr_recommendation_amd.data import make_device_batches
+    from ctr_recommendation_amd.exchange import NativeComm
+    from ctr_recommendation_amd.trainer import FC_CALIB_STEPS, FiBiNETTrainer
+    t_start = time.perf_counter()
+    d, B, L = args.dim, args.batch, 20
+    V = args.rows_per_gpu * world
+    cfg = {"embedding_dim": d, "vocab_size": V, "compute_dtype": args.dtype}
+    nb = 4
+    batches = make_device_batches(nb + FC_CALIB_STEPS, B, V, L, dev, seed=9090 + rank, zipf=args.zipf)
+    order = [nb + k for k in range(FC_CALIB_STEPS)] + [nb - 1] + list(range(nb)) * (1 + AB_CYCLES)
+    total = len(order) + 4
+    names = ("E", "Em", "Ev", "flat_p", "flat_m", "flat_v")
+
+    def run(native: bool):
+        init = _initial_state(cfg, V, world, rank, dev)
+        tr = FiBiNETTrainer(cfg, total_steps=total, batch_size=B, device=dev, rank=rank, world=world, init_state=init,
+                            shard=True, deterministic=True, sync_bn=args.bn == "sync", native_comm=native)
+        del init
+        if native:
+            assert tr.native_comm is not None
+            _lib.call("fbn_comm_watch", int(float(os.environ.get("FBN_AB_TIMEOUT_S", "120")) * 1000))
+        losses, progs, pool = [], {}, torch.cuda.MemPool() if native else None
+        for i, j in enumerate(order):
+            b, y = batches[j]
+            nxt = batches[order[i + 1]][0] if i + 1 < len(order) else batches[order[0]][0]
+            if native and i > FC_CALIB_STEPS:
+                if j not in progs:
+                    progs[j] = tr.record_program(b, y, next_batch=nxt, pool=pool)
+                else:
+                    tr.run_program(progs[j])
+            else:
+                tr.step(b, y, next_batch=nxt)
+            losses.append(tr.loss.clone())
+        tr.flush()
+        torch.cuda.synchronize()
+        tr.check_ids()
+        info = {"fc_active": bool(tr.xchg.fc_active), "fallbacks": tr.xchg.fc_fallbacks,
+                "programs": len(progs), "collectives": "native" if tr.native_comm is not None else "torch"}
+        state = {n: getattr(tr, n) for n in names}
+        return tr, torch.stack(losses), state, info
+
+    ok_a, err = True, None
+    tra = la = sa = ia = None
+    try:
+        tra, la, sa, ia = run(True)
+        ok_a = ia["fc_active"] and ia["programs"] == nb
+        if not ok_a:
+            err = f"native path did not run as step programs over the fixed-capacity exchange: {ia}"
+    except RuntimeError as e:        # a watchdog abort or an RCCL error on this rank
+        ok_a, err = False, f"{type(e).__name__}: {e}"[:400]
+    if not ok_a:
+        print(f"[bench] rank {rank}: native path failed the A/B: {err}", file=sys.stderr, flush=True)
+    healthy, _ = _ab_agree(ok_a, -1, dev)
+    out = {"steps": len(order), "batches": nb, "deterministic": True, "native_healthy": healthy,
+           "watchdog_fired": NativeComm.watchdog_fired()}
+    if not healthy:
+        if tra is not None:
+            tra.close()
+        out.update(validated=False, first_diff_step=-1, reason=err or "another rank's native path failed",
+                   seconds=round(time.perf_counter() - t_start, 1))
+        return out
+    trb, lb, sb, ib = run(False)
+    diff = (la != lb).nonzero()
+    first = int(diff[0, 0]) if diff.numel() else -1
+    same = {n: bool(torch.equal(sa[n], sb[n])) for n in names}
+    ok = first < 0 and all(same.values())
+    valid, first_all = _ab_agree(ok, first, dev)
+    for t in (tra, trb):
+        t.close()
+    del tra, trb, sa, sb
+    out.update(validated=valid, first_diff_step=first_all, equal_this_rank=same, native=ia, torch=ib,
+               loss_last=(float(la[-1]), float(lb[-1])), seconds=round(time.perf_counter() - t_start, 1))
+    if not valid:
+        out["reason"] = ("losses first differ at step %d" % first_all) if first_all >= 0 else "final state differs"
+    return out
+
+
+def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None, native=None):
+    """Build a trainer for `dtype`, bring it to steady state, time K steps; returns the result dict.
+    native (N > 1): True / False = native RCCL + step programs / torch.distributed (None: FBN_NATIVE_COMM)."""
     from ctr_recommendation_amd.data import make_device_batches
     from ctr_recommendation_amd import ops
     from ctr_recommendation_amd.trainer import FiBiNETTrainer
@@ -302,7 +408,7 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
     # step programs: the single-GPU step, and the sharded step in the fixed-capacity exchange form over
     # RCCL on the step's stream (the one-rank job; N > 1 with FBN_NATIVE_COMM=1)
     from ctr_recommendation_amd.exchange import native_comm_wanted
-    shard_prog = sharded and trmod._FC and native_comm_wanted(dev, None, rehearsal)
+    shard_prog = sharded and trmod._FC and native_comm_wanted(dev, None, rehearsal, force=native)
     use_prog = (not sharded or shard_prog) and args.mode in ("auto", "program") and args.table_adam == "lazy"
     if use_prog:
         prime = max(prime, nb)            # every batch's program is recorded (a real step each) while priming
@@ -317,7 +423,7 @@ def measure(args, dtype, world, rank, dev, rehearsal, backend, bn=None):
     tr = FiBiNETTrainer(cfg, total_steps=total, batch_size=B, device=dev, rank=rank, world=world,
                         init_state=init, stage_on_cpu=rehearsal, lazy_window=F, prefetch_rows=args.prefetch,
                         table_adam=args.table_adam,
-                        shard=sharded, sync_bn=(bn or args.bn) == "sync")
+                        shard=sharded, sync_bn=(bn or args.bn) == "sync", native_comm=native)
     del init
     batches = make_device_batches(nb, B, V, L, dev, seed=2025 + rank, zipf=args.zipf)
     graphs = []
@@ -661,7 +767,33 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=dev)
 
-    r = measure(args, args.dtype, world, rank, dev, rehearsal, backend)
+    # N > 1 on RCCL: validate the native-RCCL + step-program path against torch.distributed's (lockstep
+    # A/B, deterministic, bitwise) before timing it; the headline runs the validated path, the other
+    # one is timed beside it.  FBN_BENCH_AB=0 skips the A/B (FBN_NATIVE_COMM then decides)
+    ab, native, torch_line, native_err = None, None, None, None
+    if (world > 1 or FORCE_SHARD) and not rehearsal and os.environ.get("FBN_BENCH_AB", "1") != "0":
+        ab = native_ab(args, world, rank, dev)
+        native = bool(ab["validated"])
+        _release()
+        if rank == 0:
+            print(f"[bench] native-RCCL A/B: {json.dumps(ab)}", file=sys.stderr, flush=True)
+    if native:
+        try:
+            r = measure(args, args.dtype, world, rank, dev, rehearsal, backend, native=True)
+            ok = True
+        except RuntimeError as e:    # a watchdog abort mid-run: every rank falls back together
+            ok, native_err = False, f"{type(e).__name__}: {e}"[:400]
+            print(f"[bench] rank {rank}: native headline failed: {native_err}", file=sys.stderr, flush=True)
+        ok_all, _ = _ab_agree(ok, -1, dev)
+        _release()
+        if ok_all:
+            torch_line = measure(args, args.dtype, world, rank, dev, rehearsal, backend, native=False)
+        else:
+            native = False
+            r = measure(args, args.dtype, world, rank, dev, rehearsal, backend, native=False)
+    else:
+        r = measure(args, args.dtype, world, rank, dev, rehearsal, backend,
+                    native=None if ab is None else False)
     alt = alt16 = None
     if args.also_fp32 and args.dtype == "bf16" and world == 1:
         # each in a process of its own (_child_line), the headline's state released first
@@ -676,8 +808,9 @@ def main():
     other_bn = None
     if world > 1 and not args.no_other_bn:
         # both BatchNorm modes at N > 1: the other one as an embedded line (SyncBN = the parity mode)
+        _release()
         other_bn = measure(args, args.dtype, world, rank, dev, rehearsal, backend,
-                           bn="sync" if args.bn == "local" else "local")
+                           bn="sync" if args.bn == "local" else "local", native=native)
 
     if rank == 0:
         K, B, dt = r["K"], r["B"], r["dt"]
@@ -757,6 +890,17 @@ def main():
                               "global batch); 4 extra all-reduces per step") if mode == "sync" else
                              "per-GPU statistics (nn.DataParallel semantics, train_fibinet.py:69-70)",
                 "final_loss": round(other_bn["loss"], 5)}
+        if ab is not None:
+            out["native_ab"] = dict(ab, headline=("native RCCL + step programs (validated bitwise against "
+                                                  "torch.distributed)" if native else "torch.distributed"),
+                                    **({"native_headline_error": native_err} if native_err else {}))
+        if torch_line is not None:
+            out["torch_collectives"] = {
+                "value": round(torch_line["K"] * B * world / torch_line["dt"], 1), "unit": "samples/s",
+                "ms_per_step": round(torch_line["dt"] / torch_line["K"] * 1e3, 4), "steps": torch_line["K"],
+                "launch_mode": torch_line["launch_mode"], "collectives": torch_line["collectives"],
+                "host_enqueue_ms_per_step": round(torch_line["t_host"] / torch_line["K"] * 1e3, 4),
+                "final_loss": round(torch_line["loss"], 5)}
         if inf is not None:
             out["inference"] = inf
         if world == 1 and not args.no_cpu_baseline:

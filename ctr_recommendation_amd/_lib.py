@@ -158,6 +158,10 @@ SIGNATURES = {
     "fbn_comm_alltoall_peers": (I, [P, P, P, LL, P]),
     "fbn_comm_alltoall": (I, [P, P, P, LL, P]),
     "fbn_comm_allreduce": (I, [P, P, LL, I, P]),
+    "fbn_comm_watch": (I, [LL]),
+    "fbn_comm_heartbeat": (I, [P]),
+    "fbn_comm_abort": (I, [P]),
+    "fbn_comm_watchdog_fired": (I, [P]),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -180,7 +184,7 @@ def lib() -> ctypes.CDLL:
 
 
 _fns = {}
-_UNCHECKED = ("fbn_version", "fbn_device_ok", "fbn_probe_elapsed")
+_UNCHECKED = ("fbn_version", "fbn_device_ok", "fbn_probe_elapsed", "fbn_comm_watchdog_fired")
 _tls = threading.local()           # .prog: the StepProgram recording on this thread (or None)
 
 

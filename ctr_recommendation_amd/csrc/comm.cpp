@@ -12,11 +12,27 @@
 // The unique id travels over torch.distributed (exchange.py NativeComm); only the data path is
 // here.  All-to-all with per-peer counts = grouped ncclSend/ncclRecv (the counts are host ints,
 // read at call time); equal-split all-to-all = ncclAllToAll; sum all-reduce in place.
+//
+// Watchdog (fbn_comm_watch / fbn_comm_heartbeat): torch.distributed aborts a process group whose
+// collective does not complete in time; these communicators bypass that, so a rank whose peer
+// never posts would wait forever.  The step calls fbn_comm_heartbeat at its end (a recordable entry
+// point: every step-program replay posts it too), which notes the host time and records an event on
+// the step's stream.  A monitor thread aborts EVERY live communicator (ncclCommAbort: RCCL's kernels
+// poll the abort flag and exit, so the blocked stream -- and the host waiting on it -- drain) once
+// the last heartbeat is older than the timeout while its event has not completed.  An idle process
+// (the event complete) is never aborted.  Every call on an aborted communicator then fails with the
+// watchdog's message.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <stdio.h>
 #include <string.h>
+
+#include <atomic>
+#include <chrono>
+#include <mutex>
+#include <set>
+#include <thread>
 
 void fbn_set_error(const char* msg);
 
@@ -34,6 +50,7 @@ struct Rccl {
   decltype(&ncclAllReduce) all_reduce = nullptr;
   decltype(&ncclAllToAll) all_to_all = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
+  decltype(&ncclCommAbort) comm_abort = nullptr;   // optional (the watchdog)
 };
 
 Rccl g_rccl;
@@ -42,11 +59,70 @@ struct Comm {
   ncclComm_t comm;
   int world;
   int rank;
+  std::atomic<int> aborted{0};
 };
+
+// the watchdog's state (one per process: a hang anywhere in the step aborts every communicator)
+struct Watch {
+  std::mutex mu;
+  std::set<Comm*> live;
+  std::thread th;
+  std::atomic<bool> running{false};
+  std::atomic<long long> timeout_ms{0};
+  std::atomic<long long> beat_ms{0};        // host time of the last heartbeat (0 = none yet)
+  std::atomic<int> fired{0};
+  hipEvent_t ev = nullptr;                  // recorded by each heartbeat on the step's stream
+  int device = -1;
+  bool ev_recorded = false;
+};
+Watch g_watch;
+
+long long now_ms() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+void abort_all() {
+  std::lock_guard<std::mutex> g(g_watch.mu);
+  for (Comm* c : g_watch.live) {
+    if (c->aborted.exchange(1)) continue;
+    if (g_rccl.comm_abort && c->comm) (void)g_rccl.comm_abort(c->comm);
+  }
+}
+
+void monitor() {
+  if (g_watch.device >= 0) (void)hipSetDevice(g_watch.device);
+  while (g_watch.running.load()) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    const long long beat = g_watch.beat_ms.load(), tmo = g_watch.timeout_ms.load();
+    if (beat == 0 || tmo <= 0 || g_watch.fired.load()) continue;
+    if (now_ms() - beat <= tmo) continue;
+    bool pending = true;   // a heartbeat without an event (host-only callers, tests) counts as pending
+    {
+      std::lock_guard<std::mutex> g(g_watch.mu);
+      if (g_watch.ev && g_watch.ev_recorded) pending = hipEventQuery(g_watch.ev) == hipErrorNotReady;
+    }
+    if (!pending) continue;   // idle: the last step finished long ago
+    fprintf(stderr, "[fbn_comm] watchdog: no step completed for %lld ms -- aborting every RCCL communicator\n",
+            now_ms() - beat);
+    g_watch.fired.store(1);
+    abort_all();
+  }
+}
+
+bool aborted(const Comm* c, const char* where) {
+  if (!c->aborted.load()) return false;
+  char msg[224];
+  snprintf(msg, sizeof(msg), "%s: the communicator was aborted by the watchdog (no step completed within %lld ms)",
+           where, g_watch.timeout_ms.load());
+  fbn_set_error(msg);
+  return true;
+}
 
 int fail(const char* where, ncclResult_t r) {
   char msg[256];
-  snprintf(msg, sizeof(msg), "%s: %s", where, g_rccl.error_string ? g_rccl.error_string(r) : "rccl error");
+  snprintf(msg, sizeof(msg), "%s: %s%s", where, g_rccl.error_string ? g_rccl.error_string(r) : "rccl error",
+           g_watch.fired.load() ? " (the watchdog aborted the communicators: no step completed in time)" : "");
   fbn_set_error(msg);
   return 3;
 }
@@ -93,6 +169,7 @@ extern "C" int fbn_comm_load(const char* path) {
     dlclose(h);
     return 1;
   }
+  bind(h, "ncclCommAbort", &r.comm_abort);
   g_rccl = r;
   return 0;
 }
@@ -129,15 +206,71 @@ extern "C" int fbn_comm_init(void** out, const void* id, int world, int rank) {
     return fail("fbn_comm_init", r);
   }
   *out = c;
+  std::lock_guard<std::mutex> g(g_watch.mu);
+  g_watch.live.insert(c);
   return 0;
 }
 
 extern "C" int fbn_comm_destroy(void* comm) {
   Comm* c = static_cast<Comm*>(comm);
   if (!c) return 0;
-  if (g_rccl.handle && c->comm) (void)g_rccl.comm_destroy(c->comm);
+  {
+    std::lock_guard<std::mutex> g(g_watch.mu);
+    g_watch.live.erase(c);
+  }
+  // (an aborted communicator was already torn down by ncclCommAbort)
+  if (g_rccl.handle && c->comm && !c->aborted.load()) (void)g_rccl.comm_destroy(c->comm);
   delete c;
   return 0;
+}
+
+// Abort one communicator now (its pending and future operations fail; RCCL's kernels exit).
+extern "C" int fbn_comm_abort(void* comm) {
+  Comm* c = static_cast<Comm*>(comm);
+  if (!c) return 0;
+  std::lock_guard<std::mutex> g(g_watch.mu);
+  if (!c->aborted.exchange(1) && g_rccl.comm_abort && c->comm) (void)g_rccl.comm_abort(c->comm);
+  return 0;
+}
+
+// Start (or retune) the watchdog: timeout_ms <= 0 disarms it.  The calling thread's current device is
+// the one whose step events the monitor queries.
+extern "C" int fbn_comm_watch(long long timeout_ms) {
+  g_watch.timeout_ms.store(timeout_ms);
+  if (g_watch.running.load() || timeout_ms <= 0) return 0;
+  (void)hipGetDevice(&g_watch.device);
+  g_watch.running.store(true);
+  g_watch.th = std::thread(monitor);
+  g_watch.th.detach();   // lives as long as the process (joined by nobody: it only sleeps and polls)
+  return 0;
+}
+
+// The end of a step: the host time now, and an event on `stream` (NULL stream + host-only callers: no
+// event, the beat alone) -- the monitor aborts when the beat is older than the timeout and the event
+// has not completed.
+extern "C" int fbn_comm_heartbeat(void* stream) {
+  if (stream) {
+    std::lock_guard<std::mutex> g(g_watch.mu);
+    if (!g_watch.ev && hipEventCreateWithFlags(&g_watch.ev, hipEventDisableTiming) != hipSuccess) {
+      g_watch.ev = nullptr;
+      fbn_set_error("fbn_comm_heartbeat: hipEventCreateWithFlags failed");
+      return 2;
+    }
+    if (hipEventRecord(g_watch.ev, static_cast<hipStream_t>(stream)) != hipSuccess) {
+      fbn_set_error("fbn_comm_heartbeat: hipEventRecord failed");
+      return 2;
+    }
+    g_watch.ev_recorded = true;
+  }
+  g_watch.beat_ms.store(now_ms());
+  return 0;
+}
+
+// 1 once the watchdog has aborted the communicators (0 otherwise); a communicator's own state with
+// a handle: 1 if it was aborted (by the watchdog or fbn_comm_abort).
+extern "C" int fbn_comm_watchdog_fired(void* comm) {
+  if (comm) return static_cast<Comm*>(comm)->aborted.load();
+  return g_watch.fired.load();
 }
 
 // All-to-all with per-peer counts (rows of `row_bytes` bytes; send_counts / recv_counts: host
@@ -150,6 +283,7 @@ extern "C" int fbn_comm_alltoallv(void* comm, const void* send, const int* send_
     fbn_set_error("fbn_comm_alltoallv: bad arguments");
     return 1;
   }
+  if (aborted(c, "fbn_comm_alltoallv")) return 3;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const char* sp = static_cast<const char*>(send);
   char* rp = static_cast<char*>(recv);
@@ -183,6 +317,7 @@ extern "C" int fbn_comm_alltoall(void* comm, const void* send, void* recv, long 
     fbn_set_error("fbn_comm_alltoall: bad arguments");
     return 1;
   }
+  if (aborted(c, "fbn_comm_alltoall")) return 3;
   if (bytes_per_peer == 0) return 0;
   ncclResult_t r = g_rccl.all_to_all(send, recv, (size_t)bytes_per_peer, ncclUint8, c->comm,
                                      static_cast<hipStream_t>(stream));
@@ -201,6 +336,7 @@ extern "C" int fbn_comm_alltoall_peers(void* comm, const void* send, void* recv,
     fbn_set_error("fbn_comm_alltoall_peers: bad arguments");
     return 1;
   }
+  if (aborted(c, "fbn_comm_alltoall_peers")) return 3;
   if (bytes_per_peer == 0 || c->world <= 1) return 0;
   hipStream_t st = static_cast<hipStream_t>(stream);
   ncclResult_t r = g_rccl.group_start();
@@ -227,6 +363,7 @@ extern "C" int fbn_comm_allreduce(void* comm, void* buf, long long n, int dtype,
     fbn_set_error("fbn_comm_allreduce: bad arguments");
     return 1;
   }
+  if (aborted(c, "fbn_comm_allreduce")) return 3;
   if (n == 0) return 0;
   ncclDataType_t t = dtype == 0 ? ncclFloat32 : (dtype == 1 ? ncclFloat64 : ncclInt32);
   ncclResult_t r = g_rccl.all_reduce(buf, buf, (size_t)n, t, ncclSum, c->comm, static_cast<hipStream_t>(stream));

@@ -75,7 +75,15 @@ class NativeComm:
         h = ctypes.c_void_p()
         with torch.cuda.device(device if device is not None else torch.cuda.current_device()):
             call("fbn_comm_init", ctypes.byref(h), uid, world, rank)
+            if COMM_TIMEOUT_S > 0:
+                # the step's heartbeats (trainer: fbn_comm_heartbeat at every step's end) feed it
+                call("fbn_comm_watch", int(COMM_TIMEOUT_S * 1000))
         self.handle, self.world, self.rank = h.value, world, rank
+
+    @staticmethod
+    def watchdog_fired() -> bool:
+        """The watchdog aborted the communicators (no step completed within FBN_COMM_TIMEOUT_S)."""
+        return bool(_lib.lib().fbn_comm_watchdog_fired(None))
 
     def alltoallv(self, out: torch.Tensor, inp: torch.Tensor, recv_counts, send_counts) -> None:
         """Rows (dim 0) of inp to the ranks, send_counts[r] to rank r; recv_counts[r] rows from r."""
@@ -106,7 +114,7 @@ class NativeComm:
             self.handle = None
 
 
-def native_comm_wanted(device, group=None, stage_on_cpu: bool = False) -> bool:
+def native_comm_wanted(device, group=None, stage_on_cpu: bool = False, force: Optional[bool] = None) -> bool:
     """RCCL on the step's stream: a HIP device and an nccl (= RCCL) process group.  FBN_NATIVE_COMM
     = 1: always; 0: never (torch.distributed's collectives, on its own stream); "auto" (default): at
     world = 1 only (the sharded smoke job, where it is tested against the torch.distributed path).
@@ -114,11 +122,17 @@ def native_comm_wanted(device, group=None, stage_on_cpu: bool = False) -> bool:
     one device, and no multi-GPU box was available), and they bypass torch's watchdog timeouts, so
     the default keeps torch.distributed's collectives there until a multi-GPU run shows loss and
     table parity between the two."""
-    mode = os.environ.get("FBN_NATIVE_COMM", "auto")
+    mode = os.environ.get("FBN_NATIVE_COMM", "auto") if force is None else ("1" if force else "0")
     if not (torch.device(device).type == "cuda" and not stage_on_cpu and dist.is_initialized()
             and dist.get_backend(group) == "nccl") or mode == "0":
         return False
     return mode == "1" or dist.get_world_size(group) == 1
+
+
+# the native communicators' watchdog (csrc/comm.cpp): abort them all when no step has completed for
+# this many seconds (torch.distributed's process groups have their own collective timeout; these
+# communicators bypass it).  0 disables it.
+COMM_TIMEOUT_S = float(os.environ.get("FBN_COMM_TIMEOUT_S", "300"))
 
 
 class HipExchangeKernels:

@@ -259,7 +259,8 @@ class FiBiNETTrainer:
                  stage_on_cpu: bool = False, dropout_seed: Optional[int] = None, table_adam: str = "lazy",
                  lazy_window: Optional[int] = None, defer_table_grads: bool = True, max_norm: float = 10.0,
                  optimizer: Optional[str] = None, deterministic: Optional[bool] = None,
-                 prefetch_rows: bool = True, shard: Optional[bool] = None, sync_bn: Optional[bool] = None):
+                 prefetch_rows: bool = True, shard: Optional[bool] = None, sync_bn: Optional[bool] = None,
+                 native_comm: Optional[bool] = None):
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise RuntimeError("FiBiNETTrainer runs on a HIP device only (no CPU fallback)")
@@ -395,8 +396,9 @@ class FiBiNETTrainer:
         self.host_step = 0
         self.acts: Dict[str, torch.Tensor] = {}
         # RCCL on the step's own stream (exchange.NativeComm) when the process group is RCCL
+        # (native_comm: True / False overrides FBN_NATIVE_COMM -- bench.py's lockstep A/B of the two paths)
         self.native_comm = NativeComm(world, rank, group, dev) \
-            if (sharded or world > 1) and native_comm_wanted(dev, group, stage_on_cpu) else None
+            if (sharded or world > 1) and native_comm_wanted(dev, group, stage_on_cpu, force=native_comm) else None
         self.coll = DistCollective(world, group, stage_on_cpu, comm=self.native_comm)
         # BatchNorm at N > 1.  sync_bn (default): statistics over the GLOBAL batch (one f64
         # all-reduce per BN layer and direction) -- the single-process reference run on the
@@ -919,6 +921,10 @@ class FiBiNETTrainer:
             call("fbn_step_end", ptr(self.step_dev), ptr(self.rng), ptr(self.sumsq),
                  ptr(self.p["mlp.1.num_batches_tracked"]), ptr(self.p["mlp.5.num_batches_tracked"]), self.total_steps,
                  ptr(self.err), st)
+        if self.native_comm is not None:
+            # the watchdog's heartbeat (exchange.NativeComm): host time + an event at the step's end;
+            # recorded into a step program like any call, so every replay posts it too
+            call("fbn_comm_heartbeat", st)
         if self.fc_wanted and not self.xchg.cap and not self.xchg.fc_active:
             self._fc_calibrate()
         self.host_step += 1
@@ -953,7 +959,9 @@ class FiBiNETTrainer:
             # ahead by the previous step -- then the step is library calls and stream edges only
             if not (x.cap and self.native_comm is not None and next_batch is not None):
                 raise ValueError("the sharded step records with the fixed-capacity exchange (after its calibration "
-                                 "steps), native RCCL and a next batch")
+                                 "steps), native RCCL on the step's stream (FBN_NATIVE_COMM=1 at N > 1, or "
+                                 "FiBiNETTrainer(native_comm=True); the default at N > 1 is torch.distributed, "
+                                 "whose collectives cannot be recorded) and a next batch")
             if x.fc_next is None or x.fc_next[0] != _lib_key(x, batch):
                 raise ValueError("record the sharded step after a step that routed this batch ahead (given it as "
                                  "its next_batch)")

@@ -665,6 +665,18 @@ int fbn_comm_alltoall(void* comm, const void* send, void* recv, long long bytes_
  * no-op at one rank): the fixed-capacity exchange keeps a rank's requests to itself in place */
 int fbn_comm_alltoall_peers(void* comm, const void* send, void* recv, long long bytes_per_peer, void* stream);
 int fbn_comm_allreduce(void* comm, void* buf, long long n, int dtype, void* stream);
+/* Watchdog (torch.distributed's collective timeout, which these communicators bypass).
+ * fbn_comm_watch(timeout_ms): start the process's monitor thread (timeout_ms <= 0 disarms it).
+ * fbn_comm_heartbeat(stream): the end of a step -- the host time now, and an event recorded on
+ * `stream` (recordable: a step program's replays post it too).  Once the last heartbeat is older than
+ * the timeout while its event has not completed, the monitor aborts every live communicator
+ * (ncclCommAbort: RCCL's kernels exit, the stream and the host blocked on it drain) and every later
+ * call on them fails with error 3 and the watchdog's message.  fbn_comm_abort(comm): abort one now.
+ * fbn_comm_watchdog_fired(NULL): 1 once the watchdog fired; (comm): 1 if that communicator is aborted. */
+int fbn_comm_watch(long long timeout_ms);
+int fbn_comm_heartbeat(void* stream);
+int fbn_comm_abort(void* comm);
+int fbn_comm_watchdog_fired(void* comm);
 
 #ifdef __cplusplus
 }

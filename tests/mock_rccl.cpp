@@ -36,6 +36,7 @@ struct World {
   // all-reduce rendezvous
   int arrived = 0, generation = 0;
   std::vector<double> acc, result;   // result: the last completed generation's sums
+  bool aborted = false;              // ncclCommAbort on any rank: every wait returns an error
 };
 
 std::mutex g_mu;
@@ -72,7 +73,8 @@ static ncclResult_t complete_recvs(MockComm* c) {
   std::unique_lock<std::mutex> lk(w.mu);
   for (const PendingRecv& r : t_recvs) {
     auto key = std::make_pair(r.peer, c->rank);
-    if (!w.cv.wait_for(lk, std::chrono::seconds(20), [&] { return !w.box[key].empty(); })) return ncclInternalError;
+    if (!w.cv.wait_for(lk, std::chrono::seconds(20), [&] { return w.aborted || !w.box[key].empty(); }) || w.aborted)
+      return ncclInternalError;
     std::vector<char> msg = std::move(w.box[key].front());
     w.box[key].pop_front();
     if (msg.size() != r.bytes) return ncclInvalidArgument;   // a send / recv size mismatch
@@ -111,6 +113,17 @@ ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId id, int
 }
 
 ncclResult_t ncclCommDestroy(ncclComm_t comm) {
+  delete comm;
+  return ncclSuccess;
+}
+
+// the world's waits end with an error (a real abort also frees the communicator)
+ncclResult_t ncclCommAbort(ncclComm_t comm) {
+  {
+    std::lock_guard<std::mutex> lk(comm->w->mu);
+    comm->w->aborted = true;
+  }
+  comm->w->cv.notify_all();
   delete comm;
   return ncclSuccess;
 }
@@ -179,7 +192,8 @@ ncclResult_t ncclAllReduce(const void* send, void* recv, size_t count, ncclDataT
     w.result = w.acc;   // a rank of the next generation cannot complete it before every rank left this one
     ++w.generation;
     w.cv.notify_all();
-  } else if (!w.cv.wait_for(lk, std::chrono::seconds(20), [&] { return w.generation != gen; })) {
+  } else if (!w.cv.wait_for(lk, std::chrono::seconds(20), [&] { return w.aborted || w.generation != gen; }) ||
+             w.generation == gen) {
     return ncclInternalError;
   }
   for (size_t i = 0; i < count; ++i) {

@@ -105,3 +105,65 @@ def test_native_comm_multi_rank_bookkeeping(tmp_path):
     p = subprocess.run([sys.executable, str(script), so, os.path.dirname(HERE)], capture_output=True, text=True,
                        timeout=300)
     assert p.returncode == 0 and p.stdout.strip().endswith("ok"), (p.stdout[-2000:], p.stderr[-3000:])
+
+
+WATCHDOG_CHILD = textwrap.dedent(r"""
+import ctypes, sys, threading, time
+import numpy as np
+sys.path.insert(0, sys.argv[2])
+from ctr_recommendation_amd import _lib
+lib = _lib.lib()
+assert lib.fbn_comm_load(sys.argv[1].encode()) == 0, lib.fbn_last_error()
+uid = (ctypes.c_char * lib.fbn_comm_id_bytes())()
+assert lib.fbn_comm_unique_id(uid) == 0
+world = 3
+hs = [ctypes.c_void_p() for _ in range(world)]
+for r in range(world):
+    assert lib.fbn_comm_init(ctypes.byref(hs[r]), uid, world, r) == 0
+assert lib.fbn_comm_watchdog_fired(None) == 0
+assert lib.fbn_comm_watch(ctypes.c_longlong(700)) == 0
+assert lib.fbn_comm_heartbeat(None) == 0          # a step began (no stream: the beat alone)
+res = {}
+eq = [np.arange(world * 4, dtype=np.int32) for _ in range(world)]
+out = [np.zeros(world * 4, dtype=np.int32) for _ in range(world)]
+
+def rank(r):
+    # rank 2 never posts: ranks 0 and 1 wait for its blocks
+    t0 = time.perf_counter()
+    rc = lib.fbn_comm_alltoall_peers(hs[r], eq[r].ctypes.data_as(ctypes.c_void_p), out[r].ctypes.data_as(ctypes.c_void_p),
+                                     ctypes.c_longlong(16), None)
+    res[r] = (rc, time.perf_counter() - t0, lib.fbn_last_error().decode())
+
+ts = [threading.Thread(target=rank, args=(r,)) for r in (0, 1)]
+[t.start() for t in ts]
+[t.join(30) for t in ts]
+for r in (0, 1):
+    rc, dt, msg = res[r]
+    assert rc != 0 and dt < 10.0, (r, rc, dt, msg)       # released by the watchdog, not the mock's 20 s
+    assert "watchdog" in msg, msg
+assert lib.fbn_comm_watchdog_fired(None) == 1
+assert all(lib.fbn_comm_watchdog_fired(h) == 1 for h in hs)
+# every later call fails at once with the watchdog's message
+rc = lib.fbn_comm_allreduce(hs[2], eq[2].ctypes.data_as(ctypes.c_void_p), ctypes.c_longlong(4), 2, None)
+assert rc == 3 and "aborted by the watchdog" in lib.fbn_last_error().decode(), lib.fbn_last_error()
+for h in hs:
+    assert lib.fbn_comm_destroy(h) == 0
+print("ok")
+""")
+
+
+def test_native_comm_watchdog_aborts_a_hung_exchange(tmp_path):
+    """The watchdog of the native communicators (they bypass torch's collective timeout):
+    three ranks, rank 2 never posts its all-to-all blocks; ranks 0 and 1 block in the exchange.  With
+    fbn_comm_watch(700 ms) and a heartbeat at the step's start, the monitor aborts every communicator
+    after ~0.7 s: both blocked calls return an error naming the watchdog (well before the stand-in's own
+    20 s receive timeout), fbn_comm_watchdog_fired reports it, and any later call fails at once."""
+    so = str(tmp_path / "libmock_rccl.so")
+    r = subprocess.run(["g++", "-O1", "-shared", "-fPIC", "-std=c++17", "-o", so, os.path.join(HERE, "mock_rccl.cpp"),
+                        "-lpthread"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    script = tmp_path / "watch.py"
+    script.write_text(WATCHDOG_CHILD)
+    p = subprocess.run([sys.executable, str(script), so, os.path.dirname(HERE)], capture_output=True, text=True,
+                       timeout=120)
+    assert p.returncode == 0 and p.stdout.strip().endswith("ok"), (p.stdout[-2000:], p.stderr[-3000:])

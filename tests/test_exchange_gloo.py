@@ -214,3 +214,42 @@ def test_loader_check_raises_on_every_rank():
     for p in procs:
         p.join(timeout=60)
     assert res == [(r, "raised") for r in range(world)], res
+
+
+def _agree_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        # all ranks equal -> valid, no differing step
+        a = bench._ab_agree(True, -1, "cpu")
+        # rank 1 saw its losses part at step 5, rank 2 only a final-state difference (no loss step)
+        b = bench._ab_agree(rank not in (1, 2), 5 if rank == 1 else -1, "cpu")
+        # two ranks with differing first steps: the earliest wins
+        c = bench._ab_agree(rank == 0, {1: 9, 2: 4}.get(rank, -1), "cpu")
+        q.put((rank, a, b, c))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_native_ab_agreement():
+    """bench.py's lockstep A/B of the native-RCCL path against torch.distributed (native_ab) decides on
+    EVERY rank together: the native path is validated only if every rank saw bitwise-equal runs, and
+    the first differing step reported is the earliest over the ranks -- so all ranks time the same
+    path (a rank timing the other one would deadlock the collectives)."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_agree_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, a, b, c in res:
+        assert a == (True, -1), (rank, a)
+        assert b == (False, 5), (rank, b)
+        assert c == (False, 4), (rank, c)

@@ -181,3 +181,42 @@ def test_sharded_deterministic_matches_single_gpu_bitwise(hip_device):
     l0, l1 = out["losses"]
     assert l0 == l1, (l0, l1)
     assert all(out["equal"].values()), (out["equal"], out["maxdiff"])
+
+
+def _ab_worker(port, dtype, q):
+    import argparse
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        import bench
+        args = argparse.Namespace(dim=128, batch=1024, rows_per_gpu=60000, dtype=dtype, zipf=0.0, bn="local")
+        q.put(("ok", bench.native_ab(args, 1, 0, dev)))
+    except Exception as e:
+        q.put((repr(e), None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_bench_native_ab_one_rank(hip_device, dtype):
+    """bench.py's A/B of the two collective paths (native_ab) as a one-rank RCCL job: native RCCL +
+    step programs (calibration, recording pass, replay passes, the watchdog armed) against
+    torch.distributed's eager steps, deterministic: validated -- every loss and the final table,
+    moments and dense state bitwise equal -- with the native run really in programs over the
+    fixed-capacity exchange."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_ab_worker, args=(_port(), dtype, q))
+    p.start()
+    status, ab = q.get(timeout=300)
+    p.join(timeout=60)
+    assert status == "ok", status
+    print(f"native_ab[{dtype}]: {ab}")
+    assert ab["native_healthy"] and not ab["watchdog_fired"], ab
+    assert ab["native"]["programs"] == ab["batches"] and ab["native"]["fc_active"], ab
+    assert ab["native"]["collectives"] == "native" and ab["torch"]["collectives"] == "torch", ab
+    assert ab["validated"] and ab["first_diff_step"] == -1, ab
