@@ -261,6 +261,59 @@ def persistent(fn):
     return box["out"]
 
 
+def pool_segments(pool) -> list:
+    """[(start, end)) device address ranges of the segments a torch.cuda.MemPool owns (from the caching
+    allocator's snapshot): the step programs' recording pool, for check_outside_pool()."""
+    pid = tuple(pool.id)
+    out = []
+    for seg in torch.cuda.memory_snapshot():
+        if tuple(seg.get("segment_pool_id", ())) == pid:
+            out.append((int(seg["address"]), int(seg["address"]) + int(seg["total_size"])))
+    return sorted(out)
+
+
+def tensors_of(obj, _seen=None, _path="", _depth=0):
+    """(path, tensor) for every device tensor reachable from obj through attributes, dicts, lists and
+    tuples (the objects of this package only: a trainer, its exchange, routing sets, caches)."""
+    seen = set() if _seen is None else _seen
+    if id(obj) in seen or _depth > 8:
+        return
+    seen.add(id(obj))
+    if isinstance(obj, torch.Tensor):
+        if obj.is_cuda and obj.numel():
+            yield _path, obj
+        return
+    if isinstance(obj, dict):
+        for k, v in obj.items():
+            yield from tensors_of(v, seen, f"{_path}[{k!r}]", _depth + 1)
+    elif isinstance(obj, (list, tuple)):
+        for i, v in enumerate(obj):
+            yield from tensors_of(v, seen, f"{_path}[{i}]", _depth + 1)
+    elif type(obj).__module__.startswith("ctr_recommendation_amd") and hasattr(obj, "__dict__"):
+        for k, v in vars(obj).items():
+            yield from tensors_of(v, seen, f"{_path}.{k}", _depth + 1)
+
+
+def check_outside_pool(obj, pool) -> None:
+    """The step programs' address-lifetime invariant: no tensor that outlives a step --
+    anything reachable from obj (a trainer: its persistent state, its exchange's routing sets, its
+    caches) -- may lie in the recording pool.  The pool hands its freed blocks to the next recording,
+    and every replay of the program that recorded a temporary at such an address overwrites it (round
+    5: the sharded fold buffer).  Raises RuntimeError naming the offending tensors."""
+    segs = pool_segments(pool)
+    bad = []
+    for path, t in tensors_of(obj):
+        lo = t.data_ptr()
+        hi = lo + t.untyped_storage().nbytes()
+        for a, b in segs:
+            if lo < b and a < hi:
+                bad.append(f"{path} [{lo:#x}, {hi:#x})")
+                break
+    if bad:
+        raise RuntimeError("tensors that outlive the step lie in the step programs' recording pool "
+                           "(allocate them through _lib.persistent): " + "; ".join(bad[:12]))
+
+
 def wait_stream(dst, src) -> None:
     """dst.wait_stream(src), recorded as a stream edge while a step program is being recorded."""
     dst.wait_stream(src)

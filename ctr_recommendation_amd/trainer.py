@@ -117,6 +117,9 @@ _OWNER_CLAIM_FUSED = os.environ.get("FBN_OWNER_CLAIM_FUSED", "1") != "0"
 # fbn_sparse_fixup (A/B)
 _SHARD_W16_SIDE = os.environ.get("FBN_SHARD_W16_SIDE", "1") != "0"
 _OWNER_FOLD = os.environ.get("FBN_OWNER_FOLD", "1") != "0"
+# debug: after every record_program, check that no tensor of the trainer's persistent state lies in the
+# recording pool (check_program_memory; the tests run it explicitly)
+_CHECK_POOL = os.environ.get("FBN_CHECK_POOL", "0") == "1"
 from .schedule import OneCycle, adam_table
 
 TABLE = "item_emb.weight"
@@ -991,7 +994,17 @@ class FiBiNETTrainer:
         prog.batch_ids = (batch["item_id"], seq if seq is not None and seq.shape[1] else None)
         # the tensors the recorded calls address
         prog.keep += [batch, labels, next_batch, dict(self.acts)]
+        if _CHECK_POOL:
+            self.check_program_memory(prog.pool)
         return prog
+
+    def check_program_memory(self, pool) -> None:
+        """Debug check of the step programs' address-lifetime invariant (FBN_CHECK_POOL=1 runs it after
+        every record_program): no tensor of the trainer's persistent state -- parameters, moments,
+        claims, rings, the exchange's buffers and routing sets, cached scratch and activation buffers --
+        lies in the recording pool `pool` (_lib.check_outside_pool)."""
+        torch.cuda.synchronize(self.device)
+        _lib.check_outside_pool(self, pool)
 
     def run_program(self, prog: "_lib.StepProgram") -> torch.Tensor:
         """One training step by replaying a recorded step program (see record_program)."""

@@ -190,9 +190,13 @@ def oracle_data(p):
     return darray, BatchCollatorRef(20, ci, p["item_info"]), varray, BatchCollatorRef(20, vci, p["item_info"])
 
 
-def run_launcher(p, root, deterministic=True):
+def run_launcher(p, root, deterministic=True, noise_seed=0):
     """The launcher (python -m ctr_recommendation_amd.train) over the parity data on cuda:0:
-    {"perms": the train loader's epoch permutations, "auc", "loss", "probs": final valid probabilities}."""
+    {"perms": the train loader's epoch permutations, "auc", "loss", "probs": final valid probabilities}.
+    noise_seed k > 0: the HIP side of the ensemble -- after every step each trained parameter (the dense
+    flat buffer and the item table) is multiplied by (1 + 2^-24 N(0,1)) in float64 and rounded back to
+    fp32, as the oracle's f64_n<k> members are perturbed (device generator seeded k; test tooling,
+    torch ops on the trainer's tensors between steps, nothing in the product path)."""
     from ctr_recommendation_amd.loader import ColumnarDataset, DeviceLoader, ItemInfoTable
     from ctr_recommendation_amd.train import load_config, run
     cfg_path = os.path.join(root, "fibinet_config.yaml")
@@ -211,9 +215,19 @@ def run_launcher(p, root, deterministic=True):
     from ctr_recommendation_amd.trainer import FiBiNETTrainer
     orig_step, step_loss = FiBiNETTrainer.step, []
 
+    gen = None
+    if noise_seed:
+        gen = torch.Generator(device="cuda:0")
+        gen.manual_seed(int(noise_seed))
+
     def rec_step(self, *a, **k):
         out = orig_step(self, *a, **k)
         step_loss.append(float(out.item()))
+        if gen is not None:
+            with torch.no_grad():
+                for t in (self.flat_p, self.E):
+                    f = 1.0 + 2.0 ** -24 * torch.randn(t.shape, generator=gen, device=t.device, dtype=torch.float64)
+                    t.copy_((t.double() * f).to(t.dtype))
         return out
     FiBiNETTrainer.step = rec_step
     try:

@@ -88,6 +88,9 @@ def test_program_replay_bit_identical_to_eager(hip_device, d, dtype, det, shared
     for k in ("mlp.1.running_mean", "mlp.1.running_var", "mlp.5.running_mean", "mlp.5.num_batches_tracked"):
         assert torch.equal(eager.p[k], prog_tr.p[k]), k
     assert all(len(p) > 10 for p in progs.values())
+    # the address-lifetime invariant: nothing of the trainer's persistent state in a recording pool
+    for pg in {id(p.pool): p.pool for p in progs.values()}.values():
+        prog_tr.check_program_memory(pg)
     # out of the recorded order (the previous step prefetched another batch): refused
     with pytest.raises(RuntimeError, match="out of order"):
         prog_tr.run_program(progs[(steps + 1) % nb])
@@ -129,6 +132,31 @@ def test_persistent_allocation_escapes_recording_pool(hip_device):
     assert kept.data_ptr() != addr and again.data_ptr() == addr, (hex(kept.data_ptr()), hex(addr))
     torch.cuda.synchronize()
     assert float(kept.abs().max()) == 0.0
+
+
+def test_pool_invariant_check_catches_a_pool_allocated_buffer(hip_device):
+    """check_program_memory flags round 5's bug (7122b93's old allocation path): a buffer that outlives
+    the step, allocated INSIDE a recording without _lib.persistent, lands in the recording pool -- the
+    check names it; the same buffer through _lib.persistent passes."""
+    from ctr_recommendation_amd import _lib
+    V, B, d = 20000, 256, 128
+    cfg = {"embedding_dim": d, "vocab_size": V, "compute_dtype": "bf16"}
+    torch.manual_seed(0)
+    init = oracle_build(None, dict(cfg, honour_config=False)).state_dict()
+    tr = _trainer(cfg, init, B, hip_device)
+    bs = [tuple(t.to(hip_device) if not isinstance(t, dict) else {k: v.to(hip_device) for k, v in t.items()}
+                for t in make_batch(90 + j, B, V)) for j in range(2)]
+    tr.step(*bs[0], next_batch=bs[1][0])
+    pool = torch.cuda.MemPool()
+    prog = tr.record_program(*bs[1], next_batch=bs[0][0], pool=pool)
+    tr.check_program_memory(pool)                          # the tree: clean
+    with prog.recording(pool):
+        tr._fc_extra = torch.zeros((4096, d), device=hip_device)            # the old path: in the pool
+    with pytest.raises(RuntimeError, match="_fc_extra"):
+        tr.check_program_memory(pool)
+    with prog.recording(pool):
+        tr._fc_extra = _lib.persistent(lambda: torch.zeros((4096, d), device=hip_device))
+    tr.check_program_memory(pool)
 
 
 def test_program_refuses_unsupported_paths(hip_device):

@@ -105,6 +105,7 @@ def _worker(port, dtype, det, q):
                 except RuntimeError as e:
                     raise RuntimeError(f"step {i} (batch {j}): {e}") from e
         torch.cuda.synchronize()
+        prog_tr.check_program_memory(pool)      # the address-lifetime invariant
         res = {"caps": caps, "fallbacks": (eager.xchg.fc_fallbacks, prog_tr.xchg.fc_fallbacks),
                "fc": (eager.xchg.cap, prog_tr.xchg.cap), "losses": losses}
         for t in trs:
