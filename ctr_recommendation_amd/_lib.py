@@ -126,7 +126,7 @@ SIGNATURES = {
     "fbn_adam_owner_claim_catchup": (I, [P, I, I, P, P, P, P, P, P, LL, I, I, P, P, P, F, F, F, P, P, P, LL, I, I,
                                          P]),
     "fbn_owner_fold": (I, [P, I, I, P, P, P, I, P, LL, LL, P, I, LL, P, P, P, I, P, P, P]),
-    "fbn_sumsq_flagged": (I, [P, I, P, P, I, P, P, P, P]),
+    "fbn_sumsq_flagged": (I, [P, I, P, P, I, P, P, P, I, P]),
     "fbn_owner_claim": (I, [P, I, P, P, I, P]),
     "fbn_owner_gather": (I, [P, I, P, P, P, P, I, I, I, P]),
     "fbn_widen_bf16": (I, [P, P, LL, P]),

@@ -222,6 +222,11 @@ __global__ void adam_dense_kernel(float* __restrict__ p, const float* __restrict
 // the owner's received gradient rows in deferred-gradient ring slot step % ring_n, a slot chosen on
 // the device, so a recorded step program needs no host-side ring index)
 #define FBN_GRAD_CELL 0x20000
+// Lp1 | FBN_GRAD_BF16 (Lp1 == 1 only): the per-entry rows are bf16 (the sharded owner's bf16 deferred-
+// gradient ring: the bf16 mode's wire rows kept as they arrived; widened on every read)
+#define FBN_GRAD_BF16 0x40000
+// ring_n | FBN_RING_BF16 (PendSrc, fbn_owner_fold): the deferred-gradient ring holds bf16 rows
+#define FBN_RING_BF16 0x40000000
 #define FBN_FOLD_CHUNKS 1     // sparse_fixup_dup_kernel: 64-entry chunks per wave
 #define FBN_FOLD_THREADS 1024 // sparse_fixup_dup_kernel: 16 waves share one LDS table
 struct GradSrc {
@@ -231,10 +236,17 @@ struct GradSrc {
   int Lp1;
   int full;             // extra of a flagged claimer = the whole row gradient
   int cell;             // vec holds the address of a device cell with the row pointer (FBN_GRAD_CELL)
+  int bf16;             // per-entry rows stored as bf16 (FBN_GRAD_BF16; Lp1 == 1)
 };
 static inline GradSrc make_src(const float* vec, float* extra, int* slot_row, int lp1_flags) {
   return GradSrc{vec, extra, slot_row, lp1_flags & 0xffff, (lp1_flags & FBN_GRAD_FULL) ? 1 : 0,
-                 (lp1_flags & FBN_GRAD_CELL) ? 1 : 0};
+                 (lp1_flags & FBN_GRAD_CELL) ? 1 : 0, (lp1_flags & FBN_GRAD_BF16) ? 1 : 0};
+}
+__device__ __forceinline__ f32x4 widen_bf16x4(bf16x4 h) {
+  f32x4 x;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) x[k] = __uint_as_float((unsigned)(unsigned short)h[k] << 16);
+  return x;
 }
 // a kernel's first step with a GradSrc: FBN_GRAD_CELL's pointer read from its cell
 __device__ __forceinline__ void resolve_src(GradSrc& s) {
@@ -246,6 +258,21 @@ __device__ __forceinline__ const float* grad_base(const GradSrc& s, int e) {
   if (s.Lp1 == 1) return s.vec + (size_t)e * D;
   const int b = e / s.Lp1, t = e - b * s.Lp1;
   return s.vec + ((size_t)b * 2 + (t ? 1 : 0)) * D;
+}
+// elements [c, c + 4) of entry e's gradient, f32 (a bf16 per-entry row widened; branch-free as
+// ring_load: a bf16 row is read 16 B wide from its bf16 address, the ring padded for the last row)
+template <int D>
+__device__ __forceinline__ f32x4 grad4(const GradSrc& s, int e, int c) {
+  const char* a = s.bf16 ? reinterpret_cast<const char*>(s.vec) + 2 * ((size_t)e * D + c)
+                         : reinterpret_cast<const char*>(grad_base<D>(s, e) + c);
+  const f32x4 raw = *reinterpret_cast<const f32x4*>(a);
+  f32x4 x;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const unsigned w = __float_as_uint(raw[k >> 1]);
+    x[k] = s.bf16 ? __uint_as_float((k & 1) ? (w & 0xffff0000u) : (w << 16)) : raw[k];
+  }
+  return x;
 }
 
 // duplicates of a claimed row: single GPU -> extra[claimer] += vec(e) (and flag the claimer);
@@ -572,8 +599,8 @@ __global__ void __launch_bounds__(256) sumsq_sparse_kernel(GradSrc s, int n, dou
     const bool oka = ea < n, okb = eb < n;
     const int sra = oka ? s.slot_row[ea] : -1, srb = okb ? s.slot_row[eb] : -1;
     const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-    f32x4 va = oka ? *reinterpret_cast<const f32x4*>(grad_base<D>(s, (int)ea) + 4 * q) : z;
-    f32x4 vb = okb ? *reinterpret_cast<const f32x4*>(grad_base<D>(s, (int)eb) + 4 * q) : z;
+    f32x4 va = oka ? grad4<D>(s, (int)ea, 4 * q) : z;
+    f32x4 vb = okb ? grad4<D>(s, (int)eb, 4 * q) : z;
     if (sra != -1 && (sra & FBN_SLOT_FLAG)) {
       const f32x4 x = *reinterpret_cast<const f32x4*>(s.extra + (size_t)ea * D + 4 * q);
       va = s.full ? x : va + x;
@@ -628,7 +655,7 @@ __device__ __forceinline__ void adam_table_body(float* __restrict__ p, float* __
     f32x4 vv = __builtin_nontemporal_load(reinterpret_cast<f32x4*>(v + off));
     f32x4 gg = {0.f, 0.f, 0.f, 0.f};
     if (!UNTOUCHED_ONLY && u >= 0) {
-      gg = *reinterpret_cast<const f32x4*>(grad_base<D>(gs, u) + 4 * q);
+      gg = grad4<D>(gs, u, 4 * q);
       if (gs.extra && (gs.slot_row[u] & FBN_SLOT_FLAG)) {
         float* ex = gs.extra + (size_t)u * D + 4 * q;
         gg = gs.full ? *reinterpret_cast<const f32x4*>(ex) : gg + *reinterpret_cast<const f32x4*>(ex);
@@ -785,9 +812,31 @@ struct PendSrc {
   int* pend;
   const float* ring;
   const float* coef_hist;   // [steps] clip coefficient of each step
-  long long ring_stride;    // floats per ring slot (B * 2 * D)
+  long long ring_stride;    // elements per ring slot (B * 2 * D)
   int ring_n;
+  int bf16;                 // ring rows stored as bf16 (ring_n | FBN_RING_BF16 at the C ABI; sharded owner)
 };
+static inline PendSrc make_pend(int* pend, const float* ring, const float* coef_hist, long long stride, int ring_n) {
+  return PendSrc{pend, ring, coef_hist, stride, ring_n & ~FBN_RING_BF16, (ring_n & FBN_RING_BF16) ? 1 : 0};
+}
+// N ring elements at element offset go (f32, or bf16 widened).  Branch-free, as row_load needs (a load
+// under a branch makes hipcc drain every load in flight at the next use): ONE load of N floats' bytes
+// from the f32 address or the bf16 one -- a bf16 ring reads N bf16 values plus N more it ignores (the
+// trainer pads a bf16 ring by 16 elements so the last row's wider read stays inside the allocation) --
+// and the widening selected per element.
+template <typename V, int N>
+__device__ __forceinline__ V ring_load(const float* ring, int bf16, size_t go) {
+  const char* a = reinterpret_cast<const char*>(ring) + (bf16 ? 2 * go : 4 * go);
+  const V raw = *reinterpret_cast<const V*>(a);
+  V x;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    const unsigned w = __float_as_uint(raw[k >> 1]);
+    const float h = __uint_as_float((k & 1) ? (w & 0xffff0000u) : (w << 16));
+    x[k] = bf16 ? h : raw[k];
+  }
+  return x;
+}
 
 template <int D, bool DW>
 __device__ __forceinline__ void replay_rows(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
@@ -802,8 +851,8 @@ __device__ __forceinline__ void replay_rows(float* __restrict__ p, float* __rest
   if (ps.pend) {
     const int pe = ps.pend[(size_t)(r) * FBN_RS_I];
     if (pe >= 0) {   // step k0 with the deferred gradient (what fbn_adam_touched would have applied)
-      const f32x4 gg = *reinterpret_cast<const f32x4*>(ps.ring + (size_t)(k0 % ps.ring_n) * ps.ring_stride +
-                                                       (size_t)pe * D + 4 * q);
+      const f32x4 gg = ring_load<f32x4, 4>(ps.ring, ps.bf16, (size_t)(k0 % ps.ring_n) * ps.ring_stride +
+                                                                 (size_t)pe * D + 4 * q);
       const float coef = ps.coef_hist[k0];
       const AdamConsts k = k0 >= w0 ? win[k0 - w0] : table[k0];
       adam_tab4<DW>(pp, mm, vv, gg * coef, wd, b2, omb2, eps, k);
@@ -844,7 +893,7 @@ __device__ __forceinline__ void row_load(RowRegs& x, const float* __restrict__ p
   const float* ring = ps.ring ? ps.ring : p;
   const float* coef = ps.coef_hist ? ps.coef_hist : p;
   const size_t go = pe >= 0 ? (size_t)(k0 % ps.ring_n) * ps.ring_stride + (size_t)pe * D : 0;
-  x.g = *reinterpret_cast<const f32x4*>(ring + go + 4 * q);
+  x.g = ring_load<f32x4, 4>(ring, ps.bf16, go + 4 * q);
   x.c = coef[pe >= 0 ? k0 : 0];
   x.k = table[k0];
 }
@@ -908,7 +957,7 @@ __device__ __forceinline__ void wide_load(WideRow<D>& x, const float* __restrict
   const float* ring = ps.ring ? ps.ring : p;   // branch-free, as row_load
   const float* coef = ps.coef_hist ? ps.coef_hist : p;
   const size_t go = pe >= 0 ? (size_t)(k0 % ps.ring_n) * ps.ring_stride + (size_t)pe * D : 0;
-  x.g = *reinterpret_cast<const V*>(ring + go + lane * N);
+  x.g = ring_load<V, N>(ring, ps.bf16, go + lane * N);
   x.c = coef[pe >= 0 ? k0 : 0];
 }
 // rows a and b (k0a <= k0b after the sort): deferred-gradient steps, then the steps both still
@@ -1514,7 +1563,7 @@ __device__ __forceinline__ void replay_narrow_sorted(int r, int key, int pe, int
     const float* ring = ps.ring ? ps.ring : p;   // branch-free, as row_load
     const float* coef = ps.coef_hist ? ps.coef_hist : p;
     const size_t go = pp >= 0 ? (size_t)(k0 % ps.ring_n) * ps.ring_stride + (size_t)pp * D : 0;
-    x.g = *reinterpret_cast<const f32x4*>(ring + go + 4 * q);
+    x.g = ring_load<f32x4, 4>(ring, ps.bf16, go + 4 * q);
     x.c = coef[pp >= 0 ? k0 : 0];
   };
   int rc, kc, pc;
@@ -1967,7 +2016,7 @@ __global__ void __launch_bounds__(256) adam_touched_kernel(float* __restrict__ p
     const int sr = gs.slot_row[e];
     if (sr == -1) continue;
     const long long r = sr & ~FBN_SLOT_FLAG;
-    f32x4 gg = *reinterpret_cast<const f32x4*>(grad_base<D>(gs, (int)e) + 4 * q);
+    f32x4 gg = grad4<D>(gs, (int)e, 4 * q);
     if (sr & FBN_SLOT_FLAG) {
       float* ex = gs.extra + (size_t)e * D + 4 * q;
       gg = gs.full ? *reinterpret_cast<const f32x4*>(ex) : gg + *reinterpret_cast<const f32x4*>(ex);
@@ -2062,7 +2111,7 @@ __device__ __forceinline__ void adam_commit_body(float* __restrict__ p, float* _
       for (int h = 0; h < 2; ++h) {
         const int c = 8 * q8 + 4 * h;
         if (D < 8 && c >= D) break;
-        f32x4 gg = *reinterpret_cast<const f32x4*>(grad_base<D>(gs, (int)ee) + c);
+        f32x4 gg = grad4<D>(gs, (int)ee, c);
         if (sr_l & FBN_SLOT_FLAG) {   // duplicates folded into extra (the only claimers with one)
           float* ex = gs.extra + (size_t)ee * D + c;
           gg = gs.full ? *reinterpret_cast<const f32x4*>(ex) : gg + *reinterpret_cast<const f32x4*>(ex);
@@ -2301,6 +2350,10 @@ __global__ void __launch_bounds__(256) ring_slot_kernel(float* __restrict__ ring
 extern "C" int fbn_ring_slot(float* ring, int ring_n, long long stride, const int* step, void* cell, const void* wire,
                              int wire_bf16, long long n, const void* wire_self, long long self_lo, long long self_n,
                              void* stream) {
+  if (ring_n & FBN_RING_BF16) {
+    fbn_set_error("fbn_ring_slot: f32 rings only (a bf16 ring is filled by fbn_owner_fold)");
+    return FBN_ERR_ARG;
+  }
   if (!ring || !step || !cell || ring_n < 1 || n < 0 || n > stride || (n & 7) || (n > 0 && !wire) ||
       ((uintptr_t)ring & 15) || (stride & 7) || ((uintptr_t)wire & 15) || ((uintptr_t)wire_self & 15) ||
       (self_lo & 7) || (self_n & 7) || self_lo < 0 || self_n < 0 || self_lo + self_n > n ||
@@ -2333,10 +2386,12 @@ __global__ void __launch_bounds__(256) owner_fold_kernel(const int* __restrict__
                                                          long long stride, const int* __restrict__ step,
                                                          float** __restrict__ cell, float* __restrict__ extra,
                                                          double* __restrict__ part,
-                                                         unsigned long long* __restrict__ fx) {
+                                                         unsigned long long* __restrict__ fx, int ring_bf16) {
   constexpr int G = D / 4, RPW = 64 / G;
   __shared__ double red[256];
-  float* dst = ring + (size_t)(*step % ring_n) * stride;
+  // (a bf16 ring: `stride` and the row offsets count bf16 elements; the slot address is still a float*)
+  float* dst = ring_bf16 ? reinterpret_cast<float*>(reinterpret_cast<short*>(ring) + (size_t)(*step % ring_n) * stride)
+                         : ring + (size_t)(*step % ring_n) * stride;
   if (blockIdx.x == 0 && threadIdx.x == 0) *cell = dst;
   const int lane = threadIdx.x & 63, q = lane % G;
   double acc = 0.0;   // sumsq: the claimers' own rows (a flagged claimer's duplicates: fbn_sumsq_flagged)
@@ -2351,15 +2406,19 @@ __global__ void __launch_bounds__(256) owner_fold_kernel(const int* __restrict__
     if (u < 0) continue;
     const void* src = (wire_self && e >= self_lo && e < self_lo + self_n) ? wire_self : wire;
     f32x4 x;
+    bf16x4 h;
     if (wire_bf16) {
-      const bf16x4 h = reinterpret_cast<const bf16x4*>(src)[(size_t)e * (D / 4) + q];
+      h = reinterpret_cast<const bf16x4*>(src)[(size_t)e * (D / 4) + q];
 #pragma unroll
       for (int k = 0; k < 4; ++k) x[k] = __uint_as_float((unsigned)(unsigned short)h[k] << 16);
     } else {
       x = reinterpret_cast<const f32x4*>(src)[(size_t)e * (D / 4) + q];
     }
     if (u == (int)e) {
-      reinterpret_cast<f32x4*>(dst)[(size_t)e * (D / 4) + q] = x;
+      if (ring_bf16)   // the wire's bf16 bits as they are (half the bytes of the widened f32 row)
+        reinterpret_cast<bf16x4*>(dst)[(size_t)e * (D / 4) + q] = h;
+      else
+        reinterpret_cast<f32x4*>(dst)[(size_t)e * (D / 4) + q] = x;
       acc += (double)(x[0] * x[0]) + (double)(x[1] * x[1]) + (double)(x[2] * x[2]) + (double)(x[3] * x[3]);
     } else {
       if (q == 0) atomicOr(&slot_row[u], FBN_SLOT_FLAG);
@@ -2401,7 +2460,7 @@ __global__ void __launch_bounds__(256) sumsq_flagged_kernel(const int* __restric
                                                             float* __restrict__ extra,
                                                             const double* __restrict__ part, int nparts,
                                                             double* __restrict__ sumsq,
-                                                            unsigned long long* __restrict__ fx) {
+                                                            unsigned long long* __restrict__ fx, int ring_bf16) {
   constexpr int G = D / 4, RPW = 64 / G;
   __shared__ double red[256];
   const float* src = *cell;
@@ -2425,7 +2484,7 @@ __global__ void __launch_bounds__(256) sumsq_flagged_kernel(const int* __restric
       }
       if (mine < 0) continue;
       const long long ee = e0 + mine;
-      const f32x4 x = *reinterpret_cast<const f32x4*>(src + (size_t)ee * D + 4 * q);
+      const f32x4 x = ring_load<f32x4, 4>(src, ring_bf16, (size_t)ee * D + 4 * q);
       f32x4 t;
       if (fx) {
         unsigned long long* a = fx + (size_t)ee * D + 4 * q;
@@ -2458,21 +2517,26 @@ extern "C" int fbn_owner_fold(const int* ids, int n, int rank, const int* map, i
                               int ring_n, long long stride, const int* step, void* cell, float* extra, int D,
                               double* part, unsigned long long* fx, void* stream) {
   if (n <= 0) return FBN_OK;
+  const int ring_bf16 = (ring_n & FBN_RING_BF16) ? 1 : 0;
+  ring_n &= ~FBN_RING_BF16;
   if (!ids || !map || !slot_row || !wire || !ring || !step || !cell || !extra || ring_n < 1 ||
-      (long long)n * D > stride || self_lo < 0 || self_n < 0 || (self_n > 0 && !wire_self)) {
-    fbn_set_error("fbn_owner_fold: ids, map, slot_row, wire, ring, step, cell, extra; n * D <= stride");
+      (long long)n * D > stride || self_lo < 0 || self_n < 0 || (self_n > 0 && !wire_self) ||
+      (ring_bf16 && !wire_bf16)) {
+    fbn_set_error("fbn_owner_fold: ids, map, slot_row, wire, ring, step, cell, extra; n * D <= stride; a bf16 ring "
+                  "takes bf16 wire rows");
     return FBN_ERR_ARG;
   }
   hipStream_t st = (hipStream_t)stream;
   FBN_DISPATCH_D(owner_fold_kernel, D, group_grid(n, D, FBN_FOLD_PARTS), ids, n, rank, map, slot_row, wire,
                  wire_bf16, self_n > 0 ? wire_self : nullptr, self_lo, self_n, ring, ring_n, stride, step,
-                 (float**)cell, extra, part, fx);
+                 (float**)cell, extra, part, fx, ring_bf16);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
 
 extern "C" int fbn_sumsq_flagged(const int* slot_row, int n, const void* cell, float* extra, int D,
-                                 const double* part, double* sumsq, unsigned long long* fx, void* stream) {
+                                 const double* part, double* sumsq, unsigned long long* fx, int ring_bf16,
+                                 void* stream) {
   if (n <= 0) return FBN_OK;
   if (!slot_row || !cell || !extra || !sumsq) {
     fbn_set_error("fbn_sumsq_flagged: slot_row, cell, extra, sumsq");
@@ -2485,7 +2549,7 @@ extern "C" int fbn_sumsq_flagged(const int* slot_row, int n, const void* cell, f
   if (blocks > (fx ? FBN_SUMSQ_SLOTS : 1024)) blocks = fx ? FBN_SUMSQ_SLOTS : 1024;
   const int nparts = part ? (int)group_grid(n, D, FBN_FOLD_PARTS).x : 0;   // fbn_owner_fold's grid on the same n
   FBN_DISPATCH_D(sumsq_flagged_kernel, D, dim3(blocks), slot_row, n, (float* const*)cell, extra, part, nparts, sumsq,
-                 fx);
+                 fx, ring_bf16);
   FBN_CHECK_LAUNCH();
   return FBN_OK;
 }
@@ -2495,6 +2559,10 @@ extern "C" int fbn_sparse_fixup(const int64_t* item, const int64_t* seq, const i
                                 int rank, const int* map, const float* gvec, float* extra, int* slot_row, int Lp1,
                                 int D, void* stream) {
   if (n <= 0) return FBN_OK;
+  if (Lp1 & FBN_GRAD_BF16) {
+    fbn_set_error("fbn_sparse_fixup: f32 rows only (bf16 rows are folded by fbn_owner_fold)");
+    return FBN_ERR_ARG;
+  }
   hipStream_t st = (hipStream_t)stream;
   const GradSrc s = make_src(gvec, extra, slot_row, Lp1);
   FBN_DISPATCH_D(sparse_fixup_kernel, D, group_grid(n, D, 8192), item, L > 0 ? seq : nullptr, ids, n, L, V, rank,
@@ -2605,14 +2673,14 @@ extern "C" int fbn_adam_commit(float* p, float* m, float* v, int D, int* map, co
                                const int* step, float wd, float beta2, float eps, int* last, int* pend, float* ring,
                                float* coef_hist, int ring_n, int B, void* stream) {
   if (n <= 0) return FBN_OK;
-  if (!pend || !ring || !coef_hist || !extra || ring_n < 2 || (Lp1 & 0xffff) < 2) {
-    fbn_set_error("fbn_adam_commit: pend, ring, coef_hist and extra are required (single-GPU layout)");
+  if (!pend || !ring || !coef_hist || !extra || ring_n < 2 || (Lp1 & 0xffff) < 2 || (ring_n & FBN_RING_BF16)) {
+    fbn_set_error("fbn_adam_commit: pend, ring, coef_hist and extra are required (single-GPU layout, f32 ring)");
     return FBN_ERR_ARG;
   }
   hipStream_t st = (hipStream_t)stream;
   const float omb2 = (float)(1.0 - (double)beta2);
   const GradSrc s = make_src(gvec, extra, slot_row, Lp1);
-  const PendSrc ps{pend, ring, coef_hist, (long long)B * 2 * D, ring_n};
+  const PendSrc ps = make_pend(pend, ring, coef_hist, (long long)B * 2 * D, ring_n);
   int blocks = (n + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   FBN_DISPATCH_D(adam_commit_kernel, D, dim3(blocks), p, m, v, map, s, n, coef,
@@ -2632,7 +2700,7 @@ extern "C" int fbn_adam_step_tail(float* dp, const float* dg, float* dm, float* 
                                   int max_step, int* err, void* stream) {
   const int lp = Lp1 & 0xffff;
   if (!pend || !ring || !coef_hist || !sumsq || !ticket || ring_n < 2 || lp < 1 || (lp >= 2 && !extra) ||
-      (lp >= 2 && ring_stride != (long long)B * 2 * D)) {
+      (lp >= 2 && ring_stride != (long long)B * 2 * D) || (lp >= 2 && (ring_n & FBN_RING_BF16))) {
     fbn_set_error("fbn_adam_step_tail: pend, ring, coef_hist, sumsq, ticket (and extra with per-sample vectors, "
                   "ring_stride = B*2*D) are required");
     return FBN_ERR_ARG;
@@ -2640,7 +2708,7 @@ extern "C" int fbn_adam_step_tail(float* dp, const float* dg, float* dm, float* 
   hipStream_t st = (hipStream_t)stream;
   const float omb2 = (float)(1.0 - (double)beta2);
   const GradSrc s = make_src(gvec, extra, slot_row, Lp1);
-  const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
+  const PendSrc ps = make_pend(pend, ring, coef_hist, ring_stride, ring_n);
   const StepEnd se{step, rng, (double*)sumsq, nbt0, nbt1, ticket, max_step, err};
   long long nd = (n_dense / 4 + 255) / 256;
   // block caps (every block draws the step-end ticket; two-level, so ~16x less contention than
@@ -2705,7 +2773,7 @@ extern "C" int fbn_adam_catchup(float* p, float* m, float* v, long long nrows, i
     fbn_set_error("fbn_adam_catchup: deferred gradients need ring, coef_hist and ring_n > F");
     return FBN_ERR_ARG;
   }
-  const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
+  const PendSrc ps = make_pend(pend, ring, coef_hist, ring_stride, ring_n);
   // the window alone: the replay engine over FBN_WIN_ROWS rows per wave (FBN_WINDOW_ONEPASS=1 keeps
   // adam_catchup_kernel, A/B)
   static const bool wone = getenv("FBN_WINDOW_ONEPASS") && atoi(getenv("FBN_WINDOW_ONEPASS")) == 1;
@@ -2827,7 +2895,7 @@ extern "C" int fbn_adam_prefetch_binned(const int64_t* item, const int64_t* seq,
     return FBN_ERR_ARG;
   }
   if (pend && (!ring || !coef_hist)) { fbn_set_error("fbn_adam_prefetch_binned: pend needs ring and coef_hist"); return FBN_ERR_ARG; }
-  const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
+  const PendSrc ps = make_pend(pend, ring, coef_hist, ring_stride, ring_n);
   const ClaimSrc cs{item, L > 0 ? seq : nullptr, L, V, const_cast<int*>(map), nullptr, nullptr, nullptr, preclaim};
   return launch_prefetch_binned(cs, n, p, m, v, D, last, consts_table, step, wd, beta2, eps, ps, decoupled, ws,
                                 ws_bytes, (hipStream_t)stream);
@@ -2854,7 +2922,7 @@ extern "C" int fbn_adam_prefetch(const int64_t* item, const int64_t* seq, int B,
   }
   if (pend && (!ring || !coef_hist)) { fbn_set_error("fbn_adam_prefetch: pend needs ring and coef_hist"); return FBN_ERR_ARG; }
   const float omb2 = (float)(1.0 - (double)beta2);
-  const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
+  const PendSrc ps = make_pend(pend, ring, coef_hist, ring_stride, ring_n);
   const ClaimSrc cs{item, L > 0 ? seq : nullptr, L, V, const_cast<int*>(map), nullptr, nullptr, nullptr, preclaim};
   static const int pcap = getenv("FBN_PREFETCH_BLOCKS") ? atoi(getenv("FBN_PREFETCH_BLOCKS")) : 256;
   const dim3 grid((unsigned)std::min<long long>(pcap, (n + 63) / 64));
@@ -2957,7 +3025,7 @@ extern "C" int fbn_adam_prefetch_rows(const int* lids, int n, int skip0, long lo
     return FBN_ERR_ARG;
   }
   const float omb2 = (float)(1.0 - (double)beta2);
-  const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
+  const PendSrc ps = make_pend(pend, ring, coef_hist, ring_stride, ring_n);
   ClaimSrc cs{nullptr, nullptr, 0, nrows, const_cast<int*>(map), nullptr, nullptr, nullptr, nullptr};
   cs.lids = lids;
   cs.skip0 = skip0;
@@ -3046,7 +3114,7 @@ extern "C" int fbn_adam_owner_claim_catchup(const int* lids, int n, int skip0, i
   }
   hipStream_t st = (hipStream_t)stream;
   const float omb2 = (float)(1.0 - (double)beta2);
-  const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
+  const PendSrc ps = make_pend(pend, ring, coef_hist, ring_stride, ring_n);
   ClaimSrc cs{nullptr, nullptr, 0, nrows, map, slot_row, nullptr, nullptr, preclaim};
   cs.lids = lids;
   cs.skip0 = skip0;
@@ -3105,7 +3173,7 @@ static int claim_catchup_impl(const int64_t* item, const int64_t* seq, int B, in
   hipStream_t st = (hipStream_t)stream;
   const float omb2 = (float)(1.0 - (double)beta2);
   const long long chunk = (nrows + F - 1) / F;
-  const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
+  const PendSrc ps = make_pend(pend, ring, coef_hist, ring_stride, ring_n);
   const ClaimSrc cs{item, L > 0 ? seq : nullptr, L, V, map, slot_row, dup, hasdup, preclaim};
   // one entry per lane, row state in one round trip, the replay engine (adam_claim2_kernel);
   // FBN_CLAIM_ONEPASS=1 keeps the scans of adam_catchup_kernel (A/B)
@@ -3159,7 +3227,7 @@ extern "C" int fbn_adam_flush(float* p, float* m, float* v, long long nrows, int
   if (nrows <= 0) return FBN_OK;
   hipStream_t st = (hipStream_t)stream;
   const float omb2 = (float)(1.0 - (double)beta2);
-  const PendSrc ps{pend, ring, coef_hist, ring_stride, ring_n};
+  const PendSrc ps = make_pend(pend, ring, coef_hist, ring_stride, ring_n);
   if (decoupled) {
     FBN_DISPATCH_D_B(adam_flush_kernel, true, D, group_grid(nrows, D, 16384), p, m, v, nrows, last,
                      (const AdamConsts*)consts_table, step, wd, beta2, omb2, eps, ps);

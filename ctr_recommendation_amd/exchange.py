@@ -177,7 +177,12 @@ def _pad4(n: int) -> int:
     return (n + 3) // 4 * 4
 
 
-FC_MAX_SETS = 1024      # fixed-capacity routing sets kept (one per distinct batch; ~2 MB each at C3)
+# fixed-capacity routing sets kept, one per distinct batch (~2 MB of device memory each at C3, and a
+# pinned host word block): at most FC_SET_BYTES of them (FBN_FC_SET_BYTES, default 1 GiB; at least 8
+# sets), the oldest forgotten first.  A step program holds the sets its calls address (prog.keep), so
+# forgetting one never frees memory a program still uses; a forgotten batch is routed into a new set
+# the next time it comes round.
+FC_SET_BYTES = int(os.environ.get("FBN_FC_SET_BYTES", str(1 << 30)))
 
 
 class RowExchange:
@@ -276,9 +281,10 @@ class RowExchange:
     def _fc_routing_set(self, key):
         st = self.fc_sets.get(key)
         if st is None:
-            if len(self.fc_sets) >= FC_MAX_SETS:      # forget the oldest (a program holds its own)
-                self.fc_sets.pop(next(iter(self.fc_sets)))
             n = self.fc_slots
+            per_set = 4 * (2 * n + self.B * (self.L + 1) + 2 * _pad4(self.world + 1))
+            if len(self.fc_sets) >= max(8, FC_SET_BYTES // per_set):   # forget the oldest (a program holds its own)
+                self.fc_sets.pop(next(iter(self.fc_sets)))
             i32 = dict(dtype=torch.int32, device=self.device)
             # (a set outlives the step that routes into it: never from a program's recording pool)
             st = _lib.persistent(lambda: {
@@ -571,7 +577,8 @@ class RowExchange:
         else:
             grad = out[:n_recv] if out is not None else \
                 torch.empty((n_recv, self.d), dtype=torch.float32, device=sendbuf.device)
-            wire = grad if sendbuf.dtype == torch.float32 else \
+            # (rows of the send buffer's dtype land in `out` directly: f32, or a bf16 ring slot)
+            wire = grad if sendbuf.dtype == grad.dtype else \
                 (self.fc_wire if self.fc_active else
                  torch.empty((n_recv, self.d), dtype=sendbuf.dtype, device=sendbuf.device))
         work = None

@@ -105,6 +105,14 @@ _FC_CAP = int(os.environ.get("FBN_FC_CAP", "0"))
 _FC_MARGIN = float(os.environ.get("FBN_FC_MARGIN", "1.25"))
 FC_CALIB_STEPS = 2
 FBN_GRAD_CELL = 0x20000      # include/fibinet.h: the gradient-row argument is a device cell (fbn_ring_slot)
+FBN_GRAD_BF16 = 0x40000      # include/fibinet.h: the per-entry gradient rows are bf16
+FBN_RING_BF16 = 0x40000000   # include/fibinet.h: ring_n flag, the deferred-gradient ring holds bf16 rows
+# N > 1 in bf16 mode, opt-in (FBN_RING_BF16=1): the owner's deferred-gradient ring keeps the wire's bf16
+# gradient rows as they arrive (the fold copies them instead of widening them to f32: half the ring's
+# bytes written per step and read per replayed row; the same f32 values on every read -- bitwise equal,
+# tests/test_gpu_rccl.py).  Measured no faster at one rank (0.4825 vs 0.4787 ms/step), so
+# the f32 ring stays the default
+_RING_BF16 = os.environ.get("FBN_RING_BF16", "0") == "1"
 # N > 1, the owner's ahead-of-time catch-up of the next step's requested rows in two passes (tagged
 # pre-claims + the four-row replay engine); FBN_OWNER_PF2=0 keeps the one-pass kernel (A/B)
 _OWNER_PF2 = os.environ.get("FBN_OWNER_PF2", "1") != "0"
@@ -439,10 +447,12 @@ class FiBiNETTrainer:
         self.pend = self.ring = self.coef_hist = None
         self.ring_n = self.lazy_window + 1
         self.ring_cap = self.B * (max_len + 1) if sharded else 0
+        # sharded bf16 mode: a bf16 ring (the wire's rows as they arrived; _RING_BF16)
+        self.ring_bf16 = bool(sharded and self.fcfg.bf16 and _RING_BF16 and self.deferred)
         if self.deferred:
             self.pend = self.row_state[:, 3]
             shape = (self.ring_n, self.B, 2, d) if not sharded else (self.ring_n, self.ring_cap, d)
-            self.ring = torch.zeros(shape, dtype=torch.float32, device=dev)
+            self.ring = self._new_ring(shape)
             self.coef_hist = torch.ones(total_steps + 1, dtype=torch.float32, device=dev)
             self.ticket = torch.zeros(17, dtype=torch.int32, device=dev)    # fbn_adam_step_tail (FBN_TICKET_WORDS)
         # N > 1: forward + backward between the row exchanges replayed as hipGraph segments split at
@@ -812,23 +822,25 @@ class FiBiNETTrainer:
                     self._fc_extra = _lib.persistent(
                         lambda: torch.zeros((n_ent, d), dtype=torch.float32, device=self.device))
                 if defer_now:
-                    ring, ring_n, stride = self.ring, self.ring_n, self._ring_stride()
+                    ring, ring_n, stride = self.ring, self._ring_n_arg(), self._ring_stride()
                 else:
                     if self._fc_grad is None or self._fc_grad.shape[0] < n_ent:
                         self._fc_grad = _lib.persistent(
                             lambda: torch.empty((n_ent, d), dtype=torch.float32, device=self.device))
                     ring, ring_n, stride = self._fc_grad, 1, n_ent * d
-                if _OWNER_FOLD or self.deterministic:
+                rb = FBN_GRAD_BF16 if (defer_now and self.ring_bf16) else 0
+                if _OWNER_FOLD or self.deterministic or rb:
                     # the widen into the ring slot and the duplicate fold in one pass: a claimer's row is
                     # stored, a duplicate's added into extra[claimer] (flagged; applied at the tail); the
                     # claimers' squares summed on the way (the flagged ones corrected below).  Deterministic:
                     # the duplicates go to the fixed-point accumulator, extra becomes the FULL row gradient
-                    fx = self._det_fx(n_ent)
+                    fx = self._fold_bufs(n_ent)
                     call("fbn_owner_fold", ptr(x.recv_ids), n_ent, self.rank, ptr(self.map), ptr(self.slot_row),
                          ptr(wire), int(wire.dtype == torch.bfloat16), ptr(x.fc_send) if cnt else None, lo, cnt,
                          ptr(ring), ring_n, stride, ptr(self.step_dev), ptr(self.ring_cell), ptr(self._fc_extra), d,
                          ptr(self._fc_part), ptr(fx), st)
-                    gsrc = (self.ring_cell, self._fc_extra, 1 | FBN_GRAD_CELL | (FBN_GRAD_FULL if fx is not None else 0))
+                    gsrc = (self.ring_cell, self._fc_extra,
+                            1 | FBN_GRAD_CELL | rb | (FBN_GRAD_FULL if fx is not None else 0))
                     fold_done = True
                 else:
                     call("fbn_ring_slot", ptr(ring), ring_n, stride, ptr(self.step_dev), ptr(self.ring_cell),
@@ -843,15 +855,19 @@ class FiBiNETTrainer:
                 else:
                     grows = x.backward(sendbuf, out=slot)
                 gsrc = (grows, None, 1)
-                if self.deterministic and n_ent > 0:
-                    # the host-split form (calibration steps, overflow fallbacks): the same
-                    # deterministic fold, in place over the received rows (the claimer's row is
-                    # rewritten with itself; ring_n 1, the cell -> grows)
-                    fx = self._det_fx(n_ent)
+                g16 = grows.dtype == torch.bfloat16          # received straight into a bf16 ring slot
+                if (self.deterministic or g16) and n_ent > 0:
+                    # the host-split form (calibration steps, overflow fallbacks): the owner fold in
+                    # place over the received rows (the claimer's row is rewritten with itself; ring_n
+                    # 1, the cell -> grows) -- deterministic (fixed point), or a bf16 ring slot (no
+                    # float atomics into bf16 rows: the duplicates go to extra)
+                    fx = self._fold_bufs(n_ent)
                     call("fbn_owner_fold", ptr(x.recv_ids), n_ent, self.rank, ptr(self.map), ptr(self.slot_row),
-                         ptr(grows), 0, None, 0, 0, ptr(grows), 1, n_ent * d, ptr(self.step_dev), ptr(self.ring_cell),
-                         ptr(self._fc_extra), d, ptr(self._fc_part), ptr(fx), st)
-                    gsrc = (self.ring_cell, self._fc_extra, 1 | FBN_GRAD_CELL | FBN_GRAD_FULL)
+                         ptr(grows), int(g16), None, 0, 0, ptr(grows), 1 | (FBN_RING_BF16 if g16 else 0), n_ent * d,
+                         ptr(self.step_dev), ptr(self.ring_cell), ptr(self._fc_extra), d, ptr(self._fc_part), ptr(fx),
+                         st)
+                    gsrc = (self.ring_cell, self._fc_extra, 1 | FBN_GRAD_CELL | (FBN_GRAD_BF16 if g16 else 0) |
+                            (FBN_GRAD_FULL if fx is not None else 0))
                     fold_done = True
             if not fold_done:
                 call("fbn_sparse_fixup", None, None, ptr(x.recv_ids), n_ent, 0, self.V, self.rank, ptr(self.map),
@@ -869,7 +885,8 @@ class FiBiNETTrainer:
         elif fold_done:
             # the fold summed the claimers' own rows; only the flagged ones (duplicates) remain
             call("fbn_sumsq_flagged", ptr(self.slot_row), n_ent, ptr(self.ring_cell), ptr(self._fc_extra), d,
-                 ptr(self._fc_part), ptr(tab_acc), ptr(self._fx_sh) if self.deterministic else None, st)
+                 ptr(self._fc_part), ptr(tab_acc), ptr(self._fx_sh) if self.deterministic else None,
+                 int(bool(gsrc[2] & FBN_GRAD_BF16)), st)
         else:
             call("fbn_sumsq_sparse", ptr(gsrc[0]), ptr(gsrc[1]), ptr(self.slot_row), gsrc[2], n_ent, d, ptr(tab_acc),
                  st)
@@ -905,7 +922,7 @@ class FiBiNETTrainer:
                  self.n_dense, ptr(self.sumsq), self.max_norm, ptr(self.coef), ptr(self.norm), ptr(self.E),
                  ptr(self.Em), ptr(self.Ev), d, ptr(self.map), ptr(gsrc[0]), ptr(gsrc[1]), ptr(self.slot_row), gsrc[2],
                  n_ent, ptr(self.sched), ptr(self.step_dev), self.wd_g, self.beta2, self.eps, ptr(self.last),
-                 ptr(self.pend), ptr(self.ring), ptr(self.coef_hist), self.ring_n, self._ring_stride(), self.B,
+                 ptr(self.pend), ptr(self.ring), ptr(self.coef_hist), self._ring_n_arg(), self._ring_stride(), self.B,
                  ptr(self.rng),
                  ptr(self.p["mlp.1.num_batches_tracked"]), ptr(self.p["mlp.5.num_batches_tracked"]), ptr(self.ticket),
                  self.total_steps, ptr(self.err), st)
@@ -992,8 +1009,12 @@ class FiBiNETTrainer:
         # very batch (a replay is valid only after such a step), and the step posted its next batch's
         prog.pre_needed, prog.batch_key, prog.pre_key_after = self._used_pre, key, self._pre_key
         prog.batch_ids = (batch["item_id"], seq if seq is not None and seq.shape[1] else None)
-        # the tensors the recorded calls address
-        prog.keep += [batch, labels, next_batch, dict(self.acts)]
+        # the tensors the recorded calls address -- the batch, the activation buffers, and every buffer of
+        # the trainer's own state as it is NOW: a buffer the trainer later replaces (a fold scratch grown
+        # by a larger host-split fallback step) stays alive for this program's replays instead of being
+        # freed under its recorded addresses (per-step scratch, zero at rest: the program and the eager
+        # steps each keep their own consistent)
+        prog.keep += [batch, labels, next_batch, dict(self.acts), [t for _, t in _lib.tensors_of(self)]]
         if _CHECK_POOL:
             self.check_program_memory(prog.pool)
         return prog
@@ -1074,31 +1095,42 @@ class FiBiNETTrainer:
         if self.deferred and n > self.ring_cap:
             self.flush()
             self.ring_cap = n
-            self.ring = _lib.persistent(
-                lambda: torch.zeros((self.ring_n, n, self.d), dtype=torch.float32, device=self.device))
+            self.ring = _lib.persistent(lambda: self._new_ring((self.ring_n, n, self.d)))
         # the duplicate fold's sums per claimer (zero at rest) and its per-workgroup sums of squares
         # (fbn_owner_fold's 8192-block cap), made here rather than inside a step
         if self._fc_extra is None or self._fc_extra.shape[0] < n:
             self._fc_extra = _lib.persistent(lambda: torch.zeros((n, self.d), dtype=torch.float32, device=self.device))
         if self._fc_part is None:
             self._fc_part = _lib.persistent(lambda: torch.zeros(8192, dtype=torch.float64, device=self.device))
-        self._det_fx(n)
+        # the fold's scratch sized for the host-split fallback too (up to every rank's entries at one
+        # owner), so a fallback step after recordings never has to grow it
+        self._fold_bufs(max(n, self.world * self.B * (self.L + 1)))
         self.fc_wanted = False
 
-    def _det_fx(self, n: int):
-        """Sharded, deterministic mode: the fold's fixed-point accumulator for n received slots (and
-        the extra rows and per-workgroup partials the fold writes), grown outside any recording pool;
-        None when not deterministic."""
-        if not self.deterministic:
-            return None
+    def _fold_bufs(self, n: int):
+        """Sharded: the owner fold's buffers for n received slots -- the duplicates' extra rows (zero at
+        rest), the per-workgroup partial sums of squares and, in deterministic mode, the fixed-point
+        accumulator (returned; None otherwise) -- grown outside any recording pool."""
         d = self.d
-        if self._fx_sh is None or self._fx_sh.shape[0] < n:
+        if self.deterministic and (self._fx_sh is None or self._fx_sh.shape[0] < n):
             self._fx_sh = _lib.persistent(lambda: torch.zeros((n, d), dtype=torch.int64, device=self.device))
         if self._fc_extra is None or self._fc_extra.shape[0] < n:
             self._fc_extra = _lib.persistent(lambda: torch.zeros((n, d), dtype=torch.float32, device=self.device))
         if self._fc_part is None:
             self._fc_part = _lib.persistent(lambda: torch.zeros(8192, dtype=torch.float64, device=self.device))
-        return self._fx_sh
+        return self._fx_sh if self.deterministic else None
+
+    def _new_ring(self, shape):
+        """The deferred-gradient ring: f32, or (ring_bf16) bf16 with 16 elements of padding past its end
+        (the kernels read a bf16 row with the width of an f32 one: csrc/optim.hip ring_load)."""
+        if not self.ring_bf16:
+            return torch.zeros(shape, dtype=torch.float32, device=self.device)
+        n = int(np.prod(shape))
+        return torch.zeros(n + 16, dtype=torch.bfloat16, device=self.device)[:n].view(shape)
+
+    def _ring_n_arg(self) -> int:
+        """ring_n as the C ABI takes it: | FBN_RING_BF16 for a bf16 ring."""
+        return self.ring_n | (FBN_RING_BF16 if self.ring_bf16 else 0)
 
     def _ring_stride(self) -> int:
         return self.B * 2 * self.d if not self.sharded else self.ring_cap * self.d
@@ -1177,7 +1209,7 @@ class FiBiNETTrainer:
         """(pend, ring, coef_hist, ring_stride, ring_n) of the deferred table gradients (NULLs when off)."""
         if not self.deferred:
             return (None, None, None, 0, 0)
-        return (ptr(self.pend), ptr(self.ring), ptr(self.coef_hist), self._ring_stride(), self.ring_n)
+        return (ptr(self.pend), ptr(self.ring), ptr(self.coef_hist), self._ring_stride(), self._ring_n_arg())
 
     def close(self) -> None:
         """Destroy the native RCCL communicators (the step's and the routing one) and their proxy

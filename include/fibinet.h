@@ -344,6 +344,14 @@ int fbn_sumsq_sparse_norms(const double* gnorm, const float* gvec, float* extra,
 /* Lp1 | FBN_GRAD_CELL: the gradient-row pointer argument is the address of a device cell holding the
  * row pointer (written by fbn_ring_slot) -- readers resolve it on the device */
 #define FBN_GRAD_CELL 0x20000
+/* Lp1 | FBN_GRAD_BF16 (per-entry rows, Lp1 == 1): the rows are bf16 -- the sharded owner's deferred-gradient
+ * ring in bf16 mode keeps the wire's bf16 gradient rows as they arrived (widened on every read: the same
+ * f32 values as a widened f32 ring, half its bytes). */
+#define FBN_GRAD_BF16 0x40000
+/* ring_n | FBN_RING_BF16 wherever a deferred-gradient ring is passed (pend / ring / coef_hist / ring_stride /
+ * ring_n argument groups, fbn_owner_fold): the ring's rows are bf16 and ring_stride counts bf16 elements
+ * (sharded owner, Lp1 == 1 only; fbn_ring_slot and fbn_sparse_fixup refuse it). */
+#define FBN_RING_BF16 0x40000000
 int fbn_sparse_fold_fx(const int* dup, int* hasdup, int n, const float* gvec, int* slot_row, int Lp1, int D,
                        unsigned long long* acc, void* stream);
 /* adam_table mode 0: every row (touched rows read their gradient through map); mode 1: only the
@@ -563,9 +571,9 @@ int fbn_owner_fold(const int* ids, int n, int rank, const int* map, int* slot_ro
  * gradient float(total) to extra[claimer] and resets fx -- readers then take Lp1 = 1 | FBN_GRAD_CELL |
  * FBN_GRAD_FULL.  The fold is bitwise reproducible and equal to the single-GPU deterministic fold on
  * the same entries; with fx, fbn_sumsq_flagged runs on at most FBN_SUMSQ_SLOTS workgroups (one f64
- * addition per norm slot). */
+ * addition per norm slot).  ring_bf16: the claimers' own rows behind `cell` are bf16 (FBN_RING_BF16). */
 int fbn_sumsq_flagged(const int* slot_row, int n, const void* cell, float* extra, int D, const double* part,
-                      double* sumsq, unsigned long long* fx, void* stream);
+                      double* sumsq, unsigned long long* fx, int ring_bf16, void* stream);
 /* bf16 -> f32 (n % 8 == 0, 16-B aligned): the owner's received bf16 gradient rows (bf16 mode). */
 int fbn_widen_bf16(const void* in, float* out, long long n, void* stream);
 /* out [world][cap + 1]: out[o][j] = send_ids[offsets[o] + j] for j < counts[o], else -1, and

@@ -19,6 +19,8 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
+from tests._spawn import spawn_and_wait
+
 pytestmark = pytest.mark.gpu
 
 
@@ -35,7 +37,7 @@ def _worker(port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev, store=dist.HashStore())
     try:
         from ctr_recommendation_amd.data import make_batch
         from ctr_recommendation_amd.trainer import FiBiNETTrainer
@@ -92,12 +94,7 @@ def _worker(port, q):
 
 
 def test_sharded_path_over_rccl_matches_single_gpu(hip_device):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    p = ctx.Process(target=_worker, args=(_port(), q))
-    p.start()
-    status, out = q.get(timeout=300)
-    p.join(timeout=60)
+    status, out = spawn_and_wait(_worker, (_port(),), timeout=300)
     assert status == "ok", status
     l0, l1, de, dp, e_max = out["fp32"]
     for a, b in zip(l0, l1):
@@ -121,7 +118,7 @@ def _det_worker(port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FBN_NATIVE_COMM="1")
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev, store=dist.HashStore())
     try:
         from ctr_recommendation_amd.data import make_batch
         from ctr_recommendation_amd.trainer import FiBiNETTrainer
@@ -167,12 +164,7 @@ def test_sharded_deterministic_matches_single_gpu_bitwise(hip_device):
     kernels on the same values).  Only the clip norm is summed in another order (per-sample vector
     norms vs the rows' squares); it enters the update only when the clip engages, which it does not at
     max_norm 10 here -- both norms are reported."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    p = ctx.Process(target=_det_worker, args=(_port(), q))
-    p.start()
-    status, out = q.get(timeout=300)
-    p.join(timeout=60)
+    status, out = spawn_and_wait(_det_worker, (_port(),), timeout=300)
     assert status == "ok", status
     print(f"det one-rank sharded vs single GPU: equal {out['equal']}, max |diff| {out['maxdiff']}, "
           f"norms {out['norm']}, fc {out['fc']}")
@@ -189,7 +181,7 @@ def _ab_worker(port, dtype, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev, store=dist.HashStore())
     try:
         import bench
         args = argparse.Namespace(dim=128, batch=1024, rows_per_gpu=60000, dtype=dtype, zipf=0.0, bn="local")
@@ -208,15 +200,61 @@ def test_bench_native_ab_one_rank(hip_device, dtype):
     torch.distributed's eager steps, deterministic: validated -- every loss and the final table,
     moments and dense state bitwise equal -- with the native run really in programs over the
     fixed-capacity exchange."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    p = ctx.Process(target=_ab_worker, args=(_port(), dtype, q))
-    p.start()
-    status, ab = q.get(timeout=300)
-    p.join(timeout=60)
+    status, ab = spawn_and_wait(_ab_worker, (_port(), dtype,), timeout=300)
     assert status == "ok", status
     print(f"native_ab[{dtype}]: {ab}")
     assert ab["native_healthy"] and not ab["watchdog_fired"], ab
     assert ab["native"]["programs"] == ab["batches"] and ab["native"]["fc_active"], ab
     assert ab["native"]["collectives"] == "native" and ab["torch"]["collectives"] == "torch", ab
     assert ab["validated"] and ab["first_diff_step"] == -1, ab
+
+
+def _ring_worker(port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FBN_NATIVE_COMM="1")
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev, store=dist.HashStore())
+    try:
+        from ctr_recommendation_amd import trainer as trmod
+        from ctr_recommendation_amd.data import make_batch
+        from oracle.fibinet_oracle import build_model
+        V, B, steps = 60000, 1024, 10
+        cfg = {"embedding_dim": 128, "vocab_size": V, "honour_config": True, "net_dropout": 0.0,
+               "compute_dtype": "bf16"}
+        torch.manual_seed(0)
+        init = build_model(None, cfg, honour_config=True).state_dict()
+        bs = [make_batch(300 + s, B, V, device=dev) for s in range(steps + 1)]
+        res = []
+        for ring16 in (True, False):
+            trmod._RING_BF16 = ring16
+            tr = trmod.FiBiNETTrainer(cfg, total_steps=20, batch_size=B, device=dev, deterministic=True,
+                                      init_state={k: v.clone() for k, v in init.items()}, shard=True)
+            assert tr.ring_bf16 == ring16 and tr.ring.dtype == (torch.bfloat16 if ring16 else torch.float32)
+            losses = [tr.step(bs[s][0], bs[s][1], next_batch=bs[s + 1][0]).item() for s in range(steps)]
+            tr.flush()
+            tr.check_ids()
+            res.append((losses, {n: getattr(tr, n).cpu().clone() for n in ("E", "Em", "Ev", "flat_p", "flat_m")},
+                        tr.xchg.fc_active))
+            tr.close()
+        (l0, t0, f0), (l1, t1, f1) = res
+        q.put(("ok", {"losses": (l0, l1), "fc": (f0, f1), "equal": {k: bool(torch.equal(t0[k], t1[k])) for k in t0}}))
+    except Exception as e:
+        q.put((repr(e), None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bf16_ring_bit_identical_to_f32_ring(hip_device):
+    """bf16 mode, sharded: the owner's deferred-gradient ring in bf16 (the wire's gradient rows kept as
+    they arrived; widened on every read) against the f32 ring (widened once on arrival) -- the same
+    f32 values reach every Adam step, so losses and the final table, moments and dense state are
+    bitwise equal (deterministic mode, through the calibration steps' host-split exchange and the
+    fixed-capacity form)."""
+    status, out = spawn_and_wait(_ring_worker, (_port(),), timeout=300)
+    assert status == "ok", status
+    assert all(out["fc"]), out["fc"]
+    l0, l1 = out["losses"]
+    assert l0 == l1, (l0, l1)
+    assert all(out["equal"].values()), out["equal"]

@@ -30,6 +30,8 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
+from tests._spawn import spawn_and_wait
+
 pytestmark = pytest.mark.gpu
 
 
@@ -47,7 +49,7 @@ def _worker(port, dtype, det, q):
                       FBN_DEBUG_FC=os.environ.get("FBN_DEBUG_FC", "0"))
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev, store=dist.HashStore())
     try:
         from ctr_recommendation_amd import _lib
         from ctr_recommendation_amd.data import make_batch
@@ -134,12 +136,7 @@ def _worker(port, dtype, det, q):
 
 @pytest.mark.parametrize("dtype,det", [("fp32", True), ("bf16", True), ("fp32", False)])
 def test_sharded_step_program_matches_eager_with_overflow_fallback(hip_device, dtype, det):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    p = ctx.Process(target=_worker, args=(_port(), dtype, det, q))
-    p.start()
-    status, res = q.get(timeout=300)
-    p.join(timeout=60)
+    status, res = spawn_and_wait(_worker, (_port(), dtype, det,), timeout=300)
     assert status == "ok", status
     assert res["caps"][0] > 0 and res["fc"][0] == res["fc"][1] == res["caps"][0], (res["caps"], res["fc"])
     # the rewritten batch overflowed once per pass over it (cycles 4 and 5), in both trainers

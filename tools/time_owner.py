@@ -61,9 +61,9 @@ def timeit(name, fn):
 timeit("owner_fold", lambda: call("fbn_owner_fold", ptr(ids), n, 0, ptr(mp), ptr(slot_row), ptr(wire), 1, None, 0, 0,
                                   ptr(ring), 2, n * D, ptr(step), ptr(cell), ptr(extra), D, ptr(part), None, st))
 timeit("sumsq_flagged", lambda: call("fbn_sumsq_flagged", ptr(slot_row), n, ptr(cell), ptr(extra), D, ptr(part),
-                                     ptr(out), None, st))
+                                     ptr(out), None, 0, st))
 timeit("sumsq_sparse (cell)", lambda: call("fbn_sumsq_sparse", ptr(cell), ptr(extra), ptr(slot_row), 1 | 0x20000, n, D,
-                                           ptr(out), None, st))
+                                           ptr(out), None, 0, st))
 timeit("sumsq_sparse (direct)", lambda: call("fbn_sumsq_sparse", ptr(ring), ptr(extra), ptr(slot_row), 1, n, D,
-                                             ptr(out), None, st))
+                                             ptr(out), None, 0, st))
 timeit("owner_gather", lambda: call("fbn_owner_gather", ptr(ids), n, ptr(E), ptr(reply), None, None, 0, D, 1, st))
