@@ -158,6 +158,8 @@ SIGNATURES = {
     "fbn_comm_alltoall_peers": (I, [P, P, P, LL, P]),
     "fbn_comm_alltoall": (I, [P, P, P, LL, P]),
     "fbn_comm_allreduce": (I, [P, P, LL, I, P]),
+    "fbn_comm_allgather": (I, [P, P, P, LL, P]),
+    "fbn_sum_slices": (I, [P, I, LL, I, P, P]),
     "fbn_comm_watch": (I, [LL]),
     "fbn_comm_heartbeat": (I, [P]),
     "fbn_comm_abort": (I, [P]),

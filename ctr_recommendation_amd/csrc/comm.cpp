@@ -49,6 +49,7 @@ struct Rccl {
   decltype(&ncclGroupEnd) group_end = nullptr;
   decltype(&ncclAllReduce) all_reduce = nullptr;
   decltype(&ncclAllToAll) all_to_all = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
   decltype(&ncclCommAbort) comm_abort = nullptr;   // optional (the watchdog)
 };
@@ -163,7 +164,8 @@ extern "C" int fbn_comm_load(const char* path) {
             bind(h, "ncclCommDestroy", &r.comm_destroy) && bind(h, "ncclSend", &r.send) &&
             bind(h, "ncclRecv", &r.recv) && bind(h, "ncclGroupStart", &r.group_start) &&
             bind(h, "ncclGroupEnd", &r.group_end) && bind(h, "ncclAllReduce", &r.all_reduce) &&
-            bind(h, "ncclAllToAll", &r.all_to_all) && bind(h, "ncclGetErrorString", &r.error_string);
+            bind(h, "ncclAllToAll", &r.all_to_all) && bind(h, "ncclAllGather", &r.all_gather) &&
+            bind(h, "ncclGetErrorString", &r.error_string);
   if (!ok) {
     fbn_set_error("fbn_comm_load: the library lacks an RCCL entry point");
     dlclose(h);
@@ -368,4 +370,21 @@ extern "C" int fbn_comm_allreduce(void* comm, void* buf, long long n, int dtype,
   ncclDataType_t t = dtype == 0 ? ncclFloat32 : (dtype == 1 ? ncclFloat64 : ncclInt32);
   ncclResult_t r = g_rccl.all_reduce(buf, buf, (size_t)n, t, ncclSum, c->comm, static_cast<hipStream_t>(stream));
   return r == ncclSuccess ? 0 : fail("fbn_comm_allreduce", r);
+}
+
+// All-gather of `bytes_per_rank` bytes from every rank into recv (rank order) -- with fbn_sum_slices,
+// deterministic mode's all-reduce: the ranks' contributions summed in rank order, the same bits on
+// every rank and whatever reduction algorithm RCCL would have picked.
+extern "C" int fbn_comm_allgather(void* comm, const void* send, void* recv, long long bytes_per_rank, void* stream) {
+  if (int rc = need_loaded("fbn_comm_allgather")) return rc;
+  Comm* c = static_cast<Comm*>(comm);
+  if (!c || bytes_per_rank < 0 || (bytes_per_rank > 0 && (!send || !recv))) {
+    fbn_set_error("fbn_comm_allgather: bad arguments");
+    return 1;
+  }
+  if (aborted(c, "fbn_comm_allgather")) return 3;
+  if (bytes_per_rank == 0) return 0;
+  ncclResult_t r = g_rccl.all_gather(send, recv, (size_t)bytes_per_rank, ncclUint8, c->comm,
+                                     static_cast<hipStream_t>(stream));
+  return r == ncclSuccess ? 0 : fail("fbn_comm_allgather", r);
 }

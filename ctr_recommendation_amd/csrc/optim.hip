@@ -3288,6 +3288,34 @@ __global__ void unpack_sumsq_kernel(const float* __restrict__ in, float* __restr
     atomicAdd(sumsq + (blockIdx.x & (FBN_SUMSQ_SLOTS - 1)), t);
   }
 }
+// out[i] = ((in[0][i] + in[1][i]) + in[2][i]) + ... -- the `ns` slices of an all-gather summed in rank
+// order (deterministic mode's all-reduce: fbn_comm_allgather + this).  dtype 0 = f32, 1 = f64.
+template <typename T>
+__global__ void sum_slices_kernel(const T* __restrict__ in, int ns, long long n, T* __restrict__ out) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    T s = in[i];
+    for (int k = 1; k < ns; ++k) s += in[(size_t)k * n + i];
+    out[i] = s;
+  }
+}
+extern "C" int fbn_sum_slices(const void* in, int ns, long long n, int dtype, void* out, void* stream) {
+  if (n <= 0) return FBN_OK;
+  if (!in || !out || ns < 1 || dtype < 0 || dtype > 1) {
+    fbn_set_error("fbn_sum_slices: in, out, ns >= 1, dtype 0 (f32) / 1 (f64)");
+    return FBN_ERR_ARG;
+  }
+  long long blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (dtype == 0)
+    fbn_launch(sum_slices_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+               (const float*)in, ns, n, (float*)out);
+  else
+    fbn_launch(sum_slices_kernel<double>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+               (const double*)in, ns, n, (double*)out);
+  FBN_CHECK_LAUNCH();
+  return FBN_OK;
+}
+
 extern "C" int fbn_pack_extras(const float* loss, double* tab_slots, float* out, void* stream) {
   fbn_launch(pack_extras_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, loss, tab_slots, out);
   FBN_CHECK_LAUNCH();

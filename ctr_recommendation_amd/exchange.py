@@ -108,6 +108,11 @@ class NativeComm:
     def allreduce_(self, t: torch.Tensor) -> None:
         call("fbn_comm_allreduce", self.handle, ptr(t), t.numel(), _DTYPE_CODE[t.dtype], _lib.stream_handle(t.device))
 
+    def allgather(self, out: torch.Tensor, inp: torch.Tensor) -> None:
+        """out [world * n] <- every rank's inp [n], in rank order."""
+        call("fbn_comm_allgather", self.handle, ptr(inp), ptr(out), inp.numel() * inp.element_size(),
+             _lib.stream_handle(out.device))
+
     def close(self) -> None:
         if self.handle:
             call("fbn_comm_destroy", self.handle)
@@ -621,16 +626,53 @@ class RowExchange:
 
 
 class DistCollective:
-    """SyncBN / gradient all-reduce hook for ops.forward/backward (sum over ranks)."""
+    """SyncBN / gradient all-reduce hook for ops.forward/backward (sum over ranks).
 
-    def __init__(self, world: int, group=None, stage_on_cpu: bool = False, comm: Optional[NativeComm] = None):
+    det (deterministic mode): the sum is an all-gather followed by the ranks' slices added in rank
+    order (fbn_sum_slices; a Python loop for CPU tensors) -- the same bits on every rank, from run to
+    run and on either collective path (native RCCL or torch.distributed), where ncclAllReduce's order
+    follows the reduction algorithm RCCL picks for the communicator."""
+
+    def __init__(self, world: int, group=None, stage_on_cpu: bool = False, comm: Optional[NativeComm] = None,
+                 det: bool = False):
         self.world = world
         self.group = group
         self.stage_on_cpu = stage_on_cpu
         self.comm = comm
+        self.det = det
+        self._gbuf = {}
+
+    def _allreduce_det(self, t: torch.Tensor) -> None:
+        n, w = t.numel(), self.world
+        flat = t.view(-1)
+        if not t.is_cuda:
+            parts = [torch.empty_like(flat) for _ in range(w)]
+            dist.all_gather(parts, flat, group=self.group)
+            acc = parts[0].clone()
+            for q in parts[1:]:
+                acc += q
+            flat.copy_(acc)
+            return
+        key = (n, t.dtype, t.device)
+        buf = self._gbuf.get(key)
+        if buf is None:
+            buf = self._gbuf[key] = _lib.persistent(lambda: torch.empty(w * n, dtype=t.dtype, device=t.device))
+        if self.comm is not None:
+            self.comm.allgather(buf, flat)
+        elif self.stage_on_cpu:
+            parts = [torch.empty(n, dtype=t.dtype) for _ in range(w)]
+            dist.all_gather(parts, flat.cpu(), group=self.group)
+            buf.copy_(torch.cat(parts))
+        else:
+            dist.all_gather_into_tensor(buf, flat, group=self.group)
+        call("fbn_sum_slices", ptr(buf), w, n, {torch.float32: 0, torch.float64: 1}[t.dtype], ptr(flat),
+             _lib.stream_handle(t.device))
 
     def allreduce_(self, t: torch.Tensor) -> None:
         if self.world <= 1:
+            return
+        if self.det:
+            self._allreduce_det(t)
             return
         if self.comm is not None:
             self.comm.allreduce_(t)

@@ -410,7 +410,8 @@ class FiBiNETTrainer:
         # (native_comm: True / False overrides FBN_NATIVE_COMM -- bench.py's lockstep A/B of the two paths)
         self.native_comm = NativeComm(world, rank, group, dev) \
             if (sharded or world > 1) and native_comm_wanted(dev, group, stage_on_cpu, force=native_comm) else None
-        self.coll = DistCollective(world, group, stage_on_cpu, comm=self.native_comm)
+        # (deterministic mode: the all-reduces as all-gather + rank-ordered sums, bitwise reproducible)
+        self.coll = DistCollective(world, group, stage_on_cpu, comm=self.native_comm, det=self.deterministic)
         # BatchNorm at N > 1.  sync_bn (default): statistics over the GLOBAL batch (one f64
         # all-reduce per BN layer and direction) -- the single-process reference run on the
         # global batch.  sync_bn=False: every rank normalises its own slice, which is what the
@@ -772,7 +773,7 @@ class FiBiNETTrainer:
                          extra_sums=[(a["loss_terms"], B, 1, self.loss, 1.0 / ntot)], probe=probe,
                          hooks=bhooks)
         dense_work = None
-        if self.sharded and self._early_grad_xchg() and self.native_comm is None:
+        if self.sharded and self._early_grad_xchg() and self.native_comm is None and not self.coll.det:
             # the dense gradients are final once the compute is: their all-reduce goes out now,
             # asynchronously behind the gradient-row all-to-all on the process group's stream,
             # beside the owner's widen / fold / norm; only the loss and the table-gradient sum of

@@ -681,6 +681,11 @@ int fbn_comm_allreduce(void* comm, void* buf, long long n, int dtype, void* stre
  * (ncclCommAbort: RCCL's kernels exit, the stream and the host blocked on it drain) and every later
  * call on them fails with error 3 and the watchdog's message.  fbn_comm_abort(comm): abort one now.
  * fbn_comm_watchdog_fired(NULL): 1 once the watchdog fired; (comm): 1 if that communicator is aborted. */
+/* Deterministic mode's all-reduce (replaces the sum of torch.distributed / ncclAllReduce, whose
+ * reduction order follows the algorithm RCCL picks): fbn_comm_allgather (bytes_per_rank from every rank,
+ * rank order) then fbn_sum_slices(in, ns, n, dtype 0 f32 / 1 f64, out) = the slices summed in rank order. */
+int fbn_comm_allgather(void* comm, const void* send, void* recv, long long bytes_per_rank, void* stream);
+int fbn_sum_slices(const void* in, int ns, long long n, int dtype, void* out, void* stream);
 int fbn_comm_watch(long long timeout_ms);
 int fbn_comm_heartbeat(void* stream);
 int fbn_comm_abort(void* comm);

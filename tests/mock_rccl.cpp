@@ -174,6 +174,17 @@ ncclResult_t ncclAllToAll(const void* send, void* recv, size_t count, ncclDataTy
   return ncclGroupEnd();
 }
 
+ncclResult_t ncclAllGather(const void* send, void* recv, size_t count, ncclDataType_t dt, ncclComm_t comm,
+                           hipStream_t s) {
+  const size_t bytes = count * type_size(dt);
+  ncclGroupStart();
+  for (int p = 0; p < comm->w->n; ++p) {
+    ncclSend(send, count, dt, p, comm, s);
+    ncclRecv((char*)recv + p * bytes, count, dt, p, comm, s);
+  }
+  return ncclGroupEnd();
+}
+
 ncclResult_t ncclAllReduce(const void* send, void* recv, size_t count, ncclDataType_t dt, ncclRedOp_t,
                            ncclComm_t comm, hipStream_t) {
   World& w = *comm->w;

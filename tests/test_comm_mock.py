@@ -43,6 +43,7 @@ def run(world, seed):
     ar64 = [np.full(4, (r + 1) * 0.25, dtype=np.float64) for r in range(world)]
     ari = [np.arange(5, dtype=np.int32) * (r + 1) for r in range(world)]
     pe_out = [np.full(world * 5, -7, dtype=np.int32) for r in range(world)]   # peers-only: own block untouched
+    ag_out = [np.full(world * 3, -1.0, dtype=np.float64) for r in range(world)]   # all-gather, rank order
 
     def rank(r):
         try:
@@ -58,6 +59,9 @@ def run(world, seed):
             assert rc_ == 0, lib.fbn_last_error()
             rc_ = lib.fbn_comm_alltoall_peers(h, eq[r].ctypes.data_as(ctypes.c_void_p),
                                               pe_out[r].ctypes.data_as(ctypes.c_void_p), ctypes.c_longlong(5 * 4), None)
+            assert rc_ == 0, lib.fbn_last_error()
+            rc_ = lib.fbn_comm_allgather(h, ar64[r].ctypes.data_as(ctypes.c_void_p),
+                                         ag_out[r].ctypes.data_as(ctypes.c_void_p), ctypes.c_longlong(3 * 8), None)
             assert rc_ == 0, lib.fbn_last_error()
             for buf, code in ((ar32[r], 0), (ar64[r], 1), (ari[r], 2)):
                 rc_ = lib.fbn_comm_allreduce(h, buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_longlong(buf.size),
@@ -84,6 +88,7 @@ def run(world, seed):
         assert np.array_equal(eq_out[r], np.concatenate([eq[s][5 * r:5 * r + 5] for s in range(world)]))
         want_pe = np.concatenate([eq[s][5 * r:5 * r + 5] if s != r else np.full(5, -7, np.int32) for s in range(world)])
         assert np.array_equal(pe_out[r], want_pe), (world, r, pe_out[r], want_pe)
+        assert np.array_equal(ag_out[r], np.concatenate([np.full(3, (q + 1) * 0.25) for q in range(world)]))
         assert np.allclose(ar32[r], sum(q + 1.5 for q in range(world)))
         assert np.allclose(ar64[r], sum((q + 1) * 0.25 for q in range(world)))
         assert np.array_equal(ari[r], np.arange(5) * sum(q + 1 for q in range(world)))

@@ -253,3 +253,46 @@ def test_bench_native_ab_agreement():
         assert a == (True, -1), (rank, a)
         assert b == (False, 5), (rank, b)
         assert c == (False, 4), (rank, c)
+
+
+def _det_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ctr_recommendation_amd.exchange import DistCollective
+        gens = [torch.Generator().manual_seed(40 + r) for r in range(world)]
+        # values spanning many magnitudes: a different summation order would change the bits
+        vals = [torch.randn(4099, generator=g) * torch.exp(torch.randn(4099, generator=g) * 6) for g in gens]
+        vals64 = [v.double() * 1e-3 for v in vals]
+        want = vals[0].clone()
+        want64 = vals64[0].clone()
+        for r in range(1, world):
+            want += vals[r]
+            want64 += vals64[r]
+        c = DistCollective(world, det=True)
+        t, t64 = vals[rank].clone(), vals64[rank].clone()
+        c.allreduce_(t)
+        c.allreduce_(t64)
+        q.put((rank, bool(torch.equal(t, want)), bool(torch.equal(t64, want64))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_deterministic_allreduce_rank_order():
+    """Deterministic mode's all-reduce (DistCollective(det=True): all-gather, then the ranks' slices
+    added in rank order) gives exactly the rank-ordered sum on every rank, f32 and f64 -- whatever
+    order a reduction algorithm would have used (the same rule the native path runs as
+    fbn_comm_allgather + fbn_sum_slices)."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_det_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == [(r, True, True) for r in range(world)], res

@@ -220,3 +220,60 @@ def test_owner_prefetch_bit_identical(hip_device, tmp_path):
     for p in procs:
         p.join(timeout=120)
     assert all(r[1] == "ok" for r in res), res
+
+
+def _det_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ctr_recommendation_amd.data import make_batch
+        from ctr_recommendation_amd.trainer import FiBiNETTrainer
+        from oracle.fibinet_oracle import build_model
+        dev = torch.device("cuda:0")
+        torch.manual_seed(0)
+        init = build_model(None, _cfg(128), honour_config=True).state_dict()
+        per, steps = 256, 6
+        bs = []
+        for s in range(steps + 1):
+            b, y = make_batch(500 + s, per * world, V)
+            bs.append(({k: v[rank * per:(rank + 1) * per].to(dev) for k, v in b.items()},
+                       y[rank * per:(rank + 1) * per].to(dev)))
+        runs = []
+        for _ in range(2):
+            tr = FiBiNETTrainer(_cfg(128, "bf16"), total_steps=TOTAL, batch_size=per, device=dev, rank=rank, world=world,
+                                init_state={k: v.clone() for k, v in init.items()}, stage_on_cpu=True, sync_bn=True,
+                                deterministic=True)
+            assert tr.coll.det
+            losses = [tr.step(bs[s][0], bs[s][1], next_batch=bs[s + 1][0]).item() for s in range(steps)]
+            tr.flush()
+            runs.append((losses, tr.E.clone(), tr.flat_p.clone(), tr.flat_v.clone(), tr.xchg.fc_active))
+        (l0, e0, p0, v0, f0), (l1, e1, p1, v1, f1) = runs
+        q.put((rank, "ok", l0 == l1, bool(torch.equal(e0, e1) and torch.equal(p0, p1) and torch.equal(v0, v1)),
+               f0 and f1))
+    except Exception as e:
+        q.put((rank, repr(e), False, False, False))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_deterministic_runs_bitwise_reproducible(hip_device):
+    """Deterministic mode at N > 1 (2 ranks on one MI355X, host-staged gloo collectives): the fixed-point
+    owner fold and the rank-ordered all-reduces (all-gather + fbn_sum_slices, SyncBN's f64 moments and
+    the packed dense gradients) make two runs from the same state bitwise equal on every rank -- losses,
+    the table shard, the dense parameters and second moments -- through the calibration steps and the
+    fixed-capacity exchange."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_det_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=600) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for rank, status, same_loss, same_state, fc in res:
+        assert status == "ok", (rank, status)
+        assert same_loss and same_state, (rank, same_loss, same_state)
+        assert fc, rank
