@@ -353,7 +353,7 @@ def native_ab(args, world, rank, dev):
         ok_a = ia["fc_active"] and ia["programs"] == nb
         if not ok_a:
             err = f"native path did not run as step programs over the fixed-capacity exchange: {ia}"
-    except RuntimeError as e:        # a watchdog abort or an RCCL error on this rank
+    except Exception as e:           # a watchdog abort, an RCCL error, a recording refused on this rank
         ok_a, err = False, f"{type(e).__name__}: {e}"[:400]
     if not ok_a:
         print(f"[bench] rank {rank}: native path failed the A/B: {err}", file=sys.stderr, flush=True)
@@ -781,7 +781,7 @@ def main():
         try:
             r = measure(args, args.dtype, world, rank, dev, rehearsal, backend, native=True)
             ok = True
-        except RuntimeError as e:    # a watchdog abort mid-run: every rank falls back together
+        except Exception as e:       # a watchdog abort mid-run: every rank falls back together
             ok, native_err = False, f"{type(e).__name__}: {e}"[:400]
             print(f"[bench] rank {rank}: native headline failed: {native_err}", file=sys.stderr, flush=True)
         ok_all, _ = _ab_agree(ok, -1, dev)
