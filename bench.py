@@ -363,10 +363,25 @@ def native_ab(args, world, rank, dev):
     if not healthy:
         if tra is not None:
             tra.close()
-        out.update(validated=False, first_diff_step=-1, reason=err or "another rank's native path failed",
+        out.update(validated=False, use_native=False, first_diff_step=-1,
+                   reason=err or "another rank's native path failed", seconds=round(time.perf_counter() - t_start, 1))
+        return out
+    try:
+        trb, lb, sb, ib = run(False)
+        torch_err = None
+    except Exception as e:           # the torch.distributed path itself failed on this rank
+        trb, torch_err = None, f"{type(e).__name__}: {e}"[:400]
+    torch_ok, _ = _ab_agree(torch_err is None, -1, dev)
+    if not torch_ok:
+        # the conservative path is the broken one: the native path ran healthy on every rank, so it
+        # is timed -- unvalidated, and the line says so
+        for t in (tra, trb):
+            if t is not None:
+                t.close()
+        out.update(validated=False, use_native=True, first_diff_step=-1, native=ia,
+                   reason=f"the torch.distributed path failed: {torch_err or 'on another rank'}",
                    seconds=round(time.perf_counter() - t_start, 1))
         return out
-    trb, lb, sb, ib = run(False)
     diff = (la != lb).nonzero()
     first = int(diff[0, 0]) if diff.numel() else -1
     same = {n: bool(torch.equal(sa[n], sb[n])) for n in names}
@@ -375,8 +390,8 @@ def native_ab(args, world, rank, dev):
     for t in (tra, trb):
         t.close()
     del tra, trb, sa, sb
-    out.update(validated=valid, first_diff_step=first_all, equal_this_rank=same, native=ia, torch=ib,
-               loss_last=(float(la[-1]), float(lb[-1])), seconds=round(time.perf_counter() - t_start, 1))
+    out.update(validated=valid, use_native=valid, first_diff_step=first_all, equal_this_rank=same, native=ia,
+               torch=ib, loss_last=(float(la[-1]), float(lb[-1])), seconds=round(time.perf_counter() - t_start, 1))
     if not valid:
         out["reason"] = ("losses first differ at step %d" % first_all) if first_all >= 0 else "final state differs"
     return out
@@ -773,7 +788,7 @@ def main():
     ab, native, torch_line, native_err = None, None, None, None
     if (world > 1 or FORCE_SHARD) and not rehearsal and os.environ.get("FBN_BENCH_AB", "1") != "0":
         ab = native_ab(args, world, rank, dev)
-        native = bool(ab["validated"])
+        native = bool(ab["use_native"])
         _release()
         if rank == 0:
             print(f"[bench] native-RCCL A/B: {json.dumps(ab)}", file=sys.stderr, flush=True)
@@ -786,7 +801,7 @@ def main():
             print(f"[bench] rank {rank}: native headline failed: {native_err}", file=sys.stderr, flush=True)
         ok_all, _ = _ab_agree(ok, -1, dev)
         _release()
-        if ok_all:
+        if ok_all and ab.get("torch") is not None:      # (the torch path ran in the A/B)
             torch_line = measure(args, args.dtype, world, rank, dev, rehearsal, backend, native=False)
         else:
             native = False
@@ -891,8 +906,10 @@ def main():
                              "per-GPU statistics (nn.DataParallel semantics, train_fibinet.py:69-70)",
                 "final_loss": round(other_bn["loss"], 5)}
         if ab is not None:
-            out["native_ab"] = dict(ab, headline=("native RCCL + step programs (validated bitwise against "
-                                                  "torch.distributed)" if native else "torch.distributed"),
+            out["native_ab"] = dict(ab, headline=(("native RCCL + step programs (validated bitwise against "
+                                                   "torch.distributed)" if ab["validated"] else
+                                                   "native RCCL + step programs (UNVALIDATED: the torch path failed)")
+                                                  if native else "torch.distributed"),
                                     **({"native_headline_error": native_err} if native_err else {}))
         if torch_line is not None:
             out["torch_collectives"] = {
