@@ -286,26 +286,28 @@ struct HeadArgs {
 };
 // Linear(C,1) + sigmoid + BCE terms + dL/dlogit of one row from the wave's lane partials
 // (lane q holds columns 4q..4q+3): shared by head_fwd_kernel and the fused BN2 + head kernel
-__device__ __forceinline__ float head_row(float s, int row, int lane, const HeadArgs& h) {
-  s = wave_sum(s);
+// The row's outputs from its summed dot product s (one lane)
+__device__ __forceinline__ float head_lane(float s, int row, const HeadArgs& h) {
   float go = 0.f;
-  if (lane == 0) {
-    const float o = s + h.bias[0];
-    const float pr = 1.f / (1.f + expf(-o));
-    if (h.logits) h.logits[row] = o;
-    if (h.probs) h.probs[row] = pr;
-    if (h.labels) {
-      const float t = h.labels[row];
-      const float lp = fmaxf(logf(pr), -100.f), l1p = fmaxf(logf(1.f - pr), -100.f);
-      if (h.loss_terms) h.loss_terms[row] = -(t * lp + (1.f - t) * l1p);
-      if (h.gout) {
-        const float gp = ((pr - t) / fmaxf((1.f - pr) * pr, 1e-12f)) / h.denom;
-        go = gp * (1.f - pr) * pr;
-        h.gout[row] = go;
-      }
+  const float o = s + h.bias[0];
+  const float pr = 1.f / (1.f + expf(-o));
+  if (h.logits) h.logits[row] = o;
+  if (h.probs) h.probs[row] = pr;
+  if (h.labels) {
+    const float t = h.labels[row];
+    const float lp = fmaxf(logf(pr), -100.f), l1p = fmaxf(logf(1.f - pr), -100.f);
+    if (h.loss_terms) h.loss_terms[row] = -(t * lp + (1.f - t) * l1p);
+    if (h.gout) {
+      const float gp = ((pr - t) / fmaxf((1.f - pr) * pr, 1e-12f)) / h.denom;
+      go = gp * (1.f - pr) * pr;
+      h.gout[row] = go;
     }
   }
-  return go;   // dL/dlogit of the row on lane 0
+  return go;
+}
+__device__ __forceinline__ float head_row(float s, int row, int lane, const HeadArgs& h) {
+  s = wave_sum(s);
+  return lane == 0 ? head_lane(s, row, h) : 0.f;   // dL/dlogit of the row on lane 0
 }
 
 // Column-blocked form: block = 64 column quads (256 columns) x 4 row lanes over a chunk of rows,
@@ -356,16 +358,18 @@ __global__ void __launch_bounds__(NT) bn_act_fwd2_kernel(const float* __restrict
       um[0] = u01(rr.x); um[1] = u01(rr.y); um[2] = u01(rr.z); um[3] = u01(rr.w);
     }
     f32x4 y;
+    unsigned mk = 0u;   // the four mask bytes, one 32-bit store
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float v = fmaxf(x[e] * alpha[e] + bp[e], 0.f);
       if (p_drop > 0.f) {
         const bool kept = mask_in ? mask_in[i + e] != 0 : um[e] < keep;
         v = kept ? v * scale : 0.f;
-        if (mask_out) mask_out[i + e] = kept ? 1 : 0;
+        mk |= (kept ? 1u : 0u) << (8 * e);
       }
       y[e] = v;
     }
+    if (p_drop > 0.f && mask_out) *reinterpret_cast<unsigned*>(mask_out + i) = mk;
     if (Y) *reinterpret_cast<f32x4*>(Y + i) = y;
     if (Y16) {
       if (y16_lo) store_img4(Y16 + i, y16_lo, y);   // split images (bf16_fwd): hi here, lo y16_lo further
@@ -406,6 +410,175 @@ __global__ void __launch_bounds__(NT) bn_act_fwd2_kernel(const float* __restrict
       __syncthreads();
     }
   }
+}
+
+// bn_act_fwd2_kernel<false> with FOUR rows per wave and iteration (rows r0 + rl + 4j of a 16-row
+// chunk): the four rows' loads are issued before any row's arithmetic.  Same operations per
+// element, same outputs.
+__global__ void __launch_bounds__(256) bn_act_fwd4r_kernel(const float* __restrict__ X, float* __restrict__ Y, int B,
+                                                           int C, int rows_per_chunk, const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ g, const float* __restrict__ bta,
+                                                           float p_drop, const unsigned long long* __restrict__ rng,
+                                                           unsigned stream_id, unsigned char* __restrict__ mask_out,
+                                                           const unsigned char* __restrict__ mask_in,
+                                                           short* __restrict__ Y16, long long y16_lo) {
+  FBN_MAIN_PRIO();
+  const int q = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 256 + q * 4;
+  if (c >= C) return;
+  const int r0 = blockIdx.y * rows_per_chunk, r1 = min(B, r0 + rows_per_chunk);
+  const float keep = 1.f - p_drop;
+  const float scale = p_drop > 0.f ? 1.0f / keep : 1.f;
+  uint32_t k0 = 0, k1 = 0, off = 0;
+  if (rng) { k0 = (uint32_t)rng[0]; k1 = (uint32_t)(rng[0] >> 32); off = (uint32_t)rng[1]; }
+  float alpha[4], bp[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    alpha[e] = invstd[c + e] * g[c + e];
+    bp[e] = bta[c + e] - mean[c + e] * alpha[e];
+  }
+  for (int rb = r0 + rl; rb < r1; rb += 16) {
+    f32x4 x[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = rb + 4 * j;
+      x[j] = r < r1 ? *reinterpret_cast<const f32x4*>(X + (size_t)r * C + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = rb + 4 * j;
+      if (r >= r1) break;
+      const size_t i = (size_t)r * C + c, i4 = i >> 2;
+      float um[4] = {1.f, 1.f, 1.f, 1.f};
+      if (p_drop > 0.f && !mask_in) {
+        const Philox4 rr = philox4x32_10((uint32_t)i4, (uint32_t)(i4 >> 32), stream_id, off, k0, k1);
+        um[0] = u01(rr.x); um[1] = u01(rr.y); um[2] = u01(rr.z); um[3] = u01(rr.w);
+      }
+      f32x4 y;
+      unsigned mk = 0u;   // the four mask bytes, one 32-bit store
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = fmaxf(x[j][e] * alpha[e] + bp[e], 0.f);
+        if (p_drop > 0.f) {
+          const bool kept = mask_in ? mask_in[i + e] != 0 : um[e] < keep;
+          v = kept ? v * scale : 0.f;
+          mk |= (kept ? 1u : 0u) << (8 * e);
+        }
+        y[e] = v;
+      }
+      if (p_drop > 0.f && mask_out) *reinterpret_cast<unsigned*>(mask_out + i) = mk;
+      if (Y) *reinterpret_cast<f32x4*>(Y + i) = y;
+      if (Y16) {
+        if (y16_lo) store_img4(Y16 + i, y16_lo, y);
+        else store4(Y16 + i, y);
+      }
+    }
+  }
+}
+
+// The same fused BN2 + ReLU + dropout + head + BN2-backward first pass (C == 256) with FOUR rows
+// per wave: 4 waves per row chunk, wave rl takes rows r0 + rl + 4k in order (bn_bwd_partial4's
+// rows and accumulation order, so its partials equal that kernel's bit for bit).  The four rows'
+// loads and Philox draws are independent, their dot products are reduced side by side with
+// wave_sum's butterfly (the same order per row), and lanes 0..3 finish rows 0..3 at once
+// (head_lane, the same operations as head_row's lane 0) -- one latency chain per four rows
+// instead of one per row, and one LDS fold of 4 waves per chunk instead of 3 of 16.
+__global__ void __launch_bounds__(256) bn_act_head_bwd4_kernel(
+    const float* __restrict__ X, float* __restrict__ Y, int B, int C, int rows_per_chunk,
+    const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ g,
+    const float* __restrict__ bta, float p_drop, const unsigned long long* __restrict__ rng, unsigned stream_id,
+    unsigned char* __restrict__ mask_out, const unsigned char* __restrict__ mask_in, HeadArgs head,
+    double* __restrict__ bpart, float bscale) {
+  FBN_MAIN_PRIO();
+  __shared__ double red[3][4][256];
+  const int q = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = q * 4;
+  const int r0 = blockIdx.y * rows_per_chunk, r1 = min(B, r0 + rows_per_chunk);
+  const float keep = 1.f - p_drop;
+  const float scale = p_drop > 0.f ? 1.0f / keep : 1.f;
+  uint32_t k0 = 0, k1 = 0, off = 0;
+  if (rng) { k0 = (uint32_t)rng[0]; k1 = (uint32_t)(rng[0] >> 32); off = (uint32_t)rng[1]; }
+  float alpha[4], bp[4], mu[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    alpha[e] = invstd[c + e] * g[c + e];
+    bp[e] = bta[c + e] - mean[c + e] * alpha[e];
+    mu[e] = mean[c + e];
+  }
+  const f32x4 ww = *reinterpret_cast<const f32x4*>(head.w + c);
+  double s0[4] = {0.0, 0.0, 0.0, 0.0}, s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int rb = r0 + rl; rb < r1; rb += 16) {   // wave-uniform bound
+    f32x4 x[4], y[4];
+    float sp[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = rb + 4 * j;
+      x[j] = r < r1 ? *reinterpret_cast<const f32x4*>(X + (size_t)r * C + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = rb + 4 * j;
+      const bool ok = r < r1;
+      const size_t i = (size_t)r * C + c, i4 = i >> 2;
+      float um[4] = {1.f, 1.f, 1.f, 1.f};
+      if (p_drop > 0.f && !mask_in) {
+        const Philox4 rr = philox4x32_10((uint32_t)i4, (uint32_t)(i4 >> 32), stream_id, off, k0, k1);
+        um[0] = u01(rr.x); um[1] = u01(rr.y); um[2] = u01(rr.z); um[3] = u01(rr.w);
+      }
+      unsigned mk = 0u;   // the four mask bytes, one 32-bit store
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = fmaxf(x[j][e] * alpha[e] + bp[e], 0.f);
+        if (p_drop > 0.f) {
+          const bool kept = mask_in ? (ok && mask_in[i + e] != 0) : um[e] < keep;
+          v = kept ? v * scale : 0.f;
+          mk |= (kept ? 1u : 0u) << (8 * e);
+        }
+        y[j][e] = v;
+      }
+      if (p_drop > 0.f && mask_out && ok) *reinterpret_cast<unsigned*>(mask_out + i) = mk;
+      if (Y && ok) *reinterpret_cast<f32x4*>(Y + i) = y[j];
+      sp[j] = y[j][0] * ww[0] + y[j][1] * ww[1] + y[j][2] * ww[2] + y[j][3] * ww[3];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sp[j] += __shfl_xor(sp[j], o, 64);
+    }
+    float go = 0.f;
+    if (q < 4) {
+      const float sq = q == 0 ? sp[0] : (q == 1 ? sp[1] : (q == 2 ? sp[2] : sp[3]));
+      const int row = rb + 4 * q;
+      if (row < r1) go = head_lane(sq, row, head);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gv = __shfl(go, j, 64);
+      if (rb + 4 * j < r1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = gv * ww[e];
+          const float dy = y[j][e] > 0.f ? d * bscale : 0.f;
+          s0[e] += dy;
+          s1[e] += (double)((x[j][e] - mu[e]) * dy);
+          s2[e] += (double)(gv * y[j][e]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    red[0][rl][c + e] = s0[e];
+    red[1][rl][c + e] = s1[e];
+    red[2][rl][c + e] = s2[e];
+  }
+  __syncthreads();
+  double* pp = bpart + (size_t)blockIdx.y * 3 * C;
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+    pp[(size_t)k * C + threadIdx.x] =
+        red[k][0][threadIdx.x] + red[k][1][threadIdx.x] + red[k][2][threadIdx.x] + red[k][3][threadIdx.x];
 }
 
 // ------------------------------------------------------------------ BN backward
@@ -1158,6 +1331,11 @@ extern "C" int fbn_bn_eval_params(const float* run_mean, const float* run_var, f
 // Rows per workgroup of the BN-apply kernels: 4 = one row per wave, so every row of the batch is
 // in flight at once (the fused head reduces a whole row per wave and then runs a serial sigmoid /
 // BCE tail: with 16 rows per workgroup each wave walked 4 rows one after the other).
+// A/B knob: bn_act_fwd4r_kernel (four rows per wave, 16-row chunks) for the plain BN + ReLU + dropout
+static bool bn_act_rows4() {
+  const char* e = getenv("FBN_BN_ACT_R4");   // read per call
+  return e && atoi(e) != 0;
+}
 static int bn_act_rows_per_chunk() {
   const char* e = getenv("FBN_BN_ACT_RPC");   // A/B knob, read per call
   const int v = e ? atoi(e) : 4;
@@ -1175,6 +1353,12 @@ extern "C" int fbn_bn_act_fwd(const float* X, float* Y, int B, int C, const floa
   if (C & 3) { fbn_set_error("bn_act: C % 4"); return FBN_ERR_ARG; }
   if (p_drop > 0.f && !rng && !mask_in) { fbn_set_error("bn_act: dropout needs an rng state or a mask"); return FBN_ERR_ARG; }
   if (!Y && !Y16) { fbn_set_error("bn_act: no output"); return FBN_ERR_ARG; }
+  if (bn_act_rows4()) {
+    fbn_launch(bn_act_fwd4r_kernel, dim3(fbn_cdiv(C, 256), fbn_cdiv(B, 16)), dim3(256), 0, (hipStream_t)stream, X, Y,
+               B, C, 16, mean, invstd, g, b, p_drop, rng, stream_id, mask_out, mask_in, Y16, 0LL);
+    FBN_CHECK_LAUNCH();
+    return FBN_OK;
+  }
   const int rpc = bn_act_rows_per_chunk();
   fbn_launch(bn_act_fwd2_kernel<false>, dim3(fbn_cdiv(C, 256), fbn_cdiv(B, rpc)), dim3(256), 0,
                      (hipStream_t)stream, X, Y, B, C, rpc, mean, invstd, g, b, p_drop, rng, stream_id, mask_out, mask_in,
@@ -1192,6 +1376,13 @@ extern "C" int fbn_bn_act_fwd_img(const float* X, float* Y, int B, int C, const 
   if (B <= 0) return FBN_OK;
   if ((C & 3) || !Y_img) { fbn_set_error("bn_act_img: C % 4, Y_img"); return FBN_ERR_ARG; }
   if (p_drop > 0.f && !rng && !mask_in) { fbn_set_error("bn_act: dropout needs an rng state or a mask"); return FBN_ERR_ARG; }
+  if (bn_act_rows4()) {
+    fbn_launch(bn_act_fwd4r_kernel, dim3(fbn_cdiv(C, 256), fbn_cdiv(B, 16)), dim3(256), 0, (hipStream_t)stream, X, Y,
+               B, C, 16, mean, invstd, g, b, p_drop, rng, stream_id, mask_out, mask_in, (short*)Y_img,
+               (long long)B * C);
+    FBN_CHECK_LAUNCH();
+    return FBN_OK;
+  }
   const int rpc = bn_act_rows_per_chunk();
   fbn_launch(bn_act_fwd2_kernel<false>, dim3(fbn_cdiv(C, 256), fbn_cdiv(B, rpc)), dim3(256), 0,
                      (hipStream_t)stream, X, Y, B, C, rpc, mean, invstd, g, b, p_drop, rng, stream_id, mask_out, mask_in,
@@ -1214,6 +1405,14 @@ extern "C" int fbn_bn_act_head_fwd(const float* X, float* Y, int B, int C, const
   if (bwd_part) {
     // the row chunks of fbn_bn_bwd_fused, so its reduce reads these partials as its own
     const int nch = bn_bwd_chunks(B, C), rpc = (B + nch - 1) / nch;
+    static const bool one_row = getenv("FBN_HEAD_ONE_ROW") != nullptr;   // A/B knob: one row per wave
+    if (!one_row) {
+      fbn_launch(bn_act_head_bwd4_kernel, dim3(1, fbn_cdiv(B, rpc)), dim3(256), 0, (hipStream_t)stream, X, Y, B,
+                 C, rpc, mean, invstd, g, b, p_drop, rng, stream_id, mask_out, mask_in,
+                 HeadArgs{hw, hbias, logits, probs, labels, loss_terms, gout, denom}, bwd_part, bwd_scale);
+      FBN_CHECK_LAUNCH();
+      return FBN_OK;
+    }
     fbn_launch((bn_act_fwd2_kernel<true, 1024, true>), dim3(1, fbn_cdiv(B, rpc)), dim3(1024), 0,
                        (hipStream_t)stream, X, Y, B, C, rpc, mean, invstd, g, b, p_drop, rng, stream_id, mask_out,
                        mask_in, nullptr, HeadArgs{hw, hbias, logits, probs, labels, loss_terms, gout, denom}, bwd_part,

@@ -485,3 +485,99 @@ def test_gemm_bn_bwd_part_epilogue(hip_device, M):
     assert torch.allclose(part[:, 0], s0, rtol=1e-5, atol=1e-3)
     assert torch.allclose(part[:, 1], s1, rtol=1e-5, atol=1e-3)
     assert bool((part[:, 2] == 0).all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [8192, 1000, 37])
+def test_fused_head_four_rows_per_wave(hip_device, B):
+    """fbn_bn_act_head_fwd with the BN2 backward's first pass (bn_act_head_bwd4_kernel, four rows
+    per wave): its forward outputs equal the head launch without the backward pass bit for bit,
+    and the backward fed its partials equals the backward that computes them itself
+    (bn_bwd_partial4, the same rows in the same order) bit for bit.  B = 1000 / 37: ragged chunks."""
+    C, p_drop = 256, 0.3
+    dev = hip_device
+    g = torch.Generator(device="cpu").manual_seed(11)
+    X = (torch.randn((B, C), generator=g) * 2 + 0.3).to(dev)
+    mean = X.mean(0)
+    inv = 1.0 / torch.sqrt(X.var(0, unbiased=False) + 1e-5)
+    gamma = (1 + 0.1 * torch.randn((C,), generator=g)).to(dev)
+    beta = (0.1 * torch.randn((C,), generator=g)).to(dev)
+    hw = (torch.randn((C,), generator=g) / 16).to(dev)
+    hb = torch.randn((1,), generator=g).to(dev)
+    labels = (torch.rand((B,), generator=g) < 0.4).float().to(dev)
+    rng = torch.tensor([0x1234_5678_9abc, 7], dtype=torch.int64).to(dev)
+    st = _lib.stream_handle(dev)
+    bscale = 1.0 / (1.0 - p_drop)
+
+    def run(with_part):
+        out = {k: torch.full((B,), float("nan"), device=dev) for k in ("logits", "probs", "lt", "go")}
+        out["Y"] = torch.full((B, C), float("nan"), device=dev)
+        out["mask"] = torch.full((B, C), 7, dtype=torch.uint8, device=dev)
+        nch = _lib.lib().fbn_bn_bwd_chunks(B, C)
+        part = torch.full((nch * 3 * C,), float("nan"), dtype=torch.float64, device=dev) if with_part else None
+        _lib.call("fbn_bn_act_head_fwd", _lib.ptr(X), _lib.ptr(out["Y"]), B, C, _lib.ptr(mean), _lib.ptr(inv),
+                  _lib.ptr(gamma), _lib.ptr(beta), p_drop, _lib.ptr(rng), 2, _lib.ptr(out["mask"]), None,
+                  _lib.ptr(hw), _lib.ptr(hb), _lib.ptr(out["logits"]), _lib.ptr(out["probs"]), _lib.ptr(labels),
+                  _lib.ptr(out["lt"]), _lib.ptr(out["go"]), float(B), _lib.ptr(part), float(bscale), st)
+        return out, part
+
+    ref, _ = run(False)
+    got, part = run(True)
+    torch.cuda.synchronize()
+    for k in ref:
+        assert torch.equal(ref[k], got[k]), k
+    assert 0.55 < got["mask"].float().mean().item() < 0.85
+
+    def backward(part_pre):
+        d = {"dpre": torch.empty((B, C), device=dev), "dgamma": torch.empty(C, device=dev),
+             "dbeta": torch.empty(C, device=dev), "dw": torch.empty(C, device=dev)}
+        ops.bn_backward(None, got["go"], hw, got["Y"], bscale, X, mean, inv, gamma, B, C, float(B), d["dpre"],
+                        d["dgamma"], d["dbeta"], d["dw"], ops.NO_COLLECTIVE, st, part_pre=part_pre)
+        return d
+
+    own, fed = backward(None), backward(part)
+    torch.cuda.synchronize()
+    for k in own:
+        assert torch.equal(own[k], fed[k]), k
+    # and against float64 torch
+    dy = torch.where(got["Y"] > 0, got["go"][:, None].double() * hw.double() * bscale, torch.zeros((), dtype=torch.float64,
+                                                                                                    device=dev))
+    assert torch.allclose(fed["dbeta"].double(), dy.sum(0), rtol=1e-5, atol=1e-6)
+    assert torch.allclose(fed["dw"].double(), (got["go"][:, None].double() * got["Y"].double()).sum(0), rtol=1e-5,
+                          atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,C", [(8192, 1024), (1000, 512), (37, 256)])
+def test_bn_act_four_rows_per_wave_matches(hip_device, monkeypatch, B, C):
+    """The BN + ReLU + dropout forward with four rows per wave (FBN_BN_ACT_R4=1, read per call)
+    writes exactly what the one-row form writes: f32 output, bf16 image (and split images) and the
+    dropout mask.  B = 1000 / 37: ragged chunks."""
+    dev = hip_device
+    g = torch.Generator(device="cpu").manual_seed(12)
+    X = torch.randn((B, C), generator=g).to(dev)
+    mean = X.mean(0)
+    inv = 1.0 / torch.sqrt(X.var(0, unbiased=False) + 1e-5)
+    gamma = (1 + 0.1 * torch.randn((C,), generator=g)).to(dev)
+    beta = (0.1 * torch.randn((C,), generator=g)).to(dev)
+    rng = torch.tensor([0x0bad_cafe_1234, 3], dtype=torch.int64).to(dev)
+    st = _lib.stream_handle(dev)
+
+    def run(r4):
+        monkeypatch.setenv("FBN_BN_ACT_R4", "1" if r4 else "0")
+        Y = torch.full((B, C), float("nan"), device=dev)
+        Y16 = torch.full((B, C), 7, dtype=torch.int16, device=dev)
+        img = torch.full((2, B, C), 7, dtype=torch.int16, device=dev)
+        mask = torch.full((B, C), 9, dtype=torch.uint8, device=dev)
+        mask2 = torch.full((B, C), 9, dtype=torch.uint8, device=dev)
+        _lib.call("fbn_bn_act_fwd", _lib.ptr(X), _lib.ptr(Y), B, C, _lib.ptr(mean), _lib.ptr(inv), _lib.ptr(gamma),
+                  _lib.ptr(beta), 0.5, _lib.ptr(rng), 1, _lib.ptr(mask), None, _lib.ptr(Y16), st)
+        _lib.call("fbn_bn_act_fwd_img", _lib.ptr(X), None, B, C, _lib.ptr(mean), _lib.ptr(inv), _lib.ptr(gamma),
+                  _lib.ptr(beta), 0.5, _lib.ptr(rng), 1, _lib.ptr(mask2), None, _lib.ptr(img), st)
+        torch.cuda.synchronize()
+        return Y, Y16, img, mask, mask2
+
+    a, b = run(False), run(True)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    assert torch.equal(a[3], a[4]) and bool((a[3] <= 1).all())
