@@ -1171,6 +1171,10 @@ extern "C" int fbn_gemm_slabs_split(int M, int N, int K) { return (M > 0 && N > 
 // and summed (C3: 0.4407 -> 0.4327 ms/step; a quarter: 0.4617; profiles/r03s2_group_knobs_ab.txt).
 // FBN_GROUP_SPLIT_DIV overrides the divisor (1: fbn_gemm_slabs's own partition, whose sums the
 // group then reproduces bit for bit; tests/test_gpu_trainer.py::test_wgrad_group_bit_identical).
+static bool group_w4() {
+  const char* e = getenv("FBN_GROUP_W4");   // read per call
+  return e && atoi(e) != 0;
+}
 static int group_split(int M, int N, int K) {
   int s = slab_split(M, N, K);
   const char* e = getenv("FBN_GROUP_SPLIT_DIV");
@@ -1264,6 +1268,9 @@ extern "C" int fbn_gemm_slabs_group(const void* descs, int n, void* stream) {
                        st, G);
   else if (d[0].s3k0)
     fbn_launch((gemm_dma16_group_kernel<64, 64, true, true, 2, 2, 2, true>), dim3((unsigned)total), dim3(256), 0,
+                       st, G);
+  else if (wide && group_w4())   // A/B knob: 4 waves of 64x64 (fewer LDS fragment reads per MFMA)
+    fbn_launch((gemm_dma16_group_kernel<128, 128, true, true, 2, 2, 2>), dim3((unsigned)total), dim3(256), 0,
                        st, G);
   else if (wide && se && atoi(se) == 3)
     fbn_launch((gemm_dma16_group_kernel<128, 128, true, true, 3, 2, 4>), dim3((unsigned)total), dim3(512), 0,

@@ -441,6 +441,35 @@ def test_wgrad_group_bit_identical(hip_device, d, B):
         assert bad.numel() == 0, (name, bad[:8].tolist(), (a - c).abs().max().item())
 
 
+def test_wgrad_group_four_waves_bit_identical(hip_device, monkeypatch):
+    """The grouped weight-gradient launch on 4 waves of 64x64 per 128x128 tile (FBN_GROUP_W4=1, read
+    per call) writes the same K-slabs as the default 8 waves of 64x32: each output element's K-chunk
+    goes through the same 32x32x16 MFMA sequence.  Three bf16 steps at d = 128, B = 4096 (the wide
+    plan): losses, dense parameters and moments, table and its moments bit-identical."""
+    d, B, V = 128, 4096, 30000
+    cfg = {"embedding_dim": d, "vocab_size": V, "compute_dtype": "bf16"}
+    torch.manual_seed(0)
+    init = oracle_build(None, {"embedding_dim": d, "vocab_size": V}).state_dict()
+    batches = []
+    for s in range(4):
+        b, y = make_batch(900 + s, B, V)
+        batches.append(({k: v.to(hip_device) for k, v in b.items()}, y.to(hip_device)))
+    runs = []
+    for w4 in ("0", "1"):
+        monkeypatch.setenv("FBN_GROUP_W4", w4)
+        tr = FiBiNETTrainer(cfg, total_steps=20, batch_size=B, device=hip_device, init_state=init, lazy_window=4,
+                            deterministic=True)
+        losses = [tr.step(*batches[s], next_batch=batches[s + 1][0]).item() for s in range(3)]
+        tr.flush()
+        torch.cuda.synchronize()
+        runs.append((losses, [t.clone() for t in (tr.flat_p, tr.flat_m, tr.E, tr.Em, tr.Ev)]))
+        del tr
+    assert runs[0][0] == runs[1][0]
+    for name, a, c in zip(("p", "m", "E", "Em", "Ev"), runs[0][1], runs[1][1]):
+        bad = (a != c).nonzero()
+        assert bad.numel() == 0, (name, bad[:8].tolist(), (a - c).abs().max().item())
+
+
 @pytest.mark.parametrize("d,B", [(16, 256), (128, 512), (128, 200)])
 def test_split3_backward_matches_fp32_mfma(hip_device, d, B, monkeypatch):
     """bf16_fwd's backward GEMMs as ONE bf16 GEMM over 3 K on split images ([hi, hi, lo] x [hi, lo,
