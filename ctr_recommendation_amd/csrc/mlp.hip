@@ -886,19 +886,23 @@ __global__ void __launch_bounds__(1024) bn_bwd_reduce_finalize_kernel(const doub
   }
 }
 
-// Same reduction on 16 columns per block (C / 16 workgroups instead of C / 64): 64 chunk streams
-// per column, 16 lanes reading one 128-B row segment of the slab; then 48 threads fold the 64
-// streams of one (quantity, column) in fixed order (deterministic) and 16 finalize.
-__global__ void __launch_bounds__(1024) bn_bwd_reduce_finalize16_kernel(const double* __restrict__ part, int nchunk,
-                                                                        int C, double ntot,
-                                                                        const float* __restrict__ invstd, float* coef,
-                                                                        float* dgamma, float* dbeta, float* dw) {
+// Same reduction on NC columns per block (C / NC workgroups instead of C / 64): 64 chunk streams
+// per column, NC lanes reading one row segment of the slab; then 48 NC threads fold the 64
+// streams of one (quantity, column) in fixed order (deterministic) and NC finalize.  The fold's
+// order does not depend on NC, so every NC gives the same bits (NC = 16 by default; FBN_BN_REDUCE_NC
+// = 4 / 8: more, smaller workgroups -- A/B knob).
+template <int NC>
+__global__ void __launch_bounds__(64 * NC) bn_bwd_reduce_finalize16_kernel(const double* __restrict__ part, int nchunk,
+                                                                           int C, double ntot,
+                                                                           const float* __restrict__ invstd,
+                                                                           float* coef, float* dgamma, float* dbeta,
+                                                                           float* dw) {
   FBN_MAIN_PRIO();
-  __shared__ double red[64][3][16];
-  __shared__ double red2[16][3][16];
-  __shared__ double tot[3][16];
-  const int col = threadIdx.x & 15, str = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + col;
+  __shared__ double red[64][3][NC];
+  __shared__ double red2[16][3][NC];
+  __shared__ double tot[3][NC];
+  const int col = threadIdx.x % NC, str = threadIdx.x / NC;
+  const int c = blockIdx.x * NC + col;
   double r0 = 0.0, r1 = 0.0, r2 = 0.0;
   if (c < C) {
 #pragma unroll 4
@@ -914,20 +918,20 @@ __global__ void __launch_bounds__(1024) bn_bwd_reduce_finalize16_kernel(const do
   red[str][2][col] = r2;
   __syncthreads();
   // fixed-order two-level fold of the 64 chunk-stride partials: 16 groups of 4, then the 16
-  if (threadIdx.x < 768) {
-    const int j = threadIdx.x / 48, qc = threadIdx.x % 48, q = qc >> 4, cc = qc & 15;
+  if (threadIdx.x < 48 * NC) {
+    const int j = threadIdx.x / (3 * NC), qc = threadIdx.x % (3 * NC), q = qc / NC, cc = qc % NC;
     red2[j][q][cc] = ((red[4 * j][q][cc] + red[4 * j + 1][q][cc]) + red[4 * j + 2][q][cc]) + red[4 * j + 3][q][cc];
   }
   __syncthreads();
-  if (threadIdx.x < 48) {
-    const int q = threadIdx.x >> 4, cc = threadIdx.x & 15;
+  if (threadIdx.x < 3 * NC) {
+    const int q = threadIdx.x / NC, cc = threadIdx.x % NC;
     double r = 0.0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) r += red2[k][q][cc];
     tot[q][cc] = r;
   }
   __syncthreads();
-  if (threadIdx.x < 16 && c < C) {
+  if (threadIdx.x < NC && c < C) {
     const float is = invstd[c];
     const float sdy = (float)tot[0][col], dotp = (float)tot[1][col];
     coef[c] = sdy / (float)ntot;
@@ -1633,8 +1637,16 @@ static int bn_bwd_fused_impl(const float* G, const float* gvec, const float* w, 
     fbn_launch(bn_bwd_partial4_kernel, dim3(fbn_cdiv(C, 256), nch), dim3(256), 0, st, s, Xpre, mean, B, C, rpc,
                        part);
   static const bool wide = !getenv("FBN_BN_REDUCE64");   // A/B knob: 64 columns per workgroup
-  if (wide)
-    fbn_launch(bn_bwd_reduce_finalize16_kernel, dim3(fbn_cdiv(C, 16)), dim3(1024), 0, st, part, nch, C, ntot,
+  const char* nce = getenv("FBN_BN_REDUCE_NC");   // A/B knob, read per call: columns per workgroup
+  const int nc = nce ? atoi(nce) : 16;
+  if (wide && nc == 4)
+    fbn_launch(bn_bwd_reduce_finalize16_kernel<4>, dim3(fbn_cdiv(C, 4)), dim3(256), 0, st, part, nch, C, ntot,
+               invstd, coef, dgamma, dbeta, dw);
+  else if (wide && nc == 8)
+    fbn_launch(bn_bwd_reduce_finalize16_kernel<8>, dim3(fbn_cdiv(C, 8)), dim3(512), 0, st, part, nch, C, ntot,
+               invstd, coef, dgamma, dbeta, dw);
+  else if (wide)
+    fbn_launch(bn_bwd_reduce_finalize16_kernel<16>, dim3(fbn_cdiv(C, 16)), dim3(1024), 0, st, part, nch, C, ntot,
                        invstd, coef, dgamma, dbeta, dw);
   else
     fbn_launch(bn_bwd_reduce_finalize_kernel, dim3(fbn_cdiv(C, 64)), dim3(1024), 0, st, part, nch, C, ntot,

@@ -581,3 +581,37 @@ def test_bn_act_four_rows_per_wave_matches(hip_device, monkeypatch, B, C):
     for x, y in zip(a, b):
         assert torch.equal(x, y)
     assert torch.equal(a[3], a[4]) and bool((a[3] <= 1).all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,C", [(8192, 512), (1000, 256)])
+def test_bn_backward_reduce_columns_per_block(hip_device, monkeypatch, B, C):
+    """The BN backward's chunk reduce on 4 / 8 columns per workgroup (FBN_BN_REDUCE_NC, read per
+    call) folds every column's 64 chunk streams in the same fixed order as the default 16: the
+    whole backward (dX, dgamma, dbeta, head-weight gradient) is bit-identical."""
+    dev = hip_device
+    g = torch.Generator(device="cpu").manual_seed(13)
+    X = torch.randn((B, C), generator=g).to(dev)
+    mean = X.mean(0)
+    inv = 1.0 / torch.sqrt(X.var(0, unbiased=False) + 1e-5)
+    gamma = (1 + 0.1 * torch.randn((C,), generator=g)).to(dev)
+    hact = torch.relu(torch.randn((B, C), generator=g)).to(dev)
+    gvec = torch.randn((B,), generator=g).to(dev)
+    w = torch.randn((C,), generator=g).to(dev)
+    st = _lib.stream_handle(dev)
+    outs = []
+    for nc in ("16", "4", "8"):
+        monkeypatch.setenv("FBN_BN_REDUCE_NC", nc)
+        d = [torch.full((B, C), float("nan"), device=dev)] + [torch.full((C,), float("nan"), device=dev)
+                                                               for _ in range(3)]
+        ops.bn_backward(None, gvec, w, hact, 1.25, X, mean, inv, gamma, B, C, float(B), d[0], d[1], d[2], d[3],
+                        ops.NO_COLLECTIVE, st, tag=f"nc{nc}")
+        torch.cuda.synchronize()
+        outs.append(d)
+    for other in outs[1:]:
+        for a, b in zip(outs[0], other):
+            assert torch.equal(a, b)
+    dy = torch.where(hact > 0, gvec[:, None].double() * w.double() * 1.25, torch.zeros((), dtype=torch.float64,
+                                                                                          device=dev))
+    # dy is formed in float (gvec * w, then * scale) and summed in double: float rounding per term
+    assert torch.allclose(outs[0][2].double(), dy.sum(0), rtol=1e-4, atol=1e-3)
