@@ -1272,6 +1272,9 @@ extern "C" int fbn_gemm_slabs_group(const void* descs, int n, void* stream) {
   else if (wide && group_w4())   // A/B knob: 4 waves of 64x64 (fewer LDS fragment reads per MFMA)
     fbn_launch((gemm_dma16_group_kernel<128, 128, true, true, 2, 2, 2>), dim3((unsigned)total), dim3(256), 0,
                        st, G);
+  else if (wide && se && atoi(se) == 4)
+    fbn_launch((gemm_dma16_group_kernel<128, 128, true, true, 4, 2, 4>), dim3((unsigned)total), dim3(512), 0,
+                       st, G);
   else if (wide && se && atoi(se) == 3)
     fbn_launch((gemm_dma16_group_kernel<128, 128, true, true, 3, 2, 4>), dim3((unsigned)total), dim3(512), 0,
                        st, G);
