@@ -29,6 +29,7 @@
 #include "common.h"
 #include <cstdlib>
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 
 #ifndef FBN_DMA_STAGES
@@ -1166,21 +1167,26 @@ extern "C" int fbn_gemm_slabs(const void* A, const void* B, int M, int N, int K,
 
 extern "C" int fbn_gemm_slabs_split(int M, int N, int K) { return (M > 0 && N > 0) ? slab_split(M, N, K) : 0; }
 
-// K-slabs of a problem inside fbn_gemm_slabs_group: half fbn_gemm_slabs_split's -- the grouped
-// problems fill the chip together, so each needs fewer workgroups, and half the slabs are written
-// and summed (C3: 0.4407 -> 0.4327 ms/step; a quarter: 0.4617; profiles/r03s2_group_knobs_ab.txt).
-// FBN_GROUP_SPLIT_DIV overrides the divisor (1: fbn_gemm_slabs's own partition, whose sums the
-// group then reproduces bit for bit; tests/test_gpu_trainer.py::test_wgrad_group_bit_identical).
+// K-slabs of a problem inside fbn_gemm_slabs_group: three quarters of fbn_gemm_slabs_split's
+// (rounded) -- the grouped problems fill the chip together, so each needs fewer workgroups and
+// fewer slabs are written and summed, but the launch wants two of its 64-KB workgroups on every CU:
+// C3's four problems give 640 workgroups at fbn_gemm_slabs's partition, 476 at 3/4 and 320 at 1/2
+// (round 3's default, which left most CUs one workgroup): 0.4099 vs 0.4178 ms/step over 5
+// interleaved rounds on two boxes, C2 0.2028 vs 0.2052 (profiles/r06_wgrad_split_ab.txt; a quarter:
+// 0.44).  FBN_GROUP_SPLIT_DIV overrides the divisor, fractional allowed (1: fbn_gemm_slabs's own
+// partition, whose sums the group then reproduces bit for bit;
+// tests/test_gpu_trainer.py::test_wgrad_group_bit_identical).
+#define FBN_GROUP_SPLIT_DIV_DEFAULT (4.0 / 3.0)
 static bool group_w4() {
   const char* e = getenv("FBN_GROUP_W4");   // read per call
   return e && atoi(e) != 0;
 }
 static int group_split(int M, int N, int K) {
   int s = slab_split(M, N, K);
-  const char* e = getenv("FBN_GROUP_SPLIT_DIV");
-  const int div = e ? atoi(e) : 2;
-  if (div > 1) {
-    s = std::max(1, s / div);
+  const char* e = getenv("FBN_GROUP_SPLIT_DIV");   // slabs = s / div (integral div) or round(s / div)
+  const double div = e ? atof(e) : FBN_GROUP_SPLIT_DIV_DEFAULT;
+  if (div > 1.0) {
+    s = std::max(1, div == (double)(int)div ? s / (int)div : (int)std::lround(s / div));
     const int per = fbn_cdiv(fbn_cdiv(K, s), 64) * 64;
     s = fbn_cdiv(K, per);
   }

@@ -84,7 +84,7 @@ int fbn_gemm_slabs_split(int M, int N, int K);
  * {const void* A, *B; float* ws; size_t ws_bytes; const void* A2, *B2;
  *  int M, N, K, lda, ldb, transA, transB, lda2, kseg, ldb2, nseg, s3k0; long long lo_a, lo_b;}
  * with the meaning of fbn_gemm_slabs's arguments; each ws receives fbn_gemm_slabs_group_split(M, N, K)
- * K-slabs (half fbn_gemm_slabs_split's by default; with FBN_GROUP_SPLIT_DIV=1 exactly the slabs
+ * K-slabs (3/4 of fbn_gemm_slabs_split's, rounded, by default; with FBN_GROUP_SPLIT_DIV=1 exactly the slabs
  * fbn_gemm_slabs writes, bit for bit).  Every problem: transA = 1, transB = 0, K % 64 == 0,
  * M, N, lda, ldb % 8 == 0, no A2.  s3k0 > 0 (on every problem or none): split-bf16 x3 as
  * fbn_gemm_s3, K = 3 s3k0 over the hi images A / B and the lo images lo_a / lo_b elements past them. */

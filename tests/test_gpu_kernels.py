@@ -387,7 +387,7 @@ def _slabs_group_cases(hip_device, st, g, lib, _lib):
 
 @pytest.mark.gpu
 def test_gemm_slabs_group_default_partition_sums(hip_device):
-    """With its default K partition (half fbn_gemm_slabs's slabs) the group's slab SUM -- what the
+    """With its default K partition (3/4 of fbn_gemm_slabs's slabs) the group's slab SUM -- what the
     step's sum launch turns into the weight gradient -- equals the separate launch's within fp32
     rounding of a K-long dot product (1e-5 relative to the largest entry)."""
     import ctypes

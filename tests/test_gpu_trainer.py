@@ -401,7 +401,7 @@ def test_graph_eager_interleave_bit_identical(hip_device):
 def test_wgrad_group_bit_identical(hip_device, d, B):
     """The step's weight-gradient GEMMs deferred to ONE grouped launch at the end of the backward
     (fbn_gemm_slabs_group, ops._WGRAD_GROUP), on fbn_gemm_slabs's K partition
-    (FBN_GROUP_SPLIT_DIV=1; the default halves the slab count), write the same K-slabs as
+    (FBN_GROUP_SPLIT_DIV=1; the default takes 3/4 of the slab count), write the same K-slabs as
     launching each in place:
     every output element's K-chunk goes through the same 32x32x16 MFMA sequence whatever the
     group's tile shape.  Three bf16 steps with and without grouping: losses, dense parameters and
