@@ -983,6 +983,13 @@ static GemmPlan plan_dma16(int M, int N, int K) {
       if (sscanf(e, "%d,%d", &a, &b) == 2) return {a, b, 1};
     }
     if (N >= 1024 && (long long)fbn_cdiv(M, 128) * fbn_cdiv(N, 128) >= 256) return {128, 128, 1, 8};
+    // tuning knob: "bm,bn,waves" for an output whose 64x128 tiles leave fewer than two workgroups
+    // per CU (C3: MLP layer 2, 8192 x 256)
+    const char* mt = getenv("FBN_DMA_MID_TILE");
+    if (mt && (long long)fbn_cdiv(M, 64) * fbn_cdiv(N, 128) < 512) {
+      int a = 64, b = 128, w = 8;
+      if (sscanf(mt, "%d,%d,%d", &a, &b, &w) == 3) return {a, b, 1, w};
+    }
     if (N >= 128) return {64, 128, 1, 8};
     return {64, 64, 1};
   }
