@@ -22,10 +22,13 @@
 #define FBN_MAXR 8   // max SENET reduced width supported (reference: 3)
 #define FBN_MAX_L 32 // max history length (the reference keeps the last 20)
 #ifndef FBN_HCH
-// default history rows in flight per sample before they are summed (FBN_FIELDS_HCH: 5 / 10 / 20):
-// 5 -- in the step, beside the side-stream table-Adam passes, the lighter waves win (C3 in-process,
-// 10 rounds: 0.4184 vs 0.4203 (10) vs 0.4212 ms/step (20), profiles/r03s2_group_knobs_ab.txt)
-#define FBN_HCH 5
+// default history rows in flight per sample before they are summed (FBN_FIELDS_HCH: 5 / 10 / 20;
+// the sum runs in slot order whatever the chunk, so every choice gives the same bits): 10 -- round 3
+// measured 5 best beside the side-stream passes (0.4184 vs 0.4203 (10) vs 0.4212 ms/step (20),
+// profiles/r03s2_group_knobs_ab.txt); on round 6's step the two tie on time (0.4027 / 0.4136 vs
+// 0.4035 / 0.4141 ms/step, two boxes) and 10 runs the gather itself faster inside the step (in-step
+// fraction of the HBM roofline 0.52-0.61 vs 0.37-0.51; profiles/r06_knob_resweep_ab.txt)
+#define FBN_HCH 10
 #endif
 
 struct FieldArgs {
