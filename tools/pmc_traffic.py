@@ -35,8 +35,12 @@ KERNELS = {
 
 
 def load(d, counter):
+    import gzip
+    import os
     rows = []
-    for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
+    path = f"{d}/run_counter_collection.csv"
+    fh = open(path) if os.path.exists(path) else gzip.open(path + ".gz", "rt")   # gpu_pmc.sh gzips the passes
+    for r in csv.DictReader(fh):
         if r["Counter_Name"] == counter:
             rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"], r["Grid_Size"], float(r["Counter_Value"])))
     return sorted(rows)
