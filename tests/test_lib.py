@@ -35,6 +35,31 @@ def test_workspace_queries_are_host_only():
     assert h.fbn_bn_workspace_size(8192, 512) > 0
 
 
+def test_wgrad_group_split_fills_two_workgroups_per_cu(monkeypatch):
+    """The grouped weight-gradient launch's K-slabs (host planning only): by default 3/4 of the
+    single launches' slabs, rounded, so C3's four problems (dWa 512 x 1920, dWb 256 x 512, the
+    bilinear W 128 x 128 over K = 5B, mm_proj 128 x 128) come to at most two 128 x 128 workgroups
+    per CU on 256 CUs; FBN_GROUP_SPLIT_DIV (read per call, fractional allowed) overrides it."""
+    from ctr_recommendation_amd import _lib
+    h = _lib.lib()
+    B = 8192
+    probs = [(512, 1920, B), (256, 512, B), (128, 128, 5 * B), (128, 128, B)]
+    monkeypatch.delenv("FBN_GROUP_SPLIT_DIV", raising=False)
+
+    def total():
+        return sum(((M + 127) // 128) * ((N + 127) // 128) * h.fbn_gemm_slabs_group_split(M, N, K)
+                   for M, N, K in probs)
+    assert h.fbn_gemm_slabs_split(512, 1920, B) == 8
+    assert h.fbn_gemm_slabs_group_split(512, 1920, B) == 6
+    assert 384 < total() <= 512
+    for M, N, K in probs:
+        assert 1 <= h.fbn_gemm_slabs_group_split(M, N, K) <= h.fbn_gemm_slabs_split(M, N, K)
+    monkeypatch.setenv("FBN_GROUP_SPLIT_DIV", "2")        # round 3's halving
+    assert h.fbn_gemm_slabs_group_split(512, 1920, B) == 4 and total() == 336
+    monkeypatch.setenv("FBN_GROUP_SPLIT_DIV", "1")        # fbn_gemm_slabs's own partition
+    assert all(h.fbn_gemm_slabs_group_split(M, N, K) == h.fbn_gemm_slabs_split(M, N, K) for M, N, K in probs)
+
+
 def test_product_never_imports_oracle():
     pkg = os.path.join(ROOT, "ctr_recommendation_amd")
     for dirpath, _, files in os.walk(pkg):
