@@ -1177,7 +1177,7 @@ extern "C" int fbn_gemm_slabs_split(int M, int N, int K) { return (M > 0 && N > 
 // K-slabs of a problem inside fbn_gemm_slabs_group: three quarters of fbn_gemm_slabs_split's
 // (rounded) -- the grouped problems fill the chip together, so each needs fewer workgroups and
 // fewer slabs are written and summed, but the launch wants two of its 64-KB workgroups on every CU:
-// C3's four problems give 640 workgroups at fbn_gemm_slabs's partition, 476 at 3/4 and 320 at 1/2
+// C3's four problems give 672 workgroups at fbn_gemm_slabs's partition, 497 at 3/4 and 336 at 1/2
 // (round 3's default, which left most CUs one workgroup): 0.4099 vs 0.4178 ms/step over 5
 // interleaved rounds on two boxes, C2 0.2028 vs 0.2052 (profiles/r06_wgrad_split_ab.txt; a quarter:
 // 0.44).  FBN_GROUP_SPLIT_DIV overrides the divisor, fractional allowed (1: fbn_gemm_slabs's own
