@@ -64,6 +64,8 @@ VARIANTS = {
     "ieee": ("FBN_ADAM_IEEE",),
     # the replay engine's constants one step at a time (round 4's form; A/B of FBN_REPLAY_BLOCK4)
     "rstep1": ("FBN_REPLAY_BLOCK4=0",),
+    # the main-stream step kernels at wave priority 3 instead of 2 (A/B of FBN_MAIN_PRIO_LEVEL)
+    "prio3": ("FBN_MAIN_PRIO_LEVEL=3",),
 }
 
 
