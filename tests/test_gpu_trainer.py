@@ -316,6 +316,46 @@ def test_next_batch_prefetch_bit_identical(hip_device, defer, dups, d, binned, m
 
 
 @pytest.mark.gpu
+def test_lazy_production_path_matches_eager_over_ring_wrap(hip_device):
+    """The production table-Adam path -- lazy replay, deferred gradients, the next-batch prefetch,
+    rolling window F = 128 (d = 128's default, ring of F + 1 = 129 slots) -- against the eager
+    per-step pass over every row, for 150 steps: past the ring's wrap-around and with rows that no
+    batch touches for longer than F steps (the window replays full 128-step lags).  Ids are unique
+    within each step (no float-atomic folds), so losses, table, moments and dense state are
+    bit-identical."""
+    V, B, L, steps = 20000, 32, 20, 150
+    cfg = {"embedding_dim": 128, "vocab_size": V}
+    torch.manual_seed(0)
+    init = oracle_build(None, cfg).state_dict()
+    kw = dict(total_steps=steps + 4, batch_size=B, device=hip_device, init_state=init)
+    eager = FiBiNETTrainer(cfg, table_adam="eager", **kw)
+    lazy = FiBiNETTrainer(cfg, table_adam="lazy", **kw)
+    assert lazy.lazy_window == 128 and lazy.deferred and lazy.prefetch_rows
+    g = torch.Generator().manual_seed(11)
+    pool = torch.randperm(V - 1, generator=g)[:1500] + 1
+    batches = []
+    for s in range(steps + 1):
+        b, y = make_batch(900 + s, B, V)
+        ids = pool[torch.randperm(len(pool), generator=g)[:B * (L + 1)]].view(B, L + 1)
+        b["item_id"] = ids[:, 0].clone()
+        seq = ids[:, 1:].clone()
+        seq[b["item_seq"] == 0] = 0
+        b["item_seq"] = seq
+        batches.append(({k: v.to(hip_device) for k, v in b.items()}, y.to(hip_device)))
+    for s in range(steps):
+        db, y = batches[s]
+        le = eager.step(db, y).item()
+        ll = lazy.step(db, y, next_batch=batches[s + 1][0]).item()
+        assert le == ll, (s, le, ll)
+    lazy.flush()
+    torch.cuda.synchronize()
+    assert int(lazy.last.min()) == steps
+    for n, a, c in (("E", eager.E, lazy.E), ("Em", eager.Em, lazy.Em), ("Ev", eager.Ev, lazy.Ev),
+                    ("p", eager.flat_p, lazy.flat_p), ("m", eager.flat_m, lazy.flat_m), ("v", eager.flat_v, lazy.flat_v)):
+        assert torch.equal(a, c), (n, (a - c).abs().max().item())
+
+
+@pytest.mark.gpu
 def test_deterministic_mode_bit_identical_runs(hip_device):
     """Deterministic mode: duplicate rows are folded by int64 fixed-point sums, so
     two runs from the same state -- many duplicate ids (V = 400 rows, 256 x 21 entries per step),
