@@ -15,8 +15,8 @@ from oracle.fibinet_oracle import build_model as oracle_build
 pytestmark = pytest.mark.gpu
 
 
-def _trainer(cfg, init, B, dev, det=False):
-    return FiBiNETTrainer(cfg, total_steps=60, batch_size=B, device=dev, deterministic=det,
+def _trainer(cfg, init, B, dev, det=False, total_steps=60):
+    return FiBiNETTrainer(cfg, total_steps=total_steps, batch_size=B, device=dev, deterministic=det,
                           init_state={k: v.clone() for k, v in init.items()})
 
 
@@ -94,6 +94,49 @@ def test_program_replay_bit_identical_to_eager(hip_device, d, dtype, det, shared
     # out of the recorded order (the previous step prefetched another batch): refused
     with pytest.raises(RuntimeError, match="out of order"):
         prog_tr.run_program(progs[(steps + 1) % nb])
+
+
+def test_program_replay_bit_identical_to_eager_long(hip_device):
+    """The bench's configuration (C3's kernels at B = 512: bf16, d = 128, programs recorded into one
+    pool, four batches cycled) replayed for 140 steps against the eager run: past the deferred-gradient
+    ring's wrap-around (F + 1 = 129 slots) and through full rolling-window cycles, every loss, the
+    table, its moments and the dense state stay bit-identical."""
+    V, B, nb, steps = 40000, 512, 4, 140
+    cfg = {"embedding_dim": 128, "vocab_size": V, "compute_dtype": "bf16"}
+    torch.manual_seed(0)
+    init = oracle_build(None, dict(cfg, honour_config=False)).state_dict()
+    g = torch.Generator().manual_seed(17)
+    pool = torch.randperm(V - 1, generator=g)[:20000] + 1
+    batches = []
+    for j in range(nb):
+        b, y = make_batch(160 + j, B, V)
+        b = _unique_ids(b, V, g, pool)
+        batches.append(({k: v.to(hip_device) for k, v in b.items()}, y.to(hip_device)))
+    eager = _trainer(cfg, init, B, hip_device, total_steps=steps + 8)
+    prog_tr = _trainer(cfg, init, B, hip_device, total_steps=steps + 8)
+    wb, wy = make_batch(159, B, V)
+    wb = _unique_ids(wb, V, g, pool)
+    wb, wy = {k: v.to(hip_device) for k, v in wb.items()}, wy.to(hip_device)
+    for tr in (eager, prog_tr):
+        tr.step(wb, wy, next_batch=batches[0][0])
+    progs, mem_pool = {}, torch.cuda.MemPool()
+    le, lp = [], []
+    for i in range(steps):
+        b, y = batches[i % nb]
+        nxt = batches[(i + 1) % nb][0]
+        le.append(eager.step(b, y, next_batch=nxt).item())
+        j = i % nb
+        if j not in progs:
+            progs[j] = prog_tr.record_program(b, y, next_batch=nxt, pool=mem_pool)
+        else:
+            prog_tr.run_program(progs[j])
+        lp.append(prog_tr.loss.item())
+    assert le == lp, [(i, a, c) for i, (a, c) in enumerate(zip(le, lp)) if a != c][:4]
+    assert prog_tr.device_step() == eager.device_step() == steps + 1
+    eager.flush()
+    prog_tr.flush()
+    for name in ("E", "Em", "Ev", "flat_p", "flat_m", "flat_v", "last"):
+        assert torch.equal(getattr(eager, name), getattr(prog_tr, name)), name
 
 
 def test_program_refuses_rewritten_batch(hip_device):
